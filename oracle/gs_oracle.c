@@ -1,0 +1,780 @@
+/*
+ * gs_oracle.c -- CPU restatement of GeneralSparse's SpMM hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see gs_oracle.h).  Deliberately literal and
+ * single-threaded: each function walks the data the way the cited reference
+ * transform does, so that a reviewer can check it line by line against the
+ * reference.  Reference defects are reproduced where they change the plan
+ * arrays and guarded (error return) where the reference would crash.
+ */
+#include "gs_oracle.h"
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#define PADDING_RATE_UP_BOUND 4 /* global_config.json.bak:25 */
+
+/* ------------------------------------------------------------------ */
+/* named-array set (metadata_set.cc:147-151, :255-331)                 */
+/* ------------------------------------------------------------------ */
+
+static int fail(or_set *s, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(s->err, sizeof(s->err), fmt, ap);
+    va_end(ap);
+    return -1;
+}
+
+static void mkkey(char *out, const char *pos, const char *name, int sub) {
+    snprintf(out, OR_NAME_LEN, "%s_%s_%d", pos, name, sub);
+}
+
+or_array *or_find(or_set *s, const char *key) {
+    for (int i = 0; i < s->n; i++)
+        if (strcmp(s->a[i].key, key) == 0) return &s->a[i];
+    return NULL;
+}
+
+static or_array *get(or_set *s, const char *pos, const char *name, int sub) {
+    char k[OR_NAME_LEN];
+    mkkey(k, pos, name, sub);
+    return or_find(s, k);
+}
+
+static int exists(or_set *s, const char *pos, const char *name, int sub) {
+    return get(s, pos, name, sub) != NULL;
+}
+
+static void drop(or_set *s, const char *pos, const char *name, int sub) {
+    char k[OR_NAME_LEN];
+    mkkey(k, pos, name, sub);
+    for (int i = 0; i < s->n; i++) {
+        if (strcmp(s->a[i].key, k) == 0) {
+            free(s->a[i].u);
+            free(s->a[i].f);
+            s->a[i] = s->a[s->n - 1];
+            s->n--;
+            return;
+        }
+    }
+}
+
+/* add_element: takes ownership of data */
+static or_array *put_u(or_set *s, const char *pos, const char *name, int sub,
+                       uint64_t *data, uint64_t len) {
+    drop(s, pos, name, sub);
+    or_array *a = &s->a[s->n++];
+    memset(a, 0, sizeof(*a));
+    mkkey(a->key, pos, name, sub);
+    a->len = len;
+    a->u = data;
+    return a;
+}
+
+static or_array *put_f(or_set *s, const char *pos, const char *name, int sub,
+                       double *data, uint64_t len) {
+    drop(s, pos, name, sub);
+    or_array *a = &s->a[s->n++];
+    memset(a, 0, sizeof(*a));
+    mkkey(a->key, pos, name, sub);
+    a->len = len;
+    a->is_float = 1;
+    a->f = data;
+    return a;
+}
+
+static or_array *put_scalar(or_set *s, const char *pos, const char *name, int sub,
+                            uint64_t v) {
+    uint64_t *d = (uint64_t *)malloc(sizeof(uint64_t));
+    d[0] = v;
+    return put_u(s, pos, name, sub, d, 1);
+}
+
+static uint64_t scalar(or_set *s, const char *pos, const char *name, int sub) {
+    or_array *a = get(s, pos, name, sub);
+    return a ? a->u[0] : 0;
+}
+
+void or_set_free(or_set *s) {
+    for (int i = 0; i < s->n; i++) {
+        free(s->a[i].u);
+        free(s->a[i].f);
+    }
+    s->n = 0;
+}
+
+int or_count(const or_set *s) { return s->n; }
+const char *or_key(const or_set *s, int i) { return s->a[i].key; }
+uint64_t or_len(const or_set *s, int i) { return s->a[i].len; }
+int or_is_float(const or_set *s, int i) { return s->a[i].is_float; }
+const uint64_t *or_u(const or_set *s, int i) { return s->a[i].u; }
+const double *or_f(const or_set *s, int i) { return s->a[i].f; }
+const char *or_error(const or_set *s) { return s->err; }
+
+static uint64_t *dup_u(const uint64_t *p, uint64_t n) {
+    uint64_t *d = (uint64_t *)malloc((n ? n : 1) * sizeof(uint64_t));
+    if (n) memcpy(d, p, n * sizeof(uint64_t));
+    return d;
+}
+
+/* growable u64 / f64 vectors */
+typedef struct { uint64_t *p; uint64_t n, cap; } vu;
+static void vu_push(vu *v, uint64_t x) {
+    if (v->n == v->cap) { v->cap = v->cap ? v->cap * 2 : 16; v->p = (uint64_t *)realloc(v->p, v->cap * 8); }
+    v->p[v->n++] = x;
+}
+
+/* ------------------------------------------------------------------ */
+/* A1: .mtx reader -- struct.cc:49-261                                  */
+/* ------------------------------------------------------------------ */
+
+int or_read_mtx(const char *path, int ones_values, or_coo *out) {
+    memset(out, 0, sizeof(*out));
+    FILE *f = fopen(path, "r");
+    if (!f) return -1;
+    char buf[1024];
+    int first = 1;
+    vu rows = {0}, cols = {0};
+    float *vals = NULL;
+    uint64_t vcap = 0;
+    while (fgets(buf, sizeof(buf), f)) {
+        size_t L = strlen(buf);
+        while (L && (buf[L - 1] == '\n' || buf[L - 1] == '\r')) buf[--L] = 0;
+        /* struct.cc:97: skip empty lines, lines starting with whitespace or '%' */
+        if (L == 0 || buf[0] == ' ' || buf[0] == '\t' || buf[0] == '%') continue;
+        char *tok[3] = {0, 0, 0};
+        int nt = 0;
+        char *p = buf;
+        while (nt < 3 && p) { /* split on single spaces (struct.hpp:290) */
+            tok[nt++] = p;
+            p = strchr(p, ' ');
+            if (p) *p++ = 0;
+        }
+        if (first) { /* struct.cc:104-110: header gives max indices */
+            out->max_row_index = (uint64_t)atol(tok[0]) - 1;
+            out->max_col_index = (uint64_t)atol(tok[1]) - 1;
+            first = 0;
+            continue;
+        }
+        uint64_t r = (uint64_t)atol(tok[0]) - 1; /* struct.cc:114-116 */
+        uint64_t c = (uint64_t)atol(tok[1]) - 1;
+        float v = tok[2] ? (float)atof(tok[2]) : 1.0f;
+        if (rows.n && r < rows.p[rows.n - 1]) { /* struct.cc:120-131 */
+            fclose(f);
+            free(rows.p); free(cols.p); free(vals);
+            return -2;
+        }
+        vu_push(&rows, r);
+        vu_push(&cols, c);
+        if (rows.n > vcap) { vcap = vcap ? vcap * 2 : 16; vals = (float *)realloc(vals, vcap * sizeof(float)); }
+        vals[rows.n - 1] = ones_values ? 1.0f : v; /* struct.cc:186-200 */
+        if (r > out->max_row_index) out->max_row_index = r; /* struct.cc:203-211 */
+        if (c > out->max_col_index) out->max_col_index = c;
+    }
+    fclose(f);
+    if (rows.n == 0) { free(rows.p); free(cols.p); free(vals); return -3; } /* struct.cc:258 */
+    out->nnz = rows.n;
+    out->row = rows.p;
+    out->col = cols.p;
+    out->val = vals;
+    return 0;
+}
+
+void or_coo_free(or_coo *c) {
+    free(c->row); free(c->col); free(c->val);
+    memset(c, 0, sizeof(*c));
+}
+
+/* ------------------------------------------------------------------ */
+/* A2: create_init_metadata_set_from_file -- metadata_set.cc:612-707   */
+/* ------------------------------------------------------------------ */
+
+int or_init_set(or_set *s, uint64_t n_rows, uint64_t n_cols, uint64_t nnz,
+                const uint64_t *row, const uint64_t *col, const float *val) {
+    memset(s, 0, sizeof(*s));
+    if (nnz == 0) return fail(s, "empty matrix (struct.cc:258)");
+    uint64_t max_row = n_rows - 1, max_col = n_cols - 1;
+    for (uint64_t i = 0; i < nnz; i++) {
+        if (i && row[i] < row[i - 1]) return fail(s, "rows not sorted (struct.cc:125)");
+        if (row[i] > max_row) max_row = row[i];
+        if (col[i] > max_col) max_col = col[i];
+    }
+    put_scalar(s, "GLOBAL_META", "origin_row_num", -1, max_row + 1);
+    put_scalar(s, "GLOBAL_META", "origin_col_num", -1, max_col + 1);
+    put_scalar(s, "GLOBAL_META", "origin_nnz_num", -1, nnz);
+    put_scalar(s, "GLOBAL_META", "begin_row_index", 0, 0);
+    put_scalar(s, "GLOBAL_META", "begin_col_index", 0, 0);
+    put_scalar(s, "GLOBAL_META", "end_row_index", 0, max_row);
+    put_scalar(s, "GLOBAL_META", "end_col_index", 0, max_col);
+    put_u(s, "GLOBAL_META", "nz_row_indices", 0, dup_u(row, nnz), nnz);
+    put_u(s, "GLOBAL_META", "nz_col_indices", 0, dup_u(col, nnz), nnz);
+    double *v = (double *)malloc(nnz * sizeof(double));
+    for (uint64_t i = 0; i < nnz; i++) v[i] = (double)val[i];
+    put_f(s, "GLOBAL_META", "nz_vals", 0, v, nnz);
+    return 0;
+}
+
+/* get_nnz_of_each_row_in_spec_range -- data_transform_common.cc:7-48 */
+static uint64_t *row_nnz(const uint64_t *row, uint64_t nnz, uint64_t row_num) {
+    uint64_t *cnt = (uint64_t *)calloc(row_num ? row_num : 1, sizeof(uint64_t));
+    for (uint64_t i = 0; i < nnz; i++) cnt[row[i]]++;
+    return cnt;
+}
+
+/* the "real end row" rule repeated in every transform, e.g.
+ * get_begin_rows_of_BMT_after_fixed_blocking_in_row_direction.cc:60-66 */
+static uint64_t row_num_of(or_set *s) {
+    uint64_t b = scalar(s, "GLOBAL_META", "begin_row_index", 0);
+    uint64_t e = scalar(s, "GLOBAL_META", "end_row_index", 0);
+    or_array *r = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    uint64_t real = b + r->u[r->len - 1];
+    if (e < real) e = real;
+    return e - b + 1;
+}
+
+/* ------------------------------------------------------------------ */
+/* A3/A4: sort_operator -- operator/sort_operator.cc:70-108             */
+/* ------------------------------------------------------------------ */
+
+int or_sort_operator(or_set *s) {
+    if (exists(s, "GLOBAL_META", "original_nz_row_indices", 0))
+        return fail(s, "already sorted (sort_operator.cc:55-65)");
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    or_array *C = get(s, "GLOBAL_META", "nz_col_indices", 0);
+    or_array *V = get(s, "GLOBAL_META", "nz_vals", 0);
+    uint64_t nnz = R->len;
+    /* get_row_order_by_length.cc:36-55: row range incl. empty rows */
+    uint64_t minr = scalar(s, "GLOBAL_META", "begin_row_index", 0);
+    uint64_t maxr = scalar(s, "GLOBAL_META", "end_row_index", 0);
+    uint64_t real_max = R->u[nnz - 1];
+    if (real_max > maxr - minr) maxr = minr + real_max;
+    uint64_t nrow = maxr - minr + 1;
+    uint64_t *cnt = row_nnz(R->u, nnz, nrow);
+    uint64_t maxlen = 0;
+    for (uint64_t i = 0; i < nrow; i++) if (cnt[i] > maxlen) maxlen = cnt[i];
+    /* get_row_order_by_length.cc:67-110: buckets by length, visited from
+     * the longest; inside a bucket rows keep ascending order */
+    uint64_t *bstart = (uint64_t *)calloc(maxlen + 2, sizeof(uint64_t));
+    for (uint64_t i = 0; i < nrow; i++) bstart[cnt[i]]++;
+    /* offsets in descending length order */
+    uint64_t acc = 0;
+    for (int64_t L = (int64_t)maxlen; L >= 0; L--) {
+        uint64_t c = bstart[L];
+        bstart[L] = acc;
+        acc += c;
+    }
+    uint64_t *order = (uint64_t *)malloc(nrow * sizeof(uint64_t));
+    for (uint64_t i = 0; i < nrow; i++) order[bstart[cnt[i]]++] = i;
+    free(bstart);
+    put_u(s, "GLOBAL_META", "original_nz_row_indices", 0, order, nrow);
+
+    /* reorder_val/col/row_by_index: regroup COO in the new row order,
+     * keeping the within-row order (reorder_col_by_index.cc:55-120) */
+    uint64_t *start = (uint64_t *)malloc((nrow + 1) * sizeof(uint64_t));
+    start[0] = 0;
+    for (uint64_t i = 0; i < nrow; i++) start[i + 1] = start[i] + cnt[i];
+    /* reorder_col_by_index.cc:82-93 asserts non-decreasing cols in a row */
+    for (uint64_t i = 1; i < nnz; i++)
+        if (R->u[i] == R->u[i - 1] && C->u[i] < C->u[i - 1]) {
+            free(start); free(cnt);
+            return fail(s, "cols not sorted within row (reorder_col_by_index.cc:88)");
+        }
+    uint64_t *nr = (uint64_t *)malloc(nnz * 8), *nc = (uint64_t *)malloc(nnz * 8);
+    double *nv = (double *)malloc(nnz * 8);
+    uint64_t p = 0;
+    for (uint64_t newr = 0; newr < nrow; newr++) {
+        uint64_t old = order[newr];
+        for (uint64_t k = start[old]; k < start[old + 1]; k++) {
+            nr[p] = newr;
+            nc[p] = C->u[k];
+            nv[p] = V->f[k];
+            p++;
+        }
+    }
+    free(start); free(cnt);
+    put_f(s, "GLOBAL_META", "nz_vals", 0, nv, nnz);
+    put_u(s, "GLOBAL_META", "nz_col_indices", 0, nc, nnz);
+    put_u(s, "GLOBAL_META", "nz_row_indices", 0, nr, nnz);
+    /* remove_empty_row_in_end_of_sub_matrix.cc:13-70 */
+    uint64_t b = scalar(s, "GLOBAL_META", "begin_row_index", 0);
+    uint64_t e = scalar(s, "GLOBAL_META", "end_row_index", 0);
+    uint64_t last = nr[nnz - 1];
+    if (last < e - b) put_scalar(s, "GLOBAL_META", "end_row_index", 0, b + last);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* A6: modify_{col,val,row}_by_col_pad_in_sub_matrix                    */
+/*     modify_col_indices_by_col_pad_in_sub_matrix.cc:15-160            */
+/* ------------------------------------------------------------------ */
+
+static int col_pad(or_set *s, int mult) {
+    if (mult < 2) return fail(s, "col pad multiple < 2 (modify_col...:26)");
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    or_array *C = get(s, "GLOBAL_META", "nz_col_indices", 0);
+    or_array *V = get(s, "GLOBAL_META", "nz_vals", 0);
+    uint64_t nnz = R->len, row_num = row_num_of(s);
+    uint64_t *cnt = row_nnz(R->u, nnz, row_num);
+    uint64_t after = nnz;
+    for (uint64_t r = 0; r < row_num; r++)
+        if (cnt[r] % mult) after += (cnt[r] / mult + 1) * mult - cnt[r];
+    if ((double)after / (double)nnz >= PADDING_RATE_UP_BOUND) { /* :103-110 */
+        free(cnt);
+        return fail(s, "padding rate %.3f >= %d", (double)after / nnz, PADDING_RATE_UP_BOUND);
+    }
+    if (after == nnz) { free(cnt); return 0; } /* is_padded == false: arrays untouched */
+    uint64_t *nr = (uint64_t *)malloc(after * 8), *nc = (uint64_t *)malloc(after * 8);
+    double *nv = (double *)malloc(after * 8);
+    uint64_t p = 0, q = 0;
+    for (uint64_t r = 0; r < row_num; r++) {
+        for (uint64_t k = 0; k < cnt[r]; k++, q++) {
+            nr[p] = R->u[q]; nc[p] = C->u[q]; nv[p] = V->f[q]; p++;
+        }
+        if (cnt[r] % mult) {
+            uint64_t target = (cnt[r] / mult + 1) * mult;
+            uint64_t lastc = nc[p - 1], lastr = nr[p - 1];
+            for (uint64_t k = cnt[r]; k < target; k++) { /* :113-116, vals :114 */
+                nr[p] = lastr; nc[p] = lastc; nv[p] = 0.0; p++;
+            }
+        }
+    }
+    free(cnt);
+    put_u(s, "GLOBAL_META", "nz_col_indices", 0, nc, after);
+    put_f(s, "GLOBAL_META", "nz_vals", 0, nv, after);
+    put_u(s, "GLOBAL_META", "nz_row_indices", 0, nr, after);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* A5/A7: fixed_interval_row_direction_thread_blocking_operator,        */
+/* no-parent branch (operator/...thread_blocking_operator.cc:482-565)   */
+/* ------------------------------------------------------------------ */
+
+int or_row_dir_thread_blocking(or_set *s, int rb, int col_pad_size) {
+    if (exists(s, "TBLOCK_META", "first_row_indices", 0) || exists(s, "WARP_META", "first_row_indices", 0))
+        return fail(s, "oracle restates the no-parent branch only");
+    if (col_pad_size > 1 && col_pad(s, col_pad_size)) return -1;
+    uint64_t row_num = row_num_of(s);
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    /* get_begin_rows_of_BMT_after_fixed_blocking_in_row_direction.cc:71-97 */
+    vu fr = {0};
+    int in_bmt = 0, first = 1;
+    for (uint64_t i = 0; i < row_num; i++) {
+        if (first) { vu_push(&fr, i); first = 0; }
+        else in_bmt += 1;
+        if (in_bmt == rb) { vu_push(&fr, i); in_bmt = 0; }
+    }
+    vu_push(&fr, row_num);
+    put_u(s, "THREAD_META", "first_row_indices", 0, fr.p, fr.n);
+    /* get_begin_nzs_of_BMT_after_fixed_blocking_in_row_direction.cc:75-100
+     * (row_count / nz_count are `int` in the reference) */
+    uint64_t *cnt = row_nnz(R->u, R->len, row_num);
+    vu fn = {0};
+    vu_push(&fn, 0);
+    int rc = 0;
+    uint64_t nzc = 0;
+    for (uint64_t i = 0; i < row_num; i++) {
+        rc += 1; nzc += cnt[i];
+        if (rc == rb) { vu_push(&fn, nzc); rc = 0; }
+    }
+    if (rc != rb && rc != 0) vu_push(&fn, nzc);
+    free(cnt);
+    put_u(s, "THREAD_META", "first_nz_indices", 0, fn.p, fn.n);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* A8: fixed_interval_row_direction_tblock_blocking_operator (no pad)   */
+/* get_begin_{rows,nzs}_of_BMTBs_after_fixed_blocking_in_row_direction  */
+/* ------------------------------------------------------------------ */
+
+static void fixed_row_blocks(or_set *s, int rb, const char *pos) {
+    uint64_t row_num = row_num_of(s);
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    vu fr = {0};
+    vu_push(&fr, 0);
+    uint64_t complete = row_num / rb; /* :74-83 */
+    for (uint64_t i = 0; i < complete; i++) vu_push(&fr, (i + 1) * rb);
+    if (row_num % rb) vu_push(&fr, row_num);
+    put_u(s, pos, "first_row_indices", 0, fr.p, fr.n);
+    uint64_t *cnt = row_nnz(R->u, R->len, row_num);
+    uint64_t nb = row_num / rb + (row_num % rb ? 1 : 0);
+    vu fn = {0};
+    vu_push(&fn, 0);
+    for (uint64_t i = 0; i < nb; i++) { /* nzs...BMTBs...:70-86 */
+        uint64_t c = 0;
+        for (uint64_t r = i * rb; r < (i + 1) * rb && r < row_num; r++) c += cnt[r];
+        vu_push(&fn, fn.p[fn.n - 1] + c);
+    }
+    free(cnt);
+    put_u(s, pos, "first_nz_indices", 0, fn.p, fn.n);
+}
+
+int or_row_dir_tblock_blocking(or_set *s, int rb) {
+    if (rb < 1) return fail(s, "rb < 1");
+    fixed_row_blocks(s, rb, "TBLOCK_META");
+    return 0;
+}
+
+/* fixed_interval_row_direction_warp_blocking_operator.cc: without BMTB
+ * (get_begin_*_of_BMW_..._without_BMTB.cc) or inside BMTBs
+ * (get_begin_*_of_BMW_..._in_BMTB.cc + get_begin_BMWs_of_BMTB_...cc) */
+int or_row_dir_warp_blocking(or_set *s, int rb) {
+    if (rb < 1) return fail(s, "rb < 1");
+    or_array *TR = get(s, "TBLOCK_META", "first_row_indices", 0);
+    if (!TR) { fixed_row_blocks(s, rb, "WARP_META"); return 0; }
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    uint64_t row_num = row_num_of(s);
+    uint64_t *cnt = row_nnz(R->u, R->len, row_num);
+    vu wr = {0}, wn = {0}, tb = {0};
+    vu_push(&wn, 0);
+    for (uint64_t i = 0; i + 1 < TR->len; i++) {
+        uint64_t b = TR->u[i], e = TR->u[i + 1];
+        for (uint64_t r0 = b; r0 < e; r0 += rb) {
+            vu_push(&wr, r0);
+            uint64_t c = 0;
+            for (uint64_t r = r0; r < e && r < r0 + rb; r++) c += cnt[r];
+            vu_push(&wn, wn.p[wn.n - 1] + c);
+        }
+    }
+    vu_push(&wr, TR->u[TR->len - 1]);
+    free(cnt);
+    /* get_begin_BMWs_of_BMTB_after_blocking_in_row_direction.cc */
+    vu_push(&tb, 0);
+    uint64_t cur = 0;
+    for (uint64_t i = 0; i + 1 < TR->len; i++) {
+        uint64_t e = TR->u[i + 1];
+        uint64_t num = 0;
+        uint64_t fr = wr.p[cur];
+        while (fr < e) {
+            num++; cur++;
+            if (cur == wr.n) break;
+            fr = wr.p[cur];
+        }
+        vu_push(&tb, tb.p[tb.n - 1] + num);
+    }
+    put_u(s, "WARP_META", "first_row_indices", 0, wr.p, wr.n);
+    put_u(s, "WARP_META", "first_nz_indices", 0, wn.p, wn.n);
+    put_u(s, "TBLOCK_META", "first_BMW_indices", 0, tb.p, tb.n);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* A9: fixed_interval_nnz_direction_thread_blocking_operator            */
+/* (operator/...nnz_direction_thread_blocking_operator.cc:156-245),     */
+/* no-parent branch                                                     */
+/* ------------------------------------------------------------------ */
+
+int or_nnz_dir_thread_blocking(or_set *s, int nnz_per_bmt, int pad) {
+    if (nnz_per_bmt < 1) return fail(s, "nnz_per_BMT < 1");
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    uint64_t nnz = R->len;
+    if (pad && nnz % nnz_per_bmt) { /* modify_*_by_nnz_pad.cc:14-75 */
+        uint64_t nn = (nnz / nnz_per_bmt + 1) * nnz_per_bmt;
+        if ((double)nn / (double)nnz >= PADDING_RATE_UP_BOUND)
+            return fail(s, "nnz padding rate %.3f >= %d", (double)nn / nnz, PADDING_RATE_UP_BOUND);
+        or_array *C = get(s, "GLOBAL_META", "nz_col_indices", 0);
+        or_array *V = get(s, "GLOBAL_META", "nz_vals", 0);
+        uint64_t *nc = (uint64_t *)malloc(nn * 8), *nr = (uint64_t *)malloc(nn * 8);
+        double *nv = (double *)malloc(nn * 8);
+        for (uint64_t i = 0; i < nn; i++) {
+            uint64_t k = i < nnz ? i : nnz - 1;
+            nc[i] = C->u[k]; nr[i] = R->u[k];
+            nv[i] = i < nnz ? V->f[i] : 0.0;
+        }
+        put_u(s, "GLOBAL_META", "nz_col_indices", 0, nc, nn);
+        put_f(s, "GLOBAL_META", "nz_vals", 0, nv, nn);
+        put_u(s, "GLOBAL_META", "nz_row_indices", 0, nr, nn);
+        R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+        nnz = nn;
+    }
+    uint64_t row_num = row_num_of(s);
+    /* get_begin_rows_of_BMT_after_fixed_blocking_in_nnz_direction.cc */
+    vu fr = {0}, fn = {0};
+    for (uint64_t i = 0; i < nnz; i += nnz_per_bmt) vu_push(&fr, R->u[i]);
+    vu_push(&fr, row_num);
+    /* get_begin_nzs_of_BMT_after_fixed_blocking_in_nnz_direction.cc */
+    for (uint64_t i = 0; i < nnz; i += nnz_per_bmt) vu_push(&fn, i);
+    vu_push(&fn, nnz);
+    put_u(s, "THREAD_META", "first_row_indices", 0, fr.p, fr.n);
+    put_u(s, "THREAD_META", "first_nz_indices", 0, fn.p, fn.n);
+    /* get_BMT_size_of_each_parent.cc (GLOBAL parent): one size when all
+     * BMTs are equal, otherwise the item is not created (:118-121) */
+    uint64_t size0 = fn.p[1] - fn.p[0];
+    int same = 1;
+    for (uint64_t i = 0; i + 1 < fn.n; i++)
+        if (fn.p[i + 1] - fn.p[i] != size0) { same = 0; break; }
+    if (same) put_scalar(s, "GLOBAL_META", "BMT_size_of_each_blk", 0, size0);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* thread_bit_map_operator.cc:60-101 and its transforms                 */
+/* ------------------------------------------------------------------ */
+
+int or_thread_bit_map_operator(or_set *s, int pos_is_warp, int size) {
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    or_array *FN = get(s, "THREAD_META", "first_nz_indices", 0);
+    if (!R || !FN) return fail(s, "missing THREAD first_nz_indices");
+    uint64_t nnz = R->len, nb = FN->len - 1;
+    if (FN->u[nb] != nnz) return fail(s, "bitmap length mismatch (thread_bit_map.cc:43)");
+    /* thread_bit_map.cc:27-41 */
+    unsigned char *bit = (unsigned char *)malloc(nnz);
+    bit[0] = 1;
+    for (uint64_t j = 1; j < nnz; j++) bit[j] = R->u[j] != R->u[j - 1];
+    /* thread_bit_map.cc:45-71: with a WARP/TBLOCK parent, the head of
+     * every size-th BMT is forced to 1.  thread_size is read from the
+     * GLOBAL BMT_size_of_each_blk; the reference divides by zero without
+     * it, and writes one element past the end when nb % size == 0 -- that
+     * write never reaches an output array, so it is skipped here. */
+    if (pos_is_warp) {
+        if (!exists(s, "GLOBAL_META", "BMT_size_of_each_blk", 0)) {
+            free(bit);
+            return fail(s, "GLOBAL BMT_size_of_each_blk missing: reference divides by zero (thread_bit_map.cc:56)");
+        }
+        uint64_t ts = FN->u[1] - FN->u[0];
+        for (uint64_t i = 0; i < nnz / ts + 1; i += (uint64_t)size)
+            if (i * ts < nnz) bit[i * ts] = 1;
+    }
+    /* thread_bit_map.cc:74-90: LSB = first nz of the BMT */
+    uint64_t *tbm = (uint64_t *)malloc(nb * 8);
+    for (uint64_t i = 0; i < nb; i++) {
+        uint64_t m = 0;
+        for (uint64_t j = FN->u[i + 1]; j-- > FN->u[i];) m = (m << 1) | bit[j];
+        tbm[i] = m;
+    }
+    free(bit);
+    put_u(s, "THREAD_META", "thread_bit_map", 0, tbm, nb);
+
+    /* segment_empty_flag.cc:14-75 */
+    unsigned char *flag = (unsigned char *)calloc(nb ? nb : 1, 1);
+    for (uint64_t j = 0; j < nb; j++) {
+        for (uint64_t i = FN->u[j] + 1; i < FN->u[j + 1]; i++)
+            if (R->u[i] - R->u[i - 1] > 1) { flag[j] = 1; break; }
+    }
+    vu sef = {0};
+    for (uint64_t i = 0; i < nb; i += (uint64_t)size) {
+        uint64_t k = (i + size - 1) > (nb - 1) ? (nb - 1) : (i + size - 1);
+        uint64_t cur = 0;
+        for (uint64_t j = k + 1; j-- > i;) cur = (cur << 1) | flag[j];
+        vu_push(&sef, cur);
+    }
+    free(flag);
+    put_u(s, "THREAD_META", "segment_empty_flag", 0, sef.p, sef.n);
+
+    /* segment_empty_row_indices.cc */
+    vu seri = {0};
+    for (uint64_t j = 0; j < nb; j++) {
+        uint64_t first_row = R->u[FN->u[j]];
+        vu_push(&seri, 0);
+        for (uint64_t i = FN->u[j] + 1; i < FN->u[j + 1]; i++)
+            if (R->u[i] != R->u[i - 1]) vu_push(&seri, R->u[i] - first_row);
+    }
+    put_u(s, "THREAD_META", "segment_empty_row_indices", 0, seri.p, seri.n);
+
+    /* segment_offset.cc (parent_flag=false as called from
+     * thread_bit_map_operator.cc:81): the count pending after the last
+     * non-empty bitmap is never written back (reference behaviour). */
+    uint64_t *so = (uint64_t *)calloc(nb ? nb : 1, 8);
+    uint64_t count = 0, prev = 0;
+    for (uint64_t j = 1; j < nb; j++) {
+        if (tbm[j] == 0) count++;
+        else { so[prev] = count; count = 0; prev = j; }
+    }
+    put_u(s, "THREAD_META", "segment_offset", 0, so, nb);
+
+    /* segment_ptr.cc: running count of row segments, one entry per BMT,
+     * the last BMT's segments are not counted */
+    vu sp = {0};
+    vu_push(&sp, 0);
+    uint64_t c = 0;
+    for (uint64_t j = 0; j + 2 < FN->len; j++) {
+        c += 1;
+        for (uint64_t i = FN->u[j] + 1; i < FN->u[j + 1]; i++)
+            if (R->u[i] != R->u[i - 1]) c += 1;
+        vu_push(&sp, c);
+    }
+    put_u(s, "THREAD_META", "segment_ptr", 0, sp.p, sp.n);
+    return 0;
+}
+
+/* warp_segment_reduce_operator.cc:74-111 with merge_num = VECTOR_WIDTH:
+ * get_begin_rows_after_merge_thread.cc, get_begin_nzs_after_merge_thread.cc,
+ * get_begin_BMTs_after_merge_thread.cc */
+int or_warp_segment_operator(or_set *s, int vw) {
+    or_array *TR = get(s, "THREAD_META", "first_row_indices", 0);
+    or_array *TN = get(s, "THREAD_META", "first_nz_indices", 0);
+    if (!TR || !TN || vw < 1) return fail(s, "warp_segment: missing THREAD arrays");
+    vu wr = {0}, wn = {0}, wb = {0};
+    for (uint64_t j = 0; j + 1 < TR->len; j += vw) vu_push(&wr, TR->u[j]);
+    vu_push(&wr, TR->u[TR->len - 1]);
+    for (uint64_t j = 0; j + 1 < TN->len; j += vw) vu_push(&wn, TN->u[j]);
+    vu_push(&wn, TN->u[TN->len - 1]);
+    for (uint64_t j = 0; j + 1 < TN->len; j += vw) vu_push(&wb, j);
+    vu_push(&wb, TN->len - 1);
+    put_u(s, "WARP_META", "first_row_indices", 0, wr.p, wr.n);
+    put_u(s, "WARP_META", "first_nz_indices", 0, wn.p, wn.n);
+    put_u(s, "WARP_META", "first_BMT_indices", 0, wb.p, wb.n);
+    return 0;
+}
+
+/* A11: balanced_interval_row_direction_warp_blocking_operator, no-parent
+ * branch; split points data_transform_common.cc:934-989 */
+int or_balanced_row_dir_warp_blocking(or_set *s, uint64_t per) {
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    uint64_t row_num = row_num_of(s);
+    uint64_t *cnt = row_nnz(R->u, R->len, row_num);
+    vu br = {0}, bn = {0};
+    vu_push(&br, 0);
+    uint64_t nzc = 0;
+    for (uint64_t i = 0; i < row_num; i++) {
+        nzc += cnt[i];
+        if (nzc >= per) { vu_push(&br, i + 1); nzc = 0; }
+    }
+    if (br.p[br.n - 1] < row_num) {
+        if (nzc == 0) { free(cnt); free(br.p); return fail(s, "trailing empty rows after last cut (data_transform_common.cc:984)"); }
+        vu_push(&br, row_num);
+    }
+    vu_push(&bn, 0);
+    uint32_t c32 = 0, tot32 = 0; /* `unsigned int` counters, :938-939 */
+    for (uint64_t i = 0; i < row_num; i++) {
+        c32 += (uint32_t)cnt[i]; tot32 += (uint32_t)cnt[i];
+        if (c32 >= per) { vu_push(&bn, tot32); c32 = 0; }
+    }
+    if (c32 != 0) vu_push(&bn, tot32);
+    free(cnt);
+    put_u(s, "WARP_META", "first_row_indices", 0, br.p, br.n);
+    put_u(s, "WARP_META", "first_nz_indices", 0, bn.p, bn.n);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* canned pipelines: token_test.cc test_spmm_*                          */
+/* ------------------------------------------------------------------ */
+
+int or_pipeline(or_set *s, const char *name, int p0, int p1) {
+    if (!strcmp(name, "thread_total")) { /* token_test.cc:1003-1092, p0 = sparse_cf */
+        if (or_sort_operator(s)) return -1;
+        return or_row_dir_thread_blocking(s, 1, p0);
+    }
+    if (!strcmp(name, "warp_total")) /* token_test.cc:1188-1249 */
+        return or_row_dir_warp_blocking(s, 1);
+    if (!strcmp(name, "block_total")) /* token_test.cc:1458-1514 */
+        return or_row_dir_tblock_blocking(s, 1);
+    if (!strcmp(name, "thread_bit_map")) { /* token_test.cc:1319-1391, p0 = VW */
+        if (or_nnz_dir_thread_blocking(s, 32, 1)) return -1;
+        return or_thread_bit_map_operator(s, 0, p0);
+    }
+    if (!strcmp(name, "warp_segment")) { /* token_test.cc:1393-1455, p0 = VW */
+        if (or_nnz_dir_thread_blocking(s, 32, 1)) return -1;
+        if (or_thread_bit_map_operator(s, 1, p0)) return -1;
+        return or_warp_segment_operator(s, p0);
+    }
+    if (!strcmp(name, "tblock_warp_total")) { /* tblock rows p0 + BMW rb=1 + warp_total */
+        if (or_row_dir_tblock_blocking(s, p0)) return -1;
+        return or_row_dir_warp_blocking(s, 1);
+    }
+    if (!strcmp(name, "balanced_warp_total")) /* A11 balanced BMW + warp_total */
+        return or_balanced_row_dir_warp_blocking(s, (uint64_t)p0);
+    return fail(s, "unknown pipeline %s", name);
+}
+
+/* ------------------------------------------------------------------ */
+/* A17: CPU SpMM references                                             */
+/* ------------------------------------------------------------------ */
+
+void or_spmm_f64(uint64_t M, uint64_t N, uint64_t nnz, const uint64_t *row,
+                 const uint64_t *col, const float *val, const double *B,
+                 double *C) {
+    memset(C, 0, M * N * sizeof(double));
+    for (uint64_t p = 0; p < nnz; p++) {
+        double v = val[p];
+        const double *b = B + col[p] * N;
+        double *c = C + row[p] * N;
+        for (uint64_t j = 0; j < N; j++) c[j] += v * b[j];
+    }
+}
+
+/* kernel_lib.hpp:859-881: per row, products added in CSR order */
+void or_spmm_ref_f32(uint64_t M, uint64_t N, uint64_t nnz, const uint64_t *row,
+                     const uint64_t *col, const float *val, const float *B,
+                     float *C) {
+    memset(C, 0, M * N * sizeof(float));
+    for (uint64_t p = 0; p < nnz; p++) {
+        float v = val[p];
+        const float *b = B + col[p] * N;
+        float *c = C + row[p] * N;
+        for (uint64_t j = 0; j < N; j++) c[j] += v * b[j];
+    }
+}
+
+/* IEEE binary16 round-to-nearest-even, via bit manipulation */
+float or_round_half(float x) {
+    union { float f; uint32_t u; } in = {x};
+    uint32_t u = in.u, sign = u & 0x80000000u;
+    uint32_t a = u & 0x7fffffffu;
+    if (a >= 0x7f800000u) return x; /* inf / nan */
+    float ax;
+    union { uint32_t u; float f; } t = {a};
+    ax = t.f;
+    if (ax >= 65520.0f) { union { uint32_t u; float f; } r = {sign | 0x7f800000u}; return r.f; }
+    if (ax < 6.103515625e-05f) { /* subnormal half: quantum 2^-24 */
+        float q = 5.9604644775390625e-08f;
+        float r = nearbyintf(ax / q) * q;
+        union { float f; uint32_t u; } o = {r};
+        o.u |= sign;
+        return o.f;
+    }
+    /* normal: keep 10 mantissa bits */
+    uint32_t lsb = (a >> 13) & 1u;
+    uint32_t rounded = (a + 0x0fffu + lsb) & ~0x1fffu;
+    union { uint32_t u; float f; } o = {rounded | sign};
+    return o.f;
+}
+
+void or_spmm_ref_f16(uint64_t M, uint64_t N, uint64_t nnz, const uint64_t *row,
+                     const uint64_t *col, const float *val, const float *B,
+                     float *C) {
+    memset(C, 0, M * N * sizeof(float));
+    for (uint64_t p = 0; p < nnz; p++) {
+        float v = or_round_half(val[p]);
+        const float *b = B + col[p] * N;
+        float *c = C + row[p] * N;
+        for (uint64_t j = 0; j < N; j++)
+            c[j] = or_round_half(c[j] + or_round_half(v * or_round_half(b[j])));
+    }
+}
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+int or_time_cpu_path(uint64_t M, uint64_t K, uint64_t nnz, const uint64_t *row,
+                     const uint64_t *col, const float *val, uint64_t N,
+                     double *t_transform, double *t_spmm) {
+    or_set s;
+    double t0 = now_s();
+    if (or_init_set(&s, M, K, nnz, row, col, val)) return -1;
+    if (or_pipeline(&s, "thread_total", 4, 0)) { or_set_free(&s); return -1; }
+    double t1 = now_s();
+    or_set_free(&s);
+    float *B = (float *)malloc(K * N * sizeof(float));
+    float *C = (float *)malloc(M * N * sizeof(float));
+    for (uint64_t i = 0; i < K * N; i++) B[i] = 1.0f;
+    double t2 = now_s();
+    or_spmm_ref_f32(M, N, nnz, row, col, val, B, C);
+    double t3 = now_s();
+    volatile float sink = C[0];
+    (void)sink;
+    free(B); free(C);
+    *t_transform = t1 - t0;
+    *t_spmm = t3 - t2;
+    return 0;
+}
