@@ -1,0 +1,202 @@
+"""generalsparse_amd -- MI355X-native SpMM (C = sparse_A x dense_B) behind
+GeneralSparse's operator / plan surface.
+
+Host-side mirror of the reference interface, over the C ABI of
+libgeneralsparse.so (include/generalsparse.h):
+
+    plan = Plan.from_mtx("m.mtx")                  # create_init_metadata_set_from_file
+    plan.add_operator("sort_operator")              # operator_executer::add_and_run
+    plan.add_operator("fixed_interval_row_direction_thread_blocking_operator",
+                      1, 0, 0, 0, 0, 1, 4)
+    plan.add_operator("thread_total_reduce_operator", 0, 4, 1)
+    plan.compile()                                  # code_generator::compile
+    plan.upload(dtype="f16")
+    C = plan.spmm(B)                                # the generated kernel, on the GPU
+
+or the canned token_test pipelines: plan.run_pipeline("warp_segment", N=32).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import GS_F16, GS_F32, GsError
+
+__all__ = ["Plan", "set_config", "GsError", "GS_F16", "GS_F32", "PIPELINES", "load_library"]
+
+# token_test.cc pipelines (+ the two compositions this engine adds)
+PIPELINES = ("thread_total", "warp_total", "block_total", "thread_bit_map", "warp_segment",
+             "tblock_warp_total", "balanced_warp_total")
+
+
+def load_library():
+    return _lib.load()
+
+
+def set_config(key, value):
+    """set_config (config.cc:17-40); process-wide, in memory."""
+    L = _lib.load()
+    _lib.check(L.gs_set_config_int(key.encode(), int(value)))
+
+
+def _dtype_code(dtype):
+    if dtype in (GS_F16, "f16", "fp16", "half", np.float16):
+        return GS_F16
+    if dtype in (GS_F32, "f32", "fp32", "float", np.float32):
+        return GS_F32
+    try:
+        import torch
+        if dtype == torch.float16:
+            return GS_F16
+        if dtype == torch.float32:
+            return GS_F32
+    except ImportError:
+        pass
+    raise ValueError(f"unsupported dtype {dtype}")
+
+
+class Plan:
+    """A GeneralSparse plan: metadata set + operator history + code generator +
+    device copies.  Wraps gs_plan_t."""
+
+    def __init__(self, handle):
+        self._h = ctypes.c_void_p(handle)
+        self._L = _lib.load()
+
+    # ---------------------------------------------------------------- create
+    @classmethod
+    def from_mtx(cls, path, ones_values=True):
+        """Reference reader semantics by default: every value := 1 (struct.cc:186-200)."""
+        L = _lib.load()
+        h = ctypes.c_void_p()
+        _lib.check(L.gs_plan_create_from_mtx(str(path).encode(), int(bool(ones_values)), ctypes.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def from_coo(cls, n_rows, n_cols, row, col, val=None):
+        L = _lib.load()
+        row = np.ascontiguousarray(row, dtype=np.uint64)
+        col = np.ascontiguousarray(col, dtype=np.uint64)
+        vp = None
+        if val is not None:
+            val = np.ascontiguousarray(val, dtype=np.float32)
+            vp = val.ctypes.data_as(_lib.f32p)
+        h = ctypes.c_void_p()
+        _lib.check(L.gs_plan_create_from_coo(int(n_rows), int(n_cols), len(row), row.ctypes.data_as(_lib.u64p),
+                                             col.ctypes.data_as(_lib.u64p), vp, ctypes.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def from_scipy(cls, A):
+        A = A.tocsr()
+        A.sort_indices()
+        coo = A.tocoo()
+        return cls.from_coo(A.shape[0], A.shape[1], coo.row, coo.col, coo.data)
+
+    # ------------------------------------------------------------ operators
+    def add_operator(self, name, *args):
+        arr = (ctypes.c_longlong * max(1, len(args)))(*[int(a) for a in args])
+        _lib.check(self._L.gs_plan_add_operator(self._h, name.encode(), arr, len(args)))
+        return self
+
+    def run_pipeline(self, name, N, p0=0, p1=0):
+        _lib.check(self._L.gs_plan_run_pipeline(self._h, name.encode(), int(N), int(p0), int(p1)))
+        return self
+
+    def compile(self):
+        _lib.check(self._L.gs_plan_compile(self._h))
+        return self
+
+    def generate_program(self, root, repeat=100):
+        buf = ctypes.create_string_buffer(4096)
+        _lib.check(self._L.gs_plan_generate_program(self._h, str(root).encode(), int(repeat), buf, 4096))
+        return buf.value.decode()
+
+    # --------------------------------------------------------------- device
+    def upload(self, dtype="f16", device=0):
+        self.dtype_code = _dtype_code(dtype)
+        _lib.check(self._L.gs_plan_upload(self._h, self.dtype_code, int(device)))
+        return self
+
+    def add_replica(self):
+        _lib.check(self._L.gs_plan_add_replica(self._h))
+
+    def spmm(self, B, C=None, replica=0, stream=None):
+        """C = A @ B on the GPU.  B: (K, N) torch tensor on the plan's device, in
+        the plan's dtype.  Enqueued on torch's current stream."""
+        import torch
+        assert B.is_cuda and B.dim() == 2 and B.is_contiguous()
+        info = self.info()
+        if B.shape[0] != info["cols"]:
+            raise ValueError(f"B has {B.shape[0]} rows, A has {info['cols']} columns")
+        want = torch.float16 if info["dtype"] == GS_F16 else torch.float32
+        if B.dtype != want:
+            raise TypeError(f"B must be {want}")
+        N = B.shape[1]
+        if C is None:
+            C = torch.empty((info["rows"], N), dtype=want, device=B.device)
+        s = stream if stream is not None else torch.cuda.current_stream(B.device).cuda_stream
+        _lib.check(self._L.gs_spmm_replica(self._h, int(replica), ctypes.c_void_p(B.data_ptr()),
+                                           ctypes.c_void_p(C.data_ptr()), int(N), ctypes.c_void_p(s)))
+        return C
+
+    def spmm_rotate(self, count, first, Bs, Cs, stream=None):
+        """`count` SpMMs from native code, rotating replicas and the (B, C) pairs."""
+        import torch
+        n = len(Bs)
+        bp = (ctypes.c_void_p * n)(*[b.data_ptr() for b in Bs])
+        cp = (ctypes.c_void_p * n)(*[c.data_ptr() for c in Cs])
+        s = stream if stream is not None else torch.cuda.current_stream(Bs[0].device).cuda_stream
+        _lib.check(self._L.gs_spmm_rotate(self._h, int(count), int(first), bp, cp, n, int(Bs[0].shape[1]),
+                                          ctypes.c_void_p(s)))
+
+    def spmm_raw(self, B_ptr, C_ptr, N, replica=0, stream=0):
+        _lib.check(self._L.gs_spmm_replica(self._h, int(replica), ctypes.c_void_p(B_ptr), ctypes.c_void_p(C_ptr),
+                                           int(N), ctypes.c_void_p(stream)))
+
+    # ------------------------------------------------------------ inspection
+    def info(self):
+        i = _lib.GsPlanInfo()
+        _lib.check(self._L.gs_plan_info_get(self._h, ctypes.byref(i)))
+        return {k: (getattr(i, k).decode() if k == "kernel_name" else getattr(i, k)) for k, _ in i._fields_}
+
+    def keys(self):
+        n = self._L.gs_plan_array_count(self._h)
+        out = []
+        buf = ctypes.create_string_buffer(256)
+        for i in range(n):
+            _lib.check(self._L.gs_plan_array_key(self._h, i, buf, 256))
+            out.append(buf.value.decode())
+        return out
+
+    def array(self, key):
+        k = key.encode()
+        n = self._L.gs_plan_array_len(self._h, k)
+        if n < 0:
+            raise KeyError(key)
+        if self._L.gs_plan_array_is_float(self._h, k) == 1:
+            a = np.zeros(n, np.float64)
+            _lib.check(self._L.gs_plan_array_read_f64(self._h, k, a.ctypes.data_as(_lib.f64p), n))
+        else:
+            a = np.zeros(n, np.uint64)
+            _lib.check(self._L.gs_plan_array_read_u64(self._h, k, a.ctypes.data_as(_lib.u64p), n))
+        return a
+
+    def arrays(self):
+        return {k: self.array(k) for k in self.keys()}
+
+    def log(self):
+        buf = ctypes.create_string_buffer(1 << 16)
+        _lib.check(self._L.gs_plan_log(self._h, buf, 1 << 16))
+        return buf.value.decode()
+
+    def free(self):
+        if self._h is not None and self._h.value:
+            self._L.gs_plan_free(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

@@ -1,0 +1,426 @@
+// hip_code/kernel_lib.hpp -- hand-written gfx950 (MI355X, CDNA4) SpMM kernel families.
+//
+// Replaces cuda_code/kernel_lib.hpp of the reference (Load()/__ldg helpers,
+// kernel_lib.hpp:1006-1148) and the kernels its reduction tokens print
+// (SURVEY.md §2.2 K1-K7).  C = A * B, B row-major K x N, C row-major M x N.
+// Written for 64-lane waves: a wave is split into S = 64/X "slots" of X column
+// lanes; every lane owns CF consecutive dense columns (one 16-byte load of a B
+// row segment when CF*sizeof(VT) == 16).  A (cols/vals) is streamed once,
+// vector-loaded; B rows are gathered through L1/L2 (B is small and shared).
+// Accumulation is always fp32 (the reference accumulates fp16 in half).
+//
+// Families (selected by code_generator::compile from the reduction tokens):
+//   k_thread_total   K1: X lanes per BMT row, rows sorted + col-padded (SCF-aligned)
+//   k_warp_rows      K4: one wave per BMW, nnz split over S slots, xor-shuffle reduce
+//                       (+ optional BMTB grouping = one workgroup per BMTB)
+//   k_block_rows     K6: one 256-thread workgroup per BMTB, wave reduce + LDS reduce
+//   k_bitmap_segment K2+K3: fixed 32-nnz BMTs, row segments from bitmaps, open
+//                       head/tail partials combined per wave, then atomics
+#pragma once
+
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gsk {
+
+typedef _Float16 f16;
+
+template <int BYTES> struct raw_vec;
+template <> struct raw_vec<2> { typedef uint16_t t; };
+template <> struct raw_vec<4> { typedef uint32_t t; };
+template <> struct raw_vec<8> { typedef uint2 t; };
+template <> struct raw_vec<16> { typedef uint4 t; };
+
+// CF contiguous values -> fp32 (one vector load)
+template <class VT, int CF>
+__device__ __forceinline__ void load_f32(const VT *__restrict__ p, float (&out)[CF]) {
+    typedef typename raw_vec<CF * sizeof(VT)>::t R;
+    R r = *reinterpret_cast<const R *>(p);
+    VT tmp[CF];
+    __builtin_memcpy(tmp, &r, sizeof(R));
+#pragma unroll
+    for (int k = 0; k < CF; k++) out[k] = (float)tmp[k];
+}
+
+template <class VT, int CF>
+__device__ __forceinline__ void store_f32(VT *__restrict__ p, const float (&in)[CF]) {
+    typedef typename raw_vec<CF * sizeof(VT)>::t R;
+    VT tmp[CF];
+#pragma unroll
+    for (int k = 0; k < CF; k++) tmp[k] = (VT)in[k];
+    R r;
+    __builtin_memcpy(&r, tmp, sizeof(R));
+    *reinterpret_cast<R *>(p) = r;
+}
+
+// SCF contiguous sparse entries (cols or vals) in one load
+template <class T, int SCF>
+__device__ __forceinline__ void load_raw(const T *__restrict__ p, T (&out)[SCF]) {
+    typedef typename raw_vec<SCF * sizeof(T)>::t R;
+    R r = *reinterpret_cast<const R *>(p);
+    __builtin_memcpy(out, &r, sizeof(R));
+}
+
+template <int CF>
+__device__ __forceinline__ void wave_reduce_slots(float (&acc)[CF], int X) {
+    for (int off = X; off < 64; off <<= 1) {
+#pragma unroll
+        for (int k = 0; k < CF; k++) acc[k] += __shfl_xor(acc[k], off, 64);
+    }
+}
+
+template <class VT, int CF>
+__device__ __forceinline__ void atomic_add_vals(VT *p, const float (&v)[CF]);
+
+template <>
+__device__ __forceinline__ void atomic_add_vals<float, 1>(float *p, const float (&v)[1]) {
+    unsafeAtomicAdd(p, v[0]);
+}
+template <>
+__device__ __forceinline__ void atomic_add_vals<float, 4>(float *p, const float (&v)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) unsafeAtomicAdd(p + k, v[k]);
+}
+template <>
+__device__ __forceinline__ void atomic_add_vals<f16, 8>(f16 *p, const float (&v)[8]) {
+#pragma unroll
+    for (int k = 0; k < 8; k += 2) {
+        __half2 h = __floats2half2_rn(v[k], v[k + 1]);
+        unsafeAtomicAdd(reinterpret_cast<__half2 *>(p + k), h);
+    }
+}
+template <>
+__device__ __forceinline__ void atomic_add_vals<f16, 1>(f16 *p, const float (&v)[1]) {
+    unsafeAtomicAdd(reinterpret_cast<__half *>(p), __float2half(v[0]));
+}
+
+// one sparse entry times a CF-wide B segment
+template <class VT, int CF>
+__device__ __forceinline__ void fma_row(float (&acc)[CF], float v, const VT *__restrict__ brow) {
+    float b[CF];
+    load_f32<VT, CF>(brow, b);
+#pragma unroll
+    for (int k = 0; k < CF; k++) acc[k] = __builtin_fmaf(v, b[k], acc[k]);
+}
+
+// ---------------------------------------------------------------------------
+// K1 thread_total: the row-sorted, col-padded plan (sort_operator +
+// fixed_interval_row_direction_thread_blocking_operator(1,...,scf) +
+// thread_total_reduce_operator).  BMT b covers sorted row b; X lanes own its
+// dense columns; the row's nnz are walked SCF at a time with one vector load
+// of cols and one of vals (the reference's Load() of col4/val4,
+// total_BMT_result_reduce_to_one_register_token.cc:807-898).  Sorted rows
+// b >= n_bmt are the trailing empty rows: their C rows are zero-filled here
+// instead of relying on a memset.
+// ---------------------------------------------------------------------------
+template <class VT, class CT, int CF, int SCF>
+__global__ __launch_bounds__(256) void k_thread_total(const uint32_t *__restrict__ first_nz,  // n_bmt+1
+                                                      const uint32_t *__restrict__ order,     // n_rows: sorted->orig
+                                                      const CT *__restrict__ col, const VT *__restrict__ val,
+                                                      const VT *__restrict__ B, VT *__restrict__ C, uint32_t n_bmt,
+                                                      uint32_t n_rows, uint32_t N, uint32_t X, uint32_t row_base) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t xl = lane & (X - 1u);
+    const uint32_t groups_per_block = blockDim.x / X;
+    const uint32_t g = blockIdx.x * groups_per_block + threadIdx.x / X;
+    const uint32_t stride = gridDim.x * groups_per_block;
+    for (uint32_t ct = blockIdx.y; ct * X * CF < N; ct += gridDim.y) {
+        const uint32_t cw = ct * X * CF + xl * CF;
+        const bool cok = cw < N;
+        const uint32_t c0 = cok ? cw : 0u;
+        for (uint32_t rr = g; rr < n_rows; rr += stride) {
+            float acc[CF];
+#pragma unroll
+            for (int k = 0; k < CF; k++) acc[k] = 0.f;
+            if (rr < n_bmt) {
+                const uint32_t b = first_nz[rr], e = first_nz[rr + 1];
+                for (uint32_t p = b; p < e; p += SCF) {
+                    CT cc[SCF];
+                    VT vv[SCF];
+                    load_raw<CT, SCF>(col + p, cc);
+                    load_raw<VT, SCF>(val + p, vv);
+#pragma unroll
+                    for (int j = 0; j < SCF; j++) fma_row<VT, CF>(acc, (float)vv[j], B + (size_t)cc[j] * N + c0);
+                }
+            }
+            if (cok) store_f32<VT, CF>(C + (size_t)(order[rr] + row_base) * N + c0, acc);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K4 warp_total over BMWs (fixed_interval_row_direction_warp_blocking_operator
+// or balanced_interval_row_direction_warp_blocking_operator, optionally inside
+// BMTBs) + warp_total_reduce_operator.  One wave per BMW; the BMW's rows are
+// processed in order; each row's nnz are split over the S = 64/X slots in
+// SCF-aligned chunks (row_ptr is padded so the aligned over-read stays in
+// bounds and is masked), then reduced with xor shuffles.  With a BMTB level,
+// workgroup g owns BMWs [bmw_of_bmtb[g], bmw_of_bmtb[g+1]) and its waves stride
+// over them (keeps a BMTB's rows on one CU / XCD).
+// ---------------------------------------------------------------------------
+template <class VT, class CT, int CF, int SCF>
+__device__ __forceinline__ void wave_row(const uint32_t b, const uint32_t e, const CT *__restrict__ col,
+                                         const VT *__restrict__ val, const VT *__restrict__ B, uint32_t N,
+                                         uint32_t c0, uint32_t slot, uint32_t S, float (&acc)[CF]) {
+    const uint32_t a = b & ~(uint32_t)(SCF - 1);
+    for (uint32_t p0 = a + slot * SCF; p0 < e; p0 += S * SCF) {
+        CT cc[SCF];
+        VT vv[SCF];
+        load_raw<CT, SCF>(col + p0, cc);
+        load_raw<VT, SCF>(val + p0, vv);
+#pragma unroll
+        for (int j = 0; j < SCF; j++) {
+            const uint32_t p = p0 + j;
+            if (p >= b && p < e) fma_row<VT, CF>(acc, (float)vv[j], B + (size_t)cc[j] * N + c0);
+        }
+    }
+}
+
+template <class VT, class CT, int CF, int SCF>
+__global__ __launch_bounds__(256) void k_warp_rows(const uint32_t *__restrict__ bmw_first_row,  // n_bmw+1
+                                                   const uint32_t *__restrict__ bmw_of_bmtb,    // n_bmtb+1 or null
+                                                   const uint32_t *__restrict__ row_ptr,        // rows+1 (CSR)
+                                                   const CT *__restrict__ col, const VT *__restrict__ val,
+                                                   const VT *__restrict__ B, VT *__restrict__ C, uint32_t n_bmw,
+                                                   uint32_t N, uint32_t X, uint32_t row_base) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t xl = lane & (X - 1u);
+    const uint32_t slot = lane / X;
+    const uint32_t S = 64u / X;
+    const uint32_t wib = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    uint32_t w_begin, w_end, w_step;
+    if (bmw_of_bmtb) {
+        w_begin = bmw_of_bmtb[blockIdx.x] + wib;
+        w_end = bmw_of_bmtb[blockIdx.x + 1];
+        w_step = wpb;
+    } else {
+        w_begin = blockIdx.x * wpb + wib;
+        w_end = n_bmw;
+        w_step = gridDim.x * wpb;
+    }
+    for (uint32_t ct = blockIdx.y; ct * X * CF < N; ct += gridDim.y) {
+        const uint32_t cw = ct * X * CF + xl * CF;
+        const bool cok = cw < N;
+        const uint32_t c0 = cok ? cw : 0u;
+        for (uint32_t w = w_begin; w < w_end; w += w_step) {
+            const uint32_t r_end = bmw_first_row[w + 1];
+            for (uint32_t r = bmw_first_row[w]; r < r_end; r++) {
+                float acc[CF];
+#pragma unroll
+                for (int k = 0; k < CF; k++) acc[k] = 0.f;
+                wave_row<VT, CT, CF, SCF>(row_ptr[r], row_ptr[r + 1], col, val, B, N, c0, slot, S, acc);
+                wave_reduce_slots<CF>(acc, (int)X);
+                if (slot == 0 && cok) store_f32<VT, CF>(C + (size_t)(r + row_base) * N + c0, acc);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K6 tblock_total: one 256-thread workgroup per BMTB (fixed row-direction
+// TBLOCK blocking + tblock_total_reduce_operator).  All four waves split each
+// row's nnz (4*S slots), reduce in registers, then across waves through LDS
+// (total_block_reduce_to_one_register_token.cc:374-480 reduces over
+// blockDim.y with __syncthreads; here one LDS round of 4 partials).
+// ---------------------------------------------------------------------------
+template <class VT, class CT, int CF, int SCF>
+__global__ __launch_bounds__(256) void k_block_rows(const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
+                                                    const uint32_t *__restrict__ row_ptr,
+                                                    const CT *__restrict__ col, const VT *__restrict__ val,
+                                                    const VT *__restrict__ B, VT *__restrict__ C, uint32_t n_bmtb,
+                                                    uint32_t N, uint32_t X, uint32_t row_base) {
+    __shared__ float part[4][64][CF];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wib = threadIdx.x >> 6;
+    const uint32_t xl = lane & (X - 1u);
+    const uint32_t S = 64u / X;
+    const uint32_t slot = wib * S + lane / X;  // 0 .. 4S-1
+    for (uint32_t ct = blockIdx.y; ct * X * CF < N; ct += gridDim.y) {
+        const uint32_t cw = ct * X * CF + xl * CF;
+        const bool cok = cw < N;
+        const uint32_t c0 = cok ? cw : 0u;
+        for (uint32_t t = blockIdx.x; t < n_bmtb; t += gridDim.x) {
+            const uint32_t r_end = bmtb_first_row[t + 1];
+            for (uint32_t r = bmtb_first_row[t]; r < r_end; r++) {
+                float acc[CF];
+#pragma unroll
+                for (int k = 0; k < CF; k++) acc[k] = 0.f;
+                wave_row<VT, CT, CF, SCF>(row_ptr[r], row_ptr[r + 1], col, val, B, N, c0, slot, 4 * S, acc);
+                wave_reduce_slots<CF>(acc, (int)X);
+                if (lane < X) {
+#pragma unroll
+                    for (int k = 0; k < CF; k++) part[wib][lane][k] = acc[k];
+                }
+                __syncthreads();
+                if (wib == 0 && lane < X && cok) {
+#pragma unroll
+                    for (int k = 0; k < CF; k++) acc[k] = part[0][lane][k] + part[1][lane][k] + part[2][lane][k] + part[3][lane][k];
+                    store_f32<VT, CF>(C + (size_t)(r + row_base) * N + c0, acc);
+                }
+                __syncthreads();
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K2 + K3 bitmap segments (fixed_interval_nnz_direction_thread_blocking_operator
+// (32) + thread_bit_map_operator (+ warp_segment_reduce_operator)).  Slot s of
+// wave w walks BMT w*S+s.  Row starts come from the BMT's row-start mask (the
+// plan's thread_bit_map without the forced BMW heads, thread_bit_map.cc:45-71),
+// segment rows from segment_ptr + segment_empty_row_indices
+// (segment_ptr.cc / segment_empty_row_indices.cc).  Segments that start and
+// end inside the BMT are complete and stored; the open head/tail partials of
+// the wave's slots are merged in slot order through LDS (the K3 segmented
+// combine, warp_segment_reduce_token.cc:26-444) and added with one atomic per
+// row run.  C must be zeroed first.
+// ---------------------------------------------------------------------------
+template <class VT, class CT, int CF, int SCF>
+__global__ __launch_bounds__(256) void k_bitmap_segment(const uint32_t *__restrict__ bmt_first_nz,   // n_bmt+1
+                                                        const uint32_t *__restrict__ bmt_first_row,  // n_bmt+1
+                                                        const uint64_t *__restrict__ row_start_mask, // n_bmt
+                                                        const uint32_t *__restrict__ seg_ptr,        // n_bmt
+                                                        const uint32_t *__restrict__ seg_row_off,    // segments
+                                                        const CT *__restrict__ col, const VT *__restrict__ val,
+                                                        const VT *__restrict__ B, VT *__restrict__ C, uint32_t n_bmt,
+                                                        uint32_t N, uint32_t X, uint32_t row_base) {
+    // per wave: up to 2 open partials per slot (head, tail), S <= 64
+    __shared__ uint32_t open_row[4][64][2];
+    extern __shared__ float dyn[];  // [4 waves][S slots][2][X lanes][CF]
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wib = threadIdx.x >> 6;
+    const uint32_t xl = lane & (X - 1u);
+    const uint32_t slot = lane / X;
+    const uint32_t S = 64u / X;
+    float *my_dyn = dyn + (size_t)wib * S * 2 * X * CF;
+    const uint32_t waves_total = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t ct = blockIdx.y; ct * X * CF < N; ct += gridDim.y) {
+        const uint32_t cw = ct * X * CF + xl * CF;
+        const bool cok = cw < N;
+        const uint32_t c0 = cok ? cw : 0u;
+        for (uint32_t w = blockIdx.x * (blockDim.x >> 6) + wib; w * S < n_bmt; w += waves_total) {
+            const uint32_t bt = w * S + slot;
+            uint32_t head_row = 0xffffffffu, tail_row = 0xffffffffu;
+            float head_acc[CF], acc[CF];
+#pragma unroll
+            for (int k = 0; k < CF; k++) { acc[k] = 0.f; head_acc[k] = 0.f; }
+            if (bt < n_bmt) {
+                const uint32_t b = bmt_first_nz[bt], e = bmt_first_nz[bt + 1];
+                const uint64_t mask = row_start_mask[bt];
+                const bool next_continues = (bt + 1 < n_bmt) && !(row_start_mask[bt + 1] & 1ull);
+                const uint32_t r0 = bmt_first_row[bt];
+                const uint32_t sbase = seg_ptr[bt];
+                uint32_t seg = 0, cur_row = r0;
+                bool cur_open_head = !(mask & 1ull);
+                for (uint32_t p0 = b; p0 < e; p0 += SCF) {
+                    CT cc[SCF];
+                    VT vv[SCF];
+                    load_raw<CT, SCF>(col + p0, cc);
+                    load_raw<VT, SCF>(val + p0, vv);
+#pragma unroll
+                    for (int j = 0; j < SCF; j++) {
+                        const uint32_t i = p0 + j - b;
+                        if (i > 0 && ((mask >> i) & 1ull)) {  // a new row starts: flush the current segment
+                            if (cur_open_head) {
+                                head_row = cur_row;
+#pragma unroll
+                                for (int k = 0; k < CF; k++) head_acc[k] = acc[k];
+                            } else if (cok) {
+                                store_f32<VT, CF>(C + (size_t)(cur_row + row_base) * N + c0, acc);
+                            }
+#pragma unroll
+                            for (int k = 0; k < CF; k++) acc[k] = 0.f;
+                            seg++;
+                            cur_row = r0 + seg_row_off[sbase + seg];
+                            cur_open_head = false;
+                        }
+                        fma_row<VT, CF>(acc, (float)vv[j], B + (size_t)cc[j] * N + c0);
+                    }
+                }
+                // last segment
+                if (cur_open_head || next_continues) {
+                    if (cur_open_head && !next_continues) {
+                        head_row = cur_row;
+#pragma unroll
+                        for (int k = 0; k < CF; k++) head_acc[k] = acc[k];
+                    } else {
+                        tail_row = cur_row;  // open at the tail (and maybe at the head too)
+                        if (cur_open_head) head_row = 0xffffffffu;
+                    }
+                } else if (cok) {
+                    store_f32<VT, CF>(C + (size_t)(cur_row + row_base) * N + c0, acc);
+                }
+            }
+            // publish open partials: [slot][0] = head, [slot][1] = tail
+            if (xl == 0) {
+                open_row[wib][slot][0] = head_row;
+                open_row[wib][slot][1] = tail_row;
+            }
+            float *hp = my_dyn + ((size_t)(slot * 2 + 0) * X + xl) * CF;
+            float *tp = my_dyn + ((size_t)(slot * 2 + 1) * X + xl) * CF;
+#pragma unroll
+            for (int k = 0; k < CF; k++) { hp[k] = head_acc[k]; tp[k] = acc[k]; }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            // slot 0's lanes merge the 2S open partials in order, one atomic per row run
+            if (slot == 0 && cok) {
+                uint32_t run_row = 0xffffffffu;
+                float run[CF];
+#pragma unroll
+                for (int k = 0; k < CF; k++) run[k] = 0.f;
+                for (uint32_t q = 0; q < 2 * S; q++) {
+                    const uint32_t r = open_row[wib][q >> 1][q & 1];
+                    if (r == 0xffffffffu) continue;
+                    const float *src = my_dyn + ((size_t)q * X + xl) * CF;
+                    if (r != run_row) {
+                        if (run_row != 0xffffffffu)
+                            atomic_add_vals<VT, CF>(C + (size_t)(run_row + row_base) * N + c0, run);
+                        run_row = r;
+#pragma unroll
+                        for (int k = 0; k < CF; k++) run[k] = src[k];
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < CF; k++) run[k] += src[k];
+                    }
+                }
+                if (run_row != 0xffffffffu) atomic_add_vals<VT, CF>(C + (size_t)(run_row + row_base) * N + c0, run);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+}  // namespace gsk
+
+// ---------------------------------------------------------------------------
+// Host-side helpers shared by the library (kernels/device_plan.hip) and the
+// programs code_generator emits: the kernel-side layouts derived from plan
+// arrays.
+// ---------------------------------------------------------------------------
+#include <vector>
+
+namespace gsk_host {
+
+// CSR row pointer (u32) of a row-sorted COO row array
+inline std::vector<uint32_t> csr_row_ptr(const std::vector<uint64_t> &row, uint64_t row_num) {
+    std::vector<uint32_t> rp(row_num + 1, 0);
+    for (uint64_t r : row) rp[r + 1]++;
+    for (uint64_t i = 0; i < row_num; i++) rp[i + 1] += rp[i];
+    return rp;
+}
+
+// per fixed-nnz BMT, bit i set iff its i-th nz starts a row (no forced BMW heads)
+inline std::vector<uint64_t> row_start_masks(const std::vector<uint64_t> &row, const std::vector<uint64_t> &first_nz) {
+    std::vector<uint64_t> mask(first_nz.size() - 1, 0);
+    for (size_t i = 0; i + 1 < first_nz.size(); i++) {
+        uint64_t mm = 0;
+        for (uint64_t j = first_nz[i]; j < first_nz[i + 1]; j++)
+            if (j == 0 || row[j] != row[j - 1]) mm |= 1ull << (j - first_nz[i]);
+        mask[i] = mm;
+    }
+    return mask;
+}
+
+}  // namespace gsk_host

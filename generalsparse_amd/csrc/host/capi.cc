@@ -1,0 +1,345 @@
+// capi.cc -- extern "C" boundary (include/generalsparse.h) + the token_test pipelines.
+#include "../../../include/generalsparse.h"
+#include "gs_plan.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+struct gs_plan {
+    gs::plan_state st;
+};
+
+namespace {
+thread_local std::string g_err;
+
+template <class F>
+int guard(F &&f) {
+    try {
+        f();
+        return GS_OK;
+    } catch (const gs::gs_error &e) {
+        g_err = e.what();
+        return e.code < 0 ? e.code : GS_ERR;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return GS_ERR;
+    }
+}
+
+void init_plan(gs::plan_state &s, std::shared_ptr<gs::meta_data_set> m) {
+    s.meta = std::move(m);
+    s.cg = std::make_shared<gs::code_generator>(s.meta, 0);
+    s.exec = std::make_shared<gs::operator_executer>();
+    s.M = s.meta->scalar(gs::GLOBAL_META, "origin_row_num", -1);
+    s.K = s.meta->scalar(gs::GLOBAL_META, "origin_col_num", -1);
+    s.nnz = s.meta->scalar(gs::GLOBAL_META, "origin_nnz_num", -1);
+}
+
+uint64_t global_scalar(const gs::plan_state &s, const char *n, int sub) { return s.meta->scalar(gs::GLOBAL_META, n, sub); }
+
+}  // namespace
+
+namespace gs {
+
+// token_test.cc:1003-1582 -- the reference's end-to-end pipelines, same operators,
+// same parameters and the same VECTOR_WIDTH / block rules.
+void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1) {
+    set_config("DENSE_MATRIX_SIZE", N);
+    auto cg = s.cg;
+    auto &ex = *s.exec;
+    auto ctx = ex.get_operator_context();
+    const uint64_t rows = global_scalar(s, "origin_row_num", -1);
+    const uint64_t nnz = global_scalar(s, "origin_nnz_num", -1);
+    if (name == "thread_total") {  // token_test.cc:1003-1092, p0 = sparse_cf (4), p1 = cf (1)
+        int scf = p0 > 0 ? p0 : 4, cf = p1 > 0 ? p1 : 1;
+        ex.add_and_run(std::make_shared<sort_operator>(cg, ctx));
+        ex.add_and_run(std::make_shared<fixed_interval_row_direction_thread_blocking_operator>(
+            cg, 1, false, false, false, false, true, scf, ctx));
+        int x = N / cf < 32 ? N / cf : 32;
+        set_config("VECTOR_WIDTH", x);
+        int y = 128 / std::max(1, x);
+        ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, false, scf, cf, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)(rows / y + 1),
+                                                             std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
+    } else if (name == "warp_total") {  // token_test.cc:1188-1249
+        int cf = p1 > 0 ? p1 : 1;
+        ex.add_and_run(std::make_shared<fixed_interval_row_direction_warp_blocking_operator>(cg, 1, false, false, false, ctx));
+        int y = std::min(N / cf, 32), x = std::max(256 / std::max(1, y), 32);
+        set_config("VECTOR_WIDTH", x);
+        ex.add_and_run(std::make_shared<warp_total_reduce_operator>(cg, cf, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)rows, std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
+    } else if (name == "thread_bit_map") {  // token_test.cc:1319-1391
+        int scf = p0 > 0 ? p0 : 4, cf = p1 > 0 ? p1 : 1;
+        ex.add_and_run(std::make_shared<fixed_interval_nnz_direction_thread_blocking_operator>(cg, 32, false, false, true, ctx));
+        int x = N / cf < 32 ? N / cf : 32;
+        set_config("VECTOR_WIDTH", x);
+        int y = 128 / std::max(1, x);
+        cg->open_spec_level_of_paral(THREAD_META);
+        ex.add_and_run(std::make_shared<thread_bit_map_operator>(cg, THREAD_META, (unsigned)x, (unsigned)scf, (unsigned)cf, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)(nnz / y + 1),
+                                                             std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
+    } else if (name == "warp_segment") {  // token_test.cc:1393-1455
+        int scf = p0 > 0 ? p0 : 4, cf = p1 > 0 ? p1 : 1;
+        ex.add_and_run(std::make_shared<fixed_interval_nnz_direction_thread_blocking_operator>(cg, 32, false, false, true, ctx));
+        int x = std::min(N, 32), y = 256 / std::max(1, x);
+        set_config("VECTOR_WIDTH", x);
+        ex.add_and_run(std::make_shared<thread_bit_map_operator>(cg, WARP_META, (unsigned)get_config().VECTOR_WIDTH,
+                                                                 (unsigned)scf, (unsigned)cf, ctx));
+        ex.add_and_run(std::make_shared<warp_segment_reduce_operator>(cg, (unsigned)cf, false, false, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)(nnz / 128 + 1),
+                                                             std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
+    } else if (name == "block_total") {  // token_test.cc:1458-1514
+        int cf = p1 > 0 ? p1 : 1;
+        ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, 1, false, ctx));
+        int x = std::min(N, 32), y = 256 / std::max(1, x);
+        set_config("VECTOR_WIDTH", x);
+        ex.add_and_run(std::make_shared<tblock_total_reduce_operator>(cg, cf, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)rows, std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
+    } else if (name == "tblock_warp_total") {
+        // headline plan (BASELINE.json configs[1]): row-direction BMTB blocking,
+        // one BMW per row inside each BMTB, wave-level reduction
+        int rb = p0 > 0 ? p0 : 4, cf = p1 > 0 ? p1 : 1;
+        ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, rb, false, ctx));
+        ex.add_and_run(std::make_shared<fixed_interval_row_direction_warp_blocking_operator>(cg, 1, false, false, false, ctx));
+        ex.add_and_run(std::make_shared<warp_total_reduce_operator>(cg, cf, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)((rows + rb - 1) / rb),
+                                                             std::vector<unsigned>{64u, 4u}, cf, ctx));
+    } else if (name == "balanced_warp_total") {
+        // balanced row-direction BMWs (A11) + warp_total (the valid composition)
+        int per = p0 > 0 ? p0 : 2048, cf = p1 > 0 ? p1 : 1;
+        ex.add_and_run(std::make_shared<balanced_interval_row_direction_warp_blocking_operator>(cg, per, false, false, ctx));
+        ex.add_and_run(std::make_shared<warp_total_reduce_operator>(cg, cf, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, 1024u, std::vector<unsigned>{64u, 4u}, cf, ctx));
+    } else {
+        throw gs_error("unknown pipeline " + name, GS_ERR_ARG);
+    }
+    s.pipeline = name;
+}
+
+}  // namespace gs
+
+extern "C" {
+
+const char *gs_last_error(void) { return g_err.c_str(); }
+const char *gs_version(void) { return "generalsparse_amd 0.1 (gfx950)"; }
+
+void gs_opts_default(gs_opts *o) {
+    o->pipeline = "tblock_warp_total";
+    o->dtype = GS_F16;
+    o->dense_n = 32;
+    o->p0 = 0;
+    o->p1 = 0;
+    o->ones_values = 0;
+    o->device = 0;
+}
+
+int gs_plan_create_from_mtx(const char *path, int ones_values, gs_plan_t **out) {
+    return guard([&] {
+        GS_CHECK(path && out, "null argument");
+        auto *p = new gs_plan;
+        try {
+            init_plan(p->st, gs::create_init_metadata_set_from_file(path, path, ones_values != 0));
+        } catch (...) {
+            delete p;
+            throw;
+        }
+        *out = p;
+    });
+}
+
+int gs_plan_create_from_coo(uint64_t n_rows, uint64_t n_cols, uint64_t nnz, const uint64_t *row, const uint64_t *col,
+                            const float *val, gs_plan_t **out) {
+    return guard([&] {
+        GS_CHECK(row && col && out, "null argument");
+        auto *p = new gs_plan;
+        try {
+            init_plan(p->st, gs::create_init_metadata_set_from_coo(n_rows, n_cols, nnz, row, col, val, "coo"));
+        } catch (...) {
+            delete p;
+            throw;
+        }
+        *out = p;
+    });
+}
+
+int gs_set_config_int(const char *key, long long value) {
+    return guard([&] { gs::set_config(key, value); });
+}
+
+int gs_plan_add_operator(gs_plan_t *p, const char *op_name, const long long *args, int nargs) {
+    return guard([&] {
+        GS_CHECK(p && op_name && (nargs == 0 || args), "null argument");
+        std::vector<long long> a(args, args + nargs);
+        auto op = gs::make_operator(op_name, a, p->st.cg, p->st.exec->get_operator_context());
+        p->st.exec->add_and_run(op);
+    });
+}
+
+int gs_plan_run_pipeline(gs_plan_t *p, const char *name, int dense_n, int p0, int p1) {
+    return guard([&] {
+        GS_CHECK(p && name && dense_n > 0, "bad argument");
+        gs::run_pipeline(p->st, name, dense_n, p0, p1);
+    });
+}
+
+int gs_plan_compile(gs_plan_t *p) {
+    return guard([&] {
+        GS_CHECK(p, "null plan");
+        p->st.cg->compile();
+    });
+}
+
+int gs_plan_generate_program(gs_plan_t *p, const char *root_dir, int repeat, char *dir_out, int dir_out_len) {
+    return guard([&] {
+        GS_CHECK(p && root_dir, "null argument");
+        std::string dir;
+        p->st.cg->generate_final_program(repeat, root_dir, &dir);
+        if (dir_out && dir_out_len > 0) {
+            std::strncpy(dir_out, dir.c_str(), dir_out_len - 1);
+            dir_out[dir_out_len - 1] = 0;
+        }
+    });
+}
+
+int gs_plan_upload(gs_plan_t *p, int dtype, int device) {
+    return guard([&] {
+        GS_CHECK(p, "null plan");
+        gs::upload_plan(p->st, dtype, device);
+    });
+}
+
+int gs_plan_add_replica(gs_plan_t *p) {
+    return guard([&] {
+        GS_CHECK(p, "null plan");
+        gs::add_replica(p->st);
+    });
+}
+
+int gs_spmm_replica(gs_plan_t *p, int replica, const void *B, void *C, int N, gs_stream_t stream) {
+    return guard([&] {
+        GS_CHECK(p && B && C && N > 0, "bad argument");
+        gs::launch_spmm(p->st, replica, B, C, (uint32_t)N, (hipStream_t)stream);
+    });
+}
+
+int gs_spmm_rotate(gs_plan_t *p, int count, int first, const void *const *B_ptrs, void *const *C_ptrs, int n_ptrs,
+                   int N, gs_stream_t stream) {
+    return guard([&] {
+        GS_CHECK(p && B_ptrs && C_ptrs && n_ptrs > 0 && N > 0 && count >= 0, "bad argument");
+        const int reps = (int)p->st.dev.replicas.size();
+        GS_CHECK(reps > 0, "plan is not on the device");
+        for (int i = 0; i < count; i++) {
+            int k = first + i;
+            gs::launch_spmm(p->st, k % reps, B_ptrs[k % n_ptrs], C_ptrs[k % n_ptrs], (uint32_t)N, (hipStream_t)stream);
+        }
+    });
+}
+
+int gs_spmm(gs_plan_t *p, const void *B, void *C, int N, gs_stream_t stream) {
+    return gs_spmm_replica(p, 0, B, C, N, stream);
+}
+
+int gs_plan_info_get(gs_plan_t *p, gs_plan_info *info) {
+    return guard([&] {
+        GS_CHECK(p && info, "null argument");
+        std::memset(info, 0, sizeof(*info));
+        auto &s = p->st;
+        info->rows = s.M;
+        info->cols = s.K;
+        info->nnz = s.nnz;
+        info->nnz_stored = s.meta->u(gs::GLOBAL_META, "nz_col_indices", 0).size();
+        if (s.cg->is_compiled()) {
+            const auto &sp = s.cg->get_kernel_spec();
+            info->family = sp.family;
+            std::strncpy(info->kernel_name, sp.name().c_str(), sizeof(info->kernel_name) - 1);
+        }
+        if (s.uploaded) {
+            info->n_units = s.dev.n_units;
+            info->device_bytes_A = s.dev.bytes_A;
+            info->col_bytes = s.dev.col_bytes;
+            info->dtype = s.dev.dtype;
+            info->replicas = (int)s.dev.replicas.size();
+            info->needs_memset = s.dev.needs_memset ? 1 : 0;
+        }
+    });
+}
+
+int gs_plan_array_count(gs_plan_t *p) { return p ? (int)p->st.meta->keys().size() : GS_ERR_ARG; }
+
+int gs_plan_array_key(gs_plan_t *p, int i, char *buf, int buf_len) {
+    return guard([&] {
+        GS_CHECK(p && buf && buf_len > 0, "bad argument");
+        auto k = p->st.meta->keys();
+        GS_CHECK(i >= 0 && (size_t)i < k.size(), "index out of range");
+        std::strncpy(buf, k[i].c_str(), buf_len - 1);
+        buf[buf_len - 1] = 0;
+    });
+}
+
+long long gs_plan_array_len(gs_plan_t *p, const char *key) {
+    if (!p || !key || !p->st.meta->is_exist(key)) return -1;
+    return (long long)p->st.meta->get_element(key)->meta_data_arr->get_len();
+}
+
+int gs_plan_array_is_float(gs_plan_t *p, const char *key) {
+    if (!p || !key || !p->st.meta->is_exist(key)) return GS_ERR_ARG;
+    return p->st.meta->get_element(key)->meta_data_arr->is_float() ? 1 : 0;
+}
+
+int gs_plan_array_read_u64(gs_plan_t *p, const char *key, uint64_t *out, uint64_t n) {
+    return guard([&] {
+        GS_CHECK(p && key && out, "null argument");
+        auto a = p->st.meta->get_element(key)->meta_data_arr;
+        GS_CHECK(!a->is_float(), "array is a value array");
+        GS_CHECK(n >= a->get_len(), "buffer too small");
+        std::copy(a->u().begin(), a->u().end(), out);
+    });
+}
+
+int gs_plan_array_read_f64(gs_plan_t *p, const char *key, double *out, uint64_t n) {
+    return guard([&] {
+        GS_CHECK(p && key && out, "null argument");
+        auto a = p->st.meta->get_element(key)->meta_data_arr;
+        GS_CHECK(n >= a->get_len(), "buffer too small");
+        for (uint64_t i = 0; i < a->get_len(); i++) out[i] = a->read_float_from_arr(i);
+    });
+}
+
+int gs_plan_log(gs_plan_t *p, char *buf, int buf_len) {
+    return guard([&] {
+        GS_CHECK(p && buf && buf_len > 0, "bad argument");
+        std::string s;
+        for (auto &l : p->st.exec->log()) s += l + "\n";
+        std::strncpy(buf, s.c_str(), buf_len - 1);
+        buf[buf_len - 1] = 0;
+    });
+}
+
+int gs_plan_from_mtx(const char *path, const gs_opts *opts, gs_plan_t **out) {
+    gs_opts o;
+    if (opts) o = *opts;
+    else gs_opts_default(&o);
+    gs_plan_t *p = nullptr;
+    int rc = gs_plan_create_from_mtx(path, o.ones_values, &p);
+    if (rc) return rc;
+    rc = gs_plan_run_pipeline(p, o.pipeline ? o.pipeline : "tblock_warp_total", o.dense_n, o.p0, o.p1);
+    if (!rc) rc = gs_plan_compile(p);
+    if (!rc) rc = gs_plan_upload(p, o.dtype, o.device);
+    if (rc) {
+        gs_plan_free(p);
+        return rc;
+    }
+    *out = p;
+    return GS_OK;
+}
+
+void gs_plan_free(gs_plan_t *p) {
+    if (!p) return;
+    try {
+        gs::free_device(p->st);
+    } catch (...) {
+    }
+    delete p;
+}
+
+}  // extern "C"

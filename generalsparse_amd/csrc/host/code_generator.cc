@@ -1,0 +1,258 @@
+// code_generator.cc -- lowers the operators' reduction tokens to a gfx950 kernel
+// family and emits a standalone HIP program for it.
+#include "code_generator.hpp"
+
+#include <cstdio>
+#include <fstream>
+#include <sstream>
+#include <sys/stat.h>
+
+#include <dlfcn.h>
+
+namespace gs {
+
+const char *reduction_kind_name(reduction_kind k) {
+    switch (k) {
+        case reduction_kind::TOTAL_BMT_RESULT: return "total_BMT_result_reduce_to_one_register_token";
+        case reduction_kind::THREAD_BIT_MAP: return "thread_bit_map_reduce_to_two_register_token";
+        case reduction_kind::TOTAL_WARP_RESULT: return "total_warp_result_reduce_to_one_register_token";
+        case reduction_kind::WARP_SEGMENT: return "warp_segment_reduce_token";
+        case reduction_kind::TOTAL_BLOCK_RESULT: return "total_block_reduce_to_one_register_token";
+        default: return "none";
+    }
+}
+
+const char *kernel_family_name(int f) {
+    switch (f) {
+        case KF_THREAD_TOTAL: return "k_thread_total";
+        case KF_WARP_TOTAL: return "k_warp_rows";
+        case KF_BLOCK_TOTAL: return "k_block_rows";
+        case KF_BITMAP_SEGMENT: return "k_bitmap_segment";
+        default: return "none";
+    }
+}
+
+std::string kernel_spec::name() const {
+    std::string n = kernel_family_name(family);
+    if (family == KF_BITMAP_SEGMENT && warp_segment) n += "+warp_segment";
+    if (family == KF_WARP_TOTAL && tblock_parent) n += "+tblock";
+    return n;
+}
+
+code_generator::code_generator(std::shared_ptr<meta_data_set> m, int sub_matrix_id) : meta(std::move(m)), sub(sub_matrix_id) {
+    GS_CHECK(meta != nullptr, "code_generator needs a metadata set");
+    GS_CHECK(sub_matrix_id == 0, "one sub-matrix per code generator in this build (sub-matrix splits: SURVEY §8f rank 3)");
+}
+
+void code_generator::set_reduction_token(POS_TYPE pos, const reduction_token &tok) {
+    // code_generator.cc:2451-2485: a level holds one reduction token
+    GS_CHECK(tokens.count(pos) == 0, "a reduction token is already set for " + convert_pos_type_to_string(pos));
+    tokens[pos] = tok;
+}
+
+void code_generator::set_thread_grid(const std::vector<unsigned> &g, const std::vector<unsigned> &b) {
+    grid = g;
+    block = b;
+}
+
+// code_generator.cc:2586-2616 assembles the kernel text from the tokens; here the
+// token set selects one of the hand-written families.
+void code_generator::compile() {
+    GS_CHECK(!compiled, "code_generator::compile may run once");
+    kernel_spec s;
+    const meta_data_set &m = *meta;
+    auto tok = [&](POS_TYPE p) -> const reduction_token * { return tokens.count(p) ? &tokens.at(p) : nullptr; };
+    const reduction_token *tt = tok(THREAD_META), *tw = tok(WARP_META), *tb = tok(TBLOCK_META);
+    if (tt && tt->kind == reduction_kind::THREAD_BIT_MAP) {
+        s.family = KF_BITMAP_SEGMENT;
+        s.warp_segment = tw && tw->kind == reduction_kind::WARP_SEGMENT;
+        s.coarsen_factor = tt->coarsen_factor;
+        s.sparse_coarsen_factor = tt->sparse_coarsen_factor;
+        s.vector_width = tt->size;
+        s.arrays = {"THREAD_META_first_nz_indices_0", "THREAD_META_first_row_indices_0", "THREAD_META_thread_bit_map_0",
+                    "THREAD_META_segment_ptr_0", "THREAD_META_segment_empty_row_indices_0",
+                    "THREAD_META_segment_empty_flag_0", "THREAD_META_segment_offset_0"};
+        if (s.warp_segment)
+            for (auto k : {"WARP_META_first_row_indices_0", "WARP_META_first_nz_indices_0", "WARP_META_first_BMT_indices_0"})
+                s.arrays.push_back(k);
+    } else if (tt && tt->kind == reduction_kind::TOTAL_BMT_RESULT) {
+        GS_CHECK(!tt->need_warp_reduction,
+                 "thread_total with need_warp_reduction (col-direction warp_bit_map plans) is not built in this round");
+        GS_CHECK(!m.is_exist(WARP_META, "first_row_indices", sub) && !m.is_exist(TBLOCK_META, "first_row_indices", sub),
+                 "thread_total inside BMW/BMTB parents is not built in this round");
+        s.family = KF_THREAD_TOTAL;
+        s.coarsen_factor = tt->coarsen_factor;
+        s.sparse_coarsen_factor = tt->sparse_coarsen_factor;
+        s.row_sorted = m.is_exist(GLOBAL_META, "original_nz_row_indices", sub);
+        s.arrays = {"THREAD_META_first_nz_indices_0", "THREAD_META_first_row_indices_0"};
+        if (s.row_sorted) s.arrays.push_back("GLOBAL_META_original_nz_row_indices_0");
+    } else if (tw && tw->kind == reduction_kind::TOTAL_WARP_RESULT) {
+        s.family = KF_WARP_TOTAL;
+        s.coarsen_factor = tw->coarsen_factor;
+        s.tblock_parent = m.is_exist(TBLOCK_META, "first_BMW_indices", sub);
+        s.arrays = {"WARP_META_first_row_indices_0", "WARP_META_first_nz_indices_0"};
+        if (s.tblock_parent) {
+            s.arrays.push_back("TBLOCK_META_first_row_indices_0");
+            s.arrays.push_back("TBLOCK_META_first_nz_indices_0");
+            s.arrays.push_back("TBLOCK_META_first_BMW_indices_0");
+        }
+    } else if (tb && tb->kind == reduction_kind::TOTAL_BLOCK_RESULT) {
+        s.family = KF_BLOCK_TOTAL;
+        s.coarsen_factor = tb->coarsen_factor;
+        s.arrays = {"TBLOCK_META_first_row_indices_0", "TBLOCK_META_first_nz_indices_0"};
+    } else {
+        throw gs_error("code_generator::compile: no reduction token set (or a combination not built in this round)");
+    }
+    for (auto k : {"GLOBAL_META_nz_row_indices_0", "GLOBAL_META_nz_col_indices_0", "GLOBAL_META_nz_vals_0"})
+        s.arrays.push_back(k);
+    for (auto &k : s.arrays) GS_CHECK(m.is_exist(k), "compile: plan array missing: " + k);
+    if (grid.size() == 2) s.ref_grid = {{grid[0], grid[1]}};
+    if (block.size() == 2) s.ref_block = {{block[0], block[1]}};
+    spec = s;
+    compiled = true;
+}
+
+// ------------------------------------------------------------------ emission
+std::string code_generator::generate_kernel_file_source(int repeat) const {
+    GS_CHECK(compiled, "compile() before emitting the program");
+    const bool half = get_config().HALF;
+    std::ostringstream o;
+    o << "// kernel_file.hip -- generated by generalsparse_amd code_generator for plan family "
+      << spec.name() << "\n"
+      << "// build: sh make_kernel.sh; run: ./a.out [matrix.mtx] [N]  -> perf_result (ms, GFLOP/s)\n"
+      << "#include \"kernel_lib.hpp\"\n#include <cstdio>\n#include <cstdlib>\n#include <fstream>\n"
+      << "#include <string>\n#include <vector>\n\n"
+      << "typedef " << (half ? "gsk::f16" : "float") << " VT;\n"
+      << "static std::vector<uint64_t> rd(const char *n) {\n"
+      << "    std::ifstream f(n); std::vector<uint64_t> v; unsigned long long x;\n"
+      << "    while (f >> x) v.push_back(x); return v; }\n"
+      << "static std::vector<double> rdf(const char *n) {\n"
+      << "    std::ifstream f(n); std::vector<double> v; double x; while (f >> x) v.push_back(x); return v; }\n"
+      << "template <class T> static T *up(const std::vector<T> &h, size_t pad = 64) {\n"
+      << "    T *p; hipMalloc(&p, (h.size() + pad) * sizeof(T)); hipMemset(p, 0, (h.size() + pad) * sizeof(T));\n"
+      << "    hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice); return p; }\n"
+      << "static std::vector<uint32_t> u32(const std::vector<uint64_t> &v) { return std::vector<uint32_t>(v.begin(), v.end()); }\n\n"
+      << "int main(int argc, char **argv) {\n"
+      << "    const uint32_t N = argc > 2 ? (uint32_t)atoi(argv[2]) : " << get_config().DENSE_MATRIX_SIZE << ";\n"
+      << "    const int repeat = " << repeat << ";\n"
+      << "    const uint64_t M = " << meta->scalar(GLOBAL_META, "origin_row_num", -1) << ", K = "
+      << meta->scalar(GLOBAL_META, "origin_col_num", -1) << ", NNZ = " << meta->scalar(GLOBAL_META, "origin_nnz_num", -1)
+      << ";\n"
+      << "    auto rows = rd(\"GLOBAL_META_nz_row_indices_0\");\n"
+      << "    auto cols = rd(\"GLOBAL_META_nz_col_indices_0\");\n"
+      << "    auto vals = rdf(\"GLOBAL_META_nz_vals_0\");\n"
+      << "    std::vector<uint32_t> c32(cols.begin(), cols.end());\n"
+      << "    std::vector<VT> vv(vals.size()); for (size_t i = 0; i < vals.size(); i++) vv[i] = (VT)vals[i];\n"
+      << "    uint32_t *d_col = up(c32); VT *d_val = up(vv);\n"
+      << "    uint64_t row_num = rows.back() + 1;\n";
+    const bool vec_ok = true;
+    (void)vec_ok;
+    const char *cf = half ? "8" : "4";
+    std::string launch;
+    switch (spec.family) {
+        case KF_THREAD_TOTAL:
+            o << "    auto fn = rd(\"THREAD_META_first_nz_indices_0\");\n";
+            if (spec.row_sorted) o << "    auto order = rd(\"GLOBAL_META_original_nz_row_indices_0\");\n";
+            else o << "    std::vector<uint64_t> order(M); for (uint64_t i = 0; i < M; i++) order[i] = i;\n";
+            o << "    uint32_t *d_a0 = up(u32(fn)), *d_a1 = up(u32(order));\n"
+              << "    const uint32_t n_units = fn.size() - 1, n_aux = order.size();\n"
+              << "    bool al = true; for (auto x : fn) al &= x % 4 == 0;\n";
+            launch = "gsk::k_thread_total<VT, uint32_t, CF, SCF><<<dim3((n_aux + 256 / X - 1) / (256 / X), tiles), 256>>>("
+                     "d_a0, d_a1, d_col, d_val, d_B, d_C, n_units, n_aux, N, X, 0)";
+            break;
+        case KF_WARP_TOTAL:
+            o << "    auto wr = rd(\"WARP_META_first_row_indices_0\");\n"
+              << "    uint32_t *d_a0 = up(u32(wr)), *d_a1 = nullptr;\n"
+              << "    uint32_t *d_a2 = up(gsk_host::csr_row_ptr(rows, wr.back()));\n"
+              << "    const uint32_t n_units = wr.size() - 1; uint32_t gx = (n_units + 3) / 4; const bool al = true;\n";
+            if (spec.tblock_parent)
+                o << "    auto tbw = rd(\"TBLOCK_META_first_BMW_indices_0\"); d_a1 = up(u32(tbw)); gx = tbw.size() - 1;\n";
+            launch = "gsk::k_warp_rows<VT, uint32_t, CF, SCF><<<dim3(gx, tiles), 256>>>(d_a0, d_a1, d_a2, d_col, d_val, d_B, d_C, n_units, N, X, 0)";
+            break;
+        case KF_BLOCK_TOTAL:
+            o << "    auto tr = rd(\"TBLOCK_META_first_row_indices_0\");\n"
+              << "    uint32_t *d_a0 = up(u32(tr)); uint32_t *d_a2 = up(gsk_host::csr_row_ptr(rows, tr.back()));\n"
+              << "    const uint32_t n_units = tr.size() - 1; const bool al = true;\n";
+            launch = "gsk::k_block_rows<VT, uint32_t, CF, SCF><<<dim3(n_units, tiles), 256>>>(d_a0, d_a2, d_col, d_val, d_B, d_C, n_units, N, X, 0)";
+            break;
+        case KF_BITMAP_SEGMENT:
+            o << "    auto fn = rd(\"THREAD_META_first_nz_indices_0\"), fr = rd(\"THREAD_META_first_row_indices_0\");\n"
+              << "    auto sp = rd(\"THREAD_META_segment_ptr_0\"), so = rd(\"THREAD_META_segment_empty_row_indices_0\");\n"
+              << "    uint32_t *d_a0 = up(u32(fn)), *d_a1 = up(u32(fr)), *d_a2 = up(u32(sp)), *d_a3 = up(u32(so));\n"
+              << "    uint64_t *d_m0 = up(gsk_host::row_start_masks(rows, fn));\n"
+              << "    const uint32_t n_units = fn.size() - 1; const bool al = true;\n";
+            launch = "hipMemsetAsync(d_C, 0, M * N * sizeof(VT), 0); "
+                     "gsk::k_bitmap_segment<VT, uint32_t, CF, SCF><<<dim3((n_units + 4 * (64 / X) - 1) / (4 * (64 / X)), tiles), 256, "
+                     "4 * (64 / X) * 2 * X * CF * sizeof(float)>>>(d_a0, d_a1, d_m0, d_a2, d_a3, d_col, d_val, d_B, d_C, n_units, N, X, 0)";
+            break;
+        default:
+            throw gs_error("no family");
+    }
+    o << "    std::vector<VT> hB(K * N, (VT)1.0f);  // x_arr = 1 (code_generator.cc:464-467)\n"
+      << "    VT *d_B = up(hB, 0); VT *d_C; hipMalloc(&d_C, M * N * sizeof(VT)); hipMemset(d_C, 0, M * N * sizeof(VT));\n"
+      << "    auto run = [&]() {\n"
+      << "        if (al && N % " << cf << " == 0) {\n"
+      << "            constexpr int CF = " << cf << ", SCF = 4; uint32_t X = 1; while (X < 64 && X * CF < N) X <<= 1;\n"
+      << "            uint32_t tiles = (N + X * CF - 1) / (X * CF); " << launch << ";\n"
+      << "        } else {\n"
+      << "            constexpr int CF = 1, SCF = 1; uint32_t X = 1; while (X < 64 && X * CF < N) X <<= 1;\n"
+      << "            uint32_t tiles = (N + X * CF - 1) / (X * CF); " << launch << ";\n"
+      << "        }\n"
+      << "    };\n"
+      << "    run(); hipDeviceSynchronize();\n"
+      << "    // check (kernel_lib.hpp:884-921 of the reference): all-ones B, C[i][j] = sum of row i's values\n"
+      << "    std::vector<VT> hC(M * N); hipMemcpy(hC.data(), d_C, M * N * sizeof(VT), hipMemcpyDeviceToHost);\n"
+      << "    std::vector<double> ref(M, 0.0);\n"
+      << "    std::vector<uint64_t> orig_of(row_num);\n";
+    if (spec.row_sorted)
+        o << "    { auto order = rd(\"GLOBAL_META_original_nz_row_indices_0\"); for (uint64_t i = 0; i < row_num; i++) orig_of[i] = order[i]; }\n";
+    else
+        o << "    for (uint64_t i = 0; i < row_num; i++) orig_of[i] = i;\n";
+    o << "    for (size_t i = 0; i < rows.size(); i++) ref[orig_of[rows[i]]] += vals[i];\n"
+      << "    long wrong = 0;\n"
+      << "    for (uint64_t i = 0; i < M; i++) for (uint32_t j = 0; j < N; j++) {\n"
+      << "        double c = (double)(float)hC[i * N + j], r = (double)(float)(VT)(float)ref[i];\n"
+      << "        if (c - r > 1e-3 * (1 + (r < 0 ? -r : r)) || r - c > 1e-3 * (1 + (r < 0 ? -r : r))) {\n"
+      << "            if (wrong < 10) printf(\"Wrong result: i = %llu, j = %u, result = %f, reference = %f.\\n\", (unsigned long long)i, j, c, r);\n"
+      << "            wrong++; } }\n"
+      << "    printf(\"wrong number:%ld\\n\", wrong); if (!wrong) printf(\"correct\\n\");\n"
+      << "    hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);\n"
+      << "    hipEventRecord(e0, 0); for (int i = 0; i < repeat; i++) run(); hipEventRecord(e1, 0); hipEventSynchronize(e1);\n"
+      << "    float ms = 0; hipEventElapsedTime(&ms, e0, e1);\n"
+      << "    double gflops = " << get_config().FLOAT_RATE << ".0 * (double)NNZ * N * repeat / (ms * 1e-3) / 1e9;\n"
+      << "    FILE *pr = fopen(\"perf_result\", \"w\"); fprintf(pr, \"%f\\n%f\\n\", ms, gflops); fclose(pr);  // code_generator.cc:643-648\n"
+      << "    printf(\"time %f ms for %d launches, %f GFLOP/s\\n\", ms, repeat, gflops);\n"
+      << "    return wrong ? 1 : 0;\n}\n";
+    return o.str();
+}
+
+uint64_t code_generator::generate_final_program(int repeat, const std::string &root, std::string *dir_out) {
+    GS_CHECK(compiled, "compile() before generate_final_program");
+    std::string dir;
+    uint64_t id = meta->output_format_to_dir(root, spec.arrays, &dir);
+    {
+        std::ofstream f(dir + "/kernel_file.hip");
+        f << generate_kernel_file_source(repeat);
+    }
+    // copy the device header next to the program (code_generator.cc:686-694)
+    // the header ships next to the library: <pkg>/csrc/hip_code/kernel_lib.hpp
+    std::string lib;
+    Dl_info info;
+    if (dladdr((void *)&kernel_family_name, &info) && info.dli_fname) {
+        std::string so = info.dli_fname;
+        lib = so.substr(0, so.find_last_of('/') + 1) + "csrc/hip_code/kernel_lib.hpp";
+    }
+    if (!lib.empty()) {
+        std::ifstream in(lib, std::ios::binary);
+        std::ofstream out(dir + "/kernel_lib.hpp", std::ios::binary);
+        out << in.rdbuf();
+    }
+    {
+        std::ofstream f(dir + "/make_kernel.sh");
+        f << "hipcc --offload-arch=gfx950 -O3 -std=c++17 kernel_file.hip -o a.out\n";
+    }
+    if (dir_out) *dir_out = dir;
+    return id;
+}
+
+}  // namespace gs

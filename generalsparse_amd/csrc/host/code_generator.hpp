@@ -1,0 +1,102 @@
+// code_generator.hpp -- kernel IR and HIP emission for gfx950.
+//
+// Reference: code_generator.hpp:44-457, kernel_generator.h (token IR),
+// reduction_token/*.cc.  The reference assembles a CUDA kernel from string
+// tokens per opened level.  Here the operators attach *reduction tokens*
+// (descriptors) to the levels exactly as before (set_reduction_token /
+// open_spec_level_of_paral / set_thread_grid), and compile() lowers that
+// token set onto one of the hand-written gfx950 kernel families in
+// hip_code/kernel_lib.hpp, producing a kernel_spec.  generate_final_program()
+// emits a standalone HIP program (kernel_file.hip + plan files +
+// make_kernel.sh) that instantiates the same family, with the reference's
+// perf_result contract (code_generator.cc:643-648).
+#pragma once
+
+#include "gs_core.hpp"
+
+#include <array>
+#include <set>
+
+namespace gs {
+
+// reduction tokens the operators attach (reduction_token/*.cc)
+enum class reduction_kind {
+    NONE,
+    TOTAL_BMT_RESULT,      // total_BMT_result_reduce_to_one_register_token (K1)
+    THREAD_BIT_MAP,        // thread_bit_map_reduce_to_two_register_token (K2)
+    TOTAL_WARP_RESULT,     // total_warp_result_reduce_to_one_register_token (K4)
+    WARP_SEGMENT,          // warp_segment_reduce_token (K3)
+    TOTAL_BLOCK_RESULT,    // total_block_reduce_to_one_register_token (K6)
+};
+const char *reduction_kind_name(reduction_kind k);
+
+struct reduction_token {
+    reduction_kind kind = reduction_kind::NONE;
+    int coarsen_factor = 1;
+    int sparse_coarsen_factor = 1;
+    bool need_warp_reduction = false;
+    int size = 0;  // VECTOR_WIDTH / bitmap group size
+};
+
+// gfx950 kernel families (hip_code/kernel_lib.hpp)
+enum kernel_family : int {
+    KF_NONE = 0,
+    KF_THREAD_TOTAL = 1,    // lane group per BMT row (row-sorted, col-padded)
+    KF_WARP_TOTAL = 2,      // one 64-lane wave per BMW (row block), nnz split over lane slots
+    KF_BLOCK_TOTAL = 3,     // one workgroup per BMTB row block, LDS reduction
+    KF_BITMAP_SEGMENT = 4,  // fixed-nnz BMTs, bitmap row segments, wave-level carry combine
+};
+const char *kernel_family_name(int f);
+
+struct kernel_spec {
+    int family = KF_NONE;
+    int coarsen_factor = 1;
+    int sparse_coarsen_factor = 1;
+    int vector_width = 1;
+    bool warp_segment = false;   // K3 present on top of K2
+    bool tblock_parent = false;  // BMWs grouped into BMTBs
+    bool row_sorted = false;     // GLOBAL original_nz_row_indices present
+    std::array<unsigned, 2> ref_grid{{0, 0}}, ref_block{{0, 0}};
+    std::vector<std::string> arrays;  // metadata keys the kernel consumes (= kernel arguments)
+    std::string name() const;
+};
+
+class code_generator {
+  public:
+    code_generator(std::shared_ptr<meta_data_set> m, int sub_matrix_id);
+    std::shared_ptr<meta_data_set> get_metadata_set() const { return meta; }
+    int get_sub_matrix_id() const { return sub; }
+
+    void open_spec_level_of_paral(POS_TYPE pos) { opened.insert(pos); }
+    bool level_is_open(POS_TYPE pos) const { return opened.count(pos) != 0; }
+    // code_generator.cc:2451-2485: one token per level
+    void set_reduction_token(POS_TYPE pos, const reduction_token &tok);
+    bool reduction_token_is_existing(POS_TYPE pos) const { return tokens.count(pos) != 0; }
+    const reduction_token &get_reduction_token(POS_TYPE pos) const { return tokens.at(pos); }
+    void set_thread_for_row(bool v) { thread_for_row = v; }
+    bool get_thread_for_row() const { return thread_for_row; }
+    void set_thread_grid(const std::vector<unsigned> &grid, const std::vector<unsigned> &block);
+
+    // lowers the token set to a kernel family (code_generator.hpp:265-269)
+    void compile();
+    bool is_compiled() const { return compiled; }
+    const kernel_spec &get_kernel_spec() const { return spec; }
+
+    // HIP source of the generated program (kernel + main with perf_result)
+    std::string generate_kernel_file_source(int repeat) const;
+    // writes ROOT/data_source/<id>/{plan arrays, kernel_file.hip, make_kernel.sh}
+    // (code_generator.hpp:271-280); returns the id, optionally the directory
+    uint64_t generate_final_program(int repeat, const std::string &root, std::string *dir_out = nullptr);
+
+  private:
+    std::shared_ptr<meta_data_set> meta;
+    int sub;
+    std::set<POS_TYPE> opened;
+    std::map<POS_TYPE, reduction_token> tokens;
+    bool thread_for_row = false;
+    std::vector<unsigned> grid, block;
+    bool compiled = false;
+    kernel_spec spec;
+};
+
+}  // namespace gs

@@ -1,0 +1,683 @@
+// data_transform_step.cc -- flat-array implementations of the hot-path transforms.
+// Each function cites the reference file it reproduces.
+#include "data_transform_step.hpp"
+
+#include <algorithm>
+#include <numeric>
+
+namespace gs {
+
+void basic_data_transform_step::replace_u(POS_TYPE p, const char *n, std::vector<uint64_t> v) {
+    if (meta_data_set_ptr->is_exist(p, n, target_matrix_id)) meta_data_set_ptr->remove_element(p, n, target_matrix_id);
+    meta_data_set_ptr->add_element(p, n, target_matrix_id, std::make_shared<universal_array>(std::move(v)));
+    dst(p, n);
+}
+
+void basic_data_transform_step::replace_f(POS_TYPE p, const char *n, std::vector<double> v, data_type t) {
+    if (meta_data_set_ptr->is_exist(p, n, target_matrix_id)) meta_data_set_ptr->remove_element(p, n, target_matrix_id);
+    meta_data_set_ptr->add_element(p, n, target_matrix_id, std::make_shared<universal_array>(std::move(v), t));
+    dst(p, n);
+}
+
+static inline double padding_bound() { return (double)get_config().PADDING_RATE_UP_BOUND; }
+
+// ------------------------------------------------------------------ sort
+// get_row_order_by_length.cc:14-126: stable bucket sort by row length, longest first
+void get_row_order_by_length::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    GS_CHECK(!m.is_exist(GLOBAL_META, "original_nz_row_indices", s), "get_row_order_by_length: already sorted");
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    uint64_t minr = m.scalar(GLOBAL_META, "begin_row_index", s);
+    uint64_t maxr = m.scalar(GLOBAL_META, "end_row_index", s);
+    GS_CHECK(maxr >= minr, "end_row_index < begin_row_index");
+    uint64_t real_max = row.back();
+    if (real_max > maxr - minr) maxr = minr + real_max;
+    uint64_t nrow = maxr - minr + 1;
+    auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, nrow - 1, 0, row.size() - 1);
+    uint64_t maxlen = *std::max_element(cnt.begin(), cnt.end());
+    std::vector<uint64_t> off(maxlen + 1, 0);
+    for (uint64_t c : cnt) off[c]++;
+    uint64_t acc = 0;
+    for (int64_t L = (int64_t)maxlen; L >= 0; L--) {
+        uint64_t c = off[L];
+        off[L] = acc;
+        acc += c;
+    }
+    std::vector<uint64_t> order(nrow);
+    for (uint64_t i = 0; i < nrow; i++) order[off[cnt[i]]++] = i;
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(GLOBAL_META, "original_nz_row_indices", std::move(order));
+    is_run = true;
+}
+
+namespace {
+// start offset of every old row in the row-sorted COO
+std::vector<uint64_t> old_row_starts(const std::vector<uint64_t> &row, uint64_t nrow) {
+    std::vector<uint64_t> start(nrow + 1, 0);
+    for (uint64_t r : row) start[r + 1]++;
+    for (uint64_t i = 0; i < nrow; i++) start[i + 1] += start[i];
+    return start;
+}
+uint64_t sub_row_num(const meta_data_set &m, int s) {
+    return m.scalar(GLOBAL_META, "end_row_index", s) - m.scalar(GLOBAL_META, "begin_row_index", s) + 1;
+}
+}  // namespace
+
+// reorder_val_by_index.cc / reorder_col_by_index.cc: regroup entries in the new row order
+void reorder_val_by_index::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    const auto &order = m.u(GLOBAL_META, "original_nz_row_indices", s);
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    auto varr = m.get_element(GLOBAL_META, "nz_vals", s)->meta_data_arr;
+    uint64_t nrow = sub_row_num(m, s);
+    GS_CHECK(nrow == order.size(), "reorder_val_by_index: row count mismatch");
+    auto start = old_row_starts(row, nrow);
+    std::vector<double> nv(row.size());
+    uint64_t p = 0;
+    for (uint64_t o : order)
+        for (uint64_t k = start[o]; k < start[o + 1]; k++) nv[p++] = varr->read_float_from_arr(k);
+    src(GLOBAL_META, "nz_vals");
+    replace_f(GLOBAL_META, "nz_vals", std::move(nv), varr->get_data_type());
+    is_run = true;
+}
+
+void reorder_col_by_index::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    const auto &order = m.u(GLOBAL_META, "original_nz_row_indices", s);
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    const auto &col = m.u(GLOBAL_META, "nz_col_indices", s);
+    uint64_t nrow = sub_row_num(m, s);
+    GS_CHECK(nrow == order.size(), "reorder_col_by_index: row count mismatch");
+    if (check) {  // reorder_col_by_index.cc:82-93: cols non-decreasing inside a row
+        for (uint64_t i = 1; i < row.size(); i++)
+            GS_CHECK(row[i] != row[i - 1] || col[i] >= col[i - 1],
+                     "reorder_col_by_index: columns not sorted within a row");
+    }
+    auto start = old_row_starts(row, nrow);
+    std::vector<uint64_t> nc(row.size());
+    uint64_t p = 0;
+    for (uint64_t o : order)
+        for (uint64_t k = start[o]; k < start[o + 1]; k++) nc[p++] = col[k];
+    src(GLOBAL_META, "nz_col_indices");
+    replace_u(GLOBAL_META, "nz_col_indices", std::move(nc));
+    is_run = true;
+}
+
+// reorder_row_by_index.cc: new row id repeated nnz(old row) times
+void reorder_row_by_index::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    const auto &order = m.u(GLOBAL_META, "original_nz_row_indices", s);
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    uint64_t nrow = sub_row_num(m, s);
+    GS_CHECK(nrow == order.size(), "reorder_row_by_index: row count mismatch");
+    auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, nrow - 1, 0, row.size() - 1);
+    std::vector<uint64_t> nr(row.size());
+    uint64_t p = 0;
+    for (uint64_t newr = 0; newr < nrow; newr++)
+        for (uint64_t k = 0; k < cnt[order[newr]]; k++) nr[p++] = newr;
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(GLOBAL_META, "nz_row_indices", std::move(nr));
+    is_run = true;
+}
+
+// remove_empty_row_in_end_of_sub_matrix.cc:13-70
+void remove_empty_row_in_end_of_sub_matrix::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    uint64_t b = m.scalar(GLOBAL_META, "begin_row_index", s);
+    uint64_t e = m.scalar(GLOBAL_META, "end_row_index", s);
+    uint64_t last = m.u(GLOBAL_META, "nz_row_indices", s).back();
+    GS_CHECK(last <= e - b, "remove_empty_row: row index beyond sub-matrix");
+    if (last < e - b) {
+        m.remove_element(GLOBAL_META, "end_row_index", s);
+        m.add_scalar(GLOBAL_META, "end_row_index", s, b + last);
+        dst(GLOBAL_META, "end_row_index");
+    }
+    is_run = true;
+}
+
+// ------------------------------------------------------------- col pad (A6)
+// modify_{col,val,row}_*_by_col_pad_in_sub_matrix.cc: pad each row to a multiple;
+// padded entries repeat the row's last column with value 0
+namespace {
+struct col_pad_plan {
+    std::vector<uint64_t> start, cnt;  // per row
+    uint64_t after = 0;
+    bool padded = false;
+};
+col_pad_plan make_col_pad(const meta_data_set &m, int s, int mult, bool check) {
+    GS_CHECK(mult >= 2, "col pad multiple must be >= 2 (modify_col_indices_by_col_pad_in_sub_matrix.cc:26)");
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    uint64_t row_num = row_num_of_sub_matrix(m, s);
+    col_pad_plan p;
+    p.cnt = get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+    p.start.assign(row_num + 1, 0);
+    for (uint64_t r = 0; r < row_num; r++) p.start[r + 1] = p.start[r] + p.cnt[r];
+    p.after = row.size();
+    for (uint64_t r = 0; r < row_num; r++)
+        if (p.cnt[r] % mult) p.after += (p.cnt[r] / mult + 1) * mult - p.cnt[r];
+    p.padded = p.after != row.size();
+    if (check && (double)p.after / (double)row.size() >= padding_bound())
+        throw gs_error("col padding rate " + std::to_string((double)p.after / row.size()) +
+                       " >= PADDING_RATE_UP_BOUND (modify_col_indices_by_col_pad_in_sub_matrix.cc:103-110)");
+    return p;
+}
+template <class T, class F>
+std::vector<T> apply_col_pad(const col_pad_plan &p, int mult, F src_at, T pad_of_last_is_zero_flag) {
+    (void)pad_of_last_is_zero_flag;
+    std::vector<T> out(p.after);
+    uint64_t q = 0;
+    for (uint64_t r = 0; r + 1 < p.start.size(); r++) {
+        for (uint64_t k = p.start[r]; k < p.start[r + 1]; k++) out[q++] = src_at(k, false);
+        if (p.cnt[r] % mult) {
+            uint64_t target = (p.cnt[r] / mult + 1) * mult;
+            for (uint64_t k = p.cnt[r]; k < target; k++) out[q++] = src_at(p.start[r + 1] - 1, true);
+        }
+    }
+    return out;
+}
+}  // namespace
+
+void modify_col_indices_by_col_pad_in_sub_matrix::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    auto p = make_col_pad(m, target_matrix_id, multiple_of_each_row_size, check);
+    if (p.padded) {
+        const auto &col = m.u(GLOBAL_META, "nz_col_indices", target_matrix_id);
+        auto nc = apply_col_pad<uint64_t>(p, multiple_of_each_row_size, [&](uint64_t k, bool) { return col[k]; }, 0);
+        src(GLOBAL_META, "nz_col_indices");
+        replace_u(GLOBAL_META, "nz_col_indices", std::move(nc));
+    }
+    is_run = true;
+}
+
+void modify_vals_by_col_pad_in_sub_matrix::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    auto p = make_col_pad(m, target_matrix_id, multiple_of_each_row_size, check);
+    if (p.padded) {
+        auto va = m.get_element(GLOBAL_META, "nz_vals", target_matrix_id)->meta_data_arr;
+        auto nv = apply_col_pad<double>(p, multiple_of_each_row_size,
+                                        [&](uint64_t k, bool pad) { return pad ? 0.0 : va->read_float_from_arr(k); }, 0.0);
+        src(GLOBAL_META, "nz_vals");
+        replace_f(GLOBAL_META, "nz_vals", std::move(nv), va->get_data_type());
+    }
+    is_run = true;
+}
+
+void modify_row_indices_by_col_pad_in_sub_matrix::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    auto p = make_col_pad(m, target_matrix_id, multiple_of_each_row_size, check);
+    if (p.padded) {
+        const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+        auto nr = apply_col_pad<uint64_t>(p, multiple_of_each_row_size, [&](uint64_t k, bool) { return row[k]; }, 0);
+        src(GLOBAL_META, "nz_row_indices");
+        replace_u(GLOBAL_META, "nz_row_indices", std::move(nr));
+    }
+    is_run = true;
+}
+
+// ------------------------------------------------- fixed row-direction blocks
+// get_begin_rows_of_BMT_after_fixed_blocking_in_row_direction.cc:71-97
+void get_begin_rows_of_BMT_after_fixed_blocking_in_row_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    GS_CHECK(fixed_row_block_size >= 1, "fixed_row_block_size >= 1");
+    if (check) {
+        GS_CHECK(m.count_of_metadata_of_diff_pos(TBLOCK_META, s) == 0, "BMT blocking without parent: TBLOCK items exist");
+        GS_CHECK(m.count_of_metadata_of_diff_pos(WARP_META, s) == 0, "BMT blocking without parent: WARP items exist");
+    }
+    uint64_t row_num = row_num_of_sub_matrix(m, s);
+    std::vector<uint64_t> fr;
+    int in_bmt = 0;
+    bool first = true;
+    for (uint64_t i = 0; i < row_num; i++) {
+        if (first) { fr.push_back(i); first = false; }
+        else in_bmt += 1;
+        if (in_bmt == fixed_row_block_size) { fr.push_back(i); in_bmt = 0; }
+    }
+    fr.push_back(row_num);
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(THREAD_META, "first_row_indices", std::move(fr));
+    is_run = true;
+}
+
+// get_begin_nzs_of_BMT_after_fixed_blocking_in_row_direction.cc:75-100
+void get_begin_nzs_of_BMT_after_fixed_blocking_in_row_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    uint64_t row_num = row_num_of_sub_matrix(m, s);
+    auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+    std::vector<uint64_t> fn{0};
+    int rc = 0;
+    uint64_t nz = 0;
+    for (uint64_t i = 0; i < row_num; i++) {
+        rc += 1;
+        nz += cnt[i];
+        if (rc == fixed_row_block_size) { fn.push_back(nz); rc = 0; }
+    }
+    if (rc != fixed_row_block_size && rc != 0) fn.push_back(nz);
+    GS_CHECK(fn.back() == row.size(), "first_nz_indices must end at nnz");
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(THREAD_META, "first_nz_indices", std::move(fn));
+    is_run = true;
+}
+
+namespace {
+std::vector<uint64_t> fixed_first_rows(uint64_t row_num, uint64_t rb) {
+    std::vector<uint64_t> fr{0};
+    uint64_t complete = row_num / rb;
+    for (uint64_t i = 0; i < complete; i++) fr.push_back((i + 1) * rb);
+    if (row_num % rb) fr.push_back(row_num);
+    return fr;
+}
+std::vector<uint64_t> fixed_first_nzs(const std::vector<uint64_t> &cnt, uint64_t row_num, uint64_t rb) {
+    uint64_t nb = row_num / rb + (row_num % rb ? 1 : 0);
+    std::vector<uint64_t> fn{0};
+    for (uint64_t i = 0; i < nb; i++) {
+        uint64_t c = 0;
+        for (uint64_t r = i * rb; r < (i + 1) * rb && r < row_num; r++) c += cnt[r];
+        fn.push_back(fn.back() + c);
+    }
+    return fn;
+}
+}  // namespace
+
+// get_begin_rows_of_BMTBs_after_fixed_blocking_in_row_direction.cc
+void get_begin_rows_of_BMTBs_after_fixed_blocking_in_row_direction::run(bool check) {
+    GS_CHECK(fixed_row_block_size >= 1, "fixed_row_block_size >= 1");
+    uint64_t row_num = row_num_of_sub_matrix(*meta_data_set_ptr, target_matrix_id);
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(TBLOCK_META, "first_row_indices", fixed_first_rows(row_num, fixed_row_block_size));
+    is_run = true;
+}
+
+// get_begin_nzs_of_BMTBs_after_fixed_blocking_in_row_direction.cc
+void get_begin_nzs_of_BMTBs_after_fixed_blocking_in_row_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    uint64_t row_num = row_num_of_sub_matrix(m, target_matrix_id);
+    auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(TBLOCK_META, "first_nz_indices", fixed_first_nzs(cnt, row_num, fixed_row_block_size));
+    is_run = true;
+}
+
+void get_begin_rows_of_BMW_after_fixed_blocking_in_row_direction_without_BMTB::run(bool check) {
+    GS_CHECK(fixed_row_block_size >= 1, "fixed_row_block_size >= 1");
+    uint64_t row_num = row_num_of_sub_matrix(*meta_data_set_ptr, target_matrix_id);
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(WARP_META, "first_row_indices", fixed_first_rows(row_num, fixed_row_block_size));
+    is_run = true;
+}
+
+void get_begin_nzs_of_BMW_after_fixed_blocking_in_row_direction_without_BMTB::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    uint64_t row_num = row_num_of_sub_matrix(m, target_matrix_id);
+    auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(WARP_META, "first_nz_indices", fixed_first_nzs(cnt, row_num, fixed_row_block_size));
+    is_run = true;
+}
+
+// get_begin_rows_of_BMW_after_fixed_blocking_in_row_direction_in_BMTB.cc
+void get_begin_rows_of_BMW_after_fixed_blocking_in_row_direction_in_BMTB::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &tr = m.u(TBLOCK_META, "first_row_indices", target_matrix_id);
+    std::vector<uint64_t> wr;
+    for (uint64_t i = 0; i + 1 < tr.size(); i++)
+        for (uint64_t r = tr[i]; r < tr[i + 1]; r += fixed_row_block_size) wr.push_back(r);
+    wr.push_back(tr.back());
+    src(TBLOCK_META, "first_row_indices");
+    replace_u(WARP_META, "first_row_indices", std::move(wr));
+    is_run = true;
+}
+
+// get_begin_nzs_of_BMW_after_fixed_blocking_in_row_direction_in_BMTB.cc
+void get_begin_nzs_of_BMW_after_fixed_blocking_in_row_direction_in_BMTB::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    const auto &tr = m.u(TBLOCK_META, "first_row_indices", s);
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    uint64_t row_num = row_num_of_sub_matrix(m, s);
+    auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+    std::vector<uint64_t> wn{0};
+    for (uint64_t i = 0; i + 1 < tr.size(); i++) {
+        for (uint64_t r0 = tr[i]; r0 < tr[i + 1]; r0 += fixed_row_block_size) {
+            uint64_t c = 0;
+            for (uint64_t r = r0; r < tr[i + 1] && r < r0 + fixed_row_block_size; r++) c += cnt[r];
+            wn.push_back(wn.back() + c);
+        }
+    }
+    src(TBLOCK_META, "first_row_indices");
+    replace_u(WARP_META, "first_nz_indices", std::move(wn));
+    is_run = true;
+}
+
+// get_begin_BMWs_of_BMTB_after_blocking_in_row_direction.cc
+void get_begin_BMWs_of_BMTB_after_blocking_in_row_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    const auto &tr = m.u(TBLOCK_META, "first_row_indices", s);
+    const auto &wr = m.u(WARP_META, "first_row_indices", s);
+    std::vector<uint64_t> tb{0};
+    uint64_t cur = 0;
+    for (uint64_t i = 0; i + 1 < tr.size(); i++) {
+        uint64_t num = 0, fr = wr[cur];
+        if (check) GS_CHECK(fr == tr[i], "first BMW row != BMTB row");
+        while (fr < tr[i + 1]) {
+            num++;
+            cur++;
+            if (cur == wr.size()) break;
+            fr = wr[cur];
+        }
+        tb.push_back(tb.back() + num);
+    }
+    src(WARP_META, "first_row_indices");
+    replace_u(TBLOCK_META, "first_BMW_indices", std::move(tb));
+    is_run = true;
+}
+
+// ------------------------------------------------------ nnz-direction (A9)
+// modify_*_by_nnz_pad.cc:14-75
+namespace {
+uint64_t nnz_pad_target(uint64_t nnz, int t, bool check) {
+    if (nnz % t == 0) return nnz;
+    uint64_t nn = (nnz / t + 1) * t;
+    if (check && (double)nn / (double)nnz >= padding_bound())
+        throw gs_error("nnz padding rate " + std::to_string((double)nn / nnz) +
+                       " >= PADDING_RATE_UP_BOUND (modify_col_indices_by_nnz_pad.cc)");
+    return nn;
+}
+}  // namespace
+
+void modify_col_indices_by_nnz_pad::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    auto c = m.u(GLOBAL_META, "nz_col_indices", target_matrix_id);
+    uint64_t nn = nnz_pad_target(c.size(), nnz_target, check);
+    if (nn != c.size()) {
+        c.resize(nn, c.back());
+        src(GLOBAL_META, "nz_col_indices");
+        replace_u(GLOBAL_META, "nz_col_indices", std::move(c));
+    }
+    is_run = true;
+}
+
+void modify_vals_by_nnz_pad::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    auto va = m.get_element(GLOBAL_META, "nz_vals", target_matrix_id)->meta_data_arr;
+    uint64_t nn = nnz_pad_target(va->get_len(), nnz_target, check);
+    if (nn != va->get_len()) {
+        std::vector<double> v = va->f();
+        v.resize(nn, 0.0);
+        src(GLOBAL_META, "nz_vals");
+        replace_f(GLOBAL_META, "nz_vals", std::move(v), va->get_data_type());
+    }
+    is_run = true;
+}
+
+void modify_row_indices_by_nnz_pad::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    auto r = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    uint64_t nn = nnz_pad_target(r.size(), nnz_target, check);
+    if (nn != r.size()) {
+        r.resize(nn, r.back());
+        src(GLOBAL_META, "nz_row_indices");
+        replace_u(GLOBAL_META, "nz_row_indices", std::move(r));
+    }
+    is_run = true;
+}
+
+// get_begin_rows_of_BMT_after_fixed_blocking_in_nnz_direction.cc
+void get_begin_rows_of_BMT_after_fixed_blocking_in_nnz_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    uint64_t row_num = row_num_of_sub_matrix(m, target_matrix_id);
+    std::vector<uint64_t> fr;
+    for (uint64_t i = 0; i < row.size(); i += nnz_per_BMT) fr.push_back(row[i]);
+    GS_CHECK(row_num > fr.back(), "BMT first row beyond row count");
+    fr.push_back(row_num);
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(THREAD_META, "first_row_indices", std::move(fr));
+    is_run = true;
+}
+
+// get_begin_nzs_of_BMT_after_fixed_blocking_in_nnz_direction.cc
+void get_begin_nzs_of_BMT_after_fixed_blocking_in_nnz_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    uint64_t nnz = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id).size();
+    std::vector<uint64_t> fn;
+    for (uint64_t i = 0; i < nnz; i += nnz_per_BMT) fn.push_back(i);
+    fn.push_back(nnz);
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(THREAD_META, "first_nz_indices", std::move(fn));
+    is_run = true;
+}
+
+// get_BMT_size_of_each_parent.cc: one size per parent block, or no item at all when
+// the BMT sizes inside a parent differ (:118-121)
+void get_BMT_size_of_each_parent::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    const auto &fn = m.u(THREAD_META, "first_nz_indices", s);
+    std::vector<uint64_t> sizes;
+    if (parent_pos == GLOBAL_META) {
+        uint64_t sz = fn.size() >= 2 ? fn[1] - fn[0] : 0;
+        for (uint64_t i = 0; i + 1 < fn.size(); i++)
+            if (fn[i + 1] - fn[i] != sz) { is_run = true; return; }
+        sizes.push_back(sz);
+    } else {
+        const auto &pn = m.u(parent_pos, "first_nz_indices", s);
+        const std::vector<uint64_t> *pb = row_direction_blocking ? &m.u(parent_pos, "first_BMT_indices", s) : nullptr;
+        uint64_t cur = 0;
+        for (uint64_t p = 0; p + 1 < pn.size(); p++) {
+            uint64_t sz = 0;
+            bool seen = false;
+            uint64_t cur_nz = fn[cur];
+            while (cur_nz < pn[p + 1]) {
+                uint64_t b = fn[cur + 1] - fn[cur];
+                if (!seen) { sz = b; seen = true; }
+                else if (b != sz) { is_run = true; return; }
+                cur++;
+                cur_nz = fn[cur];
+            }
+            if (row_direction_blocking && pn[p] == pn[p + 1])
+                while (cur < (*pb)[p + 1]) cur++;
+            sizes.push_back(sz);
+        }
+    }
+    src(THREAD_META, "first_nz_indices");
+    replace_u(parent_pos, "BMT_size_of_each_blk", std::move(sizes));
+    is_run = true;
+}
+
+// ------------------------------------------------------------ bitmaps
+// thread_bit_map.cc:14-92.  Bit i of map b is 1 iff nz first_nz[b]+i starts a row
+// (LSB = first nz).  With a parent level, the head of every parent_size-th BMT is
+// forced to 1.  The reference's division by zero (no GLOBAL BMT_size_of_each_blk)
+// becomes an error; its one-past-the-end write never reaches an output.
+void thread_bit_map::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    const auto &fn = m.u(THREAD_META, "first_nz_indices", s);
+    GS_CHECK(fn.back() == row.size(), "thread_bit_map: first_nz_indices must end at nnz (thread_bit_map.cc:43)");
+    uint64_t nnz = row.size(), nb = fn.size() - 1;
+    std::vector<uint8_t> bit(nnz);
+    bit[0] = 1;
+    for (uint64_t j = 1; j < nnz; j++) bit[j] = row[j] != row[j - 1];
+    if (parent_flag) {
+        GS_CHECK(m.is_exist(GLOBAL_META, "BMT_size_of_each_blk", s),
+                 "thread_bit_map: GLOBAL BMT_size_of_each_blk missing (reference divides by zero, thread_bit_map.cc:56)");
+        uint64_t ts = fn[1] - fn[0];
+        for (uint64_t i = 0; i < nnz / ts + 1; i += (uint64_t)parent_size)
+            if (i * ts < nnz) bit[i * ts] = 1;
+    }
+    std::vector<uint64_t> maps(nb);
+    for (uint64_t i = 0; i < nb; i++) {
+        uint64_t mm = 0;
+        for (uint64_t j = fn[i + 1]; j-- > fn[i];) mm = (mm << 1) | bit[j];
+        maps[i] = mm;
+    }
+    src(GLOBAL_META, "nz_row_indices");
+    src(THREAD_META, "first_nz_indices");
+    replace_u(THREAD_META, "thread_bit_map", std::move(maps));
+    is_run = true;
+}
+
+// segment_empty_flag.cc:14-75
+void segment_empty_flag::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    const auto &fn = m.u(THREAD_META, "first_nz_indices", s);
+    uint64_t nb = fn.size() - 1;
+    std::vector<uint8_t> flag(nb, 0);
+    for (uint64_t j = 0; j < nb; j++)
+        for (uint64_t i = fn[j] + 1; i < fn[j + 1]; i++)
+            if (row[i] - row[i - 1] > 1) { flag[j] = 1; break; }
+    std::vector<uint64_t> out;
+    for (uint64_t i = 0; i < nb; i += (uint64_t)size) {
+        uint64_t k = std::min<uint64_t>(i + size - 1, nb - 1), cur = 0;
+        for (uint64_t j = k + 1; j-- > i;) cur = (cur << 1) | flag[j];
+        out.push_back(cur);
+    }
+    replace_u(THREAD_META, "segment_empty_flag", std::move(out));
+    is_run = true;
+}
+
+// segment_empty_row_indices.cc
+void segment_empty_row_indices::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    const auto &fn = m.u(THREAD_META, "first_nz_indices", s);
+    std::vector<uint64_t> out;
+    for (uint64_t j = 0; j + 1 < fn.size(); j++) {
+        uint64_t r0 = row[fn[j]];
+        out.push_back(0);
+        for (uint64_t i = fn[j] + 1; i < fn[j + 1]; i++)
+            if (row[i] != row[i - 1]) out.push_back(row[i] - r0);
+    }
+    replace_u(THREAD_META, "segment_empty_row_indices", std::move(out));
+    is_run = true;
+}
+
+// segment_offset.cc: the count pending after the last non-empty map is not written
+void segment_offset::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    const char *src_name = m.is_exist(THREAD_META, "thread_bit_map", s) ? "thread_bit_map" : "bit_map_of_thread";
+    const auto &bm = m.u(THREAD_META, src_name, s);
+    std::vector<uint64_t> out(bm.size(), 0);
+    uint64_t count = 0, prev = 0;
+    for (uint64_t j = 1; j < bm.size(); j++) {
+        if (bm[j] == 0 && ((j % size != 0) || !parent_flag)) count++;
+        else { out[prev] = count; count = 0; prev = j; }
+    }
+    replace_u(THREAD_META, "segment_offset", std::move(out));
+    is_run = true;
+}
+
+// segment_ptr.cc: exclusive running count of row segments per BMT
+void segment_ptr::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    const auto &fn = m.u(THREAD_META, "first_nz_indices", s);
+    std::vector<uint64_t> out{0};
+    uint64_t c = 0;
+    for (uint64_t j = 0; j + 2 < fn.size(); j++) {
+        c += 1;
+        for (uint64_t i = fn[j] + 1; i < fn[j + 1]; i++)
+            if (row[i] != row[i - 1]) c += 1;
+        out.push_back(c);
+    }
+    replace_u(THREAD_META, "segment_ptr", std::move(out));
+    is_run = true;
+}
+
+// get_begin_{rows,nzs,BMTs}_after_merge_thread.cc
+static std::vector<uint64_t> merge_every(const std::vector<uint64_t> &a, int k) {
+    std::vector<uint64_t> out;
+    for (uint64_t j = 0; j + 1 < a.size(); j += (uint64_t)k) out.push_back(a[j]);
+    out.push_back(a.back());
+    return out;
+}
+void get_begin_rows_after_merge_thread::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const char *n = m.is_exist(THREAD_META, "first_row_indices", target_matrix_id) ? "first_row_indices"
+                                                                                   : "first_row_indices_without_ending";
+    replace_u(pos, "first_row_indices", merge_every(m.u(THREAD_META, n, target_matrix_id), merge_num));
+    is_run = true;
+}
+void get_begin_nzs_after_merge_thread::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    replace_u(pos, "first_nz_indices", merge_every(m.u(THREAD_META, "first_nz_indices", target_matrix_id), merge_num));
+    is_run = true;
+}
+void get_begin_BMTs_after_merge_thread::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    uint64_t n = m.u(THREAD_META, "first_nz_indices", target_matrix_id).size();
+    std::vector<uint64_t> out;
+    for (uint64_t j = 0; j + 1 < n; j += (uint64_t)merge_num) out.push_back(j);
+    out.push_back(n - 1);
+    replace_u(pos, "first_BMT_indices", std::move(out));
+    is_run = true;
+}
+
+// ---------------------------------------------------------- balanced (A11)
+// data_transform_common.cc:934-957 (`unsigned int` counters kept)
+std::vector<uint64_t> get_begin_nzs_of_child_after_balance_blocking_in_row_direction(
+    const std::vector<uint64_t> &cnt, uint64_t per) {
+    std::vector<uint64_t> out{0};
+    uint32_t c = 0, tot = 0;
+    for (uint64_t x : cnt) {
+        c += (uint32_t)x;
+        tot += (uint32_t)x;
+        if (c >= per) { out.push_back(tot); c = 0; }
+    }
+    if (c != 0) out.push_back(tot);
+    return out;
+}
+// data_transform_common.cc:960-989
+std::vector<uint64_t> get_begin_rows_of_child_after_balance_blocking_in_row_direction(
+    const std::vector<uint64_t> &cnt, uint64_t per, uint64_t row_num) {
+    std::vector<uint64_t> out{0};
+    uint64_t c = 0;
+    for (uint64_t i = 0; i < row_num; i++) {
+        c += cnt[i];
+        if (c >= per) { out.push_back(i + 1); c = 0; }
+    }
+    if (out.back() < row_num) {
+        GS_CHECK(c != 0, "balanced blocking: empty rows after the last cut (data_transform_common.cc:984)");
+        out.push_back(row_num);
+    }
+    return out;
+}
+
+void get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    uint64_t row_num = row_num_of_sub_matrix(m, target_matrix_id);
+    auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+    replace_u(WARP_META, "first_row_indices",
+              get_begin_rows_of_child_after_balance_blocking_in_row_direction(cnt, nnz_per_interval, row_num));
+    is_run = true;
+}
+
+void get_begin_nzs_of_BMW_after_nnz_blocking_in_row_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    uint64_t row_num = row_num_of_sub_matrix(m, target_matrix_id);
+    auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+    replace_u(WARP_META, "first_nz_indices",
+              get_begin_nzs_of_child_after_balance_blocking_in_row_direction(cnt, nnz_per_interval));
+    is_run = true;
+}
+
+}  // namespace gs

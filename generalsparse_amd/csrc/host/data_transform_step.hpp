@@ -1,0 +1,161 @@
+// data_transform_step.hpp -- the atomic plan rewrites on the hot path.
+//
+// Class names and constructor arguments follow data_transform_step.hpp of the
+// reference (one class per transform_step/*.cc file).  Each run() is an O(nnz)
+// flat-array pass (the reference regroups through vector<vector<>>); the
+// resulting arrays are bit-identical (tests/test_plan_parity.py).
+#pragma once
+
+#include "gs_core.hpp"
+
+namespace gs {
+
+class basic_data_transform_step {
+  public:
+    basic_data_transform_step(std::string name, std::shared_ptr<meta_data_set> m, int target_matrix_id)
+        : name(std::move(name)), meta_data_set_ptr(std::move(m)), target_matrix_id(target_matrix_id) {}
+    virtual ~basic_data_transform_step() = default;
+    virtual void run(bool check) = 0;
+    virtual std::string convert_to_string() const {
+        return name + "::{name:\"" + name + "\",target_matrix_id:" + std::to_string(target_matrix_id) + "}";
+    }
+    const std::vector<std::string> &get_source_data_item_ptr_in_data_transform_step() const { return source; }
+    const std::vector<std::string> &get_dest_data_item_ptr_in_data_transform_step() const { return dest; }
+    std::string name;
+
+  protected:
+    std::shared_ptr<meta_data_set> meta_data_set_ptr;
+    int target_matrix_id;
+    bool is_run = false;
+    std::vector<std::string> source, dest;
+    void src(POS_TYPE p, const char *n) { source.push_back(get_metadata_item_name(p, n, target_matrix_id)); }
+    void dst(POS_TYPE p, const char *n) { dest.push_back(get_metadata_item_name(p, n, target_matrix_id)); }
+    void replace_u(POS_TYPE p, const char *n, std::vector<uint64_t> v);
+    void replace_f(POS_TYPE p, const char *n, std::vector<double> v, data_type t);
+};
+
+#define GS_DECLARE_STEP(cls)                                                        \
+    class cls : public basic_data_transform_step {                                  \
+      public:                                                                       \
+        cls(std::shared_ptr<meta_data_set> m, int target_matrix_id)                 \
+            : basic_data_transform_step(#cls, std::move(m), target_matrix_id) {}    \
+        void run(bool check) override;                                              \
+    };
+
+#define GS_DECLARE_STEP_P(cls, ptype, pname)                                         \
+    class cls : public basic_data_transform_step {                                  \
+      public:                                                                       \
+        cls(std::shared_ptr<meta_data_set> m, int target_matrix_id, ptype pname)    \
+            : basic_data_transform_step(#cls, std::move(m), target_matrix_id), pname(pname) {} \
+        void run(bool check) override;                                              \
+        ptype pname;                                                                \
+    };
+
+// sort_operator (A3, A4)
+GS_DECLARE_STEP(get_row_order_by_length)
+GS_DECLARE_STEP(reorder_val_by_index)
+GS_DECLARE_STEP(reorder_col_by_index)
+GS_DECLARE_STEP(reorder_row_by_index)
+GS_DECLARE_STEP(remove_empty_row_in_end_of_sub_matrix)
+
+// column padding to a multiple of each row size (A6)
+GS_DECLARE_STEP_P(modify_col_indices_by_col_pad_in_sub_matrix, int, multiple_of_each_row_size)
+GS_DECLARE_STEP_P(modify_vals_by_col_pad_in_sub_matrix, int, multiple_of_each_row_size)
+GS_DECLARE_STEP_P(modify_row_indices_by_col_pad_in_sub_matrix, int, multiple_of_each_row_size)
+
+// fixed row-direction blocking (A7, A8, BMW)
+GS_DECLARE_STEP_P(get_begin_rows_of_BMT_after_fixed_blocking_in_row_direction, int, fixed_row_block_size)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMT_after_fixed_blocking_in_row_direction, int, fixed_row_block_size)
+GS_DECLARE_STEP_P(get_begin_rows_of_BMTBs_after_fixed_blocking_in_row_direction, int, fixed_row_block_size)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMTBs_after_fixed_blocking_in_row_direction, int, fixed_row_block_size)
+GS_DECLARE_STEP_P(get_begin_rows_of_BMW_after_fixed_blocking_in_row_direction_without_BMTB, int, fixed_row_block_size)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMW_after_fixed_blocking_in_row_direction_without_BMTB, int, fixed_row_block_size)
+GS_DECLARE_STEP_P(get_begin_rows_of_BMW_after_fixed_blocking_in_row_direction_in_BMTB, int, fixed_row_block_size)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMW_after_fixed_blocking_in_row_direction_in_BMTB, int, fixed_row_block_size)
+GS_DECLARE_STEP(get_begin_BMWs_of_BMTB_after_blocking_in_row_direction)
+
+// fixed nnz-direction blocking (A9)
+GS_DECLARE_STEP_P(modify_col_indices_by_nnz_pad, int, nnz_target)
+GS_DECLARE_STEP_P(modify_vals_by_nnz_pad, int, nnz_target)
+GS_DECLARE_STEP_P(modify_row_indices_by_nnz_pad, int, nnz_target)
+GS_DECLARE_STEP_P(get_begin_rows_of_BMT_after_fixed_blocking_in_nnz_direction, int, nnz_per_BMT)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMT_after_fixed_blocking_in_nnz_direction, int, nnz_per_BMT)
+
+// get_BMT_size_of_each_parent.cc (GLOBAL parent only on the shipped pipelines)
+class get_BMT_size_of_each_parent : public basic_data_transform_step {
+  public:
+    get_BMT_size_of_each_parent(std::shared_ptr<meta_data_set> m, POS_TYPE parent_pos, int target_matrix_id,
+                                bool row_direction_blocking)
+        : basic_data_transform_step("get_BMT_size_of_each_parent", std::move(m), target_matrix_id),
+          parent_pos(parent_pos), row_direction_blocking(row_direction_blocking) {}
+    void run(bool check) override;
+    POS_TYPE parent_pos;
+    bool row_direction_blocking;
+};
+
+// thread bitmaps and segment arrays (thread_bit_map_operator.cc:60-101)
+class thread_bit_map : public basic_data_transform_step {
+  public:
+    thread_bit_map(std::shared_ptr<meta_data_set> m, bool parent_flag, int parent_size, int target_matrix_id)
+        : basic_data_transform_step("thread_bit_map", std::move(m), target_matrix_id), parent_flag(parent_flag),
+          parent_size(parent_size) {}
+    void run(bool check) override;
+    bool parent_flag;
+    int parent_size;
+};
+class segment_empty_flag : public basic_data_transform_step {
+  public:
+    segment_empty_flag(std::shared_ptr<meta_data_set> m, POS_TYPE pos, int size, int target_matrix_id)
+        : basic_data_transform_step("segment_empty_flag", std::move(m), target_matrix_id), pos(pos), size(size) {}
+    void run(bool check) override;
+    POS_TYPE pos;
+    int size;
+};
+class segment_empty_row_indices : public basic_data_transform_step {
+  public:
+    segment_empty_row_indices(std::shared_ptr<meta_data_set> m, POS_TYPE pos, int target_matrix_id)
+        : basic_data_transform_step("segment_empty_row_indices", std::move(m), target_matrix_id), pos(pos) {}
+    void run(bool check) override;
+    POS_TYPE pos;
+};
+class segment_offset : public basic_data_transform_step {
+  public:
+    segment_offset(std::shared_ptr<meta_data_set> m, bool parent_flag, int size, int target_matrix_id)
+        : basic_data_transform_step("segment_offset", std::move(m), target_matrix_id), parent_flag(parent_flag),
+          size(size) {}
+    void run(bool check) override;
+    bool parent_flag;
+    int size;
+};
+class segment_ptr : public basic_data_transform_step {
+  public:
+    segment_ptr(std::shared_ptr<meta_data_set> m, POS_TYPE pos, int target_matrix_id)
+        : basic_data_transform_step("segment_ptr", std::move(m), target_matrix_id), pos(pos) {}
+    void run(bool check) override;
+    POS_TYPE pos;
+};
+
+// warp_segment_reduce_operator.cc:74-111 (merge VW BMTs into a BMW)
+#define GS_DECLARE_MERGE(cls)                                                                   \
+    class cls : public basic_data_transform_step {                                              \
+      public:                                                                                   \
+        cls(std::shared_ptr<meta_data_set> m, POS_TYPE pos, int merge_num, int target_matrix_id) \
+            : basic_data_transform_step(#cls, std::move(m), target_matrix_id), pos(pos), merge_num(merge_num) {} \
+        void run(bool check) override;                                                          \
+        POS_TYPE pos;                                                                           \
+        int merge_num;                                                                          \
+    };
+GS_DECLARE_MERGE(get_begin_rows_after_merge_thread)
+GS_DECLARE_MERGE(get_begin_nzs_after_merge_thread)
+GS_DECLARE_MERGE(get_begin_BMTs_after_merge_thread)
+
+// balanced row-direction warp blocking (A11; data_transform_common.cc:934-989)
+GS_DECLARE_STEP_P(get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction, uint64_t, nnz_per_interval)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMW_after_nnz_blocking_in_row_direction, uint64_t, nnz_per_interval)
+
+std::vector<uint64_t> get_begin_nzs_of_child_after_balance_blocking_in_row_direction(
+    const std::vector<uint64_t> &nnz_of_each_row, uint64_t nnz_per_interval);
+std::vector<uint64_t> get_begin_rows_of_child_after_balance_blocking_in_row_direction(
+    const std::vector<uint64_t> &nnz_of_each_row, uint64_t nnz_per_interval, uint64_t row_num);
+
+}  // namespace gs

@@ -1,0 +1,52 @@
+// gs_plan.hpp -- internal state behind the C ABI handle gs_plan_t.
+#pragma once
+
+#include "operator.hpp"
+
+#include <hip/hip_runtime.h>
+
+namespace gs {
+
+// Device copies of the arrays one kernel family consumes, in the layout the
+// gfx950 kernels want (narrowest index types, A streams padded so aligned
+// over-reads stay in bounds).  One replica = one independent copy of A
+// (bench.py rotates replicas past the 256 MB Infinity Cache).
+struct device_arrays {
+    void *col = nullptr, *val = nullptr;
+    uint32_t *a0 = nullptr, *a1 = nullptr, *a2 = nullptr, *a3 = nullptr, *a4 = nullptr;
+    uint64_t *m0 = nullptr;
+};
+
+struct device_plan {
+    int device = 0;
+    int dtype = 1;         // 0 fp32, 1 fp16 (values, B and C)
+    int col_bytes = 2;     // 2 (u16) or 4 (u32)
+    int scf = 4;           // sparse entries per vector load
+    bool needs_memset = false;
+    uint64_t n_out_rows = 0;  // rows of C
+    uint64_t n_units = 0;     // BMTs / BMWs / BMTBs the grid walks
+    uint64_t n_rows_aux = 0;  // rows covered (thread_total: rows incl. trailing empty)
+    uint64_t row_base = 0;
+    uint64_t nnz_stored = 0;  // padded nnz on device
+    size_t bytes_A = 0;       // device bytes of A per replica (metadata + cols + vals)
+    std::vector<device_arrays> replicas;
+    std::vector<void *> allocations;  // everything to hipFree
+};
+
+struct plan_state {
+    std::shared_ptr<meta_data_set> meta;
+    std::shared_ptr<code_generator> cg;
+    std::shared_ptr<operator_executer> exec;
+    std::string pipeline;
+    uint64_t M = 0, K = 0, nnz = 0;
+    device_plan dev;
+    bool uploaded = false;
+};
+
+// device_plan.hip
+void upload_plan(plan_state &p, int dtype, int device);
+void add_replica(plan_state &p);
+void free_device(plan_state &p);
+void launch_spmm(const plan_state &p, int replica, const void *B, void *C, uint32_t N, hipStream_t stream);
+
+}  // namespace gs

@@ -1,0 +1,593 @@
+// operator.cc -- operators on the hot path; validity rules restate the
+// reference's name-substring checks (cited per class).
+#include "operator.hpp"
+
+#include <algorithm>
+
+namespace gs {
+
+std::string convert_operator_stage_type_to_string(OPERATOR_STAGE_TYPE t) {
+    switch (t) {
+        case CONVERTING_OP: return "CONVERTING_OP";
+        case DISTRIBUTING_OP: return "DISTRIBUTING_OP";
+        case IMPLEMENTING_OP: return "IMPLEMENTING_OP";
+        default: return "NONE_OP";
+    }
+}
+
+void operator_context::add(const std::shared_ptr<basic_operator> &op) {
+    switch (op->get_stage()) {
+        case CONVERTING_OP: converting.push_back(op); break;
+        case DISTRIBUTING_OP: distributing[op->get_target_matrix_id()].push_back(op); break;
+        case IMPLEMENTING_OP: implementing[op->get_target_matrix_id()].push_back(op); break;
+        default: break;
+    }
+}
+
+std::vector<std::shared_ptr<basic_operator>> operator_context::read_operator_context_arr(OPERATOR_STAGE_TYPE stage,
+                                                                                         int sub) const {
+    if (stage == CONVERTING_OP) return converting;
+    const auto &m = stage == DISTRIBUTING_OP ? distributing : implementing;
+    auto it = m.find(sub);
+    return it == m.end() ? std::vector<std::shared_ptr<basic_operator>>{} : it->second;
+}
+
+static bool any_name(const std::vector<std::shared_ptr<basic_operator>> &ops, const char *sub) {
+    for (auto &o : ops)
+        if (o->get_name().find(sub) != std::string::npos) return true;
+    return false;
+}
+
+bool has_row_direction_blocking_in_specific_level(const meta_data_set &m, POS_TYPE pos, int sub) {
+    if (m.is_exist(pos, "first_row_indices_without_ending", sub)) return false;
+    const auto &fr = m.u(pos, "first_row_indices", sub);
+    for (size_t i = 1; i < fr.size(); i++)
+        if (fr[i] == fr[i - 1]) return false;
+    return true;
+}
+
+static bool interlance_storage_existing(const meta_data_set &m, int s) {
+    return m.is_exist(GLOBAL_META, "nz_row_indices_after_interlance_storage", s) ||
+           m.is_exist(GLOBAL_META, "nz_col_indices_after_interlance_storage", s) ||
+           m.is_exist(GLOBAL_META, "nz_vals_after_interlance_storage", s);
+}
+
+static bool coo_present(const meta_data_set &m, int s) {
+    return m.is_exist(GLOBAL_META, "nz_row_indices", s) && m.is_exist(GLOBAL_META, "nz_col_indices", s) &&
+           m.is_exist(GLOBAL_META, "nz_vals", s) && m.is_exist(GLOBAL_META, "begin_row_index", s) &&
+           m.is_exist(GLOBAL_META, "end_row_index", s);
+}
+
+// ------------------------------------------------------------ sort_operator
+sort_operator::sort_operator(cg_ptr cg, ctx_ptr)
+    : basic_operator("sort_operator", cg->get_metadata_set(), CONVERTING_OP, cg->get_sub_matrix_id()) {}
+
+// sort_operator.cc:20-45
+bool sort_operator::is_valid_according_to_operator(ctx_ptr h) {
+    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return false;
+    if (!h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id).empty()) return false;
+    for (auto &o : h->read_operator_context_arr(CONVERTING_OP, target_matrix_id))
+        if (o->get_name().find("sort_operator") != std::string::npos && o->get_target_matrix_id() == target_matrix_id)
+            return false;
+    return true;
+}
+
+// sort_operator.cc:47-67
+bool sort_operator::is_valid_according_to_metadata() {
+    return coo_present(*meta_data_set_ptr, target_matrix_id) && !has(GLOBAL_META, "original_nz_row_indices");
+}
+
+// sort_operator.cc:70-108
+void sort_operator::run(bool check) {
+    if (check) GS_CHECK(is_valid_according_to_metadata(), "sort_operator: invalid metadata");
+    get_row_order_by_length a(meta_data_set_ptr, target_matrix_id);
+    run_step(a, check);
+    reorder_val_by_index b(meta_data_set_ptr, target_matrix_id);
+    run_step(b, check);
+    reorder_col_by_index c(meta_data_set_ptr, target_matrix_id);
+    run_step(c, check);
+    reorder_row_by_index d(meta_data_set_ptr, target_matrix_id);
+    run_step(d, check);
+    remove_empty_row_in_end_of_sub_matrix e(meta_data_set_ptr, target_matrix_id);
+    run_step(e, check);
+    is_run = true;
+}
+
+// -------------------------------------------- row-direction TBLOCK blocking
+fixed_interval_row_direction_tblock_blocking_operator::fixed_interval_row_direction_tblock_blocking_operator(
+    cg_ptr cg, int rb, bool pad, ctx_ptr)
+    : basic_operator("fixed_interval_row_direction_tblock_blocking_operator", cg->get_metadata_set(),
+                     DISTRIBUTING_OP, cg->get_sub_matrix_id()),
+      fixed_row_block_size(rb), is_padding(pad), code_generator_ptr(cg) {
+    GS_CHECK(rb > 0, "fixed_row_block_size > 0");
+}
+
+bool fixed_interval_row_direction_tblock_blocking_operator::is_valid_according_to_operator(ctx_ptr h) {
+    return h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty() &&
+           h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id).empty();
+}
+
+bool fixed_interval_row_direction_tblock_blocking_operator::is_valid_according_to_metadata() {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    return coo_present(m, s) && !interlance_storage_existing(m, s) && m.count_of_metadata_of_diff_pos(TBLOCK_META, s) == 0 &&
+           m.count_of_metadata_of_diff_pos(WARP_META, s) == 0 && m.count_of_metadata_of_diff_pos(THREAD_META, s) == 0;
+}
+
+// fixed_interval_row_direction_tblock_blocking_operator.cc:126-185
+void fixed_interval_row_direction_tblock_blocking_operator::run(bool check) {
+    if (check) GS_CHECK(is_valid_according_to_metadata(), "tblock blocking: invalid metadata");
+    if (is_padding) throw gs_error("row padding (modify_*_by_row_pad_in_sub_matrix) is not built in this round");
+    get_begin_rows_of_BMTBs_after_fixed_blocking_in_row_direction a(meta_data_set_ptr, target_matrix_id,
+                                                                    fixed_row_block_size);
+    run_step(a, check);
+    get_begin_nzs_of_BMTBs_after_fixed_blocking_in_row_direction b(meta_data_set_ptr, target_matrix_id,
+                                                                   fixed_row_block_size);
+    run_step(b, check);
+    code_generator_ptr->open_spec_level_of_paral(TBLOCK_META);
+    is_run = true;
+}
+
+// --------------------------------------------- row-direction WARP blocking
+fixed_interval_row_direction_warp_blocking_operator::fixed_interval_row_direction_warp_blocking_operator(
+    cg_ptr cg, int rb, bool rrel, bool nrel, bool pad, ctx_ptr)
+    : basic_operator("fixed_interval_row_direction_warp_blocking_operator", cg->get_metadata_set(), DISTRIBUTING_OP,
+                     cg->get_sub_matrix_id()),
+      fixed_row_block_size(rb), row_index_is_relative_to_BMTB(rrel), nz_index_is_relative_to_BMTB(nrel),
+      is_padding(pad), code_generator_ptr(cg) {
+    GS_CHECK(rb > 0, "fixed_row_block_size > 0");
+}
+
+// fixed_interval_row_direction_warp_blocking_operator.cc (is_valid_according_to_operator)
+bool fixed_interval_row_direction_warp_blocking_operator::is_valid_according_to_operator(ctx_ptr h) {
+    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return false;
+    auto d = h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
+    return !any_name(d, "thread") && !any_name(d, "warp") && !any_name(d, "col") && !any_name(d, "interlance");
+}
+
+bool fixed_interval_row_direction_warp_blocking_operator::is_valid_according_to_metadata() {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    bool ok = coo_present(m, s) && m.count_of_metadata_of_diff_pos(WARP_META, s) == 0 &&
+              m.count_of_metadata_of_diff_pos(THREAD_META, s) == 0 && !interlance_storage_existing(m, s);
+    int tb = m.count_of_metadata_of_diff_pos(TBLOCK_META, s);
+    if (tb != 0) ok = ok && has_row_direction_blocking_in_specific_level(m, TBLOCK_META, s) && !is_padding;
+    if (row_index_is_relative_to_BMTB) ok = ok && m.is_exist(TBLOCK_META, "first_row_indices", s);
+    if (nz_index_is_relative_to_BMTB) ok = ok && m.is_exist(TBLOCK_META, "first_nz_indices", s);
+    return ok;
+}
+
+void fixed_interval_row_direction_warp_blocking_operator::run(bool check) {
+    if (check) GS_CHECK(is_valid_according_to_metadata(), "warp blocking: invalid metadata");
+    if (row_index_is_relative_to_BMTB || nz_index_is_relative_to_BMTB)
+        throw gs_error("relative BMW indices (SURVEY §8f rank 1) are not built in this round");
+    if (has(TBLOCK_META, "first_row_indices")) {
+        get_begin_rows_of_BMW_after_fixed_blocking_in_row_direction_in_BMTB a(meta_data_set_ptr, target_matrix_id,
+                                                                              fixed_row_block_size);
+        run_step(a, check);
+        get_begin_nzs_of_BMW_after_fixed_blocking_in_row_direction_in_BMTB b(meta_data_set_ptr, target_matrix_id,
+                                                                             fixed_row_block_size);
+        run_step(b, check);
+        get_begin_BMWs_of_BMTB_after_blocking_in_row_direction c(meta_data_set_ptr, target_matrix_id);
+        run_step(c, check);
+    } else {
+        if (is_padding) throw gs_error("row padding is not built in this round");
+        get_begin_rows_of_BMW_after_fixed_blocking_in_row_direction_without_BMTB a(meta_data_set_ptr,
+                                                                                   target_matrix_id,
+                                                                                   fixed_row_block_size);
+        run_step(a, check);
+        get_begin_nzs_of_BMW_after_fixed_blocking_in_row_direction_without_BMTB b(meta_data_set_ptr,
+                                                                                  target_matrix_id,
+                                                                                  fixed_row_block_size);
+        run_step(b, check);
+    }
+    code_generator_ptr->open_spec_level_of_paral(WARP_META);
+    is_run = true;
+}
+
+// ------------------------------------------- row-direction THREAD blocking
+fixed_interval_row_direction_thread_blocking_operator::fixed_interval_row_direction_thread_blocking_operator(
+    cg_ptr cg, int rb, bool rrel, bool nrel, bool row_pad, bool colpad_max, bool colpad_size, int col_size, ctx_ptr)
+    : basic_operator("fixed_interval_row_direction_thread_blocking_operator", cg->get_metadata_set(),
+                     DISTRIBUTING_OP, cg->get_sub_matrix_id()),
+      fixed_row_block_size(rb), row_index_is_relative_to_parent(rrel), nz_index_is_relative_to_parent(nrel),
+      is_row_padding(row_pad), is_col_padding_with_row_max_size_with_empty_row(colpad_max),
+      is_col_padding_with_col_size(colpad_size), col_size(col_size), code_generator_ptr(cg) {
+    GS_CHECK(rb > 0, "fixed_row_block_size > 0");
+    if (row_pad) GS_CHECK(!rrel && !nrel, "row padding needs absolute indices");
+}
+
+// fixed_interval_row_direction_thread_blocking_operator.cc (is_valid_according_to_operator)
+bool fixed_interval_row_direction_thread_blocking_operator::is_valid_according_to_operator(ctx_ptr h) {
+    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return false;
+    auto d = h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
+    bool balanced_and_max_pad = any_name(d, "balanced_interval") && is_col_padding_with_row_max_size_with_empty_row;
+    return !any_name(d, "thread") && !any_name(d, "col") && !any_name(d, "interlance") && !balanced_and_max_pad;
+}
+
+bool fixed_interval_row_direction_thread_blocking_operator::is_valid_according_to_metadata() {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    bool ok = coo_present(m, s) && m.count_of_metadata_of_diff_pos(THREAD_META, s) == 0 &&
+              !interlance_storage_existing(m, s);
+    bool tb = m.is_exist(TBLOCK_META, "first_row_indices", s), wb = m.is_exist(WARP_META, "first_row_indices", s);
+    if (row_index_is_relative_to_parent) ok = ok && (tb || wb);
+    if (nz_index_is_relative_to_parent)
+        ok = ok && (m.is_exist(TBLOCK_META, "first_nz_indices", s) || m.is_exist(WARP_META, "first_nz_indices", s));
+    if (is_row_padding && (tb || wb)) ok = false;
+    if (tb) ok = ok && has_row_direction_blocking_in_specific_level(m, TBLOCK_META, s);
+    if (wb) ok = ok && has_row_direction_blocking_in_specific_level(m, WARP_META, s);
+    return ok;
+}
+
+// fixed_interval_row_direction_thread_blocking_operator.cc:198-575; the
+// no-parent branch (:482-565) is the one token_test exercises
+void fixed_interval_row_direction_thread_blocking_operator::run(bool check) {
+    if (check) GS_CHECK(is_valid_according_to_metadata(), "thread blocking: invalid metadata");
+    if (has(TBLOCK_META, "first_row_indices") || has(WARP_META, "first_row_indices"))
+        throw gs_error("BMT row blocking inside a BMTB/BMW parent is not built in this round");
+    if (is_row_padding) throw gs_error("row padding is not built in this round");
+    if (is_col_padding_with_row_max_size_with_empty_row)
+        throw gs_error("col padding to the parent's max row size is not built in this round");
+    if (is_col_padding_with_col_size) {
+        modify_col_indices_by_col_pad_in_sub_matrix a(meta_data_set_ptr, target_matrix_id, col_size);
+        run_step(a, check);
+        modify_vals_by_col_pad_in_sub_matrix b(meta_data_set_ptr, target_matrix_id, col_size);
+        run_step(b, check);
+        modify_row_indices_by_col_pad_in_sub_matrix c(meta_data_set_ptr, target_matrix_id, col_size);
+        run_step(c, check);
+    }
+    get_begin_rows_of_BMT_after_fixed_blocking_in_row_direction d(meta_data_set_ptr, target_matrix_id,
+                                                                  fixed_row_block_size);
+    run_step(d, check);
+    get_begin_nzs_of_BMT_after_fixed_blocking_in_row_direction e(meta_data_set_ptr, target_matrix_id,
+                                                                 fixed_row_block_size);
+    run_step(e, check);
+    code_generator_ptr->open_spec_level_of_paral(THREAD_META);
+    code_generator_ptr->set_thread_for_row(true);
+    is_run = true;
+}
+
+// ------------------------------------------- nnz-direction THREAD blocking
+fixed_interval_nnz_direction_thread_blocking_operator::fixed_interval_nnz_direction_thread_blocking_operator(
+    cg_ptr cg, int nnz_per_BMT, bool rrel, bool nrel, bool nnz_padding, ctx_ptr)
+    : basic_operator("fixed_interval_nnz_direction_thread_blocking_operator", cg->get_metadata_set(),
+                     DISTRIBUTING_OP, cg->get_sub_matrix_id()),
+      nnz_per_BMT(nnz_per_BMT), row_index_is_relative_to_parent(rrel), nz_index_is_relative_to_parent(nrel),
+      nnz_padding(nnz_padding), code_generator_ptr(cg) {
+    GS_CHECK(nnz_per_BMT > 0 && nnz_per_BMT <= 64, "nnz_per_BMT in [1, 64] (bitmaps are 64-bit)");
+}
+
+// fixed_interval_nnz_direction_thread_blocking_operator.cc:40-96
+bool fixed_interval_nnz_direction_thread_blocking_operator::is_valid_according_to_operator(ctx_ptr h) {
+    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return false;
+    for (auto &o : h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id)) {
+        const auto &n = o->get_name();
+        if (n.find("fixed_interval_nnz_direction_tblock_blocking_operator") == std::string::npos &&
+            n.find("fixed_interval_nnz_direction_warp_blocking_operator") == std::string::npos)
+            return false;
+    }
+    return true;
+}
+
+bool fixed_interval_nnz_direction_thread_blocking_operator::is_valid_according_to_metadata() {
+    auto &m = *meta_data_set_ptr;
+    return coo_present(m, target_matrix_id) && m.count_of_metadata_of_diff_pos(THREAD_META, target_matrix_id) == 0 &&
+           !interlance_storage_existing(m, target_matrix_id);
+}
+
+// fixed_interval_nnz_direction_thread_blocking_operator.cc:156-245 (no-parent branch)
+void fixed_interval_nnz_direction_thread_blocking_operator::run(bool check) {
+    if (check) GS_CHECK(is_valid_according_to_metadata(), "nnz blocking: invalid metadata");
+    if (row_index_is_relative_to_parent || nz_index_is_relative_to_parent ||
+        has(TBLOCK_META, "first_row_indices") || has(WARP_META, "first_row_indices"))
+        throw gs_error("nnz-direction BMT blocking inside a parent is not built in this round");
+    if (nnz_padding) {
+        modify_col_indices_by_nnz_pad a(meta_data_set_ptr, target_matrix_id, nnz_per_BMT);
+        run_step(a, check);
+        modify_vals_by_nnz_pad b(meta_data_set_ptr, target_matrix_id, nnz_per_BMT);
+        run_step(b, check);
+        modify_row_indices_by_nnz_pad c(meta_data_set_ptr, target_matrix_id, nnz_per_BMT);
+        run_step(c, check);
+    }
+    get_begin_rows_of_BMT_after_fixed_blocking_in_nnz_direction d(meta_data_set_ptr, target_matrix_id, nnz_per_BMT);
+    run_step(d, check);
+    get_begin_nzs_of_BMT_after_fixed_blocking_in_nnz_direction e(meta_data_set_ptr, target_matrix_id, nnz_per_BMT);
+    run_step(e, check);
+    get_BMT_size_of_each_parent f(meta_data_set_ptr, GLOBAL_META, target_matrix_id, false);
+    run_step(f, check);
+    code_generator_ptr->open_spec_level_of_paral(THREAD_META);
+    is_run = true;
+}
+
+// --------------------------------------- balanced row-direction WARP blocking
+balanced_interval_row_direction_warp_blocking_operator::balanced_interval_row_direction_warp_blocking_operator(
+    cg_ptr cg, int per, bool rrel, bool nrel, ctx_ptr)
+    : basic_operator("balanced_interval_row_direction_warp_blocking_operator", cg->get_metadata_set(),
+                     DISTRIBUTING_OP, cg->get_sub_matrix_id()),
+      nnz_per_interval(per), row_index_is_relative_to_BMTB(rrel), nz_index_is_relative_to_BMTB(nrel),
+      code_generator_ptr(cg) {
+    GS_CHECK(per > 0, "nnz_per_interval > 0");
+}
+
+bool balanced_interval_row_direction_warp_blocking_operator::is_valid_according_to_operator(ctx_ptr h) {
+    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return false;
+    auto d = h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
+    return !any_name(d, "thread") && !any_name(d, "warp") && !any_name(d, "nnz_direction") && !any_name(d, "col") &&
+           !any_name(d, "interlance");
+}
+
+bool balanced_interval_row_direction_warp_blocking_operator::is_valid_according_to_metadata() {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    bool ok = coo_present(m, s) && m.count_of_metadata_of_diff_pos(THREAD_META, s) == 0 &&
+              m.count_of_metadata_of_diff_pos(WARP_META, s) == 0 && !interlance_storage_existing(m, s);
+    if (m.is_exist(TBLOCK_META, "first_row_indices", s))
+        ok = ok && has_row_direction_blocking_in_specific_level(m, TBLOCK_META, s);
+    return ok;
+}
+
+// balanced_interval_row_direction_warp_blocking_operator.cc:177-227 (no-parent branch)
+void balanced_interval_row_direction_warp_blocking_operator::run(bool check) {
+    if (check) GS_CHECK(is_valid_according_to_metadata(), "balanced warp blocking: invalid metadata");
+    if (has(TBLOCK_META, "first_row_indices"))
+        throw gs_error("balanced BMWs inside BMTBs are not built in this round");
+    get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction a(meta_data_set_ptr, target_matrix_id,
+                                                               (uint64_t)nnz_per_interval);
+    run_step(a, check);
+    get_begin_nzs_of_BMW_after_nnz_blocking_in_row_direction b(meta_data_set_ptr, target_matrix_id,
+                                                              (uint64_t)nnz_per_interval);
+    run_step(b, check);
+    code_generator_ptr->open_spec_level_of_paral(WARP_META);
+    is_run = true;
+}
+
+// ------------------------------------------------------------- implementing
+thread_total_reduce_operator::thread_total_reduce_operator(cg_ptr cg, bool nwr, int scf, int cf, ctx_ptr)
+    : basic_operator("thread_total_reduce_operator", cg->get_metadata_set(), IMPLEMENTING_OP,
+                     cg->get_sub_matrix_id()),
+      need_warp_reduction(nwr), sparse_coarsen_factor(scf), coarsen_factor(cf), code_generator_ptr(cg) {}
+
+// thread_total_reduce_operator.cc:14-40
+bool thread_total_reduce_operator::is_valid_according_to_operator(ctx_ptr h) {
+    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return false;
+    auto d = h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
+    return !any_name(d, "nnz") && any_name(d, "thread");
+}
+
+bool thread_total_reduce_operator::is_valid_according_to_metadata() { return has(THREAD_META, "first_nz_indices"); }
+
+// thread_total_reduce_operator.cc:57-79
+void thread_total_reduce_operator::run(bool check) {
+    GS_CHECK(is_valid_according_to_metadata(), "thread_total_reduce: no THREAD first_nz_indices");
+    reduction_token t;
+    t.kind = reduction_kind::TOTAL_BMT_RESULT;
+    t.need_warp_reduction = need_warp_reduction;
+    t.sparse_coarsen_factor = sparse_coarsen_factor;
+    t.coarsen_factor = coarsen_factor;
+    code_generator_ptr->set_reduction_token(THREAD_META, t);
+    code_generator_ptr->open_spec_level_of_paral(THREAD_META);
+    is_run = true;
+}
+
+warp_total_reduce_operator::warp_total_reduce_operator(cg_ptr cg, int cf, ctx_ptr)
+    : basic_operator("warp_total_reduce_operator", cg->get_metadata_set(), IMPLEMENTING_OP, cg->get_sub_matrix_id()),
+      coarsen_factor(cf), code_generator_ptr(cg) {}
+
+// warp_total_reduce_operator.cc:14-38
+bool warp_total_reduce_operator::is_valid_according_to_operator(ctx_ptr h) {
+    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return false;
+    auto d = h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
+    return !any_name(d, "nnz") && any_name(d, "warp");
+}
+
+bool warp_total_reduce_operator::is_valid_according_to_metadata() { return has(WARP_META, "first_nz_indices"); }
+
+void warp_total_reduce_operator::run(bool check) {
+    GS_CHECK(is_valid_according_to_metadata(), "warp_total_reduce: no WARP first_nz_indices");
+    reduction_token t;
+    t.kind = reduction_kind::TOTAL_WARP_RESULT;
+    t.coarsen_factor = coarsen_factor;
+    code_generator_ptr->set_reduction_token(WARP_META, t);
+    code_generator_ptr->open_spec_level_of_paral(WARP_META);
+    is_run = true;
+}
+
+tblock_total_reduce_operator::tblock_total_reduce_operator(cg_ptr cg, int cf, ctx_ptr)
+    : basic_operator("tblock_total_reduce_operator", cg->get_metadata_set(), IMPLEMENTING_OP,
+                     cg->get_sub_matrix_id()),
+      coarsen_factor(cf), code_generator_ptr(cg) {}
+
+// tblock_total_reduce_operator.cc
+bool tblock_total_reduce_operator::is_valid_according_to_operator(ctx_ptr h) {
+    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return false;
+    auto d = h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
+    return !any_name(d, "nnz") && any_name(d, "tblock");
+}
+
+bool tblock_total_reduce_operator::is_valid_according_to_metadata() { return has(TBLOCK_META, "first_nz_indices"); }
+
+void tblock_total_reduce_operator::run(bool check) {
+    GS_CHECK(is_valid_according_to_metadata(), "tblock_total_reduce: no TBLOCK first_nz_indices");
+    reduction_token t;
+    t.kind = reduction_kind::TOTAL_BLOCK_RESULT;
+    t.coarsen_factor = coarsen_factor;
+    code_generator_ptr->set_reduction_token(TBLOCK_META, t);
+    code_generator_ptr->open_spec_level_of_paral(TBLOCK_META);
+    is_run = true;
+}
+
+thread_bit_map_operator::thread_bit_map_operator(cg_ptr cg, POS_TYPE pos, unsigned size, unsigned scf, unsigned cf,
+                                                 ctx_ptr)
+    : basic_operator("thread_bit_map_operator", cg->get_metadata_set(), IMPLEMENTING_OP, cg->get_sub_matrix_id()),
+      pos(pos), size(size), sparse_coarsen_factor(scf), coarsen_factor(cf), code_generator_ptr(cg) {
+    GS_CHECK(cf <= 16, "coarsen_factor <= 16");
+    GS_CHECK(size >= 1, "bitmap group size >= 1");
+    code_generator_ptr->open_spec_level_of_paral(THREAD_META);
+}
+
+// thread_bit_map_operator.cc (is_valid_according_to_operator)
+bool thread_bit_map_operator::is_valid_according_to_operator(ctx_ptr h) {
+    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return false;
+    auto d = h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
+    return any_name(d, "thread") && any_name(d, "nnz");
+}
+
+bool thread_bit_map_operator::is_valid_according_to_metadata() { return has(THREAD_META, "first_nz_indices"); }
+
+// thread_bit_map_operator.cc:60-101
+void thread_bit_map_operator::run(bool check) {
+    GS_CHECK(is_valid_according_to_metadata(), "thread_bit_map: no THREAD first_nz_indices");
+    bool parent_flag = pos != THREAD_META;
+    thread_bit_map a(meta_data_set_ptr, parent_flag, (int)size, target_matrix_id);
+    run_step(a, check);
+    segment_empty_flag b(meta_data_set_ptr, pos, (int)size, target_matrix_id);
+    run_step(b, check);
+    segment_empty_row_indices c(meta_data_set_ptr, pos, target_matrix_id);
+    run_step(c, check);
+    segment_offset d(meta_data_set_ptr, false, (int)size, target_matrix_id);
+    run_step(d, check);
+    segment_ptr e(meta_data_set_ptr, pos, target_matrix_id);
+    run_step(e, check);
+    reduction_token t;
+    t.kind = reduction_kind::THREAD_BIT_MAP;
+    t.need_warp_reduction = pos == WARP_META;
+    t.sparse_coarsen_factor = (int)sparse_coarsen_factor;
+    t.coarsen_factor = (int)coarsen_factor;
+    t.size = (int)size;
+    code_generator_ptr->set_reduction_token(THREAD_META, t);
+    code_generator_ptr->open_spec_level_of_paral(THREAD_META);
+    is_run = true;
+}
+
+warp_segment_reduce_operator::warp_segment_reduce_operator(cg_ptr cg, unsigned cf, bool rnz, bool rrow, ctx_ptr)
+    : basic_operator("warp_segment_reduce_operator", cg->get_metadata_set(), IMPLEMENTING_OP,
+                     cg->get_sub_matrix_id()),
+      coarsen_factor(cf), relative_nz(rnz), relative_row(rrow), code_generator_ptr(cg) {
+    GS_CHECK(cf <= 16, "coarsen_factor <= 16");
+    code_generator_ptr->open_spec_level_of_paral(WARP_META);
+}
+
+// warp_segment_reduce_operator.cc:14-56
+bool warp_segment_reduce_operator::is_valid_according_to_operator(ctx_ptr h) {
+    auto d = h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
+    auto i = h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id);
+    return any_name(d, "thread") && any_name(d, "nnz") && !any_name(d, "warp") && any_name(i, "thread_bit_map");
+}
+
+bool warp_segment_reduce_operator::is_valid_according_to_metadata() {
+    return has(THREAD_META, "first_nz_indices") && !has(WARP_META, "first_nz_indices");
+}
+
+// warp_segment_reduce_operator.cc:74-111; merge_num = VECTOR_WIDTH
+void warp_segment_reduce_operator::run(bool check) {
+    GS_CHECK(is_valid_according_to_metadata(), "warp_segment_reduce: invalid metadata");
+    if (relative_nz || relative_row) throw gs_error("relative BMW indices are not built in this round");
+    int vw = (int)get_config().VECTOR_WIDTH;
+    GS_CHECK(vw >= 1, "VECTOR_WIDTH >= 1");
+    get_begin_rows_after_merge_thread a(meta_data_set_ptr, WARP_META, vw, target_matrix_id);
+    run_step(a, check);
+    get_begin_nzs_after_merge_thread b(meta_data_set_ptr, WARP_META, vw, target_matrix_id);
+    run_step(b, check);
+    get_begin_BMTs_after_merge_thread c(meta_data_set_ptr, WARP_META, vw, target_matrix_id);
+    run_step(c, check);
+    reduction_token t;
+    t.kind = reduction_kind::WARP_SEGMENT;
+    t.coarsen_factor = (int)coarsen_factor;
+    t.size = vw;
+    code_generator_ptr->set_reduction_token(WARP_META, t);
+    code_generator_ptr->open_spec_level_of_paral(WARP_META);
+    is_run = true;
+}
+
+grid_block_operator::grid_block_operator(cg_ptr cg, unsigned grid_x, std::vector<unsigned> blk, unsigned cf, ctx_ptr)
+    : basic_operator("grid_block_operator", cg->get_metadata_set(), IMPLEMENTING_OP, cg->get_sub_matrix_id()),
+      code_generator_ptr(cg) {
+    // grid_block_operator.cc:13-25: grid_y covers the dense columns
+    GS_CHECK(blk.size() == 2 && blk[0] > 0 && blk[1] > 0, "block must be {x, y}");
+    if (blk[1] % 2 && blk[1] > 1) blk[1] += 1;
+    unsigned N = (unsigned)get_config().DENSE_MATRIX_SIZE;
+    unsigned per = std::max(1u, blk[0] * std::max(1u, cf));
+    grid = {grid_x, std::max(1u, (N + per - 1) / per)};
+    block = blk;
+}
+
+void grid_block_operator::run(bool) {
+    code_generator_ptr->set_thread_grid(grid, block);
+    is_run = true;
+}
+
+// -------------------------------------------------------------- executer
+// operator_executer.cc:19-26
+void operator_executer::add_and_run(const std::shared_ptr<basic_operator> &op) {
+    if (!op->is_valid_according_to_operator(ctx))
+        throw gs_error("operator_executer: " + op->get_name() + " is not valid after the operators already run");
+    bool check = get_config().OPERATOR_RUNTIME_CHECK;
+    op->run(check);
+    ctx->add(op);
+    history_log.push_back(op->convert_to_string());
+    for (auto &s : op->get_data_transform_sequence()) history_log.push_back("  " + s);
+}
+
+// -------------------------------------------------------------- factory
+std::shared_ptr<basic_operator> make_operator(const std::string &name, const std::vector<long long> &a, cg_ptr cg,
+                                              ctx_ptr ctx) {
+    auto need = [&](size_t n) {
+        GS_CHECK(a.size() == n, name + ": expected " + std::to_string(n) + " arguments");
+    };
+    if (name == "sort_operator") { need(0); return std::make_shared<sort_operator>(cg, ctx); }
+    if (name == "fixed_interval_row_direction_tblock_blocking_operator") {
+        need(2);
+        return std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, (int)a[0], a[1] != 0, ctx);
+    }
+    if (name == "fixed_interval_row_direction_warp_blocking_operator") {
+        need(4);
+        return std::make_shared<fixed_interval_row_direction_warp_blocking_operator>(cg, (int)a[0], a[1] != 0,
+                                                                                     a[2] != 0, a[3] != 0, ctx);
+    }
+    if (name == "fixed_interval_row_direction_thread_blocking_operator") {
+        need(7);
+        return std::make_shared<fixed_interval_row_direction_thread_blocking_operator>(
+            cg, (int)a[0], a[1] != 0, a[2] != 0, a[3] != 0, a[4] != 0, a[5] != 0, (int)a[6], ctx);
+    }
+    if (name == "fixed_interval_nnz_direction_thread_blocking_operator") {
+        need(4);
+        return std::make_shared<fixed_interval_nnz_direction_thread_blocking_operator>(cg, (int)a[0], a[1] != 0,
+                                                                                       a[2] != 0, a[3] != 0, ctx);
+    }
+    if (name == "balanced_interval_row_direction_warp_blocking_operator") {
+        need(3);
+        return std::make_shared<balanced_interval_row_direction_warp_blocking_operator>(cg, (int)a[0], a[1] != 0,
+                                                                                        a[2] != 0, ctx);
+    }
+    if (name == "thread_total_reduce_operator") {
+        need(3);
+        return std::make_shared<thread_total_reduce_operator>(cg, a[0] != 0, (int)a[1], (int)a[2], ctx);
+    }
+    if (name == "warp_total_reduce_operator") {
+        need(1);
+        return std::make_shared<warp_total_reduce_operator>(cg, (int)a[0], ctx);
+    }
+    if (name == "tblock_total_reduce_operator") {
+        need(1);
+        return std::make_shared<tblock_total_reduce_operator>(cg, (int)a[0], ctx);
+    }
+    if (name == "thread_bit_map_operator") {
+        need(4);  // pos (0 THREAD, 1 WARP, 2 TBLOCK), size, sparse_cf, cf
+        POS_TYPE p = a[0] == 1 ? WARP_META : (a[0] == 2 ? TBLOCK_META : THREAD_META);
+        return std::make_shared<thread_bit_map_operator>(cg, p, (unsigned)a[1], (unsigned)a[2], (unsigned)a[3], ctx);
+    }
+    if (name == "warp_segment_reduce_operator") {
+        need(3);
+        return std::make_shared<warp_segment_reduce_operator>(cg, (unsigned)a[0], a[1] != 0, a[2] != 0, ctx);
+    }
+    if (name == "grid_block_operator") {
+        need(4);  // grid_x, block_x, block_y, cf
+        return std::make_shared<grid_block_operator>(cg, (unsigned)a[0],
+                                                     std::vector<unsigned>{(unsigned)a[1], (unsigned)a[2]},
+                                                     (unsigned)a[3], ctx);
+    }
+    throw gs_error("unknown operator " + name);
+}
+
+}  // namespace gs

@@ -1,0 +1,267 @@
+// operator.hpp -- the plugin surface (operator.hpp:16-1324 of the reference).
+//
+// Same class names, stages and constructor argument order as the reference
+// (the token_test pipelines are written against them); validity is decided
+// by the same name-substring rules over the operator history.  run() calls
+// the transform steps in data_transform_step.hpp and attaches reduction
+// tokens to the code generator.
+#pragma once
+
+#include "code_generator.hpp"
+#include "data_transform_step.hpp"
+
+namespace gs {
+
+enum OPERATOR_STAGE_TYPE { CONVERTING_OP, DISTRIBUTING_OP, IMPLEMENTING_OP, NONE_OP };
+std::string convert_operator_stage_type_to_string(OPERATOR_STAGE_TYPE t);
+
+class basic_operator;
+
+// operator.hpp:191-265: CONVERTING is a flat list, the others per sub-matrix
+class operator_context {
+  public:
+    void add(const std::shared_ptr<basic_operator> &op);
+    std::vector<std::shared_ptr<basic_operator>> read_operator_context_arr(OPERATOR_STAGE_TYPE stage, int sub) const;
+
+  private:
+    std::vector<std::shared_ptr<basic_operator>> converting;
+    std::map<int, std::vector<std::shared_ptr<basic_operator>>> distributing, implementing;
+};
+
+class basic_operator {
+  public:
+    basic_operator(std::string name, std::shared_ptr<meta_data_set> m, OPERATOR_STAGE_TYPE stage, int target_matrix_id)
+        : name(std::move(name)), meta_data_set_ptr(std::move(m)), stage(stage), target_matrix_id(target_matrix_id) {}
+    virtual ~basic_operator() = default;
+    virtual void run(bool check = true) = 0;
+    virtual bool is_valid_according_to_metadata() = 0;
+    virtual bool is_valid_according_to_operator(std::shared_ptr<operator_context> history) = 0;
+    virtual std::vector<std::string> get_data_transform_sequence() const { return transform_seq; }
+    virtual std::string convert_to_string() const {
+        return name + "::{name:\"" + name + "\",stage:" + convert_operator_stage_type_to_string(stage) +
+               ",target_matrix_id:" + std::to_string(target_matrix_id) + "}";
+    }
+    virtual void set_padding_to_false() {}
+    const std::string &get_name() const { return name; }
+    OPERATOR_STAGE_TYPE get_stage() const { return stage; }
+    int get_target_matrix_id() const { return target_matrix_id; }
+
+  protected:
+    std::string name;
+    std::shared_ptr<meta_data_set> meta_data_set_ptr;
+    OPERATOR_STAGE_TYPE stage;
+    int target_matrix_id;
+    bool is_run = false;
+    std::vector<std::string> transform_seq;
+    void run_step(basic_data_transform_step &st, bool check) {
+        st.run(check);
+        transform_seq.push_back(st.convert_to_string());
+    }
+    bool has(POS_TYPE p, const char *n) const { return meta_data_set_ptr->is_exist(p, n, target_matrix_id); }
+};
+
+using cg_ptr = std::shared_ptr<code_generator>;
+using ctx_ptr = std::shared_ptr<operator_context>;
+
+// ---------------------------------------------------------------- CONVERTING
+class sort_operator : public basic_operator {  // operator/sort_operator.cc
+  public:
+    sort_operator(cg_ptr cg, ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+};
+
+// -------------------------------------------------------------- DISTRIBUTING
+class fixed_interval_row_direction_tblock_blocking_operator : public basic_operator {
+  public:
+    fixed_interval_row_direction_tblock_blocking_operator(cg_ptr cg, int fixed_row_block_size, bool is_padding,
+                                                          ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    void set_padding_to_false() override { is_padding = false; }
+    int fixed_row_block_size;
+    bool is_padding;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
+class fixed_interval_row_direction_warp_blocking_operator : public basic_operator {
+  public:
+    fixed_interval_row_direction_warp_blocking_operator(cg_ptr cg, int fixed_row_block_size,
+                                                        bool row_index_is_relative_to_BMTB,
+                                                        bool nz_index_is_relative_to_BMTB, bool is_padding,
+                                                        ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    void set_padding_to_false() override { is_padding = false; }
+    int fixed_row_block_size;
+    bool row_index_is_relative_to_BMTB, nz_index_is_relative_to_BMTB, is_padding;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
+class fixed_interval_row_direction_thread_blocking_operator : public basic_operator {
+  public:
+    fixed_interval_row_direction_thread_blocking_operator(cg_ptr cg, int fixed_row_block_size,
+                                                          bool row_index_is_relative_to_parent,
+                                                          bool nz_index_is_relative_to_parent, bool is_row_padding,
+                                                          bool is_col_padding_with_row_max_size_with_empty_row,
+                                                          bool is_col_padding_with_col_size, int col_size,
+                                                          ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    void set_padding_to_false() override {
+        is_row_padding = false;
+        is_col_padding_with_col_size = false;
+        is_col_padding_with_row_max_size_with_empty_row = false;
+    }
+    int fixed_row_block_size;
+    bool row_index_is_relative_to_parent, nz_index_is_relative_to_parent, is_row_padding;
+    bool is_col_padding_with_row_max_size_with_empty_row, is_col_padding_with_col_size;
+    int col_size;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
+class fixed_interval_nnz_direction_thread_blocking_operator : public basic_operator {
+  public:
+    fixed_interval_nnz_direction_thread_blocking_operator(cg_ptr cg, int nnz_per_BMT,
+                                                          bool row_index_is_relative_to_parent,
+                                                          bool nz_index_is_relative_to_parent, bool nnz_padding,
+                                                          ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    void set_padding_to_false() override { nnz_padding = false; }
+    int get_nnz_per_BMT() const { return nnz_per_BMT; }
+    int nnz_per_BMT;
+    bool row_index_is_relative_to_parent, nz_index_is_relative_to_parent, nnz_padding;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
+class balanced_interval_row_direction_warp_blocking_operator : public basic_operator {
+  public:
+    balanced_interval_row_direction_warp_blocking_operator(cg_ptr cg, int nnz_per_interval,
+                                                           bool row_index_is_relative, bool nz_index_is_relative,
+                                                           ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    int nnz_per_interval;
+    bool row_index_is_relative_to_BMTB, nz_index_is_relative_to_BMTB;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
+// -------------------------------------------------------------- IMPLEMENTING
+class thread_total_reduce_operator : public basic_operator {
+  public:
+    thread_total_reduce_operator(cg_ptr cg, bool need_warp_reduction, int sparse_coarsen_factor, int coarsen_factor,
+                                 ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    bool need_warp_reduction;
+    int sparse_coarsen_factor, coarsen_factor;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
+class warp_total_reduce_operator : public basic_operator {
+  public:
+    warp_total_reduce_operator(cg_ptr cg, int coarsen_factor, ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    int coarsen_factor;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
+class tblock_total_reduce_operator : public basic_operator {
+  public:
+    tblock_total_reduce_operator(cg_ptr cg, int coarsen_factor, ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    int coarsen_factor;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
+class thread_bit_map_operator : public basic_operator {
+  public:
+    thread_bit_map_operator(cg_ptr cg, POS_TYPE pos, unsigned size, unsigned sparse_coarsen_factor,
+                            unsigned coarsen_factor, ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    POS_TYPE pos;
+    unsigned size, sparse_coarsen_factor, coarsen_factor;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
+class warp_segment_reduce_operator : public basic_operator {
+  public:
+    warp_segment_reduce_operator(cg_ptr cg, unsigned coarsen_factor, bool relative_nz, bool relative_row,
+                                 ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    unsigned coarsen_factor;
+    bool relative_nz, relative_row;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
+class grid_block_operator : public basic_operator {  // operator/grid_block_operator.cc:2-35
+  public:
+    grid_block_operator(cg_ptr cg, unsigned grid_x, std::vector<unsigned> block, unsigned coarsen_factor,
+                        ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override { return true; }
+    bool is_valid_according_to_operator(ctx_ptr) override { return true; }
+    std::vector<unsigned> grid, block;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
+// operator_executer.cc:19-26: assert valid -> run -> record history
+class operator_executer {
+  public:
+    operator_executer() : ctx(std::make_shared<operator_context>()) {}
+    void add_and_run(const std::shared_ptr<basic_operator> &op);
+    std::shared_ptr<operator_context> get_operator_context() const { return ctx; }
+    const std::vector<std::string> &log() const { return history_log; }
+
+  private:
+    std::shared_ptr<operator_context> ctx;
+    std::vector<std::string> history_log;
+};
+
+// data_transform_common.cc:330-376
+bool has_row_direction_blocking_in_specific_level(const meta_data_set &m, POS_TYPE pos, int sub);
+
+// Factory used by the C ABI: builds an operator from its reference class name
+// and integer arguments (in constructor order, minus cg/history).
+std::shared_ptr<basic_operator> make_operator(const std::string &name, const std::vector<long long> &args,
+                                              cg_ptr cg, ctx_ptr ctx);
+
+}  // namespace gs

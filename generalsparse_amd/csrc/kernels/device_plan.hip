@@ -1,0 +1,298 @@
+// device_plan.hip -- uploads a compiled plan to HBM in the layout of its
+// kernel family and dispatches the gfx950 kernels of hip_code/kernel_lib.hpp.
+#include "../hip_code/kernel_lib.hpp"
+#include "../host/gs_plan.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+namespace gs {
+
+#define HIP_OK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) throw gs_error(std::string(#x) + ": " + hipGetErrorString(e_), -3); \
+    } while (0)
+
+namespace {
+
+constexpr uint64_t kPad = 64;  // extra zeroed entries after every A stream
+
+template <class T>
+T *dev_copy(device_plan &d, const std::vector<T> &h, uint64_t pad = 0) {
+    size_t n = h.size() + pad;
+    T *p = nullptr;
+    HIP_OK(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)));
+    d.allocations.push_back(p);
+    if (!h.empty()) HIP_OK(hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+    if (pad) HIP_OK(hipMemset(p + h.size(), 0, pad * sizeof(T)));
+    d.bytes_A += h.size() * sizeof(T);
+    return p;
+}
+
+std::vector<uint32_t> to_u32(const std::vector<uint64_t> &v, const char *what) {
+    std::vector<uint32_t> o(v.size());
+    for (size_t i = 0; i < v.size(); i++) {
+        GS_CHECK(v[i] <= 0xffffffffull, std::string(what) + " exceeds 32 bits");
+        o[i] = (uint32_t)v[i];
+    }
+    return o;
+}
+
+// CSR row pointer of the (possibly padded, row-sorted) COO
+std::vector<uint32_t> csr_row_ptr(const std::vector<uint64_t> &row, uint64_t row_num) {
+    std::vector<uint32_t> rp(row_num + 1, 0);
+    for (uint64_t r : row) {
+        GS_CHECK(r < row_num, "row index beyond row count");
+        rp[r + 1]++;
+    }
+    for (uint64_t i = 0; i < row_num; i++) rp[i + 1] += rp[i];
+    return rp;
+}
+
+uint16_t f32_to_f16_bits(float f) {
+    _Float16 h = (_Float16)f;
+    uint16_t b;
+    std::memcpy(&b, &h, 2);
+    return b;
+}
+
+}  // namespace
+
+void upload_plan(plan_state &p, int dtype, int device) {
+    GS_CHECK(p.cg && p.cg->is_compiled(), "plan must be compiled before upload");
+    GS_CHECK(dtype == 0 || dtype == 1, "dtype must be 0 (fp32) or 1 (fp16)");
+    free_device(p);
+    HIP_OK(hipSetDevice(device));
+    const kernel_spec &sp = p.cg->get_kernel_spec();
+    const meta_data_set &m = *p.meta;
+    device_plan &d = p.dev;
+    d = device_plan();
+    d.device = device;
+    d.dtype = dtype;
+    d.n_out_rows = p.M;
+    d.row_base = m.scalar(GLOBAL_META, "begin_row_index", 0);
+    const auto &col = m.u(GLOBAL_META, "nz_col_indices", 0);
+    const auto &rows = m.u(GLOBAL_META, "nz_row_indices", 0);
+    auto vals = m.get_element(GLOBAL_META, "nz_vals", 0)->meta_data_arr;
+    uint64_t nnz = col.size();
+    GS_CHECK(nnz < 0xffffffffull - kPad, "nnz exceeds 32-bit offsets");
+    d.nnz_stored = nnz;
+    device_arrays a;
+    // A streams: narrowest column type that holds Kc-1 (u16 when Kc <= 65536)
+    uint64_t maxc = 0;
+    for (uint64_t c : col) maxc = std::max(maxc, c);
+    d.col_bytes = maxc <= 0xffff ? 2 : 4;
+    if (d.col_bytes == 2) {
+        std::vector<uint16_t> c16(col.begin(), col.end());
+        a.col = dev_copy(d, c16, kPad);
+    } else {
+        a.col = dev_copy(d, to_u32(col, "column index"), kPad);
+    }
+    if (dtype == 0) {
+        std::vector<float> v(nnz);
+        for (uint64_t i = 0; i < nnz; i++) v[i] = (float)vals->read_float_from_arr(i);
+        a.val = dev_copy(d, v, kPad);
+    } else {
+        std::vector<uint16_t> v(nnz);
+        for (uint64_t i = 0; i < nnz; i++) v[i] = f32_to_f16_bits((float)vals->read_float_from_arr(i));
+        a.val = dev_copy(d, v, kPad);
+    }
+    uint64_t row_num = row_num_of_sub_matrix(m, 0);
+    switch (sp.family) {
+        case KF_THREAD_TOTAL: {
+            const auto &fn = m.u(THREAD_META, "first_nz_indices", 0);
+            const auto &fr = m.u(THREAD_META, "first_row_indices", 0);
+            for (size_t i = 0; i < fr.size(); i++)
+                GS_CHECK(fr[i] == i, "thread_total kernel needs one row per BMT (fixed_row_block_size 1)");
+            bool aligned = true;
+            for (uint64_t x : fn) aligned &= (x % 4 == 0);
+            d.scf = aligned ? 4 : 1;
+            a.a0 = dev_copy(d, to_u32(fn, "first_nz_indices"));
+            std::vector<uint64_t> order;
+            if (m.is_exist(GLOBAL_META, "original_nz_row_indices", 0)) {
+                order = m.u(GLOBAL_META, "original_nz_row_indices", 0);
+            } else {
+                order.resize(row_num);
+                for (uint64_t i = 0; i < row_num; i++) order[i] = i;
+            }
+            a.a1 = dev_copy(d, to_u32(order, "original_nz_row_indices"));
+            d.n_units = fn.size() - 1;
+            d.n_rows_aux = order.size();
+            break;
+        }
+        case KF_WARP_TOTAL: {
+            a.a0 = dev_copy(d, to_u32(m.u(WARP_META, "first_row_indices", 0), "BMW first_row_indices"));
+            if (sp.tblock_parent) {
+                a.a1 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_BMW_indices", 0), "first_BMW_indices"));
+                d.n_rows_aux = m.u(TBLOCK_META, "first_BMW_indices", 0).size() - 1;  // BMTB count
+            }
+            a.a2 = dev_copy(d, csr_row_ptr(rows, row_num));
+            d.n_units = m.u(WARP_META, "first_row_indices", 0).size() - 1;
+            d.scf = 4;
+            break;
+        }
+        case KF_BLOCK_TOTAL: {
+            a.a0 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_row_indices", 0), "BMTB first_row_indices"));
+            a.a2 = dev_copy(d, csr_row_ptr(rows, row_num));
+            d.n_units = m.u(TBLOCK_META, "first_row_indices", 0).size() - 1;
+            d.scf = 4;
+            break;
+        }
+        case KF_BITMAP_SEGMENT: {
+            const auto &fn = m.u(THREAD_META, "first_nz_indices", 0);
+            uint64_t nb = fn.size() - 1;
+            for (uint64_t i = 0; i < nb; i++) {
+                GS_CHECK(fn[i + 1] - fn[i] <= 64, "bitmap kernel needs BMTs of at most 64 nnz");
+                GS_CHECK(fn[i] % 4 == 0, "bitmap kernel needs 4-aligned BMTs");
+            }
+            // real row starts (the plan's thread_bit_map also carries the forced BMW heads)
+            std::vector<uint64_t> mask(nb, 0);
+            for (uint64_t i = 0; i < nb; i++) {
+                uint64_t mm = 0;
+                for (uint64_t j = fn[i]; j < fn[i + 1]; j++)
+                    if (j == 0 || rows[j] != rows[j - 1]) mm |= 1ull << (j - fn[i]);
+                mask[i] = mm;
+            }
+            a.a0 = dev_copy(d, to_u32(fn, "first_nz_indices"));
+            a.a1 = dev_copy(d, to_u32(m.u(THREAD_META, "first_row_indices", 0), "first_row_indices"));
+            a.m0 = dev_copy(d, mask);
+            a.a2 = dev_copy(d, to_u32(m.u(THREAD_META, "segment_ptr", 0), "segment_ptr"));
+            a.a3 = dev_copy(d, to_u32(m.u(THREAD_META, "segment_empty_row_indices", 0), "segment_empty_row_indices"));
+            d.n_units = nb;
+            d.scf = 4;
+            d.needs_memset = true;
+            break;
+        }
+        default:
+            throw gs_error("no gfx950 kernel family for this plan");
+    }
+    d.replicas.push_back(a);
+    p.uploaded = true;
+}
+
+void add_replica(plan_state &p) {
+    GS_CHECK(p.uploaded, "upload the plan before adding replicas");
+    HIP_OK(hipSetDevice(p.dev.device));
+    const device_arrays &s = p.dev.replicas[0];
+    device_arrays r = s;
+    // every allocation of replica 0 is duplicated (same sizes)
+    size_t n0 = p.dev.allocations.size();
+    std::vector<void *> base(p.dev.allocations.begin(), p.dev.allocations.begin() + n0);
+    auto dup = [&](void *src) -> void * {
+        if (!src) return nullptr;
+        size_t bytes = 0;
+        HIP_OK(hipMemPtrGetInfo(src, &bytes));
+        void *dst = nullptr;
+        HIP_OK(hipMalloc(&dst, bytes));
+        HIP_OK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice));
+        p.dev.allocations.push_back(dst);
+        return dst;
+    };
+    r.col = dup(s.col);
+    r.val = dup(s.val);
+    r.a0 = (uint32_t *)dup(s.a0);
+    r.a1 = (uint32_t *)dup(s.a1);
+    r.a2 = (uint32_t *)dup(s.a2);
+    r.a3 = (uint32_t *)dup(s.a3);
+    r.a4 = (uint32_t *)dup(s.a4);
+    r.m0 = (uint64_t *)dup(s.m0);
+    p.dev.replicas.push_back(r);
+}
+
+void free_device(plan_state &p) {
+    if (!p.dev.allocations.empty()) (void)hipSetDevice(p.dev.device);
+    for (void *x : p.dev.allocations) (void)hipFree(x);
+    p.dev.allocations.clear();
+    p.dev.replicas.clear();
+    p.uploaded = false;
+}
+
+// ------------------------------------------------------------------ launch
+namespace {
+
+uint32_t pow2ceil(uint32_t x) {
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+template <class VT, class CT, int CF, int SCF>
+void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT *C, uint32_t N, hipStream_t s) {
+    const device_plan &d = p.dev;
+    const kernel_spec &sp = p.cg->get_kernel_spec();
+    const uint32_t X = std::min<uint32_t>(64u, pow2ceil((N + CF - 1) / CF));
+    const uint32_t tiles = (N + X * CF - 1) / (X * CF);
+    const uint32_t row_base = (uint32_t)d.row_base;
+    const CT *col = (const CT *)a.col;
+    const VT *val = (const VT *)a.val;
+    switch (sp.family) {
+        case KF_THREAD_TOTAL: {
+            uint32_t groups = 256 / X;
+            uint32_t gx = (uint32_t)std::min<uint64_t>((d.n_rows_aux + groups - 1) / groups, 1u << 16);
+            hipLaunchKernelGGL((gsk::k_thread_total<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0,
+                               s, a.a0, a.a1, col, val, B, C, (uint32_t)d.n_units, (uint32_t)d.n_rows_aux, N, X,
+                               row_base);
+            break;
+        }
+        case KF_WARP_TOTAL: {
+            uint32_t gx;
+            if (sp.tblock_parent) gx = (uint32_t)d.n_rows_aux;
+            else gx = (uint32_t)std::min<uint64_t>((d.n_units + 3) / 4, 1u << 16);
+            hipLaunchKernelGGL((gsk::k_warp_rows<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
+                               a.a0, sp.tblock_parent ? a.a1 : nullptr, a.a2, col, val, B, C, (uint32_t)d.n_units, N,
+                               X, row_base);
+            break;
+        }
+        case KF_BLOCK_TOTAL: {
+            uint32_t gx = (uint32_t)std::min<uint64_t>(d.n_units, 1u << 16);
+            hipLaunchKernelGGL((gsk::k_block_rows<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
+                               a.a0, a.a2, col, val, B, C, (uint32_t)d.n_units, N, X, row_base);
+            break;
+        }
+        case KF_BITMAP_SEGMENT: {
+            const uint32_t S = 64 / X;
+            uint32_t gx = (uint32_t)std::min<uint64_t>((d.n_units + 4 * S - 1) / (4 * S), 1u << 16);
+            size_t lds = (size_t)4 * S * 2 * X * CF * sizeof(float);
+            HIP_OK(hipMemsetAsync(C, 0, (size_t)d.n_out_rows * N * sizeof(VT), s));
+            hipLaunchKernelGGL((gsk::k_bitmap_segment<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256),
+                               lds, s, a.a0, a.a1, a.m0, a.a2, a.a3, col, val, B, C, (uint32_t)d.n_units, N, X,
+                               row_base);
+            break;
+        }
+        default:
+            throw gs_error("no kernel family");
+    }
+    HIP_OK(hipGetLastError());
+}
+
+template <class VT, int CFV>
+void dispatch_vt(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
+    const bool vec = (N % CFV) == 0;
+    const bool u16 = p.dev.col_bytes == 2;
+    const bool s4 = p.dev.scf == 4;
+    const VT *b = (const VT *)B;
+    VT *c = (VT *)C;
+#define GS_L(CT, CF, SCF) launch_family<VT, CT, CF, SCF>(p, a, b, c, N, s)
+    if (vec) {
+        if (u16) { if (s4) GS_L(uint16_t, CFV, 4); else GS_L(uint16_t, CFV, 1); }
+        else { if (s4) GS_L(uint32_t, CFV, 4); else GS_L(uint32_t, CFV, 1); }
+    } else {
+        if (u16) { if (s4) GS_L(uint16_t, 1, 4); else GS_L(uint16_t, 1, 1); }
+        else { if (s4) GS_L(uint32_t, 1, 4); else GS_L(uint32_t, 1, 1); }
+    }
+#undef GS_L
+}
+
+}  // namespace
+
+void launch_spmm(const plan_state &p, int replica, const void *B, void *C, uint32_t N, hipStream_t stream) {
+    GS_CHECK(p.uploaded, "plan is not on the device");
+    GS_CHECK(replica >= 0 && (size_t)replica < p.dev.replicas.size(), "bad replica index");
+    GS_CHECK(N >= 1, "N >= 1");
+    const device_arrays &a = p.dev.replicas[replica];
+    if (p.dev.dtype == 0) dispatch_vt<float, 4>(p, a, B, C, N, stream);
+    else dispatch_vt<gsk::f16, 8>(p, a, B, C, N, stream);
+}
+
+}  // namespace gs

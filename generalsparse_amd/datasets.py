@@ -1,0 +1,89 @@
+"""Synthetic, seeded stand-ins for the BASELINE.json configs.
+
+The pruned OPT weights (Flash-LLM tooling) and SuiteSparse files are not
+available offline; these generators reproduce the shapes, nnz and sparsity
+structure with fixed seeds."""
+import numpy as np
+
+
+def pruned_weight(M, K, sparsity, seed):
+    """Dense Gaussian M x K pruned to exactly round(sparsity*M*K) zeros by a
+    global magnitude threshold (C2: 5120 x 5120, 70%, seed 13)."""
+    rng = np.random.default_rng(seed)
+    W = rng.standard_normal((M, K), dtype=np.float32)
+    keep = int(round((1.0 - sparsity) * M * K))
+    flat = np.abs(W).ravel()
+    idx = np.argpartition(flat, flat.size - keep)[flat.size - keep:]
+    idx.sort()
+    row = (idx // K).astype(np.uint64)
+    col = (idx % K).astype(np.uint64)
+    val = W.ravel()[idx].astype(np.float32)
+    return row, col, val
+
+
+def two_four(M, K, seed):
+    """2:4 structured by magnitude in each group of 4 along K (C3)."""
+    rng = np.random.default_rng(seed)
+    W = rng.standard_normal((M, K // 4, 4), dtype=np.float32)
+    order = np.argsort(-np.abs(W), axis=2)[:, :, :2]
+    order.sort(axis=2)
+    g = np.arange(K // 4, dtype=np.int64)[None, :, None] * 4
+    cols = (g + order).reshape(M, -1)
+    vals = np.take_along_axis(W, order, axis=2).reshape(M, -1)
+    row = np.repeat(np.arange(M, dtype=np.uint64), cols.shape[1])
+    return row, cols.ravel().astype(np.uint64), vals.ravel().astype(np.float32)
+
+
+def random_rows(M, K, mean_nnz_per_row, seed, empty_frac=0.0):
+    """Uniform columns, Poisson row lengths (IG5-18 stand-in, C1)."""
+    rng = np.random.default_rng(seed)
+    lens = rng.poisson(mean_nnz_per_row, size=M)
+    lens = np.minimum(lens, K)
+    if empty_frac > 0:
+        lens[rng.random(M) < empty_frac] = 0
+    rows, cols = [], []
+    for r in range(M):
+        if lens[r]:
+            c = np.sort(rng.choice(K, size=lens[r], replace=False))
+            rows.append(np.full(lens[r], r, np.uint64))
+            cols.append(c.astype(np.uint64))
+    row = np.concatenate(rows) if rows else np.zeros(0, np.uint64)
+    col = np.concatenate(cols) if cols else np.zeros(0, np.uint64)
+    val = rng.uniform(-1, 1, size=len(row)).astype(np.float32)
+    return row, col, val
+
+
+def rmat(scale_n, nnz, seed, a=0.57, b=0.19, c=0.19, symmetric=False):
+    """R-MAT power-law graph (C4 stand-ins), deduplicated, row-sorted."""
+    rng = np.random.default_rng(seed)
+    levels = int(np.ceil(np.log2(scale_n)))
+    n = int(nnz * 1.3) + 1024
+    r = np.zeros(n, np.int64)
+    cc = np.zeros(n, np.int64)
+    for _ in range(levels):
+        u = rng.random(n)
+        down = u >= a + b
+        right = ((u >= a) & (u < a + b)) | (u >= a + b + c)
+        r = (r << 1) | down
+        cc = (cc << 1) | right
+    keep = (r < scale_n) & (cc < scale_n)
+    r, cc = r[keep], cc[keep]
+    if symmetric:
+        r, cc = np.concatenate([r, cc]), np.concatenate([cc, r])
+    key = np.unique(r * scale_n + cc)[: nnz]
+    row = (key // scale_n).astype(np.uint64)
+    col = (key % scale_n).astype(np.uint64)
+    val = rng.uniform(-1, 1, size=len(row)).astype(np.float32)
+    return row, col, val
+
+
+def write_mtx(path, M, K, row, col, val=None):
+    """Matrix Market coordinate file, 1-based, row-sorted, single spaces
+    (what get_matrix_index_and_val_from_file parses, struct.cc:49-261)."""
+    with open(path, "w") as f:
+        f.write("%%MatrixMarket matrix coordinate real general\n")
+        f.write(f"{M} {K} {len(row)}\n")
+        if val is None:
+            val = np.ones(len(row), np.float32)
+        lines = [f"{int(r) + 1} {int(c) + 1} {float(v):.6g}\n" for r, c, v in zip(row, col, val)]
+        f.writelines(lines)

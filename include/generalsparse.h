@@ -1,0 +1,107 @@
+/*
+ * generalsparse.h -- C ABI of the MI355X-native GeneralSparse SpMM engine.
+ *
+ * This is the drop-in boundary for the reference's SpMM path.
+ * Plain pointers and sizes only; every call returns 0 or a negative error
+ * code (gs_last_error() has the message); nothing aborts across the ABI
+ * (the reference asserts everywhere).  Reentrant per plan, one HIP stream per
+ * call, no internal host threads.
+ *
+ * Reference interfaces each entry point replaces:
+ *   gs_plan_create_from_mtx   create_init_metadata_set_from_file   metadata_set.cc:612-707
+ *                             (+ get_matrix_index_and_val_from_file  struct.cc:49-261)
+ *   gs_plan_create_from_coo   same, from in-memory COO (no text round trip)
+ *   gs_plan_add_operator      operator_executer::add_and_run        operator_executer.cc:19-26
+ *                             with the operator classes of           operator.hpp:64-1324
+ *   gs_plan_run_pipeline      token_test.cc test_spmm_* functions    token_test.cc:1003-1582
+ *   gs_set_config_int         set_config                              config.cc:17-40
+ *   gs_plan_compile           code_generator::compile                code_generator.hpp:265-269
+ *   gs_plan_generate_program  code_generator::generate_final_program code_generator.hpp:271-280
+ *   gs_plan_upload / gs_spmm  the generated program's device copies + kernel launch
+ *                             (code_generator.cc:285-600, executor.cc:6-104)
+ *   gs_plan_array_*           meta_data_set::get_element / output_format_to_dir (plan arrays by key)
+ *   gs_plan_from_mtx          the one-call form proposed in SURVEY.md §8b
+ */
+#ifndef GENERALSPARSE_H
+#define GENERALSPARSE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gs_plan gs_plan_t;
+typedef void *gs_stream_t; /* hipStream_t; NULL = default stream */
+
+enum { GS_OK = 0, GS_ERR = -1, GS_ERR_ARG = -2, GS_ERR_HIP = -3 };
+enum { GS_F32 = 0, GS_F16 = 1 };
+
+typedef struct {
+    const char *pipeline;   /* token_test pipeline name, see gs_plan_run_pipeline */
+    int dtype;              /* GS_F32 / GS_F16 (A values, B and C) */
+    int dense_n;            /* DENSE_MATRIX_SIZE used to size the plan (token_test argv[2]) */
+    int p0, p1;             /* pipeline parameters (sparse_coarsen_factor / rows per BMTB / ...) */
+    int ones_values;        /* 1: reference reader semantics, every value := 1 (struct.cc:186-200) */
+    int device;             /* HIP device ordinal */
+} gs_opts;
+
+typedef struct {
+    uint64_t rows, cols, nnz;     /* original matrix */
+    uint64_t nnz_stored;          /* after padding */
+    uint64_t n_units;             /* BMTs / BMWs / BMTBs the kernel walks */
+    uint64_t device_bytes_A;      /* HBM bytes of A (metadata + cols + vals) per replica */
+    int family;                   /* 1 thread_total, 2 warp_rows, 3 block_rows, 4 bitmap_segment */
+    int col_bytes, dtype, replicas, needs_memset;
+    char kernel_name[64];
+} gs_plan_info;
+
+const char *gs_last_error(void);
+const char *gs_version(void);
+
+void gs_opts_default(gs_opts *o);
+
+int gs_plan_create_from_mtx(const char *path, int ones_values, gs_plan_t **out);
+int gs_plan_create_from_coo(uint64_t n_rows, uint64_t n_cols, uint64_t nnz, const uint64_t *row,
+                            const uint64_t *col, const float *val, gs_plan_t **out);
+int gs_set_config_int(const char *key, long long value);
+
+/* operator surface: name = reference class name; args in constructor order
+ * without the code_generator / operator_context arguments */
+int gs_plan_add_operator(gs_plan_t *p, const char *op_name, const long long *args, int nargs);
+/* canned pipelines: thread_total(p0=sparse_cf,p1=cf), warp_total(cf=p1), block_total(cf=p1),
+ * thread_bit_map(p0=sparse_cf,p1=cf), warp_segment(p0=sparse_cf,p1=cf),
+ * tblock_warp_total(p0=rows per BMTB), balanced_warp_total(p0=nnz per BMW) */
+int gs_plan_run_pipeline(gs_plan_t *p, const char *name, int dense_n, int p0, int p1);
+int gs_plan_compile(gs_plan_t *p);
+int gs_plan_generate_program(gs_plan_t *p, const char *root_dir, int repeat, char *dir_out, int dir_out_len);
+
+int gs_plan_upload(gs_plan_t *p, int dtype, int device);
+int gs_plan_add_replica(gs_plan_t *p);
+/* C = A * B.  B: K x N row-major, C: M x N row-major, device pointers of the
+ * plan's dtype.  Enqueued on `stream`; returns without synchronising. */
+int gs_spmm(gs_plan_t *p, const void *B, void *C, int N, gs_stream_t stream);
+int gs_spmm_replica(gs_plan_t *p, int replica, const void *B, void *C, int N, gs_stream_t stream);
+/* `count` SpMMs enqueued back to back from native code, call i using replica
+ * (first + i) % replicas with B_ptrs / C_ptrs entry (first + i) % n_ptrs
+ * (bench rotation without a host round trip per launch) */
+int gs_spmm_rotate(gs_plan_t *p, int count, int first, const void *const *B_ptrs, void *const *C_ptrs, int n_ptrs,
+                   int N, gs_stream_t stream);
+
+int gs_plan_info_get(gs_plan_t *p, gs_plan_info *info);
+int gs_plan_array_count(gs_plan_t *p);
+int gs_plan_array_key(gs_plan_t *p, int i, char *buf, int buf_len);
+long long gs_plan_array_len(gs_plan_t *p, const char *key);      /* -1 if absent */
+int gs_plan_array_is_float(gs_plan_t *p, const char *key);
+int gs_plan_array_read_u64(gs_plan_t *p, const char *key, uint64_t *out, uint64_t n);
+int gs_plan_array_read_f64(gs_plan_t *p, const char *key, double *out, uint64_t n);
+int gs_plan_log(gs_plan_t *p, char *buf, int buf_len); /* operator / transform history */
+
+/* one call: read + pipeline + compile + upload */
+int gs_plan_from_mtx(const char *path, const gs_opts *opts, gs_plan_t **out);
+void gs_plan_free(gs_plan_t *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

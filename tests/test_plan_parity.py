@@ -1,0 +1,218 @@
+"""Plan parity (CPU): the C++ plan builder in libgeneralsparse.so must produce
+bit-identical plan arrays to the oracle for every canned pipeline
+(token_test.cc test_spmm_*), and the C ABI must export what
+include/generalsparse.h declares.  No GPU needed."""
+import ctypes
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle_ffi as ofi
+
+import generalsparse_amd as gsa
+from generalsparse_amd import _lib
+from generalsparse_amd import datasets as ds
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden", "hand_plans.json")
+
+
+def oracle_params(name, N, p0, p1):
+    """maps a product pipeline call to the oracle's parameters"""
+    cf = p1 if p1 > 0 else 1
+    if name == "thread_total":
+        return p0 if p0 > 0 else 4
+    if name == "warp_segment":
+        return min(N, 32)
+    if name == "thread_bit_map":
+        return N // cf if N // cf < 32 else 32
+    return p0
+
+
+def product_plan(M, K, row, col, val, name, N, p0=0, p1=0):
+    p = gsa.Plan.from_coo(M, K, row, col, val)
+    p.run_pipeline(name, N, p0, p1)
+    return p
+
+
+def compare(M, K, row, col, val, name, N, p0=0, p1=0):
+    exp, err = ofi.run_pipeline(M, K, row, col, val, name, oracle_params(name, N, p0, p1))
+    if err is not None:
+        with pytest.raises(gsa.GsError):
+            product_plan(M, K, row, col, val, name, N, p0, p1)
+        return None
+    p = product_plan(M, K, row, col, val, name, N, p0, p1)
+    got = p.arrays()
+    for key, arr in exp.items():
+        assert key in got, f"{name}: product lacks {key}"
+        np.testing.assert_array_equal(got[key].astype(np.float64) if arr.dtype == np.float64 else got[key],
+                                      arr, err_msg=f"{name}: {key}")
+    return p
+
+
+def random_coo(M, K, density, seed, empty=0.2, trailing_empty=False):
+    rng = np.random.default_rng(seed)
+    mask = rng.random((M, K)) < density
+    mask[rng.random(M) < empty] = False
+    if trailing_empty:
+        mask[-3:] = False
+    r, c = np.nonzero(mask)
+    v = rng.uniform(-1, 1, size=len(r)).astype(np.float32)
+    return r.astype(np.uint64), c.astype(np.uint64), v
+
+
+PIPES = [("thread_total", 32, 4, 1), ("thread_total", 8, 8, 1), ("warp_total", 32, 0, 1),
+         ("block_total", 8, 0, 1), ("thread_bit_map", 32, 4, 1), ("thread_bit_map", 8, 4, 2),
+         ("warp_segment", 32, 4, 1), ("warp_segment", 8, 4, 1), ("tblock_warp_total", 32, 4, 1),
+         ("tblock_warp_total", 32, 7, 1), ("balanced_warp_total", 32, 64, 1)]
+
+
+@pytest.mark.parametrize("pipe", PIPES, ids=lambda p: f"{p[0]}-N{p[1]}-{p[2]}-{p[3]}")
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_plan_arrays_bit_exact(pipe, seed):
+    name, N, p0, p1 = pipe
+    M, K = 120 + 17 * seed, 90
+    r, c, v = random_coo(M, K, 0.08, seed, trailing_empty=(seed == 1))
+    compare(M, K, r, c, v, name, N, p0, p1)
+
+
+@pytest.mark.parametrize("pipe", PIPES, ids=lambda p: f"{p[0]}-N{p[1]}")
+def test_plan_edge_shapes(pipe):
+    name, N, p0, p1 = pipe
+    cases = [
+        (1, 1, np.array([0], np.uint64), np.array([0], np.uint64)),            # single nnz
+        (1, 70, np.zeros(70, np.uint64), np.arange(70, dtype=np.uint64)),     # one long row
+        (70, 1, np.arange(70, dtype=np.uint64), np.zeros(70, np.uint64)),     # one column
+        (5, 5, np.array([4], np.uint64), np.array([2], np.uint64)),            # leading empty rows
+    ]
+    for M, K, r, c in cases:
+        v = np.linspace(-1, 1, len(r)).astype(np.float32)
+        compare(M, K, r, c, v, name, N, p0, p1)
+
+
+def test_hand_derived_fixtures_through_product():
+    g = json.load(open(GOLDEN))
+    back = {"thread_total": (32, 4, 1), "warp_total": (32, 0, 1), "block_total": (8, 0, 1),
+            "tblock_warp_total": (32, 4, 1), "balanced_warp_total": (32, 16, 1)}
+    for case in g["cases"]:
+        m = g["matrices"][case["matrix"]]
+        row = np.array([e[0] for e in m["entries"]], np.uint64)
+        col = np.array([e[1] for e in m["entries"]], np.uint64)
+        val = np.arange(1, len(row) + 1, dtype=np.float32)
+        name = case["pipeline"]
+        if name in ("warp_segment", "thread_bit_map"):
+            N, p0, p1 = case["p0"], 4, 1  # VW = min(N, 32) = fixture VW
+        else:
+            N, p0, p1 = back[name]
+            if name in ("tblock_warp_total", "balanced_warp_total"):
+                p0 = case["p0"]
+        if case.get("expect_error"):
+            with pytest.raises(gsa.GsError):
+                product_plan(m["M"], m["K"], row, col, val, name, N, p0, p1)
+            continue
+        got = product_plan(m["M"], m["K"], row, col, val, name, N, p0, p1).arrays()
+        for key, exp in case["expect"].items():
+            np.testing.assert_array_equal(got[key].astype(np.float64), np.asarray(exp, np.float64), err_msg=key)
+
+
+def test_operator_surface_matches_pipeline():
+    """The same plan through gs_plan_add_operator (reference class names and
+    constructor arguments) as through the canned pipeline."""
+    M, K = 60, 50
+    r, c, v = random_coo(M, K, 0.1, 5)
+    a = gsa.Plan.from_coo(M, K, r, c, v)
+    gsa.set_config("DENSE_MATRIX_SIZE", 32)
+    a.add_operator("sort_operator")
+    a.add_operator("fixed_interval_row_direction_thread_blocking_operator", 1, 0, 0, 0, 0, 1, 4)
+    a.add_operator("thread_total_reduce_operator", 0, 4, 1)
+    b = product_plan(M, K, r, c, v, "thread_total", 32, 4, 1)
+    ga, gb = a.arrays(), b.arrays()
+    assert set(ga) == set(gb)
+    for k in ga:
+        np.testing.assert_array_equal(ga[k], gb[k], err_msg=k)
+    assert "sort_operator" in a.log()
+
+
+def test_operator_validity_rules():
+    """name-substring validity (thread_total_reduce_operator.cc:14-40 etc.)"""
+    M, K = 30, 30
+    r, c, v = random_coo(M, K, 0.2, 9)
+    p = gsa.Plan.from_coo(M, K, r, c, v)
+    with pytest.raises(gsa.GsError):  # no thread-level distributing op yet
+        p.add_operator("thread_total_reduce_operator", 0, 4, 1)
+    p.add_operator("fixed_interval_nnz_direction_thread_blocking_operator", 32, 0, 0, 1)
+    with pytest.raises(gsa.GsError):  # "nnz" distributing op forbids thread_total
+        p.add_operator("thread_total_reduce_operator", 0, 4, 1)
+    with pytest.raises(gsa.GsError):  # sort after distributing is invalid (sort_operator.cc:20-45)
+        p.add_operator("sort_operator")
+    with pytest.raises(gsa.GsError):  # warp_segment needs thread_bit_map first
+        p.add_operator("warp_segment_reduce_operator", 1, 0, 0)
+    p.add_operator("thread_bit_map_operator", 1, 8, 4, 1)
+    p.add_operator("warp_segment_reduce_operator", 1, 0, 0)
+    p.compile()
+    assert p.info()["kernel_name"].startswith("k_bitmap_segment")
+
+
+def test_mtx_reader_parity(tmp_path):
+    M, K = 40, 33
+    r, c, v = random_coo(M, K, 0.15, 11, trailing_empty=True)
+    path = tmp_path / "m.mtx"
+    ds.write_mtx(path, M, K, r, c, v)
+    L = ofi.lib()
+
+    class Coo(ctypes.Structure):
+        _fields_ = [("nnz", ctypes.c_uint64), ("row", ctypes.POINTER(ctypes.c_uint64)),
+                    ("col", ctypes.POINTER(ctypes.c_uint64)), ("val", ctypes.POINTER(ctypes.c_float)),
+                    ("max_row_index", ctypes.c_uint64), ("max_col_index", ctypes.c_uint64)]
+    for ones in (1, 0):
+        co = Coo()
+        assert L.or_read_mtx(str(path).encode(), ones, ctypes.byref(co)) == 0
+        p = gsa.Plan.from_mtx(path, ones_values=bool(ones))
+        rows = np.ctypeslib.as_array(co.row, (co.nnz,)).copy()
+        vals = np.ctypeslib.as_array(co.val, (co.nnz,)).copy()
+        np.testing.assert_array_equal(p.array("GLOBAL_META_nz_row_indices_0"), rows)
+        np.testing.assert_array_equal(p.array("GLOBAL_META_nz_vals_0"), vals.astype(np.float64))
+        assert p.array("GLOBAL_META_origin_row_num_-1")[0] == M
+        L.or_coo_free(ctypes.byref(co))
+
+
+def test_unsorted_mtx_rejected(tmp_path):
+    path = tmp_path / "bad.mtx"
+    path.write_text("3 3 2\n2 1 1.0\n1 1 1.0\n")
+    with pytest.raises(gsa.GsError):
+        gsa.Plan.from_mtx(path)
+
+
+def test_c_abi_exports_every_declared_symbol():
+    hdr = open(os.path.join(ROOT, "include", "generalsparse.h")).read()
+    declared = set(re.findall(r"\b(gs_[a-z0-9_]+)\s*\(", hdr))
+    L = _lib.load()
+    for sym in sorted(declared):
+        assert hasattr(L, sym), sym
+    assert declared == set(_lib.SIGNATURES), declared ^ set(_lib.SIGNATURES)
+
+
+def test_generate_program(tmp_path):
+    M, K = 50, 40
+    r, c, v = random_coo(M, K, 0.1, 3)
+    p = product_plan(M, K, r, c, v, "thread_total", 32, 4, 1)
+    p.compile()
+    d = p.generate_program(tmp_path, repeat=10)
+    files = set(os.listdir(d))
+    assert {"kernel_file.hip", "make_kernel.sh", "kernel_lib.hpp", "THREAD_META_first_nz_indices_0",
+            "GLOBAL_META_original_nz_row_indices_0"} <= files
+    fn = np.loadtxt(os.path.join(d, "THREAD_META_first_nz_indices_0"), dtype=np.uint64)
+    np.testing.assert_array_equal(fn, p.array("THREAD_META_first_nz_indices_0"))
+
+
+def test_synthetic_generators_shapes():
+    r, c, v = ds.pruned_weight(64, 48, 0.7, 13)
+    assert len(r) == round(0.3 * 64 * 48) and np.all(np.diff(r.astype(np.int64)) >= 0)
+    r, c, v = ds.two_four(8, 16, 30)
+    assert len(r) == 8 * 8
+    assert np.all(np.bincount((c // 4 + 4 * r).astype(np.int64)) == 2)
+    r, c, v = ds.rmat(1024, 5000, 1)
+    assert len(r) <= 5000 and np.all(np.diff(r.astype(np.int64)) >= 0)
