@@ -25,6 +25,7 @@
 namespace gsk {
 
 typedef _Float16 f16;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 template <int BYTES> struct raw_vec;
 template <> struct raw_vec<2> { typedef uint16_t t; };
@@ -435,6 +436,204 @@ __global__ __launch_bounds__(256) void k_bitmap_segment(const uint32_t *__restri
                 if (run_row != 0xffffffffu) atomic_add_vals<VT, CF>(C + (size_t)(run_row + row_base) * N + c0, run);
             }
             __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// v_fma_mix_f32: fp32 += fp16 * fp16 with the conversions folded into the FMA
+// (no v_cvt_f32_f16).  VS/BS select the low (0) or high (1) half of the packed
+// operand.
+// ---------------------------------------------------------------------------
+template <int VS, int BS>
+__device__ __forceinline__ float fma_mix(uint32_t v_h2, uint32_t b_h2, float c) {
+    float d;
+    if constexpr (VS == 0 && BS == 0)
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[1,1,0]" : "=v"(d) : "v"(v_h2), "v"(b_h2), "v"(c));
+    else if constexpr (VS == 0 && BS == 1)
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,0]" : "=v"(d) : "v"(v_h2), "v"(b_h2), "v"(c));
+    else if constexpr (VS == 1 && BS == 0)
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,1,0]" : "=v"(d) : "v"(v_h2), "v"(b_h2), "v"(c));
+    else
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,1,0]" : "=v"(d) : "v"(v_h2), "v"(b_h2), "v"(c));
+    return d;
+}
+
+// acc[0..CF) += v * b (CF fp16 values packed in b_words), v = half VS of v_word
+template <int CF, int VS>
+__device__ __forceinline__ void fma_row_mix(float (&acc)[CF], uint32_t v_word, const uint32_t *b_words) {
+#pragma unroll
+    for (int m = 0; m < CF / 2; m++) {
+        acc[2 * m] = fma_mix<VS, 0>(v_word, b_words[m], acc[2 * m]);
+        acc[2 * m + 1] = fma_mix<VS, 1>(v_word, b_words[m], acc[2 * m + 1]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K4 on an LDS-stationary B (tblock_warp_total plan, MI355X layout):
+// workgroup g owns BMTB g (<= rpw_max rows); wave w owns BMW g.first_BMW + w
+// (<= MAXR rows).  K is cut into nc chunks of KC columns.  Per chunk the
+// workgroup stages
+//   * B[kc0 : kc0+KC, 0:N]   -> LDS, rows padded to RSB bytes (bank spread),
+//   * the BMTB's A entries whose columns fall in the chunk -> LDS, right after
+//     it: [cols u16 | vals].  They are stored chunk-major at upload (tile
+//     layout [BMTB][chunk][row][entries], 16-bit chunk-local columns, rows
+//     padded to 4 entries, segments to 8), so staging is one contiguous copy,
+// with the global loads of chunk j+1 issued into registers before computing
+// chunk j and written to LDS after the compute barrier.  Every B-row read of
+// the inner loop is then an LDS ds_read_b128 instead of an L1/L2 gather: B
+// crosses L2->CU once per workgroup instead of once per nonzero.  Accumulators
+// of the wave's rows stay in registers across all chunks.
+// ---------------------------------------------------------------------------
+// compile-time unrolled loop: the index is a constant in every body, so
+// register arrays indexed by it stay in VGPRs (no scratch)
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+template <class VT, int CF, int MAXR, int MAXU>
+__global__ __launch_bounds__(1024) void k_lds_rows(
+    const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
+    const uint32_t *__restrict__ bmw_of_bmtb,     // n_bmtb+1
+    const uint32_t *__restrict__ bmw_first_row,   // n_bmw+1
+    const uint32_t *__restrict__ seg_start,       // n_bmtb*nc+1: entry offset of (g, j)
+    const uint32_t *__restrict__ seg_row_off,     // n_bmtb*nc*(rpw_max+1): row starts inside (g, j)
+    const uint16_t *__restrict__ tcol, const VT *__restrict__ tval, const VT *__restrict__ B, VT *__restrict__ C,
+    uint32_t K, uint32_t N, uint32_t X, uint32_t KC, uint32_t nc, uint32_t RSB, uint32_t rpw_max, uint32_t seg_cap,
+    uint32_t row_base) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    typedef typename raw_vec<CF * sizeof(VT)>::t RB;
+    const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+    const uint32_t lane = tid & 63u, wib = tid >> 6;
+    const uint32_t xl = lane & (X - 1u), slot = lane / X, S = 64u / X;
+    const uint32_t g = blockIdx.x;
+    const uint32_t r_first = bmtb_first_row[g];
+    const uint32_t bmw = bmw_of_bmtb[g] + wib;
+    uint32_t t0 = 0, nt = 0;
+    if (bmw < bmw_of_bmtb[g + 1]) {
+        t0 = bmw_first_row[bmw] - r_first;
+        nt = bmw_first_row[bmw + 1] - bmw_first_row[bmw];
+    }
+    const uint32_t UB = X;  // 16-B units per B row (CF * sizeof(VT) == 16)
+    const uint32_t lgUB = __builtin_ctz(UB);
+    const uint32_t lA = KC * RSB;                        // LDS byte offset of the A segment
+    const uint32_t lR = lA + seg_cap * (2u + (uint32_t)sizeof(VT));  // row offsets
+    uint32_t *lRp = reinterpret_cast<uint32_t *>(lds + lR);
+    const uint32_t c0 = xl * CF;
+    const uint32_t cb = c0 * (uint32_t)sizeof(VT);
+    const uint32_t ridx = min(tid, rpw_max);
+
+    u32x4 stage[MAXU];  // native vectors (HIP's uint4 is a union struct that defeats SROA)
+    uint32_t stage_r;
+    uint32_t s_lo = seg_start[g * nc], s_hi = seg_start[g * nc + 1];
+
+    float acc[MAXR][CF];
+#pragma unroll
+    for (int t = 0; t < MAXR; t++)
+#pragma unroll
+        for (int k = 0; k < CF; k++) acc[t][k] = 0.f;
+
+    // issue the global loads of chunk j into registers.  Branch-free: the three
+    // source streams are one base per unit picked by a select (B rows, A cols,
+    // A vals); units past the end re-read B's first unit.
+#define GS_STAGE_LOAD(j, s0, s1)                                                                         \
+    {                                                                                                  \
+        const uint32_t kc0_ = (j) * KC;                                                                \
+        const uint32_t UBt_ = min(KC, K - kc0_) * UB;                                                  \
+        const uint32_t len_ = (s1) - (s0);                                                             \
+        const uint32_t UAc_ = UBt_ + len_ / 8u, UAe_ = UAc_ + len_ * (uint32_t)sizeof(VT) / 16u;       \
+        const unsigned char *pB_ = reinterpret_cast<const unsigned char *>(B + (size_t)kc0_ * N);      \
+        const unsigned char *pC_ = reinterpret_cast<const unsigned char *>(tcol + (s0));               \
+        const unsigned char *pV_ = reinterpret_cast<const unsigned char *>(tval + (s0));               \
+        _Pragma("unroll") for (int I = 0; I < MAXU; I++) {                                             \
+            const uint32_t u = tid + I * nthr;                                                         \
+            const bool inB = u < UBt_, inC = u < UAc_, live = u < UAe_;                                \
+            const unsigned char *base = inB ? static_cast<const unsigned char *>(pB_)                  \
+                                      : inC ? static_cast<const unsigned char *>(pC_)                  \
+                                      : live ? static_cast<const unsigned char *>(pV_)                 \
+                                             : static_cast<const unsigned char *>(pB_);                \
+            const uint32_t off = inB ? u : inC ? u - UBt_ : live ? u - UAc_ : 0u;                      \
+            stage[I] = *reinterpret_cast<const u32x4 *>(base + (size_t)off * 16u);                     \
+        }                                                                                              \
+        stage_r = seg_row_off[(size_t)(g * nc + (j)) * (rpw_max + 1) + ridx];                          \
+    }
+
+    GS_STAGE_LOAD(0u, s_lo, s_hi);
+    for (uint32_t j = 0; j < nc; j++) {
+        // registers -> LDS (B rows at RSB stride, A segment contiguous)
+        {
+            const uint32_t UBt = min(KC, K - j * KC) * UB;
+            const uint32_t UAe = UBt + (s_hi - s_lo) * (2u + (uint32_t)sizeof(VT)) / 16u;
+#pragma unroll
+            for (int I = 0; I < MAXU; I++) {
+                const uint32_t u = tid + I * nthr;
+                const uint32_t db = (u >> lgUB) * RSB + (u & (UB - 1u)) * 16u;
+                const uint32_t da = lA + (u - UBt) * 16u;
+                if (u < UAe) *reinterpret_cast<u32x4 *>(lds + (u < UBt ? db : da)) = stage[I];
+            }
+            if (tid <= rpw_max) lRp[tid] = stage_r;
+        }
+        __syncthreads();
+        const uint32_t len = s_hi - s_lo;
+        if (j + 1 < nc) {  // in flight during this chunk's compute
+            const uint32_t n_lo = s_hi, n_hi = seg_start[g * nc + j + 2];
+            GS_STAGE_LOAD(j + 1, n_lo, n_hi);
+            s_lo = n_lo;
+            s_hi = n_hi;
+        }
+        const unsigned char *lAc = lds + lA;
+        const unsigned char *lAv = lds + lA + len * 2u;
+#pragma unroll
+        for (int t = 0; t < MAXR; t++) {
+            if ((uint32_t)t < nt) {
+                const uint32_t e0 = lRp[t0 + t], e1 = lRp[t0 + t + 1];
+                for (uint32_t p0 = e0 + slot * 4u; p0 < e1; p0 += S * 4u) {
+                    const uint2 craw = *reinterpret_cast<const uint2 *>(lAc + p0 * 2u);
+                    const uint32_t cc[4] = {craw.x & 0xffffu, craw.x >> 16, craw.y & 0xffffu, craw.y >> 16};
+                    RB braw[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        // 24-bit LDS byte offsets (KC * RSB <= 160 KB): one v_mad_u32_u24
+                        const uint32_t ob = __umul24(cc[q], RSB) + cb;
+                        braw[q] = *reinterpret_cast<const RB *>(lds + ob);
+                    }
+                    if constexpr (sizeof(VT) == 2) {
+                        const uint2 vraw = *reinterpret_cast<const uint2 *>(lAv + p0 * 2u);
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            uint32_t bw[CF / 2];
+                            __builtin_memcpy(bw, &braw[q], sizeof(RB));
+                            const uint32_t vw = (q < 2) ? vraw.x : vraw.y;
+                            if (q & 1) fma_row_mix<CF, 1>(acc[t], vw, bw);
+                            else fma_row_mix<CF, 0>(acc[t], vw, bw);
+                        }
+                    } else {
+                        const float4 vv = *reinterpret_cast<const float4 *>(lAv + p0 * 4u);
+                        const float vq[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            float bt[CF];
+                            __builtin_memcpy(bt, &braw[q], sizeof(RB));
+#pragma unroll
+                            for (int k = 0; k < CF; k++) acc[t][k] = __builtin_fmaf(vq[q], bt[k], acc[t][k]);
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+#undef GS_STAGE_LOAD
+#pragma unroll
+    for (int t = 0; t < MAXR; t++) {
+        if ((uint32_t)t < nt) {
+            wave_reduce_slots<CF>(acc[t], (int)X);
+            if (slot == 0) store_f32<VT, CF>(C + (size_t)(r_first + t0 + t + row_base) * N + c0, acc[t]);
         }
     }
 }

@@ -96,11 +96,11 @@ void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1)
         ex.add_and_run(std::make_shared<tblock_total_reduce_operator>(cg, cf, ctx));
         ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)rows, std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
     } else if (name == "tblock_warp_total") {
-        // headline plan (BASELINE.json configs[1]): row-direction BMTB blocking,
-        // one BMW per row inside each BMTB, wave-level reduction
-        int rb = p0 > 0 ? p0 : 4, cf = p1 > 0 ? p1 : 1;
+        // headline plan (BASELINE.json configs[1]): row-direction BMTB blocking of
+        // p0 rows, BMWs of p1 rows inside each BMTB, wave-level reduction
+        int rb = p0 > 0 ? p0 : 4, wb = p1 > 0 ? p1 : 1, cf = 1;
         ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, rb, false, ctx));
-        ex.add_and_run(std::make_shared<fixed_interval_row_direction_warp_blocking_operator>(cg, 1, false, false, false, ctx));
+        ex.add_and_run(std::make_shared<fixed_interval_row_direction_warp_blocking_operator>(cg, wb, false, false, false, ctx));
         ex.add_and_run(std::make_shared<warp_total_reduce_operator>(cg, cf, ctx));
         ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)((rows + rb - 1) / rb),
                                                              std::vector<unsigned>{64u, 4u}, cf, ctx));
@@ -260,6 +260,13 @@ int gs_plan_info_get(gs_plan_t *p, gs_plan_info *info) {
             info->dtype = s.dev.dtype;
             info->replicas = (int)s.dev.replicas.size();
             info->needs_memset = s.dev.needs_memset ? 1 : 0;
+            info->lds_stage = s.dev.lds ? 1 : 0;
+            info->lds_n = s.dev.lds_N;
+            info->lds_kc = s.dev.KC;
+            info->lds_chunks = s.dev.nc;
+            info->lds_waves = s.dev.waves;
+            info->lds_bytes = s.dev.lds_bytes;
+            info->tile_bytes = s.dev.bytes_tile;
         }
     });
 }

@@ -98,6 +98,7 @@ void apply_kv(config_t &c, const std::string &k, const std::string &v) {
     else if (k == "PERFORMANCE_FLAG") c.PERFORMANCE_FLAG = v;
     else if (k == "Graph_Algorithm") c.Graph_Algorithm = v;
     else if (k == "MODEL_DRIVEN_COMPRESS") c.MODEL_DRIVEN_COMPRESS = b();
+    else if (k == "LDS_STAGE_B") c.LDS_STAGE_B = b();
     // unknown keys are ignored, as the reference ignores 17 of its 36 keys
 }
 

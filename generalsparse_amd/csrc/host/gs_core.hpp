@@ -74,6 +74,8 @@ struct config_t {
     std::string PERFORMANCE_FLAG = "throughput";
     std::string Graph_Algorithm = "";
     bool MODEL_DRIVEN_COMPRESS = false;  // absent in the .bak -> false
+    // MI355X engine switches (not in the reference)
+    bool LDS_STAGE_B = true;  // warp_total inside BMTBs: stage B chunks in LDS (k_lds_rows)
 };
 // Process-wide config: loaded once from $GS_CONFIG or ./global_config.json if
 // present (flat JSON object of scalars), defaults otherwise.

@@ -13,6 +13,8 @@ namespace gs {
 // (bench.py rotates replicas past the 256 MB Infinity Cache).
 struct device_arrays {
     void *col = nullptr, *val = nullptr;
+    void *tcol = nullptr, *tval = nullptr;  // LDS tile layout (k_lds_rows)
+    uint32_t *t0 = nullptr, *t1 = nullptr, *t2 = nullptr, *t3 = nullptr, *t4 = nullptr;
     uint32_t *a0 = nullptr, *a1 = nullptr, *a2 = nullptr, *a3 = nullptr, *a4 = nullptr;
     uint64_t *m0 = nullptr;
 };
@@ -29,6 +31,10 @@ struct device_plan {
     uint64_t row_base = 0;
     uint64_t nnz_stored = 0;  // padded nnz on device
     size_t bytes_A = 0;       // device bytes of A per replica (metadata + cols + vals)
+    // LDS-stationary B (k_lds_rows): chunk geometry fixed for dense width lds_N
+    bool lds = false;
+    uint32_t lds_N = 0, KC = 0, nc = 0, RSB = 0, rpw_max = 0, seg_cap = 0, waves = 0, maxr = 0;
+    size_t lds_bytes = 0, bytes_tile = 0;
     std::vector<device_arrays> replicas;
     std::vector<void *> allocations;  // everything to hipFree
 };

@@ -57,6 +57,120 @@ uint16_t f32_to_f16_bits(float f) {
     return b;
 }
 
+
+// ------------------------------------------------------------------ LDS tiles
+// Chunk-major A layout for k_lds_rows (kernel_lib.hpp): for BMTB g and column
+// chunk j = [j*KC, (j+1)*KC), the entries of g's rows whose columns fall in the
+// chunk, row after row, each row padded to 4 entries (column 0, value 0) and
+// the segment padded to 8 entries so it stages as whole 16-B units.
+struct lds_tiles {
+    uint32_t KC = 0, nc = 0, RSB = 0, rpw_max = 0, seg_cap = 0, waves = 0, maxr = 0;
+    size_t lds_bytes = 0;
+    std::vector<uint32_t> seg_start, seg_row_off;
+    std::vector<uint16_t> tcol;
+    std::vector<uint32_t> src;  // source entry per tile entry (~0u: padding)
+};
+
+constexpr int kLdsMaxU = 12;  // 16-B staging registers per thread (k_lds_rows MAXU)
+
+// returns false (and the reason) when the plan/shape does not fit the kernel
+bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint64_t> &tb_bmw,
+                     const std::vector<uint64_t> &bmw_rows, const std::vector<uint32_t> &row_ptr,
+                     const std::vector<uint64_t> &col, uint64_t K, uint32_t N, uint32_t vbytes, size_t lds_budget,
+                     lds_tiles &t, std::string &why) {
+    const uint64_t nb = tb_rows.size() - 1;
+    if (nb == 0 || K == 0) { why = "empty plan"; return false; }
+    if ((N * vbytes) % 16 != 0) { why = "B rows are not whole 16-B units"; return false; }
+    const uint32_t UB = N * vbytes / 16;
+    if (UB > 64 || (UB & (UB - 1))) { why = "16-B units per B row must be a power of two <= 64"; return false; }
+    uint32_t waves = 0, maxr = 0, rpw = 0;
+    for (uint64_t g = 0; g < nb; g++) {
+        const uint64_t w0 = tb_bmw[g], w1 = tb_bmw[g + 1];
+        if (w1 <= w0 || bmw_rows[w0] != tb_rows[g] || bmw_rows[w1] != tb_rows[g + 1]) {
+            why = "BMWs do not tile their BMTB";
+            return false;
+        }
+        waves = std::max<uint32_t>(waves, (uint32_t)(w1 - w0));
+        rpw = std::max<uint32_t>(rpw, (uint32_t)(tb_rows[g + 1] - tb_rows[g]));
+        for (uint64_t w = w0; w < w1; w++) maxr = std::max<uint32_t>(maxr, (uint32_t)(bmw_rows[w + 1] - bmw_rows[w]));
+    }
+    if (waves > 16) { why = "more than 16 BMWs per BMTB"; return false; }
+    if (maxr > 4) { why = "more than 4 rows per BMW"; return false; }
+    maxr = maxr <= 1 ? 1 : (maxr <= 2 ? 2 : 4);
+    const uint32_t RSB = N * vbytes + (UB % 2 == 0 ? 16u : 0u);  // odd count of 16-B units
+    const uint32_t ebytes = 2 + vbytes;
+    const uint64_t nthr = 64ull * waves;
+    const uint64_t max_kc = std::min<uint64_t>(K, 65536);
+    // smallest chunk count whose largest segment still fits LDS and the staging registers
+    uint64_t nc = std::max<uint64_t>(1, (K * RSB + lds_budget / 2) / (lds_budget * 3 / 4));
+    std::vector<uint32_t> cap_of(0);
+    for (;; nc++) {
+        uint64_t KC = (K + nc - 1) / nc;
+        KC = (KC + 7) / 8 * 8;
+        if (KC > max_kc) continue;
+        if (KC < 64 && nc > 1) { why = "column chunks would be under 64 rows of B"; return false; }
+        const uint64_t ncc = (K + KC - 1) / KC;
+        uint64_t cap = 0;
+        std::vector<uint64_t> segl(ncc);
+        for (uint64_t g = 0; g < nb; g++) {
+            std::fill(segl.begin(), segl.end(), 0);
+            for (uint64_t r = tb_rows[g]; r < tb_rows[g + 1]; r++) {
+                uint64_t e = row_ptr[r];
+                while (e < row_ptr[r + 1]) {
+                    const uint64_t j = col[e] / KC;
+                    uint64_t e1 = e;
+                    while (e1 < row_ptr[r + 1] && col[e1] / KC == j) e1++;
+                    segl[j] += (e1 - e + 3) / 4 * 4;
+                    e = e1;
+                }
+            }
+            for (uint64_t j = 0; j < ncc; j++) cap = std::max(cap, (segl[j] + 7) / 8 * 8);
+        }
+        const uint64_t lds = KC * RSB + cap * ebytes + (rpw + 1) * 4;
+        const uint64_t units = KC * UB + cap * ebytes / 16;
+        if (lds <= lds_budget && units <= (uint64_t)kLdsMaxU * nthr) {
+            t.KC = (uint32_t)KC;
+            t.nc = (uint32_t)ncc;
+            t.seg_cap = (uint32_t)std::max<uint64_t>(cap, 8);
+            t.lds_bytes = (size_t)(KC * RSB + (uint64_t)t.seg_cap * ebytes + (rpw + 1) * 4 + 15) / 16 * 16;
+            break;
+        }
+        if (nc > K) { why = "no chunking fits LDS"; return false; }
+    }
+    t.RSB = RSB;
+    t.rpw_max = rpw;
+    t.waves = waves;
+    t.maxr = maxr;
+    t.seg_start.assign(1, 0);
+    t.seg_row_off.assign(nb * t.nc * (rpw + 1), 0);
+    std::vector<uint64_t> cur(rpw);
+    for (uint64_t g = 0; g < nb; g++) {
+        const uint64_t r0 = tb_rows[g], nr = tb_rows[g + 1] - r0;
+        for (uint64_t i = 0; i < nr; i++) cur[i] = row_ptr[r0 + i];
+        for (uint32_t j = 0; j < t.nc; j++) {
+            const uint64_t lim = (uint64_t)(j + 1) * t.KC, base = t.tcol.size();
+            uint32_t *off = &t.seg_row_off[(g * t.nc + j) * (rpw + 1)];
+            for (uint64_t i = 0; i < nr; i++) {
+                off[i] = (uint32_t)(t.tcol.size() - base);
+                uint64_t e = cur[i];
+                const uint64_t e_end = row_ptr[r0 + i + 1];
+                for (; e < e_end && col[e] < lim; e++) {
+                    t.tcol.push_back((uint16_t)(col[e] - (uint64_t)j * t.KC));
+                    t.src.push_back((uint32_t)e);
+                }
+                cur[i] = e;
+                while ((t.tcol.size() - base) % 4) { t.tcol.push_back(0); t.src.push_back(~0u); }
+            }
+            for (uint64_t i = nr; i <= rpw; i++) off[i] = (uint32_t)(t.tcol.size() - base);
+            while ((t.tcol.size() - base) % 8) { t.tcol.push_back(0); t.src.push_back(~0u); }
+            GS_CHECK(t.tcol.size() - base <= t.seg_cap, "LDS tile segment exceeds its capacity");
+            GS_CHECK(t.tcol.size() < 0xffffffffull, "LDS tile layout exceeds 32-bit offsets");
+            t.seg_start.push_back((uint32_t)t.tcol.size());
+        }
+    }
+    return true;
+}
+
 }  // namespace
 
 void upload_plan(plan_state &p, int dtype, int device) {
@@ -127,9 +241,41 @@ void upload_plan(plan_state &p, int dtype, int device) {
                 a.a1 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_BMW_indices", 0), "first_BMW_indices"));
                 d.n_rows_aux = m.u(TBLOCK_META, "first_BMW_indices", 0).size() - 1;  // BMTB count
             }
-            a.a2 = dev_copy(d, csr_row_ptr(rows, row_num));
+            std::vector<uint32_t> rp = csr_row_ptr(rows, row_num);
+            a.a2 = dev_copy(d, rp);
             d.n_units = m.u(WARP_META, "first_row_indices", 0).size() - 1;
             d.scf = 4;
+            if (sp.tblock_parent && get_config().LDS_STAGE_B) {
+                lds_tiles t;
+                std::string why;
+                const uint32_t Nd = (uint32_t)get_config().DENSE_MATRIX_SIZE;
+                const size_t budget = (size_t)std::min<int64_t>(get_config().SHARED_MEM_TOTAL_SIZE, 160 * 1024);
+                if (build_lds_tiles(m.u(TBLOCK_META, "first_row_indices", 0), m.u(TBLOCK_META, "first_BMW_indices", 0),
+                                    m.u(WARP_META, "first_row_indices", 0), rp, col, p.K, Nd, dtype ? 2u : 4u, budget,
+                                    t, why)) {
+                    d.lds = true;
+                    d.lds_N = Nd;
+                    d.KC = t.KC; d.nc = t.nc; d.RSB = t.RSB; d.rpw_max = t.rpw_max; d.seg_cap = t.seg_cap;
+                    d.waves = t.waves; d.maxr = t.maxr; d.lds_bytes = t.lds_bytes;
+                    const size_t before = d.bytes_A;
+                    a.t0 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_row_indices", 0), "BMTB first_row_indices"));
+                    a.t1 = dev_copy(d, t.seg_start);
+                    a.t2 = dev_copy(d, t.seg_row_off);
+                    a.tcol = dev_copy(d, t.tcol, kPad);
+                    if (dtype == 0) {
+                        std::vector<float> v(t.src.size());
+                        for (size_t i = 0; i < v.size(); i++)
+                            v[i] = t.src[i] == ~0u ? 0.f : (float)vals->read_float_from_arr(t.src[i]);
+                        a.tval = dev_copy(d, v, kPad);
+                    } else {
+                        std::vector<uint16_t> v(t.src.size());
+                        for (size_t i = 0; i < v.size(); i++)
+                            v[i] = t.src[i] == ~0u ? 0 : f32_to_f16_bits((float)vals->read_float_from_arr(t.src[i]));
+                        a.tval = dev_copy(d, v, kPad);
+                    }
+                    d.bytes_tile = d.bytes_A - before;
+                }
+            }
             break;
         }
         case KF_BLOCK_TOTAL: {
@@ -197,6 +343,13 @@ void add_replica(plan_state &p) {
     r.a3 = (uint32_t *)dup(s.a3);
     r.a4 = (uint32_t *)dup(s.a4);
     r.m0 = (uint64_t *)dup(s.m0);
+    r.tcol = dup(s.tcol);
+    r.tval = dup(s.tval);
+    r.t0 = (uint32_t *)dup(s.t0);
+    r.t1 = (uint32_t *)dup(s.t1);
+    r.t2 = (uint32_t *)dup(s.t2);
+    r.t3 = (uint32_t *)dup(s.t3);
+    r.t4 = (uint32_t *)dup(s.t4);
     p.dev.replicas.push_back(r);
 }
 
@@ -215,6 +368,28 @@ uint32_t pow2ceil(uint32_t x) {
     uint32_t p = 1;
     while (p < x) p <<= 1;
     return p;
+}
+
+template <class VT, int CF>
+void launch_lds(const plan_state &p, const device_arrays &a, const VT *B, VT *C, uint32_t N, hipStream_t s) {
+    const device_plan &d = p.dev;
+    const uint32_t X = N * (uint32_t)sizeof(VT) / 16u;
+    const uint32_t nb = (uint32_t)d.n_rows_aux;
+    const dim3 grid(nb), block(64 * d.waves);
+    const uint32_t K = (uint32_t)p.K;
+#define GS_LDS_ARGS                                                                                              \
+    a.t0, a.a1, a.a0, a.t1, a.t2, (const uint16_t *)a.tcol, (const VT *)a.tval, B, C, K, N, X, d.KC, d.nc, d.RSB, \
+        d.rpw_max, d.seg_cap, (uint32_t)d.row_base
+    auto go = [&](auto kern) {
+        // dynamic LDS above 64 KB must be opted into per kernel
+        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)d.lds_bytes));
+        hipLaunchKernelGGL(kern, grid, block, d.lds_bytes, s, GS_LDS_ARGS);
+    };
+    if (d.maxr == 1) go(gsk::k_lds_rows<VT, CF, 1, kLdsMaxU>);
+    else if (d.maxr == 2) go(gsk::k_lds_rows<VT, CF, 2, kLdsMaxU>);
+    else go(gsk::k_lds_rows<VT, CF, 4, kLdsMaxU>);
+#undef GS_LDS_ARGS
 }
 
 template <class VT, class CT, int CF, int SCF>
@@ -236,6 +411,12 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
             break;
         }
         case KF_WARP_TOTAL: {
+            if constexpr (CF * sizeof(VT) == 16) {
+                if (d.lds && N == d.lds_N) {
+                    launch_lds<VT, CF>(p, a, B, C, N, s);
+                    break;
+                }
+            }
             uint32_t gx;
             if (sp.tblock_parent) gx = (uint32_t)d.n_rows_aux;
             else gx = (uint32_t)std::min<uint64_t>((d.n_units + 3) / 4, 1u << 16);

@@ -54,6 +54,11 @@ typedef struct {
     int family;                   /* 1 thread_total, 2 warp_rows, 3 block_rows, 4 bitmap_segment */
     int col_bytes, dtype, replicas, needs_memset;
     char kernel_name[64];
+    /* LDS-stationary B (warp_total inside BMTBs, config LDS_STAGE_B): 1 when the
+     * upload built the chunked tile layout; it runs for dense width lds_n */
+    int lds_stage;
+    uint32_t lds_n, lds_kc, lds_chunks, lds_waves;
+    uint64_t lds_bytes, tile_bytes;
 } gs_plan_info;
 
 const char *gs_last_error(void);
@@ -71,7 +76,7 @@ int gs_set_config_int(const char *key, long long value);
 int gs_plan_add_operator(gs_plan_t *p, const char *op_name, const long long *args, int nargs);
 /* canned pipelines: thread_total(p0=sparse_cf,p1=cf), warp_total(cf=p1), block_total(cf=p1),
  * thread_bit_map(p0=sparse_cf,p1=cf), warp_segment(p0=sparse_cf,p1=cf),
- * tblock_warp_total(p0=rows per BMTB), balanced_warp_total(p0=nnz per BMW) */
+ * tblock_warp_total(p0=rows per BMTB, p1=rows per BMW), balanced_warp_total(p0=nnz per BMW) */
 int gs_plan_run_pipeline(gs_plan_t *p, const char *name, int dense_n, int p0, int p1);
 int gs_plan_compile(gs_plan_t *p);
 int gs_plan_generate_program(gs_plan_t *p, const char *root_dir, int repeat, char *dir_out, int dir_out_len);

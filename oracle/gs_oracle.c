@@ -675,9 +675,9 @@ int or_pipeline(or_set *s, const char *name, int p0, int p1) {
         if (or_thread_bit_map_operator(s, 1, p0)) return -1;
         return or_warp_segment_operator(s, p0);
     }
-    if (!strcmp(name, "tblock_warp_total")) { /* tblock rows p0 + BMW rb=1 + warp_total */
+    if (!strcmp(name, "tblock_warp_total")) { /* tblock rows p0 + BMW rows p1 (default 1) + warp_total */
         if (or_row_dir_tblock_blocking(s, p0)) return -1;
-        return or_row_dir_warp_blocking(s, 1);
+        return or_row_dir_warp_blocking(s, p1 > 0 ? p1 : 1);
     }
     if (!strcmp(name, "balanced_warp_total")) /* A11 balanced BMW + warp_total */
         return or_balanced_row_dir_warp_blocking(s, (uint64_t)p0);
@@ -776,5 +776,29 @@ int or_time_cpu_path(uint64_t M, uint64_t K, uint64_t nnz, const uint64_t *row,
     free(B); free(C);
     *t_transform = t1 - t0;
     *t_spmm = t3 - t2;
+    return 0;
+}
+
+/* CPU baseline leg of bench.py: the host SpMM (spmm_reference_host restated,
+ * fp32) repeated until at least min_s seconds of work, single thread. */
+int or_time_spmm_repeated(uint64_t M, uint64_t K, uint64_t nnz, const uint64_t *row,
+                          const uint64_t *col, const float *val, uint64_t N, double min_s,
+                          double *t_total, int *reps) {
+    float *B = (float *)malloc(K * N * sizeof(float));
+    float *C = (float *)malloc(M * N * sizeof(float));
+    if (!B || !C) { free(B); free(C); return -1; }
+    for (uint64_t i = 0; i < K * N; i++) B[i] = (float)((i * 2654435761u) % 1000) / 1000.f - 0.5f;
+    int r = 0;
+    double t0 = now_s(), t = 0;
+    do {
+        or_spmm_ref_f32(M, N, nnz, row, col, val, B, C);
+        r++;
+        t = now_s() - t0;
+    } while (t < min_s);
+    volatile float sink = C[0];
+    (void)sink;
+    free(B); free(C);
+    *t_total = t;
+    *reps = r;
     return 0;
 }

@@ -108,6 +108,10 @@ int or_time_cpu_path(uint64_t M, uint64_t K, uint64_t nnz, const uint64_t *row,
                      const uint64_t *col, const float *val, uint64_t N,
                      double *t_transform, double *t_spmm);
 
+int or_time_spmm_repeated(uint64_t M, uint64_t K, uint64_t nnz, const uint64_t *row,
+                          const uint64_t *col, const float *val, uint64_t N, double min_s,
+                          double *t_total, int *reps);
+
 #ifdef __cplusplus
 }
 #endif

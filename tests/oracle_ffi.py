@@ -118,3 +118,19 @@ def time_cpu_path(M, K, row, col, val, N):
     if rc != 0:
         raise RuntimeError("oracle cpu path failed")
     return t1.value, t2.value
+
+
+def time_spmm_repeated(M, K, row, col, val, N, min_s):
+    """host fp32 SpMM repeated for >= min_s seconds: (seconds, repetitions)"""
+    L = lib()
+    row = np.ascontiguousarray(row, dtype=np.uint64)
+    col = np.ascontiguousarray(col, dtype=np.uint64)
+    val = np.ascontiguousarray(val, dtype=np.float32)
+    t = ctypes.c_double()
+    r = ctypes.c_int()
+    rc = L.or_time_spmm_repeated(M, K, len(row), _p(row, ctypes.c_uint64), _p(col, ctypes.c_uint64),
+                                 _p(val, ctypes.c_float), N, ctypes.c_double(min_s), ctypes.byref(t),
+                                 ctypes.byref(r))
+    if rc != 0:
+        raise RuntimeError("oracle cpu path failed")
+    return t.value, r.value

@@ -106,8 +106,9 @@ def test_c2_full_size_against_torch():
     A = A.to(DEV)
     B = torch.randn((K, N), device=DEV, dtype=torch.float16)
     ref = A @ B.float()
-    for name, p0 in (("tblock_warp_total", 4), ("warp_segment", 4), ("thread_total", 4), ("block_total", 0)):
-        plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline(name, N, p0, 1).compile().upload("f16", 0)
+    for name, p0, p1 in (("tblock_warp_total", 20, 2), ("tblock_warp_total", 4, 1), ("warp_segment", 4, 1),
+                         ("thread_total", 4, 1), ("block_total", 0, 1)):
+        plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline(name, N, p0, p1).compile().upload("f16", 0)
         C = plan.spmm(B).float()
         torch.cuda.synchronize()
         err = ((C - ref).abs() / ref.abs().clamp(min=1.0)).max().item()
@@ -143,3 +144,65 @@ def test_rocsparse_comparator_agrees():
                  np.float32).reshape(K, N)
     ref = ofi.spmm_ref(M, N, row, col, v, B, "f64")
     check(out, ref, "f32")
+
+
+# ---------------------------------------------------------------- LDS-stationary B
+# tblock_warp_total(p0 rows per BMTB, p1 rows per BMW) uploads the chunk-major tile
+# layout and runs k_lds_rows when dense width N makes whole 16-B B rows.
+LDS_PIPES = [(20, 2), (8, 1), (64, 4), (4, 4), (3, 1), (48, 3)]
+
+
+def lds_cases():
+    yield from coo_cases()
+    # many column chunks: K far above one LDS chunk of B
+    yield "wide", 300, 40000, *ds.random_rows(300, 40000, 300.0, seed=5, empty_frac=0.05)
+
+
+@pytest.mark.parametrize("dtype,N", [("f16", 8), ("f16", 32), ("f16", 64), ("f32", 4), ("f32", 32)])
+@pytest.mark.parametrize("pipe", LDS_PIPES, ids=lambda p: f"{p[0]}x{p[1]}")
+def test_lds_stage_matches_oracle(pipe, dtype, N):
+    p0, p1 = pipe
+    for case, M, K, row, col, val in lds_cases():
+        plan, C, B = run(M, K, row, col, val, "tblock_warp_total", p0, p1, N, dtype)
+        info = plan.info()
+        assert info["lds_stage"] == 1 and info["lds_n"] == N, (case, info)
+        v = val.astype(np.float16).astype(np.float32) if dtype == "f16" else val
+        ref = ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64")
+        check(C, ref, dtype)
+        # a different dense width than the plan's falls back to the gather kernel
+        N2 = N + 1
+        B2 = np.random.default_rng(1).uniform(-1, 1, (K, N2)).astype(B.dtype)
+        C2 = plan.spmm(torch.from_numpy(B2).to(DEV)).float().cpu().numpy()
+        ref2 = ofi.spmm_ref(M, N2, row, col, v, B2.astype(np.float32), "f64")
+        check(C2, ref2, dtype)
+        plan.free()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f16"])
+def test_lds_stage_known_answer(dtype):
+    M, K, N = 700, 9000, 32
+    row, col, _ = ds.random_rows(M, K, 60.0, seed=8, empty_frac=0.1)
+    npdt = np.float16 if dtype == "f16" else np.float32
+    plan, C, _ = run(M, K, row, col, np.ones(len(row), np.float32), "tblock_warp_total", 20, 2, N, dtype,
+                     B=np.ones((K, N), npdt))
+    assert plan.info()["lds_stage"] == 1
+    nnz_row = np.bincount(row.astype(np.int64), minlength=M).astype(np.float32)
+    np.testing.assert_array_equal(C, np.repeat(nnz_row[:, None], N, axis=1))
+
+
+def test_lds_stage_off_and_unfit_plans_use_gather_kernel():
+    M, K, N = 300, 500, 32
+    row, col, val = ds.random_rows(M, K, 10.0, seed=9)
+    try:
+        gsa.set_config("LDS_STAGE_B", 0)
+        plan, C0, B = run(M, K, row, col, val, "tblock_warp_total", 20, 2, N, "f16")
+        assert plan.info()["lds_stage"] == 0
+    finally:
+        gsa.set_config("LDS_STAGE_B", 1)
+    plan1, C1, _ = run(M, K, row, col, val, "tblock_warp_total", 20, 2, N, "f16", B=B)
+    assert plan1.info()["lds_stage"] == 1
+    check(C1, C0, "f16")
+    # 64 one-row BMWs per BMTB exceed the 16-wave workgroup: gather kernel
+    plan2, C2, _ = run(M, K, row, col, val, "tblock_warp_total", 64, 1, N, "f16", B=B)
+    assert plan2.info()["lds_stage"] == 0
+    check(C2, C0, "f16")
