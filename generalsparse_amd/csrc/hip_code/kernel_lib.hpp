@@ -638,6 +638,176 @@ __global__ __launch_bounds__(1024) void k_lds_rows(
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// BMTB row blocks on the matrix cores (MI355X layout of a tblock/warp-total
+// plan whose row blocks are dense enough): workgroup g owns BMTB g (R <= 16*RT
+// rows) and walks K in chunks of KC columns.  Per chunk:
+//   1. B[kc0 : kc0+KC, 0:N] -> LDS, row k at k*N*2 bytes with its 32-B pieces
+//      (16 columns) permuted by b_piece() so the transposed operand reads are
+//      conflict-free; the A image rows 0..R-1 (row stride RS = 2*KC + 32 B,
+//      conflict-free ds_read_b128 operand reads) are cleared;
+//   2. the BMTB's entries of the chunk (upload layout: groups of 8 entries,
+//      [8 x u16 pos = row*KC + col][8 x f16 value]) are scattered into the A
+//      image (ds_write_b16); padding entries write 0 to row R, which is never
+//      stored;
+//   3. waves split the chunk's 32-wide k-steps: v_mfma_f32_16x16x32_f16 on
+//      A rows (ds_read_b128) x B (ds_read_b64_tr_b16), fp32 accumulation.
+// The next chunk's global loads are issued into registers between 2 and 3.
+// At the end the W per-wave partial tiles are summed in a fixed order through
+// LDS (deterministic) and rows < R are stored.  A zero of the A image times a
+// non-finite B value gives NaN: this kernel multiplies the whole row block's
+// tile, not only its nonzeros.
+// ---------------------------------------------------------------------------
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4v lds_s4v;
+
+template <int CT>
+__device__ __forceinline__ uint32_t b_piece(uint32_t k, uint32_t p) {
+    uint32_t sw;
+    if constexpr (CT == 1) sw = 0;
+    else if constexpr (CT == 2) sw = (k >> 3) & 1u;
+    else if constexpr (CT == 4) sw = ((k >> 1) & 1u) | (((k >> 3) & 1u) << 1);
+    else sw = (k & 3u) | (((k >> 3) & 1u) << 2);
+    return p ^ (sw & (uint32_t)(CT - 1));
+}
+
+template <int CT, int RT, int MAXB, int MAXA>
+__global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
+                                                   const uint32_t *__restrict__ seg_start,  // n_bmtb*nc+1 (groups)
+                                                   const u32x4 *__restrict__ tA,  // 2 u32x4 per group
+                                                   const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K,
+                                                   uint32_t N, uint32_t KC, uint32_t lgKC, uint32_t nc, uint32_t RS,
+                                                   uint32_t row_base) {
+    constexpr uint32_t RPAD = 16 * RT;
+    constexpr uint32_t UB = 2 * CT;       // 16-B units per B row
+    constexpr uint32_t RB = 32 * CT;      // bytes per B row (N == 16*CT)
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint32_t lA = KC * RB;
+    const uint32_t tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63u, wv = tid >> 6, W = nthr >> 6;
+    const uint32_t g = blockIdx.x;
+    const uint32_t r0 = bmtb_first_row[g], R = bmtb_first_row[g + 1] - r0;
+    const u32x4 zero4 = {0u, 0u, 0u, 0u};
+
+    for (uint32_t u = tid; u < (RPAD + 1) * RS / 16u; u += nthr)
+        *reinterpret_cast<u32x4 *>(lds + lA + u * 16u) = zero4;
+
+    u32x4 stB[MAXB], stP[MAXA], stV[MAXA];
+    uint32_t s_lo = seg_start[g * nc], s_hi = seg_start[g * nc + 1];
+    f4v acc[RT][CT];
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+
+    // global -> registers for chunk j (branch-free: idle units re-read unit 0;
+    // tA carries one spare group past the end)
+#define GS_MFMA_LOAD(j, s0, s1)                                                                     \
+    {                                                                                             \
+        const u32x4 *bsrc_ = reinterpret_cast<const u32x4 *>(B + (size_t)(j) * KC * N);           \
+        const uint32_t UBt_ = min(KC, K - (j) * KC) * UB;                                         \
+        _Pragma("unroll") for (int I = 0; I < MAXB; I++) {                                        \
+            const uint32_t u = tid + I * nthr;                                                    \
+            stB[I] = bsrc_[u < UBt_ ? u : 0u];                                                    \
+        }                                                                                         \
+        const uint32_t G_ = (s1) - (s0);                                                          \
+        _Pragma("unroll") for (int I = 0; I < MAXA; I++) {                                        \
+            const uint32_t q = tid + I * nthr;                                                    \
+            const size_t qq = (size_t)(s0) + (q < G_ ? q : 0u);                                   \
+            stP[I] = tA[2 * qq];                                                                  \
+            stV[I] = tA[2 * qq + 1];                                                              \
+        }                                                                                         \
+    }
+
+    GS_MFMA_LOAD(0u, s_lo, s_hi);
+    for (uint32_t j = 0; j < nc; j++) {
+        const uint32_t kr = min(KC, K - j * KC);
+        const uint32_t kr32 = (kr + 31u) & ~31u;
+        // 1. B chunk (rows kr..kr32 zero), clear A rows 0..R-1
+#pragma unroll
+        for (int I = 0; I < MAXB; I++) {
+            const uint32_t u = tid + I * nthr;
+            if (u < kr32 * UB) {
+                const uint32_t k = u / UB, s = u % UB;
+                const uint32_t a = k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u;
+                *reinterpret_cast<u32x4 *>(lds + a) = u < kr * UB ? stB[I] : zero4;
+            }
+        }
+        if (j > 0)
+            for (uint32_t u = tid; u < R * RS / 16u; u += nthr)
+                *reinterpret_cast<u32x4 *>(lds + lA + u * 16u) = zero4;
+        __syncthreads();
+        // 2. scatter the chunk's entries
+        {
+            const uint32_t G = s_hi - s_lo;
+#pragma unroll
+            for (int I = 0; I < MAXA; I++) {
+                const uint32_t q = tid + I * nthr;
+                if (q < G) {
+#pragma unroll
+                    for (int e = 0; e < 8; e++) {
+                        const uint32_t pos = (stP[I][e >> 1] >> (16 * (e & 1))) & 0xffffu;
+                        const uint16_t v = (uint16_t)((stV[I][e >> 1] >> (16 * (e & 1))) & 0xffffu);
+                        *reinterpret_cast<uint16_t *>(lds + lA + (pos >> lgKC) * RS + (pos & (KC - 1u)) * 2u) = v;
+                    }
+                }
+            }
+        }
+        // 3. next chunk's loads in flight during the matrix-core phase
+        if (j + 1 < nc) {
+            const uint32_t n_lo = s_hi, n_hi = seg_start[g * nc + j + 2];
+            GS_MFMA_LOAD(j + 1, n_lo, n_hi);
+            s_lo = n_lo;
+            s_hi = n_hi;
+        }
+        __syncthreads();
+        // 4. k-steps of 32 split over the waves
+        const uint32_t nsteps = kr32 / 32u;
+        for (uint32_t st = wv; st < nsteps; st += W) {
+            const uint32_t kb = st * 32u + 8u * (lane >> 4);
+            h8v a[RT];
+#pragma unroll
+            for (int rt = 0; rt < RT; rt++)
+                a[rt] = *reinterpret_cast<const h8v *>(lds + lA + (16u * rt + (lane & 15u)) * RS + kb * 2u);
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) {
+                s4v t[2];
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const uint32_t k = kb + 4u * h + ((lane & 15u) >> 2);
+                    const uint32_t a_ = k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u;
+                    t[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v *)(lds + a_));
+                }
+                h8v b;
+                __builtin_memcpy(&b, t, 16);
+#pragma unroll
+                for (int rt = 0; rt < RT; rt++)
+                    acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt], b, acc[rt][ct], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+#undef GS_MFMA_LOAD
+    // fixed-order reduction of the W partial tiles
+    float *red = reinterpret_cast<float *>(lds);
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++)
+            *reinterpret_cast<f4v *>(red + (((wv * RT + rt) * CT + ct) * 64u + lane) * 4u) = acc[rt][ct];
+    __syncthreads();
+    for (uint32_t e = tid; e < RT * CT * 256u; e += nthr) {
+        const uint32_t cc = e & 15u, ct = (e >> 4) % CT, rr = ((e >> 4) / CT) & 15u, rt = (e >> 4) / CT / 16u;
+        const uint32_t ln = 16u * (rr >> 2) + cc, i = rr & 3u;
+        float sum = 0.f;
+        for (uint32_t w = 0; w < W; w++) sum += red[(((w * RT + rt) * CT + ct) * 64u + ln) * 4u + i];
+        const uint32_t row = 16u * rt + rr;
+        if (row < R) C[(size_t)(row_base + r0 + row) * N + 16u * ct + cc] = (f16)sum;
+    }
+}
+
 }  // namespace gsk
 
 // ---------------------------------------------------------------------------

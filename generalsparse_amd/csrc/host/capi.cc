@@ -88,9 +88,9 @@ void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1)
         ex.add_and_run(std::make_shared<warp_segment_reduce_operator>(cg, (unsigned)cf, false, false, ctx));
         ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)(nnz / 128 + 1),
                                                              std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
-    } else if (name == "block_total") {  // token_test.cc:1458-1514
-        int cf = p1 > 0 ? p1 : 1;
-        ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, 1, false, ctx));
+    } else if (name == "block_total") {  // token_test.cc:1458-1514 (p0 = rows per BMTB, 1 there)
+        int rb = p0 > 0 ? p0 : 1, cf = p1 > 0 ? p1 : 1;
+        ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, rb, false, ctx));
         int x = std::min(N, 32), y = 256 / std::max(1, x);
         set_config("VECTOR_WIDTH", x);
         ex.add_and_run(std::make_shared<tblock_total_reduce_operator>(cg, cf, ctx));
@@ -260,7 +260,7 @@ int gs_plan_info_get(gs_plan_t *p, gs_plan_info *info) {
             info->dtype = s.dev.dtype;
             info->replicas = (int)s.dev.replicas.size();
             info->needs_memset = s.dev.needs_memset ? 1 : 0;
-            info->lds_stage = s.dev.lds ? 1 : 0;
+            info->lds_stage = s.dev.mfma ? 2 : (s.dev.lds ? 1 : 0);
             info->lds_n = s.dev.lds_N;
             info->lds_kc = s.dev.KC;
             info->lds_chunks = s.dev.nc;

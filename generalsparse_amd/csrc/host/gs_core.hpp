@@ -76,6 +76,8 @@ struct config_t {
     bool MODEL_DRIVEN_COMPRESS = false;  // absent in the .bak -> false
     // MI355X engine switches (not in the reference)
     bool LDS_STAGE_B = true;  // warp_total inside BMTBs: stage B chunks in LDS (k_lds_rows)
+    bool MFMA_TILES = true;   // fp16 BMTB row blocks on the matrix cores (k_mfma_rows)
+    int64_t MFMA_MAX_FILL = 16;  // ... when (padded row-block area) / nnz <= this
 };
 // Process-wide config: loaded once from $GS_CONFIG or ./global_config.json if
 // present (flat JSON object of scalars), defaults otherwise.

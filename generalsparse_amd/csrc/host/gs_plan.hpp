@@ -33,6 +33,7 @@ struct device_plan {
     size_t bytes_A = 0;       // device bytes of A per replica (metadata + cols + vals)
     // LDS-stationary B (k_lds_rows): chunk geometry fixed for dense width lds_N
     bool lds = false;
+    bool mfma = false;  // k_mfma_rows (uses KC, nc, lds_bytes; RS in RSB; RT in maxr)
     uint32_t lds_N = 0, KC = 0, nc = 0, RSB = 0, rpw_max = 0, seg_cap = 0, waves = 0, maxr = 0;
     size_t lds_bytes = 0, bytes_tile = 0;
     std::vector<device_arrays> replicas;

@@ -5,6 +5,8 @@
 
 #include <algorithm>
 #include <cstring>
+#include <map>
+#include <mutex>
 
 namespace gs {
 
@@ -171,6 +173,88 @@ bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uin
     return true;
 }
 
+// ------------------------------------------------------------------ MFMA tiles
+// Upload layout of k_mfma_rows (kernel_lib.hpp): for BMTB g and column chunk j,
+// the entries of g's rows with columns in [j*KC, (j+1)*KC), in groups of 8:
+// [8 x u16 pos = local_row*KC + local_col][8 x f16 value]; the last group is
+// padded with (pos = R*KC, value 0), row R being a never-stored scratch row.
+struct mfma_tiles {
+    uint32_t KC = 0, lgKC = 0, nc = 0, RS = 0, RT = 0;
+    size_t lds_bytes = 0;
+    std::vector<uint32_t> seg_start;  // in groups
+    std::vector<uint16_t> groups;     // 16 u16 per group
+};
+
+constexpr int kMfmaThreads = 512, kMfmaMaxB = 8, kMfmaMaxA = 4;
+
+bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
+                      const std::vector<uint64_t> &col, const universal_array &vals, uint64_t K, uint32_t N,
+                      size_t lds_budget, int64_t max_fill, mfma_tiles &t, std::string &why) {
+    const uint64_t nb = tb_rows.size() - 1;
+    if (nb == 0 || K == 0) { why = "empty plan"; return false; }
+    if (N % 16 || N / 16 > 8 || ((N / 16) & (N / 16 - 1))) { why = "N must be 16, 32, 64 or 128"; return false; }
+    uint64_t rmax = 0, nnz = 0;
+    for (uint64_t g = 0; g < nb; g++) rmax = std::max<uint64_t>(rmax, tb_rows[g + 1] - tb_rows[g]);
+    for (uint64_t g = 0; g < nb; g++) nnz += row_ptr[tb_rows[g + 1]] - row_ptr[tb_rows[g]];
+    if (rmax == 0 || rmax > 64) { why = "BMTBs of 1..64 rows only"; return false; }
+    const uint32_t RT = (uint32_t)((rmax + 15) / 16), RPAD = 16 * RT, CT = N / 16;
+    if (nnz == 0 || (double)nb * RPAD * K > (double)max_fill * nnz) { why = "row blocks too sparse for dense tiles"; return false; }
+    const uint32_t RB = 32 * CT, UB = 2 * CT;
+    const size_t red = (size_t)(kMfmaThreads / 64) * RT * CT * 1024;
+    for (uint32_t lg = 11; lg >= 7; lg--) {
+        const uint64_t KC = 1ull << lg;
+        const uint64_t RS = 2 * KC + 32;
+        const size_t lds = KC * RB + (RPAD + 1) * RS;
+        if ((RPAD + 1) * KC > 65536 || lds > lds_budget || lds < red) continue;
+        if (KC * UB > (uint64_t)kMfmaMaxB * kMfmaThreads && KC > 128) continue;
+        if (KC * UB > (uint64_t)kMfmaMaxB * kMfmaThreads) { why = "B chunk exceeds staging"; return false; }
+        const uint64_t nc = (K + KC - 1) / KC;
+        // largest chunk segment (groups)
+        uint64_t gmax = 0;
+        std::vector<uint64_t> cnt(nc);
+        for (uint64_t g = 0; g < nb; g++) {
+            std::fill(cnt.begin(), cnt.end(), 0);
+            for (uint64_t e = row_ptr[tb_rows[g]]; e < row_ptr[tb_rows[g + 1]]; e++) cnt[col[e] >> lg]++;
+            for (uint64_t j = 0; j < nc; j++) gmax = std::max(gmax, (cnt[j] + 7) / 8);
+        }
+        if (gmax > (uint64_t)kMfmaMaxA * kMfmaThreads) continue;
+        t.KC = (uint32_t)KC; t.lgKC = lg; t.nc = (uint32_t)nc; t.RS = (uint32_t)RS; t.RT = RT;
+        t.lds_bytes = lds;
+        break;
+    }
+    if (!t.KC) { why = "no chunk width fits LDS and the staging registers"; return false; }
+    const uint32_t KC = t.KC;
+    t.seg_start.assign(1, 0);
+    std::vector<uint64_t> cur;
+    std::vector<uint16_t> pos, hv;
+    for (uint64_t g = 0; g < nb; g++) {
+        const uint64_t r0 = tb_rows[g], R = tb_rows[g + 1] - r0;
+        cur.assign(R, 0);
+        for (uint64_t i = 0; i < R; i++) cur[i] = row_ptr[r0 + i];
+        for (uint32_t j = 0; j < t.nc; j++) {
+            const uint64_t lim = (uint64_t)(j + 1) * KC;
+            pos.clear();
+            hv.clear();
+            for (uint64_t i = 0; i < R; i++) {
+                uint64_t e = cur[i];
+                for (; e < row_ptr[r0 + i + 1] && col[e] < lim; e++) {
+                    pos.push_back((uint16_t)(i * KC + (col[e] - (uint64_t)j * KC)));
+                    hv.push_back(f32_to_f16_bits((float)vals.read_float_from_arr(e)));
+                }
+                cur[i] = e;
+            }
+            while (pos.size() % 8) { pos.push_back((uint16_t)(R * KC)); hv.push_back(0); }
+            for (size_t q = 0; q < pos.size(); q += 8) {
+                t.groups.insert(t.groups.end(), pos.begin() + q, pos.begin() + q + 8);
+                t.groups.insert(t.groups.end(), hv.begin() + q, hv.begin() + q + 8);
+            }
+            t.seg_start.push_back((uint32_t)(t.groups.size() / 16));
+        }
+    }
+    t.groups.insert(t.groups.end(), 16, 0);  // spare group for branch-free idle loads
+    return true;
+}
+
 }  // namespace
 
 void upload_plan(plan_state &p, int dtype, int device) {
@@ -213,6 +297,29 @@ void upload_plan(plan_state &p, int dtype, int device) {
         a.val = dev_copy(d, v, kPad);
     }
     uint64_t row_num = row_num_of_sub_matrix(m, 0);
+    // matrix-core row blocks for fp16 plans with BMTBs (tried before the other kernels)
+    auto try_mfma = [&](const std::vector<uint32_t> &rp) {
+        const config_t cfg = get_config();
+        if (dtype != 1 || !cfg.MFMA_TILES || !m.is_exist(TBLOCK_META, "first_row_indices", 0)) return false;
+        mfma_tiles t;
+        std::string why;
+        const uint32_t Nd = (uint32_t)cfg.DENSE_MATRIX_SIZE;
+        const size_t budget = (size_t)std::min<int64_t>(cfg.SHARED_MEM_TOTAL_SIZE, 160 * 1024);
+        if (!build_mfma_tiles(m.u(TBLOCK_META, "first_row_indices", 0), rp, col, *vals, p.K, Nd, budget,
+                              cfg.MFMA_MAX_FILL, t, why))
+            return false;
+        d.mfma = true;
+        d.lds_N = Nd;
+        d.KC = t.KC; d.nc = t.nc; d.RSB = t.RS; d.maxr = t.RT; d.rpw_max = t.lgKC;
+        d.waves = kMfmaThreads / 64; d.lds_bytes = t.lds_bytes;
+        const size_t before = d.bytes_A;
+        a.t0 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_row_indices", 0), "BMTB first_row_indices"));
+        a.t1 = dev_copy(d, t.seg_start);
+        a.tcol = dev_copy(d, t.groups);
+        d.bytes_tile = d.bytes_A - before;
+        d.n_rows_aux = m.u(TBLOCK_META, "first_row_indices", 0).size() - 1;
+        return true;
+    };
     switch (sp.family) {
         case KF_THREAD_TOTAL: {
             const auto &fn = m.u(THREAD_META, "first_nz_indices", 0);
@@ -245,6 +352,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
             a.a2 = dev_copy(d, rp);
             d.n_units = m.u(WARP_META, "first_row_indices", 0).size() - 1;
             d.scf = 4;
+            if (sp.tblock_parent && try_mfma(rp)) break;
             if (sp.tblock_parent && get_config().LDS_STAGE_B) {
                 lds_tiles t;
                 std::string why;
@@ -280,9 +388,11 @@ void upload_plan(plan_state &p, int dtype, int device) {
         }
         case KF_BLOCK_TOTAL: {
             a.a0 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_row_indices", 0), "BMTB first_row_indices"));
-            a.a2 = dev_copy(d, csr_row_ptr(rows, row_num));
+            std::vector<uint32_t> rp = csr_row_ptr(rows, row_num);
+            a.a2 = dev_copy(d, rp);
             d.n_units = m.u(TBLOCK_META, "first_row_indices", 0).size() - 1;
             d.scf = 4;
+            try_mfma(rp);
             break;
         }
         case KF_BITMAP_SEGMENT: {
@@ -381,15 +491,68 @@ void launch_lds(const plan_state &p, const device_arrays &a, const VT *B, VT *C,
     a.t0, a.a1, a.a0, a.t1, a.t2, (const uint16_t *)a.tcol, (const VT *)a.tval, B, C, K, N, X, d.KC, d.nc, d.RSB, \
         d.rpw_max, d.seg_cap, (uint32_t)d.row_base
     auto go = [&](auto kern) {
-        // dynamic LDS above 64 KB must be opted into per kernel
-        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)d.lds_bytes));
+        // dynamic LDS above 64 KB must be opted into, once per kernel and device
+        static std::mutex mu;
+        static std::map<std::pair<int, const void *>, size_t> granted;
+        {
+            std::lock_guard<std::mutex> l(mu);
+            size_t &g = granted[{d.device, reinterpret_cast<const void *>(kern)}];
+            if (g < d.lds_bytes) {
+                HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.lds_bytes));
+                g = d.lds_bytes;
+            }
+        }
         hipLaunchKernelGGL(kern, grid, block, d.lds_bytes, s, GS_LDS_ARGS);
     };
     if (d.maxr == 1) go(gsk::k_lds_rows<VT, CF, 1, kLdsMaxU>);
     else if (d.maxr == 2) go(gsk::k_lds_rows<VT, CF, 2, kLdsMaxU>);
     else go(gsk::k_lds_rows<VT, CF, 4, kLdsMaxU>);
 #undef GS_LDS_ARGS
+}
+
+template <int CT, int RT>
+void launch_mfma_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N,
+                    hipStream_t s) {
+    const device_plan &d = p.dev;
+    auto kern = gsk::k_mfma_rows<CT, RT, kMfmaMaxB, kMfmaMaxA>;
+    static std::mutex mu;
+    static std::map<int, size_t> granted;
+    {
+        std::lock_guard<std::mutex> l(mu);
+        size_t &g = granted[d.device];
+        if (g < d.lds_bytes) {
+            HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)d.lds_bytes));
+            g = d.lds_bytes;
+        }
+    }
+    hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux), dim3(kMfmaThreads), d.lds_bytes, s, a.t0, a.t1,
+                       (const gsk::u32x4 *)a.tcol, B, C, (uint32_t)p.K, N, d.KC, d.rpw_max, d.nc, d.RSB,
+                       (uint32_t)d.row_base);
+    HIP_OK(hipGetLastError());
+}
+
+template <int CT>
+void launch_mfma_ct(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N,
+                    hipStream_t s) {
+    switch (p.dev.maxr) {
+        case 1: launch_mfma_rt<CT, 1>(p, a, B, C, N, s); break;
+        case 2: launch_mfma_rt<CT, 2>(p, a, B, C, N, s); break;
+        case 3: launch_mfma_rt<CT, 3>(p, a, B, C, N, s); break;
+        default: launch_mfma_rt<CT, 4>(p, a, B, C, N, s); break;
+    }
+}
+
+void launch_mfma(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
+    const gsk::f16 *b = (const gsk::f16 *)B;
+    gsk::f16 *c = (gsk::f16 *)C;
+    switch (N / 16) {
+        case 1: launch_mfma_ct<1>(p, a, b, c, N, s); break;
+        case 2: launch_mfma_ct<2>(p, a, b, c, N, s); break;
+        case 4: launch_mfma_ct<4>(p, a, b, c, N, s); break;
+        default: launch_mfma_ct<8>(p, a, b, c, N, s); break;
+    }
 }
 
 template <class VT, class CT, int CF, int SCF>
@@ -484,6 +647,10 @@ void launch_spmm(const plan_state &p, int replica, const void *B, void *C, uint3
     GS_CHECK(replica >= 0 && (size_t)replica < p.dev.replicas.size(), "bad replica index");
     GS_CHECK(N >= 1, "N >= 1");
     const device_arrays &a = p.dev.replicas[replica];
+    if (p.dev.mfma && N == p.dev.lds_N) {
+        launch_mfma(p, a, B, C, N, stream);
+        return;
+    }
     if (p.dev.dtype == 0) dispatch_vt<float, 4>(p, a, B, C, N, stream);
     else dispatch_vt<gsk::f16, 8>(p, a, B, C, N, stream);
 }

@@ -54,8 +54,8 @@ typedef struct {
     int family;                   /* 1 thread_total, 2 warp_rows, 3 block_rows, 4 bitmap_segment */
     int col_bytes, dtype, replicas, needs_memset;
     char kernel_name[64];
-    /* LDS-stationary B (warp_total inside BMTBs, config LDS_STAGE_B): 1 when the
-     * upload built the chunked tile layout; it runs for dense width lds_n */
+    /* row-block kernels built at upload for dense width lds_n: 1 = LDS-stationary B
+     * (k_lds_rows, config LDS_STAGE_B), 2 = matrix cores (k_mfma_rows, MFMA_TILES) */
     int lds_stage;
     uint32_t lds_n, lds_kc, lds_chunks, lds_waves;
     uint64_t lds_bytes, tile_bytes;
@@ -74,7 +74,7 @@ int gs_set_config_int(const char *key, long long value);
 /* operator surface: name = reference class name; args in constructor order
  * without the code_generator / operator_context arguments */
 int gs_plan_add_operator(gs_plan_t *p, const char *op_name, const long long *args, int nargs);
-/* canned pipelines: thread_total(p0=sparse_cf,p1=cf), warp_total(cf=p1), block_total(cf=p1),
+/* canned pipelines: thread_total(p0=sparse_cf,p1=cf), warp_total(cf=p1), block_total(p0=rows per BMTB, cf=p1),
  * thread_bit_map(p0=sparse_cf,p1=cf), warp_segment(p0=sparse_cf,p1=cf),
  * tblock_warp_total(p0=rows per BMTB, p1=rows per BMW), balanced_warp_total(p0=nnz per BMW) */
 int gs_plan_run_pipeline(gs_plan_t *p, const char *name, int dense_n, int p0, int p1);

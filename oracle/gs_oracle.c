@@ -664,8 +664,8 @@ int or_pipeline(or_set *s, const char *name, int p0, int p1) {
     }
     if (!strcmp(name, "warp_total")) /* token_test.cc:1188-1249 */
         return or_row_dir_warp_blocking(s, 1);
-    if (!strcmp(name, "block_total")) /* token_test.cc:1458-1514 */
-        return or_row_dir_tblock_blocking(s, 1);
+    if (!strcmp(name, "block_total")) /* token_test.cc:1458-1514 (rb 1 there; p0 = rows per BMTB) */
+        return or_row_dir_tblock_blocking(s, p0 > 0 ? p0 : 1);
     if (!strcmp(name, "thread_bit_map")) { /* token_test.cc:1319-1391, p0 = VW */
         if (or_nnz_dir_thread_blocking(s, 32, 1)) return -1;
         return or_thread_bit_map_operator(s, 0, p0);

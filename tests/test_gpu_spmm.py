@@ -19,6 +19,7 @@ pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
 PIPES = [("thread_total", 4, 1), ("thread_total", 8, 1), ("warp_total", 0, 1), ("block_total", 0, 1),
+         ("block_total", 20, 1),
          ("thread_bit_map", 4, 1), ("warp_segment", 4, 1), ("tblock_warp_total", 4, 1),
          ("tblock_warp_total", 16, 1), ("balanced_warp_total", 256, 1)]
 TOL = {"f32": 1e-3, "f16": 1e-1}
@@ -158,9 +159,16 @@ def lds_cases():
     yield "wide", 300, 40000, *ds.random_rows(300, 40000, 300.0, seed=5, empty_frac=0.05)
 
 
+@pytest.fixture
+def no_mfma():
+    gsa.set_config("MFMA_TILES", 0)
+    yield
+    gsa.set_config("MFMA_TILES", 1)
+
+
 @pytest.mark.parametrize("dtype,N", [("f16", 8), ("f16", 32), ("f16", 64), ("f32", 4), ("f32", 32)])
 @pytest.mark.parametrize("pipe", LDS_PIPES, ids=lambda p: f"{p[0]}x{p[1]}")
-def test_lds_stage_matches_oracle(pipe, dtype, N):
+def test_lds_stage_matches_oracle(pipe, dtype, N, no_mfma):
     p0, p1 = pipe
     for case, M, K, row, col, val in lds_cases():
         plan, C, B = run(M, K, row, col, val, "tblock_warp_total", p0, p1, N, dtype)
@@ -179,7 +187,7 @@ def test_lds_stage_matches_oracle(pipe, dtype, N):
 
 
 @pytest.mark.parametrize("dtype", ["f32", "f16"])
-def test_lds_stage_known_answer(dtype):
+def test_lds_stage_known_answer(dtype, no_mfma):
     M, K, N = 700, 9000, 32
     row, col, _ = ds.random_rows(M, K, 60.0, seed=8, empty_frac=0.1)
     npdt = np.float16 if dtype == "f16" else np.float32
@@ -190,7 +198,7 @@ def test_lds_stage_known_answer(dtype):
     np.testing.assert_array_equal(C, np.repeat(nnz_row[:, None], N, axis=1))
 
 
-def test_lds_stage_off_and_unfit_plans_use_gather_kernel():
+def test_lds_stage_off_and_unfit_plans_use_gather_kernel(no_mfma):
     M, K, N = 300, 500, 32
     row, col, val = ds.random_rows(M, K, 10.0, seed=9)
     try:
@@ -206,3 +214,74 @@ def test_lds_stage_off_and_unfit_plans_use_gather_kernel():
     plan2, C2, _ = run(M, K, row, col, val, "tblock_warp_total", 64, 1, N, "f16", B=B)
     assert plan2.info()["lds_stage"] == 0
     check(C2, C0, "f16")
+
+
+# ---------------------------------------------------------------- matrix-core row blocks
+# fp16 plans with BMTB row blocks run k_mfma_rows when the blocks are dense enough
+# (MFMA_MAX_FILL); the tests raise the fill limit so sparse cases exercise it too.
+MFMA_PIPES = [("tblock_warp_total", 20, 2), ("block_total", 16, 1), ("block_total", 20, 1),
+              ("block_total", 33, 1), ("block_total", 64, 1), ("block_total", 7, 1)]
+
+
+def mfma_cases():
+    yield from coo_cases()
+    r, c, v = ds.pruned_weight(1000, 3000, 0.8, 21)
+    yield "pruned_ragged_M", 1000, 3000, r, c, v
+    r, c, v = ds.pruned_weight(300, 4100, 0.5, 22)  # K not a multiple of the chunk or of 32
+    yield "pruned_odd_K", 300, 4100, r, c, v
+    keep = (r % 7) != 3  # empty rows inside row blocks
+    yield "pruned_empty_rows", 300, 4100, r[keep], c[keep], v[keep]
+
+
+@pytest.fixture
+def mfma_everywhere():
+    gsa.set_config("MFMA_MAX_FILL", 1 << 30)
+    yield
+    gsa.set_config("MFMA_MAX_FILL", 16)
+
+
+@pytest.mark.parametrize("N", [16, 32, 64, 128])
+@pytest.mark.parametrize("pipe", MFMA_PIPES, ids=lambda p: f"{p[0]}-{p[1]}")
+def test_mfma_rows_match_oracle(pipe, N, mfma_everywhere):
+    name, p0, p1 = pipe
+    for case, M, K, row, col, val in mfma_cases():
+        plan, C, B = run(M, K, row, col, val, name, p0, p1, N, "f16")
+        info = plan.info()
+        assert info["lds_stage"] == 2, (case, info)
+        v = val.astype(np.float16).astype(np.float32)
+        ref = ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64")
+        check(C, ref, "f16")
+        plan.free()
+
+
+def test_mfma_rows_known_answer_and_fallback(mfma_everywhere):
+    M, K, N = 700, 9000, 32
+    row, col, _ = ds.random_rows(M, K, 60.0, seed=8, empty_frac=0.1)
+    plan, C, _ = run(M, K, row, col, np.ones(len(row), np.float32), "block_total", 20, 1, N, "f16",
+                     B=np.ones((K, N), np.float16))
+    assert plan.info()["lds_stage"] == 2
+    nnz_row = np.bincount(row.astype(np.int64), minlength=M).astype(np.float32)
+    np.testing.assert_array_equal(C, np.repeat(nnz_row[:, None], N, axis=1))
+    # another dense width than the plan's runs the gather kernel
+    B2 = np.random.default_rng(2).uniform(-1, 1, (K, 24)).astype(np.float16)
+    C2 = plan.spmm(torch.from_numpy(B2).to(DEV)).float().cpu().numpy()
+    ref2 = ofi.spmm_ref(M, 24, row, col, np.ones(len(row), np.float32), B2.astype(np.float32), "f64")
+    check(C2, ref2, "f16")
+
+
+def test_mfma_rows_selection():
+    M, K, N = 400, 2000, 32
+    r, c, v = ds.pruned_weight(M, K, 0.7, 5)
+    plan, _, _ = run(M, K, r, c, v, "block_total", 20, 1, N, "f16")
+    assert plan.info()["lds_stage"] == 2          # 30% dense: matrix cores
+    plan, _, _ = run(M, K, r, c, v, "block_total", 20, 1, N, "f32")
+    assert plan.info()["lds_stage"] == 0          # fp32: CUDA-core kernels
+    rr, cc, vv = ds.random_rows(M, K, 10.0, seed=6)
+    plan, _, _ = run(M, K, rr, cc, vv, "block_total", 20, 1, N, "f16")
+    assert plan.info()["lds_stage"] == 0          # 0.5% dense: too sparse for tiles
+    try:
+        gsa.set_config("MFMA_TILES", 0)
+        plan, _, _ = run(M, K, r, c, v, "tblock_warp_total", 20, 2, N, "f16")
+        assert plan.info()["lds_stage"] == 1
+    finally:
+        gsa.set_config("MFMA_TILES", 1)
