@@ -640,29 +640,34 @@ __global__ __launch_bounds__(1024) void k_lds_rows(
 
 
 // ---------------------------------------------------------------------------
-// BMTB row blocks on the matrix cores (MI355X layout of a tblock/warp-total
-// plan whose row blocks are dense enough): workgroup g owns BMTB g (R <= 16*RT
-// rows) and walks K in chunks of KC columns.  Per chunk:
-//   1. B[kc0 : kc0+KC, 0:N] -> LDS, row k at k*N*2 bytes with its 32-B pieces
-//      (16 columns) permuted by b_piece() so the transposed operand reads are
-//      conflict-free; the A image rows 0..R-1 (row stride RS = 2*KC + 32 B,
-//      conflict-free ds_read_b128 operand reads) are cleared;
-//   2. the BMTB's entries of the chunk (upload layout: groups of 8 entries,
-//      [8 x u16 pos = row*KC + col][8 x f16 value]) are scattered into the A
-//      image (ds_write_b16); padding entries write 0 to row R, which is never
-//      stored;
-//   3. waves split the chunk's 32-wide k-steps: v_mfma_f32_16x16x32_f16 on
-//      A rows (ds_read_b128) x B (ds_read_b64_tr_b16), fp32 accumulation.
-// The next chunk's global loads are issued into registers between 2 and 3.
-// At the end the W per-wave partial tiles are summed in a fixed order through
-// LDS (deterministic) and rows < R are stored.  A zero of the A image times a
-// non-finite B value gives NaN: this kernel multiplies the whole row block's
-// tile, not only its nonzeros.
+// BMTB row blocks on the matrix cores (MI355X layout of a tblock/warp/block-
+// total plan whose row blocks are dense enough).  Workgroup g owns BMTB g
+// (R <= RMAX <= 16*RT rows) and walks K in chunks of KC = 2^LGKC columns.  One
+// dynamic LDS array holds two sets of
+//   B[b]: B[kc0 : kc0+KC, 0:N], row k at k*N*2 bytes, its 32-B pieces (16
+//         columns) permuted by b_piece() so the transposed reads are
+//         conflict-free;
+//   S[b]: the chunk's compressed entries as uploaded (groups of 8:
+//         [8 x u16 pos = row*KC + col][8 x f16 value]), NA KiB per wave;
+//   D[b]: the row block's dense fp16 image, RMAX+1 rows of RS = 2*KC + 32 B
+//         (conflict-free ds_read_b128); row R stays zero and stands in for
+//         every MFMA row >= R;
+// all staged by LDS-DMA (global_load_lds_dwordx4) with counted vmcnt waits and
+// raw s_barrier, so the loads of the next chunks stay in flight across the
+// barriers.  Iteration j: wait B(j); barrier; DMA B(j+1), S(j+2); clear
+// D[next]; MFMA chunk j (waves split its 32-wide k-steps,
+// v_mfma_f32_16x16x32_f16: A by ds_read_b128, B by ds_read_b64_tr_b16, fp32
+// accumulators); wait S(j+1); barrier; scatter S(j+1) into D[next]
+// (ds_write_b16; padding entries write 0 to row R).  At the end the W per-wave
+// partial tiles are summed in a fixed order through LDS (deterministic) and
+// rows < R are stored.  A zero of the dense image times a non-finite B value
+// gives NaN: the kernel multiplies the row block's whole tile.
 // ---------------------------------------------------------------------------
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef short s4v __attribute__((ext_vector_type(4)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s4v lds_s4v;
+typedef __attribute__((address_space(3))) void lds_void;
 
 template <int CT>
 __device__ __forceinline__ uint32_t b_piece(uint32_t k, uint32_t p) {
@@ -674,137 +679,183 @@ __device__ __forceinline__ uint32_t b_piece(uint32_t k, uint32_t p) {
     return p ^ (sw & (uint32_t)(CT - 1));
 }
 
-template <int CT, int RT, int MAXB, int MAXA>
+// s_waitcnt vmcnt(n) / lgkmcnt(0) with the other counters left alone (gfx9 encoding)
+#define GS_WAIT_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | (7 << 4) | (15 << 8))
+#define GS_WAIT_LGKM0() __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4))
+#define GS_RAW_BARRIER()       \
+    {                          \
+        GS_WAIT_LGKM0();       \
+        __builtin_amdgcn_s_barrier(); \
+    }
+
+constexpr int kMfmaWaves = 8, kMfmaNA = 2;
+
+// LDS-DMA of 16 B per lane to LDS byte address lds_addr (wave-uniform) + 16*lane.
+// Inline asm on purpose: hipcc treats an in-flight global_load_lds builtin as a
+// pending write to all of LDS and drains it (vmcnt(0)) before every
+// ds_read_b64_tr_b16, which would serialise the staging pipeline; here the
+// kernel counts vmcnt itself (GS_WAIT_VMCNT).  M0 is set inside the asm.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void dma16(const void *gptr, uint32_t lds_addr) {
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "s"(lds_addr) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+template <int CT, int RT, int LGKC>
 __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
                                                    const uint32_t *__restrict__ seg_start,  // n_bmtb*nc+1 (groups)
-                                                   const u32x4 *__restrict__ tA,  // 2 u32x4 per group
+                                                   const unsigned char *__restrict__ tA,  // 32 B per group (+pad)
                                                    const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K,
-                                                   uint32_t N, uint32_t KC, uint32_t lgKC, uint32_t nc, uint32_t RS,
-                                                   uint32_t row_base) {
-    constexpr uint32_t RPAD = 16 * RT;
-    constexpr uint32_t UB = 2 * CT;       // 16-B units per B row
-    constexpr uint32_t RB = 32 * CT;      // bytes per B row (N == 16*CT)
+                                                   uint32_t N, uint32_t nc, uint32_t RMAX, uint32_t row_base) {
+    constexpr uint32_t KC = 1u << LGKC;
+    constexpr uint32_t RB = 32 * CT;                  // bytes per B row (N == 16*CT)
+    constexpr uint32_t RS = 2 * KC + 32;              // dense image row stride
+    constexpr uint32_t W = kMfmaWaves;
+    constexpr uint32_t szB = KC * RB;                 // one B buffer
+    constexpr uint32_t NP = szB / 1024u / W;          // B DMA pieces per wave per chunk
+    constexpr uint32_t NA = kMfmaNA;                  // S DMA pieces per wave per chunk
+    constexpr uint32_t szS = NA * W * 1024u;          // one S buffer
+    static_assert(szB % (1024u * W) == 0, "whole DMA pieces per wave");
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const uint32_t lA = KC * RB;
-    const uint32_t tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63u, wv = tid >> 6, W = nthr >> 6;
+    const uint32_t szD = (RMAX + 1) * RS;
+    const uint32_t oS = 2 * szB, oD = 2 * szB + 2 * szS;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t g = blockIdx.x;
     const uint32_t r0 = bmtb_first_row[g], R = bmtb_first_row[g + 1] - r0;
+    const uint32_t nseg = gridDim.x * nc;
+    const uint32_t lbase = (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char *)lds;
     const u32x4 zero4 = {0u, 0u, 0u, 0u};
 
-    for (uint32_t u = tid; u < (RPAD + 1) * RS / 16u; u += nthr)
-        *reinterpret_cast<u32x4 *>(lds + lA + u * 16u) = zero4;
+    for (uint32_t u = tid; u < 2 * szD / 16u; u += 512u) *reinterpret_cast<u32x4 *>(lds + oD + u * 16u) = zero4;
 
-    u32x4 stB[MAXB], stP[MAXA], stV[MAXA];
-    uint32_t s_lo = seg_start[g * nc], s_hi = seg_start[g * nc + 1];
     f4v acc[RT][CT];
 #pragma unroll
     for (int rt = 0; rt < RT; rt++)
 #pragma unroll
         for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
 
-    // global -> registers for chunk j (branch-free: idle units re-read unit 0;
-    // tA carries one spare group past the end)
-#define GS_MFMA_LOAD(j, s0, s1)                                                                     \
-    {                                                                                             \
-        const u32x4 *bsrc_ = reinterpret_cast<const u32x4 *>(B + (size_t)(j) * KC * N);           \
-        const uint32_t UBt_ = min(KC, K - (j) * KC) * UB;                                         \
-        _Pragma("unroll") for (int I = 0; I < MAXB; I++) {                                        \
-            const uint32_t u = tid + I * nthr;                                                    \
-            stB[I] = bsrc_[u < UBt_ ? u : 0u];                                                    \
-        }                                                                                         \
-        const uint32_t G_ = (s1) - (s0);                                                          \
-        _Pragma("unroll") for (int I = 0; I < MAXA; I++) {                                        \
-            const uint32_t q = tid + I * nthr;                                                    \
-            const size_t qq = (size_t)(s0) + (q < G_ ? q : 0u);                                   \
-            stP[I] = tA[2 * qq];                                                                  \
-            stV[I] = tA[2 * qq + 1];                                                              \
-        }                                                                                         \
-    }
-
-    GS_MFMA_LOAD(0u, s_lo, s_hi);
-    for (uint32_t j = 0; j < nc; j++) {
-        const uint32_t kr = min(KC, K - j * KC);
-        const uint32_t kr32 = (kr + 31u) & ~31u;
-        // 1. B chunk (rows kr..kr32 zero), clear A rows 0..R-1
+    // B(j) -> B[j&1]: lane-linear 1-KiB pieces, each lane fetching the 16 B that
+    // belong at its LDS position (the piece swizzle is an involution); rows past
+    // K re-read the chunk's first row (finite, multiplied by zero columns)
+    auto dma_b = [&](uint32_t j) {
+        const uint32_t kc0 = min(j, nc - 1u) * KC;
 #pragma unroll
-        for (int I = 0; I < MAXB; I++) {
-            const uint32_t u = tid + I * nthr;
-            if (u < kr32 * UB) {
-                const uint32_t k = u / UB, s = u % UB;
-                const uint32_t a = k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u;
-                *reinterpret_cast<u32x4 *>(lds + a) = u < kr * UB ? stB[I] : zero4;
+        for (uint32_t i = 0; i < NP; i++) {
+            const uint32_t pc = wv * NP + i;
+            const uint32_t p = pc * 1024u + lane * 16u;
+            const uint32_t k = p / RB, unit = (p % RB) >> 4;
+            const uint32_t lg = b_piece<CT>(k, unit >> 1);
+            const uint32_t kk = kc0 + k < K ? kc0 + k : kc0;
+            const unsigned char *src =
+                reinterpret_cast<const unsigned char *>(B) + (size_t)kk * RB + lg * 32u + (unit & 1u) * 16u;
+            dma16(src, lbase + (j & 1u) * szB + pc * 1024u);
+        }
+    };
+    // S(j) -> S[j&1]: the segment's bytes, NA pieces per wave (tA is padded)
+    auto dma_s = [&](uint32_t j) {
+        const size_t base = (size_t)seg_start[min(g * nc + j, nseg - 1u)] * 32u;
+#pragma unroll
+        for (uint32_t i = 0; i < NA; i++) {
+            const uint32_t pc = wv * NA + i;
+            dma16(tA + base + pc * 1024u + lane * 16u, lbase + oS + (j & 1u) * szS + pc * 1024u);
+        }
+    };
+    auto scatter = [&](uint32_t j) {
+        const uint32_t sidx = g * nc + j;
+        const uint32_t G = seg_start[sidx + 1] - seg_start[sidx];
+        const unsigned char *src = lds + oS + (j & 1u) * szS;
+        unsigned char *dst = lds + oD + (j & 1u) * szD;
+        for (uint32_t q = tid; q < G; q += 512u) {
+            const u32x4 P = *reinterpret_cast<const u32x4 *>(src + q * 32u);
+            const u32x4 V = *reinterpret_cast<const u32x4 *>(src + q * 32u + 16u);
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const uint32_t pos = (P[e >> 1] >> (16 * (e & 1))) & 0xffffu;
+                const uint16_t v = (uint16_t)((V[e >> 1] >> (16 * (e & 1))) & 0xffffu);
+                *reinterpret_cast<uint16_t *>(dst + (pos >> LGKC) * RS + (pos & (KC - 1u)) * 2u) = v;
             }
         }
-        if (j > 0)
-            for (uint32_t u = tid; u < R * RS / 16u; u += nthr)
-                *reinterpret_cast<u32x4 *>(lds + lA + u * 16u) = zero4;
-        __syncthreads();
-        // 2. scatter the chunk's entries
+    };
+
+    dma_b(0);
+    dma_s(0);
+    dma_s(1);
+    GS_WAIT_VMCNT(NA);  // B(0), S(0) landed (S(1) may fly)
+    GS_RAW_BARRIER();   // ... for every wave; dense images cleared
+    scatter(0);
+    for (uint32_t j = 0; j < nc; j++) {
+        GS_WAIT_VMCNT(NA);  // B(j) landed (S(j+1) may fly)
+        GS_RAW_BARRIER();   // B(j), D(j) complete; buffers of chunk j-1 free
+        dma_b(j + 1);       // always issued (re-reads at the tail): fixed counts
+        dma_s(j + 2);
+        if (j + 1 < nc)
+            for (uint32_t u = tid; u < R * RS / 16u; u += 512u)
+                *reinterpret_cast<u32x4 *>(lds + oD + ((j + 1) & 1u) * szD + u * 16u) = zero4;
         {
-            const uint32_t G = s_hi - s_lo;
+            const uint32_t kr = min(KC, K - j * KC);
+            const uint32_t nsteps = (kr + 31u) / 32u;
+            const unsigned char *la = lds + oD + (j & 1u) * szD;
+            const unsigned char *lb = lds + (j & 1u) * szB;
+            uint32_t arow[RT];
 #pragma unroll
-            for (int I = 0; I < MAXA; I++) {
-                const uint32_t q = tid + I * nthr;
-                if (q < G) {
+            for (int rt = 0; rt < RT; rt++) {
+                const uint32_t row = 16u * rt + (lane & 15u);
+                arow[rt] = (row < R ? row : R) * RS;
+            }
+            for (uint32_t st = wv; st < nsteps; st += W) {
+                const uint32_t kb = st * 32u + 8u * (lane >> 4);
+                h8v av[RT];
 #pragma unroll
-                    for (int e = 0; e < 8; e++) {
-                        const uint32_t pos = (stP[I][e >> 1] >> (16 * (e & 1))) & 0xffffu;
-                        const uint16_t v = (uint16_t)((stV[I][e >> 1] >> (16 * (e & 1))) & 0xffffu);
-                        *reinterpret_cast<uint16_t *>(lds + lA + (pos >> lgKC) * RS + (pos & (KC - 1u)) * 2u) = v;
+                for (int rt = 0; rt < RT; rt++) av[rt] = *reinterpret_cast<const h8v *>(la + arow[rt] + kb * 2u);
+#pragma unroll
+                for (int ct = 0; ct < CT; ct++) {
+                    s4v t[2];
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const uint32_t k = kb + 4u * h + ((lane & 15u) >> 2);
+                        t[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                            (lds_s4v *)(lb + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u));
                     }
+                    h8v bv;
+                    __builtin_memcpy(&bv, t, 16);
+#pragma unroll
+                    for (int rt = 0; rt < RT; rt++)
+                        acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[rt], bv, acc[rt][ct], 0, 0, 0);
                 }
             }
         }
-        // 3. next chunk's loads in flight during the matrix-core phase
-        if (j + 1 < nc) {
-            const uint32_t n_lo = s_hi, n_hi = seg_start[g * nc + j + 2];
-            GS_MFMA_LOAD(j + 1, n_lo, n_hi);
-            s_lo = n_lo;
-            s_hi = n_hi;
-        }
-        __syncthreads();
-        // 4. k-steps of 32 split over the waves
-        const uint32_t nsteps = kr32 / 32u;
-        for (uint32_t st = wv; st < nsteps; st += W) {
-            const uint32_t kb = st * 32u + 8u * (lane >> 4);
-            h8v a[RT];
+        GS_WAIT_VMCNT(NP + NA);  // S(j+1) landed (B(j+1), S(j+2) may fly)
+        GS_RAW_BARRIER();        // D[next] cleared, S(j+1) visible, MFMA(j) done with B[j&1]
+        if (j + 1 < nc) scatter(j + 1);
+    }
+    GS_WAIT_VMCNT(0);
+    GS_RAW_BARRIER();
+    // fixed-order reduction of the W partial tiles, TPP tiles per pass
+    float *red = reinterpret_cast<float *>(lds);
+    const uint32_t TPP = min((uint32_t)(RT * CT), (oD + 2 * szD) / (W * 1024u));
+    for (uint32_t t0 = 0; t0 < RT * CT; t0 += TPP) {
 #pragma unroll
-            for (int rt = 0; rt < RT; rt++)
-                a[rt] = *reinterpret_cast<const h8v *>(lds + lA + (16u * rt + (lane & 15u)) * RS + kb * 2u);
+        for (int rt = 0; rt < RT; rt++)
 #pragma unroll
             for (int ct = 0; ct < CT; ct++) {
-                s4v t[2];
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const uint32_t k = kb + 4u * h + ((lane & 15u) >> 2);
-                    const uint32_t a_ = k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u;
-                    t[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v *)(lds + a_));
-                }
-                h8v b;
-                __builtin_memcpy(&b, t, 16);
-#pragma unroll
-                for (int rt = 0; rt < RT; rt++)
-                    acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rt], b, acc[rt][ct], 0, 0, 0);
+                const uint32_t tt = rt * CT + ct;
+                if (tt >= t0 && tt < t0 + TPP)
+                    *reinterpret_cast<f4v *>(red + ((wv * TPP + (tt - t0)) * 64u + lane) * 4u) = acc[rt][ct];
             }
+        __syncthreads();
+        const uint32_t nt = min(TPP, RT * CT - t0);
+        for (uint32_t e = tid; e < nt * 256u; e += 512u) {
+            const uint32_t ti = e >> 8, cc = e & 15u, rr = (e >> 4) & 15u;
+            const uint32_t tt = t0 + ti, rt = tt / CT, ct = tt % CT;
+            const uint32_t ln = 16u * (rr >> 2) + cc, i = rr & 3u;
+            float sum = 0.f;
+#pragma unroll
+            for (uint32_t w = 0; w < W; w++) sum += red[((w * TPP + ti) * 64u + ln) * 4u + i];
+            const uint32_t row = 16u * rt + rr;
+            if (row < R) C[(size_t)(row_base + r0 + row) * N + 16u * ct + cc] = (f16)sum;
         }
         __syncthreads();
-    }
-#undef GS_MFMA_LOAD
-    // fixed-order reduction of the W partial tiles
-    float *red = reinterpret_cast<float *>(lds);
-#pragma unroll
-    for (int rt = 0; rt < RT; rt++)
-#pragma unroll
-        for (int ct = 0; ct < CT; ct++)
-            *reinterpret_cast<f4v *>(red + (((wv * RT + rt) * CT + ct) * 64u + lane) * 4u) = acc[rt][ct];
-    __syncthreads();
-    for (uint32_t e = tid; e < RT * CT * 256u; e += nthr) {
-        const uint32_t cc = e & 15u, ct = (e >> 4) % CT, rr = ((e >> 4) / CT) & 15u, rt = (e >> 4) / CT / 16u;
-        const uint32_t ln = 16u * (rr >> 2) + cc, i = rr & 3u;
-        float sum = 0.f;
-        for (uint32_t w = 0; w < W; w++) sum += red[(((w * RT + rt) * CT + ct) * 64u + ln) * 4u + i];
-        const uint32_t row = 16u * rt + rr;
-        if (row < R) C[(size_t)(row_base + r0 + row) * N + 16u * ct + cc] = (f16)sum;
     }
 }
 

@@ -177,39 +177,42 @@ bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uin
 // Upload layout of k_mfma_rows (kernel_lib.hpp): for BMTB g and column chunk j,
 // the entries of g's rows with columns in [j*KC, (j+1)*KC), in groups of 8:
 // [8 x u16 pos = local_row*KC + local_col][8 x f16 value]; the last group is
-// padded with (pos = R*KC, value 0), row R being a never-stored scratch row.
+// padded with (pos = R*KC, value 0), row R being the kernel's zero row.
 struct mfma_tiles {
-    uint32_t KC = 0, lgKC = 0, nc = 0, RS = 0, RT = 0;
+    uint32_t lgKC = 0, nc = 0, RT = 0, RMAX = 0;
     size_t lds_bytes = 0;
     std::vector<uint32_t> seg_start;  // in groups
-    std::vector<uint16_t> groups;     // 16 u16 per group
+    std::vector<uint16_t> groups;     // 16 u16 per group, + one stage buffer of padding
 };
 
-constexpr int kMfmaThreads = 512, kMfmaMaxB = 8, kMfmaMaxA = 4;
+constexpr uint32_t kMfmaThreads = 64 * gsk::kMfmaWaves;
+constexpr uint32_t kMfmaStageBytes = gsk::kMfmaNA * gsk::kMfmaWaves * 1024;
+
+size_t mfma_lds_bytes(uint32_t lgKC, uint32_t CT, uint32_t RMAX) {
+    const size_t KC = 1ull << lgKC;
+    return 2 * KC * 32 * CT + 2 * (size_t)kMfmaStageBytes + 2 * (RMAX + 1) * (2 * KC + 32);
+}
 
 bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
                       const std::vector<uint64_t> &col, const universal_array &vals, uint64_t K, uint32_t N,
                       size_t lds_budget, int64_t max_fill, mfma_tiles &t, std::string &why) {
     const uint64_t nb = tb_rows.size() - 1;
     if (nb == 0 || K == 0) { why = "empty plan"; return false; }
-    if (N % 16 || N / 16 > 8 || ((N / 16) & (N / 16 - 1))) { why = "N must be 16, 32, 64 or 128"; return false; }
+    if (N != 16 && N != 32 && N != 64) { why = "N must be 16, 32 or 64"; return false; }
+    const uint32_t CT = N / 16;
     uint64_t rmax = 0, nnz = 0;
     for (uint64_t g = 0; g < nb; g++) rmax = std::max<uint64_t>(rmax, tb_rows[g + 1] - tb_rows[g]);
     for (uint64_t g = 0; g < nb; g++) nnz += row_ptr[tb_rows[g + 1]] - row_ptr[tb_rows[g]];
     if (rmax == 0 || rmax > 64) { why = "BMTBs of 1..64 rows only"; return false; }
-    const uint32_t RT = (uint32_t)((rmax + 15) / 16), RPAD = 16 * RT, CT = N / 16;
-    if (nnz == 0 || (double)nb * RPAD * K > (double)max_fill * nnz) { why = "row blocks too sparse for dense tiles"; return false; }
-    const uint32_t RB = 32 * CT, UB = 2 * CT;
-    const size_t red = (size_t)(kMfmaThreads / 64) * RT * CT * 1024;
-    for (uint32_t lg = 11; lg >= 7; lg--) {
+    const uint32_t RT = rmax <= 16 ? 1 : (rmax <= 32 ? 2 : 4);
+    if (nnz == 0 || (double)nb * 16 * RT * K > (double)max_fill * nnz) {
+        why = "row blocks too sparse for dense tiles";
+        return false;
+    }
+    for (uint32_t lg = 10; lg >= 8; lg--) {
         const uint64_t KC = 1ull << lg;
-        const uint64_t RS = 2 * KC + 32;
-        const size_t lds = KC * RB + (RPAD + 1) * RS;
-        if ((RPAD + 1) * KC > 65536 || lds > lds_budget || lds < red) continue;
-        if (KC * UB > (uint64_t)kMfmaMaxB * kMfmaThreads && KC > 128) continue;
-        if (KC * UB > (uint64_t)kMfmaMaxB * kMfmaThreads) { why = "B chunk exceeds staging"; return false; }
+        if ((rmax + 1) * KC > 65536 || mfma_lds_bytes(lg, CT, (uint32_t)rmax) > lds_budget) continue;
         const uint64_t nc = (K + KC - 1) / KC;
-        // largest chunk segment (groups)
         uint64_t gmax = 0;
         std::vector<uint64_t> cnt(nc);
         for (uint64_t g = 0; g < nb; g++) {
@@ -217,13 +220,13 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
             for (uint64_t e = row_ptr[tb_rows[g]]; e < row_ptr[tb_rows[g + 1]]; e++) cnt[col[e] >> lg]++;
             for (uint64_t j = 0; j < nc; j++) gmax = std::max(gmax, (cnt[j] + 7) / 8);
         }
-        if (gmax > (uint64_t)kMfmaMaxA * kMfmaThreads) continue;
-        t.KC = (uint32_t)KC; t.lgKC = lg; t.nc = (uint32_t)nc; t.RS = (uint32_t)RS; t.RT = RT;
-        t.lds_bytes = lds;
+        if (gmax * 32 > kMfmaStageBytes) continue;
+        t.lgKC = lg; t.nc = (uint32_t)nc; t.RT = RT; t.RMAX = (uint32_t)rmax;
+        t.lds_bytes = mfma_lds_bytes(lg, CT, (uint32_t)rmax);
         break;
     }
-    if (!t.KC) { why = "no chunk width fits LDS and the staging registers"; return false; }
-    const uint32_t KC = t.KC;
+    if (!t.lgKC) { why = "no chunk width fits LDS and the stage buffers"; return false; }
+    const uint32_t KC = 1u << t.lgKC;
     t.seg_start.assign(1, 0);
     std::vector<uint64_t> cur;
     std::vector<uint16_t> pos, hv;
@@ -251,7 +254,7 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
             t.seg_start.push_back((uint32_t)(t.groups.size() / 16));
         }
     }
-    t.groups.insert(t.groups.end(), 16, 0);  // spare group for branch-free idle loads
+    t.groups.insert(t.groups.end(), kMfmaStageBytes / 2, 0);  // stage-sized tail: fixed-size DMA reads
     return true;
 }
 
@@ -310,7 +313,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
             return false;
         d.mfma = true;
         d.lds_N = Nd;
-        d.KC = t.KC; d.nc = t.nc; d.RSB = t.RS; d.maxr = t.RT; d.rpw_max = t.lgKC;
+        d.KC = 1u << t.lgKC; d.nc = t.nc; d.maxr = t.RT; d.rpw_max = t.RMAX; d.RSB = t.lgKC;
         d.waves = kMfmaThreads / 64; d.lds_bytes = t.lds_bytes;
         const size_t before = d.bytes_A;
         a.t0 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_row_indices", 0), "BMTB first_row_indices"));
@@ -511,11 +514,11 @@ void launch_lds(const plan_state &p, const device_arrays &a, const VT *B, VT *C,
 #undef GS_LDS_ARGS
 }
 
-template <int CT, int RT>
-void launch_mfma_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N,
-                    hipStream_t s) {
+template <int CT, int RT, int LGKC>
+void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N,
+                   hipStream_t s) {
     const device_plan &d = p.dev;
-    auto kern = gsk::k_mfma_rows<CT, RT, kMfmaMaxB, kMfmaMaxA>;
+    auto kern = gsk::k_mfma_rows<CT, RT, LGKC>;
     static std::mutex mu;
     static std::map<int, size_t> granted;
     {
@@ -528,9 +531,18 @@ void launch_mfma_rt(const plan_state &p, const device_arrays &a, const gsk::f16 
         }
     }
     hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux), dim3(kMfmaThreads), d.lds_bytes, s, a.t0, a.t1,
-                       (const gsk::u32x4 *)a.tcol, B, C, (uint32_t)p.K, N, d.KC, d.rpw_max, d.nc, d.RSB,
-                       (uint32_t)d.row_base);
+                       (const unsigned char *)a.tcol, B, C, (uint32_t)p.K, N, d.nc, d.rpw_max, (uint32_t)d.row_base);
     HIP_OK(hipGetLastError());
+}
+
+template <int CT, int RT>
+void launch_mfma_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N,
+                    hipStream_t s) {
+    switch (p.dev.RSB) {  // log2 KC
+        case 10: launch_mfma_k<CT, RT, 10>(p, a, B, C, N, s); break;
+        case 9: launch_mfma_k<CT, RT, 9>(p, a, B, C, N, s); break;
+        default: launch_mfma_k<CT, RT, 8>(p, a, B, C, N, s); break;
+    }
 }
 
 template <int CT>
@@ -539,7 +551,6 @@ void launch_mfma_ct(const plan_state &p, const device_arrays &a, const gsk::f16 
     switch (p.dev.maxr) {
         case 1: launch_mfma_rt<CT, 1>(p, a, B, C, N, s); break;
         case 2: launch_mfma_rt<CT, 2>(p, a, B, C, N, s); break;
-        case 3: launch_mfma_rt<CT, 3>(p, a, B, C, N, s); break;
         default: launch_mfma_rt<CT, 4>(p, a, B, C, N, s); break;
     }
 }
@@ -550,8 +561,7 @@ void launch_mfma(const plan_state &p, const device_arrays &a, const void *B, voi
     switch (N / 16) {
         case 1: launch_mfma_ct<1>(p, a, b, c, N, s); break;
         case 2: launch_mfma_ct<2>(p, a, b, c, N, s); break;
-        case 4: launch_mfma_ct<4>(p, a, b, c, N, s); break;
-        default: launch_mfma_ct<8>(p, a, b, c, N, s); break;
+        default: launch_mfma_ct<4>(p, a, b, c, N, s); break;
     }
 }
 

@@ -11,8 +11,8 @@ import generalsparse_amd as gsa  # noqa: E402
 from generalsparse_amd import datasets as ds  # noqa: E402
 
 
-def timeit(M, K, row, col, val, N, dtype, p0, p1, reps=8, steps=100):
-    plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline("tblock_warp_total", N, p0, p1).compile()
+def timeit(M, K, row, col, val, N, dtype, p0, p1, reps=8, steps=100, pipe="tblock_warp_total"):
+    plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline(pipe, N, p0, p1).compile()
     plan.upload(dtype, 0)
     for _ in range(reps - 1):
         plan.add_replica()
@@ -36,7 +36,16 @@ def main():
     M = K = 5120
     row, col, val = ds.pruned_weight(M, K, 0.7, 13)
     out = {}
-    shapes = [(20, 2), (16, 1), (32, 2), (40, 4), (12, 1), (24, 2), (48, 4), (64, 4), (8, 1)]
+    for p0 in (20, 16, 32, 10, 40, 64):
+        k = f"mfma_block_total_{p0}"
+        out[k] = timeit(M, K, row, col, val, 32, "f16", p0, 1, pipe="block_total")
+        print(json.dumps({k: out[k]}), flush=True)
+    for n in (16, 64, 128):
+        k = f"mfma_block_total_20_n{n}"
+        out[k] = timeit(M, K, row, col, val, n, "f16", 20, 1, pipe="block_total")
+        print(json.dumps({k: out[k]}), flush=True)
+    gsa.set_config("MFMA_TILES", 0)
+    shapes = [(20, 2), (24, 2)]
     for p0, p1 in shapes:
         out[f"f16_{p0}x{p1}"] = timeit(M, K, row, col, val, 32, "f16", p0, p1)
         print(json.dumps({f"f16_{p0}x{p1}": out[f"f16_{p0}x{p1}"]}), flush=True)
