@@ -752,13 +752,18 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
             dma16(src, lbase + (j & 1u) * szB + pc * 1024u);
         }
     };
-    // S(j) -> S[j&1]: the segment's bytes, NA pieces per wave (tA is padded)
+    // S(j) -> S[j&1]: the segment's 1-KiB pieces; every wave issues NA DMAs
+    // (fixed vmcnt counts), pieces past the segment re-read tA's first KiB
+    // (L2-resident) instead of the next segment's bytes
     auto dma_s = [&](uint32_t j) {
-        const size_t base = (size_t)seg_start[min(g * nc + j, nseg - 1u)] * 32u;
+        const uint32_t sidx = min(g * nc + j, nseg - 1u);
+        const uint32_t s0 = seg_start[sidx];
+        const uint32_t npc = j < nc ? (seg_start[sidx + 1] - s0 + 31u) / 32u : 0u;
 #pragma unroll
         for (uint32_t i = 0; i < NA; i++) {
             const uint32_t pc = wv * NA + i;
-            dma16(tA + base + pc * 1024u + lane * 16u, lbase + oS + (j & 1u) * szS + pc * 1024u);
+            const size_t off = pc < npc ? (size_t)s0 * 32u + pc * 1024u : 0u;
+            dma16(tA + off + lane * 16u, lbase + oS + (j & 1u) * szS + pc * 1024u);
         }
     };
     auto scatter = [&](uint32_t j) {

@@ -245,8 +245,9 @@ def mfma_everywhere():
 def test_mfma_rows_match_oracle(pipe, N, mfma_everywhere):
     name, p0, p1 = pipe
     # 33..64-row blocks at N=64 do not fit LDS twice over: gather kernels (still checked)
-    expect = 0 if (p0 > 32 and N == 64) else 2
+    # and 50%-dense 33..64-row chunks exceed the entry stage buffers
     for case, M, K, row, col, val in mfma_cases():
+        expect = 0 if (p0 > 32 and (N == 64 or case in ("pruned_odd_K", "pruned_empty_rows"))) else 2
         plan, C, B = run(M, K, row, col, val, name, p0, p1, N, "f16")
         info = plan.info()
         assert info["lds_stage"] == expect, (case, info)
