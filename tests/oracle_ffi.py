@@ -51,6 +51,9 @@ def lib():
         _lib.or_round_half.restype = ctypes.c_float
         _lib.or_time_cpu_path.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u64p, u64p,
                                           f32p, ctypes.c_uint64, f64p, f64p]
+        _lib.or_time_spmm_repeated.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u64p, u64p,
+                                               f32p, ctypes.c_uint64, ctypes.c_double, f64p,
+                                               ctypes.POINTER(ctypes.c_int)]
     return _lib
 
 
@@ -129,8 +132,7 @@ def time_spmm_repeated(M, K, row, col, val, N, min_s):
     t = ctypes.c_double()
     r = ctypes.c_int()
     rc = L.or_time_spmm_repeated(M, K, len(row), _p(row, ctypes.c_uint64), _p(col, ctypes.c_uint64),
-                                 _p(val, ctypes.c_float), N, ctypes.c_double(min_s), ctypes.byref(t),
-                                 ctypes.byref(r))
+                                 _p(val, ctypes.c_float), N, min_s, ctypes.byref(t), ctypes.byref(r))
     if rc != 0:
         raise RuntimeError("oracle cpu path failed")
     return t.value, r.value

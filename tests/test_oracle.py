@@ -124,3 +124,10 @@ def test_warp_segment_invariants(vw):
             assert bits[i] == int(starts)
     wb = got["WARP_META_first_BMT_indices_0"]
     assert wb[-1] == len(bm) and np.all(np.diff(wb) <= vw)
+
+
+def test_cpu_baseline_timer_runs():
+    from generalsparse_amd import datasets as ds
+    r, c, v = ds.pruned_weight(256, 256, 0.7, 1)
+    t, reps = ofi.time_spmm_repeated(256, 256, r, c, v, 8, 0.05)
+    assert t >= 0.05 and reps >= 1
