@@ -209,6 +209,12 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
         why = "row blocks too sparse for dense tiles";
         return false;
     }
+    // every workgroup streams all of B through LDS: with short row blocks that
+    // traffic outgrows A's (R = 4 on C2: 13x) and the gather kernels win
+    if ((double)nb * K * N * 2 > 6.0 * 4.0 * nnz && max_fill < (1 << 20)) {
+        why = "row blocks too short: B traffic per row block exceeds A's";
+        return false;
+    }
     for (uint32_t lg = 10; lg >= 8; lg--) {
         const uint64_t KC = 1ull << lg;
         if ((rmax + 1) * KC > 65536 || mfma_lds_bytes(lg, CT, (uint32_t)rmax) > lds_budget) continue;
