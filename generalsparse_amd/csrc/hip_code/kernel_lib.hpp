@@ -642,32 +642,33 @@ __global__ __launch_bounds__(1024) void k_lds_rows(
 // ---------------------------------------------------------------------------
 // BMTB row blocks on the matrix cores (MI355X layout of a tblock/warp/block-
 // total plan whose row blocks are dense enough).  Workgroup g owns BMTB g
-// (R <= RMAX <= 16*RT rows) and walks K in chunks of KC = 2^LGKC columns.  One
-// dynamic LDS array holds two sets of
+// (R <= RMAX <= 16*RT rows) and walks K in chunks of KC = 2^LGKC columns.
+// Loads run two chunks ahead in registers (two register sets, the loop is
+// unrolled by two so every set index is a compile-time constant); LDS holds
+// two buffer sets of
 //   B[b]: B[kc0 : kc0+KC, 0:N], row k at k*N*2 bytes, its 32-B pieces (16
-//         columns) permuted by b_piece() so the transposed reads are
-//         conflict-free;
-//   S[b]: the chunk's compressed entries as uploaded (groups of 8:
-//         [8 x u16 pos = row*KC + col][8 x f16 value]), NA KiB per wave;
+//         columns) permuted by b_piece() so the transposed operand reads
+//         (ds_read_b64_tr_b16) are conflict-free;
 //   D[b]: the row block's dense fp16 image, RMAX+1 rows of RS = 2*KC + 32 B
-//         (conflict-free ds_read_b128); row R stays zero and stands in for
-//         every MFMA row >= R;
-// all staged by LDS-DMA (global_load_lds_dwordx4) with counted vmcnt waits and
-// raw s_barrier, so the loads of the next chunks stay in flight across the
-// barriers.  Iteration j: wait B(j); barrier; DMA B(j+1), S(j+2); clear
-// D[next]; MFMA chunk j (waves split its 32-wide k-steps,
-// v_mfma_f32_16x16x32_f16: A by ds_read_b128, B by ds_read_b64_tr_b16, fp32
-// accumulators); wait S(j+1); barrier; scatter S(j+1) into D[next]
-// (ds_write_b16; padding entries write 0 to row R).  At the end the W per-wave
-// partial tiles are summed in a fixed order through LDS (deterministic) and
-// rows < R are stored.  A zero of the dense image times a non-finite B value
-// gives NaN: the kernel multiplies the row block's whole tile.
+//         (conflict-free ds_read_b128 operand reads); row R stays zero and
+//         stands in for every MFMA row >= R.
+// Iteration j (X = j&1): barrier; issue the global loads of chunk j+2 into
+// register set X (B rows, and the chunk's compressed entries: groups of 8,
+// [8 x u16 pos = row*KC + col][8 x f16 value]); clear D[X^1]; MFMA chunk j
+// (waves split its 32-wide k-steps, v_mfma_f32_16x16x32_f16, fp32
+// accumulators); barrier; chunk j+1 from register set X^1: B rows -> B[X^1],
+// entries scattered into D[X^1] (ds_write_b16; padding entries write 0 to row
+// R).  Every load is an ordinary VGPR load, so hipcc's own counted vmcnt waits
+// keep the next chunks in flight across the barriers.  At the end the W
+// per-wave partial tiles are summed in a fixed order through LDS
+// (deterministic) and rows < R are stored.  A zero of the dense image times a
+// non-finite B value gives NaN: the kernel multiplies the row block's whole
+// tile.
 // ---------------------------------------------------------------------------
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef short s4v __attribute__((ext_vector_type(4)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s4v lds_s4v;
-typedef __attribute__((address_space(3))) void lds_void;
 
 template <int CT>
 __device__ __forceinline__ uint32_t b_piece(uint32_t k, uint32_t p) {
@@ -679,163 +680,143 @@ __device__ __forceinline__ uint32_t b_piece(uint32_t k, uint32_t p) {
     return p ^ (sw & (uint32_t)(CT - 1));
 }
 
-// s_waitcnt vmcnt(n) / lgkmcnt(0) with the other counters left alone (gfx9 encoding)
-#define GS_WAIT_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | (7 << 4) | (15 << 8))
-#define GS_WAIT_LGKM0() __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4))
-#define GS_RAW_BARRIER()       \
-    {                          \
-        GS_WAIT_LGKM0();       \
-        __builtin_amdgcn_s_barrier(); \
-    }
-
-constexpr int kMfmaWaves = 8, kMfmaNA = 2;
-
-// LDS-DMA of 16 B per lane to LDS byte address lds_addr (wave-uniform) + 16*lane.
-// Inline asm on purpose: hipcc treats an in-flight global_load_lds builtin as a
-// pending write to all of LDS and drains it (vmcnt(0)) before every
-// ds_read_b64_tr_b16, which would serialise the staging pipeline; here the
-// kernel counts vmcnt itself (GS_WAIT_VMCNT).  M0 is set inside the asm.
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-__device__ __forceinline__ void dma16(const void *gptr, uint32_t lds_addr) {
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "s"(lds_addr) : "memory", "m0");
-}
-#pragma clang diagnostic pop
+constexpr int kMfmaWaves = 8, kMfmaMaxA = 2;
 
 template <int CT, int RT, int LGKC>
 __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
                                                    const uint32_t *__restrict__ seg_start,  // n_bmtb*nc+1 (groups)
-                                                   const unsigned char *__restrict__ tA,  // 32 B per group (+pad)
+                                                   const u32x4 *__restrict__ tA,  // 2 u32x4 per group (+1 spare)
                                                    const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K,
                                                    uint32_t N, uint32_t nc, uint32_t RMAX, uint32_t row_base) {
     constexpr uint32_t KC = 1u << LGKC;
     constexpr uint32_t RB = 32 * CT;                  // bytes per B row (N == 16*CT)
+    constexpr uint32_t UB = 2 * CT;                   // 16-B units per B row
     constexpr uint32_t RS = 2 * KC + 32;              // dense image row stride
-    constexpr uint32_t W = kMfmaWaves;
-    constexpr uint32_t szB = KC * RB;                 // one B buffer
-    constexpr uint32_t NP = szB / 1024u / W;          // B DMA pieces per wave per chunk
-    constexpr uint32_t NA = kMfmaNA;                  // S DMA pieces per wave per chunk
-    constexpr uint32_t szS = NA * W * 1024u;          // one S buffer
-    static_assert(szB % (1024u * W) == 0, "whole DMA pieces per wave");
+    constexpr uint32_t W = kMfmaWaves, NT = 64 * W;
+    constexpr uint32_t szB = KC * RB;
+    constexpr uint32_t NB = szB / 16 / NT;            // B units per thread per chunk
+    constexpr int MAXA = kMfmaMaxA;
+    static_assert(szB % (16 * NT) == 0, "whole B units per thread");
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint32_t szD = (RMAX + 1) * RS;
-    const uint32_t oS = 2 * szB, oD = 2 * szB + 2 * szS;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t oD = 2 * szB;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t g = blockIdx.x;
     const uint32_t r0 = bmtb_first_row[g], R = bmtb_first_row[g + 1] - r0;
-    const uint32_t nseg = gridDim.x * nc;
-    const uint32_t lbase = (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char *)lds;
     const u32x4 zero4 = {0u, 0u, 0u, 0u};
 
-    for (uint32_t u = tid; u < 2 * szD / 16u; u += 512u) *reinterpret_cast<u32x4 *>(lds + oD + u * 16u) = zero4;
+    for (uint32_t u = tid; u < 2 * szD / 16u; u += NT) *reinterpret_cast<u32x4 *>(lds + oD + u * 16u) = zero4;
 
     f4v acc[RT][CT];
 #pragma unroll
     for (int rt = 0; rt < RT; rt++)
 #pragma unroll
         for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+    uint32_t arow[RT];
+    u32x4 sB0[NB], sP0[MAXA], sV0[MAXA], sB1[NB], sP1[MAXA], sV1[MAXA];
 
-    // B(j) -> B[j&1]: lane-linear 1-KiB pieces, each lane fetching the 16 B that
-    // belong at its LDS position (the piece swizzle is an involution); rows past
-    // K re-read the chunk's first row (finite, multiplied by zero columns)
-    auto dma_b = [&](uint32_t j) {
-        const uint32_t kc0 = min(j, nc - 1u) * KC;
-#pragma unroll
-        for (uint32_t i = 0; i < NP; i++) {
-            const uint32_t pc = wv * NP + i;
-            const uint32_t p = pc * 1024u + lane * 16u;
-            const uint32_t k = p / RB, unit = (p % RB) >> 4;
-            const uint32_t lg = b_piece<CT>(k, unit >> 1);
-            const uint32_t kk = kc0 + k < K ? kc0 + k : kc0;
-            const unsigned char *src =
-                reinterpret_cast<const unsigned char *>(B) + (size_t)kk * RB + lg * 32u + (unit & 1u) * 16u;
-            dma16(src, lbase + (j & 1u) * szB + pc * 1024u);
-        }
-    };
-    // S(j) -> S[j&1]: the segment's 1-KiB pieces; every wave issues NA DMAs
-    // (fixed vmcnt counts), pieces past the segment re-read tA's first KiB
-    // (L2-resident) instead of the next segment's bytes
-    auto dma_s = [&](uint32_t j) {
-        const uint32_t sidx = min(g * nc + j, nseg - 1u);
-        const uint32_t s0 = seg_start[sidx];
-        const uint32_t npc = j < nc ? (seg_start[sidx + 1] - s0 + 31u) / 32u : 0u;
-#pragma unroll
-        for (uint32_t i = 0; i < NA; i++) {
-            const uint32_t pc = wv * NA + i;
-            const size_t off = pc < npc ? (size_t)s0 * 32u + pc * 1024u : 0u;
-            dma16(tA + off + lane * 16u, lbase + oS + (j & 1u) * szS + pc * 1024u);
-        }
-    };
-    auto scatter = [&](uint32_t j) {
-        const uint32_t sidx = g * nc + j;
-        const uint32_t G = seg_start[sidx + 1] - seg_start[sidx];
-        const unsigned char *src = lds + oS + (j & 1u) * szS;
-        unsigned char *dst = lds + oD + (j & 1u) * szD;
-        for (uint32_t q = tid; q < G; q += 512u) {
-            const u32x4 P = *reinterpret_cast<const u32x4 *>(src + q * 32u);
-            const u32x4 V = *reinterpret_cast<const u32x4 *>(src + q * 32u + 16u);
-#pragma unroll
-            for (int e = 0; e < 8; e++) {
-                const uint32_t pos = (P[e >> 1] >> (16 * (e & 1))) & 0xffffu;
-                const uint16_t v = (uint16_t)((V[e >> 1] >> (16 * (e & 1))) & 0xffffu);
-                *reinterpret_cast<uint16_t *>(dst + (pos >> LGKC) * RS + (pos & (KC - 1u)) * 2u) = v;
-            }
-        }
-    };
-
-    dma_b(0);
-    dma_s(0);
-    dma_s(1);
-    GS_WAIT_VMCNT(NA);  // B(0), S(0) landed (S(1) may fly)
-    GS_RAW_BARRIER();   // ... for every wave; dense images cleared
-    scatter(0);
-    for (uint32_t j = 0; j < nc; j++) {
-        GS_WAIT_VMCNT(NA);  // B(j) landed (S(j+1) may fly)
-        GS_RAW_BARRIER();   // B(j), D(j) complete; buffers of chunk j-1 free
-        dma_b(j + 1);       // always issued (re-reads at the tail): fixed counts
-        dma_s(j + 2);
-        if (j + 1 < nc)
-            for (uint32_t u = tid; u < R * RS / 16u; u += 512u)
-                *reinterpret_cast<u32x4 *>(lds + oD + ((j + 1) & 1u) * szD + u * 16u) = zero4;
-        {
-            const uint32_t kr = min(KC, K - j * KC);
-            const uint32_t nsteps = (kr + 31u) / 32u;
-            const unsigned char *la = lds + oD + (j & 1u) * szD;
-            const unsigned char *lb = lds + (j & 1u) * szB;
-            uint32_t arow[RT];
-#pragma unroll
-            for (int rt = 0; rt < RT; rt++) {
-                const uint32_t row = 16u * rt + (lane & 15u);
-                arow[rt] = (row < R ? row : R) * RS;
-            }
-            for (uint32_t st = wv; st < nsteps; st += W) {
-                const uint32_t kb = st * 32u + 8u * (lane >> 4);
-                h8v av[RT];
-#pragma unroll
-                for (int rt = 0; rt < RT; rt++) av[rt] = *reinterpret_cast<const h8v *>(la + arow[rt] + kb * 2u);
-#pragma unroll
-                for (int ct = 0; ct < CT; ct++) {
-                    s4v t[2];
-#pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        const uint32_t k = kb + 4u * h + ((lane & 15u) >> 2);
-                        t[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                            (lds_s4v *)(lb + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u));
-                    }
-                    h8v bv;
-                    __builtin_memcpy(&bv, t, 16);
-#pragma unroll
-                    for (int rt = 0; rt < RT; rt++)
-                        acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[rt], bv, acc[rt][ct], 0, 0, 0);
-                }
-            }
-        }
-        GS_WAIT_VMCNT(NP + NA);  // S(j+1) landed (B(j+1), S(j+2) may fly)
-        GS_RAW_BARRIER();        // D[next] cleared, S(j+1) visible, MFMA(j) done with B[j&1]
-        if (j + 1 < nc) scatter(j + 1);
+    // chunk j -> registers; chunks past the end and idle slots re-read valid
+    // data (the spare group / the last chunk), so no load sits behind a branch
+#define GS_LOAD(j, SB, SP, SV)                                                                      \
+    {                                                                                             \
+        const uint32_t jj_ = min((uint32_t)(j), nc - 1u);                                         \
+        const uint32_t kc0_ = jj_ * KC;                                                           \
+        _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                                     \
+            const uint32_t u = tid + i * NT;                                                      \
+            const uint32_t k = u / UB;                                                            \
+            const uint32_t kk = kc0_ + k < K ? kc0_ + k : kc0_;                                   \
+            SB[i] = *reinterpret_cast<const u32x4 *>(B + (size_t)kk * N + (u % UB) * 8u);         \
+        }                                                                                         \
+        const uint32_t sidx_ = g * nc + jj_;                                                      \
+        const uint32_t s0_ = seg_start[sidx_];                                                    \
+        const uint32_t G_ = (uint32_t)(j) < nc ? seg_start[sidx_ + 1] - s0_ : 0u;                 \
+        _Pragma("unroll") for (int I = 0; I < MAXA; I++) {                                        \
+            const uint32_t q = tid + I * NT;                                                      \
+            const size_t qq = (size_t)s0_ + (q < G_ ? q : 0u);                                    \
+            SP[I] = tA[2 * qq];                                                                   \
+            SV[I] = tA[2 * qq + 1];                                                               \
+        }                                                                                         \
     }
-    GS_WAIT_VMCNT(0);
-    GS_RAW_BARRIER();
+    // registers of chunk j -> B[j&1] rows and D[j&1] entries
+#define GS_STORE(j, SB, SP, SV)                                                                     \
+    {                                                                                             \
+        unsigned char *lb_ = lds + ((j) & 1u) * szB;                                              \
+        _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                                     \
+            const uint32_t u = tid + i * NT;                                                      \
+            const uint32_t k = u / UB, s = u % UB;                                                \
+            *reinterpret_cast<u32x4 *>(lb_ + k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u) = SB[i]; \
+        }                                                                                         \
+        const uint32_t sidx_ = g * nc + (j);                                                      \
+        const uint32_t G_ = seg_start[sidx_ + 1] - seg_start[sidx_];                              \
+        unsigned char *ld_ = lds + oD + ((j) & 1u) * szD;                                         \
+        _Pragma("unroll") for (int I = 0; I < MAXA; I++) {                                        \
+            const uint32_t q = tid + I * NT;                                                      \
+            if (q < G_) {                                                                         \
+                _Pragma("unroll") for (int e = 0; e < 8; e++) {                                   \
+                    const uint32_t pos = (SP[I][e >> 1] >> (16 * (e & 1))) & 0xffffu;             \
+                    const uint16_t v = (uint16_t)((SV[I][e >> 1] >> (16 * (e & 1))) & 0xffffu);   \
+                    *reinterpret_cast<uint16_t *>(ld_ + (pos >> LGKC) * RS + (pos & (KC - 1u)) * 2u) = v; \
+                }                                                                                 \
+            }                                                                                     \
+        }                                                                                         \
+    }
+#define GS_MFMA(j)                                                                                  \
+    {                                                                                             \
+        const uint32_t kr_ = min(KC, K - (j) * KC);                                               \
+        const uint32_t nsteps_ = (kr_ + 31u) / 32u;                                               \
+        const unsigned char *la_ = lds + oD + ((j) & 1u) * szD;                                   \
+        const unsigned char *lb_ = lds + ((j) & 1u) * szB;                                        \
+        for (uint32_t st = wv; st < nsteps_; st += W) {                                           \
+            const uint32_t kb = st * 32u + 8u * (lane >> 4);                                      \
+            h8v av[RT];                                                                           \
+            _Pragma("unroll") for (int rt = 0; rt < RT; rt++) av[rt] =                            \
+                *reinterpret_cast<const h8v *>(la_ + arow[rt] + kb * 2u);                         \
+            _Pragma("unroll") for (int ct = 0; ct < CT; ct++) {                                   \
+                s4v t[2];                                                                         \
+                _Pragma("unroll") for (int h = 0; h < 2; h++) {                                   \
+                    const uint32_t k = kb + 4u * h + ((lane & 15u) >> 2);                         \
+                    t[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(                               \
+                        (lds_s4v *)(lb_ + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u)); \
+                }                                                                                 \
+                h8v bv;                                                                           \
+                __builtin_memcpy(&bv, t, 16);                                                     \
+                _Pragma("unroll") for (int rt = 0; rt < RT; rt++) acc[rt][ct] =                   \
+                    __builtin_amdgcn_mfma_f32_16x16x32_f16(av[rt], bv, acc[rt][ct], 0, 0, 0);     \
+            }                                                                                     \
+        }                                                                                         \
+    }
+#define GS_ITER(j, SBn, SPn, SVn, SBs, SPs, SVs)                                                    \
+    {                                                                                             \
+        __syncthreads();                                                                          \
+        GS_LOAD((j) + 2, SBn, SPn, SVn);                                                          \
+        if ((j) + 1 < nc)                                                                         \
+            for (uint32_t u = tid; u < R * RS / 16u; u += NT)                                     \
+                *reinterpret_cast<u32x4 *>(lds + oD + (((j) + 1) & 1u) * szD + u * 16u) = zero4;  \
+        GS_MFMA(j);                                                                               \
+        __syncthreads();                                                                          \
+        if ((j) + 1 < nc) GS_STORE((j) + 1, SBs, SPs, SVs);                                       \
+    }
+
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++) {
+        const uint32_t row = 16u * rt + (lane & 15u);
+        arow[rt] = (row < R ? row : R) * RS;
+    }
+    GS_LOAD(0u, sB0, sP0, sV0);
+    GS_LOAD(1u, sB1, sP1, sV1);
+    __syncthreads();  // dense images cleared
+    GS_STORE(0u, sB0, sP0, sV0);
+    uint32_t j = 0;
+    for (; j + 1 < nc; j += 2) {
+        GS_ITER(j, sB0, sP0, sV0, sB1, sP1, sV1);
+        GS_ITER(j + 1, sB1, sP1, sV1, sB0, sP0, sV0);
+    }
+    if (j < nc) GS_ITER(j, sB0, sP0, sV0, sB1, sP1, sV1);
+#undef GS_ITER
+#undef GS_MFMA
+#undef GS_STORE
+#undef GS_LOAD
+    __syncthreads();
     // fixed-order reduction of the W partial tiles, TPP tiles per pass
     float *red = reinterpret_cast<float *>(lds);
     const uint32_t TPP = min((uint32_t)(RT * CT), (oD + 2 * szD) / (W * 1024u));
@@ -850,7 +831,7 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
             }
         __syncthreads();
         const uint32_t nt = min(TPP, RT * CT - t0);
-        for (uint32_t e = tid; e < nt * 256u; e += 512u) {
+        for (uint32_t e = tid; e < nt * 256u; e += NT) {
             const uint32_t ti = e >> 8, cc = e & 15u, rr = (e >> 4) & 15u;
             const uint32_t tt = t0 + ti, rt = tt / CT, ct = tt % CT;
             const uint32_t ln = 16u * (rr >> 2) + cc, i = rr & 3u;

@@ -186,11 +186,10 @@ struct mfma_tiles {
 };
 
 constexpr uint32_t kMfmaThreads = 64 * gsk::kMfmaWaves;
-constexpr uint32_t kMfmaStageBytes = gsk::kMfmaNA * gsk::kMfmaWaves * 1024;
 
 size_t mfma_lds_bytes(uint32_t lgKC, uint32_t CT, uint32_t RMAX) {
     const size_t KC = 1ull << lgKC;
-    return 2 * KC * 32 * CT + 2 * (size_t)kMfmaStageBytes + 2 * (RMAX + 1) * (2 * KC + 32);
+    return 2 * KC * 32 * CT + 2 * (RMAX + 1) * (2 * KC + 32);
 }
 
 bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
@@ -226,7 +225,8 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
             for (uint64_t e = row_ptr[tb_rows[g]]; e < row_ptr[tb_rows[g + 1]]; e++) cnt[col[e] >> lg]++;
             for (uint64_t j = 0; j < nc; j++) gmax = std::max(gmax, (cnt[j] + 7) / 8);
         }
-        if (gmax * 32 > kMfmaStageBytes) continue;
+        if (gmax > (uint64_t)gsk::kMfmaMaxA * kMfmaThreads) continue;
+        if (((KC * 32 * CT) / 16) % kMfmaThreads) continue;  // whole B units per thread
         t.lgKC = lg; t.nc = (uint32_t)nc; t.RT = RT; t.RMAX = (uint32_t)rmax;
         t.lds_bytes = mfma_lds_bytes(lg, CT, (uint32_t)rmax);
         break;
@@ -260,7 +260,7 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
             t.seg_start.push_back((uint32_t)(t.groups.size() / 16));
         }
     }
-    t.groups.insert(t.groups.end(), kMfmaStageBytes / 2, 0);  // stage-sized tail: fixed-size DMA reads
+    t.groups.insert(t.groups.end(), 16, 0);  // spare group: idle lanes' branch-free loads
     return true;
 }
 
@@ -537,7 +537,7 @@ void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *
         }
     }
     hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux), dim3(kMfmaThreads), d.lds_bytes, s, a.t0, a.t1,
-                       (const unsigned char *)a.tcol, B, C, (uint32_t)p.K, N, d.nc, d.rpw_max, (uint32_t)d.row_base);
+                       (const gsk::u32x4 *)a.tcol, B, C, (uint32_t)p.K, N, d.nc, d.rpw_max, (uint32_t)d.row_base);
     HIP_OK(hipGetLastError());
 }
 
