@@ -643,8 +643,8 @@ __global__ __launch_bounds__(1024) void k_lds_rows(
 // BMTB row blocks on the matrix cores (MI355X layout of a tblock/warp/block-
 // total plan whose row blocks are dense enough).  Workgroup g owns BMTB g
 // (R <= RMAX <= 16*RT rows) and walks K in chunks of KC = 2^LGKC columns.
-// Loads run two chunks ahead in registers (two register sets, the loop is
-// unrolled by two so every set index is a compile-time constant); LDS holds
+// Loads run three chunks ahead in registers (three register sets, the loop is
+// unrolled by three so every set index is a compile-time constant); LDS holds
 // two buffer sets of
 //   B[b]: B[kc0 : kc0+KC, 0:N], row k at k*N*2 bytes, its 32-B pieces (16
 //         columns) permuted by b_piece() so the transposed operand reads
@@ -652,11 +652,11 @@ __global__ __launch_bounds__(1024) void k_lds_rows(
 //   D[b]: the row block's dense fp16 image, RMAX+1 rows of RS = 2*KC + 32 B
 //         (conflict-free ds_read_b128 operand reads); row R stays zero and
 //         stands in for every MFMA row >= R.
-// Iteration j (X = j&1): barrier; issue the global loads of chunk j+2 into
-// register set X (B rows, and the chunk's compressed entries: groups of 8,
+// Iteration j (X = j&1): barrier; issue the global loads of chunk j+3 into
+// register set j%3 (B rows, and the chunk's compressed entries: groups of 8,
 // [8 x u16 pos = row*KC + col][8 x f16 value]); clear D[X^1]; MFMA chunk j
 // (waves split its 32-wide k-steps, v_mfma_f32_16x16x32_f16, fp32
-// accumulators); barrier; chunk j+1 from register set X^1: B rows -> B[X^1],
+// accumulators); barrier; chunk j+1 from register set (j+1)%3: B rows -> B[X^1],
 // entries scattered into D[X^1] (ds_write_b16; padding entries write 0 to row
 // R).  Every load is an ordinary VGPR load, so hipcc's own counted vmcnt waits
 // keep the next chunks in flight across the barriers.  At the end the W
@@ -680,9 +680,9 @@ __device__ __forceinline__ uint32_t b_piece(uint32_t k, uint32_t p) {
     return p ^ (sw & (uint32_t)(CT - 1));
 }
 
-constexpr int kMfmaWaves = 8, kMfmaMaxA = 2;
+constexpr int kMfmaWaves = 8;
 
-template <int CT, int RT, int LGKC>
+template <int CT, int RT, int LGKC, int MAXA>
 __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
                                                    const uint32_t *__restrict__ seg_start,  // n_bmtb*nc+1 (groups)
                                                    const u32x4 *__restrict__ tA,  // 2 u32x4 per group (+1 spare)
@@ -695,7 +695,6 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
     constexpr uint32_t W = kMfmaWaves, NT = 64 * W;
     constexpr uint32_t szB = KC * RB;
     constexpr uint32_t NB = szB / 16 / NT;            // B units per thread per chunk
-    constexpr int MAXA = kMfmaMaxA;
     static_assert(szB % (16 * NT) == 0, "whole B units per thread");
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint32_t szD = (RMAX + 1) * RS;
@@ -704,6 +703,10 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
     const uint32_t g = blockIdx.x;
     const uint32_t r0 = bmtb_first_row[g], R = bmtb_first_row[g + 1] - r0;
     const u32x4 zero4 = {0u, 0u, 0u, 0u};
+    // this BMTB's segment starts, lane t holding chunk t's (nc <= 63, host-checked):
+    // read with readlane, no scalar-load round trip inside the loop
+    const uint32_t segv = seg_start[g * nc + min(lane, nc)];
+#define GS_SEG(j) __builtin_amdgcn_readlane(segv, (j))
 
     for (uint32_t u = tid; u < 2 * szD / 16u; u += NT) *reinterpret_cast<u32x4 *>(lds + oD + u * 16u) = zero4;
 
@@ -713,7 +716,7 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
 #pragma unroll
         for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
     uint32_t arow[RT];
-    u32x4 sB0[NB], sP0[MAXA], sV0[MAXA], sB1[NB], sP1[MAXA], sV1[MAXA];
+    u32x4 sB0[NB], sP0[MAXA], sV0[MAXA], sB1[NB], sP1[MAXA], sV1[MAXA], sB2[NB], sP2[MAXA], sV2[MAXA];
 
     // chunk j -> registers; chunks past the end and idle slots re-read valid
     // data (the spare group / the last chunk), so no load sits behind a branch
@@ -721,16 +724,15 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
     {                                                                                             \
         const uint32_t jj_ = min((uint32_t)(j), nc - 1u);                                         \
         const uint32_t kc0_ = jj_ * KC;                                                           \
-        _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                                     \
+        _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                    \
             const uint32_t u = tid + i * NT;                                                      \
             const uint32_t k = u / UB;                                                            \
             const uint32_t kk = kc0_ + k < K ? kc0_ + k : kc0_;                                   \
             SB[i] = *reinterpret_cast<const u32x4 *>(B + (size_t)kk * N + (u % UB) * 8u);         \
         }                                                                                         \
-        const uint32_t sidx_ = g * nc + jj_;                                                      \
-        const uint32_t s0_ = seg_start[sidx_];                                                    \
-        const uint32_t G_ = (uint32_t)(j) < nc ? seg_start[sidx_ + 1] - s0_ : 0u;                 \
-        _Pragma("unroll") for (int I = 0; I < MAXA; I++) {                                        \
+        const uint32_t s0_ = GS_SEG(jj_);                                                         \
+        const uint32_t G_ = (uint32_t)(j) < nc ? GS_SEG(jj_ + 1) - s0_ : 0u;                      \
+        _Pragma("unroll") for (int I = 0; I < MAXA; I++) {                       \
             const uint32_t q = tid + I * NT;                                                      \
             const size_t qq = (size_t)s0_ + (q < G_ ? q : 0u);                                    \
             SP[I] = tA[2 * qq];                                                                   \
@@ -741,17 +743,16 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
 #define GS_STORE(j, SB, SP, SV)                                                                     \
     {                                                                                             \
         unsigned char *lb_ = lds + ((j) & 1u) * szB;                                              \
-        _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                                     \
+        _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                   \
             const uint32_t u = tid + i * NT;                                                      \
             const uint32_t k = u / UB, s = u % UB;                                                \
             *reinterpret_cast<u32x4 *>(lb_ + k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u) = SB[i]; \
         }                                                                                         \
-        const uint32_t sidx_ = g * nc + (j);                                                      \
-        const uint32_t G_ = seg_start[sidx_ + 1] - seg_start[sidx_];                              \
+        const uint32_t G_ = GS_SEG((j) + 1) - GS_SEG(j);                                          \
         unsigned char *ld_ = lds + oD + ((j) & 1u) * szD;                                         \
         _Pragma("unroll") for (int I = 0; I < MAXA; I++) {                                        \
             const uint32_t q = tid + I * NT;                                                      \
-            if (q < G_) {                                                                         \
+            if (q < G_) {                                                                          \
                 _Pragma("unroll") for (int e = 0; e < 8; e++) {                                   \
                     const uint32_t pos = (SP[I][e >> 1] >> (16 * (e & 1))) & 0xffffu;             \
                     const uint16_t v = (uint16_t)((SV[I][e >> 1] >> (16 * (e & 1))) & 0xffffu);   \
@@ -788,8 +789,8 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
 #define GS_ITER(j, SBn, SPn, SVn, SBs, SPs, SVs)                                                    \
     {                                                                                             \
         __syncthreads();                                                                          \
-        GS_LOAD((j) + 2, SBn, SPn, SVn);                                                          \
-        if ((j) + 1 < nc)                                                                         \
+        GS_LOAD((j) + 3, SBn, SPn, SVn);                                                          \
+        if ((j) + 1 < nc)                                                                          \
             for (uint32_t u = tid; u < R * RS / 16u; u += NT)                                     \
                 *reinterpret_cast<u32x4 *>(lds + oD + (((j) + 1) & 1u) * szD + u * 16u) = zero4;  \
         GS_MFMA(j);                                                                               \
@@ -802,20 +803,26 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
         const uint32_t row = 16u * rt + (lane & 15u);
         arow[rt] = (row < R ? row : R) * RS;
     }
+    // three register sets: chunk c lives in set c%3 from its load (issued three
+    // iterations ahead) to its store
     GS_LOAD(0u, sB0, sP0, sV0);
     GS_LOAD(1u, sB1, sP1, sV1);
+    GS_LOAD(2u, sB2, sP2, sV2);
     __syncthreads();  // dense images cleared
     GS_STORE(0u, sB0, sP0, sV0);
     uint32_t j = 0;
-    for (; j + 1 < nc; j += 2) {
+    for (; j + 2 < nc; j += 3) {
         GS_ITER(j, sB0, sP0, sV0, sB1, sP1, sV1);
-        GS_ITER(j + 1, sB1, sP1, sV1, sB0, sP0, sV0);
+        GS_ITER(j + 1, sB1, sP1, sV1, sB2, sP2, sV2);
+        GS_ITER(j + 2, sB2, sP2, sV2, sB0, sP0, sV0);
     }
     if (j < nc) GS_ITER(j, sB0, sP0, sV0, sB1, sP1, sV1);
+    if (j + 1 < nc) GS_ITER(j + 1, sB1, sP1, sV1, sB2, sP2, sV2);
 #undef GS_ITER
 #undef GS_MFMA
 #undef GS_STORE
 #undef GS_LOAD
+#undef GS_SEG
     __syncthreads();
     // fixed-order reduction of the W partial tiles, TPP tiles per pass
     float *red = reinterpret_cast<float *>(lds);

@@ -4,6 +4,7 @@
 #include "../host/gs_plan.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -179,7 +180,7 @@ bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uin
 // [8 x u16 pos = local_row*KC + local_col][8 x f16 value]; the last group is
 // padded with (pos = R*KC, value 0), row R being the kernel's zero row.
 struct mfma_tiles {
-    uint32_t lgKC = 0, nc = 0, RT = 0, RMAX = 0;
+    uint32_t lgKC = 0, nc = 0, RT = 0, RMAX = 0, MAXA = 0;
     size_t lds_bytes = 0;
     std::vector<uint32_t> seg_start;  // in groups
     std::vector<uint16_t> groups;     // 16 u16 per group, + one stage buffer of padding
@@ -225,9 +226,10 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
             for (uint64_t e = row_ptr[tb_rows[g]]; e < row_ptr[tb_rows[g + 1]]; e++) cnt[col[e] >> lg]++;
             for (uint64_t j = 0; j < nc; j++) gmax = std::max(gmax, (cnt[j] + 7) / 8);
         }
-        if (gmax > (uint64_t)gsk::kMfmaMaxA * kMfmaThreads) continue;
+        if (gmax > 2ull * kMfmaThreads || nc > 63) continue;
         if (((KC * 32 * CT) / 16) % kMfmaThreads) continue;  // whole B units per thread
         t.lgKC = lg; t.nc = (uint32_t)nc; t.RT = RT; t.RMAX = (uint32_t)rmax;
+        t.MAXA = gmax <= kMfmaThreads ? 1 : 2;
         t.lds_bytes = mfma_lds_bytes(lg, CT, (uint32_t)rmax);
         break;
     }
@@ -320,6 +322,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
         d.mfma = true;
         d.lds_N = Nd;
         d.KC = 1u << t.lgKC; d.nc = t.nc; d.maxr = t.RT; d.rpw_max = t.RMAX; d.RSB = t.lgKC;
+        d.seg_cap = t.MAXA;
         d.waves = kMfmaThreads / 64; d.lds_bytes = t.lds_bytes;
         const size_t before = d.bytes_A;
         a.t0 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_row_indices", 0), "BMTB first_row_indices"));
@@ -520,11 +523,11 @@ void launch_lds(const plan_state &p, const device_arrays &a, const VT *B, VT *C,
 #undef GS_LDS_ARGS
 }
 
-template <int CT, int RT, int LGKC>
+template <int CT, int RT, int LGKC, int MAXA>
 void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N,
                    hipStream_t s) {
     const device_plan &d = p.dev;
-    auto kern = gsk::k_mfma_rows<CT, RT, LGKC>;
+    auto kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA>;
     static std::mutex mu;
     static std::map<int, size_t> granted;
     {
@@ -544,10 +547,11 @@ void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *
 template <int CT, int RT>
 void launch_mfma_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N,
                     hipStream_t s) {
-    switch (p.dev.RSB) {  // log2 KC
-        case 10: launch_mfma_k<CT, RT, 10>(p, a, B, C, N, s); break;
-        case 9: launch_mfma_k<CT, RT, 9>(p, a, B, C, N, s); break;
-        default: launch_mfma_k<CT, RT, 8>(p, a, B, C, N, s); break;
+    const bool two = p.dev.seg_cap > 1;  // entry groups per thread per chunk
+    switch (p.dev.RSB) {                  // log2 KC
+        case 10: two ? launch_mfma_k<CT, RT, 10, 2>(p, a, B, C, N, s) : launch_mfma_k<CT, RT, 10, 1>(p, a, B, C, N, s); break;
+        case 9: two ? launch_mfma_k<CT, RT, 9, 2>(p, a, B, C, N, s) : launch_mfma_k<CT, RT, 9, 1>(p, a, B, C, N, s); break;
+        default: two ? launch_mfma_k<CT, RT, 8, 2>(p, a, B, C, N, s) : launch_mfma_k<CT, RT, 8, 1>(p, a, B, C, N, s); break;
     }
 }
 
