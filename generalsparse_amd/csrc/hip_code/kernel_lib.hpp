@@ -682,12 +682,15 @@ __device__ __forceinline__ uint32_t b_piece(uint32_t k, uint32_t p) {
 
 constexpr int kMfmaWaves = 8;
 
-template <int CT, int RT, int LGKC, int MAXA>
+// STAMPS (diagnostic build only, gs_debug_mfma_timeline): wave 0 of every
+// workgroup records s_memtime at phase boundaries into stamps[g*64 + i]
+template <int CT, int RT, int LGKC, int MAXA, bool STAMPS = false>
 __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
                                                    const uint32_t *__restrict__ seg_start,  // n_bmtb*nc+1 (groups)
                                                    const u32x4 *__restrict__ tA,  // 2 u32x4 per group (+1 spare)
                                                    const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K,
-                                                   uint32_t N, uint32_t nc, uint32_t RMAX, uint32_t row_base) {
+                                                   uint32_t N, uint32_t nc, uint32_t RMAX, uint32_t row_base,
+                                                   uint64_t *__restrict__ stamps = nullptr) {
     constexpr uint32_t KC = 1u << LGKC;
     constexpr uint32_t RB = 32 * CT;                  // bytes per B row (N == 16*CT)
     constexpr uint32_t UB = 2 * CT;                   // 16-B units per B row
@@ -707,6 +710,12 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
     // read with readlane, no scalar-load round trip inside the loop
     const uint32_t segv = seg_start[g * nc + min(lane, nc)];
 #define GS_SEG(j) __builtin_amdgcn_readlane(segv, (j))
+    uint64_t *lst = reinterpret_cast<uint64_t *>(lds + 2 * szB + 2 * szD);  // STAMPS only
+#define GS_STAMP(i)                                                          \
+    if constexpr (STAMPS) {                                                  \
+        if (tid == 0 && (i) < 64u) lst[(i)] = __builtin_amdgcn_s_memtime();  \
+    }
+    GS_STAMP(0u);
 
     for (uint32_t u = tid; u < 2 * szD / 16u; u += NT) *reinterpret_cast<u32x4 *>(lds + oD + u * 16u) = zero4;
 
@@ -789,13 +798,18 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
 #define GS_ITER(j, SBn, SPn, SVn, SBs, SPs, SVs)                                                    \
     {                                                                                             \
         __syncthreads();                                                                          \
+        GS_STAMP(4u + 5u * (j));                                                                  \
         GS_LOAD((j) + 3, SBn, SPn, SVn);                                                          \
         if ((j) + 1 < nc)                                                                          \
             for (uint32_t u = tid; u < R * RS / 16u; u += NT)                                     \
                 *reinterpret_cast<u32x4 *>(lds + oD + (((j) + 1) & 1u) * szD + u * 16u) = zero4;  \
+        GS_STAMP(5u + 5u * (j));                                                                  \
         GS_MFMA(j);                                                                               \
+        GS_STAMP(6u + 5u * (j));                                                                  \
         __syncthreads();                                                                          \
+        GS_STAMP(7u + 5u * (j));                                                                  \
         if ((j) + 1 < nc) GS_STORE((j) + 1, SBs, SPs, SVs);                                       \
+        GS_STAMP(8u + 5u * (j));                                                                  \
     }
 
 #pragma unroll
@@ -808,8 +822,11 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
     GS_LOAD(0u, sB0, sP0, sV0);
     GS_LOAD(1u, sB1, sP1, sV1);
     GS_LOAD(2u, sB2, sP2, sV2);
+    GS_STAMP(1u);
     __syncthreads();  // dense images cleared
+    GS_STAMP(2u);
     GS_STORE(0u, sB0, sP0, sV0);
+    GS_STAMP(3u);
     uint32_t j = 0;
     for (; j + 2 < nc; j += 3) {
         GS_ITER(j, sB0, sP0, sV0, sB1, sP1, sV1);
@@ -850,6 +867,13 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
         }
         __syncthreads();
     }
+    if constexpr (STAMPS) {
+        if (tid == 0) {
+            lst[63] = __builtin_amdgcn_s_memtime();
+            for (uint32_t i = 0; i < 64; i++) stamps[(size_t)g * 64 + i] = lst[i];
+        }
+    }
+#undef GS_STAMP
 }
 
 }  // namespace gsk

@@ -239,6 +239,14 @@ int gs_spmm(gs_plan_t *p, const void *B, void *C, int N, gs_stream_t stream) {
     return gs_spmm_replica(p, 0, B, C, N, stream);
 }
 
+int gs_debug_mfma_timeline(gs_plan_t *p, const void *B, void *C, int N, gs_stream_t stream, uint64_t *stamps,
+                           uint64_t n_stamps) {
+    return guard([&] {
+        GS_CHECK(p && B && C && stamps, "null argument");
+        gs::debug_mfma_timeline(p->st, B, C, (uint32_t)N, (hipStream_t)stream, stamps, n_stamps);
+    });
+}
+
 int gs_plan_info_get(gs_plan_t *p, gs_plan_info *info) {
     return guard([&] {
         GS_CHECK(p && info, "null argument");

@@ -55,5 +55,7 @@ void upload_plan(plan_state &p, int dtype, int device);
 void add_replica(plan_state &p);
 void free_device(plan_state &p);
 void launch_spmm(const plan_state &p, int replica, const void *B, void *C, uint32_t N, hipStream_t stream);
+void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
+                         size_t n_host);
 
 }  // namespace gs

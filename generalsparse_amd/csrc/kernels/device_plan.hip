@@ -540,7 +540,8 @@ void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *
         }
     }
     hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux), dim3(kMfmaThreads), d.lds_bytes, s, a.t0, a.t1,
-                       (const gsk::u32x4 *)a.tcol, B, C, (uint32_t)p.K, N, d.nc, d.rpw_max, (uint32_t)d.row_base);
+                       (const gsk::u32x4 *)a.tcol, B, C, (uint32_t)p.K, N, d.nc, d.rpw_max, (uint32_t)d.row_base,
+                       (uint64_t *)nullptr);
     HIP_OK(hipGetLastError());
 }
 
@@ -564,6 +565,33 @@ void launch_mfma_ct(const plan_state &p, const device_arrays &a, const gsk::f16 
         default: launch_mfma_rt<CT, 4>(p, a, B, C, N, s); break;
     }
 }
+
+}  // namespace
+
+// diagnostic: C2-shaped plans only (CT 2, RT 2, KC 512, one entry group per thread)
+void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
+                         size_t n_host) {
+    const device_plan &d = p.dev;
+    GS_CHECK(p.uploaded && d.mfma && N == d.lds_N && N == 32 && d.maxr == 2 && d.RSB == 9 && d.seg_cap == 1,
+             "timeline build exists for C2-shaped matrix-core plans only");
+    const device_arrays &a = d.replicas[0];
+    auto kern = gsk::k_mfma_rows<2, 2, 9, 1, true>;
+    const size_t lds = d.lds_bytes + 64 * 8;
+    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds));
+    uint64_t *dst = nullptr;
+    const size_t n = (size_t)d.n_rows_aux * 64;
+    HIP_OK(hipMalloc(&dst, n * 8));
+    hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux), dim3(kMfmaThreads), lds, s, a.t0, a.t1,
+                       (const gsk::u32x4 *)a.tcol, (const gsk::f16 *)B, (gsk::f16 *)C, (uint32_t)p.K, N, d.nc,
+                       d.rpw_max, (uint32_t)d.row_base, dst);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(s));
+    HIP_OK(hipMemcpy(host, dst, std::min(n, n_host) * 8, hipMemcpyDeviceToHost));
+    (void)hipFree(dst);
+}
+
+namespace {
 
 void launch_mfma(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
     const gsk::f16 *b = (const gsk::f16 *)B;

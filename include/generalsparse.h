@@ -102,6 +102,13 @@ int gs_plan_array_read_u64(gs_plan_t *p, const char *key, uint64_t *out, uint64_
 int gs_plan_array_read_f64(gs_plan_t *p, const char *key, double *out, uint64_t n);
 int gs_plan_log(gs_plan_t *p, char *buf, int buf_len); /* operator / transform history */
 
+/* diagnostics (not part of the reference surface): one launch of the matrix-core
+ * kernel's timestamped build; stamps[g*64 + i] = s_memtime of phase i in workgroup g
+ * (0 start, 1 loads issued, 2 first barrier, 3 first chunk staged, 4+5j.. per chunk j:
+ * top barrier, loads+clear issued, MFMA done, mid barrier, next chunk staged; 63 end) */
+int gs_debug_mfma_timeline(gs_plan_t *p, const void *B, void *C, int N, gs_stream_t stream, uint64_t *stamps,
+                           uint64_t n_stamps);
+
 /* one call: read + pipeline + compile + upload */
 int gs_plan_from_mtx(const char *path, const gs_opts *opts, gs_plan_t **out);
 void gs_plan_free(gs_plan_t *p);
