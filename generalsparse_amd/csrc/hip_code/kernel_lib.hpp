@@ -643,27 +643,25 @@ __global__ __launch_bounds__(1024) void k_lds_rows(
 // BMTB row blocks on the matrix cores (MI355X layout of a tblock/warp/block-
 // total plan whose row blocks are dense enough).  Workgroup g owns BMTB g
 // (R <= RMAX <= 16*RT rows) and walks K in chunks of KC = 2^LGKC columns.
-// Loads run three chunks ahead in registers (three register sets, the loop is
-// unrolled by three so every set index is a compile-time constant); LDS holds
-// two buffer sets of
-//   B[b]: B[kc0 : kc0+KC, 0:N], row k at k*N*2 bytes, its 32-B pieces (16
-//         columns) permuted by b_piece() so the transposed operand reads
-//         (ds_read_b64_tr_b16) are conflict-free;
-//   D[b]: the row block's dense fp16 image, RMAX+1 rows of RS = 2*KC + 32 B
-//         (conflict-free ds_read_b128 operand reads); row R stays zero and
-//         stands in for every MFMA row >= R.
-// Iteration j (X = j&1): barrier; issue the global loads of chunk j+3 into
-// register set j%3 (B rows, and the chunk's compressed entries: groups of 8,
-// [8 x u16 pos = row*KC + col][8 x f16 value]); clear D[X^1]; MFMA chunk j
-// (waves split its 32-wide k-steps, v_mfma_f32_16x16x32_f16, fp32
-// accumulators); barrier; chunk j+1 from register set (j+1)%3: B rows -> B[X^1],
-// entries scattered into D[X^1] (ds_write_b16; padding entries write 0 to row
-// R).  Every load is an ordinary VGPR load, so hipcc's own counted vmcnt waits
-// keep the next chunks in flight across the barriers.  At the end the W
-// per-wave partial tiles are summed in a fixed order through LDS
-// (deterministic) and rows < R are stored.  A zero of the dense image times a
-// non-finite B value gives NaN: the kernel multiplies the row block's whole
-// tile.
+// The 8 waves are specialised, one of each kind per SIMD:
+//   compute waves 0-3: v_mfma_f32_16x16x32_f16 over chunk j (A rows by
+//     ds_read_b128 from the dense image, B by ds_read_b64_tr_b16, fp32
+//     accumulators), then clear the dense image of chunk j+2;
+//   loader waves 4-7: global loads of chunk j+3 into registers (three register
+//     sets, the loop is unrolled by three so every set index is a compile-time
+//     constant), then chunk j+1 from registers into LDS: B rows and the
+//     scatter of its compressed entries (groups of 8, [8 x u16 pos = row*KC +
+//     col][8 x f16 value]; padding entries write 0 to row R) into its image.
+// One barrier per chunk separates the roles' buffers: LDS holds two B buffers
+// (row k at k*N*2 bytes, 32-B pieces permuted by b_piece() so the transposed
+// reads are conflict-free) and three dense images (RMAX+1 rows of RS = 2*KC+32
+// bytes, conflict-free ds_read_b128; row R stays zero and stands in for every
+// MFMA row >= R), so loading, staging, clearing and the matrix cores overlap.
+// Every load is an ordinary VGPR load: hipcc's own counted vmcnt waits keep
+// three chunks in flight.  At the end the compute waves' partial tiles are
+// summed in a fixed order through LDS (deterministic) and rows < R are stored.
+// A zero of the dense image times a non-finite B value gives NaN: the kernel
+// multiplies the row block's whole tile.
 // ---------------------------------------------------------------------------
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef short s4v __attribute__((ext_vector_type(4)));
@@ -680,10 +678,10 @@ __device__ __forceinline__ uint32_t b_piece(uint32_t k, uint32_t p) {
     return p ^ (sw & (uint32_t)(CT - 1));
 }
 
-constexpr int kMfmaWaves = 8;
+constexpr int kMfmaWaves = 8, kMfmaCompute = 4;  // compute waves 0..3, loader waves 4..7
 
-// STAMPS (diagnostic build only, gs_debug_mfma_timeline): wave 0 of every
-// workgroup records s_memtime at phase boundaries into stamps[g*64 + i]
+// STAMPS (diagnostic build only, gs_debug_mfma_timeline): the first loader and
+// compute lanes of every workgroup record s_memtime at phase boundaries
 template <int CT, int RT, int LGKC, int MAXA, bool STAMPS = false>
 __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
                                                    const uint32_t *__restrict__ seg_start,  // n_bmtb*nc+1 (groups)
@@ -695,29 +693,32 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
     constexpr uint32_t RB = 32 * CT;                  // bytes per B row (N == 16*CT)
     constexpr uint32_t UB = 2 * CT;                   // 16-B units per B row
     constexpr uint32_t RS = 2 * KC + 32;              // dense image row stride
-    constexpr uint32_t W = kMfmaWaves, NT = 64 * W;
+    constexpr uint32_t NT = 64 * kMfmaWaves;
+    constexpr uint32_t WC = kMfmaCompute, NL = NT - 64 * WC;  // compute waves, loader threads
     constexpr uint32_t szB = KC * RB;
-    constexpr uint32_t NB = szB / 16 / NT;            // B units per thread per chunk
-    static_assert(szB % (16 * NT) == 0, "whole B units per thread");
+    constexpr uint32_t NB = szB / 16 / NL;            // B units per loader thread per chunk
+    static_assert(szB % (16 * NL) == 0, "whole B units per loader thread");
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint32_t szD = (RMAX + 1) * RS;
-    const uint32_t oD = 2 * szB;
+    const uint32_t oD = 2 * szB;                      // D[0..2] follow B[0..1]
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const bool loader = wv >= WC;                     // wave-uniform role
+    const uint32_t lt = tid - 64 * WC;                // loader thread index
     const uint32_t g = blockIdx.x;
     const uint32_t r0 = bmtb_first_row[g], R = bmtb_first_row[g + 1] - r0;
     const u32x4 zero4 = {0u, 0u, 0u, 0u};
-    // this BMTB's segment starts, lane t holding chunk t's (nc <= 63, host-checked):
-    // read with readlane, no scalar-load round trip inside the loop
+    // this BMTB's segment starts, lane t holding chunk t's (nc <= 63, host-checked)
     const uint32_t segv = seg_start[g * nc + min(lane, nc)];
 #define GS_SEG(j) __builtin_amdgcn_readlane(segv, (j))
-    uint64_t *lst = reinterpret_cast<uint64_t *>(lds + 2 * szB + 2 * szD);  // STAMPS only
-#define GS_STAMP(i)                                                          \
-    if constexpr (STAMPS) {                                                  \
-        if (tid == 0 && (i) < 64u) lst[(i)] = __builtin_amdgcn_s_memtime();  \
+    uint64_t *lst = reinterpret_cast<uint64_t *>(lds + oD + 3 * szD);  // STAMPS only
+#define GS_STAMP(i)                                                                         \
+    if constexpr (STAMPS) {                                                                 \
+        if ((tid == 0 || tid == 64 * WC) && (i) < 32u) lst[(i) + (tid ? 32u : 0u)] =        \
+            __builtin_amdgcn_s_memtime();                                                   \
     }
     GS_STAMP(0u);
 
-    for (uint32_t u = tid; u < 2 * szD / 16u; u += NT) *reinterpret_cast<u32x4 *>(lds + oD + u * 16u) = zero4;
+    for (uint32_t u = tid; u < 3 * szD / 16u; u += NT) *reinterpret_cast<u32x4 *>(lds + oD + u * 16u) = zero4;
 
     f4v acc[RT][CT];
 #pragma unroll
@@ -725,43 +726,48 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
 #pragma unroll
         for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
     uint32_t arow[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++) {
+        const uint32_t row = 16u * rt + (lane & 15u);
+        arow[rt] = (row < R ? row : R) * RS;
+    }
     u32x4 sB0[NB], sP0[MAXA], sV0[MAXA], sB1[NB], sP1[MAXA], sV1[MAXA], sB2[NB], sP2[MAXA], sV2[MAXA];
 
-    // chunk j -> registers; chunks past the end and idle slots re-read valid
-    // data (the spare group / the last chunk), so no load sits behind a branch
+    // loader: chunk j -> registers; chunks past the end and idle slots re-read
+    // valid data (the last chunk / the spare group), so no load sits behind a branch
 #define GS_LOAD(j, SB, SP, SV)                                                                      \
     {                                                                                             \
         const uint32_t jj_ = min((uint32_t)(j), nc - 1u);                                         \
         const uint32_t kc0_ = jj_ * KC;                                                           \
-        _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                    \
-            const uint32_t u = tid + i * NT;                                                      \
+        _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                                     \
+            const uint32_t u = lt + i * NL;                                                       \
             const uint32_t k = u / UB;                                                            \
             const uint32_t kk = kc0_ + k < K ? kc0_ + k : kc0_;                                   \
             SB[i] = *reinterpret_cast<const u32x4 *>(B + (size_t)kk * N + (u % UB) * 8u);         \
         }                                                                                         \
         const uint32_t s0_ = GS_SEG(jj_);                                                         \
         const uint32_t G_ = (uint32_t)(j) < nc ? GS_SEG(jj_ + 1) - s0_ : 0u;                      \
-        _Pragma("unroll") for (int I = 0; I < MAXA; I++) {                       \
-            const uint32_t q = tid + I * NT;                                                      \
+        _Pragma("unroll") for (int I = 0; I < MAXA; I++) {                                        \
+            const uint32_t q = lt + I * NL;                                                       \
             const size_t qq = (size_t)s0_ + (q < G_ ? q : 0u);                                    \
             SP[I] = tA[2 * qq];                                                                   \
             SV[I] = tA[2 * qq + 1];                                                               \
         }                                                                                         \
     }
-    // registers of chunk j -> B[j&1] rows and D[j&1] entries
+    // loader: registers of chunk j -> B[j&1] rows and D[j%3] entries
 #define GS_STORE(j, SB, SP, SV)                                                                     \
     {                                                                                             \
         unsigned char *lb_ = lds + ((j) & 1u) * szB;                                              \
-        _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                   \
-            const uint32_t u = tid + i * NT;                                                      \
+        _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                                     \
+            const uint32_t u = lt + i * NL;                                                       \
             const uint32_t k = u / UB, s = u % UB;                                                \
             *reinterpret_cast<u32x4 *>(lb_ + k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u) = SB[i]; \
         }                                                                                         \
         const uint32_t G_ = GS_SEG((j) + 1) - GS_SEG(j);                                          \
-        unsigned char *ld_ = lds + oD + ((j) & 1u) * szD;                                         \
+        unsigned char *ld_ = lds + oD + ((j) % 3u) * szD;                                         \
         _Pragma("unroll") for (int I = 0; I < MAXA; I++) {                                        \
-            const uint32_t q = tid + I * NT;                                                      \
-            if (q < G_) {                                                                          \
+            const uint32_t q = lt + I * NL;                                                       \
+            if (q < G_) {                                                                         \
                 _Pragma("unroll") for (int e = 0; e < 8; e++) {                                   \
                     const uint32_t pos = (SP[I][e >> 1] >> (16 * (e & 1))) & 0xffffu;             \
                     const uint16_t v = (uint16_t)((SV[I][e >> 1] >> (16 * (e & 1))) & 0xffffu);   \
@@ -770,13 +776,14 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
             }                                                                                     \
         }                                                                                         \
     }
+    // compute: chunk j on the matrix cores, then clear D[(j+2)%3]
 #define GS_MFMA(j)                                                                                  \
     {                                                                                             \
         const uint32_t kr_ = min(KC, K - (j) * KC);                                               \
         const uint32_t nsteps_ = (kr_ + 31u) / 32u;                                               \
-        const unsigned char *la_ = lds + oD + ((j) & 1u) * szD;                                   \
+        const unsigned char *la_ = lds + oD + ((j) % 3u) * szD;                                   \
         const unsigned char *lb_ = lds + ((j) & 1u) * szB;                                        \
-        for (uint32_t st = wv; st < nsteps_; st += W) {                                           \
+        for (uint32_t st = wv; st < nsteps_; st += WC) {                                          \
             const uint32_t kb = st * 32u + 8u * (lane >> 4);                                      \
             h8v av[RT];                                                                           \
             _Pragma("unroll") for (int rt = 0; rt < RT; rt++) av[rt] =                            \
@@ -794,65 +801,65 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
                     __builtin_amdgcn_mfma_f32_16x16x32_f16(av[rt], bv, acc[rt][ct], 0, 0, 0);     \
             }                                                                                     \
         }                                                                                         \
+        if ((j) + 2 < nc)                                                                         \
+            for (uint32_t u = tid; u < R * RS / 16u; u += 64u * WC)                               \
+                *reinterpret_cast<u32x4 *>(lds + oD + (((j) + 2) % 3u) * szD + u * 16u) = zero4;  \
     }
+    // The roles run separate loops (one barrier per chunk in each), so hipcc's
+    // vmcnt analysis sees only the loader's loads in the loader loop.
+    if (loader) {
+        // chunk j: fetch j+3 into set j%3, stage j+1 from set (j+1)%3
 #define GS_ITER(j, SBn, SPn, SVn, SBs, SPs, SVs)                                                    \
     {                                                                                             \
-        __syncthreads();                                                                          \
-        GS_STAMP(4u + 5u * (j));                                                                  \
         GS_LOAD((j) + 3, SBn, SPn, SVn);                                                          \
-        if ((j) + 1 < nc)                                                                          \
-            for (uint32_t u = tid; u < R * RS / 16u; u += NT)                                     \
-                *reinterpret_cast<u32x4 *>(lds + oD + (((j) + 1) & 1u) * szD + u * 16u) = zero4;  \
-        GS_STAMP(5u + 5u * (j));                                                                  \
-        GS_MFMA(j);                                                                               \
-        GS_STAMP(6u + 5u * (j));                                                                  \
-        __syncthreads();                                                                          \
-        GS_STAMP(7u + 5u * (j));                                                                  \
         if ((j) + 1 < nc) GS_STORE((j) + 1, SBs, SPs, SVs);                                       \
-        GS_STAMP(8u + 5u * (j));                                                                  \
+        GS_STAMP(2u + (j));                                                                       \
+        __syncthreads();                                                                          \
     }
-
-#pragma unroll
-    for (int rt = 0; rt < RT; rt++) {
-        const uint32_t row = 16u * rt + (lane & 15u);
-        arow[rt] = (row < R ? row : R) * RS;
-    }
-    // three register sets: chunk c lives in set c%3 from its load (issued three
-    // iterations ahead) to its store
-    GS_LOAD(0u, sB0, sP0, sV0);
-    GS_LOAD(1u, sB1, sP1, sV1);
-    GS_LOAD(2u, sB2, sP2, sV2);
-    GS_STAMP(1u);
-    __syncthreads();  // dense images cleared
-    GS_STAMP(2u);
-    GS_STORE(0u, sB0, sP0, sV0);
-    GS_STAMP(3u);
-    uint32_t j = 0;
-    for (; j + 2 < nc; j += 3) {
-        GS_ITER(j, sB0, sP0, sV0, sB1, sP1, sV1);
-        GS_ITER(j + 1, sB1, sP1, sV1, sB2, sP2, sV2);
-        GS_ITER(j + 2, sB2, sP2, sV2, sB0, sP0, sV0);
-    }
-    if (j < nc) GS_ITER(j, sB0, sP0, sV0, sB1, sP1, sV1);
-    if (j + 1 < nc) GS_ITER(j + 1, sB1, sP1, sV1, sB2, sP2, sV2);
+        GS_LOAD(0u, sB0, sP0, sV0);
+        GS_LOAD(1u, sB1, sP1, sV1);
+        GS_LOAD(2u, sB2, sP2, sV2);
+        __syncthreads();  // dense images cleared
+        GS_STORE(0u, sB0, sP0, sV0);
+        GS_STAMP(1u);
+        __syncthreads();  // chunk 0 staged
+        uint32_t j = 0;
+        for (; j + 2 < nc; j += 3) {
+            GS_ITER(j, sB0, sP0, sV0, sB1, sP1, sV1);
+            GS_ITER(j + 1, sB1, sP1, sV1, sB2, sP2, sV2);
+            GS_ITER(j + 2, sB2, sP2, sV2, sB0, sP0, sV0);
+        }
+        if (j < nc) GS_ITER(j, sB0, sP0, sV0, sB1, sP1, sV1);
+        if (j + 1 < nc) GS_ITER(j + 1, sB1, sP1, sV1, sB2, sP2, sV2);
 #undef GS_ITER
+    } else {
+        __syncthreads();  // dense images cleared
+        GS_STAMP(1u);
+        __syncthreads();  // chunk 0 staged
+        for (uint32_t j = 0; j < nc; j++) {
+            GS_MFMA(j);
+            GS_STAMP(2u + j);
+            __syncthreads();
+        }
+    }
 #undef GS_MFMA
 #undef GS_STORE
 #undef GS_LOAD
 #undef GS_SEG
-    __syncthreads();
-    // fixed-order reduction of the W partial tiles, TPP tiles per pass
+    // fixed-order reduction of the compute waves' partial tiles, TPP tiles per pass
     float *red = reinterpret_cast<float *>(lds);
-    const uint32_t TPP = min((uint32_t)(RT * CT), (oD + 2 * szD) / (W * 1024u));
+    const uint32_t TPP = min((uint32_t)(RT * CT), (oD + 3 * szD) / (WC * 1024u));
     for (uint32_t t0 = 0; t0 < RT * CT; t0 += TPP) {
+        if (!loader) {
 #pragma unroll
-        for (int rt = 0; rt < RT; rt++)
+            for (int rt = 0; rt < RT; rt++)
 #pragma unroll
-            for (int ct = 0; ct < CT; ct++) {
-                const uint32_t tt = rt * CT + ct;
-                if (tt >= t0 && tt < t0 + TPP)
-                    *reinterpret_cast<f4v *>(red + ((wv * TPP + (tt - t0)) * 64u + lane) * 4u) = acc[rt][ct];
-            }
+                for (int ct = 0; ct < CT; ct++) {
+                    const uint32_t tt = rt * CT + ct;
+                    if (tt >= t0 && tt < t0 + TPP)
+                        *reinterpret_cast<f4v *>(red + ((wv * TPP + (tt - t0)) * 64u + lane) * 4u) = acc[rt][ct];
+                }
+        }
         __syncthreads();
         const uint32_t nt = min(TPP, RT * CT - t0);
         for (uint32_t e = tid; e < nt * 256u; e += NT) {
@@ -861,7 +868,7 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
             const uint32_t ln = 16u * (rr >> 2) + cc, i = rr & 3u;
             float sum = 0.f;
 #pragma unroll
-            for (uint32_t w = 0; w < W; w++) sum += red[((w * TPP + ti) * 64u + ln) * 4u + i];
+            for (uint32_t w = 0; w < WC; w++) sum += red[((w * TPP + ti) * 64u + ln) * 4u + i];
             const uint32_t row = 16u * rt + rr;
             if (row < R) C[(size_t)(row_base + r0 + row) * N + 16u * ct + cc] = (f16)sum;
         }
@@ -869,7 +876,7 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
     }
     if constexpr (STAMPS) {
         if (tid == 0) {
-            lst[63] = __builtin_amdgcn_s_memtime();
+            lst[31] = __builtin_amdgcn_s_memtime();
             for (uint32_t i = 0; i < 64; i++) stamps[(size_t)g * 64 + i] = lst[i];
         }
     }

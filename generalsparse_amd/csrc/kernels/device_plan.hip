@@ -188,9 +188,11 @@ struct mfma_tiles {
 
 constexpr uint32_t kMfmaThreads = 64 * gsk::kMfmaWaves;
 
+constexpr uint32_t kMfmaLoaders = kMfmaThreads - 64 * gsk::kMfmaCompute;
+
 size_t mfma_lds_bytes(uint32_t lgKC, uint32_t CT, uint32_t RMAX) {
     const size_t KC = 1ull << lgKC;
-    return 2 * KC * 32 * CT + 2 * (RMAX + 1) * (2 * KC + 32);
+    return 2 * KC * 32 * CT + 3 * (RMAX + 1) * (2 * KC + 32);
 }
 
 bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
@@ -226,10 +228,11 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
             for (uint64_t e = row_ptr[tb_rows[g]]; e < row_ptr[tb_rows[g + 1]]; e++) cnt[col[e] >> lg]++;
             for (uint64_t j = 0; j < nc; j++) gmax = std::max(gmax, (cnt[j] + 7) / 8);
         }
-        if (gmax > 2ull * kMfmaThreads || nc > 63) continue;
-        if (((KC * 32 * CT) / 16) % kMfmaThreads) continue;  // whole B units per thread
+        if (gmax > 2ull * kMfmaLoaders || nc > 63) continue;
+        if (((KC * 32 * CT) / 16) % kMfmaLoaders) continue;  // whole B units per loader thread
+        if ((KC * 32 * CT) / 16 / kMfmaLoaders > 8) continue;  // register budget of the loader sets
         t.lgKC = lg; t.nc = (uint32_t)nc; t.RT = RT; t.RMAX = (uint32_t)rmax;
-        t.MAXA = gmax <= kMfmaThreads ? 1 : 2;
+        t.MAXA = gmax <= kMfmaLoaders ? 1 : 2;
         t.lds_bytes = mfma_lds_bytes(lg, CT, (uint32_t)rmax);
         break;
     }
@@ -576,7 +579,7 @@ void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N
              "timeline build exists for C2-shaped matrix-core plans only");
     const device_arrays &a = d.replicas[0];
     auto kern = gsk::k_mfma_rows<2, 2, 9, 1, true>;
-    const size_t lds = d.lds_bytes + 64 * 8;
+    const size_t lds = d.lds_bytes + 64 * 8;  // + the stamp slots
     HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));
     uint64_t *dst = nullptr;

@@ -22,7 +22,7 @@ info = plan.info()
 B = torch.randn((K, N), device="cuda", dtype=torch.float16)
 C = torch.empty((M, N), device="cuda", dtype=torch.float16)
 for _ in range(20):
-    plan.spmm(B, out=C) if "out" in plan.spmm.__code__.co_varnames else plan.spmm(B)
+    plan.spmm(B)
 torch.cuda.synchronize()
 L = _lib.load()
 nb = int(M / 20)
@@ -31,13 +31,13 @@ _lib.check(L.gs_debug_mfma_timeline(plan._h, ctypes.c_void_p(B.data_ptr()), ctyp
                                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream), st, nb * 64))
 a = np.frombuffer(st, dtype=np.uint64).reshape(nb, 64).astype(np.int64)
 nc = info["lds_chunks"]
-idx = [0, 1, 2, 3] + [4 + 5 * j + p for j in range(nc) for p in range(5)] + [63]
-names = ["start", "loads0-2", "barrier0", "stage0"] + [f"c{j}.{p}" for j in range(nc)
-                                                       for p in ("top", "ld+clr", "mfma", "mid", "stage")] + ["end"]
-rel = a[:, idx] - a[:, [0]]
-d = np.diff(rel, axis=1)
-med = np.median(d, axis=0)
-out = {"total_med": float(np.median(rel[:, -1])), "total_max": float(rel[:, -1].max()),
-       "start_spread": float(a[:, 0].max() - a[:, 0].min()),
-       "phases": {names[i + 1]: float(med[i]) for i in range(len(med))}}
+t0 = a[:, [0]]
+out = {"total_med": float(np.median(a[:, 31] - a[:, 0])), "total_max": float((a[:, 31] - a[:, 0]).max())}
+# slot layout (kernel_lib.hpp k_mfma_rows STAMPS): compute lane 0 in 0..31, loader lane 0 in 32..63;
+# 0 start, 1 first barrier side (loader: chunk 0 staged), 2+j chunk j's work done (before its barrier), 31 end
+for name, base in (("compute", 0), ("loader", 32)):
+    idx = [base + 1] + [base + 2 + j for j in range(nc)]
+    rel = a[:, idx] - t0
+    out[name + "_med_done_at"] = [float(x) for x in np.median(rel, axis=0)]
+# barrier-to-barrier chunk period: compute stamp j+1 minus j
 print(json.dumps(out))
