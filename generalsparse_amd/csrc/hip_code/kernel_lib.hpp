@@ -643,11 +643,11 @@ __global__ __launch_bounds__(1024) void k_lds_rows(
 // BMTB row blocks on the matrix cores (MI355X layout of a tblock/warp/block-
 // total plan whose row blocks are dense enough).  Workgroup g owns BMTB g
 // (R <= RMAX <= 16*RT rows) and walks K in chunks of KC = 2^LGKC columns.
-// The 8 waves are specialised, one of each kind per SIMD:
+// The 12 waves are specialised (one compute and two loader waves per SIMD):
 //   compute waves 0-3: v_mfma_f32_16x16x32_f16 over chunk j (A rows by
 //     ds_read_b128 from the dense image, B by ds_read_b64_tr_b16, fp32
 //     accumulators), then clear the dense image of chunk j+2;
-//   loader waves 4-7: global loads of chunk j+3 into registers (three register
+//   loader waves 4-11: global loads of chunk j+3 into registers (three register
 //     sets, the loop is unrolled by three so every set index is a compile-time
 //     constant), then chunk j+1 from registers into LDS: B rows and the
 //     scatter of its compressed entries (groups of 8, [8 x u16 pos = row*KC +
@@ -678,12 +678,12 @@ __device__ __forceinline__ uint32_t b_piece(uint32_t k, uint32_t p) {
     return p ^ (sw & (uint32_t)(CT - 1));
 }
 
-constexpr int kMfmaWaves = 8, kMfmaCompute = 4;  // compute waves 0..3, loader waves 4..7
+constexpr int kMfmaWaves = 12, kMfmaCompute = 4;  // compute waves 0..3, loader waves 4..11
 
 // STAMPS (diagnostic build only, gs_debug_mfma_timeline): the first loader and
 // compute lanes of every workgroup record s_memtime at phase boundaries
 template <int CT, int RT, int LGKC, int MAXA, bool STAMPS = false>
-__global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
+__global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
                                                    const uint32_t *__restrict__ seg_start,  // n_bmtb*nc+1 (groups)
                                                    const u32x4 *__restrict__ tA,  // 2 u32x4 per group (+1 spare)
                                                    const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K,
@@ -711,9 +711,10 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
     const uint32_t segv = seg_start[g * nc + min(lane, nc)];
 #define GS_SEG(j) __builtin_amdgcn_readlane(segv, (j))
     uint64_t *lst = reinterpret_cast<uint64_t *>(lds + oD + 3 * szD);  // STAMPS only
+// compute lane 0 -> slots 0..31, loader lane 0 -> slots 32..63 (i relative)
 #define GS_STAMP(i)                                                                         \
     if constexpr (STAMPS) {                                                                 \
-        if ((tid == 0 || tid == 64 * WC) && (i) < 32u) lst[(i) + (tid ? 32u : 0u)] =        \
+        if ((tid == 0 || tid == 64 * WC) && (i) < 31u) lst[(i) + (tid ? 32u : 0u)] =        \
             __builtin_amdgcn_s_memtime();                                                   \
     }
     GS_STAMP(0u);
@@ -812,9 +813,11 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
 #define GS_ITER(j, SBn, SPn, SVn, SBs, SPs, SVs)                                                    \
     {                                                                                             \
         GS_LOAD((j) + 3, SBn, SPn, SVn);                                                          \
+        GS_STAMP(2u + 3u * (j));                                                                  \
         if ((j) + 1 < nc) GS_STORE((j) + 1, SBs, SPs, SVs);                                       \
-        GS_STAMP(2u + (j));                                                                       \
+        GS_STAMP(3u + 3u * (j));                                                                  \
         __syncthreads();                                                                          \
+        GS_STAMP(4u + 3u * (j));                                                                  \
     }
         GS_LOAD(0u, sB0, sP0, sV0);
         GS_LOAD(1u, sB1, sP1, sV1);
@@ -838,8 +841,9 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
         __syncthreads();  // chunk 0 staged
         for (uint32_t j = 0; j < nc; j++) {
             GS_MFMA(j);
-            GS_STAMP(2u + j);
+            GS_STAMP(2u + 3u * j);
             __syncthreads();
+            GS_STAMP(4u + 3u * j);
         }
     }
 #undef GS_MFMA
@@ -876,7 +880,7 @@ __global__ __launch_bounds__(512) void k_mfma_rows(const uint32_t *__restrict__ 
     }
     if constexpr (STAMPS) {
         if (tid == 0) {
-            lst[31] = __builtin_amdgcn_s_memtime();
+            lst[31] = __builtin_amdgcn_s_memtime();  // end (compute lane 0)
             for (uint32_t i = 0; i < 64; i++) stamps[(size_t)g * 64 + i] = lst[i];
         }
     }

@@ -571,14 +571,14 @@ void launch_mfma_ct(const plan_state &p, const device_arrays &a, const gsk::f16 
 
 }  // namespace
 
-// diagnostic: C2-shaped plans only (CT 2, RT 2, KC 512, one entry group per thread)
+// diagnostic: C2-shaped plans only (CT 2, RT 2, KC 512)
 void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
                          size_t n_host) {
     const device_plan &d = p.dev;
-    GS_CHECK(p.uploaded && d.mfma && N == d.lds_N && N == 32 && d.maxr == 2 && d.RSB == 9 && d.seg_cap == 1,
+    GS_CHECK(p.uploaded && d.mfma && N == d.lds_N && N == 32 && d.maxr == 2 && d.RSB == 9,
              "timeline build exists for C2-shaped matrix-core plans only");
     const device_arrays &a = d.replicas[0];
-    auto kern = gsk::k_mfma_rows<2, 2, 9, 1, true>;
+    auto kern = d.seg_cap > 1 ? gsk::k_mfma_rows<2, 2, 9, 2, true> : gsk::k_mfma_rows<2, 2, 9, 1, true>;
     const size_t lds = d.lds_bytes + 64 * 8;  // + the stamp slots
     HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));

@@ -33,11 +33,13 @@ a = np.frombuffer(st, dtype=np.uint64).reshape(nb, 64).astype(np.int64)
 nc = info["lds_chunks"]
 t0 = a[:, [0]]
 out = {"total_med": float(np.median(a[:, 31] - a[:, 0])), "total_max": float((a[:, 31] - a[:, 0]).max())}
-# slot layout (kernel_lib.hpp k_mfma_rows STAMPS): compute lane 0 in 0..31, loader lane 0 in 32..63;
-# 0 start, 1 first barrier side (loader: chunk 0 staged), 2+j chunk j's work done (before its barrier), 31 end
+# slot layout (kernel_lib.hpp k_mfma_rows STAMPS): compute lane 0 in 0..30, loader lane 0 in 32..62;
+# 0 start, 1 chunk 0 staged; per chunk j: 2+3j work done (loader: loads issued), 3+3j (loader: staged),
+# 4+3j after the chunk's barrier; 31 end
 for name, base in (("compute", 0), ("loader", 32)):
-    idx = [base + 1] + [base + 2 + j for j in range(nc)]
-    rel = a[:, idx] - t0
-    out[name + "_med_done_at"] = [float(x) for x in np.median(rel, axis=0)]
-# barrier-to-barrier chunk period: compute stamp j+1 minus j
-print(json.dumps(out))
+    rows = {"staged0": float(np.median(a[:, base + 1] - t0[:, 0]))}
+    for j in range(min(nc, 9)):
+        ph = [float(np.median(a[:, base + k + 3 * j] - t0[:, 0])) for k in (2, 3, 4)]
+        rows[f"c{j}"] = ph
+    out[name] = rows
+print(json.dumps(out, indent=0))
