@@ -643,11 +643,11 @@ __global__ __launch_bounds__(1024) void k_lds_rows(
 // BMTB row blocks on the matrix cores (MI355X layout of a tblock/warp/block-
 // total plan whose row blocks are dense enough).  Workgroup g owns BMTB g
 // (R <= RMAX <= 16*RT rows) and walks K in chunks of KC = 2^LGKC columns.
-// The 12 waves are specialised (one compute and two loader waves per SIMD):
-//   compute waves 0-3: v_mfma_f32_16x16x32_f16 over chunk j (A rows by
+// The 16 waves are specialised (two compute and two loader waves per SIMD):
+//   compute waves 0-7: v_mfma_f32_16x16x32_f16 over chunk j (A rows by
 //     ds_read_b128 from the dense image, B by ds_read_b64_tr_b16, fp32
 //     accumulators), then clear the dense image of chunk j+2;
-//   loader waves 4-11: global loads of chunk j+3 into registers (three register
+//   loader waves 8-15: global loads of chunk j+3 into registers (three register
 //     sets, the loop is unrolled by three so every set index is a compile-time
 //     constant), then chunk j+1 from registers into LDS: B rows and the
 //     scatter of its compressed entries (groups of 8, [8 x u16 pos = row*KC +
@@ -678,7 +678,7 @@ __device__ __forceinline__ uint32_t b_piece(uint32_t k, uint32_t p) {
     return p ^ (sw & (uint32_t)(CT - 1));
 }
 
-constexpr int kMfmaWaves = 12, kMfmaCompute = 4;  // compute waves 0..3, loader waves 4..11
+constexpr int kMfmaWaves = 16, kMfmaCompute = 8;  // compute waves 0..7, loader waves 8..15
 
 // STAMPS (diagnostic build only, gs_debug_mfma_timeline): the first loader and
 // compute lanes of every workgroup record s_memtime at phase boundaries
@@ -736,7 +736,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(const uint32_t *_
 
     // loader: chunk j -> registers; chunks past the end and idle slots re-read
     // valid data (the last chunk / the spare group), so no load sits behind a branch
-#define GS_LOAD(j, SB, SP, SV)                                                                      \
+#define GS_LOAD_B(j, SB)                                                                            \
     {                                                                                             \
         const uint32_t jj_ = min((uint32_t)(j), nc - 1u);                                         \
         const uint32_t kc0_ = jj_ * KC;                                                           \
@@ -746,6 +746,10 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(const uint32_t *_
             const uint32_t kk = kc0_ + k < K ? kc0_ + k : kc0_;                                   \
             SB[i] = *reinterpret_cast<const u32x4 *>(B + (size_t)kk * N + (u % UB) * 8u);         \
         }                                                                                         \
+    }
+#define GS_LOAD_A(j, SP, SV)                                                                        \
+    {                                                                                             \
+        const uint32_t jj_ = min((uint32_t)(j), nc - 1u);                                         \
         const uint32_t s0_ = GS_SEG(jj_);                                                         \
         const uint32_t G_ = (uint32_t)(j) < nc ? GS_SEG(jj_ + 1) - s0_ : 0u;                      \
         _Pragma("unroll") for (int I = 0; I < MAXA; I++) {                                        \
@@ -755,15 +759,14 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(const uint32_t *_
             SV[I] = tA[2 * qq + 1];                                                               \
         }                                                                                         \
     }
-    // loader: registers of chunk j -> B[j&1] rows and D[j%3] entries
-#define GS_STORE(j, SB, SP, SV)                                                                     \
+#define GS_LOAD(j, SB, SP, SV)                                                                      \
     {                                                                                             \
-        unsigned char *lb_ = lds + ((j) & 1u) * szB;                                              \
-        _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                                     \
-            const uint32_t u = lt + i * NL;                                                       \
-            const uint32_t k = u / UB, s = u % UB;                                                \
-            *reinterpret_cast<u32x4 *>(lb_ + k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u) = SB[i]; \
-        }                                                                                         \
+        GS_LOAD_B(j, SB);                                                                         \
+        GS_LOAD_A(j, SP, SV);                                                                     \
+    }
+    // loader: registers of chunk j -> B[j&1] rows and D[j%3] entries
+#define GS_SCATTER(j, SP, SV)                                                                       \
+    {                                                                                             \
         const uint32_t G_ = GS_SEG((j) + 1) - GS_SEG(j);                                          \
         unsigned char *ld_ = lds + oD + ((j) % 3u) * szD;                                         \
         _Pragma("unroll") for (int I = 0; I < MAXA; I++) {                                        \
@@ -776,6 +779,16 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(const uint32_t *_
                 }                                                                                 \
             }                                                                                     \
         }                                                                                         \
+    }
+#define GS_STORE(j, SB, SP, SV)                                                                     \
+    {                                                                                             \
+        unsigned char *lb_ = lds + ((j) & 1u) * szB;                                              \
+        _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                                     \
+            const uint32_t u = lt + i * NL;                                                       \
+            const uint32_t k = u / UB, s = u % UB;                                                \
+            *reinterpret_cast<u32x4 *>(lb_ + k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u) = SB[i]; \
+        }                                                                                         \
+        GS_SCATTER(j, SP, SV);                                                                    \
     }
     // compute: chunk j on the matrix cores, then clear D[(j+2)%3]
 #define GS_MFMA(j)                                                                                  \
@@ -812,9 +825,23 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(const uint32_t *_
         // chunk j: fetch j+3 into set j%3, stage j+1 from set (j+1)%3
 #define GS_ITER(j, SBn, SPn, SVn, SBs, SPs, SVs)                                                    \
     {                                                                                             \
-        GS_LOAD((j) + 3, SBn, SPn, SVn);                                                          \
+        /* B: each load of chunk j+3 next to a store of chunk j+1 (TA and LDS overlap); */        \
+        /* the store is unconditional: B[(nc)&1] is free at the last chunk */                     \
+        {                                                                                         \
+            const uint32_t jn_ = min((uint32_t)(j) + 3u, nc - 1u);                                \
+            const uint32_t kc0_ = jn_ * KC;                                                       \
+            unsigned char *lb_ = lds + (((j) + 1u) & 1u) * szB;                                   \
+            _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                                 \
+                const uint32_t u = lt + i * NL;                                                   \
+                const uint32_t k = u / UB, s = u % UB;                                            \
+                const uint32_t kk = kc0_ + k < K ? kc0_ + k : kc0_;                               \
+                SBn[i] = *reinterpret_cast<const u32x4 *>(B + (size_t)kk * N + s * 8u);           \
+                *reinterpret_cast<u32x4 *>(lb_ + k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u) = SBs[i]; \
+            }                                                                                     \
+        }                                                                                         \
+        GS_LOAD_A((j) + 3, SPn, SVn);                                                             \
         GS_STAMP(2u + 3u * (j));                                                                  \
-        if ((j) + 1 < nc) GS_STORE((j) + 1, SBs, SPs, SVs);                                       \
+        if ((j) + 1 < nc) GS_SCATTER((j) + 1, SPs, SVs);                                          \
         GS_STAMP(3u + 3u * (j));                                                                  \
         __syncthreads();                                                                          \
         GS_STAMP(4u + 3u * (j));                                                                  \
@@ -848,7 +875,10 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(const uint32_t *_
     }
 #undef GS_MFMA
 #undef GS_STORE
+#undef GS_SCATTER
 #undef GS_LOAD
+#undef GS_LOAD_A
+#undef GS_LOAD_B
 #undef GS_SEG
     // fixed-order reduction of the compute waves' partial tiles, TPP tiles per pass
     float *red = reinterpret_cast<float *>(lds);
