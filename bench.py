@@ -85,11 +85,27 @@ def time_plan(plan, Bs, Cs, N, steps, warmup, torch, dist=None):
         dist.barrier()
     wall = t1 - t0
     ev_ms = e0.elapsed_time(e1) / steps
-    if dist is not None:
-        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = t.item()
-    return wall, ev_ms
+    return max_over_ranks(wall, dist, torch), ev_ms
+
+
+def max_over_ranks(x, dist, torch):
+    """the job's time = the slowest rank's (RCCL on GPU ranks, gloo on CPU ranks)"""
+    if dist is None:
+        return x
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item()
+
+
+def shard_seed(rank):
+    """row-sharded batch: rank r owns its own matrix (seed 13 + r), no exchange"""
+    return 13 + rank
+
+
+def whole_job_gflops(world, flops_per_step, steps, wall_s):
+    """value = work of all ranks / the max-over-ranks time (weak scaling)"""
+    return world * flops_per_step * steps / wall_s / 1e9
 
 
 def rocsparse_baseline(M, K, N, row, col, val, copies, dtype, reps=100, warmup=10):
@@ -150,7 +166,7 @@ def main():
     from generalsparse_amd import datasets as ds
 
     M, K, N = args.M, args.K, args.N
-    row, col, val = ds.pruned_weight(M, K, args.sparsity, 13 + rank)
+    row, col, val = ds.pruned_weight(M, K, args.sparsity, shard_seed(rank))
     nnz = len(row)
     e, s_idx = 2, (2 if K <= 65536 else 4)
     alg_bytes = algorithmic_bytes(M, K, N, nnz, e, s_idx)
@@ -186,7 +202,7 @@ def main():
 
     key, wall, ev_ms, info, reps, best_cand = best
     ms_per_step = wall / args.steps * 1e3
-    value = world * flops * args.steps / wall / 1e9  # whole-job GFLOP/s
+    value = whole_job_gflops(world, flops, args.steps, wall)
     achieved = alg_bytes / (ev_ms * 1e-3) / 1e9
     traffic = None
     tf = os.path.join(ROOT, "profiles", "traffic_c2.json")
