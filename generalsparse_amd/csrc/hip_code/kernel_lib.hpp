@@ -643,25 +643,27 @@ __global__ __launch_bounds__(1024) void k_lds_rows(
 // BMTB row blocks on the matrix cores (MI355X layout of a tblock/warp/block-
 // total plan whose row blocks are dense enough).  Workgroup g owns BMTB g
 // (R <= RMAX <= 16*RT rows) and walks K in chunks of KC = 2^LGKC columns.
-// The 16 waves are specialised (two compute and two loader waves per SIMD):
+// 16 waves in three roles, each role its own loop with one barrier per chunk
+// (so hipcc's vmcnt analysis of a role sees only that role's loads):
 //   compute waves 0-7: v_mfma_f32_16x16x32_f16 over chunk j (A rows by
 //     ds_read_b128 from the dense image, B by ds_read_b64_tr_b16, fp32
 //     accumulators), then clear the dense image of chunk j+2;
-//   loader waves 8-15: global loads of chunk j+3 into registers (three register
-//     sets, the loop is unrolled by three so every set index is a compile-time
-//     constant), then chunk j+1 from registers into LDS: B rows and the
-//     scatter of its compressed entries (groups of 8, [8 x u16 pos = row*KC +
-//     col][8 x f16 value]; padding entries write 0 to row R) into its image.
-// One barrier per chunk separates the roles' buffers: LDS holds two B buffers
-// (row k at k*N*2 bytes, 32-B pieces permuted by b_piece() so the transposed
-// reads are conflict-free) and three dense images (RMAX+1 rows of RS = 2*KC+32
-// bytes, conflict-free ds_read_b128; row R stays zero and stands in for every
-// MFMA row >= R), so loading, staging, clearing and the matrix cores overlap.
-// Every load is an ordinary VGPR load: hipcc's own counted vmcnt waits keep
-// three chunks in flight.  At the end the compute waves' partial tiles are
-// summed in a fixed order through LDS (deterministic) and rows < R are stored.
-// A zero of the dense image times a non-finite B value gives NaN: the kernel
-// multiplies the row block's whole tile.
+//   B waves 8-11: B rows of chunk j+3 -> registers (three sets), each load
+//     next to the LDS store of chunk j+1's rows;
+//   entry waves 12-15: compressed entries of chunk j+4 -> registers (four
+//     sets: HBM latency is the longest), scatter of chunk j+1's entries
+//     (upload layout: per group of 8, [8 x u16 pos = row*KC + col] in one
+//     array and [8 x f16 value] in another, so both loads are coalesced;
+//     padding entries write 0 to row R) into its dense image.
+// Register set indices are compile-time constants (each role's loop is
+// unrolled by its set count).  LDS: two B buffers (row k at k*N*2 bytes, 32-B
+// pieces permuted by b_piece() so the transposed reads are conflict-free) and
+// three dense images (RMAX+1 rows of RS = 2*KC+32 bytes, conflict-free
+// ds_read_b128; row R stays zero and stands in for every MFMA row >= R).  At
+// the end the compute waves' partial tiles are summed in a fixed order through
+// LDS (deterministic) and rows < R are stored.  A zero of the dense image
+// times a non-finite B value gives NaN: the kernel multiplies the row block's
+// whole tile.
 // ---------------------------------------------------------------------------
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef short s4v __attribute__((ext_vector_type(4)));
@@ -678,32 +680,36 @@ __device__ __forceinline__ uint32_t b_piece(uint32_t k, uint32_t p) {
     return p ^ (sw & (uint32_t)(CT - 1));
 }
 
-constexpr int kMfmaWaves = 16, kMfmaCompute = 8;  // compute waves 0..7, loader waves 8..15
+// waves per role: compute 0..7, B loaders 8..11, entry loaders 12..15
+constexpr int kMfmaWaves = 16, kMfmaCompute = 8, kMfmaBWaves = 4, kMfmaAWaves = 4;
 
-// STAMPS (diagnostic build only, gs_debug_mfma_timeline): the first loader and
-// compute lanes of every workgroup record s_memtime at phase boundaries
+// STAMPS (diagnostic build only, gs_debug_mfma_timeline): lane 0 of the first
+// compute / B / entry wave records s_memtime at phase boundaries
 template <int CT, int RT, int LGKC, int MAXA, bool STAMPS = false>
-__global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
-                                                   const uint32_t *__restrict__ seg_start,  // n_bmtb*nc+1 (groups)
-                                                   const u32x4 *__restrict__ tA,  // 2 u32x4 per group (+1 spare)
-                                                   const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K,
-                                                   uint32_t N, uint32_t nc, uint32_t RMAX, uint32_t row_base,
-                                                   uint64_t *__restrict__ stamps = nullptr) {
+__global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
+    const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
+    const uint32_t *__restrict__ seg_start,       // n_bmtb*nc+1 (groups)
+    const u32x4 *__restrict__ tP,                 // per group: 8 x u16 pos (+1 spare group)
+    const u32x4 *__restrict__ tV,                 // per group: 8 x f16 value (+1 spare group)
+    const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K, uint32_t N, uint32_t nc, uint32_t RMAX,
+    uint32_t row_base, uint64_t *__restrict__ stamps = nullptr) {
     constexpr uint32_t KC = 1u << LGKC;
     constexpr uint32_t RB = 32 * CT;                  // bytes per B row (N == 16*CT)
     constexpr uint32_t UB = 2 * CT;                   // 16-B units per B row
     constexpr uint32_t RS = 2 * KC + 32;              // dense image row stride
     constexpr uint32_t NT = 64 * kMfmaWaves;
-    constexpr uint32_t WC = kMfmaCompute, NL = NT - 64 * WC;  // compute waves, loader threads
+    constexpr uint32_t WC = kMfmaCompute;
+    constexpr uint32_t NBT = 64 * kMfmaBWaves, NAT = 64 * kMfmaAWaves;  // B / entry loader threads
     constexpr uint32_t szB = KC * RB;
-    constexpr uint32_t NB = szB / 16 / NL;            // B units per loader thread per chunk
-    static_assert(szB % (16 * NL) == 0, "whole B units per loader thread");
+    constexpr uint32_t NB = szB / 16 / NBT;           // B units per B thread per chunk
+    static_assert(szB % (16 * NBT) == 0, "whole B units per B thread");
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint32_t szD = (RMAX + 1) * RS;
     const uint32_t oD = 2 * szB;                      // D[0..2] follow B[0..1]
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    const bool loader = wv >= WC;                     // wave-uniform role
-    const uint32_t lt = tid - 64 * WC;                // loader thread index
+    const uint32_t role = wv < WC ? 0u : (wv < WC + kMfmaBWaves ? 1u : 2u);  // wave-uniform
+    const uint32_t bt = tid - 64 * WC;                // B thread index (role 1)
+    const uint32_t at = tid - 64 * (WC + kMfmaBWaves);  // entry thread index (role 2)
     const uint32_t g = blockIdx.x;
     const uint32_t r0 = bmtb_first_row[g], R = bmtb_first_row[g + 1] - r0;
     const u32x4 zero4 = {0u, 0u, 0u, 0u};
@@ -711,206 +717,211 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(const uint32_t *_
     const uint32_t segv = seg_start[g * nc + min(lane, nc)];
 #define GS_SEG(j) __builtin_amdgcn_readlane(segv, (j))
     uint64_t *lst = reinterpret_cast<uint64_t *>(lds + oD + 3 * szD);  // STAMPS only
-// compute lane 0 -> slots 0..31, loader lane 0 -> slots 32..63 (i relative)
-#define GS_STAMP(i)                                                                         \
-    if constexpr (STAMPS) {                                                                 \
-        if ((tid == 0 || tid == 64 * WC) && (i) < 31u) lst[(i) + (tid ? 32u : 0u)] =        \
-            __builtin_amdgcn_s_memtime();                                                   \
+    // first lane of each role -> slots [21*role, 21*role + 21): 0 start, 1 chunk 0 staged,
+    // 2+2j chunk j's work done, 3+2j after its barrier (j < 9); slot 63 end
+#define GS_STAMP(i)                                                                               \
+    if constexpr (STAMPS) {                                                                       \
+        if ((tid == 0 || tid == 64 * WC || tid == 64 * (WC + kMfmaBWaves)) && (i) < 21u)          \
+            lst[(i) + 21u * role] = __builtin_amdgcn_s_memtime();                                 \
     }
     GS_STAMP(0u);
 
     for (uint32_t u = tid; u < 3 * szD / 16u; u += NT) *reinterpret_cast<u32x4 *>(lds + oD + u * 16u) = zero4;
 
-    f4v acc[RT][CT];
+    if (role == 0) {
+        // ---------------------------------------------------------------- compute
+        f4v acc[RT][CT];
 #pragma unroll
-    for (int rt = 0; rt < RT; rt++)
+        for (int rt = 0; rt < RT; rt++)
 #pragma unroll
-        for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
-    uint32_t arow[RT];
+            for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+        uint32_t arow[RT];
 #pragma unroll
-    for (int rt = 0; rt < RT; rt++) {
-        const uint32_t row = 16u * rt + (lane & 15u);
-        arow[rt] = (row < R ? row : R) * RS;
-    }
-    u32x4 sB0[NB], sP0[MAXA], sV0[MAXA], sB1[NB], sP1[MAXA], sV1[MAXA], sB2[NB], sP2[MAXA], sV2[MAXA];
-
-    // loader: chunk j -> registers; chunks past the end and idle slots re-read
-    // valid data (the last chunk / the spare group), so no load sits behind a branch
-#define GS_LOAD_B(j, SB)                                                                            \
+        for (int rt = 0; rt < RT; rt++) {
+            const uint32_t row = 16u * rt + (lane & 15u);
+            arow[rt] = (row < R ? row : R) * RS;
+        }
+        __syncthreads();  // dense images cleared
+        GS_STAMP(1u);
+        __syncthreads();  // chunk 0 staged
+        for (uint32_t j = 0; j < nc; j++) {
+            const uint32_t kr = min(KC, K - j * KC);
+            const uint32_t nsteps = (kr + 31u) / 32u;
+            const unsigned char *la = lds + oD + (j % 3u) * szD;
+            const unsigned char *lb = lds + (j & 1u) * szB;
+            for (uint32_t st = wv; st < nsteps; st += WC) {
+                const uint32_t kb = st * 32u + 8u * (lane >> 4);
+                h8v av[RT];
+#pragma unroll
+                for (int rt = 0; rt < RT; rt++) av[rt] = *reinterpret_cast<const h8v *>(la + arow[rt] + kb * 2u);
+#pragma unroll
+                for (int ct = 0; ct < CT; ct++) {
+                    s4v t[2];
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const uint32_t k = kb + 4u * h + ((lane & 15u) >> 2);
+                        t[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                            (lds_s4v *)(lb + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u));
+                    }
+                    h8v bv;
+                    __builtin_memcpy(&bv, t, 16);
+#pragma unroll
+                    for (int rt = 0; rt < RT; rt++)
+                        acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[rt], bv, acc[rt][ct], 0, 0, 0);
+                }
+            }
+            if (j + 2 < nc)
+                for (uint32_t u = tid; u < R * RS / 16u; u += 64u * WC)
+                    *reinterpret_cast<u32x4 *>(lds + oD + ((j + 2) % 3u) * szD + u * 16u) = zero4;
+            GS_STAMP(2u + 2u * j);
+            __syncthreads();
+            GS_STAMP(3u + 2u * j);
+        }
+        // partial tiles -> LDS for the fixed-order reduction below
+        __syncthreads();
+        float *red = reinterpret_cast<float *>(lds);
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++)
+                *reinterpret_cast<f4v *>(red + (((wv * RT + rt) * CT + ct) * 64u + lane) * 4u) = acc[rt][ct];
+    } else if (role == 1) {
+        // ---------------------------------------------------------------- B rows
+        u32x4 s0[NB], s1[NB], s2[NB];
+#define GS_BLOAD(j, S)                                                                              \
     {                                                                                             \
-        const uint32_t jj_ = min((uint32_t)(j), nc - 1u);                                         \
-        const uint32_t kc0_ = jj_ * KC;                                                           \
+        const uint32_t kc0_ = min((uint32_t)(j), nc - 1u) * KC;                                   \
         _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                                     \
-            const uint32_t u = lt + i * NL;                                                       \
+            const uint32_t u = bt + i * NBT;                                                      \
             const uint32_t k = u / UB;                                                            \
             const uint32_t kk = kc0_ + k < K ? kc0_ + k : kc0_;                                   \
-            SB[i] = *reinterpret_cast<const u32x4 *>(B + (size_t)kk * N + (u % UB) * 8u);         \
+            S[i] = *reinterpret_cast<const u32x4 *>(B + (size_t)kk * N + (u % UB) * 8u);          \
         }                                                                                         \
     }
-#define GS_LOAD_A(j, SP, SV)                                                                        \
+#define GS_BSTORE_UNIT(jb, S, i)                                                                    \
+    {                                                                                             \
+        const uint32_t u = bt + (i) * NBT;                                                        \
+        const uint32_t k = u / UB, s = u % UB;                                                    \
+        *reinterpret_cast<u32x4 *>(lds + ((jb) & 1u) * szB + k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u) = S[i]; \
+    }
+        // chunk j: fetch j+3 into set j%3 next to staging j+1 from set (j+1)%3 (the
+        // store is unconditional: B[(nc)&1] is free at the last chunk)
+#define GS_BITER(j, Sn, Ss)                                                                         \
+    {                                                                                             \
+        const uint32_t kc0_ = min((uint32_t)(j) + 3u, nc - 1u) * KC;                              \
+        _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                                     \
+            const uint32_t u = bt + i * NBT;                                                      \
+            const uint32_t k = u / UB;                                                            \
+            const uint32_t kk = kc0_ + k < K ? kc0_ + k : kc0_;                                   \
+            Sn[i] = *reinterpret_cast<const u32x4 *>(B + (size_t)kk * N + (u % UB) * 8u);         \
+            GS_BSTORE_UNIT((j) + 1u, Ss, i);                                                      \
+        }                                                                                         \
+        GS_STAMP(2u + 2u * (j));                                                                  \
+        __syncthreads();                                                                          \
+        GS_STAMP(3u + 2u * (j));                                                                  \
+    }
+        GS_BLOAD(0u, s0);
+        GS_BLOAD(1u, s1);
+        GS_BLOAD(2u, s2);
+        __syncthreads();  // dense images cleared
+#pragma unroll
+        for (uint32_t i = 0; i < NB; i++) GS_BSTORE_UNIT(0u, s0, i);
+        GS_STAMP(1u);
+        __syncthreads();  // chunk 0 staged
+        uint32_t j = 0;
+        for (; j + 2 < nc; j += 3) {
+            GS_BITER(j, s0, s1);
+            GS_BITER(j + 1, s1, s2);
+            GS_BITER(j + 2, s2, s0);
+        }
+        if (j < nc) GS_BITER(j, s0, s1);
+        if (j + 1 < nc) GS_BITER(j + 1, s1, s2);
+#undef GS_BITER
+#undef GS_BSTORE_UNIT
+#undef GS_BLOAD
+        __syncthreads();
+    } else {
+        // ---------------------------------------------------------------- entries
+        u32x4 p0[MAXA], v0[MAXA], p1[MAXA], v1[MAXA], p2[MAXA], v2[MAXA], p3[MAXA], v3[MAXA];
+#define GS_ALOAD(j, P, V)                                                                           \
     {                                                                                             \
         const uint32_t jj_ = min((uint32_t)(j), nc - 1u);                                         \
         const uint32_t s0_ = GS_SEG(jj_);                                                         \
         const uint32_t G_ = (uint32_t)(j) < nc ? GS_SEG(jj_ + 1) - s0_ : 0u;                      \
         _Pragma("unroll") for (int I = 0; I < MAXA; I++) {                                        \
-            const uint32_t q = lt + I * NL;                                                       \
+            const uint32_t q = at + I * NAT;                                                      \
             const size_t qq = (size_t)s0_ + (q < G_ ? q : 0u);                                    \
-            SP[I] = tA[2 * qq];                                                                   \
-            SV[I] = tA[2 * qq + 1];                                                               \
+            P[I] = tP[qq];                                                                        \
+            V[I] = tV[qq];                                                                        \
         }                                                                                         \
     }
-#define GS_LOAD(j, SB, SP, SV)                                                                      \
-    {                                                                                             \
-        GS_LOAD_B(j, SB);                                                                         \
-        GS_LOAD_A(j, SP, SV);                                                                     \
-    }
-    // loader: registers of chunk j -> B[j&1] rows and D[j%3] entries
-#define GS_SCATTER(j, SP, SV)                                                                       \
+#define GS_SCATTER(j, P, V)                                                                         \
     {                                                                                             \
         const uint32_t G_ = GS_SEG((j) + 1) - GS_SEG(j);                                          \
         unsigned char *ld_ = lds + oD + ((j) % 3u) * szD;                                         \
         _Pragma("unroll") for (int I = 0; I < MAXA; I++) {                                        \
-            const uint32_t q = lt + I * NL;                                                       \
+            const uint32_t q = at + I * NAT;                                                      \
             if (q < G_) {                                                                         \
                 _Pragma("unroll") for (int e = 0; e < 8; e++) {                                   \
-                    const uint32_t pos = (SP[I][e >> 1] >> (16 * (e & 1))) & 0xffffu;             \
-                    const uint16_t v = (uint16_t)((SV[I][e >> 1] >> (16 * (e & 1))) & 0xffffu);   \
+                    const uint32_t pos = (P[I][e >> 1] >> (16 * (e & 1))) & 0xffffu;              \
+                    const uint16_t v = (uint16_t)((V[I][e >> 1] >> (16 * (e & 1))) & 0xffffu);    \
                     *reinterpret_cast<uint16_t *>(ld_ + (pos >> LGKC) * RS + (pos & (KC - 1u)) * 2u) = v; \
                 }                                                                                 \
             }                                                                                     \
         }                                                                                         \
     }
-#define GS_STORE(j, SB, SP, SV)                                                                     \
+        // chunk j: fetch j+4 into set j%4, scatter j+1 from set (j+1)%4
+#define GS_AITER(j, Pn, Vn, Ps, Vs)                                                                 \
     {                                                                                             \
-        unsigned char *lb_ = lds + ((j) & 1u) * szB;                                              \
-        _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                                     \
-            const uint32_t u = lt + i * NL;                                                       \
-            const uint32_t k = u / UB, s = u % UB;                                                \
-            *reinterpret_cast<u32x4 *>(lb_ + k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u) = SB[i]; \
-        }                                                                                         \
-        GS_SCATTER(j, SP, SV);                                                                    \
-    }
-    // compute: chunk j on the matrix cores, then clear D[(j+2)%3]
-#define GS_MFMA(j)                                                                                  \
-    {                                                                                             \
-        const uint32_t kr_ = min(KC, K - (j) * KC);                                               \
-        const uint32_t nsteps_ = (kr_ + 31u) / 32u;                                               \
-        const unsigned char *la_ = lds + oD + ((j) % 3u) * szD;                                   \
-        const unsigned char *lb_ = lds + ((j) & 1u) * szB;                                        \
-        for (uint32_t st = wv; st < nsteps_; st += WC) {                                          \
-            const uint32_t kb = st * 32u + 8u * (lane >> 4);                                      \
-            h8v av[RT];                                                                           \
-            _Pragma("unroll") for (int rt = 0; rt < RT; rt++) av[rt] =                            \
-                *reinterpret_cast<const h8v *>(la_ + arow[rt] + kb * 2u);                         \
-            _Pragma("unroll") for (int ct = 0; ct < CT; ct++) {                                   \
-                s4v t[2];                                                                         \
-                _Pragma("unroll") for (int h = 0; h < 2; h++) {                                   \
-                    const uint32_t k = kb + 4u * h + ((lane & 15u) >> 2);                         \
-                    t[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(                               \
-                        (lds_s4v *)(lb_ + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u)); \
-                }                                                                                 \
-                h8v bv;                                                                           \
-                __builtin_memcpy(&bv, t, 16);                                                     \
-                _Pragma("unroll") for (int rt = 0; rt < RT; rt++) acc[rt][ct] =                   \
-                    __builtin_amdgcn_mfma_f32_16x16x32_f16(av[rt], bv, acc[rt][ct], 0, 0, 0);     \
-            }                                                                                     \
-        }                                                                                         \
-        if ((j) + 2 < nc)                                                                         \
-            for (uint32_t u = tid; u < R * RS / 16u; u += 64u * WC)                               \
-                *reinterpret_cast<u32x4 *>(lds + oD + (((j) + 2) % 3u) * szD + u * 16u) = zero4;  \
-    }
-    // The roles run separate loops (one barrier per chunk in each), so hipcc's
-    // vmcnt analysis sees only the loader's loads in the loader loop.
-    if (loader) {
-        // chunk j: fetch j+3 into set j%3, stage j+1 from set (j+1)%3
-#define GS_ITER(j, SBn, SPn, SVn, SBs, SPs, SVs)                                                    \
-    {                                                                                             \
-        /* B: each load of chunk j+3 next to a store of chunk j+1 (TA and LDS overlap); */        \
-        /* the store is unconditional: B[(nc)&1] is free at the last chunk */                     \
-        {                                                                                         \
-            const uint32_t jn_ = min((uint32_t)(j) + 3u, nc - 1u);                                \
-            const uint32_t kc0_ = jn_ * KC;                                                       \
-            unsigned char *lb_ = lds + (((j) + 1u) & 1u) * szB;                                   \
-            _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                                 \
-                const uint32_t u = lt + i * NL;                                                   \
-                const uint32_t k = u / UB, s = u % UB;                                            \
-                const uint32_t kk = kc0_ + k < K ? kc0_ + k : kc0_;                               \
-                SBn[i] = *reinterpret_cast<const u32x4 *>(B + (size_t)kk * N + s * 8u);           \
-                *reinterpret_cast<u32x4 *>(lb_ + k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u) = SBs[i]; \
-            }                                                                                     \
-        }                                                                                         \
-        GS_LOAD_A((j) + 3, SPn, SVn);                                                             \
-        GS_STAMP(2u + 3u * (j));                                                                  \
-        if ((j) + 1 < nc) GS_SCATTER((j) + 1, SPs, SVs);                                          \
-        GS_STAMP(3u + 3u * (j));                                                                  \
+        GS_ALOAD((j) + 4, Pn, Vn);                                                                \
+        if ((j) + 1 < nc) GS_SCATTER((j) + 1, Ps, Vs);                                            \
+        GS_STAMP(2u + 2u * (j));                                                                  \
         __syncthreads();                                                                          \
-        GS_STAMP(4u + 3u * (j));                                                                  \
+        GS_STAMP(3u + 2u * (j));                                                                  \
     }
-        GS_LOAD(0u, sB0, sP0, sV0);
-        GS_LOAD(1u, sB1, sP1, sV1);
-        GS_LOAD(2u, sB2, sP2, sV2);
+        GS_ALOAD(0u, p0, v0);
+        GS_ALOAD(1u, p1, v1);
+        GS_ALOAD(2u, p2, v2);
+        GS_ALOAD(3u, p3, v3);
         __syncthreads();  // dense images cleared
-        GS_STORE(0u, sB0, sP0, sV0);
+        GS_SCATTER(0u, p0, v0);
         GS_STAMP(1u);
         __syncthreads();  // chunk 0 staged
         uint32_t j = 0;
-        for (; j + 2 < nc; j += 3) {
-            GS_ITER(j, sB0, sP0, sV0, sB1, sP1, sV1);
-            GS_ITER(j + 1, sB1, sP1, sV1, sB2, sP2, sV2);
-            GS_ITER(j + 2, sB2, sP2, sV2, sB0, sP0, sV0);
+        for (; j + 3 < nc; j += 4) {
+            GS_AITER(j, p0, v0, p1, v1);
+            GS_AITER(j + 1, p1, v1, p2, v2);
+            GS_AITER(j + 2, p2, v2, p3, v3);
+            GS_AITER(j + 3, p3, v3, p0, v0);
         }
-        if (j < nc) GS_ITER(j, sB0, sP0, sV0, sB1, sP1, sV1);
-        if (j + 1 < nc) GS_ITER(j + 1, sB1, sP1, sV1, sB2, sP2, sV2);
-#undef GS_ITER
-    } else {
-        __syncthreads();  // dense images cleared
-        GS_STAMP(1u);
-        __syncthreads();  // chunk 0 staged
-        for (uint32_t j = 0; j < nc; j++) {
-            GS_MFMA(j);
-            GS_STAMP(2u + 3u * j);
-            __syncthreads();
-            GS_STAMP(4u + 3u * j);
-        }
-    }
-#undef GS_MFMA
-#undef GS_STORE
+        if (j < nc) GS_AITER(j, p0, v0, p1, v1);
+        if (j + 1 < nc) GS_AITER(j + 1, p1, v1, p2, v2);
+        if (j + 2 < nc) GS_AITER(j + 2, p2, v2, p3, v3);
+#undef GS_AITER
 #undef GS_SCATTER
-#undef GS_LOAD
-#undef GS_LOAD_A
-#undef GS_LOAD_B
-#undef GS_SEG
-    // fixed-order reduction of the compute waves' partial tiles, TPP tiles per pass
-    float *red = reinterpret_cast<float *>(lds);
-    const uint32_t TPP = min((uint32_t)(RT * CT), (oD + 3 * szD) / (WC * 1024u));
-    for (uint32_t t0 = 0; t0 < RT * CT; t0 += TPP) {
-        if (!loader) {
-#pragma unroll
-            for (int rt = 0; rt < RT; rt++)
-#pragma unroll
-                for (int ct = 0; ct < CT; ct++) {
-                    const uint32_t tt = rt * CT + ct;
-                    if (tt >= t0 && tt < t0 + TPP)
-                        *reinterpret_cast<f4v *>(red + ((wv * TPP + (tt - t0)) * 64u + lane) * 4u) = acc[rt][ct];
-                }
-        }
+#undef GS_ALOAD
         __syncthreads();
-        const uint32_t nt = min(TPP, RT * CT - t0);
-        for (uint32_t e = tid; e < nt * 256u; e += NT) {
-            const uint32_t ti = e >> 8, cc = e & 15u, rr = (e >> 4) & 15u;
-            const uint32_t tt = t0 + ti, rt = tt / CT, ct = tt % CT;
+    }
+#undef GS_SEG
+    __syncthreads();
+    // fixed-order reduction of the compute waves' partial tiles (all threads)
+    {
+        const float *red = reinterpret_cast<const float *>(lds);
+        for (uint32_t e = tid; e < RT * CT * 256u; e += NT) {
+            const uint32_t cc = e & 15u, rr = (e >> 4) & 15u, tt = e >> 8;
+            const uint32_t rt = tt / CT, ct = tt % CT;
             const uint32_t ln = 16u * (rr >> 2) + cc, i = rr & 3u;
             float sum = 0.f;
 #pragma unroll
-            for (uint32_t w = 0; w < WC; w++) sum += red[((w * TPP + ti) * 64u + ln) * 4u + i];
+            for (uint32_t w = 0; w < WC; w++) sum += red[(((w * RT + rt) * CT + ct) * 64u + ln) * 4u + i];
             const uint32_t row = 16u * rt + rr;
             if (row < R) C[(size_t)(row_base + r0 + row) * N + 16u * ct + cc] = (f16)sum;
         }
-        __syncthreads();
     }
     if constexpr (STAMPS) {
+        __syncthreads();
         if (tid == 0) {
-            lst[31] = __builtin_amdgcn_s_memtime();  // end (compute lane 0)
+            lst[63] = __builtin_amdgcn_s_memtime();
             for (uint32_t i = 0; i < 64; i++) stamps[(size_t)g * 64 + i] = lst[i];
         }
     }

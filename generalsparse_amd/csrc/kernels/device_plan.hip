@@ -183,12 +183,12 @@ struct mfma_tiles {
     uint32_t lgKC = 0, nc = 0, RT = 0, RMAX = 0, MAXA = 0;
     size_t lds_bytes = 0;
     std::vector<uint32_t> seg_start;  // in groups
-    std::vector<uint16_t> groups;     // 16 u16 per group, + one stage buffer of padding
+    std::vector<uint16_t> pos, val;   // 8 u16 per group each, + one spare group
 };
 
 constexpr uint32_t kMfmaThreads = 64 * gsk::kMfmaWaves;
 
-constexpr uint32_t kMfmaLoaders = kMfmaThreads - 64 * gsk::kMfmaCompute;
+constexpr uint32_t kMfmaBThreads = 64 * gsk::kMfmaBWaves, kMfmaAThreads = 64 * gsk::kMfmaAWaves;
 
 size_t mfma_lds_bytes(uint32_t lgKC, uint32_t CT, uint32_t RMAX) {
     const size_t KC = 1ull << lgKC;
@@ -228,11 +228,13 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
             for (uint64_t e = row_ptr[tb_rows[g]]; e < row_ptr[tb_rows[g + 1]]; e++) cnt[col[e] >> lg]++;
             for (uint64_t j = 0; j < nc; j++) gmax = std::max(gmax, (cnt[j] + 7) / 8);
         }
-        if (gmax > 2ull * kMfmaLoaders || nc > 63) continue;
-        if (((KC * 32 * CT) / 16) % kMfmaLoaders) continue;  // whole B units per loader thread
-        if ((KC * 32 * CT) / 16 / kMfmaLoaders > 8) continue;  // register budget of the loader sets
+        if (gmax > 2ull * kMfmaAThreads || nc > 63) continue;
+        if (((KC * 32 * CT) / 16) % kMfmaBThreads) continue;  // whole B units per B thread
+        if ((KC * 32 * CT) / 16 / kMfmaBThreads > 8) continue;  // register budget of the B sets
+        // the compute waves' partial tiles must fit LDS for the final reduction
+        if ((size_t)gsk::kMfmaCompute * RT * CT * 1024 > mfma_lds_bytes(lg, CT, (uint32_t)rmax)) continue;
         t.lgKC = lg; t.nc = (uint32_t)nc; t.RT = RT; t.RMAX = (uint32_t)rmax;
-        t.MAXA = gmax <= kMfmaLoaders ? 1 : 2;
+        t.MAXA = gmax <= kMfmaAThreads ? 1 : 2;
         t.lds_bytes = mfma_lds_bytes(lg, CT, (uint32_t)rmax);
         break;
     }
@@ -258,14 +260,13 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
                 cur[i] = e;
             }
             while (pos.size() % 8) { pos.push_back((uint16_t)(R * KC)); hv.push_back(0); }
-            for (size_t q = 0; q < pos.size(); q += 8) {
-                t.groups.insert(t.groups.end(), pos.begin() + q, pos.begin() + q + 8);
-                t.groups.insert(t.groups.end(), hv.begin() + q, hv.begin() + q + 8);
-            }
-            t.seg_start.push_back((uint32_t)(t.groups.size() / 16));
+            t.pos.insert(t.pos.end(), pos.begin(), pos.end());
+            t.val.insert(t.val.end(), hv.begin(), hv.end());
+            t.seg_start.push_back((uint32_t)(t.pos.size() / 8));
         }
     }
-    t.groups.insert(t.groups.end(), 16, 0);  // spare group: idle lanes' branch-free loads
+    t.pos.insert(t.pos.end(), 8, 0);  // spare group: idle lanes' branch-free loads
+    t.val.insert(t.val.end(), 8, 0);
     return true;
 }
 
@@ -330,7 +331,8 @@ void upload_plan(plan_state &p, int dtype, int device) {
         const size_t before = d.bytes_A;
         a.t0 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_row_indices", 0), "BMTB first_row_indices"));
         a.t1 = dev_copy(d, t.seg_start);
-        a.tcol = dev_copy(d, t.groups);
+        a.tcol = dev_copy(d, t.pos);
+        a.tval = dev_copy(d, t.val);
         d.bytes_tile = d.bytes_A - before;
         d.n_rows_aux = m.u(TBLOCK_META, "first_row_indices", 0).size() - 1;
         return true;
@@ -543,8 +545,8 @@ void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *
         }
     }
     hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux), dim3(kMfmaThreads), d.lds_bytes, s, a.t0, a.t1,
-                       (const gsk::u32x4 *)a.tcol, B, C, (uint32_t)p.K, N, d.nc, d.rpw_max, (uint32_t)d.row_base,
-                       (uint64_t *)nullptr);
+                       (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, B, C, (uint32_t)p.K, N, d.nc,
+                       d.rpw_max, (uint32_t)d.row_base, (uint64_t *)nullptr);
     HIP_OK(hipGetLastError());
 }
 
@@ -586,8 +588,8 @@ void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N
     const size_t n = (size_t)d.n_rows_aux * 64;
     HIP_OK(hipMalloc(&dst, n * 8));
     hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux), dim3(kMfmaThreads), lds, s, a.t0, a.t1,
-                       (const gsk::u32x4 *)a.tcol, (const gsk::f16 *)B, (gsk::f16 *)C, (uint32_t)p.K, N, d.nc,
-                       d.rpw_max, (uint32_t)d.row_base, dst);
+                       (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, (const gsk::f16 *)B, (gsk::f16 *)C,
+                       (uint32_t)p.K, N, d.nc, d.rpw_max, (uint32_t)d.row_base, dst);
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(s));
     HIP_OK(hipMemcpy(host, dst, std::min(n, n_host) * 8, hipMemcpyDeviceToHost));

@@ -32,14 +32,14 @@ _lib.check(L.gs_debug_mfma_timeline(plan._h, ctypes.c_void_p(B.data_ptr()), ctyp
 a = np.frombuffer(st, dtype=np.uint64).reshape(nb, 64).astype(np.int64)
 nc = info["lds_chunks"]
 t0 = a[:, [0]]
-out = {"total_med": float(np.median(a[:, 31] - a[:, 0])), "total_max": float((a[:, 31] - a[:, 0]).max())}
-# slot layout (kernel_lib.hpp k_mfma_rows STAMPS): compute lane 0 in 0..30, loader lane 0 in 32..62;
-# 0 start, 1 chunk 0 staged; per chunk j: 2+3j work done (loader: loads issued), 3+3j (loader: staged),
-# 4+3j after the chunk's barrier; 31 end
-for name, base in (("compute", 0), ("loader", 32)):
+out = {"total_med": float(np.median(a[:, 63] - a[:, 0])), "total_max": float((a[:, 63] - a[:, 0]).max())}
+# slot layout (kernel_lib.hpp k_mfma_rows STAMPS): role r (0 compute, 1 B rows, 2 entries) in
+# slots 21r..21r+20: 0 start, 1 chunk 0 staged, 2+2j chunk j's work done, 3+2j after its barrier
+for name, r in (("compute", 0), ("bload", 1), ("aload", 2)):
+    base = 21 * r
     rows = {"staged0": float(np.median(a[:, base + 1] - t0[:, 0]))}
     for j in range(min(nc, 9)):
-        ph = [float(np.median(a[:, base + k + 3 * j] - t0[:, 0])) for k in (2, 3, 4)]
-        rows[f"c{j}"] = ph
+        rows[f"c{j}"] = [float(np.median(a[:, base + 2 + 2 * j] - t0[:, 0])),
+                         float(np.median(a[:, base + 3 + 2 * j] - t0[:, 0]))]
     out[name] = rows
-print(json.dumps(out, indent=0))
+print(json.dumps(out))
