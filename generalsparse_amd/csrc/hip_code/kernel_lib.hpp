@@ -645,16 +645,17 @@ __global__ __launch_bounds__(1024) void k_lds_rows(
 // (R <= RMAX <= 16*RT rows) and walks K in chunks of KC = 2^LGKC columns.
 // 16 waves in three roles, each role its own loop with one barrier per chunk
 // (so hipcc's vmcnt analysis of a role sees only that role's loads):
-//   compute waves 0-7: v_mfma_f32_16x16x32_f16 over chunk j (A rows by
+//   compute waves 0-5: v_mfma_f32_16x16x32_f16 over chunk j (A rows by
 //     ds_read_b128 from the dense image, B by ds_read_b64_tr_b16, fp32
 //     accumulators), then clear the dense image of chunk j+2;
-//   B waves 8-11: B rows of chunk j+3 -> registers (three sets), each load
+//   B waves 6-9: B rows of chunk j+3 -> registers (three sets), each load
 //     next to the LDS store of chunk j+1's rows;
-//   entry waves 12-15: compressed entries of chunk j+4 -> registers (four
+//   entry waves 10-15: compressed entries of chunk j+4 -> registers (four
 //     sets: HBM latency is the longest), scatter of chunk j+1's entries
-//     (upload layout: per group of 8, [8 x u16 pos = row*KC + col] in one
-//     array and [8 x f16 value] in another, so both loads are coalesced;
-//     padding entries write 0 to row R) into its dense image.
+//     (upload layout: per group of 8, [8 x u16 h = row*RS/2 + col, the
+//     entry's halfword index in the dense image] in one array and [8 x f16
+//     value] in another, so both loads are coalesced and the LDS address is
+//     one shift; padding entries write 0 to row R) into its dense image.
 // Register set indices are compile-time constants (each role's loop is
 // unrolled by its set count).  LDS: two B buffers (row k at k*N*2 bytes, 32-B
 // pieces permuted by b_piece() so the transposed reads are conflict-free) and
@@ -680,8 +681,8 @@ __device__ __forceinline__ uint32_t b_piece(uint32_t k, uint32_t p) {
     return p ^ (sw & (uint32_t)(CT - 1));
 }
 
-// waves per role: compute 0..7, B loaders 8..11, entry loaders 12..15
-constexpr int kMfmaWaves = 16, kMfmaCompute = 8, kMfmaBWaves = 4, kMfmaAWaves = 4;
+// waves per role: compute 0..5, B loaders 6..9, entry loaders 10..15
+constexpr int kMfmaWaves = 16, kMfmaCompute = 6, kMfmaBWaves = 4, kMfmaAWaves = 6;
 
 // STAMPS (diagnostic build only, gs_debug_mfma_timeline): lane 0 of the first
 // compute / B / entry wave records s_memtime at phase boundaries
@@ -692,7 +693,8 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     const u32x4 *__restrict__ tP,                 // per group: 8 x u16 pos (+1 spare group)
     const u32x4 *__restrict__ tV,                 // per group: 8 x f16 value (+1 spare group)
     const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K, uint32_t N, uint32_t nc, uint32_t RMAX,
-    uint32_t row_base, uint64_t *__restrict__ stamps = nullptr) {
+    uint32_t row_base, uint32_t nsplit, uint32_t ncs, float *__restrict__ slabs, uint32_t *__restrict__ arrivals,
+    uint64_t *__restrict__ stamps = nullptr) {
     constexpr uint32_t KC = 1u << LGKC;
     constexpr uint32_t RB = 32 * CT;                  // bytes per B row (N == 16*CT)
     constexpr uint32_t UB = 2 * CT;                   // 16-B units per B row
@@ -710,12 +712,15 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     const uint32_t role = wv < WC ? 0u : (wv < WC + kMfmaBWaves ? 1u : 2u);  // wave-uniform
     const uint32_t bt = tid - 64 * WC;                // B thread index (role 1)
     const uint32_t at = tid - 64 * (WC + kMfmaBWaves);  // entry thread index (role 2)
-    const uint32_t g = blockIdx.x;
+    // K-split: workgroup (g, sp) takes chunks [j0, j0 + ncl) of BMTB g
+    const uint32_t g = blockIdx.x / nsplit, sp = blockIdx.x % nsplit;
+    const uint32_t j0 = sp * ncs, ncl = min(nc, j0 + ncs) - j0;
     const uint32_t r0 = bmtb_first_row[g], R = bmtb_first_row[g + 1] - r0;
     const u32x4 zero4 = {0u, 0u, 0u, 0u};
-    // this BMTB's segment starts, lane t holding chunk t's (nc <= 63, host-checked)
+    // this BMTB's segment starts, lane t holding chunk t's (nc <= 63, host-checked);
+    // GS_SEG takes a local chunk index
     const uint32_t segv = seg_start[g * nc + min(lane, nc)];
-#define GS_SEG(j) __builtin_amdgcn_readlane(segv, (j))
+#define GS_SEG(j) __builtin_amdgcn_readlane(segv, j0 + (j))
     uint64_t *lst = reinterpret_cast<uint64_t *>(lds + oD + 3 * szD);  // STAMPS only
     // first lane of each role -> slots [21*role, 21*role + 21): 0 start, 1 chunk 0 staged,
     // 2+2j chunk j's work done, 3+2j after its barrier (j < 9); slot 63 end
@@ -744,8 +749,8 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         __syncthreads();  // dense images cleared
         GS_STAMP(1u);
         __syncthreads();  // chunk 0 staged
-        for (uint32_t j = 0; j < nc; j++) {
-            const uint32_t kr = min(KC, K - j * KC);
+        for (uint32_t j = 0; j < ncl; j++) {
+            const uint32_t kr = min(KC, K - (j0 + j) * KC);
             const uint32_t nsteps = (kr + 31u) / 32u;
             const unsigned char *la = lds + oD + (j % 3u) * szD;
             const unsigned char *lb = lds + (j & 1u) * szB;
@@ -770,7 +775,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
                         acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[rt], bv, acc[rt][ct], 0, 0, 0);
                 }
             }
-            if (j + 2 < nc)
+            if (j + 2 < ncl)
                 for (uint32_t u = tid; u < R * RS / 16u; u += 64u * WC)
                     *reinterpret_cast<u32x4 *>(lds + oD + ((j + 2) % 3u) * szD + u * 16u) = zero4;
             GS_STAMP(2u + 2u * j);
@@ -790,7 +795,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         u32x4 s0[NB], s1[NB], s2[NB];
 #define GS_BLOAD(j, S)                                                                              \
     {                                                                                             \
-        const uint32_t kc0_ = min((uint32_t)(j), nc - 1u) * KC;                                   \
+        const uint32_t kc0_ = (j0 + min((uint32_t)(j), ncl - 1u)) * KC;                          \
         _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                                     \
             const uint32_t u = bt + i * NBT;                                                      \
             const uint32_t k = u / UB;                                                            \
@@ -808,7 +813,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         // store is unconditional: B[(nc)&1] is free at the last chunk)
 #define GS_BITER(j, Sn, Ss)                                                                         \
     {                                                                                             \
-        const uint32_t kc0_ = min((uint32_t)(j) + 3u, nc - 1u) * KC;                              \
+        const uint32_t kc0_ = (j0 + min((uint32_t)(j) + 3u, ncl - 1u)) * KC;                     \
         _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                                     \
             const uint32_t u = bt + i * NBT;                                                      \
             const uint32_t k = u / UB;                                                            \
@@ -829,13 +834,13 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         GS_STAMP(1u);
         __syncthreads();  // chunk 0 staged
         uint32_t j = 0;
-        for (; j + 2 < nc; j += 3) {
+        for (; j + 2 < ncl; j += 3) {
             GS_BITER(j, s0, s1);
             GS_BITER(j + 1, s1, s2);
             GS_BITER(j + 2, s2, s0);
         }
-        if (j < nc) GS_BITER(j, s0, s1);
-        if (j + 1 < nc) GS_BITER(j + 1, s1, s2);
+        if (j < ncl) GS_BITER(j, s0, s1);
+        if (j + 1 < ncl) GS_BITER(j + 1, s1, s2);
 #undef GS_BITER
 #undef GS_BSTORE_UNIT
 #undef GS_BLOAD
@@ -845,9 +850,9 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         u32x4 p0[MAXA], v0[MAXA], p1[MAXA], v1[MAXA], p2[MAXA], v2[MAXA], p3[MAXA], v3[MAXA];
 #define GS_ALOAD(j, P, V)                                                                           \
     {                                                                                             \
-        const uint32_t jj_ = min((uint32_t)(j), nc - 1u);                                         \
+        const uint32_t jj_ = min((uint32_t)(j), ncl - 1u);                                        \
         const uint32_t s0_ = GS_SEG(jj_);                                                         \
-        const uint32_t G_ = (uint32_t)(j) < nc ? GS_SEG(jj_ + 1) - s0_ : 0u;                      \
+        const uint32_t G_ = (uint32_t)(j) < ncl ? GS_SEG(jj_ + 1) - s0_ : 0u;                     \
         _Pragma("unroll") for (int I = 0; I < MAXA; I++) {                                        \
             const uint32_t q = at + I * NAT;                                                      \
             const size_t qq = (size_t)s0_ + (q < G_ ? q : 0u);                                    \
@@ -863,9 +868,9 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
             const uint32_t q = at + I * NAT;                                                      \
             if (q < G_) {                                                                         \
                 _Pragma("unroll") for (int e = 0; e < 8; e++) {                                   \
-                    const uint32_t pos = (P[I][e >> 1] >> (16 * (e & 1))) & 0xffffu;              \
+                    const uint32_t h = (P[I][e >> 1] >> (16 * (e & 1))) & 0xffffu;                \
                     const uint16_t v = (uint16_t)((V[I][e >> 1] >> (16 * (e & 1))) & 0xffffu);    \
-                    *reinterpret_cast<uint16_t *>(ld_ + (pos >> LGKC) * RS + (pos & (KC - 1u)) * 2u) = v; \
+                    *reinterpret_cast<uint16_t *>(ld_ + h * 2u) = v;                              \
                 }                                                                                 \
             }                                                                                     \
         }                                                                                         \
@@ -874,7 +879,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
 #define GS_AITER(j, Pn, Vn, Ps, Vs)                                                                 \
     {                                                                                             \
         GS_ALOAD((j) + 4, Pn, Vn);                                                                \
-        if ((j) + 1 < nc) GS_SCATTER((j) + 1, Ps, Vs);                                            \
+        if ((j) + 1 < ncl) GS_SCATTER((j) + 1, Ps, Vs);                                           \
         GS_STAMP(2u + 2u * (j));                                                                  \
         __syncthreads();                                                                          \
         GS_STAMP(3u + 2u * (j));                                                                  \
@@ -888,15 +893,15 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         GS_STAMP(1u);
         __syncthreads();  // chunk 0 staged
         uint32_t j = 0;
-        for (; j + 3 < nc; j += 4) {
+        for (; j + 3 < ncl; j += 4) {
             GS_AITER(j, p0, v0, p1, v1);
             GS_AITER(j + 1, p1, v1, p2, v2);
             GS_AITER(j + 2, p2, v2, p3, v3);
             GS_AITER(j + 3, p3, v3, p0, v0);
         }
-        if (j < nc) GS_AITER(j, p0, v0, p1, v1);
-        if (j + 1 < nc) GS_AITER(j + 1, p1, v1, p2, v2);
-        if (j + 2 < nc) GS_AITER(j + 2, p2, v2, p3, v3);
+        if (j < ncl) GS_AITER(j, p0, v0, p1, v1);
+        if (j + 1 < ncl) GS_AITER(j + 1, p1, v1, p2, v2);
+        if (j + 2 < ncl) GS_AITER(j + 2, p2, v2, p3, v3);
 #undef GS_AITER
 #undef GS_SCATTER
 #undef GS_ALOAD
@@ -905,24 +910,63 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
 #undef GS_SEG
     __syncthreads();
     // fixed-order reduction of the compute waves' partial tiles (all threads)
-    {
-        const float *red = reinterpret_cast<const float *>(lds);
-        for (uint32_t e = tid; e < RT * CT * 256u; e += NT) {
-            const uint32_t cc = e & 15u, rr = (e >> 4) & 15u, tt = e >> 8;
-            const uint32_t rt = tt / CT, ct = tt % CT;
-            const uint32_t ln = 16u * (rr >> 2) + cc, i = rr & 3u;
-            float sum = 0.f;
+    const float *red = reinterpret_cast<const float *>(lds);
+    auto tile_sum = [&](uint32_t e, uint32_t &row, uint32_t &colx) {
+        const uint32_t cc = e & 15u, rr = (e >> 4) & 15u, tt = e >> 8;
+        const uint32_t rt = tt / CT, ct = tt % CT;
+        const uint32_t ln = 16u * (rr >> 2) + cc, i = rr & 3u;
+        float sum = 0.f;
 #pragma unroll
-            for (uint32_t w = 0; w < WC; w++) sum += red[(((w * RT + rt) * CT + ct) * 64u + ln) * 4u + i];
-            const uint32_t row = 16u * rt + rr;
-            if (row < R) C[(size_t)(row_base + r0 + row) * N + 16u * ct + cc] = (f16)sum;
+        for (uint32_t w = 0; w < WC; w++) sum += red[(((w * RT + rt) * CT + ct) * 64u + ln) * 4u + i];
+        row = 16u * rt + rr;
+        colx = 16u * ct + cc;
+        return sum;
+    };
+    if (nsplit == 1) {
+        for (uint32_t e = tid; e < RT * CT * 256u; e += NT) {
+            uint32_t row, colx;
+            const float sum = tile_sum(e, row, colx);
+            if (row < R) C[(size_t)(row_base + r0 + row) * N + colx] = (f16)sum;
+        }
+    } else {
+        // K-split: this workgroup's fp32 slab, then the last of the row block's
+        // nsplit workgroups (agent-scope release/acquire around one counter)
+        // sums the slabs in split order (deterministic) and stores C
+        float *slab = slabs + ((size_t)g * nsplit + sp) * RMAX * N;
+        for (uint32_t e = tid; e < RT * CT * 256u; e += NT) {
+            uint32_t row, colx;
+            const float sum = tile_sum(e, row, colx);
+            if (row < R) slab[(size_t)row * N + colx] = sum;
+        }
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        uint32_t *flag = reinterpret_cast<uint32_t *>(lds + oD + 3 * szD + 512);
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            *flag = __hip_atomic_fetch_add(&arrivals[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (*flag == nsplit - 1u) {
+            if (tid == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(&arrivals[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();
+            const float *base = slabs + (size_t)g * nsplit * RMAX * N;
+            for (uint32_t e = tid; e < R * N; e += NT) {
+                float sum = 0.f;
+                for (uint32_t q = 0; q < nsplit; q++) sum += base[(size_t)q * RMAX * N + e];
+                C[(size_t)(row_base + r0) * N + e] = (f16)sum;
+            }
         }
     }
     if constexpr (STAMPS) {
         __syncthreads();
         if (tid == 0) {
             lst[63] = __builtin_amdgcn_s_memtime();
-            for (uint32_t i = 0; i < 64; i++) stamps[(size_t)g * 64 + i] = lst[i];
+            for (uint32_t i = 0; i < 64; i++) stamps[(size_t)blockIdx.x * 64 + i] = lst[i];
         }
     }
 #undef GS_STAMP

@@ -275,6 +275,7 @@ int gs_plan_info_get(gs_plan_t *p, gs_plan_info *info) {
             info->lds_waves = s.dev.waves;
             info->lds_bytes = s.dev.lds_bytes;
             info->tile_bytes = s.dev.bytes_tile;
+            info->ksplit = s.dev.ksplit;
         }
     });
 }

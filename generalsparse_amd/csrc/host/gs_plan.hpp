@@ -17,6 +17,7 @@ struct device_arrays {
     uint32_t *t0 = nullptr, *t1 = nullptr, *t2 = nullptr, *t3 = nullptr, *t4 = nullptr;
     uint32_t *a0 = nullptr, *a1 = nullptr, *a2 = nullptr, *a3 = nullptr, *a4 = nullptr;
     uint64_t *m0 = nullptr;
+    float *ws = nullptr;  // k_mfma_rows K-split slabs (per replica: a replica never runs concurrently with itself)
 };
 
 struct device_plan {
@@ -33,7 +34,8 @@ struct device_plan {
     size_t bytes_A = 0;       // device bytes of A per replica (metadata + cols + vals)
     // LDS-stationary B (k_lds_rows): chunk geometry fixed for dense width lds_N
     bool lds = false;
-    bool mfma = false;  // k_mfma_rows (uses KC, nc, lds_bytes; RS in RSB; RT in maxr)
+    bool mfma = false;  // k_mfma_rows (uses KC, nc, lds_bytes; log2 KC in RSB; RT in maxr; RMAX in rpw_max)
+    uint32_t ksplit = 1, ncs = 0;  // k_mfma_rows workgroups per row block, chunks per workgroup
     uint32_t lds_N = 0, KC = 0, nc = 0, RSB = 0, rpw_max = 0, seg_cap = 0, waves = 0, maxr = 0;
     size_t lds_bytes = 0, bytes_tile = 0;
     std::vector<device_arrays> replicas;

@@ -177,8 +177,9 @@ bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uin
 // ------------------------------------------------------------------ MFMA tiles
 // Upload layout of k_mfma_rows (kernel_lib.hpp): for BMTB g and column chunk j,
 // the entries of g's rows with columns in [j*KC, (j+1)*KC), in groups of 8:
-// [8 x u16 pos = local_row*KC + local_col][8 x f16 value]; the last group is
-// padded with (pos = R*KC, value 0), row R being the kernel's zero row.
+// pos[] = 8 x u16 halfword index in the dense image (local_row*(KC+16) +
+// local_col), val[] = 8 x f16; the last group is padded with (row R, value 0),
+// row R being the kernel's zero row.
 struct mfma_tiles {
     uint32_t lgKC = 0, nc = 0, RT = 0, RMAX = 0, MAXA = 0;
     size_t lds_bytes = 0;
@@ -192,7 +193,7 @@ constexpr uint32_t kMfmaBThreads = 64 * gsk::kMfmaBWaves, kMfmaAThreads = 64 * g
 
 size_t mfma_lds_bytes(uint32_t lgKC, uint32_t CT, uint32_t RMAX) {
     const size_t KC = 1ull << lgKC;
-    return 2 * KC * 32 * CT + 3 * (RMAX + 1) * (2 * KC + 32);
+    return 2 * KC * 32 * CT + 3 * (RMAX + 1) * (2 * KC + 32) + 1024;  // + stamp slots and the arrival flag
 }
 
 bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
@@ -206,7 +207,7 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
     for (uint64_t g = 0; g < nb; g++) rmax = std::max<uint64_t>(rmax, tb_rows[g + 1] - tb_rows[g]);
     for (uint64_t g = 0; g < nb; g++) nnz += row_ptr[tb_rows[g + 1]] - row_ptr[tb_rows[g]];
     if (rmax == 0 || rmax > 64) { why = "BMTBs of 1..64 rows only"; return false; }
-    const uint32_t RT = rmax <= 16 ? 1 : (rmax <= 32 ? 2 : 4);
+    const uint32_t RT = (uint32_t)((rmax + 15) / 16);
     if (nnz == 0 || (double)nb * 16 * RT * K > (double)max_fill * nnz) {
         why = "row blocks too sparse for dense tiles";
         return false;
@@ -219,7 +220,7 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
     }
     for (uint32_t lg = 10; lg >= 8; lg--) {
         const uint64_t KC = 1ull << lg;
-        if ((rmax + 1) * KC > 65536 || mfma_lds_bytes(lg, CT, (uint32_t)rmax) > lds_budget) continue;
+        if ((rmax + 1) * (KC + 16) > 65536 || mfma_lds_bytes(lg, CT, (uint32_t)rmax) > lds_budget) continue;
         const uint64_t nc = (K + KC - 1) / KC;
         uint64_t gmax = 0;
         std::vector<uint64_t> cnt(nc);
@@ -254,12 +255,13 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
             for (uint64_t i = 0; i < R; i++) {
                 uint64_t e = cur[i];
                 for (; e < row_ptr[r0 + i + 1] && col[e] < lim; e++) {
-                    pos.push_back((uint16_t)(i * KC + (col[e] - (uint64_t)j * KC)));
+                    // halfword index in the dense image (row stride RS = 2*KC + 32 bytes)
+                    pos.push_back((uint16_t)(i * (KC + 16) + (col[e] - (uint64_t)j * KC)));
                     hv.push_back(f32_to_f16_bits((float)vals.read_float_from_arr(e)));
                 }
                 cur[i] = e;
             }
-            while (pos.size() % 8) { pos.push_back((uint16_t)(R * KC)); hv.push_back(0); }
+            while (pos.size() % 8) { pos.push_back((uint16_t)(R * (KC + 16))); hv.push_back(0); }
             t.pos.insert(t.pos.end(), pos.begin(), pos.end());
             t.val.insert(t.val.end(), hv.begin(), hv.end());
             t.seg_start.push_back((uint32_t)(t.pos.size() / 8));
@@ -327,6 +329,18 @@ void upload_plan(plan_state &p, int dtype, int device) {
         d.lds_N = Nd;
         d.KC = 1u << t.lgKC; d.nc = t.nc; d.maxr = t.RT; d.rpw_max = t.RMAX; d.RSB = t.lgKC;
         d.seg_cap = t.MAXA;
+        // K-split: enough workgroups per row block to cover the CUs, at least one chunk each
+        const uint64_t nb = m.u(TBLOCK_META, "first_row_indices", 0).size() - 1;
+        uint32_t ks = cfg.MFMA_KSPLIT > 0 ? (uint32_t)cfg.MFMA_KSPLIT
+                                          : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4, 256 / std::max<uint64_t>(nb, 1)));
+        ks = std::max(1u, std::min(ks, t.nc));
+        d.ncs = (t.nc + ks - 1) / ks;
+        d.ksplit = (t.nc + d.ncs - 1) / d.ncs;  // no empty split
+        if (d.ksplit > 1) {
+            std::vector<float> z((size_t)nb * d.ksplit * t.RMAX * Nd, 0.f);
+            a.ws = dev_copy(d, z);
+            a.t2 = dev_copy(d, std::vector<uint32_t>(nb, 0u));  // arrival counters
+        }
         d.waves = kMfmaThreads / 64; d.lds_bytes = t.lds_bytes;
         const size_t before = d.bytes_A;
         a.t0 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_row_indices", 0), "BMTB first_row_indices"));
@@ -477,6 +491,7 @@ void add_replica(plan_state &p) {
     r.t2 = (uint32_t *)dup(s.t2);
     r.t3 = (uint32_t *)dup(s.t3);
     r.t4 = (uint32_t *)dup(s.t4);
+    r.ws = (float *)dup(s.ws);
     p.dev.replicas.push_back(r);
 }
 
@@ -544,9 +559,9 @@ void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *
             g = d.lds_bytes;
         }
     }
-    hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux), dim3(kMfmaThreads), d.lds_bytes, s, a.t0, a.t1,
-                       (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, B, C, (uint32_t)p.K, N, d.nc,
-                       d.rpw_max, (uint32_t)d.row_base, (uint64_t *)nullptr);
+    hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit), dim3(kMfmaThreads), d.lds_bytes, s, a.t0,
+                       a.t1, (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, B, C, (uint32_t)p.K, N, d.nc,
+                       d.rpw_max, (uint32_t)d.row_base, d.ksplit, d.ncs, a.ws, a.t2, (uint64_t *)nullptr);
     HIP_OK(hipGetLastError());
 }
 
@@ -567,6 +582,7 @@ void launch_mfma_ct(const plan_state &p, const device_arrays &a, const gsk::f16 
     switch (p.dev.maxr) {
         case 1: launch_mfma_rt<CT, 1>(p, a, B, C, N, s); break;
         case 2: launch_mfma_rt<CT, 2>(p, a, B, C, N, s); break;
+        case 3: launch_mfma_rt<CT, 3>(p, a, B, C, N, s); break;
         default: launch_mfma_rt<CT, 4>(p, a, B, C, N, s); break;
     }
 }
@@ -581,15 +597,15 @@ void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N
              "timeline build exists for C2-shaped matrix-core plans only");
     const device_arrays &a = d.replicas[0];
     auto kern = d.seg_cap > 1 ? gsk::k_mfma_rows<2, 2, 9, 2, true> : gsk::k_mfma_rows<2, 2, 9, 1, true>;
-    const size_t lds = d.lds_bytes + 64 * 8;  // + the stamp slots
+    const size_t lds = d.lds_bytes;
     HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));
     uint64_t *dst = nullptr;
-    const size_t n = (size_t)d.n_rows_aux * 64;
+    const size_t n = (size_t)d.n_rows_aux * d.ksplit * 64;
     HIP_OK(hipMalloc(&dst, n * 8));
-    hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux), dim3(kMfmaThreads), lds, s, a.t0, a.t1,
+    hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit), dim3(kMfmaThreads), lds, s, a.t0, a.t1,
                        (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, (const gsk::f16 *)B, (gsk::f16 *)C,
-                       (uint32_t)p.K, N, d.nc, d.rpw_max, (uint32_t)d.row_base, dst);
+                       (uint32_t)p.K, N, d.nc, d.rpw_max, (uint32_t)d.row_base, d.ksplit, d.ncs, a.ws, a.t2, dst);
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(s));
     HIP_OK(hipMemcpy(host, dst, std::min(n, n_host) * 8, hipMemcpyDeviceToHost));

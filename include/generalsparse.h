@@ -59,6 +59,7 @@ typedef struct {
     int lds_stage;
     uint32_t lds_n, lds_kc, lds_chunks, lds_waves;
     uint64_t lds_bytes, tile_bytes;
+    uint32_t ksplit;              /* k_mfma_rows workgroups per row block (K ranges, fp32 slab combine) */
 } gs_plan_info;
 
 const char *gs_last_error(void);

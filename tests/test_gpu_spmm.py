@@ -293,3 +293,31 @@ def test_mfma_rows_selection():
         assert plan.info()["lds_stage"] == 1
     finally:
         gsa.set_config("MFMA_TILES", 1)
+
+
+@pytest.mark.parametrize("ks", [1, 2, 3])
+def test_mfma_rows_ksplit_combine(ks, mfma_everywhere):
+    """K ranges per row block combined through fp32 slabs by the last arriving
+    workgroup: same result (within fp16 output rounding) for every split, exact
+    known answer, and the arrival counters reset for the next launch"""
+    M, K, N = 400, 6000, 32
+    r, c, v = ds.pruned_weight(M, K, 0.7, 31)
+    try:
+        gsa.set_config("MFMA_KSPLIT", ks)
+        plan, C, B = run(M, K, r, c, v, "block_total", 40, 1, N, "f16")
+        info = plan.info()
+        assert info["lds_stage"] == 2 and info["ksplit"] == ks, info
+        ref = ofi.spmm_ref(M, N, r, c, v.astype(np.float16).astype(np.float32), B.astype(np.float32), "f64")
+        check(C, ref, "f16")
+        Bt = torch.from_numpy(B).to(DEV)
+        again = [plan.spmm(Bt).float().cpu().numpy() for _ in range(3)]
+        for a in again:
+            np.testing.assert_array_equal(a, C)   # deterministic, counters reset
+        plan.add_replica()
+        np.testing.assert_array_equal(plan.spmm(Bt, replica=1).float().cpu().numpy(), C)
+        ones, _, _ = run(M, K, r, c, np.ones(len(r), np.float32), "block_total", 40, 1, N, "f16",
+                         B=np.ones((K, N), np.float16))[1:], None, None
+        nnz_row = np.bincount(r.astype(np.int64), minlength=M).astype(np.float32)
+        np.testing.assert_array_equal(ones, np.repeat(nnz_row[:, None], N, axis=1))
+    finally:
+        gsa.set_config("MFMA_KSPLIT", 0)
