@@ -86,6 +86,11 @@ __device__ __forceinline__ void atomic_add_vals<float, 4>(float *p, const float 
     for (int k = 0; k < 4; k++) unsafeAtomicAdd(p + k, v[k]);
 }
 template <>
+__device__ __forceinline__ void atomic_add_vals<float, 8>(float *p, const float (&v)[8]) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) unsafeAtomicAdd(p + k, v[k]);
+}
+template <>
 __device__ __forceinline__ void atomic_add_vals<f16, 8>(f16 *p, const float (&v)[8]) {
 #pragma unroll
     for (int k = 0; k < 8; k += 2) {
@@ -324,7 +329,10 @@ __global__ __launch_bounds__(256) void k_bitmap_segment(const uint32_t *__restri
                                                         const uint32_t *__restrict__ seg_row_off,    // segments
                                                         const CT *__restrict__ col, const VT *__restrict__ val,
                                                         const VT *__restrict__ B, VT *__restrict__ C, uint32_t n_bmt,
-                                                        uint32_t N, uint32_t X, uint32_t row_base) {
+                                                        uint32_t N, uint32_t X, uint32_t row_base,
+                                                        float *__restrict__ ws) {
+    // ws != nullptr (fp16 C): rows shared between BMTs accumulate in an fp32
+    // workspace (k_finalize_rows rounds them to C once); else atomics go to C.
     // per wave: up to 2 open partials per slot (head, tail), S <= 64
     __shared__ uint32_t open_row[4][64][2];
     extern __shared__ float dyn[];  // [4 waves][S slots][2][X lanes][CF]
@@ -423,8 +431,10 @@ __global__ __launch_bounds__(256) void k_bitmap_segment(const uint32_t *__restri
                     if (r == 0xffffffffu) continue;
                     const float *src = my_dyn + ((size_t)q * X + xl) * CF;
                     if (r != run_row) {
-                        if (run_row != 0xffffffffu)
-                            atomic_add_vals<VT, CF>(C + (size_t)(run_row + row_base) * N + c0, run);
+                        if (run_row != 0xffffffffu) {
+                            if (ws) atomic_add_vals<float, CF>(ws + (size_t)(run_row + row_base) * N + c0, run);
+                            else atomic_add_vals<VT, CF>(C + (size_t)(run_row + row_base) * N + c0, run);
+                        }
                         run_row = r;
 #pragma unroll
                         for (int k = 0; k < CF; k++) run[k] = src[k];
@@ -433,13 +443,29 @@ __global__ __launch_bounds__(256) void k_bitmap_segment(const uint32_t *__restri
                         for (int k = 0; k < CF; k++) run[k] += src[k];
                     }
                 }
-                if (run_row != 0xffffffffu) atomic_add_vals<VT, CF>(C + (size_t)(run_row + row_base) * N + c0, run);
+                if (run_row != 0xffffffffu) {
+                    if (ws) atomic_add_vals<float, CF>(ws + (size_t)(run_row + row_base) * N + c0, run);
+                    else atomic_add_vals<VT, CF>(C + (size_t)(run_row + row_base) * N + c0, run);
+                }
             }
             __builtin_amdgcn_wave_barrier();
         }
     }
 }
 
+
+// rows listed (shared between BMTs, or empty): C = fp16(workspace), workspace
+// re-zeroed for the next launch (companion of k_bitmap_segment with ws)
+template <class VT>
+__global__ __launch_bounds__(256) void k_finalize_rows(const uint32_t *__restrict__ rows, uint32_t n_rows,
+                                                       float *__restrict__ ws, VT *__restrict__ C, uint32_t N) {
+    const size_t total = (size_t)n_rows * N;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+        const size_t idx = (size_t)rows[e / N] * N + e % N;
+        C[idx] = (VT)ws[idx];
+        ws[idx] = 0.f;
+    }
+}
 
 // ---------------------------------------------------------------------------
 // v_fma_mix_f32: fp32 += fp16 * fp16 with the conversions folded into the FMA

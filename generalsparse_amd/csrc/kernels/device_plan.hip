@@ -448,7 +448,29 @@ void upload_plan(plan_state &p, int dtype, int device) {
             a.a3 = dev_copy(d, to_u32(m.u(THREAD_META, "segment_empty_row_indices", 0), "segment_empty_row_indices"));
             d.n_units = nb;
             d.scf = 4;
-            d.needs_memset = true;
+            if (dtype == 1) {
+                // fp16 C: rows whose nonzeros span BMTs accumulate in an fp32 workspace and
+                // are rounded once by k_finalize_rows, which also writes the empty rows (no memset)
+                const uint64_t rb = d.row_base;
+                std::vector<uint32_t> rp = csr_row_ptr(rows, row_num);
+                std::vector<uint8_t> fin(p.M, 0);
+                for (uint64_t r = 0; r < p.M; r++)
+                    if (r < rb || r - rb >= row_num || rp[r - rb] == rp[r - rb + 1]) fin[r] = 1;
+                for (uint64_t i = 1; i + 1 < fn.size(); i++) {  // a BMT boundary strictly inside a row
+                    const uint64_t z = fn[i];
+                    if (z == 0 || z >= rows.size()) continue;
+                    if (rows[z] == rows[z - 1]) fin[rows[z] + rb] = 1;
+                }
+                std::vector<uint32_t> list;
+                for (uint64_t r = 0; r < p.M; r++)
+                    if (fin[r]) list.push_back((uint32_t)r);
+                a.a4 = dev_copy(d, list);
+                a.ws = dev_copy(d, std::vector<float>((size_t)p.M * std::max<uint32_t>(1, (uint32_t)get_config().DENSE_MATRIX_SIZE), 0.f));
+                d.ws_n = (uint32_t)get_config().DENSE_MATRIX_SIZE;
+                d.n_fin = list.size();
+            } else {
+                d.needs_memset = true;
+            }
             break;
         }
         default:
@@ -667,10 +689,18 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
             const uint32_t S = 64 / X;
             uint32_t gx = (uint32_t)std::min<uint64_t>((d.n_units + 4 * S - 1) / (4 * S), 1u << 16);
             size_t lds = (size_t)4 * S * 2 * X * CF * sizeof(float);
-            HIP_OK(hipMemsetAsync(C, 0, (size_t)d.n_out_rows * N * sizeof(VT), s));
+            // the fp32 workspace is sized for the plan's dense width; other widths use fp16 atomics
+            const bool use_ws = a.ws && N == d.ws_n;
+            if (!use_ws) HIP_OK(hipMemsetAsync(C, 0, (size_t)d.n_out_rows * N * sizeof(VT), s));
             hipLaunchKernelGGL((gsk::k_bitmap_segment<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256),
                                lds, s, a.a0, a.a1, a.m0, a.a2, a.a3, col, val, B, C, (uint32_t)d.n_units, N, X,
-                               row_base);
+                               row_base, use_ws ? a.ws : (float *)nullptr);
+            if (use_ws && d.n_fin) {
+                HIP_OK(hipGetLastError());
+                const uint32_t fx = (uint32_t)std::min<uint64_t>((d.n_fin * N + 255) / 256, 4096);
+                hipLaunchKernelGGL((gsk::k_finalize_rows<VT>), dim3(fx), dim3(256), 0, s, a.a4, (uint32_t)d.n_fin,
+                                   a.ws, C, N);
+            }
             break;
         }
         default:
