@@ -384,7 +384,18 @@ void upload_plan(plan_state &p, int dtype, int device) {
             d.n_units = m.u(WARP_META, "first_row_indices", 0).size() - 1;
             d.scf = 4;
             if (sp.tblock_parent && try_mfma(rp)) break;
-            if (sp.tblock_parent && get_config().LDS_STAGE_B) {
+            // LDS-stationary B pays off for row blocks of >= 16 rows in BMWs of >= 2 rows
+            // (C2: 20x2 31 us vs 40 us gathered; 4x1 62 us): otherwise the gather kernel
+            bool lds_worth = false;
+            if (sp.tblock_parent) {
+                const auto &tr = m.u(TBLOCK_META, "first_row_indices", 0);
+                const auto &wr = m.u(WARP_META, "first_row_indices", 0);
+                uint64_t mt = 0, mw = 0;
+                for (size_t i = 0; i + 1 < tr.size(); i++) mt = std::max<uint64_t>(mt, tr[i + 1] - tr[i]);
+                for (size_t i = 0; i + 1 < wr.size(); i++) mw = std::max<uint64_t>(mw, wr[i + 1] - wr[i]);
+                lds_worth = mt >= 16 && mw >= 2;
+            }
+            if (sp.tblock_parent && get_config().LDS_STAGE_B && lds_worth) {
                 lds_tiles t;
                 std::string why;
                 const uint32_t Nd = (uint32_t)get_config().DENSE_MATRIX_SIZE;

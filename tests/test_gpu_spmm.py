@@ -153,7 +153,7 @@ def test_rocsparse_comparator_agrees():
 # ---------------------------------------------------------------- LDS-stationary B
 # tblock_warp_total(p0 rows per BMTB, p1 rows per BMW) uploads the chunk-major tile
 # layout and runs k_lds_rows when dense width N makes whole 16-B B rows.
-LDS_PIPES = [(20, 2), (8, 1), (64, 4), (4, 4), (3, 1), (48, 3)]
+LDS_PIPES = [(20, 2), (16, 2), (64, 4), (32, 4), (48, 3)]
 
 
 def lds_cases():
@@ -213,10 +213,12 @@ def test_lds_stage_off_and_unfit_plans_use_gather_kernel(no_mfma):
     plan1, C1, _ = run(M, K, row, col, val, "tblock_warp_total", 20, 2, N, "f16", B=B)
     assert plan1.info()["lds_stage"] == 1
     check(C1, C0, "f16")
-    # 64 one-row BMWs per BMTB exceed the 16-wave workgroup: gather kernel
-    plan2, C2, _ = run(M, K, row, col, val, "tblock_warp_total", 64, 1, N, "f16", B=B)
-    assert plan2.info()["lds_stage"] == 0
-    check(C2, C0, "f16")
+    # 64 one-row BMWs per BMTB exceed the 16-wave workgroup, and 4-row BMTBs are
+    # faster gathered: gather kernel
+    for p0, p1 in ((64, 1), (4, 1)):
+        plan2, C2, _ = run(M, K, row, col, val, "tblock_warp_total", p0, p1, N, "f16", B=B)
+        assert plan2.info()["lds_stage"] == 0
+        check(C2, C0, "f16")
 
 
 # ---------------------------------------------------------------- matrix-core row blocks
@@ -315,8 +317,8 @@ def test_mfma_rows_ksplit_combine(ks, mfma_everywhere):
             np.testing.assert_array_equal(a, C)   # deterministic, counters reset
         plan.add_replica()
         np.testing.assert_array_equal(plan.spmm(Bt, replica=1).float().cpu().numpy(), C)
-        ones, _, _ = run(M, K, r, c, np.ones(len(r), np.float32), "block_total", 40, 1, N, "f16",
-                         B=np.ones((K, N), np.float16))[1:], None, None
+        _, ones, _ = run(M, K, r, c, np.ones(len(r), np.float32), "block_total", 40, 1, N, "f16",
+                         B=np.ones((K, N), np.float16))
         nnz_row = np.bincount(r.astype(np.int64), minlength=M).astype(np.float32)
         np.testing.assert_array_equal(ones, np.repeat(nnz_row[:, None], N, axis=1))
     finally:
