@@ -731,6 +731,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     constexpr uint32_t szB = KC * RB;
     constexpr uint32_t NB = szB / 16 / NBT;           // B units per B thread per chunk
     static_assert(szB % (16 * NBT) == 0, "whole B units per B thread");
+    constexpr int MAXS = (int)((KC / 32 + WC - 1) / WC);  // k-steps per compute wave per chunk
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint32_t szD = (RMAX + 1) * RS;
     const uint32_t oD = 2 * szB;                      // D[0..2] follow B[0..1]
@@ -780,11 +781,16 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
             const uint32_t nsteps = (kr + 31u) / 32u;
             const unsigned char *la = lds + oD + (j % 3u) * szD;
             const unsigned char *lb = lds + (j & 1u) * szB;
-            for (uint32_t st = wv; st < nsteps; st += WC) {
-                const uint32_t kb = st * 32u + 8u * (lane >> 4);
-                h8v av[RT];
+            // all of this wave's k-steps of the chunk: every fragment read issued
+            // before the first MFMA (steps past the chunk's end read step 0 and
+            // multiply a zeroed A fragment: no branch around the reads)
+            h8v av[MAXS][RT], bv[MAXS][CT];
 #pragma unroll
-                for (int rt = 0; rt < RT; rt++) av[rt] = *reinterpret_cast<const h8v *>(la + arow[rt] + kb * 2u);
+            for (int q = 0; q < MAXS; q++) {
+                const uint32_t st = wv + q * WC;
+                const uint32_t kb = (st < nsteps ? st : 0u) * 32u + 8u * (lane >> 4);
+#pragma unroll
+                for (int rt = 0; rt < RT; rt++) av[q][rt] = *reinterpret_cast<const h8v *>(la + arow[rt] + kb * 2u);
 #pragma unroll
                 for (int ct = 0; ct < CT; ct++) {
                     s4v t[2];
@@ -794,11 +800,18 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
                         t[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                             (lds_s4v *)(lb + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u));
                     }
-                    h8v bv;
-                    __builtin_memcpy(&bv, t, 16);
+                    __builtin_memcpy(&bv[q][ct], t, 16);
+                }
+            }
 #pragma unroll
-                    for (int rt = 0; rt < RT; rt++)
-                        acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[rt], bv, acc[rt][ct], 0, 0, 0);
+            for (int q = 0; q < MAXS; q++) {
+                const bool live = wv + q * WC < nsteps;
+#pragma unroll
+                for (int rt = 0; rt < RT; rt++) {
+                    const h8v a = live ? av[q][rt] : h8v{};
+#pragma unroll
+                    for (int ct = 0; ct < CT; ct++)
+                        acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bv[q][ct], acc[rt][ct], 0, 0, 0);
                 }
             }
             if (j + 2 < ncl)
@@ -905,10 +918,10 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
 #define GS_AITER(j, Pn, Vn, Ps, Vs)                                                                 \
     {                                                                                             \
         GS_ALOAD((j) + 4, Pn, Vn);                                                                \
+        GS_STAMP(2u + 2u * (j)); /* entry role: loads issued, then scatter done */                \
         if ((j) + 1 < ncl) GS_SCATTER((j) + 1, Ps, Vs);                                           \
-        GS_STAMP(2u + 2u * (j));                                                                  \
-        __syncthreads();                                                                          \
         GS_STAMP(3u + 2u * (j));                                                                  \
+        __syncthreads();                                                                          \
     }
         GS_ALOAD(0u, p0, v0);
         GS_ALOAD(1u, p1, v1);

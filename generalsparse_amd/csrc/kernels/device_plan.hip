@@ -196,6 +196,54 @@ size_t mfma_lds_bytes(uint32_t lgKC, uint32_t CT, uint32_t RMAX) {
     return 2 * KC * 32 * CT + 3 * (RMAX + 1) * (2 * KC + 32) + 1024;  // + stamp slots and the arrival flag
 }
 
+// Order one segment's entries for the scatter: the kernel's 32-lane half-waves
+// write (group q, slot e) for 32 consecutive groups at once, so every such
+// "round" takes entries of distinct LDS write banks ((halfword/2) mod 32) where
+// possible (greedy: fullest banks first, a bank twice only when fewer than 32
+// banks remain).  Appends 8 u16 pos + 8 u16 values per group; padding slots write
+// 0 into the zero row (pad_h = its first halfword), on banks of their own.
+void bank_order_segment(const std::vector<uint16_t> &pos, const std::vector<uint16_t> &val, uint32_t pad_h,
+                        std::vector<uint16_t> &out_pos, std::vector<uint16_t> &out_val) {
+    const size_t n = pos.size();
+    const size_t ng = (n + 7) / 8;
+    std::vector<std::vector<uint32_t>> bucket(32);
+    for (uint32_t i = 0; i < n; i++) bucket[(pos[i] >> 1) & 31].push_back(i);
+    const size_t base = out_pos.size();
+    out_pos.resize(base + ng * 8);
+    out_val.resize(base + ng * 8);
+    std::vector<int> order(32);
+    for (size_t b0 = 0; b0 < ng; b0 += 32) {
+        const size_t gl = std::min<size_t>(32, ng - b0);
+        for (int e = 0; e < 8; e++) {
+            for (int k = 0; k < 32; k++) order[k] = k;
+            std::stable_sort(order.begin(), order.end(),
+                             [&](int a, int b) { return bucket[a].size() > bucket[b].size(); });
+            size_t l = 0;
+            bool progress = true;
+            while (l < gl && progress) {  // one entry per bank per pass, fullest banks first
+                progress = false;
+                for (int k = 0; k < 32 && l < gl; k++) {
+                    auto &bk = bucket[order[k]];
+                    if (bk.empty()) continue;
+                    const uint32_t i = bk.back();
+                    bk.pop_back();
+                    const size_t slot = base + (b0 + l) * 8 + e;
+                    out_pos[slot] = pos[i];
+                    out_val[slot] = val[i];
+                    l++;
+                    progress = true;
+                }
+            }
+            for (; l < gl; l++) {  // padding: value 0 into the zero row, one bank each
+                const size_t slot = base + (b0 + l) * 8 + e;
+                out_pos[slot] = (uint16_t)(pad_h + 2 * (l & 31));
+                out_val[slot] = 0;
+            }
+        }
+    }
+    for (const auto &bk : bucket) GS_CHECK(bk.empty(), "bank ordering lost an entry");
+}
+
 bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
                       const std::vector<uint64_t> &col, const universal_array &vals, uint64_t K, uint32_t N,
                       size_t lds_budget, int64_t max_fill, mfma_tiles &t, std::string &why) {
@@ -261,9 +309,7 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
                 }
                 cur[i] = e;
             }
-            while (pos.size() % 8) { pos.push_back((uint16_t)(R * (KC + 16))); hv.push_back(0); }
-            t.pos.insert(t.pos.end(), pos.begin(), pos.end());
-            t.val.insert(t.val.end(), hv.begin(), hv.end());
+            bank_order_segment(pos, hv, (uint32_t)(R * (KC + 16)), t.pos, t.val);
             t.seg_start.push_back((uint32_t)(t.pos.size() / 8));
         }
     }
@@ -331,8 +377,10 @@ void upload_plan(plan_state &p, int dtype, int device) {
         d.seg_cap = t.MAXA;
         // K-split: enough workgroups per row block to cover the CUs, at least one chunk each
         const uint64_t nb = m.u(TBLOCK_META, "first_row_indices", 0).size() - 1;
+        // auto: split only when the row blocks cover under half the CUs (the slab
+        // combine's cross-XCD release/acquire costs ~micro-seconds at the tail)
         uint32_t ks = cfg.MFMA_KSPLIT > 0 ? (uint32_t)cfg.MFMA_KSPLIT
-                                          : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4, 256 / std::max<uint64_t>(nb, 1)));
+                                          : (nb >= 128 ? 1u : (uint32_t)std::min<uint64_t>(4, 256 / std::max<uint64_t>(nb, 1)));
         ks = std::max(1u, std::min(ks, t.nc));
         d.ncs = (t.nc + ks - 1) / ks;
         d.ksplit = (t.nc + d.ncs - 1) / d.ncs;  // no empty split
@@ -622,14 +670,22 @@ void launch_mfma_ct(const plan_state &p, const device_arrays &a, const gsk::f16 
 
 }  // namespace
 
-// diagnostic: C2-shaped plans only (CT 2, RT 2, KC 512)
+// diagnostic: N = 32 plans with 17..48-row BMTBs and KC 256 or 512
+template <int RT, int LG>
+auto timeline_kernel(bool two) {
+    return two ? gsk::k_mfma_rows<2, RT, LG, 2, true> : gsk::k_mfma_rows<2, RT, LG, 1, true>;
+}
+
 void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
                          size_t n_host) {
     const device_plan &d = p.dev;
-    GS_CHECK(p.uploaded && d.mfma && N == d.lds_N && N == 32 && d.maxr == 2 && d.RSB == 9,
-             "timeline build exists for C2-shaped matrix-core plans only");
+    GS_CHECK(p.uploaded && d.mfma && N == d.lds_N && N == 32 && (d.maxr == 2 || d.maxr == 3) &&
+                 (d.RSB == 8 || d.RSB == 9),
+             "timeline build exists for N=32 matrix-core plans with 17..48-row BMTBs, KC 256/512 only");
     const device_arrays &a = d.replicas[0];
-    auto kern = d.seg_cap > 1 ? gsk::k_mfma_rows<2, 2, 9, 2, true> : gsk::k_mfma_rows<2, 2, 9, 1, true>;
+    const bool two = d.seg_cap > 1;
+    auto kern = d.maxr == 2 ? (d.RSB == 9 ? timeline_kernel<2, 9>(two) : timeline_kernel<2, 8>(two))
+                            : (d.RSB == 9 ? timeline_kernel<3, 9>(two) : timeline_kernel<3, 8>(two));
     const size_t lds = d.lds_bytes;
     HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));

@@ -16,8 +16,9 @@ from generalsparse_amd import datasets as ds  # noqa: E402
 
 M = K = 5120
 N = 32
+P0 = int(sys.argv[1]) if len(sys.argv) > 1 else 20  # rows per BMTB
 row, col, val = ds.pruned_weight(M, K, 0.7, 13)
-plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline("block_total", N, 20, 1).compile().upload("f16", 0)
+plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline("block_total", N, P0, 1).compile().upload("f16", 0)
 info = plan.info()
 B = torch.randn((K, N), device="cuda", dtype=torch.float16)
 C = torch.empty((M, N), device="cuda", dtype=torch.float16)
@@ -25,12 +26,12 @@ for _ in range(20):
     plan.spmm(B)
 torch.cuda.synchronize()
 L = _lib.load()
-nb = int(M / 20)
+nb = (M + P0 - 1) // P0 * info["ksplit"]
 st = (ctypes.c_uint64 * (nb * 64))()
 _lib.check(L.gs_debug_mfma_timeline(plan._h, ctypes.c_void_p(B.data_ptr()), ctypes.c_void_p(C.data_ptr()), N,
                                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream), st, nb * 64))
 a = np.frombuffer(st, dtype=np.uint64).reshape(nb, 64).astype(np.int64)
-nc = info["lds_chunks"]
+nc = (info["lds_chunks"] + info["ksplit"] - 1) // info["ksplit"]
 t0 = a[:, [0]]
 out = {"total_med": float(np.median(a[:, 63] - a[:, 0])), "total_max": float((a[:, 63] - a[:, 0]).max())}
 # slot layout (kernel_lib.hpp k_mfma_rows STAMPS): role r (0 compute, 1 B rows, 2 entries) in

@@ -1,5 +1,6 @@
 """Pretty-print gpurun_out/timeline.json (mfma_timeline.py output): per role and chunk,
-ticks of work and of waiting at the chunk's barrier."""
+ticks of work + ticks of waiting at the chunk's barrier (entry role: ticks to issue
+its loads + ticks of its scatter)."""
 import json
 import sys
 
