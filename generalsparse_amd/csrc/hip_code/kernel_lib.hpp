@@ -16,6 +16,8 @@
 //   k_block_rows     K6: one 256-thread workgroup per BMTB, wave reduce + LDS reduce
 //   k_bitmap_segment K2+K3: fixed 32-nnz BMTs, row segments from bitmaps, open
 //                       head/tail partials combined per wave, then atomics
+//   k_row_chunks     K5/K7: col-direction BMTs (chunks of one row), segmented
+//                       slot tree + a row carry per wave
 #pragma once
 
 #include <hip/hip_fp16.h>
@@ -453,9 +455,94 @@ __global__ __launch_bounds__(256) void k_bitmap_segment(const uint32_t *__restri
     }
 }
 
+// ---------------------------------------------------------------------------
+// K5 / K7 on col-direction plans (fixed_interval_col_direction_thread_blocking_
+// operator + thread_total_reduce + warp_bit_map_operator / tblock_thread_bit_map_
+// operator; token_test.cc:1250-1315, 1515-1582).  Every BMT is a chunk of ONE
+// row, so a row is a run of consecutive BMTs.  A wave owns U consecutive BMTs
+// and walks them S = 64/X at a time, one BMT per X-lane slot.  Equal-row slots
+// are summed by a segmented shuffle tree (the row-equality-guarded __shfl_down
+// of warp_bit_map_reduce_token.cc), the run reaching the end of a group is
+// carried in registers into the next group, and a row is written once it
+// closes: a plain store when the row lies inside the wave's range, fp32 atomics
+// into `ws` when a neighbouring wave shares it (k_finalize_rows then rounds
+// those rows and writes the empty ones).
+// ---------------------------------------------------------------------------
+template <class VT, class CT, int CF, int SCF>
+__global__ __launch_bounds__(256) void k_row_chunks(const uint32_t *__restrict__ bmt_nz,   // n_bmt+1
+                                                    const uint32_t *__restrict__ bmt_row,  // n_bmt
+                                                    const CT *__restrict__ col, const VT *__restrict__ val,
+                                                    const VT *__restrict__ B, VT *__restrict__ C,
+                                                    float *__restrict__ ws, uint32_t n_bmt, uint32_t U, uint32_t N,
+                                                    uint32_t X, uint32_t row_base) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t xl = lane & (X - 1u);
+    const uint32_t slot = lane / X;
+    const uint32_t S = 64u / X;
+    const uint32_t waves_total = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t ct = blockIdx.y; ct * X * CF < N; ct += gridDim.y) {
+        const uint32_t cw = ct * X * CF + xl * CF;
+        const bool cok = cw < N;
+        const uint32_t c0 = cok ? cw : 0u;
+        for (uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); (size_t)w * U < n_bmt;
+             w += waves_total) {
+            const uint32_t r0 = w * U, r1 = min(r0 + U, n_bmt);
+            const uint32_t first_row = bmt_row[r0], last_row = bmt_row[r1 - 1];
+            const bool head_shared = r0 > 0 && bmt_row[r0 - 1] == first_row;
+            const bool tail_shared = r1 < n_bmt && bmt_row[r1] == last_row;
+            float carry[CF];
+#pragma unroll
+            for (int k = 0; k < CF; k++) carry[k] = 0.f;
+            uint32_t carry_row = 0xffffffffu;
+            for (uint32_t g = r0; g < r1; g += S) {
+                const uint32_t bt = g + slot;
+                const bool valid = bt < r1;
+                const uint32_t row = valid ? bmt_row[bt] : 0xfffffffeu;
+                float acc[CF];
+#pragma unroll
+                for (int k = 0; k < CF; k++) acc[k] = 0.f;
+                if (valid) wave_row<VT, CT, CF, SCF>(bmt_nz[bt], bmt_nz[bt + 1], col, val, B, N, c0, 0u, 1u, acc);
+                // segmented suffix sums: the first slot of each run ends with the run total
+                for (uint32_t off = 1; off < S; off <<= 1) {
+                    const uint32_t rn = __shfl_down(row, off * X, 64);
+                    float v[CF];
+#pragma unroll
+                    for (int k = 0; k < CF; k++) v[k] = __shfl_down(acc[k], off * X, 64);
+                    if (slot + off < S && rn == row) {
+#pragma unroll
+                        for (int k = 0; k < CF; k++) acc[k] += v[k];
+                    }
+                }
+                const uint32_t rp = __shfl_up(row, X, 64);
+                const bool is_head = valid && (slot == 0 || rp != row);
+                if (slot == 0 && row == carry_row) {
+#pragma unroll
+                    for (int k = 0; k < CF; k++) acc[k] += carry[k];
+                }
+                const uint32_t nv = min(S, r1 - g);
+                const uint32_t lr = __shfl(row, (nv - 1) * X, 64);
+                const bool cont = g + S < r1 && bmt_row[g + S] == lr;
+                const unsigned long long hm = __ballot(is_head && row == lr);
+                const uint32_t hs = (uint32_t)__builtin_ctzll(hm) / X;
+#pragma unroll
+                for (int k = 0; k < CF; k++) carry[k] = __shfl(acc[k], hs * X + xl, 64);
+                carry_row = cont ? lr : 0xffffffffu;
+                if (is_head && !(cont && row == lr) && cok) {
+                    const size_t o = (size_t)(row_base + row) * N + cw;
+                    if ((row == first_row && head_shared) || (row == last_row && tail_shared))
+                        atomic_add_vals<float, CF>(ws + o, acc);
+                    else
+                        store_f32<VT, CF>(C + o, acc);
+                }
+            }
+        }
+    }
+}
 
+// ---------------------------------------------------------------------------
 // rows listed (shared between BMTs, or empty): C = fp16(workspace), workspace
-// re-zeroed for the next launch (companion of k_bitmap_segment with ws)
+// re-zeroed for the next launch (companion of k_bitmap_segment with ws and of
+// k_row_chunks)
 template <class VT>
 __global__ __launch_bounds__(256) void k_finalize_rows(const uint32_t *__restrict__ rows, uint32_t n_rows,
                                                        float *__restrict__ ws, VT *__restrict__ C, uint32_t N) {
@@ -1040,6 +1127,26 @@ inline std::vector<uint64_t> row_start_masks(const std::vector<uint64_t> &row, c
         mask[i] = mm;
     }
     return mask;
+}
+
+// k_row_chunks: BMTs per wave (enough waves to fill 256 CUs eight deep)
+inline uint32_t row_chunk_span(size_t n_bmt) {
+    const size_t u = (n_bmt + 8191) / 8192;
+    return (uint32_t)(u < 8 ? 8 : u);
+}
+
+// rows k_row_chunks leaves to k_finalize_rows: rows without BMTs and rows whose
+// BMTs straddle two waves' ranges (output rows = row_base + plan row)
+inline std::vector<uint32_t> row_chunk_finalize_rows(const std::vector<uint32_t> &bmt_row, uint64_t M, uint32_t U,
+                                                     uint32_t row_base) {
+    std::vector<uint8_t> fin(M, 1);
+    for (uint32_t r : bmt_row) fin[r + row_base] = 0;
+    for (size_t i = U; i < bmt_row.size(); i += U)
+        if (bmt_row[i] == bmt_row[i - 1]) fin[bmt_row[i] + row_base] = 1;
+    std::vector<uint32_t> list;
+    for (uint64_t r = 0; r < M; r++)
+        if (fin[r]) list.push_back((uint32_t)r);
+    return list;
 }
 
 }  // namespace gsk_host

@@ -88,6 +88,24 @@ void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1)
         ex.add_and_run(std::make_shared<warp_segment_reduce_operator>(cg, (unsigned)cf, false, false, ctx));
         ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)(nnz / 128 + 1),
                                                              std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
+    } else if (name == "warp_bit_map") {  // token_test.cc:1250-1315 (p0 = sparse_cf 4, p1 = cf 1)
+        int scf = p0 > 0 ? p0 : 4, cf = p1 > 0 ? p1 : 1;
+        ex.add_and_run(std::make_shared<fixed_interval_col_direction_thread_blocking_operator>(cg, 64, false, false,
+                                                                                               true, false, ctx));
+        int y = std::min(std::max(1, N / cf), 32), x = std::max(128 / y, 32);
+        set_config("VECTOR_WIDTH", x);
+        ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, true, scf, cf, ctx));
+        ex.add_and_run(std::make_shared<warp_bit_map_operator>(cg, (unsigned)cf, true, true, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)rows, std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
+    } else if (name == "tblock_bit_map") {  // token_test.cc:1515-1582 (p0 = sparse_cf 4, p1 = cf 1)
+        int scf = p0 > 0 ? p0 : 4, cf = p1 > 0 ? p1 : 1;
+        ex.add_and_run(std::make_shared<fixed_interval_col_direction_thread_blocking_operator>(cg, 64, false, false,
+                                                                                               true, false, ctx));
+        int x = std::min(std::max(1, N / cf), 32), y = 256 / x;
+        set_config("VECTOR_WIDTH", x);
+        ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, false, scf, cf, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)rows, std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
+        ex.add_and_run(std::make_shared<tblock_thread_bit_map_operator>(cg, (unsigned)cf, y, false, false, ctx));
     } else if (name == "block_total") {  // token_test.cc:1458-1514 (p0 = rows per BMTB, 1 there)
         int rb = p0 > 0 ? p0 : 1, cf = p1 > 0 ? p1 : 1;
         ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, rb, false, ctx));

@@ -18,6 +18,8 @@ const char *reduction_kind_name(reduction_kind k) {
         case reduction_kind::TOTAL_WARP_RESULT: return "total_warp_result_reduce_to_one_register_token";
         case reduction_kind::WARP_SEGMENT: return "warp_segment_reduce_token";
         case reduction_kind::TOTAL_BLOCK_RESULT: return "total_block_reduce_to_one_register_token";
+        case reduction_kind::WARP_BIT_MAP: return "warp_bit_map_reduce_token";
+        case reduction_kind::TBLOCK_BIT_MAP: return "tblock_bit_map_reduce_token";
         default: return "none";
     }
 }
@@ -28,6 +30,7 @@ const char *kernel_family_name(int f) {
         case KF_WARP_TOTAL: return "k_warp_rows";
         case KF_BLOCK_TOTAL: return "k_block_rows";
         case KF_BITMAP_SEGMENT: return "k_bitmap_segment";
+        case KF_ROW_CHUNKS: return "k_row_chunks";
         default: return "none";
     }
 }
@@ -36,6 +39,8 @@ std::string kernel_spec::name() const {
     std::string n = kernel_family_name(family);
     if (family == KF_BITMAP_SEGMENT && warp_segment) n += "+warp_segment";
     if (family == KF_WARP_TOTAL && tblock_parent) n += "+tblock";
+    if (family == KF_ROW_CHUNKS && bitmap_parent == WARP_META) n += "+warp_bit_map";
+    if (family == KF_ROW_CHUNKS && bitmap_parent == TBLOCK_META) n += "+tblock_bit_map";
     return n;
 }
 
@@ -63,7 +68,28 @@ void code_generator::compile() {
     const meta_data_set &m = *meta;
     auto tok = [&](POS_TYPE p) -> const reduction_token * { return tokens.count(p) ? &tokens.at(p) : nullptr; };
     const reduction_token *tt = tok(THREAD_META), *tw = tok(WARP_META), *tb = tok(TBLOCK_META);
-    if (tt && tt->kind == reduction_kind::THREAD_BIT_MAP) {
+    if (tt && tt->kind == reduction_kind::TOTAL_BMT_RESULT &&
+        m.is_exist(THREAD_META, "first_row_indices_without_ending", sub)) {
+        // col-direction BMTs (A10) summed per row: K5 warp_bit_map / K7 tblock_bit_map
+        s.family = KF_ROW_CHUNKS;
+        s.coarsen_factor = tt->coarsen_factor;
+        s.sparse_coarsen_factor = tt->sparse_coarsen_factor;
+        s.arrays = {"THREAD_META_first_nz_indices_0", "THREAD_META_first_row_indices_without_ending_0"};
+        if (tw && tw->kind == reduction_kind::WARP_BIT_MAP) {
+            s.bitmap_parent = WARP_META;
+            s.vector_width = tw->size;
+            for (auto k : {"WARP_META_first_row_indices_0", "WARP_META_first_nz_indices_0", "WARP_META_first_BMT_indices_0",
+                           "WARP_META_bit_map_of_thread_0"})
+                s.arrays.push_back(k);
+        } else if (tb && tb->kind == reduction_kind::TBLOCK_BIT_MAP) {
+            s.bitmap_parent = TBLOCK_META;
+            s.vector_width = tb->size;
+            for (auto k : {"TBLOCK_META_first_row_indices_0", "TBLOCK_META_first_nz_indices_0",
+                           "TBLOCK_META_first_BMT_indices_0", "THREAD_META_bit_map_of_thread_0",
+                           "THREAD_META_segment_offset_0"})
+                s.arrays.push_back(k);
+        }
+    } else if (tt && tt->kind == reduction_kind::THREAD_BIT_MAP) {
         s.family = KF_BITMAP_SEGMENT;
         s.warp_segment = tw && tw->kind == reduction_kind::WARP_SEGMENT;
         s.coarsen_factor = tt->coarsen_factor;
@@ -184,6 +210,17 @@ std::string code_generator::generate_kernel_file_source(int repeat) const {
             launch = "hipMemsetAsync(d_C, 0, M * N * sizeof(VT), 0); "
                      "gsk::k_bitmap_segment<VT, uint32_t, CF, SCF><<<dim3((n_units + 4 * (64 / X) - 1) / (4 * (64 / X)), tiles), 256, "
                      "4 * (64 / X) * 2 * X * CF * sizeof(float)>>>(d_a0, d_a1, d_m0, d_a2, d_a3, d_col, d_val, d_B, d_C, n_units, N, X, 0)";
+            break;
+        case KF_ROW_CHUNKS:
+            o << "    auto fn = rd(\"THREAD_META_first_nz_indices_0\"), fr = rd(\"THREAD_META_first_row_indices_without_ending_0\");\n"
+              << "    uint32_t *d_a0 = up(u32(fn)), *d_a1 = up(u32(fr));\n"
+              << "    const uint32_t n_units = fn.size() - 1, U = gsk_host::row_chunk_span(n_units); const bool al = true;\n"
+              << "    auto fin = gsk_host::row_chunk_finalize_rows(u32(fr), M, U, 0); uint32_t *d_a4 = up(fin);\n"
+              << "    float *d_ws; hipMalloc(&d_ws, M * N * sizeof(float)); hipMemset(d_ws, 0, M * N * sizeof(float));\n";
+            launch = "gsk::k_row_chunks<VT, uint32_t, CF, SCF><<<dim3(((n_units + U - 1) / U + 3) / 4, tiles), 256>>>("
+                     "d_a0, d_a1, d_col, d_val, d_B, d_C, d_ws, n_units, U, N, X, 0); "
+                     "if (!fin.empty()) gsk::k_finalize_rows<VT><<<dim3((fin.size() * N + 255) / 256), 256>>>("
+                     "d_a4, (uint32_t)fin.size(), d_ws, d_C, N)";
             break;
         default:
             throw gs_error("no family");

@@ -27,6 +27,8 @@ enum class reduction_kind {
     TOTAL_WARP_RESULT,     // total_warp_result_reduce_to_one_register_token (K4)
     WARP_SEGMENT,          // warp_segment_reduce_token (K3)
     TOTAL_BLOCK_RESULT,    // total_block_reduce_to_one_register_token (K6)
+    WARP_BIT_MAP,          // warp_bit_map_reduce_token (K5)
+    TBLOCK_BIT_MAP,        // tblock_bit_map_reduce_token (K7)
 };
 const char *reduction_kind_name(reduction_kind k);
 
@@ -45,6 +47,7 @@ enum kernel_family : int {
     KF_WARP_TOTAL = 2,      // one 64-lane wave per BMW (row block), nnz split over lane slots
     KF_BLOCK_TOTAL = 3,     // one workgroup per BMTB row block, LDS reduction
     KF_BITMAP_SEGMENT = 4,  // fixed-nnz BMTs, bitmap row segments, wave-level carry combine
+    KF_ROW_CHUNKS = 5,      // col-direction BMTs (chunks of one row), segmented slot tree + row carry
 };
 const char *kernel_family_name(int f);
 
@@ -56,6 +59,7 @@ struct kernel_spec {
     bool warp_segment = false;   // K3 present on top of K2
     bool tblock_parent = false;  // BMWs grouped into BMTBs
     bool row_sorted = false;     // GLOBAL original_nz_row_indices present
+    POS_TYPE bitmap_parent = THREAD_META;  // K5 (WARP) / K7 (TBLOCK) on col-direction BMTs
     std::array<unsigned, 2> ref_grid{{0, 0}}, ref_block{{0, 0}};
     std::vector<std::string> arrays;  // metadata keys the kernel consumes (= kernel arguments)
     std::string name() const;

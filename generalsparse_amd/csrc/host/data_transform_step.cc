@@ -266,6 +266,49 @@ void get_begin_nzs_of_BMT_after_fixed_blocking_in_row_direction::run(bool check)
     is_run = true;
 }
 
+// get_begin_rows_of_BMT_after_fixed_blocking_in_col_direction.cc:136-160: one entry
+// (the row index) per chunk of col_size nnz; empty rows get none; no ending
+void get_begin_rows_of_BMT_after_fixed_blocking_in_col_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    GS_CHECK(col_size > 0, "col_size > 0");
+    GS_CHECK(!m.is_exist(GLOBAL_META, "nz_row_indices_after_interlance_storage", s),
+             "col-direction blocking after interleaved storage");
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    uint64_t row_num = row_num_of_sub_matrix(m, s);
+    auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+    std::vector<uint64_t> fr;
+    for (uint64_t i = 0; i < row_num; i++) {
+        const uint64_t k = (cnt[i] + (uint64_t)col_size - 1) / (uint64_t)col_size;
+        for (uint64_t j = 0; j < k; j++) fr.push_back(i);
+    }
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(THREAD_META, "first_row_indices_without_ending", std::move(fr));
+    is_run = true;
+}
+
+// get_begin_nzs_of_BMT_after_fixed_blocking_in_col_direction.cc:124-150: chunk
+// offsets; a row's last chunk holds its remainder
+void get_begin_nzs_of_BMT_after_fixed_blocking_in_col_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    GS_CHECK(col_size > 0, "col_size > 0");
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    uint64_t row_num = row_num_of_sub_matrix(m, s);
+    auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+    std::vector<uint64_t> fn{0};
+    for (uint64_t i = 0; i < row_num; i++)
+        for (uint64_t left = cnt[i]; left > 0;) {
+            const uint64_t t = std::min<uint64_t>(left, (uint64_t)col_size);
+            fn.push_back(fn.back() + t);
+            left -= t;
+        }
+    GS_CHECK(fn.back() == row.size(), "first_nz_indices must end at nnz");
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(THREAD_META, "first_nz_indices", std::move(fn));
+    is_run = true;
+}
+
 namespace {
 std::vector<uint64_t> fixed_first_rows(uint64_t row_num, uint64_t rb) {
     std::vector<uint64_t> fr{0};
@@ -627,6 +670,72 @@ void get_begin_BMTs_after_merge_thread::run(bool check) {
     for (uint64_t j = 0; j + 1 < n; j += (uint64_t)merge_num) out.push_back(j);
     out.push_back(n - 1);
     replace_u(pos, "first_BMT_indices", std::move(out));
+    is_run = true;
+}
+
+// get_begin_{rows,nzs}_relative_to_parent_after_merge_thread.cc: offsets of each BMT
+// from the first BMT of its merged parent; the loop stops one short of the array
+// end, so over the ending-less row array the last BMT gets no entry (reference
+// behaviour).  Rows go to <pos>_..., nz offsets to THREAD_... (as the reference).
+static std::vector<uint64_t> relative_to_merged(const std::vector<uint64_t> &a, int k) {
+    std::vector<uint64_t> out;
+    for (uint64_t j = 0; j + 1 < a.size(); j += (uint64_t)k)
+        for (uint64_t i = j; i < j + (uint64_t)k && i + 1 < a.size(); i++) out.push_back(a[i] - a[j]);
+    return out;
+}
+static const char *relative_name(POS_TYPE pos, bool row) {
+    GS_CHECK(pos == WARP_META || pos == TBLOCK_META, "relative indices need a WARP or TBLOCK parent");
+    if (row)
+        return pos == WARP_META ? "first_row_indices_relative_to_BMW" : "first_row_indices_relative_to_BMTB";
+    return pos == WARP_META ? "first_nz_indices_relative_to_BMW" : "first_nz_indices_relative_to_BMTB";
+}
+void get_begin_rows_relative_to_parent_after_merge_thread::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const char *n = m.is_exist(THREAD_META, "first_row_indices", target_matrix_id) ? "first_row_indices"
+                                                                                   : "first_row_indices_without_ending";
+    replace_u(pos, relative_name(pos, true), relative_to_merged(m.u(THREAD_META, n, target_matrix_id), merge_num));
+    is_run = true;
+}
+void get_begin_nzs_relative_to_parent_after_merge_thread::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    replace_u(THREAD_META, relative_name(pos, false),
+              relative_to_merged(m.u(THREAD_META, "first_nz_indices", target_matrix_id), merge_num));
+    is_run = true;
+}
+
+// parent_bit_map_of_thread.cc: a BMT's bit is set when it starts a new row or a
+// new parent.  WARP: one word per VECTOR_WIDTH BMTs, bit t = BMT i+t (bits past
+// 64 shift out of the unsigned long, as in the reference).  TBLOCK: one 0/1 entry
+// per BMT under THREAD_META; the parent head at first_BMT_indices' ending (= the
+// BMT count) would be written one past the end in the reference and is skipped.
+void parent_bit_map_of_thread::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    const auto &fr = m.u(THREAD_META, "first_row_indices_without_ending", s);
+    const uint64_t n = fr.size();
+    std::vector<uint8_t> bit(n, 0);
+    if (n) bit[0] = 1;
+    for (uint64_t j = 1; j < n; j++) bit[j] = fr[j] != fr[j - 1];
+    std::vector<uint64_t> out;
+    if (pos == WARP_META) {
+        const uint64_t vw = (uint64_t)get_config().VECTOR_WIDTH;
+        GS_CHECK(vw >= 1, "VECTOR_WIDTH >= 1");
+        for (uint64_t i = 0; i < n; i += vw) bit[i] = 1;
+        for (uint64_t i = 0; i < n; i += vw) {
+            const uint64_t k = std::min(i + vw - 1, n - 1);
+            uint64_t map = 0;
+            for (uint64_t j = k + 1; j-- > i;) map = (map << 1) | bit[j];
+            out.push_back(map);
+        }
+        replace_u(WARP_META, "bit_map_of_thread", std::move(out));
+    } else {
+        GS_CHECK(pos == TBLOCK_META, "parent_bit_map_of_thread: parent must be WARP or TBLOCK");
+        for (uint64_t b : m.u(TBLOCK_META, "first_BMT_indices", s))
+            if (b < n) bit[b] = 1;
+        out.assign(bit.begin(), bit.end());
+        replace_u(THREAD_META, "bit_map_of_thread", std::move(out));
+    }
+    src(THREAD_META, "first_row_indices_without_ending");
     is_run = true;
 }
 

@@ -81,6 +81,10 @@ GS_DECLARE_STEP_P(modify_row_indices_by_nnz_pad, int, nnz_target)
 GS_DECLARE_STEP_P(get_begin_rows_of_BMT_after_fixed_blocking_in_nnz_direction, int, nnz_per_BMT)
 GS_DECLARE_STEP_P(get_begin_nzs_of_BMT_after_fixed_blocking_in_nnz_direction, int, nnz_per_BMT)
 
+// fixed col-direction blocking (A10): every row cut into chunks of col_size nnz
+GS_DECLARE_STEP_P(get_begin_rows_of_BMT_after_fixed_blocking_in_col_direction, int, col_size)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMT_after_fixed_blocking_in_col_direction, int, col_size)
+
 // get_BMT_size_of_each_parent.cc (GLOBAL parent only on the shipped pipelines)
 class get_BMT_size_of_each_parent : public basic_data_transform_step {
   public:
@@ -148,6 +152,17 @@ class segment_ptr : public basic_data_transform_step {
 GS_DECLARE_MERGE(get_begin_rows_after_merge_thread)
 GS_DECLARE_MERGE(get_begin_nzs_after_merge_thread)
 GS_DECLARE_MERGE(get_begin_BMTs_after_merge_thread)
+GS_DECLARE_MERGE(get_begin_rows_relative_to_parent_after_merge_thread)
+GS_DECLARE_MERGE(get_begin_nzs_relative_to_parent_after_merge_thread)
+
+// parent_bit_map_of_thread.cc (warp_bit_map_operator.cc / tblock_thread_bit_map_operator.cc)
+class parent_bit_map_of_thread : public basic_data_transform_step {
+  public:
+    parent_bit_map_of_thread(std::shared_ptr<meta_data_set> m, POS_TYPE pos, int target_matrix_id)
+        : basic_data_transform_step("parent_bit_map_of_thread", std::move(m), target_matrix_id), pos(pos) {}
+    void run(bool check) override;
+    POS_TYPE pos;
+};
 
 // balanced row-direction warp blocking (A11; data_transform_common.cc:934-989)
 GS_DECLARE_STEP_P(get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction, uint64_t, nnz_per_interval)

@@ -342,6 +342,100 @@ void balanced_interval_row_direction_warp_blocking_operator::run(bool check) {
     is_run = true;
 }
 
+// ------------------------------------------- col-direction THREAD blocking (A10)
+fixed_interval_col_direction_thread_blocking_operator::fixed_interval_col_direction_thread_blocking_operator(
+    cg_ptr cg, int fcs, bool rrel, bool nrel, bool pad_size, bool pad_max, ctx_ptr history)
+    : basic_operator("fixed_interval_col_direction_thread_blocking_operator", cg->get_metadata_set(),
+                     DISTRIBUTING_OP, cg->get_sub_matrix_id()),
+      fixed_col_block_size(fcs), row_index_is_relative_to_BMTB(false), nz_index_is_relative_to_BMTB(false),
+      is_padding_with_col_size_in_bmt(pad_size), is_col_padding_with_row_max_size_without_empty_row(pad_max),
+      code_generator_ptr(cg) {
+    GS_CHECK(fcs > 0, "fixed_col_block_size > 0");
+    // ...col_direction_thread_blocking_operator.cc:42-84: the padding level and the
+    // relative-index parent follow the distributing operators already run
+    auto d = history->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
+    bool warp = any_name(d, "warp"), tblock = any_name(d, "tblock");
+    if (warp) padding_pos = WARP_META;
+    else if (tblock) padding_pos = TBLOCK_META;
+    // relative flags name the parent found; with no parent they are unused
+    if (tblock && !warp) {
+        row_index_is_relative_to_BMTB = rrel;
+        nz_index_is_relative_to_BMTB = nrel;
+    }
+}
+
+// ...col_direction_thread_blocking_operator.cc:97-138
+bool fixed_interval_col_direction_thread_blocking_operator::is_valid_according_to_operator(ctx_ptr h) {
+    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return false;
+    auto d = h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
+    bool balanced_and_max_pad = any_name(d, "balanced_interval") && is_col_padding_with_row_max_size_without_empty_row;
+    return !any_name(d, "thread") && !any_name(d, "col") && !any_name(d, "interlance") && !balanced_and_max_pad;
+}
+
+// data_transform_common.cc:644-690 (padding_rate_valid_col_direction_with_multiple)
+static bool padding_rate_valid_col_direction_with_multiple(const meta_data_set &m, int fcs, int s) {
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    uint64_t row_num = row_num_of_sub_matrix(m, s);
+    auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+    const uint64_t orig = row.size();
+    uint64_t after = orig;
+    for (uint64_t c : cnt)
+        if (c % (uint64_t)fcs) {
+            after += (c / fcs + 1) * fcs - c;
+            if ((double)after / (double)orig >= (double)get_config().PADDING_RATE_UP_BOUND) return false;
+        }
+    return true;
+}
+
+// ...col_direction_thread_blocking_operator.cc:140-258
+bool fixed_interval_col_direction_thread_blocking_operator::is_valid_according_to_metadata() {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    bool ok = coo_present(m, s) && m.count_of_metadata_of_diff_pos(THREAD_META, s) == 0;
+    bool tb = m.is_exist(TBLOCK_META, "first_row_indices", s), wb = m.is_exist(WARP_META, "first_row_indices", s);
+    if (row_index_is_relative_to_BMTB) ok = ok && tb;
+    if (nz_index_is_relative_to_BMTB) ok = ok && m.is_exist(TBLOCK_META, "first_nz_indices", s);
+    if (is_col_padding_with_row_max_size_without_empty_row) {
+        if (padding_pos == TBLOCK_META) ok = ok && tb;
+        else if (padding_pos == WARP_META) ok = ok && wb;
+    }
+    if (tb) ok = ok && has_row_direction_blocking_in_specific_level(m, TBLOCK_META, s);
+    if (wb) ok = ok && has_row_direction_blocking_in_specific_level(m, WARP_META, s);
+    if (ok && is_padding_with_col_size_in_bmt)
+        ok = padding_rate_valid_col_direction_with_multiple(m, fixed_col_block_size, s);
+    return ok && !interlance_storage_existing(m, s);
+}
+
+// ...col_direction_thread_blocking_operator.cc:260-509; the no-parent branch
+// (the one token_test.cc:1258-1262 / 1524 exercises)
+void fixed_interval_col_direction_thread_blocking_operator::run(bool check) {
+    if (check) GS_CHECK(is_valid_according_to_metadata(), "col-direction thread blocking: invalid metadata");
+    if (has(TBLOCK_META, "first_row_indices") || has(WARP_META, "first_row_indices"))
+        throw gs_error("col-direction BMTs inside BMTB/BMW parents (former-operator re-run) are not built in this round");
+    if (is_col_padding_with_row_max_size_without_empty_row)
+        throw gs_error("col padding to the parent's max row size is not built in this round");
+    if (is_padding_with_col_size_in_bmt) {  // :313-326
+        modify_col_indices_by_col_pad_in_sub_matrix a(meta_data_set_ptr, target_matrix_id, fixed_col_block_size);
+        run_step(a, check);
+        modify_vals_by_col_pad_in_sub_matrix b(meta_data_set_ptr, target_matrix_id, fixed_col_block_size);
+        run_step(b, check);
+        modify_row_indices_by_col_pad_in_sub_matrix c(meta_data_set_ptr, target_matrix_id, fixed_col_block_size);
+        run_step(c, check);
+    }
+    get_begin_rows_of_BMT_after_fixed_blocking_in_col_direction e(meta_data_set_ptr, target_matrix_id,
+                                                                  fixed_col_block_size);
+    run_step(e, check);
+    get_begin_nzs_of_BMT_after_fixed_blocking_in_col_direction f(meta_data_set_ptr, target_matrix_id,
+                                                                 fixed_col_block_size);
+    run_step(f, check);
+    if (is_padding_with_col_size_in_bmt) {  // :477-482
+        get_BMT_size_of_each_parent g(meta_data_set_ptr, GLOBAL_META, target_matrix_id, false);
+        run_step(g, check);
+    }
+    code_generator_ptr->open_spec_level_of_paral(THREAD_META);
+    is_run = true;
+}
+
 // ------------------------------------------------------------- implementing
 thread_total_reduce_operator::thread_total_reduce_operator(cg_ptr cg, bool nwr, int scf, int cf, ctx_ptr)
     : basic_operator("thread_total_reduce_operator", cg->get_metadata_set(), IMPLEMENTING_OP,
@@ -500,6 +594,111 @@ void warp_segment_reduce_operator::run(bool check) {
     is_run = true;
 }
 
+// ------------------------------------------------ warp_bit_map_operator (K5)
+warp_bit_map_operator::warp_bit_map_operator(cg_ptr cg, unsigned cf, bool rnz, bool rrow, ctx_ptr)
+    : basic_operator("warp_bit_map_operator", cg->get_metadata_set(), IMPLEMENTING_OP, cg->get_sub_matrix_id()),
+      coarsen_factor(cf), relative_nz(rnz), relative_row(rrow), code_generator_ptr(cg) {
+    GS_CHECK(cf <= 16, "coarsen_factor <= 16");
+    code_generator_ptr->open_spec_level_of_paral(WARP_META);
+}
+
+// warp_bit_map_operator.cc:14-46: a thread-level distribution, no warp one, no nnz one
+bool warp_bit_map_operator::is_valid_according_to_operator(ctx_ptr h) {
+    auto d = h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
+    return !any_name(d, "nnz") && any_name(d, "thread") && !any_name(d, "warp");
+}
+
+bool warp_bit_map_operator::is_valid_according_to_metadata() {
+    return has(THREAD_META, "first_nz_indices") && !has(WARP_META, "first_nz_indices");
+}
+
+// warp_bit_map_operator.cc:69-109; merge_num = VECTOR_WIDTH
+void warp_bit_map_operator::run(bool check) {
+    GS_CHECK(is_valid_according_to_metadata(), "warp_bit_map: invalid metadata");
+    GS_CHECK(has(THREAD_META, "first_row_indices_without_ending"),
+             "warp_bit_map needs col-direction BMTs (parent_bit_map_of_thread.cc reads first_row_indices_without_ending)");
+    int vw = (int)get_config().VECTOR_WIDTH;
+    GS_CHECK(vw >= 1, "VECTOR_WIDTH >= 1");
+    get_begin_rows_after_merge_thread a(meta_data_set_ptr, WARP_META, vw, target_matrix_id);
+    run_step(a, check);
+    get_begin_nzs_after_merge_thread b(meta_data_set_ptr, WARP_META, vw, target_matrix_id);
+    run_step(b, check);
+    if (relative_row) {
+        get_begin_rows_relative_to_parent_after_merge_thread c(meta_data_set_ptr, WARP_META, vw, target_matrix_id);
+        run_step(c, check);
+    }
+    if (relative_nz) {
+        get_begin_nzs_relative_to_parent_after_merge_thread c(meta_data_set_ptr, WARP_META, vw, target_matrix_id);
+        run_step(c, check);
+    }
+    get_begin_BMTs_after_merge_thread e(meta_data_set_ptr, WARP_META, vw, target_matrix_id);
+    run_step(e, check);
+    parent_bit_map_of_thread f(meta_data_set_ptr, WARP_META, target_matrix_id);
+    run_step(f, check);
+    reduction_token t;
+    t.kind = reduction_kind::WARP_BIT_MAP;
+    t.coarsen_factor = (int)coarsen_factor;
+    t.size = vw;
+    code_generator_ptr->set_reduction_token(WARP_META, t);
+    code_generator_ptr->open_spec_level_of_paral(WARP_META);
+    is_run = true;
+}
+
+// ------------------------------------------ tblock_thread_bit_map_operator (K7)
+tblock_thread_bit_map_operator::tblock_thread_bit_map_operator(cg_ptr cg, unsigned cf, int bs, bool rnz, bool rrow,
+                                                               ctx_ptr)
+    : basic_operator("tblock_thread_bit_map_operator", cg->get_metadata_set(), IMPLEMENTING_OP,
+                     cg->get_sub_matrix_id()),
+      coarsen_factor(cf), block_size(bs), relative_nz(rnz), relative_row(rrow), code_generator_ptr(cg) {
+    GS_CHECK(cf <= 16, "coarsen_factor <= 16");
+    GS_CHECK(bs >= 1, "block_size >= 1");
+    code_generator_ptr->open_spec_level_of_paral(TBLOCK_META);
+}
+
+// tblock_thread_bit_map_operator.cc:14-46
+bool tblock_thread_bit_map_operator::is_valid_according_to_operator(ctx_ptr h) {
+    auto d = h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
+    return !any_name(d, "nnz") && any_name(d, "thread") && !any_name(d, "tblock");
+}
+
+bool tblock_thread_bit_map_operator::is_valid_according_to_metadata() { return has(THREAD_META, "first_nz_indices"); }
+
+// tblock_thread_bit_map_operator.cc:62-109; merge_num = block_size
+void tblock_thread_bit_map_operator::run(bool check) {
+    GS_CHECK(is_valid_according_to_metadata(), "tblock_thread_bit_map: invalid metadata");
+    GS_CHECK(has(THREAD_META, "first_row_indices_without_ending"),
+             "tblock_thread_bit_map needs col-direction BMTs (parent_bit_map_of_thread.cc)");
+    get_begin_rows_after_merge_thread a(meta_data_set_ptr, TBLOCK_META, block_size, target_matrix_id);
+    run_step(a, check);
+    get_begin_nzs_after_merge_thread b(meta_data_set_ptr, TBLOCK_META, block_size, target_matrix_id);
+    run_step(b, check);
+    if (relative_row) {
+        get_begin_rows_relative_to_parent_after_merge_thread c(meta_data_set_ptr, TBLOCK_META, block_size,
+                                                               target_matrix_id);
+        run_step(c, check);
+    }
+    if (relative_nz) {
+        get_begin_nzs_relative_to_parent_after_merge_thread c(meta_data_set_ptr, TBLOCK_META, block_size,
+                                                              target_matrix_id);
+        run_step(c, check);
+    }
+    get_begin_BMTs_after_merge_thread e(meta_data_set_ptr, TBLOCK_META, block_size, target_matrix_id);
+    run_step(e, check);
+    parent_bit_map_of_thread f(meta_data_set_ptr, TBLOCK_META, target_matrix_id);
+    run_step(f, check);
+    // segment_offset(meta, TBLOCK_META, block_size): the POS_TYPE argument lands in the
+    // bool parent_flag parameter (TBLOCK_META = -98, i.e. true)
+    segment_offset g(meta_data_set_ptr, true, block_size, target_matrix_id);
+    run_step(g, check);
+    reduction_token t;
+    t.kind = reduction_kind::TBLOCK_BIT_MAP;
+    t.coarsen_factor = (int)coarsen_factor;
+    t.size = block_size;
+    code_generator_ptr->set_reduction_token(TBLOCK_META, t);
+    code_generator_ptr->open_spec_level_of_paral(TBLOCK_META);
+    is_run = true;
+}
+
 grid_block_operator::grid_block_operator(cg_ptr cg, unsigned grid_x, std::vector<unsigned> blk, unsigned cf, ctx_ptr)
     : basic_operator("grid_block_operator", cg->get_metadata_set(), IMPLEMENTING_OP, cg->get_sub_matrix_id()),
       code_generator_ptr(cg) {
@@ -554,6 +753,21 @@ std::shared_ptr<basic_operator> make_operator(const std::string &name, const std
         need(4);
         return std::make_shared<fixed_interval_nnz_direction_thread_blocking_operator>(cg, (int)a[0], a[1] != 0,
                                                                                        a[2] != 0, a[3] != 0, ctx);
+    }
+    if (name == "fixed_interval_col_direction_thread_blocking_operator") {
+        need(5);  // fixed_col_block_size, row_relative, nz_relative, pad_to_multiple, pad_to_parent_max
+        return std::make_shared<fixed_interval_col_direction_thread_blocking_operator>(cg, (int)a[0], a[1] != 0,
+                                                                                       a[2] != 0, a[3] != 0,
+                                                                                       a[4] != 0, ctx);
+    }
+    if (name == "warp_bit_map_operator") {
+        need(3);
+        return std::make_shared<warp_bit_map_operator>(cg, (unsigned)a[0], a[1] != 0, a[2] != 0, ctx);
+    }
+    if (name == "tblock_thread_bit_map_operator") {
+        need(4);
+        return std::make_shared<tblock_thread_bit_map_operator>(cg, (unsigned)a[0], (int)a[1], a[2] != 0, a[3] != 0,
+                                                                ctx);
     }
     if (name == "balanced_interval_row_direction_warp_blocking_operator") {
         need(3);

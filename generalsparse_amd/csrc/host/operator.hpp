@@ -163,6 +163,31 @@ class balanced_interval_row_direction_warp_blocking_operator : public basic_oper
     cg_ptr code_generator_ptr;
 };
 
+// operator/fixed_interval_col_direction_thread_blocking_operator.cc (A10): BMTs are
+// chunks of fixed_col_block_size nnz along each row
+class fixed_interval_col_direction_thread_blocking_operator : public basic_operator {
+  public:
+    fixed_interval_col_direction_thread_blocking_operator(cg_ptr cg, int fixed_col_block_size,
+                                                          bool row_index_is_relative, bool nz_index_is_relative,
+                                                          bool is_padding_with_col_size_in_bmt,
+                                                          bool is_col_padding_with_row_max_size_without_empty_row,
+                                                          ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    void set_padding_to_false() override {
+        is_padding_with_col_size_in_bmt = false;
+        is_col_padding_with_row_max_size_without_empty_row = false;
+    }
+    int fixed_col_block_size;
+    bool row_index_is_relative_to_BMTB, nz_index_is_relative_to_BMTB;
+    bool is_padding_with_col_size_in_bmt, is_col_padding_with_row_max_size_without_empty_row;
+    POS_TYPE padding_pos = GLOBAL_META;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
 // -------------------------------------------------------------- IMPLEMENTING
 class thread_total_reduce_operator : public basic_operator {
   public:
@@ -224,6 +249,36 @@ class warp_segment_reduce_operator : public basic_operator {
     bool is_valid_according_to_metadata() override;
     bool is_valid_according_to_operator(ctx_ptr h) override;
     unsigned coarsen_factor;
+    bool relative_nz, relative_row;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
+// operator/warp_bit_map_operator.cc (K5): BMWs of VECTOR_WIDTH col-direction BMTs
+class warp_bit_map_operator : public basic_operator {
+  public:
+    warp_bit_map_operator(cg_ptr cg, unsigned coarsen_factor, bool relative_nz, bool relative_row, ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    unsigned coarsen_factor;
+    bool relative_nz, relative_row;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
+// operator/tblock_thread_bit_map_operator.cc (K7): BMTBs of block_size BMTs
+class tblock_thread_bit_map_operator : public basic_operator {
+  public:
+    tblock_thread_bit_map_operator(cg_ptr cg, unsigned coarsen_factor, int block_size, bool relative_nz,
+                                   bool relative_row, ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    unsigned coarsen_factor;
+    int block_size;
     bool relative_nz, relative_row;
 
   private:

@@ -532,6 +532,25 @@ void upload_plan(plan_state &p, int dtype, int device) {
             }
             break;
         }
+        case KF_ROW_CHUNKS: {
+            const auto &fn = m.u(THREAD_META, "first_nz_indices", 0);
+            const auto &fr = m.u(THREAD_META, "first_row_indices_without_ending", 0);
+            GS_CHECK(fn.size() == fr.size() + 1 && !fr.empty(), "col-direction plan: BMT arrays disagree");
+            std::vector<uint32_t> br = to_u32(fr, "first_row_indices_without_ending");
+            a.a0 = dev_copy(d, to_u32(fn, "first_nz_indices"));
+            a.a1 = dev_copy(d, br);
+            d.n_units = br.size();
+            d.scf = 4;
+            d.span = gsk_host::row_chunk_span(br.size());
+            // rows shared by two waves' BMT ranges accumulate in an fp32 workspace; the
+            // finalize pass rounds them and writes the rows without BMTs (no memset)
+            std::vector<uint32_t> list = gsk_host::row_chunk_finalize_rows(br, p.M, d.span, (uint32_t)d.row_base);
+            d.ws_n = (uint32_t)std::max<int64_t>(1, get_config().DENSE_MATRIX_SIZE);
+            a.ws = dev_copy(d, std::vector<float>((size_t)p.M * d.ws_n, 0.f));
+            if (!list.empty()) a.a4 = dev_copy(d, list);
+            d.n_fin = list.size();
+            break;
+        }
         default:
             throw gs_error("no gfx950 kernel family for this plan");
     }
@@ -763,6 +782,21 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
                                lds, s, a.a0, a.a1, a.m0, a.a2, a.a3, col, val, B, C, (uint32_t)d.n_units, N, X,
                                row_base, use_ws ? a.ws : (float *)nullptr);
             if (use_ws && d.n_fin) {
+                HIP_OK(hipGetLastError());
+                const uint32_t fx = (uint32_t)std::min<uint64_t>((d.n_fin * N + 255) / 256, 4096);
+                hipLaunchKernelGGL((gsk::k_finalize_rows<VT>), dim3(fx), dim3(256), 0, s, a.a4, (uint32_t)d.n_fin,
+                                   a.ws, C, N);
+            }
+            break;
+        }
+        case KF_ROW_CHUNKS: {
+            GS_CHECK(N <= d.ws_n, "col-direction plan built for N=" + std::to_string(d.ws_n) +
+                                      ": its workspace holds no wider B (re-run the pipeline for this N)");
+            const uint32_t nw = (uint32_t)((d.n_units + d.span - 1) / d.span);
+            const uint32_t gx = std::min<uint32_t>((nw + 3) / 4, 1u << 16);
+            hipLaunchKernelGGL((gsk::k_row_chunks<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
+                               a.a0, a.a1, col, val, B, C, a.ws, (uint32_t)d.n_units, d.span, N, X, row_base);
+            if (d.n_fin) {
                 HIP_OK(hipGetLastError());
                 const uint32_t fx = (uint32_t)std::min<uint64_t>((d.n_fin * N + 255) / 256, 4096);
                 hipLaunchKernelGGL((gsk::k_finalize_rows<VT>), dim3(fx), dim3(256), 0, s, a.a4, (uint32_t)d.n_fin,

@@ -623,6 +623,133 @@ int or_warp_segment_operator(or_set *s, int vw) {
     return 0;
 }
 
+/* ------------------------------------------------------------------ */
+/* A10: fixed_interval_col_direction_thread_blocking_operator, no-parent */
+/* branch (operator/...col_direction_thread_blocking_operator.cc:285-509) */
+/* ------------------------------------------------------------------ */
+
+int or_col_dir_thread_blocking(or_set *s, int col_size, int pad) {
+    if (col_size < 1) return fail(s, "fixed_col_block_size < 1");
+    if (exists(s, "TBLOCK_META", "first_row_indices", 0) || exists(s, "WARP_META", "first_row_indices", 0))
+        return fail(s, "oracle restates the no-parent branch only");
+    /* :313-326 -> modify_{col,val,row}_by_col_pad_in_sub_matrix (A6); the
+     * padding-rate rule is data_transform_common.cc:644-690 */
+    if (pad && col_pad(s, col_size)) return -1;
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    uint64_t nnz = R->len, row_num = row_num_of(s);
+    uint64_t *cnt = row_nnz(R->u, nnz, row_num);
+    /* get_begin_rows_of_BMT_after_fixed_blocking_in_col_direction.cc:136-160 */
+    vu fr = {0};
+    for (uint64_t i = 0; i < row_num; i++) {
+        uint64_t k = cnt[i] / col_size;
+        if (cnt[i] % col_size != 0) k = k + 1;
+        for (uint64_t j = 0; j < k; j++) vu_push(&fr, i);
+    }
+    /* get_begin_nzs_of_BMT_after_fixed_blocking_in_col_direction.cc:124-150 */
+    vu fn = {0};
+    vu_push(&fn, 0);
+    for (uint64_t i = 0; i < row_num; i++) {
+        int64_t remain = (int64_t)cnt[i];
+        while (remain > 0) {
+            if (remain < col_size) { vu_push(&fn, fn.p[fn.n - 1] + remain); remain = 0; }
+            else { vu_push(&fn, fn.p[fn.n - 1] + col_size); remain -= col_size; }
+        }
+    }
+    free(cnt);
+    put_u(s, "THREAD_META", "first_row_indices_without_ending", 0, fr.p, fr.n);
+    put_u(s, "THREAD_META", "first_nz_indices", 0, fn.p, fn.n);
+    /* :477-482 get_BMT_size_of_each_parent (GLOBAL): one size when all equal */
+    if (pad) {
+        uint64_t size0 = fn.p[1] - fn.p[0];
+        int same = 1;
+        for (uint64_t i = 0; i + 1 < fn.n; i++)
+            if (fn.p[i + 1] - fn.p[i] != size0) { same = 0; break; }
+        if (same) put_scalar(s, "GLOBAL_META", "BMT_size_of_each_blk", 0, size0);
+    }
+    return 0;
+}
+
+/* warp_bit_map_operator.cc:69-109 (pos_is_warp = 1, merge = VECTOR_WIDTH) and
+ * tblock_thread_bit_map_operator.cc:62-109 (pos_is_warp = 0, merge = block_size):
+ * get_begin_{rows,nzs}_after_merge_thread.cc, the relative variants
+ * get_begin_{rows,nzs}_relative_to_parent_after_merge_thread.cc,
+ * get_begin_BMTs_after_merge_thread.cc, parent_bit_map_of_thread.cc and, for
+ * the TBLOCK parent, segment_offset.cc (parent_flag = true: the POS_TYPE
+ * argument TBLOCK_META = -98 converts to true). */
+int or_parent_bit_map_operator(or_set *s, int pos_is_warp, int merge, int rel_nz, int rel_row) {
+    const char *pos = pos_is_warp ? "WARP_META" : "TBLOCK_META";
+    or_array *TR = get(s, "THREAD_META", "first_row_indices_without_ending", 0);
+    or_array *TN = get(s, "THREAD_META", "first_nz_indices", 0);
+    if (!TR || !TN || merge < 1) return fail(s, "bit-map operator: needs col-direction BMTs");
+    vu pr = {0}, pn = {0}, pb = {0};
+    for (uint64_t j = 0; j + 1 < TR->len; j += merge) vu_push(&pr, TR->u[j]);
+    vu_push(&pr, TR->u[TR->len - 1]);
+    for (uint64_t j = 0; j + 1 < TN->len; j += merge) vu_push(&pn, TN->u[j]);
+    vu_push(&pn, TN->u[TN->len - 1]);
+    put_u(s, pos, "first_row_indices", 0, pr.p, pr.n);
+    put_u(s, pos, "first_nz_indices", 0, pn.p, pn.n);
+    TR = get(s, "THREAD_META", "first_row_indices_without_ending", 0);
+    TN = get(s, "THREAD_META", "first_nz_indices", 0);
+    if (rel_row) { /* loop bound len-1: the last BMT gets no entry */
+        vu rr = {0};
+        for (uint64_t j = 0; j + 1 < TR->len; j += merge)
+            for (uint64_t i = j; i < j + merge && i + 1 < TR->len; i++) vu_push(&rr, TR->u[i] - TR->u[j]);
+        put_u(s, pos, pos_is_warp ? "first_row_indices_relative_to_BMW" : "first_row_indices_relative_to_BMTB", 0,
+              rr.p, rr.n);
+        TR = get(s, "THREAD_META", "first_row_indices_without_ending", 0);
+        TN = get(s, "THREAD_META", "first_nz_indices", 0);
+    }
+    if (rel_nz) {
+        vu rn = {0};
+        for (uint64_t j = 0; j + 1 < TN->len; j += merge)
+            for (uint64_t i = j; i < j + merge && i + 1 < TN->len; i++) vu_push(&rn, TN->u[i] - TN->u[j]);
+        put_u(s, "THREAD_META", pos_is_warp ? "first_nz_indices_relative_to_BMW" : "first_nz_indices_relative_to_BMTB",
+              0, rn.p, rn.n);
+        TR = get(s, "THREAD_META", "first_row_indices_without_ending", 0);
+        TN = get(s, "THREAD_META", "first_nz_indices", 0);
+    }
+    for (uint64_t j = 0; j + 1 < TN->len; j += merge) vu_push(&pb, j);
+    vu_push(&pb, TN->len - 1);
+    put_u(s, pos, "first_BMT_indices", 0, pb.p, pb.n);
+    TR = get(s, "THREAD_META", "first_row_indices_without_ending", 0);
+    /* parent_bit_map_of_thread.cc */
+    uint64_t n = TR->len;
+    unsigned char *bit = (unsigned char *)calloc(n ? n : 1, 1);
+    bit[0] = 1;
+    for (uint64_t j = 1; j < n; j++) bit[j] = TR->u[j] != TR->u[j - 1];
+    if (pos_is_warp) {
+        for (uint64_t i = 0; i < n; i += merge) bit[i] = 1;
+        vu bm = {0};
+        for (uint64_t i = 0; i < n; i += merge) {
+            uint64_t k = (i + merge - 1) > (n - 1) ? (n - 1) : (i + merge - 1);
+            uint64_t map = 0;
+            for (uint64_t j = k;; j--) {
+                map = (map << 1) | bit[j];
+                if (j == i) break;
+            }
+            vu_push(&bm, map);
+        }
+        put_u(s, "WARP_META", "bit_map_of_thread", 0, bm.p, bm.n);
+    } else {
+        or_array *FB = get(s, "TBLOCK_META", "first_BMT_indices", 0);
+        for (uint64_t i = 0; i < FB->len; i++)
+            if (FB->u[i] < n) bit[FB->u[i]] = 1; /* the ending (= n) lands past the end in the reference */
+        uint64_t *bm = (uint64_t *)malloc(n * 8);
+        for (uint64_t i = 0; i < n; i++) bm[i] = bit[i];
+        put_u(s, "THREAD_META", "bit_map_of_thread", 0, bm, n);
+        /* segment_offset.cc with parent_flag = true, size = block_size */
+        uint64_t *so = (uint64_t *)calloc(n ? n : 1, 8);
+        uint64_t count = 0, prev = 0;
+        for (uint64_t j = 1; j < n; j++) {
+            if (bit[j] == 0 && (j % (uint64_t)merge != 0)) count++;
+            else { so[prev] = count; count = 0; prev = j; }
+        }
+        put_u(s, "THREAD_META", "segment_offset", 0, so, n);
+    }
+    free(bit);
+    return 0;
+}
+
 /* A11: balanced_interval_row_direction_warp_blocking_operator, no-parent
  * branch; split points data_transform_common.cc:934-989 */
 int or_balanced_row_dir_warp_blocking(or_set *s, uint64_t per) {
@@ -678,6 +805,14 @@ int or_pipeline(or_set *s, const char *name, int p0, int p1) {
     if (!strcmp(name, "tblock_warp_total")) { /* tblock rows p0 + BMW rows p1 (default 1) + warp_total */
         if (or_row_dir_tblock_blocking(s, p0)) return -1;
         return or_row_dir_warp_blocking(s, p1 > 0 ? p1 : 1);
+    }
+    if (!strcmp(name, "warp_bit_map")) { /* token_test.cc:1250-1315, p0 = VW = max(128/min(N/cf,32), 32) */
+        if (or_col_dir_thread_blocking(s, 64, 1)) return -1;
+        return or_parent_bit_map_operator(s, 1, p0, 1, 1);
+    }
+    if (!strcmp(name, "tblock_bit_map")) { /* token_test.cc:1515-1582, p0 = block_size = 256/min(N/cf,32) */
+        if (or_col_dir_thread_blocking(s, 64, 1)) return -1;
+        return or_parent_bit_map_operator(s, 0, p0, 0, 0);
     }
     if (!strcmp(name, "balanced_warp_total")) /* A11 balanced BMW + warp_total */
         return or_balanced_row_dir_warp_blocking(s, (uint64_t)p0);

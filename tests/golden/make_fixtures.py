@@ -124,7 +124,89 @@ cases.append({
 # ex1 ends with an empty row: the balanced row splitter asserts (:984)
 cases.append({"matrix": "ex1", "pipeline": "balanced_warp_total", "p0": 4, "expect_error": True})
 
-out = {"matrices": {"ex1": EX1, "ex2": EX2}, "cases": cases}
+# ex3: 4x200; row0 cols 0..99 (100 nnz), row1 empty, row2 cols 0..29, row3 cols 0..63
+EX3 = {
+    "M": 4, "K": 200,
+    "entries": [(0, c) for c in range(100)] + [(2, c) for c in range(30)] + [(3, c) for c in range(64)],
+}
+# ex4: 3x700; row0 cols 0..599 (600 nnz), row1 cols 0..9, row2 empty (trailing)
+EX4 = {
+    "M": 3, "K": 700,
+    "entries": [(0, c) for c in range(600)] + [(1, c) for c in range(10)],
+}
+
+# warp_bit_map (token_test.cc:1250-1315), N=32 cf=1 -> y=32, VW = x = max(128/32, 32) = 32
+# col-direction blocking of 64 with padding (fixed_interval_col_direction_..._operator.cc:313-326):
+# rows 100 -> 128 (pads repeat col 99, val 0), 30 -> 64, 64 stays, empty row stays empty
+# BMT rows (get_begin_rows_of_BMT_after_fixed_blocking_in_col_direction.cc): one per 64-chunk,
+# no ending -> [0, 0, 2, 3]; BMT nzs -> [0, 64, 128, 192, 256]; GLOBAL BMT size 64
+# merge by 32 (get_begin_*_after_merge_thread.cc): rows [fr[0], fr[last]] = [0, 3]
+# relative rows stop at len-1 (last BMT dropped): [0, 0, 2]; relative nzs [0, 64, 128, 192]
+# bit_map_of_thread (parent_bit_map_of_thread.cc): bits [1, 0, 1, 1] (+ forced bit 0),
+# packed from the group's last BMT down: 0b1101 = 13
+cases.append({
+    "matrix": "ex3", "pipeline": "warp_bit_map", "p0": 32,
+    "expect": {
+        G + "nz_row_indices_0": [0] * 128 + [2] * 64 + [3] * 64,
+        G + "nz_col_indices_0": list(range(100)) + [99] * 28 + list(range(30)) + [29] * 34 + list(range(64)),
+        G + "BMT_size_of_each_blk_0": [64],
+        T + "first_row_indices_without_ending_0": [0, 0, 2, 3],
+        T + "first_nz_indices_0": [0, 64, 128, 192, 256],
+        W + "first_row_indices_0": [0, 3],
+        W + "first_nz_indices_0": [0, 256],
+        W + "first_row_indices_relative_to_BMW_0": [0, 0, 2],
+        T + "first_nz_indices_relative_to_BMW_0": [0, 64, 128, 192],
+        W + "first_BMT_indices_0": [0, 4],
+        W + "bit_map_of_thread_0": [13],
+    },
+})
+# same matrix, ex4: 600 -> 640 (10 BMTs), 10 -> 64 (1 BMT); rows [0]*10 + [1]
+# one 32-BMT group: bits 0 and 10 set -> 1 + 1024
+cases.append({
+    "matrix": "ex4", "pipeline": "warp_bit_map", "p0": 32,
+    "expect": {
+        T + "first_row_indices_without_ending_0": [0] * 10 + [1],
+        T + "first_nz_indices_0": [64 * i for i in range(11)] + [704],
+        W + "first_row_indices_0": [0, 1],
+        W + "first_nz_indices_0": [0, 704],
+        W + "first_row_indices_relative_to_BMW_0": [0] * 10,
+        T + "first_nz_indices_relative_to_BMW_0": [64 * i for i in range(11)],
+        W + "first_BMT_indices_0": [0, 11],
+        W + "bit_map_of_thread_0": [1025],
+    },
+})
+# tblock_bit_map (token_test.cc:1515-1582), N=32 cf=1 -> x=32, block_size = 256/32 = 8
+# ex4: merge by 8 -> rows [fr[0], fr[8], fr[10]] = [0, 0, 1]; nzs [0, 512, 704]; BMTs [0, 8, 11]
+# THREAD bit_map_of_thread: row starts [1,0,...,0,1] plus parent heads 0 and 8 (11 is past
+# the end) -> [1,0,0,0,0,0,0,0,1,0,1]
+# segment_offset.cc (parent_flag true, size 8): zeros between set bits, a run also
+# closing at every multiple of 8 -> so[0] = 7, so[8] = 1, others 0
+cases.append({
+    "matrix": "ex4", "pipeline": "tblock_bit_map", "p0": 8,
+    "expect": {
+        B + "first_row_indices_0": [0, 0, 1],
+        B + "first_nz_indices_0": [0, 512, 704],
+        B + "first_BMT_indices_0": [0, 8, 11],
+        T + "bit_map_of_thread_0": [1, 0, 0, 0, 0, 0, 0, 0, 1, 0, 1],
+        T + "segment_offset_0": [7, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0],
+    },
+})
+# ex3 through tblock_bit_map: one parent of 4 BMTs, bits [1, 0, 1, 1]; so = [1, 0, 0, 0]
+cases.append({
+    "matrix": "ex3", "pipeline": "tblock_bit_map", "p0": 8,
+    "expect": {
+        B + "first_row_indices_0": [0, 3],
+        B + "first_nz_indices_0": [0, 256],
+        B + "first_BMT_indices_0": [0, 4],
+        T + "bit_map_of_thread_0": [1, 0, 1, 1],
+        T + "segment_offset_0": [1, 0, 0, 0],
+    },
+})
+# ex1 rows of 2..5 nnz padded to 64: 256 / 11 >= PADDING_RATE_UP_BOUND (4): invalid
+# (padding_rate_valid_col_direction_with_multiple, data_transform_common.cc:644-690)
+cases.append({"matrix": "ex1", "pipeline": "warp_bit_map", "p0": 32, "expect_error": True})
+
+out = {"matrices": {"ex1": EX1, "ex2": EX2, "ex3": EX3, "ex4": EX4}, "cases": cases}
 path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hand_plans.json")
 with open(path, "w") as f:
     json.dump(out, f, indent=1)

@@ -79,6 +79,58 @@ def test_known_answer_all_ones(pipe, dtype):
     np.testing.assert_array_equal(C, np.repeat(nnz_row[:, None], N, axis=1))
 
 
+# col-direction pipelines (K5 warp_bit_map / K7 tblock_bit_map): BMTs are 64-nnz
+# chunks of one row, so the cases need rows long enough for the padding rule
+COL_PIPES = [("warp_bit_map", 4, 1), ("tblock_bit_map", 4, 1)]
+
+
+def col_cases():
+    yield "long", 300, 2000, *ds.random_rows(300, 2000, 150.0, seed=11, empty_frac=0.1)
+    r, c, v = ds.pruned_weight(256, 512, 0.7, 13)
+    yield "pruned", 256, 512, r, c, v
+    r, c, v = ds.two_four(96, 512, 30)
+    yield "2:4", 96, 512, r, c, v
+    # rows of 47 BMTs straddle several waves' ranges (fp32 workspace + finalize path)
+    rows = np.concatenate([np.zeros(3000, np.uint64), np.repeat(np.arange(1, 40, dtype=np.uint64), 70)])
+    cols = np.concatenate([np.arange(3000, dtype=np.uint64), np.tile(np.arange(70, dtype=np.uint64) * 7, 39)])
+    yield "ragged", 45, 3000, rows, cols, np.linspace(-1, 1, len(rows)).astype(np.float32)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f16"])
+@pytest.mark.parametrize("N", [8, 32, 13, 128])
+@pytest.mark.parametrize("pipe", COL_PIPES, ids=lambda p: p[0])
+def test_col_direction_matches_oracle(pipe, N, dtype):
+    name, p0, p1 = pipe
+    for case, M, K, row, col, val in col_cases():
+        plan, C, B = run(M, K, row, col, val, name, p0, p1, N, dtype)
+        assert plan.info()["kernel_name"].startswith("k_row_chunks"), plan.info()["kernel_name"]
+        v = val.astype(np.float16).astype(np.float32) if dtype == "f16" else val
+        ref = ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64")
+        check(C, ref, dtype)
+        # the workspace is re-zeroed by the finalize pass: a second launch agrees
+        C2 = plan.spmm(torch.from_numpy(B).to(DEV)).float().cpu().numpy()
+        check(C2, ref, dtype)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f16"])
+@pytest.mark.parametrize("pipe", COL_PIPES, ids=lambda p: p[0])
+def test_col_direction_known_answer(pipe, dtype):
+    name, p0, p1 = pipe
+    M, K, N = 200, 1500, 32
+    row, col, _ = ds.random_rows(M, K, 300.0, seed=9, empty_frac=0.1)
+    npdt = np.float16 if dtype == "f16" else np.float32
+    _, C, _ = run(M, K, row, col, np.ones(len(row), np.float32), name, p0, p1, N, dtype, B=np.ones((K, N), npdt))
+    nnz_row = np.bincount(row.astype(np.int64), minlength=M).astype(np.float32)
+    np.testing.assert_array_equal(C, np.repeat(nnz_row[:, None], N, axis=1))
+
+
+def test_col_direction_wider_B_is_refused():
+    row, col, val = ds.random_rows(64, 600, 100.0, seed=2)
+    plan = gsa.Plan.from_coo(64, 600, row, col, val).run_pipeline("warp_bit_map", 32, 4, 1).compile().upload("f16", 0)
+    with pytest.raises(gsa.GsError):
+        plan.spmm(torch.zeros((600, 64), device=DEV, dtype=torch.float16))
+
+
 def test_replicas_and_stream():
     M, K, N = 500, 400, 32
     row, col, val = ds.random_rows(M, K, 15.0, seed=3)

@@ -29,6 +29,10 @@ def oracle_params(name, N, p0, p1):
         return min(N, 32)
     if name == "thread_bit_map":
         return N // cf if N // cf < 32 else 32
+    if name == "warp_bit_map":  # token_test.cc:1277-1279
+        return max(128 // min(max(1, N // cf), 32), 32)
+    if name == "tblock_bit_map":  # token_test.cc:1546-1547
+        return 256 // min(max(1, N // cf), 32)
     return p0
 
 
@@ -67,7 +71,23 @@ def random_coo(M, K, density, seed, empty=0.2, trailing_empty=False):
 PIPES = [("thread_total", 32, 4, 1), ("thread_total", 8, 8, 1), ("warp_total", 32, 0, 1),
          ("block_total", 8, 0, 1), ("thread_bit_map", 32, 4, 1), ("thread_bit_map", 8, 4, 2),
          ("warp_segment", 32, 4, 1), ("warp_segment", 8, 4, 1), ("tblock_warp_total", 32, 4, 1),
-         ("tblock_warp_total", 32, 7, 1), ("balanced_warp_total", 32, 64, 1)]
+         ("tblock_warp_total", 32, 7, 1), ("balanced_warp_total", 32, 64, 1), ("warp_bit_map", 32, 4, 1),
+         ("tblock_bit_map", 32, 4, 1)]
+
+# col-direction pipelines need rows long enough for the 64-nnz padding rule
+COL_PIPES = [("warp_bit_map", 32, 4, 1), ("warp_bit_map", 8, 4, 2), ("warp_bit_map", 1, 4, 1),
+             ("tblock_bit_map", 32, 4, 1), ("tblock_bit_map", 128, 4, 1), ("tblock_bit_map", 2, 4, 1)]
+
+
+@pytest.mark.parametrize("pipe", COL_PIPES, ids=lambda p: f"{p[0]}-N{p[1]}-{p[3]}")
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_col_direction_plans_bit_exact(pipe, seed):
+    name, N, p0, p1 = pipe
+    M, K = 150 + 31 * seed, 400
+    r, c, v = random_coo(M, K, 0.25 + 0.1 * seed, seed, empty=0.1, trailing_empty=(seed == 2))
+    p = compare(M, K, r, c, v, name, N, p0, p1)
+    assert p is not None
+    p.compile()
 
 
 @pytest.mark.parametrize("pipe", PIPES, ids=lambda p: f"{p[0]}-N{p[1]}-{p[2]}-{p[3]}")
@@ -96,7 +116,8 @@ def test_plan_edge_shapes(pipe):
 def test_hand_derived_fixtures_through_product():
     g = json.load(open(GOLDEN))
     back = {"thread_total": (32, 4, 1), "warp_total": (32, 0, 1), "block_total": (8, 0, 1),
-            "tblock_warp_total": (32, 4, 1), "balanced_warp_total": (32, 16, 1)}
+            "tblock_warp_total": (32, 4, 1), "balanced_warp_total": (32, 16, 1),
+            "warp_bit_map": (32, 4, 1), "tblock_bit_map": (32, 4, 1)}
     for case in g["cases"]:
         m = g["matrices"][case["matrix"]]
         row = np.array([e[0] for e in m["entries"]], np.uint64)
@@ -206,6 +227,22 @@ def test_generate_program(tmp_path):
             "GLOBAL_META_original_nz_row_indices_0"} <= files
     fn = np.loadtxt(os.path.join(d, "THREAD_META_first_nz_indices_0"), dtype=np.uint64)
     np.testing.assert_array_equal(fn, p.array("THREAD_META_first_nz_indices_0"))
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc not installed")
+def test_generate_program_row_chunks_compiles(tmp_path):
+    """the emitted standalone program of a col-direction plan (K5) is valid HIP"""
+    M, K = 40, 300
+    r, c, v = random_coo(M, K, 0.4, 4)
+    p = product_plan(M, K, r, c, v, "warp_bit_map", 32, 4, 1)
+    p.compile()
+    d = p.generate_program(tmp_path, repeat=10)
+    src = open(os.path.join(d, "kernel_file.hip")).read()
+    assert "k_row_chunks" in src and "k_finalize_rows" in src
+    assert "WARP_META_bit_map_of_thread_0" in os.listdir(d)
+    import subprocess
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O1", "-std=c++17", "-c",
+                           "kernel_file.hip", "-o", "kernel_file.o"], cwd=d)
 
 
 def test_synthetic_generators_shapes():
