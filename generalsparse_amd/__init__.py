@@ -26,7 +26,7 @@ __all__ = ["Plan", "set_config", "GsError", "GS_F16", "GS_F32", "PIPELINES", "lo
 
 # token_test.cc pipelines (+ the two compositions this engine adds)
 PIPELINES = ("thread_total", "warp_total", "block_total", "thread_bit_map", "warp_segment",
-             "tblock_warp_total", "balanced_warp_total")
+             "tblock_warp_total", "balanced_warp_total", "warp_bit_map", "tblock_bit_map", "col_direction_nm")
 
 
 def load_library():

@@ -1098,6 +1098,176 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
 #undef GS_STAMP
 }
 
+// ---------------------------------------------------------------------------
+// k_nm_mfma -- fixed_interval_col_direction BMTs that are 2:4 panels
+//  on the sparse matrix cores:
+// v_smfmac_f32_16x16x64_f16 multiplies a 16x64 A tile stored as 16x32 values
+// plus 2-bit positions by a dense 64x16 B tile.
+//
+// Operand layout of the instruction (measured, scripts/probes/probe_smfmac.hip):
+// lane l holds A row l%16, dense k [16*(l/16), +16) of the 64-wide k-step as 8
+// values (two per aligned group of 4; idx bits [4g+1:4g] / [4g+3:4g+2] = the
+// positions of group g's two values, ascending); B lane l holds column l%16,
+// k [8*(l/16), +8) in elements 0-7 and k [32 + 8*(l/16), +8) in elements 8-15;
+// the accumulator is the 16x16 MFMA layout (column l%16, rows 4*(l/16)+i).
+//
+// HBM layout (device_plan.hip build_nm_panels): per row group of 64 rows (four
+// 16-row tiles) and k-step s a 4608-byte block: [tile rt][lane] 16 B of values,
+// then [lane] 8 B of positions (u16 per tile: tiles 0/1 in the low dword,
+// selected by abid 0/1, tiles 2/3 in the high dword).  Every wave load is one
+// coalesced 1 KB (or 512 B) request; A is read exactly once.
+//
+// Workgroup = 8 waves = two row groups (128 rows) x four k-phases: wave (rh, q)
+// takes k-step 4c+q of every 256-row chunk c of B.  B chunks are staged in LDS
+// (two buffers, 32-B pieces XOR-permuted by b_piece so the transposed reads
+// are conflict-free) by all 512 threads through registers, one chunk ahead;
+// each wave's A blocks are loaded two chunks ahead.  One barrier per chunk.
+// The four k-phase partial tiles are summed in a fixed order through LDS
+// ((q0 + q2) + (q1 + q3): deterministic) and stored as fp16.
+// ---------------------------------------------------------------------------
+typedef _Float16 h16v __attribute__((ext_vector_type(16)));
+constexpr int kNmWaves = 8;
+constexpr uint32_t kNmBlockBytes = 4608, kNmKC = 256;
+
+template <int CT>
+__global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *__restrict__ A,
+                                                           const f16 *__restrict__ B, f16 *__restrict__ C,
+                                                           uint32_t K, uint32_t S, uint32_t rows,
+                                                           uint32_t row_base) {
+    constexpr uint32_t N = 16 * CT, RB = 32 * CT, UB = 2 * CT;
+    constexpr uint32_t szB = kNmKC * RB;
+    constexpr uint32_t NTH = 64 * kNmWaves;
+    constexpr uint32_t NBU = szB / 16 / NTH;  // 16-B units of B per thread per chunk
+    static_assert(szB % (16 * NTH) == 0, "whole B units per thread");
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint32_t rh = wv >> 2, q = wv & 3u;
+    const uint32_t rg = blockIdx.x * 2u + rh;
+    const uint32_t nch = S / 4u;
+    const unsigned char *arow = A + (size_t)rg * S * kNmBlockBytes;
+
+    u32x4 a0v[4], a1v[4];
+    uint2 a0i, a1i;
+#define GS_NM_ALOAD(c, V, I)                                                                        \
+    {                                                                                             \
+        const uint32_t cc_ = min((uint32_t)(c), nch - 1u);                                        \
+        const unsigned char *blk_ = arow + (size_t)(4u * cc_ + q) * kNmBlockBytes;                \
+        _Pragma("unroll") for (int rt = 0; rt < 4; rt++) V[rt] =                                  \
+            *reinterpret_cast<const u32x4 *>(blk_ + rt * 1024u + lane * 16u);                     \
+        I = *reinterpret_cast<const uint2 *>(blk_ + 4096u + lane * 8u);                           \
+    }
+    u32x4 bs[NBU];
+#define GS_NM_BLOAD(c)                                                                              \
+    {                                                                                             \
+        _Pragma("unroll") for (uint32_t i = 0; i < NBU; i++) {                                    \
+            const uint32_t u = tid + i * NTH, k = u / UB;                                         \
+            const uint32_t kk = (uint32_t)(c) * kNmKC + k;                                        \
+            bs[i] = kk < K ? *reinterpret_cast<const u32x4 *>(B + (size_t)kk * N + (u % UB) * 8u) \
+                           : u32x4{0u, 0u, 0u, 0u};                                               \
+        }                                                                                         \
+    }
+#define GS_NM_BSTORE(c)                                                                             \
+    {                                                                                             \
+        unsigned char *lb_ = lds + ((uint32_t)(c) & 1u) * szB;                                    \
+        _Pragma("unroll") for (uint32_t i = 0; i < NBU; i++) {                                    \
+            const uint32_t u = tid + i * NTH, k = u / UB, s = u % UB;                             \
+            *reinterpret_cast<u32x4 *>(lb_ + k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u) = bs[i]; \
+        }                                                                                         \
+    }
+    f4v acc[4][CT];
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+    // chunk c's k-step for this wave: B rows 64q + [0, 64) of LDS buffer c&1
+#define GS_NM_COMPUTE(c, V, I)                                                                      \
+    {                                                                                             \
+        const unsigned char *lb_ = lds + ((uint32_t)(c) & 1u) * szB;                              \
+        h8v av_[4];                                                                               \
+        _Pragma("unroll") for (int rt = 0; rt < 4; rt++) __builtin_memcpy(&av_[rt], &V[rt], 16);  \
+        const int ix0_ = (int)I.x, ix1_ = (int)I.y;                                               \
+        _Pragma("unroll") for (int ct = 0; ct < CT; ct++) {                                       \
+            s4v t_[4];                                                                            \
+            _Pragma("unroll") for (int h = 0; h < 4; h++) {                                       \
+                const uint32_t k = 64u * q + 32u * (h >> 1) + 8u * (lane >> 4) + 4u * (h & 1) + ((lane & 15u) >> 2); \
+                t_[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(                                  \
+                    (lds_s4v *)(lb_ + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u));     \
+            }                                                                                     \
+            h16v bf_;                                                                             \
+            __builtin_memcpy(&bf_, t_, 32);                                                       \
+            acc[0][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[0], bf_, acc[0][ct], ix0_, 0, 0); \
+            acc[1][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[1], bf_, acc[1][ct], ix0_, 0, 1); \
+            acc[2][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[2], bf_, acc[2][ct], ix1_, 0, 0); \
+            acc[3][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[3], bf_, acc[3][ct], ix1_, 0, 1); \
+        }                                                                                         \
+    }
+    GS_NM_BLOAD(0u);
+    GS_NM_ALOAD(0u, a0v, a0i);
+    GS_NM_ALOAD(1u, a1v, a1i);
+    GS_NM_BSTORE(0u);
+    GS_NM_BLOAD(1u);
+    __syncthreads();
+    // iteration c: stage chunk c+1 (its buffer was last read in iteration c-1,
+    // before the barrier), fetch B of c+2, compute c, fetch A of c+2
+    uint32_t c = 0;
+    for (; c + 1 < nch; c += 2) {
+        GS_NM_BSTORE(c + 1u);
+        GS_NM_BLOAD(c + 2u < nch ? c + 2u : c + 1u);
+        GS_NM_COMPUTE(c, a0v, a0i);
+        GS_NM_ALOAD(c + 2u, a0v, a0i);
+        __syncthreads();
+        if (c + 2u < nch) GS_NM_BSTORE(c + 2u);
+        GS_NM_BLOAD(c + 3u < nch ? c + 3u : c + 1u);
+        GS_NM_COMPUTE(c + 1u, a1v, a1i);
+        GS_NM_ALOAD(c + 3u, a1v, a1i);
+        __syncthreads();
+    }
+    if (c < nch) GS_NM_COMPUTE(c, a0v, a0i);
+#undef GS_NM_COMPUTE
+#undef GS_NM_BSTORE
+#undef GS_NM_BLOAD
+#undef GS_NM_ALOAD
+    // fixed-order k-phase reduction: pass 1 q2 -> q0, q3 -> q1; pass 2 q1 -> q0
+    __syncthreads();
+    f4v *red = reinterpret_cast<f4v *>(lds);
+    constexpr uint32_t TW = 4 * CT * 64;  // f4v per wave
+    if (q >= 2) {
+#pragma unroll
+        for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) red[(rh * 2 + (q - 2)) * TW + (rt * CT + ct) * 64 + lane] = acc[rt][ct];
+    }
+    __syncthreads();
+    if (q < 2) {
+#pragma unroll
+        for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) acc[rt][ct] += red[(rh * 2 + q) * TW + (rt * CT + ct) * 64 + lane];
+    }
+    __syncthreads();
+    if (q == 1) {
+#pragma unroll
+        for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) red[rh * TW + (rt * CT + ct) * 64 + lane] = acc[rt][ct];
+    }
+    __syncthreads();
+    if (q == 0) {
+#pragma unroll
+        for (int rt = 0; rt < 4; rt++) {
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) {
+                const f4v v = acc[rt][ct] + red[rh * TW + (rt * CT + ct) * 64 + lane];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const uint32_t r = rg * 64u + rt * 16u + 4u * (lane >> 4) + i;
+                    if (r < rows) C[(size_t)(row_base + r) * N + ct * 16u + (lane & 15u)] = (f16)v[i];
+                }
+            }
+        }
+    }
+}
+
 }  // namespace gsk
 
 // ---------------------------------------------------------------------------

@@ -106,6 +106,18 @@ void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1)
         ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, false, scf, cf, ctx));
         ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)rows, std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
         ex.add_and_run(std::make_shared<tblock_thread_bit_map_operator>(cg, (unsigned)cf, y, false, false, ctx));
+    } else if (name == "col_direction_nm") {
+        // BASELINE.json configs[2] (C3): col-direction BMTs of p0 nnz (32 = one 64-column
+        // k-step of a 2:4 row), no padding, summed per row (the warp_bit_map tokens);
+        // rows that are 2:4 panels run on the sparse matrix cores (k_nm_mfma)
+        int fcs = p0 > 0 ? p0 : 32, cf = p1 > 0 ? p1 : 1;
+        ex.add_and_run(std::make_shared<fixed_interval_col_direction_thread_blocking_operator>(cg, fcs, false, false,
+                                                                                               false, false, ctx));
+        int y = std::min(std::max(1, N / cf), 32), x = std::max(128 / y, 32);
+        set_config("VECTOR_WIDTH", x);
+        ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, true, 4, cf, ctx));
+        ex.add_and_run(std::make_shared<warp_bit_map_operator>(cg, (unsigned)cf, true, true, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)rows, std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
     } else if (name == "block_total") {  // token_test.cc:1458-1514 (p0 = rows per BMTB, 1 there)
         int rb = p0 > 0 ? p0 : 1, cf = p1 > 0 ? p1 : 1;
         ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, rb, false, ctx));
@@ -286,7 +298,7 @@ int gs_plan_info_get(gs_plan_t *p, gs_plan_info *info) {
             info->dtype = s.dev.dtype;
             info->replicas = (int)s.dev.replicas.size();
             info->needs_memset = s.dev.needs_memset ? 1 : 0;
-            info->lds_stage = s.dev.mfma ? 2 : (s.dev.lds ? 1 : 0);
+            info->lds_stage = s.dev.nm ? 3 : (s.dev.mfma ? 2 : (s.dev.lds ? 1 : 0));
             info->lds_n = s.dev.lds_N;
             info->lds_kc = s.dev.KC;
             info->lds_chunks = s.dev.nc;

@@ -34,6 +34,7 @@ struct device_plan {
     size_t bytes_A = 0;       // device bytes of A per replica (metadata + cols + vals)
     // LDS-stationary B (k_lds_rows): chunk geometry fixed for dense width lds_N
     bool lds = false;
+    bool nm = false;    // k_nm_mfma: 2:4 panels of a col-direction plan (A blocks in tcol; k-steps in KC)
     bool mfma = false;  // k_mfma_rows (uses KC, nc, lds_bytes; log2 KC in RSB; RT in maxr; RMAX in rpw_max)
     uint32_t ksplit = 1, ncs = 0;  // k_mfma_rows workgroups per row block, chunks per workgroup
     uint32_t ws_n = 0;             // bitmap family: dense width of the fp32 workspace

@@ -318,6 +318,81 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
     return true;
 }
 
+// ------------------------------------------------------------------ 2:4 panels
+// Block layout of k_nm_mfma (kernel_lib.hpp) from the plan's COO: every row is
+// cut into 64-column k-steps (the col-direction BMTs of a 2:4 row: 32 entries
+// each), every aligned group of four columns keeps its (at most two) entries as
+// two values + two 2-bit positions.  Duplicate coordinates (col padding of the
+// plan, value 0) are summed.  Returns false (and why) when a group holds more
+// than two distinct columns or the panels would store over twice the entries
+// (beyond 4M value slots).
+bool build_nm_panels(const std::vector<uint64_t> &rows, const std::vector<uint64_t> &col, const universal_array &vals,
+                     uint64_t row_num, uint64_t K, std::vector<unsigned char> &blk, uint32_t &S, std::string &why) {
+    const uint64_t nnz = col.size();
+    if (row_num == 0 || K == 0 || nnz == 0) { why = "empty sub-matrix"; return false; }
+    const uint64_t S64 = (K + gsk::kNmKC - 1) / gsk::kNmKC * 4;  // k-steps, whole 256-column chunks
+    const uint64_t ng = (row_num + 127) / 128 * 2;               // 64-row groups, two per workgroup
+    const double slots = (double)ng * 64.0 * (double)S64 * 32.0;
+    if (slots > 2.0 * (double)nnz && slots > (double)(1 << 22)) {  // small plans always qualify
+        why = "2:4 panels would store over twice the entries";
+        return false;
+    }
+    if (S64 > 0xffffffffull || ng * S64 * gsk::kNmBlockBytes > (1ull << 40)) { why = "too large"; return false; }
+    std::vector<uint64_t> rp(row_num + 1, 0);
+    for (uint64_t r : rows) {
+        if (r >= row_num) { why = "row index beyond row count"; return false; }
+        rp[r + 1]++;
+    }
+    for (uint64_t i = 0; i < row_num; i++) rp[i + 1] += rp[i];
+    std::vector<uint64_t> cur(rp.begin(), rp.end() - 1), ord(nnz);
+    for (uint64_t e = 0; e < nnz; e++) ord[cur[rows[e]]++] = e;
+    blk.assign(ng * S64 * gsk::kNmBlockBytes, 0);
+    for (uint64_t b = 0; b < ng * S64; b++) {  // default positions (0, 1) in every group
+        uint16_t *ix = reinterpret_cast<uint16_t *>(blk.data() + b * gsk::kNmBlockBytes + 4096);
+        for (int i = 0; i < 256; i++) ix[i] = 0x4444;
+    }
+    const uint64_t Kp = S64 * 64;
+    std::vector<float> dv(Kp, 0.f);
+    std::vector<uint8_t> has(Kp, 0);
+    for (uint64_t r = 0; r < row_num; r++) {
+        if (rp[r] == rp[r + 1]) continue;
+        for (uint64_t e = rp[r]; e < rp[r + 1]; e++) {
+            const uint64_t c = col[ord[e]];
+            if (c >= K) { why = "column index beyond column count"; return false; }
+            has[c] = 1;
+            dv[c] += (float)vals.read_float_from_arr(ord[e]);
+        }
+        const uint64_t rg = r / 64, rt = (r % 64) / 16, rr = r % 16;
+        for (uint64_t gi = 0; gi < Kp / 4; gi++) {
+            int pos[2], n = 0;
+            for (int p = 0; p < 4; p++)
+                if (has[4 * gi + p]) {
+                    if (n == 2) {
+                        why = "a row holds more than two entries in an aligned group of four columns (not 2:4)";
+                        return false;
+                    }
+                    pos[n++] = p;
+                }
+            if (n == 0) continue;
+            if (n == 1) pos[1] = pos[0] == 3 ? 2 : 3;  // zero partner at another position
+            const int lo = std::min(pos[0], pos[1]), hi = std::max(pos[0], pos[1]);
+            const uint64_t s = gi / 16, j = gi % 16, g = j / 4, sg = j % 4, lane = g * 16 + rr;
+            unsigned char *b = blk.data() + (rg * S64 + s) * gsk::kNmBlockBytes;
+            uint16_t *v = reinterpret_cast<uint16_t *>(b + rt * 1024 + lane * 16) + sg * 2;
+            v[0] = has[4 * gi + lo] ? f32_to_f16_bits(dv[4 * gi + lo]) : 0;
+            v[1] = has[4 * gi + hi] ? f32_to_f16_bits(dv[4 * gi + hi]) : 0;
+            uint16_t *ix = reinterpret_cast<uint16_t *>(b + 4096 + lane * 8) + rt;
+            *ix = (uint16_t)((*ix & ~(0xfu << (4 * sg))) | ((unsigned)(lo | (hi << 2)) << (4 * sg)));
+        }
+        for (uint64_t e = rp[r]; e < rp[r + 1]; e++) {
+            has[col[ord[e]]] = 0;
+            dv[col[ord[e]]] = 0.f;
+        }
+    }
+    S = (uint32_t)S64;
+    return true;
+}
+
 }  // namespace
 
 void upload_plan(plan_state &p, int dtype, int device) {
@@ -340,6 +415,26 @@ void upload_plan(plan_state &p, int dtype, int device) {
     GS_CHECK(nnz < 0xffffffffull - kPad, "nnz exceeds 32-bit offsets");
     d.nnz_stored = nnz;
     device_arrays a;
+    const int64_t plan_n = get_config().DENSE_MATRIX_SIZE;
+    if (sp.family == KF_ROW_CHUNKS && dtype == 1 && get_config().NM_MFMA &&
+        (plan_n == 32 || plan_n == 64 || plan_n == 128)) {
+        // col-direction BMTs that are 2:4 panels: sparse matrix cores, self-contained blocks
+        std::vector<unsigned char> blk;
+        uint32_t S = 0;
+        std::string why;
+        if (build_nm_panels(rows, col, *vals, row_num_of_sub_matrix(m, 0), p.K, blk, S, why)) {
+            d.nm = true;
+            d.KC = S;
+            d.n_rows_aux = row_num_of_sub_matrix(m, 0);
+            d.n_units = m.u(THREAD_META, "first_nz_indices", 0).size() - 1;
+            d.waves = gsk::kNmWaves;
+            a.tcol = dev_copy(d, blk);
+            d.bytes_tile = d.bytes_A;
+            d.replicas.push_back(a);
+            p.uploaded = true;
+            return;
+        }
+    }
     // A streams: narrowest column type that holds Kc-1 (u16 when Kc <= 65536)
     uint64_t maxc = 0;
     for (uint64_t c : col) maxc = std::max(maxc, c);
@@ -722,6 +817,38 @@ void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N
 
 namespace {
 
+template <int CT>
+void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, void *C, hipStream_t s) {
+    const device_plan &d = p.dev;
+    auto kern = gsk::k_nm_mfma<CT>;
+    const size_t lds = (size_t)2 * gsk::kNmKC * 32 * CT;
+    static std::mutex mu;
+    static std::map<int, bool> granted;
+    {
+        std::lock_guard<std::mutex> l(mu);
+        if (!granted[d.device]) {
+            HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds));
+            granted[d.device] = true;
+        }
+    }
+    const uint32_t wg = (uint32_t)((d.n_rows_aux + 127) / 128);
+    hipLaunchKernelGGL(kern, dim3(wg), dim3(64 * gsk::kNmWaves), lds, s, (const unsigned char *)a.tcol,
+                       (const gsk::f16 *)B, (gsk::f16 *)C, (uint32_t)p.K, d.KC, (uint32_t)d.n_rows_aux,
+                       (uint32_t)d.row_base);
+    HIP_OK(hipGetLastError());
+}
+
+void launch_nm(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
+    switch (N) {
+        case 32: launch_nm_ct<2>(p, a, B, C, s); break;
+        case 64: launch_nm_ct<4>(p, a, B, C, s); break;
+        case 128: launch_nm_ct<8>(p, a, B, C, s); break;
+        default:
+            throw gs_error("2:4 panel plan (k_nm_mfma) runs N = 32, 64 or 128, not " + std::to_string(N), -2);
+    }
+}
+
 void launch_mfma(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
     const gsk::f16 *b = (const gsk::f16 *)B;
     gsk::f16 *c = (gsk::f16 *)C;
@@ -847,6 +974,10 @@ void launch_spmm(const plan_state &p, int replica, const void *B, void *C, uint3
     GS_CHECK(replica >= 0 && (size_t)replica < p.dev.replicas.size(), "bad replica index");
     GS_CHECK(N >= 1, "N >= 1");
     const device_arrays &a = p.dev.replicas[replica];
+    if (p.dev.nm) {
+        launch_nm(p, a, B, C, N, stream);
+        return;
+    }
     if (p.dev.mfma && N == p.dev.lds_N) {
         launch_mfma(p, a, B, C, N, stream);
         return;

@@ -55,7 +55,8 @@ typedef struct {
     int col_bytes, dtype, replicas, needs_memset;
     char kernel_name[64];
     /* row-block kernels built at upload for dense width lds_n: 1 = LDS-stationary B
-     * (k_lds_rows, config LDS_STAGE_B), 2 = matrix cores (k_mfma_rows, MFMA_TILES) */
+     * (k_lds_rows, config LDS_STAGE_B), 2 = matrix cores (k_mfma_rows, MFMA_TILES),
+     * 3 = 2:4 panels of a col-direction plan on the sparse matrix cores (k_nm_mfma, NM_MFMA) */
     int lds_stage;
     uint32_t lds_n, lds_kc, lds_chunks, lds_waves;
     uint64_t lds_bytes, tile_bytes;
