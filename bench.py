@@ -13,6 +13,11 @@ Multi-GPU (torchrun): weak scaling, every rank runs its own matrix (the
 row-sharded batch of independent matrices; no data-path collective), a barrier
 brackets the timed region and the time is the max over ranks.
 
+--workload c3 measures BASELINE.json configs[2] instead (OPT-30B fc1 stand-in,
+28672 x 7168, 2:4 structured by magnitude, fp16, N = 128, the col-direction
+plan on the sparse matrix cores; algorithmic bytes count the 2:4 layout's
+values + 2-bit positions).  The default stays the headline C2.
+
 Prints one JSON line on rank 0."""
 import argparse
 import ctypes
@@ -40,11 +45,25 @@ def parse():
     ap.add_argument("--rotation-mb", type=float, default=640.0)
     ap.add_argument("--no-rocsparse", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--M", type=int, default=5120)
-    ap.add_argument("--K", type=int, default=5120)
-    ap.add_argument("--N", type=int, default=32)
+    ap.add_argument("--workload", choices=("c2", "c3"), default="c2")
+    ap.add_argument("--M", type=int, default=0)
+    ap.add_argument("--K", type=int, default=0)
+    ap.add_argument("--N", type=int, default=0)
     ap.add_argument("--sparsity", type=float, default=0.7)
-    return ap.parse_args()
+    a = ap.parse_args()
+    dflt = {"c2": (5120, 5120, 32), "c3": (28672, 7168, 128)}[a.workload]
+    a.M, a.K, a.N = a.M or dflt[0], a.K or dflt[1], a.N or dflt[2]
+    return a
+
+
+WORKLOADS = {
+    "c2": {"metric": "SpMM GFLOP/s + achieved HBM GB/s vs rocSPARSE, pruned-weight fp16 N=32",
+           "workload": "OPT-13B q_proj stand-in {M}x{K} 70% unstructured, fp16, N={N}",
+           "data": "synthetic (seeded magnitude-pruned Gaussian)"},
+    "c3": {"metric": "SpMM GFLOP/s + achieved HBM GB/s vs rocSPARSE, 2:4 pruned-weight fp16 N=128 (configs[2])",
+           "workload": "OPT-30B fc1 stand-in {M}x{K} 2:4 structured, fp16, N={N}",
+           "data": "synthetic (seeded Gaussian, 2:4 magnitude pruning per group of 4)"},
+}
 
 
 # (pipeline, p0, p1).  tblock_warp_total(rows per BMTB, rows per BMW) runs the
@@ -55,13 +74,22 @@ CANDIDATES = [("block_total", 20, 1), ("block_total", 10, 1), ("block_total", 40
               ("thread_total", 4, 1)]
 
 
+# C3: the col-direction plan (32-nnz BMTs = 64-column k-steps of a 2:4 row)
+CANDIDATES_C3 = [("col_direction_nm", 32, 1)]
+
+
 def kernel_label(info):
-    return {0: info["kernel_name"], 1: "k_lds_rows", 2: "k_mfma_rows"}[info["lds_stage"]]
+    return {0: info["kernel_name"], 1: "k_lds_rows", 2: "k_mfma_rows", 3: "k_nm_mfma"}[info["lds_stage"]]
 
 
 def algorithmic_bytes(M, K, N, nnz, e, s_idx):
     # each A element once, B read once, C written once
     return nnz * (e + s_idx) + (M + 1) * 4 + K * N * e + M * N * e
+
+
+def algorithmic_bytes_24(M, K, N, nnz, e):
+    # SURVEY.md §8d, 2:4 layout on C3: values + 2-bit positions, B once, C once
+    return nnz * e + nnz // 4 + K * N * e + M * N * e
 
 
 def time_plan(plan, Bs, Cs, N, steps, warmup, torch, dist=None):
@@ -132,16 +160,23 @@ def rocsparse_baseline(M, K, N, row, col, val, copies, dtype, reps=100, warmup=1
     return best
 
 
-def cpu_baseline(M, K, N, row, col, val, min_s=10.0):
+def cpu_baseline(M, K, N, row, col, val, min_s=10.0, row_share=1):
     """the oracle's restatement of the reference's host path (checker code, timed
-    here only as the CPU baseline): plan transform once + host SpMM repeated"""
+    here only as the CPU baseline): plan transform once + host SpMM repeated.
+    row_share > 1 times the first M/row_share rows only (a bounded sample)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi as ofi
+    what = "full matrix"
+    if row_share > 1:
+        Ms = M // row_share
+        keep = row < Ms
+        row, col, val, M = row[keep], col[keep], val[keep], Ms
+        what = f"first {Ms} rows (1/{row_share} of the matrix)"
     t_tr, _ = ofi.time_cpu_path(M, K, row, col, val, N)
     t_spmm, reps = ofi.time_spmm_repeated(M, K, row, col, val, N, min_s)
     gf = 2.0 * len(row) * N * reps / t_spmm / 1e9
     return {"value": round(gf, 3), "unit": "GFLOP/s", "cores": 1, "kind": "port",
-            "sample": f"full C2 matrix: spmm_reference_host restated (fp32) x{reps} in {t_spmm:.1f} s, "
+            "sample": f"{what}: spmm_reference_host restated (fp32) x{reps} in {t_spmm:.1f} s, "
                       f"single thread; plan transform (thread_total) once {t_tr:.2f} s",
             "transform_s": round(t_tr, 3), "spmm_s_per_rep": round(t_spmm / reps, 4)}
 
@@ -166,13 +201,21 @@ def main():
     from generalsparse_amd import datasets as ds
 
     M, K, N = args.M, args.K, args.N
-    row, col, val = ds.pruned_weight(M, K, args.sparsity, shard_seed(rank))
-    nnz = len(row)
+    wl = WORKLOADS[args.workload]
     e, s_idx = 2, (2 if K <= 65536 else 4)
-    alg_bytes = algorithmic_bytes(M, K, N, nnz, e, s_idx)
+    if args.workload == "c3":
+        row, col, val = ds.two_four(M, K, 30 + rank)
+        nnz = len(row)
+        alg_bytes = algorithmic_bytes_24(M, K, N, nnz, e)
+        cand_list = CANDIDATES_C3
+    else:
+        row, col, val = ds.pruned_weight(M, K, args.sparsity, shard_seed(rank))
+        nnz = len(row)
+        alg_bytes = algorithmic_bytes(M, K, N, nnz, e, s_idx)
+        cand_list = CANDIDATES
     flops = 2.0 * nnz * N
 
-    cands = CANDIDATES if args.pipeline == "auto" else [c for c in CANDIDATES if c[0] == args.pipeline] or \
+    cands = cand_list if args.pipeline == "auto" else [c for c in cand_list if c[0] == args.pipeline] or \
         [(args.pipeline, 0, 1)]
     variants = {}
     best = None
@@ -205,18 +248,18 @@ def main():
     value = whole_job_gflops(world, flops, args.steps, wall)
     achieved = alg_bytes / (ev_ms * 1e-3) / 1e9
     traffic = None
-    tf = os.path.join(ROOT, "profiles", "traffic_c2.json")
+    tf = os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
     if os.path.exists(tf):
         try:
             traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     out = {
-        "metric": "SpMM GFLOP/s + achieved HBM GB/s vs rocSPARSE, pruned-weight fp16 N=32",
+        "metric": wl["metric"],
         "value": round(value, 1), "unit": "GFLOP/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 5), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "f16 (fp32 accumulate)", "data": "synthetic (seeded magnitude-pruned Gaussian)",
-        "config": {"workload": "OPT-13B q_proj stand-in 5120x5120 70% unstructured, fp16, N=32",
+        "dtype": "f16 (fp32 accumulate)", "data": wl["data"],
+        "config": {"workload": wl["workload"].format(M=M, K=K, N=N),
                    "M": M, "K": K, "N": N, "nnz": nnz, "plan": key, "kernel": kernel_label(info),
                    "replicas_rotated": reps, "parallelism": f"row-sharded batch x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -253,7 +296,7 @@ def main():
         except Exception as ex:  # comparator problems must not hide the main number
             out["rocsparse"] = {"error": str(ex)}
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(M, K, N, row, col, val)
+        out["cpu_baseline"] = cpu_baseline(M, K, N, row, col, val, row_share=8 if args.workload == "c3" else 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -1112,24 +1112,27 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
 // the accumulator is the 16x16 MFMA layout (column l%16, rows 4*(l/16)+i).
 //
 // HBM layout (device_plan.hip build_nm_panels): per row group of 64 rows (four
-// 16-row tiles) and k-step s a 4608-byte block: [tile rt][lane] 16 B of values,
-// then [lane] 8 B of positions (u16 per tile: tiles 0/1 in the low dword,
-// selected by abid 0/1, tiles 2/3 in the high dword).  Every wave load is one
-// coalesced 1 KB (or 512 B) request; A is read exactly once.
+// 16-row tiles) and k-step s a 4608-byte block: [lane] 8 B of positions (u16
+// per tile: tiles 0/1 in the low dword, selected by abid 0/1, tiles 2/3 in the
+// high dword), then [tile rt][lane] 16 B of values.  Every wave load is one
+// coalesced 512 B / 1 KB request; A is read exactly once.
 //
 // Workgroup = 8 waves = two row groups (128 rows) x four k-phases: wave (rh, q)
 // takes k-step 4c+q of every 256-row chunk c of B.  B chunks are staged in LDS
 // (two buffers, 32-B pieces XOR-permuted by b_piece so the transposed reads
 // are conflict-free) by all 512 threads through registers, one chunk ahead;
-// each wave's A blocks are loaded two chunks ahead.  One barrier per chunk.
-// The four k-phase partial tiles are summed in a fixed order through LDS
-// ((q0 + q2) + (q1 + q3): deterministic) and stored as fp16.
+// each wave's A blocks are loaded two chunks ahead.  One barrier per chunk;
+// sched_barriers keep the phases in issue order so each wait leaves the younger
+// prefetches in flight.  The four k-phase partial tiles are summed in a fixed
+// order through LDS ((q0 + q2) + (q1 + q3): deterministic) and stored as fp16.
 // ---------------------------------------------------------------------------
 typedef _Float16 h16v __attribute__((ext_vector_type(16)));
 constexpr int kNmWaves = 8;
 constexpr uint32_t kNmBlockBytes = 4608, kNmKC = 256;
 
-template <int CT>
+// DBG (diagnostic builds only, GS_NM_DEBUG): 1 = no B loads in the loop, 2 = no A loads,
+// 4 = s_memtime phase stamps of waves 0/4 of workgroups 0 and 100, printed
+template <int CT, int DBG = 0>
 __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *__restrict__ A,
                                                            const f16 *__restrict__ B, f16 *__restrict__ C,
                                                            uint32_t K, uint32_t S, uint32_t rows,
@@ -1138,40 +1141,61 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
     constexpr uint32_t szB = kNmKC * RB;
     constexpr uint32_t NTH = 64 * kNmWaves;
     constexpr uint32_t NBU = szB / 16 / NTH;  // 16-B units of B per thread per chunk
-    static_assert(szB % (16 * NTH) == 0, "whole B units per thread");
+    constexpr uint32_t RPU = NTH / UB;        // B rows between a thread's units
+    static_assert(szB % (16 * NTH) == 0 && NTH % UB == 0, "whole B units per thread");
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t rh = wv >> 2, q = wv & 3u;
     const uint32_t rg = blockIdx.x * 2u + rh;
     const uint32_t nch = S / 4u;
     const unsigned char *arow = A + (size_t)rg * S * kNmBlockBytes;
+    const unsigned char *bbase = reinterpret_cast<const unsigned char *>(B);
+    const uint32_t bk = tid / UB, boff = bk * RB + (tid % UB) * 16u;  // this thread's first unit
+    // LDS byte offset of unit i (row bk + i*RPU, 16-B unit tid%UB) in either buffer
+    auto bdst = [&](uint32_t i) {
+        const uint32_t k = bk + i * RPU, s = tid % UB;
+        return k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u;
+    };
 
     u32x4 a0v[4], a1v[4];
     uint2 a0i, a1i;
 #define GS_NM_ALOAD(c, V, I)                                                                        \
-    {                                                                                             \
+    if (DBG != 2 || (uint32_t)(c) < 2u) {                                                         \
         const uint32_t cc_ = min((uint32_t)(c), nch - 1u);                                        \
         const unsigned char *blk_ = arow + (size_t)(4u * cc_ + q) * kNmBlockBytes;                \
+        I = *reinterpret_cast<const uint2 *>(blk_ + lane * 8u);                                   \
         _Pragma("unroll") for (int rt = 0; rt < 4; rt++) V[rt] =                                  \
-            *reinterpret_cast<const u32x4 *>(blk_ + rt * 1024u + lane * 16u);                     \
-        I = *reinterpret_cast<const uint2 *>(blk_ + 4096u + lane * 8u);                           \
+            *reinterpret_cast<const u32x4 *>(blk_ + 512u + rt * 1024u + lane * 16u);              \
     }
     u32x4 bs[NBU];
+    // whole chunks: one lane offset, uniform bases; the last partial chunk clamps rows
 #define GS_NM_BLOAD(c)                                                                              \
-    {                                                                                             \
-        _Pragma("unroll") for (uint32_t i = 0; i < NBU; i++) {                                    \
-            const uint32_t u = tid + i * NTH, k = u / UB;                                         \
-            const uint32_t kk = (uint32_t)(c) * kNmKC + k;                                        \
-            bs[i] = kk < K ? *reinterpret_cast<const u32x4 *>(B + (size_t)kk * N + (u % UB) * 8u) \
-                           : u32x4{0u, 0u, 0u, 0u};                                               \
+    if (DBG != 1 || (uint32_t)(c) < 2u) {                                                         \
+        const uint32_t k0_ = (uint32_t)(c) * kNmKC;                                               \
+        if (k0_ + kNmKC <= K) {                                                                   \
+            const unsigned char *src_ = bbase + (size_t)k0_ * RB;                                 \
+            _Pragma("unroll") for (uint32_t i = 0; i < NBU; i++) bs[i] =                          \
+                *reinterpret_cast<const u32x4 *>(src_ + i * RPU * RB + boff);                     \
+        } else {                                                                                  \
+            _Pragma("unroll") for (uint32_t i = 0; i < NBU; i++) {                                \
+                const uint32_t kk_ = min(k0_ + bk + i * RPU, K - 1u);                             \
+                bs[i] = *reinterpret_cast<const u32x4 *>(bbase + (size_t)kk_ * RB + (tid % UB) * 16u); \
+            }                                                                                     \
         }                                                                                         \
     }
 #define GS_NM_BSTORE(c)                                                                             \
     {                                                                                             \
+        const uint32_t k0_ = (uint32_t)(c) * kNmKC;                                               \
         unsigned char *lb_ = lds + ((uint32_t)(c) & 1u) * szB;                                    \
-        _Pragma("unroll") for (uint32_t i = 0; i < NBU; i++) {                                    \
-            const uint32_t u = tid + i * NTH, k = u / UB, s = u % UB;                             \
-            *reinterpret_cast<u32x4 *>(lb_ + k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u) = bs[i]; \
+        if (k0_ + kNmKC <= K) {                                                                   \
+            _Pragma("unroll") for (uint32_t i = 0; i < NBU; i++)                                  \
+                *reinterpret_cast<u32x4 *>(lb_ + bdst(i)) = bs[i];                                \
+        } else { /* rows past K: zeros */                                                         \
+            _Pragma("unroll") for (uint32_t i = 0; i < NBU; i++) {                                \
+                const uint32_t z_ = k0_ + bk + i * RPU < K ? ~0u : 0u;                            \
+                *reinterpret_cast<u32x4 *>(lb_ + bdst(i)) = bs[i] & z_;                           \
+            }                                                                                     \
         }                                                                                         \
     }
     f4v acc[4][CT];
@@ -1179,51 +1203,105 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
     for (int rt = 0; rt < 4; rt++)
 #pragma unroll
         for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+    // transposed-read offsets of this lane (h = 0..3: k +0/+4/+32/+36 of the step)
+    const uint32_t kl = 64u * q + 8u * (lane >> 4) + ((lane & 15u) >> 2);
     // chunk c's k-step for this wave: B rows 64q + [0, 64) of LDS buffer c&1
+#define GS_NM_BFRAG(lb_, ct, BF)                                                                    \
+    {                                                                                             \
+        s4v t_[4];                                                                                \
+        _Pragma("unroll") for (int h = 0; h < 4; h++) {                                           \
+            const uint32_t k = kl + 32u * (h >> 1) + 4u * (h & 1);                                \
+            t_[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(                                      \
+                (lds_s4v *)(lb_ + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u));         \
+        }                                                                                         \
+        __builtin_memcpy(&BF, t_, 32);                                                            \
+    }
+    // B fragments double-buffered in registers: the reads of n-tile ct+1 are in
+    // flight while the four smfmac of n-tile ct run
 #define GS_NM_COMPUTE(c, V, I)                                                                      \
     {                                                                                             \
         const unsigned char *lb_ = lds + ((uint32_t)(c) & 1u) * szB;                              \
         h8v av_[4];                                                                               \
         _Pragma("unroll") for (int rt = 0; rt < 4; rt++) __builtin_memcpy(&av_[rt], &V[rt], 16);  \
         const int ix0_ = (int)I.x, ix1_ = (int)I.y;                                               \
+        h16v bf_[2];                                                                              \
+        GS_NM_BFRAG(lb_, 0, bf_[0]);                                                              \
         _Pragma("unroll") for (int ct = 0; ct < CT; ct++) {                                       \
-            s4v t_[4];                                                                            \
-            _Pragma("unroll") for (int h = 0; h < 4; h++) {                                       \
-                const uint32_t k = 64u * q + 32u * (h >> 1) + 8u * (lane >> 4) + 4u * (h & 1) + ((lane & 15u) >> 2); \
-                t_[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(                                  \
-                    (lds_s4v *)(lb_ + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u));     \
-            }                                                                                     \
-            h16v bf_;                                                                             \
-            __builtin_memcpy(&bf_, t_, 32);                                                       \
-            acc[0][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[0], bf_, acc[0][ct], ix0_, 0, 0); \
-            acc[1][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[1], bf_, acc[1][ct], ix0_, 0, 1); \
-            acc[2][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[2], bf_, acc[2][ct], ix1_, 0, 0); \
-            acc[3][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[3], bf_, acc[3][ct], ix1_, 0, 1); \
+            if (ct + 1 < CT) GS_NM_BFRAG(lb_, ct + 1, bf_[(ct + 1) & 1]);                         \
+            const h16v b_ = bf_[ct & 1];                                                          \
+            acc[0][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[0], b_, acc[0][ct], ix0_, 0, 0); \
+            acc[1][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[1], b_, acc[1][ct], ix0_, 0, 1); \
+            acc[2][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[2], b_, acc[2][ct], ix1_, 0, 0); \
+            acc[3][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[3], b_, acc[3][ct], ix1_, 0, 1); \
+        }                                                                                         \
+        /* issue order: reads of n-tile 0, then (reads of ct+1, smfmac of ct) */                  \
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);                                        \
+        _Pragma("unroll") for (int ct = 0; ct < CT; ct++) {                                       \
+            if (ct + 1 < CT) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);                   \
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                    \
         }                                                                                         \
     }
+    // prologue in the loop's steady-state issue order (B of c+1, then A of c+1)
     GS_NM_BLOAD(0u);
     GS_NM_ALOAD(0u, a0v, a0i);
-    GS_NM_ALOAD(1u, a1v, a1i);
+    __builtin_amdgcn_sched_barrier(0);
     GS_NM_BSTORE(0u);
-    GS_NM_BLOAD(1u);
+    __builtin_amdgcn_sched_barrier(0);
+    GS_NM_BLOAD(nch > 1u ? 1u : 0u);
+    __builtin_amdgcn_sched_barrier(0);
+    GS_NM_ALOAD(1u, a1v, a1i);
     __syncthreads();
     // iteration c: stage chunk c+1 (its buffer was last read in iteration c-1,
     // before the barrier), fetch B of c+2, compute c, fetch A of c+2
+    uint64_t *stl = reinterpret_cast<uint64_t *>(lds + 2 * szB);  // DBG 4 only
+#define GS_NM_STAMP(hc, k)                                                                          \
+    if constexpr (DBG == 4) {                                                                     \
+        if (lane == 0 && (hc) >= 4u && (hc) < 10u) stl[wv * 32u + ((hc) - 4u) * 5u + (k)] = __builtin_amdgcn_s_memtime(); \
+    }
     uint32_t c = 0;
     for (; c + 1 < nch; c += 2) {
         GS_NM_BSTORE(c + 1u);
+        GS_NM_STAMP(c, 0u);
+        __builtin_amdgcn_sched_barrier(0);
         GS_NM_BLOAD(c + 2u < nch ? c + 2u : c + 1u);
+        GS_NM_STAMP(c, 1u);
+        __builtin_amdgcn_sched_barrier(0);
         GS_NM_COMPUTE(c, a0v, a0i);
+        GS_NM_STAMP(c, 2u);
+        __builtin_amdgcn_sched_barrier(0);
         GS_NM_ALOAD(c + 2u, a0v, a0i);
+        GS_NM_STAMP(c, 3u);
         __syncthreads();
-        if (c + 2u < nch) GS_NM_BSTORE(c + 2u);
+        GS_NM_STAMP(c, 4u);
+        GS_NM_BSTORE(c + 2u);  /* past the end: a buffer nobody reads again */
+        GS_NM_STAMP(c + 1u, 0u);
+        __builtin_amdgcn_sched_barrier(0);
         GS_NM_BLOAD(c + 3u < nch ? c + 3u : c + 1u);
+        GS_NM_STAMP(c + 1u, 1u);
+        __builtin_amdgcn_sched_barrier(0);
         GS_NM_COMPUTE(c + 1u, a1v, a1i);
+        GS_NM_STAMP(c + 1u, 2u);
+        __builtin_amdgcn_sched_barrier(0);
         GS_NM_ALOAD(c + 3u, a1v, a1i);
+        GS_NM_STAMP(c + 1u, 3u);
         __syncthreads();
+        GS_NM_STAMP(c + 1u, 4u);
     }
+    if constexpr (DBG == 4) {
+        __syncthreads();
+        if ((blockIdx.x == 0 || blockIdx.x == 100) && lane == 0 && (wv == 0 || wv == 4)) {
+            const uint64_t t0 = stl[wv * 32u];
+            for (int hc = 0; hc < 6; hc++)
+                printf("wg %u wave %u half %d: bstore %llu bload %llu compute %llu aload %llu barrier %llu\n",
+                       blockIdx.x, wv, hc + 4, (unsigned long long)(stl[wv * 32u + hc * 5] - t0),
+                       (unsigned long long)(stl[wv * 32u + hc * 5 + 1] - t0), (unsigned long long)(stl[wv * 32u + hc * 5 + 2] - t0),
+                       (unsigned long long)(stl[wv * 32u + hc * 5 + 3] - t0), (unsigned long long)(stl[wv * 32u + hc * 5 + 4] - t0));
+        }
+    }
+#undef GS_NM_STAMP
     if (c < nch) GS_NM_COMPUTE(c, a0v, a0i);
 #undef GS_NM_COMPUTE
+#undef GS_NM_BFRAG
 #undef GS_NM_BSTORE
 #undef GS_NM_BLOAD
 #undef GS_NM_ALOAD

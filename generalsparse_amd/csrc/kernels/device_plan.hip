@@ -348,7 +348,7 @@ bool build_nm_panels(const std::vector<uint64_t> &rows, const std::vector<uint64
     for (uint64_t e = 0; e < nnz; e++) ord[cur[rows[e]]++] = e;
     blk.assign(ng * S64 * gsk::kNmBlockBytes, 0);
     for (uint64_t b = 0; b < ng * S64; b++) {  // default positions (0, 1) in every group
-        uint16_t *ix = reinterpret_cast<uint16_t *>(blk.data() + b * gsk::kNmBlockBytes + 4096);
+        uint16_t *ix = reinterpret_cast<uint16_t *>(blk.data() + b * gsk::kNmBlockBytes);
         for (int i = 0; i < 256; i++) ix[i] = 0x4444;
     }
     const uint64_t Kp = S64 * 64;
@@ -378,10 +378,10 @@ bool build_nm_panels(const std::vector<uint64_t> &rows, const std::vector<uint64
             const int lo = std::min(pos[0], pos[1]), hi = std::max(pos[0], pos[1]);
             const uint64_t s = gi / 16, j = gi % 16, g = j / 4, sg = j % 4, lane = g * 16 + rr;
             unsigned char *b = blk.data() + (rg * S64 + s) * gsk::kNmBlockBytes;
-            uint16_t *v = reinterpret_cast<uint16_t *>(b + rt * 1024 + lane * 16) + sg * 2;
+            uint16_t *v = reinterpret_cast<uint16_t *>(b + 512 + rt * 1024 + lane * 16) + sg * 2;
             v[0] = has[4 * gi + lo] ? f32_to_f16_bits(dv[4 * gi + lo]) : 0;
             v[1] = has[4 * gi + hi] ? f32_to_f16_bits(dv[4 * gi + hi]) : 0;
-            uint16_t *ix = reinterpret_cast<uint16_t *>(b + 4096 + lane * 8) + rt;
+            uint16_t *ix = reinterpret_cast<uint16_t *>(b + lane * 8) + rt;
             *ix = (uint16_t)((*ix & ~(0xfu << (4 * sg))) | ((unsigned)(lo | (hi << 2)) << (4 * sg)));
         }
         for (uint64_t e = rp[r]; e < rp[r + 1]; e++) {
@@ -820,16 +820,20 @@ namespace {
 template <int CT>
 void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, void *C, hipStream_t s) {
     const device_plan &d = p.dev;
-    auto kern = gsk::k_nm_mfma<CT>;
-    const size_t lds = (size_t)2 * gsk::kNmKC * 32 * CT;
+    // GS_NM_DEBUG=1/2: diagnostic builds without the loop's B / A loads (wrong results)
+    static const int dbg = getenv("GS_NM_DEBUG") ? atoi(getenv("GS_NM_DEBUG")) : 0;
+    auto kern = dbg == 1 ? gsk::k_nm_mfma<CT, 1>
+                         : (dbg == 2 ? gsk::k_nm_mfma<CT, 2> : (dbg == 4 ? gsk::k_nm_mfma<CT, 4> : gsk::k_nm_mfma<CT, 0>));
+    const size_t lds = (size_t)2 * gsk::kNmKC * 32 * CT + (dbg == 4 ? 4096 : 0);
     static std::mutex mu;
-    static std::map<int, bool> granted;
+    static std::map<std::pair<int, const void *>, bool> granted;
     {
         std::lock_guard<std::mutex> l(mu);
-        if (!granted[d.device]) {
+        bool &g = granted[{d.device, reinterpret_cast<const void *>(kern)}];
+        if (!g) {
             HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds));
-            granted[d.device] = true;
+            g = true;
         }
     }
     const uint32_t wg = (uint32_t)((d.n_rows_aux + 127) / 128);
