@@ -1346,6 +1346,253 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_merge_path -- merge-path levels (merge_path_{thread,warp,tblock}_operator +
+// the level's total-reduce token).  The plan's
+// level starts (first_row_indices_without_ending / first_nz_indices,
+// get_begin_{rows,nzs}_of_level_after_merge_path.cc) are decoded on the host
+// into nz-exact wave ranges [wz[w], wz[w+1]) (gsk_host::merge_path_layout);
+// rows are the non-empty rows in compact order: ends[j] = their CSR row ends,
+// rid[j] = their output rows.  A wave walks its range in rounds of 8*S
+// nonzeros (S = 64/X slots of X column lanes, 8 consecutive nonzeros per slot,
+// one 16/32-B load of cols and of vals, all 8 B-row gathers in flight):
+//   1. the rows closing in the round are staged in the wave's LDS and mark a
+//      row-start flag per position (flag at e - zb for every row end e);
+//   2. each slot walks its 8 positions with the flags as a bit mask: a run
+//      that starts and closes inside the slot is stored at once; the slot's
+//      head run (continuing from the left) is held back; its tail run is the
+//      slot's carry;
+//   3. a segmented scan over slots (stop = any row start/close in the slot)
+//      gives every slot its carry-in; held-back heads add it and are stored;
+//      the last slot's scan value is carried into the next round.
+// Each closed row also zero-fills the empty rows before it (and the last one
+// the rows after it), so C needs no memset.  Rows crossing waves: the wave the
+// row is open at the end of writes (rid, partial) to rec/rec_row, the wave
+// that closes it writes its own partial to head_rec instead of C, and
+// k_merge_fixup sums them in wave order (deterministic, one rounding).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kMpItems = 8;  // nonzeros per slot per round
+
+__host__ __device__ constexpr uint32_t merge_path_wave_lds_words(uint32_t S) {
+    return (kMpItems * S) / 4u + 2u + 2u * (kMpItems * S + 64u) + 2u;
+}
+
+template <class VT, class CT, int CF>
+__global__ __launch_bounds__(256) void k_merge_path(const uint32_t *__restrict__ wz,   // n_waves+1
+                                                    const uint32_t *__restrict__ wq,   // n_waves+1
+                                                    const uint32_t *__restrict__ ends, // n_crow
+                                                    const uint32_t *__restrict__ rid,  // n_crow
+                                                    uint32_t n_crow, const CT *__restrict__ col,
+                                                    const VT *__restrict__ val, const VT *__restrict__ B,
+                                                    VT *__restrict__ C, float *__restrict__ rec,
+                                                    uint32_t *__restrict__ rec_row, float *__restrict__ head_rec,
+                                                    uint32_t n_waves, uint32_t N, uint32_t X, uint32_t row_lo,
+                                                    uint32_t row_hi) {
+    extern __shared__ uint32_t mp_lds[];
+    const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
+    const uint32_t xl = lane & (X - 1u), slot = lane / X, S = 64u / X;
+    const uint32_t R8 = kMpItems * S;     // nonzeros per round
+    const uint32_t fw = R8 / 4u + 2u;     // flag words: bytes 0..R8
+    const uint32_t cap = R8 + 64u;        // staged rows per round
+    uint32_t *wl = mp_lds + wib * merge_path_wave_lds_words(S);
+    unsigned char *flags = reinterpret_cast<unsigned char *>(wl);
+    uint32_t *ends_l = wl + fw;           // ends[qs + k]
+    uint32_t *rid_l = ends_l + cap;       // rid[qs - 1 + k]
+    const uint32_t waves_total = gridDim.x * (blockDim.x >> 6);
+    typedef typename raw_vec<CF * sizeof(VT)>::t RB;
+    for (uint32_t ct = blockIdx.y; ct * X * CF < N; ct += gridDim.y) {
+        const uint32_t cw = ct * X * CF + xl * CF;
+        const bool cok = cw < N;
+        const uint32_t c0 = cok ? cw : 0u;
+        for (uint32_t w = blockIdx.x * (blockDim.x >> 6) + wib; w < n_waves; w += waves_total) {
+            const uint32_t zlo = wz[w], wend = wz[w + 1], q0 = wq[w];
+            // the wave starts inside row q0 (its partial goes to head_rec)
+            const bool head_open = zlo > (q0 ? ends[q0 - 1] : 0u);
+            uint32_t qs = q0;
+            float rc[CF];
+#pragma unroll
+            for (int k = 0; k < CF; k++) rc[k] = 0.f;
+            bool closed_end = false;
+            auto emit = [&](uint32_t qq, const float (&a)[CF]) {
+                if (!cok) return;
+                const uint32_t li = qq - qs;
+                const uint32_t rr = rid_l[li + 1], rp = rid_l[li];
+                if (qq == q0 && head_open) {
+#pragma unroll
+                    for (int k = 0; k < CF; k++) head_rec[(size_t)w * N + c0 + k] = a[k];
+                } else {
+                    store_f32<VT, CF>(C + (size_t)rr * N + c0, a);
+                }
+                float z[CF];
+#pragma unroll
+                for (int k = 0; k < CF; k++) z[k] = 0.f;
+                for (uint32_t r = rp + 1u; r < rr; r++) store_f32<VT, CF>(C + (size_t)r * N + c0, z);
+                if (qq + 1u == n_crow)
+                    for (uint32_t r = rr + 1u; r < row_hi; r++) store_f32<VT, CF>(C + (size_t)r * N + c0, z);
+            };
+            for (uint32_t zb = zlo & ~(kMpItems - 1u); zb < wend; zb += R8) {
+                const uint32_t zl = max(zb, zlo), ze = min(zb + R8, wend);
+                const uint32_t base = zb + kMpItems * slot;
+                CT cc[kMpItems];
+                VT vv[kMpItems];
+                if (base < ze) {
+                    load_raw<CT, kMpItems>(col + base, cc);
+                    load_raw<VT, kMpItems>(val + base, vv);
+                } else {
+#pragma unroll
+                    for (uint32_t k = 0; k < kMpItems; k++) { cc[k] = 0; vv[k] = (VT)0.f; }
+                }
+                for (uint32_t i = lane; i < fw; i += 64u) wl[i] = 0u;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                // stage the rows closing in this round and the one open at its end
+                if (lane == 0) rid_l[0] = qs ? rid[qs - 1u] : row_lo - 1u;
+                uint32_t nclose = 0;
+                closed_end = false;
+                for (uint32_t k0 = 0;; k0 += 64u) {
+                    const uint32_t j = qs + k0 + lane;
+                    const uint32_t e = j < n_crow ? ends[j] : 0xffffffffu;
+                    const uint32_t r = j < n_crow ? rid[j] : 0u;
+                    if (k0 + lane < cap) {
+                        ends_l[k0 + lane] = e;
+                        rid_l[k0 + lane + 1u] = r;
+                    }
+                    if (e > zl && e <= ze) flags[e - zb] = 1;
+                    nclose += (uint32_t)__builtin_popcountll(__ballot(e <= ze));
+                    closed_end = closed_end || __ballot(e == ze) != 0ull;
+                    if (__ballot(e >= ze) != 0ull || k0 + 64u >= cap) break;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                // this slot's row starts: bit k = position 8*slot + k (bit 8: the next slot's first)
+                const uint32_t fo = kMpItems * slot;
+                const uint2 f8 = *reinterpret_cast<const uint2 *>(flags + fo);
+                uint32_t bits = (uint32_t)flags[fo + kMpItems] << 8;
+#pragma unroll
+                for (uint32_t k = 0; k < 4; k++) bits |= ((f8.x >> (8 * k)) & 1u) << k | ((f8.y >> (8 * k)) & 1u) << (k + 4);
+                const uint32_t pc = (uint32_t)__builtin_popcount(bits & 0xffu);
+                uint32_t incl = pc;
+                for (uint32_t off = X; off < 64u; off <<= 1) {
+                    const uint32_t t = __shfl_up(incl, off, 64);
+                    if (lane >= off) incl += t;
+                }
+                uint32_t qcur = qs + incl - pc;  // row open before this slot's first position
+                RB braw[kMpItems];  // all gathers in flight before the walk
+#pragma unroll
+                for (uint32_t k = 0; k < kMpItems; k++) {
+                    const uint32_t z = base + k;
+                    const bool valid = z >= zl && z < ze;
+                    braw[k] = *reinterpret_cast<const RB *>(B + (size_t)(valid ? (uint32_t)cc[k] : 0u) * N + c0);
+                }
+                float acc[CF], h[CF];
+#pragma unroll
+                for (int k = 0; k < CF; k++) { acc[k] = 0.f; h[k] = 0.f; }
+                bool has_h = false, in_head = true;
+                uint32_t hq = 0;
+                const bool head_cont = !(bits & 1u);
+                auto close = [&](uint32_t qq) {
+                    if (in_head && head_cont) {
+                        has_h = true;
+                        hq = qq;
+#pragma unroll
+                        for (int k = 0; k < CF; k++) h[k] = acc[k];
+                    } else {
+                        emit(qq, acc);
+                    }
+                };
+#pragma unroll
+                for (uint32_t k = 0; k < kMpItems; k++) {
+                    if ((bits >> k) & 1u) {
+                        if (k > 0) close(qcur);
+                        qcur++;
+                        in_head = false;
+#pragma unroll
+                        for (int i = 0; i < CF; i++) acc[i] = 0.f;
+                    }
+                    const uint32_t z = base + k;
+                    if (z >= zl && z < ze) {
+                        VT bt[CF];
+                        __builtin_memcpy(bt, &braw[k], sizeof(RB));
+                        const float v = (float)vv[k];
+#pragma unroll
+                        for (int i = 0; i < CF; i++) acc[i] = __builtin_fmaf(v, (float)bt[i], acc[i]);
+                    }
+                }
+                if ((bits >> kMpItems) & 1u) {
+                    close(qcur);
+#pragma unroll
+                    for (int i = 0; i < CF; i++) acc[i] = 0.f;
+                }
+                // segmented inclusive scan of the slots' carries (stop: the slot starts or closes a row)
+                uint32_t stop = bits != 0u;
+                if (slot == 0 && !stop) {
+#pragma unroll
+                    for (int i = 0; i < CF; i++) acc[i] += rc[i];
+                }
+                for (uint32_t off = X; off < 64u; off <<= 1) {
+                    const uint32_t ts = __shfl_up(stop, off, 64);
+                    float t[CF];
+#pragma unroll
+                    for (int i = 0; i < CF; i++) t[i] = __shfl_up(acc[i], off, 64);
+                    if (lane >= off) {
+                        if (!stop) {
+#pragma unroll
+                            for (int i = 0; i < CF; i++) acc[i] += t[i];
+                        }
+                        stop |= ts;
+                    }
+                }
+                float cin[CF];
+#pragma unroll
+                for (int i = 0; i < CF; i++) {
+                    const float t = __shfl_up(acc[i], X, 64);
+                    cin[i] = slot ? t : rc[i];
+                }
+                if (has_h) {
+#pragma unroll
+                    for (int i = 0; i < CF; i++) h[i] += cin[i];
+                    emit(hq, h);
+                }
+#pragma unroll
+                for (int i = 0; i < CF; i++) rc[i] = __shfl(acc[i], (S - 1u) * X + xl, 64);
+                qs += nclose;
+                __builtin_amdgcn_wave_barrier();
+            }
+            // the row open at the wave's end (if any): partial for k_merge_fixup
+            if (lane == 0) rec_row[w] = closed_end ? 0xffffffffu : rid[qs];
+            if (!closed_end && slot == 0 && cok) {
+#pragma unroll
+                for (int k = 0; k < CF; k++) rec[(size_t)w * N + c0 + k] = rc[k];
+            }
+        }
+    }
+}
+
+// rows open across waves: C[r] = (sum of the open partials in wave order) + the
+// closing wave's partial, rounded once
+template <class VT>
+__global__ __launch_bounds__(256) void k_merge_fixup(const uint32_t *__restrict__ rec_row,
+                                                     const float *__restrict__ rec,
+                                                     const float *__restrict__ head_rec, VT *__restrict__ C,
+                                                     uint32_t n_waves, uint32_t N) {
+    const size_t total = (size_t)n_waves * N;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t g = (uint32_t)(e / N), c = (uint32_t)(e % N);
+        const uint32_t r = rec_row[g];
+        if (r == 0xffffffffu || (g > 0 && rec_row[g - 1] == r)) continue;
+        float s = 0.f;
+        uint32_t h = g;
+        while (h < n_waves && rec_row[h] == r) {
+            s += rec[(size_t)h * N + c];
+            h++;
+        }
+        if (h < n_waves) s += head_rec[(size_t)h * N + c];
+        C[(size_t)r * N + c] = (VT)s;
+    }
+}
+
 }  // namespace gsk
 
 // ---------------------------------------------------------------------------
@@ -1353,6 +1600,7 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
 // programs code_generator emits: the kernel-side layouts derived from plan
 // arrays.
 // ---------------------------------------------------------------------------
+#include <string>
 #include <vector>
 
 namespace gsk_host {
@@ -1395,6 +1643,65 @@ inline std::vector<uint32_t> row_chunk_finalize_rows(const std::vector<uint32_t>
     for (uint64_t r = 0; r < M; r++)
         if (fin[r]) list.push_back((uint32_t)r);
     return list;
+}
+
+// k_merge_path: nz-exact wave ranges from the plan's merge-path levels, and the
+// compact non-empty rows.  Level w starts at path step p = w*work_size; the
+// reference records (row j's index, p - j) for the first non-empty row j with
+// total_path[j] > p (get_begin_{rows,nzs}_of_level_after_merge_path.cc:84-94).
+// total_path[j] = ends[j] + j, so p == ends[j-1] + j - 1 is the step that
+// closes row j-1: the nonzeros consumed there are ends[j-1] = (p - j) + 1;
+// otherwise p - j.  Consecutive levels are grouped into waves of at least
+// target_steps path steps; waves never have an empty nz range.
+struct merge_path_layout {
+    std::vector<uint32_t> wz, wq, ends, rid;
+};
+
+inline bool merge_path_device_layout(const std::vector<uint64_t> &row, uint64_t row_num,
+                                     const std::vector<uint64_t> &lvl_rows, const std::vector<uint64_t> &lvl_nzs,
+                                     uint64_t work_size, uint32_t row_base, uint64_t target_steps,
+                                     merge_path_layout &out, std::string &why) {
+    out = merge_path_layout();
+    std::vector<uint32_t> cnt(row_num, 0);
+    for (uint64_t r : row) {
+        if (r >= row_num) { why = "row index beyond the row count"; return false; }
+        cnt[r]++;
+    }
+    std::vector<uint64_t> crow;  // plan row of compact row j
+    uint64_t acc = 0;
+    for (uint64_t r = 0; r < row_num; r++)
+        if (cnt[r]) {
+            acc += cnt[r];
+            if (acc > 0xffffffffull) { why = "nnz exceeds 32 bits"; return false; }
+            out.ends.push_back((uint32_t)acc);
+            out.rid.push_back((uint32_t)(r + row_base));
+            crow.push_back(r);
+        }
+    const uint64_t R = crow.size();
+    if (R == 0 || lvl_rows.empty() || lvl_nzs.size() != lvl_rows.size() + 1 || lvl_nzs.back() != acc || work_size == 0) {
+        why = "merge-path level arrays do not match the matrix";
+        return false;
+    }
+    uint64_t j = 0, gz = 0, gp = 0;
+    out.wz.push_back(0);
+    out.wq.push_back(0);
+    for (uint64_t w = 0; w < lvl_rows.size(); w++) {
+        while (j < R && crow[j] < lvl_rows[w]) j++;
+        const uint64_t p = w * work_size;
+        if (j == R || crow[j] != lvl_rows[w] || p < j || lvl_nzs[w] != p - j) {
+            why = "merge-path level " + std::to_string(w) + " is not on the path";
+            return false;
+        }
+        const uint64_t z = (j >= 1 && p == (uint64_t)out.ends[j - 1] + j - 1) ? (uint64_t)out.ends[j - 1] : p - j;
+        if (w == 0 || p - gp < target_steps || z <= gz) continue;
+        out.wz.push_back((uint32_t)z);
+        out.wq.push_back((uint32_t)j);
+        gz = z;
+        gp = p;
+    }
+    out.wz.push_back((uint32_t)acc);
+    out.wq.push_back((uint32_t)R);
+    return true;
 }
 
 }  // namespace gsk_host

@@ -140,6 +140,36 @@ void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1)
         ex.add_and_run(std::make_shared<balanced_interval_row_direction_warp_blocking_operator>(cg, per, false, false, ctx));
         ex.add_and_run(std::make_shared<warp_total_reduce_operator>(cg, cf, ctx));
         ex.add_and_run(std::make_shared<grid_block_operator>(cg, 1024u, std::vector<unsigned>{64u, 4u}, cf, ctx));
+    } else if (name == "balanced_block_total") {
+        // balanced row-direction BMTBs (A11, TBLOCK level) + tblock_total (K6): the reference's
+        // name rules accept it (tblock_total_reduce_operator.cc: "tblock" and not "nnz")
+        int per = p0 > 0 ? p0 : 4096, cf = p1 > 0 ? p1 : 1;
+        ex.add_and_run(std::make_shared<balanced_interval_row_direction_tblock_blocking_operator>(cg, per, ctx));
+        int x = std::min(N, 32), y = 256 / std::max(1, x);
+        set_config("VECTOR_WIDTH", x);
+        ex.add_and_run(std::make_shared<tblock_total_reduce_operator>(cg, cf, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, 1024u, std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
+    } else if (name == "balanced_thread_total") {
+        // balanced row-direction BMTs (A11, THREAD level) + thread_total (BMTs of whole rows)
+        int per = p0 > 0 ? p0 : 64, cf = p1 > 0 ? p1 : 1;
+        ex.add_and_run(std::make_shared<balanced_interval_row_direction_thread_blocking_operator>(cg, per, false, false, ctx));
+        ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, false, 4, cf, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, 1024u, std::vector<unsigned>{32u, 4u}, cf, ctx));
+    } else if (name == "merge_path") {
+        // merge-path levels of p0 path steps (A11) at level p1 (WARP: 0 or 1, TBLOCK: 2,
+        // THREAD: 3) + that level's total-reduce token -> k_merge_path (BASELINE.json configs[3])
+        int ws = p0 > 0 ? p0 : 1024, lvl = p1 == 2 ? 2 : (p1 == 3 ? 0 : 1), cf = 1;
+        if (lvl == 0) {
+            ex.add_and_run(std::make_shared<merge_path_thread_operator>(cg, ws, ctx));
+            ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, false, 4, cf, ctx));
+        } else if (lvl == 1) {
+            ex.add_and_run(std::make_shared<merge_path_warp_operator>(cg, ws, ctx));
+            ex.add_and_run(std::make_shared<warp_total_reduce_operator>(cg, cf, ctx));
+        } else {
+            ex.add_and_run(std::make_shared<merge_path_tblock_operator>(cg, ws, ctx));
+            ex.add_and_run(std::make_shared<tblock_total_reduce_operator>(cg, cf, ctx));
+        }
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, 1024u, std::vector<unsigned>{64u, 4u}, cf, ctx));
     } else {
         throw gs_error("unknown pipeline " + name, GS_ERR_ARG);
     }

@@ -31,6 +31,7 @@ const char *kernel_family_name(int f) {
         case KF_BLOCK_TOTAL: return "k_block_rows";
         case KF_BITMAP_SEGMENT: return "k_bitmap_segment";
         case KF_ROW_CHUNKS: return "k_row_chunks";
+        case KF_MERGE_PATH: return "k_merge_path";
         default: return "none";
     }
 }
@@ -68,7 +69,20 @@ void code_generator::compile() {
     const meta_data_set &m = *meta;
     auto tok = [&](POS_TYPE p) -> const reduction_token * { return tokens.count(p) ? &tokens.at(p) : nullptr; };
     const reduction_token *tt = tok(THREAD_META), *tw = tok(WARP_META), *tb = tok(TBLOCK_META);
-    if (tt && tt->kind == reduction_kind::TOTAL_BMT_RESULT &&
+    const reduction_token *tm = merge_level != GLOBAL_META ? tok(merge_level) : nullptr;
+    if (tm && (tm->kind == reduction_kind::TOTAL_BMT_RESULT || tm->kind == reduction_kind::TOTAL_WARP_RESULT ||
+               tm->kind == reduction_kind::TOTAL_BLOCK_RESULT)) {
+        // merge-path levels + the level's total-reduce token (the compositions the
+        // reference's name rules accept: merge_path_{thread,warp,tblock} followed by
+        // {thread,warp,tblock}_total_reduce).  The reference emits no working kernel
+        // for multi-row levels; here they map to k_merge_path.
+        s.family = KF_MERGE_PATH;
+        s.coarsen_factor = tm->coarsen_factor;
+        s.merge_level = merge_level;
+        s.work_size = merge_work_size;
+        const std::string L = convert_pos_type_to_string(merge_level);
+        s.arrays = {L + "_first_row_indices_without_ending_0", L + "_first_nz_indices_0"};
+    } else if (tt && tt->kind == reduction_kind::TOTAL_BMT_RESULT &&
         m.is_exist(THREAD_META, "first_row_indices_without_ending", sub)) {
         // col-direction BMTs (A10) summed per row: K5 warp_bit_map / K7 tblock_bit_map
         s.family = KF_ROW_CHUNKS;
@@ -101,6 +115,21 @@ void code_generator::compile() {
         if (s.warp_segment)
             for (auto k : {"WARP_META_first_row_indices_0", "WARP_META_first_nz_indices_0", "WARP_META_first_BMT_indices_0"})
                 s.arrays.push_back(k);
+    } else if (tt && tt->kind == reduction_kind::TOTAL_BMT_RESULT && !tt->need_warp_reduction &&
+               !m.is_exist(GLOBAL_META, "original_nz_row_indices", sub) &&
+               !m.is_exist(WARP_META, "first_row_indices", sub) && !m.is_exist(TBLOCK_META, "first_row_indices", sub) &&
+               m.is_exist(THREAD_META, "first_row_indices", sub) && [&] {
+                   const auto &fr = m.u(THREAD_META, "first_row_indices", sub);
+                   for (size_t i = 0; i < fr.size(); i++)
+                       if (fr[i] != i) return true;
+                   return false;
+               }()) {
+        // multi-row BMTs (balanced_interval_row_direction_thread_blocking_operator): every BMT
+        // is a run of whole rows, summed row by row -> the wave-per-row-group kernel
+        s.family = KF_WARP_TOTAL;
+        s.group_level = THREAD_META;
+        s.coarsen_factor = tt->coarsen_factor;
+        s.arrays = {"THREAD_META_first_row_indices_0", "THREAD_META_first_nz_indices_0"};
     } else if (tt && tt->kind == reduction_kind::TOTAL_BMT_RESULT) {
         GS_CHECK(!tt->need_warp_reduction,
                  "thread_total with need_warp_reduction (col-direction warp_bit_map plans) is not built in this round");
@@ -187,7 +216,7 @@ std::string code_generator::generate_kernel_file_source(int repeat) const {
                      "d_a0, d_a1, d_col, d_val, d_B, d_C, n_units, n_aux, N, X, 0)";
             break;
         case KF_WARP_TOTAL:
-            o << "    auto wr = rd(\"WARP_META_first_row_indices_0\");\n"
+            o << "    auto wr = rd(\"" << convert_pos_type_to_string(spec.group_level) << "_first_row_indices_0\");\n"
               << "    uint32_t *d_a0 = up(u32(wr)), *d_a1 = nullptr;\n"
               << "    uint32_t *d_a2 = up(gsk_host::csr_row_ptr(rows, wr.back()));\n"
               << "    const uint32_t n_units = wr.size() - 1; uint32_t gx = (n_units + 3) / 4; const bool al = true;\n";
@@ -222,6 +251,23 @@ std::string code_generator::generate_kernel_file_source(int repeat) const {
                      "if (!fin.empty()) gsk::k_finalize_rows<VT><<<dim3((fin.size() * N + 255) / 256), 256>>>("
                      "d_a4, (uint32_t)fin.size(), d_ws, d_C, N)";
             break;
+        case KF_MERGE_PATH: {
+            const std::string L = convert_pos_type_to_string(spec.merge_level);
+            o << "    auto lr = rd(\"" << L << "_first_row_indices_without_ending_0\"), ln = rd(\"" << L
+              << "_first_nz_indices_0\");\n"
+              << "    gsk_host::merge_path_layout lay; std::string why;\n"
+              << "    if (!gsk_host::merge_path_device_layout(rows, row_num, lr, ln, " << spec.work_size
+              << ", 0, 256, lay, why)) { printf(\"%s\\n\", why.c_str()); return 2; }\n"
+              << "    uint32_t *d_a0 = up(lay.wz), *d_a1 = up(lay.wq), *d_a2 = up(lay.ends), *d_a3 = up(lay.rid);\n"
+              << "    const uint32_t n_units = lay.wz.size() - 1, n_crow = lay.ends.size(); const bool al = true;\n"
+              << "    float *d_r0, *d_r1; uint32_t *d_rr; hipMalloc(&d_r0, n_units * N * 4); hipMalloc(&d_r1, n_units * N * 4);\n"
+              << "    hipMalloc(&d_rr, n_units * 4);\n";
+            launch = "gsk::k_merge_path<VT, uint32_t, CF><<<dim3((n_units + 3) / 4, tiles), 256, "
+                     "4 * gsk::merge_path_wave_lds_words(64 / X) * 4>>>(d_a0, d_a1, d_a2, d_a3, n_crow, d_col, d_val, d_B, d_C, "
+                     "d_r0, d_rr, d_r1, n_units, N, X, 0, (uint32_t)M); "
+                     "gsk::k_merge_fixup<VT><<<dim3((n_units * N + 255) / 256), 256>>>(d_rr, d_r0, d_r1, d_C, n_units, N)";
+            break;
+        }
         default:
             throw gs_error("no family");
     }

@@ -48,6 +48,7 @@ enum kernel_family : int {
     KF_BLOCK_TOTAL = 3,     // one workgroup per BMTB row block, LDS reduction
     KF_BITMAP_SEGMENT = 4,  // fixed-nnz BMTs, bitmap row segments, wave-level carry combine
     KF_ROW_CHUNKS = 5,      // col-direction BMTs (chunks of one row), segmented slot tree + row carry
+    KF_MERGE_PATH = 6,      // merge-path levels (A11): nz-balanced wave ranges, row-start flags, carries + fix-up
 };
 const char *kernel_family_name(int f);
 
@@ -60,6 +61,9 @@ struct kernel_spec {
     bool tblock_parent = false;  // BMWs grouped into BMTBs
     bool row_sorted = false;     // GLOBAL original_nz_row_indices present
     POS_TYPE bitmap_parent = THREAD_META;  // K5 (WARP) / K7 (TBLOCK) on col-direction BMTs
+    POS_TYPE merge_level = GLOBAL_META;    // merge-path plans: the level the operator split
+    int work_size = 0;                     // merge-path plans: path steps per level
+    POS_TYPE group_level = WARP_META;      // KF_WARP_TOTAL: level whose first_row_indices are the row groups
     std::array<unsigned, 2> ref_grid{{0, 0}}, ref_block{{0, 0}};
     std::vector<std::string> arrays;  // metadata keys the kernel consumes (= kernel arguments)
     std::string name() const;
@@ -79,6 +83,9 @@ class code_generator {
     const reduction_token &get_reduction_token(POS_TYPE pos) const { return tokens.at(pos); }
     void set_thread_for_row(bool v) { thread_for_row = v; }
     bool get_thread_for_row() const { return thread_for_row; }
+    // merge_path_*_operator: which level holds the merge-path split (the reference opens
+    // TBLOCK for all three, so the level is recorded separately)
+    void set_merge_path_level(POS_TYPE pos, int work_size) { merge_level = pos; merge_work_size = work_size; }
     void set_thread_grid(const std::vector<unsigned> &grid, const std::vector<unsigned> &block);
 
     // lowers the token set to a kernel family (code_generator.hpp:265-269)
@@ -98,6 +105,8 @@ class code_generator {
     std::set<POS_TYPE> opened;
     std::map<POS_TYPE, reduction_token> tokens;
     bool thread_for_row = false;
+    POS_TYPE merge_level = GLOBAL_META;
+    int merge_work_size = 0;
     std::vector<unsigned> grid, block;
     bool compiled = false;
     kernel_spec spec;

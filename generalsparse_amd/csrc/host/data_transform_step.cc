@@ -789,4 +789,119 @@ void get_begin_nzs_of_BMW_after_nnz_blocking_in_row_direction::run(bool check) {
     is_run = true;
 }
 
+// balanced TBLOCK level (get_begin_rows_of_BMTB_after_nnz_blocking_in_row_direction.cc:65-86,
+// get_begin_nzs_of_BMTB_after_nnz_blocking_in_row_direction.cc:55-80): same split rules, TBLOCK arrays
+void get_begin_rows_of_BMTB_after_nnz_blocking_in_row_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    uint64_t row_num = row_num_of_sub_matrix(m, target_matrix_id);
+    auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+    auto v = get_begin_rows_of_child_after_balance_blocking_in_row_direction(cnt, nnz_per_interval, row_num);
+    if (check) GS_CHECK(v.back() == row_num, "balanced BMTB rows must end at the row count (:77)");
+    replace_u(TBLOCK_META, "first_row_indices", std::move(v));
+    src(GLOBAL_META, "nz_row_indices");
+    is_run = true;
+}
+
+void get_begin_nzs_of_BMTB_after_nnz_blocking_in_row_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    uint64_t row_num = row_num_of_sub_matrix(m, target_matrix_id);
+    auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+    auto v = get_begin_nzs_of_child_after_balance_blocking_in_row_direction(cnt, nnz_per_interval);
+    if (check) GS_CHECK(v.back() == row.size(), "balanced BMTB nzs must end at nnz (:72-75)");
+    replace_u(TBLOCK_META, "first_nz_indices", std::move(v));
+    src(GLOBAL_META, "nz_row_indices");
+    is_run = true;
+}
+
+// balanced THREAD level, no parent (get_begin_rows_of_BMT_after_nnz_blocking_in_row_direction.cc:60-81,
+// get_begin_nzs_of_BMT_after_nnz_blocking_in_row_direction.cc:53-88)
+void get_begin_rows_of_BMT_after_nnz_blocking_in_row_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    uint64_t row_num = row_num_of_sub_matrix(m, target_matrix_id);
+    auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+    replace_u(THREAD_META, "first_row_indices",
+              get_begin_rows_of_child_after_balance_blocking_in_row_direction(cnt, nnz_per_interval, row_num));
+    src(GLOBAL_META, "nz_row_indices");
+    is_run = true;
+}
+
+void get_begin_nzs_of_BMT_after_nnz_blocking_in_row_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    uint64_t row_num = row_num_of_sub_matrix(m, target_matrix_id);
+    auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+    auto v = get_begin_nzs_of_child_after_balance_blocking_in_row_direction(cnt, nnz_per_interval);
+    if (check) GS_CHECK(v.back() == row.size(), "balanced BMT nzs must end at nnz (:78-81)");
+    replace_u(THREAD_META, "first_nz_indices", std::move(v));
+    src(GLOBAL_META, "nz_row_indices");
+    is_run = true;
+}
+
+// ------------------------------------------------------- merge path (A11)
+// get_begin_rows_of_level_after_merge_path.cc:58-94 and
+// get_begin_nzs_of_level_after_merge_path.cc:60-95.  The reference finds, for
+// every level start i = 0, ws, 2ws, ... < count, the first non-empty row j with
+// total_path[j] > i by a linear scan from j = 0 (quadratic); i grows, so the
+// scan resumes where the previous one stopped (same j, same outputs).
+// total_path[j] = sum_{t<=j} (nnz_t + 1) - 1 over non-empty rows; the level
+// records row = that row's index and nz = i - j; the nz list ends with nnz.
+void merge_path_levels(const std::vector<uint64_t> &cnt, uint64_t ws, std::vector<uint64_t> *level_rows,
+                       std::vector<uint64_t> *level_nzs) {
+    GS_CHECK(ws > 0, "work_size > 0");
+    std::vector<uint64_t> total_path, path_row;
+    uint64_t count = 0, nnz = 0;
+    bool first = true;
+    for (uint64_t i = 0; i < cnt.size(); i++) {
+        nnz += cnt[i];
+        if (cnt[i] != 0) {
+            count += 1;
+            if (first) { first = false; count -= 1; }
+            count += cnt[i];
+            total_path.push_back(count);
+            path_row.push_back(i);
+        }
+    }
+    uint64_t j = 0;
+    for (uint64_t i = 0; i < count; i += ws) {
+        while (j < total_path.size() && total_path[j] <= i) j++;
+        if (j == total_path.size()) break;  // unreachable: total_path.back() == count > i
+        if (level_rows) level_rows->push_back(path_row[j]);
+        if (level_nzs) level_nzs->push_back(i - j);
+    }
+    if (level_nzs) level_nzs->push_back(nnz);
+}
+
+static std::vector<uint64_t> merge_path_row_counts(const meta_data_set &m, int s) {
+    // :26-50 of either file: row_num from begin/end_row_index raised to the last row in the data
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    uint64_t row_num = row_num_of_sub_matrix(m, s);
+    return get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+}
+
+void get_begin_rows_of_level_after_merge_path::run(bool check) {
+    GS_CHECK(work_size > 0, "work_size > 0");
+    std::vector<uint64_t> rows;
+    merge_path_levels(merge_path_row_counts(*meta_data_set_ptr, target_matrix_id), (uint64_t)work_size, &rows, nullptr);
+    GS_CHECK(!rows.empty(), "merge path over a sub-matrix without nonzeros");
+    replace_u(pos, "first_row_indices_without_ending", std::move(rows));
+    src(GLOBAL_META, "nz_row_indices");
+    src(GLOBAL_META, "begin_row_index");
+    src(GLOBAL_META, "end_row_index");
+    is_run = true;
+}
+
+void get_begin_nzs_of_level_after_merge_path::run(bool check) {
+    GS_CHECK(work_size > 0, "work_size > 0");
+    std::vector<uint64_t> nzs;
+    merge_path_levels(merge_path_row_counts(*meta_data_set_ptr, target_matrix_id), (uint64_t)work_size, nullptr, &nzs);
+    replace_u(pos, "first_nz_indices", std::move(nzs));
+    src(GLOBAL_META, "nz_row_indices");
+    src(GLOBAL_META, "begin_row_index");
+    src(GLOBAL_META, "end_row_index");
+    is_run = true;
+}
+
 }  // namespace gs

@@ -168,6 +168,33 @@ class parent_bit_map_of_thread : public basic_data_transform_step {
 GS_DECLARE_STEP_P(get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction, uint64_t, nnz_per_interval)
 GS_DECLARE_STEP_P(get_begin_nzs_of_BMW_after_nnz_blocking_in_row_direction, uint64_t, nnz_per_interval)
 
+// balanced row-direction TBLOCK / THREAD blocking without a parent (A11;
+// get_begin_{rows,nzs}_of_{BMTB,BMT}_after_nnz_blocking_in_row_direction.cc)
+GS_DECLARE_STEP_P(get_begin_rows_of_BMTB_after_nnz_blocking_in_row_direction, uint64_t, nnz_per_interval)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMTB_after_nnz_blocking_in_row_direction, uint64_t, nnz_per_interval)
+GS_DECLARE_STEP_P(get_begin_rows_of_BMT_after_nnz_blocking_in_row_direction, uint64_t, nnz_per_interval)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMT_after_nnz_blocking_in_row_direction, uint64_t, nnz_per_interval)
+
+// merge-path level splits (A11; get_begin_{rows,nzs}_of_level_after_merge_path.cc).
+// Constructor order as the reference: (meta, target_matrix_id, pos, work_size).
+#define GS_DECLARE_MERGE_PATH(cls)                                                                \
+    class cls : public basic_data_transform_step {                                                \
+      public:                                                                                     \
+        cls(std::shared_ptr<meta_data_set> m, int target_matrix_id, POS_TYPE pos, int work_size)  \
+            : basic_data_transform_step(#cls, std::move(m), target_matrix_id), pos(pos), work_size(work_size) {} \
+        void run(bool check) override;                                                            \
+        POS_TYPE pos;                                                                             \
+        int work_size;                                                                            \
+    };
+GS_DECLARE_MERGE_PATH(get_begin_rows_of_level_after_merge_path)
+GS_DECLARE_MERGE_PATH(get_begin_nzs_of_level_after_merge_path)
+
+// the merge path of a sub-matrix: level starts every work_size path steps,
+// path = one step per nonzero plus one per row change between non-empty rows
+// (get_begin_rows_of_level_after_merge_path.cc:58-94); rows / nzs per level
+void merge_path_levels(const std::vector<uint64_t> &nnz_of_each_row, uint64_t work_size,
+                       std::vector<uint64_t> *level_rows, std::vector<uint64_t> *level_nzs);
+
 std::vector<uint64_t> get_begin_nzs_of_child_after_balance_blocking_in_row_direction(
     const std::vector<uint64_t> &nnz_of_each_row, uint64_t nnz_per_interval);
 std::vector<uint64_t> get_begin_rows_of_child_after_balance_blocking_in_row_direction(

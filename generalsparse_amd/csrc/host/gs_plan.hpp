@@ -18,6 +18,7 @@ struct device_arrays {
     uint32_t *a0 = nullptr, *a1 = nullptr, *a2 = nullptr, *a3 = nullptr, *a4 = nullptr;
     uint64_t *m0 = nullptr;
     float *ws = nullptr;  // k_mfma_rows K-split slabs (per replica: a replica never runs concurrently with itself)
+    float *ws2 = nullptr;  // k_merge_path: partials of the rows each wave closes first (head_rec)
 };
 
 struct device_plan {

@@ -342,6 +342,143 @@ void balanced_interval_row_direction_warp_blocking_operator::run(bool check) {
     is_run = true;
 }
 
+// -------------------------------------- balanced row-direction TBLOCK blocking
+balanced_interval_row_direction_tblock_blocking_operator::balanced_interval_row_direction_tblock_blocking_operator(
+    cg_ptr cg, int per, ctx_ptr)
+    : basic_operator("balanced_interval_row_direction_tblock_blocking_operator", cg->get_metadata_set(),
+                     DISTRIBUTING_OP, cg->get_sub_matrix_id()),
+      nnz_per_interval(per), code_generator_ptr(cg) {
+    GS_CHECK(per > 0, "nnz_per_interval > 0");
+}
+
+// balanced_interval_row_direction_tblock_blocking_operator.cc:29-45: nothing distributed or implemented yet
+bool balanced_interval_row_direction_tblock_blocking_operator::is_valid_according_to_operator(ctx_ptr h) {
+    return h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty() &&
+           h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id).empty();
+}
+
+// :47-87: COO + row bounds, no THREAD / WARP / TBLOCK metadata, no interleaved storage
+bool balanced_interval_row_direction_tblock_blocking_operator::is_valid_according_to_metadata() {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    return coo_present(m, s) && !interlance_storage_existing(m, s) && m.count_of_metadata_of_diff_pos(THREAD_META, s) == 0 &&
+           m.count_of_metadata_of_diff_pos(WARP_META, s) == 0 && m.count_of_metadata_of_diff_pos(TBLOCK_META, s) == 0;
+}
+
+// :89-120
+void balanced_interval_row_direction_tblock_blocking_operator::run(bool check) {
+    if (check) GS_CHECK(is_valid_according_to_metadata(), "balanced tblock blocking: invalid metadata");
+    get_begin_rows_of_BMTB_after_nnz_blocking_in_row_direction a(meta_data_set_ptr, target_matrix_id,
+                                                                (uint64_t)nnz_per_interval);
+    run_step(a, check);
+    get_begin_nzs_of_BMTB_after_nnz_blocking_in_row_direction b(meta_data_set_ptr, target_matrix_id,
+                                                               (uint64_t)nnz_per_interval);
+    run_step(b, check);
+    code_generator_ptr->open_spec_level_of_paral(TBLOCK_META);
+    is_run = true;
+}
+
+// -------------------------------------- balanced row-direction THREAD blocking
+balanced_interval_row_direction_thread_blocking_operator::balanced_interval_row_direction_thread_blocking_operator(
+    cg_ptr cg, int per, bool rrel, bool nrel, ctx_ptr)
+    : basic_operator("balanced_interval_row_direction_thread_blocking_operator", cg->get_metadata_set(),
+                     DISTRIBUTING_OP, cg->get_sub_matrix_id()),
+      nnz_per_interval(per), row_index_is_relative_to_parent(rrel), nz_index_is_relative_to_parent(nrel),
+      code_generator_ptr(cg) {
+    GS_CHECK(per > 0, "nnz_per_interval > 0");
+}
+
+// balanced_interval_row_direction_thread_blocking_operator.cc:35-75: no implementing
+// operator, no distributing one named thread / col / interlance / nnz_direction
+bool balanced_interval_row_direction_thread_blocking_operator::is_valid_according_to_operator(ctx_ptr h) {
+    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return false;
+    auto d = h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
+    return !any_name(d, "thread") && !any_name(d, "col") && !any_name(d, "interlance") && !any_name(d, "nnz_direction");
+}
+
+bool balanced_interval_row_direction_thread_blocking_operator::is_valid_according_to_metadata() {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    bool ok = coo_present(m, s) && m.count_of_metadata_of_diff_pos(THREAD_META, s) == 0 && !interlance_storage_existing(m, s);
+    if (m.is_exist(TBLOCK_META, "first_row_indices", s)) ok = ok && has_row_direction_blocking_in_specific_level(m, TBLOCK_META, s);
+    if (m.is_exist(WARP_META, "first_row_indices", s)) ok = ok && has_row_direction_blocking_in_specific_level(m, WARP_META, s);
+    return ok;
+}
+
+// the no-parent branch of run() (BMT rows / nzs over the whole sub-matrix)
+void balanced_interval_row_direction_thread_blocking_operator::run(bool check) {
+    if (check) GS_CHECK(is_valid_according_to_metadata(), "balanced thread blocking: invalid metadata");
+    if (has(TBLOCK_META, "first_row_indices") || has(WARP_META, "first_row_indices"))
+        throw gs_error("balanced BMTs inside BMTB/BMW parents are not built in this round");
+    if (row_index_is_relative_to_parent || nz_index_is_relative_to_parent)
+        throw gs_error("relative BMT indices need a parent level");
+    get_begin_rows_of_BMT_after_nnz_blocking_in_row_direction a(meta_data_set_ptr, target_matrix_id,
+                                                               (uint64_t)nnz_per_interval);
+    run_step(a, check);
+    get_begin_nzs_of_BMT_after_nnz_blocking_in_row_direction b(meta_data_set_ptr, target_matrix_id,
+                                                              (uint64_t)nnz_per_interval);
+    run_step(b, check);
+    code_generator_ptr->open_spec_level_of_paral(THREAD_META);
+    is_run = true;
+}
+
+// ------------------------------------------------------------- merge path
+merge_path_operator_base::merge_path_operator_base(const char *name, POS_TYPE level, cg_ptr cg, int ws)
+    : basic_operator(name, cg->get_metadata_set(), DISTRIBUTING_OP, cg->get_sub_matrix_id()), work_size(ws),
+      level(level), code_generator_ptr(cg) {
+    GS_CHECK(ws > 0, "work_size > 0");
+}
+
+// merge_path_{tblock,warp}_operator.cc is_valid_according_to_metadata: COO + row bounds,
+// no interleaved storage, no metadata at the levels the operator may not follow
+bool merge_path_operator_base::is_valid_according_to_metadata() {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    bool ok = coo_present(m, s) && !interlance_storage_existing(m, s) && m.count_of_metadata_of_diff_pos(THREAD_META, s) == 0;
+    if (level != THREAD_META) ok = ok && m.count_of_metadata_of_diff_pos(WARP_META, s) == 0;
+    if (level == TBLOCK_META) ok = ok && m.count_of_metadata_of_diff_pos(TBLOCK_META, s) == 0;
+    return ok;
+}
+
+// merge_path_warp_operator.cc:106-133 (same body at TBLOCK / THREAD)
+void merge_path_operator_base::run(bool check) {
+    if (check) GS_CHECK(is_valid_according_to_metadata(), name + ": invalid metadata");
+    get_begin_rows_of_level_after_merge_path a(meta_data_set_ptr, target_matrix_id, level, work_size);
+    run_step(a, check);
+    get_begin_nzs_of_level_after_merge_path b(meta_data_set_ptr, target_matrix_id, level, work_size);
+    run_step(b, check);
+    code_generator_ptr->open_spec_level_of_paral(TBLOCK_META);
+    code_generator_ptr->set_merge_path_level(level, work_size);
+    is_run = true;
+}
+
+merge_path_tblock_operator::merge_path_tblock_operator(cg_ptr cg, int ws, ctx_ptr)
+    : merge_path_operator_base("merge_path_tblock_operator", TBLOCK_META, cg, ws) {}
+merge_path_warp_operator::merge_path_warp_operator(cg_ptr cg, int ws, ctx_ptr)
+    : merge_path_operator_base("merge_path_warp_operator", WARP_META, cg, ws) {}
+merge_path_thread_operator::merge_path_thread_operator(cg_ptr cg, int ws, ctx_ptr)
+    : merge_path_operator_base("merge_path_thread_operator", THREAD_META, cg, ws) {}
+
+// merge_path_tblock_operator.cc: nothing distributed or implemented yet
+bool merge_path_tblock_operator::is_valid_according_to_operator(ctx_ptr h) {
+    return h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty() &&
+           h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id).empty();
+}
+
+// merge_path_warp_operator.cc:26-63: no distributing op named thread / warp / col / interlance
+bool merge_path_warp_operator::is_valid_according_to_operator(ctx_ptr h) {
+    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return false;
+    auto d = h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
+    return !any_name(d, "thread") && !any_name(d, "warp") && !any_name(d, "col") && !any_name(d, "interlance");
+}
+
+// merge_path_thread_operator.cc: no distributing op named thread / col / interlance
+bool merge_path_thread_operator::is_valid_according_to_operator(ctx_ptr h) {
+    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return false;
+    auto d = h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
+    return !any_name(d, "thread") && !any_name(d, "col") && !any_name(d, "interlance");
+}
+
 // ------------------------------------------- col-direction THREAD blocking (A10)
 fixed_interval_col_direction_thread_blocking_operator::fixed_interval_col_direction_thread_blocking_operator(
     cg_ptr cg, int fcs, bool rrel, bool nrel, bool pad_size, bool pad_max, ctx_ptr history)
@@ -774,6 +911,18 @@ std::shared_ptr<basic_operator> make_operator(const std::string &name, const std
         return std::make_shared<balanced_interval_row_direction_warp_blocking_operator>(cg, (int)a[0], a[1] != 0,
                                                                                         a[2] != 0, ctx);
     }
+    if (name == "balanced_interval_row_direction_tblock_blocking_operator") {
+        need(1);
+        return std::make_shared<balanced_interval_row_direction_tblock_blocking_operator>(cg, (int)a[0], ctx);
+    }
+    if (name == "balanced_interval_row_direction_thread_blocking_operator") {
+        need(3);
+        return std::make_shared<balanced_interval_row_direction_thread_blocking_operator>(cg, (int)a[0], a[1] != 0,
+                                                                                          a[2] != 0, ctx);
+    }
+    if (name == "merge_path_tblock_operator") { need(1); return std::make_shared<merge_path_tblock_operator>(cg, (int)a[0], ctx); }
+    if (name == "merge_path_warp_operator") { need(1); return std::make_shared<merge_path_warp_operator>(cg, (int)a[0], ctx); }
+    if (name == "merge_path_thread_operator") { need(1); return std::make_shared<merge_path_thread_operator>(cg, (int)a[0], ctx); }
     if (name == "thread_total_reduce_operator") {
         need(3);
         return std::make_shared<thread_total_reduce_operator>(cg, a[0] != 0, (int)a[1], (int)a[2], ctx);

@@ -163,6 +163,78 @@ class balanced_interval_row_direction_warp_blocking_operator : public basic_oper
     cg_ptr code_generator_ptr;
 };
 
+// balanced row-direction TBLOCK blocking (operator/balanced_interval_row_direction_tblock_blocking_operator.cc)
+class balanced_interval_row_direction_tblock_blocking_operator : public basic_operator {
+  public:
+    balanced_interval_row_direction_tblock_blocking_operator(cg_ptr cg, int nnz_per_interval, ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    std::string convert_to_string() const override {
+        return basic_operator::convert_to_string() + ",nnz_per_interval:" + std::to_string(nnz_per_interval);
+    }
+    int nnz_per_interval;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
+// balanced row-direction THREAD blocking (operator/balanced_interval_row_direction_thread_blocking_operator.cc)
+class balanced_interval_row_direction_thread_blocking_operator : public basic_operator {
+  public:
+    balanced_interval_row_direction_thread_blocking_operator(cg_ptr cg, int nnz_per_interval,
+                                                             bool row_index_is_relative, bool nz_index_is_relative,
+                                                             ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    std::string convert_to_string() const override {
+        return basic_operator::convert_to_string() + ",nnz_per_interval:" + std::to_string(nnz_per_interval);
+    }
+    int nnz_per_interval;
+    bool row_index_is_relative_to_parent, nz_index_is_relative_to_parent;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
+// merge-path distribution at one level (operator/merge_path_{tblock,warp,thread}_operator.cc).
+// All three open TBLOCK in the reference whatever their level (:118/:131/:133);
+// kept, plus the level recorded for the code generator.
+class merge_path_operator_base : public basic_operator {
+  public:
+    merge_path_operator_base(const char *name, POS_TYPE level, cg_ptr cg, int work_size);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    std::string convert_to_string() const override {
+        return basic_operator::convert_to_string() + ",work_size:" + std::to_string(work_size);
+    }
+    int get_work_size() const { return work_size; }
+    int work_size;
+    POS_TYPE level;
+
+  protected:
+    cg_ptr code_generator_ptr;
+};
+
+class merge_path_tblock_operator : public merge_path_operator_base {
+  public:
+    merge_path_tblock_operator(cg_ptr cg, int work_size, ctx_ptr history);
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+};
+
+class merge_path_warp_operator : public merge_path_operator_base {
+  public:
+    merge_path_warp_operator(cg_ptr cg, int work_size, ctx_ptr history);
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+};
+
+class merge_path_thread_operator : public merge_path_operator_base {
+  public:
+    merge_path_thread_operator(cg_ptr cg, int work_size, ctx_ptr history);
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+};
+
 // operator/fixed_interval_col_direction_thread_blocking_operator.cc (A10): BMTs are
 // chunks of fixed_col_block_size nnz along each row
 class fixed_interval_col_direction_thread_blocking_operator : public basic_operator {

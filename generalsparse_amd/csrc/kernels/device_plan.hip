@@ -53,6 +53,12 @@ std::vector<uint32_t> csr_row_ptr(const std::vector<uint64_t> &row, uint64_t row
     return rp;
 }
 
+uint32_t pow2ceil_u(uint32_t x) {
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
 uint16_t f32_to_f16_bits(float f) {
     _Float16 h = (_Float16)f;
     uint16_t b;
@@ -517,14 +523,14 @@ void upload_plan(plan_state &p, int dtype, int device) {
             break;
         }
         case KF_WARP_TOTAL: {
-            a.a0 = dev_copy(d, to_u32(m.u(WARP_META, "first_row_indices", 0), "BMW first_row_indices"));
+            a.a0 = dev_copy(d, to_u32(m.u(sp.group_level, "first_row_indices", 0), "BMW first_row_indices"));
             if (sp.tblock_parent) {
                 a.a1 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_BMW_indices", 0), "first_BMW_indices"));
                 d.n_rows_aux = m.u(TBLOCK_META, "first_BMW_indices", 0).size() - 1;  // BMTB count
             }
             std::vector<uint32_t> rp = csr_row_ptr(rows, row_num);
             a.a2 = dev_copy(d, rp);
-            d.n_units = m.u(WARP_META, "first_row_indices", 0).size() - 1;
+            d.n_units = m.u(sp.group_level, "first_row_indices", 0).size() - 1;
             d.scf = 4;
             if (sp.tblock_parent && try_mfma(rp)) break;
             // LDS-stationary B pays off for row blocks of >= 16 rows in BMWs of >= 2 rows
@@ -646,6 +652,32 @@ void upload_plan(plan_state &p, int dtype, int device) {
             d.n_fin = list.size();
             break;
         }
+        case KF_MERGE_PATH: {
+            // wave ranges decoded from the merge-path levels; S = 64/X slots per wave as launched
+            const POS_TYPE L = sp.merge_level;
+            const uint32_t Nd = (uint32_t)std::max<int64_t>(1, get_config().DENSE_MATRIX_SIZE);
+            const uint32_t cfv = dtype == 0 ? 4u : 8u, cf = Nd % cfv == 0 ? cfv : 1u;
+            const uint32_t X = std::min<uint32_t>(64u, pow2ceil_u((Nd + cf - 1) / cf));
+            const uint64_t target = 4ull * gsk::kMpItems * (64u / X);
+            gsk_host::merge_path_layout lay;
+            std::string why;
+            GS_CHECK(gsk_host::merge_path_device_layout(rows, row_num, m.u(L, "first_row_indices_without_ending", 0),
+                                                         m.u(L, "first_nz_indices", 0), (uint64_t)sp.work_size,
+                                                         (uint32_t)d.row_base, target, lay, why),
+                     "merge-path layout: " + why);
+            a.a0 = dev_copy(d, lay.wz);
+            a.a1 = dev_copy(d, lay.wq);
+            a.a2 = dev_copy(d, lay.ends);
+            a.a3 = dev_copy(d, lay.rid);
+            d.n_units = lay.wz.size() - 1;
+            d.n_rows_aux = lay.ends.size();
+            d.ws_n = Nd;
+            a.ws = dev_copy(d, std::vector<float>((size_t)d.n_units * Nd, 0.f));
+            a.ws2 = dev_copy(d, std::vector<float>((size_t)d.n_units * Nd, 0.f));
+            a.t0 = dev_copy(d, std::vector<uint32_t>(d.n_units, 0xffffffffu));
+            d.scf = 8;
+            break;
+        }
         default:
             throw gs_error("no gfx950 kernel family for this plan");
     }
@@ -687,6 +719,7 @@ void add_replica(plan_state &p) {
     r.t3 = (uint32_t *)dup(s.t3);
     r.t4 = (uint32_t *)dup(s.t4);
     r.ws = (float *)dup(s.ws);
+    r.ws2 = (float *)dup(s.ws2);
     p.dev.replicas.push_back(r);
 }
 
@@ -933,6 +966,22 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
                 hipLaunchKernelGGL((gsk::k_finalize_rows<VT>), dim3(fx), dim3(256), 0, s, a.a4, (uint32_t)d.n_fin,
                                    a.ws, C, N);
             }
+            break;
+        }
+        case KF_MERGE_PATH: {
+            GS_CHECK(N <= d.ws_n, "merge-path plan built for N=" + std::to_string(d.ws_n) +
+                                      ": its carry buffers hold no wider B (re-run the pipeline for this N)");
+            const uint32_t S = 64u / X;
+            const size_t lds = (size_t)4 * gsk::merge_path_wave_lds_words(S) * sizeof(uint32_t);
+            const uint32_t W = (uint32_t)d.n_units;
+            const uint32_t gx = std::min<uint32_t>((W + 3) / 4, 1u << 16);
+            hipLaunchKernelGGL((gsk::k_merge_path<VT, CT, CF>), dim3(std::max(gx, 1u), tiles), dim3(256), lds, s, a.a0,
+                               a.a1, a.a2, a.a3, (uint32_t)d.n_rows_aux, col, val, B, C, a.ws, a.t0, a.ws2, W, N, X,
+                               row_base, (uint32_t)d.n_out_rows);
+            HIP_OK(hipGetLastError());
+            const uint32_t fx = (uint32_t)std::min<uint64_t>(((uint64_t)W * N + 255) / 256, 4096);
+            hipLaunchKernelGGL((gsk::k_merge_fixup<VT>), dim3(std::max(fx, 1u)), dim3(256), 0, s, a.t0, a.ws, a.ws2, C,
+                               W, N);
             break;
         }
         default:

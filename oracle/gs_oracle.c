@@ -780,6 +780,82 @@ int or_balanced_row_dir_warp_blocking(or_set *s, uint64_t per) {
     return 0;
 }
 
+/* A11 at TBLOCK level: balanced_interval_row_direction_tblock_blocking_operator.cc:89-120
+ * (get_begin_{rows,nzs}_of_BMTB_after_nnz_blocking_in_row_direction.cc: the same
+ * split points as the BMW version, written to TBLOCK_META) */
+static int balanced_split(or_set *s, uint64_t per, const char *pos) {
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    uint64_t row_num = row_num_of(s);
+    uint64_t *cnt = row_nnz(R->u, R->len, row_num);
+    vu br = {0}, bn = {0};
+    vu_push(&br, 0);
+    uint64_t nzc = 0;
+    for (uint64_t i = 0; i < row_num; i++) { /* data_transform_common.cc:960-989 */
+        nzc += cnt[i];
+        if (nzc >= per) { vu_push(&br, i + 1); nzc = 0; }
+    }
+    if (br.p[br.n - 1] < row_num) {
+        if (nzc == 0) { free(cnt); free(br.p); return fail(s, "trailing empty rows after last cut (data_transform_common.cc:984)"); }
+        vu_push(&br, row_num);
+    }
+    vu_push(&bn, 0);
+    uint32_t c32 = 0, tot32 = 0; /* data_transform_common.cc:934-957, `unsigned int` counters */
+    for (uint64_t i = 0; i < row_num; i++) {
+        c32 += (uint32_t)cnt[i]; tot32 += (uint32_t)cnt[i];
+        if (c32 >= per) { vu_push(&bn, tot32); c32 = 0; }
+    }
+    if (c32 != 0) vu_push(&bn, tot32);
+    free(cnt);
+    put_u(s, pos, "first_row_indices", 0, br.p, br.n);
+    put_u(s, pos, "first_nz_indices", 0, bn.p, bn.n);
+    return 0;
+}
+
+int or_balanced_row_dir_tblock_blocking(or_set *s, uint64_t per) { return balanced_split(s, per, "TBLOCK_META"); }
+
+/* A11 at THREAD level, no parent: balanced_interval_row_direction_thread_blocking_operator.cc
+ * (get_begin_{rows,nzs}_of_BMT_after_nnz_blocking_in_row_direction.cc:60-88) */
+int or_balanced_row_dir_thread_blocking(or_set *s, uint64_t per) { return balanced_split(s, per, "THREAD_META"); }
+
+/* A11 merge path: get_begin_rows_of_level_after_merge_path.cc:43-98 and
+ * get_begin_nzs_of_level_after_merge_path.cc:43-102, written literally (the
+ * quadratic first-match search over total_path for every level start). */
+int or_merge_path(or_set *s, const char *pos, uint64_t work_size) {
+    if (work_size == 0) return fail(s, "work_size > 0");
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    uint64_t row_num = row_num_of(s);
+    uint64_t *cnt = row_nnz(R->u, R->len, row_num);
+    vu total_path = {0}, path_row = {0}, lr = {0}, ln = {0};
+    uint64_t count = 0;
+    int flag = 1;
+    for (uint64_t i = 0; i < row_num; i++) { /* :64-79 */
+        if (cnt[i] != 0) {
+            count += 1;
+            if (flag) { flag = 0; count -= 1; }
+            count += cnt[i];
+            vu_push(&total_path, count);
+            vu_push(&path_row, i);
+        }
+    }
+    free(cnt);
+    for (uint64_t i = 0; i < count; i += work_size) { /* :84-94 */
+        for (uint64_t j = 0; j < total_path.n; j++) {
+            if (total_path.p[j] > i) {
+                vu_push(&lr, path_row.p[j]);
+                vu_push(&ln, i - j);
+                break;
+            }
+        }
+    }
+    vu_push(&ln, R->len); /* nzs :95 */
+    free(total_path.p);
+    free(path_row.p);
+    if (lr.n == 0) { free(ln.p); return fail(s, "merge path over a sub-matrix without nonzeros"); }
+    put_u(s, pos, "first_row_indices_without_ending", 0, lr.p, lr.n);
+    put_u(s, pos, "first_nz_indices", 0, ln.p, ln.n);
+    return 0;
+}
+
 /* ------------------------------------------------------------------ */
 /* canned pipelines: token_test.cc test_spmm_*                          */
 /* ------------------------------------------------------------------ */
@@ -816,6 +892,13 @@ int or_pipeline(or_set *s, const char *name, int p0, int p1) {
     }
     if (!strcmp(name, "balanced_warp_total")) /* A11 balanced BMW + warp_total */
         return or_balanced_row_dir_warp_blocking(s, (uint64_t)p0);
+    if (!strcmp(name, "balanced_block_total")) /* A11 balanced BMTB + tblock_total */
+        return or_balanced_row_dir_tblock_blocking(s, (uint64_t)(p0 > 0 ? p0 : 4096));
+    if (!strcmp(name, "balanced_thread_total")) /* A11 balanced BMT + thread_total */
+        return or_balanced_row_dir_thread_blocking(s, (uint64_t)(p0 > 0 ? p0 : 64));
+    if (!strcmp(name, "merge_path")) /* A11 merge path; p1: 0/1 WARP, 2 TBLOCK, 3 THREAD */
+        return or_merge_path(s, p1 == 2 ? "TBLOCK_META" : (p1 == 3 ? "THREAD_META" : "WARP_META"),
+                             (uint64_t)(p0 > 0 ? p0 : 1024));
     return fail(s, "unknown pipeline %s", name);
 }
 

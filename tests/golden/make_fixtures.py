@@ -206,6 +206,53 @@ cases.append({
 # (padding_rate_valid_col_direction_with_multiple, data_transform_common.cc:644-690)
 cases.append({"matrix": "ex1", "pipeline": "warp_bit_map", "p0": 32, "expect_error": True})
 
+# merge path (get_begin_{rows,nzs}_of_level_after_merge_path.cc:58-95).  ex1 row nnz
+# [2,0,3,1,5,0]: non-empty rows 0,2,3,4; count starts at 0 for the first row, then
+# +1 per row change: total_path = [2, 6, 8, 14], count 14.  Level starts i = 0,4,8,12:
+# first j with total_path[j] > i -> j = 0,1,3,3 -> rows [0,2,4,4], nz = i - j = [0,3,5,9];
+# the nz list ends with nnz = 11.  (i = 8 lands on the step that closes row 3.)
+cases.append({
+    "matrix": "ex1", "pipeline": "merge_path", "p0": 4, "p1": 1,
+    "expect": {
+        W + "first_row_indices_without_ending_0": [0, 2, 4, 4],
+        W + "first_nz_indices_0": [0, 3, 5, 9, 11],
+    },
+})
+# work_size 3 at TBLOCK: i = 0,3,6,9,12 -> j = 0,1,2,3,3 -> rows [0,2,3,4,4], nz [0,2,4,6,9]
+cases.append({
+    "matrix": "ex1", "pipeline": "merge_path", "p0": 3, "p1": 2,
+    "expect": {
+        B + "first_row_indices_without_ending_0": [0, 2, 3, 4, 4],
+        B + "first_nz_indices_0": [0, 2, 4, 6, 9, 11],
+    },
+})
+# ex2 row nnz [20,0,15,5]: total_path = [20, 36, 42]; work_size 16 at THREAD: i = 0,16,32
+# -> j = 0,0,1 -> rows [0,0,2], nz [0,16,31], then 40
+cases.append({
+    "matrix": "ex2", "pipeline": "merge_path", "p0": 16, "p1": 3,
+    "expect": {
+        T + "first_row_indices_without_ending_0": [0, 0, 2],
+        T + "first_nz_indices_0": [0, 16, 31, 40],
+    },
+})
+# balanced TBLOCK blocking, 16 nnz per BMTB (data_transform_common.cc:934-989 at TBLOCK)
+cases.append({
+    "matrix": "ex2", "pipeline": "balanced_block_total", "p0": 16,
+    "expect": {
+        B + "first_row_indices_0": [0, 1, 4],
+        B + "first_nz_indices_0": [0, 20, 40],
+    },
+})
+# balanced THREAD blocking, 6 nnz per BMT: rows 0 (20) cut, row1 empty + row2 (15) cut,
+# row3 (5) left over -> rows [0,1,3,4], nzs [0,20,35,40]
+cases.append({
+    "matrix": "ex2", "pipeline": "balanced_thread_total", "p0": 6,
+    "expect": {
+        T + "first_row_indices_0": [0, 1, 3, 4],
+        T + "first_nz_indices_0": [0, 20, 35, 40],
+    },
+})
+
 out = {"matrices": {"ex1": EX1, "ex2": EX2, "ex3": EX3, "ex4": EX4}, "cases": cases}
 path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hand_plans.json")
 with open(path, "w") as f:

@@ -21,7 +21,10 @@ DEV = "cuda:0"
 PIPES = [("thread_total", 4, 1), ("thread_total", 8, 1), ("warp_total", 0, 1), ("block_total", 0, 1),
          ("block_total", 20, 1),
          ("thread_bit_map", 4, 1), ("warp_segment", 4, 1), ("tblock_warp_total", 4, 1),
-         ("tblock_warp_total", 16, 1), ("balanced_warp_total", 256, 1)]
+         ("tblock_warp_total", 16, 1), ("balanced_warp_total", 256, 1),
+         ("merge_path", 1024, 1), ("merge_path", 64, 1), ("merge_path", 7, 3), ("merge_path", 4096, 2),
+         ("balanced_block_total", 512, 1), ("balanced_thread_total", 64, 1)]
+BALANCED = ("balanced_warp_total", "balanced_block_total", "balanced_thread_total")
 TOL = {"f32": 1e-3, "f16": 1e-1}
 
 
@@ -58,7 +61,7 @@ def coo_cases():
 def test_spmm_matches_oracle(pipe, N, dtype):
     name, p0, p1 = pipe
     for case, M, K, row, col, val in coo_cases():
-        if name == "balanced_warp_total" and case == "ragged":
+        if name in BALANCED and case == "ragged":
             continue  # trailing empty rows: the reference splitter asserts (tested on CPU)
         plan, C, B = run(M, K, row, col, val, name, p0, p1, N, dtype)
         v = val.astype(np.float16).astype(np.float32) if dtype == "f16" else val
@@ -379,3 +382,49 @@ def test_mfma_rows_ksplit_combine(ks, mfma_everywhere):
         np.testing.assert_array_equal(ones, np.repeat(nnz_row[:, None], N, axis=1))
     finally:
         gsa.set_config("MFMA_KSPLIT", 0)
+
+
+# merge-path plans (A11, C4): rows crossing waves, waves closing rows exactly at their
+# end, long runs of empty rows (leading, inner, trailing), one-nnz rows
+def merge_cases():
+    rng = np.random.default_rng(21)
+    M, K = 5000, 700
+    lens = rng.integers(0, 4, M)
+    lens[:37] = 0                      # leading empty rows
+    lens[-101:] = 0                    # trailing empty rows
+    lens[1000:1400] = 0                # inner run of empty rows
+    lens[2000] = 9000                  # a row crossing many waves
+    lens[2001] = 513
+    rows = np.repeat(np.arange(M, dtype=np.uint64), lens)
+    cols = (rng.integers(0, K, len(rows))).astype(np.uint64)
+    yield "mixed", M, K, rows, cols, rng.uniform(-1, 1, len(rows)).astype(np.float32)
+    r, c, v = ds.rmat(4096, 60000, seed=3)
+    yield "rmat", 4096, 4096, r, c, v
+    rows = np.arange(2048, dtype=np.uint64)  # one nnz per row
+    yield "diag", 2048, 2048, rows, rows.copy(), np.linspace(-1, 1, 2048).astype(np.float32)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f16"])
+@pytest.mark.parametrize("N", [8, 3, 64])
+@pytest.mark.parametrize("ws,level", [(1024, 1), (37, 1), (1, 3), (512, 2), (100000, 1)])
+def test_merge_path_matches_oracle(ws, level, N, dtype):
+    for case, M, K, row, col, val in merge_cases():
+        plan, C, B = run(M, K, row, col, val, "merge_path", ws, level, N, dtype)
+        assert plan.info()["kernel_name"].startswith("k_merge_path"), plan.info()["kernel_name"]
+        v = val.astype(np.float16).astype(np.float32) if dtype == "f16" else val
+        ref = ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64")
+        check(C, ref, dtype)
+
+
+def test_merge_path_deterministic_and_no_stale_state():
+    """two launches give bit-identical C (no atomics; carries re-written every launch),
+    and C's prior content (NaN) is fully overwritten, empty rows included"""
+    M, K, row, col, val = next(merge_cases())
+    plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline("merge_path", 8, 64, 1).compile().upload("f32", 0)
+    B = torch.from_numpy(np.random.default_rng(4).uniform(-1, 1, (K, 8)).astype(np.float32)).to(DEV)
+    C1 = torch.full((M, 8), float("nan"), device=DEV)
+    plan.spmm(B, C=C1)
+    C2 = plan.spmm(B)
+    torch.cuda.synchronize()
+    assert not torch.isnan(C1).any()
+    assert torch.equal(C1, C2)

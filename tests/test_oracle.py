@@ -31,7 +31,7 @@ def test_oracle_matches_hand_derived(case_id):
     g = load_golden()
     case = g["cases"][case_id]
     M, K, row, col, val = coo_of(g["matrices"][case["matrix"]])
-    got, err = ofi.run_pipeline(M, K, row, col, val, case["pipeline"], case["p0"])
+    got, err = ofi.run_pipeline(M, K, row, col, val, case["pipeline"], case["p0"], case.get("p1", 0))
     if case.get("expect_error"):
         assert got is None and err
         return

@@ -43,7 +43,8 @@ def product_plan(M, K, row, col, val, name, N, p0=0, p1=0):
 
 
 def compare(M, K, row, col, val, name, N, p0=0, p1=0):
-    exp, err = ofi.run_pipeline(M, K, row, col, val, name, oracle_params(name, N, p0, p1))
+    exp, err = ofi.run_pipeline(M, K, row, col, val, name, oracle_params(name, N, p0, p1),
+                                p1 if name == "merge_path" else 0)
     if err is not None:
         with pytest.raises(gsa.GsError):
             product_plan(M, K, row, col, val, name, N, p0, p1)
@@ -72,7 +73,9 @@ PIPES = [("thread_total", 32, 4, 1), ("thread_total", 8, 8, 1), ("warp_total", 3
          ("block_total", 8, 0, 1), ("thread_bit_map", 32, 4, 1), ("thread_bit_map", 8, 4, 2),
          ("warp_segment", 32, 4, 1), ("warp_segment", 8, 4, 1), ("tblock_warp_total", 32, 4, 1),
          ("tblock_warp_total", 32, 7, 1), ("balanced_warp_total", 32, 64, 1), ("warp_bit_map", 32, 4, 1),
-         ("tblock_bit_map", 32, 4, 1)]
+         ("tblock_bit_map", 32, 4, 1), ("balanced_block_total", 32, 64, 1), ("balanced_block_total", 8, 7, 1),
+         ("balanced_thread_total", 8, 16, 1), ("merge_path", 8, 16, 1), ("merge_path", 8, 7, 2),
+         ("merge_path", 32, 5, 3), ("merge_path", 8, 1, 1), ("merge_path", 8, 1024, 1)]
 
 # col-direction pipelines need rows long enough for the 64-nnz padding rule
 COL_PIPES = [("warp_bit_map", 32, 4, 1), ("warp_bit_map", 8, 4, 2), ("warp_bit_map", 1, 4, 1),
@@ -116,6 +119,7 @@ def test_plan_edge_shapes(pipe):
 def test_hand_derived_fixtures_through_product():
     g = json.load(open(GOLDEN))
     back = {"thread_total": (32, 4, 1), "warp_total": (32, 0, 1), "block_total": (8, 0, 1),
+            "merge_path": (8, 0, 1), "balanced_block_total": (32, 0, 1), "balanced_thread_total": (8, 0, 1),
             "tblock_warp_total": (32, 4, 1), "balanced_warp_total": (32, 16, 1),
             "warp_bit_map": (32, 4, 1), "tblock_bit_map": (32, 4, 1)}
     for case in g["cases"]:
@@ -128,8 +132,11 @@ def test_hand_derived_fixtures_through_product():
             N, p0, p1 = case["p0"], 4, 1  # VW = min(N, 32) = fixture VW
         else:
             N, p0, p1 = back[name]
-            if name in ("tblock_warp_total", "balanced_warp_total"):
+            if name in ("tblock_warp_total", "balanced_warp_total", "merge_path", "balanced_block_total",
+                        "balanced_thread_total"):
                 p0 = case["p0"]
+            if name == "merge_path":
+                p1 = case["p1"]
         if case.get("expect_error"):
             with pytest.raises(gsa.GsError):
                 product_plan(m["M"], m["K"], row, col, val, name, N, p0, p1)
