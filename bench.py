@@ -45,13 +45,16 @@ def parse():
     ap.add_argument("--rotation-mb", type=float, default=640.0)
     ap.add_argument("--no-rocsparse", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--workload", choices=("c2", "c3"), default="c2")
+    ap.add_argument("--p0", type=int, default=None, help="with --pipeline: run only this plan parameter")
+    ap.add_argument("--p1", type=int, default=None)
+    ap.add_argument("--workload", choices=("c2", "c3", "c4", "c4o"), default="c2")
     ap.add_argument("--M", type=int, default=0)
     ap.add_argument("--K", type=int, default=0)
     ap.add_argument("--N", type=int, default=0)
     ap.add_argument("--sparsity", type=float, default=0.7)
     a = ap.parse_args()
-    dflt = {"c2": (5120, 5120, 32), "c3": (28672, 7168, 128)}[a.workload]
+    dflt = {"c2": (5120, 5120, 32), "c3": (28672, 7168, 128), "c4": (1000005, 1000005, 8),
+            "c4o": (3072441, 3072441, 8)}[a.workload]
     a.M, a.K, a.N = a.M or dflt[0], a.K or dflt[1], a.N or dflt[2]
     return a
 
@@ -62,8 +65,17 @@ WORKLOADS = {
            "data": "synthetic (seeded magnitude-pruned Gaussian)"},
     "c3": {"metric": "SpMM GFLOP/s + achieved HBM GB/s vs rocSPARSE, 2:4 pruned-weight fp16 N=128 (configs[2])",
            "workload": "OPT-30B fc1 stand-in {M}x{K} 2:4 structured, fp16, N={N}",
-           "data": "synthetic (seeded Gaussian, 2:4 magnitude pruning per group of 4)"},
+           "data": "synthetic (seeded Gaussian, 2:4 magnitude pruning per group of 4)", "dtype": "f16"},
+    "c4": {"metric": "SpMM GFLOP/s + achieved HBM GB/s vs rocSPARSE, power-law fp32 N=8 (configs[3], webbase-1M)",
+           "workload": "webbase-1M stand-in {M}x{K} nnz 3105536 R-MAT(.57,.19,.19), fp32, N={N}",
+           "data": "synthetic (seeded R-MAT, deduplicated, row-sorted; SuiteSparse files are not available offline)",
+           "dtype": "f32", "nnz": 3105536, "seed": 1, "symmetric": False},
+    "c4o": {"metric": "SpMM GFLOP/s + achieved HBM GB/s vs rocSPARSE, power-law fp32 N=8 (configs[3], com-Orkut)",
+            "workload": "com-Orkut stand-in {M}x{K} nnz 234370166 symmetric R-MAT(.57,.19,.19), fp32, N={N}",
+            "data": "synthetic (seeded R-MAT, symmetrised, deduplicated, row-sorted)",
+            "dtype": "f32", "nnz": 234370166, "seed": 2, "symmetric": True},
 }
+WORKLOADS["c2"]["dtype"] = "f16"
 
 
 # (pipeline, p0, p1).  tblock_warp_total(rows per BMTB, rows per BMW) runs the
@@ -76,6 +88,10 @@ CANDIDATES = [("block_total", 20, 1), ("block_total", 10, 1), ("block_total", 40
 
 # C3: the col-direction plan (32-nnz BMTs = 64-column k-steps of a 2:4 row)
 CANDIDATES_C3 = [("col_direction_nm", 32, 1)]
+
+# C4: merge-path levels (WARP, work_size p0) and the balanced / row-per-thread plans
+CANDIDATES_C4 = [("merge_path", 1024, 1), ("merge_path", 4096, 1), ("balanced_block_total", 2048, 1),
+                 ("thread_total", 4, 1)]
 
 
 def kernel_label(info):
@@ -202,8 +218,15 @@ def main():
 
     M, K, N = args.M, args.K, args.N
     wl = WORKLOADS[args.workload]
-    e, s_idx = 2, (2 if K <= 65536 else 4)
-    if args.workload == "c3":
+    dt = wl["dtype"]
+    tdt = torch.float16 if dt == "f16" else torch.float32
+    e, s_idx = (2 if dt == "f16" else 4), (2 if K <= 65536 else 4)
+    if args.workload in ("c4", "c4o"):
+        row, col, val = ds.rmat(M, wl["nnz"], wl["seed"] + rank, symmetric=wl["symmetric"])
+        nnz = len(row)
+        alg_bytes = algorithmic_bytes(M, K, N, nnz, e, s_idx)
+        cand_list = CANDIDATES_C4
+    elif args.workload == "c3":
         row, col, val = ds.two_four(M, K, 30 + rank)
         nnz = len(row)
         alg_bytes = algorithmic_bytes_24(M, K, N, nnz, e)
@@ -217,20 +240,26 @@ def main():
 
     cands = cand_list if args.pipeline == "auto" else [c for c in cand_list if c[0] == args.pipeline] or \
         [(args.pipeline, 0, 1)]
+    if args.p0 is not None:  # one variant (profiling runs)
+        cands = [(c[0], args.p0, c[2] if args.p1 is None else args.p1) for c in cands[:1]]
     variants = {}
     best = None
     for name, p0, p1 in cands:
         t0 = time.perf_counter()
-        plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline(name, N, p0, p1).compile()
+        try:
+            plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline(name, N, p0, p1).compile()
+        except gsa.GsError as ex:  # e.g. the balanced splitter on trailing empty rows
+            variants[f"{name}({p0},{p1})"] = {"error": str(ex)}
+            continue
         t_plan = time.perf_counter() - t0
-        plan.upload("f16", local)
+        plan.upload(dt, local)
         info = plan.info()
-        per_rep = info["device_bytes_A"] + K * N * 2
+        per_rep = info["device_bytes_A"] + K * N * e
         reps = max(2, int(math.ceil(args.rotation_mb * 1e6 / per_rep)))
         for _ in range(reps - 1):
             plan.add_replica()
-        Bs = [torch.randn((K, N), device=dev, dtype=torch.float16) for _ in range(reps)]
-        Cs = [torch.empty((M, N), device=dev, dtype=torch.float16) for _ in range(reps)]
+        Bs = [torch.randn((K, N), device=dev, dtype=tdt) for _ in range(reps)]
+        Cs = [torch.empty((M, N), device=dev, dtype=tdt) for _ in range(reps)]
         wall, ev_ms = time_plan(plan, Bs, Cs, N, args.steps, args.warmup, torch, dist)
         key = f"{name}({p0},{p1})"
         variants[key] = {"ms_per_step": round(wall / args.steps * 1e3, 5), "kernel_ms": round(ev_ms, 5),
@@ -258,7 +287,7 @@ def main():
         "metric": wl["metric"],
         "value": round(value, 1), "unit": "GFLOP/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 5), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "f16 (fp32 accumulate)", "data": wl["data"],
+        "dtype": "f16 (fp32 accumulate)" if dt == "f16" else "f32", "data": wl["data"],
         "config": {"workload": wl["workload"].format(M=M, K=K, N=N),
                    "M": M, "K": K, "N": N, "nnz": nnz, "plan": key, "kernel": kernel_label(info),
                    "replicas_rotated": reps, "parallelism": f"row-sharded batch x{world}"},
@@ -267,7 +296,15 @@ def main():
                      "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": round(ev_ms, 5)},
         "variants": variants,
     }
-    if rank == 0 and not args.no_rocsparse:
+    if rank == 0 and not args.no_rocsparse and dt == "f32":
+        try:
+            rs32 = rocsparse_baseline(M, K, N, row, col, val, min(reps, 20), dtype=0)
+            out["rocsparse"] = {"f32": rs32}
+            if rs32:
+                out["speedup_vs_rocsparse"] = round(flops / (ev_ms * 1e-3) / 1e9 / rs32["gflops"], 3)
+        except Exception as ex:
+            out["rocsparse"] = {"error": str(ex)}
+    elif rank == 0 and not args.no_rocsparse:
         try:
             rs16 = rocsparse_baseline(M, K, N, row, col, val, min(reps, 20), dtype=1)
             rs32 = rocsparse_baseline(M, K, N, row, col, val, min(reps, 20), dtype=0)
@@ -296,7 +333,8 @@ def main():
         except Exception as ex:  # comparator problems must not hide the main number
             out["rocsparse"] = {"error": str(ex)}
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(M, K, N, row, col, val, row_share=8 if args.workload == "c3" else 1)
+        share = {"c3": 8, "c4o": 64}.get(args.workload, 1)
+        out["cpu_baseline"] = cpu_baseline(M, K, N, row, col, val, row_share=share)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

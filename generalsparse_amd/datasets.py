@@ -57,7 +57,7 @@ def rmat(scale_n, nnz, seed, a=0.57, b=0.19, c=0.19, symmetric=False):
     """R-MAT power-law graph (C4 stand-ins), deduplicated, row-sorted."""
     rng = np.random.default_rng(seed)
     levels = int(np.ceil(np.log2(scale_n)))
-    n = int(nnz * 1.3) + 1024
+    n = int((nnz // 2 if symmetric else nnz) * 1.3) + 1024  # symmetric: each sample gives 2 entries
     r = np.zeros(n, np.int64)
     cc = np.zeros(n, np.int64)
     for _ in range(levels):
@@ -70,7 +70,9 @@ def rmat(scale_n, nnz, seed, a=0.57, b=0.19, c=0.19, symmetric=False):
     r, cc = r[keep], cc[keep]
     if symmetric:
         r, cc = np.concatenate([r, cc]), np.concatenate([cc, r])
-    key = np.unique(r * scale_n + cc)[: nnz]
+    key = np.unique(r * scale_n + cc)
+    if len(key) > nnz:  # exact nnz: a seeded random subset (not the lowest rows)
+        key = np.sort(rng.choice(key, size=nnz, replace=False))
     row = (key // scale_n).astype(np.uint64)
     col = (key % scale_n).astype(np.uint64)
     val = rng.uniform(-1, 1, size=len(row)).astype(np.float32)

@@ -419,7 +419,7 @@ def test_merge_path_matches_oracle(ws, level, N, dtype):
 def test_merge_path_deterministic_and_no_stale_state():
     """two launches give bit-identical C (no atomics; carries re-written every launch),
     and C's prior content (NaN) is fully overwritten, empty rows included"""
-    M, K, row, col, val = next(merge_cases())
+    _, M, K, row, col, val = next(merge_cases())
     plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline("merge_path", 8, 64, 1).compile().upload("f32", 0)
     B = torch.from_numpy(np.random.default_rng(4).uniform(-1, 1, (K, 8)).astype(np.float32)).to(DEV)
     C1 = torch.full((M, 8), float("nan"), device=DEV)
