@@ -90,7 +90,7 @@ CANDIDATES = [("block_total", 20, 1), ("block_total", 10, 1), ("block_total", 40
 CANDIDATES_C3 = [("col_direction_nm", 32, 1)]
 
 # C4: merge-path levels (WARP, work_size p0) and the balanced / row-per-thread plans
-CANDIDATES_C4 = [("merge_path", 1024, 1), ("merge_path", 4096, 1), ("balanced_block_total", 2048, 1),
+CANDIDATES_C4 = [("merge_path", 256, 1), ("merge_path", 512, 1), ("merge_path", 1024, 1), ("balanced_block_total", 2048, 1),
                  ("thread_total", 4, 1)]
 
 

@@ -1365,16 +1365,18 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
 //   3. a segmented scan over slots (stop = any row start/close in the slot)
 //      gives every slot its carry-in; held-back heads add it and are stored;
 //      the last slot's scan value is carried into the next round.
-// Each closed row also zero-fills the empty rows before it (and the last one
-// the rows after it), so C needs no memset.  Rows crossing waves: the wave the
+// Empty rows are zeroed from a list by the kernel's first fill_blocks
+// workgroups, concurrently with the path waves (no memset of C, no extra
+// launch).  Rows crossing waves: the wave the
 // row is open at the end of writes (rid, partial) to rec/rec_row, the wave
 // that closes it writes its own partial to head_rec instead of C, and
 // k_merge_fixup sums them in wave order (deterministic, one rounding).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kMpItems = 8;  // nonzeros per slot per round
 
+// per wave: row-start flags (bytes 0..8S) and the staged output rows rid_l (cap + 2)
 __host__ __device__ constexpr uint32_t merge_path_wave_lds_words(uint32_t S) {
-    return (kMpItems * S) / 4u + 2u + 2u * (kMpItems * S + 64u) + 2u;
+    return (kMpItems * S) / 4u + 2u + (kMpItems * S + 64u) + 2u;
 }
 
 template <class VT, class CT, int CF>
@@ -1387,7 +1389,25 @@ __global__ __launch_bounds__(256) void k_merge_path(const uint32_t *__restrict__
                                                     VT *__restrict__ C, float *__restrict__ rec,
                                                     uint32_t *__restrict__ rec_row, float *__restrict__ head_rec,
                                                     uint32_t n_waves, uint32_t N, uint32_t X, uint32_t row_lo,
-                                                    uint32_t row_hi) {
+                                                    uint32_t row_hi, const uint32_t *__restrict__ empty_rows,
+                                                    uint32_t n_empty, uint32_t fill_blocks, uint32_t dbg = 0) {
+    // dbg (diagnostic timing runs only, wrong results): bit 1 gathers B row 0 for every nonzero
+    if (blockIdx.x < fill_blocks) {
+        // the first fill_blocks workgroups zero the empty rows (listed; 16-B stores when a
+        // C row is whole 16-B units) while the path waves run
+        const uint32_t rbytes = N * (uint32_t)sizeof(VT);
+        const uint32_t U = rbytes % 16u == 0 ? rbytes / 16u : N;
+        const uint32_t tot = blockIdx.y == 0 ? n_empty * U : 0u;  // one column-tile row of blocks fills
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += fill_blocks * blockDim.x) {
+            const uint32_t er = empty_rows[i / U];
+            if (rbytes % 16u == 0)
+                *reinterpret_cast<uint4 *>(reinterpret_cast<unsigned char *>(C) + (size_t)er * rbytes + (i % U) * 16u) =
+                    make_uint4(0u, 0u, 0u, 0u);
+            else
+                C[(size_t)er * N + i % U] = (VT)0.f;
+        }
+        return;
+    }
     extern __shared__ uint32_t mp_lds[];
     const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
     const uint32_t xl = lane & (X - 1u), slot = lane / X, S = 64u / X;
@@ -1396,15 +1416,14 @@ __global__ __launch_bounds__(256) void k_merge_path(const uint32_t *__restrict__
     const uint32_t cap = R8 + 64u;        // staged rows per round
     uint32_t *wl = mp_lds + wib * merge_path_wave_lds_words(S);
     unsigned char *flags = reinterpret_cast<unsigned char *>(wl);
-    uint32_t *ends_l = wl + fw;           // ends[qs + k]
-    uint32_t *rid_l = ends_l + cap;       // rid[qs - 1 + k]
-    const uint32_t waves_total = gridDim.x * (blockDim.x >> 6);
+    uint32_t *rid_l = wl + fw;            // rid[qs - 1 + k]
+    const uint32_t waves_total = (gridDim.x - fill_blocks) * (blockDim.x >> 6);
     typedef typename raw_vec<CF * sizeof(VT)>::t RB;
     for (uint32_t ct = blockIdx.y; ct * X * CF < N; ct += gridDim.y) {
         const uint32_t cw = ct * X * CF + xl * CF;
         const bool cok = cw < N;
         const uint32_t c0 = cok ? cw : 0u;
-        for (uint32_t w = blockIdx.x * (blockDim.x >> 6) + wib; w < n_waves; w += waves_total) {
+        for (uint32_t w = (blockIdx.x - fill_blocks) * (blockDim.x >> 6) + wib; w < n_waves; w += waves_total) {
             const uint32_t zlo = wz[w], wend = wz[w + 1], q0 = wq[w];
             // the wave starts inside row q0 (its partial goes to head_rec)
             const bool head_open = zlo > (q0 ? ends[q0 - 1] : 0u);
@@ -1415,57 +1434,78 @@ __global__ __launch_bounds__(256) void k_merge_path(const uint32_t *__restrict__
             bool closed_end = false;
             auto emit = [&](uint32_t qq, const float (&a)[CF]) {
                 if (!cok) return;
-                const uint32_t li = qq - qs;
-                const uint32_t rr = rid_l[li + 1], rp = rid_l[li];
                 if (qq == q0 && head_open) {
 #pragma unroll
                     for (int k = 0; k < CF; k++) head_rec[(size_t)w * N + c0 + k] = a[k];
                 } else {
-                    store_f32<VT, CF>(C + (size_t)rr * N + c0, a);
+                    store_f32<VT, CF>(C + (size_t)rid_l[qq - qs + 1u] * N + c0, a);
                 }
-                float z[CF];
-#pragma unroll
-                for (int k = 0; k < CF; k++) z[k] = 0.f;
-                for (uint32_t r = rp + 1u; r < rr; r++) store_f32<VT, CF>(C + (size_t)r * N + c0, z);
-                if (qq + 1u == n_crow)
-                    for (uint32_t r = rr + 1u; r < row_hi; r++) store_f32<VT, CF>(C + (size_t)r * N + c0, z);
             };
-            for (uint32_t zb = zlo & ~(kMpItems - 1u); zb < wend; zb += R8) {
+            // software pipeline: round r+1's A entries and first staging batch are loaded
+            // while round r walks; round r's gathers are issued before that prefetch, so
+            // waiting for them leaves the prefetch in flight
+            CT cn[kMpItems];
+            VT vn[kMpItems];
+            uint32_t en = 0, rn = 0;
+            auto load_a = [&](uint32_t zb_) {
+                const uint32_t b_ = zb_ + kMpItems * slot;
+                if (b_ < wend) {
+                    load_raw<CT, kMpItems>(col + b_, cn);
+                    load_raw<VT, kMpItems>(val + b_, vn);
+                } else {
+#pragma unroll
+                    for (uint32_t k = 0; k < kMpItems; k++) { cn[k] = 0; vn[k] = (VT)0.f; }
+                }
+            };
+            auto load_s = [&](uint32_t q_) {
+                const uint32_t j = q_ + lane;
+                en = j < n_crow ? ends[j] : 0xffffffffu;
+                rn = j < n_crow ? rid[j] : 0u;
+            };
+            const uint32_t zb0 = zlo & ~(kMpItems - 1u);
+            load_a(zb0);
+            load_s(qs);
+            for (uint32_t zb = zb0; zb < wend; zb += R8) {
                 const uint32_t zl = max(zb, zlo), ze = min(zb + R8, wend);
                 const uint32_t base = zb + kMpItems * slot;
                 CT cc[kMpItems];
                 VT vv[kMpItems];
-                if (base < ze) {
-                    load_raw<CT, kMpItems>(col + base, cc);
-                    load_raw<VT, kMpItems>(val + base, vv);
-                } else {
 #pragma unroll
-                    for (uint32_t k = 0; k < kMpItems; k++) { cc[k] = 0; vv[k] = (VT)0.f; }
+                for (uint32_t k = 0; k < kMpItems; k++) { cc[k] = cn[k]; vv[k] = vn[k]; }
+                RB braw[kMpItems];  // all gathers of the round in flight before the walk
+#pragma unroll
+                for (uint32_t k = 0; k < kMpItems; k++) {
+                    const uint32_t z = base + k;
+                    const bool valid = z >= zl && z < ze;
+                    braw[k] = *reinterpret_cast<const RB *>(B + (size_t)(valid && !(dbg & 2u) ? (uint32_t)cc[k] : 0u) * N + c0);
                 }
                 for (uint32_t i = lane; i < fw; i += 64u) wl[i] = 0u;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 // stage the rows closing in this round and the one open at its end
-                if (lane == 0) rid_l[0] = qs ? rid[qs - 1u] : row_lo - 1u;
                 uint32_t nclose = 0;
                 closed_end = false;
+                uint32_t e = en, r = rn;
                 for (uint32_t k0 = 0;; k0 += 64u) {
-                    const uint32_t j = qs + k0 + lane;
-                    const uint32_t e = j < n_crow ? ends[j] : 0xffffffffu;
-                    const uint32_t r = j < n_crow ? rid[j] : 0u;
-                    if (k0 + lane < cap) {
-                        ends_l[k0 + lane] = e;
-                        rid_l[k0 + lane + 1u] = r;
+                    if (k0) {  // rows beyond the prefetched batch (short rows): synchronous
+                        const uint32_t j = qs + k0 + lane;
+                        e = j < n_crow ? ends[j] : 0xffffffffu;
+                        r = j < n_crow ? rid[j] : 0u;
                     }
+                    if (k0 + lane < cap) rid_l[k0 + lane + 1u] = r;
                     if (e > zl && e <= ze) flags[e - zb] = 1;
                     nclose += (uint32_t)__builtin_popcountll(__ballot(e <= ze));
                     closed_end = closed_end || __ballot(e == ze) != 0ull;
                     if (__ballot(e >= ze) != 0ull || k0 + 64u >= cap) break;
                 }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (zb + R8 < wend) {
+                    load_a(zb + R8);
+                    load_s(qs + nclose);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 // this slot's row starts: bit k = position 8*slot + k (bit 8: the next slot's first)
                 const uint32_t fo = kMpItems * slot;
                 const uint2 f8 = *reinterpret_cast<const uint2 *>(flags + fo);
@@ -1474,18 +1514,14 @@ __global__ __launch_bounds__(256) void k_merge_path(const uint32_t *__restrict__
                 for (uint32_t k = 0; k < 4; k++) bits |= ((f8.x >> (8 * k)) & 1u) << k | ((f8.y >> (8 * k)) & 1u) << (k + 4);
                 const uint32_t pc = (uint32_t)__builtin_popcount(bits & 0xffu);
                 uint32_t incl = pc;
-                for (uint32_t off = X; off < 64u; off <<= 1) {
+#pragma unroll
+                for (uint32_t st = 0; st < 6; st++) {
+                    const uint32_t off = X << st;
+                    if (off >= 64u) break;
                     const uint32_t t = __shfl_up(incl, off, 64);
                     if (lane >= off) incl += t;
                 }
                 uint32_t qcur = qs + incl - pc;  // row open before this slot's first position
-                RB braw[kMpItems];  // all gathers in flight before the walk
-#pragma unroll
-                for (uint32_t k = 0; k < kMpItems; k++) {
-                    const uint32_t z = base + k;
-                    const bool valid = z >= zl && z < ze;
-                    braw[k] = *reinterpret_cast<const RB *>(B + (size_t)(valid ? (uint32_t)cc[k] : 0u) * N + c0);
-                }
                 float acc[CF], h[CF];
 #pragma unroll
                 for (int k = 0; k < CF; k++) { acc[k] = 0.f; h[k] = 0.f; }
@@ -1531,7 +1567,10 @@ __global__ __launch_bounds__(256) void k_merge_path(const uint32_t *__restrict__
 #pragma unroll
                     for (int i = 0; i < CF; i++) acc[i] += rc[i];
                 }
-                for (uint32_t off = X; off < 64u; off <<= 1) {
+#pragma unroll
+                for (uint32_t st = 0; st < 6; st++) {
+                    const uint32_t off = X << st;
+                    if (off >= 64u) break;
                     const uint32_t ts = __shfl_up(stop, off, 64);
                     float t[CF];
 #pragma unroll
@@ -1577,9 +1616,9 @@ __global__ __launch_bounds__(256) void k_merge_fixup(const uint32_t *__restrict_
                                                      const float *__restrict__ rec,
                                                      const float *__restrict__ head_rec, VT *__restrict__ C,
                                                      uint32_t n_waves, uint32_t N) {
-    const size_t total = (size_t)n_waves * N;
-    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
-        const uint32_t g = (uint32_t)(e / N), c = (uint32_t)(e % N);
+    const uint32_t total = n_waves * N;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+        const uint32_t g = e / N, c = e % N;
         const uint32_t r = rec_row[g];
         if (r == 0xffffffffu || (g > 0 && rec_row[g - 1] == r)) continue;
         float s = 0.f;
@@ -1654,13 +1693,13 @@ inline std::vector<uint32_t> row_chunk_finalize_rows(const std::vector<uint32_t>
 // otherwise p - j.  Consecutive levels are grouped into waves of at least
 // target_steps path steps; waves never have an empty nz range.
 struct merge_path_layout {
-    std::vector<uint32_t> wz, wq, ends, rid;
+    std::vector<uint32_t> wz, wq, ends, rid, empty;  // empty: output rows without nonzeros
 };
 
 inline bool merge_path_device_layout(const std::vector<uint64_t> &row, uint64_t row_num,
                                      const std::vector<uint64_t> &lvl_rows, const std::vector<uint64_t> &lvl_nzs,
                                      uint64_t work_size, uint32_t row_base, uint64_t target_steps,
-                                     merge_path_layout &out, std::string &why) {
+                                     merge_path_layout &out, std::string &why, uint64_t out_rows = 0) {
     out = merge_path_layout();
     std::vector<uint32_t> cnt(row_num, 0);
     for (uint64_t r : row) {
@@ -1676,7 +1715,10 @@ inline bool merge_path_device_layout(const std::vector<uint64_t> &row, uint64_t 
             out.ends.push_back((uint32_t)acc);
             out.rid.push_back((uint32_t)(r + row_base));
             crow.push_back(r);
+        } else {
+            out.empty.push_back((uint32_t)(r + row_base));
         }
+    for (uint64_t r = row_base + row_num; r < out_rows; r++) out.empty.push_back((uint32_t)r);
     const uint64_t R = crow.size();
     if (R == 0 || lvl_rows.empty() || lvl_nzs.size() != lvl_rows.size() + 1 || lvl_nzs.back() != acc || work_size == 0) {
         why = "merge-path level arrays do not match the matrix";

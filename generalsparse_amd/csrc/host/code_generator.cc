@@ -257,14 +257,14 @@ std::string code_generator::generate_kernel_file_source(int repeat) const {
               << "_first_nz_indices_0\");\n"
               << "    gsk_host::merge_path_layout lay; std::string why;\n"
               << "    if (!gsk_host::merge_path_device_layout(rows, row_num, lr, ln, " << spec.work_size
-              << ", 0, 256, lay, why)) { printf(\"%s\\n\", why.c_str()); return 2; }\n"
-              << "    uint32_t *d_a0 = up(lay.wz), *d_a1 = up(lay.wq), *d_a2 = up(lay.ends), *d_a3 = up(lay.rid);\n"
+              << ", 0, 256, lay, why, M)) { printf(\"%s\\n\", why.c_str()); return 2; }\n"
+              << "    uint32_t *d_a0 = up(lay.wz), *d_a1 = up(lay.wq), *d_a2 = up(lay.ends), *d_a3 = up(lay.rid), *d_a4 = up(lay.empty);\n"
               << "    const uint32_t n_units = lay.wz.size() - 1, n_crow = lay.ends.size(); const bool al = true;\n"
               << "    float *d_r0, *d_r1; uint32_t *d_rr; hipMalloc(&d_r0, n_units * N * 4); hipMalloc(&d_r1, n_units * N * 4);\n"
               << "    hipMalloc(&d_rr, n_units * 4);\n";
-            launch = "gsk::k_merge_path<VT, uint32_t, CF><<<dim3((n_units + 3) / 4, tiles), 256, "
+            launch = "gsk::k_merge_path<VT, uint32_t, CF><<<dim3((n_units + 3) / 4 + 64, tiles), 256, "
                      "4 * gsk::merge_path_wave_lds_words(64 / X) * 4>>>(d_a0, d_a1, d_a2, d_a3, n_crow, d_col, d_val, d_B, d_C, "
-                     "d_r0, d_rr, d_r1, n_units, N, X, 0, (uint32_t)M); "
+                     "d_r0, d_rr, d_r1, n_units, N, X, 0, (uint32_t)M, d_a4, (uint32_t)lay.empty.size(), 64u); "
                      "gsk::k_merge_fixup<VT><<<dim3((n_units * N + 255) / 256), 256>>>(d_rr, d_r0, d_r1, d_C, n_units, N)";
             break;
         }

@@ -658,17 +658,19 @@ void upload_plan(plan_state &p, int dtype, int device) {
             const uint32_t Nd = (uint32_t)std::max<int64_t>(1, get_config().DENSE_MATRIX_SIZE);
             const uint32_t cfv = dtype == 0 ? 4u : 8u, cf = Nd % cfv == 0 ? cfv : 1u;
             const uint32_t X = std::min<uint32_t>(64u, pow2ceil_u((Nd + cf - 1) / cf));
-            const uint64_t target = 4ull * gsk::kMpItems * (64u / X);
+            const uint64_t target = (uint64_t)gsk::kMpItems * (64u / X);  // >= one round per wave
             gsk_host::merge_path_layout lay;
             std::string why;
             GS_CHECK(gsk_host::merge_path_device_layout(rows, row_num, m.u(L, "first_row_indices_without_ending", 0),
                                                          m.u(L, "first_nz_indices", 0), (uint64_t)sp.work_size,
-                                                         (uint32_t)d.row_base, target, lay, why),
+                                                         (uint32_t)d.row_base, target, lay, why, d.n_out_rows),
                      "merge-path layout: " + why);
             a.a0 = dev_copy(d, lay.wz);
             a.a1 = dev_copy(d, lay.wq);
             a.a2 = dev_copy(d, lay.ends);
             a.a3 = dev_copy(d, lay.rid);
+            a.a4 = dev_copy(d, lay.empty);
+            d.n_fin = lay.empty.size();
             d.n_units = lay.wz.size() - 1;
             d.n_rows_aux = lay.ends.size();
             d.ws_n = Nd;
@@ -733,6 +735,12 @@ void free_device(plan_state &p) {
 
 // ------------------------------------------------------------------ launch
 namespace {
+
+// GS_MP_DEBUG (diagnostic timing only): k_merge_path dbg bits
+uint32_t mp_debug() {
+    static const uint32_t v = getenv("GS_MP_DEBUG") ? (uint32_t)atoi(getenv("GS_MP_DEBUG")) : 0u;
+    return v;
+}
 
 uint32_t pow2ceil(uint32_t x) {
     uint32_t p = 1;
@@ -975,11 +983,14 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
             const size_t lds = (size_t)4 * gsk::merge_path_wave_lds_words(S) * sizeof(uint32_t);
             const uint32_t W = (uint32_t)d.n_units;
             const uint32_t gx = std::min<uint32_t>((W + 3) / 4, 1u << 16);
-            hipLaunchKernelGGL((gsk::k_merge_path<VT, CT, CF>), dim3(std::max(gx, 1u), tiles), dim3(256), lds, s, a.a0,
-                               a.a1, a.a2, a.a3, (uint32_t)d.n_rows_aux, col, val, B, C, a.ws, a.t0, a.ws2, W, N, X,
-                               row_base, (uint32_t)d.n_out_rows);
+            GS_CHECK(d.n_fin * (uint64_t)N < 0xffffffffull, "merge-path empty-row fill exceeds 32-bit indices");
+            const uint32_t fb = d.n_fin ? (uint32_t)std::min<uint64_t>(256, (d.n_fin * N / 4 + 1023) / 1024) : 0u;
+            hipLaunchKernelGGL((gsk::k_merge_path<VT, CT, CF>), dim3(gx + fb, tiles), dim3(256), lds, s, a.a0, a.a1,
+                               a.a2, a.a3, (uint32_t)d.n_rows_aux, col, val, B, C, a.ws, a.t0, a.ws2, W, N, X, row_base,
+                               (uint32_t)d.n_out_rows, a.a4, (uint32_t)d.n_fin, fb, mp_debug());
             HIP_OK(hipGetLastError());
-            const uint32_t fx = (uint32_t)std::min<uint64_t>(((uint64_t)W * N + 255) / 256, 4096);
+            GS_CHECK((uint64_t)W * N < 0xffffffffull, "merge-path fix-up indices exceed 32 bits");
+            const uint32_t fx = (uint32_t)std::min<uint64_t>(((uint64_t)W * N + 255) / 256, 1u << 16);
             hipLaunchKernelGGL((gsk::k_merge_fixup<VT>), dim3(std::max(fx, 1u)), dim3(256), 0, s, a.t0, a.ws, a.ws2, C,
                                W, N);
             break;
