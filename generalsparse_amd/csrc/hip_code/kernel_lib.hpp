@@ -1056,34 +1056,30 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         }
     } else {
         // K-split: this workgroup's fp32 slab, then the last of the row block's
-        // nsplit workgroups (agent-scope release/acquire around one counter)
-        // sums the slabs in split order (deterministic) and stores C
+        // nsplit workgroups sums the slabs in split order (deterministic) and stores C.
+        // Slabs and the arrival counter use agent-scope relaxed atomics: the stores and
+        // loads themselves are device-coherent (no L2 write-back / invalidate fences
+        // across the XCDs); the stores are complete (vmcnt 0) before the counter moves,
+        // and the combining workgroup loads only after it has seen the count.
         float *slab = slabs + ((size_t)g * nsplit + sp) * RMAX * N;
         for (uint32_t e = tid; e < RT * CT * 256u; e += NT) {
             uint32_t row, colx;
             const float sum = tile_sum(e, row, colx);
-            if (row < R) slab[(size_t)row * N + colx] = sum;
+            if (row < R) __hip_atomic_store(slab + (size_t)row * N + colx, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         uint32_t *flag = reinterpret_cast<uint32_t *>(lds + oD + 3 * szD + 512);
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (tid == 0)
             *flag = __hip_atomic_fetch_add(&arrivals[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
         __syncthreads();
         if (*flag == nsplit - 1u) {
-            if (tid == 0) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(&arrivals[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __syncthreads();
+            if (tid == 0) __hip_atomic_store(&arrivals[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const float *base = slabs + (size_t)g * nsplit * RMAX * N;
             for (uint32_t e = tid; e < R * N; e += NT) {
                 float sum = 0.f;
-                for (uint32_t q = 0; q < nsplit; q++) sum += base[(size_t)q * RMAX * N + e];
+                for (uint32_t q = 0; q < nsplit; q++)
+                    sum += __hip_atomic_load(base + (size_t)q * RMAX * N + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 C[(size_t)(row_base + r0) * N + e] = (f16)sum;
             }
         }
