@@ -57,3 +57,18 @@ def test_two_gloo_ranks_shard_and_max_time():
     assert v0 == v1                              # same job value on every rank
     assert n0 == n1 == 256 // 20 + 2             # ceil(256/20) BMTBs + 1
     assert g0[0] != g0[1]                        # each rank built its own shard
+
+
+def test_c5_lpt_split_is_balanced():
+    """C5 batch (48 OPT-30B layers): LPT on nnz gives every rank the same share at
+    1, 2, 4 and 8 ranks (balance within 2%)"""
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+    batch = [bench.C5_SLOTS[s] for _ in range(48) for s in range(len(bench.C5_SLOTS))]
+    sizes = [int(round(0.2 * m * n)) for m, n in (bench.C5_SHAPES[k] for k in batch)]
+    assert sum(sizes) == 48 * (4 * 10276045 + 2 * 41104179)
+    for world in (1, 2, 4, 8):
+        owner, load = bench.lpt_assign(sizes, world)
+        assert len(owner) == 288 and set(owner) == set(range(world))
+        assert max(load) / min(load) <= 1.02
