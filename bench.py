@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--p1", type=int, default=None)
     ap.add_argument("--workload", choices=("c2", "c3", "c4", "c4o", "c5"), default="c2")
     ap.add_argument("--layers", type=int, default=48, help="c5: OPT-30B layers in the batch")
+    ap.add_argument("--shard", choices=("batch", "rows", "nnz"), default="batch",
+                    help="c4/c4o with N>1: batch = a matrix per rank (weak); rows / nnz = one matrix split "
+                         "over the ranks (strong; nnz splits rows and combines them with one all-reduce)")
     ap.add_argument("--M", type=int, default=0)
     ap.add_argument("--K", type=int, default=0)
     ap.add_argument("--N", type=int, default=0)
@@ -131,6 +134,35 @@ def time_plan(plan, Bs, Cs, N, steps, warmup, torch, dist=None):
     wall = t1 - t0
     ev_ms = e0.elapsed_time(e1) / steps
     return max_over_ranks(wall, dist, torch), ev_ms
+
+
+def time_plan_combined(plan, Bs, Cs, N, steps, warmup, torch, dist, shards, rank):
+    """nnz-exact shards: every step is the local SpMM plus the boundary exchange
+    (shard.combine_boundaries: one all-reduce of world x N fp32 over RCCL)"""
+    from generalsparse_amd import shard as sd
+    reps = len(Bs)
+
+    def one(i):
+        plan.spmm(Bs[i % reps], C=Cs[i % reps], replica=i % plan.info()["replicas"])
+        sd.combine_boundaries(Cs[i % reps], shards, rank, dist, torch)
+
+    for i in range(warmup):
+        one(i)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for i in range(steps):
+        one(i)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    dist.barrier()
+    return max_over_ranks(wall, dist, torch), e0.elapsed_time(e1) / steps
 
 
 def max_over_ranks(x, dist, torch):
@@ -323,11 +355,18 @@ def main():
     dt = wl["dtype"]
     tdt = torch.float16 if dt == "f16" else torch.float32
     e, s_idx = (2 if dt == "f16" else 4), (2 if K <= 65536 else 4)
+    shards = None
     if args.workload in ("c4", "c4o"):
-        row, col, val = ds.rmat(M, wl["nnz"], wl["seed"] + rank, symmetric=wl["symmetric"])
+        one = args.shard != "batch"
+        row, col, val = ds.rmat(M, wl["nnz"], wl["seed"] + (0 if one else rank), symmetric=wl["symmetric"])
         nnz = len(row)
         alg_bytes = algorithmic_bytes(M, K, N, nnz, e, s_idx)
         cand_list = CANDIDATES_C4
+        if one:  # one matrix over the ranks: this rank's rows / nonzeros
+            from generalsparse_amd import shard as sd
+            full_flops = 2.0 * nnz * N
+            shards = (sd.nnz_exact_shards if args.shard == "nnz" else sd.balanced_row_shards)(row, M, world)
+            M, row, col, val = sd.local_coo(row, col, val, shards[rank])
     elif args.workload == "c3":
         row, col, val = ds.two_four(M, K, 30 + rank)
         nnz = len(row)
@@ -362,7 +401,10 @@ def main():
             plan.add_replica()
         Bs = [torch.randn((K, N), device=dev, dtype=tdt) for _ in range(reps)]
         Cs = [torch.empty((M, N), device=dev, dtype=tdt) for _ in range(reps)]
-        wall, ev_ms = time_plan(plan, Bs, Cs, N, args.steps, args.warmup, torch, dist)
+        if shards is not None and args.shard == "nnz" and dist is not None:
+            wall, ev_ms = time_plan_combined(plan, Bs, Cs, N, args.steps, args.warmup, torch, dist, shards, rank)
+        else:
+            wall, ev_ms = time_plan(plan, Bs, Cs, N, args.steps, args.warmup, torch, dist)
         key = f"{name}({p0},{p1})"
         variants[key] = {"ms_per_step": round(wall / args.steps * 1e3, 5), "kernel_ms": round(ev_ms, 5),
                          "gflops_per_gpu": round(flops / (wall / args.steps) / 1e9, 1),
@@ -377,6 +419,8 @@ def main():
     key, wall, ev_ms, info, reps, best_cand = best
     ms_per_step = wall / args.steps * 1e3
     value = whole_job_gflops(world, flops, args.steps, wall)
+    if shards is not None:  # strong scaling: the job is one matrix
+        value = full_flops * args.steps / wall / 1e9
     achieved = alg_bytes / (ev_ms * 1e-3) / 1e9
     traffic = None
     tf = os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
@@ -388,11 +432,14 @@ def main():
     out = {
         "metric": wl["metric"],
         "value": round(value, 1), "unit": "GFLOP/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 5), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "ms_per_step": round(ms_per_step, 5), "higher_is_better": True,
+        "scaling": "weak" if shards is None else "strong", "vs_baseline": None,
         "dtype": "f16 (fp32 accumulate)" if dt == "f16" else "f32", "data": wl["data"],
         "config": {"workload": wl["workload"].format(M=M, K=K, N=N),
                    "M": M, "K": K, "N": N, "nnz": nnz, "plan": key, "kernel": kernel_label(info),
-                   "replicas_rotated": reps, "parallelism": f"row-sharded batch x{world}"},
+                   "replicas_rotated": reps,
+                   "parallelism": f"row-sharded batch x{world}" if shards is None else
+                   f"one matrix, {args.shard} shards x{world}" + (" + boundary all-reduce" if args.shard == "nnz" else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": round(ev_ms, 5)},

@@ -72,3 +72,67 @@ def test_c5_lpt_split_is_balanced():
         owner, load = bench.lpt_assign(sizes, world)
         assert len(owner) == 288 and set(owner) == set(range(world))
         assert max(load) / min(load) <= 1.02
+
+
+def _shard_main(rank, world, port, mode, out):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle_ffi as ofi
+    from generalsparse_amd import datasets as ds
+    from generalsparse_amd import shard as sd
+    M, N = 3000, 8
+    rng = np.random.default_rng(5)
+    lens = rng.integers(0, 6, M)
+    lens[100] = 4000                      # a row longer than a shard: split over ranks
+    lens[-50:] = 0                        # trailing empty rows
+    row = np.repeat(np.arange(M, dtype=np.uint64), lens)
+    col = rng.integers(0, 500, len(row)).astype(np.uint64)
+    val = rng.uniform(-1, 1, len(row)).astype(np.float32)
+    B = rng.uniform(-1, 1, (500, N)).astype(np.float32)
+    shards = (sd.nnz_exact_shards if mode == "nnz" else sd.balanced_row_shards)(row, M, world)
+    sh = shards[rank]
+    m, r, c, v = sd.local_coo(row, col, val, sh)
+    C_local = torch.from_numpy(ofi.spmm_ref(m, N, r, c, v, B, "f64").astype(np.float32)) if m else torch.zeros((0, N))
+    first = sd.combine_boundaries(C_local, shards, rank, dist, torch) if mode == "nnz" else 0
+    out[rank] = (sh.row_lo + first, C_local[first:].numpy().copy(), sh.z1 - sh.z0)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["rows", "nnz"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_single_matrix_shards_combine_to_full_spmm(mode, world):
+    """one matrix over `world` gloo ranks: balanced row ranges (no exchange) or
+    nnz-exact ranges (split rows combined by one all-reduce), reassembled rows equal
+    the unsharded oracle SpMM"""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as ofi
+    port = _free_port()
+    with mp.Manager() as man:
+        out = man.dict()
+        mp.spawn(_shard_main, args=(world, port, mode, out), nprocs=world, join=True)
+        res = dict(out)
+    M, N = 3000, 8
+    rng = np.random.default_rng(5)
+    lens = rng.integers(0, 6, M)
+    lens[100] = 4000
+    lens[-50:] = 0
+    row = np.repeat(np.arange(M, dtype=np.uint64), lens)
+    col = rng.integers(0, 500, len(row)).astype(np.uint64)
+    val = rng.uniform(-1, 1, len(row)).astype(np.float32)
+    B = rng.uniform(-1, 1, (500, N)).astype(np.float32)
+    ref = ofi.spmm_ref(M, N, row, col, val, B, "f64")
+    got = np.zeros((M, N))
+    seen = np.zeros(M, int)
+    for r in range(world):
+        lo, blk, nz = res[r]
+        got[lo:lo + len(blk)] = blk
+        seen[lo:lo + len(blk)] += 1
+    assert sum(res[r][2] for r in range(world)) == len(row)
+    held = seen > 0
+    assert (seen <= 1).all()
+    np.testing.assert_allclose(got[held], ref[held], rtol=1e-5, atol=1e-5)
+    # rows no rank holds are the trailing empty rows (zero in the full product)
+    assert np.all(ref[~held] == 0)
