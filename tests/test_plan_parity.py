@@ -252,6 +252,22 @@ def test_generate_program_row_chunks_compiles(tmp_path):
                            "kernel_file.hip", "-o", "kernel_file.o"], cwd=d)
 
 
+@pytest.mark.parametrize("name,p0,p1", [("merge_path", 64, 1), ("balanced_thread_total", 16, 1)])
+def test_generate_program_new_families_compile(tmp_path, name, p0, p1):
+    """the emitted programs of a merge-path plan (k_merge_path + k_merge_fixup) and of
+    multi-row balanced BMTs (wave per row group) are valid HIP"""
+    M, K = 60, 300
+    r, c, v = random_coo(M, K, 0.3, 6, trailing_empty=False)
+    p = product_plan(M, K, r, c, v, name, 8, p0, p1)
+    p.compile()
+    d = p.generate_program(tmp_path, repeat=10)
+    src = open(os.path.join(d, "kernel_file.hip")).read()
+    assert ("k_merge_path" in src and "k_merge_fixup" in src) if name == "merge_path" else "k_warp_rows" in src
+    import subprocess
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O1", "-std=c++17", "-c",
+                           "kernel_file.hip", "-o", "kernel_file.o"], cwd=d)
+
+
 def test_synthetic_generators_shapes():
     r, c, v = ds.pruned_weight(64, 48, 0.7, 13)
     assert len(r) == round(0.3 * 64 * 48) and np.all(np.diff(r.astype(np.int64)) >= 0)
