@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--p0", type=int, default=None, help="with --pipeline: run only this plan parameter")
     ap.add_argument("--p1", type=int, default=None)
-    ap.add_argument("--workload", choices=("c2", "c3", "c4", "c4o", "c5"), default="c2")
+    ap.add_argument("--workload", choices=("c1", "c2", "c3", "c4", "c4o", "c5"), default="c2")
     ap.add_argument("--layers", type=int, default=48, help="c5: OPT-30B layers in the batch")
     ap.add_argument("--shard", choices=("batch", "rows", "nnz"), default="batch",
                     help="c4/c4o with N>1: batch = a matrix per rank (weak); rows / nnz = one matrix split "
@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--N", type=int, default=0)
     ap.add_argument("--sparsity", type=float, default=0.7)
     a = ap.parse_args()
-    dflt = {"c2": (5120, 5120, 32), "c3": (28672, 7168, 128), "c4": (1000005, 1000005, 8),
+    dflt = {"c1": (47894, 41550, 8), "c2": (5120, 5120, 32), "c3": (28672, 7168, 128), "c4": (1000005, 1000005, 8),
             "c4o": (3072441, 3072441, 8), "c5": (7168, 7168, 32)}[a.workload]
     a.M, a.K, a.N = a.M or dflt[0], a.K or dflt[1], a.N or dflt[2]
     return a
@@ -70,6 +70,10 @@ WORKLOADS = {
     "c3": {"metric": "SpMM GFLOP/s + achieved HBM GB/s vs rocSPARSE, 2:4 pruned-weight fp16 N=128 (configs[2])",
            "workload": "OPT-30B fc1 stand-in {M}x{K} 2:4 structured, fp16, N={N}",
            "data": "synthetic (seeded Gaussian, 2:4 magnitude pruning per group of 4)", "dtype": "f16"},
+    "c1": {"metric": "SpMM GFLOP/s (configs[0], IG5-18 stand-in; the reference runs it on the CPU only)",
+           "workload": "IG5-18 stand-in {M}x{K} nnz~1.79M, Poisson rows (mean 37.4), fp32, N={N}",
+           "data": "synthetic (seeded uniform columns, Poisson row lengths; the .mtx is not available offline)",
+           "dtype": "f32"},
     "c4": {"metric": "SpMM GFLOP/s + achieved HBM GB/s vs rocSPARSE, power-law fp32 N=8 (configs[3], webbase-1M)",
            "workload": "webbase-1M stand-in {M}x{K} nnz 3105536 R-MAT(.57,.19,.19), fp32, N={N}",
            "data": "synthetic (seeded R-MAT, deduplicated, row-sorted; SuiteSparse files are not available offline)",
@@ -92,6 +96,9 @@ CANDIDATES = [("block_total", 20, 1), ("block_total", 10, 1), ("block_total", 40
 
 # C3: the col-direction plan (32-nnz BMTs = 64-column k-steps of a 2:4 row)
 CANDIDATES_C3 = [("col_direction_nm", 32, 1)]
+
+# C1: token_test's default (thread_total, sparse_cf 4) and the row-block / merge-path plans
+CANDIDATES_C1 = [("thread_total", 4, 1), ("tblock_warp_total", 4, 1), ("merge_path", 512, 1)]
 
 # C4: merge-path levels (WARP, work_size p0) and the balanced / row-per-thread plans
 CANDIDATES_C4 = [("merge_path", 256, 1), ("merge_path", 512, 1), ("merge_path", 1024, 1), ("balanced_block_total", 2048, 1),
@@ -356,7 +363,12 @@ def main():
     tdt = torch.float16 if dt == "f16" else torch.float32
     e, s_idx = (2 if dt == "f16" else 4), (2 if K <= 65536 else 4)
     shards = None
-    if args.workload in ("c4", "c4o"):
+    if args.workload == "c1":
+        row, col, val = ds.random_rows(M, K, 1790490 / 47894, 18)
+        nnz = len(row)
+        alg_bytes = algorithmic_bytes(M, K, N, nnz, e, s_idx)
+        cand_list = CANDIDATES_C1
+    elif args.workload in ("c4", "c4o"):
         one = args.shard != "batch"
         row, col, val = ds.rmat(M, wl["nnz"], wl["seed"] + (0 if one else rank), symmetric=wl["symmetric"])
         nnz = len(row)

@@ -474,7 +474,10 @@ __global__ __launch_bounds__(256) void k_row_chunks(const uint32_t *__restrict__
                                                     const CT *__restrict__ col, const VT *__restrict__ val,
                                                     const VT *__restrict__ B, VT *__restrict__ C,
                                                     float *__restrict__ ws, uint32_t n_bmt, uint32_t U, uint32_t N,
-                                                    uint32_t X, uint32_t row_base) {
+                                                    uint32_t X, uint32_t row_base, uint32_t ilv = 0) {
+    // ilv > 0: interleaved storage (interlance_storage_operator, GLOBAL parent): every BMT
+    // has ilv nonzeros and the i-th of BMT b sits at b + i * n_bmt, so the slots of a wave
+    // read consecutive addresses (total_BMT_result_reduce_to_one_register_token.cc:581-624)
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t xl = lane & (X - 1u);
     const uint32_t slot = lane / X;
@@ -501,7 +504,17 @@ __global__ __launch_bounds__(256) void k_row_chunks(const uint32_t *__restrict__
                 float acc[CF];
 #pragma unroll
                 for (int k = 0; k < CF; k++) acc[k] = 0.f;
-                if (valid) wave_row<VT, CT, CF, SCF>(bmt_nz[bt], bmt_nz[bt + 1], col, val, B, N, c0, 0u, 1u, acc);
+                if (valid) {
+                    if (ilv) {
+#pragma unroll 8
+                        for (uint32_t i = 0; i < ilv; i++) {
+                            const size_t p = (size_t)bt + (size_t)i * n_bmt;
+                            fma_row<VT, CF>(acc, (float)val[p], B + (size_t)col[p] * N + c0);
+                        }
+                    } else {
+                        wave_row<VT, CT, CF, SCF>(bmt_nz[bt], bmt_nz[bt + 1], col, val, B, N, c0, 0u, 1u, acc);
+                    }
+                }
                 // segmented suffix sums: the first slot of each run ends with the run total
                 for (uint32_t off = 1; off < S; off <<= 1) {
                     const uint32_t rn = __shfl_down(row, off * X, 64);

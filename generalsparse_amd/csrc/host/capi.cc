@@ -106,6 +106,27 @@ void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1)
         ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, false, scf, cf, ctx));
         ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)rows, std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
         ex.add_and_run(std::make_shared<tblock_thread_bit_map_operator>(cg, (unsigned)cf, y, false, false, ctx));
+    } else if (name == "warp_bit_map_interleaved" || name == "tblock_bit_map_interleaved") {
+        // §8f rank 2: the warp_bit_map / tblock_bit_map plans with interleaved storage of the
+        // equal-size (padded) col-direction BMTs (interlance_storage_operator, GLOBAL parent)
+        int scf = p0 > 0 ? p0 : 4, cf = p1 > 0 ? p1 : 1;
+        const bool warp = name == "warp_bit_map_interleaved";
+        ex.add_and_run(std::make_shared<fixed_interval_col_direction_thread_blocking_operator>(cg, 64, false, false,
+                                                                                               true, false, ctx));
+        ex.add_and_run(std::make_shared<interlance_storage_operator>(cg, ctx));
+        if (warp) {
+            int y = std::min(std::max(1, N / cf), 32), x = std::max(128 / y, 32);
+            set_config("VECTOR_WIDTH", x);
+            ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, true, scf, cf, ctx));
+            ex.add_and_run(std::make_shared<warp_bit_map_operator>(cg, (unsigned)cf, true, true, ctx));
+            ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)rows, std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
+        } else {
+            int x = std::min(std::max(1, N / cf), 32), y = 256 / x;
+            set_config("VECTOR_WIDTH", x);
+            ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, false, scf, cf, ctx));
+            ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)rows, std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
+            ex.add_and_run(std::make_shared<tblock_thread_bit_map_operator>(cg, (unsigned)cf, y, false, false, ctx));
+        }
     } else if (name == "col_direction_nm") {
         // BASELINE.json configs[2] (C3): col-direction BMTs of p0 nnz (32 = one 64-column
         // k-step of a 2:4 row), no padding, summed per row (the warp_bit_map tokens);

@@ -42,6 +42,7 @@ std::string kernel_spec::name() const {
     if (family == KF_WARP_TOTAL && tblock_parent) n += "+tblock";
     if (family == KF_ROW_CHUNKS && bitmap_parent == WARP_META) n += "+warp_bit_map";
     if (family == KF_ROW_CHUNKS && bitmap_parent == TBLOCK_META) n += "+tblock_bit_map";
+    if (interleaved) n += "+interleaved";
     return n;
 }
 
@@ -157,6 +158,15 @@ void code_generator::compile() {
         s.arrays = {"TBLOCK_META_first_row_indices_0", "TBLOCK_META_first_nz_indices_0"};
     } else {
         throw gs_error("code_generator::compile: no reduction token set (or a combination not built in this round)");
+    }
+    if (interleave) {
+        // interleaved storage is consumed by the col-direction chunk kernel (GLOBAL parent)
+        GS_CHECK(s.family == KF_ROW_CHUNKS && interleave_parent == GLOBAL_META,
+                 "interleaved storage is built for col-direction BMT plans at the GLOBAL level only");
+        s.interleaved = true;
+        for (auto k : {"GLOBAL_META_nz_col_indices_after_interlance_storage_0", "GLOBAL_META_nz_vals_after_interlance_storage_0",
+                       "GLOBAL_META_BMT_size_of_each_blk_0"})
+            s.arrays.push_back(k);
     }
     for (auto k : {"GLOBAL_META_nz_row_indices_0", "GLOBAL_META_nz_col_indices_0", "GLOBAL_META_nz_vals_0"})
         s.arrays.push_back(k);

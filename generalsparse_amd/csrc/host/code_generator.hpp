@@ -64,6 +64,7 @@ struct kernel_spec {
     POS_TYPE merge_level = GLOBAL_META;    // merge-path plans: the level the operator split
     int work_size = 0;                     // merge-path plans: path steps per level
     POS_TYPE group_level = WARP_META;      // KF_WARP_TOTAL: level whose first_row_indices are the row groups
+    bool interleaved = false;              // cols / vals in interleaved storage (GLOBAL parent)
     std::array<unsigned, 2> ref_grid{{0, 0}}, ref_block{{0, 0}};
     std::vector<std::string> arrays;  // metadata keys the kernel consumes (= kernel arguments)
     std::string name() const;
@@ -86,6 +87,9 @@ class code_generator {
     // merge_path_*_operator: which level holds the merge-path split (the reference opens
     // TBLOCK for all three, so the level is recorded separately)
     void set_merge_path_level(POS_TYPE pos, int work_size) { merge_level = pos; merge_work_size = work_size; }
+    // interlance_storage_operator (code_generator.hpp set_interleave_storage): kernels read
+    // the *_after_interlance_storage arrays
+    void set_interleave_storage(POS_TYPE parent) { interleave = true; interleave_parent = parent; }
     void set_thread_grid(const std::vector<unsigned> &grid, const std::vector<unsigned> &block);
 
     // lowers the token set to a kernel family (code_generator.hpp:265-269)
@@ -107,6 +111,8 @@ class code_generator {
     bool thread_for_row = false;
     POS_TYPE merge_level = GLOBAL_META;
     int merge_work_size = 0;
+    bool interleave = false;
+    POS_TYPE interleave_parent = GLOBAL_META;
     std::vector<unsigned> grid, block;
     bool compiled = false;
     kernel_spec spec;

@@ -904,4 +904,72 @@ void get_begin_nzs_of_level_after_merge_path::run(bool check) {
     is_run = true;
 }
 
+// ----------------------------------------------- interleaved storage (§8f rank 2)
+// modify_col_indices_by_interlance_storage.cc:45-116 (the vals / rows files are the same
+// loop): GLOBAL parent -> one block of BMT_num = nnz / size BMTs, spacing BMT_num;
+// TBLOCK / WARP parent -> per parent p, BMTs [first_BMT[p], first_BMT[p+1]) of size
+// BMT_size_of_each_blk[p], spacing = their count, offset = the nonzeros before p
+std::vector<uint64_t> interlance_storage_permutation(const meta_data_set &m, POS_TYPE parent_pos, int s, bool check) {
+    const uint64_t n = m.u(GLOBAL_META, "nz_col_indices", s).size();
+    const auto &bsz = m.u(parent_pos, "BMT_size_of_each_blk", s);
+    std::vector<uint64_t> to(n);
+    if (parent_pos == GLOBAL_META) {
+        GS_CHECK(!bsz.empty() && bsz[0] > 0, "interleaved storage: BMT_size_of_each_blk missing");
+        const uint64_t sz = bsz[0];
+        if (check) GS_CHECK(n % sz == 0, "interleaved storage: nnz is not a multiple of the BMT size (:57)");
+        const uint64_t nb = n / sz;
+        for (uint64_t b = 0; b < nb; b++)
+            for (uint64_t i = 0; i < sz; i++) to[i + b * sz] = b + i * nb;
+    } else {
+        const auto &fb = m.u(parent_pos, "first_BMT_indices", s);
+        uint64_t base = 0;
+        for (uint64_t p = 0; p + 1 < fb.size(); p++) {
+            const uint64_t nb = fb[p + 1] - fb[p], sz = bsz[p];
+            if (check) GS_CHECK(m.u(parent_pos, "first_nz_indices", s)[p] == base, "interleaved storage: parent offsets (:103)");
+            for (uint64_t b = 0; b < nb; b++)
+                for (uint64_t i = 0; i < sz; i++) to[base + i + b * sz] = base + b + i * nb;
+            base += nb * sz;
+        }
+        GS_CHECK(base == n, "interleaved storage: parents do not cover the nonzeros");
+    }
+    return to;
+}
+
+void modify_col_indices_by_interlance_storage::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &c = m.u(GLOBAL_META, "nz_col_indices", target_matrix_id);
+    auto to = interlance_storage_permutation(m, parent_pos, target_matrix_id, check);
+    std::vector<uint64_t> out(c.size());
+    for (uint64_t e = 0; e < c.size(); e++) out[to[e]] = c[e];
+    replace_u(GLOBAL_META, "nz_col_indices_after_interlance_storage", std::move(out));
+    src(GLOBAL_META, "nz_col_indices");
+    src(parent_pos, "BMT_size_of_each_blk");
+    is_run = true;
+}
+
+void modify_row_indices_by_interlance_storage::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &r = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    auto to = interlance_storage_permutation(m, parent_pos, target_matrix_id, check);
+    std::vector<uint64_t> out(r.size());
+    for (uint64_t e = 0; e < r.size(); e++) out[to[e]] = r[e];
+    replace_u(GLOBAL_META, "nz_row_indices_after_interlance_storage", std::move(out));
+    src(GLOBAL_META, "nz_row_indices");
+    src(parent_pos, "BMT_size_of_each_blk");
+    is_run = true;
+}
+
+// modify_vals_by_interlance_storage.cc:69/109/125-135: same permutation, the value type kept
+void modify_vals_by_interlance_storage::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    auto varr = m.get_element(GLOBAL_META, "nz_vals", target_matrix_id)->meta_data_arr;
+    auto to = interlance_storage_permutation(m, parent_pos, target_matrix_id, check);
+    std::vector<double> out(varr->get_len());
+    for (uint64_t e = 0; e < out.size(); e++) out[to[e]] = varr->read_float_from_arr(e);
+    replace_f(GLOBAL_META, "nz_vals_after_interlance_storage", std::move(out), varr->get_data_type());
+    src(GLOBAL_META, "nz_vals");
+    src(parent_pos, "BMT_size_of_each_blk");
+    is_run = true;
+}
+
 }  // namespace gs

@@ -195,6 +195,22 @@ GS_DECLARE_MERGE_PATH(get_begin_nzs_of_level_after_merge_path)
 void merge_path_levels(const std::vector<uint64_t> &nnz_of_each_row, uint64_t work_size,
                        std::vector<uint64_t> *level_rows, std::vector<uint64_t> *level_nzs);
 
+// interleaved storage (§8f rank 2; modify_{col,val,row}_indices_by_interlance_storage.cc):
+// inside every parent block the i-th nonzero of BMT b moves to b + i * (BMTs in the parent)
+#define GS_DECLARE_INTERLANCE(cls)                                                                \
+    class cls : public basic_data_transform_step {                                                \
+      public:                                                                                     \
+        cls(std::shared_ptr<meta_data_set> m, POS_TYPE parent_pos, int target_matrix_id)          \
+            : basic_data_transform_step(#cls, std::move(m), target_matrix_id), parent_pos(parent_pos) {} \
+        void run(bool check) override;                                                            \
+        POS_TYPE parent_pos;                                                                      \
+    };
+GS_DECLARE_INTERLANCE(modify_col_indices_by_interlance_storage)
+GS_DECLARE_INTERLANCE(modify_vals_by_interlance_storage)
+GS_DECLARE_INTERLANCE(modify_row_indices_by_interlance_storage)
+// the permutation the three transforms apply: new position of old position e
+std::vector<uint64_t> interlance_storage_permutation(const meta_data_set &m, POS_TYPE parent_pos, int sub, bool check);
+
 std::vector<uint64_t> get_begin_nzs_of_child_after_balance_blocking_in_row_direction(
     const std::vector<uint64_t> &nnz_of_each_row, uint64_t nnz_per_interval);
 std::vector<uint64_t> get_begin_rows_of_child_after_balance_blocking_in_row_direction(

@@ -479,6 +479,58 @@ bool merge_path_thread_operator::is_valid_according_to_operator(ctx_ptr h) {
     return !any_name(d, "thread") && !any_name(d, "col") && !any_name(d, "interlance");
 }
 
+// ------------------------------------------------ interleaved storage (§8f rank 2)
+// interlance_storage_operator.cc:12-45: the parent level is the WARP / TBLOCK level a
+// distributing operator opened before, else GLOBAL
+interlance_storage_operator::interlance_storage_operator(cg_ptr cg, ctx_ptr history)
+    : basic_operator("interlance_storage_operator", cg->get_metadata_set(), DISTRIBUTING_OP, cg->get_sub_matrix_id()),
+      code_generator_ptr(cg) {
+    bool warp = false, tblock = false;
+    for (auto &o : history->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id)) {
+        if (o->get_name().find("warp") != std::string::npos) warp = true;
+        else if (o->get_name().find("tblock") != std::string::npos) tblock = true;
+    }
+    pos = warp ? WARP_META : (tblock ? TBLOCK_META : GLOBAL_META);
+}
+
+// :56-97: no implementing op; a col-direction thread blocking WITH padding to a multiple
+// of its size (or row-direction thread blocking padded to the row max) came before; once
+bool interlance_storage_operator::is_valid_according_to_operator(ctx_ptr h) {
+    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return false;
+    bool col_pad = false, row_pad = false;
+    for (auto &o : h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id)) {
+        if (o->get_name().find("interlance") != std::string::npos) return false;
+        if (auto *c = dynamic_cast<fixed_interval_col_direction_thread_blocking_operator *>(o.get()))
+            col_pad = col_pad || c->is_padding_with_col_size_in_bmt;
+        if (auto *r = dynamic_cast<fixed_interval_row_direction_thread_blocking_operator *>(o.get()))
+            row_pad = row_pad || r->is_col_padding_with_row_max_size_with_empty_row;
+    }
+    return col_pad || row_pad;
+}
+
+// :99-141
+bool interlance_storage_operator::is_valid_according_to_metadata() {
+    auto &m = *meta_data_set_ptr;
+    int s = target_matrix_id;
+    bool ok = !interlance_storage_existing(m, s) && m.is_exist(GLOBAL_META, "nz_row_indices", s) &&
+              m.is_exist(GLOBAL_META, "nz_col_indices", s) && m.is_exist(GLOBAL_META, "nz_vals", s);
+    if (pos != GLOBAL_META) ok = ok && m.is_exist(pos, "first_BMT_indices", s);
+    return ok && m.is_exist(pos, "BMT_size_of_each_blk", s);
+}
+
+// :144-176
+void interlance_storage_operator::run(bool check) {
+    if (check) GS_CHECK(is_valid_according_to_metadata(), "interlance_storage: invalid metadata (equal-size BMTs per parent needed)");
+    modify_col_indices_by_interlance_storage a(meta_data_set_ptr, pos, target_matrix_id);
+    run_step(a, check);
+    modify_vals_by_interlance_storage b(meta_data_set_ptr, pos, target_matrix_id);
+    run_step(b, check);
+    modify_row_indices_by_interlance_storage c(meta_data_set_ptr, pos, target_matrix_id);
+    run_step(c, check);
+    code_generator_ptr->set_interleave_storage(pos);
+    is_run = true;
+}
+
 // ------------------------------------------- col-direction THREAD blocking (A10)
 fixed_interval_col_direction_thread_blocking_operator::fixed_interval_col_direction_thread_blocking_operator(
     cg_ptr cg, int fcs, bool rrel, bool nrel, bool pad_size, bool pad_max, ctx_ptr history)
@@ -920,6 +972,7 @@ std::shared_ptr<basic_operator> make_operator(const std::string &name, const std
         return std::make_shared<balanced_interval_row_direction_thread_blocking_operator>(cg, (int)a[0], a[1] != 0,
                                                                                           a[2] != 0, ctx);
     }
+    if (name == "interlance_storage_operator") { need(0); return std::make_shared<interlance_storage_operator>(cg, ctx); }
     if (name == "merge_path_tblock_operator") { need(1); return std::make_shared<merge_path_tblock_operator>(cg, (int)a[0], ctx); }
     if (name == "merge_path_warp_operator") { need(1); return std::make_shared<merge_path_warp_operator>(cg, (int)a[0], ctx); }
     if (name == "merge_path_thread_operator") { need(1); return std::make_shared<merge_path_thread_operator>(cg, (int)a[0], ctx); }

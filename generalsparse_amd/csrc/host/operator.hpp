@@ -235,6 +235,20 @@ class merge_path_thread_operator : public merge_path_operator_base {
     bool is_valid_according_to_operator(ctx_ptr h) override;
 };
 
+// operator/interlance_storage_operator.cc (§8f rank 2): interleave the nonzeros of the
+// equal-size BMTs inside each parent (GLOBAL, or the WARP / TBLOCK level distributed before)
+class interlance_storage_operator : public basic_operator {
+  public:
+    interlance_storage_operator(cg_ptr cg, ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    POS_TYPE pos = GLOBAL_META;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
 // operator/fixed_interval_col_direction_thread_blocking_operator.cc (A10): BMTs are
 // chunks of fixed_col_block_size nnz along each row
 class fixed_interval_col_direction_thread_blocking_operator : public basic_operator {

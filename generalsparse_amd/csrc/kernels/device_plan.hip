@@ -414,15 +414,17 @@ void upload_plan(plan_state &p, int dtype, int device) {
     d.dtype = dtype;
     d.n_out_rows = p.M;
     d.row_base = m.scalar(GLOBAL_META, "begin_row_index", 0);
-    const auto &col = m.u(GLOBAL_META, "nz_col_indices", 0);
     const auto &rows = m.u(GLOBAL_META, "nz_row_indices", 0);
-    auto vals = m.get_element(GLOBAL_META, "nz_vals", 0)->meta_data_arr;
+    // interleaved storage (§8f rank 2): the kernel streams the permuted arrays
+    const auto &col = m.u(GLOBAL_META, sp.interleaved ? "nz_col_indices_after_interlance_storage" : "nz_col_indices", 0);
+    auto vals = m.get_element(GLOBAL_META, sp.interleaved ? "nz_vals_after_interlance_storage" : "nz_vals", 0)->meta_data_arr;
+    if (sp.interleaved) d.ilv = (uint32_t)m.u(GLOBAL_META, "BMT_size_of_each_blk", 0).at(0);
     uint64_t nnz = col.size();
     GS_CHECK(nnz < 0xffffffffull - kPad, "nnz exceeds 32-bit offsets");
     d.nnz_stored = nnz;
     device_arrays a;
     const int64_t plan_n = get_config().DENSE_MATRIX_SIZE;
-    if (sp.family == KF_ROW_CHUNKS && dtype == 1 && get_config().NM_MFMA &&
+    if (sp.family == KF_ROW_CHUNKS && !sp.interleaved && dtype == 1 && get_config().NM_MFMA &&
         (plan_n == 32 || plan_n == 64 || plan_n == 128)) {
         // col-direction BMTs that are 2:4 panels: sparse matrix cores, self-contained blocks
         std::vector<unsigned char> blk;
@@ -967,7 +969,7 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
             const uint32_t nw = (uint32_t)((d.n_units + d.span - 1) / d.span);
             const uint32_t gx = std::min<uint32_t>((nw + 3) / 4, 1u << 16);
             hipLaunchKernelGGL((gsk::k_row_chunks<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
-                               a.a0, a.a1, col, val, B, C, a.ws, (uint32_t)d.n_units, d.span, N, X, row_base);
+                               a.a0, a.a1, col, val, B, C, a.ws, (uint32_t)d.n_units, d.span, N, X, row_base, d.ilv);
             if (d.n_fin) {
                 HIP_OK(hipGetLastError());
                 const uint32_t fx = (uint32_t)std::min<uint64_t>((d.n_fin * N + 255) / 256, 4096);

@@ -856,6 +856,33 @@ int or_merge_path(or_set *s, const char *pos, uint64_t work_size) {
     return 0;
 }
 
+/* §8f rank 2: interlance_storage_operator at the GLOBAL parent,
+ * modify_{col,val,row}_indices_by_interlance_storage.cc:45-71: all BMTs have
+ * BMT_size_of_each_blk nonzeros; the i-th of BMT b moves to b + i * (nnz / size). */
+int or_interlance_storage_global(or_set *s) {
+    if (!exists(s, "GLOBAL_META", "BMT_size_of_each_blk", 0))
+        return fail(s, "interleaved storage needs equal-size BMTs (BMT_size_of_each_blk)");
+    uint64_t sz = scalar(s, "GLOBAL_META", "BMT_size_of_each_blk", 0);
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    or_array *C = get(s, "GLOBAL_META", "nz_col_indices", 0);
+    or_array *V = get(s, "GLOBAL_META", "nz_vals", 0);
+    uint64_t n = C->len;
+    if (sz == 0 || n % sz) return fail(s, "nnz is not a multiple of the BMT size");
+    uint64_t nb = n / sz;
+    uint64_t *nr = (uint64_t *)malloc(n * sizeof(uint64_t)), *nc = (uint64_t *)malloc(n * sizeof(uint64_t));
+    double *nv = (double *)malloc(n * sizeof(double));
+    for (uint64_t b = 0; b < nb; b++)
+        for (uint64_t i = 0; i < sz; i++) {
+            nc[b + i * nb] = C->u[i + b * sz];
+            nr[b + i * nb] = R->u[i + b * sz];
+            nv[b + i * nb] = V->f[i + b * sz];
+        }
+    put_u(s, "GLOBAL_META", "nz_col_indices_after_interlance_storage", 0, nc, n);
+    put_u(s, "GLOBAL_META", "nz_row_indices_after_interlance_storage", 0, nr, n);
+    put_f(s, "GLOBAL_META", "nz_vals_after_interlance_storage", 0, nv, n);
+    return 0;
+}
+
 /* ------------------------------------------------------------------ */
 /* canned pipelines: token_test.cc test_spmm_*                          */
 /* ------------------------------------------------------------------ */
@@ -888,6 +915,16 @@ int or_pipeline(or_set *s, const char *name, int p0, int p1) {
     }
     if (!strcmp(name, "tblock_bit_map")) { /* token_test.cc:1515-1582, p0 = block_size = 256/min(N/cf,32) */
         if (or_col_dir_thread_blocking(s, 64, 1)) return -1;
+        return or_parent_bit_map_operator(s, 0, p0, 0, 0);
+    }
+    if (!strcmp(name, "warp_bit_map_interleaved")) { /* §8f rank 2 on the warp_bit_map plan */
+        if (or_col_dir_thread_blocking(s, 64, 1)) return -1;
+        if (or_interlance_storage_global(s)) return -1;
+        return or_parent_bit_map_operator(s, 1, p0, 1, 1);
+    }
+    if (!strcmp(name, "tblock_bit_map_interleaved")) {
+        if (or_col_dir_thread_blocking(s, 64, 1)) return -1;
+        if (or_interlance_storage_global(s)) return -1;
         return or_parent_bit_map_operator(s, 0, p0, 0, 0);
     }
     if (!strcmp(name, "balanced_warp_total")) /* A11 balanced BMW + warp_total */

@@ -253,6 +253,22 @@ cases.append({
     },
 })
 
+# interleaved storage (§8f rank 2, modify_col_indices_by_interlance_storage.cc:45-71) on the
+# warp_bit_map plan of ex3: col-direction BMTs of 64 with padding -> rows 100, 0, 30, 64
+# padded to 128, 0, 64, 64 (pads repeat the row's last col) -> 4 BMTs of 64:
+# b0 = row0 cols 0..63, b1 = row0 cols 64..99 + 28 x 99, b2 = row2 cols 0..29 + 34 x 29,
+# b3 = row3 cols 0..63; element i of BMT b moves to b + 4 * i
+_bmts = [list(range(64)), list(range(64, 100)) + [99] * 28, list(range(30)) + [29] * 34, list(range(64))]
+_rows = [0, 0, 2, 3]
+cases.append({
+    "matrix": "ex3", "pipeline": "warp_bit_map_interleaved", "p0": 32,
+    "expect": {
+        G + "BMT_size_of_each_blk_0": [64],
+        G + "nz_col_indices_after_interlance_storage_0": [_bmts[b][i] for i in range(64) for b in range(4)],
+        G + "nz_row_indices_after_interlance_storage_0": [_rows[b] for i in range(64) for b in range(4)],
+    },
+})
+
 out = {"matrices": {"ex1": EX1, "ex2": EX2, "ex3": EX3, "ex4": EX4}, "cases": cases}
 path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hand_plans.json")
 with open(path, "w") as f:

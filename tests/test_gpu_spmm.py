@@ -84,7 +84,8 @@ def test_known_answer_all_ones(pipe, dtype):
 
 # col-direction pipelines (K5 warp_bit_map / K7 tblock_bit_map): BMTs are 64-nnz
 # chunks of one row, so the cases need rows long enough for the padding rule
-COL_PIPES = [("warp_bit_map", 4, 1), ("tblock_bit_map", 4, 1)]
+COL_PIPES = [("warp_bit_map", 4, 1), ("tblock_bit_map", 4, 1), ("warp_bit_map_interleaved", 4, 1),
+             ("tblock_bit_map_interleaved", 4, 1)]
 
 
 def col_cases():

@@ -29,9 +29,9 @@ def oracle_params(name, N, p0, p1):
         return min(N, 32)
     if name == "thread_bit_map":
         return N // cf if N // cf < 32 else 32
-    if name == "warp_bit_map":  # token_test.cc:1277-1279
+    if name in ("warp_bit_map", "warp_bit_map_interleaved"):  # token_test.cc:1277-1279
         return max(128 // min(max(1, N // cf), 32), 32)
-    if name == "tblock_bit_map":  # token_test.cc:1546-1547
+    if name in ("tblock_bit_map", "tblock_bit_map_interleaved"):  # token_test.cc:1546-1547
         return 256 // min(max(1, N // cf), 32)
     return p0
 
@@ -79,6 +79,7 @@ PIPES = [("thread_total", 32, 4, 1), ("thread_total", 8, 8, 1), ("warp_total", 3
 
 # col-direction pipelines need rows long enough for the 64-nnz padding rule
 COL_PIPES = [("warp_bit_map", 32, 4, 1), ("warp_bit_map", 8, 4, 2), ("warp_bit_map", 1, 4, 1),
+             ("warp_bit_map_interleaved", 32, 4, 1), ("tblock_bit_map_interleaved", 8, 4, 1),
              ("tblock_bit_map", 32, 4, 1), ("tblock_bit_map", 128, 4, 1), ("tblock_bit_map", 2, 4, 1)]
 
 
@@ -120,6 +121,7 @@ def test_hand_derived_fixtures_through_product():
     g = json.load(open(GOLDEN))
     back = {"thread_total": (32, 4, 1), "warp_total": (32, 0, 1), "block_total": (8, 0, 1),
             "merge_path": (8, 0, 1), "balanced_block_total": (32, 0, 1), "balanced_thread_total": (8, 0, 1),
+            "warp_bit_map_interleaved": (32, 4, 1),
             "tblock_warp_total": (32, 4, 1), "balanced_warp_total": (32, 16, 1),
             "warp_bit_map": (32, 4, 1), "tblock_bit_map": (32, 4, 1)}
     for case in g["cases"]:
@@ -182,6 +184,33 @@ def test_operator_validity_rules():
     p.add_operator("warp_segment_reduce_operator", 1, 0, 0)
     p.compile()
     assert p.info()["kernel_name"].startswith("k_bitmap_segment")
+
+
+def test_interlance_storage_validity():
+    """interlance_storage_operator.cc:56-141: only after a col-direction thread blocking
+    padded to its size, once, before any implementing operator"""
+    M, K = 20, 300
+    r, c, v = random_coo(M, K, 0.5, 3, empty=0.0)
+    gsa.set_config("DENSE_MATRIX_SIZE", 32)
+    p = gsa.Plan.from_coo(M, K, r, c, v)
+    p.add_operator("fixed_interval_col_direction_thread_blocking_operator", 64, 0, 0, 0, 0)  # no padding
+    with pytest.raises(gsa.GsError):
+        p.add_operator("interlance_storage_operator")
+    q = gsa.Plan.from_coo(M, K, r, c, v)
+    q.add_operator("fixed_interval_col_direction_thread_blocking_operator", 64, 0, 0, 1, 0)
+    q.add_operator("interlance_storage_operator")
+    with pytest.raises(gsa.GsError):
+        q.add_operator("interlance_storage_operator")
+    q.add_operator("thread_total_reduce_operator", 1, 4, 1)
+    q.add_operator("warp_bit_map_operator", 1, 1, 1)
+    q.compile()
+    assert q.info()["kernel_name"].endswith("+interleaved")
+    a = q.arrays()
+    n, sz = len(a["GLOBAL_META_nz_col_indices_0"]), int(a["GLOBAL_META_BMT_size_of_each_blk_0"][0])
+    nb = n // sz
+    perm = np.array([b + i * nb for b in range(nb) for i in range(sz)])
+    np.testing.assert_array_equal(a["GLOBAL_META_nz_col_indices_after_interlance_storage_0"][perm],
+                                  a["GLOBAL_META_nz_col_indices_0"])
 
 
 def test_mtx_reader_parity(tmp_path):
