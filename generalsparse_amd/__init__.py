@@ -55,6 +55,21 @@ def _dtype_code(dtype):
     raise ValueError(f"unsupported dtype {dtype}")
 
 
+def index_compression_of_array(a, type_ori=16, branch_max=5):
+    """the reference's compression decision for a raw u64 array: (kind, {coef, intercept,
+    cycle, aa, bb}, exact); type_ori = the gs data_type code of its storage (16 = u64)"""
+    L = _lib.load()
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    kind = ctypes.create_string_buffer(32)
+    prm = np.zeros(5, np.uint64)
+    ex = ctypes.c_int(0)
+    _lib.check(L.gs_index_compression_of_array(a.ctypes.data_as(_lib.u64p), len(a), int(type_ori), int(branch_max), kind, 32,
+                                               prm.ctypes.data_as(_lib.u64p), ctypes.byref(ex)))
+    p = {"coef": int(prm[0]), "intercept": int(prm[1]), "cycle": int(prm[2]),
+         "aa": int(prm[3].astype(np.int64)), "bb": int(prm[4].astype(np.int64))}
+    return kind.value.decode(), p, bool(ex.value)
+
+
 class Plan:
     """A GeneralSparse plan: metadata set + operator history + code generator +
     device copies.  Wraps gs_plan_t."""
@@ -184,6 +199,15 @@ class Plan:
 
     def arrays(self):
         return {k: self.array(k) for k in self.keys()}
+
+    def index_compression(self, key):
+        """(kind, expression of i, exact) for one integer plan array (code_generator.cc:2618-3063;
+        "none" unless MODEL_DRIVEN_COMPRESS is set)"""
+        kind = ctypes.create_string_buffer(32)
+        expr = ctypes.create_string_buffer(1 << 14)
+        ex = ctypes.c_int(0)
+        _lib.check(self._L.gs_plan_index_compression(self._h, key.encode(), kind, 32, expr, 1 << 14, ctypes.byref(ex)))
+        return kind.value.decode(), expr.value.decode(), bool(ex.value)
 
     def log(self):
         buf = ctypes.create_string_buffer(1 << 16)

@@ -1,6 +1,7 @@
 // capi.cc -- extern "C" boundary (include/generalsparse.h) + the token_test pipelines.
 #include "../../../include/generalsparse.h"
 #include "gs_plan.hpp"
+#include "index_compress.hpp"
 
 #include <algorithm>
 #include <cstring>
@@ -409,6 +410,46 @@ int gs_plan_log(gs_plan_t *p, char *buf, int buf_len) {
         for (auto &l : p->st.exec->log()) s += l + "\n";
         std::strncpy(buf, s.c_str(), buf_len - 1);
         buf[buf_len - 1] = 0;
+    });
+}
+
+int gs_plan_index_compression(gs_plan_t *p, const char *key, char *kind_out, int kind_len, char *expr_out,
+                              int expr_len, int *exact) {
+    return guard([&] {
+        GS_CHECK(p && key && kind_out && kind_len > 0 && expr_out && expr_len > 0, "bad argument");
+        std::string k = key;
+        // "<POS>_<name>_<sub>": POS is two tokens (e.g. THREAD_META), sub the last
+        const size_t a = k.find('_', k.find('_') + 1), b = k.rfind('_');
+        GS_CHECK(a != std::string::npos && b > a, "key must be <POS>_<name>_<sub>");
+        const std::string pos_s = k.substr(0, a), name = k.substr(a + 1, b - a - 1);
+        const int sub = std::stoi(k.substr(b + 1));
+        gs::POS_TYPE pos = pos_s == "GLOBAL_META" ? gs::GLOBAL_META
+                         : pos_s == "TBLOCK_META" ? gs::TBLOCK_META
+                         : pos_s == "WARP_META" ? gs::WARP_META : gs::THREAD_META;
+        GS_CHECK(p->st.meta->is_exist(pos, name, sub), "no plan array " + k);
+        auto c = gs::analyze_index_compression(*p->st.meta, pos, name, sub);
+        const std::string e = gs::code_of_index_compression(c, "i", gs::get_metadata_item_name(pos, name + "_res", sub));
+        std::strncpy(kind_out, c.kind.c_str(), kind_len - 1);
+        kind_out[kind_len - 1] = 0;
+        std::strncpy(expr_out, e.c_str(), expr_len - 1);
+        expr_out[expr_len - 1] = 0;
+        if (exact) *exact = c.exact ? 1 : 0;
+    });
+}
+
+int gs_index_compression_of_array(const uint64_t *a, uint64_t n, int type_ori, int branch_max, char *kind_out,
+                                  int kind_len, uint64_t *params, int *exact) {
+    return guard([&] {
+        GS_CHECK(a && kind_out && kind_len > 0 && params, "bad argument");
+        auto c = gs::analyze_index_compression(std::vector<uint64_t>(a, a + n), (gs::data_type)type_ori, branch_max);
+        std::strncpy(kind_out, c.kind.c_str(), kind_len - 1);
+        kind_out[kind_len - 1] = 0;
+        params[0] = c.coef;
+        params[1] = c.intercept;
+        params[2] = c.cycle;
+        params[3] = (uint64_t)c.aa;
+        params[4] = (uint64_t)c.bb;
+        if (exact) *exact = c.exact ? 1 : 0;
     });
 }
 

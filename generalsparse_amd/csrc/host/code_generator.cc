@@ -1,6 +1,7 @@
 // code_generator.cc -- lowers the operators' reduction tokens to a gfx950 kernel
 // family and emits a standalone HIP program for it.
 #include "code_generator.hpp"
+#include "index_compress.hpp"
 
 #include <cstdio>
 #include <fstream>
@@ -181,14 +182,29 @@ void code_generator::compile() {
 std::string code_generator::generate_kernel_file_source(int repeat) const {
     GS_CHECK(compiled, "compile() before emitting the program");
     const bool half = get_config().HALF;
+    // model-driven index compression (code_generator.cc:2618-3063): with
+    // MODEL_DRIVEN_COMPRESS, integer plan arrays whose formula reproduces them exactly are
+    // generated from the formula instead of read
+    std::string formulas;
+    if (get_config().MODEL_DRIVEN_COMPRESS)
+        for (const auto &k : spec.arrays) {
+            auto arr = meta->get_element(k)->meta_data_arr;
+            if (arr->is_float()) continue;
+            index_compression c = analyze_index_compression(arr->u(), arr->get_compress_data_type(),
+                                                            get_config().BRANCH_COMPRESS_MAX_SIZE);
+            if (!c.exact || c.kind == "residual") continue;
+            formulas += "    if (!std::strcmp(n, \"" + k + "\")) { std::vector<uint64_t> v(" + std::to_string(arr->get_len()) +
+                        "); for (uint64_t i = 0; i < v.size(); i++) v[i] = " + code_of_index_compression(c, "i", "") +
+                        "; return v; }  // " + c.kind + "\n";
+        }
     std::ostringstream o;
     o << "// kernel_file.hip -- generated by generalsparse_amd code_generator for plan family "
       << spec.name() << "\n"
       << "// build: sh make_kernel.sh; run: ./a.out [matrix.mtx] [N]  -> perf_result (ms, GFLOP/s)\n"
-      << "#include \"kernel_lib.hpp\"\n#include <cstdio>\n#include <cstdlib>\n#include <fstream>\n"
+      << "#include \"kernel_lib.hpp\"\n#include <cstdio>\n#include <cstdlib>\n#include <cstring>\n#include <fstream>\n"
       << "#include <string>\n#include <vector>\n\n"
       << "typedef " << (half ? "gsk::f16" : "float") << " VT;\n"
-      << "static std::vector<uint64_t> rd(const char *n) {\n"
+      << "static std::vector<uint64_t> rd(const char *n) {\n" << formulas
       << "    std::ifstream f(n); std::vector<uint64_t> v; unsigned long long x;\n"
       << "    while (f >> x) v.push_back(x); return v; }\n"
       << "static std::vector<double> rdf(const char *n) {\n"

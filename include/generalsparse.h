@@ -104,6 +104,18 @@ int gs_plan_array_read_u64(gs_plan_t *p, const char *key, uint64_t *out, uint64_
 int gs_plan_array_read_f64(gs_plan_t *p, const char *key, double *out, uint64_t n);
 int gs_plan_log(gs_plan_t *p, char *buf, int buf_len); /* operator / transform history */
 
+/* model-driven index compression of one integer plan array (code_generator.cc:2618-3063,
+ * the if_*_compress / get_*_compress pairs; honours MODEL_DRIVEN_COMPRESS): kind_out gets
+ * "none" | "linear" | "branch" | "cycle_linear" | "cycle_increase" | "residual", expr_out the
+ * expression of `idx` the generated kernel evaluates; *exact = 1 when the formula reproduces
+ * the array (the reference's acceptance tests admit some it does not).  A residual adds
+ * "<POS>_<name>_res_<sub>" to the plan. */
+int gs_plan_index_compression(gs_plan_t *p, const char *key, char *kind_out, int kind_len, char *expr_out,
+                              int expr_len, int *exact);
+/* the same analysis of a raw array (type_ori: the gs data_type code of its storage type) */
+int gs_index_compression_of_array(const uint64_t *a, uint64_t n, int type_ori, int branch_max, char *kind_out,
+                                  int kind_len, uint64_t *params /* coef, intercept, cycle, aa, bb */, int *exact);
+
 /* diagnostics (not part of the reference surface): one launch of the matrix-core
  * kernel's timestamped build; stamps[g*64 + i] = s_memtime of phase i in workgroup g
  * (0 start, 1 loads issued, 2 first barrier, 3 first chunk staged, 4+5j.. per chunk j:

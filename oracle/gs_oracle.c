@@ -883,6 +883,88 @@ int or_interlance_storage_global(or_set *s) {
     return 0;
 }
 
+/* §8f rank 1: model-driven index compression decision (code_generator.cc:16-40 order;
+ * if_linear_compress :2618-2640, if_branch_compress :2642-2670, if_cycle_linear_compress
+ * :2672-2715, if_cycle_increase_compress :2717-2760, if_residual_compress :2762-2824 and
+ * the parameters of the matching get_*_compress).  kind: 0 none, 1 linear, 2 branch,
+ * 3 cycle_linear, 4 cycle_increase, 5 residual; params = coef, intercept, cycle, aa, bb;
+ * res (n entries, may be NULL) gets the residual array.  Unsigned 64-bit arithmetic. */
+static int data_type_of_max(uint64_t m) { /* op_manager.cc:985-1016, struct.hpp enum codes */
+    if (m <= 255) return 1;          /* UNSIGNED_CHAR */
+    if (m <= 65535) return 6;        /* UNSIGNED_SHORT */
+    if (m <= 4294967295ull) return 11; /* UNSIGNED_INT */
+    return 16;                       /* UNSIGNED_LONG */
+}
+
+int or_index_compression(const uint64_t *a, uint64_t n, int type_ori, int branch_max, int *kind,
+                         uint64_t *params, uint64_t *res) {
+    for (int i = 0; i < 5; i++) params[i] = 0;
+    *kind = 0;
+    if (n < 2) return 0;
+    /* linear */
+    uint64_t coef = a[1] - a[0];
+    int ok = 1;
+    for (uint64_t i = 0; i + 1 < n && ok; i++)
+        if (a[i + 1] - a[i] != coef) ok = 0;
+    if (ok) { *kind = 1; params[0] = coef; params[1] = a[0]; return 0; }
+    /* branch */
+    uint64_t item = a[0], count = 1;
+    ok = 1;
+    for (uint64_t i = 0; i < n && ok; i++)
+        if (a[i] != item) { count++; item = a[i]; if ((int64_t)count >= branch_max) ok = 0; }
+    if (ok) { *kind = 2; return 0; }
+    /* cycle linear */
+    uint64_t icpt = a[0], cyc = 1;
+    for (uint64_t i = 1; i < n; i++)
+        if (a[i] == icpt) cyc = i;
+    ok = 1;
+    for (uint64_t i = 0; i < n && ok; i++) {
+        uint64_t in = i % cyc;
+        if (in == 0 && a[i] != icpt) ok = 0;
+        if (in != 0 && (a[i] - icpt) / in != coef) ok = 0;
+    }
+    if (ok) {
+        *kind = 3; params[0] = coef; params[1] = icpt;
+        for (uint64_t i = 0; i < n; i++) if (a[i] == icpt) params[2] = i; /* get_: last i >= 0 */
+        return 0;
+    }
+    /* cycle increase */
+    cyc = 1;
+    ok = 1;
+    for (uint64_t i = 1; i < n; i++)
+        if (a[i] != a[0]) { if (a[i] < a[0]) ok = 0; cyc = i; break; }
+    if (ok && n % cyc != 0) ok = 0;
+    for (uint64_t i = 0; i < n && ok; i++) {
+        uint64_t id = i / cyc;
+        if (id != 0 && (a[i] - a[0]) % id != 0) ok = 0;
+    }
+    if (ok) {
+        *kind = 4; params[1] = a[0];
+        for (uint64_t i = 0; i < n; i++)
+            if (a[i] != a[0]) { params[2] = i; params[0] = a[i] - a[0]; break; }
+        return 0;
+    }
+    /* residual */
+    double t1 = 0, t2 = 0, t3 = 0, t4 = 0, dn = (double)n;
+    for (uint64_t i = 0; i < n; i++) {
+        t1 += (double)(i * i); t2 += (double)i; t3 += (double)(i * a[i]); t4 += (double)a[i];
+    }
+    double fa = (t3 * dn - t2 * t4) / (t1 * dn - t2 * t2), fb = (t1 * t4 - t2 * t3) / (t1 * dn - t2 * t2);
+    int64_t aa = (int64_t)fa, bb = (int64_t)fb;
+    uint64_t m1 = 0, m2 = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        int64_t e = (int64_t)(a[i] - (uint64_t)aa * i - (uint64_t)bb);
+        if (e >= 0) { if ((uint64_t)e > m1) m1 = (uint64_t)e; }
+        else if ((uint64_t)(-e) > m2) m2 = (uint64_t)(-e);
+    }
+    bb -= (int64_t)m2;
+    if (data_type_of_max(m1 + m2) < type_ori) {
+        *kind = 5; params[3] = (uint64_t)aa; params[4] = (uint64_t)bb;
+        if (res) for (uint64_t i = 0; i < n; i++) res[i] = a[i] - (uint64_t)aa * i - (uint64_t)bb;
+    }
+    return 0;
+}
+
 /* ------------------------------------------------------------------ */
 /* canned pipelines: token_test.cc test_spmm_*                          */
 /* ------------------------------------------------------------------ */

@@ -136,3 +136,23 @@ def time_spmm_repeated(M, K, row, col, val, N, min_s):
     if rc != 0:
         raise RuntimeError("oracle cpu path failed")
     return t.value, r.value
+
+
+KINDS = {0: "none", 1: "linear", 2: "branch", 3: "cycle_linear", 4: "cycle_increase", 5: "residual"}
+
+
+def index_compression(a, type_ori=16, branch_max=5):
+    """oracle restatement of the reference's index-compression decision:
+    (kind, {coef, intercept, cycle, aa, bb}, residual array or None)"""
+    L = lib()
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    kind = ctypes.c_int(0)
+    prm = np.zeros(5, np.uint64)
+    res = np.zeros(max(1, len(a)), np.uint64)
+    rc = L.or_index_compression(_p(a, ctypes.c_uint64), ctypes.c_uint64(len(a)), int(type_ori), int(branch_max),
+                                ctypes.byref(kind), _p(prm, ctypes.c_uint64), _p(res, ctypes.c_uint64))
+    assert rc == 0
+    k = KINDS[kind.value]
+    p = {"coef": int(prm[0]), "intercept": int(prm[1]), "cycle": int(prm[2]),
+         "aa": int(prm[3].astype(np.int64)), "bb": int(prm[4].astype(np.int64))}
+    return k, p, (res[:len(a)] if k == "residual" else None)
