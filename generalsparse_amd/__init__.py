@@ -88,6 +88,19 @@ class Plan:
         return cls(h.value)
 
     @classmethod
+    def load(cls, path):
+        """a compiled plan from a binary plan file (plan_io.cc); upload() before spmm()"""
+        L = _lib.load()
+        h = ctypes.c_void_p()
+        _lib.check(L.gs_plan_load(str(path).encode(), ctypes.byref(h)))
+        return cls(h.value)
+
+    def save(self, path):
+        """writes the compiled plan (kernel selection + every plan array) to one binary file"""
+        _lib.check(self._L.gs_plan_save(self._h, str(path).encode()))
+        return self
+
+    @classmethod
     def from_coo(cls, n_rows, n_cols, row, col, val=None):
         L = _lib.load()
         row = np.ascontiguousarray(row, dtype=np.uint64)

@@ -63,6 +63,8 @@ SIGNATURES = {
     "gs_plan_array_read_u64": ([ctypes.c_void_p, ctypes.c_char_p, u64p, ctypes.c_uint64], ctypes.c_int),
     "gs_plan_array_read_f64": ([ctypes.c_void_p, ctypes.c_char_p, f64p, ctypes.c_uint64], ctypes.c_int),
     "gs_plan_log": ([ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
+    "gs_plan_save": ([ctypes.c_void_p, ctypes.c_char_p], ctypes.c_int),
+    "gs_plan_load": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
     "gs_plan_index_compression": ([ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p,
                                    ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "gs_index_compression_of_array": ([u64p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,

@@ -453,6 +453,27 @@ int gs_index_compression_of_array(const uint64_t *a, uint64_t n, int type_ori, i
     });
 }
 
+int gs_plan_save(gs_plan_t *p, const char *path) {
+    return guard([&] {
+        GS_CHECK(p && path, "null argument");
+        gs::save_plan(p->st, path);
+    });
+}
+
+int gs_plan_load(const char *path, gs_plan_t **out) {
+    return guard([&] {
+        GS_CHECK(path && out, "null argument");
+        auto *p = new gs_plan;
+        try {
+            gs::load_plan(p->st, path);
+        } catch (...) {
+            delete p;
+            throw;
+        }
+        *out = p;
+    });
+}
+
 int gs_plan_from_mtx(const char *path, const gs_opts *opts, gs_plan_t **out) {
     gs_opts o;
     if (opts) o = *opts;

@@ -95,6 +95,8 @@ class code_generator {
     // lowers the token set to a kernel family (code_generator.hpp:265-269)
     void compile();
     bool is_compiled() const { return compiled; }
+    // a plan file's spec (plan_io.cc): the selection compile() made when the plan was saved
+    void restore_compiled(const kernel_spec &s) { spec = s; compiled = true; }
     const kernel_spec &get_kernel_spec() const { return spec; }
 
     // HIP source of the generated program (kernel + main with perf_result)

@@ -58,6 +58,10 @@ struct plan_state {
     bool uploaded = false;
 };
 
+// plan_io.cc: binary plan files
+void save_plan(const plan_state &p, const std::string &path);
+void load_plan(plan_state &p, const std::string &path);
+
 // device_plan.hip
 void upload_plan(plan_state &p, int dtype, int device);
 void add_replica(plan_state &p);

@@ -123,6 +123,11 @@ int gs_index_compression_of_array(const uint64_t *a, uint64_t n, int type_ori, i
 int gs_debug_mfma_timeline(gs_plan_t *p, const void *B, void *C, int N, gs_stream_t stream, uint64_t *stamps,
                            uint64_t n_stamps);
 
+/* binary plan files: a compiled plan (kernel selection + every plan
+ * array) in one file, loaded without re-running the transforms; upload before gs_spmm */
+int gs_plan_save(gs_plan_t *p, const char *path);
+int gs_plan_load(const char *path, gs_plan_t **out);
+
 /* one call: read + pipeline + compile + upload */
 int gs_plan_from_mtx(const char *path, const gs_opts *opts, gs_plan_t **out);
 void gs_plan_free(gs_plan_t *p);

@@ -429,3 +429,32 @@ def test_merge_path_deterministic_and_no_stale_state():
     torch.cuda.synchronize()
     assert not torch.isnan(C1).any()
     assert torch.equal(C1, C2)
+
+
+def test_loaded_plan_file_computes_the_same(tmp_path):
+    """§8f rank 4: a plan loaded from its binary file gives bit-identical C (merge path,
+    matrix-core row blocks)"""
+    for name, p0, p1, dtype, N in [("merge_path", 256, 1, "f32", 8), ("tblock_warp_total", 20, 2, "f16", 32)]:
+        M, K = 640, 700
+        r, c, v = ds.random_rows(M, K, 40.0, seed=3, empty_frac=0.1)
+        plan, C, B = run(M, K, r, c, v, name, p0, p1, N, dtype)
+        f = tmp_path / f"{name}.gsplan"
+        plan.save(f)
+        q = gsa.Plan.load(f).upload(dtype, 0)
+        C2 = q.spmm(torch.from_numpy(B).to(DEV))
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(C, C2.float().cpu().numpy())
+
+
+def test_autotune_picks_a_timed_variant(tmp_path):
+    from generalsparse_amd.autotune import autotune
+    M, K = 1024, 1024
+    r, c, v = ds.rmat(1024, 20000, seed=5)
+    f = tmp_path / "best.gsplan"
+    plan, res = autotune(M, K, r, c, v, 8, "f32", reps=5, rotation_mb=16, save_path=f)
+    timed = {k: t for k, t in res.items() if isinstance(t, float)}
+    assert timed and f.exists()
+    B = np.random.default_rng(0).uniform(-1, 1, (K, 8)).astype(np.float32)
+    C = plan.spmm(torch.from_numpy(B).to(DEV))
+    torch.cuda.synchronize()
+    check(C.float().cpu().numpy(), ofi.spmm_ref(M, 8, r, c, v, B, "f64"), "f32")

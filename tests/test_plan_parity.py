@@ -305,3 +305,26 @@ def test_synthetic_generators_shapes():
     assert np.all(np.bincount((c // 4 + 4 * r).astype(np.int64)) == 2)
     r, c, v = ds.rmat(1024, 5000, 1)
     assert len(r) <= 5000 and np.all(np.diff(r.astype(np.int64)) >= 0)
+
+
+@pytest.mark.parametrize("name,N,p0,p1", [("tblock_warp_total", 32, 20, 2), ("merge_path", 8, 64, 1),
+                                          ("warp_bit_map_interleaved", 32, 4, 1), ("warp_segment", 32, 4, 1)])
+def test_binary_plan_file_round_trip(tmp_path, name, N, p0, p1):
+    """§8f rank 4: a compiled plan saved to one binary file loads back with every plan
+    array bit-identical and the same kernel selection"""
+    M, K = 150, 400
+    r, c, v = random_coo(M, K, 0.2, 8, empty=0.1)
+    p = product_plan(M, K, r, c, v, name, N, p0, p1)
+    p.compile()
+    f = tmp_path / "plan.gsplan"
+    p.save(f)
+    q = gsa.Plan.load(f)
+    assert q.info()["kernel_name"] == p.info()["kernel_name"]
+    a, b = p.arrays(), q.arrays()
+    assert set(a) == set(b)
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    bad = tmp_path / "bad.gsplan"
+    bad.write_bytes(b"not a plan")
+    with pytest.raises(gsa.GsError):
+        gsa.Plan.load(bad)
