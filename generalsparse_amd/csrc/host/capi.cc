@@ -156,6 +156,15 @@ void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1)
         ex.add_and_run(std::make_shared<warp_total_reduce_operator>(cg, cf, ctx));
         ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)((rows + rb - 1) / rb),
                                                              std::vector<unsigned>{64u, 4u}, cf, ctx));
+    } else if (name == "tblock_warp_total_relative") {
+        // §8f rank 1: the C2 plan with BMW indices relative to their BMTB as well
+        // (fixed_interval_row_direction_warp_blocking_operator with both relative flags)
+        int rb = p0 > 0 ? p0 : 4, wb = p1 > 0 ? p1 : 1, cf = 1;
+        ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, rb, false, ctx));
+        ex.add_and_run(std::make_shared<fixed_interval_row_direction_warp_blocking_operator>(cg, wb, true, true, false, ctx));
+        ex.add_and_run(std::make_shared<warp_total_reduce_operator>(cg, cf, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)((rows + rb - 1) / rb),
+                                                             std::vector<unsigned>{64u, 4u}, cf, ctx));
     } else if (name == "balanced_warp_total") {
         // balanced row-direction BMWs (A11) + warp_total (the valid composition)
         int per = p0 > 0 ? p0 : 2048, cf = p1 > 0 ? p1 : 1;

@@ -972,4 +972,42 @@ void modify_vals_by_interlance_storage::run(bool check) {
     is_run = true;
 }
 
+// ------------------------------------------------- relative indices (§8f rank 1)
+// get_begin_rows_of_BMW_after_fixed_blocking_in_row_direction_relative_to_BMTB.cc:45-70:
+// per BMTB, its BMW starts minus the BMTB's first row (no ending entry)
+void get_begin_rows_of_BMW_after_fixed_blocking_in_row_direction_relative_to_BMTB::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &tb = m.u(TBLOCK_META, "first_row_indices", target_matrix_id);
+    GS_CHECK(fixed_row_block_size > 0, "fixed_row_block_size > 0");
+    std::vector<uint64_t> out;
+    for (size_t i = 0; i + 1 < tb.size(); i++)
+        for (uint64_t r = tb[i]; r < tb[i + 1]; r += (uint64_t)fixed_row_block_size) out.push_back(r - tb[i]);
+    replace_u(WARP_META, "first_row_indices_relative_to_BMTB", std::move(out));
+    src(TBLOCK_META, "first_row_indices");
+    is_run = true;
+}
+
+// get_begin_nzs_of_BMW_after_fixed_blocking_in_row_direction_relative_to_BMTB.cc:50-85:
+// per BMTB, the nonzeros before each BMW counted from the BMTB's first row
+void get_begin_nzs_of_BMW_after_fixed_blocking_in_row_direction_relative_to_BMTB::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &tb = m.u(TBLOCK_META, "first_row_indices", target_matrix_id);
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    const uint64_t row_num = row_num_of_sub_matrix(m, target_matrix_id);
+    auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+    GS_CHECK(fixed_row_block_size > 0, "fixed_row_block_size > 0");
+    std::vector<uint64_t> out;
+    for (size_t i = 0; i + 1 < tb.size(); i++) {
+        uint64_t nz = 0;
+        for (uint64_t r = tb[i]; r < tb[i + 1]; r++) {
+            if ((r - tb[i]) % (uint64_t)fixed_row_block_size == 0) out.push_back(nz);
+            nz += r < cnt.size() ? cnt[r] : 0;
+        }
+    }
+    replace_u(WARP_META, "first_nz_indices_relative_to_BMTB", std::move(out));
+    src(TBLOCK_META, "first_row_indices");
+    src(GLOBAL_META, "nz_row_indices");
+    is_run = true;
+}
+
 }  // namespace gs

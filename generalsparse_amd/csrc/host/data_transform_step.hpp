@@ -73,6 +73,9 @@ GS_DECLARE_STEP_P(get_begin_nzs_of_BMW_after_fixed_blocking_in_row_direction_wit
 GS_DECLARE_STEP_P(get_begin_rows_of_BMW_after_fixed_blocking_in_row_direction_in_BMTB, int, fixed_row_block_size)
 GS_DECLARE_STEP_P(get_begin_nzs_of_BMW_after_fixed_blocking_in_row_direction_in_BMTB, int, fixed_row_block_size)
 GS_DECLARE_STEP(get_begin_BMWs_of_BMTB_after_blocking_in_row_direction)
+// relative indices (§8f rank 1): BMW starts relative to their BMTB
+GS_DECLARE_STEP_P(get_begin_rows_of_BMW_after_fixed_blocking_in_row_direction_relative_to_BMTB, int, fixed_row_block_size)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMW_after_fixed_blocking_in_row_direction_relative_to_BMTB, int, fixed_row_block_size)
 
 // fixed nnz-direction blocking (A9)
 GS_DECLARE_STEP_P(modify_col_indices_by_nnz_pad, int, nnz_target)

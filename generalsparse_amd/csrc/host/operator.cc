@@ -159,15 +159,25 @@ bool fixed_interval_row_direction_warp_blocking_operator::is_valid_according_to_
 
 void fixed_interval_row_direction_warp_blocking_operator::run(bool check) {
     if (check) GS_CHECK(is_valid_according_to_metadata(), "warp blocking: invalid metadata");
-    if (row_index_is_relative_to_BMTB || nz_index_is_relative_to_BMTB)
-        throw gs_error("relative BMW indices (SURVEY §8f rank 1) are not built in this round");
+    if ((row_index_is_relative_to_BMTB || nz_index_is_relative_to_BMTB) && !has(TBLOCK_META, "first_row_indices"))
+        throw gs_error("relative BMW indices need a BMTB level (fixed_interval_row_direction_warp_blocking_operator.cc:100-101)");
     if (has(TBLOCK_META, "first_row_indices")) {
         get_begin_rows_of_BMW_after_fixed_blocking_in_row_direction_in_BMTB a(meta_data_set_ptr, target_matrix_id,
                                                                               fixed_row_block_size);
         run_step(a, check);
+        if (row_index_is_relative_to_BMTB) {  // :52-58
+            get_begin_rows_of_BMW_after_fixed_blocking_in_row_direction_relative_to_BMTB r(meta_data_set_ptr, target_matrix_id,
+                                                                                           fixed_row_block_size);
+            run_step(r, check);
+        }
         get_begin_nzs_of_BMW_after_fixed_blocking_in_row_direction_in_BMTB b(meta_data_set_ptr, target_matrix_id,
                                                                              fixed_row_block_size);
         run_step(b, check);
+        if (nz_index_is_relative_to_BMTB) {  // :66-72
+            get_begin_nzs_of_BMW_after_fixed_blocking_in_row_direction_relative_to_BMTB r(meta_data_set_ptr, target_matrix_id,
+                                                                                          fixed_row_block_size);
+            run_step(r, check);
+        }
         get_begin_BMWs_of_BMTB_after_blocking_in_row_direction c(meta_data_set_ptr, target_matrix_id);
         run_step(c, check);
     } else {

@@ -965,6 +965,31 @@ int or_index_compression(const uint64_t *a, uint64_t n, int type_ori, int branch
     return 0;
 }
 
+/* §8f rank 1, relative BMW indices inside BMTBs:
+ * get_begin_rows_of_BMW_after_fixed_blocking_in_row_direction_relative_to_BMTB.cc:45-70 and
+ * get_begin_nzs_of_BMW_after_fixed_blocking_in_row_direction_relative_to_BMTB.cc:50-85
+ * (no ending entry; the nz counter restarts at every BMTB) */
+int or_bmw_relative_to_bmtb(or_set *s, int rb) {
+    or_array *TR = get(s, "TBLOCK_META", "first_row_indices", 0);
+    if (!TR || rb < 1) return fail(s, "relative BMW indices need BMTBs");
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    uint64_t row_num = row_num_of(s);
+    uint64_t *cnt = row_nnz(R->u, R->len, row_num);
+    vu rr = {0}, rn = {0};
+    for (uint64_t i = 0; i + 1 < TR->len; i++) {
+        uint64_t b = TR->u[i], e = TR->u[i + 1], nz = 0;
+        for (uint64_t r = b; r < e; r += (uint64_t)rb) vu_push(&rr, r - b);
+        for (uint64_t r = b; r < e; r++) {
+            if ((r - b) % (uint64_t)rb == 0) vu_push(&rn, nz);
+            nz += r < row_num ? cnt[r] : 0;
+        }
+    }
+    free(cnt);
+    put_u(s, "WARP_META", "first_row_indices_relative_to_BMTB", 0, rr.p, rr.n);
+    put_u(s, "WARP_META", "first_nz_indices_relative_to_BMTB", 0, rn.p, rn.n);
+    return 0;
+}
+
 /* ------------------------------------------------------------------ */
 /* canned pipelines: token_test.cc test_spmm_*                          */
 /* ------------------------------------------------------------------ */
@@ -1008,6 +1033,11 @@ int or_pipeline(or_set *s, const char *name, int p0, int p1) {
         if (or_col_dir_thread_blocking(s, 64, 1)) return -1;
         if (or_interlance_storage_global(s)) return -1;
         return or_parent_bit_map_operator(s, 0, p0, 0, 0);
+    }
+    if (!strcmp(name, "tblock_warp_total_relative")) { /* BMW indices relative to the BMTB too */
+        if (or_row_dir_tblock_blocking(s, p0)) return -1;
+        if (or_row_dir_warp_blocking(s, p1 > 0 ? p1 : 1)) return -1;
+        return or_bmw_relative_to_bmtb(s, p1 > 0 ? p1 : 1);
     }
     if (!strcmp(name, "balanced_warp_total")) /* A11 balanced BMW + warp_total */
         return or_balanced_row_dir_warp_blocking(s, (uint64_t)p0);

@@ -269,6 +269,17 @@ cases.append({
     },
 })
 
+# relative BMW indices (§8f rank 1) on ex1 with BMTBs of 4 rows and BMWs of 2 rows:
+# BMTB rows [0,4) and [4,6); BMW starts 0,2 | 4 -> relative 0,2 | 0; row nnz [2,0,3,1,5,0]:
+# BMTB 0 nonzeros before each BMW 0, 2 | BMTB 1: 0
+cases.append({
+    "matrix": "ex1", "pipeline": "tblock_warp_total_relative", "p0": 4, "p1": 2,
+    "expect": {
+        W + "first_row_indices_relative_to_BMTB_0": [0, 2, 0],
+        W + "first_nz_indices_relative_to_BMTB_0": [0, 2, 0],
+    },
+})
+
 out = {"matrices": {"ex1": EX1, "ex2": EX2, "ex3": EX3, "ex4": EX4}, "cases": cases}
 path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hand_plans.json")
 with open(path, "w") as f:

@@ -25,6 +25,8 @@ def oracle_params(name, N, p0, p1):
     cf = p1 if p1 > 0 else 1
     if name == "thread_total":
         return p0 if p0 > 0 else 4
+    if name == "tblock_warp_total_relative":
+        return p0
     if name == "warp_segment":
         return min(N, 32)
     if name == "thread_bit_map":
@@ -44,7 +46,7 @@ def product_plan(M, K, row, col, val, name, N, p0=0, p1=0):
 
 def compare(M, K, row, col, val, name, N, p0=0, p1=0):
     exp, err = ofi.run_pipeline(M, K, row, col, val, name, oracle_params(name, N, p0, p1),
-                                p1 if name == "merge_path" else 0)
+                                p1 if name in ("merge_path", "tblock_warp_total_relative") else 0)
     if err is not None:
         with pytest.raises(gsa.GsError):
             product_plan(M, K, row, col, val, name, N, p0, p1)
@@ -75,7 +77,8 @@ PIPES = [("thread_total", 32, 4, 1), ("thread_total", 8, 8, 1), ("warp_total", 3
          ("tblock_warp_total", 32, 7, 1), ("balanced_warp_total", 32, 64, 1), ("warp_bit_map", 32, 4, 1),
          ("tblock_bit_map", 32, 4, 1), ("balanced_block_total", 32, 64, 1), ("balanced_block_total", 8, 7, 1),
          ("balanced_thread_total", 8, 16, 1), ("merge_path", 8, 16, 1), ("merge_path", 8, 7, 2),
-         ("merge_path", 32, 5, 3), ("merge_path", 8, 1, 1), ("merge_path", 8, 1024, 1)]
+         ("merge_path", 32, 5, 3), ("merge_path", 8, 1, 1), ("merge_path", 8, 1024, 1),
+         ("tblock_warp_total_relative", 32, 20, 2), ("tblock_warp_total_relative", 32, 7, 3)]
 
 # col-direction pipelines need rows long enough for the 64-nnz padding rule
 COL_PIPES = [("warp_bit_map", 32, 4, 1), ("warp_bit_map", 8, 4, 2), ("warp_bit_map", 1, 4, 1),
@@ -121,7 +124,7 @@ def test_hand_derived_fixtures_through_product():
     g = json.load(open(GOLDEN))
     back = {"thread_total": (32, 4, 1), "warp_total": (32, 0, 1), "block_total": (8, 0, 1),
             "merge_path": (8, 0, 1), "balanced_block_total": (32, 0, 1), "balanced_thread_total": (8, 0, 1),
-            "warp_bit_map_interleaved": (32, 4, 1),
+            "warp_bit_map_interleaved": (32, 4, 1), "tblock_warp_total_relative": (32, 4, 2),
             "tblock_warp_total": (32, 4, 1), "balanced_warp_total": (32, 16, 1),
             "warp_bit_map": (32, 4, 1), "tblock_bit_map": (32, 4, 1)}
     for case in g["cases"]:
@@ -135,9 +138,9 @@ def test_hand_derived_fixtures_through_product():
         else:
             N, p0, p1 = back[name]
             if name in ("tblock_warp_total", "balanced_warp_total", "merge_path", "balanced_block_total",
-                        "balanced_thread_total"):
+                        "balanced_thread_total", "tblock_warp_total_relative"):
                 p0 = case["p0"]
-            if name == "merge_path":
+            if name in ("merge_path", "tblock_warp_total_relative"):
                 p1 = case["p1"]
         if case.get("expect_error"):
             with pytest.raises(gsa.GsError):
