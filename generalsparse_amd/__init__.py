@@ -122,14 +122,29 @@ class Plan:
         return cls.from_coo(A.shape[0], A.shape[1], coo.row, coo.col, coo.data)
 
     # ------------------------------------------------------------ operators
-    def add_operator(self, name, *args):
+    def add_operator(self, name, *args, sub=0):
+        """operator_executer::add_and_run of the named operator on sub-matrix `sub`
+        (the reference's code_generator(meta, sub) target)"""
         arr = (ctypes.c_longlong * max(1, len(args)))(*[int(a) for a in args])
-        _lib.check(self._L.gs_plan_add_operator(self._h, name.encode(), arr, len(args)))
+        _lib.check(self._L.gs_plan_add_operator_sub(self._h, int(sub), name.encode(), arr, len(args)))
         return self
 
-    def run_pipeline(self, name, N, p0=0, p1=0):
-        _lib.check(self._L.gs_plan_run_pipeline(self._h, name.encode(), int(N), int(p0), int(p1)))
+    def run_pipeline(self, name, N, p0=0, p1=0, sub=0):
+        _lib.check(self._L.gs_plan_run_pipeline_sub(self._h, int(sub), name.encode(), int(N), int(p0), int(p1)))
         return self
+
+    def divide_rows(self, interval, sub=0):
+        """fixed_interval_row_matrix_div_operator: one new sub-matrix per non-empty interval
+        of `interval` rows; returns the live sub-matrix ids"""
+        self.add_operator("fixed_interval_row_matrix_div_operator", int(interval), sub=sub)
+        return self.sub_matrices()
+
+    def sub_matrices(self):
+        n = self._L.gs_plan_sub_matrices(self._h, None, 0)
+        _lib.check(min(n, 0))
+        ids = (ctypes.c_int * max(1, n))()
+        _lib.check(min(self._L.gs_plan_sub_matrices(self._h, ids, n), 0))
+        return list(ids[:n])
 
     def compile(self):
         _lib.check(self._L.gs_plan_compile(self._h))

@@ -29,7 +29,8 @@ class GsPlanInfo(ctypes.Structure):
                 ("dtype", ctypes.c_int), ("replicas", ctypes.c_int), ("needs_memset", ctypes.c_int),
                 ("kernel_name", ctypes.c_char * 64), ("lds_stage", ctypes.c_int), ("lds_n", ctypes.c_uint32),
                 ("lds_kc", ctypes.c_uint32), ("lds_chunks", ctypes.c_uint32), ("lds_waves", ctypes.c_uint32),
-                ("lds_bytes", ctypes.c_uint64), ("tile_bytes", ctypes.c_uint64), ("ksplit", ctypes.c_uint32)]
+                ("lds_bytes", ctypes.c_uint64), ("tile_bytes", ctypes.c_uint64), ("ksplit", ctypes.c_uint32),
+                ("n_kernels", ctypes.c_int)]
 
 
 # every symbol include/generalsparse.h declares, with its ctypes signature
@@ -45,6 +46,11 @@ SIGNATURES = {
                              ctypes.c_int),
     "gs_plan_run_pipeline": ([ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int],
                              ctypes.c_int),
+    "gs_plan_add_operator_sub": ([ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.c_longlong),
+                                  ctypes.c_int], ctypes.c_int),
+    "gs_plan_run_pipeline_sub": ([ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_int], ctypes.c_int),
+    "gs_plan_sub_matrices": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int], ctypes.c_int),
     "gs_plan_compile": ([ctypes.c_void_p], ctypes.c_int),
     "gs_plan_generate_program": ([ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int],
                                  ctypes.c_int),

@@ -5,9 +5,17 @@
 
 #include <algorithm>
 #include <cstring>
+#include <map>
+#include <memory>
 
+// one plan per sub-matrix: st is sub-matrix 0 (the undivided matrix); a row division
+// (fixed_interval_row_matrix_div_operator, §8f rank 3) adds sub-matrices, each with its
+// own code generator / kernel / device arrays over the shared metadata set and operator
+// history, run one after another by the multi-kernel executor (gs_spmm)
 struct gs_plan {
     gs::plan_state st;
+    std::map<int, std::unique_ptr<gs::plan_state>> subs;
+    std::vector<std::pair<uint64_t, uint64_t>> gaps;  // output rows no sub-matrix writes
 };
 
 namespace {
@@ -38,6 +46,58 @@ void init_plan(gs::plan_state &s, std::shared_ptr<gs::meta_data_set> m) {
 
 uint64_t global_scalar(const gs::plan_state &s, const char *n, int sub) { return s.meta->scalar(gs::GLOBAL_META, n, sub); }
 
+bool sub_live(const gs::meta_data_set &m, int sub) { return m.is_exist(gs::GLOBAL_META, "nz_col_indices", sub); }
+
+gs::plan_state &state_of(gs_plan *p, int sub) {
+    GS_CHECK(sub >= 0, "sub-matrix id >= 0");
+    if (sub == 0) return p->st;
+    auto it = p->subs.find(sub);
+    if (it != p->subs.end()) return *it->second;
+    GS_CHECK(sub_live(*p->st.meta, sub), "no sub-matrix " + std::to_string(sub) + " in the plan");
+    auto s = std::make_unique<gs::plan_state>();
+    s->meta = p->st.meta;
+    s->exec = p->st.exec;  // one operator history, keyed by sub-matrix id
+    s->cg = std::make_shared<gs::code_generator>(s->meta, sub);
+    s->M = p->st.M;
+    s->K = p->st.K;
+    s->nnz = p->st.nnz;
+    auto &r = *s;
+    p->subs.emplace(sub, std::move(s));
+    return r;
+}
+
+// the kernels of the plan in sub-matrix order; every live sub-matrix needs one
+std::vector<gs::plan_state *> kernel_states(gs_plan *p, bool strict = true) {
+    const auto &m = *p->st.meta;
+    std::vector<gs::plan_state *> out;
+    const int mx = m.get_max_sub_matrix_id_of_data_item(gs::GLOBAL_META, "nz_col_indices");
+    for (int sb = 0; sb <= mx; sb++) {
+        if (!sub_live(m, sb)) continue;
+        if (!strict && sb != 0 && !p->subs.count(sb)) continue;
+        GS_CHECK(sb == 0 || p->subs.count(sb), "sub-matrix " + std::to_string(sb) + " has no plan (add its operators)");
+        out.push_back(sb == 0 ? &p->st : p->subs[sb].get());
+    }
+    GS_CHECK(!out.empty(), "plan has no sub-matrix");
+    return out;
+}
+
+bool divided(gs_plan *p) { return !p->subs.empty() || !sub_live(*p->st.meta, 0); }
+
+// multi-kernel executor: zero the output rows of empty row intervals, then run each
+// sub-matrix's kernel on the same stream (each writes only its own rows)
+void spmm_all(gs_plan *p, int replica, const void *B, void *C, uint32_t N, hipStream_t stream) {
+    if (!divided(p)) {
+        gs::launch_spmm(p->st, replica, B, C, N, stream);
+        return;
+    }
+    auto ks = kernel_states(p);
+    const size_t e = ks.front()->dev.dtype == 0 ? 4 : 2;
+    for (auto &g : p->gaps)
+        if (g.second > g.first)
+            gs::memset_rows(C, g.first, g.second, N, e, stream);
+    for (gs::plan_state *s : ks) gs::launch_spmm(*s, replica, B, C, N, stream);
+}
+
 }  // namespace
 
 namespace gs {
@@ -49,8 +109,11 @@ void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1)
     auto cg = s.cg;
     auto &ex = *s.exec;
     auto ctx = ex.get_operator_context();
-    const uint64_t rows = global_scalar(s, "origin_row_num", -1);
-    const uint64_t nnz = global_scalar(s, "origin_nnz_num", -1);
+    // rows / nonzeros of the plan's sub-matrix (the whole matrix for sub-matrix 0)
+    const int sb = cg->get_sub_matrix_id();
+    const uint64_t rows = sb == 0 ? global_scalar(s, "origin_row_num", -1)
+                                  : global_scalar(s, "end_row_index", sb) - global_scalar(s, "begin_row_index", sb) + 1;
+    const uint64_t nnz = s.meta->u(GLOBAL_META, "nz_col_indices", sb).size();
     if (name == "thread_total") {  // token_test.cc:1003-1092, p0 = sparse_cf (4), p1 = cf (1)
         int scf = p0 > 0 ? p0 : 4, cf = p1 > 0 ? p1 : 1;
         ex.add_and_run(std::make_shared<sort_operator>(cg, ctx));
@@ -257,32 +320,57 @@ int gs_set_config_int(const char *key, long long value) {
     return guard([&] { gs::set_config(key, value); });
 }
 
-int gs_plan_add_operator(gs_plan_t *p, const char *op_name, const long long *args, int nargs) {
+int gs_plan_add_operator_sub(gs_plan_t *p, int sub, const char *op_name, const long long *args, int nargs) {
     return guard([&] {
         GS_CHECK(p && op_name && (nargs == 0 || args), "null argument");
+        gs::plan_state &st = state_of(p, sub);
         std::vector<long long> a(args, args + nargs);
-        auto op = gs::make_operator(op_name, a, p->st.cg, p->st.exec->get_operator_context());
-        p->st.exec->add_and_run(op);
+        auto op = gs::make_operator(op_name, a, st.cg, st.exec->get_operator_context());
+        st.exec->add_and_run(op);
+    });
+}
+
+int gs_plan_add_operator(gs_plan_t *p, const char *op_name, const long long *args, int nargs) {
+    return gs_plan_add_operator_sub(p, 0, op_name, args, nargs);
+}
+
+int gs_plan_run_pipeline_sub(gs_plan_t *p, int sub, const char *name, int dense_n, int p0, int p1) {
+    return guard([&] {
+        GS_CHECK(p && name && dense_n > 0, "bad argument");
+        gs::run_pipeline(state_of(p, sub), name, dense_n, p0, p1);
     });
 }
 
 int gs_plan_run_pipeline(gs_plan_t *p, const char *name, int dense_n, int p0, int p1) {
-    return guard([&] {
-        GS_CHECK(p && name && dense_n > 0, "bad argument");
-        gs::run_pipeline(p->st, name, dense_n, p0, p1);
+    return gs_plan_run_pipeline_sub(p, 0, name, dense_n, p0, p1);
+}
+
+int gs_plan_sub_matrices(gs_plan_t *p, int *ids, int cap) {
+    int n = 0;
+    int rc = guard([&] {
+        GS_CHECK(p && (cap == 0 || ids), "bad argument");
+        const auto &m = *p->st.meta;
+        const int mx = m.get_max_sub_matrix_id_of_data_item(gs::GLOBAL_META, "nz_col_indices");
+        for (int sb = 0; sb <= mx; sb++)
+            if (sub_live(m, sb)) {
+                if (n < cap) ids[n] = sb;
+                n++;
+            }
     });
+    return rc ? rc : n;
 }
 
 int gs_plan_compile(gs_plan_t *p) {
     return guard([&] {
         GS_CHECK(p, "null plan");
-        p->st.cg->compile();
+        for (gs::plan_state *s : kernel_states(p)) s->cg->compile();
     });
 }
 
 int gs_plan_generate_program(gs_plan_t *p, const char *root_dir, int repeat, char *dir_out, int dir_out_len) {
     return guard([&] {
         GS_CHECK(p && root_dir, "null argument");
+        GS_CHECK(!divided(p), "generated programs cover undivided plans (one kernel)");
         std::string dir;
         p->st.cg->generate_final_program(repeat, root_dir, &dir);
         if (dir_out && dir_out_len > 0) {
@@ -295,21 +383,35 @@ int gs_plan_generate_program(gs_plan_t *p, const char *root_dir, int repeat, cha
 int gs_plan_upload(gs_plan_t *p, int dtype, int device) {
     return guard([&] {
         GS_CHECK(p, "null plan");
-        gs::upload_plan(p->st, dtype, device);
+        auto ks = kernel_states(p);
+        for (gs::plan_state *s : ks) gs::upload_plan(*s, dtype, device);
+        // rows of C no sub-matrix owns (intervals without nonzeros): zeroed by the executor
+        p->gaps.clear();
+        if (divided(p)) {
+            std::vector<std::pair<uint64_t, uint64_t>> own;
+            for (gs::plan_state *s : ks) own.push_back({s->dev.out_lo, s->dev.n_out_rows});
+            std::sort(own.begin(), own.end());
+            uint64_t at = 0;
+            for (auto &o : own) {
+                if (o.first > at) p->gaps.push_back({at, o.first});
+                at = std::max(at, o.second);
+            }
+            if (at < p->st.M) p->gaps.push_back({at, p->st.M});
+        }
     });
 }
 
 int gs_plan_add_replica(gs_plan_t *p) {
     return guard([&] {
         GS_CHECK(p, "null plan");
-        gs::add_replica(p->st);
+        for (gs::plan_state *s : kernel_states(p)) gs::add_replica(*s);
     });
 }
 
 int gs_spmm_replica(gs_plan_t *p, int replica, const void *B, void *C, int N, gs_stream_t stream) {
     return guard([&] {
         GS_CHECK(p && B && C && N > 0, "bad argument");
-        gs::launch_spmm(p->st, replica, B, C, (uint32_t)N, (hipStream_t)stream);
+        spmm_all(p, replica, B, C, (uint32_t)N, (hipStream_t)stream);
     });
 }
 
@@ -321,7 +423,7 @@ int gs_spmm_rotate(gs_plan_t *p, int count, int first, const void *const *B_ptrs
         GS_CHECK(reps > 0, "plan is not on the device");
         for (int i = 0; i < count; i++) {
             int k = first + i;
-            gs::launch_spmm(p->st, k % reps, B_ptrs[k % n_ptrs], C_ptrs[k % n_ptrs], (uint32_t)N, (hipStream_t)stream);
+            spmm_all(p, k % reps, B_ptrs[k % n_ptrs], C_ptrs[k % n_ptrs], (uint32_t)N, (hipStream_t)stream);
         }
     });
 }
@@ -342,11 +444,13 @@ int gs_plan_info_get(gs_plan_t *p, gs_plan_info *info) {
     return guard([&] {
         GS_CHECK(p && info, "null argument");
         std::memset(info, 0, sizeof(*info));
-        auto &s = p->st;
+        auto ks = kernel_states(p, false);
+        auto &s = *ks.front();  // kernel fields: the first sub-matrix's kernel
         info->rows = s.M;
         info->cols = s.K;
         info->nnz = s.nnz;
-        info->nnz_stored = s.meta->u(gs::GLOBAL_META, "nz_col_indices", 0).size();
+        info->n_kernels = (int)ks.size();
+        for (gs::plan_state *k : ks) info->nnz_stored += s.meta->u(gs::GLOBAL_META, "nz_col_indices", k->cg->get_sub_matrix_id()).size();
         if (s.cg->is_compiled()) {
             const auto &sp = s.cg->get_kernel_spec();
             info->family = sp.family;
@@ -465,6 +569,7 @@ int gs_index_compression_of_array(const uint64_t *a, uint64_t n, int type_ori, i
 int gs_plan_save(gs_plan_t *p, const char *path) {
     return guard([&] {
         GS_CHECK(p && path, "null argument");
+        GS_CHECK(!divided(p), "plan files hold undivided plans");
         gs::save_plan(p->st, path);
     });
 }
@@ -505,6 +610,7 @@ void gs_plan_free(gs_plan_t *p) {
     if (!p) return;
     try {
         gs::free_device(p->st);
+        for (auto &kv : p->subs) gs::free_device(*kv.second);
     } catch (...) {
     }
     delete p;

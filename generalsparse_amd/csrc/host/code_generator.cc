@@ -49,7 +49,7 @@ std::string kernel_spec::name() const {
 
 code_generator::code_generator(std::shared_ptr<meta_data_set> m, int sub_matrix_id) : meta(std::move(m)), sub(sub_matrix_id) {
     GS_CHECK(meta != nullptr, "code_generator needs a metadata set");
-    GS_CHECK(sub_matrix_id == 0, "one sub-matrix per code generator in this build (sub-matrix splits: SURVEY §8f rank 3)");
+    GS_CHECK(sub_matrix_id >= 0, "sub_matrix_id >= 0");
 }
 
 void code_generator::set_reduction_token(POS_TYPE pos, const reduction_token &tok) {
@@ -171,6 +171,10 @@ void code_generator::compile() {
     }
     for (auto k : {"GLOBAL_META_nz_row_indices_0", "GLOBAL_META_nz_col_indices_0", "GLOBAL_META_nz_vals_0"})
         s.arrays.push_back(k);
+    // the keys above are written for sub-matrix 0; a divided matrix's sub-matrices carry their id
+    if (sub != 0)
+        for (auto &k : s.arrays)
+            if (k.size() > 2 && k.compare(k.size() - 2, 2, "_0") == 0) k = k.substr(0, k.size() - 2) + "_" + std::to_string(sub);
     for (auto &k : s.arrays) GS_CHECK(m.is_exist(k), "compile: plan array missing: " + k);
     if (grid.size() == 2) s.ref_grid = {{grid[0], grid[1]}};
     if (block.size() == 2) s.ref_block = {{block[0], block[1]}};
@@ -181,6 +185,7 @@ void code_generator::compile() {
 // ------------------------------------------------------------------ emission
 std::string code_generator::generate_kernel_file_source(int repeat) const {
     GS_CHECK(compiled, "compile() before emitting the program");
+    GS_CHECK(sub == 0, "the standalone program is emitted for an undivided matrix");
     const bool half = get_config().HALF;
     // model-driven index compression (code_generator.cc:2618-3063): with
     // MODEL_DRIVEN_COMPRESS, integer plan arrays whose formula reproduces them exactly are

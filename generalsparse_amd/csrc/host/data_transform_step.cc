@@ -2,6 +2,8 @@
 // Each function cites the reference file it reproduces.
 #include "data_transform_step.hpp"
 
+#include <map>
+
 #include <algorithm>
 #include <numeric>
 
@@ -1007,6 +1009,105 @@ void get_begin_nzs_of_BMW_after_fixed_blocking_in_row_direction_relative_to_BMTB
     replace_u(WARP_META, "first_nz_indices_relative_to_BMTB", std::move(out));
     src(TBLOCK_META, "first_row_indices");
     src(GLOBAL_META, "nz_row_indices");
+    is_run = true;
+}
+
+// ------------------------------------------------ row division (§8f rank 3)
+// modify_row_start_boundary_after_fixed_div_in_row_direction.cc:31-75 (and the other six):
+// bins of fixed_row_gap_size rows over [begin_row_index, end_row_index]; a bin is
+// non-empty when a nonzero's (relative) row falls in it; each transform appends one new
+// sub-matrix per non-empty bin, its id = (max existing id of that item) + 1
+static std::vector<uint64_t> row_div_bins(const meta_data_set &m, int s, uint64_t gap) {
+    GS_CHECK(gap > 0, "fixed_row_gap_size > 0");
+    const uint64_t b = m.scalar(GLOBAL_META, "begin_row_index", s), e = m.scalar(GLOBAL_META, "end_row_index", s);
+    const uint64_t row_num = e - b + 1;
+    const uint64_t nbin = (row_num + gap - 1) / gap;
+    std::vector<uint8_t> used(nbin, 0);
+    for (uint64_t r : m.u(GLOBAL_META, "nz_row_indices", s)) {
+        GS_CHECK(r / gap < nbin, "row division: a nonzero lies past end_row_index");
+        used[r / gap] = 1;
+    }
+    std::vector<uint64_t> bins;
+    for (uint64_t i = 0; i < nbin; i++)
+        if (used[i]) bins.push_back(i);
+    return bins;
+}
+
+static void add_scalar_next(meta_data_set &m, POS_TYPE pos, const char *name, uint64_t v) {
+    m.add_scalar(pos, name, m.get_max_sub_matrix_id_of_data_item(pos, name) + 1, v);
+}
+
+void modify_row_start_boundary_after_fixed_div_in_row_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const uint64_t b = m.scalar(GLOBAL_META, "begin_row_index", target_matrix_id);
+    for (uint64_t i : row_div_bins(m, target_matrix_id, fixed_row_gap_size))
+        add_scalar_next(m, GLOBAL_META, "begin_row_index", b + i * fixed_row_gap_size);
+    is_run = true;
+}
+
+void modify_row_end_boundary_after_fixed_div_in_row_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const uint64_t b = m.scalar(GLOBAL_META, "begin_row_index", target_matrix_id);
+    const uint64_t e = m.scalar(GLOBAL_META, "end_row_index", target_matrix_id);
+    for (uint64_t i : row_div_bins(m, target_matrix_id, fixed_row_gap_size))
+        add_scalar_next(m, GLOBAL_META, "end_row_index", std::min(b + (i + 1) * fixed_row_gap_size - 1, e));
+    is_run = true;
+}
+
+void modify_col_start_boundary_after_fixed_div_in_row_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const uint64_t c = m.scalar(GLOBAL_META, "begin_col_index", target_matrix_id);
+    for (size_t n = row_div_bins(m, target_matrix_id, fixed_row_gap_size).size(); n; n--)
+        add_scalar_next(m, GLOBAL_META, "begin_col_index", c);
+    is_run = true;
+}
+
+void modify_col_end_boundary_after_fixed_div_in_row_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const uint64_t c = m.scalar(GLOBAL_META, "end_col_index", target_matrix_id);
+    for (size_t n = row_div_bins(m, target_matrix_id, fixed_row_gap_size).size(); n; n--)
+        add_scalar_next(m, GLOBAL_META, "end_col_index", c);
+    is_run = true;
+}
+
+// fixed_div_col_indices_by_corr_row_indices.cc: the cols of each bin in their order, the
+// parent's array removed
+void fixed_div_col_indices_by_corr_row_indices::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    const auto &col = m.u(GLOBAL_META, "nz_col_indices", target_matrix_id);
+    std::map<uint64_t, std::vector<uint64_t>> per;
+    for (size_t e = 0; e < row.size(); e++) per[row[e] / fixed_row_gap_size].push_back(col[e]);
+    for (auto &kv : per)
+        m.add_element(GLOBAL_META, "nz_col_indices", m.get_max_sub_matrix_id_of_data_item(GLOBAL_META, "nz_col_indices") + 1,
+                      std::make_shared<universal_array>(std::move(kv.second)));
+    m.remove_element(GLOBAL_META, "nz_col_indices", target_matrix_id);
+    is_run = true;
+}
+
+void fixed_div_vals_by_corr_row_indices::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    auto varr = m.get_element(GLOBAL_META, "nz_vals", target_matrix_id)->meta_data_arr;
+    std::map<uint64_t, std::vector<double>> per;
+    for (size_t e = 0; e < row.size(); e++) per[row[e] / fixed_row_gap_size].push_back(varr->read_float_from_arr(e));
+    for (auto &kv : per)
+        m.add_element(GLOBAL_META, "nz_vals", m.get_max_sub_matrix_id_of_data_item(GLOBAL_META, "nz_vals") + 1,
+                      std::make_shared<universal_array>(std::move(kv.second), varr->get_data_type()));
+    m.remove_element(GLOBAL_META, "nz_vals", target_matrix_id);
+    is_run = true;
+}
+
+// fixed_div_row_indices.cc:12-45: rows relative to the bin (row % gap)
+void fixed_div_row_indices::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    std::map<uint64_t, std::vector<uint64_t>> per;
+    for (uint64_t r : row) per[r / fixed_row_gap_size].push_back(r % fixed_row_gap_size);
+    for (auto &kv : per)
+        m.add_element(GLOBAL_META, "nz_row_indices", m.get_max_sub_matrix_id_of_data_item(GLOBAL_META, "nz_row_indices") + 1,
+                      std::make_shared<universal_array>(std::move(kv.second)));
+    m.remove_element(GLOBAL_META, "nz_row_indices", target_matrix_id);
     is_run = true;
 }
 

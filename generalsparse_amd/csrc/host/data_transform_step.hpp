@@ -198,6 +198,16 @@ GS_DECLARE_MERGE_PATH(get_begin_nzs_of_level_after_merge_path)
 void merge_path_levels(const std::vector<uint64_t> &nnz_of_each_row, uint64_t work_size,
                        std::vector<uint64_t> *level_rows, std::vector<uint64_t> *level_nzs);
 
+// row division into sub-matrices (§8f rank 3; fixed_interval_row_matrix_div_operator.cc:85-150):
+// every non-empty interval of fixed_row_gap_size rows becomes a new sub-matrix (ids max + 1, ...)
+GS_DECLARE_STEP_P(modify_row_start_boundary_after_fixed_div_in_row_direction, uint64_t, fixed_row_gap_size)
+GS_DECLARE_STEP_P(modify_row_end_boundary_after_fixed_div_in_row_direction, uint64_t, fixed_row_gap_size)
+GS_DECLARE_STEP_P(modify_col_start_boundary_after_fixed_div_in_row_direction, uint64_t, fixed_row_gap_size)
+GS_DECLARE_STEP_P(modify_col_end_boundary_after_fixed_div_in_row_direction, uint64_t, fixed_row_gap_size)
+GS_DECLARE_STEP_P(fixed_div_col_indices_by_corr_row_indices, uint64_t, fixed_row_gap_size)
+GS_DECLARE_STEP_P(fixed_div_vals_by_corr_row_indices, uint64_t, fixed_row_gap_size)
+GS_DECLARE_STEP_P(fixed_div_row_indices, uint64_t, fixed_row_gap_size)
+
 // interleaved storage (§8f rank 2; modify_{col,val,row}_indices_by_interlance_storage.cc):
 // inside every parent block the i-th nonzero of BMT b moves to b + i * (BMTs in the parent)
 #define GS_DECLARE_INTERLANCE(cls)                                                                \

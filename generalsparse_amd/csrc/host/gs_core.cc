@@ -263,6 +263,13 @@ std::vector<std::string> meta_data_set::all_item_of_metadata_of_diff_pos(POS_TYP
     return r;
 }
 
+int meta_data_set::get_max_sub_matrix_id_of_data_item(POS_TYPE pos, const std::string &name) const {
+    int mx = -1;
+    for (auto &kv : data_map)
+        if (kv.second->meta_position == pos && kv.second->name == name) mx = std::max(mx, kv.second->sub_matrix_id);
+    return mx;
+}
+
 std::vector<std::string> meta_data_set::keys() const {
     std::vector<std::string> r;
     for (auto &kv : data_map) r.push_back(kv.first);

@@ -145,6 +145,8 @@ class meta_data_set {
     int count_of_metadata_of_diff_pos(POS_TYPE pos, int sub) const;
     std::vector<std::string> all_item_of_metadata_of_diff_pos(POS_TYPE pos, int sub) const;
     std::vector<std::string> keys() const;
+    // metadata_set.cc get_max_sub_matrix_id_of_data_item: -1 when absent
+    int get_max_sub_matrix_id_of_data_item(POS_TYPE pos, const std::string &name) const;
     bool check() const { return true; }
     // metadata_set.cc:517-571 (no sleep(); id from a counter + time)
     uint64_t output_format_to_dir(const std::string &root, const std::vector<std::string> &keys,

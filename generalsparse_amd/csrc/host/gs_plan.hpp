@@ -27,7 +27,8 @@ struct device_plan {
     int col_bytes = 2;     // 2 (u16) or 4 (u32)
     int scf = 4;           // sparse entries per vector load
     bool needs_memset = false;
-    uint64_t n_out_rows = 0;  // rows of C
+    uint64_t n_out_rows = 0;  // one past the last row of C this plan writes
+    uint64_t out_lo = 0;      // first row of C this plan writes (a sub-matrix's range)
     uint64_t n_units = 0;     // BMTs / BMWs / BMTBs the grid walks
     uint64_t n_rows_aux = 0;  // rows covered (thread_total: rows incl. trailing empty)
     uint64_t row_base = 0;
@@ -66,6 +67,8 @@ void load_plan(plan_state &p, const std::string &path);
 void upload_plan(plan_state &p, int dtype, int device);
 void add_replica(plan_state &p);
 void free_device(plan_state &p);
+// zero rows [lo, hi) of a row-major C of width N, element size e (sub-matrix executor)
+void memset_rows(void *C, uint64_t lo, uint64_t hi, uint32_t N, size_t e, hipStream_t stream);
 void launch_spmm(const plan_state &p, int replica, const void *B, void *C, uint32_t N, hipStream_t stream);
 void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
                          size_t n_host);

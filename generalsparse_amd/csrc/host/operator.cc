@@ -128,6 +128,71 @@ void fixed_interval_row_direction_tblock_blocking_operator::run(bool check) {
     is_run = true;
 }
 
+// ------------------------------------------- row matrix division (§8f rank 3)
+fixed_interval_row_matrix_div_operator::fixed_interval_row_matrix_div_operator(cg_ptr cg, int size, ctx_ptr)
+    : basic_operator("fixed_interval_row_matrix_div_operator", cg->get_metadata_set(), CONVERTING_OP,
+                     cg->get_sub_matrix_id()),
+      fixed_row_interval_size(size) {
+    GS_CHECK(size > 0, "fixed_row_interval_size > 0");
+}
+
+// fixed_interval_row_matrix_div_operator.cc:30-60: invalid only when the target was
+// divided before AND nothing was distributed / implemented on it (the reference's flag is
+// only raised inside that branch)
+bool fixed_interval_row_matrix_div_operator::is_valid_according_to_operator(ctx_ptr h) {
+    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return true;
+    if (!h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id).empty()) return true;
+    for (auto &o : h->read_operator_context_arr(CONVERTING_OP, target_matrix_id))
+        if (o->get_name().find("div_operator") != std::string::npos && o->get_target_matrix_id() == target_matrix_id)
+            return false;
+    return true;
+}
+
+// :61-150: boundaries + COO present, no interleaved storage, more rows than the interval
+// and at most MAX_DIV_TIMES_OF_DIV non-empty intervals
+bool fixed_interval_row_matrix_div_operator::is_valid_according_to_metadata() {
+    auto &m = *meta_data_set_ptr;
+    const int s = target_matrix_id;
+    for (const char *n : {"begin_row_index", "end_row_index", "begin_col_index", "end_col_index"})
+        if (!m.is_exist(GLOBAL_META, n, s)) return false;
+    if (!coo_present(m, s) || interlance_storage_existing(m, s)) return false;
+    const uint64_t row_num = m.scalar(GLOBAL_META, "end_row_index", s) - m.scalar(GLOBAL_META, "begin_row_index", s) + 1;
+    const uint64_t g = (uint64_t)fixed_row_interval_size, nbin = (row_num + g - 1) / g;
+    std::vector<uint8_t> used(nbin, 0);
+    int64_t non_empty = 0;
+    for (uint64_t r : m.u(GLOBAL_META, "nz_row_indices", s)) {
+        if (r / g >= nbin) return false;
+        if (!used[r / g]) non_empty++;
+        used[r / g] = 1;
+    }
+    return row_num > g && non_empty <= get_config().MAX_DIV_TIMES_OF_DIV;
+}
+
+// :85-150: boundaries, then cols / vals (which read the parent's rows), then rows
+void fixed_interval_row_matrix_div_operator::run(bool check) {
+    if (check) GS_CHECK(is_valid_according_to_metadata(), "row matrix division: invalid metadata");
+    auto &m = *meta_data_set_ptr;
+    const int first = m.get_max_sub_matrix_id_of_data_item(GLOBAL_META, "nz_row_indices") + 1;
+    const uint64_t g = (uint64_t)fixed_row_interval_size;
+    modify_row_start_boundary_after_fixed_div_in_row_direction a(meta_data_set_ptr, target_matrix_id, g);
+    run_step(a, check);
+    modify_row_end_boundary_after_fixed_div_in_row_direction b(meta_data_set_ptr, target_matrix_id, g);
+    run_step(b, check);
+    modify_col_start_boundary_after_fixed_div_in_row_direction c(meta_data_set_ptr, target_matrix_id, g);
+    run_step(c, check);
+    modify_col_end_boundary_after_fixed_div_in_row_direction d(meta_data_set_ptr, target_matrix_id, g);
+    run_step(d, check);
+    fixed_div_col_indices_by_corr_row_indices e(meta_data_set_ptr, target_matrix_id, g);
+    run_step(e, check);
+    fixed_div_vals_by_corr_row_indices f(meta_data_set_ptr, target_matrix_id, g);
+    run_step(f, check);
+    fixed_div_row_indices h(meta_data_set_ptr, target_matrix_id, g);
+    run_step(h, check);
+    const int last = m.get_max_sub_matrix_id_of_data_item(GLOBAL_META, "nz_row_indices");
+    for (int k = first; k <= last; k++) new_sub_matrix_ids.push_back(k);
+    is_run = true;
+}
+
 // --------------------------------------------- row-direction WARP blocking
 fixed_interval_row_direction_warp_blocking_operator::fixed_interval_row_direction_warp_blocking_operator(
     cg_ptr cg, int rb, bool rrel, bool nrel, bool pad, ctx_ptr)
@@ -981,6 +1046,10 @@ std::shared_ptr<basic_operator> make_operator(const std::string &name, const std
         need(3);
         return std::make_shared<balanced_interval_row_direction_thread_blocking_operator>(cg, (int)a[0], a[1] != 0,
                                                                                           a[2] != 0, ctx);
+    }
+    if (name == "fixed_interval_row_matrix_div_operator") {
+        need(1);
+        return std::make_shared<fixed_interval_row_matrix_div_operator>(cg, (int)a[0], ctx);
     }
     if (name == "interlance_storage_operator") { need(0); return std::make_shared<interlance_storage_operator>(cg, ctx); }
     if (name == "merge_path_tblock_operator") { need(1); return std::make_shared<merge_path_tblock_operator>(cg, (int)a[0], ctx); }

@@ -72,6 +72,21 @@ class sort_operator : public basic_operator {  // operator/sort_operator.cc
     bool is_valid_according_to_operator(ctx_ptr h) override;
 };
 
+// operator/fixed_interval_row_matrix_div_operator.cc (§8f rank 3): CONVERTING; splits the
+// sub-matrix into sub-matrices of fixed_row_interval_size rows (non-empty intervals only)
+class fixed_interval_row_matrix_div_operator : public basic_operator {
+  public:
+    fixed_interval_row_matrix_div_operator(cg_ptr cg, int fixed_row_interval_size, ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    std::string convert_to_string() const override {
+        return basic_operator::convert_to_string() + ",fixed_row_interval_size:" + std::to_string(fixed_row_interval_size);
+    }
+    int fixed_row_interval_size;
+    std::vector<int> new_sub_matrix_ids;  // filled by run()
+};
+
 // -------------------------------------------------------------- DISTRIBUTING
 class fixed_interval_row_direction_tblock_blocking_operator : public basic_operator {
   public:

@@ -408,17 +408,23 @@ void upload_plan(plan_state &p, int dtype, int device) {
     HIP_OK(hipSetDevice(device));
     const kernel_spec &sp = p.cg->get_kernel_spec();
     const meta_data_set &m = *p.meta;
+    const int sb = p.cg->get_sub_matrix_id();
     device_plan &d = p.dev;
     d = device_plan();
     d.device = device;
     d.dtype = dtype;
-    d.n_out_rows = p.M;
-    d.row_base = m.scalar(GLOBAL_META, "begin_row_index", 0);
-    const auto &rows = m.u(GLOBAL_META, "nz_row_indices", 0);
+    d.row_base = m.scalar(GLOBAL_META, "begin_row_index", sb);
+    // output rows this plan writes: all of C for the undivided matrix; a sub-matrix of a
+    // row division (§8f rank 3) owns [begin_row_index, begin_row_index + its rows) only
+    const uint64_t out_lo = sb == 0 ? 0 : d.row_base;
+    const uint64_t out_hi = sb == 0 ? p.M : d.row_base + row_num_of_sub_matrix(m, sb);
+    d.n_out_rows = out_hi;
+    d.out_lo = out_lo;
+    const auto &rows = m.u(GLOBAL_META, "nz_row_indices", sb);
     // interleaved storage (§8f rank 2): the kernel streams the permuted arrays
-    const auto &col = m.u(GLOBAL_META, sp.interleaved ? "nz_col_indices_after_interlance_storage" : "nz_col_indices", 0);
-    auto vals = m.get_element(GLOBAL_META, sp.interleaved ? "nz_vals_after_interlance_storage" : "nz_vals", 0)->meta_data_arr;
-    if (sp.interleaved) d.ilv = (uint32_t)m.u(GLOBAL_META, "BMT_size_of_each_blk", 0).at(0);
+    const auto &col = m.u(GLOBAL_META, sp.interleaved ? "nz_col_indices_after_interlance_storage" : "nz_col_indices", sb);
+    auto vals = m.get_element(GLOBAL_META, sp.interleaved ? "nz_vals_after_interlance_storage" : "nz_vals", sb)->meta_data_arr;
+    if (sp.interleaved) d.ilv = (uint32_t)m.u(GLOBAL_META, "BMT_size_of_each_blk", sb).at(0);
     uint64_t nnz = col.size();
     GS_CHECK(nnz < 0xffffffffull - kPad, "nnz exceeds 32-bit offsets");
     d.nnz_stored = nnz;
@@ -430,11 +436,11 @@ void upload_plan(plan_state &p, int dtype, int device) {
         std::vector<unsigned char> blk;
         uint32_t S = 0;
         std::string why;
-        if (build_nm_panels(rows, col, *vals, row_num_of_sub_matrix(m, 0), p.K, blk, S, why)) {
+        if (build_nm_panels(rows, col, *vals, row_num_of_sub_matrix(m, sb), p.K, blk, S, why)) {
             d.nm = true;
             d.KC = S;
-            d.n_rows_aux = row_num_of_sub_matrix(m, 0);
-            d.n_units = m.u(THREAD_META, "first_nz_indices", 0).size() - 1;
+            d.n_rows_aux = row_num_of_sub_matrix(m, sb);
+            d.n_units = m.u(THREAD_META, "first_nz_indices", sb).size() - 1;
             d.waves = gsk::kNmWaves;
             a.tcol = dev_copy(d, blk);
             d.bytes_tile = d.bytes_A;
@@ -462,16 +468,16 @@ void upload_plan(plan_state &p, int dtype, int device) {
         for (uint64_t i = 0; i < nnz; i++) v[i] = f32_to_f16_bits((float)vals->read_float_from_arr(i));
         a.val = dev_copy(d, v, kPad);
     }
-    uint64_t row_num = row_num_of_sub_matrix(m, 0);
+    uint64_t row_num = row_num_of_sub_matrix(m, sb);
     // matrix-core row blocks for fp16 plans with BMTBs (tried before the other kernels)
     auto try_mfma = [&](const std::vector<uint32_t> &rp) {
         const config_t cfg = get_config();
-        if (dtype != 1 || !cfg.MFMA_TILES || !m.is_exist(TBLOCK_META, "first_row_indices", 0)) return false;
+        if (dtype != 1 || !cfg.MFMA_TILES || !m.is_exist(TBLOCK_META, "first_row_indices", sb)) return false;
         mfma_tiles t;
         std::string why;
         const uint32_t Nd = (uint32_t)cfg.DENSE_MATRIX_SIZE;
         const size_t budget = (size_t)std::min<int64_t>(cfg.SHARED_MEM_TOTAL_SIZE, 160 * 1024);
-        if (!build_mfma_tiles(m.u(TBLOCK_META, "first_row_indices", 0), rp, col, *vals, p.K, Nd, budget,
+        if (!build_mfma_tiles(m.u(TBLOCK_META, "first_row_indices", sb), rp, col, *vals, p.K, Nd, budget,
                               cfg.MFMA_MAX_FILL, t, why))
             return false;
         d.mfma = true;
@@ -479,7 +485,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
         d.KC = 1u << t.lgKC; d.nc = t.nc; d.maxr = t.RT; d.rpw_max = t.RMAX; d.RSB = t.lgKC;
         d.seg_cap = t.MAXA;
         // K-split: enough workgroups per row block to cover the CUs, at least one chunk each
-        const uint64_t nb = m.u(TBLOCK_META, "first_row_indices", 0).size() - 1;
+        const uint64_t nb = m.u(TBLOCK_META, "first_row_indices", sb).size() - 1;
         // auto: split only when the row blocks cover under half the CUs (the slab
         // combine's cross-XCD release/acquire costs ~micro-seconds at the tail)
         uint32_t ks = cfg.MFMA_KSPLIT > 0 ? (uint32_t)cfg.MFMA_KSPLIT
@@ -494,18 +500,18 @@ void upload_plan(plan_state &p, int dtype, int device) {
         }
         d.waves = kMfmaThreads / 64; d.lds_bytes = t.lds_bytes;
         const size_t before = d.bytes_A;
-        a.t0 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_row_indices", 0), "BMTB first_row_indices"));
+        a.t0 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_row_indices", sb), "BMTB first_row_indices"));
         a.t1 = dev_copy(d, t.seg_start);
         a.tcol = dev_copy(d, t.pos);
         a.tval = dev_copy(d, t.val);
         d.bytes_tile = d.bytes_A - before;
-        d.n_rows_aux = m.u(TBLOCK_META, "first_row_indices", 0).size() - 1;
+        d.n_rows_aux = m.u(TBLOCK_META, "first_row_indices", sb).size() - 1;
         return true;
     };
     switch (sp.family) {
         case KF_THREAD_TOTAL: {
-            const auto &fn = m.u(THREAD_META, "first_nz_indices", 0);
-            const auto &fr = m.u(THREAD_META, "first_row_indices", 0);
+            const auto &fn = m.u(THREAD_META, "first_nz_indices", sb);
+            const auto &fr = m.u(THREAD_META, "first_row_indices", sb);
             for (size_t i = 0; i < fr.size(); i++)
                 GS_CHECK(fr[i] == i, "thread_total kernel needs one row per BMT (fixed_row_block_size 1)");
             bool al4 = true, al8 = true;
@@ -513,8 +519,8 @@ void upload_plan(plan_state &p, int dtype, int device) {
             d.scf = al8 ? 8 : (al4 ? 4 : 1);
             a.a0 = dev_copy(d, to_u32(fn, "first_nz_indices"));
             std::vector<uint64_t> order;
-            if (m.is_exist(GLOBAL_META, "original_nz_row_indices", 0)) {
-                order = m.u(GLOBAL_META, "original_nz_row_indices", 0);
+            if (m.is_exist(GLOBAL_META, "original_nz_row_indices", sb)) {
+                order = m.u(GLOBAL_META, "original_nz_row_indices", sb);
             } else {
                 order.resize(row_num);
                 for (uint64_t i = 0; i < row_num; i++) order[i] = i;
@@ -525,22 +531,22 @@ void upload_plan(plan_state &p, int dtype, int device) {
             break;
         }
         case KF_WARP_TOTAL: {
-            a.a0 = dev_copy(d, to_u32(m.u(sp.group_level, "first_row_indices", 0), "BMW first_row_indices"));
+            a.a0 = dev_copy(d, to_u32(m.u(sp.group_level, "first_row_indices", sb), "BMW first_row_indices"));
             if (sp.tblock_parent) {
-                a.a1 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_BMW_indices", 0), "first_BMW_indices"));
-                d.n_rows_aux = m.u(TBLOCK_META, "first_BMW_indices", 0).size() - 1;  // BMTB count
+                a.a1 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_BMW_indices", sb), "first_BMW_indices"));
+                d.n_rows_aux = m.u(TBLOCK_META, "first_BMW_indices", sb).size() - 1;  // BMTB count
             }
             std::vector<uint32_t> rp = csr_row_ptr(rows, row_num);
             a.a2 = dev_copy(d, rp);
-            d.n_units = m.u(sp.group_level, "first_row_indices", 0).size() - 1;
+            d.n_units = m.u(sp.group_level, "first_row_indices", sb).size() - 1;
             d.scf = 4;
             if (sp.tblock_parent && try_mfma(rp)) break;
             // LDS-stationary B pays off for row blocks of >= 16 rows in BMWs of >= 2 rows
             // (C2: 20x2 31 us vs 40 us gathered; 4x1 62 us): otherwise the gather kernel
             bool lds_worth = false;
             if (sp.tblock_parent) {
-                const auto &tr = m.u(TBLOCK_META, "first_row_indices", 0);
-                const auto &wr = m.u(WARP_META, "first_row_indices", 0);
+                const auto &tr = m.u(TBLOCK_META, "first_row_indices", sb);
+                const auto &wr = m.u(WARP_META, "first_row_indices", sb);
                 uint64_t mt = 0, mw = 0;
                 for (size_t i = 0; i + 1 < tr.size(); i++) mt = std::max<uint64_t>(mt, tr[i + 1] - tr[i]);
                 for (size_t i = 0; i + 1 < wr.size(); i++) mw = std::max<uint64_t>(mw, wr[i + 1] - wr[i]);
@@ -551,15 +557,15 @@ void upload_plan(plan_state &p, int dtype, int device) {
                 std::string why;
                 const uint32_t Nd = (uint32_t)get_config().DENSE_MATRIX_SIZE;
                 const size_t budget = (size_t)std::min<int64_t>(get_config().SHARED_MEM_TOTAL_SIZE, 160 * 1024);
-                if (build_lds_tiles(m.u(TBLOCK_META, "first_row_indices", 0), m.u(TBLOCK_META, "first_BMW_indices", 0),
-                                    m.u(WARP_META, "first_row_indices", 0), rp, col, p.K, Nd, dtype ? 2u : 4u, budget,
+                if (build_lds_tiles(m.u(TBLOCK_META, "first_row_indices", sb), m.u(TBLOCK_META, "first_BMW_indices", sb),
+                                    m.u(WARP_META, "first_row_indices", sb), rp, col, p.K, Nd, dtype ? 2u : 4u, budget,
                                     t, why)) {
                     d.lds = true;
                     d.lds_N = Nd;
                     d.KC = t.KC; d.nc = t.nc; d.RSB = t.RSB; d.rpw_max = t.rpw_max; d.seg_cap = t.seg_cap;
                     d.waves = t.waves; d.maxr = t.maxr; d.lds_bytes = t.lds_bytes;
                     const size_t before = d.bytes_A;
-                    a.t0 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_row_indices", 0), "BMTB first_row_indices"));
+                    a.t0 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_row_indices", sb), "BMTB first_row_indices"));
                     a.t1 = dev_copy(d, t.seg_start);
                     a.t2 = dev_copy(d, t.seg_row_off);
                     a.tcol = dev_copy(d, t.tcol, kPad);
@@ -580,16 +586,16 @@ void upload_plan(plan_state &p, int dtype, int device) {
             break;
         }
         case KF_BLOCK_TOTAL: {
-            a.a0 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_row_indices", 0), "BMTB first_row_indices"));
+            a.a0 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_row_indices", sb), "BMTB first_row_indices"));
             std::vector<uint32_t> rp = csr_row_ptr(rows, row_num);
             a.a2 = dev_copy(d, rp);
-            d.n_units = m.u(TBLOCK_META, "first_row_indices", 0).size() - 1;
+            d.n_units = m.u(TBLOCK_META, "first_row_indices", sb).size() - 1;
             d.scf = 4;
             try_mfma(rp);
             break;
         }
         case KF_BITMAP_SEGMENT: {
-            const auto &fn = m.u(THREAD_META, "first_nz_indices", 0);
+            const auto &fn = m.u(THREAD_META, "first_nz_indices", sb);
             uint64_t nb = fn.size() - 1;
             for (uint64_t i = 0; i < nb; i++) {
                 GS_CHECK(fn[i + 1] - fn[i] <= 64, "bitmap kernel needs BMTs of at most 64 nnz");
@@ -604,10 +610,10 @@ void upload_plan(plan_state &p, int dtype, int device) {
                 mask[i] = mm;
             }
             a.a0 = dev_copy(d, to_u32(fn, "first_nz_indices"));
-            a.a1 = dev_copy(d, to_u32(m.u(THREAD_META, "first_row_indices", 0), "first_row_indices"));
+            a.a1 = dev_copy(d, to_u32(m.u(THREAD_META, "first_row_indices", sb), "first_row_indices"));
             a.m0 = dev_copy(d, mask);
-            a.a2 = dev_copy(d, to_u32(m.u(THREAD_META, "segment_ptr", 0), "segment_ptr"));
-            a.a3 = dev_copy(d, to_u32(m.u(THREAD_META, "segment_empty_row_indices", 0), "segment_empty_row_indices"));
+            a.a2 = dev_copy(d, to_u32(m.u(THREAD_META, "segment_ptr", sb), "segment_ptr"));
+            a.a3 = dev_copy(d, to_u32(m.u(THREAD_META, "segment_empty_row_indices", sb), "segment_empty_row_indices"));
             d.n_units = nb;
             d.scf = 4;
             if (dtype == 1) {
@@ -616,7 +622,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
                 const uint64_t rb = d.row_base;
                 std::vector<uint32_t> rp = csr_row_ptr(rows, row_num);
                 std::vector<uint8_t> fin(p.M, 0);
-                for (uint64_t r = 0; r < p.M; r++)
+                for (uint64_t r = out_lo; r < out_hi; r++)
                     if (r < rb || r - rb >= row_num || rp[r - rb] == rp[r - rb + 1]) fin[r] = 1;
                 for (uint64_t i = 1; i + 1 < fn.size(); i++) {  // a BMT boundary strictly inside a row
                     const uint64_t z = fn[i];
@@ -636,8 +642,8 @@ void upload_plan(plan_state &p, int dtype, int device) {
             break;
         }
         case KF_ROW_CHUNKS: {
-            const auto &fn = m.u(THREAD_META, "first_nz_indices", 0);
-            const auto &fr = m.u(THREAD_META, "first_row_indices_without_ending", 0);
+            const auto &fn = m.u(THREAD_META, "first_nz_indices", sb);
+            const auto &fr = m.u(THREAD_META, "first_row_indices_without_ending", sb);
             GS_CHECK(fn.size() == fr.size() + 1 && !fr.empty(), "col-direction plan: BMT arrays disagree");
             std::vector<uint32_t> br = to_u32(fr, "first_row_indices_without_ending");
             a.a0 = dev_copy(d, to_u32(fn, "first_nz_indices"));
@@ -648,6 +654,8 @@ void upload_plan(plan_state &p, int dtype, int device) {
             // rows shared by two waves' BMT ranges accumulate in an fp32 workspace; the
             // finalize pass rounds them and writes the rows without BMTs (no memset)
             std::vector<uint32_t> list = gsk_host::row_chunk_finalize_rows(br, p.M, d.span, (uint32_t)d.row_base);
+            list.erase(std::remove_if(list.begin(), list.end(), [&](uint32_t r) { return r < out_lo || r >= out_hi; }),
+                       list.end());
             d.ws_n = (uint32_t)std::max<int64_t>(1, get_config().DENSE_MATRIX_SIZE);
             a.ws = dev_copy(d, std::vector<float>((size_t)p.M * d.ws_n, 0.f));
             if (!list.empty()) a.a4 = dev_copy(d, list);
@@ -663,8 +671,8 @@ void upload_plan(plan_state &p, int dtype, int device) {
             const uint64_t target = (uint64_t)gsk::kMpItems * (64u / X);  // >= one round per wave
             gsk_host::merge_path_layout lay;
             std::string why;
-            GS_CHECK(gsk_host::merge_path_device_layout(rows, row_num, m.u(L, "first_row_indices_without_ending", 0),
-                                                         m.u(L, "first_nz_indices", 0), (uint64_t)sp.work_size,
+            GS_CHECK(gsk_host::merge_path_device_layout(rows, row_num, m.u(L, "first_row_indices_without_ending", sb),
+                                                         m.u(L, "first_nz_indices", sb), (uint64_t)sp.work_size,
                                                          (uint32_t)d.row_base, target, lay, why, d.n_out_rows),
                      "merge-path layout: " + why);
             a.a0 = dev_copy(d, lay.wz);
@@ -725,6 +733,10 @@ void add_replica(plan_state &p) {
     r.ws = (float *)dup(s.ws);
     r.ws2 = (float *)dup(s.ws2);
     p.dev.replicas.push_back(r);
+}
+
+void memset_rows(void *C, uint64_t lo, uint64_t hi, uint32_t N, size_t e, hipStream_t stream) {
+    HIP_OK(hipMemsetAsync((char *)C + lo * N * e, 0, (hi - lo) * N * e, stream));
 }
 
 void free_device(plan_state &p) {
@@ -951,7 +963,8 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
             size_t lds = (size_t)4 * S * 2 * X * CF * sizeof(float);
             // the fp32 workspace is sized for the plan's dense width; other widths use fp16 atomics
             const bool use_ws = a.ws && N == d.ws_n;
-            if (!use_ws) HIP_OK(hipMemsetAsync(C, 0, (size_t)d.n_out_rows * N * sizeof(VT), s));
+            if (!use_ws)
+                HIP_OK(hipMemsetAsync(C + (size_t)d.out_lo * N, 0, (size_t)(d.n_out_rows - d.out_lo) * N * sizeof(VT), s));
             hipLaunchKernelGGL((gsk::k_bitmap_segment<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256),
                                lds, s, a.a0, a.a1, a.m0, a.a2, a.a3, col, val, B, C, (uint32_t)d.n_units, N, X,
                                row_base, use_ws ? a.ws : (float *)nullptr);

@@ -61,6 +61,7 @@ typedef struct {
     uint32_t lds_n, lds_kc, lds_chunks, lds_waves;
     uint64_t lds_bytes, tile_bytes;
     uint32_t ksplit;              /* k_mfma_rows workgroups per row block (K ranges, fp32 slab combine) */
+    int n_kernels;                /* kernels gs_spmm runs: 1, or one per sub-matrix of a row division */
 } gs_plan_info;
 
 const char *gs_last_error(void);
@@ -80,6 +81,16 @@ int gs_plan_add_operator(gs_plan_t *p, const char *op_name, const long long *arg
  * thread_bit_map(p0=sparse_cf,p1=cf), warp_segment(p0=sparse_cf,p1=cf),
  * tblock_warp_total(p0=rows per BMTB, p1=rows per BMW), balanced_warp_total(p0=nnz per BMW) */
 int gs_plan_run_pipeline(gs_plan_t *p, const char *name, int dense_n, int p0, int p1);
+/* sub-matrices (§8f rank 3): after fixed_interval_row_matrix_div_operator
+ * (operator/fixed_interval_row_matrix_div_operator.cc:85-150; new sub-matrix ids = max + 1,
+ * one per non-empty row interval) each sub-matrix gets its own operators / pipeline --
+ * the reference's code_generator(meta, sub) per sub-matrix (code_generator.cc:14-40).
+ * Compile / upload / gs_spmm then cover every live sub-matrix, one kernel each, in id
+ * order on the caller's stream (rows of empty intervals are zeroed first). */
+int gs_plan_add_operator_sub(gs_plan_t *p, int sub, const char *op_name, const long long *args, int nargs);
+int gs_plan_run_pipeline_sub(gs_plan_t *p, int sub, const char *name, int dense_n, int p0, int p1);
+/* ids of the sub-matrices holding nonzeros (ascending); returns the count (< 0: error) */
+int gs_plan_sub_matrices(gs_plan_t *p, int *ids, int cap);
 int gs_plan_compile(gs_plan_t *p);
 int gs_plan_generate_program(gs_plan_t *p, const char *root_dir, int repeat, char *dir_out, int dir_out_len);
 

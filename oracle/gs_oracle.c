@@ -68,6 +68,7 @@ static void drop(or_set *s, const char *pos, const char *name, int sub) {
 static or_array *put_u(or_set *s, const char *pos, const char *name, int sub,
                        uint64_t *data, uint64_t len) {
     drop(s, pos, name, sub);
+    if (s->n >= OR_MAX_ARRAYS) abort(); /* the set's fixed capacity */
     or_array *a = &s->a[s->n++];
     memset(a, 0, sizeof(*a));
     mkkey(a->key, pos, name, sub);
@@ -79,6 +80,7 @@ static or_array *put_u(or_set *s, const char *pos, const char *name, int sub,
 static or_array *put_f(or_set *s, const char *pos, const char *name, int sub,
                        double *data, uint64_t len) {
     drop(s, pos, name, sub);
+    if (s->n >= OR_MAX_ARRAYS) abort(); /* the set's fixed capacity */
     or_array *a = &s->a[s->n++];
     memset(a, 0, sizeof(*a));
     mkkey(a->key, pos, name, sub);
@@ -994,7 +996,74 @@ int or_bmw_relative_to_bmtb(or_set *s, int rb) {
 /* canned pipelines: token_test.cc test_spmm_*                          */
 /* ------------------------------------------------------------------ */
 
+/* §8f rank 3: fixed_interval_row_matrix_div_operator on sub-matrix 0
+ * (operator/fixed_interval_row_matrix_div_operator.cc:61-150 validity + run order;
+ * transform_step/modify_{row,col}_{start,end}_boundary_after_fixed_div_in_row_direction.cc,
+ * fixed_div_{col_indices_by_corr_row_indices,vals_by_corr_row_indices,row_indices}.cc).
+ * Interval i = rows [begin + i*gap, begin + (i+1)*gap - 1] (the end clamped to
+ * end_row_index); every non-empty interval becomes sub-matrix (max id + 1), in interval
+ * order, holding its nonzeros in their order with rows reduced modulo gap; sub-matrix
+ * 0's row / col / val arrays are removed (its boundaries stay). */
+int or_fixed_interval_row_div(or_set *s, uint64_t gap) {
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    or_array *C = get(s, "GLOBAL_META", "nz_col_indices", 0);
+    or_array *V = get(s, "GLOBAL_META", "nz_vals", 0);
+    if (!R || !C || !V || gap == 0) return fail(s, "row division needs the COO of sub-matrix 0 and gap > 0");
+    if (exists(s, "GLOBAL_META", "nz_col_indices_after_interlance_storage", 0))
+        return fail(s, "row division after interleaved storage");
+    uint64_t b = scalar(s, "GLOBAL_META", "begin_row_index", 0), e = scalar(s, "GLOBAL_META", "end_row_index", 0);
+    uint64_t bc = scalar(s, "GLOBAL_META", "begin_col_index", 0), ec = scalar(s, "GLOBAL_META", "end_col_index", 0);
+    uint64_t row_num = e - b + 1, nbin = (row_num + gap - 1) / gap;
+    uint64_t *cnt = (uint64_t *)calloc(nbin ? nbin : 1, sizeof(uint64_t));
+    uint64_t non_empty = 0;
+    for (uint64_t i = 0; i < R->len; i++) {
+        if (R->u[i] / gap >= nbin) {
+            free(cnt);
+            return fail(s, "row division: a nonzero past end_row_index");
+        }
+        if (cnt[R->u[i] / gap]++ == 0) non_empty++;
+    }
+    if (!(row_num > gap) || non_empty > 12) { /* MAX_DIV_TIMES_OF_DIV default */
+        free(cnt);
+        return fail(s, "row division invalid: %llu rows, gap %llu, %llu intervals", (unsigned long long)row_num,
+                    (unsigned long long)gap, (unsigned long long)non_empty);
+    }
+    int id = 1; /* sub-matrix 0 is the only one before the division */
+    for (uint64_t bin = 0; bin < nbin; bin++) {
+        if (!cnt[bin]) continue;
+        uint64_t n = cnt[bin], k = 0;
+        uint64_t *nr = (uint64_t *)malloc(n * sizeof(uint64_t)), *nc = (uint64_t *)malloc(n * sizeof(uint64_t));
+        double *nv = (double *)malloc(n * sizeof(double));
+        for (uint64_t i = 0; i < R->len; i++)
+            if (R->u[i] / gap == bin) {
+                nr[k] = R->u[i] % gap;
+                nc[k] = C->u[i];
+                nv[k] = V->f[i];
+                k++;
+            }
+        uint64_t hi = b + (bin + 1) * gap - 1;
+        put_scalar(s, "GLOBAL_META", "begin_row_index", id, b + bin * gap);
+        put_scalar(s, "GLOBAL_META", "end_row_index", id, hi >= e ? e : hi);
+        put_scalar(s, "GLOBAL_META", "begin_col_index", id, bc);
+        put_scalar(s, "GLOBAL_META", "end_col_index", id, ec);
+        put_u(s, "GLOBAL_META", "nz_col_indices", id, nc, n);
+        put_f(s, "GLOBAL_META", "nz_vals", id, nv, n);
+        put_u(s, "GLOBAL_META", "nz_row_indices", id, nr, n);
+        R = get(s, "GLOBAL_META", "nz_row_indices", 0); /* put_* may move entries */
+        C = get(s, "GLOBAL_META", "nz_col_indices", 0);
+        V = get(s, "GLOBAL_META", "nz_vals", 0);
+        id++;
+    }
+    free(cnt);
+    drop(s, "GLOBAL_META", "nz_col_indices", 0);
+    drop(s, "GLOBAL_META", "nz_vals", 0);
+    drop(s, "GLOBAL_META", "nz_row_indices", 0);
+    return 0;
+}
+
 int or_pipeline(or_set *s, const char *name, int p0, int p1) {
+    if (!strcmp(name, "row_div")) /* p0 = fixed_row_interval_size */
+        return or_fixed_interval_row_div(s, (uint64_t)p0);
     if (!strcmp(name, "thread_total")) { /* token_test.cc:1003-1092, p0 = sparse_cf */
         if (or_sort_operator(s)) return -1;
         return or_row_dir_thread_blocking(s, 1, p0);

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OR_MAX_ARRAYS 64
+#define OR_MAX_ARRAYS 128
 #define OR_NAME_LEN 96
 
 /* One named plan array: key = "<POS>_<name>_<sub>" (metadata_set.cc:147-151).
@@ -87,6 +87,7 @@ int or_balanced_row_dir_thread_blocking(or_set *s, uint64_t nnz_per_bmt);  /* A1
 int or_merge_path(or_set *s, const char *pos, uint64_t work_size);         /* A11 */
 int or_interlance_storage_global(or_set *s);                               /* §8f rank 2 */
 int or_bmw_relative_to_bmtb(or_set *s, int rb);                            /* §8f rank 1 */
+int or_fixed_interval_row_div(or_set *s, uint64_t gap);                    /* §8f rank 3 */
 int or_index_compression(const uint64_t *a, uint64_t n, int type_ori, int branch_max, int *kind,
                          uint64_t *params, uint64_t *res);                 /* §8f rank 1 */
 int or_col_dir_thread_blocking(or_set *s, int col_size, int pad);          /* A10 */

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
 LIB = os.path.join(ORACLE_DIR, "liboracle_gs.so")
 
-OR_MAX_ARRAYS = 64
+OR_MAX_ARRAYS = 128
 OR_NAME_LEN = 96
 
 

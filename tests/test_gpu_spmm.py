@@ -458,3 +458,38 @@ def test_autotune_picks_a_timed_variant(tmp_path):
     C = plan.spmm(torch.from_numpy(B).to(DEV))
     torch.cuda.synchronize()
     check(C.float().cpu().numpy(), ofi.spmm_ref(M, 8, r, c, v, B, "f64"), "f32")
+
+
+# §8f rank 3: one kernel per sub-matrix of a row division, run in sequence by gs_spmm
+SUB_MIXES = [
+    ("merge_path", 64, 1, "thread_total", 4, 1),
+    ("tblock_warp_total", 16, 2, "warp_total", 0, 1),
+    ("balanced_warp_total", 256, 1, "block_total", 0, 1),
+    ("thread_bit_map", 4, 1, "warp_segment", 4, 1),
+]
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f16"])
+@pytest.mark.parametrize("N", [8, 32])
+@pytest.mark.parametrize("mix", SUB_MIXES, ids=lambda m: f"{m[0]}+{m[3]}")
+def test_sub_matrix_kernels_match_oracle(mix, N, dtype):
+    M, K = 900, 400
+    r, c, v = ds.random_rows(M, K, 14.0, seed=7, empty_frac=0.1)
+    keep = (r < 300) | (r >= 450)  # interval [300, 450) without nonzeros: zeroed by the executor
+    r, c, v = r[keep], c[keep], v[keep]
+    plan = gsa.Plan.from_coo(M, K, r, c, v)
+    subs = plan.divide_rows(150)
+    assert len(subs) == 5
+    for i, s in enumerate(subs):
+        name, p0, p1 = mix[0:3] if i % 2 == 0 else mix[3:6]
+        plan.run_pipeline(name, N, p0, p1, sub=s)
+    plan.compile().upload(dtype, 0)
+    assert plan.info()["n_kernels"] == 5
+    npdt = np.float16 if dtype == "f16" else np.float32
+    B = np.random.default_rng(8).uniform(-1, 1, (K, N)).astype(npdt)
+    C = torch.full((M, N), float("nan"), dtype=torch.float16 if dtype == "f16" else torch.float32, device=DEV)
+    plan.spmm(torch.from_numpy(B).to(DEV), C=C)
+    torch.cuda.synchronize()
+    Cn = C.float().cpu().numpy()
+    assert not np.isnan(Cn).any()
+    check(Cn, ofi.spmm_ref(M, N, r, c, v, B, "f64"), dtype)
