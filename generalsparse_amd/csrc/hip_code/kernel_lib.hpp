@@ -812,7 +812,7 @@ constexpr int kMfmaWaves = 16, kMfmaCompute = 6, kMfmaBWaves = 4, kMfmaAWaves = 
 
 // STAMPS (diagnostic build only, gs_debug_mfma_timeline): lane 0 of the first
 // compute / B / entry wave records s_memtime at phase boundaries
-template <int CT, int RT, int LGKC, int MAXA, bool STAMPS = false>
+template <int CT, int RT, int LGKC, int MAXA, bool STAMPS = false, bool GLDS = false>
 __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
     const uint32_t *__restrict__ seg_start,       // n_bmtb*nc+1 (groups)
@@ -834,7 +834,11 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     constexpr int MAXS = (int)((KC / 32 + WC - 1) / WC);  // k-steps per compute wave per chunk
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint32_t szD = (RMAX + 1) * RS;
-    const uint32_t oD = 2 * szB;                      // D[0..2] follow B[0..1]
+    // register-staged B: two B buffers + three dense images; GLDS (B by LDS-DMA, two
+    // chunks ahead): three B buffers + two dense images, each compute wave clearing the
+    // k-step columns it read
+    constexpr uint32_t NBUF = GLDS ? 3u : 2u, NDI = GLDS ? 2u : 3u;
+    const uint32_t oD = NBUF * szB;                   // dense images follow the B buffers
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t role = wv < WC ? 0u : (wv < WC + kMfmaBWaves ? 1u : 2u);  // wave-uniform
     const uint32_t bt = tid - 64 * WC;                // B thread index (role 1)
@@ -848,7 +852,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     // GS_SEG takes a local chunk index
     const uint32_t segv = seg_start[g * nc + min(lane, nc)];
 #define GS_SEG(j) __builtin_amdgcn_readlane(segv, j0 + (j))
-    uint64_t *lst = reinterpret_cast<uint64_t *>(lds + oD + 3 * szD);  // STAMPS only
+    uint64_t *lst = reinterpret_cast<uint64_t *>(lds + oD + NDI * szD);  // STAMPS only
     // first lane of each role -> slots [21*role, 21*role + 21): 0 start, 1 chunk 0 staged,
     // 2+2j chunk j's work done, 3+2j after its barrier (j < 9); slot 63 end
 #define GS_STAMP(i)                                                                               \
@@ -858,7 +862,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     }
     GS_STAMP(0u);
 
-    for (uint32_t u = tid; u < 3 * szD / 16u; u += NT) *reinterpret_cast<u32x4 *>(lds + oD + u * 16u) = zero4;
+    for (uint32_t u = tid; u < NDI * szD / 16u; u += NT) *reinterpret_cast<u32x4 *>(lds + oD + u * 16u) = zero4;
 
     if (role == 0) {
         // ---------------------------------------------------------------- compute
@@ -879,8 +883,8 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         for (uint32_t j = 0; j < ncl; j++) {
             const uint32_t kr = min(KC, K - (j0 + j) * KC);
             const uint32_t nsteps = (kr + 31u) / 32u;
-            const unsigned char *la = lds + oD + (j % 3u) * szD;
-            const unsigned char *lb = lds + (j & 1u) * szB;
+            const unsigned char *la = lds + oD + (j % NDI) * szD;
+            const unsigned char *lb = lds + (j % NBUF) * szB;
             // all of this wave's k-steps of the chunk: every fragment read issued
             // before the first MFMA (steps past the chunk's end read step 0 and
             // multiply a zeroed A fragment: no branch around the reads)
@@ -914,9 +918,23 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
                         acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bv[q][ct], acc[rt][ct], 0, 0, 0);
                 }
             }
-            if (j + 2 < ncl)
+            if constexpr (GLDS) {
+                // image j%2 holds chunk j+2 next: clear the k-step columns this wave read
+                // (its MFMAs consumed the reads; no other wave reads these columns)
+                if (j + 2 < ncl) {
+                    unsigned char *dj = lds + oD + (j & 1u) * szD;
+#pragma unroll
+                    for (int q = 0; q < MAXS; q++) {
+                        const uint32_t st = wv + q * WC;
+                        if (st < nsteps)
+                            for (uint32_t u = lane; u < R * 4u; u += 64u)
+                                *reinterpret_cast<u32x4 *>(dj + (u >> 2) * RS + st * 64u + (u & 3u) * 16u) = zero4;
+                    }
+                }
+            } else if (j + 2 < ncl) {
                 for (uint32_t u = tid; u < R * RS / 16u; u += 64u * WC)
                     *reinterpret_cast<u32x4 *>(lds + oD + ((j + 2) % 3u) * szD + u * 16u) = zero4;
+            }
             GS_STAMP(2u + 2u * j);
             __syncthreads();
             GS_STAMP(3u + 2u * j);
@@ -929,6 +947,45 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
 #pragma unroll
             for (int ct = 0; ct < CT; ct++)
                 *reinterpret_cast<f4v *>(red + (((wv * RT + rt) * CT + ct) * 64u + lane) * 4u) = acc[rt][ct];
+    } else if (role == 1 && GLDS) {
+        // ---------------------------------------------------------------- B rows, LDS-DMA
+        // global_load_lds_dwordx4: no VGPR round trip, no ds_write transfer cycles.
+        // Wave-instruction i of B wave bw fills the 1 KB at unit (bw*NB + i)*64 (the
+        // destination is lane-linear); b_piece's permutation rides on the source address
+        // (an XOR with a per-row constant: its own inverse).  Period j issues chunk j+2
+        // into the buffer period j-1 finished reading and retires chunk j+1 with a
+        // counted vmcnt before a raw s_barrier (__syncthreads would drain to vmcnt(0)).
+        const uint32_t bw = wv - WC;
+        auto issue = [&](uint32_t jl) {
+            const uint32_t kc0 = (j0 + jl) * KC;
+#pragma unroll
+            for (uint32_t i = 0; i < NB; i++) {
+                const uint32_t u0 = (bw * NB + i) * 64u, u = u0 + lane;
+                const uint32_t k = u / UB, s = u % UB;
+                const uint32_t kk = kc0 + k < K ? kc0 + k : kc0;
+                const f16 *src = B + (size_t)kk * N + (b_piece<CT>(k, s >> 1) * 2u + (s & 1u)) * 8u;
+                __builtin_amdgcn_global_load_lds(
+                    (const void *)src, (__attribute__((address_space(3))) void *)(lds + (jl % 3u) * szB + u0 * 16u), 16,
+                    0, 0);
+            }
+        };
+        issue(0u);
+        if (1u < ncl) issue(1u);
+        __syncthreads();  // dense images cleared (its vmcnt(0) retires chunks 0 and 1)
+        GS_STAMP(1u);
+        __syncthreads();  // chunk 0 staged
+        for (uint32_t j = 0; j < ncl; j++) {
+            if (j + 2 < ncl) {
+                issue(j + 2);
+                __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"(NB) : "memory");
+            } else {
+                __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            GS_STAMP(2u + 2u * j);
+            __builtin_amdgcn_s_barrier();
+            GS_STAMP(3u + 2u * j);
+        }
+        __syncthreads();
     } else if (role == 1) {
         // ---------------------------------------------------------------- B rows
         u32x4 s0[NB], s1[NB], s2[NB];
@@ -1002,7 +1059,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
 #define GS_SCATTER(j, P, V)                                                                         \
     {                                                                                             \
         const uint32_t G_ = GS_SEG((j) + 1) - GS_SEG(j);                                          \
-        unsigned char *ld_ = lds + oD + ((j) % 3u) * szD;                                         \
+        unsigned char *ld_ = lds + oD + ((j) % NDI) * szD;                                        \
         _Pragma("unroll") for (int I = 0; I < MAXA; I++) {                                        \
             const uint32_t q = at + I * NAT;                                                      \
             if (q < G_) {                                                                         \
@@ -1082,7 +1139,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         }
         __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        uint32_t *flag = reinterpret_cast<uint32_t *>(lds + oD + 3 * szD + 512);
+        uint32_t *flag = reinterpret_cast<uint32_t *>(lds + oD + NDI * szD + 512);
         if (tid == 0)
             *flag = __hip_atomic_fetch_add(&arrivals[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();

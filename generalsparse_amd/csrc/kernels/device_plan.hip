@@ -199,7 +199,9 @@ constexpr uint32_t kMfmaBThreads = 64 * gsk::kMfmaBWaves, kMfmaAThreads = 64 * g
 
 size_t mfma_lds_bytes(uint32_t lgKC, uint32_t CT, uint32_t RMAX) {
     const size_t KC = 1ull << lgKC;
-    return 2 * KC * 32 * CT + 3 * (RMAX + 1) * (2 * KC + 32) + 1024;  // + stamp slots and the arrival flag
+    // the larger of the two layouts (2 B buffers + 3 dense images; MFMA_GLDS: 3 + 2)
+    const size_t szB = KC * 32 * CT, szD = (RMAX + 1) * (2 * KC + 32);
+    return std::max(2 * szB + 3 * szD, 3 * szB + 2 * szD) + 1024;  // + stamp slots and the arrival flag
 }
 
 // Order one segment's entries for the scatter: the kernel's 32-lane half-waves
@@ -797,12 +799,14 @@ template <int CT, int RT, int LGKC, int MAXA>
 void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N,
                    hipStream_t s) {
     const device_plan &d = p.dev;
-    auto kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA>;
+    // B rows by LDS-DMA two chunks ahead (MFMA_GLDS) or through registers three ahead
+    auto kern = get_config().MFMA_GLDS ? gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, true>
+                                       : gsk::k_mfma_rows<CT, RT, LGKC, MAXA>;
     static std::mutex mu;
-    static std::map<int, size_t> granted;
+    static std::map<std::pair<int, const void *>, size_t> granted;
     {
         std::lock_guard<std::mutex> l(mu);
-        size_t &g = granted[d.device];
+        size_t &g = granted[{d.device, reinterpret_cast<const void *>(kern)}];
         if (g < d.lds_bytes) {
             HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)d.lds_bytes));

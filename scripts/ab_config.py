@@ -1,0 +1,53 @@
+"""A/B of a launch-time config switch on the C2 kernel (diagnostic).
+usage: ab_config.py KEY v0 v1 [pipeline p0 p1]
+Times 200 rotated SpMMs per setting (HIP events, interleaved settings x3) and checks
+every setting's C against the first (bit-exact expected)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import generalsparse_amd as gsa  # noqa: E402
+from generalsparse_amd import datasets as ds  # noqa: E402
+
+key, vals = sys.argv[1], [int(x) for x in sys.argv[2:4]]
+pipe = sys.argv[4] if len(sys.argv) > 4 else "tblock_warp_total"
+p0 = int(sys.argv[5]) if len(sys.argv) > 5 else 20
+p1 = int(sys.argv[6]) if len(sys.argv) > 6 else 2
+M = K = 5120
+N = 32
+row, col, val = ds.pruned_weight(M, K, 0.7, 13)
+plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline(pipe, N, p0, p1).compile().upload("f16", 0)
+reps = 12
+for _ in range(reps - 1):
+    plan.add_replica()
+Bs = [torch.randn((K, N), device="cuda", dtype=torch.float16) for _ in range(reps)]
+Cs = [torch.empty((M, N), device="cuda", dtype=torch.float16) for _ in range(reps)]
+ref = None
+for v in vals:
+    gsa.set_config(key, v)
+    C = plan.spmm(Bs[0])
+    torch.cuda.synchronize()
+    if ref is None:
+        ref = C.clone()
+        dense = torch.zeros((M, K), device="cuda", dtype=torch.float32)
+        dense[torch.as_tensor(row.astype("int64")).cuda(), torch.as_tensor(col.astype("int64")).cuda()] = torch.as_tensor(val).float().cuda()
+        full = dense @ Bs[0].float()
+        print("max abs err vs fp32 dense:", (C.float() - full).abs().max().item())
+    else:
+        print(key, v, "bit-exact vs first:", torch.equal(C, ref), "max diff", (C.float() - ref.float()).abs().max().item())
+res = {v: [] for v in vals}
+for rnd in range(3):
+    for v in vals:
+        gsa.set_config(key, v)
+        plan.spmm_rotate(24, 0, Bs, Cs)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        plan.spmm_rotate(200, 0, Bs, Cs)
+        e1.record()
+        torch.cuda.synchronize()
+        res[v].append(e0.elapsed_time(e1) / 200 * 1000)
+for v in vals:
+    print(f"{key}={v}: us/spmm", " ".join(f"{t:.2f}" for t in res[v]))

@@ -303,12 +303,15 @@ def mfma_everywhere():
     gsa.set_config("MFMA_MAX_FILL", 1 << 30)
     yield
     gsa.set_config("MFMA_MAX_FILL", 16)
+    gsa.set_config("MFMA_GLDS", 1)
 
 
+@pytest.mark.parametrize("glds", [1, 0])  # B rows by LDS-DMA (default) / through registers
 @pytest.mark.parametrize("N", [16, 32, 64])
 @pytest.mark.parametrize("pipe", MFMA_PIPES, ids=lambda p: f"{p[0]}-{p[1]}")
-def test_mfma_rows_match_oracle(pipe, N, mfma_everywhere):
+def test_mfma_rows_match_oracle(pipe, N, glds, mfma_everywhere):
     name, p0, p1 = pipe
+    gsa.set_config("MFMA_GLDS", glds)
     # every case must be right whichever kernel the upload picked; the matrix
     # cores must have taken at least one case (33..64-row blocks at N=64 never
     # fit LDS twice over, and 50%-dense chunks of them exceed the stage buffers)
