@@ -363,7 +363,18 @@ int gs_plan_sub_matrices(gs_plan_t *p, int *ids, int cap) {
 int gs_plan_compile(gs_plan_t *p) {
     return guard([&] {
         GS_CHECK(p, "null plan");
-        for (gs::plan_state *s : kernel_states(p)) s->cg->compile();
+        const auto &m = *p->st.meta;
+        for (gs::plan_state *s : kernel_states(p)) {
+            // a kernel writes C row begin_row_index + r: every row must lie inside its
+            // sub-matrix (row_nz_matrix_div_operator leaves them in the parent's indexing)
+            const int sb = s->cg->get_sub_matrix_id();
+            const uint64_t b = m.scalar(gs::GLOBAL_META, "begin_row_index", sb), e = m.scalar(gs::GLOBAL_META, "end_row_index", sb);
+            const auto &r = m.u(gs::GLOBAL_META, "nz_row_indices", sb);
+            GS_CHECK(r.empty() || b + r.back() <= e,
+                     "sub-matrix " + std::to_string(sb) + ": row indices lie past its end_row_index (rows left in the "
+                     "parent's indexing, div_row_indices_by_row_nnz.cc) -- plan only, not executable");
+            s->cg->compile();
+        }
     });
 }
 

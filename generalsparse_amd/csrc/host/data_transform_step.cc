@@ -1111,4 +1111,138 @@ void fixed_div_row_indices::run(bool check) {
     is_run = true;
 }
 
+// ------------------------------------------- row division by row length (§8f rank 3)
+// div_row_indices_by_row_nnz.cc:40-95 (the same loop in all seven transforms and in
+// row_nz_matrix_div_operator::is_valid_according_to_metadata)
+static void row_nz_window_of(uint64_t nz, const row_nz_window &w, uint64_t &low, uint64_t &high) {
+    low = 0;
+    high = w.nz_gap_size;
+    if (nz < w.max_gap) {
+        while (nz >= high && high <= w.max_gap) {
+            low = high;
+            high *= w.expansion_rate;
+        }
+    } else {
+        low = w.max_gap;
+        high = low * w.expansion_rate;
+    }
+}
+
+std::vector<uint64_t> row_nz_div_positions(const std::vector<uint64_t> &nnz, const row_nz_window &w, size_t max_count,
+                                           bool *over) {
+    std::vector<uint64_t> div{0};
+    if (over) *over = false;
+    uint64_t low, high;
+    row_nz_window_of(nnz[0], w, low, high);
+    for (uint64_t r = 1; r < nnz.size(); r++) {
+        const uint64_t nz = nnz[r];
+        if ((nz >= low && nz < high) || (nz >= high && high > w.max_gap)) continue;
+        div.push_back(r);
+        if (max_count && div.size() > max_count) {
+            if (over) *over = true;
+            break;
+        }
+        row_nz_window_of(nz, w, low, high);
+    }
+    return div;
+}
+
+static std::vector<uint64_t> row_nz_positions_of(const meta_data_set &m, int s, const row_nz_window &w) {
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    const uint64_t rn = m.scalar(GLOBAL_META, "end_row_index", s) - m.scalar(GLOBAL_META, "begin_row_index", s) + 1;
+    GS_CHECK(!row.empty(), "row-length division of an empty sub-matrix");
+    return row_nz_div_positions(get_nnz_of_each_row_in_spec_range(row, 0, rn - 1, 0, row.size() - 1), w);
+}
+
+// div_row_indices_by_row_nnz.cc:96-125: entries walk the buckets in row order, moving on
+// by ONE bucket whenever a row reaches the current bucket's upper bound (the last bucket's
+// bound is the last row + 1); rows keep the parent's indexing
+template <class T, class F>
+static std::vector<std::vector<T>> row_nz_buckets(const std::vector<uint64_t> &row, const std::vector<uint64_t> &div,
+                                                  F value_of) {
+    std::vector<std::vector<T>> b(div.size());
+    size_t cur = 0;
+    for (size_t i = 0; i < row.size(); i++) {
+        const uint64_t r = row[i];
+        const int64_t upper = cur < div.size() - 1 ? (int64_t)div[cur + 1] : (int64_t)row.back() + 1;
+        if (r >= div[cur] && (int64_t)r < upper) {
+            b[cur].push_back(value_of(i));
+        } else if ((int64_t)r >= upper) {
+            cur++;
+            b[cur].push_back(value_of(i));
+        }
+    }
+    return b;
+}
+
+void modify_row_start_boundary_after_div_according_to_row_nz::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    for (uint64_t d : row_nz_positions_of(m, target_matrix_id, win)) add_scalar_next(m, GLOBAL_META, "begin_row_index", d);
+    is_run = true;
+}
+
+void modify_row_end_boundary_after_div_according_to_row_nz::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    std::vector<uint64_t> div = row_nz_positions_of(m, target_matrix_id, win);
+    div.push_back(m.scalar(GLOBAL_META, "end_row_index", target_matrix_id) -
+                  m.scalar(GLOBAL_META, "begin_row_index", target_matrix_id) + 1);
+    for (size_t i = 1; i < div.size(); i++) add_scalar_next(m, GLOBAL_META, "end_row_index", div[i] - 1);
+    is_run = true;
+}
+
+void modify_col_start_boundary_after_div_according_to_row_nz::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const uint64_t c = m.scalar(GLOBAL_META, "begin_col_index", target_matrix_id);
+    for (size_t n = row_nz_positions_of(m, target_matrix_id, win).size(); n; n--)
+        add_scalar_next(m, GLOBAL_META, "begin_col_index", c);
+    is_run = true;
+}
+
+void modify_col_end_boundary_after_div_according_to_row_nz::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const uint64_t c = m.scalar(GLOBAL_META, "end_col_index", target_matrix_id);
+    for (size_t n = row_nz_positions_of(m, target_matrix_id, win).size(); n; n--)
+        add_scalar_next(m, GLOBAL_META, "end_col_index", c);
+    is_run = true;
+}
+
+void div_col_indices_by_row_nnz::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    const auto &col = m.u(GLOBAL_META, "nz_col_indices", target_matrix_id);
+    auto b = row_nz_buckets<uint64_t>(row, row_nz_positions_of(m, target_matrix_id, win), [&](size_t i) { return col[i]; });
+    for (auto &v : b)
+        if (!v.empty())
+            m.add_element(GLOBAL_META, "nz_col_indices", m.get_max_sub_matrix_id_of_data_item(GLOBAL_META, "nz_col_indices") + 1,
+                          std::make_shared<universal_array>(std::move(v)));
+    m.remove_element(GLOBAL_META, "nz_col_indices", target_matrix_id);
+    is_run = true;
+}
+
+void div_val_indices_by_row_nnz::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    auto varr = m.get_element(GLOBAL_META, "nz_vals", target_matrix_id)->meta_data_arr;
+    auto b = row_nz_buckets<double>(row, row_nz_positions_of(m, target_matrix_id, win),
+                                    [&](size_t i) { return varr->read_float_from_arr(i); });
+    for (auto &v : b)
+        if (!v.empty())
+            m.add_element(GLOBAL_META, "nz_vals", m.get_max_sub_matrix_id_of_data_item(GLOBAL_META, "nz_vals") + 1,
+                          std::make_shared<universal_array>(std::move(v), varr->get_data_type()));
+    m.remove_element(GLOBAL_META, "nz_vals", target_matrix_id);
+    is_run = true;
+}
+
+void div_row_indices_by_row_nnz::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    auto b = row_nz_buckets<uint64_t>(row, row_nz_positions_of(m, target_matrix_id, win), [&](size_t i) { return row[i]; });
+    for (auto &v : b)
+        if (!v.empty())
+            m.add_element(GLOBAL_META, "nz_row_indices", m.get_max_sub_matrix_id_of_data_item(GLOBAL_META, "nz_row_indices") + 1,
+                          std::make_shared<universal_array>(std::move(v)));
+    m.remove_element(GLOBAL_META, "nz_row_indices", target_matrix_id);
+    is_run = true;
+}
+
 }  // namespace gs

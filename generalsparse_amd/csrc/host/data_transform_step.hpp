@@ -208,6 +208,24 @@ GS_DECLARE_STEP_P(fixed_div_col_indices_by_corr_row_indices, uint64_t, fixed_row
 GS_DECLARE_STEP_P(fixed_div_vals_by_corr_row_indices, uint64_t, fixed_row_gap_size)
 GS_DECLARE_STEP_P(fixed_div_row_indices, uint64_t, fixed_row_gap_size)
 
+// row division by row length (§8f rank 3; row_nz_matrix_div_operator.cc, *_after_div_according_to_row_nz.cc,
+// div_{row,col,val}_indices_by_row_nnz.cc): a new sub-matrix starts wherever a row's nnz leaves the
+// current window [low, high) (windows grow from nz_gap_size by expansion_rate up to max_gap)
+struct row_nz_window {
+    uint64_t nz_gap_size, max_gap, expansion_rate;
+};
+// the division positions (row ids relative to the sub-matrix); max_count > 0 stops after
+// more than max_count positions (the operator's validity check) and sets *over
+std::vector<uint64_t> row_nz_div_positions(const std::vector<uint64_t> &nnz_of_each_row, const row_nz_window &w,
+                                           size_t max_count = 0, bool *over = nullptr);
+GS_DECLARE_STEP_P(modify_row_start_boundary_after_div_according_to_row_nz, row_nz_window, win)
+GS_DECLARE_STEP_P(modify_row_end_boundary_after_div_according_to_row_nz, row_nz_window, win)
+GS_DECLARE_STEP_P(modify_col_start_boundary_after_div_according_to_row_nz, row_nz_window, win)
+GS_DECLARE_STEP_P(modify_col_end_boundary_after_div_according_to_row_nz, row_nz_window, win)
+GS_DECLARE_STEP_P(div_col_indices_by_row_nnz, row_nz_window, win)
+GS_DECLARE_STEP_P(div_val_indices_by_row_nnz, row_nz_window, win)
+GS_DECLARE_STEP_P(div_row_indices_by_row_nnz, row_nz_window, win)
+
 // interleaved storage (§8f rank 2; modify_{col,val,row}_indices_by_interlance_storage.cc):
 // inside every parent block the i-th nonzero of BMT b moves to b + i * (BMTs in the parent)
 #define GS_DECLARE_INTERLANCE(cls)                                                                \

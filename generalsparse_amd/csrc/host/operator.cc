@@ -193,6 +193,64 @@ void fixed_interval_row_matrix_div_operator::run(bool check) {
     is_run = true;
 }
 
+// ---------------------------------------- row division by row length (§8f rank 3)
+row_nz_matrix_div_operator::row_nz_matrix_div_operator(cg_ptr cg, int init, int mx, int rate, ctx_ptr)
+    : basic_operator("row_nz_matrix_div_operator", cg->get_metadata_set(), CONVERTING_OP, cg->get_sub_matrix_id()),
+      init_row_size_upper_boundary(init), max_row_size_upper_boundary(mx), expansion_rate(rate) {
+    GS_CHECK(init > 0 && rate > 0, "init_row_size_upper_boundary > 0 and expansion_rate > 0");
+}
+
+// row_nz_matrix_div_operator.cc:29-57: the same rule as the fixed-interval division
+bool row_nz_matrix_div_operator::is_valid_according_to_operator(ctx_ptr h) {
+    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return true;
+    if (!h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id).empty()) return true;
+    for (auto &o : h->read_operator_context_arr(CONVERTING_OP, target_matrix_id))
+        if (o->get_name().find("div_operator") != std::string::npos && o->get_target_matrix_id() == target_matrix_id)
+            return false;
+    return true;
+}
+
+// :59-170: boundaries + COO present, no interleaved storage, at most MAX_DIV_TIMES_OF_DIV
+// division positions
+bool row_nz_matrix_div_operator::is_valid_according_to_metadata() {
+    auto &m = *meta_data_set_ptr;
+    const int s = target_matrix_id;
+    for (const char *n : {"begin_row_index", "end_row_index", "begin_col_index", "end_col_index"})
+        if (!m.is_exist(GLOBAL_META, n, s)) return false;
+    if (!coo_present(m, s) || interlance_storage_existing(m, s)) return false;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    const uint64_t rn = m.scalar(GLOBAL_META, "end_row_index", s) - m.scalar(GLOBAL_META, "begin_row_index", s) + 1;
+    if (row.empty() || row.back() >= rn) return false;
+    bool over = false;
+    row_nz_div_positions(get_nnz_of_each_row_in_spec_range(row, 0, rn - 1, 0, row.size() - 1),
+                         {(uint64_t)init_row_size_upper_boundary, (uint64_t)max_row_size_upper_boundary,
+                          (uint64_t)expansion_rate},
+                         (size_t)get_config().MAX_DIV_TIMES_OF_DIV, &over);
+    return !over;
+}
+
+// :172-250: boundaries, cols, vals, then rows
+void row_nz_matrix_div_operator::run(bool check) {
+    if (check) GS_CHECK(is_valid_according_to_metadata(), "row-length division: invalid metadata");
+    const row_nz_window w{(uint64_t)init_row_size_upper_boundary, (uint64_t)max_row_size_upper_boundary,
+                          (uint64_t)expansion_rate};
+    modify_row_start_boundary_after_div_according_to_row_nz a(meta_data_set_ptr, target_matrix_id, w);
+    run_step(a, check);
+    modify_row_end_boundary_after_div_according_to_row_nz b(meta_data_set_ptr, target_matrix_id, w);
+    run_step(b, check);
+    modify_col_start_boundary_after_div_according_to_row_nz c(meta_data_set_ptr, target_matrix_id, w);
+    run_step(c, check);
+    modify_col_end_boundary_after_div_according_to_row_nz d(meta_data_set_ptr, target_matrix_id, w);
+    run_step(d, check);
+    div_col_indices_by_row_nnz e(meta_data_set_ptr, target_matrix_id, w);
+    run_step(e, check);
+    div_val_indices_by_row_nnz f(meta_data_set_ptr, target_matrix_id, w);
+    run_step(f, check);
+    div_row_indices_by_row_nnz g(meta_data_set_ptr, target_matrix_id, w);
+    run_step(g, check);
+    is_run = true;
+}
+
 // --------------------------------------------- row-direction WARP blocking
 fixed_interval_row_direction_warp_blocking_operator::fixed_interval_row_direction_warp_blocking_operator(
     cg_ptr cg, int rb, bool rrel, bool nrel, bool pad, ctx_ptr)
@@ -1046,6 +1104,10 @@ std::shared_ptr<basic_operator> make_operator(const std::string &name, const std
         need(3);
         return std::make_shared<balanced_interval_row_direction_thread_blocking_operator>(cg, (int)a[0], a[1] != 0,
                                                                                           a[2] != 0, ctx);
+    }
+    if (name == "row_nz_matrix_div_operator") {
+        need(3);
+        return std::make_shared<row_nz_matrix_div_operator>(cg, (int)a[0], (int)a[1], (int)a[2], ctx);
     }
     if (name == "fixed_interval_row_matrix_div_operator") {
         need(1);

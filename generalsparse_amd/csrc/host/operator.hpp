@@ -87,6 +87,22 @@ class fixed_interval_row_matrix_div_operator : public basic_operator {
     std::vector<int> new_sub_matrix_ids;  // filled by run()
 };
 
+// operator/row_nz_matrix_div_operator.cc (§8f rank 3): CONVERTING; splits the sub-matrix
+// into row ranges of similar row length (windows from init_row_size_upper_boundary growing by
+// expansion_rate up to max_row_size_upper_boundary).  Restated with the reference's
+// quirks: every range gets boundaries, only ranges that receive entries get arrays, the
+// entries move on one range at a time, and row indices keep the parent's indexing
+// (such sub-matrices are planned, not executed: gs_plan_compile refuses them).
+class row_nz_matrix_div_operator : public basic_operator {
+  public:
+    row_nz_matrix_div_operator(cg_ptr cg, int init_row_size_upper_boundary, int max_row_size_upper_boundary,
+                               int expansion_rate, ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    int init_row_size_upper_boundary, max_row_size_upper_boundary, expansion_rate;
+};
+
 // -------------------------------------------------------------- DISTRIBUTING
 class fixed_interval_row_direction_tblock_blocking_operator : public basic_operator {
   public:

@@ -1061,9 +1061,109 @@ int or_fixed_interval_row_div(or_set *s, uint64_t gap) {
     return 0;
 }
 
+/* §8f rank 3: row_nz_matrix_div_operator on sub-matrix 0 (operator/row_nz_matrix_div_operator.cc
+ * :59-250; transform_step/modify_*_boundary_after_div_according_to_row_nz.cc,
+ * div_{row,col,val}_indices_by_row_nnz.cc).
+ * Window of a row length nz: [0, init) grown by rate while nz >= high and high <= max_gap;
+ * nz >= max_gap gives [max_gap, max_gap*rate).  A division position is every row whose
+ * length leaves the current window (lengths past an open-ended top window stay).  Every
+ * position gets boundaries (begin = position, end = next position - 1, cols copied); the
+ * entries walk the buckets in row order, moving on by one bucket whenever a row reaches the
+ * current bucket's bound (the last bucket's bound: last row + 1); only non-empty buckets get
+ * arrays; rows keep sub-matrix 0's indexing. */
+static void rnz_window(uint64_t nz, uint64_t init, uint64_t mx, uint64_t rate, uint64_t *lo, uint64_t *hi) {
+    *lo = 0;
+    *hi = init;
+    if (nz < mx) {
+        while (nz >= *hi && *hi <= mx) {
+            *lo = *hi;
+            *hi *= rate;
+        }
+    } else {
+        *lo = mx;
+        *hi = mx * rate;
+    }
+}
+
+int or_row_nz_div(or_set *s, uint64_t init, uint64_t mx, uint64_t rate) {
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    or_array *C = get(s, "GLOBAL_META", "nz_col_indices", 0);
+    or_array *V = get(s, "GLOBAL_META", "nz_vals", 0);
+    if (!R || !C || !V || !R->len || init == 0 || rate == 0) return fail(s, "row-length division needs the COO of sub-matrix 0");
+    uint64_t b = scalar(s, "GLOBAL_META", "begin_row_index", 0), e = scalar(s, "GLOBAL_META", "end_row_index", 0);
+    uint64_t bc = scalar(s, "GLOBAL_META", "begin_col_index", 0), ec = scalar(s, "GLOBAL_META", "end_col_index", 0);
+    uint64_t rn = e - b + 1;
+    uint64_t *cnt = row_nnz(R->u, R->len, rn);
+    uint64_t *div = (uint64_t *)malloc((rn + 1) * sizeof(uint64_t));
+    uint64_t nd = 0, lo, hi;
+    div[nd++] = 0;
+    rnz_window(cnt[0], init, mx, rate, &lo, &hi);
+    for (uint64_t r = 1; r < rn; r++) {
+        uint64_t nz = cnt[r];
+        if ((nz >= lo && nz < hi) || (nz >= hi && hi > mx)) continue;
+        div[nd++] = r;
+        if (nd > 12) { /* MAX_DIV_TIMES_OF_DIV default */
+            free(cnt);
+            free(div);
+            return fail(s, "row-length division: more than 12 positions");
+        }
+        rnz_window(nz, init, mx, rate, &lo, &hi);
+    }
+    free(cnt);
+    int id = 1;
+    for (uint64_t i = 0; i < nd; i++) {
+        put_scalar(s, "GLOBAL_META", "begin_row_index", (int)(id + i), div[i]);
+        put_scalar(s, "GLOBAL_META", "end_row_index", (int)(id + i), (i + 1 < nd ? div[i + 1] : rn) - 1);
+        put_scalar(s, "GLOBAL_META", "begin_col_index", (int)(id + i), bc);
+        put_scalar(s, "GLOBAL_META", "end_col_index", (int)(id + i), ec);
+    }
+    R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    C = get(s, "GLOBAL_META", "nz_col_indices", 0);
+    V = get(s, "GLOBAL_META", "nz_vals", 0);
+    uint64_t n = R->len, last = R->u[n - 1];
+    uint64_t *bk = (uint64_t *)malloc(n * sizeof(uint64_t)), *bn = (uint64_t *)calloc(nd, sizeof(uint64_t));
+    uint64_t cur = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t r = R->u[i], up = cur < nd - 1 ? div[cur + 1] : last + 1;
+        if (r >= up) cur++;
+        bk[i] = cur;
+        bn[cur]++;
+    }
+    free(div);
+    int nid = id;
+    for (uint64_t k = 0; k < nd; k++) {
+        if (!bn[k]) continue;
+        uint64_t *nr = (uint64_t *)malloc(bn[k] * sizeof(uint64_t)), *nc = (uint64_t *)malloc(bn[k] * sizeof(uint64_t));
+        double *nv = (double *)malloc(bn[k] * sizeof(double));
+        uint64_t q = 0;
+        for (uint64_t i = 0; i < n; i++)
+            if (bk[i] == k) {
+                nr[q] = R->u[i];
+                nc[q] = C->u[i];
+                nv[q] = V->f[i];
+                q++;
+            }
+        put_u(s, "GLOBAL_META", "nz_col_indices", nid, nc, bn[k]);
+        put_f(s, "GLOBAL_META", "nz_vals", nid, nv, bn[k]);
+        put_u(s, "GLOBAL_META", "nz_row_indices", nid, nr, bn[k]);
+        R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+        C = get(s, "GLOBAL_META", "nz_col_indices", 0);
+        V = get(s, "GLOBAL_META", "nz_vals", 0);
+        nid++;
+    }
+    free(bk);
+    free(bn);
+    drop(s, "GLOBAL_META", "nz_col_indices", 0);
+    drop(s, "GLOBAL_META", "nz_vals", 0);
+    drop(s, "GLOBAL_META", "nz_row_indices", 0);
+    return 0;
+}
+
 int or_pipeline(or_set *s, const char *name, int p0, int p1) {
     if (!strcmp(name, "row_div")) /* p0 = fixed_row_interval_size */
         return or_fixed_interval_row_div(s, (uint64_t)p0);
+    if (!strcmp(name, "row_nz_div")) /* p0 = init window, p1 = max window; expansion rate 2 */
+        return or_row_nz_div(s, (uint64_t)p0, (uint64_t)p1, 2);
     if (!strcmp(name, "thread_total")) { /* token_test.cc:1003-1092, p0 = sparse_cf */
         if (or_sort_operator(s)) return -1;
         return or_row_dir_thread_blocking(s, 1, p0);

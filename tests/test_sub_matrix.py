@@ -165,3 +165,58 @@ def test_compile_needs_every_sub_matrix():
         p.save("/tmp/gs_never_written.plan")
     with pytest.raises(gsa.GsError):
         p.run_pipeline("warp_total", 32, 0, 1, sub=99)
+
+
+# ---------------------------------------------------------------- row_nz_matrix_div_operator
+def check_row_nz_division(M, K, r, c, v, init, mx):
+    exp, err = ofi.run_pipeline(M, K, r, c, v, "row_nz_div", init, mx)
+    p = gsa.Plan.from_coo(M, K, r, c, v)
+    if err is not None:
+        with pytest.raises(gsa.GsError):
+            p.add_operator("row_nz_matrix_div_operator", init, mx, 2)
+        return None
+    p.add_operator("row_nz_matrix_div_operator", init, mx, 2)
+    got = p.arrays()
+    assert sorted(got) == sorted(exp)
+    for k, a in exp.items():
+        np.testing.assert_array_equal(got[k], a, err_msg=k)
+    return p
+
+
+def test_row_nz_division_hand_case():
+    # row lengths 5,5,0,0,5,5 with windows from 4 (x2 up to 64): positions 0, 2, 4.
+    # The entries move on one bucket at a time: row 4's first entry lands in bucket 1
+    # (rows 2-3), its others in bucket 2 -- the reference's assignment loop
+    # (div_row_indices_by_row_nnz.cc), restated as is
+    r = np.repeat(np.array([0, 1, 4, 5], np.uint64), 5)
+    c = np.tile(np.arange(5, dtype=np.uint64), 4)
+    v = np.arange(1, 21, dtype=np.float32)
+    p = check_row_nz_division(6, 5, r, c, v, 4, 64)
+    a = p.arrays()
+    assert [a[f"GLOBAL_META_begin_row_index_{s}"][0] for s in (1, 2, 3)] == [0, 2, 4]
+    assert [a[f"GLOBAL_META_end_row_index_{s}"][0] for s in (1, 2, 3)] == [1, 3, 5]
+    assert a["GLOBAL_META_nz_row_indices_1"].tolist() == [0] * 5 + [1] * 5
+    assert a["GLOBAL_META_nz_row_indices_2"].tolist() == [4]
+    assert a["GLOBAL_META_nz_row_indices_3"].tolist() == [4] * 4 + [5] * 5
+    assert a["GLOBAL_META_nz_vals_2"].tolist() == [11.0]
+    # rows stay in the parent's indexing: planned, not executed
+    for s in p.sub_matrices():
+        p.run_pipeline("warp_total", 32, 0, 1, sub=s)
+    with pytest.raises(gsa.GsError, match="not executable"):
+        p.compile()
+
+
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("win", [(4, 64), (8, 32), (2, 1024), (16, 16)])
+def test_row_nz_division_matches_oracle(seed, win):
+    rng = np.random.default_rng(40 + seed)
+    M, K = 120, 300
+    # bands of similar row length (few positions) with some noise rows
+    lens = np.repeat(rng.choice([0, 3, 12, 40, 90], size=6), 20)
+    lens[rng.random(M) < 0.03 * seed] = 1
+    rows = np.repeat(np.arange(M, dtype=np.uint64), lens)
+    cols = np.concatenate([np.sort(rng.choice(K, size=n, replace=False)) for n in lens]).astype(np.uint64)
+    if len(rows) == 0:
+        return
+    vals = rng.uniform(-1, 1, len(rows)).astype(np.float32)
+    check_row_nz_division(M, K, rows, cols, vals, *win)
