@@ -219,6 +219,18 @@ void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1)
         ex.add_and_run(std::make_shared<warp_total_reduce_operator>(cg, cf, ctx));
         ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)((rows + rb - 1) / rb),
                                                              std::vector<unsigned>{64u, 4u}, cf, ctx));
+    } else if (name == "tblock_thread_total" || name == "tblock_warp_thread_total") {
+        // §8f rank 1: BMTs of p1 rows inside BMTBs of p0 rows (and inside BMWs of 8 rows),
+        // row and nz indices relative to the parent as well
+        int rb = p0 > 0 ? p0 : 16, tbr = p1 > 0 ? p1 : 1, cf = 1;
+        ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, rb, false, ctx));
+        if (name == "tblock_warp_thread_total")
+            ex.add_and_run(std::make_shared<fixed_interval_row_direction_warp_blocking_operator>(cg, 8, false, false, false, ctx));
+        ex.add_and_run(std::make_shared<fixed_interval_row_direction_thread_blocking_operator>(
+            cg, tbr, true, true, false, false, false, 0, ctx));
+        ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, false, 1, cf, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)((rows + rb - 1) / rb),
+                                                             std::vector<unsigned>{64u, 4u}, cf, ctx));
     } else if (name == "tblock_warp_total_relative") {
         // §8f rank 1: the C2 plan with BMW indices relative to their BMTB as well
         // (fixed_interval_row_direction_warp_blocking_operator with both relative flags)

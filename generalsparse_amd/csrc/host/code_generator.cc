@@ -119,15 +119,16 @@ void code_generator::compile() {
                 s.arrays.push_back(k);
     } else if (tt && tt->kind == reduction_kind::TOTAL_BMT_RESULT && !tt->need_warp_reduction &&
                !m.is_exist(GLOBAL_META, "original_nz_row_indices", sub) &&
-               !m.is_exist(WARP_META, "first_row_indices", sub) && !m.is_exist(TBLOCK_META, "first_row_indices", sub) &&
                m.is_exist(THREAD_META, "first_row_indices", sub) && [&] {
                    const auto &fr = m.u(THREAD_META, "first_row_indices", sub);
                    for (size_t i = 0; i < fr.size(); i++)
                        if (fr[i] != i) return true;
                    return false;
                }()) {
-        // multi-row BMTs (balanced_interval_row_direction_thread_blocking_operator): every BMT
-        // is a run of whole rows, summed row by row -> the wave-per-row-group kernel
+        // multi-row BMTs (balanced_interval_row_direction_thread_blocking_operator, or fixed
+        // row blocking inside BMTB/BMW parents, whose absolute starts end with row_num / nnz
+        // like the parentless arrays): every BMT is a run of whole rows, summed row by row ->
+        // the wave-per-row-group kernel
         s.family = KF_WARP_TOTAL;
         s.group_level = THREAD_META;
         s.coarsen_factor = tt->coarsen_factor;
@@ -135,8 +136,8 @@ void code_generator::compile() {
     } else if (tt && tt->kind == reduction_kind::TOTAL_BMT_RESULT) {
         GS_CHECK(!tt->need_warp_reduction,
                  "thread_total with need_warp_reduction (col-direction warp_bit_map plans) is not built in this round");
-        GS_CHECK(!m.is_exist(WARP_META, "first_row_indices", sub) && !m.is_exist(TBLOCK_META, "first_row_indices", sub),
-                 "thread_total inside BMW/BMTB parents is not built in this round");
+        GS_CHECK(m.is_exist(THREAD_META, "first_row_indices", sub),
+                 "thread_total over col-direction BMTs without a bit-map token is not built in this round");
         s.family = KF_THREAD_TOTAL;
         s.coarsen_factor = tt->coarsen_factor;
         s.sparse_coarsen_factor = tt->sparse_coarsen_factor;

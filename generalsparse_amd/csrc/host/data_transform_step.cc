@@ -1245,4 +1245,95 @@ void div_row_indices_by_row_nnz::run(bool check) {
     is_run = true;
 }
 
+// ------------------------------------------ BMT row blocking inside parents (§8f rank 1)
+static const char *parent_tag(POS_TYPE p) { return p == TBLOCK_META ? "BMTB" : "BMW"; }
+
+// get_begin_rows_of_BMT_after_fixed_blocking_in_row_direction_in_BMTB.cc:30-75 (the _in_BMW
+// file is the same over WARP_META): BMT starts first + k*rb inside every parent, then row_num
+void get_begin_rows_of_BMT_after_fixed_blocking_in_row_direction_in_parent::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &pr = m.u(parent, "first_row_indices", target_matrix_id);
+    std::vector<uint64_t> out;
+    for (size_t j = 0; j + 1 < pr.size(); j++)
+        for (uint64_t r = pr[j]; r < pr[j + 1]; r += (uint64_t)fixed_row_block_size) out.push_back(r);
+    out.push_back(row_num_of_sub_matrix(m, target_matrix_id));
+    m.add_element(THREAD_META, "first_row_indices", target_matrix_id, std::make_shared<universal_array>(std::move(out)));
+    is_run = true;
+}
+
+// ..._relative_to_BMTB.cc:30-70: the same starts minus the parent's first row, no end entry
+void get_begin_rows_of_BMT_after_fixed_blocking_in_row_direction_relative_to_parent::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &pr = m.u(parent, "first_row_indices", target_matrix_id);
+    std::vector<uint64_t> out;
+    for (size_t j = 0; j + 1 < pr.size(); j++)
+        for (uint64_t r = pr[j]; r < pr[j + 1]; r += (uint64_t)fixed_row_block_size) out.push_back(r - pr[j]);
+    m.add_element(THREAD_META, std::string("first_row_indices_relative_to_") + parent_tag(parent), target_matrix_id,
+                  std::make_shared<universal_array>(std::move(out)));
+    is_run = true;
+}
+
+// get_begin_nzs_of_BMT_after_fixed_blocking_in_row_direction_in_BMTB.cc:35-85: every parent
+// opens a BMT at its first nz (an empty parent included); a new BMT after each rb rows that
+// do not end the parent; then the parents' last nz
+static std::vector<uint64_t> bmt_nzs_in_parent(meta_data_set &m, int s, POS_TYPE parent, int rb, bool relative) {
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    const uint64_t rn = row_num_of_sub_matrix(m, s);
+    const std::vector<uint64_t> cnt = get_nnz_of_each_row_in_spec_range(row, 0, rn - 1, 0, row.size() - 1);
+    const auto &pr = m.u(parent, "first_row_indices", s);
+    const auto &pz = m.u(parent, "first_nz_indices", s);
+    std::vector<uint64_t> out;
+    for (size_t j = 0; j + 1 < pr.size(); j++) {
+        const uint64_t base = relative ? 0 : pz[j];
+        int rc = 0;
+        uint64_t nz = 0;
+        out.push_back(base);
+        for (uint64_t i = pr[j]; i < pr[j + 1]; i++) {
+            rc += 1;
+            nz += cnt[i];
+            if (rc == rb && i != pr[j + 1] - 1) {
+                out.push_back(base + nz);
+                rc = 0;
+            }
+        }
+    }
+    if (!relative) out.push_back(pz.back());
+    return out;
+}
+
+void get_begin_nzs_of_BMT_after_fixed_blocking_in_row_direction_in_parent::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    m.add_element(THREAD_META, "first_nz_indices", target_matrix_id,
+                  std::make_shared<universal_array>(bmt_nzs_in_parent(m, target_matrix_id, parent, fixed_row_block_size, false)));
+    is_run = true;
+}
+
+void get_begin_nzs_of_BMT_after_fixed_blocking_in_row_direction_relative_to_parent::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    m.add_element(THREAD_META, std::string("first_nz_indices_relative_to_") + parent_tag(parent), target_matrix_id,
+                  std::make_shared<universal_array>(bmt_nzs_in_parent(m, target_matrix_id, parent, fixed_row_block_size, true)));
+    is_run = true;
+}
+
+// get_begin_BMTs_of_specific_parent_after_blocking_in_row_direction.cc:25-75: per parent the
+// index of its first BMT (BMTs counted while their first row lies before the next parent's)
+void get_begin_BMTs_of_specific_parent_after_blocking_in_row_direction::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const auto &bt = m.u(THREAD_META, "first_row_indices", target_matrix_id);
+    const auto &pr = m.u(parent, "first_row_indices", target_matrix_id);
+    std::vector<uint64_t> out{0};
+    size_t cur = 0;
+    for (size_t j = 0; j + 1 < pr.size(); j++) {
+        if (check) GS_CHECK(cur < bt.size() && bt[cur] == pr[j], "a parent does not start with a BMT");
+        uint64_t n = 0;
+        while (cur < bt.size() && bt[cur] < pr[j + 1]) {
+            n++;
+            cur++;
+        }
+        out.push_back(out.back() + n);
+    }
+    m.add_element(parent, "first_BMT_indices", target_matrix_id, std::make_shared<universal_array>(std::move(out)));
+    is_run = true;
+}
+
 }  // namespace gs

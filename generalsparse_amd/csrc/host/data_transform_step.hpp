@@ -198,6 +198,26 @@ GS_DECLARE_MERGE_PATH(get_begin_nzs_of_level_after_merge_path)
 void merge_path_levels(const std::vector<uint64_t> &nnz_of_each_row, uint64_t work_size,
                        std::vector<uint64_t> *level_rows, std::vector<uint64_t> *level_nzs);
 
+// BMT row blocking inside BMTB / BMW parents (§8f rank 1 relative indices;
+// get_begin_{rows,nzs}_of_BMT_after_fixed_blocking_in_row_direction_{in,relative_to}_{BMTB,BMW}.cc,
+// get_begin_BMTs_of_specific_parent_after_blocking_in_row_direction.cc): BMTs of
+// fixed_row_block_size rows start at every parent's first row
+#define GS_DECLARE_STEP_POS(cls)                                                                  \
+    class cls : public basic_data_transform_step {                                                \
+      public:                                                                                     \
+        cls(std::shared_ptr<meta_data_set> m, int target_matrix_id, POS_TYPE parent, int fixed_row_block_size) \
+            : basic_data_transform_step(#cls, std::move(m), target_matrix_id), parent(parent),    \
+              fixed_row_block_size(fixed_row_block_size) {}                                       \
+        void run(bool check) override;                                                            \
+        POS_TYPE parent;                                                                          \
+        int fixed_row_block_size;                                                                 \
+    };
+GS_DECLARE_STEP_POS(get_begin_rows_of_BMT_after_fixed_blocking_in_row_direction_in_parent)
+GS_DECLARE_STEP_POS(get_begin_rows_of_BMT_after_fixed_blocking_in_row_direction_relative_to_parent)
+GS_DECLARE_STEP_POS(get_begin_nzs_of_BMT_after_fixed_blocking_in_row_direction_in_parent)
+GS_DECLARE_STEP_POS(get_begin_nzs_of_BMT_after_fixed_blocking_in_row_direction_relative_to_parent)
+GS_DECLARE_STEP_POS(get_begin_BMTs_of_specific_parent_after_blocking_in_row_direction)
+
 // row division into sub-matrices (§8f rank 3; fixed_interval_row_matrix_div_operator.cc:85-150):
 // every non-empty interval of fixed_row_gap_size rows becomes a new sub-matrix (ids max + 1, ...)
 GS_DECLARE_STEP_P(modify_row_start_boundary_after_fixed_div_in_row_direction, uint64_t, fixed_row_gap_size)

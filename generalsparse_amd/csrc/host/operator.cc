@@ -357,8 +357,36 @@ bool fixed_interval_row_direction_thread_blocking_operator::is_valid_according_t
 // no-parent branch (:482-565) is the one token_test exercises
 void fixed_interval_row_direction_thread_blocking_operator::run(bool check) {
     if (check) GS_CHECK(is_valid_according_to_metadata(), "thread blocking: invalid metadata");
-    if (has(TBLOCK_META, "first_row_indices") || has(WARP_META, "first_row_indices"))
-        throw gs_error("BMT row blocking inside a BMTB/BMW parent is not built in this round");
+    if (has(TBLOCK_META, "first_row_indices") || has(WARP_META, "first_row_indices")) {
+        // :198-480: BMTs inside the BMWs when there are BMWs, else inside the BMTBs;
+        // absolute starts always, the relative arrays on request
+        if (is_col_padding_with_row_max_size_with_empty_row || is_col_padding_with_col_size)
+            throw gs_error("col padding of BMTs inside a parent (re-runs the parent's operators) is not built");
+        const POS_TYPE par = has(WARP_META, "first_row_indices") ? WARP_META : TBLOCK_META;
+        get_begin_rows_of_BMT_after_fixed_blocking_in_row_direction_in_parent a(meta_data_set_ptr, target_matrix_id, par,
+                                                                              fixed_row_block_size);
+        run_step(a, check);
+        if (row_index_is_relative_to_parent) {
+            get_begin_rows_of_BMT_after_fixed_blocking_in_row_direction_relative_to_parent b(
+                meta_data_set_ptr, target_matrix_id, par, fixed_row_block_size);
+            run_step(b, check);
+        }
+        get_begin_nzs_of_BMT_after_fixed_blocking_in_row_direction_in_parent c(meta_data_set_ptr, target_matrix_id, par,
+                                                                             fixed_row_block_size);
+        run_step(c, check);
+        if (nz_index_is_relative_to_parent) {
+            get_begin_nzs_of_BMT_after_fixed_blocking_in_row_direction_relative_to_parent d(
+                meta_data_set_ptr, target_matrix_id, par, fixed_row_block_size);
+            run_step(d, check);
+        }
+        get_begin_BMTs_of_specific_parent_after_blocking_in_row_direction e(meta_data_set_ptr, target_matrix_id, par,
+                                                                          fixed_row_block_size);
+        run_step(e, check);
+        code_generator_ptr->open_spec_level_of_paral(THREAD_META);
+        code_generator_ptr->set_thread_for_row(true);
+        is_run = true;
+        return;
+    }
     if (is_row_padding) throw gs_error("row padding is not built in this round");
     if (is_col_padding_with_row_max_size_with_empty_row)
         throw gs_error("col padding to the parent's max row size is not built in this round");

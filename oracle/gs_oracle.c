@@ -996,6 +996,60 @@ int or_bmw_relative_to_bmtb(or_set *s, int rb) {
 /* canned pipelines: token_test.cc test_spmm_*                          */
 /* ------------------------------------------------------------------ */
 
+/* §8f rank 1: BMT row blocking inside the BMWs (else the BMTBs), fixed_interval_row_direction_
+ * thread_blocking_operator.cc:198-480 with get_begin_{rows,nzs}_of_BMT_after_fixed_blocking_in_
+ * row_direction_{in,relative_to}_{BMTB,BMW}.cc and get_begin_BMTs_of_specific_parent_after_blocking_
+ * in_row_direction.cc.  Rows: BMTs start at first + k*rb inside each parent (+ row_num at the
+ * end; relative: minus the parent's first row, no end).  Nzs: each parent opens a BMT at its
+ * first nz, a new one after every rb rows that do not end the parent (+ the parents' last nz;
+ * relative: from 0, no end).  Parent first_BMT_indices: BMTs per parent, prefix-summed. */
+int or_bmt_in_parent(or_set *s, int rb, int rrel, int nrel) {
+    const char *pp = get(s, "WARP_META", "first_row_indices", 0) ? "WARP_META" : "TBLOCK_META";
+    const char *tag = pp[0] == 'W' ? "BMW" : "BMTB";
+    or_array *PR = get(s, pp, "first_row_indices", 0), *PZ = get(s, pp, "first_nz_indices", 0);
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    if (!PR || !PZ || !R || rb < 1) return fail(s, "BMT blocking in a parent needs BMTB/BMW row blocks");
+    uint64_t rn = row_num_of(s);
+    uint64_t *cnt = row_nnz(R->u, R->len, rn);
+    vu ar = {0}, rr = {0}, az = {0}, rz = {0}, pb = {0};
+    vu_push(&pb, 0);
+    for (uint64_t j = 0; j + 1 < PR->len; j++) {
+        uint64_t f = PR->u[j], nx = PR->u[j + 1], nbmt = 0;
+        for (uint64_t r = f; r < nx; r += (uint64_t)rb) {
+            vu_push(&ar, r);
+            vu_push(&rr, r - f);
+            nbmt++;
+        }
+        uint64_t rc = 0, nz = 0;
+        vu_push(&az, PZ->u[j]);
+        vu_push(&rz, 0);
+        for (uint64_t i = f; i < nx; i++) {
+            rc++;
+            nz += cnt[i];
+            if (rc == (uint64_t)rb && i != nx - 1) {
+                vu_push(&az, PZ->u[j] + nz);
+                vu_push(&rz, nz);
+                rc = 0;
+            }
+        }
+        vu_push(&pb, pb.p[pb.n - 1] + nbmt);
+    }
+    free(cnt);
+    vu_push(&ar, rn);
+    vu_push(&az, PZ->u[PZ->len - 1]);
+    char k1[64], k2[64];
+    snprintf(k1, sizeof k1, "first_row_indices_relative_to_%s", tag);
+    snprintf(k2, sizeof k2, "first_nz_indices_relative_to_%s", tag);
+    put_u(s, "THREAD_META", "first_row_indices", 0, ar.p, ar.n);
+    if (rrel) put_u(s, "THREAD_META", k1, 0, rr.p, rr.n);
+    else free(rr.p);
+    put_u(s, "THREAD_META", "first_nz_indices", 0, az.p, az.n);
+    if (nrel) put_u(s, "THREAD_META", k2, 0, rz.p, rz.n);
+    else free(rz.p);
+    put_u(s, pp, "first_BMT_indices", 0, pb.p, pb.n);
+    return 0;
+}
+
 /* §8f rank 3: fixed_interval_row_matrix_div_operator on sub-matrix 0
  * (operator/fixed_interval_row_matrix_div_operator.cc:61-150 validity + run order;
  * transform_step/modify_{row,col}_{start,end}_boundary_after_fixed_div_in_row_direction.cc,
@@ -1160,6 +1214,15 @@ int or_row_nz_div(or_set *s, uint64_t init, uint64_t mx, uint64_t rate) {
 }
 
 int or_pipeline(or_set *s, const char *name, int p0, int p1) {
+    if (!strcmp(name, "tblock_thread_total")) { /* BMTB rows p0, BMT rows p1 inside them (relative too) */
+        if (or_row_dir_tblock_blocking(s, p0)) return -1;
+        return or_bmt_in_parent(s, p1 > 0 ? p1 : 1, 1, 1);
+    }
+    if (!strcmp(name, "tblock_warp_thread_total")) { /* BMTB rows p0, BMW rows 8, BMT rows p1 in the BMWs */
+        if (or_row_dir_tblock_blocking(s, p0)) return -1;
+        if (or_row_dir_warp_blocking(s, 8)) return -1;
+        return or_bmt_in_parent(s, p1 > 0 ? p1 : 1, 1, 1);
+    }
     if (!strcmp(name, "row_div")) /* p0 = fixed_row_interval_size */
         return or_fixed_interval_row_div(s, (uint64_t)p0);
     if (!strcmp(name, "row_nz_div")) /* p0 = init window, p1 = max window; expansion rate 2 */

@@ -87,6 +87,7 @@ int or_balanced_row_dir_thread_blocking(or_set *s, uint64_t nnz_per_bmt);  /* A1
 int or_merge_path(or_set *s, const char *pos, uint64_t work_size);         /* A11 */
 int or_interlance_storage_global(or_set *s);                               /* §8f rank 2 */
 int or_bmw_relative_to_bmtb(or_set *s, int rb);                            /* §8f rank 1 */
+int or_bmt_in_parent(or_set *s, int rb, int rrel, int nrel);               /* §8f rank 1 */
 int or_fixed_interval_row_div(or_set *s, uint64_t gap);                    /* §8f rank 3 */
 int or_row_nz_div(or_set *s, uint64_t init, uint64_t max_gap, uint64_t rate); /* §8f rank 3 */
 int or_index_compression(const uint64_t *a, uint64_t n, int type_ori, int branch_max, int *kind,

@@ -280,6 +280,36 @@ cases.append({
     },
 })
 
+# §8f rank 1, BMTs inside parents (fixed_interval_row_direction_thread_blocking_operator.cc
+# :198-480).  ex1 row nnz [2,0,3,1,5,0], BMTBs of 4 rows: [0,4) [4,6), first nz 0 | 6 | 11.
+# BMTs of 3 rows start at 0, 3 | 4 (+ row_num 6); relative 0, 3 | 0.  Nz starts: each parent
+# opens at its first nz; after rows 0-2 (not the parent's last row) a new BMT at 0+5 = 5;
+# BMTB 1 opens at 6, its 2 rows never reach 3 -> [0, 5, 6, 11]; relative 0, 5 | 0;
+# BMTs per BMTB 2 | 1 -> first_BMT_indices [0, 2, 3]
+TB = "TBLOCK_META_"
+cases.append({
+    "matrix": "ex1", "pipeline": "tblock_thread_total", "p0": 4, "p1": 3,
+    "expect": {
+        T + "first_row_indices_0": [0, 3, 4, 6],
+        T + "first_row_indices_relative_to_BMTB_0": [0, 3, 0],
+        T + "first_nz_indices_0": [0, 5, 6, 11],
+        T + "first_nz_indices_relative_to_BMTB_0": [0, 5, 0],
+        TB + "first_BMT_indices_0": [0, 2, 3],
+    },
+})
+# the same inside BMWs of 8 rows (one per BMTB here), one row per BMT: a BMT opens after
+# every row that does not end its BMW -> nz starts 0, 2, 2, 5 | 6, 11 (+ 11)
+cases.append({
+    "matrix": "ex1", "pipeline": "tblock_warp_thread_total", "p0": 4, "p1": 1,
+    "expect": {
+        T + "first_row_indices_0": [0, 1, 2, 3, 4, 5, 6],
+        T + "first_row_indices_relative_to_BMW_0": [0, 1, 2, 3, 0, 1],
+        T + "first_nz_indices_0": [0, 2, 2, 5, 6, 11, 11],
+        T + "first_nz_indices_relative_to_BMW_0": [0, 2, 2, 5, 0, 5],
+        W + "first_BMT_indices_0": [0, 4, 6],
+    },
+})
+
 out = {"matrices": {"ex1": EX1, "ex2": EX2, "ex3": EX3, "ex4": EX4}, "cases": cases}
 path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hand_plans.json")
 with open(path, "w") as f:

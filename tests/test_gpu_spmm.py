@@ -23,7 +23,8 @@ PIPES = [("thread_total", 4, 1), ("thread_total", 8, 1), ("warp_total", 0, 1), (
          ("thread_bit_map", 4, 1), ("warp_segment", 4, 1), ("tblock_warp_total", 4, 1),
          ("tblock_warp_total", 16, 1), ("balanced_warp_total", 256, 1),
          ("merge_path", 1024, 1), ("merge_path", 64, 1), ("merge_path", 7, 3), ("merge_path", 4096, 2),
-         ("balanced_block_total", 512, 1), ("balanced_thread_total", 64, 1)]
+         ("balanced_block_total", 512, 1), ("balanced_thread_total", 64, 1),
+         ("tblock_thread_total", 16, 1), ("tblock_thread_total", 20, 3), ("tblock_warp_thread_total", 16, 2)]
 BALANCED = ("balanced_warp_total", "balanced_block_total", "balanced_thread_total")
 TOL = {"f32": 1e-3, "f16": 1e-1}
 

@@ -46,7 +46,8 @@ def product_plan(M, K, row, col, val, name, N, p0=0, p1=0):
 
 def compare(M, K, row, col, val, name, N, p0=0, p1=0):
     exp, err = ofi.run_pipeline(M, K, row, col, val, name, oracle_params(name, N, p0, p1),
-                                p1 if name in ("merge_path", "tblock_warp_total_relative") else 0)
+                                p1 if name in ("merge_path", "tblock_warp_total_relative", "tblock_thread_total",
+                                               "tblock_warp_thread_total") else 0)
     if err is not None:
         with pytest.raises(gsa.GsError):
             product_plan(M, K, row, col, val, name, N, p0, p1)
@@ -78,7 +79,10 @@ PIPES = [("thread_total", 32, 4, 1), ("thread_total", 8, 8, 1), ("warp_total", 3
          ("tblock_bit_map", 32, 4, 1), ("balanced_block_total", 32, 64, 1), ("balanced_block_total", 8, 7, 1),
          ("balanced_thread_total", 8, 16, 1), ("merge_path", 8, 16, 1), ("merge_path", 8, 7, 2),
          ("merge_path", 32, 5, 3), ("merge_path", 8, 1, 1), ("merge_path", 8, 1024, 1),
-         ("tblock_warp_total_relative", 32, 20, 2), ("tblock_warp_total_relative", 32, 7, 3)]
+         ("tblock_warp_total_relative", 32, 20, 2), ("tblock_warp_total_relative", 32, 7, 3),
+         ("tblock_thread_total", 32, 16, 1), ("tblock_thread_total", 32, 20, 3), ("tblock_thread_total", 8, 5, 7),
+         ("tblock_warp_thread_total", 32, 16, 1), ("tblock_warp_thread_total", 32, 20, 3),
+         ("tblock_warp_thread_total", 8, 33, 5)]
 
 # col-direction pipelines need rows long enough for the 64-nnz padding rule
 COL_PIPES = [("warp_bit_map", 32, 4, 1), ("warp_bit_map", 8, 4, 2), ("warp_bit_map", 1, 4, 1),
@@ -126,7 +130,8 @@ def test_hand_derived_fixtures_through_product():
             "merge_path": (8, 0, 1), "balanced_block_total": (32, 0, 1), "balanced_thread_total": (8, 0, 1),
             "warp_bit_map_interleaved": (32, 4, 1), "tblock_warp_total_relative": (32, 4, 2),
             "tblock_warp_total": (32, 4, 1), "balanced_warp_total": (32, 16, 1),
-            "warp_bit_map": (32, 4, 1), "tblock_bit_map": (32, 4, 1)}
+            "warp_bit_map": (32, 4, 1), "tblock_bit_map": (32, 4, 1),
+            "tblock_thread_total": (32, 4, 1), "tblock_warp_thread_total": (32, 4, 1)}
     for case in g["cases"]:
         m = g["matrices"][case["matrix"]]
         row = np.array([e[0] for e in m["entries"]], np.uint64)
@@ -138,9 +143,10 @@ def test_hand_derived_fixtures_through_product():
         else:
             N, p0, p1 = back[name]
             if name in ("tblock_warp_total", "balanced_warp_total", "merge_path", "balanced_block_total",
-                        "balanced_thread_total", "tblock_warp_total_relative"):
+                        "balanced_thread_total", "tblock_warp_total_relative", "tblock_thread_total",
+                        "tblock_warp_thread_total"):
                 p0 = case["p0"]
-            if name in ("merge_path", "tblock_warp_total_relative"):
+            if name in ("merge_path", "tblock_warp_total_relative", "tblock_thread_total", "tblock_warp_thread_total"):
                 p1 = case["p1"]
         if case.get("expect_error"):
             with pytest.raises(gsa.GsError):
