@@ -809,6 +809,8 @@ __device__ __forceinline__ uint32_t b_piece(uint32_t k, uint32_t p) {
 
 // waves per role: compute 0..5, B loaders 6..9, entry loaders 10..15
 constexpr int kMfmaWaves = 16, kMfmaCompute = 6, kMfmaBWaves = 4, kMfmaAWaves = 6;
+// GLDS: two waves issue the B rows (LDS-DMA), the other eight load and scatter entries
+constexpr int kMfmaBWavesG = 2, kMfmaAWavesG = 8;
 
 // STAMPS (diagnostic build only, gs_debug_mfma_timeline): lane 0 of the first
 // compute / B / entry wave records s_memtime at phase boundaries
@@ -827,7 +829,8 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     constexpr uint32_t RS = 2 * KC + 32;              // dense image row stride
     constexpr uint32_t NT = 64 * kMfmaWaves;
     constexpr uint32_t WC = kMfmaCompute;
-    constexpr uint32_t NBT = 64 * kMfmaBWaves, NAT = 64 * kMfmaAWaves;  // B / entry loader threads
+    constexpr uint32_t BWV = GLDS ? kMfmaBWavesG : kMfmaBWaves;
+    constexpr uint32_t NBT = 64 * BWV, NAT = 64 * (GLDS ? kMfmaAWavesG : kMfmaAWaves);  // B / entry threads
     constexpr uint32_t szB = KC * RB;
     constexpr uint32_t NB = szB / 16 / NBT;           // B units per B thread per chunk
     static_assert(szB % (16 * NBT) == 0, "whole B units per B thread");
@@ -840,9 +843,9 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     constexpr uint32_t NBUF = GLDS ? 3u : 2u, NDI = GLDS ? 2u : 3u;
     const uint32_t oD = NBUF * szB;                   // dense images follow the B buffers
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    const uint32_t role = wv < WC ? 0u : (wv < WC + kMfmaBWaves ? 1u : 2u);  // wave-uniform
+    const uint32_t role = wv < WC ? 0u : (wv < WC + BWV ? 1u : 2u);  // wave-uniform
     const uint32_t bt = tid - 64 * WC;                // B thread index (role 1)
-    const uint32_t at = tid - 64 * (WC + kMfmaBWaves);  // entry thread index (role 2)
+    const uint32_t at = tid - 64 * (WC + BWV);         // entry thread index (role 2)
     // K-split: workgroup (g, sp) takes chunks [j0, j0 + ncl) of BMTB g
     const uint32_t g = blockIdx.x / nsplit, sp = blockIdx.x % nsplit;
     const uint32_t j0 = sp * ncs, ncl = min(nc, j0 + ncs) - j0;
@@ -857,7 +860,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     // 2+2j chunk j's work done, 3+2j after its barrier (j < 9); slot 63 end
 #define GS_STAMP(i)                                                                               \
     if constexpr (STAMPS) {                                                                       \
-        if ((tid == 0 || tid == 64 * WC || tid == 64 * (WC + kMfmaBWaves)) && (i) < 21u)          \
+        if ((tid == 0 || tid == 64 * WC || tid == 64 * (WC + BWV)) && (i) < 21u)                  \
             lst[(i) + 21u * role] = __builtin_amdgcn_s_memtime();                                 \
     }
     GS_STAMP(0u);
@@ -977,7 +980,8 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         for (uint32_t j = 0; j < ncl; j++) {
             if (j + 2 < ncl) {
                 issue(j + 2);
-                __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"(NB) : "memory");
+                // chunk j+1 retired; vmcnt holds at most 63 (a larger NB waits for part of j+2 too)
+                __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"(NB < 63u ? NB : 63u) : "memory");
             } else {
                 __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }

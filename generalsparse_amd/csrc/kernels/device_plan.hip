@@ -187,7 +187,7 @@ bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uin
 // local_col), val[] = 8 x f16; the last group is padded with (row R, value 0),
 // row R being the kernel's zero row.
 struct mfma_tiles {
-    uint32_t lgKC = 0, nc = 0, RT = 0, RMAX = 0, MAXA = 0;
+    uint32_t lgKC = 0, nc = 0, RT = 0, RMAX = 0, MAXA = 0, gmax = 0;
     size_t lds_bytes = 0;
     std::vector<uint32_t> seg_start;  // in groups
     std::vector<uint16_t> pos, val;   // 8 u16 per group each, + one spare group
@@ -292,6 +292,7 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
         if ((size_t)gsk::kMfmaCompute * RT * CT * 1024 > mfma_lds_bytes(lg, CT, (uint32_t)rmax)) continue;
         t.lgKC = lg; t.nc = (uint32_t)nc; t.RT = RT; t.RMAX = (uint32_t)rmax;
         t.MAXA = gmax <= kMfmaAThreads ? 1 : 2;
+        t.gmax = (uint32_t)gmax;
         t.lds_bytes = mfma_lds_bytes(lg, CT, (uint32_t)rmax);
         break;
     }
@@ -485,7 +486,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
         d.mfma = true;
         d.lds_N = Nd;
         d.KC = 1u << t.lgKC; d.nc = t.nc; d.maxr = t.RT; d.rpw_max = t.RMAX; d.RSB = t.lgKC;
-        d.seg_cap = t.MAXA;
+        d.seg_cap = t.gmax;  // entry groups per chunk (max): the launch picks MAXA per variant
         // K-split: enough workgroups per row block to cover the CUs, at least one chunk each
         const uint64_t nb = m.u(TBLOCK_META, "first_row_indices", sb).size() - 1;
         // auto: split only when the row blocks cover under half the CUs (the slab
@@ -822,7 +823,9 @@ void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *
 template <int CT, int RT>
 void launch_mfma_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N,
                     hipStream_t s) {
-    const bool two = p.dev.seg_cap > 1;  // entry groups per thread per chunk
+    // entry groups per thread per chunk: the GLDS variant has 9 entry waves, the other 6
+    const uint32_t nat = 64u * (get_config().MFMA_GLDS ? gsk::kMfmaAWavesG : gsk::kMfmaAWaves);
+    const bool two = p.dev.seg_cap > nat;
     switch (p.dev.RSB) {                  // log2 KC
         case 10: two ? launch_mfma_k<CT, RT, 10, 2>(p, a, B, C, N, s) : launch_mfma_k<CT, RT, 10, 1>(p, a, B, C, N, s); break;
         case 9: two ? launch_mfma_k<CT, RT, 9, 2>(p, a, B, C, N, s) : launch_mfma_k<CT, RT, 9, 1>(p, a, B, C, N, s); break;
@@ -856,7 +859,7 @@ void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N
                  (d.RSB == 8 || d.RSB == 9),
              "timeline build exists for N=32 matrix-core plans with 17..48-row BMTBs, KC 256/512 only");
     const device_arrays &a = d.replicas[0];
-    const bool two = d.seg_cap > 1;
+    const bool two = d.seg_cap > kMfmaAThreads;
     auto kern = d.maxr == 2 ? (d.RSB == 9 ? timeline_kernel<2, 9>(two) : timeline_kernel<2, 8>(two))
                             : (d.RSB == 9 ? timeline_kernel<3, 9>(two) : timeline_kernel<3, 8>(two));
     const size_t lds = d.lds_bytes;
