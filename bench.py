@@ -39,7 +39,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=500)  # clocks settle over the first ~1000 launches
     ap.add_argument("--pipeline", default="auto",
                     help="plan pipeline, or 'auto' = best of the candidates (obtain_result.py takes the max)")
     ap.add_argument("--rotation-mb", type=float, default=640.0)
