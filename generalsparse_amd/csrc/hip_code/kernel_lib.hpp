@@ -1689,15 +1689,54 @@ __global__ __launch_bounds__(256) void k_merge_fixup(const uint32_t *__restrict_
     const uint32_t total = n_waves * N;
     for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
         const uint32_t g = e / N, c = e % N;
+        // every load of the common case (a chain of <= 8 waves) is issued at once, before
+        // any of them is tested: one memory latency instead of a chain of dependent ones
+        // (the records were written by other XCDs' waves in the previous kernel)
         const uint32_t r = rec_row[g];
-        if (r == 0xffffffffu || (g > 0 && rec_row[g - 1] == r)) continue;
+        const uint32_t rp = g > 0 ? rec_row[g - 1] : 0xffffffffu;
+        uint32_t rr[8];
+        float v[8], hv[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const bool in = g + k < n_waves, in1 = g + k + 1 < n_waves;
+            rr[k] = in ? rec_row[g + k] : 0xffffffffu;
+            v[k] = in ? rec[(size_t)(g + k) * N + c] : 0.f;
+            hv[k] = in1 ? head_rec[(size_t)(g + k + 1) * N + c] : 0.f;
+        }
+        if (r == 0xffffffffu || rp == r) continue;
+        // sum the open partials in wave order, then the closing wave's head partial
         float s = 0.f;
         uint32_t h = g;
-        while (h < n_waves && rec_row[h] == r) {
-            s += rec[(size_t)h * N + c];
-            h++;
+        bool open = true;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            if (open && rr[k] == r) {
+                s += v[k];
+                h++;
+            } else {
+                open = false;
+            }
         }
-        if (h < n_waves) s += head_rec[(size_t)h * N + c];
+        while (open) {  // chains past 8 waves (long rows): 8 waves per step
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const bool in = h + k < n_waves;
+                rr[k] = in ? rec_row[h + k] : 0xffffffffu;
+                v[k] = in ? rec[(size_t)(h + k) * N + c] : 0.f;
+            }
+            const uint32_t h0 = h;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                if (open && rr[k] == r) {
+                    s += v[k];
+                    h++;
+                } else {
+                    open = false;
+                }
+            }
+            if (h == h0) open = false;
+        }
+        if (h < n_waves) s += h - g <= 8 ? hv[h - g - 1] : head_rec[(size_t)h * N + c];
         C[(size_t)r * N + c] = (VT)s;
     }
 }
