@@ -1,6 +1,7 @@
 """A/B of a launch-time config switch (diagnostic).
 usage: ab_config.py KEY v0 v1 [pipeline p0 p1]   (C2)
        WL=c4 ab_config.py MP_WPE 0 6 merge_path 512 1   (C4 stand-in, fp32 N=8)
+       WL=c3 ab_config.py NM_NSPLIT 1 2 col_direction_nm 32 1   (C3 2:4, fp16 N=128)
 Times 200 rotated SpMMs per setting (HIP events, interleaved settings x3) and checks
 every setting's C against the first (bit-exact expected)."""
 import os
@@ -17,7 +18,11 @@ pipe = sys.argv[4] if len(sys.argv) > 4 else "tblock_warp_total"
 p0 = int(sys.argv[5]) if len(sys.argv) > 5 else 20
 p1 = int(sys.argv[6]) if len(sys.argv) > 6 else 2
 WL = os.environ.get("WL", "c2")
-if WL == "c4":
+if WL == "c3":
+    M, K, N = 28672, 7168, 128
+    row, col, val = ds.two_four(M, K, 30)
+    dt, tdt = "f16", torch.float16
+elif WL == "c4":
     M = K = 1000005
     N = 8
     row, col, val = ds.rmat(M, 3105536, 1, symmetric=False)
@@ -28,7 +33,7 @@ else:
     row, col, val = ds.pruned_weight(M, K, 0.7, 13)
     dt, tdt = "f16", torch.float16
 plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline(pipe, N, p0, p1).compile().upload(dt, 0)
-reps = 12
+reps = 3 if WL == "c3" else 12
 for _ in range(reps - 1):
     plan.add_replica()
 Bs = [torch.randn((K, N), device="cuda", dtype=tdt) for _ in range(reps)]
