@@ -592,8 +592,9 @@ int gs_index_compression_of_array(const uint64_t *a, uint64_t n, int type_ori, i
 int gs_plan_save(gs_plan_t *p, const char *path) {
     return guard([&] {
         GS_CHECK(p && path, "null argument");
-        GS_CHECK(!divided(p), "plan files hold undivided plans");
-        gs::save_plan(p->st, path);
+        std::vector<const gs::plan_state *> ks;
+        for (gs::plan_state *s : kernel_states(p)) ks.push_back(s);
+        gs::save_plan(ks, path);
     });
 }
 
@@ -602,7 +603,16 @@ int gs_plan_load(const char *path, gs_plan_t **out) {
         GS_CHECK(path && out, "null argument");
         auto *p = new gs_plan;
         try {
-            gs::load_plan(p->st, path);
+            std::vector<std::pair<int, gs::kernel_spec>> specs;
+            std::string pipeline;
+            auto m = gs::load_plan(path, specs, pipeline);
+            init_plan(p->st, m);
+            p->st.pipeline = pipeline;
+            for (auto &ks : specs) {
+                gs::plan_state &st = state_of(p, ks.first);
+                st.pipeline = pipeline;
+                st.cg->restore_compiled(ks.second);
+            }
         } catch (...) {
             delete p;
             throw;

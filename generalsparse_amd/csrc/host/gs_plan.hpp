@@ -60,8 +60,11 @@ struct plan_state {
 };
 
 // plan_io.cc: binary plan files
-void save_plan(const plan_state &p, const std::string &path);
-void load_plan(plan_state &p, const std::string &path);
+// one file holds every kernel of a plan (one per sub-matrix of a row division); load
+// returns the metadata set and the (sub-matrix id, kernel spec) list
+void save_plan(const std::vector<const plan_state *> &kernels, const std::string &path);
+std::shared_ptr<meta_data_set> load_plan(const std::string &path, std::vector<std::pair<int, kernel_spec>> &specs,
+                                         std::string &pipeline);
 
 // device_plan.hip
 void upload_plan(plan_state &p, int dtype, int device);

@@ -1,8 +1,10 @@
 // plan_io.cc -- binary plan files: one file per compiled plan
 // instead of the reference's text data_source/<id>/ directory (metadata_set.cc:517-571
 // writes one number per line with endl flushes and sleep(1) calls).  Layout, all little
-// endian: "GSPLAN01", the kernel spec the code generator selected, the plan's scalars,
-// then every metadata array as (pos, name, sub, is_float, data_type, len, payload u64/f64).
+// endian: "GSPLAN02", the number of kernels, per kernel its sub-matrix id and the kernel
+// spec the code generator selected (one per sub-matrix of a row division, §8f rank 3),
+// the pipeline and matrix names, then every metadata array as (pos, name, sub, is_float,
+// data_type, len, payload u64/f64).  "GSPLAN01" files (one kernel, sub-matrix 0) still load.
 #include "gs_plan.hpp"
 
 #include <cstdio>
@@ -34,24 +36,48 @@ struct reader {
     }
 };
 
-const char kMagic[8] = {'G', 'S', 'P', 'L', 'A', 'N', '0', '1'};
+const char kMagic1[8] = {'G', 'S', 'P', 'L', 'A', 'N', '0', '1'};
+const char kMagic2[8] = {'G', 'S', 'P', 'L', 'A', 'N', '0', '2'};
+
+void write_spec(writer &w, const kernel_spec &s) {
+    w.i64(s.family); w.i64(s.coarsen_factor); w.i64(s.sparse_coarsen_factor); w.i64(s.vector_width);
+    w.i64(s.warp_segment); w.i64(s.tblock_parent); w.i64(s.row_sorted); w.i64(s.bitmap_parent);
+    w.i64(s.merge_level); w.i64(s.work_size); w.i64(s.group_level); w.i64(s.interleaved);
+    w.u64(s.ref_grid[0]); w.u64(s.ref_grid[1]); w.u64(s.ref_block[0]); w.u64(s.ref_block[1]);
+    w.u64(s.arrays.size());
+    for (auto &a : s.arrays) w.str(a);
+}
+
+kernel_spec read_spec(reader &r) {
+    kernel_spec s;
+    s.family = (int)r.i64(); s.coarsen_factor = (int)r.i64(); s.sparse_coarsen_factor = (int)r.i64();
+    s.vector_width = (int)r.i64(); s.warp_segment = r.i64() != 0; s.tblock_parent = r.i64() != 0;
+    s.row_sorted = r.i64() != 0; s.bitmap_parent = (POS_TYPE)r.i64(); s.merge_level = (POS_TYPE)r.i64();
+    s.work_size = (int)r.i64(); s.group_level = (POS_TYPE)r.i64(); s.interleaved = r.i64() != 0;
+    s.ref_grid[0] = (unsigned)r.u64(); s.ref_grid[1] = (unsigned)r.u64();
+    s.ref_block[0] = (unsigned)r.u64(); s.ref_block[1] = (unsigned)r.u64();
+    const uint64_t na = r.u64();
+    GS_CHECK(na < 4096, "plan file: bad array list");
+    for (uint64_t i = 0; i < na; i++) s.arrays.push_back(r.str());
+    return s;
+}
 
 }  // namespace
 
-void save_plan(const plan_state &p, const std::string &path) {
-    GS_CHECK(p.cg && p.cg->is_compiled(), "save: compile the plan first");
+void save_plan(const std::vector<const plan_state *> &ks, const std::string &path) {
+    GS_CHECK(!ks.empty(), "save: no kernel");
+    for (auto *k : ks) GS_CHECK(k->cg && k->cg->is_compiled(), "save: compile the plan first");
+    const plan_state &p = *ks.front();
     FILE *f = std::fopen(path.c_str(), "wb");
     GS_CHECK(f, "cannot write " + path);
     writer w{f};
     try {
-        w.raw(kMagic, 8);
-        const kernel_spec &s = p.cg->get_kernel_spec();
-        w.i64(s.family); w.i64(s.coarsen_factor); w.i64(s.sparse_coarsen_factor); w.i64(s.vector_width);
-        w.i64(s.warp_segment); w.i64(s.tblock_parent); w.i64(s.row_sorted); w.i64(s.bitmap_parent);
-        w.i64(s.merge_level); w.i64(s.work_size); w.i64(s.group_level); w.i64(s.interleaved);
-        w.u64(s.ref_grid[0]); w.u64(s.ref_grid[1]); w.u64(s.ref_block[0]); w.u64(s.ref_block[1]);
-        w.u64(s.arrays.size());
-        for (auto &a : s.arrays) w.str(a);
+        w.raw(kMagic2, 8);
+        w.u64(ks.size());
+        for (auto *k : ks) {
+            w.i64(k->cg->get_sub_matrix_id());
+            write_spec(w, k->cg->get_kernel_spec());
+        }
         w.str(p.pipeline);
         w.str(p.meta->matrix_name);
         const auto keys = p.meta->keys();
@@ -76,29 +102,29 @@ void save_plan(const plan_state &p, const std::string &path) {
     GS_CHECK(std::fclose(f) == 0, "plan file: close failed");
 }
 
-void load_plan(plan_state &p, const std::string &path) {
+std::shared_ptr<meta_data_set> load_plan(const std::string &path, std::vector<std::pair<int, kernel_spec>> &specs,
+                                         std::string &pipeline) {
     FILE *f = std::fopen(path.c_str(), "rb");
     GS_CHECK(f, "cannot read " + path);
     reader r{f};
+    std::shared_ptr<meta_data_set> m;
     try {
         char mg[8];
         r.raw(mg, 8);
-        GS_CHECK(std::memcmp(mg, kMagic, 8) == 0, "not a generalsparse_amd plan file: " + path);
-        kernel_spec s;
-        s.family = (int)r.i64(); s.coarsen_factor = (int)r.i64(); s.sparse_coarsen_factor = (int)r.i64();
-        s.vector_width = (int)r.i64(); s.warp_segment = r.i64() != 0; s.tblock_parent = r.i64() != 0;
-        s.row_sorted = r.i64() != 0; s.bitmap_parent = (POS_TYPE)r.i64(); s.merge_level = (POS_TYPE)r.i64();
-        s.work_size = (int)r.i64(); s.group_level = (POS_TYPE)r.i64(); s.interleaved = r.i64() != 0;
-        s.ref_grid[0] = (unsigned)r.u64(); s.ref_grid[1] = (unsigned)r.u64();
-        s.ref_block[0] = (unsigned)r.u64(); s.ref_block[1] = (unsigned)r.u64();
-        const uint64_t na = r.u64();
-        GS_CHECK(na < 4096, "plan file: bad array list");
-        for (uint64_t i = 0; i < na; i++) s.arrays.push_back(r.str());
-        const std::string pipeline = r.str();
-        auto m = std::make_shared<meta_data_set>();
-        m->matrix_name = r.str();
-        const uint64_t nk = r.u64();
+        const bool v1 = std::memcmp(mg, kMagic1, 8) == 0;
+        GS_CHECK(v1 || std::memcmp(mg, kMagic2, 8) == 0, "not a generalsparse_amd plan file: " + path);
+        specs.clear();
+        const uint64_t nk = v1 ? 1 : r.u64();
+        GS_CHECK(nk >= 1 && nk < 4096, "plan file: bad kernel count");
         for (uint64_t i = 0; i < nk; i++) {
+            const int sub = v1 ? 0 : (int)r.i64();
+            specs.emplace_back(sub, read_spec(r));
+        }
+        pipeline = r.str();
+        m = std::make_shared<meta_data_set>();
+        m->matrix_name = r.str();
+        const uint64_t na = r.u64();
+        for (uint64_t i = 0; i < na; i++) {
             const POS_TYPE pos = (POS_TYPE)r.i64();
             const std::string name = r.str();
             const int sub = (int)r.i64();
@@ -116,21 +142,14 @@ void load_plan(plan_state &p, const std::string &path) {
                 m->add_element(pos, name, sub, std::make_shared<universal_array>(std::move(v), t));
             }
         }
-        for (auto &a : s.arrays) GS_CHECK(m->is_exist(a), "plan file lacks kernel array " + a);
-        p.meta = m;
-        p.cg = std::make_shared<code_generator>(m, 0);
-        p.cg->restore_compiled(s);
-        p.exec = std::make_shared<operator_executer>();
-        p.pipeline = pipeline;
-        p.M = m->scalar(GLOBAL_META, "origin_row_num", -1);
-        p.K = m->scalar(GLOBAL_META, "origin_col_num", -1);
-        p.nnz = m->scalar(GLOBAL_META, "origin_nnz_num", -1);
-        p.uploaded = false;
+        for (auto &ks : specs)
+            for (auto &a : ks.second.arrays) GS_CHECK(m->is_exist(a), "plan file lacks kernel array " + a);
     } catch (...) {
         std::fclose(f);
         throw;
     }
     std::fclose(f);
+    return m;
 }
 
 }  // namespace gs

@@ -497,3 +497,27 @@ def test_sub_matrix_kernels_match_oracle(mix, N, dtype):
     Cn = C.float().cpu().numpy()
     assert not np.isnan(Cn).any()
     check(Cn, ofi.spmm_ref(M, N, r, c, v, B, "f64"), dtype)
+
+
+def test_divided_plan_file_computes_the_same(tmp_path):
+    """a divided plan loaded from its binary file (every sub-matrix's kernel) gives
+    bit-identical C"""
+    M, K, N = 900, 400, 32
+    r, c, v = ds.random_rows(M, K, 14.0, seed=9, empty_frac=0.1)
+    keep = (r < 300) | (r >= 450)
+    r, c, v = r[keep], c[keep], v[keep]
+    plan = gsa.Plan.from_coo(M, K, r, c, v)
+    for i, s in enumerate(plan.divide_rows(150)):
+        plan.run_pipeline("merge_path" if i % 2 else "tblock_warp_total", N, 64 if i % 2 else 16, 1 if i % 2 else 2, sub=s)
+    plan.compile().upload("f16", 0)
+    f = tmp_path / "divided.gsplan"
+    plan.save(f)
+    q = gsa.Plan.load(f).upload("f16", 0)
+    B = torch.from_numpy(np.random.default_rng(3).uniform(-1, 1, (K, N)).astype(np.float16)).to(DEV)
+    C1 = torch.full((M, N), float("nan"), dtype=torch.float16, device=DEV)
+    C2 = torch.full((M, N), float("nan"), dtype=torch.float16, device=DEV)
+    plan.spmm(B, C=C1)
+    q.spmm(B, C=C2)
+    torch.cuda.synchronize()
+    assert not torch.isnan(C2).any()
+    assert torch.equal(C1, C2)

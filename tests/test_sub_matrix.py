@@ -159,12 +159,34 @@ def test_compile_needs_every_sub_matrix():
     for s in subs[1:]:
         p.run_pipeline("thread_total", 32, 4, 1, sub=s)
     p.compile()
-    with pytest.raises(gsa.GsError):  # emitted programs / plan files are one-kernel plans
+    with pytest.raises(gsa.GsError):  # emitted programs hold one kernel
         p.generate_program("/tmp/gs_never_written")
     with pytest.raises(gsa.GsError):
-        p.save("/tmp/gs_never_written.plan")
-    with pytest.raises(gsa.GsError):
         p.run_pipeline("warp_total", 32, 0, 1, sub=99)
+
+
+def test_divided_plan_file_round_trip(tmp_path):
+    """§8f ranks 3 + 4: one binary plan file holds every sub-matrix's kernel"""
+    r, c, v = random_coo(300, 90, 0.08, 7, empty=0.1)
+    keep = (r < 100) | (r >= 160)
+    r, c, v = r[keep], c[keep], v[keep]
+    p = gsa.Plan.from_coo(300, 90, r, c, v)
+    subs = p.divide_rows(60)
+    pipes = ["merge_path", "tblock_warp_total", "thread_total", "balanced_warp_total"]
+    for i, s in enumerate(subs):
+        p.run_pipeline(pipes[i % len(pipes)], 8, 16, 1, sub=s)
+    p.compile()
+    f = tmp_path / "divided.gsplan"
+    p.save(f)
+    q = gsa.Plan.load(f)
+    assert q.sub_matrices() == subs
+    a, b = p.arrays(), q.arrays()
+    assert sorted(a) == sorted(b)
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    ia, ib = p.info(), q.info()
+    for k in ("n_kernels", "rows", "cols", "nnz", "nnz_stored", "family", "kernel_name"):
+        assert ia[k] == ib[k], k
 
 
 # ---------------------------------------------------------------- row_nz_matrix_div_operator
