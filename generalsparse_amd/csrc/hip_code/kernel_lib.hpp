@@ -1169,6 +1169,142 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
 }
 
 // ---------------------------------------------------------------------------
+// k_mfma_wk -- BMTB row blocks on the matrix cores, one wave per k-step stream
+// (MFMA_WK): workgroup g owns BMTB g (R <= 16*RT rows); wave w owns the 32-column
+// k-steps w, w+16, ... of K and runs them start to finish on its own -- B rows of the
+// step and the step's entries into registers (four steps ahead), then its private LDS
+// stage: B slice stored (32-B pieces permuted by b_piece for conflict-free transposed
+// reads), entries scattered into a zeroed 32-column dense slice (row stride 80 B, row
+// R stays zero for MFMA rows >= R), fragments read, v_mfma_f32_16x16x32_f16, slice
+// rows cleared.  No workgroup barrier until the end, where the 16 partial tiles are
+// summed in wave order through LDS (deterministic) and rows < R stored.
+// Entries (upload layout): per (BMTB, k-step) a run of u32 = halfword index in the
+// slice (row*40 + col - 32*step) | f16 value << 16; seg[] the run starts.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kWkWaves = 16, kWkRss = 80, kWkRows = 33;
+
+template <int CT, int RT, int EMAX>
+__global__ __launch_bounds__(64 * kWkWaves) void k_mfma_wk(const uint32_t *__restrict__ bmtb_first_row,
+                                                          const uint32_t *__restrict__ seg,
+                                                          const uint32_t *__restrict__ ent,
+                                                          const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K,
+                                                          uint32_t N, uint32_t nsteps, uint32_t row_base) {
+    constexpr uint32_t RB = 32 * CT, UB = 2 * CT;
+    constexpr uint32_t BS = 32 * RB, DS = kWkRows * kWkRss, STG = BS + DS;
+    constexpr uint32_t NBU = (32 * UB + 63) / 64;  // B units per lane per step
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t g = blockIdx.x;
+    const uint32_t r0 = bmtb_first_row[g], R = bmtb_first_row[g + 1] - r0;
+    unsigned char *bb = lds + wv * STG;
+    unsigned char *dd = bb + BS;
+    const u32x4 zero4 = {0u, 0u, 0u, 0u};
+    for (uint32_t u = lane; u < DS / 16u; u += 64u) *reinterpret_cast<u32x4 *>(dd + u * 16u) = zero4;
+    const uint32_t nsw = nsteps > wv ? (nsteps - wv + kWkWaves - 1) / kWkWaves : 0u;  // this wave's steps
+    const uint32_t *segg = seg + (size_t)g * nsteps;
+    f4v acc[RT][CT];
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+    uint32_t arow[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++) {
+        const uint32_t row = 16u * rt + (lane & 15u);
+        arow[rt] = (row < R ? row : R) * kWkRss + 16u * (lane >> 4);
+    }
+    u32x4 b0[NBU], b1[NBU], b2[NBU], b3[NBU];
+    uint32_t e0[EMAX], e1[EMAX], e2[EMAX], e3[EMAX];
+#define GS_WK_LOAD(i, BV, EV)                                                                       \
+    {                                                                                             \
+        const uint32_t st_ = wv + (uint32_t)(i) * kWkWaves;                                       \
+        const bool live_ = (uint32_t)(i) < nsw;                                                   \
+        _Pragma("unroll") for (uint32_t j = 0; j < NBU; j++) {                                    \
+            const uint32_t u = lane + 64u * j, k = st_ * 32u + u / UB;                            \
+            BV[j] = live_ && u < 32u * UB && k < K                                                \
+                        ? *reinterpret_cast<const u32x4 *>(B + (size_t)k * N + (u % UB) * 8u)     \
+                        : zero4;                                                                  \
+        }                                                                                         \
+        const uint32_t s0_ = live_ ? segg[st_] : 0u, n_ = live_ ? segg[st_ + 1] - s0_ : 0u;       \
+        _Pragma("unroll") for (int j = 0; j < EMAX; j++) {                                        \
+            const uint32_t x = lane + 64u * j;                                                    \
+            EV[j] = x < n_ ? ent[s0_ + x] : 0xffffffffu;                                          \
+        }                                                                                         \
+    }
+#define GS_WK_STEP(i, BV, EV)                                                                       \
+    if ((uint32_t)(i) < nsw) {                                                                    \
+        _Pragma("unroll") for (uint32_t j = 0; j < NBU; j++) {                                    \
+            const uint32_t u = lane + 64u * j;                                                    \
+            if (u < 32u * UB) {                                                                   \
+                const uint32_t k = u / UB, sb = u % UB;                                           \
+                *reinterpret_cast<u32x4 *>(bb + k * RB + b_piece<CT>(k, sb >> 1) * 32u + (sb & 1u) * 16u) = BV[j]; \
+            }                                                                                     \
+        }                                                                                         \
+        _Pragma("unroll") for (int j = 0; j < EMAX; j++)                                          \
+            if (EV[j] != 0xffffffffu)                                                             \
+                *reinterpret_cast<uint16_t *>(dd + (EV[j] & 0xffffu) * 2u) = (uint16_t)(EV[j] >> 16); \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");                                    \
+        __builtin_amdgcn_wave_barrier();                                                          \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");                                    \
+        h8v av_[RT], bv_[CT];                                                                     \
+        _Pragma("unroll") for (int rt = 0; rt < RT; rt++) av_[rt] = *reinterpret_cast<const h8v *>(dd + arow[rt]); \
+        _Pragma("unroll") for (int ct = 0; ct < CT; ct++) {                                       \
+            s4v t_[2];                                                                            \
+            _Pragma("unroll") for (int h = 0; h < 2; h++) {                                       \
+                const uint32_t k = 8u * (lane >> 4) + 4u * h + ((lane & 15u) >> 2);               \
+                t_[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(                                  \
+                    (lds_s4v *)(bb + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u));      \
+            }                                                                                     \
+            __builtin_memcpy(&bv_[ct], t_, 16);                                                   \
+        }                                                                                         \
+        _Pragma("unroll") for (int rt = 0; rt < RT; rt++)                                         \
+            _Pragma("unroll") for (int ct = 0; ct < CT; ct++)                                     \
+                acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av_[rt], bv_[ct], acc[rt][ct], 0, 0, 0); \
+        /* the MFMAs consumed the reads: clear the slice rows the scatter can write */           \
+        for (uint32_t u = lane; u < R * 4u; u += 64u)                                             \
+            *reinterpret_cast<u32x4 *>(dd + (u >> 2) * kWkRss + (u & 3u) * 16u) = zero4;          \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");                                    \
+        __builtin_amdgcn_wave_barrier();                                                          \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");                                    \
+    }
+    GS_WK_LOAD(0, b0, e0);
+    GS_WK_LOAD(1, b1, e1);
+    GS_WK_LOAD(2, b2, e2);
+    GS_WK_LOAD(3, b3, e3);
+    for (uint32_t i = 0; i < nsw; i += 4) {
+        GS_WK_STEP(i, b0, e0);
+        GS_WK_LOAD(i + 4, b0, e0);
+        GS_WK_STEP(i + 1, b1, e1);
+        GS_WK_LOAD(i + 5, b1, e1);
+        GS_WK_STEP(i + 2, b2, e2);
+        GS_WK_LOAD(i + 6, b2, e2);
+        GS_WK_STEP(i + 3, b3, e3);
+        GS_WK_LOAD(i + 7, b3, e3);
+    }
+#undef GS_WK_STEP
+#undef GS_WK_LOAD
+    // fixed-order sum of the 16 waves' partial tiles
+    __syncthreads();
+    f4v *red = reinterpret_cast<f4v *>(lds);
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) red[((wv * RT + rt) * CT + ct) * 64u + lane] = acc[rt][ct];
+    __syncthreads();
+    const float *redf = reinterpret_cast<const float *>(lds);
+    for (uint32_t e = tid; e < (uint32_t)(RT * CT) * 256u; e += 64u * kWkWaves) {
+        const uint32_t cc = e & 15u, rr = (e >> 4) & 15u, tt = e >> 8;
+        const uint32_t rt = tt / CT, ct = tt % CT;
+        const uint32_t ln = 16u * (rr >> 2) + cc, i = rr & 3u;
+        float sum = 0.f;
+        for (uint32_t w = 0; w < kWkWaves; w++) sum += redf[(((w * RT + rt) * CT + ct) * 64u + ln) * 4u + i];
+        const uint32_t row = 16u * rt + rr;
+        if (row < R) C[(size_t)(row_base + r0 + row) * N + 16u * ct + cc] = (f16)sum;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_nm_mfma -- fixed_interval_col_direction BMTs that are 2:4 panels
 //  on the sparse matrix cores:
 // v_smfmac_f32_16x16x64_f16 multiplies a 16x64 A tile stored as 16x32 values

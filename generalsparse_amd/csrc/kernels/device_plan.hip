@@ -327,6 +327,47 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
     return true;
 }
 
+// ------------------------------------------------------------------ k_mfma_wk layout
+// per (BMTB g, 32-column k-step s): the entries of g's rows with columns in [32s, 32s+32),
+// row-major, as u32 = (local_row*40 + col - 32s) | f16 << 16; seg[g*nsteps + s] the starts.
+// emax = entries per lane per step (64 lanes) rounded up to 1, 2, 4 or 8.
+bool build_wk(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
+              const std::vector<uint64_t> &col, const universal_array &vals, uint64_t K, std::vector<uint32_t> &seg,
+              std::vector<uint32_t> &ent, uint32_t &emax, uint32_t &rt, std::string &why) {
+    const uint64_t nb = tb_rows.size() - 1, nsteps = (K + 31) / 32;
+    uint64_t rmax = 0;
+    for (uint64_t g = 0; g < nb; g++) rmax = std::max<uint64_t>(rmax, tb_rows[g + 1] - tb_rows[g]);
+    if (nb == 0 || rmax == 0 || rmax > 32) { why = "row blocks of 1..32 rows"; return false; }
+    rt = rmax > 16 ? 2u : 1u;
+    seg.assign(1, 0);
+    ent.clear();
+    uint64_t mx = 0;
+    std::vector<uint64_t> cur;
+    for (uint64_t g = 0; g < nb; g++) {
+        const uint64_t r0 = tb_rows[g], R = tb_rows[g + 1] - r0;
+        cur.assign(R, 0);
+        for (uint64_t i = 0; i < R; i++) cur[i] = row_ptr[r0 + i];
+        for (uint64_t st = 0; st < nsteps; st++) {
+            const uint64_t lim = 32 * (st + 1), before = ent.size();
+            for (uint64_t i = 0; i < R; i++) {
+                uint64_t e = cur[i];
+                for (; e < row_ptr[r0 + i + 1] && col[e] < lim; e++)
+                    ent.push_back((uint32_t)(i * 40 + (col[e] - 32 * st)) |
+                                  (uint32_t)f32_to_f16_bits((float)vals.read_float_from_arr(e)) << 16);
+                cur[i] = e;
+            }
+            mx = std::max<uint64_t>(mx, ent.size() - before);
+            GS_CHECK(ent.size() < 0xffffffffull, "k_mfma_wk: entry offsets exceed 32 bits");
+            seg.push_back((uint32_t)ent.size());
+        }
+    }
+    const uint64_t per = (mx + 63) / 64;
+    emax = per <= 1 ? 1 : per <= 2 ? 2 : per <= 4 ? 4 : per <= 8 ? 8 : 0;
+    if (!emax) { why = "k-steps too dense for the wave's entry registers"; return false; }
+    ent.push_back(0);
+    return true;
+}
+
 // ------------------------------------------------------------------ 2:4 panels
 // Block layout of k_nm_mfma (kernel_lib.hpp) from the plan's COO: every row is
 // cut into 64-column k-steps (the col-direction BMTs of a 2:4 row: 32 entries
@@ -479,6 +520,30 @@ void upload_plan(plan_state &p, int dtype, int device) {
         mfma_tiles t;
         std::string why;
         const uint32_t Nd = (uint32_t)cfg.DENSE_MATRIX_SIZE;
+        if (cfg.MFMA_WK && (Nd == 16 || Nd == 32)) {
+            // wave-owned k-steps (k_mfma_wk)
+            std::vector<uint32_t> seg, ent;
+            uint32_t emax = 0, rt = 0;
+            const auto &tbr = m.u(TBLOCK_META, "first_row_indices", sb);
+            if (build_wk(tbr, rp, col, *vals, p.K, seg, ent, emax, rt, why)) {
+                d.mfma = true;
+                d.wk = true;
+                d.lds_N = Nd;
+                d.maxr = rt;
+                d.wk_nb = (uint32_t)(tbr.size() - 1);
+                d.wk_steps = (uint32_t)((p.K + 31) / 32);
+                d.wk_emax = emax;
+                d.waves = gsk::kWkWaves;
+                const size_t stg = 32 * 2 * Nd + gsk::kWkRows * gsk::kWkRss;
+                d.lds_bytes = std::max<size_t>(gsk::kWkWaves * stg, (size_t)gsk::kWkWaves * rt * (Nd / 16) * 1024);
+                const size_t before = d.bytes_A;
+                a.t0 = dev_copy(d, to_u32(tbr, "BMTB first_row_indices"));
+                a.t1 = dev_copy(d, seg);
+                a.tcol = dev_copy(d, ent);
+                d.bytes_tile = d.bytes_A - before;
+                return true;
+            }
+        }
         const size_t budget = (size_t)std::min<int64_t>(cfg.SHARED_MEM_TOTAL_SIZE, 160 * 1024);
         if (!build_mfma_tiles(m.u(TBLOCK_META, "first_row_indices", sb), rp, col, *vals, p.K, Nd, budget,
                               cfg.MFMA_MAX_FILL, t, why))
@@ -915,9 +980,45 @@ void launch_nm(const plan_state &p, const device_arrays &a, const void *B, void 
     }
 }
 
+template <int CT, int RT, int EMAX>
+void launch_wk_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
+    const device_plan &d = p.dev;
+    auto kern = gsk::k_mfma_wk<CT, RT, EMAX>;
+    static std::mutex mu;
+    static std::map<int, size_t> granted;
+    {
+        std::lock_guard<std::mutex> l(mu);
+        size_t &g = granted[d.device];
+        if (g < d.lds_bytes) {
+            HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)d.lds_bytes));
+            g = d.lds_bytes;
+        }
+    }
+    hipLaunchKernelGGL(kern, dim3(d.wk_nb), dim3(64 * gsk::kWkWaves), d.lds_bytes, s, a.t0, a.t1,
+                       (const uint32_t *)a.tcol, B, C, (uint32_t)p.K, N, d.wk_steps, (uint32_t)d.row_base);
+    HIP_OK(hipGetLastError());
+}
+
+template <int CT, int RT>
+void launch_wk_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
+    switch (p.dev.wk_emax) {
+        case 1: launch_wk_k<CT, RT, 1>(p, a, B, C, N, s); break;
+        case 2: launch_wk_k<CT, RT, 2>(p, a, B, C, N, s); break;
+        case 4: launch_wk_k<CT, RT, 4>(p, a, B, C, N, s); break;
+        default: launch_wk_k<CT, RT, 8>(p, a, B, C, N, s); break;
+    }
+}
+
 void launch_mfma(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
     const gsk::f16 *b = (const gsk::f16 *)B;
     gsk::f16 *c = (gsk::f16 *)C;
+    if (p.dev.wk) {
+        const bool two = p.dev.maxr > 1;
+        if (N == 16) two ? launch_wk_rt<1, 2>(p, a, b, c, N, s) : launch_wk_rt<1, 1>(p, a, b, c, N, s);
+        else two ? launch_wk_rt<2, 2>(p, a, b, c, N, s) : launch_wk_rt<2, 1>(p, a, b, c, N, s);
+        return;
+    }
     switch (N / 16) {
         case 1: launch_mfma_ct<1>(p, a, b, c, N, s); break;
         case 2: launch_mfma_ct<2>(p, a, b, c, N, s); break;

@@ -328,6 +328,25 @@ def test_mfma_rows_match_oracle(pipe, N, glds, mfma_everywhere):
         assert 2 in used, used
 
 
+@pytest.mark.parametrize("N", [16, 32])
+@pytest.mark.parametrize("pipe", [("tblock_warp_total", 20, 2), ("block_total", 16, 1),
+                                  ("block_total", 7, 1), ("block_total", 32, 1)],
+                         ids=lambda p: f"{p[0]}-{p[1]}")
+def test_mfma_wk_matches_oracle(pipe, N, mfma_everywhere):
+    # opt-in wave-owned k-step kernel (MFMA_WK=1, k_mfma_wk): same results as the oracle
+    name, p0, p1 = pipe
+    gsa.set_config("MFMA_WK", 1)
+    try:
+        for case, M, K, row, col, val in mfma_cases():
+            plan, C, B = run(M, K, row, col, val, name, p0, p1, N, "f16")
+            v = val.astype(np.float16).astype(np.float32)
+            ref = ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64")
+            check(C, ref, "f16")
+            plan.free()
+    finally:
+        gsa.set_config("MFMA_WK", 0)
+
+
 def test_mfma_rows_known_answer_and_fallback(mfma_everywhere):
     M, K, N = 700, 9000, 32
     row, col, _ = ds.random_rows(M, K, 60.0, seed=8, empty_frac=0.1)
