@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--K", type=int, default=0)
     ap.add_argument("--N", type=int, default=0)
     ap.add_argument("--sparsity", type=float, default=0.7)
+    ap.add_argument("--config", action="append", default=[], metavar="KEY=INT",
+                    help="engine switch (gs_set_config_int), e.g. BM_VARIANT=1; repeatable")
     a = ap.parse_args()
     dflt = {"c1": (47894, 41550, 8), "c2": (5120, 5120, 32), "c3": (28672, 7168, 128), "c4": (1000005, 1000005, 8),
             "c4o": (3072441, 3072441, 8), "c5": (7168, 7168, 32)}[a.workload]
@@ -351,6 +353,9 @@ def main():
 
     import generalsparse_amd as gsa
     from generalsparse_amd import datasets as ds
+    for kv in args.config:
+        k, v = kv.split("=", 1)
+        gsa.set_config(k, int(v))
 
     if args.workload == "c5":
         run_c5(args, torch, gsa, ds, rank, world, local, dev, dist)

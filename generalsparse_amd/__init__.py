@@ -201,7 +201,8 @@ class Plan:
     def info(self):
         i = _lib.GsPlanInfo()
         _lib.check(self._L.gs_plan_info_get(self._h, ctypes.byref(i)))
-        return {k: (getattr(i, k).decode() if k == "kernel_name" else getattr(i, k)) for k, _ in i._fields_}
+        return {k: (getattr(i, k).decode() if k in ("kernel_name", "device_kernel") else getattr(i, k))
+                for k, _ in i._fields_}
 
     def keys(self):
         n = self._L.gs_plan_array_count(self._h)

@@ -809,12 +809,12 @@ __device__ __forceinline__ uint32_t b_piece(uint32_t k, uint32_t p) {
 
 // waves per role: compute 0..5, B loaders 6..9, entry loaders 10..15
 constexpr int kMfmaWaves = 16, kMfmaCompute = 6, kMfmaBWaves = 4, kMfmaAWaves = 6;
-// GLDS: two waves issue the B rows (LDS-DMA), the other eight load and scatter entries
+// GLDS = g > 0: g waves issue the B rows (LDS-DMA), the other 10 - g load and scatter entries
 constexpr int kMfmaBWavesG = 2, kMfmaAWavesG = 8;
 
 // STAMPS (diagnostic build only, gs_debug_mfma_timeline): lane 0 of the first
 // compute / B / entry wave records s_memtime at phase boundaries
-template <int CT, int RT, int LGKC, int MAXA, bool STAMPS = false, bool GLDS = false>
+template <int CT, int RT, int LGKC, int MAXA, bool STAMPS = false, int GLDS = 0>
 __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
     const uint32_t *__restrict__ seg_start,       // n_bmtb*nc+1 (groups)
@@ -829,8 +829,8 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     constexpr uint32_t RS = 2 * KC + 32;              // dense image row stride
     constexpr uint32_t NT = 64 * kMfmaWaves;
     constexpr uint32_t WC = kMfmaCompute;
-    constexpr uint32_t BWV = GLDS ? kMfmaBWavesG : kMfmaBWaves;
-    constexpr uint32_t NBT = 64 * BWV, NAT = 64 * (GLDS ? kMfmaAWavesG : kMfmaAWaves);  // B / entry threads
+    constexpr uint32_t BWV = GLDS ? GLDS : kMfmaBWaves;
+    constexpr uint32_t NBT = 64 * BWV, NAT = 64 * (GLDS ? 10 - GLDS : kMfmaAWaves);  // B / entry threads
     constexpr uint32_t szB = KC * RB;
     constexpr uint32_t NB = szB / 16 / NBT;           // B units per B thread per chunk
     static_assert(szB % (16 * NBT) == 0, "whole B units per B thread");
@@ -1299,6 +1299,251 @@ __global__ __launch_bounds__(64 * kWkWaves) void k_mfma_wk(const uint32_t *__res
         const uint32_t ln = 16u * (rr >> 2) + cc, i = rr & 3u;
         float sum = 0.f;
         for (uint32_t w = 0; w < kWkWaves; w++) sum += redf[(((w * RT + rt) * CT + ct) * 64u + ln) * 4u + i];
+        const uint32_t row = 16u * rt + rr;
+        if (row < R) C[(size_t)(row_base + r0 + row) * N + 16u * ct + cc] = (f16)sum;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_mfma_bitmap -- BMTB row blocks on the matrix cores from bitmap panels (the
+// default matrix-core layout of fp16 tblock/warp/block-total plans).
+// Upload layout (device_plan.hip build_bitmap_panels): per BMTB g and 32-column
+// k-step t one segment, 16-B aligned and at most 1 KB: R u32 row masks (bit c =
+// column 32t+c of that row holds an entry), then the entries' f16 values row
+// after row in column order; seg[g*nks + t] = its start in 16-B units.  A costs
+// 2 B per entry + 4 B per (row, k-step) instead of the 4 B per entry of a u16
+// CSR, and nothing is densified through LDS.
+// Workgroup = W waves over one BMTB; wave w owns k-steps w, w+W, ... and runs
+// them alone (no barrier in the loop): per k-step one LDS-DMA of its segment
+// into the wave's A ring (DA slots) and CT LDS-DMAs of the 32 B rows into its B
+// ring (DB slots, 32-B pieces XOR-permuted through the source address), issued
+// DA-1 / DB-1 k-steps ahead and retired by a counted vmcnt.  A fragments are
+// expanded in registers: lane (row r, k-group kg) takes byte kg of row r's mask,
+// its values' offset = the rows' popcounts scanned over 16 lanes by DPP + the
+// popcount of the lower bytes, reads each 4-column quad's values with one
+// (unaligned) ds_read_b64 and places them with two v_perm_b32 whose selectors
+// come from a 16-entry table in LDS.  B fragments by ds_read_b64_tr_b16.
+// v_mfma_f32_16x16x32_f16 into fp32 accumulators; the waves' partial tiles are
+// summed in wave order through LDS (deterministic).  Rows past R read mask 0.
+// Like every dense-tile kernel, a zero of the tile times a non-finite B value
+// gives NaN for the row block (MFMA_TILES=0 keeps the reference's
+// per-entry semantics).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kBmSeg = 1024;  // max bytes of one k-step segment (one LDS-DMA)
+
+// one 64-lane LDS-DMA of 16 B per lane: lane l's 16 bytes land at lds_dst + 16 l
+__device__ __forceinline__ void dma16(const void *gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until at most n vector-memory operations of this wave are outstanding
+// (n wave-uniform; above 15 the wait is for 15, i.e. for more than asked)
+__device__ __forceinline__ void vm_wait_dyn(uint32_t n) {
+    switch (n) {
+        case 0: vm_wait<0>(); break;
+        case 1: vm_wait<1>(); break;
+        case 2: vm_wait<2>(); break;
+        case 3: vm_wait<3>(); break;
+        case 4: vm_wait<4>(); break;
+        case 5: vm_wait<5>(); break;
+        case 6: vm_wait<6>(); break;
+        case 7: vm_wait<7>(); break;
+        case 8: vm_wait<8>(); break;
+        case 9: vm_wait<9>(); break;
+        case 10: vm_wait<10>(); break;
+        case 11: vm_wait<11>(); break;
+        case 12: vm_wait<12>(); break;
+        case 13: vm_wait<13>(); break;
+        case 14: vm_wait<14>(); break;
+        default: vm_wait<15>(); break;
+    }
+}
+
+// selectors of the quad expansion: nibble q (bit i = column i of the quad holds an
+// entry) -> two v_perm_b32 selectors over the quad's packed values (8 bytes):
+// half i of the output = packed half popcount(q & ((1 << i) - 1)) if bit i, else 0
+__device__ __forceinline__ uint2 bm_quad_selectors(uint32_t q) {
+    uint32_t s[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        uint32_t sel = 0;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint32_t i = 2u * j + h, r = __builtin_popcount(q & ((1u << i) - 1u));
+            const uint32_t lo = (q >> i) & 1u ? 2u * r : 12u, hi = (q >> i) & 1u ? 2u * r + 1u : 12u;
+            sel |= (lo | (hi << 8)) << (16 * h);
+        }
+        s[j] = sel;
+    }
+    return make_uint2(s[0], s[1]);
+}
+
+// DBG (diagnostic timing builds only, wrong results): 1 = window reads rounded down to
+// 8-B alignment, 2 = no A expansion (zero A fragments), 4 = no B fragment reads
+template <int CT, int RT, int W, int DA, int DB, int DBG = 0>
+__global__ __launch_bounds__(64 * W) void k_mfma_bitmap(const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
+                                                       const uint32_t *__restrict__ seg,  // n_bmtb*nks+1 (16-B units)
+                                                       const u32x4 *__restrict__ A,       // segments
+                                                       const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K,
+                                                       uint32_t N, uint32_t nks, uint32_t row_base) {
+    static_assert(DA >= DB && DB >= 2, "A ring at least as deep as the B ring");
+    constexpr uint32_t RB = 32 * CT, UB = 2 * CT;  // bytes / 16-B units per B row (N == 16*CT)
+    constexpr uint32_t SB = 32 * RB;               // B slot: the 32 rows of a k-step
+    constexpr uint32_t WL = DA * kBmSeg + DB * SB; // LDS per wave
+    constexpr uint32_t STEADY = (DB - 1) * (1 + CT);  // DMAs issued after B(i) once the rings run full
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t g = blockIdx.x;
+    const uint32_t r0 = bmtb_first_row[g], R = bmtb_first_row[g + 1] - r0;
+    const uint32_t ra = wv * WL, rb = ra + DA * kBmSeg;  // A ring, B ring (offsets in lds[])
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char *)lds;
+    uint2 *lut = reinterpret_cast<uint2 *>(lds + W * WL);
+    if (tid < 16u) lut[tid] = bm_quad_selectors(tid);
+    // this wave's k-steps t_i = (rot + wv + i*W) mod nks (i < nw <= 128): segment start /
+    // length in 16-B units.  rot staggers the workgroups that share an XCD's L2 (blocks
+    // b, b+8, ... under round-robin placement) over K, so most B rows a wave asks for were
+    // already fetched by a neighbour (speed only; any placement is correct).
+    const uint32_t nw = nks > wv ? (nks - wv + W - 1) / W : 0u;
+    const uint32_t rot = (uint32_t)(((uint64_t)((g >> 3) & 31u) * nks) >> 5);
+    const uint32_t *sg = seg + (size_t)g * nks;
+    uint32_t s_lo0 = 0, s_n0 = 0, s_lo1 = 0, s_n1 = 0;
+    if (lane < nw) {
+        uint32_t t = rot + wv + lane * W;
+        t = t >= nks ? t - nks : t;
+        s_lo0 = sg[t];
+        s_n0 = sg[t + 1] - s_lo0;
+    }
+    if (lane + 64u < nw) {
+        uint32_t t = rot + wv + (lane + 64u) * W;
+        t = t >= nks ? t - nks : t;
+        s_lo1 = sg[t];
+        s_n1 = sg[t + 1] - s_lo1;
+    }
+    asm volatile("" ::"v"(s_lo0), "v"(s_n0), "v"(s_lo1), "v"(s_n1));  // retire these loads before any DMA
+    __syncthreads();  // quad selectors written
+
+    auto issue_a = [&](uint32_t i) {  // k-step i's segment -> A slot i % DA
+        const uint32_t lo = i < 64u ? __builtin_amdgcn_readlane(s_lo0, i) : __builtin_amdgcn_readlane(s_lo1, i - 64u);
+        const uint32_t n = i < 64u ? __builtin_amdgcn_readlane(s_n0, i) : __builtin_amdgcn_readlane(s_n1, i - 64u);
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + ra + (i % DA) * kBmSeg);
+        if (lane < n) dma16(A + lo + lane, dst);
+    };
+    auto issue_b = [&](uint32_t i) {  // the 32 B rows of k-step i -> B slot i % DB
+        uint32_t t = rot + wv + i * W;
+        t = t >= nks ? t - nks : t;
+        const uint32_t k0 = t * 32u;
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + rb + (i % DB) * SB);
+#pragma unroll
+        for (uint32_t q = 0; q < CT; q++) {
+            const uint32_t u = q * 64u + lane, k = u / UB, s = u % UB;
+            const uint32_t kk = k0 + k < K ? k0 + k : K - 1u;
+            dma16(B + (size_t)kk * N + (b_piece<CT>(k, s >> 1) * 2u + (s & 1u)) * 8u, dst + q * 1024u);
+        }
+    };
+    // prologue = the issue pattern of iterations -(DA-1) .. -1
+    for (int v = -(DA - 1); v < 0; v++) {
+        const int ia = v + DA - 1, ib = v + DB - 1;
+        if ((uint32_t)ia < nw) issue_a((uint32_t)ia);
+        if (ib >= 0 && (uint32_t)ib < nw) issue_b((uint32_t)ib);
+    }
+
+    f4v acc[RT][CT];
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+    const uint32_t kg = lane >> 4;
+    const uint32_t lowmask = (1u << (8u * kg)) - 1u;
+
+    for (uint32_t i = 0; i < nw; i++) {
+        if (i + DA - 1 < nw) issue_a(i + DA - 1);
+        if (i + DB - 1 < nw) issue_b(i + DB - 1);
+        // retire k-step i: A(i) was issued before B(i), so waiting for B(i) covers both
+        if (i + DA - 1 < nw) {
+            vm_wait<STEADY>();
+        } else {
+            uint32_t n = 0;
+#pragma unroll
+            for (uint32_t j = 1; j < DB; j++) n += (i + DA - DB + j < nw ? 1u : 0u) + (i + j < nw ? CT : 0u);
+            vm_wait_dyn(n);
+        }
+        const unsigned char *sa = lds + ra + (i % DA) * kBmSeg;
+        const unsigned char *sb = lds + rb + (i % DB) * SB;
+        h8v bv[CT];
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) {
+            s4v t[2];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t k = 8u * kg + 4u * h + ((lane & 15u) >> 2);
+                t[h] = (DBG & 4) ? s4v{} : __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (lds_s4v *)(sb + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u));
+            }
+            __builtin_memcpy(&bv[ct], t, 16);
+        }
+        const unsigned char *vals = sa + 4u * R;
+        uint32_t rowbase = 0;
+        h8v av[RT];
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++) {
+            const uint32_t r = 16u * rt + (lane & 15u);
+            uint32_t wrd = *reinterpret_cast<const uint32_t *>(sa + 4u * r);
+            if (r >= R) wrd = 0u;
+            const uint32_t cnt = __builtin_popcount(wrd);
+            // inclusive scan of the rows' counts over each 16-lane row (lanes = rows)
+            uint32_t sc = cnt;
+            sc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sc, 0x111, 0xf, 0xf, true);
+            sc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sc, 0x112, 0xf, 0xf, true);
+            sc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sc, 0x114, 0xf, 0xf, true);
+            sc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sc, 0x118, 0xf, 0xf, true);
+            const uint32_t off = rowbase + sc - cnt + __builtin_popcount(wrd & lowmask);  // halves
+            if (rt + 1 < RT) rowbase += __builtin_amdgcn_readlane(sc, 15);
+            const uint32_t m8 = (wrd >> (8u * kg)) & 0xffu;
+            const uint32_t qa = m8 & 15u, qb = m8 >> 4;
+            const uint32_t offb = off + __builtin_popcount(qa);
+            const uint32_t am = (DBG & 1) ? ~7u : ~0u;
+            const uint2 wa = *reinterpret_cast<const uint2 *>(vals + ((2u * off) & am));   // unaligned ds_read_b64
+            const uint2 wb = *reinterpret_cast<const uint2 *>(vals + ((2u * offb) & am));
+            const uint2 la = lut[qa], lb = lut[qb];
+            uint32_t d[4];
+            d[0] = __builtin_amdgcn_perm(wa.y, wa.x, la.x);
+            d[1] = __builtin_amdgcn_perm(wa.y, wa.x, la.y);
+            d[2] = __builtin_amdgcn_perm(wb.y, wb.x, lb.x);
+            d[3] = __builtin_amdgcn_perm(wb.y, wb.x, lb.y);
+            __builtin_memcpy(&av[rt], d, 16);
+            if constexpr ((DBG & 2) != 0) av[rt] = h8v{};
+        }
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++)
+                acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[rt], bv[ct], acc[rt][ct], 0, 0, 0);
+    }
+    // fixed-order sum of the waves' partial tiles (every DMA was waited for above)
+    __syncthreads();
+    f4v *red = reinterpret_cast<f4v *>(lds);
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) red[((wv * RT + rt) * CT + ct) * 64u + lane] = acc[rt][ct];
+    __syncthreads();
+    const float *redf = reinterpret_cast<const float *>(lds);
+    for (uint32_t e = tid; e < (uint32_t)(RT * CT) * 256u; e += 64u * W) {
+        const uint32_t cc = e & 15u, rr = (e >> 4) & 15u, tt = e >> 8;
+        const uint32_t rt = tt / CT, ct = tt % CT;
+        const uint32_t ln = 16u * (rr >> 2) + cc, ii = rr & 3u;
+        float sum = 0.f;
+        for (uint32_t w = 0; w < (uint32_t)W; w++) sum += redf[(((w * RT + rt) * CT + ct) * 64u + ln) * 4u + ii];
         const uint32_t row = 16u * rt + rr;
         if (row < R) C[(size_t)(row_base + r0 + row) * N + 16u * ct + cc] = (f16)sum;
     }

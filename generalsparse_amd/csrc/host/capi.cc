@@ -494,6 +494,8 @@ int gs_plan_info_get(gs_plan_t *p, gs_plan_info *info) {
             info->lds_bytes = s.dev.lds_bytes;
             info->tile_bytes = s.dev.bytes_tile;
             info->ksplit = s.dev.ksplit;
+            const std::string dk = !s.dev.kernel.empty() ? s.dev.kernel : s.cg->get_kernel_spec().name();
+            std::strncpy(info->device_kernel, dk.c_str(), sizeof(info->device_kernel) - 1);
         }
     });
 }

@@ -96,6 +96,8 @@ void apply_kv(config_t &c, const std::string &k, const std::string &v) {
     else if (k == "MAX_DIV_TIMES_OF_DIV") c.MAX_DIV_TIMES_OF_DIV = i();
     else if (k == "MFMA_GLDS") c.MFMA_GLDS = i();
     else if (k == "MFMA_WK") c.MFMA_WK = i();
+    else if (k == "MFMA_BITMAP") c.MFMA_BITMAP = i() != 0;
+    else if (k == "BM_VARIANT") c.BM_VARIANT = i();
     else if (k == "FORMAT_OF_MTX") c.FORMAT_OF_MTX = v;
     else if (k == "PERFORMANCE_FLAG") c.PERFORMANCE_FLAG = v;
     else if (k == "Graph_Algorithm") c.Graph_Algorithm = v;

@@ -82,6 +82,8 @@ struct config_t {
     int64_t MFMA_MAX_FILL = 16;  // ... when (padded row-block area) / nnz <= this
     bool NM_MFMA = true;         // col-direction plans whose rows are 2:4 panels: sparse matrix cores (k_nm_mfma)
     int64_t MFMA_KSPLIT = 0;     // workgroups per row block (K ranges); 0 = fill the 256 CUs
+    bool MFMA_BITMAP = false;    // matrix-core row blocks from bitmap panels (k_mfma_bitmap; opt-in, slower on C2)
+    int64_t BM_VARIANT = 0;      // k_mfma_bitmap shape (device_plan.hip kBmVariant)
 };
 // Process-wide config: loaded once from $GS_CONFIG or ./global_config.json if
 // present (flat JSON object of scalars), defaults otherwise.

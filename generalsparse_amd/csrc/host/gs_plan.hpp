@@ -39,6 +39,9 @@ struct device_plan {
     bool nm = false;    // k_nm_mfma: 2:4 panels of a col-direction plan (A blocks in tcol; k-steps in KC)
     bool mfma = false;  // k_mfma_rows (uses KC, nc, lds_bytes; log2 KC in RSB; RT in maxr; RMAX in rpw_max)
     bool wk = false;    // k_mfma_wk (MFMA_WK): wave-owned k-steps; wk_nb row blocks, wk_steps steps, wk_emax
+    bool bm = false;    // k_mfma_bitmap: bitmap panels (t0 BMTB rows, t1 segment starts, tcol segments)
+    uint32_t bm_nks = 0, bm_variant = 0;
+    std::string kernel;  // the device kernel gs_spmm launches at the plan's N (empty: the family's)
     uint32_t wk_nb = 0, wk_steps = 0, wk_emax = 0;
     uint32_t ksplit = 1, ncs = 0;  // k_mfma_rows workgroups per row block, chunks per workgroup
     uint32_t ws_n = 0;             // bitmap family: dense width of the fp32 workspace

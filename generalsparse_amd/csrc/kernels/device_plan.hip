@@ -66,6 +66,51 @@ uint16_t f32_to_f16_bits(float f) {
     return b;
 }
 
+// Rows as the matrix-core layouts need them: each row's columns ascending and
+// distinct.  The reference accepts any column order inside a row and its gather
+// kernels add repeated coordinates, so entries are stably sorted by column and
+// repeated ones summed (in double, rounded to fp32 once).  rp is the CSR row
+// pointer of the plan's (row-sorted) COO.
+struct canon_rows {
+    std::vector<uint32_t> rp;
+    std::vector<uint64_t> col;
+    std::vector<float> val;
+};
+
+canon_rows canonical_rows(const std::vector<uint32_t> &rp, const std::vector<uint64_t> &col, const universal_array &vals) {
+    canon_rows c;
+    const uint64_t nr = rp.size() - 1;
+    c.rp.assign(nr + 1, 0);
+    c.col.reserve(col.size());
+    c.val.reserve(col.size());
+    std::vector<std::pair<uint64_t, uint64_t>> ent;  // (col, position)
+    for (uint64_t r = 0; r < nr; r++) {
+        bool ordered = true;
+        for (uint64_t e = rp[r] + 1; e < rp[r + 1]; e++) ordered &= col[e] > col[e - 1];
+        if (ordered) {
+            for (uint64_t e = rp[r]; e < rp[r + 1]; e++) {
+                c.col.push_back(col[e]);
+                c.val.push_back((float)vals.read_float_from_arr(e));
+            }
+        } else {
+            ent.clear();
+            for (uint64_t e = rp[r]; e < rp[r + 1]; e++) ent.push_back({col[e], e});
+            std::stable_sort(ent.begin(), ent.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+            for (size_t i = 0; i < ent.size();) {
+                double sum = 0;
+                size_t j = i;
+                for (; j < ent.size() && ent[j].first == ent[i].first; j++) sum += vals.read_float_from_arr(ent[j].second);
+                c.col.push_back(ent[i].first);
+                c.val.push_back((float)sum);
+                i = j;
+            }
+        }
+        GS_CHECK(c.col.size() < 0xffffffffull, "nnz exceeds 32-bit offsets");
+        c.rp[r + 1] = (uint32_t)c.col.size();
+    }
+    return c;
+}
+
 
 // ------------------------------------------------------------------ LDS tiles
 // Chunk-major A layout for k_lds_rows (kernel_lib.hpp): for BMTB g and column
@@ -253,7 +298,7 @@ void bank_order_segment(const std::vector<uint16_t> &pos, const std::vector<uint
 }
 
 bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
-                      const std::vector<uint64_t> &col, const universal_array &vals, uint64_t K, uint32_t N,
+                      const std::vector<uint64_t> &col, const std::vector<float> &vals, uint64_t K, uint32_t N,
                       size_t lds_budget, int64_t max_fill, mfma_tiles &t, std::string &why) {
     const uint64_t nb = tb_rows.size() - 1;
     if (nb == 0 || K == 0) { why = "empty plan"; return false; }
@@ -314,7 +359,7 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
                 for (; e < row_ptr[r0 + i + 1] && col[e] < lim; e++) {
                     // halfword index in the dense image (row stride RS = 2*KC + 32 bytes)
                     pos.push_back((uint16_t)(i * (KC + 16) + (col[e] - (uint64_t)j * KC)));
-                    hv.push_back(f32_to_f16_bits((float)vals.read_float_from_arr(e)));
+                    hv.push_back(f32_to_f16_bits(vals[e]));
                 }
                 cur[i] = e;
             }
@@ -332,7 +377,7 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
 // row-major, as u32 = (local_row*40 + col - 32s) | f16 << 16; seg[g*nsteps + s] the starts.
 // emax = entries per lane per step (64 lanes) rounded up to 1, 2, 4 or 8.
 bool build_wk(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
-              const std::vector<uint64_t> &col, const universal_array &vals, uint64_t K, std::vector<uint32_t> &seg,
+              const std::vector<uint64_t> &col, const std::vector<float> &vals, uint64_t K, std::vector<uint32_t> &seg,
               std::vector<uint32_t> &ent, uint32_t &emax, uint32_t &rt, std::string &why) {
     const uint64_t nb = tb_rows.size() - 1, nsteps = (K + 31) / 32;
     uint64_t rmax = 0;
@@ -353,7 +398,7 @@ bool build_wk(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> 
                 uint64_t e = cur[i];
                 for (; e < row_ptr[r0 + i + 1] && col[e] < lim; e++)
                     ent.push_back((uint32_t)(i * 40 + (col[e] - 32 * st)) |
-                                  (uint32_t)f32_to_f16_bits((float)vals.read_float_from_arr(e)) << 16);
+                                  (uint32_t)f32_to_f16_bits(vals[e]) << 16);
                 cur[i] = e;
             }
             mx = std::max<uint64_t>(mx, ent.size() - before);
@@ -365,6 +410,81 @@ bool build_wk(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> 
     emax = per <= 1 ? 1 : per <= 2 ? 2 : per <= 4 ? 4 : per <= 8 ? 8 : 0;
     if (!emax) { why = "k-steps too dense for the wave's entry registers"; return false; }
     ent.push_back(0);
+    return true;
+}
+
+// ------------------------------------------------------------------ bitmap panels
+// Upload layout of k_mfma_bitmap (kernel_lib.hpp) from canonical rows (columns
+// ascending and distinct): per BMTB g and 32-column k-step t a segment of R u32
+// row masks followed by the f16 values of the entries in row-major, column order,
+// zero-padded to 16 B; seg[g*nks + t] = its start in 16-B units (seg[nb*nks] =
+// the end).  Refuses (why) row blocks of more than 32 rows, segments over 1 KB,
+// more than 128 k-steps per wave, and plans whose masks would outweigh a u16
+// column index or whose row blocks are too sparse or too short for dense tiles.
+struct bitmap_panels {
+    uint32_t nks = 0, RT = 0, RMAX = 0;
+    std::vector<uint32_t> seg;
+    std::vector<uint32_t> data;  // u32 words of the segments
+};
+
+bool build_bitmap_panels(const std::vector<uint64_t> &tb_rows, const canon_rows &cr, uint64_t K, uint32_t N,
+                         uint32_t waves, int64_t max_fill, bitmap_panels &t, std::string &why) {
+    const uint64_t nb = tb_rows.size() - 1;
+    if (nb == 0 || K == 0) { why = "empty plan"; return false; }
+    if (N != 16 && N != 32 && N != 64) { why = "N must be 16, 32 or 64"; return false; }
+    uint64_t rmax = 0, nnz = cr.col.size();
+    for (uint64_t g = 0; g < nb; g++) rmax = std::max<uint64_t>(rmax, tb_rows[g + 1] - tb_rows[g]);
+    if (rmax == 0 || rmax > 32) { why = "BMTBs of 1..32 rows only"; return false; }
+    const uint64_t nks = (K + 31) / 32;
+    if (nks > 128ull * waves) { why = "more than 128 k-steps per wave"; return false; }
+    if (nnz == 0 || (double)nb * 16 * ((rmax + 15) / 16) * K > (double)max_fill * nnz) {
+        why = "row blocks too sparse for dense tiles";
+        return false;
+    }
+    if ((double)nb * K * N * 2 > 6.0 * 4.0 * nnz && max_fill < (1 << 20)) {
+        why = "row blocks too short: B traffic per row block exceeds A's";
+        return false;
+    }
+    uint64_t mask_words = 0;
+    for (uint64_t g = 0; g < nb; g++) mask_words += (tb_rows[g + 1] - tb_rows[g]) * nks;
+    if (mask_words * 4 > nnz * 2) { why = "row masks would outweigh a u16 column index"; return false; }
+    t.nks = (uint32_t)nks;
+    t.RMAX = (uint32_t)rmax;
+    t.RT = (uint32_t)((rmax + 15) / 16);
+    t.seg.assign(1, 0);
+    t.seg.reserve(nb * nks + 1);
+    t.data.clear();
+    t.data.reserve(mask_words + nnz / 2 + nb * nks * 2);
+    std::vector<uint64_t> cur;
+    std::vector<uint16_t> hv;
+    for (uint64_t g = 0; g < nb; g++) {
+        const uint64_t r0 = tb_rows[g], R = tb_rows[g + 1] - r0;
+        cur.assign(R, 0);
+        for (uint64_t i = 0; i < R; i++) cur[i] = cr.rp[r0 + i];
+        for (uint64_t st = 0; st < nks; st++) {
+            const uint64_t lim = 32 * (st + 1), start = t.data.size();
+            hv.clear();
+            for (uint64_t i = 0; i < R; i++) {
+                uint32_t m = 0;
+                uint64_t e = cur[i];
+                for (; e < cr.rp[r0 + i + 1] && cr.col[e] < lim; e++) {
+                    m |= 1u << (cr.col[e] - 32 * st);
+                    hv.push_back(f32_to_f16_bits(cr.val[e]));
+                }
+                cur[i] = e;
+                t.data.push_back(m);
+            }
+            if (hv.size() & 1) hv.push_back(0);
+            for (size_t i = 0; i < hv.size(); i += 2) t.data.push_back((uint32_t)hv[i] | ((uint32_t)hv[i + 1] << 16));
+            while ((t.data.size() - start) & 3) t.data.push_back(0);
+            if ((t.data.size() - start) * 4 > gsk::kBmSeg) {
+                why = "a k-step segment exceeds 1 KB (row block too dense for one LDS-DMA)";
+                return false;
+            }
+            GS_CHECK(t.data.size() / 4 < 0xffffffffull, "bitmap panels exceed 32-bit offsets");
+            t.seg.push_back((uint32_t)(t.data.size() / 4));
+        }
+    }
     return true;
 }
 
@@ -443,6 +563,17 @@ bool build_nm_panels(const std::vector<uint64_t> &rows, const std::vector<uint64
     return true;
 }
 
+// k_mfma_bitmap shapes (waves per workgroup, A ring slots, B ring slots); config BM_VARIANT
+struct bm_shape { int W, DA, DB; };
+constexpr bm_shape kBmVariant[] = {{8, 8, 3}, {16, 4, 2}, {8, 12, 3}, {8, 6, 5}, {12, 4, 4}, {8, 6, 2}, {8, 6, 6}};
+constexpr int kBmVariants = (int)(sizeof(kBmVariant) / sizeof(kBmVariant[0]));
+
+constexpr size_t bm_lds_bytes(uint32_t CT, uint32_t RT, bm_shape v) {
+    const size_t rings = (size_t)v.W * (v.DA * gsk::kBmSeg + v.DB * 1024u * CT) + 128u;  // + quad selectors
+    const size_t red = (size_t)v.W * RT * CT * 1024u;
+    return rings > red ? rings : red;
+}
+
 }  // namespace
 
 void upload_plan(plan_state &p, int dtype, int device) {
@@ -482,6 +613,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
         std::string why;
         if (build_nm_panels(rows, col, *vals, row_num_of_sub_matrix(m, sb), p.K, blk, S, why)) {
             d.nm = true;
+            d.kernel = "k_nm_mfma";
             d.KC = S;
             d.n_rows_aux = row_num_of_sub_matrix(m, sb);
             d.n_units = m.u(THREAD_META, "first_nz_indices", sb).size() - 1;
@@ -514,18 +646,45 @@ void upload_plan(plan_state &p, int dtype, int device) {
     }
     uint64_t row_num = row_num_of_sub_matrix(m, sb);
     // matrix-core row blocks for fp16 plans with BMTBs (tried before the other kernels)
-    auto try_mfma = [&](const std::vector<uint32_t> &rp) {
+    auto try_mfma = [&](const std::vector<uint32_t> &rp0) {
         const config_t cfg = get_config();
         if (dtype != 1 || !cfg.MFMA_TILES || !m.is_exist(TBLOCK_META, "first_row_indices", sb)) return false;
         mfma_tiles t;
         std::string why;
         const uint32_t Nd = (uint32_t)cfg.DENSE_MATRIX_SIZE;
+        const auto &tbr = m.u(TBLOCK_META, "first_row_indices", sb);
+        const canon_rows cr = canonical_rows(rp0, col, *vals);
+        const std::vector<uint32_t> &rp = cr.rp;
+        if (cfg.MFMA_BITMAP && !cfg.MFMA_WK) {
+            // bitmap panels (k_mfma_bitmap): the default matrix-core layout
+            bitmap_panels bp;
+            const uint32_t var = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(cfg.BM_VARIANT, kBmVariants - 1));
+            if (build_bitmap_panels(tbr, cr, p.K, Nd, (uint32_t)kBmVariant[var].W, cfg.MFMA_MAX_FILL, bp, why) &&
+                bm_lds_bytes(Nd / 16, bp.RT, kBmVariant[var]) <= 160 * 1024) {
+                d.mfma = true;
+                d.bm = true;
+                d.bm_variant = var;
+                d.bm_nks = bp.nks;
+                d.lds_N = Nd;
+                d.maxr = bp.RT;
+                d.rpw_max = bp.RMAX;
+                d.waves = (uint32_t)kBmVariant[var].W;
+                d.lds_bytes = bm_lds_bytes(Nd / 16, bp.RT, kBmVariant[var]);
+                d.n_rows_aux = tbr.size() - 1;
+                d.kernel = "k_mfma_bitmap";
+                const size_t before = d.bytes_A;
+                a.t0 = dev_copy(d, to_u32(tbr, "BMTB first_row_indices"));
+                a.t1 = dev_copy(d, bp.seg);
+                a.tcol = dev_copy(d, bp.data, 4);
+                d.bytes_tile = d.bytes_A - before;
+                return true;
+            }
+        }
         if (cfg.MFMA_WK && (Nd == 16 || Nd == 32)) {
             // wave-owned k-steps (k_mfma_wk)
             std::vector<uint32_t> seg, ent;
             uint32_t emax = 0, rt = 0;
-            const auto &tbr = m.u(TBLOCK_META, "first_row_indices", sb);
-            if (build_wk(tbr, rp, col, *vals, p.K, seg, ent, emax, rt, why)) {
+            if (build_wk(tbr, rp, cr.col, cr.val, p.K, seg, ent, emax, rt, why)) {
                 d.mfma = true;
                 d.wk = true;
                 d.lds_N = Nd;
@@ -536,6 +695,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
                 d.waves = gsk::kWkWaves;
                 const size_t stg = 32 * 2 * Nd + gsk::kWkRows * gsk::kWkRss;
                 d.lds_bytes = std::max<size_t>(gsk::kWkWaves * stg, (size_t)gsk::kWkWaves * rt * (Nd / 16) * 1024);
+                d.kernel = "k_mfma_wk";
                 const size_t before = d.bytes_A;
                 a.t0 = dev_copy(d, to_u32(tbr, "BMTB first_row_indices"));
                 a.t1 = dev_copy(d, seg);
@@ -545,10 +705,9 @@ void upload_plan(plan_state &p, int dtype, int device) {
             }
         }
         const size_t budget = (size_t)std::min<int64_t>(cfg.SHARED_MEM_TOTAL_SIZE, 160 * 1024);
-        if (!build_mfma_tiles(m.u(TBLOCK_META, "first_row_indices", sb), rp, col, *vals, p.K, Nd, budget,
-                              cfg.MFMA_MAX_FILL, t, why))
-            return false;
+        if (!build_mfma_tiles(tbr, rp, cr.col, cr.val, p.K, Nd, budget, cfg.MFMA_MAX_FILL, t, why)) return false;
         d.mfma = true;
+        d.kernel = "k_mfma_rows";
         d.lds_N = Nd;
         d.KC = 1u << t.lgKC; d.nc = t.nc; d.maxr = t.RT; d.rpw_max = t.RMAX; d.RSB = t.lgKC;
         d.seg_cap = t.gmax;  // entry groups per chunk (max): the launch picks MAXA per variant
@@ -629,6 +788,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
                                     m.u(WARP_META, "first_row_indices", sb), rp, col, p.K, Nd, dtype ? 2u : 4u, budget,
                                     t, why)) {
                     d.lds = true;
+                    d.kernel = "k_lds_rows";
                     d.lds_N = Nd;
                     d.KC = t.KC; d.nc = t.nc; d.RSB = t.RSB; d.rpw_max = t.rpw_max; d.seg_cap = t.seg_cap;
                     d.waves = t.waves; d.maxr = t.maxr; d.lds_bytes = t.lds_bytes;
@@ -866,8 +1026,9 @@ void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *
                    hipStream_t s) {
     const device_plan &d = p.dev;
     // B rows by LDS-DMA two chunks ahead (MFMA_GLDS) or through registers three ahead
-    auto kern = get_config().MFMA_GLDS ? gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, true>
-                                       : gsk::k_mfma_rows<CT, RT, LGKC, MAXA>;
+    const int64_t gl = get_config().MFMA_GLDS;
+    auto kern = gl >= 4 ? gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 4>
+                        : (gl ? gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2> : gsk::k_mfma_rows<CT, RT, LGKC, MAXA>);
     static std::mutex mu;
     static std::map<std::pair<int, const void *>, size_t> granted;
     {
@@ -889,7 +1050,8 @@ template <int CT, int RT>
 void launch_mfma_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N,
                     hipStream_t s) {
     // entry groups per thread per chunk: the GLDS variant has 9 entry waves, the other 6
-    const uint32_t nat = 64u * (get_config().MFMA_GLDS ? gsk::kMfmaAWavesG : gsk::kMfmaAWaves);
+    const int64_t gl = get_config().MFMA_GLDS;
+    const uint32_t nat = 64u * (gl >= 4 ? 6u : (gl ? (uint32_t)gsk::kMfmaAWavesG : (uint32_t)gsk::kMfmaAWaves));
     const bool two = p.dev.seg_cap > nat;
     switch (p.dev.RSB) {                  // log2 KC
         case 10: two ? launch_mfma_k<CT, RT, 10, 2>(p, a, B, C, N, s) : launch_mfma_k<CT, RT, 10, 1>(p, a, B, C, N, s); break;
@@ -914,7 +1076,7 @@ void launch_mfma_ct(const plan_state &p, const device_arrays &a, const gsk::f16 
 // diagnostic: N = 32 plans with 17..48-row BMTBs and KC 256 or 512
 template <int RT, int LG>
 auto timeline_kernel(bool two) {
-    return two ? gsk::k_mfma_rows<2, RT, LG, 2, true> : gsk::k_mfma_rows<2, RT, LG, 1, true>;
+    return two ? gsk::k_mfma_rows<2, RT, LG, 2, true> : gsk::k_mfma_rows<2, RT, LG, 1, true>;  // register-staged B
 }
 
 void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
@@ -1010,9 +1172,66 @@ void launch_wk_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B
     }
 }
 
+template <int CT, int RT, int VAR>
+void launch_bm_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
+    constexpr bm_shape v = kBmVariant[VAR];
+    constexpr size_t lds = bm_lds_bytes(CT, RT, v);
+    if constexpr (lds > 160 * 1024) {
+        throw gs_error("k_mfma_bitmap variant does not fit LDS at this N");
+    } else {
+        const device_plan &d = p.dev;
+        // GS_BM_DEBUG=6 (diagnostic timing build, wrong results): kernel_lib.hpp DBG bits; N=32
+        static const int dbg = getenv("GS_BM_DEBUG") ? atoi(getenv("GS_BM_DEBUG")) : 0;
+        auto kern = gsk::k_mfma_bitmap<CT, RT, v.W, v.DA, v.DB>;
+        if constexpr (CT == 2 && RT == 2) {
+            if (dbg == 6) kern = gsk::k_mfma_bitmap<CT, RT, v.W, v.DA, v.DB, 6>;
+        }
+        static std::mutex mu;
+        static std::map<std::pair<int, const void *>, bool> granted;
+        {
+            std::lock_guard<std::mutex> l(mu);
+            bool &gr = granted[{d.device, reinterpret_cast<const void *>(kern)}];
+            if (!gr) {
+                HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                gr = true;
+            }
+        }
+        hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux), dim3(64 * v.W), lds, s, a.t0, a.t1,
+                           (const gsk::u32x4 *)a.tcol, B, C, (uint32_t)p.K, N, d.bm_nks, (uint32_t)d.row_base);
+        HIP_OK(hipGetLastError());
+    }
+}
+
+template <int CT, int RT>
+void launch_bm_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
+    switch (p.dev.bm_variant) {
+        case 0: launch_bm_k<CT, RT, 0>(p, a, B, C, N, s); break;
+        case 1: launch_bm_k<CT, RT, 1>(p, a, B, C, N, s); break;
+        case 2: launch_bm_k<CT, RT, 2>(p, a, B, C, N, s); break;
+        case 3: launch_bm_k<CT, RT, 3>(p, a, B, C, N, s); break;
+        case 4: launch_bm_k<CT, RT, 4>(p, a, B, C, N, s); break;
+        case 5: launch_bm_k<CT, RT, 5>(p, a, B, C, N, s); break;
+        default: launch_bm_k<CT, RT, 6>(p, a, B, C, N, s); break;
+    }
+}
+
+template <int CT>
+void launch_bm(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
+    if (p.dev.maxr > 1) launch_bm_rt<CT, 2>(p, a, B, C, N, s);
+    else launch_bm_rt<CT, 1>(p, a, B, C, N, s);
+}
+
 void launch_mfma(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
     const gsk::f16 *b = (const gsk::f16 *)B;
     gsk::f16 *c = (gsk::f16 *)C;
+    if (p.dev.bm) {
+        GS_CHECK(N == 16 || N == 32 || N == 64, "bitmap panels run N = 16, 32 or 64");
+        if (N == 16) launch_bm<1>(p, a, b, c, N, s);
+        else if (N == 32) launch_bm<2>(p, a, b, c, N, s);
+        else launch_bm<4>(p, a, b, c, N, s);
+        return;
+    }
     if (p.dev.wk) {
         const bool two = p.dev.maxr > 1;
         if (N == 16) two ? launch_wk_rt<1, 2>(p, a, b, c, N, s) : launch_wk_rt<1, 1>(p, a, b, c, N, s);

@@ -1,7 +1,8 @@
 // rocsparse_cmp.cc -- the rocSPARSE comparator (bench / tests only, not the product).
 // Mirrors baseline/base_cusparse/spmm.cu:90-162 of the reference on MI355X:
 // CSR int32 A, row-major dense B and C, generic SpMM, warm-up then a timed loop
-// with GPU events.  fp32 or fp16 (A, B, C fp16, fp32 compute).
+// with GPU events.  fp32, or fp16 A and B with fp32 C and fp32 compute (rocSPARSE's
+// documented mixed-precision SpMM: rocsparse_spmm.h, "f16_r f16_r f32_r f32_r").
 #include <hip/hip_runtime.h>
 #include <rocsparse/rocsparse.h>
 
@@ -36,7 +37,7 @@ extern "C" {
 
 const char *rs_last_error(void) { return g_err.c_str(); }
 
-// dtype 0: fp32, 1: fp16 (vals/B/C given as fp32 on the host, converted)
+// dtype 0: fp32, 1: fp16 A and B (vals/B given as fp32 on the host, converted), fp32 C
 // alg: rocsparse_spmm_alg (0 default, 1 csr, 4 csr_row_split, 5 csr_merge/nnz_split, 9 merge_path)
 // copies: independent device copies of A and B rotated per call (cold caches)
 // out_C (host fp32, M x N) receives the result of the first call; may be null
@@ -65,7 +66,7 @@ int rs_spmm_bench(int M, int K, int nnz, const int *row_ptr, const int *col, con
         for (size_t i = 0; i < b32.size(); i++) { _Float16 x = (_Float16)b32[i]; std::memcpy(&b16[i], &x, 2); }
     }
     RS(rocsparse_create_handle(&h));
-    HP(hipMalloc(&dC, (size_t)M * N * es));
+    HP(hipMalloc(&dC, (size_t)M * N * 4));  // C is fp32 for both dtypes
     for (int c = 0; c < copies; c++) {
         void *drp, *dcol, *dval, *dB;
         HP(hipMalloc(&drp, (size_t)(M + 1) * 4));
@@ -81,7 +82,7 @@ int rs_spmm_bench(int M, int K, int nnz, const int *row_ptr, const int *col, con
                                       rocsparse_index_base_zero, dt));
         RS(rocsparse_create_dnmat_descr(&Bd[c], K, N, N, dB, dt, rocsparse_order_row));
     }
-    RS(rocsparse_create_dnmat_descr(&Cd, M, N, N, dC, dt, rocsparse_order_row));
+    RS(rocsparse_create_dnmat_descr(&Cd, M, N, N, dC, rocsparse_datatype_f32_r, rocsparse_order_row));
     RS(rocsparse_spmm(h, rocsparse_operation_none, rocsparse_operation_none, &alpha, A[0], Bd[0], &beta, Cd,
                       rocsparse_datatype_f32_r, (rocsparse_spmm_alg)alg, rocsparse_spmm_stage_buffer_size, &bsz, nullptr));
     HP(hipMalloc(&tmp, bsz ? bsz : 4));
@@ -91,15 +92,7 @@ int rs_spmm_bench(int M, int K, int nnz, const int *row_ptr, const int *col, con
     RS(rocsparse_spmm(h, rocsparse_operation_none, rocsparse_operation_none, &alpha, A[0], Bd[0], &beta, Cd,
                       rocsparse_datatype_f32_r, (rocsparse_spmm_alg)alg, rocsparse_spmm_stage_compute, &bsz, tmp));
     HP(hipDeviceSynchronize());
-    if (out_C) {
-        if (dtype == 1) {
-            std::vector<_Float16> hc((size_t)M * N);
-            HP(hipMemcpy(hc.data(), dC, hc.size() * 2, hipMemcpyDeviceToHost));
-            for (size_t i = 0; i < hc.size(); i++) out_C[i] = (float)hc[i];
-        } else {
-            HP(hipMemcpy(out_C, dC, (size_t)M * N * 4, hipMemcpyDeviceToHost));
-        }
-    }
+    if (out_C) HP(hipMemcpy(out_C, dC, (size_t)M * N * 4, hipMemcpyDeviceToHost));
     for (int i = 0; i < warmup; i++)
         RS(rocsparse_spmm(h, rocsparse_operation_none, rocsparse_operation_none, &alpha, A[i % copies], Bd[i % copies],
                           &beta, Cd, rocsparse_datatype_f32_r, (rocsparse_spmm_alg)alg, rocsparse_spmm_stage_compute,

@@ -62,6 +62,7 @@ typedef struct {
     uint64_t lds_bytes, tile_bytes;
     uint32_t ksplit;              /* k_mfma_rows workgroups per row block (K ranges, fp32 slab combine) */
     int n_kernels;                /* kernels gs_spmm runs: 1, or one per sub-matrix of a row division */
+    char device_kernel[32];       /* the device kernel gs_spmm launches at the plan's N (first sub-matrix) */
 } gs_plan_info;
 
 const char *gs_last_error(void);

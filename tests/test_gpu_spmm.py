@@ -305,6 +305,8 @@ def mfma_everywhere():
     yield
     gsa.set_config("MFMA_MAX_FILL", 16)
     gsa.set_config("MFMA_GLDS", 1)
+    gsa.set_config("MFMA_BITMAP", 0)
+    gsa.set_config("BM_VARIANT", 0)
 
 
 @pytest.mark.parametrize("glds", [1, 0])  # B rows by LDS-DMA (default) / through registers
@@ -319,13 +321,94 @@ def test_mfma_rows_match_oracle(pipe, N, glds, mfma_everywhere):
     used = []
     for case, M, K, row, col, val in mfma_cases():
         plan, C, B = run(M, K, row, col, val, name, p0, p1, N, "f16")
-        used.append(plan.info()["lds_stage"])
+        used.append(plan.info()["device_kernel"])
         v = val.astype(np.float16).astype(np.float32)
         ref = ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64")
         check(C, ref, "f16")
         plan.free()
     if not (p0 > 32 and N == 64):
-        assert 2 in used, used
+        assert "k_mfma_rows" in used, used
+
+
+BM_PIPES = [("tblock_warp_total", 20, 2), ("block_total", 16, 1), ("block_total", 20, 1),
+            ("block_total", 32, 1), ("block_total", 7, 1), ("block_total", 1, 1)]
+# device_plan.hip kBmVariant: (waves, A ring slots, B ring slots)
+BM_VARIANTS = [(8, 8, 3), (16, 4, 2), (8, 12, 3), (8, 6, 5), (12, 4, 4), (8, 6, 2), (8, 6, 6)]
+
+
+@pytest.mark.parametrize("variant", range(len(BM_VARIANTS)))
+@pytest.mark.parametrize("N", [16, 32, 64])
+@pytest.mark.parametrize("pipe", BM_PIPES, ids=lambda p: f"{p[0]}-{p[1]}")
+def test_mfma_bitmap_matches_oracle(pipe, N, variant, mfma_everywhere):
+    """bitmap panels (k_mfma_bitmap, opt-in MFMA_BITMAP=1) in every workgroup shape
+    that fits LDS: same results as the oracle, and the kernel actually ran"""
+    name, p0, p1 = pipe
+    W, DA, DB = BM_VARIANTS[variant]
+    fits = W * (DA * 1024 + DB * 1024 * (N // 16)) + 128 <= 160 * 1024
+    gsa.set_config("MFMA_BITMAP", 1)
+    gsa.set_config("BM_VARIANT", variant)
+    used = []
+    for case, M, K, row, col, val in mfma_cases():
+        plan, C, B = run(M, K, row, col, val, name, p0, p1, N, "f16")
+        used.append(plan.info()["device_kernel"])
+        v = val.astype(np.float16).astype(np.float32)
+        ref = ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64")
+        check(C, ref, "f16")
+        plan.free()
+    assert ("k_mfma_bitmap" in used) == fits, used
+
+
+@pytest.mark.parametrize("kernel", ["k_mfma_bitmap", "k_mfma_rows", "k_mfma_wk"])
+def test_mfma_unsorted_columns_and_duplicates(kernel, mfma_everywhere):
+    """the reference accepts any column order inside a row and its gather kernels
+    add repeated coordinates: the matrix-core layouts sort each row and sum
+    duplicates"""
+    M, K, N = 300, 2100, 32
+    r, c, v = ds.pruned_weight(M, K, 0.7, 41)
+    rng = np.random.default_rng(3)
+    # shuffle the columns inside every row, then repeat 5% of the entries
+    order = np.lexsort((rng.random(len(r)), r))
+    r, c, v = r[order], c[order], v[order]
+    dup = np.sort(rng.choice(len(r), len(r) // 20, replace=False))
+    r2 = np.concatenate([r, r[dup]])
+    c2 = np.concatenate([c, c[dup]])
+    v2 = np.concatenate([v, (0.5 * v[dup]).astype(np.float32)])
+    o = np.argsort(r2, kind="stable")
+    r2, c2, v2 = r2[o], c2[o], v2[o]
+    gsa.set_config("MFMA_BITMAP", 1 if kernel == "k_mfma_bitmap" else 0)
+    gsa.set_config("MFMA_WK", 1 if kernel == "k_mfma_wk" else 0)
+    try:
+        plan, C, B = run(M, K, r2, c2, v2, "block_total", 20, 1, N, "f16")
+        assert plan.info()["device_kernel"] == kernel
+        ref = ofi.spmm_ref(M, N, r2, c2, v2.astype(np.float16).astype(np.float32), B.astype(np.float32), "f64")
+        check(C, ref, "f16")
+    finally:
+        gsa.set_config("MFMA_WK", 0)
+
+
+def test_mfma_non_finite_B_deviation(mfma_everywhere):
+    """documented deviation: the matrix-core kernels multiply every
+    row block's whole tile, zeros included, so an Inf in B[k, j] makes all of output
+    column j non-finite; the reference (and MFMA_TILES=0) only poisons the rows with
+    an entry at column k.  The other columns stay finite either way."""
+    M, K, N = 200, 640, 32
+    r, c, v = ds.pruned_weight(M, K, 0.7, 43)
+    B = np.random.default_rng(5).uniform(-1, 1, (K, N)).astype(np.float16)
+    k = 77
+    B[k, 3] = np.inf
+    plan, C, _ = run(M, K, r, c, v, "block_total", 20, 1, N, "f16", B=B)
+    assert plan.info()["device_kernel"] == "k_mfma_rows"
+    has_k = np.zeros(M, bool)
+    has_k[r[c == k].astype(np.int64)] = True
+    assert not np.isfinite(C[:, 3]).any()               # the whole column (reference: rows has_k only)
+    assert np.isfinite(np.delete(C, 3, axis=1)).all()   # other columns untouched
+    try:
+        gsa.set_config("MFMA_TILES", 0)
+        plan0, C0, _ = run(M, K, r, c, v, "block_total", 20, 1, N, "f16", B=B)
+        assert not plan0.info()["device_kernel"].startswith("k_mfma")
+        np.testing.assert_array_equal(np.isfinite(C0[:, 3]), ~has_k)  # reference semantics
+    finally:
+        gsa.set_config("MFMA_TILES", 1)
 
 
 @pytest.mark.parametrize("N", [16, 32])
@@ -336,15 +419,18 @@ def test_mfma_wk_matches_oracle(pipe, N, mfma_everywhere):
     # opt-in wave-owned k-step kernel (MFMA_WK=1, k_mfma_wk): same results as the oracle
     name, p0, p1 = pipe
     gsa.set_config("MFMA_WK", 1)
+    used = []
     try:
         for case, M, K, row, col, val in mfma_cases():
             plan, C, B = run(M, K, row, col, val, name, p0, p1, N, "f16")
+            used.append(plan.info()["device_kernel"])
             v = val.astype(np.float16).astype(np.float32)
             ref = ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64")
             check(C, ref, "f16")
             plan.free()
     finally:
         gsa.set_config("MFMA_WK", 0)
+    assert "k_mfma_wk" in used, used
 
 
 def test_mfma_rows_known_answer_and_fallback(mfma_everywhere):
@@ -388,6 +474,7 @@ def test_mfma_rows_ksplit_combine(ks, mfma_everywhere):
     M, K, N = 400, 6000, 32
     r, c, v = ds.pruned_weight(M, K, 0.7, 31)
     try:
+        gsa.set_config("MFMA_BITMAP", 0)
         gsa.set_config("MFMA_KSPLIT", ks)
         plan, C, B = run(M, K, r, c, v, "block_total", 40, 1, N, "f16")
         info = plan.info()
