@@ -2,21 +2,24 @@
 """SpMM benchmark (BASELINE.json metric: SpMM GFLOP/s + achieved HBM GB/s vs
 rocSPARSE, pruned-weight fp16 N=32).
 
-Workload (configs[1]): OPT-13B q_proj stand-in, 5120 x 5120, 70% unstructured
-(global magnitude pruning of a seeded Gaussian, nnz 7,864,320), fp16 A/B/C,
-fp32 accumulation, dense N = 32, one MI355X per rank.  A "step" = one SpMM of
-one matrix.  Inputs are resident in HBM; every step uses the next of R
-independent device copies of A (and B) so the rotation set exceeds 512 MB and
-the 256 MB Infinity Cache cannot serve A (SURVEY.md §8d "cache honesty").
+N=1 workload (configs[1]): OPT-13B q_proj stand-in, 5120 x 5120, 70% unstructured
+(global magnitude pruning of a seeded Gaussian, nnz 7,864,320), fp16 A/B/C, fp32
+accumulation, dense N = 32.  A "step" = one SpMM of one matrix.  Inputs are resident
+in HBM; every step uses the next of R independent device copies of A (and B), R sized
+on the bytes the selected kernel reads so the rotation set exceeds 512 MB and the
+256 MB Infinity Cache cannot serve A (SURVEY.md §8d "cache honesty").  The plan is
+chosen first (the reference's best-variant search, obtain_result.py): every candidate
+pipeline is timed over `--search-reps` launches; then the chosen plan runs W untimed
+warm-up steps and exactly K timed steps between barriers and device syncs.
 
-Multi-GPU (torchrun): weak scaling, every rank runs its own matrix (the
-row-sharded batch of independent matrices; no data-path collective), a barrier
-brackets the timed region and the time is the max over ranks.
+Multi-GPU (`--gpus N`, N > 1): one process per GPU.  Started without WORLD_SIZE,
+bench.py launches the N ranks itself (torch.distributed.run on 127.0.0.1) before
+anything touches a GPU.  The default N > 1 workload is configs[4] (C5): the 288
+matrices of the 48-layer OPT-30B 80%-pruned batch split over the ranks by LPT on nnz
+(strong scaling, no data-path collective).  `--workload c2` keeps the weak-scaling
+batch of one C2 matrix per rank.  The time is the max over ranks.
 
---workload c3 measures BASELINE.json configs[2] instead (OPT-30B fc1 stand-in,
-28672 x 7168, 2:4 structured by magnitude, fp16, N = 128, the col-direction
-plan on the sparse matrix cores; algorithmic bytes count the 2:4 layout's
-values + 2-bit positions).  The default stays the headline C2.
+--workload c1 | c3 | c4 | c4o | c5 measures the other BASELINE.json configs.
 
 Prints one JSON line on rank 0."""
 import argparse
@@ -47,7 +50,10 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--p0", type=int, default=None, help="with --pipeline: run only this plan parameter")
     ap.add_argument("--p1", type=int, default=None)
-    ap.add_argument("--workload", choices=("c1", "c2", "c3", "c4", "c4o", "c5"), default="c2")
+    ap.add_argument("--workload", choices=("c1", "c2", "c3", "c4", "c4o", "c5"), default=None,
+                    help="default: c2 on one GPU, c5 (the sharded batch) on several")
+    ap.add_argument("--search-reps", type=int, default=100, help="launches per candidate plan in the plan search")
+    ap.add_argument("--n-sweep", default="", help="also time the chosen plan family at these dense widths, e.g. 8,32,128")
     ap.add_argument("--layers", type=int, default=48, help="c5: OPT-30B layers in the batch")
     ap.add_argument("--shard", choices=("batch", "rows", "nnz"), default="batch",
                     help="c4/c4o with N>1: batch = a matrix per rank (weak); rows / nnz = one matrix split "
@@ -58,11 +64,30 @@ def parse():
     ap.add_argument("--sparsity", type=float, default=0.7)
     ap.add_argument("--config", action="append", default=[], metavar="KEY=INT",
                     help="engine switch (gs_set_config_int), e.g. BM_VARIANT=1; repeatable")
-    a = ap.parse_args()
+    return ap.parse_args()
+
+
+def resolve_workload(a, world):
+    if a.workload is None:
+        a.workload = "c5" if world > 1 else "c2"
     dflt = {"c1": (47894, 41550, 8), "c2": (5120, 5120, 32), "c3": (28672, 7168, 128), "c4": (1000005, 1000005, 8),
             "c4o": (3072441, 3072441, 8), "c5": (7168, 7168, 32)}[a.workload]
     a.M, a.K, a.N = a.M or dflt[0], a.K or dflt[1], a.N or dflt[2]
-    return a
+
+
+def launch_ranks(n):
+    """--gpus N without a launcher: start N ranks (one per GPU) with torch.distributed.run
+    and exit with its status.  Nothing here touches a GPU."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 WORKLOADS = {
@@ -108,7 +133,8 @@ CANDIDATES_C4 = [("merge_path", 256, 1), ("merge_path", 512, 1), ("merge_path", 
 
 
 def kernel_label(info):
-    return {0: info["kernel_name"], 1: "k_lds_rows", 2: "k_mfma_rows", 3: "k_nm_mfma"}[info["lds_stage"]]
+    """the device kernel gs_spmm launches (gs_plan_info.device_kernel)"""
+    return info.get("device_kernel") or info["kernel_name"]
 
 
 def algorithmic_bytes(M, K, N, nnz, e, s_idx):
@@ -195,8 +221,8 @@ def whole_job_gflops(world, flops_per_step, steps, wall_s):
 
 
 def rocsparse_baseline(M, K, N, row, col, val, copies, dtype, reps=100, warmup=10):
-    """best rocSPARSE CSR SpMM algorithm for dtype (1 fp16, 0 fp32); None if
-    rocSPARSE rejects every algorithm (rocSPARSE 7.2 has no fp16 CSR SpMM)."""
+    """best rocSPARSE CSR SpMM algorithm for dtype (1: fp16 A and B, fp32 C and compute
+    -- rocSPARSE's documented mixed precision; 0: fp32); None if every algorithm fails"""
     lib = ctypes.CDLL(os.path.join(ROOT, "generalsparse_amd", "librocsparse_cmp.so"))
     lib.rs_last_error.restype = ctypes.c_char_p
     rp = np.zeros(M + 1, np.int64)
@@ -218,10 +244,25 @@ def rocsparse_baseline(M, K, N, row, col, val, copies, dtype, reps=100, warmup=1
     return best
 
 
+def cpu_info():
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model, os.cpu_count()
+
+
 def cpu_baseline(M, K, N, row, col, val, min_s=10.0, row_share=1):
     """the oracle's restatement of the reference's host path (checker code, timed
-    here only as the CPU baseline): plan transform once + host SpMM repeated.
-    row_share > 1 times the first M/row_share rows only (a bounded sample)."""
+    here only as the CPU baseline): plan transform once + host SpMM repeated, single
+    thread as the reference runs it; plus the build's all-cores OpenMP variant of the
+    same SpMM (not the reference's).  row_share > 1 times the first M/row_share rows
+    only (a bounded sample).  Hot cache: the same A and B every repetition."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi as ofi
     what = "full matrix"
@@ -233,10 +274,18 @@ def cpu_baseline(M, K, N, row, col, val, min_s=10.0, row_share=1):
     t_tr, _ = ofi.time_cpu_path(M, K, row, col, val, N)
     t_spmm, reps = ofi.time_spmm_repeated(M, K, row, col, val, N, min_s)
     gf = 2.0 * len(row) * N * reps / t_spmm / 1e9
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    t_mt, reps_mt = ofi.time_spmm_repeated_mt(M, K, row, col, val, N, min_s / 2, threads)
+    gf_mt = 2.0 * len(row) * N * reps_mt / t_mt / 1e9
+    model, nproc = cpu_info()
     return {"value": round(gf, 3), "unit": "GFLOP/s", "cores": 1, "kind": "port",
             "sample": f"{what}: spmm_reference_host restated (fp32) x{reps} in {t_spmm:.1f} s, "
-                      f"single thread; plan transform (thread_total) once {t_tr:.2f} s",
-            "transform_s": round(t_tr, 3), "spmm_s_per_rep": round(t_spmm / reps, 4)}
+                      f"single thread; plan transform (thread_total) once {t_tr:.2f} s; hot cache",
+            "transform_s": round(t_tr, 3), "spmm_s_per_rep": round(t_spmm / reps, 4),
+            "cpu_model": model, "nproc": nproc,
+            "all_cores": {"value": round(gf_mt, 3), "unit": "GFLOP/s", "threads": threads,
+                          "kind": "the build's OpenMP variant (the reference's host path is single-threaded)",
+                          "sample": f"{what} x{reps_mt} in {t_mt:.1f} s"}}
 
 
 # C5 (BASELINE.json configs[4]): all OPT-30B layers, 80% unstructured, fp16, N = 32.  Per layer
@@ -335,12 +384,62 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
         p.free()
 
 
+def replicas_for(info, K, N, e, rotation_mb):
+    """independent copies of A and B so the rotation set covers rotation_mb of the bytes
+    the launched kernel actually reads (the matrix-core layouts, not a deferred CSR)"""
+    read_A = info["tile_bytes"] if info["lds_stage"] in (2, 3) and info["tile_bytes"] else info["device_bytes_A"]
+    return max(2, int(math.ceil(rotation_mb * 1e6 / (read_A + K * N * e))))
+
+
+def event_ms(plan, Bs, Cs, reps, torch, warm=20, rotate=True):
+    """average kernel time (ms) of `reps` launches from HIP events on the launch stream"""
+    stream = torch.cuda.current_stream()
+    if rotate:
+        plan.spmm_rotate(warm, 0, Bs, Cs)
+    else:
+        for _ in range(warm):
+            plan.spmm(Bs[0], C=Cs[0])
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    if rotate:
+        plan.spmm_rotate(reps, 0, Bs, Cs)
+    else:
+        for _ in range(reps):
+            plan.spmm(Bs[0], C=Cs[0])
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def build_plan(gsa, M, K, row, col, val, cand, N, dt, local, rotation_mb, e, tdt, dev, torch):
+    name, p0, p1 = cand
+    t0 = time.perf_counter()
+    plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline(name, N, p0, p1).compile()
+    t_plan = time.perf_counter() - t0
+    plan.upload(dt, local)
+    info = plan.info()
+    reps = replicas_for(info, K, N, e, rotation_mb)
+    for _ in range(reps - 1):
+        plan.add_replica()
+    Bs = [torch.randn((K, N), device=dev, dtype=tdt) for _ in range(reps)]
+    Cs = [torch.empty((M, N), device=dev, dtype=tdt) for _ in range(reps)]
+    return plan, Bs, Cs, reps, t_plan
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the real world size",
+              file=sys.stderr, flush=True)
+    resolve_workload(args, world)
     dist = None
     if world > 1:
         import torch.distributed as td
@@ -400,40 +499,37 @@ def main():
         [(args.pipeline, 0, 1)]
     if args.p0 is not None:  # one variant (profiling runs)
         cands = [(c[0], args.p0, c[2] if args.p1 is None else args.p1) for c in cands[:1]]
+    # plan search (obtain_result.py's best variant): every candidate timed over search_reps
+    # launches (max over ranks, so every rank keeps the same plan)
     variants = {}
     best = None
-    for name, p0, p1 in cands:
-        t0 = time.perf_counter()
+    for cand in cands:
+        key = f"{cand[0]}({cand[1]},{cand[2]})"
         try:
-            plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline(name, N, p0, p1).compile()
+            plan, Bs, Cs, reps, t_plan = build_plan(gsa, M, K, row, col, val, cand, N, dt, local, args.rotation_mb, e,
+                                                    tdt, dev, torch)
         except gsa.GsError as ex:  # e.g. the balanced splitter on trailing empty rows
-            variants[f"{name}({p0},{p1})"] = {"error": str(ex)}
+            variants[key] = {"error": str(ex)}
             continue
-        t_plan = time.perf_counter() - t0
-        plan.upload(dt, local)
+        ms = max_over_ranks(event_ms(plan, Bs, Cs, args.search_reps, torch), dist, torch)
         info = plan.info()
-        per_rep = info["device_bytes_A"] + K * N * e
-        reps = max(2, int(math.ceil(args.rotation_mb * 1e6 / per_rep)))
-        for _ in range(reps - 1):
-            plan.add_replica()
-        Bs = [torch.randn((K, N), device=dev, dtype=tdt) for _ in range(reps)]
-        Cs = [torch.empty((M, N), device=dev, dtype=tdt) for _ in range(reps)]
-        if shards is not None and args.shard == "nnz" and dist is not None:
-            wall, ev_ms = time_plan_combined(plan, Bs, Cs, N, args.steps, args.warmup, torch, dist, shards, rank)
+        variants[key] = {"kernel_ms": round(ms, 5), "gflops_per_gpu": round(flops / (ms * 1e-3) / 1e9, 1),
+                         "kernel": kernel_label(info), "replicas": reps, "plan_s": round(t_plan, 2)}
+        if best is None or ms < best[0]:
+            if best is not None:
+                best[1].free()
+            best = (ms, plan, Bs, Cs, reps, cand, key, info)
         else:
-            wall, ev_ms = time_plan(plan, Bs, Cs, N, args.steps, args.warmup, torch, dist)
-        key = f"{name}({p0},{p1})"
-        variants[key] = {"ms_per_step": round(wall / args.steps * 1e3, 5), "kernel_ms": round(ev_ms, 5),
-                         "gflops_per_gpu": round(flops / (wall / args.steps) / 1e9, 1),
-                         "kernel": kernel_label(info),
-                         "replicas": reps, "plan_s": round(t_plan, 2)}
-        if best is None or wall < best[1]:
-            best = (key, wall, ev_ms, info, reps, (name, p0, p1))
+            plan.free()
         del Bs, Cs
-        plan.free()
         torch.cuda.empty_cache()
-
-    key, wall, ev_ms, info, reps, best_cand = best
+    _, plan, Bs, Cs, reps, best_cand, key, info = best
+    # the measurement: W untimed warm-up steps, exactly K timed steps
+    if shards is not None and args.shard == "nnz" and dist is not None:
+        wall, ev_ms = time_plan_combined(plan, Bs, Cs, N, args.steps, args.warmup, torch, dist, shards, rank)
+    else:
+        wall, ev_ms = time_plan(plan, Bs, Cs, N, args.steps, args.warmup, torch, dist)
+    hot_ms = event_ms(plan, Bs, Cs, 100, torch, rotate=False)
     ms_per_step = wall / args.steps * 1e3
     value = whole_job_gflops(world, flops, args.steps, wall)
     if shards is not None:  # strong scaling: the job is one matrix
@@ -443,7 +539,9 @@ def main():
     tf = os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
     if os.path.exists(tf):
         try:
-            traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
+            tj = json.load(open(tf))
+            if tj.get("kernel") in (None, kernel_label(info)):
+                traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     out = {
@@ -454,48 +552,21 @@ def main():
         "dtype": "f16 (fp32 accumulate)" if dt == "f16" else "f32", "data": wl["data"],
         "config": {"workload": wl["workload"].format(M=M, K=K, N=N),
                    "M": M, "K": K, "N": N, "nnz": nnz, "plan": key, "kernel": kernel_label(info),
-                   "replicas_rotated": reps,
+                   "replicas_rotated": reps, "rotated_read_bytes_per_replica": info["tile_bytes"] or info["device_bytes_A"],
                    "parallelism": f"row-sharded batch x{world}" if shards is None else
                    f"one matrix, {args.shard} shards x{world}" + (" + boundary all-reduce" if args.shard == "nnz" else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": round(ev_ms, 5)},
+                     "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": round(ev_ms, 5),
+                     "hot_cache_kernel_ms": round(hot_ms, 5)},
         "variants": variants,
     }
-    if rank == 0 and not args.no_rocsparse and dt == "f32":
+    if args.n_sweep and rank == 0:
+        out["n_sweep"] = n_sweep(gsa, M, K, row, col, val, best_cand, args, dt, local, e, tdt, dev, torch, nnz)
+    if rank == 0 and not args.no_rocsparse:
         try:
-            rs32 = rocsparse_baseline(M, K, N, row, col, val, min(reps, 20), dtype=0)
-            out["rocsparse"] = {"f32": rs32}
-            if rs32:
-                out["speedup_vs_rocsparse"] = round(flops / (ev_ms * 1e-3) / 1e9 / rs32["gflops"], 3)
-        except Exception as ex:
-            out["rocsparse"] = {"error": str(ex)}
-    elif rank == 0 and not args.no_rocsparse:
-        try:
-            rs16 = rocsparse_baseline(M, K, N, row, col, val, min(reps, 20), dtype=1)
-            rs32 = rocsparse_baseline(M, K, N, row, col, val, min(reps, 20), dtype=0)
-            # our fp32 path on the same plan, same rotation discipline (apples to apples)
-            name, p0, p1 = best_cand
-            plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline(name, N, p0, p1).compile().upload("f32", local)
-            r32 = max(2, int(math.ceil(args.rotation_mb * 1e6 / (plan.info()["device_bytes_A"] + K * N * 4))))
-            for _ in range(r32 - 1):
-                plan.add_replica()
-            Bs = [torch.randn((K, N), device=dev, dtype=torch.float32) for _ in range(r32)]
-            Cs = [torch.empty((M, N), device=dev, dtype=torch.float32) for _ in range(r32)]
-            _, ev32 = time_plan(plan, Bs, Cs, N, args.steps, args.warmup, torch, None)
-            plan.free()
-            del Bs, Cs
-            ours16 = flops / (ev_ms * 1e-3) / 1e9
-            ours32 = flops / (ev32 * 1e-3) / 1e9
-            out["rocsparse"] = {"f16": rs16 if rs16 else "not supported by rocSPARSE 7.2 (CSR SpMM fp16/fp32-compute)",
-                                "f32": rs32, "ours_f32_gflops": round(ours32, 1), "ours_f32_kernel_ms": round(ev32, 5)}
-            if rs16:
-                out["speedup_vs_rocsparse"] = round(ours16 / rs16["gflops"], 3)
-            elif rs32:
-                out["speedup_vs_rocsparse"] = round(ours16 / rs32["gflops"], 3)
-                out["speedup_vs_rocsparse_note"] = "ours fp16 vs rocSPARSE fp32 (no fp16 CSR SpMM in rocSPARSE)"
-            if rs32:
-                out["speedup_vs_rocsparse_f32"] = round(ours32 / rs32["gflops"], 3)
+            out.update(rocsparse_compare(gsa, M, K, N, row, col, val, dt, best_cand, args, local, flops, ev_ms, dev,
+                                         torch, min(reps, 20)))
         except Exception as ex:  # comparator problems must not hide the main number
             out["rocsparse"] = {"error": str(ex)}
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -503,9 +574,55 @@ def main():
         out["cpu_baseline"] = cpu_baseline(M, K, N, row, col, val, row_share=share)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    plan.free()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def n_sweep(gsa, M, K, row, col, val, cand, args, dt, local, e, tdt, dev, torch, nnz):
+    """the chosen pipeline at other dense widths (N in {8, 32, 128})"""
+    out = []
+    for n in [int(x) for x in args.n_sweep.split(",") if x]:
+        try:
+            plan, Bs, Cs, reps, _ = build_plan(gsa, M, K, row, col, val, cand, n, dt, local, args.rotation_mb, e, tdt,
+                                               dev, torch)
+        except gsa.GsError as ex:
+            out.append({"N": n, "error": str(ex)})
+            continue
+        ms = event_ms(plan, Bs, Cs, args.search_reps, torch)
+        out.append({"N": n, "kernel": kernel_label(plan.info()), "kernel_ms": round(ms, 5),
+                    "gflops": round(2.0 * nnz * n / (ms * 1e-3) / 1e9, 1)})
+        plan.free()
+        del Bs, Cs
+        torch.cuda.empty_cache()
+    return out
+
+
+def rocsparse_compare(gsa, M, K, N, row, col, val, dt, cand, args, local, flops, ev_ms, dev, torch, copies):
+    """rocSPARSE CSR SpMM on the same matrix (cold: rotated copies), fp16 inputs against
+    ours at fp16 and fp32 against ours at fp32 (the same plan, same rotation rule)"""
+    rs32 = rocsparse_baseline(M, K, N, row, col, val, copies, dtype=0)
+    res = {"rocsparse": {"f32": rs32}}
+    ours = flops / (ev_ms * 1e-3) / 1e9
+    if dt == "f32":
+        if rs32:
+            res["speedup_vs_rocsparse"] = round(ours / rs32["gflops"], 3)
+        return res
+    rs16 = rocsparse_baseline(M, K, N, row, col, val, copies, dtype=1)
+    res["rocsparse"]["f16"] = rs16 if rs16 else "every algorithm failed"
+    res["rocsparse"]["f16_note"] = "fp16 A and B, fp32 C and compute (rocsparse_spmm.h mixed precision)"
+    if rs16:
+        res["speedup_vs_rocsparse"] = round(ours / rs16["gflops"], 3)
+    plan, Bs, Cs, reps, _ = build_plan(gsa, M, K, row, col, val, cand, N, "f32", local, args.rotation_mb, 4,
+                                       torch.float32, dev, torch)
+    ms32 = event_ms(plan, Bs, Cs, args.search_reps, torch)
+    plan.free()
+    ours32 = flops / (ms32 * 1e-3) / 1e9
+    res["rocsparse"].update({"ours_f32_gflops": round(ours32, 1), "ours_f32_kernel_ms": round(ms32, 5)})
+    if rs32:
+        res["speedup_vs_rocsparse_f32"] = round(ours32 / rs32["gflops"], 3)
+    return res
 
 
 if __name__ == "__main__":

@@ -77,7 +77,9 @@ void add_replica(plan_state &p);
 void free_device(plan_state &p);
 // zero rows [lo, hi) of a row-major C of width N, element size e (sub-matrix executor)
 void memset_rows(void *C, uint64_t lo, uint64_t hi, uint32_t N, size_t e, hipStream_t stream);
-void launch_spmm(const plan_state &p, int replica, const void *B, void *C, uint32_t N, hipStream_t stream);
+void launch_spmm(plan_state &p, int replica, const void *B, void *C, uint32_t N, hipStream_t stream);
+// uploads the CSR arrays a matrix-core plan deferred (every replica), for a launch at another dense width
+void ensure_csr(plan_state &p);
 void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
                          size_t n_host);
 

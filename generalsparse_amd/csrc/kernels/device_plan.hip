@@ -576,6 +576,34 @@ constexpr size_t bm_lds_bytes(uint32_t CT, uint32_t RT, bm_shape v) {
 
 }  // namespace
 
+// the plan's column indices (u16 when they fit, else u32) and values (plan dtype) of
+// one replica, padded for the kernels' aligned over-reads
+void upload_csr(plan_state &p, device_arrays &a) {
+    const kernel_spec &sp = p.cg->get_kernel_spec();
+    const meta_data_set &m = *p.meta;
+    const int sb = p.cg->get_sub_matrix_id();
+    device_plan &d = p.dev;
+    HIP_OK(hipSetDevice(d.device));
+    const auto &col = m.u(GLOBAL_META, sp.interleaved ? "nz_col_indices_after_interlance_storage" : "nz_col_indices", sb);
+    auto vals = m.get_element(GLOBAL_META, sp.interleaved ? "nz_vals_after_interlance_storage" : "nz_vals", sb)->meta_data_arr;
+    const uint64_t nnz = col.size();
+    if (d.col_bytes == 2) {
+        std::vector<uint16_t> c16(col.begin(), col.end());
+        a.col = dev_copy(d, c16, kPad);
+    } else {
+        a.col = dev_copy(d, to_u32(col, "column index"), kPad);
+    }
+    if (d.dtype == 0) {
+        std::vector<float> v(nnz);
+        for (uint64_t i = 0; i < nnz; i++) v[i] = (float)vals->read_float_from_arr(i);
+        a.val = dev_copy(d, v, kPad);
+    } else {
+        std::vector<uint16_t> v(nnz);
+        for (uint64_t i = 0; i < nnz; i++) v[i] = f32_to_f16_bits((float)vals->read_float_from_arr(i));
+        a.val = dev_copy(d, v, kPad);
+    }
+}
+
 void upload_plan(plan_state &p, int dtype, int device) {
     GS_CHECK(p.cg && p.cg->is_compiled(), "plan must be compiled before upload");
     GS_CHECK(dtype == 0 || dtype == 1, "dtype must be 0 (fp32) or 1 (fp16)");
@@ -625,25 +653,17 @@ void upload_plan(plan_state &p, int dtype, int device) {
             return;
         }
     }
-    // A streams: narrowest column type that holds Kc-1 (u16 when Kc <= 65536)
+    // A streams: narrowest column type that holds Kc-1 (u16 when Kc <= 65536).  fp16 BMTB
+    // plans try the matrix cores first: their kernels never read the CSR arrays, which
+    // are then uploaded only if a launch at another dense width falls back to a gather
+    // kernel (ensure_csr), so A is not resident twice.
     uint64_t maxc = 0;
     for (uint64_t c : col) maxc = std::max(maxc, c);
     d.col_bytes = maxc <= 0xffff ? 2 : 4;
-    if (d.col_bytes == 2) {
-        std::vector<uint16_t> c16(col.begin(), col.end());
-        a.col = dev_copy(d, c16, kPad);
-    } else {
-        a.col = dev_copy(d, to_u32(col, "column index"), kPad);
-    }
-    if (dtype == 0) {
-        std::vector<float> v(nnz);
-        for (uint64_t i = 0; i < nnz; i++) v[i] = (float)vals->read_float_from_arr(i);
-        a.val = dev_copy(d, v, kPad);
-    } else {
-        std::vector<uint16_t> v(nnz);
-        for (uint64_t i = 0; i < nnz; i++) v[i] = f32_to_f16_bits((float)vals->read_float_from_arr(i));
-        a.val = dev_copy(d, v, kPad);
-    }
+    const bool defer_csr = dtype == 1 && get_config().MFMA_TILES &&
+                           (sp.family == KF_WARP_TOTAL || sp.family == KF_BLOCK_TOTAL) &&
+                           m.is_exist(TBLOCK_META, "first_row_indices", sb);
+    if (!defer_csr) upload_csr(p, a);
     uint64_t row_num = row_num_of_sub_matrix(m, sb);
     // matrix-core row blocks for fp16 plans with BMTBs (tried before the other kernels)
     auto try_mfma = [&](const std::vector<uint32_t> &rp0) {
@@ -921,8 +941,14 @@ void upload_plan(plan_state &p, int dtype, int device) {
         default:
             throw gs_error("no gfx950 kernel family for this plan");
     }
+    if (defer_csr && !d.mfma) upload_csr(p, a);
     d.replicas.push_back(a);
     p.uploaded = true;
+}
+
+void ensure_csr(plan_state &p) {
+    for (device_arrays &a : p.dev.replicas)
+        if (!a.col) upload_csr(p, a);
 }
 
 void add_replica(plan_state &p) {
@@ -1375,19 +1401,20 @@ void dispatch_vt(const plan_state &p, const device_arrays &a, const void *B, voi
 
 }  // namespace
 
-void launch_spmm(const plan_state &p, int replica, const void *B, void *C, uint32_t N, hipStream_t stream) {
+void launch_spmm(plan_state &p, int replica, const void *B, void *C, uint32_t N, hipStream_t stream) {
     GS_CHECK(p.uploaded, "plan is not on the device");
     GS_CHECK(replica >= 0 && (size_t)replica < p.dev.replicas.size(), "bad replica index");
     GS_CHECK(N >= 1, "N >= 1");
-    const device_arrays &a = p.dev.replicas[replica];
     if (p.dev.nm) {
-        launch_nm(p, a, B, C, N, stream);
+        launch_nm(p, p.dev.replicas[replica], B, C, N, stream);
         return;
     }
     if (p.dev.mfma && N == p.dev.lds_N) {
-        launch_mfma(p, a, B, C, N, stream);
+        launch_mfma(p, p.dev.replicas[replica], B, C, N, stream);
         return;
     }
+    if (!p.dev.replicas[replica].col) ensure_csr(p);  // matrix-core plan at another dense width
+    const device_arrays &a = p.dev.replicas[replica];
     if (p.dev.dtype == 0) dispatch_vt<float, 4>(p, a, B, C, N, stream);
     else dispatch_vt<gsk::f16, 8>(p, a, B, C, N, stream);
 }

@@ -1401,3 +1401,44 @@ int or_time_spmm_repeated(uint64_t M, uint64_t K, uint64_t nnz, const uint64_t *
     *reps = r;
     return 0;
 }
+
+/* The build's all-cores variant of the host SpMM (NOT the reference's: its host path is
+ * single-threaded): the same fp32 products and row sums over a CSR of the
+ * row-sorted COO, rows split over `threads` OpenMP threads.  Timed like
+ * or_time_spmm_repeated. */
+int or_time_spmm_repeated_mt(uint64_t M, uint64_t K, uint64_t nnz, const uint64_t *row,
+                             const uint64_t *col, const float *val, uint64_t N, double min_s,
+                             int threads, double *t_total, int *reps) {
+    float *B = (float *)malloc(K * N * sizeof(float));
+    float *C = (float *)malloc(M * N * sizeof(float));
+    uint64_t *rp = (uint64_t *)calloc(M + 1, sizeof(uint64_t));
+    if (!B || !C || !rp) { free(B); free(C); free(rp); return -1; }
+    for (uint64_t i = 0; i < K * N; i++) B[i] = (float)((i * 2654435761u) % 1000) / 1000.f - 0.5f;
+    for (uint64_t p = 0; p < nnz; p++) {
+        if (row[p] >= M || (p && row[p] < row[p - 1])) { free(B); free(C); free(rp); return -2; }
+        rp[row[p] + 1]++;
+    }
+    for (uint64_t i = 0; i < M; i++) rp[i + 1] += rp[i];
+    int r = 0;
+    double t0 = now_s(), t = 0;
+    do {
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 64)
+        for (int64_t i = 0; i < (int64_t)M; i++) {
+            float *c = C + (uint64_t)i * N;
+            for (uint64_t j = 0; j < N; j++) c[j] = 0.f;
+            for (uint64_t p = rp[i]; p < rp[i + 1]; p++) {
+                const float v = val[p];
+                const float *b = B + col[p] * N;
+                for (uint64_t j = 0; j < N; j++) c[j] += v * b[j];
+            }
+        }
+        r++;
+        t = now_s() - t0;
+    } while (t < min_s);
+    volatile float sink = C[0];
+    (void)sink;
+    free(B); free(C); free(rp);
+    *t_total = t;
+    *reps = r;
+    return 0;
+}

@@ -123,6 +123,10 @@ int or_time_cpu_path(uint64_t M, uint64_t K, uint64_t nnz, const uint64_t *row,
 int or_time_spmm_repeated(uint64_t M, uint64_t K, uint64_t nnz, const uint64_t *row,
                           const uint64_t *col, const float *val, uint64_t N, double min_s,
                           double *t_total, int *reps);
+/* the build's all-cores variant (OpenMP over rows; the reference's host path is single-threaded) */
+int or_time_spmm_repeated_mt(uint64_t M, uint64_t K, uint64_t nnz, const uint64_t *row,
+                             const uint64_t *col, const float *val, uint64_t N, double min_s,
+                             int threads, double *t_total, int *reps);
 
 #ifdef __cplusplus
 }

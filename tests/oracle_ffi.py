@@ -123,6 +123,26 @@ def time_cpu_path(M, K, row, col, val, N):
     return t1.value, t2.value
 
 
+def time_spmm_repeated_mt(M, K, row, col, val, N, min_s, threads):
+    """the build's all-cores host SpMM (OpenMP over rows) repeated for >= min_s seconds"""
+    L = lib()
+    L.or_time_spmm_repeated_mt.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                           ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                           ctypes.POINTER(ctypes.c_float), ctypes.c_uint64, ctypes.c_double,
+                                           ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_int)]
+    row = np.ascontiguousarray(row, dtype=np.uint64)
+    col = np.ascontiguousarray(col, dtype=np.uint64)
+    val = np.ascontiguousarray(val, dtype=np.float32)
+    t = ctypes.c_double()
+    r = ctypes.c_int()
+    rc = L.or_time_spmm_repeated_mt(M, K, len(row), _p(row, ctypes.c_uint64), _p(col, ctypes.c_uint64),
+                                    _p(val, ctypes.c_float), N, min_s, int(threads), ctypes.byref(t), ctypes.byref(r))
+    if rc != 0:
+        raise RuntimeError("oracle cpu path failed")
+    return t.value, r.value
+
+
 def time_spmm_repeated(M, K, row, col, val, N, min_s):
     """host fp32 SpMM repeated for >= min_s seconds: (seconds, repetitions)"""
     L = lib()
