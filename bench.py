@@ -288,58 +288,23 @@ def cpu_baseline(M, K, N, row, col, val, min_s=10.0, row_share=1):
                           "sample": f"{what} x{reps_mt} in {t_mt:.1f} s"}}
 
 
-# C5 (BASELINE.json configs[4]): all OPT-30B layers, 80% unstructured, fp16, N = 32.  Per layer
-# q, k, v, out (7168 x 7168), fc1 (28672 x 7168), fc2 (7168 x 28672).
-C5_SHAPES = {"attn": (7168, 7168), "fc1": (28672, 7168), "fc2": (7168, 28672)}
-C5_SLOTS = ["attn", "attn", "attn", "attn", "fc1", "fc2"]
-
-
-def lpt_assign(sizes, world):
-    """longest-processing-time greedy: matrix i -> rank"""
-    load = [0] * world
-    owner = [0] * len(sizes)
-    for i in sorted(range(len(sizes)), key=lambda i: -sizes[i]):
-        r = min(range(world), key=lambda r: load[r])
-        owner[i] = r
-        load[r] += sizes[i]
-    return owner, load
-
-
 def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
-    """The batch is split over the ranks by LPT on nnz; each rank runs its share of
-    SpMMs per step (no exchange).  One distinct seeded matrix per shape per rank;
-    every matrix instance of the batch streams its own HBM copy of A (a plan
-    replica), so no instance is served from a cache another one warmed."""
-    N, sp = args.N, 0.8
-    batch = [(l, s, C5_SLOTS[s]) for l in range(args.layers) for s in range(len(C5_SLOTS))]
-    nnz_of = {k: int(round((1 - sp) * m * n)) for k, (m, n) in C5_SHAPES.items()}
-    owner, load = lpt_assign([nnz_of[b[2]] for b in batch], world)
-    mine = [b for b, o in zip(batch, owner) if o == rank]
-    count = {k: sum(1 for b in mine if b[2] == k) for k in C5_SHAPES}
-    plans, Bs, Cs = {}, {}, {}
+    """BASELINE.json configs[4]: the OPT-30B batch split over the ranks by LPT on nnz
+    (generalsparse_amd/batch.py); each rank runs its share of SpMMs per step, no
+    exchange.  One distinct seeded matrix per shape per rank; every matrix instance of
+    the batch streams its own HBM copy of A (a plan replica)."""
+    from generalsparse_amd import batch as bt
+    N = args.N
+    batch, owner, load = bt.c5_assignment(args.layers, world)
+    seq = bt.rank_sequence(batch, owner, rank)
     t0 = time.perf_counter()
-    for k, (m, n) in C5_SHAPES.items():
-        if not count[k]:
-            continue
-        row, col, val = ds.pruned_weight(m, n, sp, 1000 + 8 * rank + list(C5_SHAPES).index(k))
-        plan = gsa.Plan.from_coo(m, n, row, col, val).run_pipeline("tblock_warp_total", N, 20, 2).compile()
-        plan.upload("f16", local)
-        for _ in range(count[k] - 1):
-            plan.add_replica()
-        plans[k] = plan
-        Bs[k] = [torch.randn((n, N), device=dev, dtype=torch.float16) for _ in range(2)]
-        Cs[k] = [torch.empty((m, N), device=dev, dtype=torch.float16) for _ in range(2)]
-        del row, col, val
+    plans, launches, _ = bt.build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local)
     t_setup = time.perf_counter() - t0
     stream = torch.cuda.current_stream().cuda_stream
-    seq = []
-    rep = {k: 0 for k in C5_SHAPES}
-    for i, (_, _, k) in enumerate(mine):
-        seq.append((plans[k], rep[k], Bs[k][i % 2].data_ptr(), Cs[k][i % 2].data_ptr()))
-        rep[k] += 1
+    raw = [(p, r, b.data_ptr(), c.data_ptr()) for (p, r, b, c, _) in launches]
 
     def step():
-        for plan, r, b, c in seq:
+        for plan, r, b, c in raw:
             plan.spmm_raw(b, c, N, r, stream)
 
     for _ in range(args.warmup):
@@ -355,13 +320,14 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
     wall = max_over_ranks(time.perf_counter() - t1, dist, torch)
     if dist is not None:
         dist.barrier()
-    total_nnz = sum(nnz_of[b[2]] for b in batch)
+    total_nnz = sum(bt.nnz_of_shape(b[2]) for b in batch)
     flops = 2.0 * total_nnz * N
     value = flops * args.steps / wall / 1e9
     e = 2
-    alg = sum(nnz_of[k] * (e + 2) + (C5_SHAPES[k][0] + 1) * 4 + C5_SHAPES[k][1] * N * e + C5_SHAPES[k][0] * N * e
-              for (_, _, k) in batch)
+    alg = sum(bt.nnz_of_shape(k) * (e + 2) + (bt.C5_SHAPES[k][0] + 1) * 4 + bt.C5_SHAPES[k][1] * N * e +
+              bt.C5_SHAPES[k][0] * N * e for (_, _, k) in batch)
     ms = wall / args.steps * 1e3
+    info = next(iter(plans.values())).info()
     out = {
         "metric": "SpMM GFLOP/s, OPT-30B 80%-pruned weight batch fp16 N=32 (configs[4])",
         "value": round(value, 1), "unit": "GFLOP/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -371,7 +337,7 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
                 "its own HBM copy of A)",
         "config": {"workload": f"OPT-30B weight batch: {args.layers} layers x (4 x 7168^2, 28672x7168, 7168x28672), "
                                f"80% unstructured, fp16, N={N}", "matrices": len(batch), "nnz": total_nnz,
-                   "plan": "tblock_warp_total(20,2)", "kernel": kernel_label(next(iter(plans.values())).info()),
+                   "plan": "tblock_warp_total(20,2)", "kernel": kernel_label(info),
                    "parallelism": f"LPT batch split x{world} (max rank nnz share {max(load) / total_nnz:.4f})"},
         "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9 / world, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / world / HBM_PEAK_GBS, 4),

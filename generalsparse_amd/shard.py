@@ -86,22 +86,41 @@ def local_coo(row, col, val, sh):
     return sh.row_hi - sh.row_lo + 1, r, col[sh.z0:sh.z1], val[sh.z0:sh.z1]
 
 
-def combine_boundaries(C_local, shards, rank, dist, torch):
+def edge_rows(row, col, val, sh):
+    """the shard's first and last row as a 2-row COO (rows 0 and 1; the same row twice when
+    the shard holds one row): the rows a nnz-exact split can share with other ranks"""
+    if sh.row_hi < sh.row_lo:
+        return None
+    r = np.asarray(row[sh.z0:sh.z1], dtype=np.int64)
+    first = r == sh.row_lo
+    last = r == sh.row_hi
+    rr = np.concatenate([np.zeros(first.sum(), np.uint64), np.ones(last.sum(), np.uint64)])
+    cc = np.concatenate([col[sh.z0:sh.z1][first], col[sh.z0:sh.z1][last]])
+    vv = np.concatenate([val[sh.z0:sh.z1][first], val[sh.z0:sh.z1][last]])
+    return rr, cc, vv
+
+
+def combine_boundaries(C_local, shards, rank, dist, torch, edges_fp32=None):
     """nnz-exact shards: the exchange step.  Every rank publishes the partial of its
     first row in its slot of a world x N buffer; one all-reduce (SUM, one writer per
     slot) gathers them; a rank whose last row continues into later ranks (it starts
     that row) adds their partials in rank order.  C_local: (rows held, N) tensor on
-    this rank's device, rows [row_lo, row_hi] of C.  Returns the index of the first
-    complete row of C_local (1 when another rank starts our first row)."""
+    this rank's device, rows [row_lo, row_hi] of C.  edges_fp32: optional (2, N) fp32
+    partials of the shard's first and last rows (e.g. from a 2-row fp32 side plan over
+    ``edge_rows``), so fp16 plans round a split row once, after the sum; without it the
+    partials are read from C_local.  Returns the index of the first complete row of
+    C_local (1 when another rank starts our first row)."""
     world = len(shards)
     sh = shards[rank]
     has = sh.row_hi >= sh.row_lo
     buf = torch.zeros((world, C_local.shape[1]), dtype=torch.float32, device=C_local.device)
+    first = edges_fp32[0] if edges_fp32 is not None else (C_local[0].float() if has else None)
+    last = edges_fp32[1] if edges_fp32 is not None else (C_local[-1].float() if has else None)
     if has:
-        buf[rank] = C_local[0].float()
+        buf[rank] = first
     dist.all_reduce(buf, op=dist.ReduceOp.SUM)
     if has and (sh.owns_first or sh.row_hi != sh.row_lo):
-        acc = C_local[-1].float()
+        acc = last.clone()
         for q in range(rank + 1, world):
             s = shards[q]
             if s.row_hi < s.row_lo or s.row_lo != sh.row_hi:

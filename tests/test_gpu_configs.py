@@ -1,0 +1,193 @@
+"""Every BASELINE.json config once on the GPU, at full size, through the C ABI
+(VERDICT r01 "configs_untested"), plus the emitted programs and the token_test CLI.
+
+- C1 IG5-18 stand-in: `token_test <mtx> 8 --f32` on a written .mtx (the reference's
+  entry, token_test.cc:1625-1847): the reader, thread_total(4,1), the all-ones known
+  answer checked bit-exactly inside the CLI, and the two-line perf_result
+  (code_generator.cc:643-648).
+- C3 OPT-30B fc1 2:4, 28672 x 7168, fp16, N=128: k_nm_mfma against a torch fp32 dense
+  matmul of the same fp16 inputs.
+- C4 webbase-1M stand-in (1,000,005^2, 3,105,536 nnz, fp32, N=8): merge path against the
+  oracle's SpMM.  com-Orkut stand-in (3,072,441^2, 234,370,166 nnz, drawn on the GPU):
+  all-ones known answer bit-exactly, and a seeded row sample against numpy fp64.
+- C5 OPT-30B 80% batch: each of the three shapes against torch fp32, and two layers of
+  the batch through the same assignment / sequence code bench.py's run_c5 uses.
+- The generated programs build() emitted and compiled (A16; executor.cc:6-104): each runs,
+  prints "correct" and writes perf_result.
+
+Tolerances (north_star): fp32 1e-3, fp16 1e-1, relative to max(1, |ref|)."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_ffi as ofi
+
+torch = pytest.importorskip("torch")
+import generalsparse_amd as gsa  # noqa: E402
+from generalsparse_amd import batch as bt  # noqa: E402
+from generalsparse_amd import datasets as ds  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+PKG = os.path.dirname(gsa.__file__)
+TOL = {"f32": 1e-3, "f16": 1e-1}
+
+
+def check(C, ref, dtype):
+    err = np.abs(C - ref) / np.maximum(1.0, np.abs(ref))
+    assert err.max() <= TOL[dtype], f"max rel err {err.max()} > {TOL[dtype]}"
+
+
+def dense_ref(M, K, row, col, val, B):
+    """torch fp32 dense matmul of the fp16-rounded A with B (on the GPU)"""
+    A = torch.zeros((M, K), dtype=torch.float32, device=DEV)
+    r = torch.from_numpy(row.astype(np.int64)).to(DEV)
+    c = torch.from_numpy(col.astype(np.int64)).to(DEV)
+    A[r, c] = torch.from_numpy(val.astype(np.float16).astype(np.float32)).to(DEV)
+    out = (A @ B.float()).cpu().numpy()
+    del A
+    torch.cuda.empty_cache()
+    return out
+
+
+# ------------------------------------------------------------------ emitted programs
+def test_emitted_programs_run_and_check():
+    man_path = os.path.join(PKG, "emitted", "manifest.json")
+    assert os.path.exists(man_path), "build() emits and compiles the example programs"
+    man = json.load(open(man_path))
+    assert len(man) >= 5
+    for name, m in man.items():
+        d = os.path.join(PKG, m["dir"])
+        r = subprocess.run(["./a.out"], cwd=d, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0 and "correct" in r.stdout, (name, r.stdout[-2000:], r.stderr[-2000:])
+        lines = open(os.path.join(d, "perf_result")).read().split("\n")
+        assert len(lines) == 3 and lines[2] == "", lines   # "<ms>\n<GFLOP/s>\n"
+        ms, gf = float(lines[0]), float(lines[1])
+        assert ms > 0 and gf > 0, (name, lines)
+
+
+# ------------------------------------------------------------------ C1
+def test_c1_token_test_ig5_18_standin(tmp_path):
+    M, K = 47894, 41550
+    row, col, val = ds.random_rows(M, K, 1790490 / 47894, 18)
+    mtx = tmp_path / "IG5-18-standin.mtx"
+    ds.write_mtx(str(mtx), M, K, row, col, val)
+    env = dict(os.environ, GS_ROOT_PATH=str(tmp_path))
+    r = subprocess.run([os.path.join(PKG, "token_test"), str(mtx), "8", "--f32"], capture_output=True, text=True,
+                       env=env, timeout=300)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert "wrong number:0" in r.stdout and "correct" in r.stdout
+    assert f"rows={M} cols={K} nnz={len(row)}" in r.stdout
+    prs = list(tmp_path.glob("data_source/*/perf_result"))
+    assert len(prs) == 1
+    lines = prs[0].read_text().split("\n")
+    assert len(lines) == 3 and float(lines[0]) > 0 and float(lines[1]) > 0
+
+
+# ------------------------------------------------------------------ C3
+def test_c3_full_size_against_torch():
+    M, K, N = 28672, 7168, 128
+    row, col, val = ds.two_four(M, K, 30)
+    plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline("col_direction_nm", N, 32, 1).compile().upload("f16", 0)
+    assert plan.info()["device_kernel"] == "k_nm_mfma"
+    g = torch.Generator(device=DEV)
+    g.manual_seed(3)
+    B = (torch.rand((K, N), device=DEV, generator=g) * 2 - 1).half()
+    C = plan.spmm(B)
+    torch.cuda.synchronize()
+    check(C.float().cpu().numpy(), dense_ref(M, K, row, col, val, B), "f16")
+    plan.free()
+
+
+# ------------------------------------------------------------------ C4
+def test_c4_webbase_standin_against_oracle():
+    M, N = 1000005, 8
+    row, col, val = ds.rmat(M, 3105536, 1)
+    assert len(row) == 3105536
+    plan = gsa.Plan.from_coo(M, M, row, col, val).run_pipeline("merge_path", N, 512, 1).compile().upload("f32", 0)
+    assert plan.info()["device_kernel"] == "k_merge_path"
+    B = np.random.default_rng(4).uniform(-1, 1, (M, N)).astype(np.float32)
+    C = plan.spmm(torch.from_numpy(B).to(DEV))
+    torch.cuda.synchronize()
+    ref = ofi.spmm_ref(M, N, row, col, val, B, "f64")
+    check(C.cpu().numpy(), ref, "f32")
+    plan.free()
+
+
+@pytest.mark.timeout(300)
+def test_c4_orkut_standin_known_answer_and_row_sample():
+    M, NNZ, N = 3072441, 234370166, 8
+    row, col, _ = ds.rmat_torch(M, NNZ, 2, DEV, symmetric=True)
+    assert len(row) == NNZ
+    print("orkut stand-in drawn", flush=True)
+    ones = np.ones(len(row), np.float32)
+    plan = gsa.Plan.from_coo(M, M, row, col, ones).run_pipeline("merge_path", N, 512, 1).compile().upload("f32", 0)
+    assert plan.info()["device_kernel"] == "k_merge_path"
+    print("orkut plan on the device", flush=True)
+    C = plan.spmm(torch.ones((M, N), device=DEV, dtype=torch.float32)).cpu().numpy()
+    nnz_row = np.bincount(row.astype(np.int64), minlength=M).astype(np.float32)
+    np.testing.assert_array_equal(C, np.repeat(nnz_row[:, None], N, axis=1))   # known answer, exact
+    g = torch.Generator(device=DEV)
+    g.manual_seed(9)
+    Bt = torch.rand((M, N), device=DEV, generator=g) * 2 - 1
+    C2 = plan.spmm(Bt).cpu().numpy()
+    Bn = Bt.cpu().numpy().astype(np.float64)
+    rp = np.concatenate([[0], np.cumsum(nnz_row.astype(np.int64))])
+    rows = np.random.default_rng(11).choice(M, 3000, replace=False)
+    rows = np.concatenate([rows, np.argsort(-nnz_row)[:20]])   # and the longest rows
+    for r in rows:
+        ref = Bn[col[rp[r]:rp[r + 1]].astype(np.int64)].sum(axis=0) if rp[r + 1] > rp[r] else np.zeros(N)
+        check(C2[r][None], ref[None], "f32")
+    plan.free()
+
+
+# ------------------------------------------------------------------ C5
+@pytest.fixture(scope="module")
+def c5_coo():
+    return {k: ds.pruned_weight(m, n, bt.C5_SPARSITY, bt.shape_seed(0, k)) for k, (m, n) in bt.C5_SHAPES.items()}
+
+
+def test_c5_shapes_against_torch(c5_coo):
+    N = 32
+    for k, (m, n) in bt.C5_SHAPES.items():
+        row, col, val = c5_coo[k]
+        assert len(row) == bt.nnz_of_shape(k)
+        plan = gsa.Plan.from_coo(m, n, row, col, val).run_pipeline("tblock_warp_total", N, 20, 2).compile()
+        plan.upload("f16", 0)
+        assert plan.info()["device_kernel"].startswith("k_mfma"), plan.info()["device_kernel"]
+        g = torch.Generator(device=DEV)
+        g.manual_seed(5)
+        B = (torch.rand((n, N), device=DEV, generator=g) * 2 - 1).half()
+        C = plan.spmm(B)
+        torch.cuda.synchronize()
+        check(C.float().cpu().numpy(), dense_ref(m, n, row, col, val, B), "f16")
+        plan.free()
+
+
+def test_c5_two_layer_batch_sequence():
+    """two layers of the batch on one rank through generalsparse_amd.batch (bench.py run_c5):
+    every launch of the sequence, with its replica and its B/C pair, gives that shape's
+    product"""
+    N = 32
+    batch, owner, load = bt.c5_assignment(2, 1)
+    seq = bt.rank_sequence(batch, owner, 0)
+    assert len(seq) == 12
+    plans, launches, coo = bt.build_rank_batch(seq, 0, N, gsa, ds, torch, DEV, 0, keep_coo=True)
+    assert {k: p.info()["replicas"] for k, p in plans.items()} == {"attn": 8, "fc1": 2, "fc2": 2}
+    stream = torch.cuda.current_stream().cuda_stream
+    refs = {}
+    for i, (plan, rep, B, C, k) in enumerate(launches):
+        C.fill_(float("nan"))
+        plan.spmm_raw(B.data_ptr(), C.data_ptr(), N, rep, stream)
+        torch.cuda.synchronize()
+        key = (k, i % 2)
+        if key not in refs:
+            m, n = bt.C5_SHAPES[k]
+            refs[key] = dense_ref(m, n, *coo[k], B)
+        check(C.float().cpu().numpy(), refs[key], "f16")
+    for p in plans.values():
+        p.free()

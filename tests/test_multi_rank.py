@@ -64,14 +64,57 @@ def test_c5_lpt_split_is_balanced():
     1, 2, 4 and 8 ranks (balance within 2%)"""
     if ROOT not in sys.path:
         sys.path.insert(0, ROOT)
-    import bench
-    batch = [bench.C5_SLOTS[s] for _ in range(48) for s in range(len(bench.C5_SLOTS))]
-    sizes = [int(round(0.2 * m * n)) for m, n in (bench.C5_SHAPES[k] for k in batch)]
-    assert sum(sizes) == 48 * (4 * 10276045 + 2 * 41104179)
+    from generalsparse_amd import batch as bt
     for world in (1, 2, 4, 8):
-        owner, load = bench.lpt_assign(sizes, world)
+        batch, owner, load = bt.c5_assignment(48, world)
+        sizes = [bt.nnz_of_shape(b[2]) for b in batch]
+        assert sum(sizes) == 48 * (4 * 10276045 + 2 * 41104179)
         assert len(owner) == 288 and set(owner) == set(range(world))
         assert max(load) / min(load) <= 1.02
+
+
+def _c5_main(rank, world, port, layers, out):
+    """run_c5's per-rank part without the GPU: the assignment every rank computes on its
+    own, its launch sequence, and the job nnz gathered over the ranks"""
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from generalsparse_amd import batch as bt
+    batch, owner, load = bt.c5_assignment(layers, world)
+    seq = bt.rank_sequence(batch, owner, rank)
+    mine = torch.tensor([float(sum(bt.nnz_of_shape(s[2]) for s in seq))], dtype=torch.float64)
+    allv = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(allv, mine)
+    out[rank] = (seq, [v.item() for v in allv], owner)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("layers", [2, 48])
+def test_c5_batch_sequence_two_gloo_ranks(layers):
+    """the C5 batch over 2 gloo ranks: both ranks compute the same LPT assignment, their
+    launch sequences cover every matrix of the batch exactly once in layer order, replica
+    k of a shape is that shape's k-th instance on the rank, and the gathered per-rank nnz
+    add up to the batch (bench.py run_c5's assignment and sequencing)"""
+    sys.path.insert(0, ROOT)
+    from generalsparse_amd import batch as bt
+    port = _free_port()
+    with mp.Manager() as man:
+        out = man.dict()
+        mp.spawn(_c5_main, args=(2, port, layers, out), nprocs=2, join=True)
+        res = dict(out)
+    assert res[0][2] == res[1][2]                         # one assignment, computed twice
+    covered = sorted((l, s) for r in (0, 1) for (l, s, _, _) in res[r][0])
+    assert covered == [(l, s) for l in range(layers) for s in range(6)]
+    for r in (0, 1):
+        seq = res[r][0]
+        assert [(l, s) for (l, s, _, _) in seq] == sorted((l, s) for (l, s, _, _) in seq)
+        for shape in bt.C5_SHAPES:
+            reps = [k for (_, _, sh, k) in seq if sh == shape]
+            assert reps == list(range(len(reps)))
+    total = sum(bt.nnz_of_shape(b[2]) for b in bt.c5_batch(layers))
+    assert res[0][1] == res[1][1] and sum(res[0][1]) == total
+    assert max(res[0][1]) / min(res[0][1]) <= (1.02 if layers == 48 else 1.5)
 
 
 def _shard_main(rank, world, port, mode, out):
@@ -95,7 +138,13 @@ def _shard_main(rank, world, port, mode, out):
     sh = shards[rank]
     m, r, c, v = sd.local_coo(row, col, val, sh)
     C_local = torch.from_numpy(ofi.spmm_ref(m, N, r, c, v, B, "f64").astype(np.float32)) if m else torch.zeros((0, N))
-    first = sd.combine_boundaries(C_local, shards, rank, dist, torch) if mode == "nnz" else 0
+    edges = None
+    if mode == "nnz" and m:
+        er, ec, ev = sd.edge_rows(row, col, val, sh)
+        edges = torch.from_numpy(ofi.spmm_ref(2, N, er, ec, ev, B, "f64").astype(np.float32))
+        C_local = C_local.half()   # an fp16 plan's output; the split rows use the fp32 edge partials
+    first = sd.combine_boundaries(C_local, shards, rank, dist, torch, edges) if mode == "nnz" else 0
+    C_local = C_local.float()
     out[rank] = (sh.row_lo + first, C_local[first:].numpy().copy(), sh.z1 - sh.z0)
     dist.barrier()
     dist.destroy_process_group()
@@ -133,6 +182,10 @@ def test_single_matrix_shards_combine_to_full_spmm(mode, world):
     assert sum(res[r][2] for r in range(world)) == len(row)
     held = seen > 0
     assert (seen <= 1).all()
-    np.testing.assert_allclose(got[held], ref[held], rtol=1e-5, atol=1e-5)
+    tol = 1e-3 if mode == "nnz" else 1e-5   # nnz mode: fp16 rows, split rows rounded once after the fp32 sum
+    np.testing.assert_allclose(got[held], ref[held], rtol=tol, atol=tol)
+    if mode == "nnz":
+        long_row = got[100]    # split over every rank: exactly the fp16 rounding of the fp32 sum
+        np.testing.assert_array_equal(long_row, ref[100].astype(np.float32).astype(np.float16).astype(np.float64))
     # rows no rank holds are the trailing empty rows (zero in the full product)
     assert np.all(ref[~held] == 0)
