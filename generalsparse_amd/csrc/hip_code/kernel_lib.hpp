@@ -814,7 +814,12 @@ constexpr int kMfmaBWavesG = 2, kMfmaAWavesG = 8;
 
 // STAMPS (diagnostic build only, gs_debug_mfma_timeline): lane 0 of the first
 // compute / B / entry wave records s_memtime at phase boundaries
-template <int CT, int RT, int LGKC, int MAXA, bool STAMPS = false, int GLDS = 0>
+// NBG (GLDS only): B buffers, the B rows of chunk j + NBG - 1 issued in period j
+// WCT: compute waves (the entry waves are the other 16 - WCT - B waves)
+// DBG (diagnostic timing builds only, wrong results): 1 no B DMA, 2 no scatter, 4 no compute-wave
+// LDS reads or clears, 8 no entry loads
+template <int CT, int RT, int LGKC, int MAXA, bool STAMPS = false, int GLDS = 0, int NBG = 3, int WCT = kMfmaCompute,
+          int DBG = 0>
 __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
     const uint32_t *__restrict__ seg_start,       // n_bmtb*nc+1 (groups)
@@ -828,9 +833,9 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     constexpr uint32_t UB = 2 * CT;                   // 16-B units per B row
     constexpr uint32_t RS = 2 * KC + 32;              // dense image row stride
     constexpr uint32_t NT = 64 * kMfmaWaves;
-    constexpr uint32_t WC = kMfmaCompute;
+    constexpr uint32_t WC = WCT;
     constexpr uint32_t BWV = GLDS ? GLDS : kMfmaBWaves;
-    constexpr uint32_t NBT = 64 * BWV, NAT = 64 * (GLDS ? 10 - GLDS : kMfmaAWaves);  // B / entry threads
+    constexpr uint32_t NBT = 64 * BWV, NAT = 64 * (kMfmaWaves - WC - BWV);  // B / entry threads
     constexpr uint32_t szB = KC * RB;
     constexpr uint32_t NB = szB / 16 / NBT;           // B units per B thread per chunk
     static_assert(szB % (16 * NBT) == 0, "whole B units per B thread");
@@ -840,7 +845,8 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     // register-staged B: two B buffers + three dense images; GLDS (B by LDS-DMA, two
     // chunks ahead): three B buffers + two dense images, each compute wave clearing the
     // k-step columns it read
-    constexpr uint32_t NBUF = GLDS ? 3u : 2u, NDI = GLDS ? 2u : 3u;
+    constexpr uint32_t NBUF = GLDS ? (uint32_t)NBG : 2u, NDI = GLDS ? 2u : 3u;
+    static_assert(!GLDS || NBG >= 3, "LDS-DMA B ring of at least three buffers");
     const uint32_t oD = NBUF * szB;                   // dense images follow the B buffers
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t role = wv < WC ? 0u : (wv < WC + BWV ? 1u : 2u);  // wave-uniform
@@ -897,14 +903,15 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
                 const uint32_t st = wv + q * WC;
                 const uint32_t kb = (st < nsteps ? st : 0u) * 32u + 8u * (lane >> 4);
 #pragma unroll
-                for (int rt = 0; rt < RT; rt++) av[q][rt] = *reinterpret_cast<const h8v *>(la + arow[rt] + kb * 2u);
+                for (int rt = 0; rt < RT; rt++)
+                    av[q][rt] = (DBG & 4) ? h8v{} : *reinterpret_cast<const h8v *>(la + arow[rt] + kb * 2u);
 #pragma unroll
                 for (int ct = 0; ct < CT; ct++) {
                     s4v t[2];
 #pragma unroll
                     for (int h = 0; h < 2; h++) {
                         const uint32_t k = kb + 4u * h + ((lane & 15u) >> 2);
-                        t[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        t[h] = (DBG & 4) ? s4v{} : __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                             (lds_s4v *)(lb + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u));
                     }
                     __builtin_memcpy(&bv[q][ct], t, 16);
@@ -924,7 +931,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
             if constexpr (GLDS) {
                 // image j%2 holds chunk j+2 next: clear the k-step columns this wave read
                 // (its MFMAs consumed the reads; no other wave reads these columns)
-                if (j + 2 < ncl) {
+                if (j + 2 < ncl && !(DBG & 4)) {
                     unsigned char *dj = lds + oD + (j & 1u) * szD;
 #pragma unroll
                     for (int q = 0; q < MAXS; q++) {
@@ -968,22 +975,37 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
                 const uint32_t kk = kc0 + k < K ? kc0 + k : kc0;
                 const f16 *src = B + (size_t)kk * N + (b_piece<CT>(k, s >> 1) * 2u + (s & 1u)) * 8u;
                 __builtin_amdgcn_global_load_lds(
-                    (const void *)src, (__attribute__((address_space(3))) void *)(lds + (jl % 3u) * szB + u0 * 16u), 16,
-                    0, 0);
+                    (const void *)src, (__attribute__((address_space(3))) void *)(lds + (jl % NBUF) * szB + u0 * 16u),
+                    16, 0, 0);
             }
         };
-        issue(0u);
-        if (1u < ncl) issue(1u);
-        __syncthreads();  // dense images cleared (its vmcnt(0) retires chunks 0 and 1)
+        for (uint32_t jl = 0; jl + 1 < NBUF && jl < ncl; jl++)
+            if (!(DBG & 1)) issue(jl);
+        __syncthreads();  // dense images cleared (its vmcnt(0) retires the first chunks)
         GS_STAMP(1u);
         __syncthreads();  // chunk 0 staged
         for (uint32_t j = 0; j < ncl; j++) {
-            if (j + 2 < ncl) {
-                issue(j + 2);
-                // chunk j+1 retired; vmcnt holds at most 63 (a larger NB waits for part of j+2 too)
-                __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"(NB < 63u ? NB : 63u) : "memory");
+            if (j + NBUF - 1 < ncl) {
+                if (!(DBG & 1)) issue(j + NBUF - 1);
+                // chunk j+1 retired, chunks j+2 .. j+NBUF-1 left in flight
+                // (vmcnt holds at most 63: a larger count waits for more than chunk j+1)
+                __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 2) * NB < 63u ? (NBUF - 2) * NB : 63u) : "memory");
             } else {
-                __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                // tail: chunks j+2 .. ncl-1 are in flight
+                const uint32_t left = ncl > j + 2 ? ncl - j - 2 : 0u;
+                if constexpr (NBUF >= 5) {
+                    if (left >= 3) __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NB < 63u ? 3 * NB : 63u) : "memory");
+                    else if (left == 2) __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NB < 63u ? 2 * NB : 63u) : "memory");
+                    else if (left == 1) __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"(NB < 63u ? NB : 63u) : "memory");
+                    else __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                } else if constexpr (NBUF == 4) {
+                    if (left >= 2) __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NB < 63u ? 2 * NB : 63u) : "memory");
+                    else if (left == 1) __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"(NB < 63u ? NB : 63u) : "memory");
+                    else __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                } else {
+                    if (left >= 1) __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"(NB < 63u ? NB : 63u) : "memory");
+                    else __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
             }
             GS_STAMP(2u + 2u * j);
             __builtin_amdgcn_s_barrier();
@@ -1078,9 +1100,9 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         // chunk j: fetch j+4 into set j%4, scatter j+1 from set (j+1)%4
 #define GS_AITER(j, Pn, Vn, Ps, Vs)                                                                 \
     {                                                                                             \
-        GS_ALOAD((j) + 4, Pn, Vn);                                                                \
+        if (!(DBG & 8)) GS_ALOAD((j) + 4, Pn, Vn);                                                \
         GS_STAMP(2u + 2u * (j)); /* entry role: loads issued, then scatter done */                \
-        if ((j) + 1 < ncl) GS_SCATTER((j) + 1, Ps, Vs);                                           \
+        if ((j) + 1 < ncl && !(DBG & 2)) GS_SCATTER((j) + 1, Ps, Vs);                             \
         GS_STAMP(3u + 2u * (j));                                                                  \
         __syncthreads();                                                                          \
     }

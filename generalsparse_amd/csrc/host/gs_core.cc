@@ -95,6 +95,8 @@ void apply_kv(config_t &c, const std::string &k, const std::string &v) {
     else if (k == "SHARED_MEM_TOTAL_SIZE") c.SHARED_MEM_TOTAL_SIZE = i();
     else if (k == "MAX_DIV_TIMES_OF_DIV") c.MAX_DIV_TIMES_OF_DIV = i();
     else if (k == "MFMA_GLDS") c.MFMA_GLDS = i();
+    else if (k == "MFMA_GLDS_NBUF") c.MFMA_GLDS_NBUF = i();
+    else if (k == "MFMA_COMPUTE_WAVES") c.MFMA_COMPUTE_WAVES = i();
     else if (k == "MFMA_WK") c.MFMA_WK = i();
     else if (k == "MFMA_BITMAP") c.MFMA_BITMAP = i() != 0;
     else if (k == "BM_VARIANT") c.BM_VARIANT = i();

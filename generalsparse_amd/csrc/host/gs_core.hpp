@@ -71,6 +71,8 @@ struct config_t {
     int64_t SHARED_MEM_TOTAL_SIZE = 160 * 1024;  // MI355X LDS per CU
     int64_t MAX_DIV_TIMES_OF_DIV = 12;
     int64_t MFMA_GLDS = 1;  // k_mfma_rows: B rows by global_load_lds (two chunks ahead)
+    int64_t MFMA_COMPUTE_WAVES = 6;  // k_mfma_rows compute waves (6, or 8 with two fewer entry waves)
+    int64_t MFMA_GLDS_NBUF = 3;  // ... into this many B buffers, NBUF-1 chunks ahead (4, 5: 256-column chunks)
     int64_t MFMA_WK = 0;    // row blocks of <= 32 rows on k_mfma_wk (wave-owned k-steps; opt-in, slower on C2)
     std::string FORMAT_OF_MTX = "COO";
     std::string PERFORMANCE_FLAG = "throughput";

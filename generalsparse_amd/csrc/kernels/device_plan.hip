@@ -244,9 +244,10 @@ constexpr uint32_t kMfmaBThreads = 64 * gsk::kMfmaBWaves, kMfmaAThreads = 64 * g
 
 size_t mfma_lds_bytes(uint32_t lgKC, uint32_t CT, uint32_t RMAX) {
     const size_t KC = 1ull << lgKC;
-    // the larger of the two layouts (2 B buffers + 3 dense images; MFMA_GLDS: 3 + 2)
+    // the larger of the two layouts (2 B buffers + 3 dense images; MFMA_GLDS: MFMA_GLDS_NBUF + 2)
+    const size_t nb = (size_t)std::max<int64_t>(3, get_config().MFMA_GLDS_NBUF);
     const size_t szB = KC * 32 * CT, szD = (RMAX + 1) * (2 * KC + 32);
-    return std::max(2 * szB + 3 * szD, 3 * szB + 2 * szD) + 1024;  // + stamp slots and the arrival flag
+    return std::max(2 * szB + 3 * szD, nb * szB + 2 * szD) + 1024;  // + stamp slots and the arrival flag
 }
 
 // Order one segment's entries for the scatter: the kernel's 32-lane half-waves
@@ -1052,9 +1053,24 @@ void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *
                    hipStream_t s) {
     const device_plan &d = p.dev;
     // B rows by LDS-DMA two chunks ahead (MFMA_GLDS) or through registers three ahead
-    const int64_t gl = get_config().MFMA_GLDS;
+    const int64_t gl = get_config().MFMA_GLDS, nbuf = get_config().MFMA_GLDS_NBUF;
     auto kern = gl >= 4 ? gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 4>
                         : (gl ? gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2> : gsk::k_mfma_rows<CT, RT, LGKC, MAXA>);
+    if (gl == 1 && get_config().MFMA_COMPUTE_WAVES == 8) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 8>;
+    // GS_MFMA_DEBUG (diagnostic timing builds, wrong results): kernel_lib.hpp k_mfma_rows DBG bits, C2 shape only
+    static const int mdbg = getenv("GS_MFMA_DEBUG") ? atoi(getenv("GS_MFMA_DEBUG")) : 0;
+    if constexpr (CT == 2 && RT == 2 && LGKC == 9 && MAXA == 1) {
+        if (gl == 1 && mdbg == 1) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 1>;
+        if (gl == 1 && mdbg == 2) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 2>;
+        if (gl == 1 && mdbg == 4) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 4>;
+        if (gl == 1 && mdbg == 10) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 10>;
+        if (gl == 1 && mdbg == 11) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 11>;
+        if (gl == 1 && mdbg == 15) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 15>;
+    }
+    if constexpr (LGKC == 8) {  // deeper B rings fit LDS with 256-column chunks
+        if (gl && !(gl >= 4) && nbuf == 4) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 4>;
+        if (gl && !(gl >= 4) && nbuf >= 5) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 5>;
+    }
     static std::mutex mu;
     static std::map<std::pair<int, const void *>, size_t> granted;
     {
@@ -1077,7 +1093,8 @@ void launch_mfma_rt(const plan_state &p, const device_arrays &a, const gsk::f16 
                     hipStream_t s) {
     // entry groups per thread per chunk: the GLDS variant has 9 entry waves, the other 6
     const int64_t gl = get_config().MFMA_GLDS;
-    const uint32_t nat = 64u * (gl >= 4 ? 6u : (gl ? (uint32_t)gsk::kMfmaAWavesG : (uint32_t)gsk::kMfmaAWaves));
+    const uint32_t wct = get_config().MFMA_COMPUTE_WAVES == 8 && gl == 1 ? 8u : (uint32_t)gsk::kMfmaCompute;
+    const uint32_t nat = 64u * (gsk::kMfmaWaves - wct - (gl >= 4 ? 4u : (gl ? 2u : (uint32_t)gsk::kMfmaBWaves)));
     const bool two = p.dev.seg_cap > nat;
     switch (p.dev.RSB) {                  // log2 KC
         case 10: two ? launch_mfma_k<CT, RT, 10, 2>(p, a, B, C, N, s) : launch_mfma_k<CT, RT, 10, 1>(p, a, B, C, N, s); break;
@@ -1102,7 +1119,7 @@ void launch_mfma_ct(const plan_state &p, const device_arrays &a, const gsk::f16 
 // diagnostic: N = 32 plans with 17..48-row BMTBs and KC 256 or 512
 template <int RT, int LG>
 auto timeline_kernel(bool two) {
-    return two ? gsk::k_mfma_rows<2, RT, LG, 2, true> : gsk::k_mfma_rows<2, RT, LG, 1, true>;  // register-staged B
+    return two ? gsk::k_mfma_rows<2, RT, LG, 2, true, 2> : gsk::k_mfma_rows<2, RT, LG, 1, true, 2>;  // LDS-DMA B (default)
 }
 
 void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
@@ -1112,7 +1129,7 @@ void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N
                  (d.RSB == 8 || d.RSB == 9),
              "timeline build exists for N=32 matrix-core plans with 17..48-row BMTBs, KC 256/512 only");
     const device_arrays &a = d.replicas[0];
-    const bool two = d.seg_cap > kMfmaAThreads;
+    const bool two = d.seg_cap > 64u * gsk::kMfmaAWavesG;
     auto kern = d.maxr == 2 ? (d.RSB == 9 ? timeline_kernel<2, 9>(two) : timeline_kernel<2, 8>(two))
                             : (d.RSB == 9 ? timeline_kernel<3, 9>(two) : timeline_kernel<3, 8>(two));
     const size_t lds = d.lds_bytes;
