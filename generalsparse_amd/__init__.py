@@ -238,6 +238,19 @@ class Plan:
         _lib.check(self._L.gs_plan_index_compression(self._h, key.encode(), kind, 32, expr, 1 << 14, ctypes.byref(ex)))
         return kind.value.decode(), expr.value.decode(), bool(ex.value)
 
+    def logical_check(self):
+        """"" when the metadata set is consistent, else the first violation
+        (logical_check, metadata_set.cc:806-1890)"""
+        buf = ctypes.create_string_buffer(1024)
+        rc = self._L.gs_plan_logical_check(self._h, buf, 1024)
+        _lib.check(min(rc, 0))
+        return buf.value.decode()
+
+    def set_array_entry(self, key, i, value):
+        """metadata editing (tools / tests): entry i of an integer plan array"""
+        _lib.check(self._L.gs_plan_array_set_u64(self._h, key.encode(), int(i), int(value)))
+        return self
+
     def log(self):
         buf = ctypes.create_string_buffer(1 << 16)
         _lib.check(self._L.gs_plan_log(self._h, buf, 1 << 16))

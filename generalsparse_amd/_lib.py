@@ -35,6 +35,8 @@ class GsPlanInfo(ctypes.Structure):
 
 # every symbol include/generalsparse.h declares, with its ctypes signature
 SIGNATURES = {
+    "gs_plan_logical_check": ([ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
+    "gs_plan_array_set_u64": ([ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64], ctypes.c_int),
     "gs_last_error": ([], ctypes.c_char_p),
     "gs_version": ([], ctypes.c_char_p),
     "gs_opts_default": ([ctypes.POINTER(GsOpts)], None),

@@ -387,6 +387,33 @@ int gs_plan_compile(gs_plan_t *p) {
                      "parent's indexing, div_row_indices_by_row_nnz.cc) -- plan only, not executable");
             s->cg->compile();
         }
+        // the reference asserts logical_check after every pipeline (token_test.cc:517-1541)
+        const std::string bad = gs::logical_check(m);
+        GS_CHECK(bad.empty(), "logical_check: " + bad);
+    });
+}
+
+int gs_plan_logical_check(gs_plan_t *p, char *msg, int msg_len) {
+    int rc = 0;
+    const int g = guard([&] {
+        GS_CHECK(p, "null plan");
+        const std::string bad = gs::logical_check(*p->st.meta);
+        if (msg && msg_len > 0) {
+            std::strncpy(msg, bad.c_str(), msg_len - 1);
+            msg[msg_len - 1] = 0;
+        }
+        rc = bad.empty() ? 0 : 1;
+    });
+    return g ? g : rc;
+}
+
+int gs_plan_array_set_u64(gs_plan_t *p, const char *key, uint64_t i, uint64_t value) {
+    return guard([&] {
+        GS_CHECK(p && key, "null argument");
+        auto a = p->st.meta->get_element(key)->meta_data_arr;
+        GS_CHECK(!a->is_float(), "array is a value array");
+        GS_CHECK(i < a->get_len(), "index out of range");
+        a->u_mut()[i] = value;
     });
 }
 

@@ -436,4 +436,8 @@ bool has_row_direction_blocking_in_specific_level(const meta_data_set &m, POS_TY
 std::shared_ptr<basic_operator> make_operator(const std::string &name, const std::vector<long long> &args,
                                               cg_ptr cg, ctx_ptr ctx);
 
+// logical_check.cc: cross-array consistency of the metadata set (metadata_set.cc:806-1890);
+// "" when consistent, else the first violation
+std::string logical_check(const meta_data_set &m);
+
 }  // namespace gs

@@ -140,6 +140,14 @@ int gs_debug_mfma_timeline(gs_plan_t *p, const void *B, void *C, int N, gs_strea
 int gs_plan_save(gs_plan_t *p, const char *path);
 int gs_plan_load(const char *path, gs_plan_t **out);
 
+/* logical_check (metadata_set.cc:806-1890): cross-array consistency of the plan's metadata
+ * (the reference's checks, with its relative-vs-absolute checks made exact); 0 consistent,
+ * 1 a violation (described in msg), < 0 error.  gs_plan_compile runs it and fails on a
+ * violation, as token_test asserts it after every pipeline. */
+int gs_plan_logical_check(gs_plan_t *p, char *msg, int msg_len);
+/* metadata editing (tools and tests): entry i of an integer plan array */
+int gs_plan_array_set_u64(gs_plan_t *p, const char *key, uint64_t i, uint64_t value);
+
 /* one call: read + pipeline + compile + upload */
 int gs_plan_from_mtx(const char *path, const gs_opts *opts, gs_plan_t **out);
 void gs_plan_free(gs_plan_t *p);
