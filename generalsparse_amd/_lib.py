@@ -6,7 +6,8 @@ import ctypes
 import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libgeneralsparse.so")
+# GS_LIBRARY: another build of the same library (e.g. the ASan/UBSan host build, make -C csrc san)
+LIB_PATH = os.environ.get("GS_LIBRARY") or os.path.join(PKG_DIR, "libgeneralsparse.so")
 
 GS_F32 = 0
 GS_F16 = 1
