@@ -31,7 +31,8 @@ class GsPlanInfo(ctypes.Structure):
                 ("kernel_name", ctypes.c_char * 64), ("lds_stage", ctypes.c_int), ("lds_n", ctypes.c_uint32),
                 ("lds_kc", ctypes.c_uint32), ("lds_chunks", ctypes.c_uint32), ("lds_waves", ctypes.c_uint32),
                 ("lds_bytes", ctypes.c_uint64), ("tile_bytes", ctypes.c_uint64), ("ksplit", ctypes.c_uint32),
-                ("n_kernels", ctypes.c_int), ("device_kernel", ctypes.c_char * 32)]
+                ("n_kernels", ctypes.c_int), ("device_kernel", ctypes.c_char * 32),
+                ("index_formulas", ctypes.c_int), ("index_bytes_saved", ctypes.c_uint64)]
 
 
 # every symbol include/generalsparse.h declares, with its ctypes signature

@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "idx_formula.hpp"
+
 namespace gsk {
 
 typedef _Float16 f16;
@@ -105,6 +107,19 @@ __device__ __forceinline__ void atomic_add_vals<f16, 1>(f16 *p, const float (&v)
     unsafeAtomicAdd(reinterpret_cast<__half *>(p), __float2half(v[0]));
 }
 
+// XCD-aware block numbering (cdna_hip_programming.md §5.5 T1): blocks b and b + 8 are
+// observed to share an XCD (round-robin dispatch, MI355X_MICROARCH.md §Workgroup dispatch),
+// so consecutive blockIdx read the neighbouring cache lines of A's streams from eight
+// different L2s.  The bijective renumbering gives each XCD one contiguous range of
+// logical block ids instead; a speed choice only, any placement stays correct.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
+#ifdef GS_NO_XCD_SWIZZLE  // A/B diagnostic builds only
+    return b;
+#endif
+    const uint32_t q = n >> 3, r = n & 7u, x = b & 7u;
+    return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + (b >> 3);
+}
+
 // one sparse entry times a CF-wide B segment
 template <class VT, int CF>
 __device__ __forceinline__ void fma_row(float (&acc)[CF], float v, const VT *__restrict__ brow) {
@@ -124,15 +139,19 @@ __device__ __forceinline__ void fma_row(float (&acc)[CF], float v, const VT *__r
 // b >= n_bmt are the trailing empty rows: their C rows are zero-filled here
 // instead of relying on a memset.
 // ---------------------------------------------------------------------------
-template <class VT, class CT, int CF, int SCF>
-__global__ __launch_bounds__(256) void k_thread_total(const uint32_t *__restrict__ first_nz,  // n_bmt+1
+template <class VT, class CT, int CF, int SCF, bool FX>
+__device__ __forceinline__ void thread_total_body(const uint32_t *__restrict__ first_nz,  // n_bmt+1
+                                                      const idx_formula f_nz,
                                                       const uint32_t *__restrict__ order,     // n_rows: sorted->orig
+                                                      const idx_formula f_order,
                                                       const CT *__restrict__ col, const VT *__restrict__ val,
                                                       const VT *__restrict__ B, VT *__restrict__ C, uint32_t n_bmt,
                                                       uint32_t n_rows, uint32_t N, uint32_t X, uint32_t row_base) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t xl = lane & (X - 1u);
     const uint32_t groups_per_block = blockDim.x / X;
+    // plain block order: the rows are sorted by length, so XCD-contiguous ranges would
+    // give one XCD all the longest rows (measured slower on C1)
     const uint32_t g = blockIdx.x * groups_per_block + threadIdx.x / X;
     const uint32_t stride = gridDim.x * groups_per_block;
     for (uint32_t ct = blockIdx.y; ct * X * CF < N; ct += gridDim.y) {
@@ -144,7 +163,8 @@ __global__ __launch_bounds__(256) void k_thread_total(const uint32_t *__restrict
 #pragma unroll
             for (int k = 0; k < CF; k++) acc[k] = 0.f;
             if (rr < n_bmt) {
-                const uint32_t b = first_nz[rr], e = first_nz[rr + 1];
+                uint32_t b, e;
+                idx_range<FX>(first_nz, f_nz, rr, b, e);
                 typedef typename raw_vec<CF * sizeof(VT)>::t RB;
                 for (uint32_t p = b; p < e; p += SCF) {
                     CT cc[SCF];
@@ -164,9 +184,21 @@ __global__ __launch_bounds__(256) void k_thread_total(const uint32_t *__restrict
                     }
                 }
             }
-            if (cok) store_f32<VT, CF>(C + (size_t)(order[rr] + row_base) * N + c0, acc);
+            if (cok) store_f32<VT, CF>(C + (size_t)(idx_at<FX>(order, f_order, rr) + row_base) * N + c0, acc);
         }
     }
+}
+
+template <class VT, class CT, int CF, int SCF>
+__global__ __launch_bounds__(256) void k_thread_total(const uint32_t *__restrict__ first_nz, const idx_formula f_nz,
+                                                      const uint32_t *__restrict__ order, const idx_formula f_order,
+                                                      const CT *__restrict__ col, const VT *__restrict__ val,
+                                                      const VT *__restrict__ B, VT *__restrict__ C, uint32_t n_bmt,
+                                                      uint32_t n_rows, uint32_t N, uint32_t X, uint32_t row_base) {
+    if (f_nz.kind == IDX_ARRAY && f_order.kind == IDX_ARRAY)
+        thread_total_body<VT, CT, CF, SCF, false>(first_nz, f_nz, order, f_order, col, val, B, C, n_bmt, n_rows, N, X, row_base);
+    else
+        thread_total_body<VT, CT, CF, SCF, true>(first_nz, f_nz, order, f_order, col, val, B, C, n_bmt, n_rows, N, X, row_base);
 }
 
 // ---------------------------------------------------------------------------
@@ -224,9 +256,11 @@ __device__ __forceinline__ void wave_row(const uint32_t b, const uint32_t e, con
     }
 }
 
-template <class VT, class CT, int CF, int SCF>
-__global__ __launch_bounds__(256) void k_warp_rows(const uint32_t *__restrict__ bmw_first_row,  // n_bmw+1
+template <class VT, class CT, int CF, int SCF, bool FX>
+__device__ __forceinline__ void warp_rows_body(const uint32_t *__restrict__ bmw_first_row,  // n_bmw+1
+                                                   const idx_formula f_row,
                                                    const uint32_t *__restrict__ bmw_of_bmtb,    // n_bmtb+1 or null
+                                                   const idx_formula f_bmw,                     // kind ARRAY + null: no BMTB level
                                                    const uint32_t *__restrict__ row_ptr,        // rows+1 (CSR)
                                                    const CT *__restrict__ col, const VT *__restrict__ val,
                                                    const VT *__restrict__ B, VT *__restrict__ C, uint32_t n_bmw,
@@ -237,12 +271,13 @@ __global__ __launch_bounds__(256) void k_warp_rows(const uint32_t *__restrict__ 
     const uint32_t S = 64u / X;
     const uint32_t wib = threadIdx.x >> 6, wpb = blockDim.x >> 6;
     uint32_t w_begin, w_end, w_step;
-    if (bmw_of_bmtb) {
-        w_begin = bmw_of_bmtb[blockIdx.x] + wib;
-        w_end = bmw_of_bmtb[blockIdx.x + 1];
+    if (bmw_of_bmtb || f_bmw.kind != IDX_ARRAY) {
+        const uint32_t t = xcd_block(blockIdx.x, gridDim.x);
+        idx_range<FX>(bmw_of_bmtb, f_bmw, t, w_begin, w_end);
+        w_begin += wib;
         w_step = wpb;
     } else {
-        w_begin = blockIdx.x * wpb + wib;
+        w_begin = xcd_block(blockIdx.x, gridDim.x) * wpb + wib;
         w_end = n_bmw;
         w_step = gridDim.x * wpb;
     }
@@ -251,8 +286,9 @@ __global__ __launch_bounds__(256) void k_warp_rows(const uint32_t *__restrict__ 
         const bool cok = cw < N;
         const uint32_t c0 = cok ? cw : 0u;
         for (uint32_t w = w_begin; w < w_end; w += w_step) {
-            const uint32_t r_end = bmw_first_row[w + 1];
-            for (uint32_t r = bmw_first_row[w]; r < r_end; r++) {
+            uint32_t r_begin, r_end;
+            idx_range<FX>(bmw_first_row, f_row, w, r_begin, r_end);
+            for (uint32_t r = r_begin; r < r_end; r++) {
                 float acc[CF];
 #pragma unroll
                 for (int k = 0; k < CF; k++) acc[k] = 0.f;
@@ -264,6 +300,20 @@ __global__ __launch_bounds__(256) void k_warp_rows(const uint32_t *__restrict__ 
     }
 }
 
+template <class VT, class CT, int CF, int SCF>
+__global__ __launch_bounds__(256) void k_warp_rows(const uint32_t *__restrict__ bmw_first_row, const idx_formula f_row,
+                                                   const uint32_t *__restrict__ bmw_of_bmtb, const idx_formula f_bmw,
+                                                   const uint32_t *__restrict__ row_ptr, const CT *__restrict__ col,
+                                                   const VT *__restrict__ val, const VT *__restrict__ B, VT *__restrict__ C,
+                                                   uint32_t n_bmw, uint32_t N, uint32_t X, uint32_t row_base) {
+    if (f_row.kind == IDX_ARRAY && f_bmw.kind == IDX_ARRAY)
+        warp_rows_body<VT, CT, CF, SCF, false>(bmw_first_row, f_row, bmw_of_bmtb, f_bmw, row_ptr, col, val, B, C, n_bmw, N, X,
+                                               row_base);
+    else
+        warp_rows_body<VT, CT, CF, SCF, true>(bmw_first_row, f_row, bmw_of_bmtb, f_bmw, row_ptr, col, val, B, C, n_bmw, N, X,
+                                              row_base);
+}
+
 // ---------------------------------------------------------------------------
 // K6 tblock_total: one 256-thread workgroup per BMTB (fixed row-direction
 // TBLOCK blocking + tblock_total_reduce_operator).  All four waves split each
@@ -271,13 +321,14 @@ __global__ __launch_bounds__(256) void k_warp_rows(const uint32_t *__restrict__ 
 // (total_block_reduce_to_one_register_token.cc:374-480 reduces over
 // blockDim.y with __syncthreads; here one LDS round of 4 partials).
 // ---------------------------------------------------------------------------
-template <class VT, class CT, int CF, int SCF>
-__global__ __launch_bounds__(256) void k_block_rows(const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
+template <class VT, class CT, int CF, int SCF, bool FX>
+__device__ __forceinline__ void block_rows_body(const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
+                                                    const idx_formula f_row,
                                                     const uint32_t *__restrict__ row_ptr,
                                                     const CT *__restrict__ col, const VT *__restrict__ val,
                                                     const VT *__restrict__ B, VT *__restrict__ C, uint32_t n_bmtb,
-                                                    uint32_t N, uint32_t X, uint32_t row_base) {
-    __shared__ float part[4][64][CF];
+                                                    uint32_t N, uint32_t X, uint32_t row_base,
+                                                    float (*part)[64][CF]) {  // [4][64][CF] in LDS
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wib = threadIdx.x >> 6;
     const uint32_t xl = lane & (X - 1u);
@@ -287,9 +338,10 @@ __global__ __launch_bounds__(256) void k_block_rows(const uint32_t *__restrict__
         const uint32_t cw = ct * X * CF + xl * CF;
         const bool cok = cw < N;
         const uint32_t c0 = cok ? cw : 0u;
-        for (uint32_t t = blockIdx.x; t < n_bmtb; t += gridDim.x) {
-            const uint32_t r_end = bmtb_first_row[t + 1];
-            for (uint32_t r = bmtb_first_row[t]; r < r_end; r++) {
+        for (uint32_t t = xcd_block(blockIdx.x, gridDim.x); t < n_bmtb; t += gridDim.x) {
+            uint32_t r_begin, r_end;
+            idx_range<FX>(bmtb_first_row, f_row, t, r_begin, r_end);
+            for (uint32_t r = r_begin; r < r_end; r++) {
                 float acc[CF];
 #pragma unroll
                 for (int k = 0; k < CF; k++) acc[k] = 0.f;
@@ -311,6 +363,18 @@ __global__ __launch_bounds__(256) void k_block_rows(const uint32_t *__restrict__
     }
 }
 
+template <class VT, class CT, int CF, int SCF>
+__global__ __launch_bounds__(256) void k_block_rows(const uint32_t *__restrict__ bmtb_first_row, const idx_formula f_row,
+                                                    const uint32_t *__restrict__ row_ptr, const CT *__restrict__ col,
+                                                    const VT *__restrict__ val, const VT *__restrict__ B, VT *__restrict__ C,
+                                                    uint32_t n_bmtb, uint32_t N, uint32_t X, uint32_t row_base) {
+    __shared__ float part[4][64][CF];
+    if (f_row.kind == IDX_ARRAY)
+        block_rows_body<VT, CT, CF, SCF, false>(bmtb_first_row, f_row, row_ptr, col, val, B, C, n_bmtb, N, X, row_base, part);
+    else
+        block_rows_body<VT, CT, CF, SCF, true>(bmtb_first_row, f_row, row_ptr, col, val, B, C, n_bmtb, N, X, row_base, part);
+}
+
 // ---------------------------------------------------------------------------
 // K2 + K3 bitmap segments (fixed_interval_nnz_direction_thread_blocking_operator
 // (32) + thread_bit_map_operator (+ warp_segment_reduce_operator)).  Slot s of
@@ -323,20 +387,22 @@ __global__ __launch_bounds__(256) void k_block_rows(const uint32_t *__restrict__
 // combine, warp_segment_reduce_token.cc:26-444) and added with one atomic per
 // row run.  C must be zeroed first.
 // ---------------------------------------------------------------------------
-template <class VT, class CT, int CF, int SCF>
-__global__ __launch_bounds__(256) void k_bitmap_segment(const uint32_t *__restrict__ bmt_first_nz,   // n_bmt+1
+template <class VT, class CT, int CF, int SCF, bool FX>
+__device__ __forceinline__ void bitmap_segment_body(const uint32_t *__restrict__ bmt_first_nz,   // n_bmt+1
+                                                        const idx_formula f_nz,
                                                         const uint32_t *__restrict__ bmt_first_row,  // n_bmt+1
+                                                        const idx_formula f_row,
                                                         const uint64_t *__restrict__ row_start_mask, // n_bmt
                                                         const uint32_t *__restrict__ seg_ptr,        // n_bmt
                                                         const uint32_t *__restrict__ seg_row_off,    // segments
                                                         const CT *__restrict__ col, const VT *__restrict__ val,
                                                         const VT *__restrict__ B, VT *__restrict__ C, uint32_t n_bmt,
                                                         uint32_t N, uint32_t X, uint32_t row_base,
-                                                        float *__restrict__ ws) {
+                                                        float *__restrict__ ws,
+                                                        uint32_t (*open_row)[64][2]) {  // [4][64][2] in LDS
     // ws != nullptr (fp16 C): rows shared between BMTs accumulate in an fp32
     // workspace (k_finalize_rows rounds them to C once); else atomics go to C.
     // per wave: up to 2 open partials per slot (head, tail), S <= 64
-    __shared__ uint32_t open_row[4][64][2];
     extern __shared__ float dyn[];  // [4 waves][S slots][2][X lanes][CF]
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wib = threadIdx.x >> 6;
@@ -349,17 +415,18 @@ __global__ __launch_bounds__(256) void k_bitmap_segment(const uint32_t *__restri
         const uint32_t cw = ct * X * CF + xl * CF;
         const bool cok = cw < N;
         const uint32_t c0 = cok ? cw : 0u;
-        for (uint32_t w = blockIdx.x * (blockDim.x >> 6) + wib; w * S < n_bmt; w += waves_total) {
+        for (uint32_t w = xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + wib; w * S < n_bmt; w += waves_total) {
             const uint32_t bt = w * S + slot;
             uint32_t head_row = 0xffffffffu, tail_row = 0xffffffffu;
             float head_acc[CF], acc[CF];
 #pragma unroll
             for (int k = 0; k < CF; k++) { acc[k] = 0.f; head_acc[k] = 0.f; }
             if (bt < n_bmt) {
-                const uint32_t b = bmt_first_nz[bt], e = bmt_first_nz[bt + 1];
+                uint32_t b, e;
+                idx_range<FX>(bmt_first_nz, f_nz, bt, b, e);
                 const uint64_t mask = row_start_mask[bt];
                 const bool next_continues = (bt + 1 < n_bmt) && !(row_start_mask[bt + 1] & 1ull);
-                const uint32_t r0 = bmt_first_row[bt];
+                const uint32_t r0 = idx_at<FX>(bmt_first_row, f_row, bt);
                 const uint32_t sbase = seg_ptr[bt];
                 uint32_t seg = 0, cur_row = r0;
                 bool cur_open_head = !(mask & 1ull);
@@ -455,6 +522,24 @@ __global__ __launch_bounds__(256) void k_bitmap_segment(const uint32_t *__restri
     }
 }
 
+template <class VT, class CT, int CF, int SCF>
+__global__ __launch_bounds__(256) void k_bitmap_segment(const uint32_t *__restrict__ bmt_first_nz, const idx_formula f_nz,
+                                                        const uint32_t *__restrict__ bmt_first_row, const idx_formula f_row,
+                                                        const uint64_t *__restrict__ row_start_mask,
+                                                        const uint32_t *__restrict__ seg_ptr,
+                                                        const uint32_t *__restrict__ seg_row_off, const CT *__restrict__ col,
+                                                        const VT *__restrict__ val, const VT *__restrict__ B,
+                                                        VT *__restrict__ C, uint32_t n_bmt, uint32_t N, uint32_t X,
+                                                        uint32_t row_base, float *__restrict__ ws) {
+    __shared__ uint32_t open_row[4][64][2];
+    if (f_nz.kind == IDX_ARRAY && f_row.kind == IDX_ARRAY)
+        bitmap_segment_body<VT, CT, CF, SCF, false>(bmt_first_nz, f_nz, bmt_first_row, f_row, row_start_mask, seg_ptr,
+                                                    seg_row_off, col, val, B, C, n_bmt, N, X, row_base, ws, open_row);
+    else
+        bitmap_segment_body<VT, CT, CF, SCF, true>(bmt_first_nz, f_nz, bmt_first_row, f_row, row_start_mask, seg_ptr,
+                                                   seg_row_off, col, val, B, C, n_bmt, N, X, row_base, ws, open_row);
+}
+
 // ---------------------------------------------------------------------------
 // K5 / K7 on col-direction plans (fixed_interval_col_direction_thread_blocking_
 // operator + thread_total_reduce + warp_bit_map_operator / tblock_thread_bit_map_
@@ -468,9 +553,11 @@ __global__ __launch_bounds__(256) void k_bitmap_segment(const uint32_t *__restri
 // into `ws` when a neighbouring wave shares it (k_finalize_rows then rounds
 // those rows and writes the empty ones).
 // ---------------------------------------------------------------------------
-template <class VT, class CT, int CF, int SCF>
-__global__ __launch_bounds__(256) void k_row_chunks(const uint32_t *__restrict__ bmt_nz,   // n_bmt+1
+template <class VT, class CT, int CF, int SCF, bool FX>
+__device__ __forceinline__ void row_chunks_body(const uint32_t *__restrict__ bmt_nz,   // n_bmt+1
+                                                    const idx_formula f_nz,
                                                     const uint32_t *__restrict__ bmt_row,  // n_bmt
+                                                    const idx_formula f_row,
                                                     const CT *__restrict__ col, const VT *__restrict__ val,
                                                     const VT *__restrict__ B, VT *__restrict__ C,
                                                     float *__restrict__ ws, uint32_t n_bmt, uint32_t U, uint32_t N,
@@ -487,12 +574,12 @@ __global__ __launch_bounds__(256) void k_row_chunks(const uint32_t *__restrict__
         const uint32_t cw = ct * X * CF + xl * CF;
         const bool cok = cw < N;
         const uint32_t c0 = cok ? cw : 0u;
-        for (uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); (size_t)w * U < n_bmt;
+        for (uint32_t w = xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6); (size_t)w * U < n_bmt;
              w += waves_total) {
             const uint32_t r0 = w * U, r1 = min(r0 + U, n_bmt);
-            const uint32_t first_row = bmt_row[r0], last_row = bmt_row[r1 - 1];
-            const bool head_shared = r0 > 0 && bmt_row[r0 - 1] == first_row;
-            const bool tail_shared = r1 < n_bmt && bmt_row[r1] == last_row;
+            const uint32_t first_row = idx_at<FX>(bmt_row, f_row, r0), last_row = idx_at<FX>(bmt_row, f_row, r1 - 1);
+            const bool head_shared = r0 > 0 && idx_at<FX>(bmt_row, f_row, r0 - 1) == first_row;
+            const bool tail_shared = r1 < n_bmt && idx_at<FX>(bmt_row, f_row, r1) == last_row;
             float carry[CF];
 #pragma unroll
             for (int k = 0; k < CF; k++) carry[k] = 0.f;
@@ -500,7 +587,7 @@ __global__ __launch_bounds__(256) void k_row_chunks(const uint32_t *__restrict__
             for (uint32_t g = r0; g < r1; g += S) {
                 const uint32_t bt = g + slot;
                 const bool valid = bt < r1;
-                const uint32_t row = valid ? bmt_row[bt] : 0xfffffffeu;
+                const uint32_t row = valid ? idx_at<FX>(bmt_row, f_row, bt) : 0xfffffffeu;
                 float acc[CF];
 #pragma unroll
                 for (int k = 0; k < CF; k++) acc[k] = 0.f;
@@ -512,7 +599,9 @@ __global__ __launch_bounds__(256) void k_row_chunks(const uint32_t *__restrict__
                             fma_row<VT, CF>(acc, (float)val[p], B + (size_t)col[p] * N + c0);
                         }
                     } else {
-                        wave_row<VT, CT, CF, SCF>(bmt_nz[bt], bmt_nz[bt + 1], col, val, B, N, c0, 0u, 1u, acc);
+                        uint32_t b, e;
+                        idx_range<FX>(bmt_nz, f_nz, bt, b, e);
+                        wave_row<VT, CT, CF, SCF>(b, e, col, val, B, N, c0, 0u, 1u, acc);
                     }
                 }
                 // segmented suffix sums: the first slot of each run ends with the run total
@@ -534,7 +623,7 @@ __global__ __launch_bounds__(256) void k_row_chunks(const uint32_t *__restrict__
                 }
                 const uint32_t nv = min(S, r1 - g);
                 const uint32_t lr = __shfl(row, (nv - 1) * X, 64);
-                const bool cont = g + S < r1 && bmt_row[g + S] == lr;
+                const bool cont = g + S < r1 && idx_at<FX>(bmt_row, f_row, g + S) == lr;
                 const unsigned long long hm = __ballot(is_head && row == lr);
                 const uint32_t hs = (uint32_t)__builtin_ctzll(hm) / X;
 #pragma unroll
@@ -550,6 +639,19 @@ __global__ __launch_bounds__(256) void k_row_chunks(const uint32_t *__restrict__
             }
         }
     }
+}
+
+template <class VT, class CT, int CF, int SCF>
+__global__ __launch_bounds__(256) void k_row_chunks(const uint32_t *__restrict__ bmt_nz, const idx_formula f_nz,
+                                                    const uint32_t *__restrict__ bmt_row, const idx_formula f_row,
+                                                    const CT *__restrict__ col, const VT *__restrict__ val,
+                                                    const VT *__restrict__ B, VT *__restrict__ C,
+                                                    float *__restrict__ ws, uint32_t n_bmt, uint32_t U, uint32_t N,
+                                                    uint32_t X, uint32_t row_base, uint32_t ilv = 0) {
+    if (f_nz.kind == IDX_ARRAY && f_row.kind == IDX_ARRAY)
+        row_chunks_body<VT, CT, CF, SCF, false>(bmt_nz, f_nz, bmt_row, f_row, col, val, B, C, ws, n_bmt, U, N, X, row_base, ilv);
+    else
+        row_chunks_body<VT, CT, CF, SCF, true>(bmt_nz, f_nz, bmt_row, f_row, col, val, B, C, ws, n_bmt, U, N, X, row_base, ilv);
 }
 
 // ---------------------------------------------------------------------------
@@ -1865,13 +1967,14 @@ __global__ __launch_bounds__(256) void k_merge_path(const uint32_t *__restrict__
                                                     uint32_t row_hi, const uint32_t *__restrict__ empty_rows,
                                                     uint32_t n_empty, uint32_t fill_blocks, uint32_t dbg = 0) {
     // dbg (diagnostic timing runs only, wrong results): bit 1 gathers B row 0 for every nonzero
-    if (blockIdx.x < fill_blocks) {
+    const uint32_t lb = blockIdx.x;  // (XCD-contiguous numbering measured no faster cold on C4)
+    if (lb < fill_blocks) {
         // the first fill_blocks workgroups zero the empty rows (listed; 16-B stores when a
         // C row is whole 16-B units) while the path waves run
         const uint32_t rbytes = N * (uint32_t)sizeof(VT);
         const uint32_t U = rbytes % 16u == 0 ? rbytes / 16u : N;
         const uint32_t tot = blockIdx.y == 0 ? n_empty * U : 0u;  // one column-tile row of blocks fills
-        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += fill_blocks * blockDim.x) {
+        for (uint32_t i = lb * blockDim.x + threadIdx.x; i < tot; i += fill_blocks * blockDim.x) {
             const uint32_t er = empty_rows[i / U];
             if (rbytes % 16u == 0)
                 *reinterpret_cast<uint4 *>(reinterpret_cast<unsigned char *>(C) + (size_t)er * rbytes + (i % U) * 16u) =
@@ -1896,7 +1999,7 @@ __global__ __launch_bounds__(256) void k_merge_path(const uint32_t *__restrict__
         const uint32_t cw = ct * X * CF + xl * CF;
         const bool cok = cw < N;
         const uint32_t c0 = cok ? cw : 0u;
-        for (uint32_t w = (blockIdx.x - fill_blocks) * (blockDim.x >> 6) + wib; w < n_waves; w += waves_total) {
+        for (uint32_t w = (lb - fill_blocks) * (blockDim.x >> 6) + wib; w < n_waves; w += waves_total) {
             const uint32_t zlo = wz[w], wend = wz[w + 1], q0 = wq[w];
             // the wave starts inside row q0 (its partial goes to head_rec)
             const bool head_open = zlo > (q0 ? ends[q0 - 1] : 0u);

@@ -523,6 +523,8 @@ int gs_plan_info_get(gs_plan_t *p, gs_plan_info *info) {
             info->ksplit = s.dev.ksplit;
             const std::string dk = !s.dev.kernel.empty() ? s.dev.kernel : s.cg->get_kernel_spec().name();
             std::strncpy(info->device_kernel, dk.c_str(), sizeof(info->device_kernel) - 1);
+            info->index_formulas = s.dev.index_formulas;
+            info->index_bytes_saved = s.dev.index_bytes_saved;
         }
     });
 }

@@ -232,55 +232,81 @@ std::string code_generator::generate_kernel_file_source(int repeat) const {
       << "    std::vector<VT> vv(vals.size()); for (size_t i = 0; i < vals.size(); i++) vv[i] = (VT)vals[i];\n"
       << "    uint32_t *d_col = up(c32); VT *d_val = up(vv);\n"
       << "    uint64_t row_num = rows.back() + 1;\n";
-    const bool vec_ok = true;
-    (void)vec_ok;
+    // the index arrays the gather kernels read through gsk::idx_at: an exact formula is a
+    // kernel argument and the array is not uploaded (the reference prints the expression
+    // into the kernel instead, code_generator.cc:2618-3063)
+    auto fml = [&](const std::string &key) {
+        gsk::idx_formula f;
+        if (!get_config().MODEL_DRIVEN_COMPRESS || !meta->is_exist(key)) return f;
+        auto arr = meta->get_element(key)->meta_data_arr;
+        index_compression c = analyze_index_compression(arr->u(), arr->get_compress_data_type(),
+                                                        get_config().BRANCH_COMPRESS_MAX_SIZE);
+        if (c.kind == "residual" || !device_formula_of(c, f)) f = gsk::idx_formula();
+        return f;
+    };
+    auto decl = [&](const char *name, const gsk::idx_formula &f) {
+        o << "    const gsk::idx_formula " << name << " = " << code_of_device_formula(f) << ";\n";
+    };
+    gsk::idx_formula identity;
+    identity.kind = gsk::IDX_LINEAR;
+    identity.coef = 1;
     const char *cf = half ? "8" : "4";
     std::string launch;
     switch (spec.family) {
         case KF_THREAD_TOTAL:
+            decl("F0", fml("THREAD_META_first_nz_indices_0"));
+            decl("F1", spec.row_sorted ? fml("GLOBAL_META_original_nz_row_indices_0")
+                                       : (get_config().MODEL_DRIVEN_COMPRESS ? identity : gsk::idx_formula()));
             o << "    auto fn = rd(\"THREAD_META_first_nz_indices_0\");\n";
             if (spec.row_sorted) o << "    auto order = rd(\"GLOBAL_META_original_nz_row_indices_0\");\n";
             else o << "    std::vector<uint64_t> order(M); for (uint64_t i = 0; i < M; i++) order[i] = i;\n";
-            o << "    uint32_t *d_a0 = up(u32(fn)), *d_a1 = up(u32(order));\n"
+            o << "    uint32_t *d_a0 = F0.kind ? nullptr : up(u32(fn)), *d_a1 = F1.kind ? nullptr : up(u32(order));\n"
               << "    const uint32_t n_units = fn.size() - 1, n_aux = order.size();\n"
               << "    bool al = true; for (auto x : fn) al &= x % 4 == 0;\n";
             launch = "gsk::k_thread_total<VT, uint32_t, CF, SCF><<<dim3((n_aux + 256 / X - 1) / (256 / X), tiles), 256>>>("
-                     "d_a0, d_a1, d_col, d_val, d_B, d_C, n_units, n_aux, N, X, 0)";
+                     "d_a0, F0, d_a1, F1, d_col, d_val, d_B, d_C, n_units, n_aux, N, X, 0)";
             break;
         case KF_WARP_TOTAL:
+            decl("F0", fml(convert_pos_type_to_string(spec.group_level) + "_first_row_indices_0"));
+            decl("F1", spec.tblock_parent ? fml("TBLOCK_META_first_BMW_indices_0") : gsk::idx_formula());
             o << "    auto wr = rd(\"" << convert_pos_type_to_string(spec.group_level) << "_first_row_indices_0\");\n"
-              << "    uint32_t *d_a0 = up(u32(wr)), *d_a1 = nullptr;\n"
+              << "    uint32_t *d_a0 = F0.kind ? nullptr : up(u32(wr)), *d_a1 = nullptr;\n"
               << "    uint32_t *d_a2 = up(gsk_host::csr_row_ptr(rows, wr.back()));\n"
               << "    const uint32_t n_units = wr.size() - 1; uint32_t gx = (n_units + 3) / 4; const bool al = true;\n";
             if (spec.tblock_parent)
-                o << "    auto tbw = rd(\"TBLOCK_META_first_BMW_indices_0\"); d_a1 = up(u32(tbw)); gx = tbw.size() - 1;\n";
-            launch = "gsk::k_warp_rows<VT, uint32_t, CF, SCF><<<dim3(gx, tiles), 256>>>(d_a0, d_a1, d_a2, d_col, d_val, d_B, d_C, n_units, N, X, 0)";
+                o << "    auto tbw = rd(\"TBLOCK_META_first_BMW_indices_0\"); d_a1 = F1.kind ? nullptr : up(u32(tbw)); gx = tbw.size() - 1;\n";
+            launch = "gsk::k_warp_rows<VT, uint32_t, CF, SCF><<<dim3(gx, tiles), 256>>>(d_a0, F0, d_a1, F1, d_a2, d_col, d_val, d_B, d_C, n_units, N, X, 0)";
             break;
         case KF_BLOCK_TOTAL:
+            decl("F0", fml("TBLOCK_META_first_row_indices_0"));
             o << "    auto tr = rd(\"TBLOCK_META_first_row_indices_0\");\n"
-              << "    uint32_t *d_a0 = up(u32(tr)); uint32_t *d_a2 = up(gsk_host::csr_row_ptr(rows, tr.back()));\n"
+              << "    uint32_t *d_a0 = F0.kind ? nullptr : up(u32(tr)); uint32_t *d_a2 = up(gsk_host::csr_row_ptr(rows, tr.back()));\n"
               << "    const uint32_t n_units = tr.size() - 1; const bool al = true;\n";
-            launch = "gsk::k_block_rows<VT, uint32_t, CF, SCF><<<dim3(n_units, tiles), 256>>>(d_a0, d_a2, d_col, d_val, d_B, d_C, n_units, N, X, 0)";
+            launch = "gsk::k_block_rows<VT, uint32_t, CF, SCF><<<dim3(n_units, tiles), 256>>>(d_a0, F0, d_a2, d_col, d_val, d_B, d_C, n_units, N, X, 0)";
             break;
         case KF_BITMAP_SEGMENT:
+            decl("F0", fml("THREAD_META_first_nz_indices_0"));
+            decl("F1", fml("THREAD_META_first_row_indices_0"));
             o << "    auto fn = rd(\"THREAD_META_first_nz_indices_0\"), fr = rd(\"THREAD_META_first_row_indices_0\");\n"
               << "    auto sp = rd(\"THREAD_META_segment_ptr_0\"), so = rd(\"THREAD_META_segment_empty_row_indices_0\");\n"
-              << "    uint32_t *d_a0 = up(u32(fn)), *d_a1 = up(u32(fr)), *d_a2 = up(u32(sp)), *d_a3 = up(u32(so));\n"
+              << "    uint32_t *d_a0 = F0.kind ? nullptr : up(u32(fn)), *d_a1 = F1.kind ? nullptr : up(u32(fr)), *d_a2 = up(u32(sp)), *d_a3 = up(u32(so));\n"
               << "    uint64_t *d_m0 = up(gsk_host::row_start_masks(rows, fn));\n"
               << "    const uint32_t n_units = fn.size() - 1; const bool al = true;\n";
             launch = "hipMemsetAsync(d_C, 0, M * N * sizeof(VT), 0); "
                      "gsk::k_bitmap_segment<VT, uint32_t, CF, SCF><<<dim3((n_units + 4 * (64 / X) - 1) / (4 * (64 / X)), tiles), 256, "
-                     "4 * (64 / X) * 2 * X * CF * sizeof(float)>>>(d_a0, d_a1, d_m0, d_a2, d_a3, d_col, d_val, d_B, d_C, n_units, N, X, 0, "
+                     "4 * (64 / X) * 2 * X * CF * sizeof(float)>>>(d_a0, F0, d_a1, F1, d_m0, d_a2, d_a3, d_col, d_val, d_B, d_C, n_units, N, X, 0, "
                      "(float *)nullptr)";  // no workspace: open rows by atomics into the zeroed C
             break;
         case KF_ROW_CHUNKS:
+            decl("F0", fml("THREAD_META_first_nz_indices_0"));
+            decl("F1", fml("THREAD_META_first_row_indices_without_ending_0"));
             o << "    auto fn = rd(\"THREAD_META_first_nz_indices_0\"), fr = rd(\"THREAD_META_first_row_indices_without_ending_0\");\n"
-              << "    uint32_t *d_a0 = up(u32(fn)), *d_a1 = up(u32(fr));\n"
+              << "    uint32_t *d_a0 = F0.kind ? nullptr : up(u32(fn)), *d_a1 = F1.kind ? nullptr : up(u32(fr));\n"
               << "    const uint32_t n_units = fn.size() - 1, U = gsk_host::row_chunk_span(n_units); const bool al = true;\n"
               << "    auto fin = gsk_host::row_chunk_finalize_rows(u32(fr), M, U, 0); uint32_t *d_a4 = up(fin);\n"
               << "    float *d_ws; hipMalloc(&d_ws, M * N * sizeof(float)); hipMemset(d_ws, 0, M * N * sizeof(float));\n";
             launch = "gsk::k_row_chunks<VT, uint32_t, CF, SCF><<<dim3(((n_units + U - 1) / U + 3) / 4, tiles), 256>>>("
-                     "d_a0, d_a1, d_col, d_val, d_B, d_C, d_ws, n_units, U, N, X, 0); "
+                     "d_a0, F0, d_a1, F1, d_col, d_val, d_B, d_C, d_ws, n_units, U, N, X, 0); "
                      "if (!fin.empty()) gsk::k_finalize_rows<VT><<<dim3((fin.size() * N + 255) / 256), 256>>>("
                      "d_a4, (uint32_t)fin.size(), d_ws, d_C, N)";
             break;
@@ -351,19 +377,20 @@ uint64_t code_generator::generate_final_program(int repeat, const std::string &r
         std::ofstream f(dir + "/kernel_file.hip");
         f << generate_kernel_file_source(repeat);
     }
-    // copy the device header next to the program (code_generator.cc:686-694)
-    // the header ships next to the library: <pkg>/csrc/hip_code/kernel_lib.hpp
-    std::string lib;
+    // copy the device headers next to the program (code_generator.cc:686-694); they ship
+    // next to the library: <pkg>/csrc/hip_code/{kernel_lib,idx_formula}.hpp
+    std::string hdr_dir;
     Dl_info info;
     if (dladdr((void *)&kernel_family_name, &info) && info.dli_fname) {
         std::string so = info.dli_fname;
-        lib = so.substr(0, so.find_last_of('/') + 1) + "csrc/hip_code/kernel_lib.hpp";
+        hdr_dir = so.substr(0, so.find_last_of('/') + 1) + "csrc/hip_code/";
     }
-    if (!lib.empty()) {
-        std::ifstream in(lib, std::ios::binary);
-        std::ofstream out(dir + "/kernel_lib.hpp", std::ios::binary);
-        out << in.rdbuf();
-    }
+    if (!hdr_dir.empty())
+        for (const char *h : {"kernel_lib.hpp", "idx_formula.hpp"}) {
+            std::ifstream in(hdr_dir + h, std::ios::binary);
+            std::ofstream out(dir + "/" + h, std::ios::binary);
+            out << in.rdbuf();
+        }
     {
         std::ofstream f(dir + "/make_kernel.sh");
         f << "hipcc --offload-arch=gfx950 -O3 -std=c++17 kernel_file.hip -o a.out\n";

@@ -2,6 +2,7 @@
 #pragma once
 
 #include "operator.hpp"
+#include "../hip_code/idx_formula.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -50,6 +51,11 @@ struct device_plan {
     uint32_t ilv = 0;              // k_row_chunks: BMT size of an interleaved layout (0: contiguous)
     uint32_t lds_N = 0, KC = 0, nc = 0, RSB = 0, rpw_max = 0, seg_cap = 0, waves = 0, maxr = 0;
     size_t lds_bytes = 0, bytes_tile = 0;
+    // model-driven index compression on the device (MODEL_DRIVEN_COMPRESS):
+    // the formulas the gather families evaluate for a0 / a1 (kind IDX_ARRAY: read the array)
+    gsk::idx_formula f0, f1;
+    int index_formulas = 0;         // arrays replaced by a formula (or narrowed to residuals)
+    uint64_t index_bytes_saved = 0;  // u32 index bytes per replica not uploaded because of them
     std::vector<device_arrays> replicas;
     std::vector<void *> allocations;  // everything to hipFree
 };

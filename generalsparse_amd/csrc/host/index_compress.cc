@@ -1,6 +1,8 @@
 // index_compress.cc -- see index_compress.hpp (code_generator.cc:2618-3063).
 #include "index_compress.hpp"
 
+#include <algorithm>
+
 namespace gs {
 
 namespace {
@@ -185,6 +187,52 @@ std::string code_of_index_compression(const index_compression &c, const std::str
     if (c.kind == "residual")  // :3045-3060
         return std::to_string(c.aa) + " * (" + idx + ") + (" + std::to_string(c.bb) + ") + " + res_name + "[" + idx + "]";
     return "";
+}
+
+bool device_formula_of(const index_compression &c, gsk::idx_formula &f) {
+    f = gsk::idx_formula();
+    if (!c.exact) return false;
+    auto fits = [](uint64_t x) { return x <= 0xffffffffull; };
+    if (c.kind == "linear" || c.kind == "cycle_linear" || c.kind == "cycle_increase") {
+        if (!fits(c.coef) || !fits(c.intercept) || !fits(c.cycle)) return false;
+        f.kind = c.kind == "linear" ? gsk::IDX_LINEAR : (c.kind == "cycle_linear" ? gsk::IDX_CYCLE_LINEAR : gsk::IDX_CYCLE_INCREASE);
+        f.coef = (uint32_t)c.coef;
+        f.intercept = (uint32_t)c.intercept;
+        f.cycle = c.kind == "linear" ? 1u : (uint32_t)c.cycle;
+        return true;
+    }
+    if (c.kind == "branch") {
+        if (c.lo.size() > (size_t)gsk::kIdxBranchMax) return false;
+        for (size_t b = 0; b < c.lo.size(); b++)
+            if (!fits(c.lo[b]) || !fits(c.val[b])) return false;
+        f.kind = gsk::IDX_BRANCH;
+        f.n_runs = (uint32_t)c.lo.size();
+        for (size_t b = 0; b < c.lo.size(); b++) {
+            f.lo[b] = (uint32_t)c.lo[b];
+            f.val[b] = (uint32_t)c.val[b];
+        }
+        return true;
+    }
+    if (c.kind == "residual") {
+        uint64_t mx = 0;
+        for (uint64_t r : c.res) mx = std::max(mx, r);
+        if (mx > 0xffff) return false;
+        f.kind = mx <= 0xff ? gsk::IDX_RESIDUAL_U8 : gsk::IDX_RESIDUAL_U16;
+        f.coef = (uint32_t)(uint64_t)c.aa;  // mod 2^32: the decoded values are < 2^32
+        f.intercept = (uint32_t)(uint64_t)c.bb;
+        return true;
+    }
+    return false;
+}
+
+std::string code_of_device_formula(const gsk::idx_formula &f) {
+    auto u = [](uint32_t x) { return std::to_string(x) + "u"; };
+    std::string r = "gsk::idx_formula{" + u(f.kind) + ", " + u(f.coef) + ", " + u(f.intercept) + ", " + u(f.cycle) + ", " +
+                    u(f.n_runs) + ", {";
+    for (int b = 0; b < gsk::kIdxBranchMax; b++) r += (b ? ", " : "") + u(f.lo[b]);
+    r += "}, {";
+    for (int b = 0; b < gsk::kIdxBranchMax; b++) r += (b ? ", " : "") + u(f.val[b]);
+    return r + "}}";
 }
 
 }  // namespace gs

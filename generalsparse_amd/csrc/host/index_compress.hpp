@@ -16,6 +16,7 @@
 #pragma once
 
 #include "gs_core.hpp"
+#include "../hip_code/idx_formula.hpp"
 
 namespace gs {
 
@@ -36,5 +37,11 @@ index_compression analyze_index_compression(meta_data_set &m, POS_TYPE pos, cons
 uint64_t decode_index_compression(const index_compression &c, uint64_t i);
 // the expression the generated kernel evaluates (get_*_compress, :2826-3063)
 std::string code_of_index_compression(const index_compression &c, const std::string &idx, const std::string &res_name);
+// the kernel-argument form of an exact compression (hip_code/idx_formula.hpp): false when
+// the device kernels cannot evaluate it (not exact, values or constants beyond 32 bits,
+// more than kIdxBranchMax runs, residuals wider than u16)
+bool device_formula_of(const index_compression &c, gsk::idx_formula &f);
+// its C++ initializer, for emitted programs
+std::string code_of_device_formula(const gsk::idx_formula &f);
 
 }  // namespace gs

@@ -2,6 +2,7 @@
 // kernel family and dispatches the gfx950 kernels of hip_code/kernel_lib.hpp.
 #include "../hip_code/kernel_lib.hpp"
 #include "../host/gs_plan.hpp"
+#include "../host/index_compress.hpp"
 
 #include <algorithm>
 #include <cstdlib>
@@ -40,6 +41,39 @@ std::vector<uint32_t> to_u32(const std::vector<uint64_t> &v, const char *what) {
         o[i] = (uint32_t)v[i];
     }
     return o;
+}
+
+// An index array a gather kernel reads through gsk::idx_at.  With MODEL_DRIVEN_COMPRESS and
+// an exact formula for it (index_compress.cc; the reference prints the same formulas into its
+// kernels, code_generator.cc:2618-3063) nothing is uploaded (linear / branch / cycle kinds) or
+// only the narrow residuals are; otherwise the u32 array.  type_ori: the array's compressed
+// data type, which bounds the residual width as in the reference's if_residual.
+uint32_t *upload_index(device_plan &d, const std::vector<uint64_t> &v, data_type type_ori, const char *what,
+                       gsk::idx_formula &f) {
+    f = gsk::idx_formula();
+    if (get_config().MODEL_DRIVEN_COMPRESS) {
+        const index_compression c = analyze_index_compression(v, type_ori, get_config().BRANCH_COMPRESS_MAX_SIZE);
+        if (device_formula_of(c, f)) {
+            d.index_formulas++;
+            if (f.kind == gsk::IDX_RESIDUAL_U8) {
+                d.index_bytes_saved += v.size() * 3;
+                return (uint32_t *)dev_copy(d, std::vector<uint8_t>(c.res.begin(), c.res.end()), 4);
+            }
+            if (f.kind == gsk::IDX_RESIDUAL_U16) {
+                d.index_bytes_saved += v.size() * 2;
+                return (uint32_t *)dev_copy(d, std::vector<uint16_t>(c.res.begin(), c.res.end()), 2);
+            }
+            d.index_bytes_saved += v.size() * 4;
+            return nullptr;
+        }
+    }
+    return dev_copy(d, to_u32(v, what));
+}
+
+uint32_t *upload_index(device_plan &d, const meta_data_set &m, POS_TYPE pos, const char *name, int sb,
+                       gsk::idx_formula &f) {
+    return upload_index(d, m.u(pos, name, sb), m.get_element(pos, name, sb)->meta_data_arr->get_compress_data_type(), name,
+                        f);
 }
 
 // CSR row pointer of the (possibly padded, row-sorted) COO
@@ -765,30 +799,42 @@ void upload_plan(plan_state &p, int dtype, int device) {
             bool al4 = true, al8 = true;
             for (uint64_t x : fn) { al4 &= (x % 4 == 0); al8 &= (x % 8 == 0); }
             d.scf = al8 ? 8 : (al4 ? 4 : 1);
-            a.a0 = dev_copy(d, to_u32(fn, "first_nz_indices"));
-            std::vector<uint64_t> order;
+            a.a0 = upload_index(d, m, THREAD_META, "first_nz_indices", sb, d.f0);
             if (m.is_exist(GLOBAL_META, "original_nz_row_indices", sb)) {
-                order = m.u(GLOBAL_META, "original_nz_row_indices", sb);
+                a.a1 = upload_index(d, m, GLOBAL_META, "original_nz_row_indices", sb, d.f1);
+                d.n_rows_aux = m.u(GLOBAL_META, "original_nz_row_indices", sb).size();
             } else {
-                order.resize(row_num);
-                for (uint64_t i = 0; i < row_num; i++) order[i] = i;
+                // rows were not sorted: the row of BMT i is i (the reference indexes C by it
+                // directly); an identity array unless the formulas are on
+                std::vector<uint64_t> order(row_num);
+                for (uint64_t r = 0; r < row_num; r++) order[r] = r;
+                a.a1 = upload_index(d, order, UNSIGNED_INT, "row order", d.f1);
+                d.n_rows_aux = row_num;
             }
-            a.a1 = dev_copy(d, to_u32(order, "original_nz_row_indices"));
             d.n_units = fn.size() - 1;
-            d.n_rows_aux = order.size();
             break;
         }
         case KF_WARP_TOTAL: {
-            a.a0 = dev_copy(d, to_u32(m.u(sp.group_level, "first_row_indices", sb), "BMW first_row_indices"));
-            if (sp.tblock_parent) {
-                a.a1 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_BMW_indices", sb), "first_BMW_indices"));
-                d.n_rows_aux = m.u(TBLOCK_META, "first_BMW_indices", sb).size() - 1;  // BMTB count
-            }
+            // BMW rows and BMTB->BMW map: formulas for k_warp_rows; k_lds_rows reads the arrays
+            auto upload_groups = [&](bool formulas) {
+                if (formulas) {
+                    a.a0 = upload_index(d, m, sp.group_level, "first_row_indices", sb, d.f0);
+                    if (sp.tblock_parent) a.a1 = upload_index(d, m, TBLOCK_META, "first_BMW_indices", sb, d.f1);
+                } else {
+                    a.a0 = dev_copy(d, to_u32(m.u(sp.group_level, "first_row_indices", sb), "BMW first_row_indices"));
+                    if (sp.tblock_parent)
+                        a.a1 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_BMW_indices", sb), "first_BMW_indices"));
+                }
+            };
+            if (sp.tblock_parent) d.n_rows_aux = m.u(TBLOCK_META, "first_BMW_indices", sb).size() - 1;  // BMTB count
             std::vector<uint32_t> rp = csr_row_ptr(rows, row_num);
             a.a2 = dev_copy(d, rp);
             d.n_units = m.u(sp.group_level, "first_row_indices", sb).size() - 1;
             d.scf = 4;
-            if (sp.tblock_parent && try_mfma(rp)) break;
+            if (sp.tblock_parent && try_mfma(rp)) {
+                upload_groups(true);  // the gather fallback at other dense widths
+                break;
+            }
             // LDS-stationary B pays off for row blocks of >= 16 rows in BMWs of >= 2 rows
             // (C2: 20x2 31 us vs 40 us gathered; 4x1 62 us): otherwise the gather kernel
             bool lds_worth = false;
@@ -832,10 +878,11 @@ void upload_plan(plan_state &p, int dtype, int device) {
                     d.bytes_tile = d.bytes_A - before;
                 }
             }
+            upload_groups(!d.lds);
             break;
         }
         case KF_BLOCK_TOTAL: {
-            a.a0 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_row_indices", sb), "BMTB first_row_indices"));
+            a.a0 = upload_index(d, m, TBLOCK_META, "first_row_indices", sb, d.f0);
             std::vector<uint32_t> rp = csr_row_ptr(rows, row_num);
             a.a2 = dev_copy(d, rp);
             d.n_units = m.u(TBLOCK_META, "first_row_indices", sb).size() - 1;
@@ -858,8 +905,8 @@ void upload_plan(plan_state &p, int dtype, int device) {
                     if (j == 0 || rows[j] != rows[j - 1]) mm |= 1ull << (j - fn[i]);
                 mask[i] = mm;
             }
-            a.a0 = dev_copy(d, to_u32(fn, "first_nz_indices"));
-            a.a1 = dev_copy(d, to_u32(m.u(THREAD_META, "first_row_indices", sb), "first_row_indices"));
+            a.a0 = upload_index(d, m, THREAD_META, "first_nz_indices", sb, d.f0);
+            a.a1 = upload_index(d, m, THREAD_META, "first_row_indices", sb, d.f1);
             a.m0 = dev_copy(d, mask);
             a.a2 = dev_copy(d, to_u32(m.u(THREAD_META, "segment_ptr", sb), "segment_ptr"));
             a.a3 = dev_copy(d, to_u32(m.u(THREAD_META, "segment_empty_row_indices", sb), "segment_empty_row_indices"));
@@ -895,8 +942,8 @@ void upload_plan(plan_state &p, int dtype, int device) {
             const auto &fr = m.u(THREAD_META, "first_row_indices_without_ending", sb);
             GS_CHECK(fn.size() == fr.size() + 1 && !fr.empty(), "col-direction plan: BMT arrays disagree");
             std::vector<uint32_t> br = to_u32(fr, "first_row_indices_without_ending");
-            a.a0 = dev_copy(d, to_u32(fn, "first_nz_indices"));
-            a.a1 = dev_copy(d, br);
+            a.a0 = upload_index(d, m, THREAD_META, "first_nz_indices", sb, d.f0);
+            a.a1 = upload_index(d, m, THREAD_META, "first_row_indices_without_ending", sb, d.f1);
             d.n_units = br.size();
             d.scf = 4;
             d.span = gsk_host::row_chunk_span(br.size());
@@ -1302,7 +1349,7 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
             uint32_t groups = 256 / X;
             uint32_t gx = (uint32_t)std::min<uint64_t>((d.n_rows_aux + groups - 1) / groups, 1u << 16);
             hipLaunchKernelGGL((gsk::k_thread_total<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0,
-                               s, a.a0, a.a1, col, val, B, C, (uint32_t)d.n_units, (uint32_t)d.n_rows_aux, N, X,
+                               s, a.a0, d.f0, a.a1, d.f1, col, val, B, C, (uint32_t)d.n_units, (uint32_t)d.n_rows_aux, N, X,
                                row_base);
             break;
         }
@@ -1317,14 +1364,14 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
             if (sp.tblock_parent) gx = (uint32_t)d.n_rows_aux;
             else gx = (uint32_t)std::min<uint64_t>((d.n_units + 3) / 4, 1u << 16);
             hipLaunchKernelGGL((gsk::k_warp_rows<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
-                               a.a0, sp.tblock_parent ? a.a1 : nullptr, a.a2, col, val, B, C, (uint32_t)d.n_units, N,
+                               a.a0, d.f0, sp.tblock_parent ? a.a1 : nullptr, sp.tblock_parent ? d.f1 : gsk::idx_formula(), a.a2, col, val, B, C, (uint32_t)d.n_units, N,
                                X, row_base);
             break;
         }
         case KF_BLOCK_TOTAL: {
             uint32_t gx = (uint32_t)std::min<uint64_t>(d.n_units, 1u << 16);
             hipLaunchKernelGGL((gsk::k_block_rows<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
-                               a.a0, a.a2, col, val, B, C, (uint32_t)d.n_units, N, X, row_base);
+                               a.a0, d.f0, a.a2, col, val, B, C, (uint32_t)d.n_units, N, X, row_base);
             break;
         }
         case KF_BITMAP_SEGMENT: {
@@ -1336,7 +1383,7 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
             if (!use_ws)
                 HIP_OK(hipMemsetAsync(C + (size_t)d.out_lo * N, 0, (size_t)(d.n_out_rows - d.out_lo) * N * sizeof(VT), s));
             hipLaunchKernelGGL((gsk::k_bitmap_segment<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256),
-                               lds, s, a.a0, a.a1, a.m0, a.a2, a.a3, col, val, B, C, (uint32_t)d.n_units, N, X,
+                               lds, s, a.a0, d.f0, a.a1, d.f1, a.m0, a.a2, a.a3, col, val, B, C, (uint32_t)d.n_units, N, X,
                                row_base, use_ws ? a.ws : (float *)nullptr);
             if (use_ws && d.n_fin) {
                 HIP_OK(hipGetLastError());
@@ -1352,7 +1399,7 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
             const uint32_t nw = (uint32_t)((d.n_units + d.span - 1) / d.span);
             const uint32_t gx = std::min<uint32_t>((nw + 3) / 4, 1u << 16);
             hipLaunchKernelGGL((gsk::k_row_chunks<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
-                               a.a0, a.a1, col, val, B, C, a.ws, (uint32_t)d.n_units, d.span, N, X, row_base, d.ilv);
+                               a.a0, d.f0, a.a1, d.f1, col, val, B, C, a.ws, (uint32_t)d.n_units, d.span, N, X, row_base, d.ilv);
             if (d.n_fin) {
                 HIP_OK(hipGetLastError());
                 const uint32_t fx = (uint32_t)std::min<uint64_t>((d.n_fin * N + 255) / 256, 4096);

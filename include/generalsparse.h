@@ -63,6 +63,8 @@ typedef struct {
     uint32_t ksplit;              /* k_mfma_rows workgroups per row block (K ranges, fp32 slab combine) */
     int n_kernels;                /* kernels gs_spmm runs: 1, or one per sub-matrix of a row division */
     char device_kernel[32];       /* the device kernel gs_spmm launches at the plan's N (first sub-matrix) */
+    int index_formulas;           /* index arrays the kernel evaluates as formulas (MODEL_DRIVEN_COMPRESS) */
+    uint64_t index_bytes_saved;   /* u32 index bytes per replica those formulas keep out of HBM */
 } gs_plan_info;
 
 const char *gs_last_error(void);

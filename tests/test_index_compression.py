@@ -125,5 +125,10 @@ def test_emitted_program_uses_exact_formulas(tmp_path):
         gsa.set_config("MODEL_DRIVEN_COMPRESS", 0)
     src = open(os.path.join(d, "kernel_file.hip")).read()
     assert '"TBLOCK_META_first_row_indices_0"' in src and "20 * (i)" in src
+    # the kernel evaluates the BMW row starts and the BMTB -> BMW map (5 BMTBs of 10 BMWs):
+    # both linear, passed as gsk::idx_formula arguments, their arrays never uploaded
+    assert "const gsk::idx_formula F1 = gsk::idx_formula{1u, 10u, 0u, 1u," in src
+    assert "const gsk::idx_formula F0 = gsk::idx_formula{1u," in src
+    assert "F0.kind ? nullptr : up(u32(wr))" in src and "(d_a0, F0, d_a1, F1, d_a2," in src
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O1", "-std=c++17", "-c",
                            "kernel_file.hip", "-o", "kernel_file.o"], cwd=d)

@@ -76,3 +76,20 @@ def test_corrupted_plan_is_refused(case):
     assert words in msg, msg
     with pytest.raises(gsa.GsError, match="logical_check"):
         plan.compile()
+
+
+def test_merged_col_direction_rows_one_short_are_accepted():
+    """929 col-direction BMTs merged 32 to a BMW: get_begin_rows_after_merge_thread.cc:39-44
+    leaves the BMW row starts one short of the nz starts (30 vs 31) when n_BMT - 1 is a
+    multiple of 32; the plan runs (its kernel reads the BMT arrays) and is accepted, the
+    short array checked as group starts without an ending"""
+    row, col, _ = ds.random_rows(200, 1500, 300.0, seed=9, empty_frac=0.1)
+    p = gsa.Plan.from_coo(200, 1500, row, col, np.ones(len(row), np.float32)).run_pipeline("warp_bit_map", 32, 4, 1)
+    a = p.arrays()
+    assert len(a["THREAD_META_first_nz_indices_0"]) == 930
+    assert len(a["WARP_META_first_row_indices_0"]) + 1 == len(a["WARP_META_first_nz_indices_0"]) == 31
+    p.compile()
+    assert p.logical_check() == ""
+    # still a real check: a decreasing group start is caught
+    p.set_array_entry("WARP_META_first_row_indices_0", 5, 0)
+    assert "decreasing" in p.logical_check()
