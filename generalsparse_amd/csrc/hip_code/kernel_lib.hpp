@@ -1942,12 +1942,59 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
 //      the last slot's scan value is carried into the next round.
 // Empty rows are zeroed from a list by the kernel's first fill_blocks
 // workgroups, concurrently with the path waves (no memset of C, no extra
-// launch).  Rows crossing waves: the wave the
-// row is open at the end of writes (rid, partial) to rec/rec_row, the wave
-// that closes it writes its own partial to head_rec instead of C, and
-// k_merge_fixup sums them in wave order (deterministic, one rounding).
+// launch).  Rows crossing waves: the wave the row is open at the end of writes
+// its partial to rec[w], the wave that closes it writes its own partial to
+// head_rec instead of C.  With `chain` (one column tile) the partials are
+// combined in the same launch: every contributing wave publishes its partial
+// with agent-scope (L2 write-through) stores, waits for them, and bumps the
+// closing wave's arrival counter; the last arriver reads the chain's partials
+// back in wave order, stores the row (one rounding, deterministic) and re-arms
+// the counter.  No wave waits on another, so any dispatch order is safe.
+// Without `chain`, rec_row[w] names the open row and k_merge_fixup sums them.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kMpItems = 8;  // nonzeros per slot per round
+
+// Rows split across waves, combined in the launch.  A partial is published to part[src]
+// with agent-scope stores (written through the XCD's L2); its arrival (the X lanes of
+// one slot; lane0 = the slot's first lane) waits for the wave's stores, then the slot's
+// first lane bumps the closing wave's counter.  The arrival that completes the chain
+// (parts = close - first + 1) sums rec[first .. close-1] and head_rec[close] in wave
+// order with agent-scope loads, writes the row and re-arms the counter.
+template <int CF>
+__device__ __forceinline__ void merge_chain_publish(const float (&a)[CF], float *part, uint32_t src, uint32_t N,
+                                                    uint32_t c0, bool cok) {
+    if (cok) {
+#pragma unroll
+        for (int k = 0; k < CF; k++)
+            __hip_atomic_store(part + (size_t)src * N + c0 + k, a[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <class VT, int CF>
+__device__ __forceinline__ void merge_chain_arrive(uint32_t close, uint32_t first, const float *rec, const float *head_rec,
+                                                   uint32_t *cnt, uint32_t row, VT *C, uint32_t N, uint32_t c0, bool cok,
+                                                   uint32_t lane0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t old = 0;
+    if ((threadIdx.x & 63u) == lane0) old = __hip_atomic_fetch_add(cnt + close, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __shfl(old, (int)lane0, 64);
+    if (old + 1u != close - first + 1u) return;
+    if (cok) {
+        float s[CF];
+#pragma unroll
+        for (int k = 0; k < CF; k++) s[k] = 0.f;
+        for (uint32_t v = first; v < close; v++) {
+#pragma unroll
+            for (int k = 0; k < CF; k++)
+                s[k] += __hip_atomic_load(rec + (size_t)v * N + c0 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int k = 0; k < CF; k++)
+            s[k] += __hip_atomic_load(head_rec + (size_t)close * N + c0 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        store_f32<VT, CF>(C + (size_t)row * N + c0, s);
+    }
+    if ((threadIdx.x & 63u) == lane0) __hip_atomic_store(cnt + close, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // per wave: row-start flags (bytes 0..8S) and the staged output rows rid_l (cap + 2)
 __host__ __device__ constexpr uint32_t merge_path_wave_lds_words(uint32_t S) {
@@ -1955,7 +2002,7 @@ __host__ __device__ constexpr uint32_t merge_path_wave_lds_words(uint32_t S) {
 }
 
 template <class VT, class CT, int CF>
-__global__ __launch_bounds__(256) void k_merge_path(const uint32_t *__restrict__ wz,   // n_waves+1
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_merge_path(const uint32_t *__restrict__ wz,   // n_waves+1
                                                     const uint32_t *__restrict__ wq,   // n_waves+1
                                                     const uint32_t *__restrict__ ends, // n_crow
                                                     const uint32_t *__restrict__ rid,  // n_crow
@@ -1965,7 +2012,10 @@ __global__ __launch_bounds__(256) void k_merge_path(const uint32_t *__restrict__
                                                     uint32_t *__restrict__ rec_row, float *__restrict__ head_rec,
                                                     uint32_t n_waves, uint32_t N, uint32_t X, uint32_t row_lo,
                                                     uint32_t row_hi, const uint32_t *__restrict__ empty_rows,
-                                                    uint32_t n_empty, uint32_t fill_blocks, uint32_t dbg = 0) {
+                                                    uint32_t n_empty, uint32_t fill_blocks,
+                                                    const uint32_t *__restrict__ chain,  // 2 n_waves or null
+                                                    uint32_t *__restrict__ chain_cnt,    // n_waves, zero between launches
+                                                    uint32_t dbg = 0) {
     // dbg (diagnostic timing runs only, wrong results): bit 1 gathers B row 0 for every nonzero
     const uint32_t lb = blockIdx.x;  // (XCD-contiguous numbering measured no faster cold on C4)
     if (lb < fill_blocks) {
@@ -2003,17 +2053,25 @@ __global__ __launch_bounds__(256) void k_merge_path(const uint32_t *__restrict__
             const uint32_t zlo = wz[w], wend = wz[w + 1], q0 = wq[w];
             // the wave starts inside row q0 (its partial goes to head_rec)
             const bool head_open = zlo > (q0 ? ends[q0 - 1] : 0u);
+            const uint32_t head_first = chain && head_open ? chain[n_waves + w] : 0u;
             uint32_t qs = q0;
             float rc[CF];
 #pragma unroll
             for (int k = 0; k < CF; k++) rc[k] = 0.f;
             bool closed_end = false;
+            bool head_done = false;  // chain mode: this slot published the head row's partial
             auto emit = [&](uint32_t qq, const float (&a)[CF]) {
-                if (!cok) return;
                 if (qq == q0 && head_open) {
+                    if (chain) {  // published now (agent-scope stores), arrives after the walk
+                        merge_chain_publish<CF>(a, head_rec, w, N, c0, cok);
+                        head_done = true;
+                        return;
+                    }
+                    if (!cok) return;
 #pragma unroll
                     for (int k = 0; k < CF; k++) head_rec[(size_t)w * N + c0 + k] = a[k];
                 } else {
+                    if (!cok) return;
                     store_f32<VT, CF>(C + (size_t)rid_l[qq - qs + 1u] * N + c0, a);
                 }
             };
@@ -2033,10 +2091,11 @@ __global__ __launch_bounds__(256) void k_merge_path(const uint32_t *__restrict__
                     for (uint32_t k = 0; k < kMpItems; k++) { cn[k] = 0; vn[k] = (VT)0.f; }
                 }
             };
-            auto load_s = [&](uint32_t q_) {
+            auto load_s = [&](uint32_t q_) {  // the first 64 rows a round stages
                 const uint32_t j = q_ + lane;
                 en = j < n_crow ? ends[j] : 0xffffffffu;
                 rn = j < n_crow ? rid[j] : 0u;
+
             };
             const uint32_t zb0 = zlo & ~(kMpItems - 1u);
             load_a(zb0);
@@ -2064,7 +2123,7 @@ __global__ __launch_bounds__(256) void k_merge_path(const uint32_t *__restrict__
                 closed_end = false;
                 uint32_t e = en, r = rn;
                 for (uint32_t k0 = 0;; k0 += 64u) {
-                    if (k0) {  // rows beyond the prefetched batch (short rows): synchronous
+                    if (k0) {  // rows beyond the prefetched batches (short rows): synchronous
                         const uint32_t j = qs + k0 + lane;
                         e = j < n_crow ? ends[j] : 0xffffffffu;
                         r = j < n_crow ? rid[j] : 0u;
@@ -2175,11 +2234,22 @@ __global__ __launch_bounds__(256) void k_merge_path(const uint32_t *__restrict__
                 qs += nclose;
                 __builtin_amdgcn_wave_barrier();
             }
-            // the row open at the wave's end (if any): partial for k_merge_fixup
-            if (lane == 0) rec_row[w] = closed_end ? 0xffffffffu : rid[qs];
-            if (!closed_end && slot == 0 && cok) {
+            // the row open at the wave's end (if any): its partial joins the row's chain
+            if (chain) {
+                if (head_done)  // the slot that closed the head row
+                    merge_chain_arrive<VT, CF>(w, head_first, rec, head_rec, chain_cnt, rid[q0], C, N, c0, cok, lane - xl);
+                if (!closed_end && slot == 0) {
+                    const uint32_t cw_ = chain[w];  // the wave closing the row
+                    merge_chain_publish<CF>(rc, rec, w, N, c0, cok);
+                    merge_chain_arrive<VT, CF>(cw_, chain[n_waves + cw_], rec, head_rec, chain_cnt, rid[qs], C, N, c0, cok,
+                                               0u);
+                }
+            } else {
+                if (lane == 0) rec_row[w] = closed_end ? 0xffffffffu : rid[qs];
+                if (!closed_end && slot == 0 && cok) {
 #pragma unroll
-                for (int k = 0; k < CF; k++) rec[(size_t)w * N + c0 + k] = rc[k];
+                    for (int k = 0; k < CF; k++) rec[(size_t)w * N + c0 + k] = rc[k];
+                }
             }
         }
     }
@@ -2306,15 +2376,44 @@ inline std::vector<uint32_t> row_chunk_finalize_rows(const std::vector<uint32_t>
 // total_path[j] = ends[j] + j, so p == ends[j-1] + j - 1 is the step that
 // closes row j-1: the nonzeros consumed there are ends[j-1] = (p - j) + 1;
 // otherwise p - j.  Consecutive levels are grouped into waves of at least
-// target_steps path steps; waves never have an empty nz range.
+// target_steps path steps; waves never have an empty nz range.  snap > 0: a wave
+// boundary strictly inside a row of at most `snap` nonzeros moves to the nearer end of
+// that row, so the row is summed by one wave (no cross-wave combine for it; the
+// reference's own merge path splits such rows over threads and adds them atomically).
 struct merge_path_layout {
     std::vector<uint32_t> wz, wq, ends, rid, empty;  // empty: output rows without nonzeros
+    // rows split across waves: chain[w] = the wave closing the row open at w's end,
+    // chain[W + w] = the first wave of the row w closes at its head (~0: none)
+    std::vector<uint32_t> chain;
 };
+
+// the split-row chains of a layout (k_merge_path's in-launch combine)
+inline void merge_path_chains(merge_path_layout &L) {
+    const size_t W = L.wz.size() - 1;
+    L.chain.assign(2 * W, 0xffffffffu);
+    uint32_t start = 0xffffffffu;
+    size_t q_last = 0;
+    for (size_t w = 0; w < W; w++) {
+        const uint32_t zlo = L.wz[w], zhi = L.wz[w + 1], q0 = L.wq[w];
+        const bool head_open = zlo > (q0 ? L.ends[q0 - 1] : 0u);
+        q_last = std::max<size_t>(q_last, q0);
+        while (L.ends[q_last] < zhi) q_last++;  // the row holding position zhi - 1
+        const bool end_open = L.ends[q_last] > zhi;
+        const bool through = head_open && end_open && q_last == q0;  // the row spans the whole wave
+        if (head_open && !through) {
+            L.chain[W + w] = start;
+            for (uint32_t v = start; v < w; v++) L.chain[v] = (uint32_t)w;
+            start = 0xffffffffu;
+        }
+        if (end_open && !through) start = (uint32_t)w;
+    }
+}
 
 inline bool merge_path_device_layout(const std::vector<uint64_t> &row, uint64_t row_num,
                                      const std::vector<uint64_t> &lvl_rows, const std::vector<uint64_t> &lvl_nzs,
                                      uint64_t work_size, uint32_t row_base, uint64_t target_steps,
-                                     merge_path_layout &out, std::string &why, uint64_t out_rows = 0) {
+                                     merge_path_layout &out, std::string &why, uint64_t out_rows = 0,
+                                     uint64_t snap = 0) {
     out = merge_path_layout();
     std::vector<uint32_t> cnt(row_num, 0);
     for (uint64_t r : row) {
@@ -2349,15 +2448,29 @@ inline bool merge_path_device_layout(const std::vector<uint64_t> &row, uint64_t 
             why = "merge-path level " + std::to_string(w) + " is not on the path";
             return false;
         }
-        const uint64_t z = (j >= 1 && p == (uint64_t)out.ends[j - 1] + j - 1) ? (uint64_t)out.ends[j - 1] : p - j;
-        if (w == 0 || p - gp < target_steps || z <= gz) continue;
+        uint64_t z = (j >= 1 && p == (uint64_t)out.ends[j - 1] + j - 1) ? (uint64_t)out.ends[j - 1] : p - j;
+        uint64_t q = j;
+        if (w == 0 || p - gp < target_steps) continue;
+        if (snap && q < R) {
+            const uint64_t rs = q ? out.ends[q - 1] : 0, re = out.ends[q];
+            if (z > rs && re - rs <= snap) {
+                if (z - rs <= re - z) {
+                    z = rs;
+                } else {
+                    z = re;
+                    q++;
+                }
+            }
+        }
+        if (z <= gz || z >= acc) continue;
         out.wz.push_back((uint32_t)z);
-        out.wq.push_back((uint32_t)j);
+        out.wq.push_back((uint32_t)q);
         gz = z;
         gp = p;
     }
     out.wz.push_back((uint32_t)acc);
     out.wq.push_back((uint32_t)R);
+    merge_path_chains(out);
     return true;
 }
 

@@ -323,7 +323,7 @@ std::string code_generator::generate_kernel_file_source(int repeat) const {
               << "    hipMalloc(&d_rr, n_units * 4);\n";
             launch = "gsk::k_merge_path<VT, uint32_t, CF><<<dim3((n_units + 3) / 4 + 64, tiles), 256, "
                      "4 * gsk::merge_path_wave_lds_words(64 / X) * 4>>>(d_a0, d_a1, d_a2, d_a3, n_crow, d_col, d_val, d_B, d_C, "
-                     "d_r0, d_rr, d_r1, n_units, N, X, 0, (uint32_t)M, d_a4, (uint32_t)lay.empty.size(), 64u); "
+                     "d_r0, d_rr, d_r1, n_units, N, X, 0, (uint32_t)M, d_a4, (uint32_t)lay.empty.size(), 64u, nullptr, nullptr); "
                      "gsk::k_merge_fixup<VT><<<dim3((n_units * N + 255) / 256), 256>>>(d_rr, d_r0, d_r1, d_C, n_units, N)";
             break;
         }

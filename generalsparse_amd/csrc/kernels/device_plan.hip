@@ -969,7 +969,8 @@ void upload_plan(plan_state &p, int dtype, int device) {
             std::string why;
             GS_CHECK(gsk_host::merge_path_device_layout(rows, row_num, m.u(L, "first_row_indices_without_ending", sb),
                                                          m.u(L, "first_nz_indices", sb), (uint64_t)sp.work_size,
-                                                         (uint32_t)d.row_base, target, lay, why, d.n_out_rows),
+                                                         (uint32_t)d.row_base, target, lay, why, d.n_out_rows,
+                                                         2 * target),
                      "merge-path layout: " + why);
             a.a0 = dev_copy(d, lay.wz);
             a.a1 = dev_copy(d, lay.wq);
@@ -983,6 +984,8 @@ void upload_plan(plan_state &p, int dtype, int device) {
             a.ws = dev_copy(d, std::vector<float>((size_t)d.n_units * Nd, 0.f));
             a.ws2 = dev_copy(d, std::vector<float>((size_t)d.n_units * Nd, 0.f));
             a.t0 = dev_copy(d, std::vector<uint32_t>(d.n_units, 0xffffffffu));
+            a.t1 = dev_copy(d, lay.chain);                                 // split-row chains
+            a.t2 = dev_copy(d, std::vector<uint32_t>(d.n_units, 0u));     // their arrival counters
             d.scf = 8;
             break;
         }
@@ -1417,10 +1420,14 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
             const uint32_t gx = std::min<uint32_t>((W + 3) / 4, 1u << 16);
             GS_CHECK(d.n_fin * (uint64_t)N < 0xffffffffull, "merge-path empty-row fill exceeds 32-bit indices");
             const uint32_t fb = d.n_fin ? (uint32_t)std::min<uint64_t>(256, (d.n_fin * N / 4 + 1023) / 1024) : 0u;
+            // one column tile: split rows are combined inside the launch (chain arrivals)
+            const bool fused = tiles == 1 && !(mp_debug() & 4u);
             hipLaunchKernelGGL((gsk::k_merge_path<VT, CT, CF>), dim3(gx + fb, tiles), dim3(256), lds, s, a.a0, a.a1,
                                a.a2, a.a3, (uint32_t)d.n_rows_aux, col, val, B, C, a.ws, a.t0, a.ws2, W, N, X, row_base,
-                               (uint32_t)d.n_out_rows, a.a4, (uint32_t)d.n_fin, fb, mp_debug());
+                               (uint32_t)d.n_out_rows, a.a4, (uint32_t)d.n_fin, fb, fused ? a.t1 : nullptr,
+                               fused ? a.t2 : nullptr, mp_debug());
             HIP_OK(hipGetLastError());
+            if (fused) break;
             GS_CHECK((uint64_t)W * N < 0xffffffffull, "merge-path fix-up indices exceed 32 bits");
             const uint32_t fx = (uint32_t)std::min<uint64_t>(((uint64_t)W * N + 255) / 256, 1u << 16);
             hipLaunchKernelGGL((gsk::k_merge_fixup<VT>), dim3(std::max(fx, 1u)), dim3(256), 0, s, a.t0, a.ws, a.ws2, C,
