@@ -114,6 +114,14 @@ void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1)
     const uint64_t rows = sb == 0 ? global_scalar(s, "origin_row_num", -1)
                                   : global_scalar(s, "end_row_index", sb) - global_scalar(s, "begin_row_index", sb) + 1;
     const uint64_t nnz = s.meta->u(GLOBAL_META, "nz_col_indices", sb).size();
+    if (name.rfind("empty_pad_", 0) == 0) {
+        // empty_row_pad_operator first (every empty row gets one zero entry), then the
+        // named pipeline on the padded matrix
+        ex.add_and_run(std::make_shared<empty_row_pad_operator>(cg, ctx));
+        run_pipeline(s, name.substr(10), N, p0, p1);
+        s.pipeline = name;
+        return;
+    }
     if (name == "thread_total") {  // token_test.cc:1003-1092, p0 = sparse_cf (4), p1 = cf (1)
         int scf = p0 > 0 ? p0 : 4, cf = p1 > 0 ? p1 : 1;
         ex.add_and_run(std::make_shared<sort_operator>(cg, ctx));

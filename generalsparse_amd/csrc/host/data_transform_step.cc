@@ -142,6 +142,79 @@ void remove_empty_row_in_end_of_sub_matrix::run(bool check) {
     is_run = true;
 }
 
+// ----------------------------------------------------------- empty-row padding
+// modify_{col,val,row}_*_by_empty_pad_in_submatrix.cc:15-110: a nonzero whose next
+// nonzero (the sub-matrix's row count for the last one) lies more than one row further is
+// followed by one entry per skipped row -- that row, the nonzero's column, value 0.  The walk
+// starts at the first nonzero (leading empty rows stay empty); a nonzero followed by a
+// smaller row index is dropped, as the reference's loop emits nothing for it.  The row count
+// grows to the largest stored row (:27-33).
+namespace {
+struct empty_pad_plan {
+    std::vector<uint64_t> src, row;  // per output entry: source nonzero, row
+    std::vector<uint8_t> pad;        // 1: a padding entry (value 0)
+    bool padded = false;
+};
+empty_pad_plan make_empty_pad(const meta_data_set &m, int s) {
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    GS_CHECK(!row.empty(), "empty_row_pad: no nonzeros");
+    const uint64_t b = m.scalar(GLOBAL_META, "begin_row_index", s);
+    uint64_t e = m.scalar(GLOBAL_META, "end_row_index", s);
+    if (row.back() > e - b) e = b + row.back();
+    const uint64_t rn = e - b + 1;
+    empty_pad_plan p;
+    p.src.reserve(row.size());
+    for (uint64_t i = 0; i < row.size(); i++) {
+        const uint64_t r = row[i], nxt = i + 1 == row.size() ? rn : row[i + 1];
+        if (nxt == r || nxt == r + 1) {
+            p.src.push_back(i); p.row.push_back(r); p.pad.push_back(0);
+            continue;
+        }
+        for (uint64_t id = r; id < nxt; id++) {
+            p.src.push_back(i); p.row.push_back(id); p.pad.push_back(id > r);
+            if (id > r) p.padded = true;
+        }
+    }
+    return p;
+}
+}  // namespace
+
+void modify_col_indices_by_empty_pad_in_submatrix::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    auto p = make_empty_pad(m, target_matrix_id);
+    if (p.padded) {
+        const auto &col = m.u(GLOBAL_META, "nz_col_indices", target_matrix_id);
+        std::vector<uint64_t> nc(p.src.size());
+        for (size_t k = 0; k < nc.size(); k++) nc[k] = col[p.src[k]];
+        src(GLOBAL_META, "nz_col_indices");
+        replace_u(GLOBAL_META, "nz_col_indices", std::move(nc));
+    }
+    is_run = true;
+}
+
+void modify_vals_by_empty_pad_in_submatrix::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    auto p = make_empty_pad(m, target_matrix_id);
+    if (p.padded) {
+        auto va = m.get_element(GLOBAL_META, "nz_vals", target_matrix_id)->meta_data_arr;
+        std::vector<double> nv(p.src.size());
+        for (size_t k = 0; k < nv.size(); k++) nv[k] = p.pad[k] ? 0.0 : va->read_float_from_arr(p.src[k]);
+        src(GLOBAL_META, "nz_vals");
+        replace_f(GLOBAL_META, "nz_vals", std::move(nv), va->get_data_type());
+    }
+    is_run = true;
+}
+
+void modify_row_indices_by_empty_pad_in_submatrix::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    auto p = make_empty_pad(m, target_matrix_id);
+    if (p.padded) {
+        src(GLOBAL_META, "nz_row_indices");
+        replace_u(GLOBAL_META, "nz_row_indices", std::move(p.row));
+    }
+    is_run = true;
+}
+
 // ------------------------------------------------------------- col pad (A6)
 // modify_{col,val,row}_*_by_col_pad_in_sub_matrix.cc: pad each row to a multiple;
 // padded entries repeat the row's last column with value 0

@@ -58,6 +58,11 @@ GS_DECLARE_STEP(reorder_col_by_index)
 GS_DECLARE_STEP(reorder_row_by_index)
 GS_DECLARE_STEP(remove_empty_row_in_end_of_sub_matrix)
 
+// empty_row_pad_operator: one zero entry per empty row
+GS_DECLARE_STEP(modify_col_indices_by_empty_pad_in_submatrix)
+GS_DECLARE_STEP(modify_vals_by_empty_pad_in_submatrix)
+GS_DECLARE_STEP(modify_row_indices_by_empty_pad_in_submatrix)
+
 // column padding to a multiple of each row size (A6)
 GS_DECLARE_STEP_P(modify_col_indices_by_col_pad_in_sub_matrix, int, multiple_of_each_row_size)
 GS_DECLARE_STEP_P(modify_vals_by_col_pad_in_sub_matrix, int, multiple_of_each_row_size)

@@ -93,6 +93,58 @@ void sort_operator::run(bool check) {
     is_run = true;
 }
 
+// -------------------------------------------- empty_row_pad_operator
+empty_row_pad_operator::empty_row_pad_operator(cg_ptr cg, ctx_ptr)
+    : basic_operator("empty_row_pad_operator", cg->get_metadata_set(), CONVERTING_OP, cg->get_sub_matrix_id()) {}
+
+// empty_row_pad_operator.cc:25-55: no implementing or distributing operator yet, and no
+// sort_operator or empty_row_pad_operator before it on this sub-matrix
+bool empty_row_pad_operator::is_valid_according_to_operator(ctx_ptr h) {
+    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return false;
+    if (!h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id).empty()) return false;
+    for (auto &o : h->read_operator_context_arr(CONVERTING_OP, target_matrix_id)) {
+        if (o->get_target_matrix_id() != target_matrix_id) continue;
+        if (o->get_name().find("sort_operator") != std::string::npos ||
+            o->get_name().find("empty_row_pad_operator") != std::string::npos)
+            return false;
+    }
+    return true;
+}
+
+// empty_row_pad_operator.cc:57-135: the COO and its row range, no interleaved arrays, no
+// blocking metadata, at least one empty row in the (grown) row range, and the padding rate
+// of one entry per empty row under PADDING_RATE_UP_BOUND
+// (padding_rate_valid_empty_padding, data_transform_common.cc:600-643)
+bool empty_row_pad_operator::is_valid_according_to_metadata() {
+    auto &m = *meta_data_set_ptr;
+    const int s = target_matrix_id;
+    if (!coo_present(m, s) || interlance_storage_existing(m, s)) return false;
+    if (m.count_of_metadata_of_diff_pos(THREAD_META, s) || m.count_of_metadata_of_diff_pos(WARP_META, s) ||
+        m.count_of_metadata_of_diff_pos(TBLOCK_META, s))
+        return false;
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    if (row.empty()) return false;
+    const uint64_t b = m.scalar(GLOBAL_META, "begin_row_index", s);
+    uint64_t e = m.scalar(GLOBAL_META, "end_row_index", s);
+    if (row.back() > e - b) e = b + row.back();
+    const auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, e - b, 0, row.size() - 1);
+    const uint64_t zeros = (uint64_t)std::count(cnt.begin(), cnt.end(), 0ull);
+    if (!zeros) return false;
+    return (double)(row.size() + zeros) / (double)row.size() < (double)get_config().PADDING_RATE_UP_BOUND;
+}
+
+// empty_row_pad_operator.cc:137-170: the column, value and row transforms, in that order
+void empty_row_pad_operator::run(bool check) {
+    if (check) GS_CHECK(is_valid_according_to_metadata(), "empty_row_pad_operator: invalid metadata");
+    modify_col_indices_by_empty_pad_in_submatrix a(meta_data_set_ptr, target_matrix_id);
+    run_step(a, check);
+    modify_vals_by_empty_pad_in_submatrix b(meta_data_set_ptr, target_matrix_id);
+    run_step(b, check);
+    modify_row_indices_by_empty_pad_in_submatrix c(meta_data_set_ptr, target_matrix_id);
+    run_step(c, check);
+    is_run = true;
+}
+
 // -------------------------------------------- row-direction TBLOCK blocking
 fixed_interval_row_direction_tblock_blocking_operator::fixed_interval_row_direction_tblock_blocking_operator(
     cg_ptr cg, int rb, bool pad, ctx_ptr)
@@ -1085,6 +1137,7 @@ std::shared_ptr<basic_operator> make_operator(const std::string &name, const std
         GS_CHECK(a.size() == n, name + ": expected " + std::to_string(n) + " arguments");
     };
     if (name == "sort_operator") { need(0); return std::make_shared<sort_operator>(cg, ctx); }
+    if (name == "empty_row_pad_operator") { need(0); return std::make_shared<empty_row_pad_operator>(cg, ctx); }
     if (name == "fixed_interval_row_direction_tblock_blocking_operator") {
         need(2);
         return std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, (int)a[0], a[1] != 0, ctx);

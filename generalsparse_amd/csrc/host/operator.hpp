@@ -72,6 +72,16 @@ class sort_operator : public basic_operator {  // operator/sort_operator.cc
     bool is_valid_according_to_operator(ctx_ptr h) override;
 };
 
+// operator/empty_row_pad_operator.cc: CONVERTING; gives every empty row of the sub-matrix
+// one zero entry (before any blocking, not after sort_operator)
+class empty_row_pad_operator : public basic_operator {
+  public:
+    empty_row_pad_operator(cg_ptr cg, ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+};
+
 // operator/fixed_interval_row_matrix_div_operator.cc (§8f rank 3): CONVERTING; splits the
 // sub-matrix into sub-matrices of fixed_row_interval_size rows (non-empty intervals only)
 class fixed_interval_row_matrix_div_operator : public basic_operator {

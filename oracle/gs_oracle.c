@@ -311,6 +311,66 @@ int or_sort_operator(or_set *s) {
 }
 
 /* ------------------------------------------------------------------ */
+/* empty_row_pad_operator (operator/empty_row_pad_operator.cc:30-147)  */
+/* + modify_{col,val,row}_*_by_empty_pad_in_submatrix.cc:15-110         */
+/* ------------------------------------------------------------------ */
+
+int or_empty_row_pad(or_set *s) {
+    /* is_valid_according_to_operator (:25-55): not after sort_operator; the canned
+     * sequences here never run it twice or after a distributing operator */
+    if (exists(s, "GLOBAL_META", "original_nz_row_indices", 0))
+        return fail(s, "empty_row_pad after sort_operator (empty_row_pad_operator.cc:37-52)");
+    for (int i = 0; i < s->n; i++)
+        if (!strncmp(s->a[i].key, "THREAD_META", 11) || !strncmp(s->a[i].key, "WARP_META", 9) ||
+            !strncmp(s->a[i].key, "TBLOCK_META", 11))
+            return fail(s, "empty_row_pad with blocking metadata (empty_row_pad_operator.cc:117-121)");
+    if (exists(s, "GLOBAL_META", "nz_col_indices_after_interlance_storage", 0))
+        return fail(s, "empty_row_pad after interleaving (empty_row_pad_operator.cc:106-112)");
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    or_array *C = get(s, "GLOBAL_META", "nz_col_indices", 0);
+    or_array *V = get(s, "GLOBAL_META", "nz_vals", 0);
+    uint64_t nnz = R->len;
+    /* :82-95: the row range grows to the largest stored row */
+    uint64_t b = scalar(s, "GLOBAL_META", "begin_row_index", 0);
+    uint64_t e = scalar(s, "GLOBAL_META", "end_row_index", 0);
+    if (R->u[nnz - 1] > e - b) e = b + R->u[nnz - 1];
+    uint64_t rn = e - b + 1;
+    uint64_t *cnt = row_nnz(R->u, nnz, rn), zeros = 0;
+    for (uint64_t r = 0; r < rn; r++) zeros += cnt[r] == 0;
+    free(cnt);
+    if (!zeros) return fail(s, "no empty row (empty_row_pad_operator.cc:124)");
+    /* padding_rate_valid_empty_padding (data_transform_common.cc:600-643) */
+    if ((double)(nnz + zeros) / (double)nnz >= PADDING_RATE_UP_BOUND)
+        return fail(s, "empty padding rate %.3f >= %d", (double)(nnz + zeros) / nnz, PADDING_RATE_UP_BOUND);
+    /* the three transforms: a nonzero whose next nonzero (rn for the last) lies more than
+     * one row further is followed by one entry per skipped row (that row, its column,
+     * value 0); the walk starts at the first nonzero, so leading empty rows stay empty */
+    vu nr = {0}, nc = {0};
+    uint64_t fcap = nnz + zeros + 1, fn = 0;
+    double *nv = (double *)malloc(fcap * sizeof(double));
+    int padded = 0;
+    for (uint64_t i = 0; i < nnz; i++) {
+        uint64_t r = R->u[i], nxt = i + 1 == nnz ? rn : R->u[i + 1];
+        if (nxt == r || nxt == r + 1) {
+            vu_push(&nr, r); vu_push(&nc, C->u[i]); nv[fn++] = V->f[i];
+            continue;
+        }
+        double v = V->f[i];
+        for (uint64_t id = r; id < nxt; id++) { /* :63-72 (nothing when nxt < r) */
+            if (fn == fcap) { fcap *= 2; nv = (double *)realloc(nv, fcap * sizeof(double)); }
+            vu_push(&nr, id); vu_push(&nc, C->u[i]); nv[fn++] = v;
+            v = 0.0;
+            if (id > r) padded = 1;
+        }
+    }
+    if (!padded) { free(nr.p); free(nc.p); free(nv); return 0; }
+    put_u(s, "GLOBAL_META", "nz_col_indices", 0, nc.p, nc.n);
+    put_f(s, "GLOBAL_META", "nz_vals", 0, nv, fn);
+    put_u(s, "GLOBAL_META", "nz_row_indices", 0, nr.p, nr.n);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
 /* A6: modify_{col,val,row}_by_col_pad_in_sub_matrix                    */
 /*     modify_col_indices_by_col_pad_in_sub_matrix.cc:15-160            */
 /* ------------------------------------------------------------------ */
@@ -1227,6 +1287,11 @@ int or_pipeline(or_set *s, const char *name, int p0, int p1) {
         return or_fixed_interval_row_div(s, (uint64_t)p0);
     if (!strcmp(name, "row_nz_div")) /* p0 = init window, p1 = max window; expansion rate 2 */
         return or_row_nz_div(s, (uint64_t)p0, (uint64_t)p1, 2);
+    if (!strcmp(name, "empty_row_pad")) return or_empty_row_pad(s);
+    if (!strncmp(name, "empty_pad_", 10)) { /* empty_row_pad_operator, then the named sequence */
+        if (or_empty_row_pad(s)) return -1;
+        return or_pipeline(s, name + 10, p0, p1);
+    }
     if (!strcmp(name, "thread_total")) { /* token_test.cc:1003-1092, p0 = sparse_cf */
         if (or_sort_operator(s)) return -1;
         return or_row_dir_thread_blocking(s, 1, p0);

@@ -75,6 +75,7 @@ const char *or_error(const or_set *s);
 
 /* Operators (return 0 on success, <0 with s->err on a reference assert). */
 int or_sort_operator(or_set *s);                                           /* A3,A4 */
+int or_empty_row_pad(or_set *s);                                           /* empty_row_pad_operator */
 int or_row_dir_thread_blocking(or_set *s, int rb, int col_pad_size);       /* A5-A7 */
 int or_row_dir_tblock_blocking(or_set *s, int rb);                         /* A8 */
 int or_row_dir_warp_blocking(or_set *s, int rb);                           /* BMW */
