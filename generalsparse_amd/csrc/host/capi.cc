@@ -150,6 +150,30 @@ void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1)
         ex.add_and_run(std::make_shared<thread_bit_map_operator>(cg, THREAD_META, (unsigned)x, (unsigned)scf, (unsigned)cf, ctx));
         ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)(nnz / y + 1),
                                                              std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
+    } else if (name == "nnz_warp_bitmap" || name == "nnz_tblock_bitmap" || name == "nnz_tblock_warp_bitmap") {
+        // nnz-direction parents (fixed_interval_nnz_direction_{warp,tblock}_blocking_operator; p0 =
+        // nnz per BMW / BMTB, padded, p1 = nnz per BMW inside the BMTBs), 32-nnz BMTs inside them
+        // with indices relative to the parent (token_test.cc:851-870's composition), thread bitmaps
+        const int cf = 1;
+        if (name == "nnz_warp_bitmap") {
+            ex.add_and_run(std::make_shared<fixed_interval_nnz_direction_warp_blocking_operator>(cg, p0 > 0 ? p0 : 256, false,
+                                                                                                 false, true, ctx));
+        } else {
+            ex.add_and_run(std::make_shared<fixed_interval_nnz_direction_tblock_blocking_operator>(cg, p0 > 0 ? p0 : 1024,
+                                                                                                   true, ctx));
+            if (name == "nnz_tblock_warp_bitmap")
+                ex.add_and_run(std::make_shared<fixed_interval_nnz_direction_warp_blocking_operator>(cg, p1 > 0 ? p1 : 256,
+                                                                                                     true, true, false, ctx));
+        }
+        ex.add_and_run(std::make_shared<fixed_interval_nnz_direction_thread_blocking_operator>(cg, 32, true, true, false, ctx));
+        int x = N / cf < 32 ? N / cf : 32;
+        set_config("VECTOR_WIDTH", x);
+        int y = 128 / std::max(1, x);
+        cg->open_spec_level_of_paral(THREAD_META);
+        ex.add_and_run(std::make_shared<thread_bit_map_operator>(cg, THREAD_META, (unsigned)x, 4u, (unsigned)cf, ctx));
+        const uint64_t nz = s.meta->u(GLOBAL_META, "nz_col_indices", sb).size();
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)(nz / y + 1),
+                                                             std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
     } else if (name == "warp_segment") {  // token_test.cc:1393-1455
         int scf = p0 > 0 ? p0 : 4, cf = p1 > 0 ? p1 : 1;
         ex.add_and_run(std::make_shared<fixed_interval_nnz_direction_thread_blocking_operator>(cg, 32, false, false, true, ctx));

@@ -613,6 +613,192 @@ void get_BMT_size_of_each_parent::run(bool check) {
     is_run = true;
 }
 
+// ------------------------------------------- nnz-direction WARP / TBLOCK units
+namespace {
+// get_begin_rows_of_{BMW,BMTB}_after_fixed_blocking_in_nnz_direction.cc:20-40
+std::vector<uint64_t> nnz_unit_rows(const meta_data_set &m, int s, uint64_t k) {
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    const uint64_t b = m.scalar(GLOBAL_META, "begin_row_index", s);
+    uint64_t e = m.scalar(GLOBAL_META, "end_row_index", s);
+    if (e < b + row.back()) e = b + row.back();
+    std::vector<uint64_t> fr;
+    for (uint64_t i = 0; i < row.size(); i += k) fr.push_back(row[i]);
+    fr.push_back(e - b + 1);
+    return fr;
+}
+// get_begin_nzs_of_{BMW,BMTB}_after_fixed_blocking_in_nnz_direction.cc:18-30
+std::vector<uint64_t> nnz_unit_nzs(uint64_t nnz, uint64_t k) {
+    std::vector<uint64_t> fn;
+    for (uint64_t i = 0; i < nnz; i += k) fn.push_back(i);
+    fn.push_back(nnz);
+    return fn;
+}
+// *_relative_to_{BMTB,BMW}.cc:25-45: the parent advances by one when a unit start reaches
+// the next parent's first nonzero (an `if`, as in the reference: parents are never skipped
+// when their sizes are multiples of the unit size, which the operators require)
+std::vector<uint64_t> nnz_unit_relative(const meta_data_set &m, int s, POS_TYPE parent, uint64_t k, bool rows) {
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    const auto &pn = m.u(parent, "first_nz_indices", s);
+    const std::vector<uint64_t> *pr = rows ? &m.u(parent, "first_row_indices", s) : nullptr;
+    std::vector<uint64_t> out;
+    uint64_t pid = 0;
+    for (uint64_t i = 0; i < row.size(); i += k) {
+        GS_CHECK(pid + 1 < pn.size(), "nnz-direction unit beyond its parents");
+        if (i >= pn[pid + 1]) pid++;
+        out.push_back(rows ? row[i] - (*pr)[pid] : i - pn[pid]);
+    }
+    return out;
+}
+// children per parent: the first child index of every parent, parents start on a child
+std::vector<uint64_t> children_of_parents(const std::vector<uint64_t> &cn, const std::vector<uint64_t> &pn,
+                                          const char *what) {
+    std::vector<uint64_t> out{0};
+    uint64_t cur = 0;
+    for (uint64_t p = 0; p + 1 < pn.size(); p++) {
+        GS_CHECK(cur < cn.size() && cn[cur] == pn[p], std::string(what) + ": a parent does not start on a child");
+        uint64_t num = 0;
+        while (cn[cur] < pn[p + 1]) {
+            num++;
+            cur++;
+            GS_CHECK(cur < cn.size(), std::string(what) + ": children end before the parents");
+        }
+        out.push_back(out.back() + num);
+    }
+    return out;
+}
+// one size per parent when all children of it have the same number of nonzeros; a
+// parent with mixed sizes: nullopt (get_BMW_size_of_each_parent.cc returns without
+// writing the array)
+bool equal_sizes(const std::vector<uint64_t> &cn, const std::vector<uint64_t> *pn, std::vector<uint64_t> &out) {
+    out.clear();
+    if (!pn) {
+        uint64_t sz = 0;
+        for (uint64_t i = 0; i + 1 < cn.size(); i++) {
+            const uint64_t b = cn[i + 1] - cn[i];
+            if (i == 0) sz = b;
+            else if (b != sz) return false;
+        }
+        out.push_back(sz);
+        return true;
+    }
+    uint64_t cur = 0;
+    for (uint64_t p = 0; p + 1 < pn->size(); p++) {
+        uint64_t sz = 0;
+        bool seen = false;
+        while (cur + 1 < cn.size() && cn[cur] < (*pn)[p + 1]) {
+            const uint64_t b = cn[cur + 1] - cn[cur];
+            if (!seen) { sz = b; seen = true; }
+            else if (b != sz) return false;
+            cur++;
+        }
+        out.push_back(sz);
+    }
+    return true;
+}
+}  // namespace
+
+void get_begin_rows_of_BMW_after_fixed_blocking_in_nnz_direction::run(bool check) {
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(WARP_META, "first_row_indices", nnz_unit_rows(*meta_data_set_ptr, target_matrix_id, nnz_per_BMW));
+    is_run = true;
+}
+void get_begin_nzs_of_BMW_after_fixed_blocking_in_nnz_direction::run(bool check) {
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(WARP_META, "first_nz_indices",
+              nnz_unit_nzs(meta_data_set_ptr->u(GLOBAL_META, "nz_row_indices", target_matrix_id).size(), nnz_per_BMW));
+    is_run = true;
+}
+void get_begin_rows_of_BMW_after_fixed_blocking_in_nnz_direction_relative_to_BMTB::run(bool check) {
+    src(TBLOCK_META, "first_row_indices");
+    replace_u(WARP_META, "first_row_indices_relative_to_BMTB",
+              nnz_unit_relative(*meta_data_set_ptr, target_matrix_id, TBLOCK_META, nnz_per_BMW, true));
+    is_run = true;
+}
+void get_begin_nzs_of_BMW_after_fixed_blocking_in_nnz_direction_relative_to_BMTB::run(bool check) {
+    src(TBLOCK_META, "first_nz_indices");
+    replace_u(WARP_META, "first_nz_indices_relative_to_BMTB",
+              nnz_unit_relative(*meta_data_set_ptr, target_matrix_id, TBLOCK_META, nnz_per_BMW, false));
+    is_run = true;
+}
+void get_begin_rows_of_BMTB_after_fixed_blocking_in_nnz_direction::run(bool check) {
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(TBLOCK_META, "first_row_indices", nnz_unit_rows(*meta_data_set_ptr, target_matrix_id, nnz_per_BMTB));
+    is_run = true;
+}
+void get_begin_nzs_of_BMTB_after_fixed_blocking_in_nnz_direction::run(bool check) {
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(TBLOCK_META, "first_nz_indices",
+              nnz_unit_nzs(meta_data_set_ptr->u(GLOBAL_META, "nz_row_indices", target_matrix_id).size(), nnz_per_BMTB));
+    is_run = true;
+}
+void get_begin_rows_of_BMT_after_fixed_blocking_in_nnz_direction_relative_to_BMTB::run(bool check) {
+    src(TBLOCK_META, "first_row_indices");
+    replace_u(THREAD_META, "first_row_indices_relative_to_BMTB",
+              nnz_unit_relative(*meta_data_set_ptr, target_matrix_id, TBLOCK_META, nnz_per_BMT, true));
+    is_run = true;
+}
+void get_begin_nzs_of_BMT_after_fixed_blocking_in_nnz_direction_relative_to_BMTB::run(bool check) {
+    src(TBLOCK_META, "first_nz_indices");
+    replace_u(THREAD_META, "first_nz_indices_relative_to_BMTB",
+              nnz_unit_relative(*meta_data_set_ptr, target_matrix_id, TBLOCK_META, nnz_per_BMT, false));
+    is_run = true;
+}
+void get_begin_rows_of_BMT_after_fixed_blocking_in_nnz_direction_relative_to_BMW::run(bool check) {
+    src(WARP_META, "first_row_indices");
+    replace_u(THREAD_META, "first_row_indices_relative_to_BMW",
+              nnz_unit_relative(*meta_data_set_ptr, target_matrix_id, WARP_META, nnz_per_BMT, true));
+    is_run = true;
+}
+void get_begin_nzs_of_BMT_after_fixed_blocking_in_nnz_direction_relative_to_BMW::run(bool check) {
+    src(WARP_META, "first_nz_indices");
+    replace_u(THREAD_META, "first_nz_indices_relative_to_BMW",
+              nnz_unit_relative(*meta_data_set_ptr, target_matrix_id, WARP_META, nnz_per_BMT, false));
+    is_run = true;
+}
+// get_begin_BMWs_of_BMTB_after_blocking.cc:20-60
+void get_begin_BMWs_of_BMTB_after_blocking::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    src(WARP_META, "first_nz_indices");
+    src(TBLOCK_META, "first_nz_indices");
+    replace_u(TBLOCK_META, "first_BMW_indices",
+              children_of_parents(m.u(WARP_META, "first_nz_indices", target_matrix_id),
+                                  m.u(TBLOCK_META, "first_nz_indices", target_matrix_id), "get_begin_BMWs_of_BMTB_after_blocking"));
+    is_run = true;
+}
+// get_begin_BMTs_of_specific_parent_after_blocking.cc:20-75
+void get_begin_BMTs_of_specific_parent_after_blocking::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    GS_CHECK(parent_pos == TBLOCK_META || parent_pos == WARP_META, "BMT parent must be TBLOCK or WARP");
+    src(THREAD_META, "first_nz_indices");
+    src(parent_pos, "first_nz_indices");
+    replace_u(parent_pos, "first_BMT_indices",
+              children_of_parents(m.u(THREAD_META, "first_nz_indices", target_matrix_id),
+                                  m.u(parent_pos, "first_nz_indices", target_matrix_id),
+                                  "get_begin_BMTs_of_specific_parent_after_blocking"));
+    is_run = true;
+}
+// get_BMW_size_of_each_parent.cc:20-150 (mixed sizes: nothing written)
+void get_BMW_size_of_each_parent::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    std::vector<uint64_t> sizes;
+    const std::vector<uint64_t> *pn = parent_pos == GLOBAL_META ? nullptr : &m.u(parent_pos, "first_nz_indices", target_matrix_id);
+    if (equal_sizes(m.u(WARP_META, "first_nz_indices", target_matrix_id), pn, sizes)) {
+        src(WARP_META, "first_nz_indices");
+        replace_u(parent_pos, "BMW_size_of_each_blk", std::move(sizes));
+    }
+    is_run = true;
+}
+// get_BMTB_size.cc:20-95 (mixed sizes assert)
+void get_BMTB_size::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    std::vector<uint64_t> sizes;
+    GS_CHECK(equal_sizes(m.u(TBLOCK_META, "first_nz_indices", target_matrix_id), nullptr, sizes),
+             "get_BMTB_size: the BMTB sizes are not the same (get_BMTB_size.cc:81-85)");
+    src(TBLOCK_META, "first_nz_indices");
+    replace_u(GLOBAL_META, "BMTB_size_of_each_blk", std::move(sizes));
+    is_run = true;
+}
+
 // ------------------------------------------------------------ bitmaps
 // thread_bit_map.cc:14-92.  Bit i of map b is 1 iff nz first_nz[b]+i starts a row
 // (LSB = first nz).  With a parent level, the head of every parent_size-th BMT is

@@ -89,6 +89,28 @@ GS_DECLARE_STEP_P(modify_row_indices_by_nnz_pad, int, nnz_target)
 GS_DECLARE_STEP_P(get_begin_rows_of_BMT_after_fixed_blocking_in_nnz_direction, int, nnz_per_BMT)
 GS_DECLARE_STEP_P(get_begin_nzs_of_BMT_after_fixed_blocking_in_nnz_direction, int, nnz_per_BMT)
 
+// nnz-direction BMW / BMTB blocking and BMTs inside them
+// (fixed_interval_nnz_direction_{warp,tblock,thread}_blocking_operator.cc): a unit starts every
+// nnz_per_* nonzeros; its row is the row of that nonzero; the row array ends with the row
+// count; indices relative to the parent subtract the parent's first row / first nonzero
+GS_DECLARE_STEP_P(get_begin_rows_of_BMW_after_fixed_blocking_in_nnz_direction, int, nnz_per_BMW)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMW_after_fixed_blocking_in_nnz_direction, int, nnz_per_BMW)
+GS_DECLARE_STEP_P(get_begin_rows_of_BMW_after_fixed_blocking_in_nnz_direction_relative_to_BMTB, int, nnz_per_BMW)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMW_after_fixed_blocking_in_nnz_direction_relative_to_BMTB, int, nnz_per_BMW)
+GS_DECLARE_STEP_P(get_begin_rows_of_BMTB_after_fixed_blocking_in_nnz_direction, int, nnz_per_BMTB)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMTB_after_fixed_blocking_in_nnz_direction, int, nnz_per_BMTB)
+GS_DECLARE_STEP_P(get_begin_rows_of_BMT_after_fixed_blocking_in_nnz_direction_relative_to_BMTB, int, nnz_per_BMT)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMT_after_fixed_blocking_in_nnz_direction_relative_to_BMTB, int, nnz_per_BMT)
+GS_DECLARE_STEP_P(get_begin_rows_of_BMT_after_fixed_blocking_in_nnz_direction_relative_to_BMW, int, nnz_per_BMT)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMT_after_fixed_blocking_in_nnz_direction_relative_to_BMW, int, nnz_per_BMT)
+// children per parent (get_begin_BMWs_of_BMTB_after_blocking.cc,
+// get_begin_BMTs_of_specific_parent_after_blocking.cc), the unit sizes
+// (get_BMW_size_of_each_parent.cc, get_BMTB_size.cc)
+GS_DECLARE_STEP(get_begin_BMWs_of_BMTB_after_blocking)
+GS_DECLARE_STEP(get_BMTB_size)
+GS_DECLARE_STEP_P(get_BMW_size_of_each_parent, POS_TYPE, parent_pos)
+GS_DECLARE_STEP_P(get_begin_BMTs_of_specific_parent_after_blocking, POS_TYPE, parent_pos)
+
 // fixed col-direction blocking (A10): every row cut into chunks of col_size nnz
 GS_DECLARE_STEP_P(get_begin_rows_of_BMT_after_fixed_blocking_in_col_direction, int, col_size)
 GS_DECLARE_STEP_P(get_begin_nzs_of_BMT_after_fixed_blocking_in_col_direction, int, col_size)

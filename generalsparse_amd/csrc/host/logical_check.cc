@@ -148,8 +148,19 @@ std::string logical_check(const meta_data_set &m) {
         for (int l = 0; l < 3; l++) {
             const auto *nz = L[l].nz;
             if (!nz) continue;
-            // the BMWs of bitmap and col-direction plans group BMTs that split rows
-            const bool shared_rows = nnz_dir_thread || L[2].row_we != nullptr;
+            // the BMWs of bitmap and col-direction plans group BMTs that split rows; units of a
+            // fixed number of nonzeros (nnz-direction blocking at this level or below) split
+            // rows too
+            bool fixed_nnz = nz->size() >= 3;
+            for (size_t j = 0; fixed_nnz && j + 2 < nz->size(); j++)
+                fixed_nnz = (*nz)[j + 1] - (*nz)[j] == (*nz)[1] - (*nz)[0];
+            for (int d = l + 1; d < 3 && !fixed_nnz; d++) {
+                const auto *dn = L[d].nz;
+                bool f = dn && dn->size() >= 3;
+                for (size_t j = 0; f && j + 2 < dn->size(); j++) f = (*dn)[j + 1] - (*dn)[j] == (*dn)[1] - (*dn)[0];
+                fixed_nnz = f;
+            }
+            const bool shared_rows = nnz_dir_thread || L[2].row_we != nullptr || fixed_nnz;
             if (L[l].row)
                 for (size_t j = 0; j + 1 < nz->size(); j++) {
                     if ((*nz)[j + 1] == (*nz)[j]) continue;

@@ -472,29 +472,76 @@ fixed_interval_nnz_direction_thread_blocking_operator::fixed_interval_nnz_direct
 }
 
 // fixed_interval_nnz_direction_thread_blocking_operator.cc:40-96
+// fixed_interval_nnz_direction_thread_blocking_operator.cc:40-96: only nnz-direction parents,
+// whose sizes are multiples of nnz_per_BMT
 bool fixed_interval_nnz_direction_thread_blocking_operator::is_valid_according_to_operator(ctx_ptr h) {
-    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return false;
+    bool ok = true;
     for (auto &o : h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id)) {
         const auto &n = o->get_name();
-        if (n.find("fixed_interval_nnz_direction_tblock_blocking_operator") == std::string::npos &&
+        if (h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty() &&
+            n.find("fixed_interval_nnz_direction_tblock_blocking_operator") == std::string::npos &&
             n.find("fixed_interval_nnz_direction_warp_blocking_operator") == std::string::npos)
-            return false;
+            ok = false;
+        if (auto t = std::dynamic_pointer_cast<fixed_interval_nnz_direction_tblock_blocking_operator>(o))
+            if (t->get_nnz_per_BMTB() % nnz_per_BMT) ok = false;
+        if (auto w = std::dynamic_pointer_cast<fixed_interval_nnz_direction_warp_blocking_operator>(o))
+            if (w->get_nnz_per_BMW() % nnz_per_BMT) ok = false;
     }
+    return ok;
+}
+
+// fixed_interval_nnz_direction_thread_blocking_operator.cc:98-150: relative indices need a
+// parent; padding only without parents
+bool fixed_interval_nnz_direction_thread_blocking_operator::is_valid_according_to_metadata() {
+    auto &m = *meta_data_set_ptr;
+    const int s = target_matrix_id;
+    if (!coo_present(m, s) || m.count_of_metadata_of_diff_pos(THREAD_META, s) != 0 || interlance_storage_existing(m, s))
+        return false;
+    const bool bmtb = has(TBLOCK_META, "first_row_indices"), bmw = has(WARP_META, "first_row_indices");
+    if ((row_index_is_relative_to_parent || nz_index_is_relative_to_parent) && !(bmtb || has(WARP_META, "first_nz_indices")))
+        return false;
+    if (nnz_padding && (bmtb || bmw)) return false;
     return true;
 }
 
-bool fixed_interval_nnz_direction_thread_blocking_operator::is_valid_according_to_metadata() {
-    auto &m = *meta_data_set_ptr;
-    return coo_present(m, target_matrix_id) && m.count_of_metadata_of_diff_pos(THREAD_META, target_matrix_id) == 0 &&
-           !interlance_storage_existing(m, target_matrix_id);
-}
-
-// fixed_interval_nnz_direction_thread_blocking_operator.cc:156-245 (no-parent branch)
+// fixed_interval_nnz_direction_thread_blocking_operator.cc:156-245
 void fixed_interval_nnz_direction_thread_blocking_operator::run(bool check) {
     if (check) GS_CHECK(is_valid_according_to_metadata(), "nnz blocking: invalid metadata");
-    if (row_index_is_relative_to_parent || nz_index_is_relative_to_parent ||
-        has(TBLOCK_META, "first_row_indices") || has(WARP_META, "first_row_indices"))
-        throw gs_error("nnz-direction BMT blocking inside a parent is not built in this round");
+    const bool bmtb = has(TBLOCK_META, "first_row_indices"), bmw = has(WARP_META, "first_row_indices");
+    if (bmtb || bmw) {
+        // BMTs inside the nearest parent: absolute starts, the relative ones, the parent's
+        // first BMT of each block; the size step keeps the reference's GLOBAL parent
+        const POS_TYPE par = bmw ? WARP_META : TBLOCK_META;
+        get_begin_rows_of_BMT_after_fixed_blocking_in_nnz_direction d(meta_data_set_ptr, target_matrix_id, nnz_per_BMT);
+        run_step(d, check);
+        if (row_index_is_relative_to_parent) {
+            if (bmw) {
+                get_begin_rows_of_BMT_after_fixed_blocking_in_nnz_direction_relative_to_BMW r(meta_data_set_ptr, target_matrix_id, nnz_per_BMT);
+                run_step(r, check);
+            } else {
+                get_begin_rows_of_BMT_after_fixed_blocking_in_nnz_direction_relative_to_BMTB r(meta_data_set_ptr, target_matrix_id, nnz_per_BMT);
+                run_step(r, check);
+            }
+        }
+        get_begin_nzs_of_BMT_after_fixed_blocking_in_nnz_direction e(meta_data_set_ptr, target_matrix_id, nnz_per_BMT);
+        run_step(e, check);
+        if (nz_index_is_relative_to_parent) {
+            if (bmw) {
+                get_begin_nzs_of_BMT_after_fixed_blocking_in_nnz_direction_relative_to_BMW r(meta_data_set_ptr, target_matrix_id, nnz_per_BMT);
+                run_step(r, check);
+            } else {
+                get_begin_nzs_of_BMT_after_fixed_blocking_in_nnz_direction_relative_to_BMTB r(meta_data_set_ptr, target_matrix_id, nnz_per_BMT);
+                run_step(r, check);
+            }
+        }
+        get_begin_BMTs_of_specific_parent_after_blocking g(meta_data_set_ptr, target_matrix_id, par);
+        run_step(g, check);
+        get_BMT_size_of_each_parent f(meta_data_set_ptr, GLOBAL_META, target_matrix_id, false);
+        run_step(f, check);
+        code_generator_ptr->open_spec_level_of_paral(THREAD_META);
+        is_run = true;
+        return;
+    }
     if (nnz_padding) {
         modify_col_indices_by_nnz_pad a(meta_data_set_ptr, target_matrix_id, nnz_per_BMT);
         run_step(a, check);
@@ -510,6 +557,123 @@ void fixed_interval_nnz_direction_thread_blocking_operator::run(bool check) {
     get_BMT_size_of_each_parent f(meta_data_set_ptr, GLOBAL_META, target_matrix_id, false);
     run_step(f, check);
     code_generator_ptr->open_spec_level_of_paral(THREAD_META);
+    is_run = true;
+}
+
+// ------------------------------------------ nnz-direction TBLOCK / WARP blocking
+fixed_interval_nnz_direction_tblock_blocking_operator::fixed_interval_nnz_direction_tblock_blocking_operator(
+    cg_ptr cg, int nnz_per_BMTB, bool nnz_padding, ctx_ptr)
+    : basic_operator("fixed_interval_nnz_direction_tblock_blocking_operator", cg->get_metadata_set(), DISTRIBUTING_OP,
+                     cg->get_sub_matrix_id()),
+      nnz_per_BMTB(nnz_per_BMTB), nnz_padding(nnz_padding), code_generator_ptr(cg) {
+    GS_CHECK(nnz_per_BMTB > 0, "nnz_per_BMTB > 0");
+}
+
+// fixed_interval_nnz_direction_tblock_blocking_operator.cc:35-48: the first distributing operator
+bool fixed_interval_nnz_direction_tblock_blocking_operator::is_valid_according_to_operator(ctx_ptr h) {
+    return h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty() &&
+           h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id).empty();
+}
+
+// :50-85: the COO, no blocking metadata at any level, no interleaved arrays
+bool fixed_interval_nnz_direction_tblock_blocking_operator::is_valid_according_to_metadata() {
+    auto &m = *meta_data_set_ptr;
+    const int s = target_matrix_id;
+    return coo_present(m, s) && !interlance_storage_existing(m, s) && m.count_of_metadata_of_diff_pos(THREAD_META, s) == 0 &&
+           m.count_of_metadata_of_diff_pos(WARP_META, s) == 0 && m.count_of_metadata_of_diff_pos(TBLOCK_META, s) == 0;
+}
+
+// :87-135
+void fixed_interval_nnz_direction_tblock_blocking_operator::run(bool check) {
+    if (check) GS_CHECK(is_valid_according_to_metadata(), "nnz-direction tblock blocking: invalid metadata");
+    if (nnz_padding) {
+        modify_col_indices_by_nnz_pad a(meta_data_set_ptr, target_matrix_id, nnz_per_BMTB);
+        run_step(a, check);
+        modify_vals_by_nnz_pad b(meta_data_set_ptr, target_matrix_id, nnz_per_BMTB);
+        run_step(b, check);
+        modify_row_indices_by_nnz_pad c(meta_data_set_ptr, target_matrix_id, nnz_per_BMTB);
+        run_step(c, check);
+    }
+    get_begin_rows_of_BMTB_after_fixed_blocking_in_nnz_direction d(meta_data_set_ptr, target_matrix_id, nnz_per_BMTB);
+    run_step(d, check);
+    get_begin_nzs_of_BMTB_after_fixed_blocking_in_nnz_direction e(meta_data_set_ptr, target_matrix_id, nnz_per_BMTB);
+    run_step(e, check);
+    if (nnz_padding) {
+        get_BMTB_size f(meta_data_set_ptr, target_matrix_id);
+        run_step(f, check);
+    }
+    code_generator_ptr->open_spec_level_of_paral(TBLOCK_META);
+    is_run = true;
+}
+
+fixed_interval_nnz_direction_warp_blocking_operator::fixed_interval_nnz_direction_warp_blocking_operator(
+    cg_ptr cg, int nnz_per_BMW, bool rrel, bool nrel, bool nnz_padding, ctx_ptr)
+    : basic_operator("fixed_interval_nnz_direction_warp_blocking_operator", cg->get_metadata_set(), DISTRIBUTING_OP,
+                     cg->get_sub_matrix_id()),
+      nnz_per_BMW(nnz_per_BMW), row_index_is_relative_to_parent(rrel), nz_index_is_relative_to_parent(nrel),
+      nnz_padding(nnz_padding), code_generator_ptr(cg) {
+    GS_CHECK(nnz_per_BMW > 0, "nnz_per_BMW > 0");
+}
+
+// fixed_interval_nnz_direction_warp_blocking_operator.cc:40-85: only an nnz-direction BMTB
+// before it, whose size is a multiple of nnz_per_BMW
+bool fixed_interval_nnz_direction_warp_blocking_operator::is_valid_according_to_operator(ctx_ptr h) {
+    bool ok = true;
+    for (auto &o : h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id)) {
+        if (h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty() &&
+            o->get_name().find("fixed_interval_nnz_direction_tblock_blocking_operator") == std::string::npos)
+            ok = false;
+        if (auto t = std::dynamic_pointer_cast<fixed_interval_nnz_direction_tblock_blocking_operator>(o))
+            if (t->get_nnz_per_BMTB() % nnz_per_BMW) ok = false;
+    }
+    return ok;
+}
+
+// :87-130: no THREAD / WARP metadata yet; relative indices need the BMTB level; padding
+// only without it; no interleaved arrays
+bool fixed_interval_nnz_direction_warp_blocking_operator::is_valid_according_to_metadata() {
+    auto &m = *meta_data_set_ptr;
+    const int s = target_matrix_id;
+    if (!coo_present(m, s) || interlance_storage_existing(m, s) || m.count_of_metadata_of_diff_pos(THREAD_META, s) != 0 ||
+        m.count_of_metadata_of_diff_pos(WARP_META, s) != 0)
+        return false;
+    const bool bmtb = has(TBLOCK_META, "first_row_indices");
+    if ((row_index_is_relative_to_parent || nz_index_is_relative_to_parent) && !bmtb) return false;
+    if (nnz_padding && bmtb) return false;
+    return true;
+}
+
+// :132-200
+void fixed_interval_nnz_direction_warp_blocking_operator::run(bool check) {
+    if (check) GS_CHECK(is_valid_according_to_metadata(), "nnz-direction warp blocking: invalid metadata");
+    const bool bmtb = has(TBLOCK_META, "first_row_indices");
+    if (nnz_padding) {
+        modify_col_indices_by_nnz_pad a(meta_data_set_ptr, target_matrix_id, nnz_per_BMW);
+        run_step(a, check);
+        modify_vals_by_nnz_pad b(meta_data_set_ptr, target_matrix_id, nnz_per_BMW);
+        run_step(b, check);
+        modify_row_indices_by_nnz_pad c(meta_data_set_ptr, target_matrix_id, nnz_per_BMW);
+        run_step(c, check);
+    }
+    get_begin_rows_of_BMW_after_fixed_blocking_in_nnz_direction d(meta_data_set_ptr, target_matrix_id, nnz_per_BMW);
+    run_step(d, check);
+    get_begin_nzs_of_BMW_after_fixed_blocking_in_nnz_direction e(meta_data_set_ptr, target_matrix_id, nnz_per_BMW);
+    run_step(e, check);
+    if (row_index_is_relative_to_parent) {
+        get_begin_rows_of_BMW_after_fixed_blocking_in_nnz_direction_relative_to_BMTB r(meta_data_set_ptr, target_matrix_id, nnz_per_BMW);
+        run_step(r, check);
+    }
+    if (nz_index_is_relative_to_parent) {
+        get_begin_nzs_of_BMW_after_fixed_blocking_in_nnz_direction_relative_to_BMTB r(meta_data_set_ptr, target_matrix_id, nnz_per_BMW);
+        run_step(r, check);
+    }
+    if (bmtb) {
+        get_begin_BMWs_of_BMTB_after_blocking g(meta_data_set_ptr, target_matrix_id);
+        run_step(g, check);
+    }
+    get_BMW_size_of_each_parent f(meta_data_set_ptr, target_matrix_id, GLOBAL_META);
+    run_step(f, check);
+    code_generator_ptr->open_spec_level_of_paral(WARP_META);
     is_run = true;
 }
 
@@ -1151,6 +1315,15 @@ std::shared_ptr<basic_operator> make_operator(const std::string &name, const std
         need(7);
         return std::make_shared<fixed_interval_row_direction_thread_blocking_operator>(
             cg, (int)a[0], a[1] != 0, a[2] != 0, a[3] != 0, a[4] != 0, a[5] != 0, (int)a[6], ctx);
+    }
+    if (name == "fixed_interval_nnz_direction_tblock_blocking_operator") {
+        need(2);
+        return std::make_shared<fixed_interval_nnz_direction_tblock_blocking_operator>(cg, (int)a[0], a[1] != 0, ctx);
+    }
+    if (name == "fixed_interval_nnz_direction_warp_blocking_operator") {
+        need(4);
+        return std::make_shared<fixed_interval_nnz_direction_warp_blocking_operator>(cg, (int)a[0], a[1] != 0, a[2] != 0,
+                                                                                     a[3] != 0, ctx);
     }
     if (name == "fixed_interval_nnz_direction_thread_blocking_operator") {
         need(4);

@@ -171,6 +171,49 @@ class fixed_interval_row_direction_thread_blocking_operator : public basic_opera
     cg_ptr code_generator_ptr;
 };
 
+// operator/fixed_interval_nnz_direction_tblock_blocking_operator.cc: DISTRIBUTING; BMTBs of
+// nnz_per_BMTB nonzeros (optionally padded to a multiple), first of all distributing operators
+class fixed_interval_nnz_direction_tblock_blocking_operator : public basic_operator {
+  public:
+    fixed_interval_nnz_direction_tblock_blocking_operator(cg_ptr cg, int nnz_per_BMTB, bool nnz_padding,
+                                                          ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    void set_padding_to_false() override { nnz_padding = false; }
+    int get_nnz_per_BMTB() const { return nnz_per_BMTB; }
+    std::string convert_to_string() const override {
+        return basic_operator::convert_to_string() + ",nnz_per_BMTB:" + std::to_string(nnz_per_BMTB);
+    }
+    int nnz_per_BMTB;
+    bool nnz_padding;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
+// operator/fixed_interval_nnz_direction_warp_blocking_operator.cc: DISTRIBUTING; BMWs of
+// nnz_per_BMW nonzeros, alone or inside nnz-direction BMTBs (a multiple of nnz_per_BMW)
+class fixed_interval_nnz_direction_warp_blocking_operator : public basic_operator {
+  public:
+    fixed_interval_nnz_direction_warp_blocking_operator(cg_ptr cg, int nnz_per_BMW, bool row_index_is_relative_to_parent,
+                                                        bool nz_index_is_relative_to_parent, bool nnz_padding,
+                                                        ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    void set_padding_to_false() override { nnz_padding = false; }
+    int get_nnz_per_BMW() const { return nnz_per_BMW; }
+    std::string convert_to_string() const override {
+        return basic_operator::convert_to_string() + ",nnz_per_BMW:" + std::to_string(nnz_per_BMW);
+    }
+    int nnz_per_BMW;
+    bool row_index_is_relative_to_parent, nz_index_is_relative_to_parent, nnz_padding;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
 class fixed_interval_nnz_direction_thread_blocking_operator : public basic_operator {
   public:
     fixed_interval_nnz_direction_thread_blocking_operator(cg_ptr cg, int nnz_per_BMT,

@@ -576,6 +576,150 @@ int or_nnz_dir_thread_blocking(or_set *s, int nnz_per_bmt, int pad) {
 }
 
 /* ------------------------------------------------------------------ */
+/* nnz-direction BMTB / BMW blocking and BMTs inside them               */
+/* fixed_interval_nnz_direction_{tblock,warp,thread}_blocking_operator  */
+/* ------------------------------------------------------------------ */
+
+/* modify_{col,val,row}_*_by_nnz_pad.cc:14-75: pad the COO to a multiple of k with copies
+ * of the last entry's row / column and value 0 */
+static int nnz_pad_to(or_set *s, uint64_t k) {
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    uint64_t nnz = R->len;
+    if (nnz % k == 0) return 0;
+    uint64_t nn = (nnz / k + 1) * k;
+    if ((double)nn / (double)nnz >= PADDING_RATE_UP_BOUND)
+        return fail(s, "nnz padding rate %.3f >= %d", (double)nn / nnz, PADDING_RATE_UP_BOUND);
+    or_array *C = get(s, "GLOBAL_META", "nz_col_indices", 0);
+    or_array *V = get(s, "GLOBAL_META", "nz_vals", 0);
+    uint64_t *nc = (uint64_t *)malloc(nn * 8), *nr = (uint64_t *)malloc(nn * 8);
+    double *nv = (double *)malloc(nn * 8);
+    for (uint64_t i = 0; i < nn; i++) {
+        uint64_t q = i < nnz ? i : nnz - 1;
+        nc[i] = C->u[q]; nr[i] = R->u[q];
+        nv[i] = i < nnz ? V->f[i] : 0.0;
+    }
+    put_u(s, "GLOBAL_META", "nz_col_indices", 0, nc, nn);
+    put_f(s, "GLOBAL_META", "nz_vals", 0, nv, nn);
+    put_u(s, "GLOBAL_META", "nz_row_indices", 0, nr, nn);
+    return 0;
+}
+
+/* get_begin_{rows,nzs}_of_<unit>_after_fixed_blocking_in_nnz_direction.cc: a unit every k
+ * nonzeros, its row = the row of that nonzero, the row array closed by the row count */
+static void nnz_units(or_set *s, const char *pos, uint64_t k) {
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    uint64_t nnz = R->len, row_num = row_num_of(s);
+    vu fr = {0}, fn = {0};
+    for (uint64_t i = 0; i < nnz; i += k) { vu_push(&fr, R->u[i]); vu_push(&fn, i); }
+    vu_push(&fr, row_num);
+    vu_push(&fn, nnz);
+    put_u(s, pos, "first_row_indices", 0, fr.p, fr.n);
+    put_u(s, pos, "first_nz_indices", 0, fn.p, fn.n);
+}
+
+/* *_relative_to_{BMTB,BMW}.cc:25-45: the parent id moves on by one (an `if`) when a unit
+ * start reaches the next parent's first nonzero */
+static void nnz_units_relative(or_set *s, const char *pos, const char *parent, const char *suffix, uint64_t k,
+                               int rows, int nzs) {
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    or_array *PN = get(s, parent, "first_nz_indices", 0), *PR = get(s, parent, "first_row_indices", 0);
+    vu rr = {0}, rn = {0};
+    uint64_t pid = 0;
+    for (uint64_t i = 0; i < R->len; i += k) {
+        if (i >= PN->u[pid + 1]) pid++;
+        vu_push(&rr, R->u[i] - PR->u[pid]);
+        vu_push(&rn, i - PN->u[pid]);
+    }
+    char nr_[64], nn_[64];
+    snprintf(nr_, sizeof nr_, "first_row_indices_relative_to_%s", suffix);
+    snprintf(nn_, sizeof nn_, "first_nz_indices_relative_to_%s", suffix);
+    if (rows) put_u(s, pos, nr_, 0, rr.p, rr.n); else free(rr.p);
+    if (nzs) put_u(s, pos, nn_, 0, rn.p, rn.n); else free(rn.p);
+}
+
+/* get_begin_BMWs_of_BMTB_after_blocking.cc / get_begin_BMTs_of_specific_parent_after_blocking.cc:
+ * the first child of every parent */
+static int children_of(or_set *s, const char *child, const char *parent, const char *name) {
+    or_array *CN = get(s, child, "first_nz_indices", 0), *PN = get(s, parent, "first_nz_indices", 0);
+    vu out = {0};
+    vu_push(&out, 0);
+    uint64_t cur = 0;
+    for (uint64_t p = 0; p + 1 < PN->len; p++) {
+        if (CN->u[cur] != PN->u[p]) { free(out.p); return fail(s, "a parent does not start on a child"); }
+        uint64_t num = 0;
+        while (CN->u[cur] < PN->u[p + 1]) { num++; cur++; }
+        vu_push(&out, out.p[out.n - 1] + num);
+    }
+    put_u(s, parent, name, 0, out.p, out.n);
+    return 0;
+}
+
+/* one size when every unit of the level has the same number of nonzeros (GLOBAL parent) */
+static int same_size(or_set *s, const char *pos, uint64_t *size) {
+    or_array *FN = get(s, pos, "first_nz_indices", 0);
+    *size = FN->u[1] - FN->u[0];
+    for (uint64_t i = 0; i + 1 < FN->len; i++)
+        if (FN->u[i + 1] - FN->u[i] != *size) return 0;
+    return 1;
+}
+
+static int has_level(or_set *s, const char *pos) {
+    size_t n = strlen(pos);
+    for (int i = 0; i < s->n; i++)
+        if (!strncmp(s->a[i].key, pos, n)) return 1;
+    return 0;
+}
+
+int or_nnz_dir_tblock_blocking(or_set *s, uint64_t k, int pad) {
+    /* fixed_interval_nnz_direction_tblock_blocking_operator.cc:50-135 */
+    if (has_level(s, "THREAD_META") || has_level(s, "WARP_META") || has_level(s, "TBLOCK_META"))
+        return fail(s, "nnz-direction tblock blocking after other blocking (:63-70)");
+    if (pad && nnz_pad_to(s, k)) return -1;
+    nnz_units(s, "TBLOCK_META", k);
+    uint64_t sz;
+    if (pad) {
+        if (!same_size(s, "TBLOCK_META", &sz)) return fail(s, "BMTB sizes differ (get_BMTB_size.cc:81-85)");
+        put_scalar(s, "GLOBAL_META", "BMTB_size_of_each_blk", 0, sz);
+    }
+    return 0;
+}
+
+int or_nnz_dir_warp_blocking(or_set *s, uint64_t k, int rrel, int nrel, int pad) {
+    /* fixed_interval_nnz_direction_warp_blocking_operator.cc:87-200 */
+    int bmtb = exists(s, "TBLOCK_META", "first_row_indices", 0);
+    if (has_level(s, "THREAD_META") || has_level(s, "WARP_META")) return fail(s, "warp level exists (:95-99)");
+    if ((rrel || nrel) && !bmtb) return fail(s, "relative BMW indices without a BMTB (:102-105)");
+    if (pad && bmtb) return fail(s, "nnz padding inside a BMTB (:106-109)");
+    if (bmtb) {
+        or_array *PN = get(s, "TBLOCK_META", "first_nz_indices", 0);
+        uint64_t bsz = PN->u[1] - PN->u[0];
+        if (bsz % k) return fail(s, "nnz_per_BMTB %% nnz_per_BMW != 0 (:60-70)");
+    }
+    if (pad && nnz_pad_to(s, k)) return -1;
+    nnz_units(s, "WARP_META", k);
+    if (rrel || nrel) nnz_units_relative(s, "WARP_META", "TBLOCK_META", "BMTB", k, rrel, nrel);
+    if (bmtb && children_of(s, "WARP_META", "TBLOCK_META", "first_BMW_indices")) return -1;
+    uint64_t sz;
+    if (same_size(s, "WARP_META", &sz)) put_scalar(s, "GLOBAL_META", "BMW_size_of_each_blk", 0, sz);
+    return 0;
+}
+
+/* BMTs inside an nnz-direction parent (fixed_interval_nnz_direction_thread_blocking_operator.cc:156-245) */
+int or_nnz_dir_thread_in_parent(or_set *s, uint64_t k, int rrel, int nrel) {
+    int bmw = exists(s, "WARP_META", "first_row_indices", 0), bmtb = exists(s, "TBLOCK_META", "first_row_indices", 0);
+    if (!bmw && !bmtb) return fail(s, "no parent level");
+    const char *par = bmw ? "WARP_META" : "TBLOCK_META";
+    or_array *PN = get(s, par, "first_nz_indices", 0);
+    if ((PN->u[1] - PN->u[0]) % k) return fail(s, "parent size %% nnz_per_BMT != 0 (:66-90)");
+    nnz_units(s, "THREAD_META", k);
+    if (rrel || nrel) nnz_units_relative(s, "THREAD_META", par, bmw ? "BMW" : "BMTB", k, rrel, nrel);
+    if (children_of(s, "THREAD_META", par, "first_BMT_indices")) return -1;
+    uint64_t sz;
+    if (same_size(s, "THREAD_META", &sz)) put_scalar(s, "GLOBAL_META", "BMT_size_of_each_blk", 0, sz);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
 /* thread_bit_map_operator.cc:60-101 and its transforms                 */
 /* ------------------------------------------------------------------ */
 
@@ -1300,6 +1444,25 @@ int or_pipeline(or_set *s, const char *name, int p0, int p1) {
         return or_row_dir_warp_blocking(s, 1);
     if (!strcmp(name, "block_total")) /* token_test.cc:1458-1514 (rb 1 there; p0 = rows per BMTB) */
         return or_row_dir_tblock_blocking(s, p0 > 0 ? p0 : 1);
+    /* nnz-direction parents (p0 = nnz per BMW / BMTB, p1 = nnz per BMW inside the BMTBs),
+     * padded at the outer level, 32-nnz BMTs inside (relative indices), thread bitmaps of
+     * VW 32 (N >= 32) */
+    if (!strcmp(name, "nnz_warp_bitmap")) {
+        if (or_nnz_dir_warp_blocking(s, (uint64_t)p0, 0, 0, 1)) return -1;
+        if (or_nnz_dir_thread_in_parent(s, 32, 1, 1)) return -1;
+        return or_thread_bit_map_operator(s, 0, 32);
+    }
+    if (!strcmp(name, "nnz_tblock_bitmap")) {
+        if (or_nnz_dir_tblock_blocking(s, (uint64_t)p0, 1)) return -1;
+        if (or_nnz_dir_thread_in_parent(s, 32, 1, 1)) return -1;
+        return or_thread_bit_map_operator(s, 0, 32);
+    }
+    if (!strcmp(name, "nnz_tblock_warp_bitmap")) {
+        if (or_nnz_dir_tblock_blocking(s, (uint64_t)p0, 1)) return -1;
+        if (or_nnz_dir_warp_blocking(s, (uint64_t)p1, 1, 1, 0)) return -1;
+        if (or_nnz_dir_thread_in_parent(s, 32, 1, 1)) return -1;
+        return or_thread_bit_map_operator(s, 0, 32);
+    }
     if (!strcmp(name, "thread_bit_map")) { /* token_test.cc:1319-1391, p0 = VW */
         if (or_nnz_dir_thread_blocking(s, 32, 1)) return -1;
         return or_thread_bit_map_operator(s, 0, p0);

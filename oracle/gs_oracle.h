@@ -80,6 +80,9 @@ int or_row_dir_thread_blocking(or_set *s, int rb, int col_pad_size);       /* A5
 int or_row_dir_tblock_blocking(or_set *s, int rb);                         /* A8 */
 int or_row_dir_warp_blocking(or_set *s, int rb);                           /* BMW */
 int or_nnz_dir_thread_blocking(or_set *s, int nnz_per_bmt, int pad);       /* A9 */
+int or_nnz_dir_tblock_blocking(or_set *s, uint64_t nnz_per_bmtb, int pad); /* nnz-direction BMTBs */
+int or_nnz_dir_warp_blocking(or_set *s, uint64_t nnz_per_bmw, int rrel, int nrel, int pad); /* nnz BMWs */
+int or_nnz_dir_thread_in_parent(or_set *s, uint64_t nnz_per_bmt, int rrel, int nrel); /* BMTs in them */
 int or_thread_bit_map_operator(or_set *s, int pos_is_warp, int size);      /* A9 */
 int or_warp_segment_operator(or_set *s, int vw);                           /* A9 */
 int or_balanced_row_dir_warp_blocking(or_set *s, uint64_t nnz_per_bmw);    /* A11 */
