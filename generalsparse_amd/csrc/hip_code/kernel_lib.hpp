@@ -658,6 +658,21 @@ __global__ __launch_bounds__(256) void k_row_chunks(const uint32_t *__restrict__
 // rows listed (shared between BMTs, or empty): C = fp16(workspace), workspace
 // re-zeroed for the next launch (companion of k_bitmap_segment with ws and of
 // k_row_chunks)
+// parent-indexed sub-matrices (row_nz_matrix_div_operator): C row r of the divided range is
+// the sum, in sub-matrix order, of row r of every scratch output that has a row r
+template <class VT>
+__global__ __launch_bounds__(256) void k_combine_parts(const VT *const *__restrict__ parts,
+                                                       const uint32_t *__restrict__ rows, uint32_t n,
+                                                       VT *__restrict__ C, uint64_t total, uint32_t N) {
+    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (uint64_t)gridDim.x * 256) {
+        const uint64_t r = e / N;
+        float s = 0.f;
+        for (uint32_t q = 0; q < n; q++)
+            if (r < rows[q]) s += (float)parts[q][e];
+        C[e] = (VT)s;
+    }
+}
+
 template <class VT>
 __global__ __launch_bounds__(256) void k_finalize_rows(const uint32_t *__restrict__ rows, uint32_t n_rows,
                                                        float *__restrict__ ws, VT *__restrict__ C, uint32_t N) {

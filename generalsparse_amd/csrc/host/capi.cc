@@ -12,10 +12,25 @@
 // (fixed_interval_row_matrix_div_operator, §8f rank 3) adds sub-matrices, each with its
 // own code generator / kernel / device arrays over the shared metadata set and operator
 // history, run one after another by the multi-kernel executor (gs_spmm)
+// Sub-matrices of row_nz_matrix_div_operator keep the divided sub-matrix's row indexing
+// and a row can straddle two of them: each runs into a zeroed scratch output, and
+// gs::combine_parts sums the scratch outputs into C's rows [base, base + rows).
+struct parent_group {
+    uint64_t base = 0, rows = 0;
+    std::vector<gs::plan_state *> subs;
+    std::vector<void *> bufs;  // one scratch output per sub-matrix (rows_of(sub) x N)
+    std::vector<uint32_t> part_rows;
+    void **ptrs_dev = nullptr;
+    uint32_t *rows_dev = nullptr;
+    uint32_t N = 0;  // dense width the scratch outputs are sized for
+    int device = 0;
+};
+
 struct gs_plan {
     gs::plan_state st;
     std::map<int, std::unique_ptr<gs::plan_state>> subs;
     std::vector<std::pair<uint64_t, uint64_t>> gaps;  // output rows no sub-matrix writes
+    std::vector<parent_group> groups;
 };
 
 namespace {
@@ -83,19 +98,65 @@ std::vector<gs::plan_state *> kernel_states(gs_plan *p, bool strict = true) {
 
 bool divided(gs_plan *p) { return !p->subs.empty() || !sub_live(*p->st.meta, 0); }
 
+#define GS_HIP(x) GS_CHECK((x) == hipSuccess, #x " failed")
+
+void free_group(parent_group &g) {
+    if (!g.bufs.empty() || g.ptrs_dev) (void)hipSetDevice(g.device);
+    for (void *b : g.bufs) (void)hipFree(b);
+    if (g.ptrs_dev) (void)hipFree(g.ptrs_dev);
+    if (g.rows_dev) (void)hipFree(g.rows_dev);
+    g.bufs.clear();
+    g.ptrs_dev = nullptr;
+    g.rows_dev = nullptr;
+    g.N = 0;
+}
+
+void free_groups(gs_plan *p) {
+    for (auto &g : p->groups) free_group(g);
+    p->groups.clear();
+}
+
+// scratch outputs for dense width N (allocated on first use, grown for a wider N)
+void ensure_scratch(parent_group &g, uint32_t N, size_t e) {
+    if (g.N >= N) return;
+    free_group(g);
+    GS_HIP(hipSetDevice(g.device));
+    for (size_t i = 0; i < g.subs.size(); i++) {
+        void *b = nullptr;
+        GS_HIP(hipMalloc(&b, std::max<size_t>(1, (size_t)g.part_rows[i] * N * e)));
+        g.bufs.push_back(b);
+    }
+    GS_HIP(hipMalloc((void **)&g.ptrs_dev, g.bufs.size() * sizeof(void *)));
+    GS_HIP(hipMemcpy(g.ptrs_dev, g.bufs.data(), g.bufs.size() * sizeof(void *), hipMemcpyHostToDevice));
+    GS_HIP(hipMalloc((void **)&g.rows_dev, g.part_rows.size() * sizeof(uint32_t)));
+    GS_HIP(hipMemcpy(g.rows_dev, g.part_rows.data(), g.part_rows.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    g.N = N;
+}
+
 // multi-kernel executor: zero the output rows of empty row intervals, then run each
-// sub-matrix's kernel on the same stream (each writes only its own rows)
+// sub-matrix's kernel on the same stream (each writes only its own rows); parent-indexed
+// sub-matrices run into their scratch outputs, summed into C per divided range
 void spmm_all(gs_plan *p, int replica, const void *B, void *C, uint32_t N, hipStream_t stream) {
     if (!divided(p)) {
         gs::launch_spmm(p->st, replica, B, C, N, stream);
         return;
     }
     auto ks = kernel_states(p);
-    const size_t e = ks.front()->dev.dtype == 0 ? 4 : 2;
+    const int dtype = ks.front()->dev.dtype;
+    const size_t e = dtype == 0 ? 4 : 2;
     for (auto &g : p->gaps)
         if (g.second > g.first)
             gs::memset_rows(C, g.first, g.second, N, e, stream);
-    for (gs::plan_state *s : ks) gs::launch_spmm(*s, replica, B, C, N, stream);
+    for (gs::plan_state *s : ks)
+        if (s->parent_row_base < 0) gs::launch_spmm(*s, replica, B, C, N, stream);
+    for (auto &g : p->groups) {
+        ensure_scratch(g, N, e);
+        for (size_t i = 0; i < g.subs.size(); i++) {
+            gs::memset_rows(g.bufs[i], 0, g.part_rows[i], N, e, stream);
+            gs::launch_spmm(*g.subs[i], replica, B, g.bufs[i], N, stream);
+        }
+        gs::combine_parts(g.ptrs_dev, g.rows_dev, (uint32_t)g.subs.size(), C, g.base, g.rows, N, dtype, stream);
+    }
 }
 
 }  // namespace
@@ -408,15 +469,41 @@ int gs_plan_compile(gs_plan_t *p) {
     return guard([&] {
         GS_CHECK(p, "null plan");
         const auto &m = *p->st.meta;
+        // sub-matrices of row_nz_matrix_div_operator keep the divided sub-matrix's row
+        // indexing (div_row_indices_by_row_nnz.cc): their rows refer to its row range; a
+        // fixed-interval division of such a sub-matrix has no row range to write to
+        std::map<int, std::pair<uint64_t, uint64_t>> pidx;
+        std::map<int, bool> unexec;
+        for (auto &o : p->st.exec->get_operator_context()->read_operator_context_arr(gs::CONVERTING_OP, 0)) {
+            const int t = o->get_target_matrix_id();
+            if (auto *r = dynamic_cast<gs::row_nz_matrix_div_operator *>(o.get())) {
+                const auto range = pidx.count(t) ? pidx[t] : std::make_pair(r->parent_row_base, r->parent_rows);
+                for (int id : r->new_sub_matrix_ids) {
+                    pidx[id] = range;
+                    if (unexec.count(t)) unexec[id] = true;
+                }
+            } else if (auto *f = dynamic_cast<gs::fixed_interval_row_matrix_div_operator *>(o.get())) {
+                if (pidx.count(t) || unexec.count(t))
+                    for (int id : f->new_sub_matrix_ids) unexec[id] = true;
+            }
+        }
         for (gs::plan_state *s : kernel_states(p)) {
-            // a kernel writes C row begin_row_index + r: every row must lie inside its
-            // sub-matrix (row_nz_matrix_div_operator leaves them in the parent's indexing)
             const int sb = s->cg->get_sub_matrix_id();
+            GS_CHECK(!unexec.count(sb), "sub-matrix " + std::to_string(sb) + ": a fixed-interval division of a row_nz "
+                     "sub-matrix (rows in its parent's indexing) -- plan only, not executable");
             const uint64_t b = m.scalar(gs::GLOBAL_META, "begin_row_index", sb), e = m.scalar(gs::GLOBAL_META, "end_row_index", sb);
             const auto &r = m.u(gs::GLOBAL_META, "nz_row_indices", sb);
-            GS_CHECK(r.empty() || b + r.back() <= e,
-                     "sub-matrix " + std::to_string(sb) + ": row indices lie past its end_row_index (rows left in the "
-                     "parent's indexing, div_row_indices_by_row_nnz.cc) -- plan only, not executable");
+            auto it = pidx.find(sb);
+            if (it != pidx.end()) {
+                s->parent_row_base = (int64_t)it->second.first;
+                s->parent_rows = it->second.second;
+                GS_CHECK(r.empty() || r.back() < s->parent_rows, "sub-matrix " + std::to_string(sb) +
+                         ": row indices lie past the divided sub-matrix's rows");
+            } else {
+                // a kernel writes C row begin_row_index + r: every row inside the sub-matrix
+                GS_CHECK(r.empty() || b + r.back() <= e,
+                         "sub-matrix " + std::to_string(sb) + ": row indices lie past its end_row_index");
+            }
             s->cg->compile();
         }
         // the reference asserts logical_check after every pipeline (token_test.cc:517-1541)
@@ -467,11 +554,31 @@ int gs_plan_upload(gs_plan_t *p, int dtype, int device) {
         GS_CHECK(p, "null plan");
         auto ks = kernel_states(p);
         for (gs::plan_state *s : ks) gs::upload_plan(*s, dtype, device);
+        // parent-indexed sub-matrices, grouped by the row range they refer to
+        free_groups(p);
+        for (gs::plan_state *s : ks) {
+            if (s->parent_row_base < 0) continue;
+            auto g = std::find_if(p->groups.begin(), p->groups.end(), [&](const parent_group &x) {
+                return x.base == (uint64_t)s->parent_row_base && x.rows == s->parent_rows;
+            });
+            if (g == p->groups.end()) {
+                p->groups.emplace_back();
+                g = p->groups.end() - 1;
+                g->base = (uint64_t)s->parent_row_base;
+                g->rows = s->parent_rows;
+                g->device = device;
+            }
+            GS_CHECK(s->dev.n_out_rows <= g->rows && g->base + g->rows <= s->M, "parent-indexed sub-matrix outside its range");
+            g->subs.push_back(s);
+            g->part_rows.push_back((uint32_t)s->dev.n_out_rows);
+        }
         // rows of C no sub-matrix owns (intervals without nonzeros): zeroed by the executor
         p->gaps.clear();
         if (divided(p)) {
             std::vector<std::pair<uint64_t, uint64_t>> own;
-            for (gs::plan_state *s : ks) own.push_back({s->dev.out_lo, s->dev.n_out_rows});
+            for (gs::plan_state *s : ks)
+                if (s->parent_row_base < 0) own.push_back({s->dev.out_lo, s->dev.n_out_rows});
+            for (auto &g : p->groups) own.push_back({g.base, g.base + g.rows});
             std::sort(own.begin(), own.end());
             uint64_t at = 0;
             for (auto &o : own) {
@@ -666,15 +773,17 @@ int gs_plan_load(const char *path, gs_plan_t **out) {
         GS_CHECK(path && out, "null argument");
         auto *p = new gs_plan;
         try {
-            std::vector<std::pair<int, gs::kernel_spec>> specs;
+            std::vector<gs::loaded_kernel> specs;
             std::string pipeline;
             auto m = gs::load_plan(path, specs, pipeline);
             init_plan(p->st, m);
             p->st.pipeline = pipeline;
             for (auto &ks : specs) {
-                gs::plan_state &st = state_of(p, ks.first);
+                gs::plan_state &st = state_of(p, ks.sub);
                 st.pipeline = pipeline;
-                st.cg->restore_compiled(ks.second);
+                st.parent_row_base = ks.parent_row_base;
+                st.parent_rows = ks.parent_rows;
+                st.cg->restore_compiled(ks.spec);
             }
         } catch (...) {
             delete p;
@@ -705,6 +814,7 @@ int gs_plan_from_mtx(const char *path, const gs_opts *opts, gs_plan_t **out) {
 void gs_plan_free(gs_plan_t *p) {
     if (!p) return;
     try {
+        free_groups(p);
         gs::free_device(p->st);
         for (auto &kv : p->subs) gs::free_device(*kv.second);
     } catch (...) {

@@ -68,13 +68,25 @@ struct plan_state {
     uint64_t M = 0, K = 0, nnz = 0;
     device_plan dev;
     bool uploaded = false;
+    // a sub-matrix of row_nz_matrix_div_operator: its row indices refer to the divided
+    // sub-matrix (rows [parent_row_base, parent_row_base + parent_rows) of C); -1 otherwise
+    int64_t parent_row_base = -1;
+    uint64_t parent_rows = 0;
+};
+
+// a kernel of a plan file: sub-matrix id, kernel spec, parent-indexed row range
+struct loaded_kernel {
+    int sub = 0;
+    kernel_spec spec;
+    int64_t parent_row_base = -1;
+    uint64_t parent_rows = 0;
 };
 
 // plan_io.cc: binary plan files
 // one file holds every kernel of a plan (one per sub-matrix of a row division); load
 // returns the metadata set and the (sub-matrix id, kernel spec) list
 void save_plan(const std::vector<const plan_state *> &kernels, const std::string &path);
-std::shared_ptr<meta_data_set> load_plan(const std::string &path, std::vector<std::pair<int, kernel_spec>> &specs,
+std::shared_ptr<meta_data_set> load_plan(const std::string &path, std::vector<loaded_kernel> &kernels,
                                          std::string &pipeline);
 
 // device_plan.hip
@@ -83,6 +95,10 @@ void add_replica(plan_state &p);
 void free_device(plan_state &p);
 // zero rows [lo, hi) of a row-major C of width N, element size e (sub-matrix executor)
 void memset_rows(void *C, uint64_t lo, uint64_t hi, uint32_t N, size_t e, hipStream_t stream);
+// C[row0 + r] = sum of parts[q][r] over the q with r < rows[q], r < P (parent-indexed
+// sub-matrices' scratch outputs; parts / rows are device arrays of n entries)
+void combine_parts(const void *const *parts, const uint32_t *rows, uint32_t n, void *C, uint64_t row0, uint64_t P,
+                   uint32_t N, int dtype, hipStream_t stream);
 void launch_spmm(plan_state &p, int replica, const void *B, void *C, uint32_t N, hipStream_t stream);
 // uploads the CSR arrays a matrix-core plan deferred (every replica), for a launch at another dense width
 void ensure_csr(plan_state &p);

@@ -286,6 +286,10 @@ void row_nz_matrix_div_operator::run(bool check) {
     if (check) GS_CHECK(is_valid_according_to_metadata(), "row-length division: invalid metadata");
     const row_nz_window w{(uint64_t)init_row_size_upper_boundary, (uint64_t)max_row_size_upper_boundary,
                           (uint64_t)expansion_rate};
+    auto &m = *meta_data_set_ptr;
+    parent_row_base = m.scalar(GLOBAL_META, "begin_row_index", target_matrix_id);
+    parent_rows = row_num_of_sub_matrix(m, target_matrix_id);
+    const int first = m.get_max_sub_matrix_id_of_data_item(GLOBAL_META, "nz_row_indices") + 1;
     modify_row_start_boundary_after_div_according_to_row_nz a(meta_data_set_ptr, target_matrix_id, w);
     run_step(a, check);
     modify_row_end_boundary_after_div_according_to_row_nz b(meta_data_set_ptr, target_matrix_id, w);
@@ -300,6 +304,9 @@ void row_nz_matrix_div_operator::run(bool check) {
     run_step(f, check);
     div_row_indices_by_row_nnz g(meta_data_set_ptr, target_matrix_id, w);
     run_step(g, check);
+    const int last = m.get_max_sub_matrix_id_of_data_item(GLOBAL_META, "nz_row_indices");
+    new_sub_matrix_ids.clear();
+    for (int k = first; k <= last; k++) new_sub_matrix_ids.push_back(k);
     is_run = true;
 }
 

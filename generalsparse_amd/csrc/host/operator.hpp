@@ -101,8 +101,9 @@ class fixed_interval_row_matrix_div_operator : public basic_operator {
 // into row ranges of similar row length (windows from init_row_size_upper_boundary growing by
 // expansion_rate up to max_row_size_upper_boundary).  Restated with the reference's
 // quirks: every range gets boundaries, only ranges that receive entries get arrays, the
-// entries move on one range at a time, and row indices keep the parent's indexing
-// (such sub-matrices are planned, not executed: gs_plan_compile refuses them).
+// entries move on one range at a time, and row indices keep the parent's indexing.  The
+// executor runs such "parent-indexed" sub-matrices into scratch outputs in the parent's
+// row indexing and sums them into C (a row can straddle two of them; capi.cc spmm_all).
 class row_nz_matrix_div_operator : public basic_operator {
   public:
     row_nz_matrix_div_operator(cg_ptr cg, int init_row_size_upper_boundary, int max_row_size_upper_boundary,
@@ -111,6 +112,10 @@ class row_nz_matrix_div_operator : public basic_operator {
     bool is_valid_according_to_metadata() override;
     bool is_valid_according_to_operator(ctx_ptr h) override;
     int init_row_size_upper_boundary, max_row_size_upper_boundary, expansion_rate;
+    // filled by run(): the sub-matrices that received arrays, and the row range of the
+    // divided sub-matrix their row indices refer to (its begin_row_index and row count)
+    std::vector<int> new_sub_matrix_ids;
+    uint64_t parent_row_base = 0, parent_rows = 0;
 };
 
 // -------------------------------------------------------------- DISTRIBUTING

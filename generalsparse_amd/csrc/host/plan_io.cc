@@ -4,7 +4,9 @@
 // endian: "GSPLAN02", the number of kernels, per kernel its sub-matrix id and the kernel
 // spec the code generator selected (one per sub-matrix of a row division, §8f rank 3),
 // the pipeline and matrix names, then every metadata array as (pos, name, sub, is_float,
-// data_type, len, payload u64/f64).  "GSPLAN01" files (one kernel, sub-matrix 0) still load.
+// data_type, len, payload u64/f64).  "GSPLAN03" adds, per kernel after its sub-matrix id,
+// the parent-indexed row range of a row_nz_matrix_div_operator sub-matrix (base, rows; -1
+// otherwise).  "GSPLAN02" and "GSPLAN01" files (one kernel, sub-matrix 0) still load.
 #include "gs_plan.hpp"
 
 #include <cstdio>
@@ -38,6 +40,7 @@ struct reader {
 
 const char kMagic1[8] = {'G', 'S', 'P', 'L', 'A', 'N', '0', '1'};
 const char kMagic2[8] = {'G', 'S', 'P', 'L', 'A', 'N', '0', '2'};
+const char kMagic3[8] = {'G', 'S', 'P', 'L', 'A', 'N', '0', '3'};
 
 void write_spec(writer &w, const kernel_spec &s) {
     w.i64(s.family); w.i64(s.coarsen_factor); w.i64(s.sparse_coarsen_factor); w.i64(s.vector_width);
@@ -72,10 +75,12 @@ void save_plan(const std::vector<const plan_state *> &ks, const std::string &pat
     GS_CHECK(f, "cannot write " + path);
     writer w{f};
     try {
-        w.raw(kMagic2, 8);
+        w.raw(kMagic3, 8);
         w.u64(ks.size());
         for (auto *k : ks) {
             w.i64(k->cg->get_sub_matrix_id());
+            w.i64(k->parent_row_base);
+            w.u64(k->parent_rows);
             write_spec(w, k->cg->get_kernel_spec());
         }
         w.str(p.pipeline);
@@ -102,7 +107,7 @@ void save_plan(const std::vector<const plan_state *> &ks, const std::string &pat
     GS_CHECK(std::fclose(f) == 0, "plan file: close failed");
 }
 
-std::shared_ptr<meta_data_set> load_plan(const std::string &path, std::vector<std::pair<int, kernel_spec>> &specs,
+std::shared_ptr<meta_data_set> load_plan(const std::string &path, std::vector<loaded_kernel> &specs,
                                          std::string &pipeline) {
     FILE *f = std::fopen(path.c_str(), "rb");
     GS_CHECK(f, "cannot read " + path);
@@ -111,14 +116,20 @@ std::shared_ptr<meta_data_set> load_plan(const std::string &path, std::vector<st
     try {
         char mg[8];
         r.raw(mg, 8);
-        const bool v1 = std::memcmp(mg, kMagic1, 8) == 0;
-        GS_CHECK(v1 || std::memcmp(mg, kMagic2, 8) == 0, "not a generalsparse_amd plan file: " + path);
+        const bool v1 = std::memcmp(mg, kMagic1, 8) == 0, v3 = std::memcmp(mg, kMagic3, 8) == 0;
+        GS_CHECK(v1 || v3 || std::memcmp(mg, kMagic2, 8) == 0, "not a generalsparse_amd plan file: " + path);
         specs.clear();
         const uint64_t nk = v1 ? 1 : r.u64();
         GS_CHECK(nk >= 1 && nk < 4096, "plan file: bad kernel count");
         for (uint64_t i = 0; i < nk; i++) {
-            const int sub = v1 ? 0 : (int)r.i64();
-            specs.emplace_back(sub, read_spec(r));
+            loaded_kernel k;
+            k.sub = v1 ? 0 : (int)r.i64();
+            if (v3) {
+                k.parent_row_base = r.i64();
+                k.parent_rows = r.u64();
+            }
+            k.spec = read_spec(r);
+            specs.push_back(std::move(k));
         }
         pipeline = r.str();
         m = std::make_shared<meta_data_set>();
@@ -143,7 +154,7 @@ std::shared_ptr<meta_data_set> load_plan(const std::string &path, std::vector<st
             }
         }
         for (auto &ks : specs)
-            for (auto &a : ks.second.arrays) GS_CHECK(m->is_exist(a), "plan file lacks kernel array " + a);
+            for (auto &a : ks.spec.arrays) GS_CHECK(m->is_exist(a), "plan file lacks kernel array " + a);
     } catch (...) {
         std::fclose(f);
         throw;

@@ -651,10 +651,13 @@ void upload_plan(plan_state &p, int dtype, int device) {
     d = device_plan();
     d.device = device;
     d.dtype = dtype;
-    d.row_base = m.scalar(GLOBAL_META, "begin_row_index", sb);
+    // a parent-indexed sub-matrix (row_nz_matrix_div_operator) writes a scratch output whose
+    // row r is its row index r (capi.cc combines the scratch outputs into C)
+    const bool pidx = p.parent_row_base >= 0;
+    d.row_base = pidx ? 0 : m.scalar(GLOBAL_META, "begin_row_index", sb);
     // output rows this plan writes: all of C for the undivided matrix; a sub-matrix of a
     // row division (§8f rank 3) owns [begin_row_index, begin_row_index + its rows) only
-    const uint64_t out_lo = sb == 0 ? 0 : d.row_base;
+    const uint64_t out_lo = sb == 0 || pidx ? 0 : d.row_base;
     const uint64_t out_hi = sb == 0 ? p.M : d.row_base + row_num_of_sub_matrix(m, sb);
     d.n_out_rows = out_hi;
     d.out_lo = out_lo;
@@ -1042,6 +1045,21 @@ void add_replica(plan_state &p) {
 
 void memset_rows(void *C, uint64_t lo, uint64_t hi, uint32_t N, size_t e, hipStream_t stream) {
     HIP_OK(hipMemsetAsync((char *)C + lo * N * e, 0, (hi - lo) * N * e, stream));
+}
+
+void combine_parts(const void *const *parts, const uint32_t *rows, uint32_t n, void *C, uint64_t row0, uint64_t P,
+                   uint32_t N, int dtype, hipStream_t stream) {
+    GS_CHECK(P * N < (1ull << 40) && n > 0, "combine_parts: bad sizes");
+    const uint64_t total = P * N;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((total + 255) / 256, 4096);
+    if (blocks == 0) return;
+    if (dtype == 0)
+        hipLaunchKernelGGL(gsk::k_combine_parts<float>, dim3(blocks), dim3(256), 0, stream,
+                           (const float *const *)parts, rows, n, (float *)C + row0 * N, total, N);
+    else
+        hipLaunchKernelGGL(gsk::k_combine_parts<gsk::f16>, dim3(blocks), dim3(256), 0, stream,
+                           (const gsk::f16 *const *)parts, rows, n, (gsk::f16 *)C + row0 * N, total, N);
+    HIP_OK(hipGetLastError());
 }
 
 void free_device(plan_state &p) {

@@ -221,11 +221,35 @@ def test_row_nz_division_hand_case():
     assert a["GLOBAL_META_nz_row_indices_2"].tolist() == [4]
     assert a["GLOBAL_META_nz_row_indices_3"].tolist() == [4] * 4 + [5] * 5
     assert a["GLOBAL_META_nz_vals_2"].tolist() == [11.0]
-    # rows stay in the parent's indexing: planned, not executed
+    # rows stay in the parent's indexing: the sub-matrices compile as parent-indexed
+    # (scratch outputs summed by the executor; GPU parity in test_gpu_row_nz.py)
     for s in p.sub_matrices():
         p.run_pipeline("warp_total", 32, 0, 1, sub=s)
+    p.compile()
+    # the sort-based pipelines fail like the reference's row-count assert
+    # (reorder_val_by_index.cc:42: end_row_index - begin_row_index + 1 rows expected)
+    q = check_row_nz_division(6, 5, r, c, v, 4, 64)
+    with pytest.raises(gsa.GsError, match="row count"):
+        q.run_pipeline("thread_total", 8, 4, 1, sub=3)
+
+
+def test_row_nz_then_fixed_division_refused():
+    # a fixed-interval division of a row_nz sub-matrix (rows in its parent's indexing) has
+    # no row range to write to: compile refuses it
+    r = np.repeat(np.array([0, 1, 4, 5], np.uint64), 5)
+    c = np.tile(np.arange(5, dtype=np.uint64), 4)
+    v = np.arange(1, 21, dtype=np.float32)
+    p = gsa.Plan.from_coo(6, 5, r, c, v)
+    p.add_operator("row_nz_matrix_div_operator", 4, 64, 2)
+    try:
+        subs = p.divide_rows(1, sub=3)
+    except gsa.GsError:
+        return  # the division itself may be invalid on such a sub-matrix
+    for s in p.sub_matrices():
+        p.run_pipeline("warp_total", 8, 0, 1, sub=s)
     with pytest.raises(gsa.GsError, match="not executable"):
         p.compile()
+    assert subs
 
 
 @pytest.mark.parametrize("seed", range(4))
