@@ -312,6 +312,43 @@ void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1)
         ex.add_and_run(std::make_shared<warp_total_reduce_operator>(cg, cf, ctx));
         ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)((rows + rb - 1) / rb),
                                                              std::vector<unsigned>{64u, 4u}, cf, ctx));
+    } else if (name == "col_warp_total" || name == "col_tblock_total" || name == "tblock_col_warp_total") {
+        // col-direction parents (fixed_interval_col_direction_{warp,tblock}_blocking_operator): BMWs /
+        // BMTBs of p0 nonzeros of one row (tblock_col_warp_total: BMWs of p1 nonzeros inside
+        // row-direction BMTBs of p0 rows, indices relative to the BMTB too), total-reduced
+        const int cf = 1;
+        if (name == "col_tblock_total") {
+            ex.add_and_run(std::make_shared<fixed_interval_col_direction_tblock_blocking_operator>(cg, p0 > 0 ? p0 : 256, false,
+                                                                                                   false, ctx));
+            ex.add_and_run(std::make_shared<tblock_total_reduce_operator>(cg, cf, ctx));
+        } else {
+            int c = p0 > 0 ? p0 : 64;
+            if (name == "tblock_col_warp_total") {
+                ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, p0 > 0 ? p0 : 16,
+                                                                                                       false, ctx));
+                c = p1 > 0 ? p1 : 64;
+            }
+            const bool rel = name == "tblock_col_warp_total";
+            ex.add_and_run(std::make_shared<fixed_interval_col_direction_warp_blocking_operator>(cg, c, rel, rel, false, false, ctx));
+            ex.add_and_run(std::make_shared<warp_total_reduce_operator>(cg, cf, ctx));
+        }
+        const uint64_t units = s.meta->u(name == "col_tblock_total" ? TBLOCK_META : WARP_META, "first_nz_indices", sb).size() - 1;
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)std::max<uint64_t>(1, units),
+                                                             std::vector<unsigned>{64u, 4u}, cf, ctx));
+    } else if (name == "tblock_col_thread_total" || name == "warp_col_thread_total" || name == "tblock_col_thread_total_padded") {
+        // col-direction BMTs of p1 nonzeros inside row-direction BMTBs (or BMWs) of p0 rows, row and
+        // nz indices relative to the parent; _padded pads every row to a multiple of p1 first
+        // (the parent level is rebuilt on the padded COO: the operator re-runs the former ones)
+        const int rb = p0 > 0 ? p0 : 16, c = p1 > 0 ? p1 : 32, cf = 1;
+        if (name == "warp_col_thread_total")
+            ex.add_and_run(std::make_shared<fixed_interval_row_direction_warp_blocking_operator>(cg, rb, false, false, false, ctx));
+        else
+            ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, rb, false, ctx));
+        ex.add_and_run(std::make_shared<fixed_interval_col_direction_thread_blocking_operator>(
+            cg, c, true, true, name == "tblock_col_thread_total_padded", false, ctx));
+        ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, false, 1, cf, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)((rows + rb - 1) / rb),
+                                                             std::vector<unsigned>{64u, 4u}, cf, ctx));
     } else if (name == "tblock_thread_total" || name == "tblock_warp_thread_total") {
         // §8f rank 1: BMTs of p1 rows inside BMTBs of p0 rows (and inside BMWs of 8 rows),
         // row and nz indices relative to the parent as well

@@ -144,6 +144,19 @@ void code_generator::compile() {
         s.row_sorted = m.is_exist(GLOBAL_META, "original_nz_row_indices", sub);
         s.arrays = {"THREAD_META_first_nz_indices_0", "THREAD_META_first_row_indices_0"};
         if (s.row_sorted) s.arrays.push_back("GLOBAL_META_original_nz_row_indices_0");
+    } else if ((tw && tw->kind == reduction_kind::TOTAL_WARP_RESULT &&
+                m.is_exist(WARP_META, "first_row_indices_without_ending", sub)) ||
+               (tb && tb->kind == reduction_kind::TOTAL_BLOCK_RESULT && !tw &&
+                m.is_exist(TBLOCK_META, "first_row_indices_without_ending", sub))) {
+        // col-direction BMWs / BMTBs (fixed_interval_col_direction_{warp,tblock}_blocking_operator):
+        // chunks of one row, so a row's chunks are summed across units -> the row-chunk kernel
+        // over that level's chunks.  The reference's total-reduce tokens read first_row_indices,
+        // which these levels do not have (total_warp_result_reduce_to_one_register_token.cc:661)
+        const bool w = tw && tw->kind == reduction_kind::TOTAL_WARP_RESULT;
+        const std::string L = w ? "WARP_META" : "TBLOCK_META";
+        s.family = KF_ROW_CHUNKS;
+        s.coarsen_factor = w ? tw->coarsen_factor : tb->coarsen_factor;
+        s.arrays = {L + "_first_nz_indices_0", L + "_first_row_indices_without_ending_0"};
     } else if (tw && tw->kind == reduction_kind::TOTAL_WARP_RESULT) {
         s.family = KF_WARP_TOTAL;
         s.coarsen_factor = tw->coarsen_factor;
@@ -297,10 +310,12 @@ std::string code_generator::generate_kernel_file_source(int repeat) const {
                      "4 * (64 / X) * 2 * X * CF * sizeof(float)>>>(d_a0, F0, d_a1, F1, d_m0, d_a2, d_a3, d_col, d_val, d_B, d_C, n_units, N, X, 0, "
                      "(float *)nullptr)";  // no workspace: open rows by atomics into the zeroed C
             break;
-        case KF_ROW_CHUNKS:
-            decl("F0", fml("THREAD_META_first_nz_indices_0"));
-            decl("F1", fml("THREAD_META_first_row_indices_without_ending_0"));
-            o << "    auto fn = rd(\"THREAD_META_first_nz_indices_0\"), fr = rd(\"THREAD_META_first_row_indices_without_ending_0\");\n"
+        case KF_ROW_CHUNKS: {
+            // the chunk level: THREAD (col-direction BMTs) or a col-direction WARP / TBLOCK level
+            const std::string L = spec.arrays[0].substr(0, spec.arrays[0].find("_META_") + 5);
+            decl("F0", fml(L + "_first_nz_indices_0"));
+            decl("F1", fml(L + "_first_row_indices_without_ending_0"));
+            o << "    auto fn = rd(\"" << L << "_first_nz_indices_0\"), fr = rd(\"" << L << "_first_row_indices_without_ending_0\");\n"
               << "    uint32_t *d_a0 = F0.kind ? nullptr : up(u32(fn)), *d_a1 = F1.kind ? nullptr : up(u32(fr));\n"
               << "    const uint32_t n_units = fn.size() - 1, U = gsk_host::row_chunk_span(n_units); const bool al = true;\n"
               << "    auto fin = gsk_host::row_chunk_finalize_rows(u32(fr), M, U, 0); uint32_t *d_a4 = up(fin);\n"
@@ -310,6 +325,7 @@ std::string code_generator::generate_kernel_file_source(int repeat) const {
                      "if (!fin.empty()) gsk::k_finalize_rows<VT><<<dim3((fin.size() * N + 255) / 256), 256>>>("
                      "d_a4, (uint32_t)fin.size(), d_ws, d_C, N)";
             break;
+        }
         case KF_MERGE_PATH: {
             const std::string L = convert_pos_type_to_string(spec.merge_level);
             o << "    auto lr = rd(\"" << L << "_first_row_indices_without_ending_0\"), ln = rd(\"" << L

@@ -384,6 +384,124 @@ void get_begin_nzs_of_BMT_after_fixed_blocking_in_col_direction::run(bool check)
     is_run = true;
 }
 
+// ------------------------------------------- col-direction units (A10 and its parents)
+namespace {
+// the nnz of every row of the sub-matrix (rows up to the real end row)
+std::vector<uint64_t> col_row_counts(const meta_data_set &m, int s) {
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    GS_CHECK(!m.is_exist(GLOBAL_META, "nz_row_indices_after_interlance_storage", s),
+             "col-direction blocking after interleaved storage");
+    const uint64_t row_num = row_num_of_sub_matrix(m, s);
+    return get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+}
+// get_begin_rows_of_<unit>_after_fixed_blocking_in_col_direction.cc:75-100: one entry (the
+// row) per chunk of c nonzeros of that row; empty rows get none; no ending
+std::vector<uint64_t> col_unit_rows(const std::vector<uint64_t> &cnt, uint64_t c) {
+    std::vector<uint64_t> fr;
+    for (uint64_t i = 0; i < cnt.size(); i++)
+        for (uint64_t k = (cnt[i] + c - 1) / c; k; k--) fr.push_back(i);
+    return fr;
+}
+// get_begin_nzs_of_<unit>_after_fixed_blocking_in_col_direction.cc:75-105: chunk starts, a
+// row's last chunk holding its remainder, closed by nnz
+std::vector<uint64_t> col_unit_nzs(const std::vector<uint64_t> &cnt, uint64_t c) {
+    std::vector<uint64_t> fn{0};
+    for (uint64_t n : cnt)
+        for (uint64_t left = n; left > 0;) {
+            const uint64_t t = std::min(left, c);
+            fn.push_back(fn.back() + t);
+            left -= t;
+        }
+    return fn;
+}
+// *_relative_to_{BMTB,BMW}.cc / *_relative_to_parents.cc: the chunks of each row-direction
+// parent block, rows minus the parent's first row (rows = true) or nz starts counted from
+// the parent's first nonzero (a 0 pushed per parent, the parent's closing offset popped)
+std::vector<uint64_t> col_unit_relative(const meta_data_set &m, int s, POS_TYPE parent, uint64_t c, bool rows) {
+    const auto cnt = col_row_counts(m, s);
+    const auto &pr = m.u(parent, "first_row_indices", s);
+    GS_CHECK(pr.size() >= 2 && pr.back() <= cnt.size(), "relative col-direction units need row-direction parents");
+    std::vector<uint64_t> out;
+    for (size_t p = 0; p + 1 < pr.size(); p++) {
+        uint64_t off = 0;
+        for (uint64_t r = pr[p]; r < pr[p + 1]; r++)
+            for (uint64_t left = cnt[r]; left > 0;) {
+                const uint64_t t = std::min(left, c);
+                out.push_back(rows ? r - pr[p] : off);
+                off += t;
+                left -= t;
+            }
+    }
+    return out;
+}
+}  // namespace
+
+void get_begin_rows_of_BMW_after_fixed_blocking_in_col_direction::run(bool check) {
+    GS_CHECK(col_size > 0, "col_size > 0");
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(WARP_META, "first_row_indices_without_ending",
+              col_unit_rows(col_row_counts(*meta_data_set_ptr, target_matrix_id), (uint64_t)col_size));
+    is_run = true;
+}
+void get_begin_nzs_of_BMW_after_fixed_blocking_in_col_direction::run(bool check) {
+    GS_CHECK(col_size > 0, "col_size > 0");
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(WARP_META, "first_nz_indices", col_unit_nzs(col_row_counts(*meta_data_set_ptr, target_matrix_id), (uint64_t)col_size));
+    is_run = true;
+}
+void get_begin_rows_of_BMTB_after_fixed_blocking_in_col_direction::run(bool check) {
+    GS_CHECK(col_size > 0, "col_size > 0");
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(TBLOCK_META, "first_row_indices_without_ending",
+              col_unit_rows(col_row_counts(*meta_data_set_ptr, target_matrix_id), (uint64_t)col_size));
+    is_run = true;
+}
+void get_begin_nzs_of_BMTB_after_fixed_blocking_in_col_direction::run(bool check) {
+    GS_CHECK(col_size > 0, "col_size > 0");
+    src(GLOBAL_META, "nz_row_indices");
+    replace_u(TBLOCK_META, "first_nz_indices", col_unit_nzs(col_row_counts(*meta_data_set_ptr, target_matrix_id), (uint64_t)col_size));
+    is_run = true;
+}
+void get_begin_rows_of_BMW_after_fixed_blocking_in_col_direction_relative_to_BMTB::run(bool check) {
+    src(TBLOCK_META, "first_row_indices");
+    replace_u(WARP_META, "first_row_indices_relative_to_BMTB",
+              col_unit_relative(*meta_data_set_ptr, target_matrix_id, TBLOCK_META, (uint64_t)col_size, true));
+    is_run = true;
+}
+void get_begin_nzs_of_BMW_after_fixed_blocking_in_col_direction_relative_to_BMTB::run(bool check) {
+    src(TBLOCK_META, "first_row_indices");
+    replace_u(WARP_META, "first_nz_indices_relative_to_BMTB",
+              col_unit_relative(*meta_data_set_ptr, target_matrix_id, TBLOCK_META, (uint64_t)col_size, false));
+    is_run = true;
+}
+void get_begin_rows_of_BMT_after_fixed_blocking_in_col_direction_relative_to_BMTB::run(bool check) {
+    src(TBLOCK_META, "first_row_indices");
+    replace_u(THREAD_META, "first_row_indices_relative_to_BMTB",
+              col_unit_relative(*meta_data_set_ptr, target_matrix_id, TBLOCK_META, (uint64_t)col_size, true));
+    is_run = true;
+}
+void get_begin_rows_of_BMT_after_fixed_blocking_in_col_direction_relative_to_BMW::run(bool check) {
+    src(WARP_META, "first_row_indices");
+    replace_u(THREAD_META, "first_row_indices_relative_to_BMW",
+              col_unit_relative(*meta_data_set_ptr, target_matrix_id, WARP_META, (uint64_t)col_size, true));
+    is_run = true;
+}
+void get_begin_nzs_of_BMT_after_fixed_blocking_in_col_direction_relative_to_parents::run(bool check) {
+    GS_CHECK(parent_pos == TBLOCK_META || parent_pos == WARP_META, "relative BMT nz starts: TBLOCK or WARP parent");
+    src(parent_pos, "first_row_indices");
+    replace_u(THREAD_META, parent_pos == TBLOCK_META ? "first_nz_indices_relative_to_BMTB" : "first_nz_indices_relative_to_BMW",
+              col_unit_relative(*meta_data_set_ptr, target_matrix_id, parent_pos, (uint64_t)col_size, false));
+    is_run = true;
+}
+// remove_item_of_metadata.cc:20-40
+void remove_item_of_metadata::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    if (check) GS_CHECK(m.is_exist(pos, item_name, target_matrix_id), "remove_item_of_metadata: no item " + item_name);
+    src(pos, item_name.c_str());
+    m.remove_element(pos, item_name, target_matrix_id);
+    is_run = true;
+}
+
 namespace {
 std::vector<uint64_t> fixed_first_rows(uint64_t row_num, uint64_t rb) {
     std::vector<uint64_t> fr{0};

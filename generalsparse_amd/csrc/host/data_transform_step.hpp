@@ -114,6 +114,38 @@ GS_DECLARE_STEP_P(get_begin_BMTs_of_specific_parent_after_blocking, POS_TYPE, pa
 // fixed col-direction blocking (A10): every row cut into chunks of col_size nnz
 GS_DECLARE_STEP_P(get_begin_rows_of_BMT_after_fixed_blocking_in_col_direction, int, col_size)
 GS_DECLARE_STEP_P(get_begin_nzs_of_BMT_after_fixed_blocking_in_col_direction, int, col_size)
+// the same chunks as BMWs / BMTBs (fixed_interval_col_direction_{warp,tblock}_blocking_operator.cc):
+// rows without ending, nz starts with ending; relative variants restart per row-direction parent
+GS_DECLARE_STEP_P(get_begin_rows_of_BMW_after_fixed_blocking_in_col_direction, int, col_size)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMW_after_fixed_blocking_in_col_direction, int, col_size)
+GS_DECLARE_STEP_P(get_begin_rows_of_BMW_after_fixed_blocking_in_col_direction_relative_to_BMTB, int, col_size)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMW_after_fixed_blocking_in_col_direction_relative_to_BMTB, int, col_size)
+GS_DECLARE_STEP_P(get_begin_rows_of_BMTB_after_fixed_blocking_in_col_direction, int, col_size)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMTB_after_fixed_blocking_in_col_direction, int, col_size)
+GS_DECLARE_STEP_P(get_begin_rows_of_BMT_after_fixed_blocking_in_col_direction_relative_to_BMTB, int, col_size)
+GS_DECLARE_STEP_P(get_begin_rows_of_BMT_after_fixed_blocking_in_col_direction_relative_to_BMW, int, col_size)
+class get_begin_nzs_of_BMT_after_fixed_blocking_in_col_direction_relative_to_parents : public basic_data_transform_step {
+  public:
+    get_begin_nzs_of_BMT_after_fixed_blocking_in_col_direction_relative_to_parents(std::shared_ptr<meta_data_set> m,
+                                                                                  int target_matrix_id, int col_size,
+                                                                                  POS_TYPE parent_pos)
+        : basic_data_transform_step("get_begin_nzs_of_BMT_after_fixed_blocking_in_col_direction_relative_to_parents",
+                                    std::move(m), target_matrix_id),
+          col_size(col_size), parent_pos(parent_pos) {}
+    void run(bool check) override;
+    int col_size;
+    POS_TYPE parent_pos;
+};
+// remove_item_of_metadata.cc: drop one item (a parent level re-built after padding)
+class remove_item_of_metadata : public basic_data_transform_step {
+  public:
+    remove_item_of_metadata(std::shared_ptr<meta_data_set> m, int target_matrix_id, std::string item_name, POS_TYPE pos)
+        : basic_data_transform_step("remove_item_of_metadata", std::move(m), target_matrix_id),
+          item_name(std::move(item_name)), pos(pos) {}
+    void run(bool check) override;
+    std::string item_name;
+    POS_TYPE pos;
+};
 
 // get_BMT_size_of_each_parent.cc (GLOBAL parent only on the shipped pipelines)
 class get_BMT_size_of_each_parent : public basic_data_transform_step {

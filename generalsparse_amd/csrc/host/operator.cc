@@ -924,14 +924,21 @@ fixed_interval_col_direction_thread_blocking_operator::fixed_interval_col_direct
       is_padding_with_col_size_in_bmt(pad_size), is_col_padding_with_row_max_size_without_empty_row(pad_max),
       code_generator_ptr(cg) {
     GS_CHECK(fcs > 0, "fixed_col_block_size > 0");
-    // ...col_direction_thread_blocking_operator.cc:42-84: the padding level and the
-    // relative-index parent follow the distributing operators already run
-    auto d = history->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
-    bool warp = any_name(d, "warp"), tblock = any_name(d, "tblock");
-    if (warp) padding_pos = WARP_META;
-    else if (tblock) padding_pos = TBLOCK_META;
-    // relative flags name the parent found; with no parent they are unused
-    if (tblock && !warp) {
+    // ...col_direction_thread_blocking_operator.cc:25-85: the padding level and the
+    // relative-index parent follow the distributing operators already run (a "warp" one
+    // wins over a "tblock" one); with no parent the relative flags are unused
+    former_operator = history->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
+    bool warp = false, tblock = false;
+    for (auto &o : former_operator) {
+        if (o->get_name().find("warp") != std::string::npos) warp = true;
+        else if (o->get_name().find("tblock") != std::string::npos) tblock = true;
+    }
+    if (warp) {
+        padding_pos = WARP_META;
+        row_index_is_relative_to_BMW = rrel;
+        nz_index_is_relative_to_BMW = nrel;
+    } else if (tblock) {
+        padding_pos = TBLOCK_META;
         row_index_is_relative_to_BMTB = rrel;
         nz_index_is_relative_to_BMTB = nrel;
     }
@@ -968,6 +975,8 @@ bool fixed_interval_col_direction_thread_blocking_operator::is_valid_according_t
     bool tb = m.is_exist(TBLOCK_META, "first_row_indices", s), wb = m.is_exist(WARP_META, "first_row_indices", s);
     if (row_index_is_relative_to_BMTB) ok = ok && tb;
     if (nz_index_is_relative_to_BMTB) ok = ok && m.is_exist(TBLOCK_META, "first_nz_indices", s);
+    if (row_index_is_relative_to_BMW) ok = ok && wb;
+    if (nz_index_is_relative_to_BMW) ok = ok && m.is_exist(WARP_META, "first_nz_indices", s);
     if (is_col_padding_with_row_max_size_without_empty_row) {
         if (padding_pos == TBLOCK_META) ok = ok && tb;
         else if (padding_pos == WARP_META) ok = ok && wb;
@@ -979,33 +988,217 @@ bool fixed_interval_col_direction_thread_blocking_operator::is_valid_according_t
     return ok && !interlance_storage_existing(m, s);
 }
 
-// ...col_direction_thread_blocking_operator.cc:260-509; the no-parent branch
-// (the one token_test.cc:1258-1262 / 1524 exercises)
+// ...col_direction_thread_blocking_operator.cc:297-368 (shared by the WARP / THREAD col-direction
+// operators): pad every row to a multiple of c, drop the parent levels and run the former
+// operators again on the padded COO with their own padding off
+static void col_pad_and_rerun(const std::shared_ptr<meta_data_set> &m, int s, int c, bool drop_tblock, bool drop_warp,
+                              const std::vector<std::shared_ptr<basic_operator>> &former, bool check,
+                              std::vector<std::string> &seq) {
+    modify_col_indices_by_col_pad_in_sub_matrix a(m, s, c);
+    a.run(check);
+    seq.push_back(a.convert_to_string());
+    modify_vals_by_col_pad_in_sub_matrix b(m, s, c);
+    b.run(check);
+    seq.push_back(b.convert_to_string());
+    modify_row_indices_by_col_pad_in_sub_matrix r(m, s, c);
+    r.run(check);
+    seq.push_back(r.convert_to_string());
+    for (POS_TYPE pos : {TBLOCK_META, WARP_META}) {
+        if ((pos == TBLOCK_META && !drop_tblock) || (pos == WARP_META && !drop_warp)) continue;
+        for (const auto &n : m->all_item_of_metadata_of_diff_pos(pos, s)) {
+            remove_item_of_metadata d(m, s, n, pos);
+            d.run(check);
+            seq.push_back(d.convert_to_string());
+        }
+    }
+    for (auto &o : former) {
+        const size_t before = o->get_data_transform_sequence().size();
+        o->set_padding_to_false();
+        o->run(check);
+        const auto after = o->get_data_transform_sequence();
+        for (size_t k = before; k < after.size(); k++) seq.push_back(after[k]);
+    }
+}
+
+// ...col_direction_thread_blocking_operator.cc:260-487
 void fixed_interval_col_direction_thread_blocking_operator::run(bool check) {
     if (check) GS_CHECK(is_valid_according_to_metadata(), "col-direction thread blocking: invalid metadata");
-    if (has(TBLOCK_META, "first_row_indices") || has(WARP_META, "first_row_indices"))
-        throw gs_error("col-direction BMTs inside BMTB/BMW parents (former-operator re-run) are not built in this round");
     if (is_col_padding_with_row_max_size_without_empty_row)
-        throw gs_error("col padding to the parent's max row size is not built in this round");
-    if (is_padding_with_col_size_in_bmt) {  // :313-326
-        modify_col_indices_by_col_pad_in_sub_matrix a(meta_data_set_ptr, target_matrix_id, fixed_col_block_size);
-        run_step(a, check);
-        modify_vals_by_col_pad_in_sub_matrix b(meta_data_set_ptr, target_matrix_id, fixed_col_block_size);
-        run_step(b, check);
-        modify_row_indices_by_col_pad_in_sub_matrix c(meta_data_set_ptr, target_matrix_id, fixed_col_block_size);
-        run_step(c, check);
+        throw gs_error("col padding to the parent's max row size (modify_*_by_col_pad_parent_blk_to_max_row_size) is not built");
+    const bool bmtb = has(TBLOCK_META, "first_row_indices"), bmw = has(WARP_META, "first_row_indices");
+    const int c = fixed_col_block_size;
+    if (is_padding_with_col_size_in_bmt) {  // :313-368
+        col_pad_and_rerun(meta_data_set_ptr, target_matrix_id, c, bmtb, bmw, former_operator, check, transform_seq);
     }
-    get_begin_rows_of_BMT_after_fixed_blocking_in_col_direction e(meta_data_set_ptr, target_matrix_id,
-                                                                  fixed_col_block_size);
+    get_begin_rows_of_BMT_after_fixed_blocking_in_col_direction e(meta_data_set_ptr, target_matrix_id, c);
     run_step(e, check);
-    get_begin_nzs_of_BMT_after_fixed_blocking_in_col_direction f(meta_data_set_ptr, target_matrix_id,
-                                                                 fixed_col_block_size);
+    get_begin_nzs_of_BMT_after_fixed_blocking_in_col_direction f(meta_data_set_ptr, target_matrix_id, c);
     run_step(f, check);
-    if (is_padding_with_col_size_in_bmt) {  // :477-482
+    if (row_index_is_relative_to_BMTB) {  // :381-395
+        get_begin_rows_of_BMT_after_fixed_blocking_in_col_direction_relative_to_BMTB r(meta_data_set_ptr, target_matrix_id, c);
+        run_step(r, check);
+    }
+    if (nz_index_is_relative_to_BMTB) {  // :397-412
+        get_begin_nzs_of_BMT_after_fixed_blocking_in_col_direction_relative_to_parents r(meta_data_set_ptr, target_matrix_id, c, TBLOCK_META);
+        run_step(r, check);
+    }
+    if (bmtb) {  // :414-420
+        get_begin_BMTs_of_specific_parent_after_blocking g(meta_data_set_ptr, target_matrix_id, TBLOCK_META);
+        run_step(g, check);
+    }
+    if (is_padding_with_col_size_in_bmt && bmtb) {  // :422-428
+        get_BMT_size_of_each_parent g(meta_data_set_ptr, TBLOCK_META, target_matrix_id, false);
+        run_step(g, check);
+    }
+    if (row_index_is_relative_to_BMW) {  // :430-444
+        get_begin_rows_of_BMT_after_fixed_blocking_in_col_direction_relative_to_BMW r(meta_data_set_ptr, target_matrix_id, c);
+        run_step(r, check);
+    }
+    if (nz_index_is_relative_to_BMW) {  // :446-460
+        get_begin_nzs_of_BMT_after_fixed_blocking_in_col_direction_relative_to_parents r(meta_data_set_ptr, target_matrix_id, c, WARP_META);
+        run_step(r, check);
+    }
+    if (bmw) {  // :462-468
+        get_begin_BMTs_of_specific_parent_after_blocking g(meta_data_set_ptr, target_matrix_id, WARP_META);
+        run_step(g, check);
+    }
+    if (is_padding_with_col_size_in_bmt && bmw) {  // :470-476
+        get_BMT_size_of_each_parent g(meta_data_set_ptr, WARP_META, target_matrix_id, false);
+        run_step(g, check);
+    }
+    if (is_padding_with_col_size_in_bmt) {  // :478-483
         get_BMT_size_of_each_parent g(meta_data_set_ptr, GLOBAL_META, target_matrix_id, false);
         run_step(g, check);
     }
     code_generator_ptr->open_spec_level_of_paral(THREAD_META);
+    is_run = true;
+}
+
+// ------------------------------------------- col-direction TBLOCK blocking
+fixed_interval_col_direction_tblock_blocking_operator::fixed_interval_col_direction_tblock_blocking_operator(
+    cg_ptr cg, int fcs, bool pad_size, bool pad_max, ctx_ptr)
+    : basic_operator("fixed_interval_col_direction_tblock_blocking_operator", cg->get_metadata_set(), DISTRIBUTING_OP,
+                     cg->get_sub_matrix_id()),
+      fixed_col_block_size(fcs), is_padding_with_col_size_in_bmtb(pad_size),
+      is_col_padding_with_row_max_size_without_empty_row(pad_max), code_generator_ptr(cg) {
+    GS_CHECK(fcs > 0, "fixed_col_block_size > 0");
+}
+
+// fixed_interval_col_direction_tblock_blocking_operator.cc:37-77: the first distributing operator
+bool fixed_interval_col_direction_tblock_blocking_operator::is_valid_according_to_operator(ctx_ptr h) {
+    return h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty() &&
+           h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id).empty();
+}
+
+// :80-128: the COO, no blocking at any level, the padding rates, no interleaved arrays
+bool fixed_interval_col_direction_tblock_blocking_operator::is_valid_according_to_metadata() {
+    auto &m = *meta_data_set_ptr;
+    const int s = target_matrix_id;
+    bool ok = coo_present(m, s) && m.count_of_metadata_of_diff_pos(THREAD_META, s) == 0 &&
+              m.count_of_metadata_of_diff_pos(WARP_META, s) == 0 && m.count_of_metadata_of_diff_pos(TBLOCK_META, s) == 0;
+    if (ok && is_padding_with_col_size_in_bmtb) ok = padding_rate_valid_col_direction_with_multiple(m, fixed_col_block_size, s);
+    return ok && !interlance_storage_existing(m, s);
+}
+
+// :130-201
+void fixed_interval_col_direction_tblock_blocking_operator::run(bool check) {
+    if (check) GS_CHECK(is_valid_according_to_metadata(), "col-direction tblock blocking: invalid metadata");
+    if (is_col_padding_with_row_max_size_without_empty_row)
+        throw gs_error("col padding to the parent's max row size (modify_*_by_col_pad_parent_blk_to_max_row_size) is not built");
+    const int c = fixed_col_block_size;
+    if (is_padding_with_col_size_in_bmtb) {
+        modify_col_indices_by_col_pad_in_sub_matrix a(meta_data_set_ptr, target_matrix_id, c);
+        run_step(a, check);
+        modify_vals_by_col_pad_in_sub_matrix b(meta_data_set_ptr, target_matrix_id, c);
+        run_step(b, check);
+        modify_row_indices_by_col_pad_in_sub_matrix r(meta_data_set_ptr, target_matrix_id, c);
+        run_step(r, check);
+    }
+    get_begin_rows_of_BMTB_after_fixed_blocking_in_col_direction d(meta_data_set_ptr, target_matrix_id, c);
+    run_step(d, check);
+    get_begin_nzs_of_BMTB_after_fixed_blocking_in_col_direction e(meta_data_set_ptr, target_matrix_id, c);
+    run_step(e, check);
+    if (is_padding_with_col_size_in_bmtb) {
+        get_BMTB_size f(meta_data_set_ptr, target_matrix_id);
+        run_step(f, check);
+    }
+    code_generator_ptr->open_spec_level_of_paral(TBLOCK_META);
+    is_run = true;
+}
+
+// ------------------------------------------- col-direction WARP blocking
+fixed_interval_col_direction_warp_blocking_operator::fixed_interval_col_direction_warp_blocking_operator(
+    cg_ptr cg, int fcs, bool rrel, bool nrel, bool pad_size, bool pad_max, ctx_ptr history)
+    : basic_operator("fixed_interval_col_direction_warp_blocking_operator", cg->get_metadata_set(), DISTRIBUTING_OP,
+                     cg->get_sub_matrix_id()),
+      fixed_col_block_size(fcs), row_index_is_relative_to_BMTB(rrel), nz_index_is_relative_to_BMTB(nrel),
+      is_padding_with_col_size_in_bmw(pad_size), is_col_padding_with_row_max_size_without_empty_row(pad_max),
+      code_generator_ptr(cg) {
+    GS_CHECK(fcs > 0, "fixed_col_block_size > 0");
+    // fixed_interval_col_direction_warp_blocking_operator.cc:20-50
+    former_operator = history->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
+    padding_pos = any_name(former_operator, "tblock") ? TBLOCK_META : GLOBAL_META;
+}
+
+// :60-100
+bool fixed_interval_col_direction_warp_blocking_operator::is_valid_according_to_operator(ctx_ptr h) {
+    if (!h->read_operator_context_arr(IMPLEMENTING_OP, target_matrix_id).empty()) return false;
+    auto d = h->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
+    bool balanced_and_max_pad = any_name(d, "balanced_interval") && is_col_padding_with_row_max_size_without_empty_row;
+    return !any_name(d, "thread") && !any_name(d, "warp") && !any_name(d, "col") && !any_name(d, "interlance") &&
+           !balanced_and_max_pad;
+}
+
+// :102-190
+bool fixed_interval_col_direction_warp_blocking_operator::is_valid_according_to_metadata() {
+    auto &m = *meta_data_set_ptr;
+    const int s = target_matrix_id;
+    bool ok = coo_present(m, s) && m.count_of_metadata_of_diff_pos(THREAD_META, s) == 0 &&
+              m.count_of_metadata_of_diff_pos(WARP_META, s) == 0;
+    const bool tb = m.is_exist(TBLOCK_META, "first_row_indices", s);
+    if (row_index_is_relative_to_BMTB) ok = ok && tb;
+    if (nz_index_is_relative_to_BMTB) ok = ok && m.is_exist(TBLOCK_META, "first_nz_indices", s);
+    if (is_col_padding_with_row_max_size_without_empty_row && padding_pos == TBLOCK_META) ok = ok && tb;
+    if (tb) ok = ok && has_row_direction_blocking_in_specific_level(m, TBLOCK_META, s);
+    if (ok && is_padding_with_col_size_in_bmw) ok = padding_rate_valid_col_direction_with_multiple(m, fixed_col_block_size, s);
+    const bool balanced_and_max_pad = any_name(former_operator, "balanced_interval") && is_col_padding_with_row_max_size_without_empty_row;
+    return ok && !interlance_storage_existing(m, s) && !balanced_and_max_pad;
+}
+
+// :192-372
+void fixed_interval_col_direction_warp_blocking_operator::run(bool check) {
+    if (check) GS_CHECK(is_valid_according_to_metadata(), "col-direction warp blocking: invalid metadata");
+    if (is_col_padding_with_row_max_size_without_empty_row)
+        throw gs_error("col padding to the parent's max row size (modify_*_by_col_pad_parent_blk_to_max_row_size) is not built");
+    const bool bmtb = has(TBLOCK_META, "first_row_indices");
+    const int c = fixed_col_block_size;
+    if (is_padding_with_col_size_in_bmw)
+        col_pad_and_rerun(meta_data_set_ptr, target_matrix_id, c, bmtb, false, former_operator, check, transform_seq);
+    get_begin_rows_of_BMW_after_fixed_blocking_in_col_direction d(meta_data_set_ptr, target_matrix_id, c);
+    run_step(d, check);
+    get_begin_nzs_of_BMW_after_fixed_blocking_in_col_direction e(meta_data_set_ptr, target_matrix_id, c);
+    run_step(e, check);
+    if (row_index_is_relative_to_BMTB) {
+        get_begin_rows_of_BMW_after_fixed_blocking_in_col_direction_relative_to_BMTB r(meta_data_set_ptr, target_matrix_id, c);
+        run_step(r, check);
+    }
+    if (nz_index_is_relative_to_BMTB) {
+        get_begin_nzs_of_BMW_after_fixed_blocking_in_col_direction_relative_to_BMTB r(meta_data_set_ptr, target_matrix_id, c);
+        run_step(r, check);
+    }
+    if (bmtb) {
+        get_begin_BMWs_of_BMTB_after_blocking g(meta_data_set_ptr, target_matrix_id);
+        run_step(g, check);
+    }
+    if (is_padding_with_col_size_in_bmw && bmtb) {
+        get_BMW_size_of_each_parent f(meta_data_set_ptr, target_matrix_id, TBLOCK_META);
+        run_step(f, check);
+    }
+    if (is_padding_with_col_size_in_bmw) {
+        get_BMW_size_of_each_parent f(meta_data_set_ptr, target_matrix_id, GLOBAL_META);
+        run_step(f, check);
+    }
+    code_generator_ptr->open_spec_level_of_paral(WARP_META);
     is_run = true;
 }
 
@@ -1342,6 +1535,16 @@ std::shared_ptr<basic_operator> make_operator(const std::string &name, const std
         return std::make_shared<fixed_interval_col_direction_thread_blocking_operator>(cg, (int)a[0], a[1] != 0,
                                                                                        a[2] != 0, a[3] != 0,
                                                                                        a[4] != 0, ctx);
+    }
+    if (name == "fixed_interval_col_direction_tblock_blocking_operator") {
+        need(3);  // fixed_col_block_size, pad_to_multiple, pad_to_parent_max
+        return std::make_shared<fixed_interval_col_direction_tblock_blocking_operator>(cg, (int)a[0], a[1] != 0, a[2] != 0,
+                                                                                       ctx);
+    }
+    if (name == "fixed_interval_col_direction_warp_blocking_operator") {
+        need(5);  // fixed_col_block_size, row_relative, nz_relative, pad_to_multiple, pad_to_parent_max
+        return std::make_shared<fixed_interval_col_direction_warp_blocking_operator>(cg, (int)a[0], a[1] != 0, a[2] != 0,
+                                                                                     a[3] != 0, a[4] != 0, ctx);
     }
     if (name == "warp_bit_map_operator") {
         need(3);

@@ -356,8 +356,64 @@ class fixed_interval_col_direction_thread_blocking_operator : public basic_opera
     }
     int fixed_col_block_size;
     bool row_index_is_relative_to_BMTB, nz_index_is_relative_to_BMTB;
+    bool row_index_is_relative_to_BMW = false, nz_index_is_relative_to_BMW = false;
     bool is_padding_with_col_size_in_bmt, is_col_padding_with_row_max_size_without_empty_row;
     POS_TYPE padding_pos = GLOBAL_META;
+    std::vector<std::shared_ptr<basic_operator>> former_operator;  // distributing ops before it (re-run after padding)
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
+// operator/fixed_interval_col_direction_tblock_blocking_operator.cc: DISTRIBUTING; BMTBs are
+// chunks of fixed_col_block_size nonzeros of one row (the first distributing operator)
+class fixed_interval_col_direction_tblock_blocking_operator : public basic_operator {
+  public:
+    fixed_interval_col_direction_tblock_blocking_operator(cg_ptr cg, int fixed_col_block_size,
+                                                          bool is_padding_with_col_size_in_bmtb,
+                                                          bool is_col_padding_with_row_max_size_without_empty_row,
+                                                          ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    void set_padding_to_false() override {
+        is_padding_with_col_size_in_bmtb = false;
+        is_col_padding_with_row_max_size_without_empty_row = false;
+    }
+    std::string convert_to_string() const override {
+        return basic_operator::convert_to_string() + ",fixed_col_block_size:" + std::to_string(fixed_col_block_size);
+    }
+    int fixed_col_block_size;
+    bool is_padding_with_col_size_in_bmtb, is_col_padding_with_row_max_size_without_empty_row;
+
+  private:
+    cg_ptr code_generator_ptr;
+};
+
+// operator/fixed_interval_col_direction_warp_blocking_operator.cc: DISTRIBUTING; BMWs are
+// chunks of fixed_col_block_size nonzeros of one row, alone or inside row-direction BMTBs
+class fixed_interval_col_direction_warp_blocking_operator : public basic_operator {
+  public:
+    fixed_interval_col_direction_warp_blocking_operator(cg_ptr cg, int fixed_col_block_size,
+                                                        bool row_index_is_relative_to_BMTB, bool nz_index_is_relative_to_BMTB,
+                                                        bool is_padding_with_col_size_in_bmw,
+                                                        bool is_col_padding_with_row_max_size_without_empty_row,
+                                                        ctx_ptr history);
+    void run(bool check = true) override;
+    bool is_valid_according_to_metadata() override;
+    bool is_valid_according_to_operator(ctx_ptr h) override;
+    void set_padding_to_false() override {
+        is_padding_with_col_size_in_bmw = false;
+        is_col_padding_with_row_max_size_without_empty_row = false;
+    }
+    std::string convert_to_string() const override {
+        return basic_operator::convert_to_string() + ",fixed_col_block_size:" + std::to_string(fixed_col_block_size);
+    }
+    int fixed_col_block_size;
+    bool row_index_is_relative_to_BMTB, nz_index_is_relative_to_BMTB;
+    bool is_padding_with_col_size_in_bmw, is_col_padding_with_row_max_size_without_empty_row;
+    POS_TYPE padding_pos = GLOBAL_META;
+    std::vector<std::shared_ptr<basic_operator>> former_operator;
 
   private:
     cg_ptr code_generator_ptr;

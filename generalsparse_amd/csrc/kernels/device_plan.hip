@@ -941,12 +941,17 @@ void upload_plan(plan_state &p, int dtype, int device) {
             break;
         }
         case KF_ROW_CHUNKS: {
-            const auto &fn = m.u(THREAD_META, "first_nz_indices", sb);
-            const auto &fr = m.u(THREAD_META, "first_row_indices_without_ending", sb);
-            GS_CHECK(fn.size() == fr.size() + 1 && !fr.empty(), "col-direction plan: BMT arrays disagree");
+            // chunks of one row: col-direction BMTs, or col-direction BMWs / BMTBs (the spec's
+            // first array names the level)
+            const POS_TYPE L = sp.arrays[0].rfind("WARP_META", 0) == 0
+                                   ? WARP_META
+                                   : (sp.arrays[0].rfind("TBLOCK_META", 0) == 0 ? TBLOCK_META : THREAD_META);
+            const auto &fn = m.u(L, "first_nz_indices", sb);
+            const auto &fr = m.u(L, "first_row_indices_without_ending", sb);
+            GS_CHECK(fn.size() == fr.size() + 1 && !fr.empty(), "col-direction plan: chunk arrays disagree");
             std::vector<uint32_t> br = to_u32(fr, "first_row_indices_without_ending");
-            a.a0 = upload_index(d, m, THREAD_META, "first_nz_indices", sb, d.f0);
-            a.a1 = upload_index(d, m, THREAD_META, "first_row_indices_without_ending", sb, d.f1);
+            a.a0 = upload_index(d, m, L, "first_nz_indices", sb, d.f0);
+            a.a1 = upload_index(d, m, L, "first_row_indices_without_ending", sb, d.f1);
             d.n_units = br.size();
             d.scf = 4;
             d.span = gsk_host::row_chunk_span(br.size());

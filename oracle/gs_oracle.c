@@ -875,6 +875,149 @@ int or_col_dir_thread_blocking(or_set *s, int col_size, int pad) {
     return 0;
 }
 
+/* ------------------------------------------------------------------ */
+/* col-direction BMWs / BMTBs and BMTs inside row-direction parents     */
+/* fixed_interval_col_direction_{tblock,warp,thread}_blocking_operator  */
+/* ------------------------------------------------------------------ */
+
+/* get_begin_{rows,nzs}_of_{BMW,BMTB}_after_fixed_blocking_in_col_direction.cc:75-105: a unit
+ * per chunk of c nonzeros of one row; rows without ending, nz starts closed by nnz */
+static void col_units(or_set *s, const char *pos, uint64_t c) {
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    uint64_t row_num = row_num_of(s);
+    uint64_t *cnt = row_nnz(R->u, R->len, row_num);
+    vu fr = {0}, fn = {0};
+    vu_push(&fn, 0);
+    for (uint64_t i = 0; i < row_num; i++) {
+        int64_t remain = (int64_t)cnt[i];
+        while (remain > 0) {
+            uint64_t t = remain < (int64_t)c ? (uint64_t)remain : c;
+            vu_push(&fr, i);
+            vu_push(&fn, fn.p[fn.n - 1] + t);
+            remain -= (int64_t)t;
+        }
+    }
+    free(cnt);
+    put_u(s, pos, "first_row_indices_without_ending", 0, fr.p, fr.n);
+    put_u(s, pos, "first_nz_indices", 0, fn.p, fn.n);
+}
+
+/* get_begin_rows_of_<unit>_after_fixed_blocking_in_col_direction_relative_to_<P>.cc:85-120 and
+ * get_begin_nzs_of_..._relative_to_{BMTB,parents}.cc:100-170: per parent block, the chunks of
+ * its rows; rows minus the parent's first row, nz starts from 0 (a 0 pushed per parent, the
+ * parent's closing offset popped) */
+static void col_units_relative(or_set *s, const char *pos, const char *parent, const char *tag, uint64_t c, int rows,
+                               int nzs) {
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0), *PR = get(s, parent, "first_row_indices", 0);
+    uint64_t row_num = row_num_of(s);
+    uint64_t *cnt = row_nnz(R->u, R->len, row_num);
+    vu rr = {0}, rn = {0};
+    for (uint64_t p = 0; p + 1 < PR->len; p++) {
+        vu off = {0};
+        vu_push(&off, 0);
+        for (uint64_t r = PR->u[p]; r < PR->u[p + 1]; r++) {
+            int64_t remain = (int64_t)(r < row_num ? cnt[r] : 0);
+            while (remain > 0) {
+                uint64_t t = remain < (int64_t)c ? (uint64_t)remain : c;
+                vu_push(&rr, r - PR->u[p]);
+                vu_push(&off, off.p[off.n - 1] + t);
+                remain -= (int64_t)t;
+            }
+        }
+        for (uint64_t k = 0; k + 1 < off.n; k++) vu_push(&rn, off.p[k]); /* pop_back of the last */
+        free(off.p);
+    }
+    free(cnt);
+    char k1[64], k2[64];
+    snprintf(k1, sizeof k1, "first_row_indices_relative_to_%s", tag);
+    snprintf(k2, sizeof k2, "first_nz_indices_relative_to_%s", tag);
+    if (rows) put_u(s, pos, k1, 0, rr.p, rr.n); else free(rr.p);
+    if (nzs) put_u(s, pos, k2, 0, rn.p, rn.n); else free(rn.p);
+}
+
+/* get_BMT_size_of_each_parent.cc (parent level, row_direction_blocking false): the BMT size of
+ * every parent block (0 for a parent without BMTs), no item when one parent mixes sizes */
+static void unit_sizes_per_parent(or_set *s, const char *child, const char *parent, const char *name) {
+    or_array *CN = get(s, child, "first_nz_indices", 0), *PN = get(s, parent, "first_nz_indices", 0);
+    vu out = {0};
+    uint64_t cur = 0;
+    for (uint64_t p = 0; p + 1 < PN->len; p++) {
+        uint64_t sz = 0;
+        int seen = 0;
+        while (cur + 1 < CN->len && CN->u[cur] < PN->u[p + 1]) {
+            uint64_t b = CN->u[cur + 1] - CN->u[cur];
+            if (!seen) { sz = b; seen = 1; }
+            else if (b != sz) { free(out.p); return; }
+            cur++;
+        }
+        vu_push(&out, sz);
+    }
+    put_u(s, parent, name, 0, out.p, out.n);
+}
+
+int or_col_dir_tblock_blocking(or_set *s, uint64_t c, int pad) {
+    /* fixed_interval_col_direction_tblock_blocking_operator.cc:80-201 */
+    if (c < 1) return fail(s, "fixed_col_block_size < 1");
+    if (has_level(s, "THREAD_META") || has_level(s, "WARP_META") || has_level(s, "TBLOCK_META"))
+        return fail(s, "col-direction tblock blocking after other blocking (:94-99)");
+    if (pad && col_pad(s, (int)c)) return -1;
+    col_units(s, "TBLOCK_META", c);
+    uint64_t sz;
+    if (pad) {
+        if (!same_size(s, "TBLOCK_META", &sz)) return fail(s, "BMTB sizes differ (get_BMTB_size.cc:81-85)");
+        put_scalar(s, "GLOBAL_META", "BMTB_size_of_each_blk", 0, sz);
+    }
+    return 0;
+}
+
+int or_col_dir_warp_blocking(or_set *s, uint64_t c, int rrel, int nrel) {
+    /* fixed_interval_col_direction_warp_blocking_operator.cc:102-372 (no padding) */
+    int bmtb = exists(s, "TBLOCK_META", "first_row_indices", 0);
+    if (c < 1) return fail(s, "fixed_col_block_size < 1");
+    if (has_level(s, "THREAD_META") || has_level(s, "WARP_META")) return fail(s, "warp level exists (:118-124)");
+    if ((rrel || nrel) && !bmtb) return fail(s, "relative BMW indices without a BMTB (:126-134)");
+    col_units(s, "WARP_META", c);
+    if (rrel || nrel) col_units_relative(s, "WARP_META", "TBLOCK_META", "BMTB", c, rrel, nrel);
+    if (bmtb && children_of(s, "WARP_META", "TBLOCK_META", "first_BMW_indices")) return -1;
+    return 0;
+}
+
+/* col-direction BMTs inside the nearest row-direction parent (a BMW, else a BMTB), relative
+ * indices to it, the parent's first BMT per block; pad = rows padded to a multiple of c first
+ * (the reference pads, drops the parent level and re-runs its operator on the padded COO --
+ * the caller runs the parent blocking after or_col_pad_rows) and the BMT sizes */
+int or_col_dir_thread_in_parent(or_set *s, uint64_t c, int rrel, int nrel, int pad) {
+    int bmw = exists(s, "WARP_META", "first_row_indices", 0), bmtb = exists(s, "TBLOCK_META", "first_row_indices", 0);
+    if (!bmw && !bmtb) return fail(s, "no parent level");
+    if (c < 1) return fail(s, "fixed_col_block_size < 1");
+    const char *par = bmw ? "WARP_META" : "TBLOCK_META";
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    uint64_t row_num = row_num_of(s);
+    uint64_t *cnt = row_nnz(R->u, R->len, row_num);
+    vu fr = {0}, fn = {0};
+    vu_push(&fn, 0);
+    for (uint64_t i = 0; i < row_num; i++) { /* get_begin_{rows,nzs}_of_BMT_..._in_col_direction.cc */
+        int64_t remain = (int64_t)cnt[i];
+        while (remain > 0) {
+            uint64_t t = remain < (int64_t)c ? (uint64_t)remain : c;
+            vu_push(&fr, i);
+            vu_push(&fn, fn.p[fn.n - 1] + t);
+            remain -= (int64_t)t;
+        }
+    }
+    free(cnt);
+    put_u(s, "THREAD_META", "first_row_indices_without_ending", 0, fr.p, fr.n);
+    put_u(s, "THREAD_META", "first_nz_indices", 0, fn.p, fn.n);
+    if (rrel || nrel) col_units_relative(s, "THREAD_META", par, bmw ? "BMW" : "BMTB", c, rrel, nrel);
+    if (bmtb && children_of(s, "THREAD_META", "TBLOCK_META", "first_BMT_indices")) return -1;
+    if (pad && bmtb) unit_sizes_per_parent(s, "THREAD_META", "TBLOCK_META", "BMT_size_of_each_blk");
+    if (bmw && children_of(s, "THREAD_META", "WARP_META", "first_BMT_indices")) return -1;
+    if (pad && bmw) unit_sizes_per_parent(s, "THREAD_META", "WARP_META", "BMT_size_of_each_blk");
+    uint64_t sz;
+    if (pad && same_size(s, "THREAD_META", &sz)) put_scalar(s, "GLOBAL_META", "BMT_size_of_each_blk", 0, sz);
+    return 0;
+}
+
 /* warp_bit_map_operator.cc:69-109 (pos_is_warp = 1, merge = VECTOR_WIDTH) and
  * tblock_thread_bit_map_operator.cc:62-109 (pos_is_warp = 0, merge = block_size):
  * get_begin_{rows,nzs}_after_merge_thread.cc, the relative variants
@@ -1447,6 +1590,25 @@ int or_pipeline(or_set *s, const char *name, int p0, int p1) {
     /* nnz-direction parents (p0 = nnz per BMW / BMTB, p1 = nnz per BMW inside the BMTBs),
      * padded at the outer level, 32-nnz BMTs inside (relative indices), thread bitmaps of
      * VW 32 (N >= 32) */
+    /* col-direction parents: BMWs / BMTBs of p0 nonzeros of a row (tblock_col_warp_total: BMWs
+     * of p1 nonzeros inside row-direction BMTBs of p0 rows, relative indices), and col-direction
+     * BMTs of p1 nonzeros inside row-direction BMTBs / BMWs of p0 rows (relative indices) */
+    if (!strcmp(name, "col_warp_total")) return or_col_dir_warp_blocking(s, p0 > 0 ? (uint64_t)p0 : 64, 0, 0);
+    if (!strcmp(name, "col_tblock_total")) return or_col_dir_tblock_blocking(s, p0 > 0 ? (uint64_t)p0 : 256, 0);
+    if (!strcmp(name, "tblock_col_warp_total")) {
+        if (or_row_dir_tblock_blocking(s, p0 > 0 ? p0 : 16)) return -1;
+        return or_col_dir_warp_blocking(s, p1 > 0 ? (uint64_t)p1 : 64, 1, 1);
+    }
+    if (!strcmp(name, "tblock_col_thread_total") || !strcmp(name, "warp_col_thread_total") ||
+        !strcmp(name, "tblock_col_thread_total_padded")) {
+        int pad = !strcmp(name, "tblock_col_thread_total_padded");
+        uint64_t c = p1 > 0 ? (uint64_t)p1 : 32;
+        if (pad && col_pad(s, (int)c)) return -1;
+        if (!strcmp(name, "warp_col_thread_total")) {
+            if (or_row_dir_warp_blocking(s, p0 > 0 ? p0 : 16)) return -1;
+        } else if (or_row_dir_tblock_blocking(s, p0 > 0 ? p0 : 16)) return -1;
+        return or_col_dir_thread_in_parent(s, c, 1, 1, pad);
+    }
     if (!strcmp(name, "nnz_warp_bitmap")) {
         if (or_nnz_dir_warp_blocking(s, (uint64_t)p0, 0, 0, 1)) return -1;
         if (or_nnz_dir_thread_in_parent(s, 32, 1, 1)) return -1;

@@ -97,6 +97,10 @@ int or_row_nz_div(or_set *s, uint64_t init, uint64_t max_gap, uint64_t rate); /*
 int or_index_compression(const uint64_t *a, uint64_t n, int type_ori, int branch_max, int *kind,
                          uint64_t *params, uint64_t *res);                 /* §8f rank 1 */
 int or_col_dir_thread_blocking(or_set *s, int col_size, int pad);          /* A10 */
+/* col-direction BMWs / BMTBs and col-direction BMTs inside row-direction parents */
+int or_col_dir_tblock_blocking(or_set *s, uint64_t col_size, int pad);
+int or_col_dir_warp_blocking(or_set *s, uint64_t col_size, int rrel, int nrel);
+int or_col_dir_thread_in_parent(or_set *s, uint64_t col_size, int rrel, int nrel, int pad);
 int or_parent_bit_map_operator(or_set *s, int pos_is_warp, int merge, int rel_nz, int rel_row); /* K5/K7 */
 
 /* Canned pipelines = token_test.cc test_spmm_* operator sequences. */
