@@ -337,7 +337,7 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
                 "its own HBM copy of A)",
         "config": {"workload": f"OPT-30B weight batch: {args.layers} layers x (4 x 7168^2, 28672x7168, 7168x28672), "
                                f"80% unstructured, fp16, N={N}", "matrices": len(batch), "nnz": total_nnz,
-                   "plan": "tblock_warp_total(20,2)", "kernel": kernel_label(info),
+                   "plan": {k: "%s(%d,%d)" % bt.shape_pipeline(k) for k in plans}, "kernel": kernel_label(info),
                    "parallelism": f"LPT batch split x{world} (max rank nnz share {max(load) / total_nnz:.4f})"},
         "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9 / world, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / world / HBM_PEAK_GBS, 4),

@@ -16,6 +16,18 @@ DEFAULT_CANDIDATES = {
 }
 
 
+def row_block_rows(M, cus=256, max_rows=64):
+    """BMTB height for the matrix-core row blocks (k_mfma_rows): the fewest whole rounds
+    of one workgroup per CU, then the lowest height that keeps to that many rounds.  A
+    workgroup streams all of B whatever its height, so a row block count just past a
+    multiple of the CU count costs a whole extra round: 7168 rows in 20-row blocks are
+    358 workgroups (two rounds on 256 CUs, 28.9 us on the C5 q/k/v/out shape), in 28-row
+    blocks 256 (one round, 16.9 us); 28672 rows run best at 56 (two rounds).  MI355X:
+    256 CUs (8 XCDs x 32)."""
+    rounds = max(1, math.ceil(M / (cus * max_rows)))
+    return max(1, math.ceil(M / (cus * rounds)))
+
+
 def autotune(M, K, row, col, val, N, dtype="f16", candidates=None, device=0, reps=50, rotation_mb=640.0,
              save_path=None):
     """returns (best Plan (uploaded), {variant: kernel microseconds or error string})"""
@@ -24,7 +36,11 @@ def autotune(M, K, row, col, val, N, dtype="f16", candidates=None, device=0, rep
     e = 2 if dtype == "f16" else 4
     dev = torch.device(f"cuda:{device}")
     results, best = {}, None
-    for name, p0, p1 in candidates or DEFAULT_CANDIDATES[dtype]:
+    if candidates is None:
+        candidates = list(DEFAULT_CANDIDATES[dtype])
+        if dtype == "f16" and ("tblock_warp_total", row_block_rows(M), 2) not in candidates:
+            candidates.insert(0, ("tblock_warp_total", row_block_rows(M), 2))
+    for name, p0, p1 in candidates:
         key = f"{name}({p0},{p1})"
         try:
             plan = Plan.from_coo(M, K, row, col, val).run_pipeline(name, N, p0, p1).compile().upload(dtype, device)

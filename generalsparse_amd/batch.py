@@ -60,9 +60,17 @@ def shape_seed(rank, shape):
     return 1000 + 8 * rank + list(C5_SHAPES).index(shape)
 
 
-def build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, pipeline=("tblock_warp_total", 20, 2), keep_coo=False):
+def shape_pipeline(shape):
+    """the pipeline of a shape's plan: BMTB row blocks sized to whole CU rounds
+    (autotune.row_block_rows: 28 rows for the 7168-row shapes, 56 for fc1)"""
+    from .autotune import row_block_rows
+    return ("tblock_warp_total", row_block_rows(C5_SHAPES[shape][0]), 2)
+
+
+def build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, pipeline=None, keep_coo=False):
     """plans (one per shape, one replica per instance), B and C buffers (two per shape,
-    alternating), and the launch list [(plan, replica, B, C, shape)]"""
+    alternating), and the launch list [(plan, replica, B, C, shape)].  `pipeline`
+    (name, p0, p1) overrides the per-shape choice of shape_pipeline."""
     count = {}
     for (_, _, k, _) in seq:
         count[k] = count.get(k, 0) + 1
@@ -71,7 +79,8 @@ def build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, pipeline=("tblock
         if not count.get(k):
             continue
         row, col, val = ds.pruned_weight(m, n, C5_SPARSITY, shape_seed(rank, k))
-        plan = gsa.Plan.from_coo(m, n, row, col, val).run_pipeline(pipeline[0], N, pipeline[1], pipeline[2]).compile()
+        pl = pipeline or shape_pipeline(k)
+        plan = gsa.Plan.from_coo(m, n, row, col, val).run_pipeline(pl[0], N, pl[1], pl[2]).compile()
         plan.upload("f16", local)
         for _ in range(count[k] - 1):
             plan.add_replica()

@@ -156,16 +156,19 @@ def test_c5_shapes_against_torch(c5_coo):
     for k, (m, n) in bt.C5_SHAPES.items():
         row, col, val = c5_coo[k]
         assert len(row) == bt.nnz_of_shape(k)
-        plan = gsa.Plan.from_coo(m, n, row, col, val).run_pipeline("tblock_warp_total", N, 20, 2).compile()
-        plan.upload("f16", 0)
-        assert plan.info()["device_kernel"].startswith("k_mfma"), plan.info()["device_kernel"]
         g = torch.Generator(device=DEV)
         g.manual_seed(5)
         B = (torch.rand((n, N), device=DEV, generator=g) * 2 - 1).half()
-        C = plan.spmm(B)
-        torch.cuda.synchronize()
-        check(C.float().cpu().numpy(), dense_ref(m, n, row, col, val, B), "f16")
-        plan.free()
+        ref = dense_ref(m, n, row, col, val, B)
+        # the round-1 20-row blocks and the batch's per-shape heights (28 / 56 rows)
+        for rows in sorted({20, bt.shape_pipeline(k)[1]}):
+            plan = gsa.Plan.from_coo(m, n, row, col, val).run_pipeline("tblock_warp_total", N, rows, 2).compile()
+            plan.upload("f16", 0)
+            assert plan.info()["device_kernel"].startswith("k_mfma"), (rows, plan.info()["device_kernel"])
+            C = plan.spmm(B)
+            torch.cuda.synchronize()
+            check(C.float().cpu().numpy(), ref, "f16")
+            plan.free()
 
 
 def test_c5_two_layer_batch_sequence():
@@ -178,6 +181,8 @@ def test_c5_two_layer_batch_sequence():
     assert len(seq) == 12
     plans, launches, coo = bt.build_rank_batch(seq, 0, N, gsa, ds, torch, DEV, 0, keep_coo=True)
     assert {k: p.info()["replicas"] for k, p in plans.items()} == {"attn": 8, "fc1": 2, "fc2": 2}
+    assert {k: bt.shape_pipeline(k)[1] for k in plans} == {"attn": 28, "fc1": 56, "fc2": 28}
+    assert all(p.info()["device_kernel"].startswith("k_mfma") for p in plans.values())
     stream = torch.cuda.current_stream().cuda_stream
     refs = {}
     for i, (plan, rep, B, C, k) in enumerate(launches):

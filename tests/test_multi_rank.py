@@ -189,3 +189,19 @@ def test_single_matrix_shards_combine_to_full_spmm(mode, world):
         np.testing.assert_array_equal(long_row, ref[100].astype(np.float32).astype(np.float16).astype(np.float64))
     # rows no rank holds are the trailing empty rows (zero in the full product)
     assert np.all(ref[~held] == 0)
+
+
+def test_row_block_rows_fill_whole_cu_rounds():
+    """matrix-core BMTB heights: whole rounds of one workgroup per CU (256 on MI355X) at
+    the lowest height, at most 64 rows (C2 keeps 20; the C5 shapes get 28 / 56)"""
+    import math
+    from generalsparse_amd.autotune import row_block_rows
+    from generalsparse_amd import batch as bt
+    assert row_block_rows(5120) == 20
+    assert {k: bt.shape_pipeline(k)[1] for k in bt.C5_SHAPES} == {"attn": 28, "fc1": 56, "fc2": 28}
+    for M in (1, 255, 256, 257, 5120, 7168, 16385, 28672, 100000):
+        r = row_block_rows(M)
+        assert 1 <= r <= 64
+        rounds = math.ceil(math.ceil(M / r) / 256)
+        assert rounds == max(1, math.ceil(M / (256 * 64)))
+        assert r == 1 or math.ceil(math.ceil(M / (r - 1)) / 256) > rounds
