@@ -944,7 +944,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     const u32x4 *__restrict__ tV,                 // per group: 8 x f16 value (+1 spare group)
     const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K, uint32_t N, uint32_t nc, uint32_t RMAX,
     uint32_t row_base, uint32_t nsplit, uint32_t ncs, float *__restrict__ slabs, uint32_t *__restrict__ arrivals,
-    uint64_t *__restrict__ stamps = nullptr) {
+    uint64_t *__restrict__ stamps = nullptr, uint32_t krot = 0) {
     constexpr uint32_t KC = 1u << LGKC;
     constexpr uint32_t RB = 32 * CT;                  // bytes per B row (N == 16*CT)
     constexpr uint32_t UB = 2 * CT;                   // 16-B units per B row
@@ -978,6 +978,12 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     // GS_SEG takes a local chunk index
     const uint32_t segv = seg_start[g * nc + min(lane, nc)];
 #define GS_SEG(j) __builtin_amdgcn_readlane(segv, j0 + (j))
+    // chunk order: period j works on chunk jr(j); with krot every workgroup starts at its
+    // own chunk (g mod ncl) and wraps, so the 256 workgroups are not all pulling the same
+    // B rows from the same L2 channels at once (wave-uniform; the k order of a row block's
+    // partial sums changes, the result stays deterministic per plan)
+    const uint32_t rot = krot ? g % ncl : 0u;
+    auto jr = [&](uint32_t j) -> uint32_t { const uint32_t x = j + rot; return x >= ncl ? x - ncl : x; };
     uint64_t *lst = reinterpret_cast<uint64_t *>(lds + oD + NDI * szD);  // STAMPS only
     // first lane of each role -> slots [21*role, 21*role + 21): 0 start, 1 chunk 0 staged,
     // 2+2j chunk j's work done, 3+2j after its barrier (j < 9); slot 63 end
@@ -1007,7 +1013,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         GS_STAMP(1u);
         __syncthreads();  // chunk 0 staged
         for (uint32_t j = 0; j < ncl; j++) {
-            const uint32_t kr = min(KC, K - (j0 + j) * KC);
+            const uint32_t kr = min(KC, K - (j0 + jr(j)) * KC);
             const uint32_t nsteps = (kr + 31u) / 32u;
             const unsigned char *la = lds + oD + (j % NDI) * szD;
             const unsigned char *lb = lds + (j % NBUF) * szB;
@@ -1084,7 +1090,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         // counted vmcnt before a raw s_barrier (__syncthreads would drain to vmcnt(0)).
         const uint32_t bw = wv - WC;
         auto issue = [&](uint32_t jl) {
-            const uint32_t kc0 = (j0 + jl) * KC;
+            const uint32_t kc0 = (j0 + jr(jl)) * KC;
 #pragma unroll
             for (uint32_t i = 0; i < NB; i++) {
                 const uint32_t u0 = (bw * NB + i) * 64u, u = u0 + lane;
@@ -1134,7 +1140,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         u32x4 s0[NB], s1[NB], s2[NB];
 #define GS_BLOAD(j, S)                                                                              \
     {                                                                                             \
-        const uint32_t kc0_ = (j0 + min((uint32_t)(j), ncl - 1u)) * KC;                          \
+        const uint32_t kc0_ = (j0 + jr(min((uint32_t)(j), ncl - 1u))) * KC;                      \
         _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                                     \
             const uint32_t u = bt + i * NBT;                                                      \
             const uint32_t k = u / UB;                                                            \
@@ -1152,7 +1158,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         // store is unconditional: B[(nc)&1] is free at the last chunk)
 #define GS_BITER(j, Sn, Ss)                                                                         \
     {                                                                                             \
-        const uint32_t kc0_ = (j0 + min((uint32_t)(j) + 3u, ncl - 1u)) * KC;                     \
+        const uint32_t kc0_ = (j0 + jr(min((uint32_t)(j) + 3u, ncl - 1u))) * KC;                 \
         _Pragma("unroll") for (uint32_t i = 0; i < NB; i++) {                                     \
             const uint32_t u = bt + i * NBT;                                                      \
             const uint32_t k = u / UB;                                                            \
@@ -1189,7 +1195,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         u32x4 p0[MAXA], v0[MAXA], p1[MAXA], v1[MAXA], p2[MAXA], v2[MAXA], p3[MAXA], v3[MAXA];
 #define GS_ALOAD(j, P, V)                                                                           \
     {                                                                                             \
-        const uint32_t jj_ = min((uint32_t)(j), ncl - 1u);                                        \
+        const uint32_t jj_ = jr(min((uint32_t)(j), ncl - 1u));                                    \
         const uint32_t s0_ = GS_SEG(jj_);                                                         \
         const uint32_t G_ = (uint32_t)(j) < ncl ? GS_SEG(jj_ + 1) - s0_ : 0u;                     \
         _Pragma("unroll") for (int I = 0; I < MAXA; I++) {                                        \
@@ -1201,7 +1207,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     }
 #define GS_SCATTER(j, P, V)                                                                         \
     {                                                                                             \
-        const uint32_t G_ = GS_SEG((j) + 1) - GS_SEG(j);                                          \
+        const uint32_t G_ = GS_SEG(jr(j) + 1) - GS_SEG(jr(j));                                    \
         unsigned char *ld_ = lds + oD + ((j) % NDI) * szD;                                        \
         _Pragma("unroll") for (int I = 0; I < MAXA; I++) {                                        \
             const uint32_t q = at + I * NAT;                                                      \
@@ -1726,7 +1732,7 @@ template <int CT, int DBG = 0>
 __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *__restrict__ A,
                                                            const f16 *__restrict__ B, f16 *__restrict__ C,
                                                            uint32_t K, uint32_t S, uint32_t rows,
-                                                           uint32_t row_base) {
+                                                           uint32_t row_base, uint32_t krot = 0) {
     constexpr uint32_t N = 16 * CT, RB = 32 * CT, UB = 2 * CT;
     constexpr uint32_t szB = kNmKC * RB;
     constexpr uint32_t NTH = 64 * kNmWaves;
@@ -1739,6 +1745,10 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
     const uint32_t rh = wv >> 2, q = wv & 3u;
     const uint32_t rg = blockIdx.x * 2u + rh;
     const uint32_t nch = S / 4u;
+    // chunk order (krot, as in k_mfma_rows): iteration c works on chunk jr(c), every
+    // workgroup starting at its own chunk so they do not all pull the same B rows at once
+    const uint32_t rot = krot ? blockIdx.x % nch : 0u;
+    auto jr = [&](uint32_t c) -> uint32_t { const uint32_t x = c + rot; return x >= nch ? x - nch : x; };
     const unsigned char *arow = A + (size_t)rg * S * kNmBlockBytes;
     const unsigned char *bbase = reinterpret_cast<const unsigned char *>(B);
     const uint32_t bk = tid / UB, boff = bk * RB + (tid % UB) * 16u;  // this thread's first unit
@@ -1752,7 +1762,7 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
     uint2 a0i, a1i;
 #define GS_NM_ALOAD(c, V, I)                                                                        \
     if (DBG != 2 || (uint32_t)(c) < 2u) {                                                         \
-        const uint32_t cc_ = min((uint32_t)(c), nch - 1u);                                        \
+        const uint32_t cc_ = jr(min((uint32_t)(c), nch - 1u));                                    \
         const unsigned char *blk_ = arow + (size_t)(4u * cc_ + q) * kNmBlockBytes;                \
         I = *reinterpret_cast<const uint2 *>(blk_ + lane * 8u);                                   \
         _Pragma("unroll") for (int rt = 0; rt < 4; rt++) V[rt] =                                  \
@@ -1762,7 +1772,7 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
     // whole chunks: one lane offset, uniform bases; the last partial chunk clamps rows
 #define GS_NM_BLOAD(c)                                                                              \
     if (DBG != 1 || (uint32_t)(c) < 2u) {                                                         \
-        const uint32_t k0_ = (uint32_t)(c) * kNmKC;                                               \
+        const uint32_t k0_ = jr(min((uint32_t)(c), nch - 1u)) * kNmKC;                            \
         if (k0_ + kNmKC <= K) {                                                                   \
             const unsigned char *src_ = bbase + (size_t)k0_ * RB;                                 \
             _Pragma("unroll") for (uint32_t i = 0; i < NBU; i++) bs[i] =                          \
@@ -1776,7 +1786,7 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
     }
 #define GS_NM_BSTORE(c)                                                                             \
     {                                                                                             \
-        const uint32_t k0_ = (uint32_t)(c) * kNmKC;                                               \
+        const uint32_t k0_ = jr(min((uint32_t)(c), nch - 1u)) * kNmKC;                            \
         unsigned char *lb_ = lds + ((uint32_t)(c) & 1u) * szB;                                    \
         if (k0_ + kNmKC <= K) {                                                                   \
             _Pragma("unroll") for (uint32_t i = 0; i < NBU; i++)                                  \

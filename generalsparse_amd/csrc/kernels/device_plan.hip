@@ -1157,7 +1157,8 @@ void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *
     }
     hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit), dim3(kMfmaThreads), d.lds_bytes, s, a.t0,
                        a.t1, (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, B, C, (uint32_t)p.K, N, d.nc,
-                       d.rpw_max, (uint32_t)d.row_base, d.ksplit, d.ncs, a.ws, a.t2, (uint64_t *)nullptr);
+                       d.rpw_max, (uint32_t)d.row_base, d.ksplit, d.ncs, a.ws, a.t2, (uint64_t *)nullptr,
+                       (uint32_t)get_config().MFMA_KROT);
     HIP_OK(hipGetLastError());
 }
 
@@ -1213,7 +1214,7 @@ void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N
     HIP_OK(hipMalloc(&dst, n * 8));
     hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit), dim3(kMfmaThreads), lds, s, a.t0, a.t1,
                        (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, (const gsk::f16 *)B, (gsk::f16 *)C,
-                       (uint32_t)p.K, N, d.nc, d.rpw_max, (uint32_t)d.row_base, d.ksplit, d.ncs, a.ws, a.t2, dst);
+                       (uint32_t)p.K, N, d.nc, d.rpw_max, (uint32_t)d.row_base, d.ksplit, d.ncs, a.ws, a.t2, dst, 0u);
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(s));
     HIP_OK(hipMemcpy(host, dst, std::min(n, n_host) * 8, hipMemcpyDeviceToHost));
@@ -1244,7 +1245,7 @@ void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, vo
     const uint32_t wg = (uint32_t)((d.n_rows_aux + 127) / 128);
     hipLaunchKernelGGL(kern, dim3(wg), dim3(64 * gsk::kNmWaves), lds, s, (const unsigned char *)a.tcol,
                        (const gsk::f16 *)B, (gsk::f16 *)C, (uint32_t)p.K, d.KC, (uint32_t)d.n_rows_aux,
-                       (uint32_t)d.row_base);
+                       (uint32_t)d.row_base, (uint32_t)get_config().MFMA_KROT);
     HIP_OK(hipGetLastError());
 }
 

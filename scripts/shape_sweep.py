@@ -1,5 +1,5 @@
 """Kernel time of matrix-core row-block variants per C2 / C5 shape (diagnostic).
-usage: shape_sweep.py <shape> [rows:bmw:ksplit ...]
+usage: shape_sweep.py <shape> [rows:bmw:ksplit[:krot] ...]
 shape: c2 (5120^2, 70%) | attn (7168^2, 80%) | fc1 (28672x7168, 80%) | fc2 (7168x28672, 80%)
 ksplit 0 = the upload's automatic choice.  Event time over a rotation of >= 600 MB of
 the bytes the kernel reads, fp16, N = 32."""
@@ -23,8 +23,9 @@ else:
     M, K = bt.C5_SHAPES[shape]
     row, col, val = ds.pruned_weight(M, K, bt.C5_SPARSITY, bt.shape_seed(0, shape))
 for spec in sys.argv[2:]:
-    r, w, ks = (int(x) for x in spec.split(":"))
+    r, w, ks, kr = ([int(x) for x in spec.split(":")] + [0])[:4]
     gsa.set_config("MFMA_KSPLIT", ks)
+    gsa.set_config("MFMA_KROT", kr)
     plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline("tblock_warp_total", N, r, w).compile().upload("f16", 0)
     info = plan.info()
     rd = info["tile_bytes"] or info["device_bytes_A"]
@@ -47,7 +48,7 @@ for spec in sys.argv[2:]:
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / n * 1e3
     alg = len(row) * 4 + (M + 1) * 4 + K * N * 2 + M * N * 2
-    print(f"{shape} rows={r} bmw={w} ksplit={ks}: {info.get('device_kernel') or info['kernel_name']} {us:.2f} us, "
+    print(f"{shape} rows={r} bmw={w} ksplit={ks} krot={kr}: {info.get('device_kernel') or info['kernel_name']} {us:.2f} us, "
           f"{2.0 * len(row) * N / us / 1e3:.0f} GFLOP/s, {alg / us / 1e3:.0f} GB/s "
           f"({alg / us / 1e3 / 8000:.3f} of 8 TB/s)", flush=True)
     plan.free()
