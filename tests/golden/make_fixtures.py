@@ -269,6 +269,37 @@ cases.append({
     },
 })
 
+# interleaving in the tblock_bit_map plan (token_test.cc:1515-1582 + interlance_storage_operator):
+# the operator takes its parent level from the DISTRIBUTING operators run before it
+# (interlance_storage_operator.cc:12-45); here only the col-direction THREAD blocking ran (the
+# TBLOCK level comes later, from the implementing tblock_thread_bit_map_operator), so it
+# interleaves at GLOBAL level (modify_col_indices_by_interlance_storage.cc:45-72): spacing =
+# the number of BMTs, element i of BMT b -> b + n_BMT * i.  ex3: same arrays as warp_bit_map.
+cases.append({
+    "matrix": "ex3", "pipeline": "tblock_bit_map_interleaved", "p0": 8,
+    "expect": {
+        G + "BMT_size_of_each_blk_0": [64],
+        G + "nz_col_indices_after_interlance_storage_0": [_bmts[b][i] for i in range(64) for b in range(4)],
+        G + "nz_row_indices_after_interlance_storage_0": [_rows[b] for i in range(64) for b in range(4)],
+    },
+})
+# ex4: 11 BMTs of 64 (row0: cols 64b..64b+63 for b < 9, b9 = cols 576..599 + 40 x 599; b10 =
+# row1 cols 0..9 + 54 x 9; pads repeat the row's last col) -> element i of BMT b at b + 11 i;
+# the TBLOCK parents [0, 8) [8, 11) that tblock_thread_bit_map_operator builds afterwards
+# index the interleaved arrays unchanged (first_BMT_indices [0, 8, 11]).
+_b4 = [list(range(64 * b, 64 * b + 64)) for b in range(9)] + [list(range(576, 600)) + [599] * 40,
+                                                             list(range(10)) + [9] * 54]
+_r4 = [0] * 10 + [1]
+cases.append({
+    "matrix": "ex4", "pipeline": "tblock_bit_map_interleaved", "p0": 8,
+    "expect": {
+        G + "BMT_size_of_each_blk_0": [64],
+        B + "first_BMT_indices_0": [0, 8, 11],
+        G + "nz_col_indices_after_interlance_storage_0": [_b4[b][i] for i in range(64) for b in range(11)],
+        G + "nz_row_indices_after_interlance_storage_0": [_r4[b] for i in range(64) for b in range(11)],
+    },
+})
+
 # relative BMW indices (§8f rank 1) on ex1 with BMTBs of 4 rows and BMWs of 2 rows:
 # BMTB rows [0,4) and [4,6); BMW starts 0,2 | 4 -> relative 0,2 | 0; row nnz [2,0,3,1,5,0]:
 # BMTB 0 nonzeros before each BMW 0, 2 | BMTB 1: 0

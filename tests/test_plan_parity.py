@@ -130,7 +130,7 @@ def test_hand_derived_fixtures_through_product():
             "merge_path": (8, 0, 1), "balanced_block_total": (32, 0, 1), "balanced_thread_total": (8, 0, 1),
             "warp_bit_map_interleaved": (32, 4, 1), "tblock_warp_total_relative": (32, 4, 2),
             "tblock_warp_total": (32, 4, 1), "balanced_warp_total": (32, 16, 1),
-            "warp_bit_map": (32, 4, 1), "tblock_bit_map": (32, 4, 1),
+            "warp_bit_map": (32, 4, 1), "tblock_bit_map": (32, 4, 1), "tblock_bit_map_interleaved": (32, 4, 1),
             "tblock_thread_total": (32, 4, 1), "tblock_warp_thread_total": (32, 4, 1)}
     for case in g["cases"]:
         m = g["matrices"][case["matrix"]]
