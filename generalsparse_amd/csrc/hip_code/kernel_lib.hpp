@@ -561,10 +561,15 @@ __device__ __forceinline__ void row_chunks_body(const uint32_t *__restrict__ bmt
                                                     const CT *__restrict__ col, const VT *__restrict__ val,
                                                     const VT *__restrict__ B, VT *__restrict__ C,
                                                     float *__restrict__ ws, uint32_t n_bmt, uint32_t U, uint32_t N,
-                                                    uint32_t X, uint32_t row_base, uint32_t ilv = 0) {
+                                                    uint32_t X, uint32_t row_base, uint32_t ilv = 0,
+                                                    const uint32_t *__restrict__ ilv_base = nullptr,
+                                                    const uint32_t *__restrict__ ilv_stride = nullptr) {
     // ilv > 0: interleaved storage (interlance_storage_operator, GLOBAL parent): every BMT
     // has ilv nonzeros and the i-th of BMT b sits at b + i * n_bmt, so the slots of a wave
-    // read consecutive addresses (total_BMT_result_reduce_to_one_register_token.cc:581-624)
+    // read consecutive addresses (total_BMT_result_reduce_to_one_register_token.cc:581-624).
+    // ilv_base: interleaved per TBLOCK / WARP parent (modify_col_indices_by_interlance_storage.cc
+    // :73-118): the i-th nonzero of BMT b sits at ilv_base[b] + i * ilv_stride[b] = the parent's
+    // first nonzero + (b - its first BMT) + i * its BMT count; BMT b keeps its own size
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t xl = lane & (X - 1u);
     const uint32_t slot = lane / X;
@@ -592,7 +597,16 @@ __device__ __forceinline__ void row_chunks_body(const uint32_t *__restrict__ bmt
 #pragma unroll
                 for (int k = 0; k < CF; k++) acc[k] = 0.f;
                 if (valid) {
-                    if (ilv) {
+                    if (ilv_base) {
+                        uint32_t b, e;
+                        idx_range<FX>(bmt_nz, f_nz, bt, b, e);
+                        const uint32_t q0 = ilv_base[bt], st = ilv_stride[bt];
+#pragma unroll 4
+                        for (uint32_t i = 0; i < e - b; i++) {
+                            const size_t p = (size_t)q0 + (size_t)i * st;
+                            fma_row<VT, CF>(acc, (float)val[p], B + (size_t)col[p] * N + c0);
+                        }
+                    } else if (ilv) {
 #pragma unroll 8
                         for (uint32_t i = 0; i < ilv; i++) {
                             const size_t p = (size_t)bt + (size_t)i * n_bmt;
@@ -647,11 +661,15 @@ __global__ __launch_bounds__(256) void k_row_chunks(const uint32_t *__restrict__
                                                     const CT *__restrict__ col, const VT *__restrict__ val,
                                                     const VT *__restrict__ B, VT *__restrict__ C,
                                                     float *__restrict__ ws, uint32_t n_bmt, uint32_t U, uint32_t N,
-                                                    uint32_t X, uint32_t row_base, uint32_t ilv = 0) {
+                                                    uint32_t X, uint32_t row_base, uint32_t ilv = 0,
+                                                    const uint32_t *__restrict__ ilv_base = nullptr,
+                                                    const uint32_t *__restrict__ ilv_stride = nullptr) {
     if (f_nz.kind == IDX_ARRAY && f_row.kind == IDX_ARRAY)
-        row_chunks_body<VT, CT, CF, SCF, false>(bmt_nz, f_nz, bmt_row, f_row, col, val, B, C, ws, n_bmt, U, N, X, row_base, ilv);
+        row_chunks_body<VT, CT, CF, SCF, false>(bmt_nz, f_nz, bmt_row, f_row, col, val, B, C, ws, n_bmt, U, N, X, row_base, ilv,
+                                                ilv_base, ilv_stride);
     else
-        row_chunks_body<VT, CT, CF, SCF, true>(bmt_nz, f_nz, bmt_row, f_row, col, val, B, C, ws, n_bmt, U, N, X, row_base, ilv);
+        row_chunks_body<VT, CT, CF, SCF, true>(bmt_nz, f_nz, bmt_row, f_row, col, val, B, C, ws, n_bmt, U, N, X, row_base, ilv,
+                                               ilv_base, ilv_stride);
 }
 
 // ---------------------------------------------------------------------------

@@ -175,13 +175,21 @@ void code_generator::compile() {
         throw gs_error("code_generator::compile: no reduction token set (or a combination not built in this round)");
     }
     if (interleave) {
-        // interleaved storage is consumed by the col-direction chunk kernel (GLOBAL parent)
-        GS_CHECK(s.family == KF_ROW_CHUNKS && interleave_parent == GLOBAL_META,
-                 "interleaved storage is built for col-direction BMT plans at the GLOBAL level only");
+        // interleaved storage is consumed by the col-direction chunk kernel over the BMTs,
+        // interleaved as one run (GLOBAL parent) or per TBLOCK / WARP parent
+        GS_CHECK(s.family == KF_ROW_CHUNKS && s.arrays[0].rfind("THREAD_META", 0) == 0,
+                 "interleaved storage is built for col-direction BMT plans only");
         s.interleaved = true;
-        for (auto k : {"GLOBAL_META_nz_col_indices_after_interlance_storage_0", "GLOBAL_META_nz_vals_after_interlance_storage_0",
-                       "GLOBAL_META_BMT_size_of_each_blk_0"})
+        s.interleave_parent = interleave_parent;
+        for (auto k : {"GLOBAL_META_nz_col_indices_after_interlance_storage_0", "GLOBAL_META_nz_vals_after_interlance_storage_0"})
             s.arrays.push_back(k);
+        const std::string L = interleave_parent == GLOBAL_META ? "GLOBAL_META"
+                              : (interleave_parent == TBLOCK_META ? "TBLOCK_META" : "WARP_META");
+        s.arrays.push_back(L + "_BMT_size_of_each_blk_0");
+        if (interleave_parent != GLOBAL_META) {
+            s.arrays.push_back(L + "_first_BMT_indices_0");
+            s.arrays.push_back(L + "_first_nz_indices_0");
+        }
     }
     for (auto k : {"GLOBAL_META_nz_row_indices_0", "GLOBAL_META_nz_col_indices_0", "GLOBAL_META_nz_vals_0"})
         s.arrays.push_back(k);

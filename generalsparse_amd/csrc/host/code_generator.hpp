@@ -64,7 +64,8 @@ struct kernel_spec {
     POS_TYPE merge_level = GLOBAL_META;    // merge-path plans: the level the operator split
     int work_size = 0;                     // merge-path plans: path steps per level
     POS_TYPE group_level = WARP_META;      // KF_WARP_TOTAL: level whose first_row_indices are the row groups
-    bool interleaved = false;              // cols / vals in interleaved storage (GLOBAL parent)
+    bool interleaved = false;              // cols / vals in interleaved storage
+    int interleave_parent = 0;             // ... per GLOBAL_META (one run of BMTs) or per TBLOCK / WARP parent
     std::array<unsigned, 2> ref_grid{{0, 0}}, ref_block{{0, 0}};
     std::vector<std::string> arrays;  // metadata keys the kernel consumes (= kernel arguments)
     std::string name() const;

@@ -45,7 +45,7 @@ const char kMagic3[8] = {'G', 'S', 'P', 'L', 'A', 'N', '0', '3'};
 void write_spec(writer &w, const kernel_spec &s) {
     w.i64(s.family); w.i64(s.coarsen_factor); w.i64(s.sparse_coarsen_factor); w.i64(s.vector_width);
     w.i64(s.warp_segment); w.i64(s.tblock_parent); w.i64(s.row_sorted); w.i64(s.bitmap_parent);
-    w.i64(s.merge_level); w.i64(s.work_size); w.i64(s.group_level); w.i64(s.interleaved);
+    w.i64(s.merge_level); w.i64(s.work_size); w.i64(s.group_level); w.i64(!s.interleaved ? 0 : (s.interleave_parent == GLOBAL_META ? 1 : 2 + (int64_t)s.interleave_parent));
     w.u64(s.ref_grid[0]); w.u64(s.ref_grid[1]); w.u64(s.ref_block[0]); w.u64(s.ref_block[1]);
     w.u64(s.arrays.size());
     for (auto &a : s.arrays) w.str(a);
@@ -56,7 +56,9 @@ kernel_spec read_spec(reader &r) {
     s.family = (int)r.i64(); s.coarsen_factor = (int)r.i64(); s.sparse_coarsen_factor = (int)r.i64();
     s.vector_width = (int)r.i64(); s.warp_segment = r.i64() != 0; s.tblock_parent = r.i64() != 0;
     s.row_sorted = r.i64() != 0; s.bitmap_parent = (POS_TYPE)r.i64(); s.merge_level = (POS_TYPE)r.i64();
-    s.work_size = (int)r.i64(); s.group_level = (POS_TYPE)r.i64(); s.interleaved = r.i64() != 0;
+    s.work_size = (int)r.i64(); s.group_level = (POS_TYPE)r.i64(); const int64_t il = r.i64();  // 0 none, 1 GLOBAL parent, 2 + pos a TBLOCK / WARP parent
+    s.interleaved = il != 0;
+    s.interleave_parent = il >= 2 ? (int)(il - 2) : (int)GLOBAL_META;
     s.ref_grid[0] = (unsigned)r.u64(); s.ref_grid[1] = (unsigned)r.u64();
     s.ref_block[0] = (unsigned)r.u64(); s.ref_block[1] = (unsigned)r.u64();
     const uint64_t na = r.u64();

@@ -665,7 +665,8 @@ void upload_plan(plan_state &p, int dtype, int device) {
     // interleaved storage (§8f rank 2): the kernel streams the permuted arrays
     const auto &col = m.u(GLOBAL_META, sp.interleaved ? "nz_col_indices_after_interlance_storage" : "nz_col_indices", sb);
     auto vals = m.get_element(GLOBAL_META, sp.interleaved ? "nz_vals_after_interlance_storage" : "nz_vals", sb)->meta_data_arr;
-    if (sp.interleaved) d.ilv = (uint32_t)m.u(GLOBAL_META, "BMT_size_of_each_blk", sb).at(0);
+    if (sp.interleaved && sp.interleave_parent == GLOBAL_META)
+        d.ilv = (uint32_t)m.u(GLOBAL_META, "BMT_size_of_each_blk", sb).at(0);
     uint64_t nnz = col.size();
     GS_CHECK(nnz < 0xffffffffull - kPad, "nnz exceeds 32-bit offsets");
     d.nnz_stored = nnz;
@@ -955,6 +956,23 @@ void upload_plan(plan_state &p, int dtype, int device) {
             d.n_units = br.size();
             d.scf = 4;
             d.span = gsk_host::row_chunk_span(br.size());
+            if (sp.interleaved && sp.interleave_parent != GLOBAL_META) {
+                // per-parent interleaving: BMT b of parent j (first BMT F, first nonzero P, n BMTs)
+                // has its i-th nonzero at P + (b - F) + i * n (k_row_chunks ilv_base / ilv_stride)
+                const POS_TYPE pp = (POS_TYPE)sp.interleave_parent;
+                const auto &pf = m.u(pp, "first_BMT_indices", sb);
+                const auto &pn = m.u(pp, "first_nz_indices", sb);
+                GS_CHECK(pf.size() == pn.size() && !pf.empty() && pf.back() == br.size(),
+                         "interleaved parents: first_BMT_indices / first_nz_indices disagree with the BMTs");
+                std::vector<uint32_t> ib(br.size()), is(br.size());
+                for (size_t j = 0; j + 1 < pf.size(); j++)
+                    for (uint64_t b = pf[j]; b < pf[j + 1]; b++) {
+                        ib[b] = (uint32_t)(pn[j] + (b - pf[j]));
+                        is[b] = (uint32_t)(pf[j + 1] - pf[j]);
+                    }
+                a.a2 = dev_copy(d, ib);
+                a.a3 = dev_copy(d, is);
+            }
             // rows shared by two waves' BMT ranges accumulate in an fp32 workspace; the
             // finalize pass rounds them and writes the rows without BMTs (no memset)
             std::vector<uint32_t> list = gsk_host::row_chunk_finalize_rows(br, p.M, d.span, (uint32_t)d.row_base);
@@ -1426,7 +1444,8 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
             const uint32_t nw = (uint32_t)((d.n_units + d.span - 1) / d.span);
             const uint32_t gx = std::min<uint32_t>((nw + 3) / 4, 1u << 16);
             hipLaunchKernelGGL((gsk::k_row_chunks<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
-                               a.a0, d.f0, a.a1, d.f1, col, val, B, C, a.ws, (uint32_t)d.n_units, d.span, N, X, row_base, d.ilv);
+                               a.a0, d.f0, a.a1, d.f1, col, val, B, C, a.ws, (uint32_t)d.n_units, d.span, N, X, row_base, d.ilv,
+                               a.a2, a.a3);
             if (d.n_fin) {
                 HIP_OK(hipGetLastError());
                 const uint32_t fx = (uint32_t)std::min<uint64_t>((d.n_fin * N + 255) / 256, 4096);

@@ -1232,6 +1232,39 @@ int or_interlance_storage_global(or_set *s) {
     return 0;
 }
 
+/* §8f rank 2 under a TBLOCK / WARP parent (modify_{col,val,row}_indices_by_interlance_storage.cc
+ * :73-118): per parent j, spacing = its BMT count n_j, size = its BMT_size_of_each_blk[j],
+ * offset = the nonzeros of the parents before it (asserted equal to first_nz_indices[j]);
+ * the i-th nonzero of the parent's BMT b moves to offset + b + i * n_j. */
+int or_interlance_storage_parent(or_set *s, const char *pos) {
+    if (!exists(s, pos, "first_BMT_indices", 0) || !exists(s, pos, "BMT_size_of_each_blk", 0))
+        return fail(s, "interleaved storage in a parent needs first_BMT_indices and BMT_size_of_each_blk");
+    or_array *F = get(s, pos, "first_BMT_indices", 0), *Z = get(s, pos, "BMT_size_of_each_blk", 0);
+    or_array *P = get(s, pos, "first_nz_indices", 0);
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    or_array *C = get(s, "GLOBAL_META", "nz_col_indices", 0);
+    or_array *V = get(s, "GLOBAL_META", "nz_vals", 0);
+    uint64_t n = C->len, off = 0;
+    uint64_t *nr = (uint64_t *)calloc(n ? n : 1, sizeof(uint64_t)), *nc = (uint64_t *)calloc(n ? n : 1, sizeof(uint64_t));
+    double *nv = (double *)calloc(n ? n : 1, sizeof(double));
+    for (uint64_t j = 0; j + 1 < F->len; j++) {
+        uint64_t nb = F->u[j + 1] - F->u[j], sz = Z->u[j];
+        if (P && P->u[j] != off) { free(nr); free(nc); free(nv); return fail(s, "parent first nz != interleaved offset"); }
+        if (off + nb * sz > n) { free(nr); free(nc); free(nv); return fail(s, "parent BMTs past the nonzeros"); }
+        for (uint64_t b = 0; b < nb; b++)
+            for (uint64_t i = 0; i < sz; i++) {
+                nc[b + i * nb + off] = C->u[i + b * sz + off];
+                nr[b + i * nb + off] = R->u[i + b * sz + off];
+                nv[b + i * nb + off] = V->f[i + b * sz + off];
+            }
+        off += nb * sz;
+    }
+    put_u(s, "GLOBAL_META", "nz_col_indices_after_interlance_storage", 0, nc, n);
+    put_u(s, "GLOBAL_META", "nz_row_indices_after_interlance_storage", 0, nr, n);
+    put_f(s, "GLOBAL_META", "nz_vals_after_interlance_storage", 0, nv, n);
+    return 0;
+}
+
 /* §8f rank 1: model-driven index compression decision (code_generator.cc:16-40 order;
  * if_linear_compress :2618-2640, if_branch_compress :2642-2670, if_cycle_linear_compress
  * :2672-2715, if_cycle_increase_compress :2717-2760, if_residual_compress :2762-2824 and
@@ -1598,6 +1631,13 @@ int or_pipeline(or_set *s, const char *name, int p0, int p1) {
     if (!strcmp(name, "tblock_col_warp_total")) {
         if (or_row_dir_tblock_blocking(s, p0 > 0 ? p0 : 16)) return -1;
         return or_col_dir_warp_blocking(s, p1 > 0 ? (uint64_t)p1 : 64, 1, 1);
+    }
+    if (!strcmp(name, "tblock_col_thread_interleaved")) { /* the padded plan + per-BMTB interleave */
+        uint64_t c = p1 > 0 ? (uint64_t)p1 : 32;
+        if (col_pad(s, (int)c)) return -1;
+        if (or_row_dir_tblock_blocking(s, p0 > 0 ? p0 : 16)) return -1;
+        if (or_col_dir_thread_in_parent(s, c, 1, 1, 1)) return -1;
+        return or_interlance_storage_parent(s, "TBLOCK_META");
     }
     if (!strcmp(name, "tblock_col_thread_total") || !strcmp(name, "warp_col_thread_total") ||
         !strcmp(name, "tblock_col_thread_total_padded")) {

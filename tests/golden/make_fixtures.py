@@ -300,6 +300,25 @@ cases.append({
     },
 })
 
+# interleaving under a TBLOCK parent: tblock_col_thread_interleaved on ex1 with BMTBs of 4 rows and
+# BMTs of 2.  Rows padded to a multiple of 2 first (pads repeat the row's last col): cols
+# [0 2 | 1 3 4 4 | 0 0 | 0 1 2 3 4 4], rows [0 0 2 2 2 2 3 3 4 4 4 4 4 4]; BMTs b0 (0,2) r0,
+# b1 (1,3) r2, b2 (4,4) r2, b3 (0,0) r3 | b4 (0,1) b5 (2,3) b6 (4,4) r4; BMTBs rows [0,4) [4,6)
+# -> first_BMT [0, 4, 7], sizes [2, 2].  The operator's parent is TBLOCK (a "tblock" distributing
+# operator ran before it, interlance_storage_operator.cc:12-45); per parent
+# (modify_col_indices_by_interlance_storage.cc:73-118) element i of BMT b -> offset + b + i * n:
+# parent 0 (n 4): [b0[0] b1[0] b2[0] b3[0] b0[1] b1[1] b2[1] b3[1]] = [0 1 4 0 2 3 4 0];
+# parent 1 (n 3, offset 8): [0 2 4 1 3 4].
+cases.append({
+    "matrix": "ex1", "pipeline": "tblock_col_thread_interleaved", "p0": 4, "p1": 2,
+    "expect": {
+        B + "first_BMT_indices_0": [0, 4, 7],
+        B + "BMT_size_of_each_blk_0": [2, 2],
+        G + "nz_col_indices_after_interlance_storage_0": [0, 1, 4, 0, 2, 3, 4, 0, 0, 2, 4, 1, 3, 4],
+        G + "nz_row_indices_after_interlance_storage_0": [0, 2, 2, 3, 0, 2, 2, 3, 4, 4, 4, 4, 4, 4],
+    },
+})
+
 # relative BMW indices (§8f rank 1) on ex1 with BMTBs of 4 rows and BMWs of 2 rows:
 # BMTB rows [0,4) and [4,6); BMW starts 0,2 | 4 -> relative 0,2 | 0; row nnz [2,0,3,1,5,0]:
 # BMTB 0 nonzeros before each BMW 0, 2 | BMTB 1: 0

@@ -78,7 +78,8 @@ def test_hand_case_col_warp_and_padding():
 PIPES = [("col_warp_total", 16, 0), ("col_warp_total", 5, 0), ("col_tblock_total", 40, 0),
          ("tblock_col_warp_total", 16, 8), ("tblock_col_warp_total", 7, 3), ("tblock_col_thread_total", 16, 8),
          ("tblock_col_thread_total", 5, 4), ("warp_col_thread_total", 4, 8), ("warp_col_thread_total", 1, 3),
-         ("tblock_col_thread_total_padded", 16, 8), ("tblock_col_thread_total_padded", 3, 4)]
+         ("tblock_col_thread_total_padded", 16, 8), ("tblock_col_thread_total_padded", 3, 4),
+         ("tblock_col_thread_interleaved", 16, 8), ("tblock_col_thread_interleaved", 3, 4)]
 
 
 def _compare(M, K, r, c, v, name, p0, p1):
@@ -153,3 +154,43 @@ def test_plans_on_gpu(pipe, dtype):
             err = np.abs(C - ref) / np.maximum(1.0, np.abs(ref))
             assert err.max() <= (1e-1 if dtype == "f16" else 1e-3), (name, N, err.max())
             plan.free()
+
+
+def test_interleaved_in_tblock_parent_plan_file(tmp_path):
+    """per-BMTB interleaved storage: the compiled spec names the parent, and a plan file keeps
+    it (GSPLAN03 stores 2 + parent level in the interleave field)"""
+    M, K = 120, 70
+    r, c, v = random_coo(M, K, 0.1, 7, empty=0.2)
+    p = gsa.Plan.from_coo(M, K, r, c, v).run_pipeline("tblock_col_thread_interleaved", 32, 8, 4).compile()
+    assert p.info()["kernel_name"] == "k_row_chunks+interleaved"
+    f = str(tmp_path / "ilv.gsplan")
+    p.save(f)
+    q = gsa.Plan.load(f)
+    assert q.info()["kernel_name"] == "k_row_chunks+interleaved"
+    a, b = p.arrays(), q.arrays()
+    for k in ("GLOBAL_META_nz_col_indices_after_interlance_storage_0", "TBLOCK_META_first_BMT_indices_0"):
+        np.testing.assert_array_equal(a[k], b[k])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["f32", "f16"])
+def test_interleaved_in_tblock_parent_loaded_plan_on_gpu(tmp_path, dtype):
+    """the per-BMTB interleaved plan, saved and loaded, computes the same C on the device"""
+    torch = pytest.importorskip("torch")
+    M, K, N = 700, 300, 32
+    row, col, val = ds.random_rows(M, K, 12.0, seed=9, empty_frac=0.1)
+    p = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline("tblock_col_thread_interleaved", N, 16, 8).compile()
+    f = str(tmp_path / "ilv.gsplan")
+    p.save(f)
+    npdt = np.float16 if dtype == "f16" else np.float32
+    B = torch.from_numpy(np.random.default_rng(4).uniform(-1, 1, (K, N)).astype(npdt)).to("cuda:0")
+    Cs = []
+    for plan in (p.upload(dtype, 0), gsa.Plan.load(f).upload(dtype, 0)):
+        assert plan.info()["device_kernel"].startswith("k_row_chunks")
+        Cs.append(plan.spmm(B).float().cpu().numpy())
+        plan.free()
+    v = val.astype(np.float16).astype(np.float32) if dtype == "f16" else val
+    ref = ofi.spmm_ref(M, N, row, col, v, B.float().cpu().numpy(), "f64")
+    for C in Cs:
+        err = np.abs(C - ref) / np.maximum(1.0, np.abs(ref))
+        assert err.max() <= (1e-1 if dtype == "f16" else 1e-3), err.max()
