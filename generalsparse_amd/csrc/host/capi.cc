@@ -335,14 +335,18 @@ void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1)
         const uint64_t units = s.meta->u(name == "col_tblock_total" ? TBLOCK_META : WARP_META, "first_nz_indices", sb).size() - 1;
         ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)std::max<uint64_t>(1, units),
                                                              std::vector<unsigned>{64u, 4u}, cf, ctx));
-    } else if (name == "tblock_col_thread_interleaved") {
+    } else if (name == "tblock_col_thread_interleaved" || name == "warp_col_thread_interleaved") {
         // §8f rank 2 under a parent: tblock_col_thread_total_padded (every row padded to a
         // multiple of p1, BMTs of p1 nonzeros inside BMTBs of p0 rows), then
         // interlance_storage_operator, which takes the TBLOCK level from the distributing
         // operators before it (interlance_storage_operator.cc:12-45) and interleaves the BMTs of
         // each BMTB among themselves (modify_col_indices_by_interlance_storage.cc:73-118)
+        // (warp_: the same inside BMWs of p0 rows, interleaved per BMW)
         const int rb = p0 > 0 ? p0 : 16, c = p1 > 0 ? p1 : 32, cf = 1;
-        ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, rb, false, ctx));
+        if (name == "warp_col_thread_interleaved")
+            ex.add_and_run(std::make_shared<fixed_interval_row_direction_warp_blocking_operator>(cg, rb, false, false, false, ctx));
+        else
+            ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, rb, false, ctx));
         ex.add_and_run(std::make_shared<fixed_interval_col_direction_thread_blocking_operator>(cg, c, true, true, true, false, ctx));
         ex.add_and_run(std::make_shared<interlance_storage_operator>(cg, ctx));
         ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, false, 1, cf, ctx));

@@ -1632,12 +1632,14 @@ int or_pipeline(or_set *s, const char *name, int p0, int p1) {
         if (or_row_dir_tblock_blocking(s, p0 > 0 ? p0 : 16)) return -1;
         return or_col_dir_warp_blocking(s, p1 > 0 ? (uint64_t)p1 : 64, 1, 1);
     }
-    if (!strcmp(name, "tblock_col_thread_interleaved")) { /* the padded plan + per-BMTB interleave */
+    if (!strcmp(name, "tblock_col_thread_interleaved") || !strcmp(name, "warp_col_thread_interleaved")) {
+        /* the padded plan + interleave per BMTB (per BMW) */
+        int warp = !strcmp(name, "warp_col_thread_interleaved");
         uint64_t c = p1 > 0 ? (uint64_t)p1 : 32;
         if (col_pad(s, (int)c)) return -1;
-        if (or_row_dir_tblock_blocking(s, p0 > 0 ? p0 : 16)) return -1;
+        if (warp ? or_row_dir_warp_blocking(s, p0 > 0 ? p0 : 16) : or_row_dir_tblock_blocking(s, p0 > 0 ? p0 : 16)) return -1;
         if (or_col_dir_thread_in_parent(s, c, 1, 1, 1)) return -1;
-        return or_interlance_storage_parent(s, "TBLOCK_META");
+        return or_interlance_storage_parent(s, warp ? "WARP_META" : "TBLOCK_META");
     }
     if (!strcmp(name, "tblock_col_thread_total") || !strcmp(name, "warp_col_thread_total") ||
         !strcmp(name, "tblock_col_thread_total_padded")) {

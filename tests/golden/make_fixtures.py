@@ -319,6 +319,17 @@ cases.append({
     },
 })
 
+# the same inside BMWs of 4 rows (warp_col_thread_interleaved): the operator's parent is WARP
+cases.append({
+    "matrix": "ex1", "pipeline": "warp_col_thread_interleaved", "p0": 4, "p1": 2,
+    "expect": {
+        W + "first_BMT_indices_0": [0, 4, 7],
+        W + "BMT_size_of_each_blk_0": [2, 2],
+        G + "nz_col_indices_after_interlance_storage_0": [0, 1, 4, 0, 2, 3, 4, 0, 0, 2, 4, 1, 3, 4],
+        G + "nz_row_indices_after_interlance_storage_0": [0, 2, 2, 3, 0, 2, 2, 3, 4, 4, 4, 4, 4, 4],
+    },
+})
+
 # relative BMW indices (§8f rank 1) on ex1 with BMTBs of 4 rows and BMWs of 2 rows:
 # BMTB rows [0,4) and [4,6); BMW starts 0,2 | 4 -> relative 0,2 | 0; row nnz [2,0,3,1,5,0]:
 # BMTB 0 nonzeros before each BMW 0, 2 | BMTB 1: 0

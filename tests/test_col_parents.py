@@ -79,7 +79,8 @@ PIPES = [("col_warp_total", 16, 0), ("col_warp_total", 5, 0), ("col_tblock_total
          ("tblock_col_warp_total", 16, 8), ("tblock_col_warp_total", 7, 3), ("tblock_col_thread_total", 16, 8),
          ("tblock_col_thread_total", 5, 4), ("warp_col_thread_total", 4, 8), ("warp_col_thread_total", 1, 3),
          ("tblock_col_thread_total_padded", 16, 8), ("tblock_col_thread_total_padded", 3, 4),
-         ("tblock_col_thread_interleaved", 16, 8), ("tblock_col_thread_interleaved", 3, 4)]
+         ("tblock_col_thread_interleaved", 16, 8), ("tblock_col_thread_interleaved", 3, 4),
+         ("warp_col_thread_interleaved", 8, 8), ("warp_col_thread_interleaved", 1, 4)]
 
 
 def _compare(M, K, r, c, v, name, p0, p1):
