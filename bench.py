@@ -125,7 +125,7 @@ CANDIDATES = [("block_total", 20, 1), ("block_total", 10, 1), ("block_total", 40
 CANDIDATES_C3 = [("col_direction_nm", 32, 1)]
 
 # C1: token_test's default (thread_total, sparse_cf 4) and the row-block / merge-path plans
-CANDIDATES_C1 = [("thread_total", 4, 1), ("tblock_warp_total", 4, 1), ("merge_path", 512, 1)]
+CANDIDATES_C1 = [("thread_total", 4, 1), ("tblock_warp_total", 4, 1), ("tblock_warp_total", 32, 8), ("merge_path", 512, 1)]
 
 # C4: merge-path levels (WARP, work_size p0) and the balanced / row-per-thread plans
 CANDIDATES_C4 = [("merge_path", 256, 1), ("merge_path", 512, 1), ("merge_path", 1024, 1), ("balanced_block_total", 2048, 1),

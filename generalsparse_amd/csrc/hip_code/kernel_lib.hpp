@@ -264,11 +264,15 @@ __device__ __forceinline__ void warp_rows_body(const uint32_t *__restrict__ bmw_
                                                    const uint32_t *__restrict__ row_ptr,        // rows+1 (CSR)
                                                    const CT *__restrict__ col, const VT *__restrict__ val,
                                                    const VT *__restrict__ B, VT *__restrict__ C, uint32_t n_bmw,
-                                                   uint32_t N, uint32_t X, uint32_t row_base) {
+                                                   uint32_t N, uint32_t X, uint32_t row_base, uint32_t G) {
+    // G slots per row (a power of two <= S): the wave takes S/G consecutive rows of the BMW at
+    // a time, so rows much shorter than S*SCF nonzeros do not leave most slots idle (C1: rows
+    // of ~37 nonzeros against 128-nonzero wave passes at N = 8)
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t xl = lane & (X - 1u);
-    const uint32_t slot = lane / X;
-    const uint32_t S = 64u / X;
+    const uint32_t S0 = 64u / X;
+    const uint32_t S = G < S0 ? G : S0, RP = S0 / S;
+    const uint32_t slot = (lane / X) % S, grp = (lane / X) / S;
     const uint32_t wib = threadIdx.x >> 6, wpb = blockDim.x >> 6;
     uint32_t w_begin, w_end, w_step;
     if (bmw_of_bmtb || f_bmw.kind != IDX_ARRAY) {
@@ -288,13 +292,89 @@ __device__ __forceinline__ void warp_rows_body(const uint32_t *__restrict__ bmw_
         for (uint32_t w = w_begin; w < w_end; w += w_step) {
             uint32_t r_begin, r_end;
             idx_range<FX>(bmw_first_row, f_row, w, r_begin, r_end);
-            for (uint32_t r = r_begin; r < r_end; r++) {
+            if (RP > 1 && r_end - r_begin <= 63u) {
+                // grouped passes, software-pipelined: the BMW's row starts in one load (lane i
+                // holds row_ptr[r_begin + i]); the first chunk of pass ps+1 is loaded before the
+                // B gathers of pass ps, so a pass waits on one gather latency, not three
+                typedef typename raw_vec<CF * sizeof(VT)>::t RB;
+                const uint32_t nr = r_end - r_begin, npass = (nr + RP - 1) / RP;
+                const uint32_t rpv = lane <= nr ? row_ptr[r_begin + lane] : 0u;
+                auto bounds = [&](uint32_t ps, uint32_t &b, uint32_t &e) {  // rows past the end: b == e
+                    const uint32_t i = ps * RP + grp;
+                    b = (uint32_t)__shfl((int)rpv, (int)min(i, nr), 64);
+                    e = (uint32_t)__shfl((int)rpv, (int)min(i + 1u, nr), 64);
+                };
+                auto chunk = [&](uint32_t q, uint32_t b, uint32_t e, const CT (&cc)[SCF], const VT (&vv)[SCF],
+                                 float (&acc)[CF]) {
+                    RB braw[SCF];
+#pragma unroll
+                    for (int j = 0; j < SCF; j++) braw[j] = *reinterpret_cast<const RB *>(B + (size_t)cc[j] * N + c0);
+#pragma unroll
+                    for (int j = 0; j < SCF; j++) {
+                        const float v = (q + j >= b && q + j < e) ? (float)vv[j] : 0.f;
+                        VT bt[CF];
+                        __builtin_memcpy(bt, &braw[j], sizeof(RB));
+#pragma unroll
+                        for (int k = 0; k < CF; k++) acc[k] = __builtin_fmaf(v, (float)bt[k], acc[k]);
+                    }
+                };
+                uint32_t b, e;
+                bounds(0u, b, e);
+                uint32_t p = (b & ~(uint32_t)(SCF - 1)) + slot * SCF;
+                CT cn[SCF];
+                VT vn[SCF];
+                if (p < e) {
+                    load_raw<CT, SCF>(col + p, cn);
+                    load_raw<VT, SCF>(val + p, vn);
+                }
+                for (uint32_t ps = 0; ps < npass; ps++) {
+                    CT cc[SCF];
+                    VT vv[SCF];
+#pragma unroll
+                    for (int j = 0; j < SCF; j++) { cc[j] = cn[j]; vv[j] = vn[j]; }
+                    const uint32_t cb = b, ce = e, cp = p;
+                    if (ps + 1 < npass) {
+                        bounds(ps + 1u, b, e);
+                        p = (b & ~(uint32_t)(SCF - 1)) + slot * SCF;
+                        if (p < e) {
+                            load_raw<CT, SCF>(col + p, cn);
+                            load_raw<VT, SCF>(val + p, vn);
+                        }
+                    }
+                    float acc[CF];
+#pragma unroll
+                    for (int k = 0; k < CF; k++) acc[k] = 0.f;
+                    if (cp < ce) {
+                        chunk(cp, cb, ce, cc, vv, acc);
+                        for (uint32_t q = cp + S * SCF; q < ce; q += S * SCF) {  // rest of a long row
+                            CT cq[SCF];
+                            VT vq[SCF];
+                            load_raw<CT, SCF>(col + q, cq);
+                            load_raw<VT, SCF>(val + q, vq);
+                            chunk(q, cb, ce, cq, vq, acc);
+                        }
+                    }
+                    for (uint32_t off = X; off < X * S; off <<= 1) {
+#pragma unroll
+                        for (int k = 0; k < CF; k++) acc[k] += __shfl_xor(acc[k], (int)off, 64);
+                    }
+                    const uint32_t r = r_begin + ps * RP + grp;
+                    if (slot == 0 && cok && r < r_end) store_f32<VT, CF>(C + (size_t)(r + row_base) * N + c0, acc);
+                }
+                continue;
+            }
+            for (uint32_t r0 = r_begin; r0 < r_end; r0 += RP) {
+                const uint32_t r = r0 + grp;
+                const bool live = r < r_end;
                 float acc[CF];
 #pragma unroll
                 for (int k = 0; k < CF; k++) acc[k] = 0.f;
-                wave_row<VT, CT, CF, SCF>(row_ptr[r], row_ptr[r + 1], col, val, B, N, c0, slot, S, acc);
-                wave_reduce_slots<CF>(acc, (int)X);
-                if (slot == 0 && cok) store_f32<VT, CF>(C + (size_t)(r + row_base) * N + c0, acc);
+                if (live) wave_row<VT, CT, CF, SCF>(row_ptr[r], row_ptr[r + 1], col, val, B, N, c0, slot, S, acc);
+                for (uint32_t off = X; off < X * S; off <<= 1) {
+#pragma unroll
+                    for (int k = 0; k < CF; k++) acc[k] += __shfl_xor(acc[k], (int)off, 64);
+                }
+                if (slot == 0 && cok && live) store_f32<VT, CF>(C + (size_t)(r + row_base) * N + c0, acc);
             }
         }
     }
@@ -305,13 +385,14 @@ __global__ __launch_bounds__(256) void k_warp_rows(const uint32_t *__restrict__ 
                                                    const uint32_t *__restrict__ bmw_of_bmtb, const idx_formula f_bmw,
                                                    const uint32_t *__restrict__ row_ptr, const CT *__restrict__ col,
                                                    const VT *__restrict__ val, const VT *__restrict__ B, VT *__restrict__ C,
-                                                   uint32_t n_bmw, uint32_t N, uint32_t X, uint32_t row_base) {
+                                                   uint32_t n_bmw, uint32_t N, uint32_t X, uint32_t row_base,
+                                                   uint32_t G = 64) {
     if (f_row.kind == IDX_ARRAY && f_bmw.kind == IDX_ARRAY)
         warp_rows_body<VT, CT, CF, SCF, false>(bmw_first_row, f_row, bmw_of_bmtb, f_bmw, row_ptr, col, val, B, C, n_bmw, N, X,
-                                               row_base);
+                                               row_base, G);
     else
         warp_rows_body<VT, CT, CF, SCF, true>(bmw_first_row, f_row, bmw_of_bmtb, f_bmw, row_ptr, col, val, B, C, n_bmw, N, X,
-                                              row_base);
+                                              row_base, G);
 }
 
 // ---------------------------------------------------------------------------

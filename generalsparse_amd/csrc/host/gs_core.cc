@@ -108,6 +108,7 @@ void apply_kv(config_t &c, const std::string &k, const std::string &v) {
     else if (k == "MFMA_TILES") c.MFMA_TILES = b();
     else if (k == "MFMA_MAX_FILL") c.MFMA_MAX_FILL = i();
     else if (k == "MFMA_KROT") c.MFMA_KROT = i();
+    else if (k == "WARP_ROWS_GROUPS") c.WARP_ROWS_GROUPS = i();
     else if (k == "MFMA_KSPLIT") c.MFMA_KSPLIT = i();
     else if (k == "NM_MFMA") c.NM_MFMA = b();
     // unknown keys are ignored, as the reference ignores 17 of its 36 keys

@@ -81,7 +81,8 @@ struct config_t {
     // MI355X engine switches (not in the reference)
     bool LDS_STAGE_B = true;  // warp_total inside BMTBs: stage B chunks in LDS (k_lds_rows)
     bool MFMA_TILES = true;   // fp16 BMTB row blocks on the matrix cores (k_mfma_rows)
-    int64_t MFMA_KROT = 0;    // k_mfma_rows / k_nm_mfma: each workgroup starts at its own K chunk
+    int64_t MFMA_KROT = 0;
+    int64_t WARP_ROWS_GROUPS = 1;  // k_warp_rows: several short rows of a BMW per wave pass    // k_mfma_rows / k_nm_mfma: each workgroup starts at its own K chunk
     int64_t MFMA_MAX_FILL = 16;  // ... when (padded row-block area) / nnz <= this
     bool NM_MFMA = true;         // col-direction plans whose rows are 2:4 panels: sparse matrix cores (k_nm_mfma)
     int64_t MFMA_KSPLIT = 0;     // workgroups per row block (K ranges); 0 = fill the 256 CUs

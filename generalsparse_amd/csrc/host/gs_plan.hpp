@@ -48,6 +48,8 @@ struct device_plan {
     uint32_t ws_n = 0;             // bitmap family: dense width of the fp32 workspace
     uint64_t n_fin = 0;            // bitmap family: rows k_finalize_rows writes
     uint32_t span = 0;             // k_row_chunks: BMTs per wave
+    uint32_t bmw_rows_max = 0;     // k_warp_rows: most rows in one BMW
+    double mean_row_nnz = 0.0;     // ... and the mean row length (slots per row)
     uint32_t ilv = 0;              // k_row_chunks: BMT size of an interleaved layout (0: contiguous)
     uint32_t lds_N = 0, KC = 0, nc = 0, RSB = 0, rpw_max = 0, seg_cap = 0, waves = 0, maxr = 0;
     size_t lds_bytes = 0, bytes_tile = 0;

@@ -834,6 +834,13 @@ void upload_plan(plan_state &p, int dtype, int device) {
             std::vector<uint32_t> rp = csr_row_ptr(rows, row_num);
             a.a2 = dev_copy(d, rp);
             d.n_units = m.u(sp.group_level, "first_row_indices", sb).size() - 1;
+            {
+                const auto &gr = m.u(sp.group_level, "first_row_indices", sb);
+                uint64_t mx = 0;
+                for (size_t i = 0; i + 1 < gr.size(); i++) mx = std::max<uint64_t>(mx, gr[i + 1] - gr[i]);
+                d.bmw_rows_max = (uint32_t)mx;
+                d.mean_row_nnz = row_num ? (double)rp.back() / (double)row_num : 0.0;
+            }
             d.scf = 4;
             if (sp.tblock_parent && try_mfma(rp)) {
                 upload_groups(true);  // the gather fallback at other dense widths
@@ -1408,9 +1415,16 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
             uint32_t gx;
             if (sp.tblock_parent) gx = (uint32_t)d.n_rows_aux;
             else gx = (uint32_t)std::min<uint64_t>((d.n_units + 3) / 4, 1u << 16);
+            // slots per row: enough SCF-chunks for the plan's mean row, the rest of the wave on the
+            // next rows of the BMW (only when BMWs hold several rows)
+            uint32_t G = 64u / X;
+            if (d.bmw_rows_max > 1 && get_config().WARP_ROWS_GROUPS) {
+                const uint32_t need = (uint32_t)std::max<double>(1.0, std::ceil(d.mean_row_nnz / 4.0));
+                G = std::min<uint32_t>(G, pow2ceil(need));
+            }
             hipLaunchKernelGGL((gsk::k_warp_rows<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
                                a.a0, d.f0, sp.tblock_parent ? a.a1 : nullptr, sp.tblock_parent ? d.f1 : gsk::idx_formula(), a.a2, col, val, B, C, (uint32_t)d.n_units, N,
-                               X, row_base);
+                               X, row_base, G);
             break;
         }
         case KF_BLOCK_TOTAL: {

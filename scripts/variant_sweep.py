@@ -2,6 +2,7 @@
 usage: variant_sweep.py <c1|c2|c4> dtype N pipeline:p0:p1 [pipeline:p0:p1 ...]"""
 import os
 import sys
+import time
 
 import torch
 
@@ -32,13 +33,17 @@ for spec in sys.argv[4:]:
     Cs = [torch.empty((M, N), device="cuda", dtype=tdt) for _ in range(reps)]
     plan.spmm_rotate(10, 0, Bs, Cs)
     torch.cuda.synchronize()
+    t_end = time.perf_counter() + 0.3  # clocks up before timing
+    while time.perf_counter() < t_end:
+        plan.spmm_rotate(reps, 0, Bs, Cs)
+        torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     plan.spmm_rotate(100, 0, Bs, Cs)
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / 100 * 1e3
-    print(f"{wl} {dtype} N={N} {name}({p0},{p1}) {info['kernel_name']}: {us:.2f} us, "
+    print(f"{wl} {dtype} N={N} {name}({p0},{p1}) {info.get('device_kernel') or info['kernel_name']}: {us:.2f} us, "
           f"{2.0 * len(row) * N / us / 1e3:.1f} GFLOP/s, A bytes {info['device_bytes_A']}", flush=True)
     plan.free()
     del Bs, Cs

@@ -21,7 +21,8 @@ DEV = "cuda:0"
 PIPES = [("thread_total", 4, 1), ("thread_total", 8, 1), ("warp_total", 0, 1), ("block_total", 0, 1),
          ("block_total", 20, 1),
          ("thread_bit_map", 4, 1), ("warp_segment", 4, 1), ("tblock_warp_total", 4, 1),
-         ("tblock_warp_total", 16, 1), ("balanced_warp_total", 256, 1),
+         ("tblock_warp_total", 16, 1), ("tblock_warp_total", 32, 8), ("tblock_warp_total", 64, 16),
+         ("balanced_warp_total", 256, 1),
          ("merge_path", 1024, 1), ("merge_path", 64, 1), ("merge_path", 7, 3), ("merge_path", 4096, 2),
          ("balanced_block_total", 512, 1), ("balanced_thread_total", 64, 1),
          ("tblock_thread_total", 16, 1), ("tblock_thread_total", 20, 3), ("tblock_warp_thread_total", 16, 2)]
@@ -627,3 +628,21 @@ def test_divided_plan_file_computes_the_same(tmp_path):
     torch.cuda.synchronize()
     assert not torch.isnan(C2).any()
     assert torch.equal(C1, C2)
+
+
+@pytest.mark.parametrize("groups", [1, 0])
+@pytest.mark.parametrize("N", [8, 32])
+def test_warp_rows_grouped_passes(groups, N):
+    """k_warp_rows with several short rows of a BMW per wave pass (WARP_ROWS_GROUPS, the
+    software-pipelined path; C1-like rows of ~37 nonzeros in BMWs of 8 rows) and without:
+    both match the oracle"""
+    M, K = 3000, 2000
+    row, col, val = ds.random_rows(M, K, 37.0, seed=6, empty_frac=0.05)
+    gsa.set_config("WARP_ROWS_GROUPS", groups)
+    try:
+        plan, C, B = run(M, K, row, col, val, "tblock_warp_total", 32, 8, N, "f32")
+    finally:
+        gsa.set_config("WARP_ROWS_GROUPS", 1)
+    assert plan.info()["device_kernel"].startswith("k_warp_rows"), plan.info()["device_kernel"]
+    check(C, ofi.spmm_ref(M, N, row, col, val, B, "f64"), "f32")
+    plan.free()
