@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-2 bench lines of every BASELINE config + rocprofv3 kernel stats (profiles/r02_*).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/r02
+OUT=gpurun_out/${TAG:-r02}
 mkdir -p $OUT
 export TMPDIR=/tmp
 set -e
