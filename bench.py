@@ -328,6 +328,15 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
               bt.C5_SHAPES[k][0] * N * e for (_, _, k) in batch)
     ms = wall / args.steps * 1e3
     info = next(iter(plans.values())).info()
+    # HBM bytes per step from the PMC passes of scripts/gpu_traffic_c5.sh (per GPU: the LPT
+    # split is balanced on nnz); only for the full 48-layer batch it was scaled to
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "traffic_c5.json")
+    if os.path.exists(tf) and args.layers == 48:
+        try:
+            traffic = int(json.load(open(tf))["hbm_bytes_per_step"] / world)
+        except Exception:
+            traffic = None
     out = {
         "metric": "SpMM GFLOP/s, OPT-30B 80%-pruned weight batch fp16 N=32 (configs[4])",
         "value": round(value, 1), "unit": "GFLOP/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -341,7 +350,7 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
                    "parallelism": f"LPT batch split x{world} (max rank nnz share {max(load) / total_nnz:.4f})"},
         "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9 / world, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / world / HBM_PEAK_GBS, 4),
-                     "traffic": None, "algorithmic_bytes_per_step": alg, "note": "per GPU, whole step"},
+                     "traffic": traffic, "algorithmic_bytes_per_step": alg, "note": "per GPU, whole step"},
         "setup_s": round(t_setup, 1),
     }
     if rank == 0:
