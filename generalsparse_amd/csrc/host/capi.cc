@@ -335,6 +335,19 @@ void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1)
         const uint64_t units = s.meta->u(name == "col_tblock_total" ? TBLOCK_META : WARP_META, "first_nz_indices", sb).size() - 1;
         ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)std::max<uint64_t>(1, units),
                                                              std::vector<unsigned>{64u, 4u}, cf, ctx));
+    } else if (name == "tblock_col_thread_maxpad" || name == "warp_col_thread_maxpad") {
+        // col-direction BMTs of p1 nonzeros inside BMTBs (BMWs) of p0 rows, every non-empty row
+        // first padded to its parent's longest row (is_col_padding_with_row_max_size_without_empty_row,
+        // modify_*_by_col_pad_parent_blk_to_max_row_size; the parent level is then rebuilt)
+        const int rb = p0 > 0 ? p0 : 16, c = p1 > 0 ? p1 : 32, cf = 1;
+        if (name == "warp_col_thread_maxpad")
+            ex.add_and_run(std::make_shared<fixed_interval_row_direction_warp_blocking_operator>(cg, rb, false, false, false, ctx));
+        else
+            ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, rb, false, ctx));
+        ex.add_and_run(std::make_shared<fixed_interval_col_direction_thread_blocking_operator>(cg, c, true, true, false, true, ctx));
+        ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, false, 1, cf, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)((rows + rb - 1) / rb),
+                                                             std::vector<unsigned>{64u, 4u}, cf, ctx));
     } else if (name == "tblock_col_thread_interleaved" || name == "warp_col_thread_interleaved") {
         // §8f rank 2 under a parent: tblock_col_thread_total_padded (every row padded to a
         // multiple of p1, BMTs of p1 nonzeros inside BMTBs of p0 rows), then

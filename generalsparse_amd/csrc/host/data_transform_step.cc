@@ -220,7 +220,7 @@ void modify_row_indices_by_empty_pad_in_submatrix::run(bool check) {
 // padded entries repeat the row's last column with value 0
 namespace {
 struct col_pad_plan {
-    std::vector<uint64_t> start, cnt;  // per row
+    std::vector<uint64_t> start, cnt, tgt;  // per row (tgt: max-row padding only)
     uint64_t after = 0;
     bool padded = false;
 };
@@ -288,6 +288,92 @@ void modify_row_indices_by_col_pad_in_sub_matrix::run(bool check) {
     if (p.padded) {
         const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
         auto nr = apply_col_pad<uint64_t>(p, multiple_of_each_row_size, [&](uint64_t k, bool) { return row[k]; }, 0);
+        src(GLOBAL_META, "nz_row_indices");
+        replace_u(GLOBAL_META, "nz_row_indices", std::move(nr));
+    }
+    is_run = true;
+}
+
+// ------------------------------------------- col pad to the parent's max row
+// modify_{col,vals,row}_*_by_col_pad_parent_blk_to_max_row_size.cc (padding_with_empty_row
+// false): rows [0, row_num) with row_num from the sub-matrix's row range widened to its last
+// nonzero's row (:40-52); per parent (GLOBAL: all rows; TBLOCK / WARP: first_row_indices
+// ranges) every non-empty row grows to the parent's longest row, pads repeating the row's last
+// column with value 0; the padding rate is checked against PADDING_RATE_UP_BOUND (:95-103)
+namespace {
+col_pad_plan make_max_pad(const meta_data_set &m, int s, POS_TYPE pos, bool check) {
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    GS_CHECK(!row.empty(), "max-row padding of an empty sub-matrix");
+    const uint64_t b = m.scalar(GLOBAL_META, "begin_row_index", s);
+    uint64_t e = m.scalar(GLOBAL_META, "end_row_index", s);
+    e = std::max<uint64_t>(e, b + row.back());
+    const uint64_t row_num = e - b + 1;
+    col_pad_plan p;
+    p.cnt = get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+    p.start.assign(row_num + 1, 0);
+    for (uint64_t r = 0; r < row_num; r++) p.start[r + 1] = p.start[r] + p.cnt[r];
+    p.tgt = p.cnt;
+    std::vector<uint64_t> bounds;
+    if (pos == GLOBAL_META) bounds = {0, row_num};
+    else bounds = m.u(pos, "first_row_indices", s);
+    for (size_t i = 0; i + 1 < bounds.size(); i++) {
+        uint64_t mx = 0;
+        for (uint64_t r = bounds[i]; r < bounds[i + 1] && r < row_num; r++) mx = std::max(mx, p.cnt[r]);
+        for (uint64_t r = bounds[i]; r < bounds[i + 1] && r < row_num; r++)
+            if (mx && p.cnt[r]) {
+                p.tgt[r] = mx;
+                p.padded = true;  // the reference rewrites the arrays once any row is visited
+            }
+    }
+    p.after = 0;
+    for (uint64_t r = 0; r < row_num; r++) p.after += p.tgt[r];
+    if (check && (double)p.after / (double)row.size() >= padding_bound())
+        throw gs_error("max-row padding rate " + std::to_string((double)p.after / row.size()) +
+                       " >= PADDING_RATE_UP_BOUND (modify_col_indices_by_col_pad_parent_blk_to_max_row_size.cc:95-103)");
+    return p;
+}
+template <class T, class F>
+std::vector<T> apply_max_pad(const col_pad_plan &p, F src_at) {
+    std::vector<T> out;
+    out.reserve(p.after);
+    for (uint64_t r = 0; r + 1 < p.start.size(); r++) {
+        for (uint64_t k = p.start[r]; k < p.start[r + 1]; k++) out.push_back(src_at(k, false));
+        for (uint64_t k = p.cnt[r]; k < p.tgt[r]; k++) out.push_back(src_at(p.start[r + 1] - 1, true));
+    }
+    return out;
+}
+}  // namespace
+
+void modify_col_indices_by_col_pad_parent_blk_to_max_row_size::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    auto p = make_max_pad(m, target_matrix_id, parent_pos, check);
+    if (p.padded) {
+        const auto &col = m.u(GLOBAL_META, "nz_col_indices", target_matrix_id);
+        auto nc = apply_max_pad<uint64_t>(p, [&](uint64_t k, bool) { return col[k]; });
+        src(GLOBAL_META, "nz_col_indices");
+        replace_u(GLOBAL_META, "nz_col_indices", std::move(nc));
+    }
+    is_run = true;
+}
+
+void modify_vals_by_col_pad_parent_blk_to_max_row_size::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    auto p = make_max_pad(m, target_matrix_id, parent_pos, check);
+    if (p.padded) {
+        auto va = m.get_element(GLOBAL_META, "nz_vals", target_matrix_id)->meta_data_arr;
+        auto nv = apply_max_pad<double>(p, [&](uint64_t k, bool pad) { return pad ? 0.0 : va->read_float_from_arr(k); });
+        src(GLOBAL_META, "nz_vals");
+        replace_f(GLOBAL_META, "nz_vals", std::move(nv), va->get_data_type());
+    }
+    is_run = true;
+}
+
+void modify_row_indices_by_col_pad_parent_blk_to_max_row_size::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    auto p = make_max_pad(m, target_matrix_id, parent_pos, check);
+    if (p.padded) {
+        const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+        auto nr = apply_max_pad<uint64_t>(p, [&](uint64_t k, bool) { return row[k]; });
         src(GLOBAL_META, "nz_row_indices");
         replace_u(GLOBAL_META, "nz_row_indices", std::move(nr));
     }

@@ -991,18 +991,37 @@ bool fixed_interval_col_direction_thread_blocking_operator::is_valid_according_t
 // ...col_direction_thread_blocking_operator.cc:297-368 (shared by the WARP / THREAD col-direction
 // operators): pad every row to a multiple of c, drop the parent levels and run the former
 // operators again on the padded COO with their own padding off
-static void col_pad_and_rerun(const std::shared_ptr<meta_data_set> &m, int s, int c, bool drop_tblock, bool drop_warp,
-                              const std::vector<std::shared_ptr<basic_operator>> &former, bool check,
-                              std::vector<std::string> &seq) {
-    modify_col_indices_by_col_pad_in_sub_matrix a(m, s, c);
+// (max_pad: first every non-empty row to its max_pos parent's longest row, :297-310;
+// col_size: then to a multiple of c, :313-326; either one drops and rebuilds the parents)
+static void run_max_row_pad(const std::shared_ptr<meta_data_set> &m, int s, POS_TYPE pos, bool check,
+                            std::vector<std::string> &seq) {
+    modify_col_indices_by_col_pad_parent_blk_to_max_row_size a(m, s, pos);
     a.run(check);
     seq.push_back(a.convert_to_string());
-    modify_vals_by_col_pad_in_sub_matrix b(m, s, c);
+    modify_vals_by_col_pad_parent_blk_to_max_row_size b(m, s, pos);
     b.run(check);
     seq.push_back(b.convert_to_string());
-    modify_row_indices_by_col_pad_in_sub_matrix r(m, s, c);
+    modify_row_indices_by_col_pad_parent_blk_to_max_row_size r(m, s, pos);
     r.run(check);
     seq.push_back(r.convert_to_string());
+}
+
+static void col_pad_and_rerun(const std::shared_ptr<meta_data_set> &m, int s, int c, bool drop_tblock, bool drop_warp,
+                              const std::vector<std::shared_ptr<basic_operator>> &former, bool check,
+                              std::vector<std::string> &seq, bool col_size = true, bool max_pad = false,
+                              POS_TYPE max_pos = GLOBAL_META) {
+    if (max_pad) run_max_row_pad(m, s, max_pos, check, seq);
+    if (col_size) {
+        modify_col_indices_by_col_pad_in_sub_matrix a(m, s, c);
+        a.run(check);
+        seq.push_back(a.convert_to_string());
+        modify_vals_by_col_pad_in_sub_matrix b(m, s, c);
+        b.run(check);
+        seq.push_back(b.convert_to_string());
+        modify_row_indices_by_col_pad_in_sub_matrix r(m, s, c);
+        r.run(check);
+        seq.push_back(r.convert_to_string());
+    }
     for (POS_TYPE pos : {TBLOCK_META, WARP_META}) {
         if ((pos == TBLOCK_META && !drop_tblock) || (pos == WARP_META && !drop_warp)) continue;
         for (const auto &n : m->all_item_of_metadata_of_diff_pos(pos, s)) {
@@ -1023,12 +1042,11 @@ static void col_pad_and_rerun(const std::shared_ptr<meta_data_set> &m, int s, in
 // ...col_direction_thread_blocking_operator.cc:260-487
 void fixed_interval_col_direction_thread_blocking_operator::run(bool check) {
     if (check) GS_CHECK(is_valid_according_to_metadata(), "col-direction thread blocking: invalid metadata");
-    if (is_col_padding_with_row_max_size_without_empty_row)
-        throw gs_error("col padding to the parent's max row size (modify_*_by_col_pad_parent_blk_to_max_row_size) is not built");
     const bool bmtb = has(TBLOCK_META, "first_row_indices"), bmw = has(WARP_META, "first_row_indices");
     const int c = fixed_col_block_size;
-    if (is_padding_with_col_size_in_bmt) {  // :313-368
-        col_pad_and_rerun(meta_data_set_ptr, target_matrix_id, c, bmtb, bmw, former_operator, check, transform_seq);
+    if (is_padding_with_col_size_in_bmt || is_col_padding_with_row_max_size_without_empty_row) {  // :297-368
+        col_pad_and_rerun(meta_data_set_ptr, target_matrix_id, c, bmtb, bmw, former_operator, check, transform_seq,
+                          is_padding_with_col_size_in_bmt, is_col_padding_with_row_max_size_without_empty_row, padding_pos);
     }
     get_begin_rows_of_BMT_after_fixed_blocking_in_col_direction e(meta_data_set_ptr, target_matrix_id, c);
     run_step(e, check);
@@ -1103,9 +1121,9 @@ bool fixed_interval_col_direction_tblock_blocking_operator::is_valid_according_t
 // :130-201
 void fixed_interval_col_direction_tblock_blocking_operator::run(bool check) {
     if (check) GS_CHECK(is_valid_according_to_metadata(), "col-direction tblock blocking: invalid metadata");
-    if (is_col_padding_with_row_max_size_without_empty_row)
-        throw gs_error("col padding to the parent's max row size (modify_*_by_col_pad_parent_blk_to_max_row_size) is not built");
     const int c = fixed_col_block_size;
+    if (is_col_padding_with_row_max_size_without_empty_row)  // :149-162, GLOBAL parent
+        run_max_row_pad(meta_data_set_ptr, target_matrix_id, GLOBAL_META, check, transform_seq);
     if (is_padding_with_col_size_in_bmtb) {
         modify_col_indices_by_col_pad_in_sub_matrix a(meta_data_set_ptr, target_matrix_id, c);
         run_step(a, check);
@@ -1168,12 +1186,11 @@ bool fixed_interval_col_direction_warp_blocking_operator::is_valid_according_to_
 // :192-372
 void fixed_interval_col_direction_warp_blocking_operator::run(bool check) {
     if (check) GS_CHECK(is_valid_according_to_metadata(), "col-direction warp blocking: invalid metadata");
-    if (is_col_padding_with_row_max_size_without_empty_row)
-        throw gs_error("col padding to the parent's max row size (modify_*_by_col_pad_parent_blk_to_max_row_size) is not built");
     const bool bmtb = has(TBLOCK_META, "first_row_indices");
     const int c = fixed_col_block_size;
-    if (is_padding_with_col_size_in_bmw)
-        col_pad_and_rerun(meta_data_set_ptr, target_matrix_id, c, bmtb, false, former_operator, check, transform_seq);
+    if (is_padding_with_col_size_in_bmw || is_col_padding_with_row_max_size_without_empty_row)  // :242-290
+        col_pad_and_rerun(meta_data_set_ptr, target_matrix_id, c, bmtb, false, former_operator, check, transform_seq,
+                          is_padding_with_col_size_in_bmw, is_col_padding_with_row_max_size_without_empty_row, padding_pos);
     get_begin_rows_of_BMW_after_fixed_blocking_in_col_direction d(meta_data_set_ptr, target_matrix_id, c);
     run_step(d, check);
     get_begin_nzs_of_BMW_after_fixed_blocking_in_col_direction e(meta_data_set_ptr, target_matrix_id, c);

@@ -412,6 +412,46 @@ static int col_pad(or_set *s, int mult) {
     return 0;
 }
 
+/* modify_{col,vals,row}_*_by_col_pad_parent_blk_to_max_row_size.cc (padding_with_empty_row
+ * false): rows [0, row_num), row_num = max(end_row_index, begin + last nonzero's row) - begin
+ * + 1 (:40-52); parents = all rows (interval 0, GLOBAL) or fixed row intervals (the parent
+ * level's first_row_indices of a fixed row-direction blocking); every non-empty row grows to
+ * its parent's longest row, pads repeating the row's last column with value 0 (:54-103). */
+static int col_pad_max(or_set *s, uint64_t interval) {
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    or_array *C = get(s, "GLOBAL_META", "nz_col_indices", 0);
+    or_array *V = get(s, "GLOBAL_META", "nz_vals", 0);
+    uint64_t nnz = R->len;
+    if (!nnz) return fail(s, "max-row padding of an empty sub-matrix");
+    uint64_t b = scalar(s, "GLOBAL_META", "begin_row_index", 0), e = scalar(s, "GLOBAL_META", "end_row_index", 0);
+    if (b + R->u[nnz - 1] > e) e = b + R->u[nnz - 1];
+    uint64_t row_num = e - b + 1;
+    uint64_t *cnt = row_nnz(R->u, nnz, row_num);
+    uint64_t *tgt = (uint64_t *)malloc(row_num * 8);
+    uint64_t iv = interval ? interval : row_num, after = 0;
+    for (uint64_t p0 = 0; p0 < row_num; p0 += iv) {
+        uint64_t p1 = p0 + iv < row_num ? p0 + iv : row_num, mx = 0;
+        for (uint64_t r = p0; r < p1; r++) if (cnt[r] > mx) mx = cnt[r];
+        for (uint64_t r = p0; r < p1; r++) { tgt[r] = (mx && cnt[r]) ? mx : cnt[r]; after += tgt[r]; }
+    }
+    if ((double)after / (double)nnz >= PADDING_RATE_UP_BOUND) { /* :95-103 */
+        free(cnt); free(tgt);
+        return fail(s, "max-row padding rate %.3f >= %d", (double)after / nnz, PADDING_RATE_UP_BOUND);
+    }
+    uint64_t *nr = (uint64_t *)malloc(after * 8), *nc = (uint64_t *)malloc(after * 8);
+    double *nv = (double *)malloc(after * 8);
+    uint64_t p = 0, q = 0;
+    for (uint64_t r = 0; r < row_num; r++) {
+        for (uint64_t k = 0; k < cnt[r]; k++, q++) { nr[p] = R->u[q]; nc[p] = C->u[q]; nv[p] = V->f[q]; p++; }
+        for (uint64_t k = cnt[r]; k < tgt[r]; k++) { nr[p] = nr[p - 1]; nc[p] = nc[p - 1]; nv[p] = 0.0; p++; }
+    }
+    free(cnt); free(tgt);
+    put_u(s, "GLOBAL_META", "nz_col_indices", 0, nc, after);
+    put_f(s, "GLOBAL_META", "nz_vals", 0, nv, after);
+    put_u(s, "GLOBAL_META", "nz_row_indices", 0, nr, after);
+    return 0;
+}
+
 /* ------------------------------------------------------------------ */
 /* A5/A7: fixed_interval_row_direction_thread_blocking_operator,        */
 /* no-parent branch (operator/...thread_blocking_operator.cc:482-565)   */
@@ -1631,6 +1671,14 @@ int or_pipeline(or_set *s, const char *name, int p0, int p1) {
     if (!strcmp(name, "tblock_col_warp_total")) {
         if (or_row_dir_tblock_blocking(s, p0 > 0 ? p0 : 16)) return -1;
         return or_col_dir_warp_blocking(s, p1 > 0 ? (uint64_t)p1 : 64, 1, 1);
+    }
+    if (!strcmp(name, "tblock_col_thread_maxpad") || !strcmp(name, "warp_col_thread_maxpad")) {
+        /* every non-empty row padded to its BMTB's (BMW's) longest row, then BMTs of p1 in it */
+        int warp = !strcmp(name, "warp_col_thread_maxpad");
+        uint64_t rb = p0 > 0 ? (uint64_t)p0 : 16, c = p1 > 0 ? (uint64_t)p1 : 32;
+        if (col_pad_max(s, rb)) return -1;
+        if (warp ? or_row_dir_warp_blocking(s, (int)rb) : or_row_dir_tblock_blocking(s, (int)rb)) return -1;
+        return or_col_dir_thread_in_parent(s, c, 1, 1, 0);
     }
     if (!strcmp(name, "tblock_col_thread_interleaved") || !strcmp(name, "warp_col_thread_interleaved")) {
         /* the padded plan + interleave per BMTB (per BMW) */

@@ -330,6 +330,24 @@ cases.append({
     },
 })
 
+# col padding to the parent's longest row (modify_*_by_col_pad_parent_blk_to_max_row_size.cc,
+# padding_with_empty_row false) in tblock_col_thread_maxpad on ex1, BMTBs of 4 rows, BMTs of 2:
+# row nnz [2,0,3,1,5,0]; parent rows [0,4) max 3: row0 -> 3 (one pad, col 2), row1 stays empty,
+# row3 -> 3 (two pads, col 0); parent [4,6) max 5.  Cols [0 2 2 | 1 3 4 | 0 0 0 | 0 1 2 3 4],
+# vals [1 2 0 | 3 4 5 | 6 0 0 | 7 8 9 10 11]; the BMTB level is rebuilt on the padded COO
+# (first nz 0, 9, 14); each row cut into chunks of 2: starts 0 2 | 3 5 | 6 8 | 9 11 13, end 14.
+cases.append({
+    "matrix": "ex1", "pipeline": "tblock_col_thread_maxpad", "p0": 4, "p1": 2,
+    "expect": {
+        G + "nz_col_indices_0": [0, 2, 2, 1, 3, 4, 0, 0, 0, 0, 1, 2, 3, 4],
+        G + "nz_row_indices_0": [0, 0, 0, 2, 2, 2, 3, 3, 3, 4, 4, 4, 4, 4],
+        G + "nz_vals_0": [1, 2, 0, 3, 4, 5, 6, 0, 0, 7, 8, 9, 10, 11],
+        B + "first_nz_indices_0": [0, 9, 14],
+        T + "first_nz_indices_0": [0, 2, 3, 5, 6, 8, 9, 11, 13, 14],
+        T + "first_row_indices_without_ending_0": [0, 0, 2, 2, 3, 3, 4, 4, 4],
+    },
+})
+
 # relative BMW indices (§8f rank 1) on ex1 with BMTBs of 4 rows and BMWs of 2 rows:
 # BMTB rows [0,4) and [4,6); BMW starts 0,2 | 4 -> relative 0,2 | 0; row nnz [2,0,3,1,5,0]:
 # BMTB 0 nonzeros before each BMW 0, 2 | BMTB 1: 0

@@ -80,7 +80,9 @@ PIPES = [("col_warp_total", 16, 0), ("col_warp_total", 5, 0), ("col_tblock_total
          ("tblock_col_thread_total", 5, 4), ("warp_col_thread_total", 4, 8), ("warp_col_thread_total", 1, 3),
          ("tblock_col_thread_total_padded", 16, 8), ("tblock_col_thread_total_padded", 3, 4),
          ("tblock_col_thread_interleaved", 16, 8), ("tblock_col_thread_interleaved", 3, 4),
-         ("warp_col_thread_interleaved", 8, 8), ("warp_col_thread_interleaved", 1, 4)]
+         ("warp_col_thread_interleaved", 8, 8), ("warp_col_thread_interleaved", 1, 4),
+         ("tblock_col_thread_maxpad", 16, 8), ("tblock_col_thread_maxpad", 3, 4),
+         ("warp_col_thread_maxpad", 8, 8), ("warp_col_thread_maxpad", 1, 2)]
 
 
 def _compare(M, K, r, c, v, name, p0, p1):
@@ -132,8 +134,12 @@ def test_validity_rules():
     q = gsa.Plan.from_coo(M, K, r, c, v)
     with pytest.raises(gsa.GsError):  # relative BMW indices without a BMTB
         q.add_operator("fixed_interval_col_direction_warp_blocking_operator", 16, 1, 0, 0, 0)
-    with pytest.raises(gsa.GsError):  # padding to the parent's max row size is not built
-        q.add_operator("fixed_interval_col_direction_warp_blocking_operator", 16, 0, 0, 0, 1)
+    # padding to the parent's max row size at GLOBAL level (no parent): every non-empty row to
+    # the longest row, then col-direction BMWs of 16
+    q.add_operator("fixed_interval_col_direction_warp_blocking_operator", 16, 0, 0, 0, 1)
+    a = q.arrays()
+    cnt = np.bincount(a["GLOBAL_META_nz_row_indices_0"].astype(np.int64), minlength=M)
+    assert set(cnt[cnt > 0].tolist()) == {np.bincount(r.astype(np.int64)).max()}
 
 
 @pytest.mark.gpu
