@@ -391,6 +391,19 @@ void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1)
         ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, false, 1, cf, ctx));
         ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)((rows + rb - 1) / rb),
                                                              std::vector<unsigned>{64u, 4u}, cf, ctx));
+    } else if (name == "tblock_thread_total_maxpad" || name == "thread_total_maxpad") {
+        // row-direction BMTs with is_col_padding_with_row_max_size_with_empty_row: every row, empty
+        // ones too, padded to its BMTB's (tblock_: p0 rows, BMTs of p1 rows) or the matrix's
+        // (thread_total_maxpad: BMTs of p0 rows) longest row
+        // (fixed_interval_row_direction_thread_blocking_operator.cc:369-437 / :506-521)
+        const bool tb = name == "tblock_thread_total_maxpad";
+        int rb = p0 > 0 ? p0 : 16, tbr = tb ? (p1 > 0 ? p1 : 1) : rb, cf = 1;
+        if (tb) ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, rb, false, ctx));
+        ex.add_and_run(std::make_shared<fixed_interval_row_direction_thread_blocking_operator>(
+            cg, tbr, tb, tb, false, true, false, 0, ctx));
+        ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, false, 1, cf, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)((rows + rb - 1) / rb),
+                                                             std::vector<unsigned>{64u, 4u}, cf, ctx));
     } else if (name == "tblock_warp_total_relative") {
         // §8f rank 1: the C2 plan with BMW indices relative to their BMTB as well
         // (fixed_interval_row_direction_warp_blocking_operator with both relative flags)

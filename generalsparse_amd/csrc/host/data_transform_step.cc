@@ -301,7 +301,7 @@ void modify_row_indices_by_col_pad_in_sub_matrix::run(bool check) {
 // ranges) every non-empty row grows to the parent's longest row, pads repeating the row's last
 // column with value 0; the padding rate is checked against PADDING_RATE_UP_BOUND (:95-103)
 namespace {
-col_pad_plan make_max_pad(const meta_data_set &m, int s, POS_TYPE pos, bool check) {
+col_pad_plan make_max_pad(const meta_data_set &m, int s, POS_TYPE pos, bool with_empty, bool check) {
     const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
     GS_CHECK(!row.empty(), "max-row padding of an empty sub-matrix");
     const uint64_t b = m.scalar(GLOBAL_META, "begin_row_index", s);
@@ -320,7 +320,7 @@ col_pad_plan make_max_pad(const meta_data_set &m, int s, POS_TYPE pos, bool chec
         uint64_t mx = 0;
         for (uint64_t r = bounds[i]; r < bounds[i + 1] && r < row_num; r++) mx = std::max(mx, p.cnt[r]);
         for (uint64_t r = bounds[i]; r < bounds[i + 1] && r < row_num; r++)
-            if (mx && p.cnt[r]) {
+            if (mx && (p.cnt[r] || with_empty)) {
                 p.tgt[r] = mx;
                 p.padded = true;  // the reference rewrites the arrays once any row is visited
             }
@@ -332,13 +332,16 @@ col_pad_plan make_max_pad(const meta_data_set &m, int s, POS_TYPE pos, bool chec
                        " >= PADDING_RATE_UP_BOUND (modify_col_indices_by_col_pad_parent_blk_to_max_row_size.cc:95-103)");
     return p;
 }
+// src_at(k, pad, r): a pad repeats element k = the row's last nonzero (an empty row: the last
+// nonzero before it, the first one when there is none: :70-72) in row r
 template <class T, class F>
 std::vector<T> apply_max_pad(const col_pad_plan &p, F src_at) {
     std::vector<T> out;
     out.reserve(p.after);
     for (uint64_t r = 0; r + 1 < p.start.size(); r++) {
-        for (uint64_t k = p.start[r]; k < p.start[r + 1]; k++) out.push_back(src_at(k, false));
-        for (uint64_t k = p.cnt[r]; k < p.tgt[r]; k++) out.push_back(src_at(p.start[r + 1] - 1, true));
+        for (uint64_t k = p.start[r]; k < p.start[r + 1]; k++) out.push_back(src_at(k, false, r));
+        const uint64_t last = p.start[r + 1] ? p.start[r + 1] - 1 : 0;
+        for (uint64_t k = p.cnt[r]; k < p.tgt[r]; k++) out.push_back(src_at(last, true, r));
     }
     return out;
 }
@@ -346,10 +349,10 @@ std::vector<T> apply_max_pad(const col_pad_plan &p, F src_at) {
 
 void modify_col_indices_by_col_pad_parent_blk_to_max_row_size::run(bool check) {
     auto &m = *meta_data_set_ptr;
-    auto p = make_max_pad(m, target_matrix_id, parent_pos, check);
+    auto p = make_max_pad(m, target_matrix_id, parent_pos, padding_with_empty_row, check);
     if (p.padded) {
         const auto &col = m.u(GLOBAL_META, "nz_col_indices", target_matrix_id);
-        auto nc = apply_max_pad<uint64_t>(p, [&](uint64_t k, bool) { return col[k]; });
+        auto nc = apply_max_pad<uint64_t>(p, [&](uint64_t k, bool, uint64_t) { return col[k]; });
         src(GLOBAL_META, "nz_col_indices");
         replace_u(GLOBAL_META, "nz_col_indices", std::move(nc));
     }
@@ -358,10 +361,10 @@ void modify_col_indices_by_col_pad_parent_blk_to_max_row_size::run(bool check) {
 
 void modify_vals_by_col_pad_parent_blk_to_max_row_size::run(bool check) {
     auto &m = *meta_data_set_ptr;
-    auto p = make_max_pad(m, target_matrix_id, parent_pos, check);
+    auto p = make_max_pad(m, target_matrix_id, parent_pos, padding_with_empty_row, check);
     if (p.padded) {
         auto va = m.get_element(GLOBAL_META, "nz_vals", target_matrix_id)->meta_data_arr;
-        auto nv = apply_max_pad<double>(p, [&](uint64_t k, bool pad) { return pad ? 0.0 : va->read_float_from_arr(k); });
+        auto nv = apply_max_pad<double>(p, [&](uint64_t k, bool pad, uint64_t) { return pad ? 0.0 : va->read_float_from_arr(k); });
         src(GLOBAL_META, "nz_vals");
         replace_f(GLOBAL_META, "nz_vals", std::move(nv), va->get_data_type());
     }
@@ -370,10 +373,10 @@ void modify_vals_by_col_pad_parent_blk_to_max_row_size::run(bool check) {
 
 void modify_row_indices_by_col_pad_parent_blk_to_max_row_size::run(bool check) {
     auto &m = *meta_data_set_ptr;
-    auto p = make_max_pad(m, target_matrix_id, parent_pos, check);
+    auto p = make_max_pad(m, target_matrix_id, parent_pos, padding_with_empty_row, check);
     if (p.padded) {
         const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
-        auto nr = apply_max_pad<uint64_t>(p, [&](uint64_t k, bool) { return row[k]; });
+        auto nr = apply_max_pad<uint64_t>(p, [&](uint64_t k, bool pad, uint64_t r) { return pad ? r : row[k]; });
         src(GLOBAL_META, "nz_row_indices");
         replace_u(GLOBAL_META, "nz_row_indices", std::move(nr));
     }

@@ -68,11 +68,21 @@ GS_DECLARE_STEP_P(modify_col_indices_by_col_pad_in_sub_matrix, int, multiple_of_
 GS_DECLARE_STEP_P(modify_vals_by_col_pad_in_sub_matrix, int, multiple_of_each_row_size)
 GS_DECLARE_STEP_P(modify_row_indices_by_col_pad_in_sub_matrix, int, multiple_of_each_row_size)
 
-// column padding of every non-empty row to its parent's longest row (GLOBAL / TBLOCK / WARP parent;
-// the operators call them with padding_with_empty_row = false, the only form built)
-GS_DECLARE_STEP_P(modify_col_indices_by_col_pad_parent_blk_to_max_row_size, POS_TYPE, parent_pos)
-GS_DECLARE_STEP_P(modify_vals_by_col_pad_parent_blk_to_max_row_size, POS_TYPE, parent_pos)
-GS_DECLARE_STEP_P(modify_row_indices_by_col_pad_parent_blk_to_max_row_size, POS_TYPE, parent_pos)
+// column padding of every row to its parent's longest row (GLOBAL / TBLOCK / WARP parent); empty
+// rows too with padding_with_empty_row (the row-direction thread blocking), else they stay empty
+#define GS_DECLARE_STEP_MAXPAD(cls)                                                  \
+    class cls : public basic_data_transform_step {                                  \
+      public:                                                                       \
+        cls(std::shared_ptr<meta_data_set> m, int target_matrix_id, POS_TYPE parent_pos, bool padding_with_empty_row) \
+            : basic_data_transform_step(#cls, std::move(m), target_matrix_id), parent_pos(parent_pos), \
+              padding_with_empty_row(padding_with_empty_row) {}                    \
+        void run(bool check) override;                                              \
+        POS_TYPE parent_pos;                                                        \
+        bool padding_with_empty_row;                                                \
+    };
+GS_DECLARE_STEP_MAXPAD(modify_col_indices_by_col_pad_parent_blk_to_max_row_size)
+GS_DECLARE_STEP_MAXPAD(modify_vals_by_col_pad_parent_blk_to_max_row_size)
+GS_DECLARE_STEP_MAXPAD(modify_row_indices_by_col_pad_parent_blk_to_max_row_size)
 
 // fixed row-direction blocking (A7, A8, BMW)
 GS_DECLARE_STEP_P(get_begin_rows_of_BMT_after_fixed_blocking_in_row_direction, int, fixed_row_block_size)

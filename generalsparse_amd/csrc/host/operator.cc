@@ -378,8 +378,14 @@ void fixed_interval_row_direction_warp_blocking_operator::run(bool check) {
 }
 
 // ------------------------------------------- row-direction THREAD blocking
+static void run_max_row_pad(const std::shared_ptr<meta_data_set> &m, int s, POS_TYPE pos, bool check,
+                            std::vector<std::string> &seq, bool with_empty);
+static void col_pad_and_rerun(const std::shared_ptr<meta_data_set> &m, int s, int c, bool drop_tblock, bool drop_warp,
+                              const std::vector<std::shared_ptr<basic_operator>> &former, bool check,
+                              std::vector<std::string> &seq, bool col_size, bool max_pad, POS_TYPE max_pos);
+
 fixed_interval_row_direction_thread_blocking_operator::fixed_interval_row_direction_thread_blocking_operator(
-    cg_ptr cg, int rb, bool rrel, bool nrel, bool row_pad, bool colpad_max, bool colpad_size, int col_size, ctx_ptr)
+    cg_ptr cg, int rb, bool rrel, bool nrel, bool row_pad, bool colpad_max, bool colpad_size, int col_size, ctx_ptr history)
     : basic_operator("fixed_interval_row_direction_thread_blocking_operator", cg->get_metadata_set(),
                      DISTRIBUTING_OP, cg->get_sub_matrix_id()),
       fixed_row_block_size(rb), row_index_is_relative_to_parent(rrel), nz_index_is_relative_to_parent(nrel),
@@ -387,6 +393,7 @@ fixed_interval_row_direction_thread_blocking_operator::fixed_interval_row_direct
       is_col_padding_with_col_size(colpad_size), col_size(col_size), code_generator_ptr(cg) {
     GS_CHECK(rb > 0, "fixed_row_block_size > 0");
     if (row_pad) GS_CHECK(!rrel && !nrel, "row padding needs absolute indices");
+    former_operator = history->read_operator_context_arr(DISTRIBUTING_OP, target_matrix_id);
 }
 
 // fixed_interval_row_direction_thread_blocking_operator.cc (is_valid_according_to_operator)
@@ -419,9 +426,19 @@ void fixed_interval_row_direction_thread_blocking_operator::run(bool check) {
     if (has(TBLOCK_META, "first_row_indices") || has(WARP_META, "first_row_indices")) {
         // :198-480: BMTs inside the BMWs when there are BMWs, else inside the BMTBs;
         // absolute starts always, the relative arrays on request
-        if (is_col_padding_with_row_max_size_with_empty_row || is_col_padding_with_col_size)
-            throw gs_error("col padding of BMTs inside a parent (re-runs the parent's operators) is not built");
         const POS_TYPE par = has(WARP_META, "first_row_indices") ? WARP_META : TBLOCK_META;
+        const bool bmtb = has(TBLOCK_META, "first_row_indices"), bmw = has(WARP_META, "first_row_indices");
+        // :225-317 / :369-437: every row (empty ones too) to the BMW's (else the BMTB's) longest
+        // row, then to a multiple of col_size; each drops the parent levels and re-runs the
+        // former operators on the padded COO
+        if (is_col_padding_with_row_max_size_with_empty_row) {
+            run_max_row_pad(meta_data_set_ptr, target_matrix_id, par, check, transform_seq, true);
+            col_pad_and_rerun(meta_data_set_ptr, target_matrix_id, col_size, bmtb, bmw, former_operator, check,
+                              transform_seq, false, false, GLOBAL_META);
+        }
+        if (is_col_padding_with_col_size)
+            col_pad_and_rerun(meta_data_set_ptr, target_matrix_id, col_size, bmtb, bmw, former_operator, check,
+                              transform_seq, true, false, GLOBAL_META);
         get_begin_rows_of_BMT_after_fixed_blocking_in_row_direction_in_parent a(meta_data_set_ptr, target_matrix_id, par,
                                                                               fixed_row_block_size);
         run_step(a, check);
@@ -447,8 +464,8 @@ void fixed_interval_row_direction_thread_blocking_operator::run(bool check) {
         return;
     }
     if (is_row_padding) throw gs_error("row padding is not built in this round");
-    if (is_col_padding_with_row_max_size_with_empty_row)
-        throw gs_error("col padding to the parent's max row size is not built in this round");
+    if (is_col_padding_with_row_max_size_with_empty_row)  // :506-521, GLOBAL parent, empty rows too
+        run_max_row_pad(meta_data_set_ptr, target_matrix_id, GLOBAL_META, check, transform_seq, true);
     if (is_col_padding_with_col_size) {
         modify_col_indices_by_col_pad_in_sub_matrix a(meta_data_set_ptr, target_matrix_id, col_size);
         run_step(a, check);
@@ -994,23 +1011,22 @@ bool fixed_interval_col_direction_thread_blocking_operator::is_valid_according_t
 // (max_pad: first every non-empty row to its max_pos parent's longest row, :297-310;
 // col_size: then to a multiple of c, :313-326; either one drops and rebuilds the parents)
 static void run_max_row_pad(const std::shared_ptr<meta_data_set> &m, int s, POS_TYPE pos, bool check,
-                            std::vector<std::string> &seq) {
-    modify_col_indices_by_col_pad_parent_blk_to_max_row_size a(m, s, pos);
+                            std::vector<std::string> &seq, bool with_empty) {
+    modify_col_indices_by_col_pad_parent_blk_to_max_row_size a(m, s, pos, with_empty);
     a.run(check);
     seq.push_back(a.convert_to_string());
-    modify_vals_by_col_pad_parent_blk_to_max_row_size b(m, s, pos);
+    modify_vals_by_col_pad_parent_blk_to_max_row_size b(m, s, pos, with_empty);
     b.run(check);
     seq.push_back(b.convert_to_string());
-    modify_row_indices_by_col_pad_parent_blk_to_max_row_size r(m, s, pos);
+    modify_row_indices_by_col_pad_parent_blk_to_max_row_size r(m, s, pos, with_empty);
     r.run(check);
     seq.push_back(r.convert_to_string());
 }
 
 static void col_pad_and_rerun(const std::shared_ptr<meta_data_set> &m, int s, int c, bool drop_tblock, bool drop_warp,
                               const std::vector<std::shared_ptr<basic_operator>> &former, bool check,
-                              std::vector<std::string> &seq, bool col_size = true, bool max_pad = false,
-                              POS_TYPE max_pos = GLOBAL_META) {
-    if (max_pad) run_max_row_pad(m, s, max_pos, check, seq);
+                              std::vector<std::string> &seq, bool col_size, bool max_pad, POS_TYPE max_pos) {
+    if (max_pad) run_max_row_pad(m, s, max_pos, check, seq, false);
     if (col_size) {
         modify_col_indices_by_col_pad_in_sub_matrix a(m, s, c);
         a.run(check);
@@ -1123,7 +1139,7 @@ void fixed_interval_col_direction_tblock_blocking_operator::run(bool check) {
     if (check) GS_CHECK(is_valid_according_to_metadata(), "col-direction tblock blocking: invalid metadata");
     const int c = fixed_col_block_size;
     if (is_col_padding_with_row_max_size_without_empty_row)  // :149-162, GLOBAL parent
-        run_max_row_pad(meta_data_set_ptr, target_matrix_id, GLOBAL_META, check, transform_seq);
+        run_max_row_pad(meta_data_set_ptr, target_matrix_id, GLOBAL_META, check, transform_seq, false);
     if (is_padding_with_col_size_in_bmtb) {
         modify_col_indices_by_col_pad_in_sub_matrix a(meta_data_set_ptr, target_matrix_id, c);
         run_step(a, check);

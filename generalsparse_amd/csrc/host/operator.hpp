@@ -171,6 +171,7 @@ class fixed_interval_row_direction_thread_blocking_operator : public basic_opera
     bool row_index_is_relative_to_parent, nz_index_is_relative_to_parent, is_row_padding;
     bool is_col_padding_with_row_max_size_with_empty_row, is_col_padding_with_col_size;
     int col_size;
+    std::vector<std::shared_ptr<basic_operator>> former_operator;
 
   private:
     cg_ptr code_generator_ptr;

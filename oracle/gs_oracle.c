@@ -417,7 +417,7 @@ static int col_pad(or_set *s, int mult) {
  * + 1 (:40-52); parents = all rows (interval 0, GLOBAL) or fixed row intervals (the parent
  * level's first_row_indices of a fixed row-direction blocking); every non-empty row grows to
  * its parent's longest row, pads repeating the row's last column with value 0 (:54-103). */
-static int col_pad_max(or_set *s, uint64_t interval) {
+static int col_pad_max(or_set *s, uint64_t interval, int with_empty) {
     or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
     or_array *C = get(s, "GLOBAL_META", "nz_col_indices", 0);
     or_array *V = get(s, "GLOBAL_META", "nz_vals", 0);
@@ -432,7 +432,7 @@ static int col_pad_max(or_set *s, uint64_t interval) {
     for (uint64_t p0 = 0; p0 < row_num; p0 += iv) {
         uint64_t p1 = p0 + iv < row_num ? p0 + iv : row_num, mx = 0;
         for (uint64_t r = p0; r < p1; r++) if (cnt[r] > mx) mx = cnt[r];
-        for (uint64_t r = p0; r < p1; r++) { tgt[r] = (mx && cnt[r]) ? mx : cnt[r]; after += tgt[r]; }
+        for (uint64_t r = p0; r < p1; r++) { tgt[r] = (mx && (cnt[r] || with_empty)) ? mx : cnt[r]; after += tgt[r]; }
     }
     if ((double)after / (double)nnz >= PADDING_RATE_UP_BOUND) { /* :95-103 */
         free(cnt); free(tgt);
@@ -443,7 +443,8 @@ static int col_pad_max(or_set *s, uint64_t interval) {
     uint64_t p = 0, q = 0;
     for (uint64_t r = 0; r < row_num; r++) {
         for (uint64_t k = 0; k < cnt[r]; k++, q++) { nr[p] = R->u[q]; nc[p] = C->u[q]; nv[p] = V->f[q]; p++; }
-        for (uint64_t k = cnt[r]; k < tgt[r]; k++) { nr[p] = nr[p - 1]; nc[p] = nc[p - 1]; nv[p] = 0.0; p++; }
+        /* a pad repeats the last column written so far (the first column before any: :70-72) */
+        for (uint64_t k = cnt[r]; k < tgt[r]; k++) { nr[p] = r; nc[p] = p ? nc[p - 1] : C->u[0]; nv[p] = 0.0; p++; }
     }
     free(cnt); free(tgt);
     put_u(s, "GLOBAL_META", "nz_col_indices", 0, nc, after);
@@ -1638,6 +1639,15 @@ int or_pipeline(or_set *s, const char *name, int p0, int p1) {
         if (or_row_dir_tblock_blocking(s, p0)) return -1;
         return or_bmt_in_parent(s, p1 > 0 ? p1 : 1, 1, 1);
     }
+    if (!strcmp(name, "tblock_thread_total_maxpad")) { /* every row (empty ones too) to its BMTB's longest */
+        if (col_pad_max(s, p0 > 0 ? (uint64_t)p0 : 16, 1)) return -1;
+        if (or_row_dir_tblock_blocking(s, p0 > 0 ? p0 : 16)) return -1;
+        return or_bmt_in_parent(s, p1 > 0 ? p1 : 1, 1, 1);
+    }
+    if (!strcmp(name, "thread_total_maxpad")) { /* ELL-like: every row to the longest, BMTs of p0 rows */
+        if (col_pad_max(s, 0, 1)) return -1;
+        return or_row_dir_thread_blocking(s, p0 > 0 ? p0 : 1, 0);
+    }
     if (!strcmp(name, "tblock_warp_thread_total")) { /* BMTB rows p0, BMW rows 8, BMT rows p1 in the BMWs */
         if (or_row_dir_tblock_blocking(s, p0)) return -1;
         if (or_row_dir_warp_blocking(s, 8)) return -1;
@@ -1676,7 +1686,7 @@ int or_pipeline(or_set *s, const char *name, int p0, int p1) {
         /* every non-empty row padded to its BMTB's (BMW's) longest row, then BMTs of p1 in it */
         int warp = !strcmp(name, "warp_col_thread_maxpad");
         uint64_t rb = p0 > 0 ? (uint64_t)p0 : 16, c = p1 > 0 ? (uint64_t)p1 : 32;
-        if (col_pad_max(s, rb)) return -1;
+        if (col_pad_max(s, rb, 0)) return -1;
         if (warp ? or_row_dir_warp_blocking(s, (int)rb) : or_row_dir_tblock_blocking(s, (int)rb)) return -1;
         return or_col_dir_thread_in_parent(s, c, 1, 1, 0);
     }

@@ -348,6 +348,23 @@ cases.append({
     },
 })
 
+# row-direction BMTs with is_col_padding_with_row_max_size_with_empty_row inside BMTBs of 4 rows
+# (tblock_thread_total_maxpad, BMTs of 1 row; fixed_interval_row_direction_thread_blocking_operator
+# .cc:369-437 -> modify_*_by_col_pad_parent_blk_to_max_row_size with padding_with_empty_row):
+# parent [0,4) max 3, parent [4,6) max 5, EMPTY rows padded too, a pad repeating the last column
+# written so far: row0 [0 2 2], row1 [2 2 2], row2 [1 3 4], row3 [0 0 0], row4 [0 1 2 3 4],
+# row5 [4 4 4 4 4]; BMTB first nz 0, 12, 22; one BMT per row.
+cases.append({
+    "matrix": "ex1", "pipeline": "tblock_thread_total_maxpad", "p0": 4, "p1": 1,
+    "expect": {
+        G + "nz_col_indices_0": [0, 2, 2, 2, 2, 2, 1, 3, 4, 0, 0, 0, 0, 1, 2, 3, 4, 4, 4, 4, 4, 4],
+        G + "nz_row_indices_0": [0, 0, 0, 1, 1, 1, 2, 2, 2, 3, 3, 3, 4, 4, 4, 4, 4, 5, 5, 5, 5, 5],
+        G + "nz_vals_0": [1, 2, 0, 0, 0, 0, 3, 4, 5, 6, 0, 0, 7, 8, 9, 10, 11, 0, 0, 0, 0, 0],
+        B + "first_nz_indices_0": [0, 12, 22],
+        T + "first_nz_indices_0": [0, 3, 6, 9, 12, 17, 22],
+    },
+})
+
 # relative BMW indices (§8f rank 1) on ex1 with BMTBs of 4 rows and BMWs of 2 rows:
 # BMTB rows [0,4) and [4,6); BMW starts 0,2 | 4 -> relative 0,2 | 0; row nnz [2,0,3,1,5,0]:
 # BMTB 0 nonzeros before each BMW 0, 2 | BMTB 1: 0

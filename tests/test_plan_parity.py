@@ -132,7 +132,7 @@ def test_hand_derived_fixtures_through_product():
             "tblock_warp_total": (32, 4, 1), "balanced_warp_total": (32, 16, 1),
             "warp_bit_map": (32, 4, 1), "tblock_bit_map": (32, 4, 1), "tblock_bit_map_interleaved": (32, 4, 1),
             "tblock_col_thread_interleaved": (32, 4, 2), "warp_col_thread_interleaved": (32, 4, 2),
-            "tblock_col_thread_maxpad": (32, 4, 2),
+            "tblock_col_thread_maxpad": (32, 4, 2), "tblock_thread_total_maxpad": (32, 4, 1),
             "tblock_thread_total": (32, 4, 1), "tblock_warp_thread_total": (32, 4, 1)}
     for case in g["cases"]:
         m = g["matrices"][case["matrix"]]
@@ -146,10 +146,12 @@ def test_hand_derived_fixtures_through_product():
             N, p0, p1 = back[name]
             if name in ("tblock_warp_total", "balanced_warp_total", "merge_path", "balanced_block_total",
                         "balanced_thread_total", "tblock_warp_total_relative", "tblock_thread_total",
-                        "tblock_warp_thread_total", "tblock_col_thread_interleaved", "warp_col_thread_interleaved", "tblock_col_thread_maxpad"):
+                        "tblock_warp_thread_total", "tblock_col_thread_interleaved", "warp_col_thread_interleaved", "tblock_col_thread_maxpad",
+                        "tblock_thread_total_maxpad"):
                 p0 = case["p0"]
             if name in ("merge_path", "tblock_warp_total_relative", "tblock_thread_total", "tblock_warp_thread_total",
-                        "tblock_col_thread_interleaved", "warp_col_thread_interleaved", "tblock_col_thread_maxpad"):
+                        "tblock_col_thread_interleaved", "warp_col_thread_interleaved", "tblock_col_thread_maxpad",
+                        "tblock_thread_total_maxpad"):
                 p1 = case["p1"]
         if case.get("expect_error"):
             with pytest.raises(gsa.GsError):
