@@ -391,6 +391,16 @@ void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1)
         ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, false, 1, cf, ctx));
         ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)((rows + rb - 1) / rb),
                                                              std::vector<unsigned>{64u, 4u}, cf, ctx));
+    } else if (name == "tblock_thread_total_colpad") {
+        // BMTs of one row inside BMTBs of p0 rows with is_col_padding_with_col_size (rows to a
+        // multiple of p1; the BMTB level is rebuilt on the padded COO, :272-317 / :406-437)
+        int rb = p0 > 0 ? p0 : 16, cs = p1 > 1 ? p1 : 2, cf = 1;
+        ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, rb, false, ctx));
+        ex.add_and_run(std::make_shared<fixed_interval_row_direction_thread_blocking_operator>(
+            cg, 1, true, true, false, false, true, cs, ctx));
+        ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, false, 1, cf, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)((rows + rb - 1) / rb),
+                                                             std::vector<unsigned>{64u, 4u}, cf, ctx));
     } else if (name == "tblock_thread_total_maxpad" || name == "thread_total_maxpad") {
         // row-direction BMTs with is_col_padding_with_row_max_size_with_empty_row: every row, empty
         // ones too, padded to its BMTB's (tblock_: p0 rows, BMTs of p1 rows) or the matrix's

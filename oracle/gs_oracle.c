@@ -1644,6 +1644,11 @@ int or_pipeline(or_set *s, const char *name, int p0, int p1) {
         if (or_row_dir_tblock_blocking(s, p0 > 0 ? p0 : 16)) return -1;
         return or_bmt_in_parent(s, p1 > 0 ? p1 : 1, 1, 1);
     }
+    if (!strcmp(name, "tblock_thread_total_colpad")) { /* BMTs of one row in BMTBs of p0 rows, rows to a multiple of p1 */
+        if (col_pad(s, p1 > 1 ? p1 : 2)) return -1;
+        if (or_row_dir_tblock_blocking(s, p0 > 0 ? p0 : 16)) return -1;
+        return or_bmt_in_parent(s, 1, 1, 1);
+    }
     if (!strcmp(name, "thread_total_maxpad")) { /* ELL-like: every row to the longest, BMTs of p0 rows */
         if (col_pad_max(s, 0, 1)) return -1;
         return or_row_dir_thread_blocking(s, p0 > 0 ? p0 : 1, 0);

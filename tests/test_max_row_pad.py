@@ -1,5 +1,6 @@
 """Row padding to the parent's longest row (modify_{col,vals,row}_*_by_col_pad_parent_blk_to_max_row_size,
 SURVEY.md §8a A6/A7 padding branches):
+- row-direction BMTs padded to a multiple of a column count inside BMTBs (tblock_thread_total_colpad);
 - row-direction BMTs with is_col_padding_with_row_max_size_with_empty_row, inside BMTBs
   (tblock_thread_total_maxpad) and with no parent (thread_total_maxpad, the ELL-like layout):
   product plan arrays bit-exact against the oracle's restatement (oracle/gs_oracle.c col_pad_max);
@@ -19,7 +20,8 @@ import generalsparse_amd as gsa  # noqa: E402
 from generalsparse_amd import datasets as ds  # noqa: E402
 
 PIPES = [("tblock_thread_total_maxpad", 16, 1), ("tblock_thread_total_maxpad", 4, 2),
-         ("tblock_thread_total_maxpad", 3, 3), ("thread_total_maxpad", 1, 0), ("thread_total_maxpad", 4, 0)]
+         ("tblock_thread_total_maxpad", 3, 3), ("thread_total_maxpad", 1, 0), ("thread_total_maxpad", 4, 0),
+         ("tblock_thread_total_colpad", 16, 4), ("tblock_thread_total_colpad", 3, 2)]
 
 
 def cases():
