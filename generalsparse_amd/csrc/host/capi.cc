@@ -296,6 +296,21 @@ void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1)
         ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, true, 4, cf, ctx));
         ex.add_and_run(std::make_shared<warp_bit_map_operator>(cg, (unsigned)cf, true, true, ctx));
         ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)rows, std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
+    } else if (name == "block_total_rowpad" || name == "warp_total_rowpad") {
+        // row-direction BMTBs (BMWs) of p0 rows with is_padding: the row count padded up to a
+        // multiple of p0 first (modify_*_by_row_pad_in_sub_matrix; one zero entry per added row)
+        int rb = p0 > 0 ? p0 : 1, cf = p1 > 0 ? p1 : 1;
+        int x = std::min(N, 32), y = 256 / std::max(1, x);
+        set_config("VECTOR_WIDTH", x);
+        if (name == "block_total_rowpad") {
+            ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, rb, true, ctx));
+            ex.add_and_run(std::make_shared<tblock_total_reduce_operator>(cg, cf, ctx));
+        } else {
+            ex.add_and_run(std::make_shared<fixed_interval_row_direction_warp_blocking_operator>(cg, rb, false, false, true, ctx));
+            ex.add_and_run(std::make_shared<warp_total_reduce_operator>(cg, cf, ctx));
+        }
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)((rows + rb - 1) / rb),
+                                                             std::vector<unsigned>{(unsigned)x, (unsigned)y}, cf, ctx));
     } else if (name == "block_total") {  // token_test.cc:1458-1514 (p0 = rows per BMTB, 1 there)
         int rb = p0 > 0 ? p0 : 1, cf = p1 > 0 ? p1 : 1;
         ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, rb, false, ctx));
@@ -591,7 +606,9 @@ int gs_plan_compile(gs_plan_t *p) {
                          ": row indices lie past the divided sub-matrix's rows");
             } else {
                 // a kernel writes C row begin_row_index + r: every row inside the sub-matrix
-                GS_CHECK(r.empty() || b + r.back() <= e,
+                // (an undivided row-padded matrix is the exception: its padding rows run into
+                // the scratch output upload_plan gives it)
+                GS_CHECK(r.empty() || b + r.back() <= e || (sb == 0 && !divided(p)),
                          "sub-matrix " + std::to_string(sb) + ": row indices lie past its end_row_index");
             }
             s->cg->compile();

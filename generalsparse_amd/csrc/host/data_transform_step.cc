@@ -294,6 +294,68 @@ void modify_row_indices_by_col_pad_in_sub_matrix::run(bool check) {
     is_run = true;
 }
 
+// ------------------------------------------------------------ row padding
+// modify_{col,vals,row}_*_by_row_pad_in_sub_matrix.cc: row_num = end_row_index - begin_row_index
+// + 1 (the recorded range, :15-17); when it is not a multiple, one entry per added row is
+// appended: column = the last column, value 0, row = row_num + i (:40-47 / :86-107); the
+// padding rate is checked against PADDING_RATE_UP_BOUND (:33-38)
+namespace {
+uint64_t rows_added_by_row_pad(const meta_data_set &m, int s, int mult, bool check) {
+    GS_CHECK(mult > 0, "row pad multiple > 0");
+    const uint64_t b = m.scalar(GLOBAL_META, "begin_row_index", s), e = m.scalar(GLOBAL_META, "end_row_index", s);
+    const uint64_t rn = e - b + 1;
+    if (rn % (uint64_t)mult == 0) return 0;
+    const uint64_t add = (rn / mult + 1) * mult - rn;
+    const uint64_t nnz = m.u(GLOBAL_META, "nz_row_indices", s).size();
+    GS_CHECK(nnz > 0, "row padding of an empty sub-matrix");
+    if (check && (double)(nnz + add) / (double)nnz >= padding_bound())
+        throw gs_error("row padding rate >= PADDING_RATE_UP_BOUND (modify_col_indices_by_row_pad_in_sub_matrix.cc:33-38)");
+    return add;
+}
+}  // namespace
+
+void modify_col_indices_by_row_pad_in_sub_matrix::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const uint64_t add = rows_added_by_row_pad(m, target_matrix_id, multiple, check);
+    if (add) {
+        std::vector<uint64_t> nc = m.u(GLOBAL_META, "nz_col_indices", target_matrix_id);
+        const uint64_t last = nc.back();
+        nc.insert(nc.end(), add, last);
+        src(GLOBAL_META, "nz_col_indices");
+        replace_u(GLOBAL_META, "nz_col_indices", std::move(nc));
+    }
+    is_run = true;
+}
+
+void modify_vals_by_row_pad_in_sub_matrix::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const uint64_t add = rows_added_by_row_pad(m, target_matrix_id, multiple, check);
+    if (add) {
+        auto va = m.get_element(GLOBAL_META, "nz_vals", target_matrix_id)->meta_data_arr;
+        std::vector<double> nv(va->get_len());
+        for (uint64_t i = 0; i < nv.size(); i++) nv[i] = va->read_float_from_arr(i);
+        nv.insert(nv.end(), add, 0.0);
+        src(GLOBAL_META, "nz_vals");
+        replace_f(GLOBAL_META, "nz_vals", std::move(nv), va->get_data_type());
+    }
+    is_run = true;
+}
+
+void modify_row_indices_by_row_pad_in_sub_matrix::run(bool check) {
+    auto &m = *meta_data_set_ptr;
+    const uint64_t add = rows_added_by_row_pad(m, target_matrix_id, multiple, check);
+    if (add) {
+        const uint64_t rn = m.scalar(GLOBAL_META, "end_row_index", target_matrix_id) -
+                            m.scalar(GLOBAL_META, "begin_row_index", target_matrix_id) + 1;
+        std::vector<uint64_t> nr = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);
+        if (check) GS_CHECK(nr.back() < rn, "row padding: a nonzero past end_row_index (:96-99)");
+        for (uint64_t i = 0; i < add; i++) nr.push_back(rn + i);
+        src(GLOBAL_META, "nz_row_indices");
+        replace_u(GLOBAL_META, "nz_row_indices", std::move(nr));
+    }
+    is_run = true;
+}
+
 // ------------------------------------------- col pad to the parent's max row
 // modify_{col,vals,row}_*_by_col_pad_parent_blk_to_max_row_size.cc (padding_with_empty_row
 // false): rows [0, row_num) with row_num from the sub-matrix's row range widened to its last

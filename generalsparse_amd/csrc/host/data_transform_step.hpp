@@ -68,6 +68,12 @@ GS_DECLARE_STEP_P(modify_col_indices_by_col_pad_in_sub_matrix, int, multiple_of_
 GS_DECLARE_STEP_P(modify_vals_by_col_pad_in_sub_matrix, int, multiple_of_each_row_size)
 GS_DECLARE_STEP_P(modify_row_indices_by_col_pad_in_sub_matrix, int, multiple_of_each_row_size)
 
+// row padding: the sub-matrix's row count (end - begin + 1) up to a multiple, one zero entry per
+// added row (its row index, the last column) -- modify_*_by_row_pad_in_sub_matrix.cc
+GS_DECLARE_STEP_P(modify_col_indices_by_row_pad_in_sub_matrix, int, multiple)
+GS_DECLARE_STEP_P(modify_vals_by_row_pad_in_sub_matrix, int, multiple)
+GS_DECLARE_STEP_P(modify_row_indices_by_row_pad_in_sub_matrix, int, multiple)
+
 // column padding of every row to its parent's longest row (GLOBAL / TBLOCK / WARP parent); empty
 // rows too with padding_with_empty_row (the row-direction thread blocking), else they stay empty
 #define GS_DECLARE_STEP_MAXPAD(cls)                                                  \

@@ -14,6 +14,7 @@ namespace gs {
 // (bench.py rotates replicas past the 256 MB Infinity Cache).
 struct device_arrays {
     void *col = nullptr, *val = nullptr;
+    void *pad_out = nullptr;  // row-padded plans: scratch output of all the plan's rows
     void *tcol = nullptr, *tval = nullptr;  // LDS tile layout (k_lds_rows)
     uint32_t *t0 = nullptr, *t1 = nullptr, *t2 = nullptr, *t3 = nullptr, *t4 = nullptr;
     uint32_t *a0 = nullptr, *a1 = nullptr, *a2 = nullptr, *a3 = nullptr, *a4 = nullptr;
@@ -29,6 +30,8 @@ struct device_plan {
     int scf = 4;           // sparse entries per vector load
     bool needs_memset = false;
     uint64_t n_out_rows = 0;  // one past the last row of C this plan writes
+    uint64_t pad_rows = 0;    // row-padded plan (modify_*_by_row_pad_in_sub_matrix): its rows, > M
+    uint32_t pad_N = 0;       // ... the dense width its scratch output holds
     uint64_t out_lo = 0;      // first row of C this plan writes (a sub-matrix's range)
     uint64_t n_units = 0;     // BMTs / BMWs / BMTBs the grid walks
     uint64_t n_rows_aux = 0;  // rows covered (thread_total: rows incl. trailing empty)

@@ -166,10 +166,24 @@ bool fixed_interval_row_direction_tblock_blocking_operator::is_valid_according_t
            m.count_of_metadata_of_diff_pos(WARP_META, s) == 0 && m.count_of_metadata_of_diff_pos(THREAD_META, s) == 0;
 }
 
+// modify_{col,vals,row}_*_by_row_pad_in_sub_matrix in the row-direction operators' order
+static void run_row_pad(const std::shared_ptr<meta_data_set> &m, int s, int mult, bool check,
+                        std::vector<std::string> &seq) {
+    modify_col_indices_by_row_pad_in_sub_matrix a(m, s, mult);
+    a.run(check);
+    seq.push_back(a.convert_to_string());
+    modify_vals_by_row_pad_in_sub_matrix b(m, s, mult);
+    b.run(check);
+    seq.push_back(b.convert_to_string());
+    modify_row_indices_by_row_pad_in_sub_matrix r(m, s, mult);
+    r.run(check);
+    seq.push_back(r.convert_to_string());
+}
+
 // fixed_interval_row_direction_tblock_blocking_operator.cc:126-185
 void fixed_interval_row_direction_tblock_blocking_operator::run(bool check) {
     if (check) GS_CHECK(is_valid_according_to_metadata(), "tblock blocking: invalid metadata");
-    if (is_padding) throw gs_error("row padding (modify_*_by_row_pad_in_sub_matrix) is not built in this round");
+    if (is_padding) run_row_pad(meta_data_set_ptr, target_matrix_id, fixed_row_block_size, check, transform_seq);  // :142-158
     get_begin_rows_of_BMTBs_after_fixed_blocking_in_row_direction a(meta_data_set_ptr, target_matrix_id,
                                                                     fixed_row_block_size);
     run_step(a, check);
@@ -363,7 +377,7 @@ void fixed_interval_row_direction_warp_blocking_operator::run(bool check) {
         get_begin_BMWs_of_BMTB_after_blocking_in_row_direction c(meta_data_set_ptr, target_matrix_id);
         run_step(c, check);
     } else {
-        if (is_padding) throw gs_error("row padding is not built in this round");
+        if (is_padding) run_row_pad(meta_data_set_ptr, target_matrix_id, fixed_row_block_size, check, transform_seq);  // :287-302
         get_begin_rows_of_BMW_after_fixed_blocking_in_row_direction_without_BMTB a(meta_data_set_ptr,
                                                                                    target_matrix_id,
                                                                                    fixed_row_block_size);
@@ -463,7 +477,7 @@ void fixed_interval_row_direction_thread_blocking_operator::run(bool check) {
         is_run = true;
         return;
     }
-    if (is_row_padding) throw gs_error("row padding is not built in this round");
+    if (is_row_padding) run_row_pad(meta_data_set_ptr, target_matrix_id, fixed_row_block_size, check, transform_seq);  // :488-504
     if (is_col_padding_with_row_max_size_with_empty_row)  // :506-521, GLOBAL parent, empty rows too
         run_max_row_pad(meta_data_set_ptr, target_matrix_id, GLOBAL_META, check, transform_seq, true);
     if (is_col_padding_with_col_size) {

@@ -1026,6 +1026,15 @@ void upload_plan(plan_state &p, int dtype, int device) {
             throw gs_error("no gfx950 kernel family for this plan");
     }
     if (defer_csr && !d.mfma) upload_csr(p, a);
+    // row-padded plans (modify_*_by_row_pad_in_sub_matrix): the padding rows lie past the
+    // output, so every launch writes a scratch output of all the plan's rows and launch_spmm
+    // copies its first M rows to C
+    const uint64_t prows = row_num_of_sub_matrix(m, sb);
+    if (sb == 0 && !pidx && prows > p.M) {
+        d.pad_rows = prows;
+        d.pad_N = (uint32_t)std::max<int64_t>(1, get_config().DENSE_MATRIX_SIZE);
+        a.pad_out = dev_copy(d, std::vector<uint32_t>((prows * d.pad_N * (dtype == 0 ? 4u : 2u) + 3) / 4, 0u));
+    }
     d.replicas.push_back(a);
     p.uploaded = true;
 }
@@ -1070,6 +1079,7 @@ void add_replica(plan_state &p) {
     r.t4 = (uint32_t *)dup(s.t4);
     r.ws = (float *)dup(s.ws);
     r.ws2 = (float *)dup(s.ws2);
+    r.pad_out = dup(s.pad_out);
     p.dev.replicas.push_back(r);
 }
 
@@ -1529,10 +1539,7 @@ void dispatch_vt(const plan_state &p, const device_arrays &a, const void *B, voi
 
 }  // namespace
 
-void launch_spmm(plan_state &p, int replica, const void *B, void *C, uint32_t N, hipStream_t stream) {
-    GS_CHECK(p.uploaded, "plan is not on the device");
-    GS_CHECK(replica >= 0 && (size_t)replica < p.dev.replicas.size(), "bad replica index");
-    GS_CHECK(N >= 1, "N >= 1");
+static void launch_body(plan_state &p, int replica, const void *B, void *C, uint32_t N, hipStream_t stream) {
     if (p.dev.nm) {
         launch_nm(p, p.dev.replicas[replica], B, C, N, stream);
         return;
@@ -1545,6 +1552,22 @@ void launch_spmm(plan_state &p, int replica, const void *B, void *C, uint32_t N,
     const device_arrays &a = p.dev.replicas[replica];
     if (p.dev.dtype == 0) dispatch_vt<float, 4>(p, a, B, C, N, stream);
     else dispatch_vt<gsk::f16, 8>(p, a, B, C, N, stream);
+}
+
+void launch_spmm(plan_state &p, int replica, const void *B, void *C, uint32_t N, hipStream_t stream) {
+    GS_CHECK(p.uploaded, "plan is not on the device");
+    GS_CHECK(replica >= 0 && (size_t)replica < p.dev.replicas.size(), "bad replica index");
+    GS_CHECK(N >= 1, "N >= 1");
+    if (p.dev.pad_rows) {
+        GS_CHECK(N <= p.dev.pad_N, "row-padded plan built for N=" + std::to_string(p.dev.pad_N) +
+                                       ": its scratch output holds no wider B (re-run the pipeline for this N)");
+        void *scr = p.dev.replicas[replica].pad_out;
+        launch_body(p, replica, B, scr, N, stream);
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipMemcpyAsync(C, scr, (size_t)p.M * N * (p.dev.dtype == 0 ? 4u : 2u), hipMemcpyDeviceToDevice, stream));
+        return;
+    }
+    launch_body(p, replica, B, C, N, stream);
 }
 
 }  // namespace gs

@@ -412,6 +412,29 @@ static int col_pad(or_set *s, int mult) {
     return 0;
 }
 
+/* modify_{col,vals,row}_*_by_row_pad_in_sub_matrix.cc: the recorded row range (end - begin + 1)
+ * up to a multiple, one entry per added row appended (row = row_num + i, the last column, 0) */
+static int row_pad(or_set *s, int mult) {
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    or_array *C = get(s, "GLOBAL_META", "nz_col_indices", 0);
+    or_array *V = get(s, "GLOBAL_META", "nz_vals", 0);
+    uint64_t nnz = R->len;
+    uint64_t rn = scalar(s, "GLOBAL_META", "end_row_index", 0) - scalar(s, "GLOBAL_META", "begin_row_index", 0) + 1;
+    if (mult <= 0) return fail(s, "row pad multiple <= 0");
+    if (rn % (uint64_t)mult == 0) return 0;
+    if (!nnz) return fail(s, "row padding of an empty sub-matrix");
+    uint64_t add = (rn / mult + 1) * mult - rn, n = nnz + add;
+    if ((double)n / (double)nnz >= PADDING_RATE_UP_BOUND) return fail(s, "row padding rate >= %d", PADDING_RATE_UP_BOUND);
+    uint64_t *nr = (uint64_t *)malloc(n * 8), *nc = (uint64_t *)malloc(n * 8);
+    double *nv = (double *)malloc(n * 8);
+    for (uint64_t i = 0; i < nnz; i++) { nr[i] = R->u[i]; nc[i] = C->u[i]; nv[i] = V->f[i]; }
+    for (uint64_t i = 0; i < add; i++) { nr[nnz + i] = rn + i; nc[nnz + i] = C->u[nnz - 1]; nv[nnz + i] = 0.0; }
+    put_u(s, "GLOBAL_META", "nz_col_indices", 0, nc, n);
+    put_f(s, "GLOBAL_META", "nz_vals", 0, nv, n);
+    put_u(s, "GLOBAL_META", "nz_row_indices", 0, nr, n);
+    return 0;
+}
+
 /* modify_{col,vals,row}_*_by_col_pad_parent_blk_to_max_row_size.cc (padding_with_empty_row
  * false): rows [0, row_num), row_num = max(end_row_index, begin + last nonzero's row) - begin
  * + 1 (:40-52); parents = all rows (interval 0, GLOBAL) or fixed row intervals (the parent
@@ -1673,6 +1696,14 @@ int or_pipeline(or_set *s, const char *name, int p0, int p1) {
     }
     if (!strcmp(name, "warp_total")) /* token_test.cc:1188-1249 */
         return or_row_dir_warp_blocking(s, 1);
+    if (!strcmp(name, "block_total_rowpad")) { /* BMTBs of p0 rows, the rows padded to a multiple of p0 */
+        if (row_pad(s, p0 > 0 ? p0 : 1)) return -1;
+        return or_row_dir_tblock_blocking(s, p0 > 0 ? p0 : 1);
+    }
+    if (!strcmp(name, "warp_total_rowpad")) { /* BMWs of p0 rows, padded likewise */
+        if (row_pad(s, p0 > 0 ? p0 : 1)) return -1;
+        return or_row_dir_warp_blocking(s, p0 > 0 ? p0 : 1);
+    }
     if (!strcmp(name, "block_total")) /* token_test.cc:1458-1514 (rb 1 there; p0 = rows per BMTB) */
         return or_row_dir_tblock_blocking(s, p0 > 0 ? p0 : 1);
     /* nnz-direction parents (p0 = nnz per BMW / BMTB, p1 = nnz per BMW inside the BMTBs),

@@ -1,6 +1,10 @@
 """Row padding to the parent's longest row (modify_{col,vals,row}_*_by_col_pad_parent_blk_to_max_row_size,
 SURVEY.md §8a A6/A7 padding branches):
 - row-direction BMTs padded to a multiple of a column count inside BMTBs (tblock_thread_total_colpad);
+- row padding (modify_*_by_row_pad_in_sub_matrix: the row count up to a multiple of the BMTB /
+  BMW height, one zero entry per added row past the matrix) in block_total_rowpad /
+  warp_total_rowpad; on the device those plans run into a scratch output of all their rows
+  and the first M rows are copied to C;
 - row-direction BMTs with is_col_padding_with_row_max_size_with_empty_row, inside BMTBs
   (tblock_thread_total_maxpad) and with no parent (thread_total_maxpad, the ELL-like layout):
   product plan arrays bit-exact against the oracle's restatement (oracle/gs_oracle.c col_pad_max);
@@ -21,7 +25,9 @@ from generalsparse_amd import datasets as ds  # noqa: E402
 
 PIPES = [("tblock_thread_total_maxpad", 16, 1), ("tblock_thread_total_maxpad", 4, 2),
          ("tblock_thread_total_maxpad", 3, 3), ("thread_total_maxpad", 1, 0), ("thread_total_maxpad", 4, 0),
-         ("tblock_thread_total_colpad", 16, 4), ("tblock_thread_total_colpad", 3, 2)]
+         ("tblock_thread_total_colpad", 16, 4), ("tblock_thread_total_colpad", 3, 2),
+         ("block_total_rowpad", 16, 0), ("block_total_rowpad", 3, 0), ("warp_total_rowpad", 16, 0),
+         ("warp_total_rowpad", 5, 0)]
 
 
 def cases():
@@ -75,3 +81,17 @@ def test_plans_on_gpu(pipe, dtype):
             err = np.abs(C - ref) / np.maximum(1.0, np.abs(ref))
             assert err.max() <= (1e-1 if dtype == "f16" else 1e-3), (name, N, plan.info()["device_kernel"], err.max())
             plan.free()
+
+
+def test_row_pad_hand_case():
+    """ex1-like 7 x 5 matrix, BMTBs of 4 rows with row padding: end_row_index 6 -> 7 rows, one
+    row added (row 7, the last column 4, value 0); BMTB rows [0, 4, 8], first nz [0, 6, 12]"""
+    r = np.array([0, 0, 2, 2, 2, 3, 4, 4, 4, 4, 4], np.uint64)
+    c = np.array([0, 2, 1, 3, 4, 0, 0, 1, 2, 3, 4], np.uint64)
+    v = np.arange(1, 12, dtype=np.float32)
+    a = gsa.Plan.from_coo(7, 5, r, c, v).run_pipeline("block_total_rowpad", 32, 4, 0).arrays()
+    assert a["GLOBAL_META_nz_row_indices_0"].tolist() == [0, 0, 2, 2, 2, 3, 4, 4, 4, 4, 4, 7]
+    assert a["GLOBAL_META_nz_col_indices_0"].tolist() == [0, 2, 1, 3, 4, 0, 0, 1, 2, 3, 4, 4]
+    assert a["GLOBAL_META_nz_vals_0"].tolist() == list(range(1, 12)) + [0]
+    assert a["TBLOCK_META_first_row_indices_0"].tolist() == [0, 4, 8]
+    assert a["TBLOCK_META_first_nz_indices_0"].tolist() == [0, 6, 12]
