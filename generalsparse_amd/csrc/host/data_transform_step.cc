@@ -1309,6 +1309,70 @@ void get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction::run(bool check) 
     is_run = true;
 }
 
+// balanced BMWs inside BMTBs (data_transform_common.cc:794-901): per BMTB a new BMW after the
+// row whose running count reaches nnz_per_interval, never at the BMTB's last row (the next
+// BMTB starts one anyway); absolute arrays end with row_num / the last BMTB nz, the
+// relative ones restart at 0 per BMTB and have no ending.  row_num widens the recorded range to
+// the last nonzero's row (get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction_in_BMTB.cc:33-40)
+namespace {
+struct bmw_in_bmtb {
+    std::vector<uint64_t> rows, rows_rel, nzs, nzs_rel;
+};
+bmw_in_bmtb balanced_bmw_in_bmtb(const meta_data_set &m, int s, uint64_t per) {
+    GS_CHECK(per > 0, "nnz_per_interval > 0");
+    const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
+    GS_CHECK(!row.empty(), "balanced BMWs of an empty sub-matrix");
+    const uint64_t b = m.scalar(GLOBAL_META, "begin_row_index", s);
+    const uint64_t e = std::max<uint64_t>(m.scalar(GLOBAL_META, "end_row_index", s), b + row.back());
+    const uint64_t row_num = e - b + 1;
+    auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
+    const auto &pr = m.u(TBLOCK_META, "first_row_indices", s);
+    const auto &pn = m.u(TBLOCK_META, "first_nz_indices", s);
+    GS_CHECK(pr.size() == pn.size() && pr.size() >= 2, "BMTB first_row_indices / first_nz_indices disagree");
+    bmw_in_bmtb o;
+    for (size_t j = 0; j + 1 < pr.size(); j++) {
+        o.rows.push_back(pr[j]);
+        o.rows_rel.push_back(0);
+        o.nzs.push_back(pn[j]);
+        o.nzs_rel.push_back(0);
+        uint64_t run = 0, in_blk = 0;
+        for (uint64_t i = pr[j]; i < pr[j + 1]; i++) {
+            run += cnt[i];
+            in_blk += cnt[i];
+            if (run >= per && i != pr[j + 1] - 1) {
+                o.rows.push_back(i + 1);
+                o.rows_rel.push_back(i + 1 - pr[j]);
+                o.nzs.push_back(pn[j] + in_blk);
+                o.nzs_rel.push_back(in_blk);
+                run = 0;
+            }
+        }
+    }
+    o.rows.push_back(row_num);
+    o.nzs.push_back(pn.back());
+    return o;
+}
+}  // namespace
+
+void get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction_in_BMTB::run(bool check) {
+    replace_u(WARP_META, "first_row_indices", balanced_bmw_in_bmtb(*meta_data_set_ptr, target_matrix_id, nnz_per_interval).rows);
+    is_run = true;
+}
+void get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction_relative_to_BMTB::run(bool check) {
+    replace_u(WARP_META, "first_row_indices_relative_to_BMTB",
+              balanced_bmw_in_bmtb(*meta_data_set_ptr, target_matrix_id, nnz_per_interval).rows_rel);
+    is_run = true;
+}
+void get_begin_nzs_of_BMW_after_nnz_blocking_in_row_direction_in_BMTB::run(bool check) {
+    replace_u(WARP_META, "first_nz_indices", balanced_bmw_in_bmtb(*meta_data_set_ptr, target_matrix_id, nnz_per_interval).nzs);
+    is_run = true;
+}
+void get_begin_nzs_of_BMW_after_nnz_blocking_in_row_direction_relative_to_BMTB::run(bool check) {
+    replace_u(WARP_META, "first_nz_indices_relative_to_BMTB",
+              balanced_bmw_in_bmtb(*meta_data_set_ptr, target_matrix_id, nnz_per_interval).nzs_rel);
+    is_run = true;
+}
+
 void get_begin_nzs_of_BMW_after_nnz_blocking_in_row_direction::run(bool check) {
     auto &m = *meta_data_set_ptr;
     const auto &row = m.u(GLOBAL_META, "nz_row_indices", target_matrix_id);

@@ -251,6 +251,11 @@ class parent_bit_map_of_thread : public basic_data_transform_step {
 // balanced row-direction warp blocking (A11; data_transform_common.cc:934-989)
 GS_DECLARE_STEP_P(get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction, uint64_t, nnz_per_interval)
 GS_DECLARE_STEP_P(get_begin_nzs_of_BMW_after_nnz_blocking_in_row_direction, uint64_t, nnz_per_interval)
+// ... inside BMTBs (balanced_interval_row_direction_warp_blocking_operator.cc:165-207)
+GS_DECLARE_STEP_P(get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction_in_BMTB, uint64_t, nnz_per_interval)
+GS_DECLARE_STEP_P(get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction_relative_to_BMTB, uint64_t, nnz_per_interval)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMW_after_nnz_blocking_in_row_direction_in_BMTB, uint64_t, nnz_per_interval)
+GS_DECLARE_STEP_P(get_begin_nzs_of_BMW_after_nnz_blocking_in_row_direction_relative_to_BMTB, uint64_t, nnz_per_interval)
 
 // balanced row-direction TBLOCK / THREAD blocking without a parent (A11;
 // get_begin_{rows,nzs}_of_{BMTB,BMT}_after_nnz_blocking_in_row_direction.cc)

@@ -745,8 +745,26 @@ bool balanced_interval_row_direction_warp_blocking_operator::is_valid_according_
 // balanced_interval_row_direction_warp_blocking_operator.cc:177-227 (no-parent branch)
 void balanced_interval_row_direction_warp_blocking_operator::run(bool check) {
     if (check) GS_CHECK(is_valid_according_to_metadata(), "balanced warp blocking: invalid metadata");
-    if (has(TBLOCK_META, "first_row_indices"))
-        throw gs_error("balanced BMWs inside BMTBs are not built in this round");
+    if (has(TBLOCK_META, "first_row_indices")) {  // :165-207
+        const uint64_t per = (uint64_t)nnz_per_interval;
+        get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction_in_BMTB a(meta_data_set_ptr, target_matrix_id, per);
+        run_step(a, check);
+        if (row_index_is_relative_to_BMTB) {
+            get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction_relative_to_BMTB r(meta_data_set_ptr, target_matrix_id, per);
+            run_step(r, check);
+        }
+        get_begin_nzs_of_BMW_after_nnz_blocking_in_row_direction_in_BMTB b(meta_data_set_ptr, target_matrix_id, per);
+        run_step(b, check);
+        if (nz_index_is_relative_to_BMTB) {
+            get_begin_nzs_of_BMW_after_nnz_blocking_in_row_direction_relative_to_BMTB r(meta_data_set_ptr, target_matrix_id, per);
+            run_step(r, check);
+        }
+        get_begin_BMWs_of_BMTB_after_blocking_in_row_direction c(meta_data_set_ptr, target_matrix_id);
+        run_step(c, check);
+        code_generator_ptr->open_spec_level_of_paral(WARP_META);
+        is_run = true;
+        return;
+    }
     get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction a(meta_data_set_ptr, target_matrix_id,
                                                                (uint64_t)nnz_per_interval);
     run_step(a, check);

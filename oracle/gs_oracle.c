@@ -1226,6 +1226,47 @@ static int balanced_split(or_set *s, uint64_t per, const char *pos) {
 
 int or_balanced_row_dir_tblock_blocking(or_set *s, uint64_t per) { return balanced_split(s, per, "TBLOCK_META"); }
 
+/* A11 at WARP level inside BMTBs: balanced_interval_row_direction_warp_blocking_operator.cc:165-207
+ * with data_transform_common.cc:794-901: per BMTB a new BMW after the row whose running count
+ * reaches per, never at the BMTB's last row; absolute arrays end with row_num / the last BMTB
+ * nz, relative ones restart at 0 and have no ending; first_BMW_indices = BMWs before each BMTB */
+static int or_balanced_bmw_in_bmtb(or_set *s, uint64_t per, int rel) {
+    if (!per) return fail(s, "nnz_per_interval > 0");
+    or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
+    if (!R->len) return fail(s, "balanced BMWs of an empty sub-matrix");
+    uint64_t b = scalar(s, "GLOBAL_META", "begin_row_index", 0), e = scalar(s, "GLOBAL_META", "end_row_index", 0);
+    if (b + R->u[R->len - 1] > e) e = b + R->u[R->len - 1];
+    uint64_t row_num = e - b + 1;
+    uint64_t *cnt = row_nnz(R->u, R->len, row_num);
+    or_array *PR = get(s, "TBLOCK_META", "first_row_indices", 0), *PN = get(s, "TBLOCK_META", "first_nz_indices", 0);
+    vu rows = {0}, rrel = {0}, nzs = {0}, nrel = {0}, fb = {0};
+    for (uint64_t j = 0; j + 1 < PR->len; j++) {
+        vu_push(&fb, rows.n);
+        vu_push(&rows, PR->u[j]); vu_push(&rrel, 0); vu_push(&nzs, PN->u[j]); vu_push(&nrel, 0);
+        uint64_t run = 0, in_blk = 0;
+        for (uint64_t i = PR->u[j]; i < PR->u[j + 1]; i++) {
+            run += cnt[i]; in_blk += cnt[i];
+            if (run >= per && i != PR->u[j + 1] - 1) {
+                vu_push(&rows, i + 1); vu_push(&rrel, i + 1 - PR->u[j]);
+                vu_push(&nzs, PN->u[j] + in_blk); vu_push(&nrel, in_blk);
+                run = 0;
+            }
+        }
+    }
+    vu_push(&fb, rows.n);
+    vu_push(&rows, row_num);
+    vu_push(&nzs, PN->u[PN->len - 1]);
+    free(cnt);
+    put_u(s, "WARP_META", "first_row_indices", 0, rows.p, rows.n);
+    put_u(s, "WARP_META", "first_nz_indices", 0, nzs.p, nzs.n);
+    if (rel) {
+        put_u(s, "WARP_META", "first_row_indices_relative_to_BMTB", 0, rrel.p, rrel.n);
+        put_u(s, "WARP_META", "first_nz_indices_relative_to_BMTB", 0, nrel.p, nrel.n);
+    } else { free(rrel.p); free(nrel.p); }
+    put_u(s, "TBLOCK_META", "first_BMW_indices", 0, fb.p, fb.n);
+    return 0;
+}
+
 /* A11 at THREAD level, no parent: balanced_interval_row_direction_thread_blocking_operator.cc
  * (get_begin_{rows,nzs}_of_BMT_after_nnz_blocking_in_row_direction.cc:60-88) */
 int or_balanced_row_dir_thread_blocking(or_set *s, uint64_t per) { return balanced_split(s, per, "THREAD_META"); }
@@ -1661,6 +1702,10 @@ int or_pipeline(or_set *s, const char *name, int p0, int p1) {
     if (!strcmp(name, "tblock_thread_total")) { /* BMTB rows p0, BMT rows p1 inside them (relative too) */
         if (or_row_dir_tblock_blocking(s, p0)) return -1;
         return or_bmt_in_parent(s, p1 > 0 ? p1 : 1, 1, 1);
+    }
+    if (!strcmp(name, "tblock_balanced_warp_total")) { /* BMTBs of p0 rows, balanced BMWs of p1 nnz inside */
+        if (or_row_dir_tblock_blocking(s, p0 > 0 ? p0 : 64)) return -1;
+        return or_balanced_bmw_in_bmtb(s, p1 > 0 ? (uint64_t)p1 : 256, 1);
     }
     if (!strcmp(name, "tblock_thread_total_maxpad")) { /* every row (empty ones too) to its BMTB's longest */
         if (col_pad_max(s, p0 > 0 ? (uint64_t)p0 : 16, 1)) return -1;
