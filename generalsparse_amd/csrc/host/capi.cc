@@ -438,6 +438,15 @@ void run_pipeline(plan_state &s, const std::string &name, int N, int p0, int p1)
         ex.add_and_run(std::make_shared<warp_total_reduce_operator>(cg, cf, ctx));
         ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)((rows + rb - 1) / rb),
                                                              std::vector<unsigned>{64u, 4u}, cf, ctx));
+    } else if (name == "tblock_balanced_thread_total") {
+        // balanced BMTs of ~p1 nonzeros inside row-direction BMTBs of p0 rows, indices relative to
+        // the BMTB as well (balanced_interval_row_direction_thread_blocking_operator.cc:207-249)
+        int rb = p0 > 0 ? p0 : 64, per = p1 > 0 ? p1 : 64, cf = 1;
+        ex.add_and_run(std::make_shared<fixed_interval_row_direction_tblock_blocking_operator>(cg, rb, false, ctx));
+        ex.add_and_run(std::make_shared<balanced_interval_row_direction_thread_blocking_operator>(cg, per, true, true, ctx));
+        ex.add_and_run(std::make_shared<thread_total_reduce_operator>(cg, false, 1, cf, ctx));
+        ex.add_and_run(std::make_shared<grid_block_operator>(cg, (unsigned)((rows + rb - 1) / rb),
+                                                             std::vector<unsigned>{64u, 4u}, cf, ctx));
     } else if (name == "tblock_balanced_warp_total") {
         // balanced BMWs of ~p1 nonzeros inside row-direction BMTBs of p0 rows, indices relative
         // to the BMTB as well (balanced_interval_row_direction_warp_blocking_operator.cc:165-207)

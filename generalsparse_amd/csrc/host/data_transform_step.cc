@@ -1318,7 +1318,7 @@ namespace {
 struct bmw_in_bmtb {
     std::vector<uint64_t> rows, rows_rel, nzs, nzs_rel;
 };
-bmw_in_bmtb balanced_bmw_in_bmtb(const meta_data_set &m, int s, uint64_t per) {
+bmw_in_bmtb balanced_in_parent(const meta_data_set &m, int s, POS_TYPE parent, uint64_t per) {
     GS_CHECK(per > 0, "nnz_per_interval > 0");
     const auto &row = m.u(GLOBAL_META, "nz_row_indices", s);
     GS_CHECK(!row.empty(), "balanced BMWs of an empty sub-matrix");
@@ -1326,9 +1326,9 @@ bmw_in_bmtb balanced_bmw_in_bmtb(const meta_data_set &m, int s, uint64_t per) {
     const uint64_t e = std::max<uint64_t>(m.scalar(GLOBAL_META, "end_row_index", s), b + row.back());
     const uint64_t row_num = e - b + 1;
     auto cnt = get_nnz_of_each_row_in_spec_range(row, 0, row_num - 1, 0, row.size() - 1);
-    const auto &pr = m.u(TBLOCK_META, "first_row_indices", s);
-    const auto &pn = m.u(TBLOCK_META, "first_nz_indices", s);
-    GS_CHECK(pr.size() == pn.size() && pr.size() >= 2, "BMTB first_row_indices / first_nz_indices disagree");
+    const auto &pr = m.u(parent, "first_row_indices", s);
+    const auto &pn = m.u(parent, "first_nz_indices", s);
+    GS_CHECK(pr.size() == pn.size() && pr.size() >= 2, "parent first_row_indices / first_nz_indices disagree");
     bmw_in_bmtb o;
     for (size_t j = 0; j + 1 < pr.size(); j++) {
         o.rows.push_back(pr[j]);
@@ -1352,7 +1352,30 @@ bmw_in_bmtb balanced_bmw_in_bmtb(const meta_data_set &m, int s, uint64_t per) {
     o.nzs.push_back(pn.back());
     return o;
 }
+bmw_in_bmtb balanced_bmw_in_bmtb(const meta_data_set &m, int s, uint64_t per) { return balanced_in_parent(m, s, TBLOCK_META, per); }
+std::string rel_name(const char *base, POS_TYPE parent) {
+    return std::string(base) + (parent == WARP_META ? "_relative_to_BMW" : "_relative_to_BMTB");
+}
 }  // namespace
+
+void get_begin_rows_of_BMT_after_nnz_blocking_in_row_direction_in_parent::run(bool check) {
+    replace_u(THREAD_META, "first_row_indices", balanced_in_parent(*meta_data_set_ptr, target_matrix_id, parent_pos, nnz_per_interval).rows);
+    is_run = true;
+}
+void get_begin_rows_of_BMT_after_nnz_blocking_in_row_direction_relative_to_parent::run(bool check) {
+    replace_u(THREAD_META, rel_name("first_row_indices", parent_pos).c_str(),
+              balanced_in_parent(*meta_data_set_ptr, target_matrix_id, parent_pos, nnz_per_interval).rows_rel);
+    is_run = true;
+}
+void get_begin_nzs_of_BMT_after_nnz_blocking_in_row_direction_in_parent::run(bool check) {
+    replace_u(THREAD_META, "first_nz_indices", balanced_in_parent(*meta_data_set_ptr, target_matrix_id, parent_pos, nnz_per_interval).nzs);
+    is_run = true;
+}
+void get_begin_nzs_of_BMT_after_nnz_blocking_in_row_direction_relative_to_parent::run(bool check) {
+    replace_u(THREAD_META, rel_name("first_nz_indices", parent_pos).c_str(),
+              balanced_in_parent(*meta_data_set_ptr, target_matrix_id, parent_pos, nnz_per_interval).nzs_rel);
+    is_run = true;
+}
 
 void get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction_in_BMTB::run(bool check) {
     replace_u(WARP_META, "first_row_indices", balanced_bmw_in_bmtb(*meta_data_set_ptr, target_matrix_id, nnz_per_interval).rows);

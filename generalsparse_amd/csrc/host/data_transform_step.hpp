@@ -251,7 +251,23 @@ class parent_bit_map_of_thread : public basic_data_transform_step {
 // balanced row-direction warp blocking (A11; data_transform_common.cc:934-989)
 GS_DECLARE_STEP_P(get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction, uint64_t, nnz_per_interval)
 GS_DECLARE_STEP_P(get_begin_nzs_of_BMW_after_nnz_blocking_in_row_direction, uint64_t, nnz_per_interval)
-// ... inside BMTBs (balanced_interval_row_direction_warp_blocking_operator.cc:165-207)
+// balanced BMTs inside a BMTB / BMW parent: get_begin_{rows,nzs}_of_BMT_after_nnz_blocking_in_row_
+// direction_{in,relative_to}_{BMTB,BMW}.cc (one class per array, the parent level a parameter)
+#define GS_DECLARE_STEP_BAL(cls)                                                     \
+    class cls : public basic_data_transform_step {                                  \
+      public:                                                                       \
+        cls(std::shared_ptr<meta_data_set> m, int target_matrix_id, POS_TYPE parent_pos, uint64_t nnz_per_interval) \
+            : basic_data_transform_step(#cls, std::move(m), target_matrix_id), parent_pos(parent_pos), \
+              nnz_per_interval(nnz_per_interval) {}                                \
+        void run(bool check) override;                                              \
+        POS_TYPE parent_pos;                                                        \
+        uint64_t nnz_per_interval;                                                  \
+    };
+GS_DECLARE_STEP_BAL(get_begin_rows_of_BMT_after_nnz_blocking_in_row_direction_in_parent)
+GS_DECLARE_STEP_BAL(get_begin_rows_of_BMT_after_nnz_blocking_in_row_direction_relative_to_parent)
+GS_DECLARE_STEP_BAL(get_begin_nzs_of_BMT_after_nnz_blocking_in_row_direction_in_parent)
+GS_DECLARE_STEP_BAL(get_begin_nzs_of_BMT_after_nnz_blocking_in_row_direction_relative_to_parent)
+// ... BMWs inside BMTBs (balanced_interval_row_direction_warp_blocking_operator.cc:165-207)
 GS_DECLARE_STEP_P(get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction_in_BMTB, uint64_t, nnz_per_interval)
 GS_DECLARE_STEP_P(get_begin_rows_of_BMW_after_nnz_blocking_in_row_direction_relative_to_BMTB, uint64_t, nnz_per_interval)
 GS_DECLARE_STEP_P(get_begin_nzs_of_BMW_after_nnz_blocking_in_row_direction_in_BMTB, uint64_t, nnz_per_interval)

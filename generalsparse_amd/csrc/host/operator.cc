@@ -841,8 +841,28 @@ bool balanced_interval_row_direction_thread_blocking_operator::is_valid_accordin
 // the no-parent branch of run() (BMT rows / nzs over the whole sub-matrix)
 void balanced_interval_row_direction_thread_blocking_operator::run(bool check) {
     if (check) GS_CHECK(is_valid_according_to_metadata(), "balanced thread blocking: invalid metadata");
-    if (has(TBLOCK_META, "first_row_indices") || has(WARP_META, "first_row_indices"))
-        throw gs_error("balanced BMTs inside BMTB/BMW parents are not built in this round");
+    if (has(TBLOCK_META, "first_row_indices") || has(WARP_META, "first_row_indices")) {
+        // :162-249: inside the BMWs when there are BMWs, else inside the BMTBs
+        const POS_TYPE par = has(WARP_META, "first_row_indices") ? WARP_META : TBLOCK_META;
+        const uint64_t per = (uint64_t)nnz_per_interval;
+        get_begin_rows_of_BMT_after_nnz_blocking_in_row_direction_in_parent a(meta_data_set_ptr, target_matrix_id, par, per);
+        run_step(a, check);
+        if (row_index_is_relative_to_parent) {
+            get_begin_rows_of_BMT_after_nnz_blocking_in_row_direction_relative_to_parent r(meta_data_set_ptr, target_matrix_id, par, per);
+            run_step(r, check);
+        }
+        get_begin_nzs_of_BMT_after_nnz_blocking_in_row_direction_in_parent b(meta_data_set_ptr, target_matrix_id, par, per);
+        run_step(b, check);
+        if (nz_index_is_relative_to_parent) {
+            get_begin_nzs_of_BMT_after_nnz_blocking_in_row_direction_relative_to_parent r(meta_data_set_ptr, target_matrix_id, par, per);
+            run_step(r, check);
+        }
+        get_begin_BMTs_of_specific_parent_after_blocking_in_row_direction e(meta_data_set_ptr, target_matrix_id, par, 1);
+        run_step(e, check);
+        code_generator_ptr->open_spec_level_of_paral(THREAD_META);
+        is_run = true;
+        return;
+    }
     if (row_index_is_relative_to_parent || nz_index_is_relative_to_parent)
         throw gs_error("relative BMT indices need a parent level");
     get_begin_rows_of_BMT_after_nnz_blocking_in_row_direction a(meta_data_set_ptr, target_matrix_id,

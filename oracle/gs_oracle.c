@@ -1230,7 +1230,8 @@ int or_balanced_row_dir_tblock_blocking(or_set *s, uint64_t per) { return balanc
  * with data_transform_common.cc:794-901: per BMTB a new BMW after the row whose running count
  * reaches per, never at the BMTB's last row; absolute arrays end with row_num / the last BMTB
  * nz, relative ones restart at 0 and have no ending; first_BMW_indices = BMWs before each BMTB */
-static int or_balanced_bmw_in_bmtb(or_set *s, uint64_t per, int rel) {
+static int or_balanced_in_parent(or_set *s, uint64_t per, int rel, const char *child, const char *parent,
+                                 const char *rel_suffix, const char *first_child) {
     if (!per) return fail(s, "nnz_per_interval > 0");
     or_array *R = get(s, "GLOBAL_META", "nz_row_indices", 0);
     if (!R->len) return fail(s, "balanced BMWs of an empty sub-matrix");
@@ -1238,7 +1239,7 @@ static int or_balanced_bmw_in_bmtb(or_set *s, uint64_t per, int rel) {
     if (b + R->u[R->len - 1] > e) e = b + R->u[R->len - 1];
     uint64_t row_num = e - b + 1;
     uint64_t *cnt = row_nnz(R->u, R->len, row_num);
-    or_array *PR = get(s, "TBLOCK_META", "first_row_indices", 0), *PN = get(s, "TBLOCK_META", "first_nz_indices", 0);
+    or_array *PR = get(s, parent, "first_row_indices", 0), *PN = get(s, parent, "first_nz_indices", 0);
     vu rows = {0}, rrel = {0}, nzs = {0}, nrel = {0}, fb = {0};
     for (uint64_t j = 0; j + 1 < PR->len; j++) {
         vu_push(&fb, rows.n);
@@ -1257,14 +1258,20 @@ static int or_balanced_bmw_in_bmtb(or_set *s, uint64_t per, int rel) {
     vu_push(&rows, row_num);
     vu_push(&nzs, PN->u[PN->len - 1]);
     free(cnt);
-    put_u(s, "WARP_META", "first_row_indices", 0, rows.p, rows.n);
-    put_u(s, "WARP_META", "first_nz_indices", 0, nzs.p, nzs.n);
+    char nm[96];
+    put_u(s, child, "first_row_indices", 0, rows.p, rows.n);
+    put_u(s, child, "first_nz_indices", 0, nzs.p, nzs.n);
     if (rel) {
-        put_u(s, "WARP_META", "first_row_indices_relative_to_BMTB", 0, rrel.p, rrel.n);
-        put_u(s, "WARP_META", "first_nz_indices_relative_to_BMTB", 0, nrel.p, nrel.n);
+        snprintf(nm, sizeof nm, "first_row_indices_relative_to_%s", rel_suffix);
+        put_u(s, child, nm, 0, rrel.p, rrel.n);
+        snprintf(nm, sizeof nm, "first_nz_indices_relative_to_%s", rel_suffix);
+        put_u(s, child, nm, 0, nrel.p, nrel.n);
     } else { free(rrel.p); free(nrel.p); }
-    put_u(s, "TBLOCK_META", "first_BMW_indices", 0, fb.p, fb.n);
+    put_u(s, parent, first_child, 0, fb.p, fb.n);
     return 0;
+}
+static int or_balanced_bmw_in_bmtb(or_set *s, uint64_t per, int rel) {
+    return or_balanced_in_parent(s, per, rel, "WARP_META", "TBLOCK_META", "BMTB", "first_BMW_indices");
 }
 
 /* A11 at THREAD level, no parent: balanced_interval_row_direction_thread_blocking_operator.cc
@@ -1702,6 +1709,11 @@ int or_pipeline(or_set *s, const char *name, int p0, int p1) {
     if (!strcmp(name, "tblock_thread_total")) { /* BMTB rows p0, BMT rows p1 inside them (relative too) */
         if (or_row_dir_tblock_blocking(s, p0)) return -1;
         return or_bmt_in_parent(s, p1 > 0 ? p1 : 1, 1, 1);
+    }
+    if (!strcmp(name, "tblock_balanced_thread_total")) { /* BMTBs of p0 rows, balanced BMTs of p1 nnz inside */
+        if (or_row_dir_tblock_blocking(s, p0 > 0 ? p0 : 64)) return -1;
+        return or_balanced_in_parent(s, p1 > 0 ? (uint64_t)p1 : 64, 1, "THREAD_META", "TBLOCK_META", "BMTB",
+                                     "first_BMT_indices");
     }
     if (!strcmp(name, "tblock_balanced_warp_total")) { /* BMTBs of p0 rows, balanced BMWs of p1 nnz inside */
         if (or_row_dir_tblock_blocking(s, p0 > 0 ? p0 : 64)) return -1;

@@ -1,4 +1,5 @@
-"""Balanced row-direction BMWs inside row-direction BMTBs (SURVEY.md §8a A11 inside a parent;
+"""Balanced row-direction BMWs (and BMTs: tblock_balanced_thread_total,
+balanced_interval_row_direction_thread_blocking_operator.cc:162-249) inside row-direction BMTBs (SURVEY.md §8a A11 inside a parent;
 balanced_interval_row_direction_warp_blocking_operator.cc:165-207 with
 data_transform_common.cc:794-901): the tblock_balanced_warp_total plans (BMTBs of p0 rows,
 BMWs cut after the row whose running count reaches p1 nonzeros, never at a BMTB's last row;
@@ -17,7 +18,10 @@ import oracle_ffi as ofi  # noqa: E402
 import generalsparse_amd as gsa  # noqa: E402
 from generalsparse_amd import datasets as ds  # noqa: E402
 
-PIPES = [(64, 256), (16, 40), (5, 3), (100, 1000)]
+PIPES = [("tblock_balanced_warp_total", 64, 256), ("tblock_balanced_warp_total", 16, 40),
+         ("tblock_balanced_warp_total", 5, 3), ("tblock_balanced_warp_total", 100, 1000),
+         ("tblock_balanced_thread_total", 64, 64), ("tblock_balanced_thread_total", 16, 8),
+         ("tblock_balanced_thread_total", 7, 3)]
 
 
 def cases():
@@ -26,13 +30,13 @@ def cases():
     yield (1024, 1024) + tuple(ds.rmat(1024, 20000, seed=2))
 
 
-@pytest.mark.parametrize("pipe", PIPES, ids=lambda p: f"{p[0]}-{p[1]}")
+@pytest.mark.parametrize("pipe", PIPES, ids=lambda p: f"{p[0]}-{p[1]}-{p[2]}")
 def test_plans_bit_exact(pipe):
-    p0, p1 = pipe
+    name, p0, p1 = pipe
     for M, K, r, c, v in cases():
-        exp, err = ofi.run_pipeline(M, K, r, c, v, "tblock_balanced_warp_total", p0, p1)
+        exp, err = ofi.run_pipeline(M, K, r, c, v, name, p0, p1)
         assert err is None, err
-        p = gsa.Plan.from_coo(M, K, r, c, v).run_pipeline("tblock_balanced_warp_total", 32, p0, p1)
+        p = gsa.Plan.from_coo(M, K, r, c, v).run_pipeline(name, 32, p0, p1)
         got = p.arrays()
         assert set(got) == set(exp), set(got) ^ set(exp)
         for key, arr in exp.items():
@@ -61,13 +65,13 @@ def test_hand_case():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["f32", "f16"])
-@pytest.mark.parametrize("pipe", PIPES, ids=lambda p: f"{p[0]}-{p[1]}")
+@pytest.mark.parametrize("pipe", PIPES, ids=lambda p: f"{p[0]}-{p[1]}-{p[2]}")
 def test_plans_on_gpu(pipe, dtype):
     torch = pytest.importorskip("torch")
-    p0, p1 = pipe
+    name, p0, p1 = pipe
     for N in (8, 32):
         for M, K, row, col, val in cases():
-            plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline("tblock_balanced_warp_total", N, p0, p1)
+            plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline(name, N, p0, p1)
             plan.compile().upload(dtype, 0)
             npdt = np.float16 if dtype == "f16" else np.float32
             B = np.random.default_rng(3).uniform(-1, 1, (K, N)).astype(npdt)
