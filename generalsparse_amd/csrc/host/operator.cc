@@ -1427,13 +1427,20 @@ bool warp_segment_reduce_operator::is_valid_according_to_metadata() {
 // warp_segment_reduce_operator.cc:74-111; merge_num = VECTOR_WIDTH
 void warp_segment_reduce_operator::run(bool check) {
     GS_CHECK(is_valid_according_to_metadata(), "warp_segment_reduce: invalid metadata");
-    if (relative_nz || relative_row) throw gs_error("relative BMW indices are not built in this round");
     int vw = (int)get_config().VECTOR_WIDTH;
     GS_CHECK(vw >= 1, "VECTOR_WIDTH >= 1");
     get_begin_rows_after_merge_thread a(meta_data_set_ptr, WARP_META, vw, target_matrix_id);
     run_step(a, check);
     get_begin_nzs_after_merge_thread b(meta_data_set_ptr, WARP_META, vw, target_matrix_id);
     run_step(b, check);
+    if (relative_row) {  // :86-91
+        get_begin_rows_relative_to_parent_after_merge_thread r(meta_data_set_ptr, WARP_META, vw, target_matrix_id);
+        run_step(r, check);
+    }
+    if (relative_nz) {  // :93-98
+        get_begin_nzs_relative_to_parent_after_merge_thread r(meta_data_set_ptr, WARP_META, vw, target_matrix_id);
+        run_step(r, check);
+    }
     get_begin_BMTs_after_merge_thread c(meta_data_set_ptr, WARP_META, vw, target_matrix_id);
     run_step(c, check);
     reduction_token t;

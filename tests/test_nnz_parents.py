@@ -136,3 +136,28 @@ def test_plans_on_gpu(pipe, dtype):
         err = np.abs(C - ref) / np.maximum(1.0, np.abs(ref))
         assert err.max() <= (1e-1 if dtype == "f16" else 1e-3), (name, err.max())
         plan.free()
+
+
+def test_warp_segment_relative_indices():
+    """warp_segment_reduce_operator with relative_row / relative_nz (warp_segment_reduce_operator.cc
+    :86-98): the BMTs' row and nz starts relative to their BMW, written next to the absolute
+    ones; every relative start = absolute start - its BMW's start, and logical_check holds"""
+    r, c, v = ds.random_rows(300, 200, 12.0, seed=1, empty_frac=0.15)
+    gsa.set_config("DENSE_MATRIX_SIZE", 32)
+    gsa.set_config("VECTOR_WIDTH", 32)
+    p = gsa.Plan.from_coo(300, 200, r, c, v)
+    p.add_operator("fixed_interval_nnz_direction_thread_blocking_operator", 32, 0, 0, 1)
+    p.add_operator("thread_bit_map_operator", 2, 32, 4, 1)
+    p.add_operator("warp_segment_reduce_operator", 1, 1, 1)
+    a = p.arrays()
+    rel_row = a["WARP_META_first_row_indices_relative_to_BMW_0"]
+    rel_nz = a["THREAD_META_first_nz_indices_relative_to_BMW_0"]
+    fb = a["WARP_META_first_BMT_indices_0"]
+    wr, wn = a["WARP_META_first_row_indices_0"], a["WARP_META_first_nz_indices_0"]
+    tr, tn = a["THREAD_META_first_row_indices_0"], a["THREAD_META_first_nz_indices_0"]
+    for w in range(len(fb) - 1):
+        for t in range(int(fb[w]), int(fb[w + 1])):
+            assert rel_nz[t] == tn[t] - wn[w]
+            if t < len(rel_row):
+                assert rel_row[t] == tr[t] - wr[w]
+    assert p.logical_check() == ""
