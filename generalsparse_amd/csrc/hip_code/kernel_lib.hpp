@@ -1413,40 +1413,119 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
 }
 
 // ---------------------------------------------------------------------------
-// k_mfma_wk -- BMTB row blocks on the matrix cores, one wave per k-step stream
-// (MFMA_WK): workgroup g owns BMTB g (R <= 16*RT rows); wave w owns the 32-column
-// k-steps w, w+16, ... of K and runs them start to finish on its own -- B rows of the
-// step and the step's entries into registers (four steps ahead), then its private LDS
-// stage: B slice stored (32-B pieces permuted by b_piece for conflict-free transposed
-// reads), entries scattered into a zeroed 32-column dense slice (row stride 80 B, row
-// R stays zero for MFMA rows >= R), fragments read, v_mfma_f32_16x16x32_f16, slice
-// rows cleared.  No workgroup barrier until the end, where the 16 partial tiles are
-// summed in wave order through LDS (deterministic) and rows < R stored.
-// Entries (upload layout): per (BMTB, k-step) a run of u32 = halfword index in the
-// slice (row*40 + col - 32*step) | f16 value << 16; seg[] the run starts.
+// k_mfma_ks -- BMTB row blocks on the matrix cores with K split over S workgroups
+// and every wave running on its own (the default matrix-core kernel for row blocks of
+// >= 40 rows).
+// Why: a workgroup that owns a row block over all of K streams all of B (327 KB on C2)
+// for its ~120 KB of A; one CU takes in ~50-70 GB/s, so B, not A, set the time
+// (scripts/probes/probe_floor.hip: loading A + B alone takes 10.9 us at S = 1, 7.2 us at
+// S = 4).  Here workgroup (g, q) owns row block g over the K range [q*KR, q*KR + KR) and
+// reads only that slice of B (KR rows).
+// Wave w owns the range's 32-column k-steps w, w+W, ... and runs them with no
+// workgroup barrier until the end: per k-step it loads (D steps ahead, into registers)
+// the step's 32 B rows and its entries (upload layout: GCAP groups per step, each 8 x
+// [u16 halfword position in the wave's dense image] + 8 x [f16 value]; padding writes 0
+// into the image's zero row), stores the B rows into its private stage (32-B pieces
+// permuted by b_piece so the ds_read_b64_tr_b16 fragment reads are conflict-free),
+// scatters the entries into its private image of 16*RT+1 rows x 96 B (conflict-free
+// ds_read_b128), reads the RT A fragments and the CT B fragments, writes zeros back at
+// the entries' positions, and runs RT x CT v_mfma_f32_16x16x32_f16 into fp32
+// accumulators.  Every step issues the same loads (steps past the wave's last read the
+// first B rows and the spare group: one cached line each), so the compiler's waits
+// stay counted ones.  At the end the W partial tiles are summed through LDS in wave
+// order; with S > 1 each workgroup publishes its fp32 slab (16-B sc1 write-through
+// stores, drained by every storing wave, then one arrival add), and the last of the row
+// block's S workgroups sums the S slabs in q order (deterministic, whichever arrives
+// last) and writes C: the hand-off form of MI355X_MICROARCH.md §Workgroup dispatch,
+// table row 1 (sc1 stores + vmcnt(0) + barrier + one agent add; the last adder, told by
+// the returned value, loads with sc1 loads after a barrier).  Workgroup order: unit
+// u = g*S + q, XCD-contiguous (xcd_block), so a row block's S workgroups are normally on
+// one XCD (speed only).  Rows of B past K are stored as zeros; a zero of the dense tile
+// times a non-finite in-range B value gives NaN for the row block (DESIGN.md deviation,
+// as for k_mfma_rows).
 // ---------------------------------------------------------------------------
-constexpr uint32_t kWkWaves = 16, kWkRss = 80, kWkRows = 33;
+// s_waitcnt immediate (gfx9 encoding) waiting for vmcnt <= N only (expcnt / lgkmcnt at their maxima)
+template <int N>
+__device__ constexpr int vmcnt_imm() {
+    static_assert(N >= 0 && N < 64, "vmcnt is six bits");
+    return (N & 0xF) | ((N >> 4) << 14) | 0x70 | 0xF00;
+}
 
-template <int CT, int RT, int EMAX>
-__global__ __launch_bounds__(64 * kWkWaves) void k_mfma_wk(const uint32_t *__restrict__ bmtb_first_row,
-                                                          const uint32_t *__restrict__ seg,
-                                                          const uint32_t *__restrict__ ent,
-                                                          const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K,
-                                                          uint32_t N, uint32_t nsteps, uint32_t row_base) {
-    constexpr uint32_t RB = 32 * CT, UB = 2 * CT;
-    constexpr uint32_t BS = 32 * RB, DS = kWkRows * kWkRss, STG = BS + DS;
-    constexpr uint32_t NBU = (32 * UB + 63) / 64;  // B units per lane per step
+constexpr uint32_t kKsStride = 96;  // image row stride: conflict-free ds_read_b128 fragment reads
+
+template <int RT>
+__host__ __device__ constexpr uint32_t ks_image_bytes() {
+    return (16u * RT + 1u) * kKsStride;
+}
+
+// dynamic LDS of k_mfma_ks: W x (wave image + one k-step of B rows), or the W partial
+// tiles of the final reduction (+ the arrival flag), whichever is larger
+__host__ __device__ constexpr size_t ks_lds_bytes(uint32_t CT, uint32_t RT, uint32_t W) {
+    const size_t stage = (size_t)W * ((16u * RT + 1u) * kKsStride + 32u * 32u * CT);
+    const size_t red = (size_t)W * RT * CT * 1024u + 16u;
+    return stage > red ? stage : red;
+}
+
+// STAMPS (diagnostic build only, gs_debug_mfma_timeline): lane 0 of every wave records
+// s_memtime into stamps[(workgroup * W + wave) * 32 + slot]: 0 start, 1 loads issued,
+// 3 + i after step i (i < 16), 20 loop done, 21 reduced, 22 end
+template <int CT, int RT, int W, int D, int MAXG, bool STAMPS = false>
+__global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__ bmtb_first_row,  // nb+1
+                                                    const u32x4 *__restrict__ tP,  // 8 x u16 position per group
+                                                    const u32x4 *__restrict__ tV,  // 8 x f16 value per group
+                                                    const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K,
+                                                    uint32_t N, uint32_t S, uint32_t NS, uint32_t GCAP, uint32_t nwg,
+                                                    uint32_t row_base, float *__restrict__ slabs,
+                                                    uint32_t *__restrict__ arrivals, uint64_t *__restrict__ stamps = nullptr) {
+    constexpr uint32_t RB = 32 * CT;  // bytes per B row (N == 16 * CT)
+    constexpr uint32_t UB = 2 * CT;   // 16-B units per B row
+    constexpr uint32_t IMG = ks_image_bytes<RT>();
+    constexpr uint32_t STG = 32u * RB;  // one k-step of B rows
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t g = blockIdx.x;
-    const uint32_t r0 = bmtb_first_row[g], R = bmtb_first_row[g + 1] - r0;
-    unsigned char *bb = lds + wv * STG;
-    unsigned char *dd = bb + BS;
+    const uint32_t u = xcd_block(blockIdx.x, nwg);  // nwg == gridDim.x (an argument: kernarg preload)
+    const uint32_t g = u / S, q = u - g * S;
+#define GS_KS_STAMP(slot)                                                                          \
+    if constexpr (STAMPS) {                                                                        \
+        if (lane == 0) stamps[((size_t)blockIdx.x * W + wv) * 32u + (slot)] = __builtin_amdgcn_s_memtime(); \
+    }
+    GS_KS_STAMP(0u);
+    const uint32_t k0 = q * NS * 32u;
+    unsigned char *img = lds + wv * (IMG + STG);
+    unsigned char *bst = img + IMG;
     const u32x4 zero4 = {0u, 0u, 0u, 0u};
-    for (uint32_t u = lane; u < DS / 16u; u += 64u) *reinterpret_cast<u32x4 *>(dd + u * 16u) = zero4;
-    const uint32_t nsw = nsteps > wv ? (nsteps - wv + kWkWaves - 1) / kWkWaves : 0u;  // this wave's steps
-    const uint32_t *segg = seg + (size_t)g * nsteps;
+
+    // ---- this wave's k-steps w, w+W, ...: step s of unit u is GCAP groups at (u*NS + s)*GCAP
+    // (every step padded to the plan's largest, so no address waits on a load)
+    const uint32_t nsw = NS > wv ? (NS - wv + W - 1u) / W : 0u;
+    const size_t ubase = (size_t)u * NS * GCAP;
+    u32x4 P[D][MAXG], V[D][MAXG], BR[D][CT];
+    // steps past the wave's last re-read the unit's first step (cached; the same lane-varying
+    // load form as a live step, so no path of the loop issues a different count)
+    auto load_set = [&](uint32_t i, u32x4 (&P_)[MAXG], u32x4 (&V_)[MAXG], u32x4 (&B_)[CT]) {
+        const uint32_t st = __builtin_amdgcn_readfirstlane(i < nsw ? wv + i * W : 0u);
+        const size_t b0 = ubase + (size_t)st * GCAP;
+        const uint32_t kr = k0 + st * 32u;  // first B row of the step
+#pragma unroll
+        for (int c = 0; c < CT; c++) {
+            const uint32_t un = lane + 64u * c;  // 16-B unit of the step's 32 rows
+            const uint32_t k = kr + un / UB;
+            B_[c] = *reinterpret_cast<const u32x4 *>(B + (size_t)(k < K ? k : K - 1u) * N + (un % UB) * 8u);
+        }
+#pragma unroll
+        for (int j = 0; j < MAXG; j++) {
+            const uint32_t qg = lane + 64u * j;
+            const size_t at = b0 + (qg < GCAP ? qg : 0u);
+            P_[j] = tP[at];
+            V_[j] = tV[at];
+        }
+    };
+#pragma unroll
+    for (int d = 0; d < D; d++) load_set((uint32_t)d, P[d], V[d], BR[d]);
+    for (uint32_t x = lane; x < IMG / 16u; x += 64u) *reinterpret_cast<u32x4 *>(img + x * 16u) = zero4;
+    GS_KS_STAMP(1u);
+
     f4v acc[RT][CT];
 #pragma unroll
     for (int rt = 0; rt < RT; rt++)
@@ -1454,343 +1533,148 @@ __global__ __launch_bounds__(64 * kWkWaves) void k_mfma_wk(const uint32_t *__res
         for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
     uint32_t arow[RT];
 #pragma unroll
-    for (int rt = 0; rt < RT; rt++) {
-        const uint32_t row = 16u * rt + (lane & 15u);
-        arow[rt] = (row < R ? row : R) * kWkRss + 16u * (lane >> 4);
-    }
-    u32x4 b0[NBU], b1[NBU], b2[NBU], b3[NBU];
-    uint32_t e0[EMAX], e1[EMAX], e2[EMAX], e3[EMAX];
-#define GS_WK_LOAD(i, BV, EV)                                                                       \
-    {                                                                                             \
-        const uint32_t st_ = wv + (uint32_t)(i) * kWkWaves;                                       \
-        const bool live_ = (uint32_t)(i) < nsw;                                                   \
-        _Pragma("unroll") for (uint32_t j = 0; j < NBU; j++) {                                    \
-            const uint32_t u = lane + 64u * j, k = st_ * 32u + u / UB;                            \
-            BV[j] = live_ && u < 32u * UB && k < K                                                \
-                        ? *reinterpret_cast<const u32x4 *>(B + (size_t)k * N + (u % UB) * 8u)     \
-                        : zero4;                                                                  \
-        }                                                                                         \
-        const uint32_t s0_ = live_ ? segg[st_] : 0u, n_ = live_ ? segg[st_ + 1] - s0_ : 0u;       \
-        _Pragma("unroll") for (int j = 0; j < EMAX; j++) {                                        \
-            const uint32_t x = lane + 64u * j;                                                    \
-            EV[j] = x < n_ ? ent[s0_ + x] : 0xffffffffu;                                          \
-        }                                                                                         \
-    }
-#define GS_WK_STEP(i, BV, EV)                                                                       \
-    if ((uint32_t)(i) < nsw) {                                                                    \
-        _Pragma("unroll") for (uint32_t j = 0; j < NBU; j++) {                                    \
-            const uint32_t u = lane + 64u * j;                                                    \
-            if (u < 32u * UB) {                                                                   \
-                const uint32_t k = u / UB, sb = u % UB;                                           \
-                *reinterpret_cast<u32x4 *>(bb + k * RB + b_piece<CT>(k, sb >> 1) * 32u + (sb & 1u) * 16u) = BV[j]; \
-            }                                                                                     \
-        }                                                                                         \
-        _Pragma("unroll") for (int j = 0; j < EMAX; j++)                                          \
-            if (EV[j] != 0xffffffffu)                                                             \
-                *reinterpret_cast<uint16_t *>(dd + (EV[j] & 0xffffu) * 2u) = (uint16_t)(EV[j] >> 16); \
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");                                    \
-        __builtin_amdgcn_wave_barrier();                                                          \
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");                                    \
-        h8v av_[RT], bv_[CT];                                                                     \
-        _Pragma("unroll") for (int rt = 0; rt < RT; rt++) av_[rt] = *reinterpret_cast<const h8v *>(dd + arow[rt]); \
-        _Pragma("unroll") for (int ct = 0; ct < CT; ct++) {                                       \
-            s4v t_[2];                                                                            \
-            _Pragma("unroll") for (int h = 0; h < 2; h++) {                                       \
-                const uint32_t k = 8u * (lane >> 4) + 4u * h + ((lane & 15u) >> 2);               \
-                t_[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(                                  \
-                    (lds_s4v *)(bb + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u));      \
-            }                                                                                     \
-            __builtin_memcpy(&bv_[ct], t_, 16);                                                   \
-        }                                                                                         \
-        _Pragma("unroll") for (int rt = 0; rt < RT; rt++)                                         \
-            _Pragma("unroll") for (int ct = 0; ct < CT; ct++)                                     \
-                acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av_[rt], bv_[ct], acc[rt][ct], 0, 0, 0); \
-        /* the MFMAs consumed the reads: clear the slice rows the scatter can write */           \
-        for (uint32_t u = lane; u < R * 4u; u += 64u)                                             \
-            *reinterpret_cast<u32x4 *>(dd + (u >> 2) * kWkRss + (u & 3u) * 16u) = zero4;          \
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");                                    \
-        __builtin_amdgcn_wave_barrier();                                                          \
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");                                    \
-    }
-    GS_WK_LOAD(0, b0, e0);
-    GS_WK_LOAD(1, b1, e1);
-    GS_WK_LOAD(2, b2, e2);
-    GS_WK_LOAD(3, b3, e3);
-    for (uint32_t i = 0; i < nsw; i += 4) {
-        GS_WK_STEP(i, b0, e0);
-        GS_WK_LOAD(i + 4, b0, e0);
-        GS_WK_STEP(i + 1, b1, e1);
-        GS_WK_LOAD(i + 5, b1, e1);
-        GS_WK_STEP(i + 2, b2, e2);
-        GS_WK_LOAD(i + 6, b2, e2);
-        GS_WK_STEP(i + 3, b3, e3);
-        GS_WK_LOAD(i + 7, b3, e3);
-    }
-#undef GS_WK_STEP
-#undef GS_WK_LOAD
-    // fixed-order sum of the 16 waves' partial tiles
-    __syncthreads();
-    f4v *red = reinterpret_cast<f4v *>(lds);
-#pragma unroll
-    for (int rt = 0; rt < RT; rt++)
-#pragma unroll
-        for (int ct = 0; ct < CT; ct++) red[((wv * RT + rt) * CT + ct) * 64u + lane] = acc[rt][ct];
-    __syncthreads();
-    const float *redf = reinterpret_cast<const float *>(lds);
-    for (uint32_t e = tid; e < (uint32_t)(RT * CT) * 256u; e += 64u * kWkWaves) {
-        const uint32_t cc = e & 15u, rr = (e >> 4) & 15u, tt = e >> 8;
-        const uint32_t rt = tt / CT, ct = tt % CT;
-        const uint32_t ln = 16u * (rr >> 2) + cc, i = rr & 3u;
-        float sum = 0.f;
-        for (uint32_t w = 0; w < kWkWaves; w++) sum += redf[(((w * RT + rt) * CT + ct) * 64u + ln) * 4u + i];
-        const uint32_t row = 16u * rt + rr;
-        if (row < R) C[(size_t)(row_base + r0 + row) * N + 16u * ct + cc] = (f16)sum;
-    }
-}
+    for (int rt = 0; rt < RT; rt++) arow[rt] = (16u * rt + (lane & 15u)) * kKsStride + 16u * (lane >> 4);
 
-// ---------------------------------------------------------------------------
-// k_mfma_bitmap -- BMTB row blocks on the matrix cores from bitmap panels (the
-// default matrix-core layout of fp16 tblock/warp/block-total plans).
-// Upload layout (device_plan.hip build_bitmap_panels): per BMTB g and 32-column
-// k-step t one segment, 16-B aligned and at most 1 KB: R u32 row masks (bit c =
-// column 32t+c of that row holds an entry), then the entries' f16 values row
-// after row in column order; seg[g*nks + t] = its start in 16-B units.  A costs
-// 2 B per entry + 4 B per (row, k-step) instead of the 4 B per entry of a u16
-// CSR, and nothing is densified through LDS.
-// Workgroup = W waves over one BMTB; wave w owns k-steps w, w+W, ... and runs
-// them alone (no barrier in the loop): per k-step one LDS-DMA of its segment
-// into the wave's A ring (DA slots) and CT LDS-DMAs of the 32 B rows into its B
-// ring (DB slots, 32-B pieces XOR-permuted through the source address), issued
-// DA-1 / DB-1 k-steps ahead and retired by a counted vmcnt.  A fragments are
-// expanded in registers: lane (row r, k-group kg) takes byte kg of row r's mask,
-// its values' offset = the rows' popcounts scanned over 16 lanes by DPP + the
-// popcount of the lower bytes, reads each 4-column quad's values with one
-// (unaligned) ds_read_b64 and places them with two v_perm_b32 whose selectors
-// come from a 16-entry table in LDS.  B fragments by ds_read_b64_tr_b16.
-// v_mfma_f32_16x16x32_f16 into fp32 accumulators; the waves' partial tiles are
-// summed in wave order through LDS (deterministic).  Rows past R read mask 0.
-// Like every dense-tile kernel, a zero of the tile times a non-finite B value
-// gives NaN for the row block (MFMA_TILES=0 keeps the reference's
-// per-entry semantics).
-// ---------------------------------------------------------------------------
-constexpr uint32_t kBmSeg = 1024;  // max bytes of one k-step segment (one LDS-DMA)
-
-// one 64-lane LDS-DMA of 16 B per lane: lane l's 16 bytes land at lds_dst + 16 l
-__device__ __forceinline__ void dma16(const void *gsrc, uint32_t lds_dst) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds_dst)
-                 : "memory");
-}
-
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// wait until at most n vector-memory operations of this wave are outstanding
-// (n wave-uniform; above 15 the wait is for 15, i.e. for more than asked)
-__device__ __forceinline__ void vm_wait_dyn(uint32_t n) {
-    switch (n) {
-        case 0: vm_wait<0>(); break;
-        case 1: vm_wait<1>(); break;
-        case 2: vm_wait<2>(); break;
-        case 3: vm_wait<3>(); break;
-        case 4: vm_wait<4>(); break;
-        case 5: vm_wait<5>(); break;
-        case 6: vm_wait<6>(); break;
-        case 7: vm_wait<7>(); break;
-        case 8: vm_wait<8>(); break;
-        case 9: vm_wait<9>(); break;
-        case 10: vm_wait<10>(); break;
-        case 11: vm_wait<11>(); break;
-        case 12: vm_wait<12>(); break;
-        case 13: vm_wait<13>(); break;
-        case 14: vm_wait<14>(); break;
-        default: vm_wait<15>(); break;
-    }
-}
-
-// selectors of the quad expansion: nibble q (bit i = column i of the quad holds an
-// entry) -> two v_perm_b32 selectors over the quad's packed values (8 bytes):
-// half i of the output = packed half popcount(q & ((1 << i) - 1)) if bit i, else 0
-__device__ __forceinline__ uint2 bm_quad_selectors(uint32_t q) {
-    uint32_t s[2];
+    // step i on its set, then the set is reloaded with step i + D (issued whether or not
+    // step i exists: every loop iteration issues the same loads)
+    auto step = [&](uint32_t i, u32x4 (&P_)[MAXG], u32x4 (&V_)[MAXG], u32x4 (&B_)[CT]) {
+        const bool live = i < nsw;  // wave-uniform
+        h8v av[RT], bv[CT];
+        if (live) {
+            const uint32_t kr = k0 + (wv + i * W) * 32u;
+            // the step's B rows into the stage (rows past K as zeros)
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
-        uint32_t sel = 0;
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const uint32_t i = 2u * j + h, r = __builtin_popcount(q & ((1u << i) - 1u));
-            const uint32_t lo = (q >> i) & 1u ? 2u * r : 12u, hi = (q >> i) & 1u ? 2u * r + 1u : 12u;
-            sel |= (lo | (hi << 8)) << (16 * h);
-        }
-        s[j] = sel;
-    }
-    return make_uint2(s[0], s[1]);
-}
-
-// DBG (diagnostic timing builds only, wrong results): 1 = window reads rounded down to
-// 8-B alignment, 2 = no A expansion (zero A fragments), 4 = no B fragment reads
-template <int CT, int RT, int W, int DA, int DB, int DBG = 0>
-__global__ __launch_bounds__(64 * W) void k_mfma_bitmap(const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
-                                                       const uint32_t *__restrict__ seg,  // n_bmtb*nks+1 (16-B units)
-                                                       const u32x4 *__restrict__ A,       // segments
-                                                       const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K,
-                                                       uint32_t N, uint32_t nks, uint32_t row_base) {
-    static_assert(DA >= DB && DB >= 2, "A ring at least as deep as the B ring");
-    constexpr uint32_t RB = 32 * CT, UB = 2 * CT;  // bytes / 16-B units per B row (N == 16*CT)
-    constexpr uint32_t SB = 32 * RB;               // B slot: the 32 rows of a k-step
-    constexpr uint32_t WL = DA * kBmSeg + DB * SB; // LDS per wave
-    constexpr uint32_t STEADY = (DB - 1) * (1 + CT);  // DMAs issued after B(i) once the rings run full
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t g = blockIdx.x;
-    const uint32_t r0 = bmtb_first_row[g], R = bmtb_first_row[g + 1] - r0;
-    const uint32_t ra = wv * WL, rb = ra + DA * kBmSeg;  // A ring, B ring (offsets in lds[])
-    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char *)lds;
-    uint2 *lut = reinterpret_cast<uint2 *>(lds + W * WL);
-    if (tid < 16u) lut[tid] = bm_quad_selectors(tid);
-    // this wave's k-steps t_i = (rot + wv + i*W) mod nks (i < nw <= 128): segment start /
-    // length in 16-B units.  rot staggers the workgroups that share an XCD's L2 (blocks
-    // b, b+8, ... under round-robin placement) over K, so most B rows a wave asks for were
-    // already fetched by a neighbour (speed only; any placement is correct).
-    const uint32_t nw = nks > wv ? (nks - wv + W - 1) / W : 0u;
-    const uint32_t rot = (uint32_t)(((uint64_t)((g >> 3) & 31u) * nks) >> 5);
-    const uint32_t *sg = seg + (size_t)g * nks;
-    uint32_t s_lo0 = 0, s_n0 = 0, s_lo1 = 0, s_n1 = 0;
-    if (lane < nw) {
-        uint32_t t = rot + wv + lane * W;
-        t = t >= nks ? t - nks : t;
-        s_lo0 = sg[t];
-        s_n0 = sg[t + 1] - s_lo0;
-    }
-    if (lane + 64u < nw) {
-        uint32_t t = rot + wv + (lane + 64u) * W;
-        t = t >= nks ? t - nks : t;
-        s_lo1 = sg[t];
-        s_n1 = sg[t + 1] - s_lo1;
-    }
-    asm volatile("" ::"v"(s_lo0), "v"(s_n0), "v"(s_lo1), "v"(s_n1));  // retire these loads before any DMA
-    __syncthreads();  // quad selectors written
-
-    auto issue_a = [&](uint32_t i) {  // k-step i's segment -> A slot i % DA
-        const uint32_t lo = i < 64u ? __builtin_amdgcn_readlane(s_lo0, i) : __builtin_amdgcn_readlane(s_lo1, i - 64u);
-        const uint32_t n = i < 64u ? __builtin_amdgcn_readlane(s_n0, i) : __builtin_amdgcn_readlane(s_n1, i - 64u);
-        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + ra + (i % DA) * kBmSeg);
-        if (lane < n) dma16(A + lo + lane, dst);
-    };
-    auto issue_b = [&](uint32_t i) {  // the 32 B rows of k-step i -> B slot i % DB
-        uint32_t t = rot + wv + i * W;
-        t = t >= nks ? t - nks : t;
-        const uint32_t k0 = t * 32u;
-        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + rb + (i % DB) * SB);
-#pragma unroll
-        for (uint32_t q = 0; q < CT; q++) {
-            const uint32_t u = q * 64u + lane, k = u / UB, s = u % UB;
-            const uint32_t kk = k0 + k < K ? k0 + k : K - 1u;
-            dma16(B + (size_t)kk * N + (b_piece<CT>(k, s >> 1) * 2u + (s & 1u)) * 8u, dst + q * 1024u);
-        }
-    };
-    // prologue = the issue pattern of iterations -(DA-1) .. -1
-    for (int v = -(DA - 1); v < 0; v++) {
-        const int ia = v + DA - 1, ib = v + DB - 1;
-        if ((uint32_t)ia < nw) issue_a((uint32_t)ia);
-        if (ib >= 0 && (uint32_t)ib < nw) issue_b((uint32_t)ib);
-    }
-
-    f4v acc[RT][CT];
-#pragma unroll
-    for (int rt = 0; rt < RT; rt++)
-#pragma unroll
-        for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
-    const uint32_t kg = lane >> 4;
-    const uint32_t lowmask = (1u << (8u * kg)) - 1u;
-
-    for (uint32_t i = 0; i < nw; i++) {
-        if (i + DA - 1 < nw) issue_a(i + DA - 1);
-        if (i + DB - 1 < nw) issue_b(i + DB - 1);
-        // retire k-step i: A(i) was issued before B(i), so waiting for B(i) covers both
-        if (i + DA - 1 < nw) {
-            vm_wait<STEADY>();
-        } else {
-            uint32_t n = 0;
-#pragma unroll
-            for (uint32_t j = 1; j < DB; j++) n += (i + DA - DB + j < nw ? 1u : 0u) + (i + j < nw ? CT : 0u);
-            vm_wait_dyn(n);
-        }
-        const unsigned char *sa = lds + ra + (i % DA) * kBmSeg;
-        const unsigned char *sb = lds + rb + (i % DB) * SB;
-        h8v bv[CT];
-#pragma unroll
-        for (int ct = 0; ct < CT; ct++) {
-            s4v t[2];
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const uint32_t k = 8u * kg + 4u * h + ((lane & 15u) >> 2);
-                t[h] = (DBG & 4) ? s4v{} : __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (lds_s4v *)(sb + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u));
+            for (int c = 0; c < CT; c++) {
+                const uint32_t un = lane + 64u * c, k = un / UB, s = un % UB;
+                *reinterpret_cast<u32x4 *>(bst + k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u) =
+                    kr + k < K ? B_[c] : zero4;
             }
-            __builtin_memcpy(&bv[ct], t, 16);
+            // scatter the step's entries into the image
+#pragma unroll
+            for (int j = 0; j < MAXG; j++) {
+                if (lane + 64u * j < GCAP) {
+#pragma unroll
+                    for (int e = 0; e < 8; e++) {
+                        const uint32_t h = (P_[j][e >> 1] >> (16 * (e & 1))) & 0xffffu;
+                        const uint16_t v = (uint16_t)((V_[j][e >> 1] >> (16 * (e & 1))) & 0xffffu);
+                        *reinterpret_cast<uint16_t *>(img + h * 2u) = v;
+                    }
+                }
+            }
+            // fragments (LDS runs a wave's operations in order: the reads see the stores)
+#pragma unroll
+            for (int rt = 0; rt < RT; rt++) av[rt] = *reinterpret_cast<const h8v *>(img + arow[rt]);
+            const uint32_t kb = 8u * (lane >> 4);
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) {
+                s4v t[2];
+#pragma unroll
+                for (int hh = 0; hh < 2; hh++) {
+                    const uint32_t k = kb + 4u * hh + ((lane & 15u) >> 2);
+                    t[hh] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s4v *)(bst + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u));
+                }
+                __builtin_memcpy(&bv[ct], t, 16);
+            }
+            // the image back to zero at the entries' positions
+#pragma unroll
+            for (int j = 0; j < MAXG; j++) {
+                if (lane + 64u * j < GCAP) {
+#pragma unroll
+                    for (int e = 0; e < 8; e++) {
+                        const uint32_t h = (P_[j][e >> 1] >> (16 * (e & 1))) & 0xffffu;
+                        *reinterpret_cast<uint16_t *>(img + h * 2u) = (uint16_t)0;
+                    }
+                }
+            }
         }
-        const unsigned char *vals = sa + 4u * R;
-        uint32_t rowbase = 0;
-        h8v av[RT];
+        load_set(i + D, P_, V_, B_);
+        if (live) {
 #pragma unroll
-        for (int rt = 0; rt < RT; rt++) {
-            const uint32_t r = 16u * rt + (lane & 15u);
-            uint32_t wrd = *reinterpret_cast<const uint32_t *>(sa + 4u * r);
-            if (r >= R) wrd = 0u;
-            const uint32_t cnt = __builtin_popcount(wrd);
-            // inclusive scan of the rows' counts over each 16-lane row (lanes = rows)
-            uint32_t sc = cnt;
-            sc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sc, 0x111, 0xf, 0xf, true);
-            sc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sc, 0x112, 0xf, 0xf, true);
-            sc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sc, 0x114, 0xf, 0xf, true);
-            sc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sc, 0x118, 0xf, 0xf, true);
-            const uint32_t off = rowbase + sc - cnt + __builtin_popcount(wrd & lowmask);  // halves
-            if (rt + 1 < RT) rowbase += __builtin_amdgcn_readlane(sc, 15);
-            const uint32_t m8 = (wrd >> (8u * kg)) & 0xffu;
-            const uint32_t qa = m8 & 15u, qb = m8 >> 4;
-            const uint32_t offb = off + __builtin_popcount(qa);
-            const uint32_t am = (DBG & 1) ? ~7u : ~0u;
-            const uint2 wa = *reinterpret_cast<const uint2 *>(vals + ((2u * off) & am));   // unaligned ds_read_b64
-            const uint2 wb = *reinterpret_cast<const uint2 *>(vals + ((2u * offb) & am));
-            const uint2 la = lut[qa], lb = lut[qb];
-            uint32_t d[4];
-            d[0] = __builtin_amdgcn_perm(wa.y, wa.x, la.x);
-            d[1] = __builtin_amdgcn_perm(wa.y, wa.x, la.y);
-            d[2] = __builtin_amdgcn_perm(wb.y, wb.x, lb.x);
-            d[3] = __builtin_amdgcn_perm(wb.y, wb.x, lb.y);
-            __builtin_memcpy(&av[rt], d, 16);
-            if constexpr ((DBG & 2) != 0) av[rt] = h8v{};
+            for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+                for (int ct = 0; ct < CT; ct++)
+                    acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[rt], bv[ct], acc[rt][ct], 0, 0, 0);
+            if (i < 16u) GS_KS_STAMP(3u + i);
         }
+    };
+    for (uint32_t i0 = 0; i0 < nsw; i0 += D) {
 #pragma unroll
-        for (int rt = 0; rt < RT; rt++)
-#pragma unroll
-            for (int ct = 0; ct < CT; ct++)
-                acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[rt], bv[ct], acc[rt][ct], 0, 0, 0);
+        for (int d = 0; d < D; d++) step(i0 + d, P[d], V[d], BR[d]);
     }
-    // fixed-order sum of the waves' partial tiles (every DMA was waited for above)
-    __syncthreads();
+    GS_KS_STAMP(20u);
+    // ---- wave partial tiles -> LDS (the trailing loads write registers only), summed in
+    // wave order.  Item t = (tile, lane) of a 16x16 tile: the 4 rows 4*(lane/16)+i of
+    // column lane%16
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __asm__ volatile("" ::: "memory");
     f4v *red = reinterpret_cast<f4v *>(lds);
 #pragma unroll
     for (int rt = 0; rt < RT; rt++)
 #pragma unroll
         for (int ct = 0; ct < CT; ct++) red[((wv * RT + rt) * CT + ct) * 64u + lane] = acc[rt][ct];
-    __syncthreads();
-    const float *redf = reinterpret_cast<const float *>(lds);
-    for (uint32_t e = tid; e < (uint32_t)(RT * CT) * 256u; e += 64u * W) {
-        const uint32_t cc = e & 15u, rr = (e >> 4) & 15u, tt = e >> 8;
-        const uint32_t rt = tt / CT, ct = tt % CT;
-        const uint32_t ln = 16u * (rr >> 2) + cc, ii = rr & 3u;
-        float sum = 0.f;
-        for (uint32_t w = 0; w < (uint32_t)W; w++) sum += redf[(((w * RT + rt) * CT + ct) * 64u + ln) * 4u + ii];
-        const uint32_t row = 16u * rt + rr;
-        if (row < R) C[(size_t)(row_base + r0 + row) * N + 16u * ct + cc] = (f16)sum;
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __asm__ volatile("" ::: "memory");
+    constexpr uint32_t NI = RT * CT * 64u, NT = 64u * W;
+    const uint32_t r0 = bmtb_first_row[g], R = bmtb_first_row[g + 1] - r0;
+    auto item_sum = [&](uint32_t t) {
+        f4v sum = red[t];
+#pragma unroll
+        for (uint32_t w = 1; w < (uint32_t)W; w++) sum += red[w * NI + t];
+        return sum;
+    };
+    auto store_item = [&](uint32_t t, const f4v &v) {
+        const uint32_t ln = t & 63u, tt = t >> 6, rt = tt / CT, ct = tt % CT;
+        const uint32_t col = 16u * ct + (ln & 15u), rb = 16u * rt + 4u * (ln >> 4);
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++)
+            if (rb + i < R) C[(size_t)(row_base + r0 + rb + i) * N + col] = (f16)v[i];
+    };
+    GS_KS_STAMP(21u);
+    if (S == 1) {
+        for (uint32_t t = tid; t < NI; t += NT) store_item(t, item_sum(t));
+        GS_KS_STAMP(22u);
+        return;
     }
+    // K-split: this workgroup's fp32 slab (16-B write-through stores), then the last of
+    // the row block's S workgroups sums the slabs in q order
+    f4v *slab = reinterpret_cast<f4v *>(slabs) + (size_t)u * NI;
+    for (uint32_t t = tid; t < NI; t += NT) {
+        const f4v v = item_sum(t);
+        // 16-B write-through store (vector memory, sc1): retired by the vmcnt(0) below
+        __asm__ volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(slab + t), "v"(v) : "memory");
+    }
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    uint32_t *flag = reinterpret_cast<uint32_t *>(lds + (size_t)W * NI * 16u);
+    if (tid == 0) *flag = __hip_atomic_fetch_add(&arrivals[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*flag != S - 1u) {
+        GS_KS_STAMP(22u);
+        return;
+    }
+    if (tid == 0) __hip_atomic_store(&arrivals[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const f4v *base = reinterpret_cast<const f4v *>(slabs) + (size_t)g * S * NI;
+    for (uint32_t t = tid; t < NI; t += NT) {
+        const f4v own = item_sum(t);
+        f4v sum = {0.f, 0.f, 0.f, 0.f};
+        for (uint32_t qq = 0; qq < S; qq++) {
+            if (qq == q) {
+                sum += own;
+                continue;
+            }
+            const float *src = reinterpret_cast<const float *>(base + (size_t)qq * NI + t);
+            f4v x;
+#pragma unroll
+            for (int i = 0; i < 4; i++) x[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sum += x;
+        }
+        store_item(t, sum);
+    }
+    GS_KS_STAMP(22u);
+#undef GS_KS_STAMP
 }
 
 // ---------------------------------------------------------------------------

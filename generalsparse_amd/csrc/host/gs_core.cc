@@ -97,9 +97,6 @@ void apply_kv(config_t &c, const std::string &k, const std::string &v) {
     else if (k == "MFMA_GLDS") c.MFMA_GLDS = i();
     else if (k == "MFMA_GLDS_NBUF") c.MFMA_GLDS_NBUF = i();
     else if (k == "MFMA_COMPUTE_WAVES") c.MFMA_COMPUTE_WAVES = i();
-    else if (k == "MFMA_WK") c.MFMA_WK = i();
-    else if (k == "MFMA_BITMAP") c.MFMA_BITMAP = i() != 0;
-    else if (k == "BM_VARIANT") c.BM_VARIANT = i();
     else if (k == "FORMAT_OF_MTX") c.FORMAT_OF_MTX = v;
     else if (k == "PERFORMANCE_FLAG") c.PERFORMANCE_FLAG = v;
     else if (k == "Graph_Algorithm") c.Graph_Algorithm = v;
@@ -111,6 +108,9 @@ void apply_kv(config_t &c, const std::string &k, const std::string &v) {
     else if (k == "WARP_ROWS_GROUPS") c.WARP_ROWS_GROUPS = i();
     else if (k == "MFMA_KSPLIT") c.MFMA_KSPLIT = i();
     else if (k == "NM_MFMA") c.NM_MFMA = b();
+    else if (k == "MFMA_KS") c.MFMA_KS = b();
+    else if (k == "KS_MIN_ROWS") c.KS_MIN_ROWS = i();
+    else if (k == "KS_SPLIT") c.KS_SPLIT = i();
     // unknown keys are ignored, as the reference ignores 17 of its 36 keys
 }
 

@@ -73,7 +73,6 @@ struct config_t {
     int64_t MFMA_GLDS = 1;  // k_mfma_rows: B rows by global_load_lds (two chunks ahead)
     int64_t MFMA_COMPUTE_WAVES = 6;  // k_mfma_rows compute waves (6, or 8 with two fewer entry waves)
     int64_t MFMA_GLDS_NBUF = 3;  // ... into this many B buffers, NBUF-1 chunks ahead (4, 5: 256-column chunks)
-    int64_t MFMA_WK = 0;    // row blocks of <= 32 rows on k_mfma_wk (wave-owned k-steps; opt-in, slower on C2)
     std::string FORMAT_OF_MTX = "COO";
     std::string PERFORMANCE_FLAG = "throughput";
     std::string Graph_Algorithm = "";
@@ -86,8 +85,9 @@ struct config_t {
     int64_t MFMA_MAX_FILL = 16;  // ... when (padded row-block area) / nnz <= this
     bool NM_MFMA = true;         // col-direction plans whose rows are 2:4 panels: sparse matrix cores (k_nm_mfma)
     int64_t MFMA_KSPLIT = 0;     // workgroups per row block (K ranges); 0 = fill the 256 CUs
-    bool MFMA_BITMAP = false;    // matrix-core row blocks from bitmap panels (k_mfma_bitmap; opt-in, slower on C2)
-    int64_t BM_VARIANT = 0;      // k_mfma_bitmap shape (device_plan.hip kBmVariant)
+    bool MFMA_KS = true;         // row blocks of >= KS_MIN_ROWS rows: K-split, B-stationary k_mfma_ks
+    int64_t KS_MIN_ROWS = 40;    // ... from this many rows per BMTB (shorter blocks: k_mfma_rows)
+    int64_t KS_SPLIT = 0;        // k_mfma_ks K ranges per row block (0: the fewest that fit LDS and fill the CUs)
 };
 // Process-wide config: loaded once from $GS_CONFIG or ./global_config.json if
 // present (flat JSON object of scalars), defaults otherwise.

@@ -42,11 +42,11 @@ struct device_plan {
     bool lds = false;
     bool nm = false;    // k_nm_mfma: 2:4 panels of a col-direction plan (A blocks in tcol; k-steps in KC)
     bool mfma = false;  // k_mfma_rows (uses KC, nc, lds_bytes; log2 KC in RSB; RT in maxr; RMAX in rpw_max)
-    bool wk = false;    // k_mfma_wk (MFMA_WK): wave-owned k-steps; wk_nb row blocks, wk_steps steps, wk_emax
-    bool bm = false;    // k_mfma_bitmap: bitmap panels (t0 BMTB rows, t1 segment starts, tcol segments)
-    uint32_t bm_nks = 0, bm_variant = 0;
+    bool ks = false;    // k_mfma_ks: K split over ksplit workgroups per row block, B slice in LDS
+                        // (t0 BMTB rows, tcol/tval groups; ks_ns k-steps per range,
+                        // RT in maxr, MAXG in seg_cap, ws slabs + t2 arrivals when ksplit > 1)
+    uint32_t ks_ns = 0, ks_gcap = 0;  // k_mfma_ks: k-steps per K range, entry groups per step
     std::string kernel;  // the device kernel gs_spmm launches at the plan's N (empty: the family's)
-    uint32_t wk_nb = 0, wk_steps = 0, wk_emax = 0;
     uint32_t ksplit = 1, ncs = 0;  // k_mfma_rows workgroups per row block, chunks per workgroup
     uint32_t ws_n = 0;             // bitmap family: dense width of the fp32 workspace
     uint64_t n_fin = 0;            // bitmap family: rows k_finalize_rows writes
@@ -109,5 +109,15 @@ void launch_spmm(plan_state &p, int replica, const void *B, void *C, uint32_t N,
 void ensure_csr(plan_state &p);
 void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
                          size_t n_host);
+// mfma_launch.hip: k_mfma_rows / k_nm_mfma (and k_mfma_ks through launch_ks) at the plan's N
+void launch_mfma(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s);
+void launch_nm(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s);
+// gather_launch.hip: the CUDA-core gather families and k_lds_rows
+void launch_gather(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s);
+// ks_launch.hip: k_mfma_ks (K-split, wave-autonomous matrix-core row blocks)
+constexpr uint32_t kKsWaves = 8, kKsDepth = 4;
+void launch_ks(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s);
+void debug_ks_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
+                       size_t n_host);
 
 }  // namespace gs

@@ -291,7 +291,7 @@ size_t mfma_lds_bytes(uint32_t lgKC, uint32_t CT, uint32_t RMAX) {
 // banks remain).  Appends 8 u16 pos + 8 u16 values per group; padding slots write
 // 0 into the zero row (pad_h = its first halfword), on banks of their own.
 void bank_order_segment(const std::vector<uint16_t> &pos, const std::vector<uint16_t> &val, uint32_t pad_h,
-                        std::vector<uint16_t> &out_pos, std::vector<uint16_t> &out_val) {
+                        std::vector<uint16_t> &out_pos, std::vector<uint16_t> &out_val, uint32_t pad_slots = 32) {
     const size_t n = pos.size();
     const size_t ng = (n + 7) / 8;
     std::vector<std::vector<uint32_t>> bucket(32);
@@ -324,7 +324,7 @@ void bank_order_segment(const std::vector<uint16_t> &pos, const std::vector<uint
             }
             for (; l < gl; l++) {  // padding: value 0 into the zero row, one bank each
                 const size_t slot = base + (b0 + l) * 8 + e;
-                out_pos[slot] = (uint16_t)(pad_h + 2 * (l & 31));
+                out_pos[slot] = (uint16_t)(pad_h + 2 * (l % pad_slots));  // inside the zero row
                 out_val[slot] = 0;
             }
         }
@@ -407,119 +407,99 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
     return true;
 }
 
-// ------------------------------------------------------------------ k_mfma_wk layout
-// per (BMTB g, 32-column k-step s): the entries of g's rows with columns in [32s, 32s+32),
-// row-major, as u32 = (local_row*40 + col - 32s) | f16 << 16; seg[g*nsteps + s] the starts.
-// emax = entries per lane per step (64 lanes) rounded up to 1, 2, 4 or 8.
-bool build_wk(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
-              const std::vector<uint64_t> &col, const std::vector<float> &vals, uint64_t K, std::vector<uint32_t> &seg,
-              std::vector<uint32_t> &ent, uint32_t &emax, uint32_t &rt, std::string &why) {
-    const uint64_t nb = tb_rows.size() - 1, nsteps = (K + 31) / 32;
+// ------------------------------------------------------------------ k_mfma_ks layout
+// Upload layout of k_mfma_ks (kernel_lib.hpp): the K range is split into S ranges of
+// KR = 32*NS columns; for every (BMTB g, range q, 32-column k-step s) -- unit u = g*S + q --
+// the entries of g's rows in the step's columns, in groups of 8: pos = halfword index in a
+// wave image of 96-B rows (local_row*48 + column - step base), val = f16.  Every step holds
+// exactly GCAP groups (the plan's largest step; the rest padding that writes 0 into the
+// image's zero row 16*RT), at group (u*NS + s)*GCAP, so the kernel computes every address
+// without loading offsets first.  One spare group follows.  The entry order inside a step
+// is bank-ordered for the scatter.
+struct ks_tiles {
+    uint32_t S = 0, NS = 0, RT = 0, RMAX = 0, MAXG = 0, GCAP = 0, W = 0;
+    size_t lds_bytes = 0;
+    std::vector<uint16_t> pos, val;  // 8 u16 per group each
+};
+
+using gsk::ks_lds_bytes;
+
+bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
+                    const std::vector<uint64_t> &col, const std::vector<float> &vals, uint64_t K, uint32_t N,
+                    int64_t s_cfg, int64_t min_rows, int64_t max_fill, ks_tiles &t, std::string &why) {
+    const uint64_t nb = tb_rows.size() - 1;
+    if (nb == 0 || K == 0) { why = "empty plan"; return false; }
+    if (N != 16 && N != 32 && N != 64) { why = "N must be 16, 32 or 64"; return false; }
+    const uint32_t CT = N / 16, W = kKsWaves;  // gs_plan.hpp
     uint64_t rmax = 0;
     for (uint64_t g = 0; g < nb; g++) rmax = std::max<uint64_t>(rmax, tb_rows[g + 1] - tb_rows[g]);
-    if (nb == 0 || rmax == 0 || rmax > 32) { why = "row blocks of 1..32 rows"; return false; }
-    rt = rmax > 16 ? 2u : 1u;
-    seg.assign(1, 0);
-    ent.clear();
-    uint64_t mx = 0;
+    if (rmax < (uint64_t)std::max<int64_t>(1, min_rows) || rmax > 80) { why = "row blocks outside the k_mfma_ks range"; return false; }
+    const uint32_t RT = std::max<uint32_t>(2, (uint32_t)((rmax + 15) / 16));  // kernels built for RT 2..5
+    const uint64_t nnz = row_ptr[tb_rows[nb]] - row_ptr[tb_rows[0]];
+    if (nnz == 0 || (double)nb * 16 * RT * K > (double)max_fill * nnz) {  // as build_mfma_tiles
+        why = "row blocks too sparse for dense tiles";
+        return false;
+    }
+    // K ranges: enough workgroups for the 256 CUs (each reads only its range's B rows)
+    t.lds_bytes = ks_lds_bytes(CT, RT, W);
+    if (t.lds_bytes > 160 * 1024) { why = "k_mfma_ks wave stages exceed LDS"; return false; }
+    uint64_t S = s_cfg > 0 ? (uint64_t)s_cfg : std::min<uint64_t>(8, (256 + nb - 1) / nb);
+    S = std::max<uint64_t>(1, std::min<uint64_t>(S, (K + 31) / 32));
+    uint64_t KR = ((K + S - 1) / S + 31) / 32 * 32;
+    S = (K + KR - 1) / KR;
+    t.S = (uint32_t)S;
+    t.NS = (uint32_t)(KR / 32);
+    t.RT = RT;
+    t.RMAX = (uint32_t)rmax;
+    t.W = W;
+    // pass 1: the largest step (entries of a row block in 32 columns)
+    uint64_t gmax = 1;
+    {
+        std::vector<uint32_t> cnt((size_t)S * t.NS);
+        for (uint64_t g = 0; g < nb; g++) {
+            std::fill(cnt.begin(), cnt.end(), 0u);
+            for (uint64_t e = row_ptr[tb_rows[g]]; e < row_ptr[tb_rows[g + 1]]; e++) cnt[col[e] / 32]++;
+            for (uint32_t c : cnt) gmax = std::max<uint64_t>(gmax, (c + 7) / 8);
+        }
+    }
+    t.GCAP = (uint32_t)gmax;
+    t.MAXG = gmax <= 64 ? 1 : (gmax <= 128 ? 2 : (gmax <= 256 ? 4 : 0));
+    if (!t.MAXG) { why = "a k-step holds more than 256 entry groups"; return false; }
+    GS_CHECK((double)nb * S * t.NS * t.GCAP < 4.0e9, "k_mfma_ks layout exceeds 32-bit group indices");
+    const uint32_t RS = gsk::kKsStride / 2;  // halfwords per image row
+    const uint32_t pad_h = 16 * RT * RS;      // the zero row
+    t.pos.reserve((size_t)nb * S * t.NS * t.GCAP * 8 + 8);
+    t.val.reserve(t.pos.capacity());
     std::vector<uint64_t> cur;
+    std::vector<uint16_t> pos, hv;
     for (uint64_t g = 0; g < nb; g++) {
         const uint64_t r0 = tb_rows[g], R = tb_rows[g + 1] - r0;
         cur.assign(R, 0);
         for (uint64_t i = 0; i < R; i++) cur[i] = row_ptr[r0 + i];
-        for (uint64_t st = 0; st < nsteps; st++) {
-            const uint64_t lim = 32 * (st + 1), before = ent.size();
-            for (uint64_t i = 0; i < R; i++) {
-                uint64_t e = cur[i];
-                for (; e < row_ptr[r0 + i + 1] && col[e] < lim; e++)
-                    ent.push_back((uint32_t)(i * 40 + (col[e] - 32 * st)) |
-                                  (uint32_t)f32_to_f16_bits(vals[e]) << 16);
-                cur[i] = e;
-            }
-            mx = std::max<uint64_t>(mx, ent.size() - before);
-            GS_CHECK(ent.size() < 0xffffffffull, "k_mfma_wk: entry offsets exceed 32 bits");
-            seg.push_back((uint32_t)ent.size());
-        }
-    }
-    const uint64_t per = (mx + 63) / 64;
-    emax = per <= 1 ? 1 : per <= 2 ? 2 : per <= 4 ? 4 : per <= 8 ? 8 : 0;
-    if (!emax) { why = "k-steps too dense for the wave's entry registers"; return false; }
-    ent.push_back(0);
-    return true;
-}
-
-// ------------------------------------------------------------------ bitmap panels
-// Upload layout of k_mfma_bitmap (kernel_lib.hpp) from canonical rows (columns
-// ascending and distinct): per BMTB g and 32-column k-step t a segment of R u32
-// row masks followed by the f16 values of the entries in row-major, column order,
-// zero-padded to 16 B; seg[g*nks + t] = its start in 16-B units (seg[nb*nks] =
-// the end).  Refuses (why) row blocks of more than 32 rows, segments over 1 KB,
-// more than 128 k-steps per wave, and plans whose masks would outweigh a u16
-// column index or whose row blocks are too sparse or too short for dense tiles.
-struct bitmap_panels {
-    uint32_t nks = 0, RT = 0, RMAX = 0;
-    std::vector<uint32_t> seg;
-    std::vector<uint32_t> data;  // u32 words of the segments
-};
-
-bool build_bitmap_panels(const std::vector<uint64_t> &tb_rows, const canon_rows &cr, uint64_t K, uint32_t N,
-                         uint32_t waves, int64_t max_fill, bitmap_panels &t, std::string &why) {
-    const uint64_t nb = tb_rows.size() - 1;
-    if (nb == 0 || K == 0) { why = "empty plan"; return false; }
-    if (N != 16 && N != 32 && N != 64) { why = "N must be 16, 32 or 64"; return false; }
-    uint64_t rmax = 0, nnz = cr.col.size();
-    for (uint64_t g = 0; g < nb; g++) rmax = std::max<uint64_t>(rmax, tb_rows[g + 1] - tb_rows[g]);
-    if (rmax == 0 || rmax > 32) { why = "BMTBs of 1..32 rows only"; return false; }
-    const uint64_t nks = (K + 31) / 32;
-    if (nks > 128ull * waves) { why = "more than 128 k-steps per wave"; return false; }
-    if (nnz == 0 || (double)nb * 16 * ((rmax + 15) / 16) * K > (double)max_fill * nnz) {
-        why = "row blocks too sparse for dense tiles";
-        return false;
-    }
-    if ((double)nb * K * N * 2 > 6.0 * 4.0 * nnz && max_fill < (1 << 20)) {
-        why = "row blocks too short: B traffic per row block exceeds A's";
-        return false;
-    }
-    uint64_t mask_words = 0;
-    for (uint64_t g = 0; g < nb; g++) mask_words += (tb_rows[g + 1] - tb_rows[g]) * nks;
-    if (mask_words * 4 > nnz * 2) { why = "row masks would outweigh a u16 column index"; return false; }
-    t.nks = (uint32_t)nks;
-    t.RMAX = (uint32_t)rmax;
-    t.RT = (uint32_t)((rmax + 15) / 16);
-    t.seg.assign(1, 0);
-    t.seg.reserve(nb * nks + 1);
-    t.data.clear();
-    t.data.reserve(mask_words + nnz / 2 + nb * nks * 2);
-    std::vector<uint64_t> cur;
-    std::vector<uint16_t> hv;
-    for (uint64_t g = 0; g < nb; g++) {
-        const uint64_t r0 = tb_rows[g], R = tb_rows[g + 1] - r0;
-        cur.assign(R, 0);
-        for (uint64_t i = 0; i < R; i++) cur[i] = cr.rp[r0 + i];
-        for (uint64_t st = 0; st < nks; st++) {
-            const uint64_t lim = 32 * (st + 1), start = t.data.size();
-            hv.clear();
-            for (uint64_t i = 0; i < R; i++) {
-                uint32_t m = 0;
-                uint64_t e = cur[i];
-                for (; e < cr.rp[r0 + i + 1] && cr.col[e] < lim; e++) {
-                    m |= 1u << (cr.col[e] - 32 * st);
-                    hv.push_back(f32_to_f16_bits(cr.val[e]));
+        for (uint64_t q = 0; q < S; q++)
+            for (uint32_t s = 0; s < t.NS; s++) {
+                const uint64_t base = q * KR + 32ull * s, lim = base + 32;
+                pos.clear();
+                hv.clear();
+                for (uint64_t i = 0; i < R; i++) {
+                    uint64_t e = cur[i];
+                    for (; e < row_ptr[r0 + i + 1] && col[e] < lim; e++) {
+                        pos.push_back((uint16_t)(i * RS + (col[e] - base)));
+                        hv.push_back(f32_to_f16_bits(vals[e]));
+                    }
+                    cur[i] = e;
                 }
-                cur[i] = e;
-                t.data.push_back(m);
+                const size_t before = t.pos.size();
+                bank_order_segment(pos, hv, pad_h, t.pos, t.val, RS / 2);  // pads stay inside the zero row
+                for (size_t x = t.pos.size(); x < before + (size_t)t.GCAP * 8; x++) {  // up to GCAP groups
+                    t.pos.push_back((uint16_t)(pad_h + 2 * ((x / 8) % (RS / 2))));
+                    t.val.push_back(0);
+                }
+                GS_CHECK(t.pos.size() == before + (size_t)t.GCAP * 8, "k_mfma_ks step exceeds its capacity");
             }
-            if (hv.size() & 1) hv.push_back(0);
-            for (size_t i = 0; i < hv.size(); i += 2) t.data.push_back((uint32_t)hv[i] | ((uint32_t)hv[i + 1] << 16));
-            while ((t.data.size() - start) & 3) t.data.push_back(0);
-            if ((t.data.size() - start) * 4 > gsk::kBmSeg) {
-                why = "a k-step segment exceeds 1 KB (row block too dense for one LDS-DMA)";
-                return false;
-            }
-            GS_CHECK(t.data.size() / 4 < 0xffffffffull, "bitmap panels exceed 32-bit offsets");
-            t.seg.push_back((uint32_t)(t.data.size() / 4));
-        }
     }
+    t.pos.insert(t.pos.end(), 8, (uint16_t)pad_h);  // spare group: loads past a wave's last step
+    t.val.insert(t.val.end(), 8, 0);
     return true;
 }
 
@@ -596,17 +576,6 @@ bool build_nm_panels(const std::vector<uint64_t> &rows, const std::vector<uint64
     }
     S = (uint32_t)S64;
     return true;
-}
-
-// k_mfma_bitmap shapes (waves per workgroup, A ring slots, B ring slots); config BM_VARIANT
-struct bm_shape { int W, DA, DB; };
-constexpr bm_shape kBmVariant[] = {{8, 8, 3}, {16, 4, 2}, {8, 12, 3}, {8, 6, 5}, {12, 4, 4}, {8, 6, 2}, {8, 6, 6}};
-constexpr int kBmVariants = (int)(sizeof(kBmVariant) / sizeof(kBmVariant[0]));
-
-constexpr size_t bm_lds_bytes(uint32_t CT, uint32_t RT, bm_shape v) {
-    const size_t rings = (size_t)v.W * (v.DA * gsk::kBmSeg + v.DB * 1024u * CT) + 128u;  // + quad selectors
-    const size_t red = (size_t)v.W * RT * CT * 1024u;
-    return rings > red ? rings : red;
 }
 
 }  // namespace
@@ -714,52 +683,34 @@ void upload_plan(plan_state &p, int dtype, int device) {
         const auto &tbr = m.u(TBLOCK_META, "first_row_indices", sb);
         const canon_rows cr = canonical_rows(rp0, col, *vals);
         const std::vector<uint32_t> &rp = cr.rp;
-        if (cfg.MFMA_BITMAP && !cfg.MFMA_WK) {
-            // bitmap panels (k_mfma_bitmap): the default matrix-core layout
-            bitmap_panels bp;
-            const uint32_t var = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(cfg.BM_VARIANT, kBmVariants - 1));
-            if (build_bitmap_panels(tbr, cr, p.K, Nd, (uint32_t)kBmVariant[var].W, cfg.MFMA_MAX_FILL, bp, why) &&
-                bm_lds_bytes(Nd / 16, bp.RT, kBmVariant[var]) <= 160 * 1024) {
+        if (cfg.MFMA_KS) {
+            // tall row blocks: K split over workgroups, B slice stationary in LDS (k_mfma_ks)
+            ks_tiles kt;
+            if (build_ks_tiles(tbr, rp, cr.col, cr.val, p.K, Nd, cfg.KS_SPLIT, cfg.KS_MIN_ROWS, cfg.MFMA_MAX_FILL, kt,
+                               why)) {
                 d.mfma = true;
-                d.bm = true;
-                d.bm_variant = var;
-                d.bm_nks = bp.nks;
+                d.ks = true;
+                d.kernel = "k_mfma_ks";
                 d.lds_N = Nd;
-                d.maxr = bp.RT;
-                d.rpw_max = bp.RMAX;
-                d.waves = (uint32_t)kBmVariant[var].W;
-                d.lds_bytes = bm_lds_bytes(Nd / 16, bp.RT, kBmVariant[var]);
-                d.n_rows_aux = tbr.size() - 1;
-                d.kernel = "k_mfma_bitmap";
+                d.ksplit = kt.S;
+                d.ks_ns = kt.NS;
+                d.maxr = kt.RT;
+                d.rpw_max = kt.RMAX;
+                d.seg_cap = kt.MAXG;
+                d.waves = kt.W;
+                d.lds_bytes = kt.lds_bytes;
+                const uint64_t nb = tbr.size() - 1;
+                d.n_rows_aux = nb;
                 const size_t before = d.bytes_A;
+                d.ks_gcap = kt.GCAP;
                 a.t0 = dev_copy(d, to_u32(tbr, "BMTB first_row_indices"));
-                a.t1 = dev_copy(d, bp.seg);
-                a.tcol = dev_copy(d, bp.data, 4);
+                a.tcol = dev_copy(d, kt.pos);
+                a.tval = dev_copy(d, kt.val);
                 d.bytes_tile = d.bytes_A - before;
-                return true;
-            }
-        }
-        if (cfg.MFMA_WK && (Nd == 16 || Nd == 32)) {
-            // wave-owned k-steps (k_mfma_wk)
-            std::vector<uint32_t> seg, ent;
-            uint32_t emax = 0, rt = 0;
-            if (build_wk(tbr, rp, cr.col, cr.val, p.K, seg, ent, emax, rt, why)) {
-                d.mfma = true;
-                d.wk = true;
-                d.lds_N = Nd;
-                d.maxr = rt;
-                d.wk_nb = (uint32_t)(tbr.size() - 1);
-                d.wk_steps = (uint32_t)((p.K + 31) / 32);
-                d.wk_emax = emax;
-                d.waves = gsk::kWkWaves;
-                const size_t stg = 32 * 2 * Nd + gsk::kWkRows * gsk::kWkRss;
-                d.lds_bytes = std::max<size_t>(gsk::kWkWaves * stg, (size_t)gsk::kWkWaves * rt * (Nd / 16) * 1024);
-                d.kernel = "k_mfma_wk";
-                const size_t before = d.bytes_A;
-                a.t0 = dev_copy(d, to_u32(tbr, "BMTB first_row_indices"));
-                a.t1 = dev_copy(d, seg);
-                a.tcol = dev_copy(d, ent);
-                d.bytes_tile = d.bytes_A - before;
+                if (kt.S > 1) {
+                    a.ws = dev_copy(d, std::vector<float>((size_t)nb * kt.S * 16 * kt.RT * Nd, 0.f));
+                    a.t2 = dev_copy(d, std::vector<uint32_t>(nb, 0u));  // arrival counters
+                }
                 return true;
             }
         }
@@ -1110,435 +1061,6 @@ void free_device(plan_state &p) {
     p.uploaded = false;
 }
 
-// ------------------------------------------------------------------ launch
-namespace {
-
-// GS_MP_DEBUG (diagnostic timing only): k_merge_path dbg bits
-uint32_t mp_debug() {
-    static const uint32_t v = getenv("GS_MP_DEBUG") ? (uint32_t)atoi(getenv("GS_MP_DEBUG")) : 0u;
-    return v;
-}
-
-uint32_t pow2ceil(uint32_t x) {
-    uint32_t p = 1;
-    while (p < x) p <<= 1;
-    return p;
-}
-
-template <class VT, int CF>
-void launch_lds(const plan_state &p, const device_arrays &a, const VT *B, VT *C, uint32_t N, hipStream_t s) {
-    const device_plan &d = p.dev;
-    const uint32_t X = N * (uint32_t)sizeof(VT) / 16u;
-    const uint32_t nb = (uint32_t)d.n_rows_aux;
-    const dim3 grid(nb), block(64 * d.waves);
-    const uint32_t K = (uint32_t)p.K;
-#define GS_LDS_ARGS                                                                                              \
-    a.t0, a.a1, a.a0, a.t1, a.t2, (const uint16_t *)a.tcol, (const VT *)a.tval, B, C, K, N, X, d.KC, d.nc, d.RSB, \
-        d.rpw_max, d.seg_cap, (uint32_t)d.row_base
-    auto go = [&](auto kern) {
-        // dynamic LDS above 64 KB must be opted into, once per kernel and device
-        static std::mutex mu;
-        static std::map<std::pair<int, const void *>, size_t> granted;
-        {
-            std::lock_guard<std::mutex> l(mu);
-            size_t &g = granted[{d.device, reinterpret_cast<const void *>(kern)}];
-            if (g < d.lds_bytes) {
-                HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.lds_bytes));
-                g = d.lds_bytes;
-            }
-        }
-        hipLaunchKernelGGL(kern, grid, block, d.lds_bytes, s, GS_LDS_ARGS);
-    };
-    if (d.maxr == 1) go(gsk::k_lds_rows<VT, CF, 1, kLdsMaxU>);
-    else if (d.maxr == 2) go(gsk::k_lds_rows<VT, CF, 2, kLdsMaxU>);
-    else go(gsk::k_lds_rows<VT, CF, 4, kLdsMaxU>);
-#undef GS_LDS_ARGS
-}
-
-template <int CT, int RT, int LGKC, int MAXA>
-void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N,
-                   hipStream_t s) {
-    const device_plan &d = p.dev;
-    // B rows by LDS-DMA two chunks ahead (MFMA_GLDS) or through registers three ahead
-    const int64_t gl = get_config().MFMA_GLDS, nbuf = get_config().MFMA_GLDS_NBUF;
-    auto kern = gl >= 4 ? gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 4>
-                        : (gl ? gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2> : gsk::k_mfma_rows<CT, RT, LGKC, MAXA>);
-    if (gl == 1 && get_config().MFMA_COMPUTE_WAVES == 8) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 8>;
-    // GS_MFMA_DEBUG (diagnostic timing builds, wrong results): kernel_lib.hpp k_mfma_rows DBG bits, C2 shape only
-    static const int mdbg = getenv("GS_MFMA_DEBUG") ? atoi(getenv("GS_MFMA_DEBUG")) : 0;
-    if constexpr (CT == 2 && RT == 2 && LGKC == 9 && MAXA == 1) {
-        if (gl == 1 && mdbg == 1) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 1>;
-        if (gl == 1 && mdbg == 2) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 2>;
-        if (gl == 1 && mdbg == 4) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 4>;
-        if (gl == 1 && mdbg == 10) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 10>;
-        if (gl == 1 && mdbg == 11) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 11>;
-        if (gl == 1 && mdbg == 15) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 15>;
-    }
-    if constexpr (LGKC == 8) {  // deeper B rings fit LDS with 256-column chunks
-        if (gl && !(gl >= 4) && nbuf == 4) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 4>;
-        if (gl && !(gl >= 4) && nbuf >= 5) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 5>;
-    }
-    static std::mutex mu;
-    static std::map<std::pair<int, const void *>, size_t> granted;
-    {
-        std::lock_guard<std::mutex> l(mu);
-        size_t &g = granted[{d.device, reinterpret_cast<const void *>(kern)}];
-        if (g < d.lds_bytes) {
-            HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)d.lds_bytes));
-            g = d.lds_bytes;
-        }
-    }
-    hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit), dim3(kMfmaThreads), d.lds_bytes, s, a.t0,
-                       a.t1, (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, B, C, (uint32_t)p.K, N, d.nc,
-                       d.rpw_max, (uint32_t)d.row_base, d.ksplit, d.ncs, a.ws, a.t2, (uint64_t *)nullptr,
-                       (uint32_t)get_config().MFMA_KROT);
-    HIP_OK(hipGetLastError());
-}
-
-template <int CT, int RT>
-void launch_mfma_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N,
-                    hipStream_t s) {
-    // entry groups per thread per chunk: the GLDS variant has 9 entry waves, the other 6
-    const int64_t gl = get_config().MFMA_GLDS;
-    const uint32_t wct = get_config().MFMA_COMPUTE_WAVES == 8 && gl == 1 ? 8u : (uint32_t)gsk::kMfmaCompute;
-    const uint32_t nat = 64u * (gsk::kMfmaWaves - wct - (gl >= 4 ? 4u : (gl ? 2u : (uint32_t)gsk::kMfmaBWaves)));
-    const bool two = p.dev.seg_cap > nat;
-    switch (p.dev.RSB) {                  // log2 KC
-        case 10: two ? launch_mfma_k<CT, RT, 10, 2>(p, a, B, C, N, s) : launch_mfma_k<CT, RT, 10, 1>(p, a, B, C, N, s); break;
-        case 9: two ? launch_mfma_k<CT, RT, 9, 2>(p, a, B, C, N, s) : launch_mfma_k<CT, RT, 9, 1>(p, a, B, C, N, s); break;
-        default: two ? launch_mfma_k<CT, RT, 8, 2>(p, a, B, C, N, s) : launch_mfma_k<CT, RT, 8, 1>(p, a, B, C, N, s); break;
-    }
-}
-
-template <int CT>
-void launch_mfma_ct(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N,
-                    hipStream_t s) {
-    switch (p.dev.maxr) {
-        case 1: launch_mfma_rt<CT, 1>(p, a, B, C, N, s); break;
-        case 2: launch_mfma_rt<CT, 2>(p, a, B, C, N, s); break;
-        case 3: launch_mfma_rt<CT, 3>(p, a, B, C, N, s); break;
-        default: launch_mfma_rt<CT, 4>(p, a, B, C, N, s); break;
-    }
-}
-
-}  // namespace
-
-// diagnostic: N = 32 plans with 17..48-row BMTBs and KC 256 or 512
-template <int RT, int LG>
-auto timeline_kernel(bool two) {
-    return two ? gsk::k_mfma_rows<2, RT, LG, 2, true, 2> : gsk::k_mfma_rows<2, RT, LG, 1, true, 2>;  // LDS-DMA B (default)
-}
-
-void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
-                         size_t n_host) {
-    const device_plan &d = p.dev;
-    GS_CHECK(p.uploaded && d.mfma && N == d.lds_N && N == 32 && (d.maxr == 2 || d.maxr == 3) &&
-                 (d.RSB == 8 || d.RSB == 9),
-             "timeline build exists for N=32 matrix-core plans with 17..48-row BMTBs, KC 256/512 only");
-    const device_arrays &a = d.replicas[0];
-    const bool two = d.seg_cap > 64u * gsk::kMfmaAWavesG;
-    auto kern = d.maxr == 2 ? (d.RSB == 9 ? timeline_kernel<2, 9>(two) : timeline_kernel<2, 8>(two))
-                            : (d.RSB == 9 ? timeline_kernel<3, 9>(two) : timeline_kernel<3, 8>(two));
-    const size_t lds = d.lds_bytes;
-    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)lds));
-    uint64_t *dst = nullptr;
-    const size_t n = (size_t)d.n_rows_aux * d.ksplit * 64;
-    HIP_OK(hipMalloc(&dst, n * 8));
-    hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit), dim3(kMfmaThreads), lds, s, a.t0, a.t1,
-                       (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, (const gsk::f16 *)B, (gsk::f16 *)C,
-                       (uint32_t)p.K, N, d.nc, d.rpw_max, (uint32_t)d.row_base, d.ksplit, d.ncs, a.ws, a.t2, dst, 0u);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipStreamSynchronize(s));
-    HIP_OK(hipMemcpy(host, dst, std::min(n, n_host) * 8, hipMemcpyDeviceToHost));
-    (void)hipFree(dst);
-}
-
-namespace {
-
-template <int CT>
-void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, void *C, hipStream_t s) {
-    const device_plan &d = p.dev;
-    // GS_NM_DEBUG=1/2: diagnostic builds without the loop's B / A loads (wrong results)
-    static const int dbg = getenv("GS_NM_DEBUG") ? atoi(getenv("GS_NM_DEBUG")) : 0;
-    auto kern = dbg == 1 ? gsk::k_nm_mfma<CT, 1>
-                         : (dbg == 2 ? gsk::k_nm_mfma<CT, 2> : (dbg == 4 ? gsk::k_nm_mfma<CT, 4> : gsk::k_nm_mfma<CT, 0>));
-    const size_t lds = (size_t)2 * gsk::kNmKC * 32 * CT + (dbg == 4 ? 4096 : 0);
-    static std::mutex mu;
-    static std::map<std::pair<int, const void *>, bool> granted;
-    {
-        std::lock_guard<std::mutex> l(mu);
-        bool &g = granted[{d.device, reinterpret_cast<const void *>(kern)}];
-        if (!g) {
-            HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds));
-            g = true;
-        }
-    }
-    const uint32_t wg = (uint32_t)((d.n_rows_aux + 127) / 128);
-    hipLaunchKernelGGL(kern, dim3(wg), dim3(64 * gsk::kNmWaves), lds, s, (const unsigned char *)a.tcol,
-                       (const gsk::f16 *)B, (gsk::f16 *)C, (uint32_t)p.K, d.KC, (uint32_t)d.n_rows_aux,
-                       (uint32_t)d.row_base, (uint32_t)get_config().MFMA_KROT);
-    HIP_OK(hipGetLastError());
-}
-
-void launch_nm(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
-    switch (N) {
-        case 32: launch_nm_ct<2>(p, a, B, C, s); break;
-        case 64: launch_nm_ct<4>(p, a, B, C, s); break;
-        case 128: launch_nm_ct<8>(p, a, B, C, s); break;
-        default:
-            throw gs_error("2:4 panel plan (k_nm_mfma) runs N = 32, 64 or 128, not " + std::to_string(N), -2);
-    }
-}
-
-template <int CT, int RT, int EMAX>
-void launch_wk_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
-    const device_plan &d = p.dev;
-    auto kern = gsk::k_mfma_wk<CT, RT, EMAX>;
-    static std::mutex mu;
-    static std::map<int, size_t> granted;
-    {
-        std::lock_guard<std::mutex> l(mu);
-        size_t &g = granted[d.device];
-        if (g < d.lds_bytes) {
-            HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)d.lds_bytes));
-            g = d.lds_bytes;
-        }
-    }
-    hipLaunchKernelGGL(kern, dim3(d.wk_nb), dim3(64 * gsk::kWkWaves), d.lds_bytes, s, a.t0, a.t1,
-                       (const uint32_t *)a.tcol, B, C, (uint32_t)p.K, N, d.wk_steps, (uint32_t)d.row_base);
-    HIP_OK(hipGetLastError());
-}
-
-template <int CT, int RT>
-void launch_wk_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
-    switch (p.dev.wk_emax) {
-        case 1: launch_wk_k<CT, RT, 1>(p, a, B, C, N, s); break;
-        case 2: launch_wk_k<CT, RT, 2>(p, a, B, C, N, s); break;
-        case 4: launch_wk_k<CT, RT, 4>(p, a, B, C, N, s); break;
-        default: launch_wk_k<CT, RT, 8>(p, a, B, C, N, s); break;
-    }
-}
-
-template <int CT, int RT, int VAR>
-void launch_bm_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
-    constexpr bm_shape v = kBmVariant[VAR];
-    constexpr size_t lds = bm_lds_bytes(CT, RT, v);
-    if constexpr (lds > 160 * 1024) {
-        throw gs_error("k_mfma_bitmap variant does not fit LDS at this N");
-    } else {
-        const device_plan &d = p.dev;
-        // GS_BM_DEBUG=6 (diagnostic timing build, wrong results): kernel_lib.hpp DBG bits; N=32
-        static const int dbg = getenv("GS_BM_DEBUG") ? atoi(getenv("GS_BM_DEBUG")) : 0;
-        auto kern = gsk::k_mfma_bitmap<CT, RT, v.W, v.DA, v.DB>;
-        if constexpr (CT == 2 && RT == 2) {
-            if (dbg == 6) kern = gsk::k_mfma_bitmap<CT, RT, v.W, v.DA, v.DB, 6>;
-        }
-        static std::mutex mu;
-        static std::map<std::pair<int, const void *>, bool> granted;
-        {
-            std::lock_guard<std::mutex> l(mu);
-            bool &gr = granted[{d.device, reinterpret_cast<const void *>(kern)}];
-            if (!gr) {
-                HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-                gr = true;
-            }
-        }
-        hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux), dim3(64 * v.W), lds, s, a.t0, a.t1,
-                           (const gsk::u32x4 *)a.tcol, B, C, (uint32_t)p.K, N, d.bm_nks, (uint32_t)d.row_base);
-        HIP_OK(hipGetLastError());
-    }
-}
-
-template <int CT, int RT>
-void launch_bm_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
-    switch (p.dev.bm_variant) {
-        case 0: launch_bm_k<CT, RT, 0>(p, a, B, C, N, s); break;
-        case 1: launch_bm_k<CT, RT, 1>(p, a, B, C, N, s); break;
-        case 2: launch_bm_k<CT, RT, 2>(p, a, B, C, N, s); break;
-        case 3: launch_bm_k<CT, RT, 3>(p, a, B, C, N, s); break;
-        case 4: launch_bm_k<CT, RT, 4>(p, a, B, C, N, s); break;
-        case 5: launch_bm_k<CT, RT, 5>(p, a, B, C, N, s); break;
-        default: launch_bm_k<CT, RT, 6>(p, a, B, C, N, s); break;
-    }
-}
-
-template <int CT>
-void launch_bm(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
-    if (p.dev.maxr > 1) launch_bm_rt<CT, 2>(p, a, B, C, N, s);
-    else launch_bm_rt<CT, 1>(p, a, B, C, N, s);
-}
-
-void launch_mfma(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
-    const gsk::f16 *b = (const gsk::f16 *)B;
-    gsk::f16 *c = (gsk::f16 *)C;
-    if (p.dev.bm) {
-        GS_CHECK(N == 16 || N == 32 || N == 64, "bitmap panels run N = 16, 32 or 64");
-        if (N == 16) launch_bm<1>(p, a, b, c, N, s);
-        else if (N == 32) launch_bm<2>(p, a, b, c, N, s);
-        else launch_bm<4>(p, a, b, c, N, s);
-        return;
-    }
-    if (p.dev.wk) {
-        const bool two = p.dev.maxr > 1;
-        if (N == 16) two ? launch_wk_rt<1, 2>(p, a, b, c, N, s) : launch_wk_rt<1, 1>(p, a, b, c, N, s);
-        else two ? launch_wk_rt<2, 2>(p, a, b, c, N, s) : launch_wk_rt<2, 1>(p, a, b, c, N, s);
-        return;
-    }
-    switch (N / 16) {
-        case 1: launch_mfma_ct<1>(p, a, b, c, N, s); break;
-        case 2: launch_mfma_ct<2>(p, a, b, c, N, s); break;
-        default: launch_mfma_ct<4>(p, a, b, c, N, s); break;
-    }
-}
-
-template <class VT, class CT, int CF, int SCF>
-void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT *C, uint32_t N, hipStream_t s) {
-    const device_plan &d = p.dev;
-    const kernel_spec &sp = p.cg->get_kernel_spec();
-    const uint32_t X = std::min<uint32_t>(64u, pow2ceil((N + CF - 1) / CF));
-    const uint32_t tiles = (N + X * CF - 1) / (X * CF);
-    const uint32_t row_base = (uint32_t)d.row_base;
-    const CT *col = (const CT *)a.col;
-    const VT *val = (const VT *)a.val;
-    switch (sp.family) {
-        case KF_THREAD_TOTAL: {
-            uint32_t groups = 256 / X;
-            uint32_t gx = (uint32_t)std::min<uint64_t>((d.n_rows_aux + groups - 1) / groups, 1u << 16);
-            hipLaunchKernelGGL((gsk::k_thread_total<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0,
-                               s, a.a0, d.f0, a.a1, d.f1, col, val, B, C, (uint32_t)d.n_units, (uint32_t)d.n_rows_aux, N, X,
-                               row_base);
-            break;
-        }
-        case KF_WARP_TOTAL: {
-            if constexpr (CF * sizeof(VT) == 16) {
-                if (d.lds && N == d.lds_N) {
-                    launch_lds<VT, CF>(p, a, B, C, N, s);
-                    break;
-                }
-            }
-            uint32_t gx;
-            if (sp.tblock_parent) gx = (uint32_t)d.n_rows_aux;
-            else gx = (uint32_t)std::min<uint64_t>((d.n_units + 3) / 4, 1u << 16);
-            // slots per row: enough SCF-chunks for the plan's mean row, the rest of the wave on the
-            // next rows of the BMW (only when BMWs hold several rows)
-            uint32_t G = 64u / X;
-            if (d.bmw_rows_max > 1 && get_config().WARP_ROWS_GROUPS) {
-                const uint32_t need = (uint32_t)std::max<double>(1.0, std::ceil(d.mean_row_nnz / 4.0));
-                G = std::min<uint32_t>(G, pow2ceil(need));
-            }
-            hipLaunchKernelGGL((gsk::k_warp_rows<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
-                               a.a0, d.f0, sp.tblock_parent ? a.a1 : nullptr, sp.tblock_parent ? d.f1 : gsk::idx_formula(), a.a2, col, val, B, C, (uint32_t)d.n_units, N,
-                               X, row_base, G);
-            break;
-        }
-        case KF_BLOCK_TOTAL: {
-            uint32_t gx = (uint32_t)std::min<uint64_t>(d.n_units, 1u << 16);
-            hipLaunchKernelGGL((gsk::k_block_rows<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
-                               a.a0, d.f0, a.a2, col, val, B, C, (uint32_t)d.n_units, N, X, row_base);
-            break;
-        }
-        case KF_BITMAP_SEGMENT: {
-            const uint32_t S = 64 / X;
-            uint32_t gx = (uint32_t)std::min<uint64_t>((d.n_units + 4 * S - 1) / (4 * S), 1u << 16);
-            size_t lds = (size_t)4 * S * 2 * X * CF * sizeof(float);
-            // the fp32 workspace is sized for the plan's dense width; other widths use fp16 atomics
-            const bool use_ws = a.ws && N == d.ws_n;
-            if (!use_ws)
-                HIP_OK(hipMemsetAsync(C + (size_t)d.out_lo * N, 0, (size_t)(d.n_out_rows - d.out_lo) * N * sizeof(VT), s));
-            hipLaunchKernelGGL((gsk::k_bitmap_segment<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256),
-                               lds, s, a.a0, d.f0, a.a1, d.f1, a.m0, a.a2, a.a3, col, val, B, C, (uint32_t)d.n_units, N, X,
-                               row_base, use_ws ? a.ws : (float *)nullptr);
-            if (use_ws && d.n_fin) {
-                HIP_OK(hipGetLastError());
-                const uint32_t fx = (uint32_t)std::min<uint64_t>((d.n_fin * N + 255) / 256, 4096);
-                hipLaunchKernelGGL((gsk::k_finalize_rows<VT>), dim3(fx), dim3(256), 0, s, a.a4, (uint32_t)d.n_fin,
-                                   a.ws, C, N);
-            }
-            break;
-        }
-        case KF_ROW_CHUNKS: {
-            GS_CHECK(N <= d.ws_n, "col-direction plan built for N=" + std::to_string(d.ws_n) +
-                                      ": its workspace holds no wider B (re-run the pipeline for this N)");
-            const uint32_t nw = (uint32_t)((d.n_units + d.span - 1) / d.span);
-            const uint32_t gx = std::min<uint32_t>((nw + 3) / 4, 1u << 16);
-            hipLaunchKernelGGL((gsk::k_row_chunks<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
-                               a.a0, d.f0, a.a1, d.f1, col, val, B, C, a.ws, (uint32_t)d.n_units, d.span, N, X, row_base, d.ilv,
-                               a.a2, a.a3);
-            if (d.n_fin) {
-                HIP_OK(hipGetLastError());
-                const uint32_t fx = (uint32_t)std::min<uint64_t>((d.n_fin * N + 255) / 256, 4096);
-                hipLaunchKernelGGL((gsk::k_finalize_rows<VT>), dim3(fx), dim3(256), 0, s, a.a4, (uint32_t)d.n_fin,
-                                   a.ws, C, N);
-            }
-            break;
-        }
-        case KF_MERGE_PATH: {
-            GS_CHECK(N <= d.ws_n, "merge-path plan built for N=" + std::to_string(d.ws_n) +
-                                      ": its carry buffers hold no wider B (re-run the pipeline for this N)");
-            const uint32_t S = 64u / X;
-            const size_t lds = (size_t)4 * gsk::merge_path_wave_lds_words(S) * sizeof(uint32_t);
-            const uint32_t W = (uint32_t)d.n_units;
-            const uint32_t gx = std::min<uint32_t>((W + 3) / 4, 1u << 16);
-            GS_CHECK(d.n_fin * (uint64_t)N < 0xffffffffull, "merge-path empty-row fill exceeds 32-bit indices");
-            const uint32_t fb = d.n_fin ? (uint32_t)std::min<uint64_t>(256, (d.n_fin * N / 4 + 1023) / 1024) : 0u;
-            // one column tile: split rows are combined inside the launch (chain arrivals)
-            const bool fused = tiles == 1 && !(mp_debug() & 4u);
-            hipLaunchKernelGGL((gsk::k_merge_path<VT, CT, CF>), dim3(gx + fb, tiles), dim3(256), lds, s, a.a0, a.a1,
-                               a.a2, a.a3, (uint32_t)d.n_rows_aux, col, val, B, C, a.ws, a.t0, a.ws2, W, N, X, row_base,
-                               (uint32_t)d.n_out_rows, a.a4, (uint32_t)d.n_fin, fb, fused ? a.t1 : nullptr,
-                               fused ? a.t2 : nullptr, mp_debug());
-            HIP_OK(hipGetLastError());
-            if (fused) break;
-            GS_CHECK((uint64_t)W * N < 0xffffffffull, "merge-path fix-up indices exceed 32 bits");
-            const uint32_t fx = (uint32_t)std::min<uint64_t>(((uint64_t)W * N + 255) / 256, 1u << 16);
-            hipLaunchKernelGGL((gsk::k_merge_fixup<VT>), dim3(std::max(fx, 1u)), dim3(256), 0, s, a.t0, a.ws, a.ws2, C,
-                               W, N);
-            break;
-        }
-        default:
-            throw gs_error("no kernel family");
-    }
-    HIP_OK(hipGetLastError());
-}
-
-// compile-time shapes: CF = dense columns per lane (16 B of B when N allows),
-// SCF = sparse entries per A load (16 B for the wave families; the plan's row
-// alignment for thread_total)
-template <class VT, class CT, int CF>
-void dispatch_scf(const plan_state &p, const device_arrays &a, const VT *b, VT *c, uint32_t N, hipStream_t s) {
-    constexpr int VEC = 16 / sizeof(VT);
-    const kernel_spec &sp = p.cg->get_kernel_spec();
-    if (sp.family == KF_THREAD_TOTAL) {
-        if (p.dev.scf >= 8) launch_family<VT, CT, CF, 8>(p, a, b, c, N, s);
-        else if (p.dev.scf >= 4) launch_family<VT, CT, CF, 4>(p, a, b, c, N, s);
-        else launch_family<VT, CT, CF, 1>(p, a, b, c, N, s);
-    } else {
-        launch_family<VT, CT, CF, VEC>(p, a, b, c, N, s);
-    }
-}
-
-template <class VT, int CFV>
-void dispatch_vt(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
-    const VT *b = (const VT *)B;
-    VT *c = (VT *)C;
-    const bool vec = (N % CFV) == 0;
-    if (p.dev.col_bytes == 2) {
-        if (vec) dispatch_scf<VT, uint16_t, CFV>(p, a, b, c, N, s);
-        else dispatch_scf<VT, uint16_t, 1>(p, a, b, c, N, s);
-    } else {
-        if (vec) dispatch_scf<VT, uint32_t, CFV>(p, a, b, c, N, s);
-        else dispatch_scf<VT, uint32_t, 1>(p, a, b, c, N, s);
-    }
-}
-
-}  // namespace
-
 static void launch_body(plan_state &p, int replica, const void *B, void *C, uint32_t N, hipStream_t stream) {
     if (p.dev.nm) {
         launch_nm(p, p.dev.replicas[replica], B, C, N, stream);
@@ -1549,9 +1071,7 @@ static void launch_body(plan_state &p, int replica, const void *B, void *C, uint
         return;
     }
     if (!p.dev.replicas[replica].col) ensure_csr(p);  // matrix-core plan at another dense width
-    const device_arrays &a = p.dev.replicas[replica];
-    if (p.dev.dtype == 0) dispatch_vt<float, 4>(p, a, B, C, N, stream);
-    else dispatch_vt<gsk::f16, 8>(p, a, B, C, N, stream);
+    launch_gather(p, p.dev.replicas[replica], B, C, N, stream);
 }
 
 void launch_spmm(plan_state &p, int replica, const void *B, void *C, uint32_t N, hipStream_t stream) {

@@ -1,0 +1,216 @@
+// gather_launch.hip -- launches of the CUDA-core gather families (k_thread_total,
+// k_warp_rows, k_block_rows, k_bitmap_segment, k_row_chunks, k_merge_path) and the
+// LDS-staged k_lds_rows (hip_code/kernel_lib.hpp).
+#include "../hip_code/kernel_lib.hpp"
+#include "../host/gs_plan.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+
+namespace gs {
+
+#define HIP_OK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) throw gs_error(std::string(#x) + ": " + hipGetErrorString(e_), -3); \
+    } while (0)
+
+namespace {
+
+constexpr int kLdsMaxU = 12;  // 16-B staging registers per thread (k_lds_rows MAXU; device_plan.hip sizes the tiles)
+
+// GS_MP_DEBUG (diagnostic timing only): k_merge_path dbg bits
+uint32_t mp_debug() {
+    static const uint32_t v = getenv("GS_MP_DEBUG") ? (uint32_t)atoi(getenv("GS_MP_DEBUG")) : 0u;
+    return v;
+}
+
+uint32_t pow2ceil(uint32_t x) {
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+template <class VT, int CF>
+void launch_lds(const plan_state &p, const device_arrays &a, const VT *B, VT *C, uint32_t N, hipStream_t s) {
+    const device_plan &d = p.dev;
+    const uint32_t X = N * (uint32_t)sizeof(VT) / 16u;
+    const uint32_t nb = (uint32_t)d.n_rows_aux;
+    const dim3 grid(nb), block(64 * d.waves);
+    const uint32_t K = (uint32_t)p.K;
+#define GS_LDS_ARGS                                                                                              \
+    a.t0, a.a1, a.a0, a.t1, a.t2, (const uint16_t *)a.tcol, (const VT *)a.tval, B, C, K, N, X, d.KC, d.nc, d.RSB, \
+        d.rpw_max, d.seg_cap, (uint32_t)d.row_base
+    auto go = [&](auto kern) {
+        // dynamic LDS above 64 KB must be opted into, once per kernel and device
+        static std::mutex mu;
+        static std::map<std::pair<int, const void *>, size_t> granted;
+        {
+            std::lock_guard<std::mutex> l(mu);
+            size_t &g = granted[{d.device, reinterpret_cast<const void *>(kern)}];
+            if (g < d.lds_bytes) {
+                HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.lds_bytes));
+                g = d.lds_bytes;
+            }
+        }
+        hipLaunchKernelGGL(kern, grid, block, d.lds_bytes, s, GS_LDS_ARGS);
+    };
+    if (d.maxr == 1) go(gsk::k_lds_rows<VT, CF, 1, kLdsMaxU>);
+    else if (d.maxr == 2) go(gsk::k_lds_rows<VT, CF, 2, kLdsMaxU>);
+    else go(gsk::k_lds_rows<VT, CF, 4, kLdsMaxU>);
+#undef GS_LDS_ARGS
+}
+
+template <class VT, class CT, int CF, int SCF>
+void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT *C, uint32_t N, hipStream_t s) {
+    const device_plan &d = p.dev;
+    const kernel_spec &sp = p.cg->get_kernel_spec();
+    const uint32_t X = std::min<uint32_t>(64u, pow2ceil((N + CF - 1) / CF));
+    const uint32_t tiles = (N + X * CF - 1) / (X * CF);
+    const uint32_t row_base = (uint32_t)d.row_base;
+    const CT *col = (const CT *)a.col;
+    const VT *val = (const VT *)a.val;
+    switch (sp.family) {
+        case KF_THREAD_TOTAL: {
+            uint32_t groups = 256 / X;
+            uint32_t gx = (uint32_t)std::min<uint64_t>((d.n_rows_aux + groups - 1) / groups, 1u << 16);
+            hipLaunchKernelGGL((gsk::k_thread_total<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0,
+                               s, a.a0, d.f0, a.a1, d.f1, col, val, B, C, (uint32_t)d.n_units, (uint32_t)d.n_rows_aux, N, X,
+                               row_base);
+            break;
+        }
+        case KF_WARP_TOTAL: {
+            if constexpr (CF * sizeof(VT) == 16) {
+                if (d.lds && N == d.lds_N) {
+                    launch_lds<VT, CF>(p, a, B, C, N, s);
+                    break;
+                }
+            }
+            uint32_t gx;
+            if (sp.tblock_parent) gx = (uint32_t)d.n_rows_aux;
+            else gx = (uint32_t)std::min<uint64_t>((d.n_units + 3) / 4, 1u << 16);
+            // slots per row: enough SCF-chunks for the plan's mean row, the rest of the wave on the
+            // next rows of the BMW (only when BMWs hold several rows)
+            uint32_t G = 64u / X;
+            if (d.bmw_rows_max > 1 && get_config().WARP_ROWS_GROUPS) {
+                const uint32_t need = (uint32_t)std::max<double>(1.0, std::ceil(d.mean_row_nnz / 4.0));
+                G = std::min<uint32_t>(G, pow2ceil(need));
+            }
+            hipLaunchKernelGGL((gsk::k_warp_rows<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
+                               a.a0, d.f0, sp.tblock_parent ? a.a1 : nullptr, sp.tblock_parent ? d.f1 : gsk::idx_formula(), a.a2, col, val, B, C, (uint32_t)d.n_units, N,
+                               X, row_base, G);
+            break;
+        }
+        case KF_BLOCK_TOTAL: {
+            uint32_t gx = (uint32_t)std::min<uint64_t>(d.n_units, 1u << 16);
+            hipLaunchKernelGGL((gsk::k_block_rows<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
+                               a.a0, d.f0, a.a2, col, val, B, C, (uint32_t)d.n_units, N, X, row_base);
+            break;
+        }
+        case KF_BITMAP_SEGMENT: {
+            const uint32_t S = 64 / X;
+            uint32_t gx = (uint32_t)std::min<uint64_t>((d.n_units + 4 * S - 1) / (4 * S), 1u << 16);
+            size_t lds = (size_t)4 * S * 2 * X * CF * sizeof(float);
+            // the fp32 workspace is sized for the plan's dense width; other widths use fp16 atomics
+            const bool use_ws = a.ws && N == d.ws_n;
+            if (!use_ws)
+                HIP_OK(hipMemsetAsync(C + (size_t)d.out_lo * N, 0, (size_t)(d.n_out_rows - d.out_lo) * N * sizeof(VT), s));
+            hipLaunchKernelGGL((gsk::k_bitmap_segment<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256),
+                               lds, s, a.a0, d.f0, a.a1, d.f1, a.m0, a.a2, a.a3, col, val, B, C, (uint32_t)d.n_units, N, X,
+                               row_base, use_ws ? a.ws : (float *)nullptr);
+            if (use_ws && d.n_fin) {
+                HIP_OK(hipGetLastError());
+                const uint32_t fx = (uint32_t)std::min<uint64_t>((d.n_fin * N + 255) / 256, 4096);
+                hipLaunchKernelGGL((gsk::k_finalize_rows<VT>), dim3(fx), dim3(256), 0, s, a.a4, (uint32_t)d.n_fin,
+                                   a.ws, C, N);
+            }
+            break;
+        }
+        case KF_ROW_CHUNKS: {
+            GS_CHECK(N <= d.ws_n, "col-direction plan built for N=" + std::to_string(d.ws_n) +
+                                      ": its workspace holds no wider B (re-run the pipeline for this N)");
+            const uint32_t nw = (uint32_t)((d.n_units + d.span - 1) / d.span);
+            const uint32_t gx = std::min<uint32_t>((nw + 3) / 4, 1u << 16);
+            hipLaunchKernelGGL((gsk::k_row_chunks<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
+                               a.a0, d.f0, a.a1, d.f1, col, val, B, C, a.ws, (uint32_t)d.n_units, d.span, N, X, row_base, d.ilv,
+                               a.a2, a.a3);
+            if (d.n_fin) {
+                HIP_OK(hipGetLastError());
+                const uint32_t fx = (uint32_t)std::min<uint64_t>((d.n_fin * N + 255) / 256, 4096);
+                hipLaunchKernelGGL((gsk::k_finalize_rows<VT>), dim3(fx), dim3(256), 0, s, a.a4, (uint32_t)d.n_fin,
+                                   a.ws, C, N);
+            }
+            break;
+        }
+        case KF_MERGE_PATH: {
+            GS_CHECK(N <= d.ws_n, "merge-path plan built for N=" + std::to_string(d.ws_n) +
+                                      ": its carry buffers hold no wider B (re-run the pipeline for this N)");
+            const uint32_t S = 64u / X;
+            const size_t lds = (size_t)4 * gsk::merge_path_wave_lds_words(S) * sizeof(uint32_t);
+            const uint32_t W = (uint32_t)d.n_units;
+            const uint32_t gx = std::min<uint32_t>((W + 3) / 4, 1u << 16);
+            GS_CHECK(d.n_fin * (uint64_t)N < 0xffffffffull, "merge-path empty-row fill exceeds 32-bit indices");
+            const uint32_t fb = d.n_fin ? (uint32_t)std::min<uint64_t>(256, (d.n_fin * N / 4 + 1023) / 1024) : 0u;
+            // one column tile: split rows are combined inside the launch (chain arrivals)
+            const bool fused = tiles == 1 && !(mp_debug() & 4u);
+            hipLaunchKernelGGL((gsk::k_merge_path<VT, CT, CF>), dim3(gx + fb, tiles), dim3(256), lds, s, a.a0, a.a1,
+                               a.a2, a.a3, (uint32_t)d.n_rows_aux, col, val, B, C, a.ws, a.t0, a.ws2, W, N, X, row_base,
+                               (uint32_t)d.n_out_rows, a.a4, (uint32_t)d.n_fin, fb, fused ? a.t1 : nullptr,
+                               fused ? a.t2 : nullptr, mp_debug());
+            HIP_OK(hipGetLastError());
+            if (fused) break;
+            GS_CHECK((uint64_t)W * N < 0xffffffffull, "merge-path fix-up indices exceed 32 bits");
+            const uint32_t fx = (uint32_t)std::min<uint64_t>(((uint64_t)W * N + 255) / 256, 1u << 16);
+            hipLaunchKernelGGL((gsk::k_merge_fixup<VT>), dim3(std::max(fx, 1u)), dim3(256), 0, s, a.t0, a.ws, a.ws2, C,
+                               W, N);
+            break;
+        }
+        default:
+            throw gs_error("no kernel family");
+    }
+    HIP_OK(hipGetLastError());
+}
+
+// compile-time shapes: CF = dense columns per lane (16 B of B when N allows),
+// SCF = sparse entries per A load (16 B for the wave families; the plan's row
+// alignment for thread_total)
+template <class VT, class CT, int CF>
+void dispatch_scf(const plan_state &p, const device_arrays &a, const VT *b, VT *c, uint32_t N, hipStream_t s) {
+    constexpr int VEC = 16 / sizeof(VT);
+    const kernel_spec &sp = p.cg->get_kernel_spec();
+    if (sp.family == KF_THREAD_TOTAL) {
+        if (p.dev.scf >= 8) launch_family<VT, CT, CF, 8>(p, a, b, c, N, s);
+        else if (p.dev.scf >= 4) launch_family<VT, CT, CF, 4>(p, a, b, c, N, s);
+        else launch_family<VT, CT, CF, 1>(p, a, b, c, N, s);
+    } else {
+        launch_family<VT, CT, CF, VEC>(p, a, b, c, N, s);
+    }
+}
+
+template <class VT, int CFV>
+void dispatch_vt(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
+    const VT *b = (const VT *)B;
+    VT *c = (VT *)C;
+    const bool vec = (N % CFV) == 0;
+    if (p.dev.col_bytes == 2) {
+        if (vec) dispatch_scf<VT, uint16_t, CFV>(p, a, b, c, N, s);
+        else dispatch_scf<VT, uint16_t, 1>(p, a, b, c, N, s);
+    } else {
+        if (vec) dispatch_scf<VT, uint32_t, CFV>(p, a, b, c, N, s);
+        else dispatch_scf<VT, uint32_t, 1>(p, a, b, c, N, s);
+    }
+}
+
+}  // namespace
+
+
+void launch_gather(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
+    if (p.dev.dtype == 0) dispatch_vt<float, 4>(p, a, B, C, N, s);
+    else dispatch_vt<gsk::f16, 8>(p, a, B, C, N, s);
+}
+
+}  // namespace gs

@@ -1,0 +1,97 @@
+// ks_launch.hip -- launches of k_mfma_ks (hip_code/kernel_lib.hpp), the K-split,
+// B-stationary matrix-core kernel for tall BMTB row blocks.  Its own translation unit
+// so the kernel's instantiations build in parallel with device_plan.hip.
+#include "../hip_code/kernel_lib.hpp"
+#include "../host/gs_plan.hpp"
+
+#include <map>
+#include <mutex>
+
+namespace gs {
+
+#define HIP_OK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) throw gs_error(std::string(#x) + ": " + hipGetErrorString(e_), -3); \
+    } while (0)
+
+namespace {
+
+template <class KERN>
+void grant_lds(int device, KERN kern, size_t bytes) {
+    // dynamic LDS above 64 KB is opted into once per kernel and device
+    static std::mutex mu;
+    static std::map<std::pair<int, const void *>, size_t> granted;
+    std::lock_guard<std::mutex> l(mu);
+    size_t &g = granted[{device, reinterpret_cast<const void *>(kern)}];
+    if (g < bytes) {
+        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)bytes));
+        g = bytes;
+    }
+}
+
+template <int CT, int RT, int MAXG, bool STAMPS = false>
+void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s,
+                 uint64_t *stamps = nullptr) {
+    const device_plan &d = p.dev;
+    auto kern = gsk::k_mfma_ks<CT, RT, (int)kKsWaves, (int)kKsDepth, MAXG, STAMPS>;
+    // the LDS this instantiation needs at the plan's range width, against what the upload sized
+    GS_CHECK(gsk::ks_lds_bytes(CT, RT, kKsWaves) <= d.lds_bytes, "k_mfma_ks: LDS size disagrees with the upload");
+    grant_lds(d.device, kern, d.lds_bytes);
+    hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit), dim3(64 * kKsWaves), d.lds_bytes, s, a.t0,
+                       (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, B, C, (uint32_t)p.K, N, d.ksplit,
+                       d.ks_ns, d.ks_gcap, (uint32_t)d.n_rows_aux * d.ksplit, (uint32_t)d.row_base, a.ws, a.t2, stamps);
+    HIP_OK(hipGetLastError());
+}
+
+template <int CT, int RT>
+void launch_ks_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
+    switch (p.dev.seg_cap) {  // MAXG: entry groups per lane per k-step
+        case 1: launch_ks_k<CT, RT, 1>(p, a, B, C, N, s); break;
+        case 2: launch_ks_k<CT, RT, 2>(p, a, B, C, N, s); break;
+        default: launch_ks_k<CT, RT, 4>(p, a, B, C, N, s); break;
+    }
+}
+
+template <int CT>
+void launch_ks_ct(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
+    switch (p.dev.maxr) {  // RT: 16-row tiles per row block (the upload builds RT >= 2)
+        case 2: launch_ks_rt<CT, 2>(p, a, B, C, N, s); break;
+        case 3: launch_ks_rt<CT, 3>(p, a, B, C, N, s); break;
+        case 4: launch_ks_rt<CT, 4>(p, a, B, C, N, s); break;
+        case 5: launch_ks_rt<CT, 5>(p, a, B, C, N, s); break;
+        default: throw gs_error("k_mfma_ks: row tiles outside 2..5");
+    }
+}
+
+}  // namespace
+
+void launch_ks(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
+    const gsk::f16 *b = (const gsk::f16 *)B;
+    gsk::f16 *c = (gsk::f16 *)C;
+    GS_CHECK(N == p.dev.lds_N, "k_mfma_ks runs the plan's dense width");
+    switch (N) {
+        case 16: launch_ks_ct<1>(p, a, b, c, N, s); break;
+        case 32: launch_ks_ct<2>(p, a, b, c, N, s); break;
+        case 64: launch_ks_ct<4>(p, a, b, c, N, s); break;
+        default: throw gs_error("k_mfma_ks runs N = 16, 32 or 64");
+    }
+}
+
+// diagnostic: the C2 shape (N = 32, 65..80-row blocks, <= 128 entry groups per k-step)
+void debug_ks_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
+                       size_t n_host) {
+    const device_plan &d = p.dev;
+    GS_CHECK(N == 32 && d.maxr == 5 && d.seg_cap == 2, "k_mfma_ks timeline build: N=32, RT=5, MAXG=2 only");
+    const size_t n = (size_t)d.n_rows_aux * d.ksplit * kKsWaves * 32;
+    uint64_t *dst = nullptr;
+    HIP_OK(hipMalloc(&dst, n * 8));
+    HIP_OK(hipMemsetAsync(dst, 0, n * 8, s));
+    launch_ks_k<2, 5, 2, true>(p, d.replicas[0], (const gsk::f16 *)B, (gsk::f16 *)C, N, s, dst);
+    HIP_OK(hipStreamSynchronize(s));
+    HIP_OK(hipMemcpy(host, dst, std::min(n, n_host) * 8, hipMemcpyDeviceToHost));
+    (void)hipFree(dst);
+}
+
+}  // namespace gs

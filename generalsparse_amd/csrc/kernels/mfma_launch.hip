@@ -1,0 +1,182 @@
+// mfma_launch.hip -- launches of the dense-tile matrix-core kernels k_mfma_rows and
+// k_nm_mfma (hip_code/kernel_lib.hpp); k_mfma_ks has ks_launch.hip.  Separate
+// translation units so the kernel instantiations build in parallel.
+#include "../hip_code/kernel_lib.hpp"
+#include "../host/gs_plan.hpp"
+
+#include <cstdlib>
+#include <map>
+#include <mutex>
+
+namespace gs {
+
+#define HIP_OK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) throw gs_error(std::string(#x) + ": " + hipGetErrorString(e_), -3); \
+    } while (0)
+
+namespace {
+
+constexpr uint32_t kMfmaThreads = 64 * gsk::kMfmaWaves;
+
+template <int CT, int RT, int LGKC, int MAXA>
+void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N,
+                   hipStream_t s) {
+    const device_plan &d = p.dev;
+    // B rows by LDS-DMA two chunks ahead (MFMA_GLDS) or through registers three ahead
+    const int64_t gl = get_config().MFMA_GLDS, nbuf = get_config().MFMA_GLDS_NBUF;
+    auto kern = gl >= 4 ? gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 4>
+                        : (gl ? gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2> : gsk::k_mfma_rows<CT, RT, LGKC, MAXA>);
+    if (gl == 1 && get_config().MFMA_COMPUTE_WAVES == 8) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 8>;
+    // GS_MFMA_DEBUG (diagnostic timing builds, wrong results): kernel_lib.hpp k_mfma_rows DBG bits, C2 shape only
+    static const int mdbg = getenv("GS_MFMA_DEBUG") ? atoi(getenv("GS_MFMA_DEBUG")) : 0;
+    if constexpr (CT == 2 && RT == 2 && LGKC == 9 && MAXA == 1) {
+        if (gl == 1 && mdbg == 1) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 1>;
+        if (gl == 1 && mdbg == 2) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 2>;
+        if (gl == 1 && mdbg == 4) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 4>;
+        if (gl == 1 && mdbg == 10) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 10>;
+        if (gl == 1 && mdbg == 11) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 11>;
+        if (gl == 1 && mdbg == 15) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 15>;
+    }
+    if constexpr (LGKC == 8) {  // deeper B rings fit LDS with 256-column chunks
+        if (gl && !(gl >= 4) && nbuf == 4) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 4>;
+        if (gl && !(gl >= 4) && nbuf >= 5) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 5>;
+    }
+    static std::mutex mu;
+    static std::map<std::pair<int, const void *>, size_t> granted;
+    {
+        std::lock_guard<std::mutex> l(mu);
+        size_t &g = granted[{d.device, reinterpret_cast<const void *>(kern)}];
+        if (g < d.lds_bytes) {
+            HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)d.lds_bytes));
+            g = d.lds_bytes;
+        }
+    }
+    hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit), dim3(kMfmaThreads), d.lds_bytes, s, a.t0,
+                       a.t1, (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, B, C, (uint32_t)p.K, N, d.nc,
+                       d.rpw_max, (uint32_t)d.row_base, d.ksplit, d.ncs, a.ws, a.t2, (uint64_t *)nullptr,
+                       (uint32_t)get_config().MFMA_KROT);
+    HIP_OK(hipGetLastError());
+}
+
+template <int CT, int RT>
+void launch_mfma_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N,
+                    hipStream_t s) {
+    // entry groups per thread per chunk: the GLDS variant has 9 entry waves, the other 6
+    const int64_t gl = get_config().MFMA_GLDS;
+    const uint32_t wct = get_config().MFMA_COMPUTE_WAVES == 8 && gl == 1 ? 8u : (uint32_t)gsk::kMfmaCompute;
+    const uint32_t nat = 64u * (gsk::kMfmaWaves - wct - (gl >= 4 ? 4u : (gl ? 2u : (uint32_t)gsk::kMfmaBWaves)));
+    const bool two = p.dev.seg_cap > nat;
+    switch (p.dev.RSB) {                  // log2 KC
+        case 10: two ? launch_mfma_k<CT, RT, 10, 2>(p, a, B, C, N, s) : launch_mfma_k<CT, RT, 10, 1>(p, a, B, C, N, s); break;
+        case 9: two ? launch_mfma_k<CT, RT, 9, 2>(p, a, B, C, N, s) : launch_mfma_k<CT, RT, 9, 1>(p, a, B, C, N, s); break;
+        default: two ? launch_mfma_k<CT, RT, 8, 2>(p, a, B, C, N, s) : launch_mfma_k<CT, RT, 8, 1>(p, a, B, C, N, s); break;
+    }
+}
+
+template <int CT>
+void launch_mfma_ct(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N,
+                    hipStream_t s) {
+    switch (p.dev.maxr) {
+        case 1: launch_mfma_rt<CT, 1>(p, a, B, C, N, s); break;
+        case 2: launch_mfma_rt<CT, 2>(p, a, B, C, N, s); break;
+        case 3: launch_mfma_rt<CT, 3>(p, a, B, C, N, s); break;
+        default: launch_mfma_rt<CT, 4>(p, a, B, C, N, s); break;
+    }
+}
+
+}  // namespace
+
+// diagnostic: N = 32 plans with 17..48-row BMTBs and KC 256 or 512
+template <int RT, int LG>
+auto timeline_kernel(bool two) {
+    return two ? gsk::k_mfma_rows<2, RT, LG, 2, true, 2> : gsk::k_mfma_rows<2, RT, LG, 1, true, 2>;  // LDS-DMA B (default)
+}
+
+void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
+                         size_t n_host) {
+    const device_plan &d = p.dev;
+    if (d.ks) {
+        debug_ks_timeline(p, B, C, N, s, host, n_host);
+        return;
+    }
+    GS_CHECK(p.uploaded && d.mfma && N == d.lds_N && N == 32 && (d.maxr == 2 || d.maxr == 3) &&
+                 (d.RSB == 8 || d.RSB == 9),
+             "timeline build exists for N=32 matrix-core plans with 17..48-row BMTBs, KC 256/512 only");
+    const device_arrays &a = d.replicas[0];
+    const bool two = d.seg_cap > 64u * gsk::kMfmaAWavesG;
+    auto kern = d.maxr == 2 ? (d.RSB == 9 ? timeline_kernel<2, 9>(two) : timeline_kernel<2, 8>(two))
+                            : (d.RSB == 9 ? timeline_kernel<3, 9>(two) : timeline_kernel<3, 8>(two));
+    const size_t lds = d.lds_bytes;
+    HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds));
+    uint64_t *dst = nullptr;
+    const size_t n = (size_t)d.n_rows_aux * d.ksplit * 64;
+    HIP_OK(hipMalloc(&dst, n * 8));
+    hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit), dim3(kMfmaThreads), lds, s, a.t0, a.t1,
+                       (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, (const gsk::f16 *)B, (gsk::f16 *)C,
+                       (uint32_t)p.K, N, d.nc, d.rpw_max, (uint32_t)d.row_base, d.ksplit, d.ncs, a.ws, a.t2, dst, 0u);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(s));
+    HIP_OK(hipMemcpy(host, dst, std::min(n, n_host) * 8, hipMemcpyDeviceToHost));
+    (void)hipFree(dst);
+}
+
+namespace {
+
+template <int CT>
+void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, void *C, hipStream_t s) {
+    const device_plan &d = p.dev;
+    // GS_NM_DEBUG=1/2: diagnostic builds without the loop's B / A loads (wrong results)
+    static const int dbg = getenv("GS_NM_DEBUG") ? atoi(getenv("GS_NM_DEBUG")) : 0;
+    auto kern = dbg == 1 ? gsk::k_nm_mfma<CT, 1>
+                         : (dbg == 2 ? gsk::k_nm_mfma<CT, 2> : (dbg == 4 ? gsk::k_nm_mfma<CT, 4> : gsk::k_nm_mfma<CT, 0>));
+    const size_t lds = (size_t)2 * gsk::kNmKC * 32 * CT + (dbg == 4 ? 4096 : 0);
+    static std::mutex mu;
+    static std::map<std::pair<int, const void *>, bool> granted;
+    {
+        std::lock_guard<std::mutex> l(mu);
+        bool &g = granted[{d.device, reinterpret_cast<const void *>(kern)}];
+        if (!g) {
+            HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds));
+            g = true;
+        }
+    }
+    const uint32_t wg = (uint32_t)((d.n_rows_aux + 127) / 128);
+    hipLaunchKernelGGL(kern, dim3(wg), dim3(64 * gsk::kNmWaves), lds, s, (const unsigned char *)a.tcol,
+                       (const gsk::f16 *)B, (gsk::f16 *)C, (uint32_t)p.K, d.KC, (uint32_t)d.n_rows_aux,
+                       (uint32_t)d.row_base, (uint32_t)get_config().MFMA_KROT);
+    HIP_OK(hipGetLastError());
+}
+
+}  // namespace
+
+void launch_nm(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
+    switch (N) {
+        case 32: launch_nm_ct<2>(p, a, B, C, s); break;
+        case 64: launch_nm_ct<4>(p, a, B, C, s); break;
+        case 128: launch_nm_ct<8>(p, a, B, C, s); break;
+        default:
+            throw gs_error("2:4 panel plan (k_nm_mfma) runs N = 32, 64 or 128, not " + std::to_string(N), -2);
+    }
+}
+
+void launch_mfma(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
+    const gsk::f16 *b = (const gsk::f16 *)B;
+    gsk::f16 *c = (gsk::f16 *)C;
+    if (p.dev.ks) {
+        launch_ks(p, a, B, C, N, s);  // ks_launch.hip
+        return;
+    }
+    switch (N / 16) {
+        case 1: launch_mfma_ct<1>(p, a, b, c, N, s); break;
+        case 2: launch_mfma_ct<2>(p, a, b, c, N, s); break;
+        default: launch_mfma_ct<4>(p, a, b, c, N, s); break;
+    }
+}
+
+
+}  // namespace gs

@@ -306,8 +306,7 @@ def mfma_everywhere():
     yield
     gsa.set_config("MFMA_MAX_FILL", 16)
     gsa.set_config("MFMA_GLDS", 1)
-    gsa.set_config("MFMA_BITMAP", 0)
-    gsa.set_config("BM_VARIANT", 0)
+    gsa.set_config("MFMA_KS", 1)
 
 
 @pytest.mark.parametrize("glds", [1, 0])  # B rows by LDS-DMA (default) / through registers
@@ -328,38 +327,68 @@ def test_mfma_rows_match_oracle(pipe, N, glds, mfma_everywhere):
         check(C, ref, "f16")
         plan.free()
     if not (p0 > 32 and N == 64):
-        assert "k_mfma_rows" in used, used
+        assert any(k in ("k_mfma_rows", "k_mfma_ks") for k in used), used
 
 
-BM_PIPES = [("tblock_warp_total", 20, 2), ("block_total", 16, 1), ("block_total", 20, 1),
-            ("block_total", 32, 1), ("block_total", 7, 1), ("block_total", 1, 1)]
-# device_plan.hip kBmVariant: (waves, A ring slots, B ring slots)
-BM_VARIANTS = [(8, 8, 3), (16, 4, 2), (8, 12, 3), (8, 6, 5), (12, 4, 4), (8, 6, 2), (8, 6, 6)]
+# K-split matrix-core kernel (k_mfma_ks): row blocks of >= KS_MIN_ROWS rows, K ranges per
+# row block (KS_SPLIT; 0 = enough workgroups for the CUs), slabs combined by the last arriver
+KS_PIPES = [("block_total", 40, 1), ("block_total", 48, 1), ("block_total", 64, 1), ("block_total", 80, 1),
+            ("tblock_warp_total", 80, 2)]
 
 
-@pytest.mark.parametrize("variant", range(len(BM_VARIANTS)))
+@pytest.mark.parametrize("split", [0, 1, 3])
 @pytest.mark.parametrize("N", [16, 32, 64])
-@pytest.mark.parametrize("pipe", BM_PIPES, ids=lambda p: f"{p[0]}-{p[1]}")
-def test_mfma_bitmap_matches_oracle(pipe, N, variant, mfma_everywhere):
-    """bitmap panels (k_mfma_bitmap, opt-in MFMA_BITMAP=1) in every workgroup shape
-    that fits LDS: same results as the oracle, and the kernel actually ran"""
+@pytest.mark.parametrize("pipe", KS_PIPES, ids=lambda p: f"{p[0]}-{p[1]}")
+def test_mfma_ks_matches_oracle(pipe, N, split, mfma_everywhere):
     name, p0, p1 = pipe
-    W, DA, DB = BM_VARIANTS[variant]
-    fits = W * (DA * 1024 + DB * 1024 * (N // 16)) + 128 <= 160 * 1024
-    gsa.set_config("MFMA_BITMAP", 1)
-    gsa.set_config("BM_VARIANT", variant)
+    gsa.set_config("KS_SPLIT", split)
     used = []
-    for case, M, K, row, col, val in mfma_cases():
-        plan, C, B = run(M, K, row, col, val, name, p0, p1, N, "f16")
-        used.append(plan.info()["device_kernel"])
-        v = val.astype(np.float16).astype(np.float32)
-        ref = ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64")
-        check(C, ref, "f16")
-        plan.free()
-    assert ("k_mfma_bitmap" in used) == fits, used
+    try:
+        for case, M, K, row, col, val in mfma_cases():
+            plan, C, B = run(M, K, row, col, val, name, p0, p1, N, "f16")
+            info = plan.info()
+            used.append(info["device_kernel"])
+            v = val.astype(np.float16).astype(np.float32)
+            ref = ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64")
+            check(C, ref, "f16")
+            if info["device_kernel"] == "k_mfma_ks":
+                # deterministic whichever K range arrives last; arrival counters reset; replicas agree
+                Bt = torch.from_numpy(B).to(DEV)
+                np.testing.assert_array_equal(plan.spmm(Bt).float().cpu().numpy(), C)
+                plan.add_replica()
+                np.testing.assert_array_equal(plan.spmm(Bt, replica=1).float().cpu().numpy(), C)
+            plan.free()
+    finally:
+        gsa.set_config("KS_SPLIT", 0)
+    assert "k_mfma_ks" in used, used
 
 
-@pytest.mark.parametrize("kernel", ["k_mfma_bitmap", "k_mfma_rows", "k_mfma_wk"])
+def test_mfma_ks_known_answer_and_c2():
+    """all-ones known answer bit-exactly, and the C2 shape (80-row blocks, 4 K ranges) against
+    a torch fp32 dense product of the same fp16 inputs"""
+    M, K, N = 700, 9000, 32
+    row, col, _ = ds.random_rows(M, K, 700.0, seed=8, empty_frac=0.1)  # row nnz < 2048: exact in fp16
+    plan, C, _ = run(M, K, row, col, np.ones(len(row), np.float32), "block_total", 64, 1, N, "f16",
+                     B=np.ones((K, N), np.float16))
+    assert plan.info()["device_kernel"] == "k_mfma_ks", plan.info()
+    nnz_row = np.bincount(row.astype(np.int64), minlength=M).astype(np.float32)
+    np.testing.assert_array_equal(C, np.repeat(nnz_row[:, None], N, axis=1))
+    M = K = 5120
+    r, c, v = ds.pruned_weight(M, K, 0.7, 13)
+    A = torch.zeros((M, K), dtype=torch.float32)
+    A[torch.from_numpy(r.astype(np.int64)), torch.from_numpy(c.astype(np.int64))] = torch.from_numpy(v).half().float()
+    B = torch.randn((K, N), device=DEV, dtype=torch.float16)
+    ref = A.to(DEV) @ B.float()
+    plan = gsa.Plan.from_coo(M, K, r, c, v).run_pipeline("block_total", N, 80, 1).compile().upload("f16", 0)
+    info = plan.info()
+    assert info["device_kernel"] == "k_mfma_ks" and info["ksplit"] == 4, info
+    C = plan.spmm(B).float()
+    err = ((C - ref).abs() / ref.abs().clamp(min=1.0)).max().item()
+    assert err <= 1e-1, err
+    assert torch.equal(plan.spmm(B * 2).float(), 2 * C)  # linearity, deterministic
+
+
+@pytest.mark.parametrize("kernel", ["k_mfma_rows", "k_mfma_ks"])
 def test_mfma_unsorted_columns_and_duplicates(kernel, mfma_everywhere):
     """the reference accepts any column order inside a row and its gather kernels
     add repeated coordinates: the matrix-core layouts sort each row and sum
@@ -376,15 +405,10 @@ def test_mfma_unsorted_columns_and_duplicates(kernel, mfma_everywhere):
     v2 = np.concatenate([v, (0.5 * v[dup]).astype(np.float32)])
     o = np.argsort(r2, kind="stable")
     r2, c2, v2 = r2[o], c2[o], v2[o]
-    gsa.set_config("MFMA_BITMAP", 1 if kernel == "k_mfma_bitmap" else 0)
-    gsa.set_config("MFMA_WK", 1 if kernel == "k_mfma_wk" else 0)
-    try:
-        plan, C, B = run(M, K, r2, c2, v2, "block_total", 20, 1, N, "f16")
-        assert plan.info()["device_kernel"] == kernel
-        ref = ofi.spmm_ref(M, N, r2, c2, v2.astype(np.float16).astype(np.float32), B.astype(np.float32), "f64")
-        check(C, ref, "f16")
-    finally:
-        gsa.set_config("MFMA_WK", 0)
+    plan, C, B = run(M, K, r2, c2, v2, "block_total", 20 if kernel == "k_mfma_rows" else 48, 1, N, "f16")
+    assert plan.info()["device_kernel"] == kernel
+    ref = ofi.spmm_ref(M, N, r2, c2, v2.astype(np.float16).astype(np.float32), B.astype(np.float32), "f64")
+    check(C, ref, "f16")
 
 
 def test_mfma_non_finite_B_deviation(mfma_everywhere):
@@ -410,28 +434,6 @@ def test_mfma_non_finite_B_deviation(mfma_everywhere):
         np.testing.assert_array_equal(np.isfinite(C0[:, 3]), ~has_k)  # reference semantics
     finally:
         gsa.set_config("MFMA_TILES", 1)
-
-
-@pytest.mark.parametrize("N", [16, 32])
-@pytest.mark.parametrize("pipe", [("tblock_warp_total", 20, 2), ("block_total", 16, 1),
-                                  ("block_total", 7, 1), ("block_total", 32, 1)],
-                         ids=lambda p: f"{p[0]}-{p[1]}")
-def test_mfma_wk_matches_oracle(pipe, N, mfma_everywhere):
-    # opt-in wave-owned k-step kernel (MFMA_WK=1, k_mfma_wk): same results as the oracle
-    name, p0, p1 = pipe
-    gsa.set_config("MFMA_WK", 1)
-    used = []
-    try:
-        for case, M, K, row, col, val in mfma_cases():
-            plan, C, B = run(M, K, row, col, val, name, p0, p1, N, "f16")
-            used.append(plan.info()["device_kernel"])
-            v = val.astype(np.float16).astype(np.float32)
-            ref = ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64")
-            check(C, ref, "f16")
-            plan.free()
-    finally:
-        gsa.set_config("MFMA_WK", 0)
-    assert "k_mfma_wk" in used, used
 
 
 def test_mfma_rows_known_answer_and_fallback(mfma_everywhere):
@@ -475,7 +477,7 @@ def test_mfma_rows_ksplit_combine(ks, mfma_everywhere):
     M, K, N = 400, 6000, 32
     r, c, v = ds.pruned_weight(M, K, 0.7, 31)
     try:
-        gsa.set_config("MFMA_BITMAP", 0)
+        gsa.set_config("MFMA_KS", 0)  # the k_mfma_rows split (k_mfma_ks: test_mfma_ks_*)
         gsa.set_config("MFMA_KSPLIT", ks)
         plan, C, B = run(M, K, r, c, v, "block_total", 40, 1, N, "f16")
         info = plan.info()
