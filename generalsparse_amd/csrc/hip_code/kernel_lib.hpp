@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include "idx_formula.hpp"
+#include "kernel_consts.hpp"
 
 namespace gsk {
 
@@ -1023,10 +1024,6 @@ __device__ __forceinline__ uint32_t b_piece(uint32_t k, uint32_t p) {
     return p ^ (sw & (uint32_t)(CT - 1));
 }
 
-// waves per role: compute 0..5, B loaders 6..9, entry loaders 10..15
-constexpr int kMfmaWaves = 16, kMfmaCompute = 6, kMfmaBWaves = 4, kMfmaAWaves = 6;
-// GLDS = g > 0: g waves issue the B rows (LDS-DMA), the other 10 - g load and scatter entries
-constexpr int kMfmaBWavesG = 2, kMfmaAWavesG = 8;
 
 // STAMPS (diagnostic build only, gs_debug_mfma_timeline): lane 0 of the first
 // compute / B / entry wave records s_memtime at phase boundaries
@@ -1451,20 +1448,7 @@ __device__ constexpr int vmcnt_imm() {
     return (N & 0xF) | ((N >> 4) << 14) | 0x70 | 0xF00;
 }
 
-constexpr uint32_t kKsStride = 96;  // image row stride: conflict-free ds_read_b128 fragment reads
-
-template <int RT>
-__host__ __device__ constexpr uint32_t ks_image_bytes() {
-    return (16u * RT + 1u) * kKsStride;
-}
-
-// dynamic LDS of k_mfma_ks: W x (wave image + one k-step of B rows), or the W partial
-// tiles of the final reduction (+ the arrival flag), whichever is larger
-__host__ __device__ constexpr size_t ks_lds_bytes(uint32_t CT, uint32_t RT, uint32_t W) {
-    const size_t stage = (size_t)W * ((16u * RT + 1u) * kKsStride + 32u * 32u * CT);
-    const size_t red = (size_t)W * RT * CT * 1024u + 16u;
-    return stage > red ? stage : red;
-}
+// kKsStride, ks_image_bytes, ks_lds_bytes: kernel_consts.hpp
 
 // STAMPS (diagnostic build only, gs_debug_mfma_timeline): lane 0 of every wave records
 // s_memtime into stamps[(workgroup * W + wave) * 32 + slot]: 0 start, 1 loads issued,
@@ -1706,8 +1690,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
 // order through LDS ((q0 + q2) + (q1 + q3): deterministic) and stored as fp16.
 // ---------------------------------------------------------------------------
 typedef _Float16 h16v __attribute__((ext_vector_type(16)));
-constexpr int kNmWaves = 8;
-constexpr uint32_t kNmBlockBytes = 4608, kNmKC = 256;
+// kNmWaves, kNmBlockBytes, kNmKC: kernel_consts.hpp
 
 // DBG (diagnostic builds only, GS_NM_DEBUG): 1 = no B loads in the loop, 2 = no A loads,
 // 4 = s_memtime phase stamps of waves 0/4 of workgroups 0 and 100, printed

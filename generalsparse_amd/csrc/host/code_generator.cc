@@ -1,6 +1,7 @@
 // code_generator.cc -- lowers the operators' reduction tokens to a gfx950 kernel
 // family and emits a standalone HIP program for it.
 #include "code_generator.hpp"
+#include "device_layout.hpp"
 #include "index_compress.hpp"
 
 #include <cstdio>
@@ -205,9 +206,142 @@ void code_generator::compile() {
 }
 
 // ------------------------------------------------------------------ emission
+namespace {
+
+// the matrix-core program: the layout arrays (binary sidecars next to the plan's text
+// arrays, code_generator.cc:311-336 writes the reference's as text) uploaded as they are,
+// and the kernel launched with the template arguments and scalars gs_spmm uses
+// (kernels/{ks,mfma}_launch.hip); the check and perf_result as for the other families
+std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int repeat) {
+    std::ostringstream o;
+    const uint32_t N = L.N, CT = N / 16;
+    const char *kname = L.kind == mc_layout::KS ? "k_mfma_ks" : (L.kind == mc_layout::ROWS ? "k_mfma_rows" : "k_nm_mfma");
+    o << "// kernel_file.hip -- generated by generalsparse_amd code_generator: the matrix-core kernel " << kname << "\n"
+      << "// build: sh make_kernel.sh; run: ./a.out [matrix.mtx] [N]  -> perf_result (ms, GFLOP/s)\n"
+      << "#include \"kernel_lib.hpp\"\n#include <cstdio>\n#include <cstdlib>\n#include <cstring>\n#include <fstream>\n"
+      << "#include <string>\n#include <vector>\n\n"
+      << "typedef gsk::f16 VT;\n"
+      << "static std::vector<uint64_t> rd(const char *n) {\n"
+      << "    std::ifstream f(n); std::vector<uint64_t> v; unsigned long long x; while (f >> x) v.push_back(x); return v; }\n"
+      << "static std::vector<double> rdf(const char *n) {\n"
+      << "    std::ifstream f(n); std::vector<double> v; double x; while (f >> x) v.push_back(x); return v; }\n"
+      << "template <class T> static std::vector<T> rdb(const char *n) {  // binary sidecar\n"
+      << "    std::ifstream f(n, std::ios::binary | std::ios::ate); std::vector<T> v((size_t)f.tellg() / sizeof(T));\n"
+      << "    f.seekg(0); f.read(reinterpret_cast<char *>(v.data()), v.size() * sizeof(T)); return v; }\n"
+      << "template <class T> static T *up(const std::vector<T> &h, size_t pad = 64) {\n"
+      << "    T *p; hipMalloc(&p, (h.size() + pad) * sizeof(T)); hipMemset(p, 0, (h.size() + pad) * sizeof(T));\n"
+      << "    hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice); return p; }\n\n"
+      << "int main(int argc, char **argv) {\n"
+      << "    const uint32_t N = argc > 2 ? (uint32_t)atoi(argv[2]) : " << N << ";\n"
+      << "    if (N != " << N << ") { printf(\"this program's " << kname << " layout is built for N = " << N
+      << "\\n\"); return 2; }\n"
+      << "    const int repeat = " << repeat << ";\n"
+      << "    const uint64_t M = " << m.scalar(GLOBAL_META, "origin_row_num", -1) << ", K = "
+      << m.scalar(GLOBAL_META, "origin_col_num", -1) << ", NNZ = " << m.scalar(GLOBAL_META, "origin_nnz_num", -1) << ";\n"
+      << "    auto rows = rd(\"GLOBAL_META_nz_row_indices_0\");\n"
+      << "    auto vals = rdf(\"GLOBAL_META_nz_vals_0\");\n"
+      << "    uint64_t row_num = rows.back() + 1;\n";
+    std::string launch, setup;
+    if (L.kind == mc_layout::KS) {
+        const ks_tiles &t = L.ks;
+        const uint64_t nb = L.tbr.size() - 1, nwg = nb * t.S;
+        o << "    auto tbr = rd(\"TBLOCK_META_first_row_indices_0\");\n"
+          << "    std::vector<uint32_t> t32(tbr.begin(), tbr.end()); uint32_t *d_tbr = up(t32);\n"
+          << "    uint16_t *d_pos = up(rdb<uint16_t>(\"TBLOCK_META_mfma_ks_entry_pos_0.bin\"));\n"
+          << "    uint16_t *d_val = up(rdb<uint16_t>(\"TBLOCK_META_mfma_ks_entry_val_0.bin\"));\n"
+          << "    float *d_ws; uint32_t *d_arr; hipMalloc(&d_ws, " << nwg * 16 * t.RT * N * 4 << "ull + 16);\n"
+          << "    hipMalloc(&d_arr, " << nb * 4 << "ull + 4); hipMemset(d_arr, 0, " << nb * 4 << "ull + 4);\n";
+        const std::string k = "gsk::k_mfma_ks<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ", " +
+                              std::to_string(kKsWaves) + ", " + std::to_string(kKsDepth) + ", " + std::to_string(t.MAXG) + ">";
+        setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
+                std::to_string(t.lds_bytes) + ")";
+        launch = k + "<<<" + std::to_string(nwg) + ", " + std::to_string(64 * kKsWaves) + ", " + std::to_string(t.lds_bytes) +
+                 ">>>(d_tbr, (const gsk::u32x4 *)d_pos, (const gsk::u32x4 *)d_val, d_B, d_C, (uint32_t)K, N, " +
+                 std::to_string(t.S) + "u, " + std::to_string(t.NS) + "u, " + std::to_string(t.GCAP) + "u, " +
+                 std::to_string(nwg) + "u, 0u, d_ws, d_arr, nullptr)";
+    } else if (L.kind == mc_layout::ROWS) {
+        const mfma_tiles &t = L.rows;
+        const uint64_t nb = L.tbr.size() - 1;
+        o << "    auto tbr = rd(\"TBLOCK_META_first_row_indices_0\");\n"
+          << "    std::vector<uint32_t> t32(tbr.begin(), tbr.end()); uint32_t *d_tbr = up(t32);\n"
+          << "    uint32_t *d_seg = up(rdb<uint32_t>(\"TBLOCK_META_mfma_seg_start_0.bin\"));\n"
+          << "    uint16_t *d_pos = up(rdb<uint16_t>(\"TBLOCK_META_mfma_entry_pos_0.bin\"));\n"
+          << "    uint16_t *d_val = up(rdb<uint16_t>(\"TBLOCK_META_mfma_entry_val_0.bin\"));\n"
+          << "    float *d_ws = nullptr; uint32_t *d_arr = nullptr;\n";
+        if (L.rows_ksplit > 1)
+            o << "    hipMalloc(&d_ws, " << nb * L.rows_ksplit * t.RMAX * N * 4 << "ull); hipMalloc(&d_arr, " << nb * 4
+              << "ull); hipMemset(d_arr, 0, " << nb * 4 << "ull);\n";
+        const std::string k = "gsk::k_mfma_rows<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ", " +
+                              std::to_string(t.lgKC) + ", " + std::to_string(L.rows_maxa) + ", false, " +
+                              std::to_string(L.rows_glds) + ", " + std::to_string(L.rows_nbg) + ", " +
+                              std::to_string(L.rows_wct) + ">";
+        setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
+                std::to_string(t.lds_bytes) + ")";
+        launch = k + "<<<" + std::to_string(nb * L.rows_ksplit) + ", " + std::to_string(kMfmaThreads) + ", " +
+                 std::to_string(t.lds_bytes) + ">>>(d_tbr, d_seg, (const gsk::u32x4 *)d_pos, (const gsk::u32x4 *)d_val, d_B, d_C, " +
+                 "(uint32_t)K, N, " + std::to_string(t.nc) + "u, " + std::to_string(t.RMAX) + "u, 0u, " +
+                 std::to_string(L.rows_ksplit) + "u, " + std::to_string(L.rows_ncs) + "u, d_ws, d_arr, nullptr, 0u)";
+    } else {
+        o << "    unsigned char *d_blk = up(rdb<unsigned char>(\"THREAD_META_nm_panels_0.bin\"));\n";
+        const std::string k = "gsk::k_nm_mfma<" + std::to_string(CT) + ">";
+        const size_t lds = (size_t)2 * gsk::kNmKC * 32 * CT;
+        setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
+                std::to_string(lds) + ")";
+        launch = k + "<<<" + std::to_string((L.nm_rows + 127) / 128) + ", " + std::to_string(64 * gsk::kNmWaves) + ", " +
+                 std::to_string(lds) + ">>>(d_blk, d_B, d_C, (uint32_t)K, " + std::to_string(L.nm_S) + "u, " +
+                 std::to_string(L.nm_rows) + "u, 0u, 0u)";
+    }
+    o << "    std::vector<VT> hB(K * N, (VT)1.0f);  // x_arr = 1 (code_generator.cc:464-467)\n"
+      << "    VT *d_B = up(hB, 0); VT *d_C; hipMalloc(&d_C, M * N * sizeof(VT)); hipMemset(d_C, 0, M * N * sizeof(VT));\n"
+      << "    " << setup << ";\n"
+      << "    auto run = [&]() { " << launch << "; };\n"
+      << "    run(); if (hipDeviceSynchronize() != hipSuccess) { printf(\"launch failed\\n\"); return 3; }\n"
+      << "    // check (kernel_lib.hpp:884-921 of the reference): all-ones B, C[i][j] = sum of row i's values\n"
+      << "    std::vector<VT> hC(M * N); hipMemcpy(hC.data(), d_C, M * N * sizeof(VT), hipMemcpyDeviceToHost);\n"
+      << "    std::vector<double> ref(M, 0.0);\n"
+      << "    for (size_t i = 0; i < rows.size(); i++) ref[rows[i]] += vals[i];\n"
+      << "    long wrong = 0;\n"
+      << "    for (uint64_t i = 0; i < M; i++) for (uint32_t j = 0; j < N; j++) {\n"
+      << "        double c = (double)(float)hC[i * N + j], r = (double)(float)(VT)(float)ref[i];\n"
+      << "        const double tol = 1e-1 * (1 + (r < 0 ? -r : r));  // north_star fp16\n"
+      << "        if (c - r > tol || r - c > tol) {\n"
+      << "            if (wrong < 10) printf(\"Wrong result: i = %llu, j = %u, result = %f, reference = %f.\\n\", (unsigned long long)i, j, c, r);\n"
+      << "            wrong++; } }\n"
+      << "    printf(\"wrong number:%ld\\n\", wrong); if (!wrong) printf(\"correct\\n\");\n"
+      << "    hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);\n"
+      << "    for (int i = 0; i < 20; i++) run();  // warm-up\n"
+      << "    hipEventRecord(e0, 0); for (int i = 0; i < repeat; i++) run(); hipEventRecord(e1, 0); hipEventSynchronize(e1);\n"
+      << "    float ms = 0; hipEventElapsedTime(&ms, e0, e1);\n"
+      << "    double gflops = " << get_config().FLOAT_RATE << ".0 * (double)NNZ * N * repeat / (ms * 1e-3) / 1e9;\n"
+      << "    FILE *pr = fopen(\"perf_result\", \"w\"); fprintf(pr, \"%f\\n%f\\n\", ms, gflops); fclose(pr);  // code_generator.cc:643-648\n"
+      << "    printf(\"time %f ms for %d launches, %f GFLOP/s\\n\", ms, repeat, gflops);\n"
+      << "    return wrong ? 1 : 0;\n}\n";
+    return o.str();
+}
+
+template <class T>
+void write_bin(const std::string &path, const std::vector<T> &v) {
+    std::ofstream f(path, std::ios::binary);
+    f.write(reinterpret_cast<const char *>(v.data()), (std::streamsize)(v.size() * sizeof(T)));
+    GS_CHECK(f.good(), "cannot write " + path);
+}
+
+mc_layout emitted_layout(const meta_data_set &m, const kernel_spec &spec, int sub) {
+    if (!get_config().HALF) return mc_layout();
+    return choose_matrix_core_layout(m, spec, sub, m.scalar(GLOBAL_META, "origin_col_num", -1), 1);
+}
+
+}  // namespace
+
 std::string code_generator::generate_kernel_file_source(int repeat) const {
     GS_CHECK(compiled, "compile() before emitting the program");
     GS_CHECK(sub == 0, "the standalone program is emitted for an undivided matrix");
+    const mc_layout L = emitted_layout(*meta, spec, sub);
+    if (L.kind != mc_layout::NONE) return matrix_core_source(*meta, L, repeat);
+    return generate_gather_source(repeat);
+}
+
+std::string code_generator::generate_gather_source(int repeat) const {
     const bool half = get_config().HALF;
     // model-driven index compression (code_generator.cc:2618-3063): with
     // MODEL_DRIVEN_COMPRESS, integer plan arrays whose formula reproduces them exactly are
@@ -395,11 +529,23 @@ std::string code_generator::generate_kernel_file_source(int repeat) const {
 
 uint64_t code_generator::generate_final_program(int repeat, const std::string &root, std::string *dir_out) {
     GS_CHECK(compiled, "compile() before generate_final_program");
+    GS_CHECK(sub == 0, "the standalone program is emitted for an undivided matrix");
     std::string dir;
     uint64_t id = meta->output_format_to_dir(root, spec.arrays, &dir);
+    const mc_layout L = emitted_layout(*meta, spec, sub);
+    if (L.kind == mc_layout::KS) {
+        write_bin(dir + "/TBLOCK_META_mfma_ks_entry_pos_0.bin", L.ks.pos);
+        write_bin(dir + "/TBLOCK_META_mfma_ks_entry_val_0.bin", L.ks.val);
+    } else if (L.kind == mc_layout::ROWS) {
+        write_bin(dir + "/TBLOCK_META_mfma_seg_start_0.bin", L.rows.seg_start);
+        write_bin(dir + "/TBLOCK_META_mfma_entry_pos_0.bin", L.rows.pos);
+        write_bin(dir + "/TBLOCK_META_mfma_entry_val_0.bin", L.rows.val);
+    } else if (L.kind == mc_layout::NM) {
+        write_bin(dir + "/THREAD_META_nm_panels_0.bin", L.nm_blk);
+    }
     {
         std::ofstream f(dir + "/kernel_file.hip");
-        f << generate_kernel_file_source(repeat);
+        f << (L.kind != mc_layout::NONE ? matrix_core_source(*meta, L, repeat) : generate_gather_source(repeat));
     }
     // copy the device headers next to the program (code_generator.cc:686-694); they ship
     // next to the library: <pkg>/csrc/hip_code/{kernel_lib,idx_formula}.hpp
@@ -410,7 +556,7 @@ uint64_t code_generator::generate_final_program(int repeat, const std::string &r
         hdr_dir = so.substr(0, so.find_last_of('/') + 1) + "csrc/hip_code/";
     }
     if (!hdr_dir.empty())
-        for (const char *h : {"kernel_lib.hpp", "idx_formula.hpp"}) {
+        for (const char *h : {"kernel_lib.hpp", "idx_formula.hpp", "kernel_consts.hpp"}) {
             std::ifstream in(hdr_dir + h, std::ios::binary);
             std::ofstream out(dir + "/" + h, std::ios::binary);
             out << in.rdbuf();

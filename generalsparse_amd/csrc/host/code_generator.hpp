@@ -100,13 +100,16 @@ class code_generator {
     void restore_compiled(const kernel_spec &s) { spec = s; compiled = true; }
     const kernel_spec &get_kernel_spec() const { return spec; }
 
-    // HIP source of the generated program (kernel + main with perf_result)
+    // HIP source of the generated program (kernel + main with perf_result).  fp16 plans whose
+    // device kernel is a matrix-core one (device_layout.hpp) launch that kernel on the layout
+    // arrays generate_final_program writes next to the plan arrays
     std::string generate_kernel_file_source(int repeat) const;
     // writes ROOT/data_source/<id>/{plan arrays, kernel_file.hip, make_kernel.sh}
     // (code_generator.hpp:271-280); returns the id, optionally the directory
     uint64_t generate_final_program(int repeat, const std::string &root, std::string *dir_out = nullptr);
 
   private:
+    std::string generate_gather_source(int repeat) const;  // the CUDA-core families' program
     std::shared_ptr<meta_data_set> meta;
     int sub;
     std::set<POS_TYPE> opened;

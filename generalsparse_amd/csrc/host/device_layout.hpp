@@ -1,0 +1,84 @@
+// host/device_layout.hpp -- the HBM layouts of the matrix-core kernels (k_mfma_rows,
+// k_mfma_ks, k_nm_mfma), built on the host from a compiled plan.  Shared by the device
+// upload (kernels/device_plan.hip) and the code generator (code_generator.cc), so the
+// program generate_final_program emits launches exactly the layout gs_spmm runs.
+#pragma once
+
+#include "gs_core.hpp"
+#include "code_generator.hpp"
+#include "../hip_code/kernel_consts.hpp"
+
+#include <string>
+#include <vector>
+
+namespace gs {
+
+constexpr uint32_t kMfmaThreads = 64 * gsk::kMfmaWaves;
+constexpr uint32_t kKsWaves = 8, kKsDepth = 4;  // k_mfma_ks workgroup waves, entry sets in flight
+
+// fp32 -> fp16 bits, round to nearest even (bit-identical to the device conversion)
+uint16_t f32_to_f16_bits(float f);
+
+struct canon_rows {
+    std::vector<uint32_t> rp;
+    std::vector<uint64_t> col;
+    std::vector<float> val;
+};
+
+canon_rows canonical_rows(const std::vector<uint32_t> &rp, const std::vector<uint64_t> &col, const universal_array &vals);
+
+// k_mfma_rows upload layout (kernel_lib.hpp): per (BMTB g, 2^lgKC-column chunk j), the
+// chunk's entries in groups of 8 = [8 x u16 halfword position in the dense image] +
+// [8 x f16]; seg_start[g*nc + j] the first group
+struct mfma_tiles {
+    uint32_t lgKC = 0, nc = 0, RT = 0, RMAX = 0, MAXA = 0, gmax = 0;
+    size_t lds_bytes = 0;
+    std::vector<uint32_t> seg_start;  // in groups
+    std::vector<uint16_t> pos, val;   // 8 u16 per group each, + one spare group
+};
+
+size_t mfma_lds_bytes(uint32_t lgKC, uint32_t CT, uint32_t RMAX);
+// LDS one k_mfma_rows variant needs (B ring + dense images, or the compute waves' partial tiles)
+size_t mfma_rows_lds_need(uint32_t lgKC, uint32_t CT, uint32_t RT, uint32_t RMAX, int glds, int nbg, int wct);
+bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
+                      const std::vector<uint64_t> &col, const std::vector<float> &vals, uint64_t K, uint32_t N,
+                      size_t lds_budget, int64_t max_fill, mfma_tiles &t, std::string &why);
+
+// k_mfma_ks upload layout: GCAP groups per (BMTB g, K range q, 32-column k-step s) at
+// group ((g*S + q)*NS + s)*GCAP, + one spare group
+struct ks_tiles {
+    uint32_t S = 0, NS = 0, RT = 0, RMAX = 0, MAXG = 0, GCAP = 0, W = 0;
+    size_t lds_bytes = 0;
+    std::vector<uint16_t> pos, val;  // 8 u16 per group each
+};
+
+bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
+                    const std::vector<uint64_t> &col, const std::vector<float> &vals, uint64_t K, uint32_t N,
+                    int64_t s_cfg, int64_t min_rows, int64_t max_fill, ks_tiles &t, std::string &why);
+
+// k_nm_mfma upload layout: one 4,608-B block per (64-row group, 64-column k-step)
+bool build_nm_panels(const std::vector<uint64_t> &rows, const std::vector<uint64_t> &col, const universal_array &vals,
+                     uint64_t row_num, uint64_t K, std::vector<unsigned char> &blk, uint32_t &S, std::string &why);
+
+// The matrix-core layout gs_spmm runs for a compiled plan at its dense width
+// (DENSE_MATRIX_SIZE), chosen and built once here for both the device upload and the
+// emitted program: k_nm_mfma for col-direction 2:4 panels, k_mfma_ks for row blocks of
+// >= KS_MIN_ROWS rows, k_mfma_rows for the other fp16 BMTB plans; NONE = a gather family.
+// The k_mfma_rows variant (B by LDS-DMA or registers, ring depth, compute waves) is fixed
+// here from the config, so the LDS size and the launch agree whatever changes later.
+struct mc_layout {
+    enum kind_t { NONE, ROWS, KS, NM } kind = NONE;
+    uint32_t N = 0;
+    std::vector<uint64_t> tbr;  // BMTB first rows (ROWS, KS)
+    mfma_tiles rows;
+    uint32_t rows_ksplit = 1, rows_ncs = 0;  // k_mfma_rows K ranges per row block, chunks per range
+    int rows_glds = 2, rows_nbg = 3, rows_wct = 6, rows_maxa = 1;  // k_mfma_rows template arguments
+    ks_tiles ks;
+    std::vector<unsigned char> nm_blk;  // k_nm_mfma blocks
+    uint32_t nm_S = 0;                  // ... k-steps per row group
+    uint64_t nm_rows = 0;
+    std::string why;  // why NONE
+};
+mc_layout choose_matrix_core_layout(const meta_data_set &m, const kernel_spec &sp, int sb, uint64_t K, int dtype);
+
+}  // namespace gs

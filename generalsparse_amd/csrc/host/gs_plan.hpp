@@ -2,6 +2,7 @@
 #pragma once
 
 #include "operator.hpp"
+#include "device_layout.hpp"
 #include "../hip_code/idx_formula.hpp"
 
 #include <hip/hip_runtime.h>
@@ -45,7 +46,10 @@ struct device_plan {
     bool ks = false;    // k_mfma_ks: K split over ksplit workgroups per row block, B slice in LDS
                         // (t0 BMTB rows, tcol/tval groups; ks_ns k-steps per range,
                         // RT in maxr, MAXG in seg_cap, ws slabs + t2 arrivals when ksplit > 1)
-    uint32_t ks_ns = 0, ks_gcap = 0;  // k_mfma_ks: k-steps per K range, entry groups per step
+    uint32_t ks_ns = 0, ks_gcap = 0;
+    // k_mfma_rows variant fixed at upload (device_layout.cc): GLDS / B ring depth / compute
+    // waves / entry groups per thread -- the launch uses these, not the config of the moment
+    int mfma_glds = 2, mfma_nbg = 3, mfma_wct = 6, mfma_maxa = 1;  // k_mfma_ks: k-steps per K range, entry groups per step
     std::string kernel;  // the device kernel gs_spmm launches at the plan's N (empty: the family's)
     uint32_t ksplit = 1, ncs = 0;  // k_mfma_rows workgroups per row block, chunks per workgroup
     uint32_t ws_n = 0;             // bitmap family: dense width of the fp32 workspace
@@ -115,7 +119,6 @@ void launch_nm(const plan_state &p, const device_arrays &a, const void *B, void 
 // gather_launch.hip: the CUDA-core gather families and k_lds_rows
 void launch_gather(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s);
 // ks_launch.hip: k_mfma_ks (K-split, wave-autonomous matrix-core row blocks)
-constexpr uint32_t kKsWaves = 8, kKsDepth = 4;
 void launch_ks(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s);
 void debug_ks_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
                        size_t n_host);

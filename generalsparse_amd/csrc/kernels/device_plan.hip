@@ -3,6 +3,7 @@
 #include "../hip_code/kernel_lib.hpp"
 #include "../host/gs_plan.hpp"
 #include "../host/index_compress.hpp"
+#include "../host/device_layout.hpp"
 
 #include <algorithm>
 #include <cstdlib>
@@ -92,59 +93,6 @@ uint32_t pow2ceil_u(uint32_t x) {
     while (p < x) p <<= 1;
     return p;
 }
-
-uint16_t f32_to_f16_bits(float f) {
-    _Float16 h = (_Float16)f;
-    uint16_t b;
-    std::memcpy(&b, &h, 2);
-    return b;
-}
-
-// Rows as the matrix-core layouts need them: each row's columns ascending and
-// distinct.  The reference accepts any column order inside a row and its gather
-// kernels add repeated coordinates, so entries are stably sorted by column and
-// repeated ones summed (in double, rounded to fp32 once).  rp is the CSR row
-// pointer of the plan's (row-sorted) COO.
-struct canon_rows {
-    std::vector<uint32_t> rp;
-    std::vector<uint64_t> col;
-    std::vector<float> val;
-};
-
-canon_rows canonical_rows(const std::vector<uint32_t> &rp, const std::vector<uint64_t> &col, const universal_array &vals) {
-    canon_rows c;
-    const uint64_t nr = rp.size() - 1;
-    c.rp.assign(nr + 1, 0);
-    c.col.reserve(col.size());
-    c.val.reserve(col.size());
-    std::vector<std::pair<uint64_t, uint64_t>> ent;  // (col, position)
-    for (uint64_t r = 0; r < nr; r++) {
-        bool ordered = true;
-        for (uint64_t e = rp[r] + 1; e < rp[r + 1]; e++) ordered &= col[e] > col[e - 1];
-        if (ordered) {
-            for (uint64_t e = rp[r]; e < rp[r + 1]; e++) {
-                c.col.push_back(col[e]);
-                c.val.push_back((float)vals.read_float_from_arr(e));
-            }
-        } else {
-            ent.clear();
-            for (uint64_t e = rp[r]; e < rp[r + 1]; e++) ent.push_back({col[e], e});
-            std::stable_sort(ent.begin(), ent.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
-            for (size_t i = 0; i < ent.size();) {
-                double sum = 0;
-                size_t j = i;
-                for (; j < ent.size() && ent[j].first == ent[i].first; j++) sum += vals.read_float_from_arr(ent[j].second);
-                c.col.push_back(ent[i].first);
-                c.val.push_back((float)sum);
-                i = j;
-            }
-        }
-        GS_CHECK(c.col.size() < 0xffffffffull, "nnz exceeds 32-bit offsets");
-        c.rp[r + 1] = (uint32_t)c.col.size();
-    }
-    return c;
-}
-
 
 // ------------------------------------------------------------------ LDS tiles
 // Chunk-major A layout for k_lds_rows (kernel_lib.hpp): for BMTB g and column
@@ -259,325 +207,6 @@ bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uin
     return true;
 }
 
-// ------------------------------------------------------------------ MFMA tiles
-// Upload layout of k_mfma_rows (kernel_lib.hpp): for BMTB g and column chunk j,
-// the entries of g's rows with columns in [j*KC, (j+1)*KC), in groups of 8:
-// pos[] = 8 x u16 halfword index in the dense image (local_row*(KC+16) +
-// local_col), val[] = 8 x f16; the last group is padded with (row R, value 0),
-// row R being the kernel's zero row.
-struct mfma_tiles {
-    uint32_t lgKC = 0, nc = 0, RT = 0, RMAX = 0, MAXA = 0, gmax = 0;
-    size_t lds_bytes = 0;
-    std::vector<uint32_t> seg_start;  // in groups
-    std::vector<uint16_t> pos, val;   // 8 u16 per group each, + one spare group
-};
-
-constexpr uint32_t kMfmaThreads = 64 * gsk::kMfmaWaves;
-
-constexpr uint32_t kMfmaBThreads = 64 * gsk::kMfmaBWaves, kMfmaAThreads = 64 * gsk::kMfmaAWaves;
-
-size_t mfma_lds_bytes(uint32_t lgKC, uint32_t CT, uint32_t RMAX) {
-    const size_t KC = 1ull << lgKC;
-    // the larger of the two layouts (2 B buffers + 3 dense images; MFMA_GLDS: MFMA_GLDS_NBUF + 2)
-    const size_t nb = (size_t)std::max<int64_t>(3, get_config().MFMA_GLDS_NBUF);
-    const size_t szB = KC * 32 * CT, szD = (RMAX + 1) * (2 * KC + 32);
-    return std::max(2 * szB + 3 * szD, nb * szB + 2 * szD) + 1024;  // + stamp slots and the arrival flag
-}
-
-// Order one segment's entries for the scatter: the kernel's 32-lane half-waves
-// write (group q, slot e) for 32 consecutive groups at once, so every such
-// "round" takes entries of distinct LDS write banks ((halfword/2) mod 32) where
-// possible (greedy: fullest banks first, a bank twice only when fewer than 32
-// banks remain).  Appends 8 u16 pos + 8 u16 values per group; padding slots write
-// 0 into the zero row (pad_h = its first halfword), on banks of their own.
-void bank_order_segment(const std::vector<uint16_t> &pos, const std::vector<uint16_t> &val, uint32_t pad_h,
-                        std::vector<uint16_t> &out_pos, std::vector<uint16_t> &out_val, uint32_t pad_slots = 32) {
-    const size_t n = pos.size();
-    const size_t ng = (n + 7) / 8;
-    std::vector<std::vector<uint32_t>> bucket(32);
-    for (uint32_t i = 0; i < n; i++) bucket[(pos[i] >> 1) & 31].push_back(i);
-    const size_t base = out_pos.size();
-    out_pos.resize(base + ng * 8);
-    out_val.resize(base + ng * 8);
-    std::vector<int> order(32);
-    for (size_t b0 = 0; b0 < ng; b0 += 32) {
-        const size_t gl = std::min<size_t>(32, ng - b0);
-        for (int e = 0; e < 8; e++) {
-            for (int k = 0; k < 32; k++) order[k] = k;
-            std::stable_sort(order.begin(), order.end(),
-                             [&](int a, int b) { return bucket[a].size() > bucket[b].size(); });
-            size_t l = 0;
-            bool progress = true;
-            while (l < gl && progress) {  // one entry per bank per pass, fullest banks first
-                progress = false;
-                for (int k = 0; k < 32 && l < gl; k++) {
-                    auto &bk = bucket[order[k]];
-                    if (bk.empty()) continue;
-                    const uint32_t i = bk.back();
-                    bk.pop_back();
-                    const size_t slot = base + (b0 + l) * 8 + e;
-                    out_pos[slot] = pos[i];
-                    out_val[slot] = val[i];
-                    l++;
-                    progress = true;
-                }
-            }
-            for (; l < gl; l++) {  // padding: value 0 into the zero row, one bank each
-                const size_t slot = base + (b0 + l) * 8 + e;
-                out_pos[slot] = (uint16_t)(pad_h + 2 * (l % pad_slots));  // inside the zero row
-                out_val[slot] = 0;
-            }
-        }
-    }
-    for (const auto &bk : bucket) GS_CHECK(bk.empty(), "bank ordering lost an entry");
-}
-
-bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
-                      const std::vector<uint64_t> &col, const std::vector<float> &vals, uint64_t K, uint32_t N,
-                      size_t lds_budget, int64_t max_fill, mfma_tiles &t, std::string &why) {
-    const uint64_t nb = tb_rows.size() - 1;
-    if (nb == 0 || K == 0) { why = "empty plan"; return false; }
-    if (N != 16 && N != 32 && N != 64) { why = "N must be 16, 32 or 64"; return false; }
-    const uint32_t CT = N / 16;
-    uint64_t rmax = 0, nnz = 0;
-    for (uint64_t g = 0; g < nb; g++) rmax = std::max<uint64_t>(rmax, tb_rows[g + 1] - tb_rows[g]);
-    for (uint64_t g = 0; g < nb; g++) nnz += row_ptr[tb_rows[g + 1]] - row_ptr[tb_rows[g]];
-    if (rmax == 0 || rmax > 64) { why = "BMTBs of 1..64 rows only"; return false; }
-    const uint32_t RT = (uint32_t)((rmax + 15) / 16);
-    if (nnz == 0 || (double)nb * 16 * RT * K > (double)max_fill * nnz) {
-        why = "row blocks too sparse for dense tiles";
-        return false;
-    }
-    // every workgroup streams all of B through LDS: with short row blocks that
-    // traffic outgrows A's (R = 4 on C2: 13x) and the gather kernels win
-    if ((double)nb * K * N * 2 > 6.0 * 4.0 * nnz && max_fill < (1 << 20)) {
-        why = "row blocks too short: B traffic per row block exceeds A's";
-        return false;
-    }
-    for (uint32_t lg = 10; lg >= 8; lg--) {
-        const uint64_t KC = 1ull << lg;
-        if ((rmax + 1) * (KC + 16) > 65536 || mfma_lds_bytes(lg, CT, (uint32_t)rmax) > lds_budget) continue;
-        const uint64_t nc = (K + KC - 1) / KC;
-        uint64_t gmax = 0;
-        std::vector<uint64_t> cnt(nc);
-        for (uint64_t g = 0; g < nb; g++) {
-            std::fill(cnt.begin(), cnt.end(), 0);
-            for (uint64_t e = row_ptr[tb_rows[g]]; e < row_ptr[tb_rows[g + 1]]; e++) cnt[col[e] >> lg]++;
-            for (uint64_t j = 0; j < nc; j++) gmax = std::max(gmax, (cnt[j] + 7) / 8);
-        }
-        if (gmax > 2ull * kMfmaAThreads || nc > 63) continue;
-        if (((KC * 32 * CT) / 16) % kMfmaBThreads) continue;  // whole B units per B thread
-        if ((KC * 32 * CT) / 16 / kMfmaBThreads > 8) continue;  // register budget of the B sets
-        // the compute waves' partial tiles must fit LDS for the final reduction
-        if ((size_t)gsk::kMfmaCompute * RT * CT * 1024 > mfma_lds_bytes(lg, CT, (uint32_t)rmax)) continue;
-        t.lgKC = lg; t.nc = (uint32_t)nc; t.RT = RT; t.RMAX = (uint32_t)rmax;
-        t.MAXA = gmax <= kMfmaAThreads ? 1 : 2;
-        t.gmax = (uint32_t)gmax;
-        t.lds_bytes = mfma_lds_bytes(lg, CT, (uint32_t)rmax);
-        break;
-    }
-    if (!t.lgKC) { why = "no chunk width fits LDS and the stage buffers"; return false; }
-    const uint32_t KC = 1u << t.lgKC;
-    t.seg_start.assign(1, 0);
-    std::vector<uint64_t> cur;
-    std::vector<uint16_t> pos, hv;
-    for (uint64_t g = 0; g < nb; g++) {
-        const uint64_t r0 = tb_rows[g], R = tb_rows[g + 1] - r0;
-        cur.assign(R, 0);
-        for (uint64_t i = 0; i < R; i++) cur[i] = row_ptr[r0 + i];
-        for (uint32_t j = 0; j < t.nc; j++) {
-            const uint64_t lim = (uint64_t)(j + 1) * KC;
-            pos.clear();
-            hv.clear();
-            for (uint64_t i = 0; i < R; i++) {
-                uint64_t e = cur[i];
-                for (; e < row_ptr[r0 + i + 1] && col[e] < lim; e++) {
-                    // halfword index in the dense image (row stride RS = 2*KC + 32 bytes)
-                    pos.push_back((uint16_t)(i * (KC + 16) + (col[e] - (uint64_t)j * KC)));
-                    hv.push_back(f32_to_f16_bits(vals[e]));
-                }
-                cur[i] = e;
-            }
-            bank_order_segment(pos, hv, (uint32_t)(R * (KC + 16)), t.pos, t.val);
-            t.seg_start.push_back((uint32_t)(t.pos.size() / 8));
-        }
-    }
-    t.pos.insert(t.pos.end(), 8, 0);  // spare group: idle lanes' branch-free loads
-    t.val.insert(t.val.end(), 8, 0);
-    return true;
-}
-
-// ------------------------------------------------------------------ k_mfma_ks layout
-// Upload layout of k_mfma_ks (kernel_lib.hpp): the K range is split into S ranges of
-// KR = 32*NS columns; for every (BMTB g, range q, 32-column k-step s) -- unit u = g*S + q --
-// the entries of g's rows in the step's columns, in groups of 8: pos = halfword index in a
-// wave image of 96-B rows (local_row*48 + column - step base), val = f16.  Every step holds
-// exactly GCAP groups (the plan's largest step; the rest padding that writes 0 into the
-// image's zero row 16*RT), at group (u*NS + s)*GCAP, so the kernel computes every address
-// without loading offsets first.  One spare group follows.  The entry order inside a step
-// is bank-ordered for the scatter.
-struct ks_tiles {
-    uint32_t S = 0, NS = 0, RT = 0, RMAX = 0, MAXG = 0, GCAP = 0, W = 0;
-    size_t lds_bytes = 0;
-    std::vector<uint16_t> pos, val;  // 8 u16 per group each
-};
-
-using gsk::ks_lds_bytes;
-
-bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
-                    const std::vector<uint64_t> &col, const std::vector<float> &vals, uint64_t K, uint32_t N,
-                    int64_t s_cfg, int64_t min_rows, int64_t max_fill, ks_tiles &t, std::string &why) {
-    const uint64_t nb = tb_rows.size() - 1;
-    if (nb == 0 || K == 0) { why = "empty plan"; return false; }
-    if (N != 16 && N != 32 && N != 64) { why = "N must be 16, 32 or 64"; return false; }
-    const uint32_t CT = N / 16, W = kKsWaves;  // gs_plan.hpp
-    uint64_t rmax = 0;
-    for (uint64_t g = 0; g < nb; g++) rmax = std::max<uint64_t>(rmax, tb_rows[g + 1] - tb_rows[g]);
-    if (rmax < (uint64_t)std::max<int64_t>(1, min_rows) || rmax > 80) { why = "row blocks outside the k_mfma_ks range"; return false; }
-    const uint32_t RT = std::max<uint32_t>(2, (uint32_t)((rmax + 15) / 16));  // kernels built for RT 2..5
-    const uint64_t nnz = row_ptr[tb_rows[nb]] - row_ptr[tb_rows[0]];
-    if (nnz == 0 || (double)nb * 16 * RT * K > (double)max_fill * nnz) {  // as build_mfma_tiles
-        why = "row blocks too sparse for dense tiles";
-        return false;
-    }
-    // K ranges: enough workgroups for the 256 CUs (each reads only its range's B rows)
-    t.lds_bytes = ks_lds_bytes(CT, RT, W);
-    if (t.lds_bytes > 160 * 1024) { why = "k_mfma_ks wave stages exceed LDS"; return false; }
-    uint64_t S = s_cfg > 0 ? (uint64_t)s_cfg : std::min<uint64_t>(8, (256 + nb - 1) / nb);
-    S = std::max<uint64_t>(1, std::min<uint64_t>(S, (K + 31) / 32));
-    uint64_t KR = ((K + S - 1) / S + 31) / 32 * 32;
-    S = (K + KR - 1) / KR;
-    t.S = (uint32_t)S;
-    t.NS = (uint32_t)(KR / 32);
-    t.RT = RT;
-    t.RMAX = (uint32_t)rmax;
-    t.W = W;
-    // pass 1: the largest step (entries of a row block in 32 columns)
-    uint64_t gmax = 1;
-    {
-        std::vector<uint32_t> cnt((size_t)S * t.NS);
-        for (uint64_t g = 0; g < nb; g++) {
-            std::fill(cnt.begin(), cnt.end(), 0u);
-            for (uint64_t e = row_ptr[tb_rows[g]]; e < row_ptr[tb_rows[g + 1]]; e++) cnt[col[e] / 32]++;
-            for (uint32_t c : cnt) gmax = std::max<uint64_t>(gmax, (c + 7) / 8);
-        }
-    }
-    t.GCAP = (uint32_t)gmax;
-    t.MAXG = gmax <= 64 ? 1 : (gmax <= 128 ? 2 : (gmax <= 256 ? 4 : 0));
-    if (!t.MAXG) { why = "a k-step holds more than 256 entry groups"; return false; }
-    GS_CHECK((double)nb * S * t.NS * t.GCAP < 4.0e9, "k_mfma_ks layout exceeds 32-bit group indices");
-    const uint32_t RS = gsk::kKsStride / 2;  // halfwords per image row
-    const uint32_t pad_h = 16 * RT * RS;      // the zero row
-    t.pos.reserve((size_t)nb * S * t.NS * t.GCAP * 8 + 8);
-    t.val.reserve(t.pos.capacity());
-    std::vector<uint64_t> cur;
-    std::vector<uint16_t> pos, hv;
-    for (uint64_t g = 0; g < nb; g++) {
-        const uint64_t r0 = tb_rows[g], R = tb_rows[g + 1] - r0;
-        cur.assign(R, 0);
-        for (uint64_t i = 0; i < R; i++) cur[i] = row_ptr[r0 + i];
-        for (uint64_t q = 0; q < S; q++)
-            for (uint32_t s = 0; s < t.NS; s++) {
-                const uint64_t base = q * KR + 32ull * s, lim = base + 32;
-                pos.clear();
-                hv.clear();
-                for (uint64_t i = 0; i < R; i++) {
-                    uint64_t e = cur[i];
-                    for (; e < row_ptr[r0 + i + 1] && col[e] < lim; e++) {
-                        pos.push_back((uint16_t)(i * RS + (col[e] - base)));
-                        hv.push_back(f32_to_f16_bits(vals[e]));
-                    }
-                    cur[i] = e;
-                }
-                const size_t before = t.pos.size();
-                bank_order_segment(pos, hv, pad_h, t.pos, t.val, RS / 2);  // pads stay inside the zero row
-                for (size_t x = t.pos.size(); x < before + (size_t)t.GCAP * 8; x++) {  // up to GCAP groups
-                    t.pos.push_back((uint16_t)(pad_h + 2 * ((x / 8) % (RS / 2))));
-                    t.val.push_back(0);
-                }
-                GS_CHECK(t.pos.size() == before + (size_t)t.GCAP * 8, "k_mfma_ks step exceeds its capacity");
-            }
-    }
-    t.pos.insert(t.pos.end(), 8, (uint16_t)pad_h);  // spare group: loads past a wave's last step
-    t.val.insert(t.val.end(), 8, 0);
-    return true;
-}
-
-// ------------------------------------------------------------------ 2:4 panels
-// Block layout of k_nm_mfma (kernel_lib.hpp) from the plan's COO: every row is
-// cut into 64-column k-steps (the col-direction BMTs of a 2:4 row: 32 entries
-// each), every aligned group of four columns keeps its (at most two) entries as
-// two values + two 2-bit positions.  Duplicate coordinates (col padding of the
-// plan, value 0) are summed.  Returns false (and why) when a group holds more
-// than two distinct columns or the panels would store over twice the entries
-// (beyond 4M value slots).
-bool build_nm_panels(const std::vector<uint64_t> &rows, const std::vector<uint64_t> &col, const universal_array &vals,
-                     uint64_t row_num, uint64_t K, std::vector<unsigned char> &blk, uint32_t &S, std::string &why) {
-    const uint64_t nnz = col.size();
-    if (row_num == 0 || K == 0 || nnz == 0) { why = "empty sub-matrix"; return false; }
-    const uint64_t S64 = (K + gsk::kNmKC - 1) / gsk::kNmKC * 4;  // k-steps, whole 256-column chunks
-    const uint64_t ng = (row_num + 127) / 128 * 2;               // 64-row groups, two per workgroup
-    const double slots = (double)ng * 64.0 * (double)S64 * 32.0;
-    if (slots > 2.0 * (double)nnz && slots > (double)(1 << 22)) {  // small plans always qualify
-        why = "2:4 panels would store over twice the entries";
-        return false;
-    }
-    if (S64 > 0xffffffffull || ng * S64 * gsk::kNmBlockBytes > (1ull << 40)) { why = "too large"; return false; }
-    std::vector<uint64_t> rp(row_num + 1, 0);
-    for (uint64_t r : rows) {
-        if (r >= row_num) { why = "row index beyond row count"; return false; }
-        rp[r + 1]++;
-    }
-    for (uint64_t i = 0; i < row_num; i++) rp[i + 1] += rp[i];
-    std::vector<uint64_t> cur(rp.begin(), rp.end() - 1), ord(nnz);
-    for (uint64_t e = 0; e < nnz; e++) ord[cur[rows[e]]++] = e;
-    blk.assign(ng * S64 * gsk::kNmBlockBytes, 0);
-    for (uint64_t b = 0; b < ng * S64; b++) {  // default positions (0, 1) in every group
-        uint16_t *ix = reinterpret_cast<uint16_t *>(blk.data() + b * gsk::kNmBlockBytes);
-        for (int i = 0; i < 256; i++) ix[i] = 0x4444;
-    }
-    const uint64_t Kp = S64 * 64;
-    std::vector<float> dv(Kp, 0.f);
-    std::vector<uint8_t> has(Kp, 0);
-    for (uint64_t r = 0; r < row_num; r++) {
-        if (rp[r] == rp[r + 1]) continue;
-        for (uint64_t e = rp[r]; e < rp[r + 1]; e++) {
-            const uint64_t c = col[ord[e]];
-            if (c >= K) { why = "column index beyond column count"; return false; }
-            has[c] = 1;
-            dv[c] += (float)vals.read_float_from_arr(ord[e]);
-        }
-        const uint64_t rg = r / 64, rt = (r % 64) / 16, rr = r % 16;
-        for (uint64_t gi = 0; gi < Kp / 4; gi++) {
-            int pos[2], n = 0;
-            for (int p = 0; p < 4; p++)
-                if (has[4 * gi + p]) {
-                    if (n == 2) {
-                        why = "a row holds more than two entries in an aligned group of four columns (not 2:4)";
-                        return false;
-                    }
-                    pos[n++] = p;
-                }
-            if (n == 0) continue;
-            if (n == 1) pos[1] = pos[0] == 3 ? 2 : 3;  // zero partner at another position
-            const int lo = std::min(pos[0], pos[1]), hi = std::max(pos[0], pos[1]);
-            const uint64_t s = gi / 16, j = gi % 16, g = j / 4, sg = j % 4, lane = g * 16 + rr;
-            unsigned char *b = blk.data() + (rg * S64 + s) * gsk::kNmBlockBytes;
-            uint16_t *v = reinterpret_cast<uint16_t *>(b + 512 + rt * 1024 + lane * 16) + sg * 2;
-            v[0] = has[4 * gi + lo] ? f32_to_f16_bits(dv[4 * gi + lo]) : 0;
-            v[1] = has[4 * gi + hi] ? f32_to_f16_bits(dv[4 * gi + hi]) : 0;
-            uint16_t *ix = reinterpret_cast<uint16_t *>(b + lane * 8) + rt;
-            *ix = (uint16_t)((*ix & ~(0xfu << (4 * sg))) | ((unsigned)(lo | (hi << 2)) << (4 * sg)));
-        }
-        for (uint64_t e = rp[r]; e < rp[r + 1]; e++) {
-            has[col[ord[e]]] = 0;
-            dv[col[ord[e]]] = 0.f;
-        }
-    }
-    S = (uint32_t)S64;
-    return true;
-}
-
 }  // namespace
 
 // the plan's column indices (u16 when they fit, else u32) and values (plan dtype) of
@@ -640,26 +269,21 @@ void upload_plan(plan_state &p, int dtype, int device) {
     GS_CHECK(nnz < 0xffffffffull - kPad, "nnz exceeds 32-bit offsets");
     d.nnz_stored = nnz;
     device_arrays a;
-    const int64_t plan_n = get_config().DENSE_MATRIX_SIZE;
-    if (sp.family == KF_ROW_CHUNKS && !sp.interleaved && dtype == 1 && get_config().NM_MFMA &&
-        (plan_n == 32 || plan_n == 64 || plan_n == 128)) {
+    // the matrix-core layout (device_layout.cc: the same choice the emitted program makes)
+    mc_layout mc = choose_matrix_core_layout(m, sp, sb, p.K, dtype);
+    if (mc.kind == mc_layout::NM) {
         // col-direction BMTs that are 2:4 panels: sparse matrix cores, self-contained blocks
-        std::vector<unsigned char> blk;
-        uint32_t S = 0;
-        std::string why;
-        if (build_nm_panels(rows, col, *vals, row_num_of_sub_matrix(m, sb), p.K, blk, S, why)) {
-            d.nm = true;
-            d.kernel = "k_nm_mfma";
-            d.KC = S;
-            d.n_rows_aux = row_num_of_sub_matrix(m, sb);
-            d.n_units = m.u(THREAD_META, "first_nz_indices", sb).size() - 1;
-            d.waves = gsk::kNmWaves;
-            a.tcol = dev_copy(d, blk);
-            d.bytes_tile = d.bytes_A;
-            d.replicas.push_back(a);
-            p.uploaded = true;
-            return;
-        }
+        d.nm = true;
+        d.kernel = "k_nm_mfma";
+        d.KC = mc.nm_S;
+        d.n_rows_aux = mc.nm_rows;
+        d.n_units = m.u(THREAD_META, "first_nz_indices", sb).size() - 1;
+        d.waves = gsk::kNmWaves;
+        a.tcol = dev_copy(d, mc.nm_blk);
+        d.bytes_tile = d.bytes_A;
+        d.replicas.push_back(a);
+        p.uploaded = true;
+        return;
     }
     // A streams: narrowest column type that holds Kc-1 (u16 when Kc <= 65536).  fp16 BMTB
     // plans try the matrix cores first: their kernels never read the CSR arrays, which
@@ -674,75 +298,59 @@ void upload_plan(plan_state &p, int dtype, int device) {
     if (!defer_csr) upload_csr(p, a);
     uint64_t row_num = row_num_of_sub_matrix(m, sb);
     // matrix-core row blocks for fp16 plans with BMTBs (tried before the other kernels)
-    auto try_mfma = [&](const std::vector<uint32_t> &rp0) {
-        const config_t cfg = get_config();
-        if (dtype != 1 || !cfg.MFMA_TILES || !m.is_exist(TBLOCK_META, "first_row_indices", sb)) return false;
-        mfma_tiles t;
-        std::string why;
-        const uint32_t Nd = (uint32_t)cfg.DENSE_MATRIX_SIZE;
-        const auto &tbr = m.u(TBLOCK_META, "first_row_indices", sb);
-        const canon_rows cr = canonical_rows(rp0, col, *vals);
-        const std::vector<uint32_t> &rp = cr.rp;
-        if (cfg.MFMA_KS) {
-            // tall row blocks: K split over workgroups, B slice stationary in LDS (k_mfma_ks)
-            ks_tiles kt;
-            if (build_ks_tiles(tbr, rp, cr.col, cr.val, p.K, Nd, cfg.KS_SPLIT, cfg.KS_MIN_ROWS, cfg.MFMA_MAX_FILL, kt,
-                               why)) {
-                d.mfma = true;
-                d.ks = true;
-                d.kernel = "k_mfma_ks";
-                d.lds_N = Nd;
-                d.ksplit = kt.S;
-                d.ks_ns = kt.NS;
-                d.maxr = kt.RT;
-                d.rpw_max = kt.RMAX;
-                d.seg_cap = kt.MAXG;
-                d.waves = kt.W;
-                d.lds_bytes = kt.lds_bytes;
-                const uint64_t nb = tbr.size() - 1;
-                d.n_rows_aux = nb;
-                const size_t before = d.bytes_A;
-                d.ks_gcap = kt.GCAP;
-                a.t0 = dev_copy(d, to_u32(tbr, "BMTB first_row_indices"));
-                a.tcol = dev_copy(d, kt.pos);
-                a.tval = dev_copy(d, kt.val);
-                d.bytes_tile = d.bytes_A - before;
-                if (kt.S > 1) {
-                    a.ws = dev_copy(d, std::vector<float>((size_t)nb * kt.S * 16 * kt.RT * Nd, 0.f));
-                    a.t2 = dev_copy(d, std::vector<uint32_t>(nb, 0u));  // arrival counters
-                }
-                return true;
+    auto try_mfma = [&](const std::vector<uint32_t> &) {
+        if (mc.kind == mc_layout::KS) {
+            // tall row blocks: K split over workgroups, wave-autonomous (k_mfma_ks)
+            const ks_tiles &kt = mc.ks;
+            d.mfma = true;
+            d.ks = true;
+            d.kernel = "k_mfma_ks";
+            d.lds_N = mc.N;
+            d.ksplit = kt.S;
+            d.ks_ns = kt.NS;
+            d.maxr = kt.RT;
+            d.rpw_max = kt.RMAX;
+            d.seg_cap = kt.MAXG;
+            d.waves = kt.W;
+            d.lds_bytes = kt.lds_bytes;
+            const uint64_t nb = mc.tbr.size() - 1;
+            d.n_rows_aux = nb;
+            const size_t before = d.bytes_A;
+            d.ks_gcap = kt.GCAP;
+            a.t0 = dev_copy(d, to_u32(mc.tbr, "BMTB first_row_indices"));
+            a.tcol = dev_copy(d, kt.pos);
+            a.tval = dev_copy(d, kt.val);
+            d.bytes_tile = d.bytes_A - before;
+            if (kt.S > 1) {
+                a.ws = dev_copy(d, std::vector<float>((size_t)nb * kt.S * 16 * kt.RT * mc.N, 0.f));
+                a.t2 = dev_copy(d, std::vector<uint32_t>(nb, 0u));  // arrival counters
             }
+            return true;
         }
-        const size_t budget = (size_t)std::min<int64_t>(cfg.SHARED_MEM_TOTAL_SIZE, 160 * 1024);
-        if (!build_mfma_tiles(tbr, rp, cr.col, cr.val, p.K, Nd, budget, cfg.MFMA_MAX_FILL, t, why)) return false;
+        if (mc.kind != mc_layout::ROWS) return false;
+        const mfma_tiles &t = mc.rows;
         d.mfma = true;
         d.kernel = "k_mfma_rows";
-        d.lds_N = Nd;
+        d.lds_N = mc.N;
         d.KC = 1u << t.lgKC; d.nc = t.nc; d.maxr = t.RT; d.rpw_max = t.RMAX; d.RSB = t.lgKC;
-        d.seg_cap = t.gmax;  // entry groups per chunk (max): the launch picks MAXA per variant
-        // K-split: enough workgroups per row block to cover the CUs, at least one chunk each
-        const uint64_t nb = m.u(TBLOCK_META, "first_row_indices", sb).size() - 1;
-        // auto: split only when the row blocks cover under half the CUs (the slab
-        // combine's cross-XCD release/acquire costs ~micro-seconds at the tail)
-        uint32_t ks = cfg.MFMA_KSPLIT > 0 ? (uint32_t)cfg.MFMA_KSPLIT
-                                          : (nb >= 128 ? 1u : (uint32_t)std::min<uint64_t>(4, 256 / std::max<uint64_t>(nb, 1)));
-        ks = std::max(1u, std::min(ks, t.nc));
-        d.ncs = (t.nc + ks - 1) / ks;
-        d.ksplit = (t.nc + d.ncs - 1) / d.ncs;  // no empty split
+        d.seg_cap = t.gmax;
+        d.mfma_glds = mc.rows_glds; d.mfma_nbg = mc.rows_nbg; d.mfma_wct = mc.rows_wct; d.mfma_maxa = mc.rows_maxa;
+        const uint64_t nb = mc.tbr.size() - 1;
+        d.ncs = mc.rows_ncs;
+        d.ksplit = mc.rows_ksplit;
         if (d.ksplit > 1) {
-            std::vector<float> z((size_t)nb * d.ksplit * t.RMAX * Nd, 0.f);
+            std::vector<float> z((size_t)nb * d.ksplit * t.RMAX * mc.N, 0.f);
             a.ws = dev_copy(d, z);
             a.t2 = dev_copy(d, std::vector<uint32_t>(nb, 0u));  // arrival counters
         }
         d.waves = kMfmaThreads / 64; d.lds_bytes = t.lds_bytes;
         const size_t before = d.bytes_A;
-        a.t0 = dev_copy(d, to_u32(m.u(TBLOCK_META, "first_row_indices", sb), "BMTB first_row_indices"));
+        a.t0 = dev_copy(d, to_u32(mc.tbr, "BMTB first_row_indices"));
         a.t1 = dev_copy(d, t.seg_start);
         a.tcol = dev_copy(d, t.pos);
         a.tval = dev_copy(d, t.val);
         d.bytes_tile = d.bytes_A - before;
-        d.n_rows_aux = m.u(TBLOCK_META, "first_row_indices", sb).size() - 1;
+        d.n_rows_aux = nb;
         return true;
     };
     switch (sp.family) {

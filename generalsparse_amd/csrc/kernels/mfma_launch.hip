@@ -18,30 +18,31 @@ namespace gs {
 
 namespace {
 
-constexpr uint32_t kMfmaThreads = 64 * gsk::kMfmaWaves;
-
 template <int CT, int RT, int LGKC, int MAXA>
 void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N,
                    hipStream_t s) {
     const device_plan &d = p.dev;
-    // B rows by LDS-DMA two chunks ahead (MFMA_GLDS) or through registers three ahead
-    const int64_t gl = get_config().MFMA_GLDS, nbuf = get_config().MFMA_GLDS_NBUF;
-    auto kern = gl >= 4 ? gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 4>
+    // the variant the upload fixed (device_layout.cc choose_matrix_core_layout): B rows by
+    // LDS-DMA (GLDS 2 or 4 B waves, a ring of NBG buffers) or through registers (GLDS 0)
+    const int gl = d.mfma_glds, nbg = d.mfma_nbg, wct = d.mfma_wct;
+    GS_CHECK(mfma_rows_lds_need(LGKC, CT, RT, d.rpw_max, gl, nbg, wct) <= d.lds_bytes,
+             "k_mfma_rows: the variant needs more LDS than the upload sized");
+    auto kern = gl == 4 ? gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 4>
                         : (gl ? gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2> : gsk::k_mfma_rows<CT, RT, LGKC, MAXA>);
-    if (gl == 1 && get_config().MFMA_COMPUTE_WAVES == 8) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 8>;
+    if (gl == 2 && wct == 8) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 8>;
+    if constexpr (LGKC == 8) {  // deeper B rings fit LDS with 256-column chunks
+        if (gl == 2 && wct == 6 && nbg == 4) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 4>;
+        if (gl == 2 && wct == 6 && nbg == 5) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 5>;
+    }
     // GS_MFMA_DEBUG (diagnostic timing builds, wrong results): kernel_lib.hpp k_mfma_rows DBG bits, C2 shape only
     static const int mdbg = getenv("GS_MFMA_DEBUG") ? atoi(getenv("GS_MFMA_DEBUG")) : 0;
     if constexpr (CT == 2 && RT == 2 && LGKC == 9 && MAXA == 1) {
-        if (gl == 1 && mdbg == 1) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 1>;
-        if (gl == 1 && mdbg == 2) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 2>;
-        if (gl == 1 && mdbg == 4) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 4>;
-        if (gl == 1 && mdbg == 10) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 10>;
-        if (gl == 1 && mdbg == 11) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 11>;
-        if (gl == 1 && mdbg == 15) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 15>;
-    }
-    if constexpr (LGKC == 8) {  // deeper B rings fit LDS with 256-column chunks
-        if (gl && !(gl >= 4) && nbuf == 4) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 4>;
-        if (gl && !(gl >= 4) && nbuf >= 5) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 5>;
+        if (gl == 2 && wct == 6 && mdbg == 1) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 1>;
+        if (gl == 2 && wct == 6 && mdbg == 2) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 2>;
+        if (gl == 2 && wct == 6 && mdbg == 4) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 4>;
+        if (gl == 2 && wct == 6 && mdbg == 10) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 10>;
+        if (gl == 2 && wct == 6 && mdbg == 11) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 11>;
+        if (gl == 2 && wct == 6 && mdbg == 15) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 15>;
     }
     static std::mutex mu;
     static std::map<std::pair<int, const void *>, size_t> granted;
@@ -64,11 +65,7 @@ void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *
 template <int CT, int RT>
 void launch_mfma_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N,
                     hipStream_t s) {
-    // entry groups per thread per chunk: the GLDS variant has 9 entry waves, the other 6
-    const int64_t gl = get_config().MFMA_GLDS;
-    const uint32_t wct = get_config().MFMA_COMPUTE_WAVES == 8 && gl == 1 ? 8u : (uint32_t)gsk::kMfmaCompute;
-    const uint32_t nat = 64u * (gsk::kMfmaWaves - wct - (gl >= 4 ? 4u : (gl ? 2u : (uint32_t)gsk::kMfmaBWaves)));
-    const bool two = p.dev.seg_cap > nat;
+    const bool two = p.dev.mfma_maxa == 2;  // entry groups per thread per chunk (fixed at upload)
     switch (p.dev.RSB) {                  // log2 KC
         case 10: two ? launch_mfma_k<CT, RT, 10, 2>(p, a, B, C, N, s) : launch_mfma_k<CT, RT, 10, 1>(p, a, B, C, N, s); break;
         case 9: two ? launch_mfma_k<CT, RT, 9, 2>(p, a, B, C, N, s) : launch_mfma_k<CT, RT, 9, 1>(p, a, B, C, N, s); break;

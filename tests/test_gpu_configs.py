@@ -18,6 +18,7 @@
 Tolerances (north_star): fp32 1e-3, fp16 1e-1, relative to max(1, |ref|)."""
 import json
 import os
+import shutil
 import subprocess
 import sys
 
@@ -55,19 +56,67 @@ def dense_ref(M, K, row, col, val, B):
 
 
 # ------------------------------------------------------------------ emitted programs
-def test_emitted_programs_run_and_check():
+def _run_program(d):
+    r = subprocess.run(["./a.out"], cwd=d, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and "correct" in r.stdout, (d, r.stdout[-2000:], r.stderr[-2000:])
+    lines = open(os.path.join(d, "perf_result")).read().split("\n")
+    assert len(lines) == 3 and lines[2] == "", lines   # "<ms>\n<GFLOP/s>\n"
+    ms, gf = float(lines[0]), float(lines[1])
+    assert ms > 0 and gf > 0, (d, lines)
+    return ms
+
+
+def _gs_spmm_ms(m, reps):
+    """gs_spmm on the same plan, hot like the program's loop: `reps` launches of one B and C
+    from native code (spmm_rotate), HIP events on the launch stream"""
+    from generalsparse_amd import emit_examples as ee
+    M, K, row, col, val = ee.matrix(m["matrix"])
+    plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline(m["pipeline"], m["N"], m["p0"], m["p1"]).compile()
+    plan.upload("f16" if m["half"] else "f32", 0)
+    assert plan.info()["device_kernel"] == m["kernel"], (plan.info()["device_kernel"], m["kernel"])
+    tdt = torch.float16 if m["half"] else torch.float32
+    B = torch.ones((K, m["N"]), device=DEV, dtype=tdt)
+    C = torch.empty((M, m["N"]), device=DEV, dtype=tdt)
+    plan.spmm_rotate(20, 0, [B], [C])
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    plan.spmm_rotate(reps, 0, [B], [C])
+    e1.record()
+    torch.cuda.synchronize()
+    plan.free()
+    return e0.elapsed_time(e1)
+
+
+def test_emitted_programs_run_and_check(tmp_path):
+    """every emitted program runs, checks the known answer and writes perf_result; the
+    matrix-core programs (k_mfma_rows / k_mfma_ks / k_nm_mfma: the kernel gs_spmm runs for
+    their plan) take the time gs_spmm takes on the same plan (within 10%
+    expected, asserted within 25% against run-to-run noise; the ratios are printed)"""
+    from generalsparse_amd import emit_examples as ee
     man_path = os.path.join(PKG, "emitted", "manifest.json")
     assert os.path.exists(man_path), "build() emits and compiles the example programs"
     man = json.load(open(man_path))
-    assert len(man) >= 5
+    assert len(man) >= 10
+    kernels = set()
     for name, m in man.items():
         d = os.path.join(PKG, m["dir"])
-        r = subprocess.run(["./a.out"], cwd=d, capture_output=True, text=True, timeout=120)
-        assert r.returncode == 0 and "correct" in r.stdout, (name, r.stdout[-2000:], r.stderr[-2000:])
-        lines = open(os.path.join(d, "perf_result")).read().split("\n")
-        assert len(lines) == 3 and lines[2] == "", lines   # "<ms>\n<GFLOP/s>\n"
-        ms, gf = float(lines[0]), float(lines[1])
-        assert ms > 0 and gf > 0, (name, lines)
+        if m["regen"]:
+            # re-emit the plan arrays from the same seeded matrix; the program must be the
+            # one compiled by build()
+            nd = ee.emit(name, m["matrix"], m["pipeline"], m["p0"], m["p1"], m["N"], m["half"], m["compressed"],
+                         str(tmp_path / name))
+            assert open(os.path.join(nd, "kernel_file.hip")).read() == open(os.path.join(d, "kernel_file.hip")).read()
+            shutil.copy2(os.path.join(d, "a.out"), os.path.join(nd, "a.out"))
+            d = nd
+        ms = _run_program(d)
+        kernels.add(m["kernel"])
+        if m["kernel"] in ("k_mfma_rows", "k_mfma_ks", "k_nm_mfma"):
+            ref = _gs_spmm_ms(m, 100)
+            print(f"{name}: {m['kernel']} emitted {ms / 100 * 1e3:.2f} us, gs_spmm {ref / 100 * 1e3:.2f} us, "
+                  f"ratio {ms / ref:.3f}")
+            assert 0.75 < ms / ref < 1.25, (name, ms, ref)
+    assert {"k_mfma_rows", "k_mfma_ks", "k_nm_mfma"} <= kernels, kernels
 
 
 # ------------------------------------------------------------------ C1
