@@ -19,7 +19,8 @@ matrices of the 48-layer OPT-30B 80%-pruned batch split over the ranks by LPT on
 (strong scaling, no data-path collective).  `--workload c2` keeps the weak-scaling
 batch of one C2 matrix per rank.  The time is the max over ranks.
 
---workload c1 | c3 | c4 | c4o | c5 measures the other BASELINE.json configs.
+--workload c1 | c3 | c4 | c4o | c5 measures the other BASELINE.json configs; c5h the
+north_star headline (one OPT-30B layer at 70%, with rocSPARSE per shape).
 
 Prints one JSON line on rank 0."""
 import argparse
@@ -50,7 +51,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--p0", type=int, default=None, help="with --pipeline: run only this plan parameter")
     ap.add_argument("--p1", type=int, default=None)
-    ap.add_argument("--workload", choices=("c1", "c2", "c3", "c4", "c4o", "c5"), default=None,
+    ap.add_argument("--workload", choices=("c1", "c2", "c3", "c4", "c4o", "c5", "c5h"), default=None,
                     help="default: c2 on one GPU, c5 (the sharded batch) on several")
     ap.add_argument("--search-reps", type=int, default=100, help="launches per candidate plan in the plan search")
     ap.add_argument("--n-sweep", default="", help="also time the chosen plan family at these dense widths, e.g. 8,32,128")
@@ -71,7 +72,7 @@ def resolve_workload(a, world):
     if a.workload is None:
         a.workload = "c5" if world > 1 else "c2"
     dflt = {"c1": (47894, 41550, 8), "c2": (5120, 5120, 32), "c3": (28672, 7168, 128), "c4": (1000005, 1000005, 8),
-            "c4o": (3072441, 3072441, 8), "c5": (7168, 7168, 32)}[a.workload]
+            "c4o": (3072441, 3072441, 8), "c5": (7168, 7168, 32), "c5h": (7168, 7168, 32)}[a.workload]
     a.M, a.K, a.N = a.M or dflt[0], a.K or dflt[1], a.N or dflt[2]
 
 
@@ -359,6 +360,101 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
         p.free()
 
 
+def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
+    """north_star headline: one OPT-30B decoder layer's six pruned weights
+    (q, k, v, out 7168^2; fc1 28672x7168; fc2 7168x28672) at 70% unstructured, fp16, N=32,
+    one GPU.  Per shape: the plan search over generalsparse_amd.batch.shape_candidates
+    (event time with rotated replicas) and rocSPARSE 7.2 CSR SpMM (fp16 A/B, fp32 C) on the
+    same matrix.  The timed step = the layer's six SpMMs, one plan replica per instance (the
+    layer's A is ~800 MB, past the 256 MB Infinity Cache)."""
+    from generalsparse_amd import batch as bt
+    N, sp = args.N, args.sparsity
+    e = 2
+    choice, per_shape = {}, {}
+    for k, (m, n) in bt.C5_SHAPES.items():
+        row, col, val = ds.pruned_weight(m, n, sp, bt.shape_seed(rank, k))
+        nnz = len(row)
+        flops = 2.0 * nnz * N
+        alg = algorithmic_bytes(m, n, N, nnz, e, 2)
+        best, variants = None, {}
+        for cand in bt.shape_candidates(k):
+            key = "%s(%d,%d)%s" % (cand[0], cand[1], cand[2], "".join(f" {a}={b}" for a, b in cand[3].items()))
+            try:
+                plan = bt.build_plan(gsa, m, n, row, col, val, N, cand, local)
+            except gsa.GsError as ex:
+                variants[key] = {"error": str(ex)}
+                continue
+            info = plan.info()
+            reps = replicas_for(info, n, N, e, args.rotation_mb)
+            for _ in range(reps - 1):
+                plan.add_replica()
+            Bs = [torch.randn((n, N), device=dev, dtype=torch.float16) for _ in range(reps)]
+            Cs = [torch.empty((m, N), device=dev, dtype=torch.float16) for _ in range(reps)]
+            ms = event_ms(plan, Bs, Cs, args.search_reps, torch)
+            variants[key] = {"kernel": kernel_label(info), "kernel_us": round(ms * 1e3, 2)}
+            if best is None or ms < best[0]:
+                best = (ms, cand, key, kernel_label(info), reps)
+            plan.free()
+            del Bs, Cs
+            torch.cuda.empty_cache()
+        ms, cand, key, kern, reps = best
+        choice[k] = cand
+        rs = None if args.no_rocsparse else rocsparse_baseline(m, n, N, row, col, val, min(reps, 20), dtype=1)
+        per_shape[k] = {"M": m, "K": n, "nnz": nnz, "plan": key, "kernel": kern, "kernel_us": round(ms * 1e3, 2),
+                        "gflops": round(flops / (ms * 1e-3) / 1e9, 1),
+                        "hbm_frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "variants": variants,
+                        "rocsparse_f16": rs,
+                        "speedup_vs_rocsparse": round(rs["ms"] / ms, 3) if rs else None}
+        del row, col, val
+    # the timed layer: 4 x attn (replicas 0..3), fc1, fc2
+    seq = [(0, s, bt.C5_SLOTS[s], bt.C5_SLOTS[:s].count(bt.C5_SLOTS[s])) for s in range(len(bt.C5_SLOTS))]
+    plans, launches, _ = bt.build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, sparsity=sp, choice=choice)
+    stream = torch.cuda.current_stream().cuda_stream
+    raw = [(p, r, b.data_ptr(), c.data_ptr()) for (p, r, b, c, _) in launches]
+
+    def step():
+        for plan, r, b, c in raw:
+            plan.spmm_raw(b, c, N, r, stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ms_step = wall / args.steps * 1e3
+    nnz_l = sum(bt.nnz_of_shape(k, sp) for k in bt.C5_SLOTS)
+    flops_l = 2.0 * nnz_l * N
+    alg_l = sum(algorithmic_bytes(*bt.C5_SHAPES[k], N, bt.nnz_of_shape(k, sp), e, 2) for k in bt.C5_SLOTS)
+    rs_l = None
+    if all(per_shape[k]["rocsparse_f16"] for k in bt.C5_SHAPES):
+        rs_l = sum(per_shape[k]["rocsparse_f16"]["ms"] for k in bt.C5_SLOTS)
+    out = {
+        "metric": "SpMM GFLOP/s + achieved HBM GB/s vs rocSPARSE, OPT-30B 70%-pruned layer fp16 N=32 (north_star headline)",
+        "value": round(flops_l * args.steps / wall / 1e9, 1), "unit": "GFLOP/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 5), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f16 (fp32 accumulate)",
+        "data": "synthetic (one seeded magnitude-pruned Gaussian per shape; each layer instance streams its own HBM "
+                "copy of A); OPT-30B weights are not available offline",
+        "config": {"workload": f"OPT-30B decoder layer: 4 x 7168^2, 28672x7168, 7168x28672, {round(sp * 100)}% "
+                               f"unstructured, fp16, N={N}", "nnz": nnz_l,
+                   "plan": {k: per_shape[k]["plan"] for k in per_shape}, "kernel": {k: per_shape[k]["kernel"] for k in per_shape},
+                   "parallelism": "one GPU"},
+        "roofline": {"bound": "hbm", "achieved": round(alg_l / (ms_step * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(alg_l / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                     "algorithmic_bytes_per_step": alg_l, "note": "whole layer step (six launches, host-timed)"},
+        "per_shape": per_shape,
+        "speedup_vs_rocsparse": round(rs_l / ms_step, 3) if rs_l else None,
+        "rocsparse_layer_ms": round(rs_l, 4) if rs_l else None,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    for p in plans.values():
+        p.free()
+
+
 def replicas_for(info, K, N, e, rotation_mb):
     """independent copies of A and B so the rotation set covers rotation_mb of the bytes
     the launched kernel actually reads (the matrix-core layouts, not a deferred CSR)"""
@@ -431,6 +527,11 @@ def main():
         k, v = kv.split("=", 1)
         gsa.set_config(k, int(v))
 
+    if args.workload == "c5h":
+        run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     if args.workload == "c5":
         run_c5(args, torch, gsa, ds, rank, world, local, dev, dist)
         if dist is not None:

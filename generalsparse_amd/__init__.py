@@ -39,6 +39,14 @@ def set_config(key, value):
     _lib.check(L.gs_set_config_int(key.encode(), int(value)))
 
 
+def get_config(key):
+    """the current value of an integer / bool config key"""
+    L = _lib.load()
+    v = ctypes.c_longlong()
+    _lib.check(L.gs_get_config_int(key.encode(), ctypes.byref(v)))
+    return v.value
+
+
 def _dtype_code(dtype):
     if dtype in (GS_F16, "f16", "fp16", "half", np.float16):
         return GS_F16

@@ -46,6 +46,7 @@ SIGNATURES = {
     "gs_plan_create_from_coo": ([ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u64p, u64p, f32p,
                                  ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
     "gs_set_config_int": ([ctypes.c_char_p, ctypes.c_longlong], ctypes.c_int),
+    "gs_get_config_int": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_longlong)], ctypes.c_int),
     "gs_plan_add_operator": ([ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int],
                              ctypes.c_int),
     "gs_plan_run_pipeline": ([ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int],

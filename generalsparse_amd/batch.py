@@ -67,10 +67,39 @@ def shape_pipeline(shape):
     return ("tblock_warp_total", row_block_rows(C5_SHAPES[shape][0]), 2)
 
 
-def build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, pipeline=None, keep_coo=False):
+# per-shape plan candidates for the matrix-core kernels (bench.py searches them for the
+# headline layer): (pipeline, p0, p1, config overrides applied while the plan is uploaded).
+# KS_MIN_ROWS 1000 keeps a block on k_mfma_rows; 56-row blocks of 7168-row shapes are 128
+# row blocks x 2 K ranges on k_mfma_ks
+def shape_candidates(shape):
+    from .autotune import row_block_rows
+    rb = row_block_rows(C5_SHAPES[shape][0])
+    return [("tblock_warp_total", rb, 2, {"KS_MIN_ROWS": 1000}), ("block_total", 56, 1, {}),
+            ("block_total", 40, 1, {}), ("block_total", 80, 1, {})]
+
+
+def build_plan(gsa, m, n, row, col, val, N, cand, local):
+    """a shape's plan from a candidate (pipeline, p0, p1[, config overrides])"""
+    name, p0, p1 = cand[:3]
+    over = cand[3] if len(cand) > 3 else {}
+    old = {k: gsa.get_config(k) for k in over}
+    for k, v in over.items():
+        gsa.set_config(k, v)
+    try:
+        plan = gsa.Plan.from_coo(m, n, row, col, val).run_pipeline(name, N, p0, p1).compile()
+        plan.upload("f16", local)
+    finally:
+        for k, v in old.items():
+            gsa.set_config(k, v)
+    return plan
+
+
+def build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, pipeline=None, keep_coo=False,
+                     sparsity=C5_SPARSITY, choice=None):
     """plans (one per shape, one replica per instance), B and C buffers (two per shape,
     alternating), and the launch list [(plan, replica, B, C, shape)].  `pipeline`
-    (name, p0, p1) overrides the per-shape choice of shape_pipeline."""
+    (name, p0, p1) overrides the per-shape choice of shape_pipeline; `choice` maps a
+    shape to a shape_candidates entry."""
     count = {}
     for (_, _, k, _) in seq:
         count[k] = count.get(k, 0) + 1
@@ -78,10 +107,9 @@ def build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, pipeline=None, ke
     for k, (m, n) in C5_SHAPES.items():
         if not count.get(k):
             continue
-        row, col, val = ds.pruned_weight(m, n, C5_SPARSITY, shape_seed(rank, k))
-        pl = pipeline or shape_pipeline(k)
-        plan = gsa.Plan.from_coo(m, n, row, col, val).run_pipeline(pl[0], N, pl[1], pl[2]).compile()
-        plan.upload("f16", local)
+        row, col, val = ds.pruned_weight(m, n, sparsity, shape_seed(rank, k))
+        pl = pipeline or (choice or {}).get(k) or shape_pipeline(k)
+        plan = build_plan(gsa, m, n, row, col, val, N, pl, local)
         for _ in range(count[k] - 1):
             plan.add_replica()
         plans[k] = plan

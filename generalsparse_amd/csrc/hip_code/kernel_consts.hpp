@@ -29,9 +29,13 @@ GSK_HD constexpr uint32_t ks_image_bytes() {
 
 // dynamic LDS of k_mfma_ks: W x (wave image + one k-step of B rows), or the W partial
 // tiles of the final reduction (+ the arrival flag), whichever is larger
+// (the reduction runs in two halves of W/2 waves when W tiles would exceed the 160 KB)
+GSK_HD constexpr bool ks_red_halves(uint32_t CT, uint32_t RT, uint32_t W) {
+    return (size_t)W * RT * CT * 1024u + 16u > 160u * 1024u;
+}
 GSK_HD constexpr size_t ks_lds_bytes(uint32_t CT, uint32_t RT, uint32_t W) {
     const size_t stage = (size_t)W * ((16u * RT + 1u) * kKsStride + 32u * 32u * CT);
-    const size_t red = (size_t)W * RT * CT * 1024u + 16u;
+    const size_t red = (size_t)(ks_red_halves(CT, RT, W) ? W / 2 : W) * RT * CT * 1024u + 16u;
     return stage > red ? stage : red;
 }
 

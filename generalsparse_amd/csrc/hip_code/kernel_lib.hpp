@@ -1042,7 +1042,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     uint32_t row_base, uint32_t nsplit, uint32_t ncs, float *__restrict__ slabs, uint32_t *__restrict__ arrivals,
     uint64_t *__restrict__ stamps = nullptr, uint32_t krot = 0) {
     constexpr uint32_t KC = 1u << LGKC;
-    constexpr uint32_t RB = 32 * CT;                  // bytes per B row (N == 16*CT)
+    constexpr uint32_t RB = 32 * CT;                  // bytes per LDS B row (N <= 16*CT)
     constexpr uint32_t UB = 2 * CT;                   // 16-B units per B row
     constexpr uint32_t RS = 2 * KC + 32;              // dense image row stride
     constexpr uint32_t NT = 64 * kMfmaWaves;
@@ -1192,7 +1192,9 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
                 const uint32_t u0 = (bw * NB + i) * 64u, u = u0 + lane;
                 const uint32_t k = u / UB, s = u % UB;
                 const uint32_t kk = kc0 + k < K ? kc0 + k : kc0;
-                const f16 *src = B + (size_t)kk * N + (b_piece<CT>(k, s >> 1) * 2u + (s & 1u)) * 8u;
+                // N < 16*CT (N = 8): the tile's columns past N copy column 0; their outputs are not stored
+                const uint32_t cu = (b_piece<CT>(k, s >> 1) * 2u + (s & 1u)) * 8u;
+                const f16 *src = B + (size_t)kk * N + (cu < N ? cu : 0u);
                 __builtin_amdgcn_global_load_lds(
                     (const void *)src, (__attribute__((address_space(3))) void *)(lds + (jl % NBUF) * szB + u0 * 16u),
                     16, 0, 0);
@@ -1241,7 +1243,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
             const uint32_t u = bt + i * NBT;                                                      \
             const uint32_t k = u / UB;                                                            \
             const uint32_t kk = kc0_ + k < K ? kc0_ + k : kc0_;                                   \
-            S[i] = *reinterpret_cast<const u32x4 *>(B + (size_t)kk * N + (u % UB) * 8u);          \
+            S[i] = *reinterpret_cast<const u32x4 *>(B + (size_t)kk * N + ((u % UB) * 8u < N ? (u % UB) * 8u : 0u)); \
         }                                                                                         \
     }
 #define GS_BSTORE_UNIT(jb, S, i)                                                                    \
@@ -1259,7 +1261,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
             const uint32_t u = bt + i * NBT;                                                      \
             const uint32_t k = u / UB;                                                            \
             const uint32_t kk = kc0_ + k < K ? kc0_ + k : kc0_;                                   \
-            Sn[i] = *reinterpret_cast<const u32x4 *>(B + (size_t)kk * N + (u % UB) * 8u);         \
+            Sn[i] = *reinterpret_cast<const u32x4 *>(B + (size_t)kk * N + ((u % UB) * 8u < N ? (u % UB) * 8u : 0u)); \
             GS_BSTORE_UNIT((j) + 1u, Ss, i);                                                      \
         }                                                                                         \
         GS_STAMP(2u + 2u * (j));                                                                  \
@@ -1367,7 +1369,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         for (uint32_t e = tid; e < RT * CT * 256u; e += NT) {
             uint32_t row, colx;
             const float sum = tile_sum(e, row, colx);
-            if (row < R) C[(size_t)(row_base + r0 + row) * N + colx] = (f16)sum;
+            if (row < R && colx < N) C[(size_t)(row_base + r0 + row) * N + colx] = (f16)sum;
         }
     } else {
         // K-split: this workgroup's fp32 slab, then the last of the row block's
@@ -1380,7 +1382,8 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         for (uint32_t e = tid; e < RT * CT * 256u; e += NT) {
             uint32_t row, colx;
             const float sum = tile_sum(e, row, colx);
-            if (row < R) __hip_atomic_store(slab + (size_t)row * N + colx, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (row < R && colx < N)
+                __hip_atomic_store(slab + (size_t)row * N + colx, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -1461,7 +1464,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
                                                     uint32_t N, uint32_t S, uint32_t NS, uint32_t GCAP, uint32_t nwg,
                                                     uint32_t row_base, float *__restrict__ slabs,
                                                     uint32_t *__restrict__ arrivals, uint64_t *__restrict__ stamps = nullptr) {
-    constexpr uint32_t RB = 32 * CT;  // bytes per B row (N == 16 * CT)
+    constexpr uint32_t RB = 32 * CT;  // bytes per LDS B row (a 16*CT-column tile)
     constexpr uint32_t UB = 2 * CT;   // 16-B units per B row
     constexpr uint32_t IMG = ks_image_bytes<RT>();
     constexpr uint32_t STG = 32u * RB;  // one k-step of B rows
@@ -1476,6 +1479,9 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
     }
     GS_KS_STAMP(0u);
     const uint32_t k0 = q * NS * 32u;
+    // column tile blockIdx.y: columns [col0, col0 + nv) of B and C (N > 16*CT: several
+    // tiles; N = 8: one partial tile)
+    const uint32_t col0 = blockIdx.y * 16u * CT, nv = min(16u * CT, N - col0);
     unsigned char *img = lds + wv * (IMG + STG);
     unsigned char *bst = img + IMG;
     const u32x4 zero4 = {0u, 0u, 0u, 0u};
@@ -1494,8 +1500,10 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
 #pragma unroll
         for (int c = 0; c < CT; c++) {
             const uint32_t un = lane + 64u * c;  // 16-B unit of the step's 32 rows
-            const uint32_t k = kr + un / UB;
-            B_[c] = *reinterpret_cast<const u32x4 *>(B + (size_t)(k < K ? k : K - 1u) * N + (un % UB) * 8u);
+            const uint32_t k = kr + un / UB, cu = (un % UB) * 8u;
+            // columns past N (a partial column tile: N = 8, 24, ...) read column 0 and are
+            // stored as zeros below
+            B_[c] = *reinterpret_cast<const u32x4 *>(B + (size_t)(k < K ? k : K - 1u) * N + col0 + (cu < nv ? cu : 0u));
         }
 #pragma unroll
         for (int j = 0; j < MAXG; j++) {
@@ -1531,7 +1539,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
             for (int c = 0; c < CT; c++) {
                 const uint32_t un = lane + 64u * c, k = un / UB, s = un % UB;
                 *reinterpret_cast<u32x4 *>(bst + k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u) =
-                    kr + k < K ? B_[c] : zero4;
+                    kr + k < K && s * 8u < nv ? B_[c] : zero4;
             }
             // scatter the step's entries into the image
 #pragma unroll
@@ -1594,10 +1602,35 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
     __builtin_amdgcn_s_barrier();
     __asm__ volatile("" ::: "memory");
     f4v *red = reinterpret_cast<f4v *>(lds);
+    // with W partial tiles over the LDS, waves W/2.. hand theirs to waves 0..W/2-1 first
+    constexpr bool HALVES = ks_red_halves(CT, RT, W);
+    constexpr uint32_t WR = HALVES ? W / 2 : W;  // partial tiles summed from LDS
+    if constexpr (HALVES) {
+        if (wv >= WR) {
 #pragma unroll
-    for (int rt = 0; rt < RT; rt++)
+            for (int rt = 0; rt < RT; rt++)
 #pragma unroll
-        for (int ct = 0; ct < CT; ct++) red[((wv * RT + rt) * CT + ct) * 64u + lane] = acc[rt][ct];
+                for (int ct = 0; ct < CT; ct++) red[(((wv - WR) * RT + rt) * CT + ct) * 64u + lane] = acc[rt][ct];
+        }
+        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __asm__ volatile("" ::: "memory");
+        if (wv < WR) {
+#pragma unroll
+            for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+                for (int ct = 0; ct < CT; ct++) acc[rt][ct] += red[((wv * RT + rt) * CT + ct) * 64u + lane];
+        }
+        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __asm__ volatile("" ::: "memory");
+    }
+    if (wv < WR) {
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) red[((wv * RT + rt) * CT + ct) * 64u + lane] = acc[rt][ct];
+    }
     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __asm__ volatile("" ::: "memory");
@@ -1606,15 +1639,16 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
     auto item_sum = [&](uint32_t t) {
         f4v sum = red[t];
 #pragma unroll
-        for (uint32_t w = 1; w < (uint32_t)W; w++) sum += red[w * NI + t];
+        for (uint32_t w = 1; w < WR; w++) sum += red[w * NI + t];
         return sum;
     };
     auto store_item = [&](uint32_t t, const f4v &v) {
         const uint32_t ln = t & 63u, tt = t >> 6, rt = tt / CT, ct = tt % CT;
         const uint32_t col = 16u * ct + (ln & 15u), rb = 16u * rt + 4u * (ln >> 4);
+        if (col >= nv) return;
 #pragma unroll
         for (uint32_t i = 0; i < 4; i++)
-            if (rb + i < R) C[(size_t)(row_base + r0 + rb + i) * N + col] = (f16)v[i];
+            if (rb + i < R) C[(size_t)(row_base + r0 + rb + i) * N + col0 + col] = (f16)v[i];
     };
     GS_KS_STAMP(21u);
     if (S == 1) {
@@ -1624,7 +1658,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
     }
     // K-split: this workgroup's fp32 slab (16-B write-through stores), then the last of
     // the row block's S workgroups sums the slabs in q order
-    f4v *slab = reinterpret_cast<f4v *>(slabs) + (size_t)u * NI;
+    f4v *slab = reinterpret_cast<f4v *>(slabs) + ((size_t)u * gridDim.y + blockIdx.y) * NI;
     for (uint32_t t = tid; t < NI; t += NT) {
         const f4v v = item_sum(t);
         // 16-B write-through store (vector memory, sc1): retired by the vmcnt(0) below
@@ -1632,15 +1666,17 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
     }
     __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    uint32_t *flag = reinterpret_cast<uint32_t *>(lds + (size_t)W * NI * 16u);
-    if (tid == 0) *flag = __hip_atomic_fetch_add(&arrivals[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t *flag = reinterpret_cast<uint32_t *>(lds + (size_t)WR * NI * 16u);
+    uint32_t *arr = arrivals + (size_t)g * gridDim.y + blockIdx.y;
+    if (tid == 0) *flag = __hip_atomic_fetch_add(arr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (*flag != S - 1u) {
         GS_KS_STAMP(22u);
         return;
     }
-    if (tid == 0) __hip_atomic_store(&arrivals[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const f4v *base = reinterpret_cast<const f4v *>(slabs) + (size_t)g * S * NI;
+    if (tid == 0) __hip_atomic_store(arr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const f4v *base = reinterpret_cast<const f4v *>(slabs) + blockIdx.y * NI;
+    const size_t qstride = (size_t)gridDim.y * NI;  // slab of (g, qq) = base + (g*S + qq) * qstride
     for (uint32_t t = tid; t < NI; t += NT) {
         const f4v own = item_sum(t);
         f4v sum = {0.f, 0.f, 0.f, 0.f};
@@ -1649,7 +1685,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
                 sum += own;
                 continue;
             }
-            const float *src = reinterpret_cast<const float *>(base + (size_t)qq * NI + t);
+            const float *src = reinterpret_cast<const float *>(base + ((size_t)g * S + qq) * qstride + t);
             f4v x;
 #pragma unroll
             for (int i = 0; i < 4; i++) x[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

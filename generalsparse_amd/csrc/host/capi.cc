@@ -548,6 +548,13 @@ int gs_set_config_int(const char *key, long long value) {
     return guard([&] { gs::set_config(key, value); });
 }
 
+int gs_get_config_int(const char *key, long long *value) {
+    return guard([&] {
+        GS_CHECK(key && value, "null argument");
+        *value = (long long)gs::get_config_int(key);
+    });
+}
+
 int gs_plan_add_operator_sub(gs_plan_t *p, int sub, const char *op_name, const long long *args, int nargs) {
     return guard([&] {
         GS_CHECK(p && op_name && (nargs == 0 || args), "null argument");

@@ -214,7 +214,7 @@ namespace {
 // (kernels/{ks,mfma}_launch.hip); the check and perf_result as for the other families
 std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int repeat) {
     std::ostringstream o;
-    const uint32_t N = L.N, CT = N / 16;
+    const uint32_t N = L.N, CT = L.kind == mc_layout::NM ? N / 16 : ks_ct(N);
     const char *kname = L.kind == mc_layout::KS ? "k_mfma_ks" : (L.kind == mc_layout::ROWS ? "k_mfma_rows" : "k_nm_mfma");
     o << "// kernel_file.hip -- generated by generalsparse_amd code_generator: the matrix-core kernel " << kname << "\n"
       << "// build: sh make_kernel.sh; run: ./a.out [matrix.mtx] [N]  -> perf_result (ms, GFLOP/s)\n"
@@ -249,13 +249,15 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
           << "    std::vector<uint32_t> t32(tbr.begin(), tbr.end()); uint32_t *d_tbr = up(t32);\n"
           << "    uint16_t *d_pos = up(rdb<uint16_t>(\"TBLOCK_META_mfma_ks_entry_pos_0.bin\"));\n"
           << "    uint16_t *d_val = up(rdb<uint16_t>(\"TBLOCK_META_mfma_ks_entry_val_0.bin\"));\n"
-          << "    float *d_ws; uint32_t *d_arr; hipMalloc(&d_ws, " << nwg * 16 * t.RT * N * 4 << "ull + 16);\n"
-          << "    hipMalloc(&d_arr, " << nb * 4 << "ull + 4); hipMemset(d_arr, 0, " << nb * 4 << "ull + 4);\n";
+          << "    float *d_ws; uint32_t *d_arr; hipMalloc(&d_ws, " << nwg * ks_col_tiles(N) * 256 * t.RT * CT * 4 << "ull + 16);\n"
+          << "    hipMalloc(&d_arr, " << nb * ks_col_tiles(N) * 4 << "ull + 4); hipMemset(d_arr, 0, " << nb * ks_col_tiles(N) * 4
+          << "ull + 4);\n";
         const std::string k = "gsk::k_mfma_ks<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ", " +
                               std::to_string(kKsWaves) + ", " + std::to_string(kKsDepth) + ", " + std::to_string(t.MAXG) + ">";
         setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
                 std::to_string(t.lds_bytes) + ")";
-        launch = k + "<<<" + std::to_string(nwg) + ", " + std::to_string(64 * kKsWaves) + ", " + std::to_string(t.lds_bytes) +
+        launch = k + "<<<dim3(" + std::to_string(nwg) + ", " + std::to_string(ks_col_tiles(N)) + "), " +
+                 std::to_string(64 * kKsWaves) + ", " + std::to_string(t.lds_bytes) +
                  ">>>(d_tbr, (const gsk::u32x4 *)d_pos, (const gsk::u32x4 *)d_val, d_B, d_C, (uint32_t)K, N, " +
                  std::to_string(t.S) + "u, " + std::to_string(t.NS) + "u, " + std::to_string(t.GCAP) + "u, " +
                  std::to_string(nwg) + "u, 0u, d_ws, d_arr, nullptr)";

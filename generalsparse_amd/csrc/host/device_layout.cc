@@ -148,8 +148,8 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
                       size_t lds_budget, int64_t max_fill, mfma_tiles &t, std::string &why) {
     const uint64_t nb = tb_rows.size() - 1;
     if (nb == 0 || K == 0) { why = "empty plan"; return false; }
-    if (N != 16 && N != 32 && N != 64) { why = "N must be 16, 32 or 64"; return false; }
-    const uint32_t CT = N / 16;
+    if (N == 0 || N > 64 || N % 8 != 0) { why = "N must be a multiple of 8 up to 64"; return false; }
+    const uint32_t CT = ks_ct(N);  // 16-column tiles (N = 8: one tile of which 8 columns are stored)
     uint64_t rmax = 0, nnz = 0;
     for (uint64_t g = 0; g < nb; g++) rmax = std::max<uint64_t>(rmax, tb_rows[g + 1] - tb_rows[g]);
     for (uint64_t g = 0; g < nb; g++) nnz += row_ptr[tb_rows[g + 1]] - row_ptr[tb_rows[g]];
@@ -235,8 +235,8 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
                     int64_t s_cfg, int64_t min_rows, int64_t max_fill, ks_tiles &t, std::string &why) {
     const uint64_t nb = tb_rows.size() - 1;
     if (nb == 0 || K == 0) { why = "empty plan"; return false; }
-    if (N != 16 && N != 32 && N != 64) { why = "N must be 16, 32 or 64"; return false; }
-    const uint32_t CT = N / 16, W = kKsWaves;
+    if (N == 0 || N % 8 != 0) { why = "N must be a multiple of 8"; return false; }
+    const uint32_t CT = ks_ct(N), W = kKsWaves;
     uint64_t rmax = 0;
     for (uint64_t g = 0; g < nb; g++) rmax = std::max<uint64_t>(rmax, tb_rows[g + 1] - tb_rows[g]);
     if (rmax < (uint64_t)std::max<int64_t>(1, min_rows) || rmax > 80) { why = "row blocks outside the k_mfma_ks range"; return false; }

@@ -52,6 +52,11 @@ struct ks_tiles {
     std::vector<uint16_t> pos, val;  // 8 u16 per group each
 };
 
+// k_mfma_ks column tiles: CT 16-column MFMA tiles per workgroup (N = 8 runs one partial
+// tile), ks_col_tiles(N) tiles in the grid's y dimension (N = 128: two)
+inline uint32_t ks_ct(uint32_t N) { return N <= 16 ? 1u : (N <= 32 ? 2u : 4u); }
+inline uint32_t ks_col_tiles(uint32_t N) { return (N + 16 * ks_ct(N) - 1) / (16 * ks_ct(N)); }
+
 bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
                     const std::vector<uint64_t> &col, const std::vector<float> &vals, uint64_t K, uint32_t N,
                     int64_t s_cfg, int64_t min_rows, int64_t max_fill, ks_tiles &t, std::string &why);

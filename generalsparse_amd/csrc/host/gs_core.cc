@@ -168,6 +168,20 @@ void set_config(const std::string &key, int64_t value) {
     apply_kv(g_cfg, key, std::to_string(value));
 }
 
+int64_t get_config_int(const std::string &k) {
+    const config_t c = get_config();
+#define GS_KEY(name) \
+    if (k == #name) return (int64_t)c.name;
+    GS_KEY(DENSE_MATRIX_SIZE) GS_KEY(VECTOR_WIDTH) GS_KEY(HALF) GS_KEY(OPERATOR_RUNTIME_CHECK)
+    GS_KEY(PADDING_RATE_UP_BOUND) GS_KEY(DATA_TYPE_COMPRESS) GS_KEY(BRANCH_COMPRESS_MAX_SIZE) GS_KEY(FLOAT_RATE)
+    GS_KEY(SHARED_MEM_TOTAL_SIZE) GS_KEY(MAX_DIV_TIMES_OF_DIV) GS_KEY(MFMA_GLDS) GS_KEY(MFMA_COMPUTE_WAVES)
+    GS_KEY(MFMA_GLDS_NBUF) GS_KEY(MODEL_DRIVEN_COMPRESS) GS_KEY(LDS_STAGE_B) GS_KEY(MFMA_TILES) GS_KEY(MFMA_KROT)
+    GS_KEY(WARP_ROWS_GROUPS) GS_KEY(MFMA_MAX_FILL) GS_KEY(NM_MFMA) GS_KEY(MFMA_KSPLIT) GS_KEY(MFMA_KS)
+    GS_KEY(KS_MIN_ROWS) GS_KEY(KS_SPLIT)
+#undef GS_KEY
+    throw gs_error("get_config_int: no integer key " + k);
+}
+
 void set_config_str(const std::string &key, const std::string &value) {
     std::lock_guard<std::mutex> l(g_cfg_mu);
     ensure_loaded();

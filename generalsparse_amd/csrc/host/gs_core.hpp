@@ -93,6 +93,7 @@ struct config_t {
 // present (flat JSON object of scalars), defaults otherwise.
 config_t get_config();
 void set_config(const std::string &key, int64_t value);
+int64_t get_config_int(const std::string &key);  // integer / bool keys
 void set_config_str(const std::string &key, const std::string &value);
 void reset_config();
 

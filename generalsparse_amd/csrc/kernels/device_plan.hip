@@ -322,8 +322,9 @@ void upload_plan(plan_state &p, int dtype, int device) {
             a.tval = dev_copy(d, kt.val);
             d.bytes_tile = d.bytes_A - before;
             if (kt.S > 1) {
-                a.ws = dev_copy(d, std::vector<float>((size_t)nb * kt.S * 16 * kt.RT * mc.N, 0.f));
-                a.t2 = dev_copy(d, std::vector<uint32_t>(nb, 0u));  // arrival counters
+                const uint32_t nt = ks_col_tiles(mc.N), CT = ks_ct(mc.N);
+                a.ws = dev_copy(d, std::vector<float>((size_t)nb * kt.S * nt * 256 * kt.RT * CT, 0.f));
+                a.t2 = dev_copy(d, std::vector<uint32_t>((size_t)nb * nt, 0u));  // arrival counters
             }
             return true;
         }

@@ -39,7 +39,7 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
     // the LDS this instantiation needs at the plan's range width, against what the upload sized
     GS_CHECK(gsk::ks_lds_bytes(CT, RT, kKsWaves) <= d.lds_bytes, "k_mfma_ks: LDS size disagrees with the upload");
     grant_lds(d.device, kern, d.lds_bytes);
-    hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit), dim3(64 * kKsWaves), d.lds_bytes, s, a.t0,
+    hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit, ks_col_tiles(N)), dim3(64 * kKsWaves), d.lds_bytes, s, a.t0,
                        (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, B, C, (uint32_t)p.K, N, d.ksplit,
                        d.ks_ns, d.ks_gcap, (uint32_t)d.n_rows_aux * d.ksplit, (uint32_t)d.row_base, a.ws, a.t2, stamps);
     HIP_OK(hipGetLastError());
@@ -71,11 +71,10 @@ void launch_ks(const plan_state &p, const device_arrays &a, const void *B, void 
     const gsk::f16 *b = (const gsk::f16 *)B;
     gsk::f16 *c = (gsk::f16 *)C;
     GS_CHECK(N == p.dev.lds_N, "k_mfma_ks runs the plan's dense width");
-    switch (N) {
-        case 16: launch_ks_ct<1>(p, a, b, c, N, s); break;
-        case 32: launch_ks_ct<2>(p, a, b, c, N, s); break;
-        case 64: launch_ks_ct<4>(p, a, b, c, N, s); break;
-        default: throw gs_error("k_mfma_ks runs N = 16, 32 or 64");
+    switch (ks_ct(N)) {  // 16-column tiles per workgroup; ks_col_tiles(N) workgroups across N
+        case 1: launch_ks_ct<1>(p, a, b, c, N, s); break;
+        case 2: launch_ks_ct<2>(p, a, b, c, N, s); break;
+        default: launch_ks_ct<4>(p, a, b, c, N, s); break;
     }
 }
 
@@ -84,7 +83,7 @@ void debug_ks_timeline(const plan_state &p, const void *B, void *C, uint32_t N, 
                        size_t n_host) {
     const device_plan &d = p.dev;
     GS_CHECK(N == 32 && d.maxr == 5 && d.seg_cap == 2, "k_mfma_ks timeline build: N=32, RT=5, MAXG=2 only");
-    const size_t n = (size_t)d.n_rows_aux * d.ksplit * kKsWaves * 32;
+    const size_t n = (size_t)d.n_rows_aux * d.ksplit * ks_col_tiles(N) * kKsWaves * 32;
     uint64_t *dst = nullptr;
     HIP_OK(hipMalloc(&dst, n * 8));
     HIP_OK(hipMemsetAsync(dst, 0, n * 8, s));

@@ -168,7 +168,8 @@ void launch_mfma(const plan_state &p, const device_arrays &a, const void *B, voi
         launch_ks(p, a, B, C, N, s);  // ks_launch.hip
         return;
     }
-    switch (N / 16) {
+    GS_CHECK(N % 8 == 0 && N <= 64, "k_mfma_rows runs N = 8..64, a multiple of 8");
+    switch (ks_ct(N)) {  // 16-column tiles (device_layout.hpp)
         case 1: launch_mfma_ct<1>(p, a, b, c, N, s); break;
         case 2: launch_mfma_ct<2>(p, a, b, c, N, s); break;
         default: launch_mfma_ct<4>(p, a, b, c, N, s); break;

@@ -29,6 +29,15 @@
         }                                                                     \
     } while (0)
 
+#define HK(x)                                                                           \
+    do {                                                                                \
+        hipError_t e_ = (x);                                                            \
+        if (e_ != hipSuccess) {                                                         \
+            std::fprintf(stderr, "%s failed: %s\n", #x, hipGetErrorString(e_));         \
+            return 1;                                                                   \
+        }                                                                               \
+    } while (0)
+
 int main(int argc, char **argv) {
     if (argc < 3) {
         std::fprintf(stderr, "usage: token_test <matrix.mtx> <N> [pipeline] [p0] [p1] [--f32] [--exec-program]\n");
@@ -69,10 +78,11 @@ int main(int argc, char **argv) {
     std::vector<uint16_t> hB16(info.cols * N, 0x3c00);  // fp16 1.0
     std::vector<float> hB32(info.cols * N, 1.0f);
     void *dB = nullptr, *dC = nullptr;
-    if (hipMalloc(&dB, info.cols * N * es) || hipMalloc(&dC, info.rows * N * es)) return 1;
-    hipMemcpy(dB, f32 ? (void *)hB32.data() : (void *)hB16.data(), info.cols * N * es, hipMemcpyHostToDevice);
+    HK(hipMalloc(&dB, info.cols * N * es));
+    HK(hipMalloc(&dC, info.rows * N * es));
+    HK(hipMemcpy(dB, f32 ? (void *)hB32.data() : (void *)hB16.data(), info.cols * N * es, hipMemcpyHostToDevice));
     CK(gs_spmm(plan, dB, dC, N, nullptr));
-    hipDeviceSynchronize();
+    HK(hipDeviceSynchronize());
     // known answer: C[i][j] = nnz(row i)
     std::vector<uint64_t> row(info.nnz);
     std::vector<uint64_t> nnz_row(info.rows, 0);
@@ -86,10 +96,10 @@ int main(int argc, char **argv) {
     }
     std::vector<float> out(info.rows * N);
     if (f32) {
-        hipMemcpy(out.data(), dC, out.size() * 4, hipMemcpyDeviceToHost);
+        HK(hipMemcpy(out.data(), dC, out.size() * 4, hipMemcpyDeviceToHost));
     } else {
         std::vector<_Float16> h(info.rows * N);
-        hipMemcpy(h.data(), dC, h.size() * 2, hipMemcpyDeviceToHost);
+        HK(hipMemcpy(h.data(), dC, h.size() * 2, hipMemcpyDeviceToHost));
         for (size_t i = 0; i < h.size(); i++) out[i] = (float)h[i];
     }
     long wrong = 0;
@@ -104,14 +114,16 @@ int main(int argc, char **argv) {
     std::printf("wrong number:%ld\n", wrong);
     if (!wrong) std::printf("correct\n");
     hipEvent_t e0, e1;
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
-    hipEventRecord(e0, nullptr);
-    for (int i = 0; i < repeat; i++) gs_spmm(plan, dB, dC, N, nullptr);
-    hipEventRecord(e1, nullptr);
-    hipEventSynchronize(e1);
+    HK(hipEventCreate(&e0));
+    HK(hipEventCreate(&e1));
+    HK(hipEventRecord(e0, nullptr));
+    for (int i = 0; i < repeat; i++) CK(gs_spmm(plan, dB, dC, N, nullptr));
+    HK(hipEventRecord(e1, nullptr));
+    HK(hipEventSynchronize(e1));
     float ms = 0;
-    hipEventElapsedTime(&ms, e0, e1);
+    HK(hipEventElapsedTime(&ms, e0, e1));
+    HK(hipEventDestroy(e0));
+    HK(hipEventDestroy(e1));
     double gflops = 2.0 * (double)info.nnz * N * repeat / (ms * 1e-3) / 1e9;  // padding excluded
     std::string pr = std::string(dir) + "/perf_result";
     if (FILE *f = std::fopen(pr.c_str(), "w")) {
@@ -125,9 +137,10 @@ int main(int argc, char **argv) {
                           " " + std::to_string(N);
         int rc = std::system(cmd.c_str());
         std::printf("generated program exit code %d\n", rc);
+        if (rc != 0) wrong = wrong ? wrong : -1;
     }
-    hipFree(dB);
-    hipFree(dC);
+    HK(hipFree(dB));
+    HK(hipFree(dC));
     gs_plan_free(plan);
     return wrong ? 1 : 0;
 }

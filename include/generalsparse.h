@@ -15,6 +15,7 @@
  *                             with the operator classes of           operator.hpp:64-1324
  *   gs_plan_run_pipeline      token_test.cc test_spmm_* functions    token_test.cc:1003-1582
  *   gs_set_config_int         set_config                              config.cc:17-40
+ *   gs_get_config_int         get_config                              config.cc:42-70
  *   gs_plan_compile           code_generator::compile                code_generator.hpp:265-269
  *   gs_plan_generate_program  code_generator::generate_final_program code_generator.hpp:271-280
  *   gs_plan_upload / gs_spmm  the generated program's device copies + kernel launch
@@ -76,6 +77,9 @@ int gs_plan_create_from_mtx(const char *path, int ones_values, gs_plan_t **out);
 int gs_plan_create_from_coo(uint64_t n_rows, uint64_t n_cols, uint64_t nnz, const uint64_t *row,
                             const uint64_t *col, const float *val, gs_plan_t **out);
 int gs_set_config_int(const char *key, long long value);
+/* the current value of an integer / bool key (the reference reads get_config per use,
+ * config.cc:42-70) */
+int gs_get_config_int(const char *key, long long *value);
 
 /* operator surface: name = reference class name; args in constructor order
  * without the code_generator / operator_context arguments */

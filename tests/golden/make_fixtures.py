@@ -406,6 +406,119 @@ cases.append({
     },
 })
 
+# balanced BMTs inside row-direction BMTBs (balanced_interval_row_direction_thread_blocking_operator
+# .cc:207-249 -> data_transform_common.cc:794-932, get_begin_BMTs_of_specific_parent_after_blocking_
+# in_row_direction.cc).  ex1 row nnz [2,0,3,1,5,0], BMTBs of 4 rows [0,4) [4,6) (first nz 0, 6, 11),
+# 3 nnz per BMT: a BMT closes after the row where the running count reaches 3, unless that row ends
+# the parent.  BMTB 0: rows 0 (2), 1 (2), 2 (5 >= 3) -> cut before row 3 at nz 5; BMTB 1: row 4
+# (5 >= 3, not the last row) -> cut before row 5 at nz 6 + 5 = 11.  Rows close with row_num 6, nzs
+# with the last parent nz 11.  BMTs per BMTB 2 | 2.
+cases.append({
+    "matrix": "ex1", "pipeline": "tblock_balanced_thread_total", "p0": 4, "p1": 3,
+    "expect": {
+        T + "first_row_indices_0": [0, 3, 4, 5, 6],
+        T + "first_row_indices_relative_to_BMTB_0": [0, 3, 0, 1],
+        T + "first_nz_indices_0": [0, 5, 6, 11, 11],
+        T + "first_nz_indices_relative_to_BMTB_0": [0, 5, 0, 5],
+        B + "first_BMT_indices_0": [0, 2, 4],
+    },
+})
+# ex2 row nnz [20,0,15,5], BMTBs of 2 rows [0,2) [2,4) (first nz 0, 20, 40), 6 nnz per BMT: row 0
+# (20) and row 2 (15) each close a BMT; the empty row 1 and row 3 end their parents.
+cases.append({
+    "matrix": "ex2", "pipeline": "tblock_balanced_thread_total", "p0": 2, "p1": 6,
+    "expect": {
+        T + "first_row_indices_0": [0, 1, 2, 3, 4],
+        T + "first_row_indices_relative_to_BMTB_0": [0, 1, 0, 1],
+        T + "first_nz_indices_0": [0, 20, 20, 35, 40],
+        T + "first_nz_indices_relative_to_BMTB_0": [0, 20, 0, 15],
+        B + "first_BMT_indices_0": [0, 2, 4],
+    },
+})
+
+# one-row BMTs inside BMTBs with every row padded to a multiple of the column count
+# (fixed_interval_row_direction_thread_blocking_operator.cc:272-310 with is_col_padding_with_col_size:
+# modify_*_by_col_pad_in_sub_matrix, then the BMTB operator rerun on the padded COO).  ex1 with
+# col_size 2: row nnz [2,0,3,1,5,0] -> [2,0,4,2,6,0], pads repeat the row's last column with value
+# 0; BMTBs of 4 rows: first nz 0, 8, 14; one BMT per row (empty rows too).
+cases.append({
+    "matrix": "ex1", "pipeline": "tblock_thread_total_colpad", "p0": 4, "p1": 2,
+    "expect": {
+        G + "nz_col_indices_0": [0, 2, 1, 3, 4, 4, 0, 0, 0, 1, 2, 3, 4, 4],
+        G + "nz_row_indices_0": [0, 0, 2, 2, 2, 2, 3, 3, 4, 4, 4, 4, 4, 4],
+        G + "nz_vals_0": [1, 2, 3, 4, 5, 0, 6, 0, 7, 8, 9, 10, 11, 0],
+        B + "first_nz_indices_0": [0, 8, 14],
+        T + "first_row_indices_0": [0, 1, 2, 3, 4, 5, 6],
+        T + "first_nz_indices_0": [0, 2, 2, 6, 8, 14, 14],
+        T + "first_row_indices_relative_to_BMTB_0": [0, 1, 2, 3, 0, 1],
+        T + "first_nz_indices_relative_to_BMTB_0": [0, 2, 2, 6, 0, 6],
+        B + "first_BMT_indices_0": [0, 4, 6],
+    },
+})
+
+# nnz-direction BMTBs (fixed_interval_nnz_direction_tblock_blocking_operator.cc:95-147): the COO is
+# padded to a multiple of nnz_per_BMTB by repeating the last entry's row and column with value 0
+# (modify_*_by_nnz_pad.cc), BMTB i starts at nz i * p0 and at that entry's row, the row list closes
+# with row_num (get_begin_{rows,nzs}_of_BMTB_after_fixed_blocking_in_nnz_direction.cc).  Then 32-nnz
+# BMTs inside with indices relative to the BMTB (fixed_interval_nnz_direction_thread_blocking_operator
+# + get_begin_{rows,nzs}_of_BMT_after_fixed_blocking_in_nnz_direction_relative_to_BMTB.cc) and the
+# thread bitmap (a bit per row start inside each BMT).
+# ex2: 40 nnz -> 64 (24 pads of row 3, col 4); rows of entries 0..19 = 0, 20..34 = 2, 35..63 = 3.
+cases.append({
+    "matrix": "ex2", "pipeline": "nnz_tblock_bitmap", "p0": 64,
+    "expect": {
+        G + "nz_row_indices_0": [0] * 20 + [2] * 15 + [3] * 29,
+        G + "nz_col_indices_0": list(range(20)) + list(range(15)) + list(range(5)) + [4] * 24,
+        B + "first_row_indices_0": [0, 4],
+        B + "first_nz_indices_0": [0, 64],
+        T + "first_row_indices_0": [0, 2, 4],
+        T + "first_nz_indices_0": [0, 32, 64],
+        T + "first_row_indices_relative_to_BMTB_0": [0, 2],
+        T + "first_nz_indices_relative_to_BMTB_0": [0, 32],
+        B + "first_BMT_indices_0": [0, 2],
+        T + "thread_bit_map_0": [1 + (1 << 20), 8],
+    },
+})
+# the same with BMTBs of 32 nnz: one BMT per BMTB, BMTB 1 opens mid-row 2
+cases.append({
+    "matrix": "ex2", "pipeline": "nnz_tblock_bitmap", "p0": 32,
+    "expect": {
+        B + "first_row_indices_0": [0, 2, 4],
+        B + "first_nz_indices_0": [0, 32, 64],
+        T + "first_row_indices_0": [0, 2, 4],
+        T + "first_row_indices_relative_to_BMTB_0": [0, 0],
+        T + "first_nz_indices_relative_to_BMTB_0": [0, 0],
+        B + "first_BMT_indices_0": [0, 1, 2],
+        T + "thread_bit_map_0": [1 + (1 << 20), 8],
+    },
+})
+# nnz-direction BMWs of 128 inside BMTBs of 256 (fixed_interval_nnz_direction_warp_blocking_operator,
+# relative to the BMTB) and 32-nnz BMTs inside the BMWs (relative to the BMW).  ex4: 610 nnz -> 768
+# (158 pads of row 1, col 9); entries 0..599 row 0, 600..767 row 1; row_num 3.
+# BMTBs at nz 0, 256, 512 all open in row 0.  BMWs at nz 0, 128, ..., 640: rows 0 x5, then 1;
+# relative to their BMTB (first row 0): the same.  BMTs every 32 nz: rows 0 for nz 0..576 (19
+# BMTs), 1 for nz 608..736 (5); relative to the BMW: the BMT at 608 lies in BMW 4 (first row 0) -> 1,
+# those at 640.. in BMW 5 (first row 1) -> 0.  Row starts: nz 0 (BMT 0, bit 0), nz 600 (BMT 18,
+# bit 24).
+cases.append({
+    "matrix": "ex4", "pipeline": "nnz_tblock_warp_bitmap", "p0": 256, "p1": 128,
+    "expect": {
+        B + "first_row_indices_0": [0, 0, 0, 3],
+        B + "first_nz_indices_0": [0, 256, 512, 768],
+        W + "first_row_indices_0": [0, 0, 0, 0, 0, 1, 3],
+        W + "first_nz_indices_0": [0, 128, 256, 384, 512, 640, 768],
+        W + "first_row_indices_relative_to_BMTB_0": [0, 0, 0, 0, 0, 1],
+        W + "first_nz_indices_relative_to_BMTB_0": [0, 128, 0, 128, 0, 128],
+        B + "first_BMW_indices_0": [0, 2, 4, 6],
+        T + "first_row_indices_0": [0] * 19 + [1] * 5 + [3],
+        T + "first_nz_indices_0": [32 * i for i in range(25)],
+        T + "first_row_indices_relative_to_BMW_0": [0] * 19 + [1] + [0] * 4,
+        T + "first_nz_indices_relative_to_BMW_0": [0, 32, 64, 96] * 6,
+        W + "first_BMT_indices_0": [0, 4, 8, 12, 16, 20, 24],
+        T + "thread_bit_map_0": [1] + [0] * 17 + [1 << 24] + [0] * 5,
+    },
+})
+
 out = {"matrices": {"ex1": EX1, "ex2": EX2, "ex3": EX3, "ex4": EX4}, "cases": cases}
 path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hand_plans.json")
 with open(path, "w") as f:

@@ -126,10 +126,12 @@ def test_c1_token_test_ig5_18_standin(tmp_path):
     mtx = tmp_path / "IG5-18-standin.mtx"
     ds.write_mtx(str(mtx), M, K, row, col, val)
     env = dict(os.environ, GS_ROOT_PATH=str(tmp_path))
-    r = subprocess.run([os.path.join(PKG, "token_test"), str(mtx), "8", "--f32"], capture_output=True, text=True,
-                       env=env, timeout=300)
+    # --exec-program: also builds (hipcc) and runs the generated program, like execute_binary
+    r = subprocess.run([os.path.join(PKG, "token_test"), str(mtx), "8", "--f32", "--exec-program"],
+                       capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
     assert "wrong number:0" in r.stdout and "correct" in r.stdout
+    assert "generated program exit code 0" in r.stdout, r.stdout[-3000:]
     assert f"rows={M} cols={K} nnz={len(row)}" in r.stdout
     prs = list(tmp_path.glob("data_source/*/perf_result"))
     assert len(prs) == 1

@@ -310,7 +310,7 @@ def mfma_everywhere():
 
 
 @pytest.mark.parametrize("glds", [1, 0])  # B rows by LDS-DMA (default) / through registers
-@pytest.mark.parametrize("N", [16, 32, 64])
+@pytest.mark.parametrize("N", [8, 16, 32, 64])
 @pytest.mark.parametrize("pipe", MFMA_PIPES, ids=lambda p: f"{p[0]}-{p[1]}")
 def test_mfma_rows_match_oracle(pipe, N, glds, mfma_everywhere):
     name, p0, p1 = pipe
@@ -337,7 +337,7 @@ KS_PIPES = [("block_total", 40, 1), ("block_total", 48, 1), ("block_total", 64, 
 
 
 @pytest.mark.parametrize("split", [0, 1, 3])
-@pytest.mark.parametrize("N", [16, 32, 64])
+@pytest.mark.parametrize("N", [8, 16, 24, 32, 64, 128])
 @pytest.mark.parametrize("pipe", KS_PIPES, ids=lambda p: f"{p[0]}-{p[1]}")
 def test_mfma_ks_matches_oracle(pipe, N, split, mfma_everywhere):
     name, p0, p1 = pipe

@@ -142,6 +142,9 @@ def test_hand_derived_fixtures_through_product():
         name = case["pipeline"]
         if name in ("warp_segment", "thread_bit_map"):
             N, p0, p1 = case["p0"], 4, 1  # VW = min(N, 32) = fixture VW
+        elif name in ("tblock_balanced_thread_total", "tblock_thread_total_colpad", "nnz_tblock_bitmap",
+                      "nnz_tblock_warp_bitmap"):
+            N, p0, p1 = 32, case["p0"], case.get("p1", 0)  # the fixture's own parameters
         else:
             N, p0, p1 = back[name]
             if name in ("tblock_warp_total", "balanced_warp_total", "merge_path", "balanced_block_total",
