@@ -299,7 +299,10 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
     batch, owner, load = bt.c5_assignment(args.layers, world)
     seq = bt.rank_sequence(batch, owner, rank)
     t0 = time.perf_counter()
-    plans, launches, _ = bt.build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local)
+    # per-shape plan choice (this rank's shapes, its own matrices), then the batch's plans
+    choice, per_shape = search_shapes(args, torch, gsa, ds, rank, local, dev, sorted({k for (_, _, k, _) in seq}),
+                                      bt.C5_SPARSITY, rocsparse=False)
+    plans, launches, _ = bt.build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, choice=choice)
     t_setup = time.perf_counter() - t0
     stream = torch.cuda.current_stream().cuda_stream
     raw = [(p, r, b.data_ptr(), c.data_ptr()) for (p, r, b, c, _) in launches]
@@ -328,14 +331,16 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
     alg = sum(bt.nnz_of_shape(k) * (e + 2) + (bt.C5_SHAPES[k][0] + 1) * 4 + bt.C5_SHAPES[k][1] * N * e +
               bt.C5_SHAPES[k][0] * N * e for (_, _, k) in batch)
     ms = wall / args.steps * 1e3
-    info = next(iter(plans.values())).info()
     # HBM bytes per step from the PMC passes of scripts/gpu_traffic_c5.sh (per GPU: the LPT
     # split is balanced on nnz); only for the full 48-layer batch it was scaled to
     traffic = None
     tf = os.path.join(ROOT, "profiles", "traffic_c5.json")
+    kinds = {kernel_label(p.info()) for p in plans.values()}
     if os.path.exists(tf) and args.layers == 48:
         try:
-            traffic = int(json.load(open(tf))["hbm_bytes_per_step"] / world)
+            tj = json.load(open(tf))
+            if kinds == {tj.get("kernel")}:  # measured on the same kernels
+                traffic = int(tj["hbm_bytes_per_step"] / world)
         except Exception:
             traffic = None
     out = {
@@ -347,12 +352,14 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
                 "its own HBM copy of A)",
         "config": {"workload": f"OPT-30B weight batch: {args.layers} layers x (4 x 7168^2, 28672x7168, 7168x28672), "
                                f"80% unstructured, fp16, N={N}", "matrices": len(batch), "nnz": total_nnz,
-                   "plan": {k: "%s(%d,%d)" % bt.shape_pipeline(k) for k in plans}, "kernel": kernel_label(info),
+                   "plan": {k: per_shape[k]["plan"] for k in plans},
+                   "kernel": {k: kernel_label(plans[k].info()) for k in plans},
                    "parallelism": f"LPT batch split x{world} (max rank nnz share {max(load) / total_nnz:.4f})"},
         "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9 / world, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / world / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "algorithmic_bytes_per_step": alg, "note": "per GPU, whole step"},
         "setup_s": round(t_setup, 1),
+        "per_shape": {k: {x: v[x] for x in ("plan", "kernel", "kernel_us", "hbm_frac")} for k, v in per_shape.items()},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -360,18 +367,15 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
         p.free()
 
 
-def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
-    """north_star headline (BASELINE.md §4): one OPT-30B decoder layer's six pruned weights
-    (q, k, v, out 7168^2; fc1 28672x7168; fc2 7168x28672) at 70% unstructured, fp16, N=32,
-    one GPU.  Per shape: the plan search over generalsparse_amd.batch.shape_candidates
-    (event time with rotated replicas) and rocSPARSE 7.2 CSR SpMM (fp16 A/B, fp32 C) on the
-    same matrix.  The timed step = the layer's six SpMMs, one plan replica per instance (the
-    layer's A is ~800 MB, past the 256 MB Infinity Cache)."""
+def search_shapes(args, torch, gsa, ds, rank, local, dev, shapes, sp, rocsparse=True):
+    """per shape: every generalsparse_amd.batch.shape_candidates plan timed by events with
+    rotated replicas (the plan search obtain_result.py does), the best kept as the shape's
+    choice; rocSPARSE 7.2 CSR SpMM (fp16 A/B, fp32 C) on the same matrix beside it"""
     from generalsparse_amd import batch as bt
-    N, sp = args.N, args.sparsity
-    e = 2
+    N, e = args.N, 2
     choice, per_shape = {}, {}
-    for k, (m, n) in bt.C5_SHAPES.items():
+    for k in shapes:
+        m, n = bt.C5_SHAPES[k]
         row, col, val = ds.pruned_weight(m, n, sp, bt.shape_seed(rank, k))
         nnz = len(row)
         flops = 2.0 * nnz * N
@@ -399,13 +403,28 @@ def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
             torch.cuda.empty_cache()
         ms, cand, key, kern, reps = best
         choice[k] = cand
-        rs = None if args.no_rocsparse else rocsparse_baseline(m, n, N, row, col, val, min(reps, 20), dtype=1)
+        rs = rocsparse_baseline(m, n, N, row, col, val, min(reps, 20), dtype=1) if rocsparse else None
         per_shape[k] = {"M": m, "K": n, "nnz": nnz, "plan": key, "kernel": kern, "kernel_us": round(ms * 1e3, 2),
                         "gflops": round(flops / (ms * 1e-3) / 1e9, 1),
                         "hbm_frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "variants": variants,
                         "rocsparse_f16": rs,
                         "speedup_vs_rocsparse": round(rs["ms"] / ms, 3) if rs else None}
         del row, col, val
+    return choice, per_shape
+
+
+def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
+    """north_star headline (BASELINE.md §4): one OPT-30B decoder layer's six pruned weights
+    (q, k, v, out 7168^2; fc1 28672x7168; fc2 7168x28672) at 70% unstructured, fp16, N=32,
+    one GPU.  Per shape: the plan search over generalsparse_amd.batch.shape_candidates
+    (event time with rotated replicas) and rocSPARSE 7.2 CSR SpMM (fp16 A/B, fp32 C) on the
+    same matrix.  The timed step = the layer's six SpMMs, one plan replica per instance (the
+    layer's A is ~800 MB, past the 256 MB Infinity Cache)."""
+    from generalsparse_amd import batch as bt
+    N, sp = args.N, args.sparsity
+    e = 2
+    choice, per_shape = search_shapes(args, torch, gsa, ds, rank, local, dev, list(bt.C5_SHAPES), sp,
+                                      rocsparse=not args.no_rocsparse)
     # the timed layer: 4 x attn (replicas 0..3), fc1, fc2
     seq = [(0, s, bt.C5_SLOTS[s], bt.C5_SLOTS[:s].count(bt.C5_SLOTS[s])) for s in range(len(bt.C5_SLOTS))]
     plans, launches, _ = bt.build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, sparsity=sp, choice=choice)

@@ -398,11 +398,20 @@ __global__ __launch_bounds__(256) void k_warp_rows(const uint32_t *__restrict__ 
 
 // ---------------------------------------------------------------------------
 // K6 tblock_total: one 256-thread workgroup per BMTB (fixed row-direction
-// TBLOCK blocking + tblock_total_reduce_operator).  All four waves split each
-// row's nnz (4*S slots), reduce in registers, then across waves through LDS
-// (total_block_reduce_to_one_register_token.cc:374-480 reduces over
-// blockDim.y with __syncthreads; here one LDS round of 4 partials).
+// TBLOCK blocking + tblock_total_reduce_operator; the reference reduces every
+// row of the BMTB over blockDim.y with __syncthreads,
+// total_block_reduce_to_one_register_token.cc:374-480).  Here the BMTB's rows
+// are taken in windows of kBrWindow: the 4S slots (X column lanes each) walk the
+// window's rows slot-per-row and store the short ones (<= kBrSolo nonzeros)
+// directly; longer rows are listed in LDS and then reduced by the whole
+// workgroup (all 4S slots split the row, registers, then one LDS round of four
+// wave partials).  Short-row BMTBs (balanced_block_total on power-law graphs:
+// hundreds of 1-10 nnz rows) cost three barriers per window instead of two per
+// row; long-row BMTBs keep the cooperative path.
 // ---------------------------------------------------------------------------
+constexpr uint32_t kBrWindow = 1024;  // rows per window (the long-row list's capacity)
+constexpr uint32_t kBrSolo = 64;      // a row of at most this many nonzeros is one slot's
+
 template <class VT, class CT, int CF, int SCF, bool FX>
 __device__ __forceinline__ void block_rows_body(const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
                                                     const idx_formula f_row,
@@ -410,12 +419,15 @@ __device__ __forceinline__ void block_rows_body(const uint32_t *__restrict__ bmt
                                                     const CT *__restrict__ col, const VT *__restrict__ val,
                                                     const VT *__restrict__ B, VT *__restrict__ C, uint32_t n_bmtb,
                                                     uint32_t N, uint32_t X, uint32_t row_base,
-                                                    float (*part)[64][CF]) {  // [4][64][CF] in LDS
+                                                    float (*part)[64][CF],  // [4][64][CF] in LDS
+                                                    uint32_t *long_rows,    // [kBrWindow + 1] in LDS
+                                                    uint32_t solo) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wib = threadIdx.x >> 6;
     const uint32_t xl = lane & (X - 1u);
     const uint32_t S = 64u / X;
     const uint32_t slot = wib * S + lane / X;  // 0 .. 4S-1
+    uint32_t *n_long = long_rows + kBrWindow;
     for (uint32_t ct = blockIdx.y; ct * X * CF < N; ct += gridDim.y) {
         const uint32_t cw = ct * X * CF + xl * CF;
         const bool cok = cw < N;
@@ -423,23 +435,45 @@ __device__ __forceinline__ void block_rows_body(const uint32_t *__restrict__ bmt
         for (uint32_t t = xcd_block(blockIdx.x, gridDim.x); t < n_bmtb; t += gridDim.x) {
             uint32_t r_begin, r_end;
             idx_range<FX>(bmtb_first_row, f_row, t, r_begin, r_end);
-            for (uint32_t r = r_begin; r < r_end; r++) {
-                float acc[CF];
+            for (uint32_t w0 = r_begin; w0 < r_end; w0 += kBrWindow) {
+                const uint32_t w1 = min(r_end, w0 + kBrWindow);
+                if (threadIdx.x == 0) *n_long = 0u;
+                __syncthreads();
+                // slot-per-row over the window; long rows are listed
+                for (uint32_t r = w0 + slot; r < w1; r += 4u * S) {
+                    const uint32_t rb = row_ptr[r], re = row_ptr[r + 1];
+                    if (re - rb <= solo) {
+                        float acc[CF];
 #pragma unroll
-                for (int k = 0; k < CF; k++) acc[k] = 0.f;
-                wave_row<VT, CT, CF, SCF>(row_ptr[r], row_ptr[r + 1], col, val, B, N, c0, slot, 4 * S, acc);
-                wave_reduce_slots<CF>(acc, (int)X);
-                if (lane < X) {
-#pragma unroll
-                    for (int k = 0; k < CF; k++) part[wib][lane][k] = acc[k];
+                        for (int k = 0; k < CF; k++) acc[k] = 0.f;
+                        wave_row<VT, CT, CF, SCF>(rb, re, col, val, B, N, c0, 0u, 1u, acc);
+                        if (cok) store_f32<VT, CF>(C + (size_t)(r + row_base) * N + c0, acc);
+                    } else if (xl == 0u) {
+                        long_rows[atomicAdd(n_long, 1u)] = r;
+                    }
                 }
                 __syncthreads();
-                if (wib == 0 && lane < X && cok) {
+                const uint32_t nl = *n_long;
+                for (uint32_t i = 0; i < nl; i++) {  // the window's long rows, the whole workgroup each
+                    const uint32_t r = long_rows[i];
+                    float acc[CF];
 #pragma unroll
-                    for (int k = 0; k < CF; k++) acc[k] = part[0][lane][k] + part[1][lane][k] + part[2][lane][k] + part[3][lane][k];
-                    store_f32<VT, CF>(C + (size_t)(r + row_base) * N + c0, acc);
+                    for (int k = 0; k < CF; k++) acc[k] = 0.f;
+                    wave_row<VT, CT, CF, SCF>(row_ptr[r], row_ptr[r + 1], col, val, B, N, c0, slot, 4 * S, acc);
+                    wave_reduce_slots<CF>(acc, (int)X);
+                    if (lane < X) {
+#pragma unroll
+                        for (int k = 0; k < CF; k++) part[wib][lane][k] = acc[k];
+                    }
+                    __syncthreads();
+                    if (wib == 0 && lane < X && cok) {
+#pragma unroll
+                        for (int k = 0; k < CF; k++) acc[k] = part[0][lane][k] + part[1][lane][k] + part[2][lane][k] + part[3][lane][k];
+                        store_f32<VT, CF>(C + (size_t)(r + row_base) * N + c0, acc);
+                    }
+                    __syncthreads();
                 }
-                __syncthreads();
+                __syncthreads();  // every thread has read n_long before the next window resets it
             }
         }
     }
@@ -449,12 +483,16 @@ template <class VT, class CT, int CF, int SCF>
 __global__ __launch_bounds__(256) void k_block_rows(const uint32_t *__restrict__ bmtb_first_row, const idx_formula f_row,
                                                     const uint32_t *__restrict__ row_ptr, const CT *__restrict__ col,
                                                     const VT *__restrict__ val, const VT *__restrict__ B, VT *__restrict__ C,
-                                                    uint32_t n_bmtb, uint32_t N, uint32_t X, uint32_t row_base) {
+                                                    uint32_t n_bmtb, uint32_t N, uint32_t X, uint32_t row_base,
+                                                    uint32_t solo = kBrSolo) {
     __shared__ float part[4][64][CF];
+    __shared__ uint32_t long_rows[kBrWindow + 1];
     if (f_row.kind == IDX_ARRAY)
-        block_rows_body<VT, CT, CF, SCF, false>(bmtb_first_row, f_row, row_ptr, col, val, B, C, n_bmtb, N, X, row_base, part);
+        block_rows_body<VT, CT, CF, SCF, false>(bmtb_first_row, f_row, row_ptr, col, val, B, C, n_bmtb, N, X, row_base, part,
+                                                long_rows, solo);
     else
-        block_rows_body<VT, CT, CF, SCF, true>(bmtb_first_row, f_row, row_ptr, col, val, B, C, n_bmtb, N, X, row_base, part);
+        block_rows_body<VT, CT, CF, SCF, true>(bmtb_first_row, f_row, row_ptr, col, val, B, C, n_bmtb, N, X, row_base, part,
+                                               long_rows, solo);
 }
 
 // ---------------------------------------------------------------------------
@@ -2276,6 +2314,247 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                 if (!closed_end && slot == 0 && cok) {
 #pragma unroll
                     for (int k = 0; k < CF; k++) rec[(size_t)w * N + c0 + k] = rc[k];
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_merge_rows -- the same merge-path plan (wave ranges wz/wq, compact rows
+// ends/rid, split-row chains) with a two-phase walk per round of R = S*J
+// nonzeros instead of k_merge_path's flag/scan machinery:
+//   1. products: slot s owns the J consecutive nonzeros zb + s*J .. (one vector
+//      load of cols and of vals, J B-row gathers in flight), multiplies them and
+//      writes the fp32 products (X*CF columns per nonzero) to the wave's LDS;
+//   2. rows: the rows meeting the round are dealt to the slots, S at a time; a
+//      slot adds its row's products from LDS (rows of more than `solo` products
+//      are summed by the whole wave, slot-strided, one xor-shuffle reduction)
+//      and stores the row.  The row left open at the round's end carries its
+//      partial into the next round's first row.
+// Row bounds come from two 64-row batches of `ends` loaded at the wave's start
+// (exchanged with shuffles; rows past them are loaded directly).  The head row
+// (open at zlo) and the tail row (open at zhi) join the row's chain exactly as
+// in k_merge_path (agent-scope publish, last arriver combines), or go to
+// head_rec / rec + rec_row for k_merge_fixup when the launch has several column
+// tiles.  Deterministic: every row is summed in a fixed order.
+// ---------------------------------------------------------------------------
+template <int CF>
+__host__ __device__ constexpr uint32_t merge_rows_j() { return CF >= 8 ? 4u : 8u; }
+// fp32 words of one wave's product buffer: R entries of X*CF words + 4 words per slot group
+__host__ __device__ constexpr uint32_t merge_rows_wave_words(uint32_t X, uint32_t CF, uint32_t J) {
+    return (64u / X) * J * X * CF + (64u / X) * 4u;
+}
+
+template <class VT, class CT, int CF>
+__global__ __launch_bounds__(256) void k_merge_rows(const uint32_t *__restrict__ wz,   // n_waves+1
+                                                    const uint32_t *__restrict__ wq,   // n_waves+1
+                                                    const uint32_t *__restrict__ ends, // n_crow
+                                                    const uint32_t *__restrict__ rid,  // n_crow
+                                                    uint32_t n_crow, const CT *__restrict__ col,
+                                                    const VT *__restrict__ val, const VT *__restrict__ B,
+                                                    VT *__restrict__ C, float *__restrict__ rec,
+                                                    uint32_t *__restrict__ rec_row, float *__restrict__ head_rec,
+                                                    uint32_t n_waves, uint32_t N, uint32_t X,
+                                                    const uint32_t *__restrict__ empty_rows, uint32_t n_empty,
+                                                    uint32_t fill_blocks,
+                                                    const uint32_t *__restrict__ chain,  // 2 n_waves or null
+                                                    uint32_t *__restrict__ chain_cnt,    // n_waves, zero between launches
+                                                    uint32_t solo) {
+    constexpr uint32_t J = merge_rows_j<CF>();
+    const uint32_t lb = blockIdx.x;
+    if (lb < fill_blocks) {  // empty rows, as in k_merge_path
+        const uint32_t rbytes = N * (uint32_t)sizeof(VT);
+        const uint32_t U = rbytes % 16u == 0 ? rbytes / 16u : N;
+        const uint32_t tot = blockIdx.y == 0 ? n_empty * U : 0u;
+        for (uint32_t i = lb * blockDim.x + threadIdx.x; i < tot; i += fill_blocks * blockDim.x) {
+            const uint32_t er = empty_rows[i / U];
+            if (rbytes % 16u == 0)
+                *reinterpret_cast<uint4 *>(reinterpret_cast<unsigned char *>(C) + (size_t)er * rbytes + (i % U) * 16u) =
+                    make_uint4(0u, 0u, 0u, 0u);
+            else
+                C[(size_t)er * N + i % U] = (VT)0.f;
+        }
+        return;
+    }
+    extern __shared__ float mr_lds[];
+    const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
+    const uint32_t xl = lane & (X - 1u), slot = lane / X, S = 64u / X;
+    const uint32_t R = S * J, TW = X * CF;
+    float *P = mr_lds + wib * merge_rows_wave_words(X, CF, J);
+    // float offset of product entry e (this lane's columns); 4 words of padding per slot group
+    auto pofs = [&](uint32_t e) { return e * TW + (e / J) * 4u + xl * CF; };
+    const uint32_t waves_total = (gridDim.x - fill_blocks) * (blockDim.x >> 6);
+    const uint64_t slot_bits = X >= 64u ? ~0ull : ((1ull << X) - 1ull);
+    typedef typename raw_vec<CF * sizeof(VT)>::t RB;
+    for (uint32_t ct = blockIdx.y; ct * X * CF < N; ct += gridDim.y) {
+        const uint32_t cw = ct * X * CF + xl * CF;
+        const bool cok = cw < N;
+        const uint32_t c0 = cok ? cw : 0u;
+        for (uint32_t w = (lb - fill_blocks) * (blockDim.x >> 6) + wib; w < n_waves; w += waves_total) {
+            const uint32_t zlo = wz[w], zhi = wz[w + 1], q0 = wq[w], qn = wq[w + 1];
+            const uint32_t zb0 = zlo & ~(J - 1u);
+            // A entries of the first round, and the first 128 rows' ends
+            CT cn[J];
+            VT vn[J];
+            auto load_a = [&](uint32_t zb_) {
+                const uint32_t b_ = zb_ + J * slot;
+                if (b_ < zhi) {
+                    load_raw<CT, (int)J>(col + b_, cn);
+                    load_raw<VT, (int)J>(val + b_, vn);
+                } else {
+#pragma unroll
+                    for (uint32_t k = 0; k < J; k++) { cn[k] = 0; vn[k] = (VT)0.f; }
+                }
+            };
+            load_a(zb0);
+            const uint32_t e0 = q0 + lane < n_crow ? ends[q0 + lane] : 0xffffffffu;
+            const uint32_t e1 = q0 + 64u + lane < n_crow ? ends[q0 + 64u + lane] : 0xffffffffu;
+            const uint32_t sq0 = q0 ? ends[q0 - 1u] : 0u;
+            // end of wave row i (row q0 + i); i may differ per lane
+            auto row_end = [&](uint32_t i) -> uint32_t {
+                const uint32_t a0 = (uint32_t)__shfl((int)e0, (int)(i & 63u), 64);
+                const uint32_t a1 = (uint32_t)__shfl((int)e1, (int)(i & 63u), 64);
+                if (i < 64u) return a0;
+                if (i < 128u) return a1;
+                return q0 + i < n_crow ? ends[q0 + i] : 0xffffffffu;
+            };
+            const bool head_open = zlo > sq0;
+            const uint32_t q_last = (qn < n_crow && (qn ? ends[qn - 1] : 0u) < zhi) ? qn : qn - 1u;
+            const bool tail_open = ends[q_last] > zhi;
+            bool head_mine = false;
+            float carry[CF];
+#pragma unroll
+            for (int k = 0; k < CF; k++) carry[k] = 0.f;
+            uint32_t qi0 = 0;  // wave row index of the round's first row
+            for (uint32_t zb = zb0; zb < zhi; zb += R) {
+                const uint32_t zl = max(zb, zlo), ze = min(zb + R, zhi);
+                CT cc[J];
+                VT vv[J];
+#pragma unroll
+                for (uint32_t k = 0; k < J; k++) { cc[k] = cn[k]; vv[k] = vn[k]; }
+                RB braw[J];
+#pragma unroll
+                for (uint32_t k = 0; k < J; k++) {
+                    const uint32_t z = zb + J * slot + k;
+                    const bool valid = z >= zl && z < ze;
+                    braw[k] = *reinterpret_cast<const RB *>(B + (size_t)(valid ? (uint32_t)cc[k] : 0u) * N + c0);
+                }
+                if (zb + R < zhi) load_a(zb + R);
+#pragma unroll
+                for (uint32_t k = 0; k < J; k++) {
+                    const uint32_t z = zb + J * slot + k;
+                    const float v = (z >= zl && z < ze) ? (float)vv[k] : 0.f;
+                    VT bt[CF];
+                    __builtin_memcpy(bt, &braw[k], sizeof(RB));
+                    float pr[CF];
+#pragma unroll
+                    for (int i = 0; i < CF; i++) pr[i] = v * (float)bt[i];
+                    float *dst = P + pofs(J * slot + k);
+                    if constexpr (CF % 4 == 0) {
+#pragma unroll
+                        for (int i = 0; i < CF; i += 4)
+                            *reinterpret_cast<float4 *>(dst + i) = make_float4(pr[i], pr[i + 1], pr[i + 2], pr[i + 3]);
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < CF; i++) dst[i] = pr[i];
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                // rows meeting [zl, ze), S at a time
+                for (uint32_t bi = qi0;; bi += S) {
+                    const uint32_t i = bi + slot;
+                    const uint32_t q = q0 + i;
+                    // (both shuffles with every lane active: a shuffle reads only active lanes)
+                    const uint32_t en_ = row_end(i), st_ = row_end(i ? i - 1u : 0u);
+                    const uint32_t en = q < n_crow ? en_ : 0xffffffffu;
+                    const uint32_t st = i == 0u ? sq0 : st_;
+                    const bool active = q < n_crow && st < ze;
+                    const uint32_t rs = active ? max(st, zl) - zb : 0u, re = active ? min(en, ze) - zb : 0u;
+                    const bool is_long = re - rs > solo;
+                    float acc[CF];
+#pragma unroll
+                    for (int k = 0; k < CF; k++) acc[k] = 0.f;
+                    if (active && !is_long) {
+                        for (uint32_t e = rs; e < re; e++) {
+                            const float *src = P + pofs(e);
+#pragma unroll
+                            for (int k = 0; k < CF; k++) acc[k] += src[k];
+                        }
+                    }
+                    uint64_t lm = __ballot(is_long);
+                    while (lm) {  // long rows: the whole wave, slot-strided, one at a time
+                        const uint32_t l = (uint32_t)__builtin_ctzll(lm);
+                        lm &= ~(slot_bits << l);
+                        const uint32_t lrs = (uint32_t)__shfl((int)rs, (int)l, 64), lre = (uint32_t)__shfl((int)re, (int)l, 64);
+                        float a2[CF];
+#pragma unroll
+                        for (int k = 0; k < CF; k++) a2[k] = 0.f;
+                        for (uint32_t e = lrs + slot; e < lre; e += S) {
+                            const float *src = P + pofs(e);
+#pragma unroll
+                            for (int k = 0; k < CF; k++) a2[k] += src[k];
+                        }
+                        wave_reduce_slots<CF>(a2, (int)X);
+                        if (slot == l / X) {
+#pragma unroll
+                            for (int k = 0; k < CF; k++) acc[k] = a2[k];
+                        }
+                    }
+                    if (bi == qi0 && slot == 0u) {  // the row carried in from the previous round
+#pragma unroll
+                        for (int k = 0; k < CF; k++) acc[k] += carry[k];
+                    }
+                    const bool closes = active && en <= ze;
+                    if (closes) {
+                        if (q == q0 && head_open) {
+                            if (chain) {
+                                merge_chain_publish<CF>(acc, head_rec, w, N, c0, cok);
+                                head_mine = true;
+                            } else if (cok) {
+#pragma unroll
+                                for (int k = 0; k < CF; k++) head_rec[(size_t)w * N + c0 + k] = acc[k];
+                            }
+                        } else if (cok) {
+                            store_f32<VT, CF>(C + (size_t)rid[q] * N + c0, acc);
+                        }
+                    }
+                    const uint64_t om = __ballot(active && !closes);  // the row left open at ze
+                    const uint64_t am = __ballot(active);
+                    if (om) {
+                        const uint32_t l = (uint32_t)__builtin_ctzll(om);
+#pragma unroll
+                        for (int k = 0; k < CF; k++) carry[k] = __shfl(acc[k], (int)((l & ~(X - 1u)) + xl), 64);
+                        qi0 = bi + l / X;
+                        break;
+                    }
+                    if (am != ~0ull) {  // the round's rows are done; the next round opens a new row
+#pragma unroll
+                        for (int k = 0; k < CF; k++) carry[k] = 0.f;
+                        qi0 = bi + (uint32_t)__builtin_popcountll(am) / X;
+                        break;
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            // carry = the tail row's partial when the wave ends inside a row
+            if (chain) {
+                if (head_mine && !(head_open && tail_open && q_last == q0))
+                    merge_chain_arrive<VT, CF>(w, chain[n_waves + w], rec, head_rec, chain_cnt, rid[q0], C, N, c0, cok,
+                                               lane - xl);
+                if (tail_open && slot == 0u) {
+                    const uint32_t cw_ = chain[w];  // the wave closing the row
+                    merge_chain_publish<CF>(carry, rec, w, N, c0, cok);
+                    merge_chain_arrive<VT, CF>(cw_, chain[n_waves + cw_], rec, head_rec, chain_cnt, rid[q_last], C, N, c0,
+                                               cok, 0u);
+                }
+            } else {
+                if (lane == 0) rec_row[w] = tail_open ? rid[q_last] : 0xffffffffu;
+                if (tail_open && slot == 0u && cok) {
+#pragma unroll
+                    for (int k = 0; k < CF; k++) rec[(size_t)w * N + c0 + k] = carry[k];
                 }
             }
         }

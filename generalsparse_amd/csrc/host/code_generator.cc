@@ -33,7 +33,7 @@ const char *kernel_family_name(int f) {
         case KF_BLOCK_TOTAL: return "k_block_rows";
         case KF_BITMAP_SEGMENT: return "k_bitmap_segment";
         case KF_ROW_CHUNKS: return "k_row_chunks";
-        case KF_MERGE_PATH: return "k_merge_path";
+        case KF_MERGE_PATH: return "k_merge_path";  // the family; MP_ROWS picks the k_merge_rows walk
         default: return "none";
     }
 }
@@ -481,10 +481,17 @@ std::string code_generator::generate_gather_source(int repeat) const {
               << "    const uint32_t n_units = lay.wz.size() - 1, n_crow = lay.ends.size(); const bool al = true;\n"
               << "    float *d_r0, *d_r1; uint32_t *d_rr; hipMalloc(&d_r0, n_units * N * 4); hipMalloc(&d_r1, n_units * N * 4);\n"
               << "    hipMalloc(&d_rr, n_units * 4);\n";
-            launch = "gsk::k_merge_path<VT, uint32_t, CF><<<dim3((n_units + 3) / 4 + 64, tiles), 256, "
-                     "4 * gsk::merge_path_wave_lds_words(64 / X) * 4>>>(d_a0, d_a1, d_a2, d_a3, n_crow, d_col, d_val, d_B, d_C, "
-                     "d_r0, d_rr, d_r1, n_units, N, X, 0, (uint32_t)M, d_a4, (uint32_t)lay.empty.size(), 64u, nullptr, nullptr); "
-                     "gsk::k_merge_fixup<VT><<<dim3((n_units * N + 255) / 256), 256>>>(d_rr, d_r0, d_r1, d_C, n_units, N)";
+            if (get_config().MP_ROWS)  // the walk gs_spmm runs (device_plan.hip fixes it at upload)
+                launch = "gsk::k_merge_rows<VT, uint32_t, CF><<<dim3((n_units + 3) / 4 + 64, tiles), 256, "
+                         "4 * gsk::merge_rows_wave_words(X, CF, gsk::merge_rows_j<CF>()) * 4>>>(d_a0, d_a1, "
+                         "d_a2, d_a3, n_crow, d_col, d_val, d_B, d_C, d_r0, d_rr, d_r1, n_units, N, X, d_a4, "
+                         "(uint32_t)lay.empty.size(), 64u, nullptr, nullptr, " + std::to_string(std::max<int64_t>(1, get_config().MP_SOLO)) + "u); "
+                         "gsk::k_merge_fixup<VT><<<dim3((n_units * N + 255) / 256), 256>>>(d_rr, d_r0, d_r1, d_C, n_units, N)";
+            else
+                launch = "gsk::k_merge_path<VT, uint32_t, CF><<<dim3((n_units + 3) / 4 + 64, tiles), 256, "
+                         "4 * gsk::merge_path_wave_lds_words(64 / X) * 4>>>(d_a0, d_a1, d_a2, d_a3, n_crow, d_col, d_val, d_B, d_C, "
+                         "d_r0, d_rr, d_r1, n_units, N, X, 0, (uint32_t)M, d_a4, (uint32_t)lay.empty.size(), 64u, nullptr, nullptr); "
+                         "gsk::k_merge_fixup<VT><<<dim3((n_units * N + 255) / 256), 256>>>(d_rr, d_r0, d_r1, d_C, n_units, N)";
             break;
         }
         default:

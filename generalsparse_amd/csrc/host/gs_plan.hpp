@@ -47,6 +47,8 @@ struct device_plan {
                         // (t0 BMTB rows, tcol/tval groups; ks_ns k-steps per range,
                         // RT in maxr, MAXG in seg_cap, ws slabs + t2 arrivals when ksplit > 1)
     uint32_t ks_ns = 0, ks_gcap = 0;
+    bool mp_rows = false;   // merge-path plans: k_merge_rows (fixed at upload, MP_ROWS), else k_merge_path
+    uint32_t mp_solo = 16;  // k_merge_rows: slot-alone row length (MP_SOLO)
     // k_mfma_rows variant fixed at upload (device_layout.cc): GLDS / B ring depth / compute
     // waves / entry groups per thread -- the launch uses these, not the config of the moment
     int mfma_glds = 2, mfma_nbg = 3, mfma_wct = 6, mfma_maxa = 1;  // k_mfma_ks: k-steps per K range, entry groups per step

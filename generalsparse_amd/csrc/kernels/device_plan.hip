@@ -580,6 +580,12 @@ void upload_plan(plan_state &p, int dtype, int device) {
             a.t1 = dev_copy(d, lay.chain);                                 // split-row chains
             a.t2 = dev_copy(d, std::vector<uint32_t>(d.n_units, 0u));     // their arrival counters
             d.scf = 8;
+            {
+                const config_t cfg = get_config();
+                d.mp_rows = cfg.MP_ROWS;
+                d.mp_solo = (uint32_t)std::max<int64_t>(1, cfg.MP_SOLO);
+                d.kernel = d.mp_rows ? "k_merge_rows" : "k_merge_path";
+            }
             break;
         }
         default:

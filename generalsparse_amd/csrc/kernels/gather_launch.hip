@@ -157,10 +157,17 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
             const uint32_t fb = d.n_fin ? (uint32_t)std::min<uint64_t>(256, (d.n_fin * N / 4 + 1023) / 1024) : 0u;
             // one column tile: split rows are combined inside the launch (chain arrivals)
             const bool fused = tiles == 1 && !(mp_debug() & 4u);
-            hipLaunchKernelGGL((gsk::k_merge_path<VT, CT, CF>), dim3(gx + fb, tiles), dim3(256), lds, s, a.a0, a.a1,
-                               a.a2, a.a3, (uint32_t)d.n_rows_aux, col, val, B, C, a.ws, a.t0, a.ws2, W, N, X, row_base,
-                               (uint32_t)d.n_out_rows, a.a4, (uint32_t)d.n_fin, fb, fused ? a.t1 : nullptr,
-                               fused ? a.t2 : nullptr, mp_debug());
+            if (d.mp_rows)
+                hipLaunchKernelGGL((gsk::k_merge_rows<VT, CT, CF>), dim3(gx + fb, tiles), dim3(256),
+                                   (size_t)4 * gsk::merge_rows_wave_words(X, CF, gsk::merge_rows_j<CF>()) * sizeof(float), s, a.a0,
+                                   a.a1, a.a2, a.a3, (uint32_t)d.n_rows_aux, col, val, B, C, a.ws, a.t0, a.ws2, W, N, X,
+                                   a.a4, (uint32_t)d.n_fin, fb, fused ? a.t1 : nullptr, fused ? a.t2 : nullptr,
+                                   d.mp_solo);
+            else
+                hipLaunchKernelGGL((gsk::k_merge_path<VT, CT, CF>), dim3(gx + fb, tiles), dim3(256), lds, s, a.a0, a.a1,
+                                   a.a2, a.a3, (uint32_t)d.n_rows_aux, col, val, B, C, a.ws, a.t0, a.ws2, W, N, X, row_base,
+                                   (uint32_t)d.n_out_rows, a.a4, (uint32_t)d.n_fin, fb, fused ? a.t1 : nullptr,
+                                   fused ? a.t2 : nullptr, mp_debug());
             HIP_OK(hipGetLastError());
             if (fused) break;
             GS_CHECK((uint64_t)W * N < 0xffffffffull, "merge-path fix-up indices exceed 32 bits");

@@ -74,7 +74,7 @@ def device_kernel(d):
     """the kernel a generated program launches (from its source)"""
     src = open(os.path.join(d, "kernel_file.hip")).read()
     for k in ("k_mfma_ks", "k_mfma_rows", "k_nm_mfma", "k_thread_total", "k_warp_rows", "k_block_rows",
-              "k_bitmap_segment", "k_row_chunks", "k_merge_path"):
+              "k_bitmap_segment", "k_row_chunks", "k_merge_rows", "k_merge_path"):
         if f"gsk::{k}<" in src:
             return k
     return "?"

@@ -84,6 +84,31 @@ def test_known_answer_all_ones(pipe, dtype):
     np.testing.assert_array_equal(C, np.repeat(nnz_row[:, None], N, axis=1))
 
 
+@pytest.mark.parametrize("dtype", ["f32", "f16"])
+@pytest.mark.parametrize("N", [8, 32])
+@pytest.mark.parametrize("pipe", [("block_total", 2500, 1), ("balanced_block_total", 2048, 1),
+                                  ("block_total", 1024, 1)], ids=lambda p: f"{p[0]}-{p[1]}")
+def test_block_rows_short_and_long_rows(pipe, N, dtype):
+    """k_block_rows: slot-per-row walks of short rows, the workgroup-wide reduction of
+    rows over kBrSolo nonzeros, and BMTBs of more than one 1024-row window"""
+    name, p0, p1 = pipe
+    M = K = 3000
+    row, col, val = ds.rmat(M, 24000, seed=5)
+    # a few long rows (> 64 nnz) in the middle of short ones
+    extra_r = np.repeat(np.array([17, 1100, 2999], np.uint64), 300)
+    extra_c = np.tile(np.arange(300, dtype=np.uint64) * 9, 3)
+    keep = ~np.isin(row, [17, 1100, 2999])
+    row = np.concatenate([row[keep], extra_r])
+    col = np.concatenate([col[keep], extra_c])
+    val = np.concatenate([val[keep], np.linspace(-1, 1, len(extra_r)).astype(np.float32)])
+    o = np.lexsort((col, row))
+    row, col, val = row[o], col[o], val[o]
+    plan, C, B = run(M, K, row, col, val, name, p0, p1, N, dtype)
+    assert plan.info()["device_kernel"] == "k_block_rows"
+    v = val.astype(np.float16).astype(np.float32) if dtype == "f16" else val
+    check(C, ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64"), dtype)
+
+
 # col-direction pipelines (K5 warp_bit_map / K7 tblock_bit_map): BMTs are 64-nnz
 # chunks of one row, so the cases need rows long enough for the padding rule
 COL_PIPES = [("warp_bit_map", 4, 1), ("tblock_bit_map", 4, 1), ("warp_bit_map_interleaved", 4, 1),
@@ -518,21 +543,32 @@ def merge_cases():
     yield "diag", 2048, 2048, rows, rows.copy(), np.linspace(-1, 1, 2048).astype(np.float32)
 
 
+@pytest.fixture(params=[0, 1], ids=["k_merge_path", "k_merge_rows"])
+def merge_walk(request):
+    """both merge-path walks (MP_ROWS fixes the kernel at upload)"""
+    gsa.set_config("MP_ROWS", request.param)
+    yield "k_merge_rows" if request.param else "k_merge_path"
+    gsa.set_config("MP_ROWS", 0)
+
+
 @pytest.mark.parametrize("dtype", ["f32", "f16"])
 @pytest.mark.parametrize("N", [8, 3, 64])
 @pytest.mark.parametrize("ws,level", [(1024, 1), (37, 1), (1, 3), (512, 2), (100000, 1)])
-def test_merge_path_matches_oracle(ws, level, N, dtype):
+def test_merge_path_matches_oracle(ws, level, N, dtype, merge_walk):
     for case, M, K, row, col, val in merge_cases():
         plan, C, B = run(M, K, row, col, val, "merge_path", ws, level, N, dtype)
         assert plan.info()["kernel_name"].startswith("k_merge_path"), plan.info()["kernel_name"]
+        assert plan.info()["device_kernel"] == merge_walk
         v = val.astype(np.float16).astype(np.float32) if dtype == "f16" else val
         ref = ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64")
         check(C, ref, dtype)
 
 
-def test_merge_path_deterministic_and_no_stale_state():
-    """two launches give bit-identical C (no atomics; carries re-written every launch),
-    and C's prior content (NaN) is fully overwritten, empty rows included"""
+def test_merge_path_deterministic_and_no_stale_state(merge_walk):
+    """two launches give bit-identical C (no floating-point atomics: a split row's partials
+    are combined in wave order by the last arriver on an integer arrival counter, and the
+    carries are re-written every launch), and C's prior content (NaN) is fully overwritten,
+    empty rows included"""
     _, M, K, row, col, val = next(merge_cases())
     plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline("merge_path", 8, 64, 1).compile().upload("f32", 0)
     B = torch.from_numpy(np.random.default_rng(4).uniform(-1, 1, (K, 8)).astype(np.float32)).to(DEV)
