@@ -1427,7 +1427,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         __syncthreads();
         uint32_t *flag = reinterpret_cast<uint32_t *>(lds + oD + NDI * szD + 512);
         if (tid == 0)
-            *flag = __hip_atomic_fetch_add(&arrivals[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *flag = __hip_atomic_fetch_add(&arrivals[g], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
         if (*flag == nsplit - 1u) {
             if (tid == 0) __hip_atomic_store(&arrivals[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1706,7 +1706,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
     __syncthreads();
     uint32_t *flag = reinterpret_cast<uint32_t *>(lds + (size_t)WR * NI * 16u);
     uint32_t *arr = arrivals + (size_t)g * gridDim.y + blockIdx.y;
-    if (tid == 0) *flag = __hip_atomic_fetch_add(arr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) *flag = __hip_atomic_fetch_add(arr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (*flag != S - 1u) {
         GS_KS_STAMP(22u);
@@ -2041,7 +2041,7 @@ __device__ __forceinline__ void merge_chain_arrive(uint32_t close, uint32_t firs
                                                    uint32_t lane0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t old = 0;
-    if ((threadIdx.x & 63u) == lane0) old = __hip_atomic_fetch_add(cnt + close, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((threadIdx.x & 63u) == lane0) old = __hip_atomic_fetch_add(cnt + close, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     old = __shfl(old, (int)lane0, 64);
     if (old + 1u != close - first + 1u) return;
     if (cok) {

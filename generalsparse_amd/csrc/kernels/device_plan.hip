@@ -605,9 +605,18 @@ void upload_plan(plan_state &p, int dtype, int device) {
     p.uploaded = true;
 }
 
+// The deferred CSR of a matrix-core plan, uploaded the first time the plan runs at a dense
+// width other than the one its tiles were built for.  Synchronous (hipMalloc + hipMemcpy),
+// so refused inside stream capture (launch_body); the caller's current device is restored.
 void ensure_csr(plan_state &p) {
+    bool need = false;
+    for (device_arrays &a : p.dev.replicas) need |= !a.col;
+    if (!need) return;
+    int prev = 0;
+    HIP_OK(hipGetDevice(&prev));
     for (device_arrays &a : p.dev.replicas)
         if (!a.col) upload_csr(p, a);
+    HIP_OK(hipSetDevice(prev));
 }
 
 void add_replica(plan_state &p) {
@@ -685,7 +694,14 @@ static void launch_body(plan_state &p, int replica, const void *B, void *C, uint
         launch_mfma(p, p.dev.replicas[replica], B, C, N, stream);
         return;
     }
-    if (!p.dev.replicas[replica].col) ensure_csr(p);  // matrix-core plan at another dense width
+    if (!p.dev.replicas[replica].col) {  // matrix-core plan at another dense width
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        HIP_OK(hipStreamIsCapturing(stream, &cs));
+        GS_CHECK(cs == hipStreamCaptureStatusNone,
+                 "the first gs_spmm of a matrix-core plan at N != its tile width uploads its CSR "
+                 "synchronously: run it once outside stream capture");
+        ensure_csr(p);
+    }
     launch_gather(p, p.dev.replicas[replica], B, C, N, stream);
 }
 
