@@ -1427,7 +1427,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         __syncthreads();
         uint32_t *flag = reinterpret_cast<uint32_t *>(lds + oD + NDI * szD + 512);
         if (tid == 0)
-            *flag = __hip_atomic_fetch_add(&arrivals[g], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            *flag = __hip_atomic_fetch_add(&arrivals[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
         if (*flag == nsplit - 1u) {
             if (tid == 0) __hip_atomic_store(&arrivals[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1706,7 +1706,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
     __syncthreads();
     uint32_t *flag = reinterpret_cast<uint32_t *>(lds + (size_t)WR * NI * 16u);
     uint32_t *arr = arrivals + (size_t)g * gridDim.y + blockIdx.y;
-    if (tid == 0) *flag = __hip_atomic_fetch_add(arr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) *flag = __hip_atomic_fetch_add(arr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (*flag != S - 1u) {
         GS_KS_STAMP(22u);
@@ -2025,6 +2025,14 @@ constexpr uint32_t kMpItems = 8;  // nonzeros per slot per round
 // first lane bumps the closing wave's counter.  The arrival that completes the chain
 // (parts = close - first + 1) sums rec[first .. close-1] and head_rec[close] in wave
 // order with agent-scope loads, writes the row and re-arms the counter.
+// Ordering: every access of the hand-off is an agent-scope atomic (sc1: written through
+// to / read from the memory-side coherence point, no stale XCD-L2 copy), and the
+// publisher's vmcnt(0) retires its stores before its counter add is issued; the reader
+// loads only after its add returned the completing count (a control dependency).  That
+// is MI355X_MICROARCH.md §Workgroup dispatch's hand-off form.  The language-level form
+// (acq_rel on the add) is not used: on gfx950 an agent-scope release is a
+// buffer_wbl2 sc1 (write-back of the XCD's whole L2) and the acquire a buffer_inv sc1,
+// per arrival -- measured C4 merge_path(1024) 49 -> 84 us, r03 session 1.
 template <int CF>
 __device__ __forceinline__ void merge_chain_publish(const float (&a)[CF], float *part, uint32_t src, uint32_t N,
                                                     uint32_t c0, bool cok) {
@@ -2041,7 +2049,7 @@ __device__ __forceinline__ void merge_chain_arrive(uint32_t close, uint32_t firs
                                                    uint32_t lane0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t old = 0;
-    if ((threadIdx.x & 63u) == lane0) old = __hip_atomic_fetch_add(cnt + close, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if ((threadIdx.x & 63u) == lane0) old = __hip_atomic_fetch_add(cnt + close, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     old = __shfl(old, (int)lane0, 64);
     if (old + 1u != close - first + 1u) return;
     if (cok) {

@@ -117,7 +117,19 @@ def test_c5_batch_sequence_two_gloo_ranks(layers):
     assert max(res[0][1]) / min(res[0][1]) <= (1.02 if layers == 48 else 1.5)
 
 
-def _shard_main(rank, world, port, mode, out):
+def _hip_spmm(M, K, N, row, col, val, B, dtype, pipeline, p0):
+    """C = A B through the HIP library on cuda:0 (a gs plan of the shard's COO), on the host"""
+    import generalsparse_amd as gsa
+    plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline(pipeline, N, p0, 1).compile().upload(dtype, 0)
+    tdt = torch.float16 if dtype == "f16" else torch.float32
+    C = plan.spmm(torch.from_numpy(B).to("cuda:0", tdt))
+    torch.cuda.synchronize()
+    out = C.cpu()
+    plan.free()
+    return out
+
+
+def _shard_main(rank, world, port, mode, out, hip=False):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -137,12 +149,22 @@ def _shard_main(rank, world, port, mode, out):
     shards = (sd.nnz_exact_shards if mode == "nnz" else sd.balanced_row_shards)(row, M, world)
     sh = shards[rank]
     m, r, c, v = sd.local_coo(row, col, val, sh)
-    C_local = torch.from_numpy(ofi.spmm_ref(m, N, r, c, v, B, "f64").astype(np.float32)) if m else torch.zeros((0, N))
+    if hip:
+        # the GPU path: the shard's plan (fp16 for nnz shards, fp32 for row shards) on the
+        # HIP library; the fp32 edge partials from a 2-row fp32 side plan, as bench.py does
+        dt = "f16" if mode == "nnz" else "f32"
+        Bx = B.astype(np.float16).astype(np.float32) if dt == "f16" else B
+        C_local = _hip_spmm(m, 500, N, r, c, v, Bx, dt, "merge_path", 64) if m else torch.zeros((0, N))
+    else:
+        C_local = torch.from_numpy(ofi.spmm_ref(m, N, r, c, v, B, "f64").astype(np.float32)) if m else torch.zeros((0, N))
     edges = None
     if mode == "nnz" and m:
         er, ec, ev = sd.edge_rows(row, col, val, sh)
-        edges = torch.from_numpy(ofi.spmm_ref(2, N, er, ec, ev, B, "f64").astype(np.float32))
-        C_local = C_local.half()   # an fp16 plan's output; the split rows use the fp32 edge partials
+        if hip:
+            edges = _hip_spmm(2, 500, N, er, ec, ev, B.astype(np.float16).astype(np.float32), "f32", "merge_path", 64)
+        else:
+            edges = torch.from_numpy(ofi.spmm_ref(2, N, er, ec, ev, B, "f64").astype(np.float32))
+            C_local = C_local.half()   # an fp16 plan's output; the split rows use the fp32 edge partials
     first = sd.combine_boundaries(C_local, shards, rank, dist, torch, edges) if mode == "nnz" else 0
     C_local = C_local.float()
     out[rank] = (sh.row_lo + first, C_local[first:].numpy().copy(), sh.z1 - sh.z0)
@@ -150,18 +172,13 @@ def _shard_main(rank, world, port, mode, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["rows", "nnz"])
-@pytest.mark.parametrize("world", [2, 3])
-def test_single_matrix_shards_combine_to_full_spmm(mode, world):
-    """one matrix over `world` gloo ranks: balanced row ranges (no exchange) or
-    nnz-exact ranges (split rows combined by one all-reduce), reassembled rows equal
-    the unsharded oracle SpMM"""
+def _check_shards(mode, world, hip):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi as ofi
     port = _free_port()
     with mp.Manager() as man:
         out = man.dict()
-        mp.spawn(_shard_main, args=(world, port, mode, out), nprocs=world, join=True)
+        mp.spawn(_shard_main, args=(world, port, mode, out, hip), nprocs=world, join=True)
         res = dict(out)
     M, N = 3000, 8
     rng = np.random.default_rng(5)
@@ -172,6 +189,8 @@ def test_single_matrix_shards_combine_to_full_spmm(mode, world):
     col = rng.integers(0, 500, len(row)).astype(np.uint64)
     val = rng.uniform(-1, 1, len(row)).astype(np.float32)
     B = rng.uniform(-1, 1, (500, N)).astype(np.float32)
+    if hip and mode == "nnz":
+        B = B.astype(np.float16).astype(np.float32)   # the fp16 plan's B
     ref = ofi.spmm_ref(M, N, row, col, val, B, "f64")
     got = np.zeros((M, N))
     seen = np.zeros(M, int)
@@ -183,12 +202,31 @@ def test_single_matrix_shards_combine_to_full_spmm(mode, world):
     held = seen > 0
     assert (seen <= 1).all()
     tol = 1e-3 if mode == "nnz" else 1e-5   # nnz mode: fp16 rows, split rows rounded once after the fp32 sum
+    if hip and mode == "nnz":
+        tol = 4e-3                           # fp16 values of the plan; fp32 accumulation on the device
     np.testing.assert_allclose(got[held], ref[held], rtol=tol, atol=tol)
-    if mode == "nnz":
+    if mode == "nnz" and not hip:
         long_row = got[100]    # split over every rank: exactly the fp16 rounding of the fp32 sum
         np.testing.assert_array_equal(long_row, ref[100].astype(np.float32).astype(np.float16).astype(np.float64))
     # rows no rank holds are the trailing empty rows (zero in the full product)
     assert np.all(ref[~held] == 0)
+
+
+@pytest.mark.parametrize("mode", ["rows", "nnz"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_single_matrix_shards_combine_to_full_spmm(mode, world):
+    """one matrix over `world` gloo ranks: balanced row ranges (no exchange) or
+    nnz-exact ranges (split rows combined by one all-reduce), reassembled rows equal
+    the unsharded oracle SpMM"""
+    _check_shards(mode, world, hip=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["rows", "nnz"])
+def test_single_matrix_shards_hip_local_spmm(mode):
+    """the same over two gloo ranks whose local SpMM (and fp32 edge partials) run on the
+    HIP library on cuda:0 -- the product path of every rank, combined on the host"""
+    _check_shards(mode, 2, hip=True)
 
 
 def test_row_block_rows_fill_whole_cu_rounds():
