@@ -117,7 +117,7 @@ WORKLOADS["c2"]["dtype"] = "f16"
 # (pipeline, p0, p1).  tblock_warp_total(rows per BMTB, rows per BMW) runs the
 # LDS-stationary-B kernel when its BMTBs fit one workgroup; the others are the
 # reference's token_test plans on the gather kernels.
-CANDIDATES = [("block_total", 20, 1), ("block_total", 10, 1), ("block_total", 40, 1),
+CANDIDATES = [("block_total", 20, 1), ("block_total", 10, 1), ("block_total", 40, 1), ("block_total", 80, 1),
               ("tblock_warp_total", 20, 2), ("tblock_warp_total", 4, 1), ("warp_segment", 4, 1),
               ("thread_total", 4, 1)]
 

@@ -39,6 +39,42 @@ GSK_HD constexpr size_t ks_lds_bytes(uint32_t CT, uint32_t RT, uint32_t W) {
     return stage > red ? stage : red;
 }
 
+// k_mfma_bm: per (row block, K range, 32-column k-step) one 8-byte record per lane (RT <= 6
+// mask bytes, u16 value offset in bytes 6..7); B by LDS-DMA into NBT k-step slots per wave.
+// NBT (k-steps a wave keeps in flight): the value windows take 4 VGPRs per tile per step
+// (<= ~100 VGPRs), the slots W * NBT * 1 KB * CT of LDS.  bm_sel: the v_perm_b32 selector
+// that expands the packed halves of mask nibble n into output halves 2w, 2w+1 (0x0c: zero)
+GSK_HD constexpr uint32_t bm_nbt(uint32_t CT, uint32_t RT) {
+    const uint32_t by_vgpr = 25u / RT < 12u ? 25u / RT : 12u;
+    const uint32_t by_lds = 18u / CT;
+    return by_vgpr < by_lds ? by_vgpr : by_lds;
+}
+GSK_HD constexpr uint32_t bm_sel(uint32_t n, uint32_t w) {
+    uint32_t sel = 0;
+    for (uint32_t j = 0; j < 2; j++) {
+        const uint32_t h = 2 * w + j;
+        uint32_t b0 = 0x0c, b1 = 0x0c;
+        if ((n >> h) & 1u) {
+            uint32_t src = 0;
+            for (uint32_t b = 0; b < h; b++) src += (n >> b) & 1u;
+            b0 = 2 * src;
+            b1 = 2 * src + 1;
+        }
+        sel |= (b0 | (b1 << 8)) << (16 * j);
+    }
+    return sel;
+}
+GSK_HD constexpr bool bm_red_halves(uint32_t CT, uint32_t RT, uint32_t W) {
+    return (size_t)W * RT * CT * 1024u + 16u > 64u * 1024u;
+}
+// dynamic LDS of k_mfma_bm: selector table + W x NBT k-step slots, or the partial tiles of
+// the final reduction (+ the arrival flag)
+GSK_HD constexpr size_t bm_lds_bytes(uint32_t CT, uint32_t RT, uint32_t W) {
+    const size_t ring = 128u + (size_t)W * bm_nbt(CT, RT) * 32u * 32u * CT;
+    const size_t red = (size_t)(bm_red_halves(CT, RT, W) ? W / 2 : W) * RT * CT * 1024u + 16u;
+    return ring > red ? ring : red;
+}
+
 // k_nm_mfma: 8 waves, 4,608-B blocks per (64 rows, 64-column k-step), B chunks of 256 rows
 constexpr int kNmWaves = 8;
 constexpr uint32_t kNmBlockBytes = 4608, kNmKC = 256;

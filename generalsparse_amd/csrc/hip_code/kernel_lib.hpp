@@ -1736,6 +1736,252 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
 }
 
 // ---------------------------------------------------------------------------
+// k_mfma_bm -- BMTB row blocks on the matrix cores from a bitmap layout, with the
+// dense A fragments built in registers (no dense image, no LDS scatter).
+// Why: k_mfma_rows / k_mfma_ks move 4 B per nonzero ([u16 position][f16 value]) and
+// scatter every entry into a dense LDS image (two LDS stores per entry, one to clear
+// it); at 30% density a bitmap costs 0.42 B per nonzero, so A is ~2.4 B per nonzero
+// and no entry ever passes through LDS.
+// Layout (host/device_layout.cc build_bm_tiles): unit u = (row block g, K range q) of
+// NS 32-column k-steps; per (u, step) one 8-byte record per lane l: byte t (t < RT) is
+// the occupancy of row 16t + l%16, columns 32*step + 8*(l/16) + [0, 8) -- exactly the 8
+// halves lane l holds of the A operand of v_mfma_f32_16x16x32_f16 for row tile t --
+// and bytes 6..7 the lane's first value (halves, from the step's base sbase[u*NS+step]);
+// a step's values are stored lane after lane, tile after tile, ascending columns.
+// Wave w of the workgroup owns the range's k-steps w, w+W, ...: per k-step it loads the
+// 32 B rows into registers and stores them into its own LDS ring slot (32-B pieces
+// permuted by b_piece, so the ds_read_b64_tr_b16 fragment reads are conflict-free; not
+// LDS-DMA: the compiler then waits for every DMA in flight before each LDS read of the
+// same wave), loads the record, then per row tile two 8-byte
+// value windows (at the tile's first value and past the low nibble's values; 2-byte
+// aligned loads) that two v_perm_b32 each expand into the tile's dense fragment with
+// selectors from a 16-entry table in LDS, and runs RT x CT MFMAs.  Pipeline per wave:
+// B + record two steps ahead, B store + values one step ahead (counted waits); no
+// workgroup barrier until the end.  Epilogue as k_mfma_ks: the W partial tiles summed in
+// wave order through LDS, then C (S = 1) or a write-through fp32 slab + one arrival add,
+// the last of the row block's S workgroups summing the slabs in q order (deterministic).
+// Rows of B past K are read as row K-1 against zero A columns (a non-finite B value
+// there gives NaN: the documented matrix-core deviation).
+// ---------------------------------------------------------------------------
+typedef uint32_t u32x2_a2 __attribute__((ext_vector_type(2), aligned(2)));
+
+template <int CT, int RT, int W, int NBT>
+__global__ __launch_bounds__(64 * W) void k_mfma_bm(const uint32_t *__restrict__ bmtb_first_row,  // nb+1
+                                                    const uint2 *__restrict__ rec,       // (u*NS + step)*64 + lane
+                                                    const uint32_t *__restrict__ sbase,  // u*NS + step
+                                                    const f16 *__restrict__ vals, const f16 *__restrict__ B,
+                                                    f16 *__restrict__ C, uint32_t K, uint32_t N, uint32_t S,
+                                                    uint32_t NS, uint32_t nwg, uint32_t row_base,
+                                                    float *__restrict__ slabs, uint32_t *__restrict__ arrivals) {
+    static_assert(RT >= 1 && RT <= 6, "six mask bytes per record");
+    constexpr uint32_t RB = 32 * CT;     // bytes per LDS B row (a 16*CT-column tile)
+    constexpr uint32_t UB = 2 * CT;      // 16-B units per B row
+    constexpr uint32_t STG = 32u * RB;   // one k-step of B rows = CT LDS-DMA wave-instructions
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t u = xcd_block(blockIdx.x, nwg);  // nwg == gridDim.x
+    const uint32_t g = u / S, q = u - g * S;
+    const uint32_t col0 = blockIdx.y * 16u * CT, nv = min(16u * CT, N - col0);
+    uint2 *lut = reinterpret_cast<uint2 *>(lds);
+    unsigned char *ring = lds + 128u + wv * NBT * STG;  // this wave's NBT k-step slots
+    if (tid < 16u) lut[tid] = make_uint2(bm_sel(tid, 0), bm_sel(tid, 1));
+    const uint32_t k0 = q * NS * 32u;
+    const uint32_t nsw = NS > wv ? (NS - wv + W - 1u) / W : 0u;  // this wave's k-steps
+    const size_t ub = (size_t)u * NS;
+    // steps past the wave's last re-read its first (cached)
+    auto step_of = [&](uint32_t i) -> uint32_t { return i < nsw ? wv + i * W : wv; };
+    // B rows of step i -> registers (16-B units, lane-linear over the step's 32 rows), then into
+    // slot j with the 32-B pieces permuted by b_piece (conflict-free transposed reads).  Not
+    // LDS-DMA: the compiler then waits for all DMA in flight before the wave's next
+    // dependent load, which serialises the records and the value windows behind the B rows
+    auto load_b = [&](uint32_t i, u32x4 (&BR)[CT]) {
+        const uint32_t kr = k0 + step_of(i) * 32u;
+#pragma unroll
+        for (uint32_t c = 0; c < CT; c++) {
+            const uint32_t un = c * 64u + lane, k = un / UB, cu = (un % UB) * 8u;
+            const uint32_t kk = kr + k < K ? kr + k : K - 1u;
+            BR[c] = *reinterpret_cast<const u32x4 *>(B + (size_t)kk * N + col0 + (cu < nv ? cu : 0u));
+        }
+    };
+    auto store_b = [&](uint32_t j, const u32x4 (&BR)[CT]) {
+        unsigned char *dst = ring + j * STG;
+#pragma unroll
+        for (uint32_t c = 0; c < CT; c++) {
+            const uint32_t un = c * 64u + lane, k = un / UB, s = un % UB;
+            *reinterpret_cast<u32x4 *>(dst + k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u) = BR[c];
+        }
+    };
+    auto mbyte = [](const uint2 &r, int t) -> uint32_t {
+        return t < 4 ? (r.x >> (8 * t)) & 0xffu : (r.y >> (8 * (t - 4))) & 0xffu;
+    };
+    f4v acc[RT][CT];
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+    const uint32_t kb = 8u * (lane >> 4);
+    bool first = true;
+    // batches of NBT k-steps: every load of the batch in flight at once (records, then the B
+    // rows by DMA, then -- once each record is in -- the value windows), then the MFMAs
+    for (uint32_t i0 = 0; i0 < nsw; i0 += NBT) {
+        // B rows first (L2-served: they return before the records from HBM, and loads retire
+        // in order, so waiting for the records costs nothing extra)
+        u32x4 br[NBT][CT];
+#pragma unroll
+        for (int j = 0; j < NBT; j++) load_b(i0 + j, br[j]);
+        uint2 rc[NBT];
+        uint32_t sb[NBT];
+#pragma unroll
+        for (int j = 0; j < NBT; j++) {
+            sb[j] = sbase[ub + step_of(i0 + j)];  // wave-uniform: a scalar load
+            rc[j] = rec[(ub + step_of(i0 + j)) * 64u + lane];
+        }
+        u32x2_a2 vv[NBT][RT][2];
+#pragma unroll
+        for (int j = 0; j < NBT; j++) {
+            uint32_t p = sb[j] + (rc[j].y >> 16);
+#pragma unroll
+            for (int t = 0; t < RT; t++) {
+                const uint32_t m = mbyte(rc[j], t);
+                vv[j][t][0] = *reinterpret_cast<const u32x2_a2 *>(vals + p);
+                vv[j][t][1] = *reinterpret_cast<const u32x2_a2 *>(vals + p + __builtin_popcount(m & 15u));
+                p += __builtin_popcount(m);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NBT; j++) store_b(j, br[j]);
+        if (first) {  // the selector table (its stores, once)
+            __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            __asm__ volatile("" ::: "memory");
+            first = false;
+        }
+#pragma unroll
+        for (int j = 0; j < NBT; j++) {
+            if (i0 + j < nsw) {
+                const unsigned char *bst = ring + j * STG;
+                h8v bv[CT];
+#pragma unroll
+                for (int ct = 0; ct < CT; ct++) {
+                    s4v t2[2];
+#pragma unroll
+                    for (int hh = 0; hh < 2; hh++) {
+                        const uint32_t k = kb + 4u * hh + ((lane & 15u) >> 2);
+                        t2[hh] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                            (lds_s4v *)(bst + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u));
+                    }
+                    __builtin_memcpy(&bv[ct], t2, 16);
+                }
+#pragma unroll
+                for (int t = 0; t < RT; t++) {
+                    const uint32_t m = mbyte(rc[j], t);
+                    const uint2 sl = lut[m & 15u], sh = lut[m >> 4];
+                    const u32x2_a2 lo = vv[j][t][0], hi = vv[j][t][1];
+                    uint32_t w[4];
+                    w[0] = __builtin_amdgcn_perm(lo.y, lo.x, sl.x);
+                    w[1] = __builtin_amdgcn_perm(lo.y, lo.x, sl.y);
+                    w[2] = __builtin_amdgcn_perm(hi.y, hi.x, sh.x);
+                    w[3] = __builtin_amdgcn_perm(hi.y, hi.x, sh.y);
+                    h8v a;
+                    __builtin_memcpy(&a, w, 16);
+#pragma unroll
+                    for (int ct = 0; ct < CT; ct++)
+                        acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bv[ct], acc[t][ct], 0, 0, 0);
+                }
+            }
+        }
+    }
+    if (first) {  // a wave with no k-steps still meets the table barrier
+        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __asm__ volatile("" ::: "memory");
+    }
+    // every wave is done with its ring before it is reused for the partial tiles
+    __syncthreads();
+    f4v *red = reinterpret_cast<f4v *>(lds);
+    constexpr bool HALVES = bm_red_halves(CT, RT, W);
+    constexpr uint32_t WR = HALVES ? W / 2 : W;
+    if constexpr (HALVES) {
+        if (wv >= WR) {
+#pragma unroll
+            for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+                for (int ct = 0; ct < CT; ct++) red[(((wv - WR) * RT + rt) * CT + ct) * 64u + lane] = acc[rt][ct];
+        }
+        __syncthreads();
+        if (wv < WR) {
+#pragma unroll
+            for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+                for (int ct = 0; ct < CT; ct++) acc[rt][ct] += red[((wv * RT + rt) * CT + ct) * 64u + lane];
+        }
+        __syncthreads();
+    }
+    if (wv < WR) {
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) red[((wv * RT + rt) * CT + ct) * 64u + lane] = acc[rt][ct];
+    }
+    __syncthreads();
+    constexpr uint32_t NI = RT * CT * 64u, NT = 64u * W;
+    const uint32_t r0 = bmtb_first_row[g], R = bmtb_first_row[g + 1] - r0;
+    auto item_sum = [&](uint32_t t) {
+        f4v sum = red[t];
+#pragma unroll
+        for (uint32_t w = 1; w < WR; w++) sum += red[w * NI + t];
+        return sum;
+    };
+    auto store_item = [&](uint32_t t, const f4v &v) {
+        const uint32_t ln = t & 63u, tt = t >> 6, rt = tt / CT, ct = tt % CT;
+        const uint32_t col = 16u * ct + (ln & 15u), rb = 16u * rt + 4u * (ln >> 4);
+        if (col >= nv) return;
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++)
+            if (rb + i < R) C[(size_t)(row_base + r0 + rb + i) * N + col0 + col] = (f16)v[i];
+    };
+    if (S == 1) {
+        for (uint32_t t = tid; t < NI; t += NT) store_item(t, item_sum(t));
+        return;
+    }
+    // K-split hand-off (k_mfma_ks's form): 16-B write-through slab stores, every storing
+    // wave's vmcnt(0), a barrier, one agent-scope arrival add; the last adder (told by the
+    // returned count) loads the other slabs with agent-scope (sc1) loads
+    f4v *slab = reinterpret_cast<f4v *>(slabs) + ((size_t)u * gridDim.y + blockIdx.y) * NI;
+    for (uint32_t t = tid; t < NI; t += NT) {
+        const f4v v = item_sum(t);
+        __asm__ volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(slab + t), "v"(v) : "memory");
+    }
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    uint32_t *flag = reinterpret_cast<uint32_t *>(lds + (size_t)WR * NI * 16u);
+    uint32_t *arr = arrivals + (size_t)g * gridDim.y + blockIdx.y;
+    if (tid == 0) *flag = __hip_atomic_fetch_add(arr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*flag != S - 1u) return;
+    if (tid == 0) __hip_atomic_store(arr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const f4v *base = reinterpret_cast<const f4v *>(slabs) + blockIdx.y * NI;
+    const size_t qstride = (size_t)gridDim.y * NI;
+    for (uint32_t t = tid; t < NI; t += NT) {
+        const f4v own = item_sum(t);
+        f4v sum = {0.f, 0.f, 0.f, 0.f};
+        for (uint32_t qq = 0; qq < S; qq++) {
+            if (qq == q) {
+                sum += own;
+                continue;
+            }
+            const float *src = reinterpret_cast<const float *>(base + ((size_t)g * S + qq) * qstride + t);
+            f4v x;
+#pragma unroll
+            for (int i = 0; i < 4; i++) x[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sum += x;
+        }
+        store_item(t, sum);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_nm_mfma -- fixed_interval_col_direction BMTs that are 2:4 panels
 //  on the sparse matrix cores:
 // v_smfmac_f32_16x16x64_f16 multiplies a 16x64 A tile stored as 16x32 values

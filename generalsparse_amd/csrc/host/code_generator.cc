@@ -215,7 +215,9 @@ namespace {
 std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int repeat) {
     std::ostringstream o;
     const uint32_t N = L.N, CT = L.kind == mc_layout::NM ? N / 16 : ks_ct(N);
-    const char *kname = L.kind == mc_layout::KS ? "k_mfma_ks" : (L.kind == mc_layout::ROWS ? "k_mfma_rows" : "k_nm_mfma");
+    const char *kname = L.kind == mc_layout::KS ? "k_mfma_ks"
+                        : L.kind == mc_layout::BM ? "k_mfma_bm"
+                        : (L.kind == mc_layout::ROWS ? "k_mfma_rows" : "k_nm_mfma");
     o << "// kernel_file.hip -- generated by generalsparse_amd code_generator: the matrix-core kernel " << kname << "\n"
       << "// build: sh make_kernel.sh; run: ./a.out [matrix.mtx] [N]  -> perf_result (ms, GFLOP/s)\n"
       << "#include \"kernel_lib.hpp\"\n#include <cstdio>\n#include <cstdlib>\n#include <cstring>\n#include <fstream>\n"
@@ -261,6 +263,25 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
                  ">>>(d_tbr, (const gsk::u32x4 *)d_pos, (const gsk::u32x4 *)d_val, d_B, d_C, (uint32_t)K, N, " +
                  std::to_string(t.S) + "u, " + std::to_string(t.NS) + "u, " + std::to_string(t.GCAP) + "u, " +
                  std::to_string(nwg) + "u, 0u, d_ws, d_arr, nullptr)";
+    } else if (L.kind == mc_layout::BM) {
+        const bm_tiles &t = L.bm;
+        const uint64_t nb = L.tbr.size() - 1, nwg = nb * t.S;
+        o << "    auto tbr = rd(\"TBLOCK_META_first_row_indices_0\");\n"
+          << "    std::vector<uint32_t> t32(tbr.begin(), tbr.end()); uint32_t *d_tbr = up(t32);\n"
+          << "    uint32_t *d_rec = up(rdb<uint32_t>(\"TBLOCK_META_mfma_bm_records_0.bin\"));\n"
+          << "    uint32_t *d_sb = up(rdb<uint32_t>(\"TBLOCK_META_mfma_bm_step_base_0.bin\"));\n"
+          << "    uint16_t *d_val = up(rdb<uint16_t>(\"TBLOCK_META_mfma_bm_values_0.bin\"));\n"
+          << "    float *d_ws; uint32_t *d_arr; hipMalloc(&d_ws, " << nwg * ks_col_tiles(N) * 256 * t.RT * CT * 4 << "ull + 16);\n"
+          << "    hipMalloc(&d_arr, " << nb * ks_col_tiles(N) * 4 << "ull + 4); hipMemset(d_arr, 0, " << nb * ks_col_tiles(N) * 4
+          << "ull + 4);\n";
+        const std::string k = "gsk::k_mfma_bm<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ", " +
+                              std::to_string(t.W) + ", " + std::to_string(gsk::bm_nbt(CT, t.RT)) + ">";
+        setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
+                std::to_string(t.lds_bytes) + ")";
+        launch = k + "<<<dim3(" + std::to_string(nwg) + ", " + std::to_string(ks_col_tiles(N)) + "), " +
+                 std::to_string(64 * t.W) + ", " + std::to_string(t.lds_bytes) +
+                 ">>>(d_tbr, (const uint2 *)d_rec, d_sb, (const gsk::f16 *)d_val, d_B, d_C, (uint32_t)K, N, " +
+                 std::to_string(t.S) + "u, " + std::to_string(t.NS) + "u, " + std::to_string(nwg) + "u, 0u, d_ws, d_arr)";
     } else if (L.kind == mc_layout::ROWS) {
         const mfma_tiles &t = L.rows;
         const uint64_t nb = L.tbr.size() - 1;
@@ -545,6 +566,10 @@ uint64_t code_generator::generate_final_program(int repeat, const std::string &r
     if (L.kind == mc_layout::KS) {
         write_bin(dir + "/TBLOCK_META_mfma_ks_entry_pos_0.bin", L.ks.pos);
         write_bin(dir + "/TBLOCK_META_mfma_ks_entry_val_0.bin", L.ks.val);
+    } else if (L.kind == mc_layout::BM) {
+        write_bin(dir + "/TBLOCK_META_mfma_bm_records_0.bin", L.bm.rec);
+        write_bin(dir + "/TBLOCK_META_mfma_bm_step_base_0.bin", L.bm.sbase);
+        write_bin(dir + "/TBLOCK_META_mfma_bm_values_0.bin", L.bm.val);
     } else if (L.kind == mc_layout::ROWS) {
         write_bin(dir + "/TBLOCK_META_mfma_seg_start_0.bin", L.rows.seg_start);
         write_bin(dir + "/TBLOCK_META_mfma_entry_pos_0.bin", L.rows.pos);

@@ -309,6 +309,90 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     return true;
 }
 
+// ------------------------------------------------------------------ bitmap records
+// k_mfma_bm (kernel_lib.hpp): see bm_tiles.  Row blocks of up to 96 rows (RT <= 6 mask
+// bytes per record); K split into S ranges of whole k-steps so nb * S workgroups cover
+// the CUs (s_cfg > 0: that many).
+bool build_bm_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
+                    const std::vector<uint64_t> &col, const std::vector<float> &vals, uint64_t K, uint32_t N,
+                    int64_t s_cfg, int64_t waves, int64_t max_fill, bm_tiles &t, std::string &why) {
+    const uint64_t nb = tb_rows.size() - 1;
+    if (nb == 0 || K == 0) { why = "empty plan"; return false; }
+    if (N == 0 || N % 8 != 0) { why = "N must be a multiple of 8"; return false; }
+    uint64_t rmax = 0;
+    for (uint64_t g = 0; g < nb; g++) rmax = std::max<uint64_t>(rmax, tb_rows[g + 1] - tb_rows[g]);
+    if (rmax == 0 || rmax > 96) { why = "row blocks outside the k_mfma_bm range (1..96 rows)"; return false; }
+    const uint32_t RT = (uint32_t)((rmax + 15) / 16);
+    const uint64_t nnz = row_ptr[tb_rows[nb]] - row_ptr[tb_rows[0]];
+    if (nnz == 0 || (double)nb * 16 * RT * K > (double)max_fill * nnz) {
+        why = "row blocks too sparse for dense tiles";
+        return false;
+    }
+    const uint32_t W = waves == 4 ? 4u : 8u;
+    uint64_t S = s_cfg > 0 ? (uint64_t)s_cfg : std::max<uint64_t>(1, std::min<uint64_t>(8, 256 / nb));
+    S = std::max<uint64_t>(1, std::min<uint64_t>(S, (K + 31) / 32));
+    const uint64_t KR = ((K + S - 1) / S + 31) / 32 * 32;
+    S = (K + KR - 1) / KR;
+    t.S = (uint32_t)S;
+    t.NS = (uint32_t)(KR / 32);
+    t.RT = RT;
+    t.RMAX = (uint32_t)rmax;
+    t.W = W;
+    t.lds_bytes = gsk::bm_lds_bytes(ks_ct(N), RT, W);
+    const uint64_t nrec = nb * S * t.NS * 64;
+    GS_CHECK(nrec < (1ull << 31), "k_mfma_bm layout exceeds 31-bit record indices");
+    t.rec.assign(nrec * 2, 0u);
+    auto rec_of = [&](uint64_t g, uint64_t i, uint64_t c, uint32_t &tt, uint32_t &bit) -> uint64_t {
+        const uint64_t qq = c / KR, cc = c % KR, st = cc / 32, w = cc % 32;
+        tt = (uint32_t)(i / 16);
+        bit = (uint32_t)(w % 8);
+        const uint64_t lane = (w / 8) * 16 + i % 16;
+        return ((g * S + qq) * t.NS + st) * 64 + lane;
+    };
+    auto mask_byte = [&](uint64_t r, uint32_t tt) -> uint32_t {
+        return tt < 4 ? (t.rec[2 * r] >> (8 * tt)) & 0xffu : (t.rec[2 * r + 1] >> (8 * (tt - 4))) & 0xffu;
+    };
+    for (uint64_t g = 0; g < nb; g++)
+        for (uint64_t i = 0; i < tb_rows[g + 1] - tb_rows[g]; i++)
+            for (uint64_t e = row_ptr[tb_rows[g] + i]; e < row_ptr[tb_rows[g] + i + 1]; e++) {
+                uint32_t tt, bit;
+                const uint64_t r = rec_of(g, i, col[e], tt, bit);
+                if (tt < 4) t.rec[2 * r] |= 1u << (8 * tt + bit);
+                else t.rec[2 * r + 1] |= 1u << (8 * (tt - 4) + bit);
+            }
+    // step bases and lane offsets (lane after lane, tile after tile)
+    const uint64_t nst = nb * S * t.NS;
+    t.sbase.assign(nst + 1, 0u);
+    uint64_t run = 0;
+    std::vector<uint32_t> lane_pre(nrec, 0);  // values before (lane, tile 0) within the step
+    for (uint64_t x = 0; x < nst; x++) {
+        GS_CHECK(run < (1ull << 32) - 64, "k_mfma_bm values exceed 32-bit offsets");
+        t.sbase[x] = (uint32_t)run;
+        uint32_t off = 0;
+        for (uint32_t l = 0; l < 64; l++) {
+            const uint64_t r = x * 64 + l;
+            lane_pre[r] = off;
+            t.rec[2 * r + 1] |= off << 16;
+            for (uint32_t tt = 0; tt < RT; tt++) off += (uint32_t)__builtin_popcount(mask_byte(r, tt));
+        }
+        GS_CHECK(off < 65536u, "k_mfma_bm step holds more than 65535 values");
+        run += off;
+    }
+    t.sbase[nst] = (uint32_t)run;
+    t.val.assign(run + 16, 0);
+    for (uint64_t g = 0; g < nb; g++)
+        for (uint64_t i = 0; i < tb_rows[g + 1] - tb_rows[g]; i++)
+            for (uint64_t e = row_ptr[tb_rows[g] + i]; e < row_ptr[tb_rows[g] + i + 1]; e++) {
+                uint32_t tt, bit;
+                const uint64_t r = rec_of(g, i, col[e], tt, bit);
+                uint64_t pos = t.sbase[r / 64] + lane_pre[r];
+                for (uint32_t t2 = 0; t2 < tt; t2++) pos += (uint32_t)__builtin_popcount(mask_byte(r, t2));
+                pos += (uint32_t)__builtin_popcount(mask_byte(r, tt) & ((1u << bit) - 1u));
+                t.val[pos] = f32_to_f16_bits(vals[e]);
+            }
+    return true;
+}
+
 // ------------------------------------------------------------------ 2:4 panels
 // Block layout of k_nm_mfma (kernel_lib.hpp) from the plan's COO: every row is
 // cut into 64-column k-steps (the col-direction BMTs of a 2:4 row: 32 entries
@@ -418,6 +502,11 @@ mc_layout choose_matrix_core_layout(const meta_data_set &m, const kernel_spec &s
     L.tbr = m.u(TBLOCK_META, "first_row_indices", sb);
     const canon_rows cr = canonical_rows(rp0, col, *vals);
     const uint32_t N = (uint32_t)Nd;
+    if (cfg.MFMA_BM && build_bm_tiles(L.tbr, cr.rp, cr.col, cr.val, K, N, cfg.BM_SPLIT, cfg.BM_WAVES,
+                                      cfg.MFMA_MAX_FILL, L.bm, L.why)) {
+        L.kind = mc_layout::BM;
+        return L;
+    }
     if (cfg.MFMA_KS &&
         build_ks_tiles(L.tbr, cr.rp, cr.col, cr.val, K, N, cfg.KS_SPLIT, cfg.KS_MIN_ROWS, cfg.MFMA_MAX_FILL, L.ks, L.why)) {
         L.kind = mc_layout::KS;

@@ -61,6 +61,22 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
                     const std::vector<uint64_t> &col, const std::vector<float> &vals, uint64_t K, uint32_t N,
                     int64_t s_cfg, int64_t min_rows, int64_t max_fill, ks_tiles &t, std::string &why);
 
+// k_mfma_bm upload layout: unit u = (BMTB g, K range q) of NS 32-column k-steps; per
+// (u*NS + step)*64 + lane one 8-byte record (rec[2i] = mask bytes of tiles 0..3, rec[2i+1]
+// = tiles 4..5 | u16 value offset << 16), sbase[u*NS + step] the step's first value, the
+// values (f16 bits) lane after lane, tile after tile, ascending columns (+ 16 halves pad)
+struct bm_tiles {
+    uint32_t S = 0, NS = 0, RT = 0, RMAX = 0, W = 0;
+    size_t lds_bytes = 0;
+    std::vector<uint32_t> rec;
+    std::vector<uint32_t> sbase;
+    std::vector<uint16_t> val;
+};
+
+bool build_bm_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
+                    const std::vector<uint64_t> &col, const std::vector<float> &vals, uint64_t K, uint32_t N,
+                    int64_t s_cfg, int64_t waves, int64_t max_fill, bm_tiles &t, std::string &why);
+
 // k_nm_mfma upload layout: one 4,608-B block per (64-row group, 64-column k-step)
 bool build_nm_panels(const std::vector<uint64_t> &rows, const std::vector<uint64_t> &col, const universal_array &vals,
                      uint64_t row_num, uint64_t K, std::vector<unsigned char> &blk, uint32_t &S, std::string &why);
@@ -72,13 +88,14 @@ bool build_nm_panels(const std::vector<uint64_t> &rows, const std::vector<uint64
 // The k_mfma_rows variant (B by LDS-DMA or registers, ring depth, compute waves) is fixed
 // here from the config, so the LDS size and the launch agree whatever changes later.
 struct mc_layout {
-    enum kind_t { NONE, ROWS, KS, NM } kind = NONE;
+    enum kind_t { NONE, ROWS, KS, NM, BM } kind = NONE;
     uint32_t N = 0;
     std::vector<uint64_t> tbr;  // BMTB first rows (ROWS, KS)
     mfma_tiles rows;
     uint32_t rows_ksplit = 1, rows_ncs = 0;  // k_mfma_rows K ranges per row block, chunks per range
     int rows_glds = 2, rows_nbg = 3, rows_wct = 6, rows_maxa = 1;  // k_mfma_rows template arguments
     ks_tiles ks;
+    bm_tiles bm;
     std::vector<unsigned char> nm_blk;  // k_nm_mfma blocks
     uint32_t nm_S = 0;                  // ... k-steps per row group
     uint64_t nm_rows = 0;

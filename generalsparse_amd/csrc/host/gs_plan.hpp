@@ -47,6 +47,9 @@ struct device_plan {
                         // (t0 BMTB rows, tcol/tval groups; ks_ns k-steps per range,
                         // RT in maxr, MAXG in seg_cap, ws slabs + t2 arrivals when ksplit > 1)
     uint32_t ks_ns = 0, ks_gcap = 0;
+    bool bm = false;    // k_mfma_bm: bitmap records (tcol), step bases (t1), values (tval), t0 BMTB rows;
+                        // ksplit K ranges of ks_ns k-steps, RT in maxr, W in waves
+
     bool mp_rows = false;   // merge-path plans: k_merge_rows (fixed at upload, MP_ROWS), else k_merge_path
     uint32_t mp_solo = 16;  // k_merge_rows: slot-alone row length (MP_SOLO)
     // k_mfma_rows variant fixed at upload (device_layout.cc): GLDS / B ring depth / compute
@@ -122,6 +125,7 @@ void launch_nm(const plan_state &p, const device_arrays &a, const void *B, void 
 void launch_gather(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s);
 // ks_launch.hip: k_mfma_ks (K-split, wave-autonomous matrix-core row blocks)
 void launch_ks(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s);
+void launch_bm(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s);
 void debug_ks_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
                        size_t n_host);
 

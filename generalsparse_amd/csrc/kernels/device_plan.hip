@@ -328,6 +328,34 @@ void upload_plan(plan_state &p, int dtype, int device) {
             }
             return true;
         }
+        if (mc.kind == mc_layout::BM) {
+            // bitmap records, fragments expanded in registers (k_mfma_bm)
+            const bm_tiles &bt = mc.bm;
+            d.mfma = true;
+            d.bm = true;
+            d.kernel = "k_mfma_bm";
+            d.lds_N = mc.N;
+            d.ksplit = bt.S;
+            d.ks_ns = bt.NS;
+            d.maxr = bt.RT;
+            d.rpw_max = bt.RMAX;
+            d.waves = bt.W;
+            d.lds_bytes = bt.lds_bytes;
+            const uint64_t nb = mc.tbr.size() - 1;
+            d.n_rows_aux = nb;
+            const size_t before = d.bytes_A;
+            a.t0 = dev_copy(d, to_u32(mc.tbr, "BMTB first_row_indices"));
+            a.tcol = dev_copy(d, bt.rec);
+            a.t1 = dev_copy(d, bt.sbase);
+            a.tval = dev_copy(d, bt.val);
+            d.bytes_tile = d.bytes_A - before;
+            if (bt.S > 1) {
+                const uint32_t nt = ks_col_tiles(mc.N), CT = ks_ct(mc.N);
+                a.ws = dev_copy(d, std::vector<float>((size_t)nb * bt.S * nt * 256 * bt.RT * CT, 0.f));
+                a.t2 = dev_copy(d, std::vector<uint32_t>((size_t)nb * nt, 0u));  // arrival counters
+            }
+            return true;
+        }
         if (mc.kind != mc_layout::ROWS) return false;
         const mfma_tiles &t = mc.rows;
         d.mfma = true;

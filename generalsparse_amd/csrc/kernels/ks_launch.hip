@@ -65,7 +65,50 @@ void launch_ks_ct(const plan_state &p, const device_arrays &a, const gsk::f16 *B
     }
 }
 
+template <int CT, int RT, int W>
+void launch_bm_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
+    const device_plan &d = p.dev;
+    auto kern = gsk::k_mfma_bm<CT, RT, W, (int)gsk::bm_nbt(CT, RT)>;
+    GS_CHECK(gsk::bm_lds_bytes(CT, RT, W) <= d.lds_bytes, "k_mfma_bm: LDS size disagrees with the upload");
+    grant_lds(d.device, kern, d.lds_bytes);
+    const uint32_t nwg = (uint32_t)d.n_rows_aux * d.ksplit;
+    hipLaunchKernelGGL(kern, dim3(nwg, ks_col_tiles(N)), dim3(64 * W), d.lds_bytes, s, a.t0, (const uint2 *)a.tcol, a.t1,
+                       (const gsk::f16 *)a.tval, B, C, (uint32_t)p.K, N, d.ksplit, d.ks_ns, nwg, (uint32_t)d.row_base,
+                       a.ws, a.t2);
+    HIP_OK(hipGetLastError());
+}
+
+template <int CT, int RT>
+void launch_bm_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
+    if (p.dev.waves == 4) launch_bm_k<CT, RT, 4>(p, a, B, C, N, s);
+    else launch_bm_k<CT, RT, 8>(p, a, B, C, N, s);
+}
+
+template <int CT>
+void launch_bm_ct(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
+    switch (p.dev.maxr) {  // RT: 16-row tiles per row block
+        case 1: launch_bm_rt<CT, 1>(p, a, B, C, N, s); break;
+        case 2: launch_bm_rt<CT, 2>(p, a, B, C, N, s); break;
+        case 3: launch_bm_rt<CT, 3>(p, a, B, C, N, s); break;
+        case 4: launch_bm_rt<CT, 4>(p, a, B, C, N, s); break;
+        case 5: launch_bm_rt<CT, 5>(p, a, B, C, N, s); break;
+        case 6: launch_bm_rt<CT, 6>(p, a, B, C, N, s); break;
+        default: throw gs_error("k_mfma_bm: row tiles outside 1..6");
+    }
+}
+
 }  // namespace
+
+void launch_bm(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
+    const gsk::f16 *b = (const gsk::f16 *)B;
+    gsk::f16 *c = (gsk::f16 *)C;
+    GS_CHECK(N == p.dev.lds_N, "k_mfma_bm runs the plan's dense width");
+    switch (ks_ct(N)) {
+        case 1: launch_bm_ct<1>(p, a, b, c, N, s); break;
+        case 2: launch_bm_ct<2>(p, a, b, c, N, s); break;
+        default: launch_bm_ct<4>(p, a, b, c, N, s); break;
+    }
+}
 
 void launch_ks(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
     const gsk::f16 *b = (const gsk::f16 *)B;

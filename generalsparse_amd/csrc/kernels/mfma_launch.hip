@@ -168,6 +168,10 @@ void launch_mfma(const plan_state &p, const device_arrays &a, const void *B, voi
         launch_ks(p, a, B, C, N, s);  // ks_launch.hip
         return;
     }
+    if (p.dev.bm) {
+        launch_bm(p, a, B, C, N, s);  // ks_launch.hip
+        return;
+    }
     GS_CHECK(N % 8 == 0 && N <= 64, "k_mfma_rows runs N = 8..64, a multiple of 8");
     switch (ks_ct(N)) {  // 16-column tiles (device_layout.hpp)
         case 1: launch_mfma_ct<1>(p, a, b, c, N, s); break;
