@@ -1765,15 +1765,25 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
 // ---------------------------------------------------------------------------
 typedef uint32_t u32x2_a2 __attribute__((ext_vector_type(2), aligned(2)));
 
-template <int CT, int RT, int W, int NBT>
+// STAMPS (diagnostic build only, gs_debug_mfma_timeline): lane 0 of every wave records
+// s_memtime into stamps[(workgroup * W + wave) * 16 + slot]: 0 start, 1 B + records issued,
+// 2 values issued, 3 B stored (all landed), 4 MFMAs done (first batch), 5 loop done,
+// 6 reduced, 7 slab published, 8 end
+template <int CT, int RT, int W, int NBT, bool STAMPS = false>
 __global__ __launch_bounds__(64 * W) void k_mfma_bm(const uint32_t *__restrict__ bmtb_first_row,  // nb+1
                                                     const uint2 *__restrict__ rec,       // (u*NS + step)*64 + lane
                                                     const uint32_t *__restrict__ sbase,  // u*NS + step
                                                     const f16 *__restrict__ vals, const f16 *__restrict__ B,
                                                     f16 *__restrict__ C, uint32_t K, uint32_t N, uint32_t S,
                                                     uint32_t NS, uint32_t nwg, uint32_t row_base,
-                                                    float *__restrict__ slabs, uint32_t *__restrict__ arrivals) {
+                                                    float *__restrict__ slabs, uint32_t *__restrict__ arrivals,
+                                                    uint64_t *__restrict__ stamps = nullptr) {
     static_assert(RT >= 1 && RT <= 6, "six mask bytes per record");
+#define GS_BM_STAMP(slot)                                                                          \
+    if constexpr (STAMPS) {                                                                        \
+        if ((threadIdx.x & 63u) == 0) stamps[((size_t)blockIdx.x * W + (threadIdx.x >> 6)) * 16u + (slot)] = __builtin_amdgcn_s_memtime(); \
+    }
+    GS_BM_STAMP(0u);
     constexpr uint32_t RB = 32 * CT;     // bytes per LDS B row (a 16*CT-column tile)
     constexpr uint32_t UB = 2 * CT;      // 16-B units per B row
     constexpr uint32_t STG = 32u * RB;   // one k-step of B rows = CT LDS-DMA wave-instructions
@@ -1837,6 +1847,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_bm(const uint32_t *__restrict__
             sb[j] = sbase[ub + step_of(i0 + j)];  // wave-uniform: a scalar load
             rc[j] = rec[(ub + step_of(i0 + j)) * 64u + lane];
         }
+        if (first) GS_BM_STAMP(1u);
         u32x2_a2 vv[NBT][RT][2];
 #pragma unroll
         for (int j = 0; j < NBT; j++) {
@@ -1849,13 +1860,14 @@ __global__ __launch_bounds__(64 * W) void k_mfma_bm(const uint32_t *__restrict__
                 p += __builtin_popcount(m);
             }
         }
+        if (first) GS_BM_STAMP(2u);
 #pragma unroll
         for (int j = 0; j < NBT; j++) store_b(j, br[j]);
         if (first) {  // the selector table (its stores, once)
             __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             __asm__ volatile("" ::: "memory");
-            first = false;
+            GS_BM_STAMP(3u);
         }
 #pragma unroll
         for (int j = 0; j < NBT; j++) {
@@ -1891,7 +1903,12 @@ __global__ __launch_bounds__(64 * W) void k_mfma_bm(const uint32_t *__restrict__
                 }
             }
         }
+        if (first) {
+            GS_BM_STAMP(4u);
+            first = false;
+        }
     }
+    GS_BM_STAMP(5u);
     if (first) {  // a wave with no k-steps still meets the table barrier
         __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -1941,8 +1958,10 @@ __global__ __launch_bounds__(64 * W) void k_mfma_bm(const uint32_t *__restrict__
         for (uint32_t i = 0; i < 4; i++)
             if (rb + i < R) C[(size_t)(row_base + r0 + rb + i) * N + col0 + col] = (f16)v[i];
     };
+    GS_BM_STAMP(6u);
     if (S == 1) {
         for (uint32_t t = tid; t < NI; t += NT) store_item(t, item_sum(t));
+        GS_BM_STAMP(8u);
         return;
     }
     // K-split hand-off (k_mfma_ks's form): 16-B write-through slab stores, every storing
@@ -1959,7 +1978,11 @@ __global__ __launch_bounds__(64 * W) void k_mfma_bm(const uint32_t *__restrict__
     uint32_t *arr = arrivals + (size_t)g * gridDim.y + blockIdx.y;
     if (tid == 0) *flag = __hip_atomic_fetch_add(arr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    if (*flag != S - 1u) return;
+    GS_BM_STAMP(7u);
+    if (*flag != S - 1u) {
+        GS_BM_STAMP(8u);
+        return;
+    }
     if (tid == 0) __hip_atomic_store(arr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const f4v *base = reinterpret_cast<const f4v *>(slabs) + blockIdx.y * NI;
     const size_t qstride = (size_t)gridDim.y * NI;
@@ -1979,6 +2002,8 @@ __global__ __launch_bounds__(64 * W) void k_mfma_bm(const uint32_t *__restrict__
         }
         store_item(t, sum);
     }
+    GS_BM_STAMP(8u);
+#undef GS_BM_STAMP
 }
 
 // ---------------------------------------------------------------------------

@@ -126,6 +126,8 @@ void launch_gather(const plan_state &p, const device_arrays &a, const void *B, v
 // ks_launch.hip: k_mfma_ks (K-split, wave-autonomous matrix-core row blocks)
 void launch_ks(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s);
 void launch_bm(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s);
+void debug_bm_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
+                       size_t n_host);
 void debug_ks_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
                        size_t n_host);
 

@@ -65,16 +65,17 @@ void launch_ks_ct(const plan_state &p, const device_arrays &a, const gsk::f16 *B
     }
 }
 
-template <int CT, int RT, int W>
-void launch_bm_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
+template <int CT, int RT, int W, bool STAMPS = false>
+void launch_bm_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s,
+                 uint64_t *stamps = nullptr) {
     const device_plan &d = p.dev;
-    auto kern = gsk::k_mfma_bm<CT, RT, W, (int)gsk::bm_nbt(CT, RT)>;
+    auto kern = gsk::k_mfma_bm<CT, RT, W, (int)gsk::bm_nbt(CT, RT), STAMPS>;
     GS_CHECK(gsk::bm_lds_bytes(CT, RT, W) <= d.lds_bytes, "k_mfma_bm: LDS size disagrees with the upload");
     grant_lds(d.device, kern, d.lds_bytes);
     const uint32_t nwg = (uint32_t)d.n_rows_aux * d.ksplit;
     hipLaunchKernelGGL(kern, dim3(nwg, ks_col_tiles(N)), dim3(64 * W), d.lds_bytes, s, a.t0, (const uint2 *)a.tcol, a.t1,
                        (const gsk::f16 *)a.tval, B, C, (uint32_t)p.K, N, d.ksplit, d.ks_ns, nwg, (uint32_t)d.row_base,
-                       a.ws, a.t2);
+                       a.ws, a.t2, stamps);
     HIP_OK(hipGetLastError());
 }
 
@@ -119,6 +120,21 @@ void launch_ks(const plan_state &p, const device_arrays &a, const void *B, void 
         case 2: launch_ks_ct<2>(p, a, b, c, N, s); break;
         default: launch_ks_ct<4>(p, a, b, c, N, s); break;
     }
+}
+
+// diagnostic: k_mfma_bm at N = 32, 65..80-row blocks, 8 waves (stamps: kernel_lib.hpp)
+void debug_bm_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
+                       size_t n_host) {
+    const device_plan &d = p.dev;
+    GS_CHECK(N == 32 && d.maxr == 5 && d.waves == 8, "k_mfma_bm timeline build: N=32, RT=5, 8 waves only");
+    const size_t n = (size_t)d.n_rows_aux * d.ksplit * 8 * 16;
+    uint64_t *dst = nullptr;
+    HIP_OK(hipMalloc(&dst, n * 8));
+    HIP_OK(hipMemsetAsync(dst, 0, n * 8, s));
+    launch_bm_k<2, 5, 8, true>(p, d.replicas[0], (const gsk::f16 *)B, (gsk::f16 *)C, N, s, dst);
+    HIP_OK(hipStreamSynchronize(s));
+    HIP_OK(hipMemcpy(host, dst, std::min(n, n_host) * 8, hipMemcpyDeviceToHost));
+    (void)hipFree(dst);
 }
 
 // diagnostic: the C2 shape (N = 32, 65..80-row blocks, <= 128 entry groups per k-step)

@@ -99,6 +99,10 @@ void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N
         debug_ks_timeline(p, B, C, N, s, host, n_host);
         return;
     }
+    if (d.bm) {
+        debug_bm_timeline(p, B, C, N, s, host, n_host);
+        return;
+    }
     GS_CHECK(p.uploaded && d.mfma && N == d.lds_N && N == 32 && (d.maxr == 2 || d.maxr == 3) &&
                  (d.RSB == 8 || d.RSB == 9),
              "timeline build exists for N=32 matrix-core plans with 17..48-row BMTBs, KC 256/512 only");
