@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--search-reps", type=int, default=100, help="launches per candidate plan in the plan search")
     ap.add_argument("--n-sweep", default="", help="also time the chosen plan family at these dense widths, e.g. 8,32,128")
     ap.add_argument("--layers", type=int, default=48, help="c5: OPT-30B layers in the batch")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="c5/c5h: HIP streams the batch's launches rotate over (2: one launch's tail overlaps the "
+                         "next one's start; profiles/r03_c5_streams.json)")
     ap.add_argument("--shard", choices=("batch", "rows", "nnz"), default="batch",
                     help="c4/c4o with N>1: batch = a matrix per rank (weak); rows / nnz = one matrix split "
                          "over the ranks (strong; nnz splits rows and combines them with one all-reduce)")
@@ -304,12 +307,7 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
                                       bt.C5_SPARSITY, rocsparse=False)
     plans, launches, _ = bt.build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, choice=choice)
     t_setup = time.perf_counter() - t0
-    stream = torch.cuda.current_stream().cuda_stream
-    raw = [(p, r, b.data_ptr(), c.data_ptr()) for (p, r, b, c, _) in launches]
-
-    def step():
-        for plan, r, b, c in raw:
-            plan.spmm_raw(b, c, N, r, stream)
+    step, _ = batch_step(launches, N, torch, args.streams)
 
     for _ in range(args.warmup):
         step()
@@ -354,7 +352,8 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
                                f"80% unstructured, fp16, N={N}", "matrices": len(batch), "nnz": total_nnz,
                    "plan": {k: per_shape[k]["plan"] for k in plans},
                    "kernel": {k: kernel_label(plans[k].info()) for k in plans},
-                   "parallelism": f"LPT batch split x{world} (max rank nnz share {max(load) / total_nnz:.4f})"},
+                   "parallelism": f"LPT batch split x{world} (max rank nnz share {max(load) / total_nnz:.4f})",
+                   "streams": args.streams},
         "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9 / world, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / world / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "algorithmic_bytes_per_step": alg, "note": "per GPU, whole step"},
@@ -365,6 +364,25 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
         print(json.dumps(out), flush=True)
     for p in plans.values():
         p.free()
+
+
+def batch_step(launches, N, torch, n_streams):
+    """one pass over a batch of independent SpMMs: launch i on stream i % n_streams (the
+    current stream first), so one launch's tail overlaps the next one's start; with more
+    than one stream every launch writes its own C.  Returns (step, streams)."""
+    cur = torch.cuda.current_stream()
+    streams = [cur] + [torch.cuda.Stream() for _ in range(max(1, n_streams) - 1)]
+    raw = []
+    for i, (p, r, b, c, _) in enumerate(launches):
+        if n_streams > 1:
+            c = torch.empty_like(c)
+        raw.append((p, r, b.data_ptr(), c.data_ptr(), streams[i % len(streams)].cuda_stream, c))
+
+    def step():
+        for plan, r, b, c, s, _ in raw:
+            plan.spmm_raw(b, c, N, r, s)
+
+    return step, streams
 
 
 def search_shapes(args, torch, gsa, ds, rank, local, dev, shapes, sp, rocsparse=True):
@@ -428,12 +446,7 @@ def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
     # the timed layer: 4 x attn (replicas 0..3), fc1, fc2
     seq = [(0, s, bt.C5_SLOTS[s], bt.C5_SLOTS[:s].count(bt.C5_SLOTS[s])) for s in range(len(bt.C5_SLOTS))]
     plans, launches, _ = bt.build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, sparsity=sp, choice=choice)
-    stream = torch.cuda.current_stream().cuda_stream
-    raw = [(p, r, b.data_ptr(), c.data_ptr()) for (p, r, b, c, _) in launches]
-
-    def step():
-        for plan, r, b, c in raw:
-            plan.spmm_raw(b, c, N, r, stream)
+    step, _ = batch_step(launches, N, torch, args.streams)
 
     for _ in range(args.warmup):
         step()
@@ -460,7 +473,7 @@ def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
         "config": {"workload": f"OPT-30B decoder layer: 4 x 7168^2, 28672x7168, 7168x28672, {round(sp * 100)}% "
                                f"unstructured, fp16, N={N}", "nnz": nnz_l,
                    "plan": {k: per_shape[k]["plan"] for k in per_shape}, "kernel": {k: per_shape[k]["kernel"] for k in per_shape},
-                   "parallelism": "one GPU"},
+                   "parallelism": "one GPU", "streams": args.streams},
         "roofline": {"bound": "hbm", "achieved": round(alg_l / (ms_step * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg_l / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
                      "algorithmic_bytes_per_step": alg_l, "note": "whole layer step (six launches, host-timed)"},
@@ -657,7 +670,7 @@ def main():
         "variants": variants,
     }
     if args.n_sweep and rank == 0:
-        out["n_sweep"] = n_sweep(gsa, M, K, row, col, val, best_cand, args, dt, local, e, tdt, dev, torch, nnz)
+        out["n_sweep"] = n_sweep(gsa, M, K, row, col, val, cands, args, dt, local, e, tdt, dev, torch, nnz)
     if rank == 0 and not args.no_rocsparse:
         try:
             out.update(rocsparse_compare(gsa, M, K, N, row, col, val, dt, best_cand, args, local, flops, ev_ms, dev,
@@ -675,22 +688,39 @@ def main():
         dist.destroy_process_group()
 
 
-def n_sweep(gsa, M, K, row, col, val, cand, args, dt, local, e, tdt, dev, torch, nnz):
-    """the chosen pipeline at other dense widths (N in {8, 32, 128})"""
+def n_sweep(gsa, M, K, row, col, val, cands, args, dt, local, e, tdt, dev, torch, nnz):
+    """the workload's plan search at other dense widths (N in {8, 32, 128}): per N
+    every candidate plan is built for that N and timed (events, rotated replicas); the fastest
+    is reported with its kernel and HBM roofline fraction (algorithmic bytes at that N)"""
     out = []
+    s_idx = 2 if K <= 65536 else 4
     for n in [int(x) for x in args.n_sweep.split(",") if x]:
-        try:
-            plan, Bs, Cs, reps, _ = build_plan(gsa, M, K, row, col, val, cand, n, dt, local, args.rotation_mb, e, tdt,
-                                               dev, torch)
-        except gsa.GsError as ex:
-            out.append({"N": n, "error": str(ex)})
+        tried, best = {}, None
+        for cand in cands:
+            key = "%s(%d,%d)" % cand
+            try:
+                plan, Bs, Cs, reps, _ = build_plan(gsa, M, K, row, col, val, cand, n, dt, local, args.rotation_mb, e,
+                                                   tdt, dev, torch)
+            except gsa.GsError as ex:
+                tried[key] = {"error": str(ex)[:80]}
+                continue
+            ms = event_ms(plan, Bs, Cs, args.search_reps, torch)
+            kern = kernel_label(plan.info())
+            tried[key] = {"kernel": kern, "kernel_ms": round(ms, 5)}
+            if best is None or ms < best[0]:
+                best = (ms, key, kern)
+            plan.free()
+            del Bs, Cs
+            torch.cuda.empty_cache()
+        if best is None:
+            out.append({"N": n, "error": "no candidate plan runs", "tried": tried})
             continue
-        ms = event_ms(plan, Bs, Cs, args.search_reps, torch)
-        out.append({"N": n, "kernel": kernel_label(plan.info()), "kernel_ms": round(ms, 5),
-                    "gflops": round(2.0 * nnz * n / (ms * 1e-3) / 1e9, 1)})
-        plan.free()
-        del Bs, Cs
-        torch.cuda.empty_cache()
+        ms, key, kern = best
+        alg = (algorithmic_bytes_24(M, K, n, nnz, e) if args.workload == "c3" else
+               algorithmic_bytes(M, K, n, nnz, e, s_idx))
+        out.append({"N": n, "plan": key, "kernel": kern, "kernel_ms": round(ms, 5),
+                    "gflops": round(2.0 * nnz * n / (ms * 1e-3) / 1e9, 1),
+                    "hbm_frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "tried": tried})
     return out
 
 
