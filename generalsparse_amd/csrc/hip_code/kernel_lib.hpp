@@ -2258,6 +2258,224 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
 }
 
 // ---------------------------------------------------------------------------
+// k_nm_mfma_ks -- the same 2:4 panels (same HBM blocks as k_nm_mfma) with one 64-row
+// group per wave, four waves = 256 rows per workgroup and K split over `nsplit`
+// workgroups (config C3, N = 128).
+// Why: a k_nm_mfma workgroup (128 rows) streams all of B (1.8 MB at N = 128) for its
+// 1.0 MB of A, and one CU takes in only ~45-70 GB/s, so B is 64% of every CU's intake
+// (C3 runs at 69% of HBM at N = 32 and 40% at N = 128, profiles/r03_n_sweep.json).  Here a
+// workgroup owns 256 rows over half of K: B 0.9 MB + A 1.0 MB per CU (-32%).
+// One wave per SIMD: each wave holds its 64 x N fp32 tile (4 x CT accumulators, 128
+// registers at N = 128, the rest of the 512-register budget for the look-ahead), the A
+// blocks of the next 256-column chunk (four k-steps) in registers while it computes the
+// current one, and the B chunk is staged through registers by all 256 threads into a
+// double-buffered LDS image (b_piece permutation, one raw s_barrier per chunk: global
+// loads stay in flight across it).  No cross-wave reduction: every wave owns its rows.
+// K split: each wave publishes its fp32 tile (8-B agent-scope stores, its own vmcnt(0),
+// then one agent-scope add on its row group's counter); the wave whose add completes the
+// count sums the slabs in split order with agent-scope loads and stores C
+// (deterministic), then re-arms the counter.
+// ---------------------------------------------------------------------------
+template <int CT>
+__global__ __launch_bounds__(256) void k_nm_mfma_ks(const unsigned char *__restrict__ A,
+                                                   const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K,
+                                                   uint32_t S, uint32_t rows, uint32_t row_base, uint32_t nsplit,
+                                                   uint32_t ncs, float *__restrict__ slabs,
+                                                   uint32_t *__restrict__ arrivals) {
+    constexpr uint32_t N = 16 * CT, RB = 32 * CT, UB = 2 * CT;
+    constexpr uint32_t szB = kNmKC * RB;
+    constexpr uint32_t NTH = 256;
+    constexpr uint32_t NBU = szB / 16 / NTH;  // 16-B units of B per thread per chunk
+    constexpr uint32_t RPU = NTH / UB;        // B rows between a thread's units
+    static_assert(szB % (16 * NTH) == 0 && NTH % UB == 0, "whole B units per thread");
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t g = blockIdx.x / nsplit, sp = blockIdx.x - g * nsplit;
+    const uint32_t rg = g * 4u + wv;  // this wave's 64-row group
+    const uint32_t nch = S / 4u;
+    const uint32_t c0 = sp * ncs, ncl = min(nch, c0 + ncs) - c0;  // this workgroup's chunks
+    const unsigned char *arow = A + (size_t)rg * S * kNmBlockBytes;
+    const unsigned char *bbase = reinterpret_cast<const unsigned char *>(B);
+    const uint32_t bk = tid / UB, boff = bk * RB + (tid % UB) * 16u;  // this thread's first unit
+    auto bdst = [&](uint32_t i) {
+        const uint32_t k = bk + i * RPU, s = tid % UB;
+        return k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u;
+    };
+    // the four k-step blocks of chunk c (clamped: past the range re-reads the last)
+    auto aload = [&](uint32_t i, u32x4 (&V)[4][4], uint2 (&I)[4]) {
+        const uint32_t c = c0 + min(i, ncl - 1u);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const unsigned char *blk = arow + (size_t)(4u * c + q) * kNmBlockBytes;
+            I[q] = *reinterpret_cast<const uint2 *>(blk + lane * 8u);
+#pragma unroll
+            for (int rt = 0; rt < 4; rt++) V[q][rt] = *reinterpret_cast<const u32x4 *>(blk + 512u + rt * 1024u + lane * 16u);
+        }
+    };
+    u32x4 bs[NBU];
+    auto bload = [&](uint32_t i) {
+        const uint32_t k0 = (c0 + min(i, ncl - 1u)) * kNmKC;
+        if (k0 + kNmKC <= K) {
+            const unsigned char *src = bbase + (size_t)k0 * RB;
+#pragma unroll
+            for (uint32_t u = 0; u < NBU; u++) bs[u] = *reinterpret_cast<const u32x4 *>(src + u * RPU * RB + boff);
+        } else {
+#pragma unroll
+            for (uint32_t u = 0; u < NBU; u++) {
+                const uint32_t kk = min(k0 + bk + u * RPU, K - 1u);
+                bs[u] = *reinterpret_cast<const u32x4 *>(bbase + (size_t)kk * RB + (tid % UB) * 16u);
+            }
+        }
+    };
+    auto bstore = [&](uint32_t i) {
+        const uint32_t k0 = (c0 + min(i, ncl - 1u)) * kNmKC;
+        unsigned char *lb = lds + (i & 1u) * szB;
+        if (k0 + kNmKC <= K) {
+#pragma unroll
+            for (uint32_t u = 0; u < NBU; u++) *reinterpret_cast<u32x4 *>(lb + bdst(u)) = bs[u];
+        } else {  // rows past K: zeros
+#pragma unroll
+            for (uint32_t u = 0; u < NBU; u++) {
+                const uint32_t z = k0 + bk + u * RPU < K ? ~0u : 0u;
+                *reinterpret_cast<u32x4 *>(lb + bdst(u)) = bs[u] & z;
+            }
+        }
+    };
+    f4v acc[4][CT];
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+    const uint32_t kl0 = 8u * (lane >> 4) + ((lane & 15u) >> 2);
+    auto compute = [&](uint32_t i, const u32x4 (&V)[4][4], const uint2 (&I)[4]) {
+        const unsigned char *lb = lds + (i & 1u) * szB;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            h8v av[4];
+#pragma unroll
+            for (int rt = 0; rt < 4; rt++) __builtin_memcpy(&av[rt], &V[q][rt], 16);
+            const int ix0 = (int)I[q].x, ix1 = (int)I[q].y;
+            const uint32_t kl = 64u * q + kl0;
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) {
+                s4v t[4];
+#pragma unroll
+                for (int h = 0; h < 4; h++) {
+                    const uint32_t k = kl + 32u * (h >> 1) + 4u * (h & 1);
+                    t[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s4v *)(lb + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u));
+                }
+                h16v b;
+                __builtin_memcpy(&b, t, 32);
+                acc[0][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av[0], b, acc[0][ct], ix0, 0, 0);
+                acc[1][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av[1], b, acc[1][ct], ix0, 0, 1);
+                acc[2][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av[2], b, acc[2][ct], ix1, 0, 0);
+                acc[3][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av[3], b, acc[3][ct], ix1, 0, 1);
+            }
+        }
+    };
+    // LDS stores of this thread done, then a raw barrier (the look-ahead loads stay in flight)
+    auto barrier = [&]() {
+        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __asm__ volatile("" ::: "memory");
+    };
+    u32x4 va[4][4], vb[4][4];
+    uint2 ia[4], ib[4];
+    aload(0, va, ia);
+    bload(0);
+    bstore(0);
+    barrier();
+    // chunk i: B of i+1 and A of i+1 in flight while i computes; B of i+1 staged after it
+    uint32_t i = 0;
+    // (sched_barriers keep the look-ahead loads in front of the MFMAs: the scheduler would
+    // otherwise sink them past the compute to shorten register lifetimes)
+    for (; i + 1 < ncl; i += 2) {
+        bload(i + 1);
+        aload(i + 1, vb, ib);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(i, va, ia);
+        __builtin_amdgcn_sched_barrier(0);
+        bstore(i + 1);
+        barrier();
+        bload(i + 2);
+        aload(i + 2, va, ia);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(i + 1, vb, ib);
+        __builtin_amdgcn_sched_barrier(0);
+        bstore(i + 2);
+        barrier();
+    }
+    if (i < ncl) compute(i, va, ia);
+    // the trailing look-ahead loads land in registers only
+    const bool live = rg * 64u < rows;
+    auto store_tile = [&](const f4v (&v)[4][CT]) {
+#pragma unroll
+        for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++)
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const uint32_t r = rg * 64u + rt * 16u + 4u * (lane >> 4) + e;
+                    if (r < rows) C[(size_t)(row_base + r) * N + ct * 16u + (lane & 15u)] = (f16)v[rt][ct][e];
+                }
+    };
+    if (nsplit == 1) {
+        if (live) store_tile(acc);
+        return;
+    }
+    if (!live) return;  // a row group past the matrix has no counter traffic
+    // K split: this wave's tile -> its slab (8-B agent-scope stores: write-through, and
+    // compiler-visible, so the MFMA-result -> store wait states are inserted -- an inline-asm
+    // 16-B store of the accumulators read one register before the smfmac had written it),
+    // then one add
+    constexpr uint32_t TI = 4u * CT * 64u;  // f4v per wave tile
+    f4v *slab = reinterpret_cast<f4v *>(slabs) + ((size_t)rg * nsplit + sp) * TI;
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) {
+            uint64_t *dst = reinterpret_cast<uint64_t *>(slab + (rt * CT + ct) * 64u + lane);
+            uint64_t w[2];
+            __builtin_memcpy(w, &acc[rt][ct], 16);
+            __hip_atomic_store(dst, w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(dst + 1, w[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(&arrivals[rg], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old != nsplit - 1u) return;
+    if (lane == 0) __hip_atomic_store(&arrivals[rg], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const f4v *base = reinterpret_cast<const f4v *>(slabs) + (size_t)rg * nsplit * TI;
+    f4v sum[4][CT];
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) sum[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+    for (uint32_t qq = 0; qq < nsplit; qq++) {
+#pragma unroll
+        for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) {
+                if (qq == sp) {
+                    sum[rt][ct] += acc[rt][ct];
+                } else {
+                    const uint64_t *src = reinterpret_cast<const uint64_t *>(base + (size_t)qq * TI + (rt * CT + ct) * 64u + lane);
+                    uint64_t w[2];
+                    w[0] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    w[1] = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    f4v x;
+                    __builtin_memcpy(&x, w, 16);
+                    sum[rt][ct] += x;
+                }
+            }
+    }
+    store_tile(sum);
+}
+
+// ---------------------------------------------------------------------------
 // k_merge_path -- merge-path levels (merge_path_{thread,warp,tblock}_operator +
 // the level's total-reduce token).  The plan's
 // level starts (first_row_indices_without_ending / first_nz_indices,

@@ -217,7 +217,8 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
     const uint32_t N = L.N, CT = L.kind == mc_layout::NM ? N / 16 : ks_ct(N);
     const char *kname = L.kind == mc_layout::KS ? "k_mfma_ks"
                         : L.kind == mc_layout::BM ? "k_mfma_bm"
-                        : (L.kind == mc_layout::ROWS ? "k_mfma_rows" : "k_nm_mfma");
+                        : L.kind == mc_layout::ROWS ? "k_mfma_rows"
+                        : (L.nm_ks ? "k_nm_mfma_ks" : "k_nm_mfma");
     o << "// kernel_file.hip -- generated by generalsparse_amd code_generator: the matrix-core kernel " << kname << "\n"
       << "// build: sh make_kernel.sh; run: ./a.out [matrix.mtx] [N]  -> perf_result (ms, GFLOP/s)\n"
       << "#include \"kernel_lib.hpp\"\n#include <cstdio>\n#include <cstdlib>\n#include <cstring>\n#include <fstream>\n"
@@ -304,6 +305,18 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
                  std::to_string(t.lds_bytes) + ">>>(d_tbr, d_seg, (const gsk::u32x4 *)d_pos, (const gsk::u32x4 *)d_val, d_B, d_C, " +
                  "(uint32_t)K, N, " + std::to_string(t.nc) + "u, " + std::to_string(t.RMAX) + "u, 0u, " +
                  std::to_string(L.rows_ksplit) + "u, " + std::to_string(L.rows_ncs) + "u, d_ws, d_arr, nullptr, 0u)";
+    } else if (L.nm_ks) {
+        const uint64_t nb = (L.nm_rows + 255) / 256, ngr = nb * 4;
+        o << "    unsigned char *d_blk = up(rdb<unsigned char>(\"THREAD_META_nm_panels_0.bin\"));\n"
+          << "    float *d_ws; uint32_t *d_arr; hipMalloc(&d_ws, " << ngr * L.nm_split * 64 * N * 4 << "ull + 16);\n"
+          << "    hipMalloc(&d_arr, " << ngr * 4 << "ull); hipMemset(d_arr, 0, " << ngr * 4 << "ull);\n";
+        const std::string k = "gsk::k_nm_mfma_ks<" + std::to_string(CT) + ">";
+        const size_t lds = (size_t)2 * gsk::kNmKC * 32 * CT;
+        setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
+                std::to_string(lds) + ")";
+        launch = k + "<<<" + std::to_string(nb * L.nm_split) + ", 256, " + std::to_string(lds) +
+                 ">>>(d_blk, d_B, d_C, (uint32_t)K, " + std::to_string(L.nm_S) + "u, " + std::to_string(L.nm_rows) +
+                 "u, 0u, " + std::to_string(L.nm_split) + "u, " + std::to_string(L.nm_ncs) + "u, d_ws, d_arr)";
     } else {
         o << "    unsigned char *d_blk = up(rdb<unsigned char>(\"THREAD_META_nm_panels_0.bin\"));\n";
         const std::string k = "gsk::k_nm_mfma<" + std::to_string(CT) + ">";

@@ -406,7 +406,7 @@ bool build_nm_panels(const std::vector<uint64_t> &rows, const std::vector<uint64
     const uint64_t nnz = col.size();
     if (row_num == 0 || K == 0 || nnz == 0) { why = "empty sub-matrix"; return false; }
     const uint64_t S64 = (K + gsk::kNmKC - 1) / gsk::kNmKC * 4;  // k-steps, whole 256-column chunks
-    const uint64_t ng = (row_num + 127) / 128 * 2;               // 64-row groups, two per workgroup
+    const uint64_t ng = (row_num + 255) / 256 * 4;               // 64-row groups, whole 256-row workgroups
     const double slots = (double)ng * 64.0 * (double)S64 * 32.0;
     if (slots > 2.0 * (double)nnz && slots > (double)(1 << 22)) {  // small plans always qualify
         why = "2:4 panels would store over twice the entries";
@@ -483,6 +483,13 @@ mc_layout choose_matrix_core_layout(const meta_data_set &m, const kernel_spec &s
         if (build_nm_panels(rows, col, *vals, row_num, K, L.nm_blk, L.nm_S, L.why)) {
             L.kind = mc_layout::NM;
             L.nm_rows = row_num;
+            // k_nm_mfma_ks (NM_KS): 256-row workgroups, K split so they cover the CUs
+            const uint32_t nch = L.nm_S / 4, nb = (uint32_t)((row_num + 255) / 256);
+            uint32_t sp = cfg.NM_SPLIT > 0 ? (uint32_t)cfg.NM_SPLIT : std::max<uint32_t>(1, 256 / std::max<uint32_t>(nb, 1));
+            sp = std::max(1u, std::min(sp, nch));
+            L.nm_ks = cfg.NM_KS != 0;
+            L.nm_ncs = (nch + sp - 1) / sp;
+            L.nm_split = (nch + L.nm_ncs - 1) / L.nm_ncs;
         }
         return L;
     }

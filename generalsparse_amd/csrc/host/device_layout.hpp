@@ -99,6 +99,8 @@ struct mc_layout {
     std::vector<unsigned char> nm_blk;  // k_nm_mfma blocks
     uint32_t nm_S = 0;                  // ... k-steps per row group
     uint64_t nm_rows = 0;
+    bool nm_ks = false;                    // k_nm_mfma_ks (256-row workgroups, K split) instead of k_nm_mfma
+    uint32_t nm_split = 1, nm_ncs = 0;     // ... K ranges per row block, 256-column chunks per range
     std::string why;  // why NONE
 };
 mc_layout choose_matrix_core_layout(const meta_data_set &m, const kernel_spec &sp, int sb, uint64_t K, int dtype);

@@ -41,6 +41,7 @@ struct device_plan {
     size_t bytes_A = 0;       // device bytes of A per replica (metadata + cols + vals)
     // LDS-stationary B (k_lds_rows): chunk geometry fixed for dense width lds_N
     bool lds = false;
+    bool nm_ks = false;  // k_nm_mfma_ks (ksplit K ranges of ncs chunks; ws slabs + t2 counters when ksplit > 1)
     bool nm = false;    // k_nm_mfma: 2:4 panels of a col-direction plan (A blocks in tcol; k-steps in KC)
     bool mfma = false;  // k_mfma_rows (uses KC, nc, lds_bytes; log2 KC in RSB; RT in maxr; RMAX in rpw_max)
     bool ks = false;    // k_mfma_ks: K split over ksplit workgroups per row block, B slice in LDS

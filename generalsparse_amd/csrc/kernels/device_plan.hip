@@ -274,13 +274,21 @@ void upload_plan(plan_state &p, int dtype, int device) {
     if (mc.kind == mc_layout::NM) {
         // col-direction BMTs that are 2:4 panels: sparse matrix cores, self-contained blocks
         d.nm = true;
-        d.kernel = "k_nm_mfma";
+        d.kernel = mc.nm_ks ? "k_nm_mfma_ks" : "k_nm_mfma";
         d.KC = mc.nm_S;
         d.n_rows_aux = mc.nm_rows;
         d.n_units = m.u(THREAD_META, "first_nz_indices", sb).size() - 1;
-        d.waves = gsk::kNmWaves;
+        d.waves = mc.nm_ks ? 4 : gsk::kNmWaves;
+        d.nm_ks = mc.nm_ks;
+        d.ksplit = mc.nm_ks ? mc.nm_split : 1;
+        d.ncs = mc.nm_ncs;
         a.tcol = dev_copy(d, mc.nm_blk);
         d.bytes_tile = d.bytes_A;
+        if (mc.nm_ks && mc.nm_split > 1) {  // fp32 slabs (one 64 x N tile per row group and K range) + counters
+            const uint64_t ngr = (mc.nm_rows + 255) / 256 * 4;
+            a.ws = dev_copy(d, std::vector<float>((size_t)ngr * mc.nm_split * 64 * mc.N, 0.f));
+            a.t2 = dev_copy(d, std::vector<uint32_t>((size_t)ngr, 0u));
+        }
         d.replicas.push_back(a);
         p.uploaded = true;
         return;

@@ -146,6 +146,27 @@ void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, vo
             g = true;
         }
     }
+    if (d.nm_ks) {
+        auto kk = gsk::k_nm_mfma_ks<CT>;
+        const size_t lds2 = (size_t)2 * gsk::kNmKC * 32 * CT;
+        static std::mutex mu2;
+        static std::map<std::pair<int, const void *>, bool> granted2;
+        {
+            std::lock_guard<std::mutex> l(mu2);
+            bool &g = granted2[{d.device, reinterpret_cast<const void *>(kk)}];
+            if (!g) {
+                HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kk), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds2));
+                g = true;
+            }
+        }
+        const uint32_t nb = (uint32_t)((d.n_rows_aux + 255) / 256);
+        hipLaunchKernelGGL(kk, dim3(nb * d.ksplit), dim3(256), lds2, s, (const unsigned char *)a.tcol, (const gsk::f16 *)B,
+                           (gsk::f16 *)C, (uint32_t)p.K, d.KC, (uint32_t)d.n_rows_aux, (uint32_t)d.row_base, d.ksplit,
+                           d.ncs, a.ws, a.t2);
+        HIP_OK(hipGetLastError());
+        return;
+    }
     const uint32_t wg = (uint32_t)((d.n_rows_aux + 127) / 128);
     hipLaunchKernelGGL(kern, dim3(wg), dim3(64 * gsk::kNmWaves), lds, s, (const unsigned char *)a.tcol,
                        (const gsk::f16 *)B, (gsk::f16 *)C, (uint32_t)p.K, d.KC, (uint32_t)d.n_rows_aux,

@@ -148,3 +148,32 @@ def test_nm_c3_scale_against_dense():
     C = plan.spmm(B.to(DEV))
     torch.cuda.synchronize()
     check(C.float().cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("ks,split", [(0, 0), (1, 1), (1, 3), (1, 0)])
+@pytest.mark.parametrize("N", [32, 128])
+@pytest.mark.parametrize("shape", [(333, 772), (520, 3000), (1, 4096)], ids=lambda s: f"{s[0]}x{s[1]}")
+def test_nm_ks_and_classic_kernels(shape, N, ks, split):
+    """k_nm_mfma_ks (256-row workgroups, K split over NM_SPLIT ranges, slab combine by the
+    last arriver) and the classic k_nm_mfma: oracle parity, determinism, replicas"""
+    old = {k: gsa.get_config(k) for k in ("NM_KS", "NM_SPLIT")}
+    try:
+        gsa.set_config("NM_KS", ks)
+        gsa.set_config("NM_SPLIT", split)
+        M, K = shape
+        r, c, v = thinned(M, K, 70 + M, keep=0.8, empty_rows=(0, M // 2))
+        plan = plan_for(M, K, r, c, v, N)
+        assert plan.info()["device_kernel"] == ("k_nm_mfma_ks" if ks else "k_nm_mfma"), plan.info()
+        B = np.random.default_rng(M + N).uniform(-1, 1, (K, N)).astype(np.float16)
+        ref = ofi.spmm_ref(M, N, r, c, v.astype(np.float16).astype(np.float32), B.astype(np.float32), "f64")
+        C = spmm(plan, B)
+        check(C, ref)
+        np.testing.assert_array_equal(spmm(plan, B), C)  # counters re-armed, same order
+        plan.add_replica()
+        C1 = plan.spmm(torch.from_numpy(B).to(DEV), replica=1)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(C1.float().cpu().numpy(), C)
+        plan.free()
+    finally:
+        for k, val in old.items():
+            gsa.set_config(k, val)
