@@ -2007,6 +2007,184 @@ __global__ __launch_bounds__(64 * W) void k_mfma_bm(const uint32_t *__restrict__
 }
 
 // ---------------------------------------------------------------------------
+// k_mfma_bm2 -- k_mfma_bm's layout with one wave per 16-row tile (RT waves per
+// workgroup): no cross-wave reduction, and every wave streams its tile's records and
+// value windows through register rings (records 16 k-steps ahead, values 8 ahead) while
+// the workgroup's B slice (NS k-steps, staged once by all waves, one barrier) stays in
+// LDS.  K split: each wave publishes its 16 x N fp32 tile (8-B agent-scope stores), one
+// agent-scope add per (row block, tile), the last adder sums the slabs in K-range order
+// (deterministic) and stores C.
+// ---------------------------------------------------------------------------
+template <int CT, int RT>
+__global__ __launch_bounds__(64 * RT) void k_mfma_bm2(const uint32_t *__restrict__ bmtb_first_row,  // nb+1
+                                                     const uint2 *__restrict__ rec, const uint32_t *__restrict__ sbase,
+                                                     const f16 *__restrict__ vals, const f16 *__restrict__ B,
+                                                     f16 *__restrict__ C, uint32_t K, uint32_t N, uint32_t S,
+                                                     uint32_t NS, uint32_t nwg, uint32_t row_base,
+                                                     float *__restrict__ slabs, uint32_t *__restrict__ arrivals) {
+    constexpr uint32_t RB = 32 * CT, UB = 2 * CT, STG = 32u * RB;
+    constexpr uint32_t DR = 16, DV = 8;  // look-ahead of the records / value windows (k-steps)
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // = this wave's row tile
+    const uint32_t u = xcd_block(blockIdx.x, nwg);
+    const uint32_t g = u / S, q = u - g * S;
+    const uint32_t col0 = blockIdx.y * 16u * CT, nv = min(16u * CT, N - col0);
+    uint2 *lut = reinterpret_cast<uint2 *>(lds);
+    unsigned char *bsl = lds + 128u;  // NS k-steps of B rows
+    if (tid < 16u) lut[tid] = make_uint2(bm_sel(tid, 0), bm_sel(tid, 1));
+    const uint32_t k0 = q * NS * 32u;
+    const size_t ub = (size_t)u * NS;
+    const uint32_t tsh = 8u * (wv & 3u);  // this tile's mask byte in the record word
+    auto mask_of = [&](const uint2 &r) -> uint32_t { return ((wv < 4u ? r.x : r.y) >> tsh) & 0xffu; };
+    // the value offset of this lane's run for this tile: the record's lane offset + the
+    // values of the lower tiles (bytes below this tile's)
+    auto vstart = [&](const uint2 &r, uint32_t sb) -> uint32_t {
+        uint32_t lower = wv < 4u ? (wv ? r.x & ((1u << (8u * wv)) - 1u) : 0u)
+                                 : r.x;
+        uint32_t p = sb + (r.y >> 16) + (uint32_t)__builtin_popcount(lower);
+        if (wv >= 4u) p += (uint32_t)__builtin_popcount(r.y & ((1u << (8u * (wv - 4u))) - 1u) & 0xffffu);
+        return p;
+    };
+    auto ld_rec = [&](uint32_t s, uint32_t &sb) -> uint2 {
+        const uint32_t ss = s < NS ? s : NS - 1u;
+        sb = sbase[ub + ss];
+        return rec[(ub + ss) * 64u + lane];
+    };
+    auto ld_vals = [&](const uint2 &r, uint32_t sb, u32x2_a2 (&V)[2]) {
+        const uint32_t p = vstart(r, sb), m = mask_of(r);
+        V[0] = *reinterpret_cast<const u32x2_a2 *>(vals + p);
+        V[1] = *reinterpret_cast<const u32x2_a2 *>(vals + p + __builtin_popcount(m & 15u));
+    };
+    // records of the first DR steps (the critical HBM chain) before the B slice
+    uint2 rr[DR];
+    uint32_t rs[DR];
+#pragma unroll
+    for (uint32_t j = 0; j < DR; j++) rr[j] = ld_rec(j, rs[j]);
+    // B slice: step s staged by wave s % RT (registers -> ds_write_b128, b_piece permutation)
+    for (uint32_t s = wv; s < NS; s += RT) {
+        const uint32_t kr = k0 + s * 32u;
+        u32x4 br[CT];
+#pragma unroll
+        for (uint32_t c = 0; c < CT; c++) {
+            const uint32_t un = c * 64u + lane, k = un / UB, cu = (un % UB) * 8u;
+            const uint32_t kk = kr + k < K ? kr + k : K - 1u;
+            br[c] = *reinterpret_cast<const u32x4 *>(B + (size_t)kk * N + col0 + (cu < nv ? cu : 0u));
+        }
+#pragma unroll
+        for (uint32_t c = 0; c < CT; c++) {
+            const uint32_t un = c * 64u + lane, k = un / UB, sx = un % UB;
+            *reinterpret_cast<u32x4 *>(bsl + s * STG + k * RB + b_piece<CT>(k, sx >> 1) * 32u + (sx & 1u) * 16u) = br[c];
+        }
+    }
+    // the value windows of the first DV steps
+    u32x2_a2 vv[DV][2];
+#pragma unroll
+    for (uint32_t j = 0; j < DV; j++) ld_vals(rr[j], rs[j], vv[j]);
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // the B slice and the selector table
+    __asm__ volatile("" ::: "memory");
+    f4v acc[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ct++) acc[ct] = f4v{0.f, 0.f, 0.f, 0.f};
+    const uint32_t kb = 8u * (lane >> 4);
+    // step i (ring slots i % DR, i % DV): compute i, then refill: values of i + DV (their
+    // record is in slot (i + DV) % DR), record of i + DR
+    for (uint32_t i0 = 0; i0 < NS; i0 += DR) {
+#pragma unroll
+        for (uint32_t d = 0; d < DR; d++) {
+            const uint32_t i = i0 + d;
+            if (i < NS) {
+                const unsigned char *bst = bsl + i * STG;
+                const uint32_t m = mask_of(rr[d]);
+                const uint2 sl = lut[m & 15u], sh = lut[m >> 4];
+                const u32x2_a2 lo = vv[d % DV][0], hi = vv[d % DV][1];
+                uint32_t w[4];
+                w[0] = __builtin_amdgcn_perm(lo.y, lo.x, sl.x);
+                w[1] = __builtin_amdgcn_perm(lo.y, lo.x, sl.y);
+                w[2] = __builtin_amdgcn_perm(hi.y, hi.x, sh.x);
+                w[3] = __builtin_amdgcn_perm(hi.y, hi.x, sh.y);
+                h8v a;
+                __builtin_memcpy(&a, w, 16);
+#pragma unroll
+                for (int ct = 0; ct < CT; ct++) {
+                    s4v t2[2];
+#pragma unroll
+                    for (int hh = 0; hh < 2; hh++) {
+                        const uint32_t k = kb + 4u * hh + ((lane & 15u) >> 2);
+                        t2[hh] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                            (lds_s4v *)(bst + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u));
+                    }
+                    h8v bv;
+                    __builtin_memcpy(&bv, t2, 16);
+                    acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bv, acc[ct], 0, 0, 0);
+                }
+            }
+            // refill (past NS: re-reads of the last step, never used)
+            ld_vals(rr[(d + DV) % DR], rs[(d + DV) % DR], vv[d % DV]);
+            rr[d] = ld_rec(i + DR, rs[d]);
+        }
+    }
+    const uint32_t r0 = bmtb_first_row[g], R = bmtb_first_row[g + 1] - r0;
+    auto store_tile = [&](const f4v (&v)[CT]) {
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) {
+            const uint32_t col = 16u * ct + (lane & 15u);
+            if (col >= nv) continue;
+#pragma unroll
+            for (uint32_t e = 0; e < 4; e++) {
+                const uint32_t rw = 16u * wv + 4u * (lane >> 4) + e;
+                if (rw < R) C[(size_t)(row_base + r0 + rw) * N + col0 + col] = (f16)v[ct][e];
+            }
+        }
+    };
+    if (S == 1) {
+        store_tile(acc);
+        return;
+    }
+    if (16u * wv >= R) return;  // a tile past the block's rows: no counter traffic
+    // K split hand-off per (row block, tile, column tile)
+    constexpr uint32_t TI = CT * 64u;
+    const size_t tix = ((size_t)g * gridDim.y + blockIdx.y) * RT + wv;
+    f4v *slab = reinterpret_cast<f4v *>(slabs) + (tix * S + q) * TI;
+#pragma unroll
+    for (int ct = 0; ct < CT; ct++) {
+        uint64_t *dst = reinterpret_cast<uint64_t *>(slab + ct * 64u + lane);
+        uint64_t w[2];
+        __builtin_memcpy(w, &acc[ct], 16);
+        __hip_atomic_store(dst, w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(dst + 1, w[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(&arrivals[tix], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old != S - 1u) return;
+    if (lane == 0) __hip_atomic_store(&arrivals[tix], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    f4v sum[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ct++) sum[ct] = f4v{0.f, 0.f, 0.f, 0.f};
+    const f4v *base = reinterpret_cast<const f4v *>(slabs) + tix * S * TI;
+    for (uint32_t qq = 0; qq < S; qq++) {
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) {
+            if (qq == q) {
+                sum[ct] += acc[ct];
+            } else {
+                const uint64_t *src = reinterpret_cast<const uint64_t *>(base + (size_t)qq * TI + ct * 64u + lane);
+                uint64_t w[2];
+                w[0] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                w[1] = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                f4v x;
+                __builtin_memcpy(&x, w, 16);
+                sum[ct] += x;
+            }
+        }
+    }
+    store_tile(sum);
+}
+
+// ---------------------------------------------------------------------------
 // k_nm_mfma -- fixed_interval_col_direction BMTs that are 2:4 panels
 //  on the sparse matrix cores:
 // v_smfmac_f32_16x16x64_f16 multiplies a 16x64 A tile stored as 16x32 values

@@ -216,7 +216,7 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
     std::ostringstream o;
     const uint32_t N = L.N, CT = L.kind == mc_layout::NM ? N / 16 : ks_ct(N);
     const char *kname = L.kind == mc_layout::KS ? "k_mfma_ks"
-                        : L.kind == mc_layout::BM ? "k_mfma_bm"
+                        : L.kind == mc_layout::BM ? (L.bm.v2 ? "k_mfma_bm2" : "k_mfma_bm")
                         : L.kind == mc_layout::ROWS ? "k_mfma_rows"
                         : (L.nm_ks ? "k_nm_mfma_ks" : "k_nm_mfma");
     o << "// kernel_file.hip -- generated by generalsparse_amd code_generator: the matrix-core kernel " << kname << "\n"
@@ -273,10 +273,11 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
           << "    uint32_t *d_sb = up(rdb<uint32_t>(\"TBLOCK_META_mfma_bm_step_base_0.bin\"));\n"
           << "    uint16_t *d_val = up(rdb<uint16_t>(\"TBLOCK_META_mfma_bm_values_0.bin\"));\n"
           << "    float *d_ws; uint32_t *d_arr; hipMalloc(&d_ws, " << nwg * ks_col_tiles(N) * 256 * t.RT * CT * 4 << "ull + 16);\n"
-          << "    hipMalloc(&d_arr, " << nb * ks_col_tiles(N) * 4 << "ull + 4); hipMemset(d_arr, 0, " << nb * ks_col_tiles(N) * 4
-          << "ull + 4);\n";
-        const std::string k = "gsk::k_mfma_bm<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ", " +
-                              std::to_string(t.W) + ", " + std::to_string(gsk::bm_nbt(CT, t.RT)) + ">";
+          << "    hipMalloc(&d_arr, " << nb * ks_col_tiles(N) * t.RT * 4 << "ull + 4); hipMemset(d_arr, 0, "
+          << nb * ks_col_tiles(N) * t.RT * 4 << "ull + 4);\n";
+        const std::string k = t.v2 ? "gsk::k_mfma_bm2<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ">"
+                                   : "gsk::k_mfma_bm<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ", " +
+                                         std::to_string(t.W) + ", " + std::to_string(gsk::bm_nbt(CT, t.RT)) + ">";
         setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
                 std::to_string(t.lds_bytes) + ")";
         launch = k + "<<<dim3(" + std::to_string(nwg) + ", " + std::to_string(ks_col_tiles(N)) + "), " +

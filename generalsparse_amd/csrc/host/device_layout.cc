@@ -339,6 +339,13 @@ bool build_bm_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     t.RMAX = (uint32_t)rmax;
     t.W = W;
     t.lds_bytes = gsk::bm_lds_bytes(ks_ct(N), RT, W);
+    // k_mfma_bm2 when the range's B slice fits LDS next to the selector table
+    const size_t slice = 128u + (size_t)t.NS * 32u * 32u * ks_ct(N);
+    t.v2 = get_config().BM_V2 && slice <= 160u * 1024u;
+    if (t.v2) {
+        t.lds_bytes = slice;
+        t.W = RT;
+    }
     const uint64_t nrec = nb * S * t.NS * 64;
     GS_CHECK(nrec < (1ull << 31), "k_mfma_bm layout exceeds 31-bit record indices");
     t.rec.assign(nrec * 2, 0u);

@@ -91,6 +91,8 @@ struct config_t {
     bool MFMA_BM = false;        // fp16 BMTB row blocks of <= 96 rows: bitmap records, k_mfma_bm
     int64_t BM_SPLIT = 0;        // k_mfma_bm K ranges per row block (0: fill the CUs)
     int64_t BM_WAVES = 8;        // k_mfma_bm waves per workgroup (4 or 8)
+    bool BM_V2 = false;          // ... k_mfma_bm2 (one wave per row tile) when the B slice fits LDS
+                                 // (C2 22.9 us against 18.4 for k_mfma_bm, profiles/r03_c2_bm_timeline.json)
     bool MFMA_KS = true;         // row blocks of >= KS_MIN_ROWS rows: K-split, B-stationary k_mfma_ks
     int64_t KS_MIN_ROWS = 40;    // ... from this many rows per BMTB (shorter blocks: k_mfma_rows)
     bool MP_ROWS = false;        // merge-path plans: k_merge_rows (product/row walk) instead of k_merge_path

@@ -341,7 +341,8 @@ void upload_plan(plan_state &p, int dtype, int device) {
             const bm_tiles &bt = mc.bm;
             d.mfma = true;
             d.bm = true;
-            d.kernel = "k_mfma_bm";
+            d.bm2 = bt.v2;
+            d.kernel = bt.v2 ? "k_mfma_bm2" : "k_mfma_bm";
             d.lds_N = mc.N;
             d.ksplit = bt.S;
             d.ks_ns = bt.NS;
@@ -360,7 +361,8 @@ void upload_plan(plan_state &p, int dtype, int device) {
             if (bt.S > 1) {
                 const uint32_t nt = ks_col_tiles(mc.N), CT = ks_ct(mc.N);
                 a.ws = dev_copy(d, std::vector<float>((size_t)nb * bt.S * nt * 256 * bt.RT * CT, 0.f));
-                a.t2 = dev_copy(d, std::vector<uint32_t>((size_t)nb * nt, 0u));  // arrival counters
+                // arrival counters: per (row block, column tile), per row tile too for k_mfma_bm2
+                a.t2 = dev_copy(d, std::vector<uint32_t>((size_t)nb * nt * (bt.v2 ? bt.RT : 1u), 0u));
             }
             return true;
         }

@@ -19,8 +19,13 @@ def _decode(d, M, K, tbr):
     val = np.fromfile(os.path.join(d, "TBLOCK_META_mfma_bm_values_0.bin"), np.uint16).view(np.float16)
     src = open(os.path.join(d, "kernel_file.hip")).read()
     m = re.search(r"k_mfma_bm<(\d+), (\d+), (\d+), \d+>.*\(uint32_t\)K, N, (\d+)u, (\d+)u, (\d+)u, 0u, d_ws", src)
-    assert m, "no k_mfma_bm launch in the emitted program"
-    CT, RT, W, S, NS, nwg = map(int, m.groups())
+    if m:
+        CT, RT, W, S, NS, nwg = map(int, m.groups())
+    else:
+        m = re.search(r"k_mfma_bm2<(\d+), (\d+)>.*\(uint32_t\)K, N, (\d+)u, (\d+)u, (\d+)u, 0u, d_ws", src)
+        assert m, "no k_mfma_bm / k_mfma_bm2 launch in the emitted program"
+        CT, RT, S, NS, nwg = map(int, m.groups())
+        W = RT
     nb = len(tbr) - 1
     assert nwg == nb * S and len(sb) == nb * S * NS + 1 and len(rec) == nb * S * NS * 64
     KR = 32 * NS
@@ -53,16 +58,18 @@ def _decode(d, M, K, tbr):
     return dense, cnt, (CT, RT, W, S, NS)
 
 
+@pytest.mark.parametrize("v2", [0, 1])
 @pytest.mark.parametrize("p0,split,waves", [(80, 0, 8), (40, 0, 4), (96, 3, 8), (20, 1, 8), (7, 2, 4)])
-def test_bm_layout_decodes_to_the_matrix(tmp_path, p0, split, waves):
+def test_bm_layout_decodes_to_the_matrix(tmp_path, p0, split, waves, v2):
     M, K, N = 300, 500, 32
     row, col, val = ds.pruned_weight(M, K, 0.7, 31)
-    old = {k: gsa.get_config(k) for k in ("MFMA_BM", "BM_SPLIT", "BM_WAVES", "HALF")}
+    old = {k: gsa.get_config(k) for k in ("MFMA_BM", "BM_SPLIT", "BM_WAVES", "HALF", "BM_V2")}
     try:
         gsa.set_config("MFMA_BM", 1)
         gsa.set_config("BM_SPLIT", split)
         gsa.set_config("BM_WAVES", waves)
         gsa.set_config("HALF", 1)
+        gsa.set_config("BM_V2", v2)
         p = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline("block_total", N, p0, 1).compile()
         d = p.generate_program(tmp_path, repeat=10)
         tbr = p.array("TBLOCK_META_first_row_indices_0")
@@ -70,7 +77,8 @@ def test_bm_layout_decodes_to_the_matrix(tmp_path, p0, split, waves):
         for k, v in old.items():
             gsa.set_config(k, v)
     dense, cnt, (CT, RT, W, S, NS) = _decode(d, M, K, tbr)
-    assert W == waves and RT == (max(np.diff(tbr.astype(np.int64))) + 15) // 16
+    assert RT == (max(np.diff(tbr.astype(np.int64))) + 15) // 16
+    assert W == (RT if v2 else waves)
     if split:
         assert S == split
     ref = np.zeros((M, K), np.float64)

@@ -17,7 +17,7 @@ DEV = "cuda:0"
 
 @pytest.fixture
 def bm_on():
-    old = {k: gsa.get_config(k) for k in ("MFMA_BM", "BM_SPLIT", "BM_WAVES", "MFMA_MAX_FILL")}
+    old = {k: gsa.get_config(k) for k in ("MFMA_BM", "BM_SPLIT", "BM_WAVES", "MFMA_MAX_FILL", "BM_V2")}
     gsa.set_config("MFMA_BM", 1)
     gsa.set_config("MFMA_MAX_FILL", 1 << 30)
     yield
@@ -50,14 +50,16 @@ SHAPES = [(p0, N, split, waves) for p0 in (7, 40, 96) for N in (8, 16, 32, 64, 1
           for waves in (8,)] + [(p0, 32, split, waves) for p0 in (20, 80) for split in (0, 1, 3) for waves in (8, 4)]
 
 
+@pytest.mark.parametrize("v2", [0, 1])
 @pytest.mark.parametrize("p0,N,split,waves", SHAPES)
-def test_bm_matches_oracle(p0, N, split, waves, bm_on):
+def test_bm_matches_oracle(p0, N, split, waves, v2, bm_on):
     gsa.set_config("BM_SPLIT", split)
     gsa.set_config("BM_WAVES", waves)
+    gsa.set_config("BM_V2", v2)
     for case, M, K, row, col, val in cases():
         plan, C, B = run(M, K, row, col, val, p0, N)
         info = plan.info()
-        assert info["device_kernel"] == "k_mfma_bm", (case, info)
+        assert info["device_kernel"] in ("k_mfma_bm", "k_mfma_bm2"), (case, info)
         ref = ofi.spmm_ref(M, N, row, col, val.astype(np.float16).astype(np.float32), B.astype(np.float32), "f64")
         err = np.abs(C - ref) / np.maximum(1.0, np.abs(ref))
         assert err.max() <= 1e-1, (case, err.max())
@@ -73,7 +75,7 @@ def test_bm_known_answer_and_c2(bm_on):
     M, K, N = 700, 9000, 32
     row, col, _ = ds.random_rows(M, K, 700.0, seed=8, empty_frac=0.1)  # row nnz < 2048: exact in fp16
     plan, C, _ = run(M, K, row, col, np.ones(len(row), np.float32), 64, N, B=np.ones((K, N), np.float16))
-    assert plan.info()["device_kernel"] == "k_mfma_bm"
+    assert plan.info()["device_kernel"] in ("k_mfma_bm", "k_mfma_bm2")
     nnz_row = np.bincount(row.astype(np.int64), minlength=M).astype(np.float32)
     np.testing.assert_array_equal(C, np.repeat(nnz_row[:, None], N, axis=1))
     M = K = 5120
@@ -85,7 +87,7 @@ def test_bm_known_answer_and_c2(bm_on):
     for p0 in (80, 40):
         plan = gsa.Plan.from_coo(M, K, r, c, v).run_pipeline("block_total", N, p0, 1).compile().upload("f16", 0)
         info = plan.info()
-        assert info["device_kernel"] == "k_mfma_bm" and info["ksplit"] == 256 // (M // p0), info
+        assert info["device_kernel"] in ("k_mfma_bm", "k_mfma_bm2") and info["ksplit"] == 256 // (M // p0), info
         C = plan.spmm(B).float()
         err = ((C - ref).abs() / ref.abs().clamp(min=1.0)).max().item()
         assert err <= 1e-1, err
