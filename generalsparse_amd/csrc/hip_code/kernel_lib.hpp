@@ -1069,8 +1069,13 @@ __device__ __forceinline__ uint32_t b_piece(uint32_t k, uint32_t p) {
 // WCT: compute waves (the entry waves are the other 16 - WCT - B waves)
 // DBG (diagnostic timing builds only, wrong results): 1 no B DMA, 2 no scatter, 4 no compute-wave
 // LDS reads or clears, 8 no entry loads
+// FLG (round 3, MFMA_FLAGS, LDS-DMA variant only): the roles hand buffers over through three
+// LDS counters instead of one workgroup barrier per chunk -- B full (B waves, after the
+// chunk's DMA retired), image full (entry waves, after the scatter), chunk consumed (compute
+// waves, after their reads and clears); each wave waits (s_sleep polling) only for what
+// it consumes, so a role runs ahead of the others by the ring depth
 template <int CT, int RT, int LGKC, int MAXA, bool STAMPS = false, int GLDS = 0, int NBG = 3, int WCT = kMfmaCompute,
-          int DBG = 0>
+          int DBG = 0, bool FLG = false>
 __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
     const uint32_t *__restrict__ seg_start,       // n_bmtb*nc+1 (groups)
@@ -1098,7 +1103,27 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     // k-step columns it read
     constexpr uint32_t NBUF = GLDS ? (uint32_t)NBG : 2u, NDI = GLDS ? 2u : 3u;
     static_assert(!GLDS || NBG >= 3, "LDS-DMA B ring of at least three buffers");
+    static_assert(!FLG || (GLDS && !STAMPS), "counter hand-offs: LDS-DMA variant, no stamps");
     const uint32_t oD = NBUF * szB;                   // dense images follow the B buffers
+    constexpr uint32_t NAW = kMfmaWaves - WCT - (GLDS ? GLDS : kMfmaBWaves);  // entry waves
+    // FLG counters (in the launch's 1 KB tail slack): [0] B chunks full x BWV, [1] images full
+    // x NAW, [2] chunks consumed x WC
+    uint32_t *flg = reinterpret_cast<uint32_t *>(lds + oD + NDI * ((RMAX + 1) * (2u * KC + 32u)) + 768u);
+    auto flg_wait = [&](uint32_t idx, uint32_t target) {
+        if constexpr (FLG) {
+            while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(flg + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <
+                   target)
+                __builtin_amdgcn_s_sleep(1);
+            __asm__ volatile("" ::: "memory");
+        }
+    };
+    auto flg_arrive = [&](uint32_t idx) {
+        if constexpr (FLG) {
+            __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if ((threadIdx.x & 63u) == 0u) __hip_atomic_fetch_add(flg + idx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __asm__ volatile("" ::: "memory");
+        }
+    };
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t role = wv < WC ? 0u : (wv < WC + BWV ? 1u : 2u);  // wave-uniform
     const uint32_t bt = tid - 64 * WC;                // B thread index (role 1)
@@ -1129,6 +1154,9 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     GS_STAMP(0u);
 
     for (uint32_t u = tid; u < NDI * szD / 16u; u += NT) *reinterpret_cast<u32x4 *>(lds + oD + u * 16u) = zero4;
+    if constexpr (FLG) {
+        if (tid < 4u) flg[tid] = 0u;
+    }
 
     if (role == 0) {
         // ---------------------------------------------------------------- compute
@@ -1147,6 +1175,8 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         GS_STAMP(1u);
         __syncthreads();  // chunk 0 staged
         for (uint32_t j = 0; j < ncl; j++) {
+            flg_wait(0, BWV * j);  // chunk j's B rows landed (FLG)
+            flg_wait(1, NAW * j);  // ... and its dense image scattered
             const uint32_t kr = min(KC, K - (j0 + jr(j)) * KC);
             const uint32_t nsteps = (kr + 31u) / 32u;
             const unsigned char *la = lds + oD + (j % NDI) * szD;
@@ -1203,7 +1233,8 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
                     *reinterpret_cast<u32x4 *>(lds + oD + ((j + 2) % 3u) * szD + u * 16u) = zero4;
             }
             GS_STAMP(2u + 2u * j);
-            __syncthreads();
+            if constexpr (FLG) flg_arrive(2);  // reads and clears of chunk j done
+            else __syncthreads();
             GS_STAMP(3u + 2u * j);
         }
         // partial tiles -> LDS for the fixed-order reduction below
@@ -1244,6 +1275,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
         GS_STAMP(1u);
         __syncthreads();  // chunk 0 staged
         for (uint32_t j = 0; j < ncl; j++) {
+            flg_wait(2, WC * j);  // chunk j-1 consumed: its buffer takes chunk j+NBUF-1 (FLG)
             if (j + NBUF - 1 < ncl) {
                 if (!(DBG & 1)) issue(j + NBUF - 1);
                 // chunk j+1 retired, chunks j+2 .. j+NBUF-1 left in flight
@@ -1267,7 +1299,8 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
                 }
             }
             GS_STAMP(2u + 2u * j);
-            __builtin_amdgcn_s_barrier();
+            if constexpr (FLG) flg_arrive(0);  // chunk j+1 landed
+            else __builtin_amdgcn_s_barrier();
             GS_STAMP(3u + 2u * j);
         }
         __syncthreads();
@@ -1361,9 +1394,11 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
     {                                                                                             \
         if (!(DBG & 8)) GS_ALOAD((j) + 4, Pn, Vn);                                                \
         GS_STAMP(2u + 2u * (j)); /* entry role: loads issued, then scatter done */                \
+        flg_wait(2, WC * (uint32_t)(j)); /* FLG: chunk j-1 consumed, its image cleared */         \
         if ((j) + 1 < ncl && !(DBG & 2)) GS_SCATTER((j) + 1, Ps, Vs);                             \
         GS_STAMP(3u + 2u * (j));                                                                  \
-        __syncthreads();                                                                          \
+        if constexpr (FLG) flg_arrive(1);                                                         \
+        else __syncthreads();                                                                     \
     }
         GS_ALOAD(0u, p0, v0);
         GS_ALOAD(1u, p1, v1);

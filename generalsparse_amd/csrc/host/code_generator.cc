@@ -299,7 +299,7 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
         const std::string k = "gsk::k_mfma_rows<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ", " +
                               std::to_string(t.lgKC) + ", " + std::to_string(L.rows_maxa) + ", false, " +
                               std::to_string(L.rows_glds) + ", " + std::to_string(L.rows_nbg) + ", " +
-                              std::to_string(L.rows_wct) + ">";
+                              std::to_string(L.rows_wct) + (L.rows_flags ? ", 0, true>" : ">");
         setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
                 std::to_string(t.lds_bytes) + ")";
         launch = k + "<<<" + std::to_string(nb * L.rows_ksplit) + ", " + std::to_string(kMfmaThreads) + ", " +

@@ -537,6 +537,7 @@ mc_layout choose_matrix_core_layout(const meta_data_set &m, const kernel_spec &s
         L.rows_nbg = cfg.MFMA_GLDS_NBUF >= 5 ? 5 : (cfg.MFMA_GLDS_NBUF == 4 ? 4 : 3);
     const uint32_t nat = 64u * (gsk::kMfmaWaves - L.rows_wct - (L.rows_glds ? (uint32_t)L.rows_glds : (uint32_t)gsk::kMfmaBWaves));
     L.rows_maxa = L.rows.gmax > nat ? 2 : 1;
+    L.rows_flags = cfg.MFMA_FLAGS && L.rows_glds == 2 && L.rows_nbg == 3 && L.rows_wct == gsk::kMfmaCompute;
     // K-split: enough workgroups per row block to cover the CUs, at least one chunk each; auto:
     // split only when the row blocks cover under half the CUs (the slab combine costs
     // ~micro-seconds at the tail)

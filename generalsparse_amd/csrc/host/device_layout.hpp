@@ -95,6 +95,7 @@ struct mc_layout {
     mfma_tiles rows;
     uint32_t rows_ksplit = 1, rows_ncs = 0;  // k_mfma_rows K ranges per row block, chunks per range
     int rows_glds = 2, rows_nbg = 3, rows_wct = 6, rows_maxa = 1;  // k_mfma_rows template arguments
+    bool rows_flags = false;  // ... FLG (MFMA_FLAGS: LDS counter hand-offs, GLDS 2 / NBG 3 / 6 compute waves)
     ks_tiles ks;
     bm_tiles bm;
     std::vector<unsigned char> nm_blk;  // k_nm_mfma blocks

@@ -85,6 +85,7 @@ struct config_t {
     int64_t MFMA_MAX_FILL = 16;  // ... when (padded row-block area) / nnz <= this
     bool NM_MFMA = true;         // col-direction plans whose rows are 2:4 panels: sparse matrix cores (k_nm_mfma)
     int64_t MFMA_KSPLIT = 0;     // workgroups per row block (K ranges); 0 = fill the 256 CUs
+    bool MFMA_FLAGS = false;     // k_mfma_rows roles hand buffers over through LDS counters
     bool NM_KS = false;          // 2:4 panels: k_nm_mfma_ks (256-row workgroups, K split) instead of k_nm_mfma
                                  // (opt-in: C3 93 us against 66 us, profiles/r03_c3_nmks.json)
     int64_t NM_SPLIT = 0;        // ... its K ranges per row block (0: cover the CUs)

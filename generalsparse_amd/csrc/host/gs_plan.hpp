@@ -56,7 +56,8 @@ struct device_plan {
     uint32_t mp_solo = 16;  // k_merge_rows: slot-alone row length (MP_SOLO)
     // k_mfma_rows variant fixed at upload (device_layout.cc): GLDS / B ring depth / compute
     // waves / entry groups per thread -- the launch uses these, not the config of the moment
-    int mfma_glds = 2, mfma_nbg = 3, mfma_wct = 6, mfma_maxa = 1;  // k_mfma_ks: k-steps per K range, entry groups per step
+    int mfma_glds = 2, mfma_nbg = 3, mfma_wct = 6, mfma_maxa = 1;
+    bool mfma_flags = false;  // k_mfma_rows: LDS counter hand-offs instead of per-chunk barriers  // k_mfma_ks: k-steps per K range, entry groups per step
     std::string kernel;  // the device kernel gs_spmm launches at the plan's N (empty: the family's)
     uint32_t ksplit = 1, ncs = 0;  // k_mfma_rows workgroups per row block, chunks per workgroup
     uint32_t ws_n = 0;             // bitmap family: dense width of the fp32 workspace

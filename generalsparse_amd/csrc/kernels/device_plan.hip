@@ -374,6 +374,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
         d.KC = 1u << t.lgKC; d.nc = t.nc; d.maxr = t.RT; d.rpw_max = t.RMAX; d.RSB = t.lgKC;
         d.seg_cap = t.gmax;
         d.mfma_glds = mc.rows_glds; d.mfma_nbg = mc.rows_nbg; d.mfma_wct = mc.rows_wct; d.mfma_maxa = mc.rows_maxa;
+        d.mfma_flags = mc.rows_flags;
         const uint64_t nb = mc.tbr.size() - 1;
         d.ncs = mc.rows_ncs;
         d.ksplit = mc.rows_ksplit;

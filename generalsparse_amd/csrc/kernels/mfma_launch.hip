@@ -30,6 +30,8 @@ void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *
     auto kern = gl == 4 ? gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 4>
                         : (gl ? gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2> : gsk::k_mfma_rows<CT, RT, LGKC, MAXA>);
     if (gl == 2 && wct == 8) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 8>;
+    // LDS counter hand-offs between the roles instead of per-chunk barriers (MFMA_FLAGS)
+    if (gl == 2 && wct == 6 && nbg == 3 && d.mfma_flags) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 0, true>;
     if constexpr (LGKC == 8) {  // deeper B rings fit LDS with 256-column chunks
         if (gl == 2 && wct == 6 && nbg == 4) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 4>;
         if (gl == 2 && wct == 6 && nbg == 5) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 5>;

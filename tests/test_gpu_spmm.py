@@ -684,3 +684,26 @@ def test_warp_rows_grouped_passes(groups, N):
     assert plan.info()["device_kernel"].startswith("k_warp_rows"), plan.info()["device_kernel"]
     check(C, ofi.spmm_ref(M, N, row, col, val, B, "f64"), "f32")
     plan.free()
+
+
+@pytest.mark.parametrize("N", [16, 32, 64])
+@pytest.mark.parametrize("pipe", MFMA_PIPES, ids=lambda p: f"{p[0]}-{p[1]}")
+def test_mfma_rows_counter_handoffs(pipe, N, mfma_everywhere):
+    """k_mfma_rows with MFMA_FLAGS (the roles hand buffers over through LDS counters, no
+    per-chunk barrier): oracle parity, determinism, and the C2 shape against torch"""
+    name, p0, p1 = pipe
+    gsa.set_config("MFMA_GLDS", 1)
+    gsa.set_config("MFMA_FLAGS", 1)
+    try:
+        used = []
+        for case, M, K, row, col, val in mfma_cases():
+            plan, C, B = run(M, K, row, col, val, name, p0, p1, N, "f16")
+            used.append(plan.info()["device_kernel"])
+            ref = ofi.spmm_ref(M, N, row, col, val.astype(np.float16).astype(np.float32), B.astype(np.float32), "f64")
+            check(C, ref, "f16")
+            np.testing.assert_array_equal(plan.spmm(torch.from_numpy(B).to(DEV)).float().cpu().numpy(), C)
+            plan.free()
+        if N == 32 and p0 <= 32:
+            assert "k_mfma_rows" in used, used
+    finally:
+        gsa.set_config("MFMA_FLAGS", 0)
