@@ -15,14 +15,20 @@
 // Sub-matrices of row_nz_matrix_div_operator keep the divided sub-matrix's row indexing
 // and a row can straddle two of them: each runs into a zeroed scratch output, and
 // gs::combine_parts sums the scratch outputs into C's rows [base, base + rows).
+// one plan replica's scratch outputs: one per sub-matrix (rows_of(sub) x N), so replicas
+// (and gs_spmm_replica calls on different streams) never share a buffer
+struct replica_scratch {
+    std::vector<void *> bufs;
+    void **ptrs_dev = nullptr;
+    uint32_t N = 0;  // dense width the scratch outputs are sized for
+};
+
 struct parent_group {
     uint64_t base = 0, rows = 0;
     std::vector<gs::plan_state *> subs;
-    std::vector<void *> bufs;  // one scratch output per sub-matrix (rows_of(sub) x N)
     std::vector<uint32_t> part_rows;
-    void **ptrs_dev = nullptr;
+    std::vector<replica_scratch> rep;
     uint32_t *rows_dev = nullptr;
-    uint32_t N = 0;  // dense width the scratch outputs are sized for
     int device = 0;
 };
 
@@ -100,15 +106,22 @@ bool divided(gs_plan *p) { return !p->subs.empty() || !sub_live(*p->st.meta, 0);
 
 #define GS_HIP(x) GS_CHECK((x) == hipSuccess, #x " failed")
 
+void free_scratch(replica_scratch &r) {
+    for (void *b : r.bufs) (void)hipFree(b);
+    if (r.ptrs_dev) (void)hipFree(r.ptrs_dev);
+    r.bufs.clear();
+    r.ptrs_dev = nullptr;
+    r.N = 0;
+}
+
 void free_group(parent_group &g) {
-    if (!g.bufs.empty() || g.ptrs_dev) (void)hipSetDevice(g.device);
-    for (void *b : g.bufs) (void)hipFree(b);
-    if (g.ptrs_dev) (void)hipFree(g.ptrs_dev);
+    bool any = g.rows_dev != nullptr;
+    for (auto &r : g.rep) any |= r.ptrs_dev != nullptr || !r.bufs.empty();
+    if (any) (void)hipSetDevice(g.device);
+    for (auto &r : g.rep) free_scratch(r);
+    g.rep.clear();
     if (g.rows_dev) (void)hipFree(g.rows_dev);
-    g.bufs.clear();
-    g.ptrs_dev = nullptr;
     g.rows_dev = nullptr;
-    g.N = 0;
 }
 
 void free_groups(gs_plan *p) {
@@ -116,21 +129,27 @@ void free_groups(gs_plan *p) {
     p->groups.clear();
 }
 
-// scratch outputs for dense width N (allocated on first use, grown for a wider N)
-void ensure_scratch(parent_group &g, uint32_t N, size_t e) {
-    if (g.N >= N) return;
-    free_group(g);
+// replica `replica`'s scratch outputs for dense width N (allocated on first use, grown for a
+// wider N); the row counts are shared
+replica_scratch &ensure_scratch(parent_group &g, int replica, uint32_t N, size_t e) {
+    if ((size_t)replica >= g.rep.size()) g.rep.resize((size_t)replica + 1);
+    replica_scratch &r = g.rep[(size_t)replica];
+    if (r.N >= N && g.rows_dev) return r;
     GS_HIP(hipSetDevice(g.device));
+    free_scratch(r);
     for (size_t i = 0; i < g.subs.size(); i++) {
         void *b = nullptr;
         GS_HIP(hipMalloc(&b, std::max<size_t>(1, (size_t)g.part_rows[i] * N * e)));
-        g.bufs.push_back(b);
+        r.bufs.push_back(b);
     }
-    GS_HIP(hipMalloc((void **)&g.ptrs_dev, g.bufs.size() * sizeof(void *)));
-    GS_HIP(hipMemcpy(g.ptrs_dev, g.bufs.data(), g.bufs.size() * sizeof(void *), hipMemcpyHostToDevice));
-    GS_HIP(hipMalloc((void **)&g.rows_dev, g.part_rows.size() * sizeof(uint32_t)));
-    GS_HIP(hipMemcpy(g.rows_dev, g.part_rows.data(), g.part_rows.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    g.N = N;
+    GS_HIP(hipMalloc((void **)&r.ptrs_dev, r.bufs.size() * sizeof(void *)));
+    GS_HIP(hipMemcpy(r.ptrs_dev, r.bufs.data(), r.bufs.size() * sizeof(void *), hipMemcpyHostToDevice));
+    if (!g.rows_dev) {
+        GS_HIP(hipMalloc((void **)&g.rows_dev, g.part_rows.size() * sizeof(uint32_t)));
+        GS_HIP(hipMemcpy(g.rows_dev, g.part_rows.data(), g.part_rows.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
+    r.N = N;
+    return r;
 }
 
 // multi-kernel executor: zero the output rows of empty row intervals, then run each
@@ -150,12 +169,12 @@ void spmm_all(gs_plan *p, int replica, const void *B, void *C, uint32_t N, hipSt
     for (gs::plan_state *s : ks)
         if (s->parent_row_base < 0) gs::launch_spmm(*s, replica, B, C, N, stream);
     for (auto &g : p->groups) {
-        ensure_scratch(g, N, e);
+        replica_scratch &r = ensure_scratch(g, replica, N, e);
         for (size_t i = 0; i < g.subs.size(); i++) {
-            gs::memset_rows(g.bufs[i], 0, g.part_rows[i], N, e, stream);
-            gs::launch_spmm(*g.subs[i], replica, B, g.bufs[i], N, stream);
+            gs::memset_rows(r.bufs[i], 0, g.part_rows[i], N, e, stream);
+            gs::launch_spmm(*g.subs[i], replica, B, r.bufs[i], N, stream);
         }
-        gs::combine_parts(g.ptrs_dev, g.rows_dev, (uint32_t)g.subs.size(), C, g.base, g.rows, N, dtype, stream);
+        gs::combine_parts(r.ptrs_dev, g.rows_dev, (uint32_t)g.subs.size(), C, g.base, g.rows, N, dtype, stream);
     }
 }
 

@@ -121,3 +121,30 @@ def test_row_nz_plan_file_computes_the_same(tmp_path):
     C2, _ = spmm(q, M, K, N, "f16")
     assert np.array_equal(C1, C2)
     check(C1, ofi.spmm_ref(M, N, r, c, v, B, "f64"), "f16")
+
+
+def test_row_nz_replicas_on_two_streams():
+    """every plan replica has its own scratch outputs: two replicas launched on
+    two streams at once give the single-replica result"""
+    M, K, r, c, v = banded(1)
+    N = 32
+    p = gsa.Plan.from_coo(M, K, r, c, v)
+    p.add_operator("row_nz_matrix_div_operator", 4, 64, 2)
+    for i, s in enumerate(p.sub_matrices()):
+        name, p0, p1 = RUNNABLE[i % len(RUNNABLE)]
+        p.run_pipeline(name, N, p0, p1, sub=s)
+    p.compile().upload("f32", 0)
+    p.add_replica()
+    C0, B = spmm(p, M, K, N, "f32")
+    Bt = torch.from_numpy(B).to(DEV)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    Ca = torch.empty((M, N), device=DEV)
+    Cb = torch.empty((M, N), device=DEV)
+    torch.cuda.synchronize()
+    for _ in range(20):
+        with torch.cuda.stream(s1):
+            p.spmm(Bt, C=Ca, replica=0)
+        with torch.cuda.stream(s2):
+            p.spmm(Bt, C=Cb, replica=1)
+    torch.cuda.synchronize()
+    assert np.array_equal(Ca.cpu().numpy(), C0) and np.array_equal(Cb.cpu().numpy(), C0)
