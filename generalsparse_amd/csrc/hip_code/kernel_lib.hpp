@@ -402,15 +402,19 @@ __global__ __launch_bounds__(256) void k_warp_rows(const uint32_t *__restrict__ 
 // row of the BMTB over blockDim.y with __syncthreads,
 // total_block_reduce_to_one_register_token.cc:374-480).  Here the BMTB's rows
 // are taken in windows of kBrWindow: the 4S slots (X column lanes each) walk the
-// window's rows slot-per-row and store the short ones (<= kBrSolo nonzeros)
-// directly; longer rows are listed in LDS and then reduced by the whole
-// workgroup (all 4S slots split the row, registers, then one LDS round of four
-// wave partials).  Short-row BMTBs (balanced_block_total on power-law graphs:
-// hundreds of 1-10 nnz rows) cost three barriers per window instead of two per
-// row; long-row BMTBs keep the cooperative path.
+// window's rows slot-per-row and store the short ones (<= kBrSlot nonzeros)
+// directly; medium rows (<= solo) are listed and each taken by one wave (its S
+// slots split the row, one xor-shuffle reduction, no barrier); longer rows are
+// listed in LDS and then reduced by the whole workgroup (all 4S slots split the
+// row, registers, then one LDS round of four wave partials).  Short-row BMTBs
+// (balanced_block_total on power-law graphs: hundreds of 1-10 nnz rows) cost three
+// barriers per window instead of two per row; a medium row no longer serialises
+// its slot's wave (one dependent gather round per 4 nonzeros); long-row BMTBs keep
+// the cooperative path.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kBrWindow = 1024;  // rows per window (the long-row list's capacity)
-constexpr uint32_t kBrSolo = 64;      // a row of at most this many nonzeros is one slot's
+constexpr uint32_t kBrWindow = 1024;  // rows per window (the long/medium row lists' capacity)
+constexpr uint32_t kBrSlot = 8;       // a row of at most this many nonzeros is one slot's
+constexpr uint32_t kBrSolo = 512;     // ... at most this many one wave's (more: the workgroup's)
 
 template <class VT, class CT, int CF, int SCF, bool FX>
 __device__ __forceinline__ void block_rows_body(const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
@@ -421,6 +425,7 @@ __device__ __forceinline__ void block_rows_body(const uint32_t *__restrict__ bmt
                                                     uint32_t N, uint32_t X, uint32_t row_base,
                                                     float (*part)[64][CF],  // [4][64][CF] in LDS
                                                     uint32_t *long_rows,    // [kBrWindow + 1] in LDS
+                                                    uint32_t *med_rows,     // [kBrWindow + 1] in LDS
                                                     uint32_t solo) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wib = threadIdx.x >> 6;
@@ -428,6 +433,8 @@ __device__ __forceinline__ void block_rows_body(const uint32_t *__restrict__ bmt
     const uint32_t S = 64u / X;
     const uint32_t slot = wib * S + lane / X;  // 0 .. 4S-1
     uint32_t *n_long = long_rows + kBrWindow;
+    uint32_t *n_med = med_rows + kBrWindow;
+    const uint32_t one = min(solo, kBrSlot);  // slot-per-row bound
     for (uint32_t ct = blockIdx.y; ct * X * CF < N; ct += gridDim.y) {
         const uint32_t cw = ct * X * CF + xl * CF;
         const bool cok = cw < N;
@@ -437,22 +444,48 @@ __device__ __forceinline__ void block_rows_body(const uint32_t *__restrict__ bmt
             idx_range<FX>(bmtb_first_row, f_row, t, r_begin, r_end);
             for (uint32_t w0 = r_begin; w0 < r_end; w0 += kBrWindow) {
                 const uint32_t w1 = min(r_end, w0 + kBrWindow);
-                if (threadIdx.x == 0) *n_long = 0u;
+                if (threadIdx.x == 0) {
+                    *n_long = 0u;
+                    *n_med = 0u;
+                }
                 __syncthreads();
-                // slot-per-row over the window; long rows are listed
+                // slot-per-row over the window; medium and long rows are listed.  The next
+                // row's bounds are loaded before this row's entries (one dependent round trip
+                // less per row: a slot walks hundreds of short rows in a 17,864-row BMTB)
+                uint32_t rbn = 0, ren = 0;
+                if (w0 + slot < w1) {
+                    rbn = row_ptr[w0 + slot];
+                    ren = row_ptr[w0 + slot + 1];
+                }
                 for (uint32_t r = w0 + slot; r < w1; r += 4u * S) {
-                    const uint32_t rb = row_ptr[r], re = row_ptr[r + 1];
-                    if (re - rb <= solo) {
+                    const uint32_t rb = rbn, re = ren;
+                    if (r + 4u * S < w1) {
+                        rbn = row_ptr[r + 4u * S];
+                        ren = row_ptr[r + 4u * S + 1];
+                    }
+                    if (re - rb <= one) {
                         float acc[CF];
 #pragma unroll
                         for (int k = 0; k < CF; k++) acc[k] = 0.f;
                         wave_row<VT, CT, CF, SCF>(rb, re, col, val, B, N, c0, 0u, 1u, acc);
                         if (cok) store_f32<VT, CF>(C + (size_t)(r + row_base) * N + c0, acc);
                     } else if (xl == 0u) {
-                        long_rows[atomicAdd(n_long, 1u)] = r;
+                        if (re - rb <= solo) med_rows[atomicAdd(n_med, 1u)] = r;
+                        else long_rows[atomicAdd(n_long, 1u)] = r;
                     }
                 }
                 __syncthreads();
+                // medium rows: one wave each (its S slots split the row)
+                const uint32_t nm = *n_med;
+                for (uint32_t i = wib; i < nm; i += 4u) {
+                    const uint32_t r = med_rows[i];
+                    float acc[CF];
+#pragma unroll
+                    for (int k = 0; k < CF; k++) acc[k] = 0.f;
+                    wave_row<VT, CT, CF, SCF>(row_ptr[r], row_ptr[r + 1], col, val, B, N, c0, lane / X, S, acc);
+                    wave_reduce_slots<CF>(acc, (int)X);
+                    if (lane < X && cok) store_f32<VT, CF>(C + (size_t)(r + row_base) * N + c0, acc);
+                }
                 const uint32_t nl = *n_long;
                 for (uint32_t i = 0; i < nl; i++) {  // the window's long rows, the whole workgroup each
                     const uint32_t r = long_rows[i];
@@ -487,12 +520,13 @@ __global__ __launch_bounds__(256) void k_block_rows(const uint32_t *__restrict__
                                                     uint32_t solo = kBrSolo) {
     __shared__ float part[4][64][CF];
     __shared__ uint32_t long_rows[kBrWindow + 1];
+    __shared__ uint32_t med_rows[kBrWindow + 1];
     if (f_row.kind == IDX_ARRAY)
         block_rows_body<VT, CT, CF, SCF, false>(bmtb_first_row, f_row, row_ptr, col, val, B, C, n_bmtb, N, X, row_base, part,
-                                                long_rows, solo);
+                                                long_rows, med_rows, solo);
     else
         block_rows_body<VT, CT, CF, SCF, true>(bmtb_first_row, f_row, row_ptr, col, val, B, C, n_bmtb, N, X, row_base, part,
-                                               long_rows, solo);
+                                               long_rows, med_rows, solo);
 }
 
 // ---------------------------------------------------------------------------
