@@ -256,11 +256,11 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
           << "    hipMalloc(&d_arr, " << nb * ks_col_tiles(N) * 4 << "ull + 4); hipMemset(d_arr, 0, " << nb * ks_col_tiles(N) * 4
           << "ull + 4);\n";
         const std::string k = "gsk::k_mfma_ks<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ", " +
-                              std::to_string(kKsWaves) + ", " + std::to_string(kKsDepth) + ", " + std::to_string(t.MAXG) + ">";
+                              std::to_string(t.W) + ", " + std::to_string(kKsDepth) + ", " + std::to_string(t.MAXG) + ">";
         setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
                 std::to_string(t.lds_bytes) + ")";
         launch = k + "<<<dim3(" + std::to_string(nwg) + ", " + std::to_string(ks_col_tiles(N)) + "), " +
-                 std::to_string(64 * kKsWaves) + ", " + std::to_string(t.lds_bytes) +
+                 std::to_string(64 * t.W) + ", " + std::to_string(t.lds_bytes) +
                  ">>>(d_tbr, (const gsk::u32x4 *)d_pos, (const gsk::u32x4 *)d_val, d_B, d_C, (uint32_t)K, N, " +
                  std::to_string(t.S) + "u, " + std::to_string(t.NS) + "u, " + std::to_string(t.GCAP) + "u, " +
                  std::to_string(nwg) + "u, 0u, d_ws, d_arr, nullptr)";

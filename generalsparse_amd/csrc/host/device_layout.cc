@@ -236,11 +236,14 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     const uint64_t nb = tb_rows.size() - 1;
     if (nb == 0 || K == 0) { why = "empty plan"; return false; }
     if (N == 0 || N % 8 != 0) { why = "N must be a multiple of 8"; return false; }
-    const uint32_t CT = ks_ct(N), W = kKsWaves;
+    const uint32_t CT = ks_ct(N);
+    // KS_WAVES = 16: twice the waves (more loads in flight per CU) when their stages fit LDS
+    uint32_t W = kKsWaves;
     uint64_t rmax = 0;
     for (uint64_t g = 0; g < nb; g++) rmax = std::max<uint64_t>(rmax, tb_rows[g + 1] - tb_rows[g]);
     if (rmax < (uint64_t)std::max<int64_t>(1, min_rows) || rmax > 80) { why = "row blocks outside the k_mfma_ks range"; return false; }
     const uint32_t RT = std::max<uint32_t>(2, (uint32_t)((rmax + 15) / 16));  // kernels built for RT 2..5
+    if (get_config().KS_WAVES == 16 && gsk::ks_lds_bytes(CT, RT, 16) <= 160 * 1024) W = 16;
     const uint64_t nnz = row_ptr[tb_rows[nb]] - row_ptr[tb_rows[0]];
     if (nnz == 0 || (double)nb * 16 * RT * K > (double)max_fill * nnz) {  // as build_mfma_tiles
         why = "row blocks too sparse for dense tiles";

@@ -98,6 +98,7 @@ struct config_t {
     int64_t KS_MIN_ROWS = 40;    // ... from this many rows per BMTB (shorter blocks: k_mfma_rows)
     bool MP_ROWS = false;        // merge-path plans: k_merge_rows (product/row walk) instead of k_merge_path
     int64_t MP_SOLO = 16;        // k_merge_rows: rows of at most this many nonzeros are one slot's
+    int64_t KS_WAVES = 8;        // k_mfma_ks waves per workgroup (8 or 16)
     int64_t KS_SPLIT = 0;        // k_mfma_ks K ranges per row block (0: the fewest that fit LDS and fill the CUs)
 };
 // Process-wide config: loaded once from $GS_CONFIG or ./global_config.json if

@@ -31,15 +31,21 @@ void grant_lds(int device, KERN kern, size_t bytes) {
     }
 }
 
-template <int CT, int RT, int MAXG, bool STAMPS = false>
+template <int CT, int RT, int MAXG, bool STAMPS = false, int W = (int)kKsWaves>
 void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s,
                  uint64_t *stamps = nullptr) {
     const device_plan &d = p.dev;
-    auto kern = gsk::k_mfma_ks<CT, RT, (int)kKsWaves, (int)kKsDepth, MAXG, STAMPS>;
+    if constexpr (W == (int)kKsWaves && !STAMPS) {
+        if (d.waves == 16) {  // KS_WAVES = 16, fixed at upload
+            launch_ks_k<CT, RT, MAXG, false, 16>(p, a, B, C, N, s, stamps);
+            return;
+        }
+    }
+    auto kern = gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, STAMPS>;
     // the LDS this instantiation needs at the plan's range width, against what the upload sized
-    GS_CHECK(gsk::ks_lds_bytes(CT, RT, kKsWaves) <= d.lds_bytes, "k_mfma_ks: LDS size disagrees with the upload");
+    GS_CHECK(gsk::ks_lds_bytes(CT, RT, W) <= d.lds_bytes, "k_mfma_ks: LDS size disagrees with the upload");
     grant_lds(d.device, kern, d.lds_bytes);
-    hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit, ks_col_tiles(N)), dim3(64 * kKsWaves), d.lds_bytes, s, a.t0,
+    hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit, ks_col_tiles(N)), dim3(64 * W), d.lds_bytes, s, a.t0,
                        (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, B, C, (uint32_t)p.K, N, d.ksplit,
                        d.ks_ns, d.ks_gcap, (uint32_t)d.n_rows_aux * d.ksplit, (uint32_t)d.row_base, a.ws, a.t2, stamps);
     HIP_OK(hipGetLastError());
@@ -155,7 +161,7 @@ void debug_bm_timeline(const plan_state &p, const void *B, void *C, uint32_t N, 
 void debug_ks_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
                        size_t n_host) {
     const device_plan &d = p.dev;
-    GS_CHECK(N == 32 && d.maxr == 5 && d.seg_cap == 2, "k_mfma_ks timeline build: N=32, RT=5, MAXG=2 only");
+    GS_CHECK(N == 32 && d.maxr == 5 && d.seg_cap == 2 && d.waves == kKsWaves, "k_mfma_ks timeline build: N=32, RT=5, MAXG=2, 8 waves only");
     const size_t n = (size_t)d.n_rows_aux * d.ksplit * ks_col_tiles(N) * kKsWaves * 32;
     uint64_t *dst = nullptr;
     HIP_OK(hipMalloc(&dst, n * 8));

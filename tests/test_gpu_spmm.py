@@ -707,3 +707,27 @@ def test_mfma_rows_counter_handoffs(pipe, N, mfma_everywhere):
             assert "k_mfma_rows" in used, used
     finally:
         gsa.set_config("MFMA_FLAGS", 0)
+
+
+@pytest.mark.parametrize("N", [8, 32, 128])
+@pytest.mark.parametrize("pipe", KS_PIPES, ids=lambda p: f"{p[0]}-{p[1]}")
+def test_mfma_ks_16_waves(pipe, N, mfma_everywhere):
+    """k_mfma_ks with KS_WAVES=16 (twice the waves per workgroup where their stages fit LDS):
+    oracle parity, determinism of the K-range combine"""
+    name, p0, p1 = pipe
+    gsa.set_config("KS_WAVES", 16)
+    try:
+        waves = []
+        for case, M, K, row, col, val in mfma_cases():
+            plan, C, B = run(M, K, row, col, val, name, p0, p1, N, "f16")
+            info = plan.info()
+            if info["device_kernel"] == "k_mfma_ks":
+                waves.append(info["lds_waves"])
+            ref = ofi.spmm_ref(M, N, row, col, val.astype(np.float16).astype(np.float32), B.astype(np.float32), "f64")
+            check(C, ref, "f16")
+            np.testing.assert_array_equal(plan.spmm(torch.from_numpy(B).to(DEV)).float().cpu().numpy(), C)
+            plan.free()
+        if N <= 32:  # (at N = 128 a 64-row block's 16 wave stages exceed LDS: 8 waves)
+            assert 16 in waves, waves
+    finally:
+        gsa.set_config("KS_WAVES", 8)
