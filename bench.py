@@ -460,6 +460,21 @@ def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
     nnz_l = sum(bt.nnz_of_shape(k, sp) for k in bt.C5_SLOTS)
     flops_l = 2.0 * nnz_l * N
     alg_l = sum(algorithmic_bytes(*bt.C5_SHAPES[k], N, bt.nnz_of_shape(k, sp), e, 2) for k in bt.C5_SLOTS)
+    # L2->fabric bytes per launch of each (shape, plan) from the PMC passes of
+    # scripts/gpu_traffic_c5h.sh, summed over the six slots with the plans the search chose
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "traffic_c5h.json")
+    if os.path.exists(tf):
+        try:
+            tj = json.load(open(tf))
+            if tj["N"] == N and abs(tj["sparsity"] - sp) < 1e-9:
+                pl = tj["per_launch"]
+                for k in per_shape:
+                    per_shape[k]["traffic"] = pl.get(k, {}).get(per_shape[k]["plan"], {}).get("hbm_bytes")
+                if all(per_shape[k]["traffic"] for k in bt.C5_SLOTS):
+                    traffic = sum(per_shape[k]["traffic"] for k in bt.C5_SLOTS)
+        except Exception:
+            traffic = None
     rs_l = None
     if all(per_shape[k]["rocsparse_f16"] for k in bt.C5_SHAPES):
         rs_l = sum(per_shape[k]["rocsparse_f16"]["ms"] for k in bt.C5_SLOTS)
@@ -475,7 +490,7 @@ def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
                    "plan": {k: per_shape[k]["plan"] for k in per_shape}, "kernel": {k: per_shape[k]["kernel"] for k in per_shape},
                    "parallelism": "one GPU", "streams": args.streams},
         "roofline": {"bound": "hbm", "achieved": round(alg_l / (ms_step * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(alg_l / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                     "unit": "GB/s", "frac": round(alg_l / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "algorithmic_bytes_per_step": alg_l, "note": "whole layer step (six launches, host-timed)"},
         "per_shape": per_shape,
         "speedup_vs_rocsparse": round(rs_l / ms_step, 3) if rs_l else None,
