@@ -31,6 +31,7 @@ namespace gsk {
 
 typedef _Float16 f16;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 template <int BYTES> struct raw_vec;
 template <> struct raw_vec<2> { typedef uint16_t t; };
@@ -1530,9 +1531,10 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
 // reads only that slice of B (KR rows).
 // Wave w owns the range's 32-column k-steps w, w+W, ... and runs them with no
 // workgroup barrier until the end: per k-step it loads (D steps ahead, into registers)
-// the step's 32 B rows and its entries (upload layout: GCAP groups per step, each 8 x
-// [u16 halfword position in the wave's dense image] + 8 x [f16 value]; padding writes 0
-// into the image's zero row), stores the B rows into its private stage (32-B pieces
+// the step's 32 B rows and its entries (upload layout: the step's groups back to back,
+// each 8 x [u16 halfword position in the wave's dense image] + 8 x [f16 value], found by
+// the step's {first group, group count} record, loaded D steps ahead of the groups;
+// padding inside a group writes 0 into the image's zero row), stores the B rows into its private stage (32-B pieces
 // permuted by b_piece so the ds_read_b64_tr_b16 fragment reads are conflict-free),
 // scatters the entries into its private image of 16*RT+1 rows x 96 B (conflict-free
 // ds_read_b128), reads the RT A fragments and the CT B fragments, writes zeros back at
@@ -1567,8 +1569,9 @@ template <int CT, int RT, int W, int D, int MAXG, bool STAMPS = false>
 __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__ bmtb_first_row,  // nb+1
                                                     const u32x4 *__restrict__ tP,  // 8 x u16 position per group
                                                     const u32x4 *__restrict__ tV,  // 8 x f16 value per group
+                                                    const u32x2 *__restrict__ steps,  // per (unit, k-step): first group, count
                                                     const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K,
-                                                    uint32_t N, uint32_t S, uint32_t NS, uint32_t GCAP, uint32_t nwg,
+                                                    uint32_t N, uint32_t S, uint32_t NS, uint32_t nwg,
                                                     uint32_t row_base, float *__restrict__ slabs,
                                                     uint32_t *__restrict__ arrivals, uint64_t *__restrict__ stamps = nullptr) {
     constexpr uint32_t RB = 32 * CT;  // bytes per LDS B row (a 16*CT-column tile)
@@ -1593,16 +1596,27 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
     unsigned char *bst = img + IMG;
     const u32x4 zero4 = {0u, 0u, 0u, 0u};
 
-    // ---- this wave's k-steps w, w+W, ...: step s of unit u is GCAP groups at (u*NS + s)*GCAP
-    // (every step padded to the plan's largest, so no address waits on a load)
+    // ---- this wave's k-steps w, w+W, ...: step s of unit u is record steps[u*NS + s] =
+    // {first group, group count}; a slot's next record is loaded one round (D steps) before
+    // its groups, so the groups' addresses wait on a load issued a round earlier
     const uint32_t nsw = NS > wv ? (NS - wv + W - 1u) / W : 0u;
-    const size_t ubase = (size_t)u * NS * GCAP;
+    const size_t ubase = (size_t)u * NS;
     u32x4 P[D][MAXG], V[D][MAXG], BR[D][CT];
+    u32x2 NX[D];      // per slot: record of the step the slot loads next
+    uint32_t CN[D];   // per slot: group count of the step whose groups it holds
+    auto rec_of = [&](uint32_t i) -> u32x2 {
+        const uint32_t st = __builtin_amdgcn_readfirstlane(i < nsw ? wv + i * W : 0u);
+        return steps[ubase + st];
+    };
     // steps past the wave's last re-read the unit's first step (cached; the same lane-varying
     // load form as a live step, so no path of the loop issues a different count)
-    auto load_set = [&](uint32_t i, u32x4 (&P_)[MAXG], u32x4 (&V_)[MAXG], u32x4 (&B_)[CT]) {
+    auto load_set = [&](uint32_t i, u32x2 &NX_, uint32_t &CN_, u32x4 (&P_)[MAXG], u32x4 (&V_)[MAXG],
+                        u32x4 (&B_)[CT]) {
         const uint32_t st = __builtin_amdgcn_readfirstlane(i < nsw ? wv + i * W : 0u);
-        const size_t b0 = ubase + (size_t)st * GCAP;
+        const uint32_t b0 = __builtin_amdgcn_readfirstlane(NX_[0]);
+        const uint32_t gc = __builtin_amdgcn_readfirstlane(NX_[1]);
+        CN_ = gc;
+        NX_ = rec_of(i + D);
         const uint32_t kr = k0 + st * 32u;  // first B row of the step
 #pragma unroll
         for (int c = 0; c < CT; c++) {
@@ -1615,13 +1629,15 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
 #pragma unroll
         for (int j = 0; j < MAXG; j++) {
             const uint32_t qg = lane + 64u * j;
-            const size_t at = b0 + (qg < GCAP ? qg : 0u);
+            const size_t at = (size_t)b0 + (qg < gc ? qg : 0u);
             P_[j] = tP[at];
             V_[j] = tV[at];
         }
     };
 #pragma unroll
-    for (int d = 0; d < D; d++) load_set((uint32_t)d, P[d], V[d], BR[d]);
+    for (int d = 0; d < D; d++) NX[d] = rec_of((uint32_t)d);
+#pragma unroll
+    for (int d = 0; d < D; d++) load_set((uint32_t)d, NX[d], CN[d], P[d], V[d], BR[d]);
     for (uint32_t x = lane; x < IMG / 16u; x += 64u) *reinterpret_cast<u32x4 *>(img + x * 16u) = zero4;
     GS_KS_STAMP(1u);
 
@@ -1636,8 +1652,9 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
 
     // step i on its set, then the set is reloaded with step i + D (issued whether or not
     // step i exists: every loop iteration issues the same loads)
-    auto step = [&](uint32_t i, u32x4 (&P_)[MAXG], u32x4 (&V_)[MAXG], u32x4 (&B_)[CT]) {
+    auto step = [&](uint32_t i, u32x2 &NX_, uint32_t &CN_, u32x4 (&P_)[MAXG], u32x4 (&V_)[MAXG], u32x4 (&B_)[CT]) {
         const bool live = i < nsw;  // wave-uniform
+        const uint32_t gc = CN_;
         h8v av[RT], bv[CT];
         if (live) {
             const uint32_t kr = k0 + (wv + i * W) * 32u;
@@ -1651,7 +1668,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
             // scatter the step's entries into the image
 #pragma unroll
             for (int j = 0; j < MAXG; j++) {
-                if (lane + 64u * j < GCAP) {
+                if (lane + 64u * j < gc) {
 #pragma unroll
                     for (int e = 0; e < 8; e++) {
                         const uint32_t h = (P_[j][e >> 1] >> (16 * (e & 1))) & 0xffffu;
@@ -1678,7 +1695,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
             // the image back to zero at the entries' positions
 #pragma unroll
             for (int j = 0; j < MAXG; j++) {
-                if (lane + 64u * j < GCAP) {
+                if (lane + 64u * j < gc) {
 #pragma unroll
                     for (int e = 0; e < 8; e++) {
                         const uint32_t h = (P_[j][e >> 1] >> (16 * (e & 1))) & 0xffffu;
@@ -1687,7 +1704,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
                 }
             }
         }
-        load_set(i + D, P_, V_, B_);
+        load_set(i + D, NX_, CN_, P_, V_, B_);
         if (live) {
 #pragma unroll
             for (int rt = 0; rt < RT; rt++)
@@ -1699,7 +1716,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
     };
     for (uint32_t i0 = 0; i0 < nsw; i0 += D) {
 #pragma unroll
-        for (int d = 0; d < D; d++) step(i0 + d, P[d], V[d], BR[d]);
+        for (int d = 0; d < D; d++) step(i0 + d, NX[d], CN[d], P[d], V[d], BR[d]);
     }
     GS_KS_STAMP(20u);
     // ---- wave partial tiles -> LDS (the trailing loads write registers only), summed in

@@ -252,6 +252,7 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
           << "    std::vector<uint32_t> t32(tbr.begin(), tbr.end()); uint32_t *d_tbr = up(t32);\n"
           << "    uint16_t *d_pos = up(rdb<uint16_t>(\"TBLOCK_META_mfma_ks_entry_pos_0.bin\"));\n"
           << "    uint16_t *d_val = up(rdb<uint16_t>(\"TBLOCK_META_mfma_ks_entry_val_0.bin\"));\n"
+          << "    uint32_t *d_steps = up(rdb<uint32_t>(\"TBLOCK_META_mfma_ks_steps_0.bin\"));\n"
           << "    float *d_ws; uint32_t *d_arr; hipMalloc(&d_ws, " << nwg * ks_col_tiles(N) * 256 * t.RT * CT * 4 << "ull + 16);\n"
           << "    hipMalloc(&d_arr, " << nb * ks_col_tiles(N) * 4 << "ull + 4); hipMemset(d_arr, 0, " << nb * ks_col_tiles(N) * 4
           << "ull + 4);\n";
@@ -261,9 +262,8 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
                 std::to_string(t.lds_bytes) + ")";
         launch = k + "<<<dim3(" + std::to_string(nwg) + ", " + std::to_string(ks_col_tiles(N)) + "), " +
                  std::to_string(64 * t.W) + ", " + std::to_string(t.lds_bytes) +
-                 ">>>(d_tbr, (const gsk::u32x4 *)d_pos, (const gsk::u32x4 *)d_val, d_B, d_C, (uint32_t)K, N, " +
-                 std::to_string(t.S) + "u, " + std::to_string(t.NS) + "u, " + std::to_string(t.GCAP) + "u, " +
-                 std::to_string(nwg) + "u, 0u, d_ws, d_arr, nullptr)";
+                 ">>>(d_tbr, (const gsk::u32x4 *)d_pos, (const gsk::u32x4 *)d_val, (const gsk::u32x2 *)d_steps, d_B, d_C, "
+                 "(uint32_t)K, N, " + std::to_string(t.S) + "u, " + std::to_string(t.NS) + "u, " + std::to_string(nwg) + "u, 0u, d_ws, d_arr, nullptr)";
     } else if (L.kind == mc_layout::BM) {
         const bm_tiles &t = L.bm;
         const uint64_t nb = L.tbr.size() - 1, nwg = nb * t.S;
@@ -580,6 +580,7 @@ uint64_t code_generator::generate_final_program(int repeat, const std::string &r
     if (L.kind == mc_layout::KS) {
         write_bin(dir + "/TBLOCK_META_mfma_ks_entry_pos_0.bin", L.ks.pos);
         write_bin(dir + "/TBLOCK_META_mfma_ks_entry_val_0.bin", L.ks.val);
+        write_bin(dir + "/TBLOCK_META_mfma_ks_steps_0.bin", L.ks.steps);
     } else if (L.kind == mc_layout::BM) {
         write_bin(dir + "/TBLOCK_META_mfma_bm_records_0.bin", L.bm.rec);
         write_bin(dir + "/TBLOCK_META_mfma_bm_step_base_0.bin", L.bm.sbase);

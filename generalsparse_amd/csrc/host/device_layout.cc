@@ -222,11 +222,14 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
 // Upload layout of k_mfma_ks (kernel_lib.hpp): the K range is split into S ranges of
 // KR = 32*NS columns; for every (BMTB g, range q, 32-column k-step s) -- unit u = g*S + q --
 // the entries of g's rows in the step's columns, in groups of 8: pos = halfword index in a
-// wave image of 96-B rows (local_row*48 + column - step base), val = f16.  Every step holds
-// exactly GCAP groups (the plan's largest step; the rest padding that writes 0 into the
-// image's zero row 16*RT), at group (u*NS + s)*GCAP, so the kernel computes every address
-// without loading offsets first.  One spare group follows.  The entry order inside a step
-// is bank-ordered for the scatter.
+// wave image of 96-B rows (local_row*48 + column - step base), val = f16.  The steps'
+// groups lie back to back in (u, s) order; steps[2*(u*NS + s)] = the step's first group,
+// steps[2*(u*NS + s) + 1] = its group count (at most GCAP, the plan's largest: it sets
+// MAXG).  A group's unused entries write 0 into the image's zero row 16*RT.  One spare
+// group follows (an empty last step's loads).  The entry order inside a step is
+// bank-ordered for the scatter.  (Round 3 padded every step to GCAP groups so that no
+// address waited on a load: 1.19-1.35x the algorithmic bytes on the headline layer,
+// profiles/traffic_c5h.json.)
 
 
 
@@ -275,10 +278,12 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     t.MAXG = gmax <= 64 ? 1 : (gmax <= 128 ? 2 : (gmax <= 256 ? 4 : 0));
     if (!t.MAXG) { why = "a k-step holds more than 256 entry groups"; return false; }
     GS_CHECK((double)nb * S * t.NS * t.GCAP < 4.0e9, "k_mfma_ks layout exceeds 32-bit group indices");
+    GS_CHECK((double)nb * S * t.NS < 4.0e9, "k_mfma_ks layout exceeds 32-bit step indices");
     const uint32_t RS = gsk::kKsStride / 2;  // halfwords per image row
     const uint32_t pad_h = 16 * RT * RS;      // the zero row
-    t.pos.reserve((size_t)nb * S * t.NS * t.GCAP * 8 + 8);
+    t.pos.reserve(row_ptr[tb_rows[nb]] - row_ptr[tb_rows[0]] + (size_t)nb * S * t.NS * 8 + 8);
     t.val.reserve(t.pos.capacity());
+    t.steps.reserve((size_t)nb * S * t.NS * 2);
     std::vector<uint64_t> cur;
     std::vector<uint16_t> pos, hv;
     for (uint64_t g = 0; g < nb; g++) {
@@ -300,11 +305,10 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
                 }
                 const size_t before = t.pos.size();
                 bank_order_segment(pos, hv, pad_h, t.pos, t.val, RS / 2);  // pads stay inside the zero row
-                for (size_t x = t.pos.size(); x < before + (size_t)t.GCAP * 8; x++) {  // up to GCAP groups
-                    t.pos.push_back((uint16_t)(pad_h + 2 * ((x / 8) % (RS / 2))));
-                    t.val.push_back(0);
-                }
-                GS_CHECK(t.pos.size() == before + (size_t)t.GCAP * 8, "k_mfma_ks step exceeds its capacity");
+                const size_t ng = (t.pos.size() - before) / 8;
+                GS_CHECK(ng <= t.GCAP, "k_mfma_ks step exceeds its capacity");
+                t.steps.push_back((uint32_t)(before / 8));
+                t.steps.push_back((uint32_t)ng);
             }
     }
     t.pos.insert(t.pos.end(), 8, (uint16_t)pad_h);  // spare group: loads past a wave's last step

@@ -50,6 +50,7 @@ struct ks_tiles {
     uint32_t S = 0, NS = 0, RT = 0, RMAX = 0, MAXG = 0, GCAP = 0, W = 0;
     size_t lds_bytes = 0;
     std::vector<uint16_t> pos, val;  // 8 u16 per group each
+    std::vector<uint32_t> steps;     // per (unit, k-step): first group, group count
 };
 
 // k_mfma_ks column tiles: CT 16-column MFMA tiles per workgroup (N = 8 runs one partial

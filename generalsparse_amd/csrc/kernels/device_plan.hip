@@ -328,6 +328,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
             a.t0 = dev_copy(d, to_u32(mc.tbr, "BMTB first_row_indices"));
             a.tcol = dev_copy(d, kt.pos);
             a.tval = dev_copy(d, kt.val);
+            a.t1 = dev_copy(d, kt.steps);
             d.bytes_tile = d.bytes_A - before;
             if (kt.S > 1) {
                 const uint32_t nt = ks_col_tiles(mc.N), CT = ks_ct(mc.N);

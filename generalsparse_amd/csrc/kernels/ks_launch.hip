@@ -46,8 +46,8 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
     GS_CHECK(gsk::ks_lds_bytes(CT, RT, W) <= d.lds_bytes, "k_mfma_ks: LDS size disagrees with the upload");
     grant_lds(d.device, kern, d.lds_bytes);
     hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit, ks_col_tiles(N)), dim3(64 * W), d.lds_bytes, s, a.t0,
-                       (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, B, C, (uint32_t)p.K, N, d.ksplit,
-                       d.ks_ns, d.ks_gcap, (uint32_t)d.n_rows_aux * d.ksplit, (uint32_t)d.row_base, a.ws, a.t2, stamps);
+                       (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, (const gsk::u32x2 *)a.t1, B, C,
+                       (uint32_t)p.K, N, d.ksplit, d.ks_ns, (uint32_t)d.n_rows_aux * d.ksplit, (uint32_t)d.row_base, a.ws, a.t2, stamps);
     HIP_OK(hipGetLastError());
 }
 
