@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-3 final-tree session: -m gpu suite + smoke (PART=a), bench lines + rocprofv3 kernel stats.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/r03b
+OUT=gpurun_out/${TAG:-r03b}
 mkdir -p $OUT
 export TMPDIR=/tmp
 set -e
