@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--workload", choices=("c1", "c2", "c3", "c4", "c4o", "c5", "c5h"), default=None,
                     help="default: c2 on one GPU, c5 (the sharded batch) on several")
     ap.add_argument("--search-reps", type=int, default=100, help="launches per candidate plan in the plan search")
+    ap.add_argument("--search-rounds", type=int, default=3,
+                    help="interleaved timing rounds per candidate plan (the median decides)")
     ap.add_argument("--n-sweep", default="", help="also time the chosen plan family at these dense widths, e.g. 8,32,128")
     ap.add_argument("--layers", type=int, default=48, help="c5: OPT-30B layers in the batch")
     ap.add_argument("--streams", type=int, default=2,
@@ -152,8 +154,10 @@ def algorithmic_bytes_24(M, K, N, nnz, e):
 
 
 def time_plan(plan, Bs, Cs, N, steps, warmup, torch, dist=None):
-    """returns (seconds for `steps` launches (max over ranks), avg kernel ms by events)"""
-    reps = plan.info()["replicas"]
+    """returns (host wall seconds for `steps` launches, seconds by HIP events on the launch
+    stream over the same `steps` launches), each the max over ranks.  The event time is the
+    reference's own measure (GpuTimer around the launches, baseline/base_cusparse/spmm.cu:137-154);
+    the wall time adds the host enqueue and the final synchronisation."""
     stream = torch.cuda.current_stream()
     plan.spmm_rotate(warmup, 0, Bs, Cs)
     torch.cuda.synchronize()
@@ -171,8 +175,8 @@ def time_plan(plan, Bs, Cs, N, steps, warmup, torch, dist=None):
     if dist is not None:
         dist.barrier()
     wall = t1 - t0
-    ev_ms = e0.elapsed_time(e1) / steps
-    return max_over_ranks(wall, dist, torch), ev_ms
+    ev_s = e0.elapsed_time(e1) * 1e-3
+    return max_over_ranks(wall, dist, torch), max_over_ranks(ev_s, dist, torch)
 
 
 def time_plan_combined(plan, Bs, Cs, N, steps, warmup, torch, dist, shards, rank):
@@ -201,7 +205,7 @@ def time_plan_combined(plan, Bs, Cs, N, steps, warmup, torch, dist, shards, rank
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     dist.barrier()
-    return max_over_ranks(wall, dist, torch), e0.elapsed_time(e1) / steps
+    return max_over_ranks(wall, dist, torch), max_over_ranks(e0.elapsed_time(e1) * 1e-3, dist, torch)
 
 
 def max_over_ranks(x, dist, torch):
@@ -287,9 +291,11 @@ def cpu_baseline(M, K, N, row, col, val, min_s=10.0, row_share=1):
                       f"single thread; plan transform (thread_total) once {t_tr:.2f} s; hot cache",
             "transform_s": round(t_tr, 3), "spmm_s_per_rep": round(t_spmm / reps, 4),
             "cpu_model": model, "nproc": nproc,
-            "all_cores": {"value": round(gf_mt, 3), "unit": "GFLOP/s", "threads": threads,
-                          "kind": "the build's OpenMP variant (the reference's host path is single-threaded)",
-                          "sample": f"{what} x{reps_mt} in {t_mt:.1f} s"}}
+            "multi_thread": {"value": round(gf_mt, 3), "unit": "GFLOP/s", "threads": threads,
+                             "label": f"{threads} threads of nproc {nproc} (OMP_NUM_THREADS: the one-GPU box's CPU "
+                                      f"share), not all cores",
+                             "kind": "the build's OpenMP variant (the reference's host path is single-threaded)",
+                             "sample": f"{what} x{reps_mt} in {t_mt:.1f} s"}}
 
 
 def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
@@ -307,7 +313,7 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
                                       bt.C5_SPARSITY, rocsparse=False)
     plans, launches, _ = bt.build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, choice=choice)
     t_setup = time.perf_counter() - t0
-    step, _ = batch_step(launches, N, torch, args.streams)
+    step, streams = batch_step(launches, N, torch, args.streams)
 
     for _ in range(args.warmup):
         step()
@@ -315,20 +321,18 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    wall = max_over_ranks(time.perf_counter() - t1, dist, torch)
+    wall, ev_s = timed_batch(step, streams, args.steps, torch)
+    wall = max_over_ranks(wall, dist, torch)
+    ev_s = max_over_ranks(ev_s, dist, torch)
     if dist is not None:
         dist.barrier()
     total_nnz = sum(bt.nnz_of_shape(b[2]) for b in batch)
     flops = 2.0 * total_nnz * N
-    value = flops * args.steps / wall / 1e9
+    value = flops * args.steps / ev_s / 1e9
     e = 2
     alg = sum(bt.nnz_of_shape(k) * (e + 2) + (bt.C5_SHAPES[k][0] + 1) * 4 + bt.C5_SHAPES[k][1] * N * e +
               bt.C5_SHAPES[k][0] * N * e for (_, _, k) in batch)
-    ms = wall / args.steps * 1e3
+    ms = ev_s / args.steps * 1e3
     # HBM bytes per step from the PMC passes of scripts/gpu_traffic_c5.sh (per GPU: the LPT
     # split is balanced on nnz); only for the full 48-layer batch it was scaled to
     traffic = None
@@ -345,6 +349,8 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
         "metric": "SpMM GFLOP/s, OPT-30B 80%-pruned weight batch fp16 N=32 (configs[4])",
         "value": round(value, 1), "unit": "GFLOP/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "timing": "HIP events around the K timed steps (all streams joined), max over ranks",
+        "wall_ms_per_step": round(wall / args.steps * 1e3, 4),
         "dtype": "f16 (fp32 accumulate)",
         "data": "synthetic (one seeded magnitude-pruned Gaussian per shape per rank; each batch instance streams "
                 "its own HBM copy of A)",
@@ -364,6 +370,27 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
         print(json.dumps(out), flush=True)
     for p in plans.values():
         p.free()
+
+
+def timed_batch(step, streams, steps, torch):
+    """`steps` calls of a batch step over its streams; returns (host wall s, HIP-event s).
+    The events sit on the first stream; the other streams wait for the start event and the
+    first stream waits for their last launches before the stop event."""
+    cur = streams[0]
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(cur)
+    for s in streams[1:]:
+        s.wait_event(e0)
+    for _ in range(steps):
+        step()
+    for s in streams[1:]:
+        cur.wait_event(s.record_event())
+    e1.record(cur)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0, e0.elapsed_time(e1) * 1e-3
 
 
 def batch_step(launches, N, torch, n_streams):
@@ -406,6 +433,9 @@ def search_shapes(args, torch, gsa, ds, rank, local, dev, shapes, sp, rocsparse=
             except gsa.GsError as ex:
                 variants[key] = {"error": str(ex)}
                 continue
+            except Exception as ex:  # noqa: BLE001 -- recorded with the shape, never a silent skip
+                variants[key] = {"error": f"{type(ex).__name__}: {ex}"}
+                continue
             info = plan.info()
             reps = replicas_for(info, n, N, e, args.rotation_mb)
             for _ in range(reps - 1):
@@ -419,6 +449,9 @@ def search_shapes(args, torch, gsa, ds, rank, local, dev, shapes, sp, rocsparse=
             plan.free()
             del Bs, Cs
             torch.cuda.empty_cache()
+        if best is None:  # every candidate of the shape failed: report them, do not crash
+            print(json.dumps({"error": f"no plan runs for shape {k}", "shape": k, "variants": variants}), flush=True)
+            raise SystemExit(1)
         ms, cand, key, kern, reps = best
         choice[k] = cand
         rs = rocsparse_baseline(m, n, N, row, col, val, min(reps, 20), dtype=1) if rocsparse else None
@@ -446,17 +479,16 @@ def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
     # the timed layer: 4 x attn (replicas 0..3), fc1, fc2
     seq = [(0, s, bt.C5_SLOTS[s], bt.C5_SLOTS[:s].count(bt.C5_SLOTS[s])) for s in range(len(bt.C5_SLOTS))]
     plans, launches, _ = bt.build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, sparsity=sp, choice=choice)
-    step, _ = batch_step(launches, N, torch, args.streams)
+    step, streams = batch_step(launches, N, torch, args.streams)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    ms_step = wall / args.steps * 1e3
+    wall, ev_s = timed_batch(step, streams, args.steps, torch)
+    ms_step = ev_s / args.steps * 1e3
+    # the layer's kernels one at a time (each shape's search time = its own launch alone):
+    # their serial sum against the overlapped layer step
+    serial_ms = sum(per_shape[k]["kernel_us"] for k in bt.C5_SLOTS) * 1e-3
     nnz_l = sum(bt.nnz_of_shape(k, sp) for k in bt.C5_SLOTS)
     flops_l = 2.0 * nnz_l * N
     alg_l = sum(algorithmic_bytes(*bt.C5_SHAPES[k], N, bt.nnz_of_shape(k, sp), e, 2) for k in bt.C5_SLOTS)
@@ -480,8 +512,14 @@ def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
         rs_l = sum(per_shape[k]["rocsparse_f16"]["ms"] for k in bt.C5_SLOTS)
     out = {
         "metric": "SpMM GFLOP/s + achieved HBM GB/s vs rocSPARSE, OPT-30B 70%-pruned layer fp16 N=32 (north_star headline)",
-        "value": round(flops_l * args.steps / wall / 1e9, 1), "unit": "GFLOP/s", "n_gpus": world, "steps": args.steps,
+        "value": round(flops_l * args.steps / ev_s / 1e9, 1), "unit": "GFLOP/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 5), "higher_is_better": True, "scaling": "weak",
+        "timing": "HIP events around the K timed steps (all streams joined)",
+        "wall_ms_per_step": round(wall / args.steps * 1e3, 5),
+        "serial_kernels": {"ms": round(serial_ms, 5), "gflops": round(flops_l / (serial_ms * 1e-3) / 1e9, 1),
+                           "hbm_frac": round(alg_l / (serial_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                           "note": "sum of the six launches timed alone (per_shape kernel_us); the layer step "
+                                   "overlaps them over the streams"},
         "vs_baseline": None, "dtype": "f16 (fp32 accumulate)",
         "data": "synthetic (one seeded magnitude-pruned Gaussian per shape; each layer instance streams its own HBM "
                 "copy of A); OPT-30B weights are not available offline",
@@ -491,7 +529,9 @@ def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
                    "parallelism": "one GPU", "streams": args.streams},
         "roofline": {"bound": "hbm", "achieved": round(alg_l / (ms_step * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg_l / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "algorithmic_bytes_per_step": alg_l, "note": "whole layer step (six launches, host-timed)"},
+                     "algorithmic_bytes_per_step": alg_l,
+                     "note": "whole layer step (six launches over the streams, HIP events); per-kernel fractions in "
+                             "per_shape.hbm_frac, their serial sum in serial_kernels"},
         "per_shape": per_shape,
         "speedup_vs_rocsparse": round(rs_l / ms_step, 3) if rs_l else None,
         "rocsparse_layer_ms": round(rs_l, 4) if rs_l else None,
@@ -622,10 +662,33 @@ def main():
         [(args.pipeline, 0, 1)]
     if args.p0 is not None:  # one variant (profiling runs)
         cands = [(c[0], args.p0, c[2] if args.p1 is None else args.p1) for c in cands[:1]]
-    # plan search (obtain_result.py's best variant): every candidate timed over search_reps
-    # launches (max over ranks, so every rank keeps the same plan)
+    # plan search (obtain_result.py's best variant): every candidate built, then timed in
+    # `--search-rounds` interleaved rounds of search_reps launches each; a candidate's time is
+    # its median over the rounds (max over ranks, so every rank keeps the same plan).
+    # Interleaving and the median keep candidates within a few percent of each other from
+    # flipping the choice with the chip's clock from run to run.
+    # (matrices of more than 50M nonzeros -- the com-Orkut stand-in -- are built and timed one
+    # candidate at a time, one round, so that only one candidate's host and device copies live)
     variants = {}
+    built = []
+    one_at_a_time = nnz > 50_000_000
+    rounds = 1 if one_at_a_time else max(1, args.search_rounds)
     best = None
+
+    def settle(b):
+        nonlocal best
+        plan_, Bs_, Cs_, reps_, cand_, key_, info_, t_plan_, times_ = b
+        ms_ = float(np.median(times_))
+        variants[key_] = {"kernel_ms": round(ms_, 5), "rounds_ms": [round(t, 5) for t in times_],
+                          "gflops_per_gpu": round(flops / (ms_ * 1e-3) / 1e9, 1),
+                          "kernel": kernel_label(info_), "replicas": reps_, "plan_s": round(t_plan_, 2)}
+        if best is None or ms_ < best[0]:
+            if best is not None:
+                best[1].free()
+            best = (ms_, plan_, Bs_, Cs_, reps_, cand_, key_, info_)
+        else:
+            plan_.free()
+
     for cand in cands:
         key = f"{cand[0]}({cand[1]},{cand[2]})"
         try:
@@ -634,29 +697,40 @@ def main():
         except gsa.GsError as ex:  # e.g. the balanced splitter on trailing empty rows
             variants[key] = {"error": str(ex)}
             continue
-        ms = max_over_ranks(event_ms(plan, Bs, Cs, args.search_reps, torch), dist, torch)
-        info = plan.info()
-        variants[key] = {"kernel_ms": round(ms, 5), "gflops_per_gpu": round(flops / (ms * 1e-3) / 1e9, 1),
-                         "kernel": kernel_label(info), "replicas": reps, "plan_s": round(t_plan, 2)}
-        if best is None or ms < best[0]:
-            if best is not None:
-                best[1].free()
-            best = (ms, plan, Bs, Cs, reps, cand, key, info)
+        b = [plan, Bs, Cs, reps, cand, key, plan.info(), t_plan, []]
+        if one_at_a_time:
+            b[8].append(max_over_ranks(event_ms(plan, Bs, Cs, args.search_reps, torch), dist, torch))
+            settle(b)
+            del b, Bs, Cs
+            torch.cuda.empty_cache()
         else:
-            plan.free()
-        del Bs, Cs
-        torch.cuda.empty_cache()
+            built.append(b)
+    for _ in range(rounds if built else 0):
+        for b in built:
+            b[8].append(max_over_ranks(event_ms(b[0], b[1], b[2], args.search_reps, torch), dist, torch))
+    for b in built:
+        settle(b)
+    del built
+    torch.cuda.empty_cache()
+    if best is None:
+        print(json.dumps({"metric": wl["metric"], "error": "no candidate plan runs", "variants": variants}), flush=True)
+        raise SystemExit(1)
     _, plan, Bs, Cs, reps, best_cand, key, info = best
     # the measurement: W untimed warm-up steps, exactly K timed steps
     if shards is not None and args.shard == "nnz" and dist is not None:
-        wall, ev_ms = time_plan_combined(plan, Bs, Cs, N, args.steps, args.warmup, torch, dist, shards, rank)
+        wall, ev_s = time_plan_combined(plan, Bs, Cs, N, args.steps, args.warmup, torch, dist, shards, rank)
     else:
-        wall, ev_ms = time_plan(plan, Bs, Cs, N, args.steps, args.warmup, torch, dist)
+        wall, ev_s = time_plan(plan, Bs, Cs, N, args.steps, args.warmup, torch, dist)
     hot_ms = event_ms(plan, Bs, Cs, 100, torch, rotate=False)
-    ms_per_step = wall / args.steps * 1e3
-    value = whole_job_gflops(world, flops, args.steps, wall)
+    # value and ms_per_step from the HIP events around the K timed steps (max over ranks);
+    # the host wall time of the same region is reported beside them
+    ev_ms = ev_s / args.steps * 1e3
+    ms_per_step = ev_ms
+    value = whole_job_gflops(world, flops, args.steps, ev_s)
+    wall_value = whole_job_gflops(world, flops, args.steps, wall)
     if shards is not None:  # strong scaling: the job is one matrix
-        value = full_flops * args.steps / wall / 1e9
+        value = full_flops * args.steps / ev_s / 1e9
+        wall_value = full_flops * args.steps / wall / 1e9
     achieved = alg_bytes / (ev_ms * 1e-3) / 1e9
     traffic = None
     tf = os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
@@ -671,6 +745,8 @@ def main():
         "metric": wl["metric"],
         "value": round(value, 1), "unit": "GFLOP/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 5), "higher_is_better": True,
+        "timing": "HIP events on the launch stream around the K timed steps, max over ranks",
+        "wall_ms_per_step": round(wall / args.steps * 1e3, 5), "wall_value": round(wall_value, 1),
         "scaling": "weak" if shards is None else "strong", "vs_baseline": None,
         "dtype": "f16 (fp32 accumulate)" if dt == "f16" else "f32", "data": wl["data"],
         "config": {"workload": wl["workload"].format(M=M, K=K, N=N),

@@ -1826,6 +1826,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
 #undef GS_KS_STAMP
 }
 
+#ifdef GS_EXPERIMENTS  // opt-in, measured slower than k_mfma_rows / k_mfma_ks (make EXPERIMENTS=1)
 // ---------------------------------------------------------------------------
 // k_mfma_bm -- BMTB row blocks on the matrix cores from a bitmap layout, with the
 // dense A fragments built in registers (no dense image, no LDS scatter).
@@ -2275,6 +2276,7 @@ __global__ __launch_bounds__(64 * RT) void k_mfma_bm2(const uint32_t *__restrict
     store_tile(sum);
 }
 
+#endif  // GS_EXPERIMENTS (k_mfma_bm, k_mfma_bm2)
 // ---------------------------------------------------------------------------
 // k_nm_mfma -- fixed_interval_col_direction BMTs that are 2:4 panels
 //  on the sparse matrix cores:
@@ -2526,6 +2528,7 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
     }
 }
 
+#ifdef GS_EXPERIMENTS  // opt-in, measured slower than k_nm_mfma (make EXPERIMENTS=1)
 // ---------------------------------------------------------------------------
 // k_nm_mfma_ks -- the same 2:4 panels (same HBM blocks as k_nm_mfma) with one 64-row
 // group per wave, four waves = 256 rows per workgroup and K split over `nsplit`
@@ -2744,6 +2747,7 @@ __global__ __launch_bounds__(256) void k_nm_mfma_ks(const unsigned char *__restr
     store_tile(sum);
 }
 
+#endif  // GS_EXPERIMENTS (k_nm_mfma_ks)
 // ---------------------------------------------------------------------------
 // k_merge_path -- merge-path levels (merge_path_{thread,warp,tblock}_operator +
 // the level's total-reduce token).  The plan's
@@ -3086,6 +3090,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     }
 }
 
+#ifdef GS_EXPERIMENTS  // opt-in, measured slower than k_merge_path (make EXPERIMENTS=1)
 // ---------------------------------------------------------------------------
 // k_merge_rows -- the same merge-path plan (wave ranges wz/wq, compact rows
 // ends/rid, split-row chains) with a two-phase walk per round of R = S*J
@@ -3327,6 +3332,7 @@ __global__ __launch_bounds__(256) void k_merge_rows(const uint32_t *__restrict__
     }
 }
 
+#endif  // GS_EXPERIMENTS (k_merge_rows)
 // rows open across waves: C[r] = (sum of the open partials in wave order) + the
 // closing wave's partial, rounded once
 template <class VT>

@@ -221,6 +221,7 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
                         : (L.nm_ks ? "k_nm_mfma_ks" : "k_nm_mfma");
     o << "// kernel_file.hip -- generated by generalsparse_amd code_generator: the matrix-core kernel " << kname << "\n"
       << "// build: sh make_kernel.sh; run: ./a.out [matrix.mtx] [N]  -> perf_result (ms, GFLOP/s)\n"
+      << (L.kind == mc_layout::BM || L.nm_ks || L.rows_flags ? "#define GS_EXPERIMENTS  // an experiments-build kernel\n" : "")
       << "#include \"kernel_lib.hpp\"\n#include <cstdio>\n#include <cstdlib>\n#include <cstring>\n#include <fstream>\n"
       << "#include <string>\n#include <vector>\n\n"
       << "typedef gsk::f16 VT;\n"
@@ -399,6 +400,7 @@ std::string code_generator::generate_gather_source(int repeat) const {
     o << "// kernel_file.hip -- generated by generalsparse_amd code_generator for plan family "
       << spec.name() << "\n"
       << "// build: sh make_kernel.sh; run: ./a.out [matrix.mtx] [N]  -> perf_result (ms, GFLOP/s)\n"
+      << (get_config().MP_ROWS ? "#define GS_EXPERIMENTS  // an experiments-build kernel\n" : "")
       << "#include \"kernel_lib.hpp\"\n#include <cstdio>\n#include <cstdlib>\n#include <cstring>\n#include <fstream>\n"
       << "#include <string>\n#include <vector>\n\n"
       << "typedef " << (half ? "gsk::f16" : "float") << " VT;\n"

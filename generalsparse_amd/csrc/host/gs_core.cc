@@ -172,13 +172,28 @@ config_t get_config() {
     return g_cfg;
 }
 
+// switches that select kernels kept only in the experiments build (make -C csrc exp):
+// measured slower than the default kernels, parity-tested there
+bool experiments_key(const std::string &k) {
+    return k == "MFMA_BM" || k == "NM_KS" || k == "MFMA_FLAGS" || k == "BM_V2" || k == "MP_ROWS";
+}
+
 void set_config(const std::string &key, int64_t value) {
+#ifndef GS_EXPERIMENTS
+    if (value != 0 && experiments_key(key))
+        throw gs_error(key + " selects an experiments-build kernel (make -C generalsparse_amd/csrc exp)", -2);
+#endif
     std::lock_guard<std::mutex> l(g_cfg_mu);
     ensure_loaded();
     apply_kv(g_cfg, key, std::to_string(value));
 }
 
 int64_t get_config_int(const std::string &k) {
+#ifdef GS_EXPERIMENTS
+    if (k == "GS_EXPERIMENTS") return 1;
+#else
+    if (k == "GS_EXPERIMENTS") return 0;
+#endif
     const config_t c = get_config();
 #define GS_KEY(name) \
     if (k == #name) return (int64_t)c.name;

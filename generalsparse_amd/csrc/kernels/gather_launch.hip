@@ -24,8 +24,12 @@ constexpr int kLdsMaxU = 12;  // 16-B staging registers per thread (k_lds_rows M
 
 // GS_MP_DEBUG (diagnostic timing only): k_merge_path dbg bits
 uint32_t mp_debug() {
+#ifdef GS_EXPERIMENTS
     static const uint32_t v = getenv("GS_MP_DEBUG") ? (uint32_t)atoi(getenv("GS_MP_DEBUG")) : 0u;
     return v;
+#else
+    return 0u;
+#endif
 }
 
 uint32_t pow2ceil(uint32_t x) {
@@ -157,6 +161,7 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
             const uint32_t fb = d.n_fin ? (uint32_t)std::min<uint64_t>(256, (d.n_fin * N / 4 + 1023) / 1024) : 0u;
             // one column tile: split rows are combined inside the launch (chain arrivals)
             const bool fused = tiles == 1 && !(mp_debug() & 4u);
+#ifdef GS_EXPERIMENTS
             if (d.mp_rows)
                 hipLaunchKernelGGL((gsk::k_merge_rows<VT, CT, CF>), dim3(gx + fb, tiles), dim3(256),
                                    (size_t)4 * gsk::merge_rows_wave_words(X, CF, gsk::merge_rows_j<CF>()) * sizeof(float), s, a.a0,
@@ -164,6 +169,9 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
                                    a.a4, (uint32_t)d.n_fin, fb, fused ? a.t1 : nullptr, fused ? a.t2 : nullptr,
                                    d.mp_solo);
             else
+#else
+            GS_CHECK(!d.mp_rows, "k_merge_rows is an experiments-build kernel");
+#endif
                 hipLaunchKernelGGL((gsk::k_merge_path<VT, CT, CF>), dim3(gx + fb, tiles), dim3(256), lds, s, a.a0, a.a1,
                                    a.a2, a.a3, (uint32_t)d.n_rows_aux, col, val, B, C, a.ws, a.t0, a.ws2, W, N, X, row_base,
                                    (uint32_t)d.n_out_rows, a.a4, (uint32_t)d.n_fin, fb, fused ? a.t1 : nullptr,

@@ -71,6 +71,7 @@ void launch_ks_ct(const plan_state &p, const device_arrays &a, const gsk::f16 *B
     }
 }
 
+#ifdef GS_EXPERIMENTS
 template <int CT, int RT, int W, bool STAMPS = false>
 void launch_bm_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s,
                  uint64_t *stamps = nullptr) {
@@ -118,8 +119,11 @@ void launch_bm_ct(const plan_state &p, const device_arrays &a, const gsk::f16 *B
     }
 }
 
+#endif  // GS_EXPERIMENTS
+
 }  // namespace
 
+#ifdef GS_EXPERIMENTS
 void launch_bm(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
     const gsk::f16 *b = (const gsk::f16 *)B;
     gsk::f16 *c = (gsk::f16 *)C;
@@ -130,6 +134,12 @@ void launch_bm(const plan_state &p, const device_arrays &a, const void *B, void 
         default: launch_bm_ct<4>(p, a, b, c, N, s); break;
     }
 }
+
+#else
+void launch_bm(const plan_state &, const device_arrays &, const void *, void *, uint32_t, hipStream_t) {
+    throw gs_error("k_mfma_bm is an experiments-build kernel (make -C generalsparse_amd/csrc exp)", -2);
+}
+#endif
 
 void launch_ks(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
     const gsk::f16 *b = (const gsk::f16 *)B;
@@ -142,6 +152,7 @@ void launch_ks(const plan_state &p, const device_arrays &a, const void *B, void 
     }
 }
 
+#ifdef GS_EXPERIMENTS  // diagnostics (s_memtime stamps)
 // diagnostic: k_mfma_bm at N = 32, 65..80-row blocks, 8 waves (stamps: kernel_lib.hpp)
 void debug_bm_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
                        size_t n_host) {
@@ -161,15 +172,34 @@ void debug_bm_timeline(const plan_state &p, const void *B, void *C, uint32_t N, 
 void debug_ks_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
                        size_t n_host) {
     const device_plan &d = p.dev;
-    GS_CHECK(N == 32 && d.maxr == 5 && d.seg_cap == 2 && d.waves == kKsWaves, "k_mfma_ks timeline build: N=32, RT=5, MAXG=2, 8 waves only");
+    GS_CHECK(N == 32 && d.maxr >= 2 && d.maxr <= 5 && d.seg_cap <= 2 && d.waves == kKsWaves,
+             "k_mfma_ks timeline build: N=32, RT 2..5, MAXG <= 2, 8 waves only");
     const size_t n = (size_t)d.n_rows_aux * d.ksplit * ks_col_tiles(N) * kKsWaves * 32;
     uint64_t *dst = nullptr;
     HIP_OK(hipMalloc(&dst, n * 8));
     HIP_OK(hipMemsetAsync(dst, 0, n * 8, s));
-    launch_ks_k<2, 5, 2, true>(p, d.replicas[0], (const gsk::f16 *)B, (gsk::f16 *)C, N, s, dst);
+    const device_arrays &a = d.replicas[0];
+    const gsk::f16 *b = (const gsk::f16 *)B;
+    gsk::f16 *c = (gsk::f16 *)C;
+    const bool g1 = d.seg_cap == 1;
+    switch (d.maxr) {
+        case 2: g1 ? launch_ks_k<2, 2, 1, true>(p, a, b, c, N, s, dst) : launch_ks_k<2, 2, 2, true>(p, a, b, c, N, s, dst); break;
+        case 3: g1 ? launch_ks_k<2, 3, 1, true>(p, a, b, c, N, s, dst) : launch_ks_k<2, 3, 2, true>(p, a, b, c, N, s, dst); break;
+        case 4: g1 ? launch_ks_k<2, 4, 1, true>(p, a, b, c, N, s, dst) : launch_ks_k<2, 4, 2, true>(p, a, b, c, N, s, dst); break;
+        default: g1 ? launch_ks_k<2, 5, 1, true>(p, a, b, c, N, s, dst) : launch_ks_k<2, 5, 2, true>(p, a, b, c, N, s, dst); break;
+    }
     HIP_OK(hipStreamSynchronize(s));
     HIP_OK(hipMemcpy(host, dst, std::min(n, n_host) * 8, hipMemcpyDeviceToHost));
     (void)hipFree(dst);
 }
+
+#else
+void debug_bm_timeline(const plan_state &, const void *, void *, uint32_t, hipStream_t, uint64_t *, size_t) {
+    throw gs_error("timeline builds are diagnostics of the experiments build (make -C generalsparse_amd/csrc exp)", -2);
+}
+void debug_ks_timeline(const plan_state &, const void *, void *, uint32_t, hipStream_t, uint64_t *, size_t) {
+    throw gs_error("timeline builds are diagnostics of the experiments build (make -C generalsparse_amd/csrc exp)", -2);
+}
+#endif  // GS_EXPERIMENTS
 
 }  // namespace gs

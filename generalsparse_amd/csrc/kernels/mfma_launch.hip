@@ -30,12 +30,15 @@ void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *
     auto kern = gl == 4 ? gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 4>
                         : (gl ? gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2> : gsk::k_mfma_rows<CT, RT, LGKC, MAXA>);
     if (gl == 2 && wct == 8) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 8>;
+#ifdef GS_EXPERIMENTS
     // LDS counter hand-offs between the roles instead of per-chunk barriers (MFMA_FLAGS)
     if (gl == 2 && wct == 6 && nbg == 3 && d.mfma_flags) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 0, true>;
+#endif
     if constexpr (LGKC == 8) {  // deeper B rings fit LDS with 256-column chunks
         if (gl == 2 && wct == 6 && nbg == 4) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 4>;
         if (gl == 2 && wct == 6 && nbg == 5) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 5>;
     }
+#ifdef GS_EXPERIMENTS
     // GS_MFMA_DEBUG (diagnostic timing builds, wrong results): kernel_lib.hpp k_mfma_rows DBG bits, C2 shape only
     static const int mdbg = getenv("GS_MFMA_DEBUG") ? atoi(getenv("GS_MFMA_DEBUG")) : 0;
     if constexpr (CT == 2 && RT == 2 && LGKC == 9 && MAXA == 1) {
@@ -46,6 +49,7 @@ void launch_mfma_k(const plan_state &p, const device_arrays &a, const gsk::f16 *
         if (gl == 2 && wct == 6 && mdbg == 11) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 11>;
         if (gl == 2 && wct == 6 && mdbg == 15) kern = gsk::k_mfma_rows<CT, RT, LGKC, MAXA, false, 2, 3, 6, 15>;
     }
+#endif
     static std::mutex mu;
     static std::map<std::pair<int, const void *>, size_t> granted;
     {
@@ -88,6 +92,7 @@ void launch_mfma_ct(const plan_state &p, const device_arrays &a, const gsk::f16 
 
 }  // namespace
 
+#ifdef GS_EXPERIMENTS  // diagnostics (s_memtime stamps)
 // diagnostic: N = 32 plans with 17..48-row BMTBs and KC 256 or 512
 template <int RT, int LG>
 auto timeline_kernel(bool two) {
@@ -127,15 +132,26 @@ void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N
     (void)hipFree(dst);
 }
 
+#else
+void debug_mfma_timeline(const plan_state &, const void *, void *, uint32_t, hipStream_t, uint64_t *, size_t) {
+    throw gs_error("timeline builds are diagnostics of the experiments build (make -C generalsparse_amd/csrc exp)", -2);
+}
+#endif  // GS_EXPERIMENTS
+
 namespace {
 
 template <int CT>
 void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, void *C, hipStream_t s) {
     const device_plan &d = p.dev;
+#ifdef GS_EXPERIMENTS
     // GS_NM_DEBUG=1/2: diagnostic builds without the loop's B / A loads (wrong results)
     static const int dbg = getenv("GS_NM_DEBUG") ? atoi(getenv("GS_NM_DEBUG")) : 0;
     auto kern = dbg == 1 ? gsk::k_nm_mfma<CT, 1>
                          : (dbg == 2 ? gsk::k_nm_mfma<CT, 2> : (dbg == 4 ? gsk::k_nm_mfma<CT, 4> : gsk::k_nm_mfma<CT, 0>));
+#else
+    constexpr int dbg = 0;
+    auto kern = gsk::k_nm_mfma<CT, 0>;
+#endif
     const size_t lds = (size_t)2 * gsk::kNmKC * 32 * CT + (dbg == 4 ? 4096 : 0);
     static std::mutex mu;
     static std::map<std::pair<int, const void *>, bool> granted;
@@ -148,6 +164,7 @@ void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, vo
             g = true;
         }
     }
+#ifdef GS_EXPERIMENTS
     if (d.nm_ks) {
         auto kk = gsk::k_nm_mfma_ks<CT>;
         const size_t lds2 = (size_t)2 * gsk::kNmKC * 32 * CT;
@@ -169,6 +186,9 @@ void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, vo
         HIP_OK(hipGetLastError());
         return;
     }
+#else
+    GS_CHECK(!d.nm_ks, "k_nm_mfma_ks is an experiments-build kernel");
+#endif
     const uint32_t wg = (uint32_t)((d.n_rows_aux + 127) / 128);
     hipLaunchKernelGGL(kern, dim3(wg), dim3(64 * gsk::kNmWaves), lds, s, (const unsigned char *)a.tcol,
                        (const gsk::f16 *)B, (gsk::f16 *)C, (uint32_t)p.K, d.KC, (uint32_t)d.n_rows_aux,

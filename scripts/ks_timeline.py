@@ -34,7 +34,9 @@ _lib.check(L.gs_debug_mfma_timeline(plan._h, ctypes.c_void_p(B.data_ptr()), ctyp
 a = np.frombuffer(st, dtype=np.uint64).reshape(nwg, 8, 32).astype(np.int64)
 t0 = a[:, :, 0].min(axis=1)[:, None]
 glob0 = a[:, :, 0].min()
-out = {"ksplit": info["ksplit"], "wg_start_spread": [float(np.percentile(t0 - glob0, p)) for p in (0, 50, 90, 100)]}
+# s_memtime is per XCD (clocks of different XCDs are not aligned): every delta is taken
+# inside one workgroup (from its first stamp)
+out = {"ksplit": info["ksplit"], "rows": P0}
 for slot in [1, 2] + list(range(3, 16)) + [20, 21, 22]:
     v = a[:, :, slot]
     ok = v > 0
@@ -42,6 +44,6 @@ for slot in [1, 2] + list(range(3, 16)) + [20, 21, 22]:
         continue
     d = (v - t0)[ok]
     out[str(slot)] = [float(np.median(d)), float(np.percentile(d, 90)), int(ok.sum())]
-end = (a[:, :, 22].max(axis=1) - glob0)
-out["kernel_span_clk"] = float(end.max())
+span = a[:, :, 22].max(axis=1) - t0[:, 0]
+out["wg_span_clk"] = [float(np.median(span)), float(np.percentile(span, 90)), float(span.max())]
 print(json.dumps(out))

@@ -11,6 +11,9 @@ import pytest
 
 import generalsparse_amd as gsa
 from generalsparse_amd import datasets as ds
+from build_flags import experiments
+
+pytestmark = experiments
 
 
 def _decode(d, M, K, tbr):

@@ -11,7 +11,9 @@ torch = pytest.importorskip("torch")
 import generalsparse_amd as gsa  # noqa: E402
 from generalsparse_amd import datasets as ds  # noqa: E402
 
-pytestmark = pytest.mark.gpu
+from build_flags import experiments  # noqa: E402
+
+pytestmark = [pytest.mark.gpu, experiments]
 DEV = "cuda:0"
 
 

@@ -222,6 +222,47 @@ def test_c5_shapes_against_torch(c5_coo):
             plan.free()
 
 
+# The exact plans behind the C5 batch line (80%: block_total(56,1) on every shape,
+# profiles/r03d_c5_bench.json) and the 70% headline layer (fc1 block_total(80,1), fc2
+# block_total(56,1), attn tblock_warp_total(28,2), profiles/r03d_c5h_bench.json), at full
+# size against a torch fp32 dense product.  Expected kernel and K ranges:
+# row blocks of >= KS_MIN_ROWS rows run k_mfma_ks with S = min(8, ceil(256 / blocks)).
+HEADLINE_PLANS = [
+    (0.8, "attn", ("block_total", 56, 1), "k_mfma_ks", 2),
+    (0.8, "fc1", ("block_total", 56, 1), "k_mfma_ks", 1),
+    (0.8, "fc2", ("block_total", 56, 1), "k_mfma_ks", 2),
+    (0.7, "attn", ("tblock_warp_total", 28, 2), "k_mfma_rows", None),
+    (0.7, "fc1", ("block_total", 80, 1), "k_mfma_ks", 1),
+    (0.7, "fc2", ("block_total", 56, 1), "k_mfma_ks", 2),
+]
+
+
+@pytest.mark.parametrize("sp,shape,cand,kernel,ksplit", HEADLINE_PLANS,
+                         ids=[f"{round(p[0] * 100)}-{p[1]}-{p[2][0]}{p[2][1]}" for p in HEADLINE_PLANS])
+def test_batch_and_headline_plans_against_torch(sp, shape, cand, kernel, ksplit):
+    N = 32
+    m, n = bt.C5_SHAPES[shape]
+    row, col, val = ds.pruned_weight(m, n, sp, bt.shape_seed(0, shape))
+    plan = gsa.Plan.from_coo(m, n, row, col, val).run_pipeline(cand[0], N, cand[1], cand[2]).compile().upload("f16", 0)
+    info = plan.info()
+    assert info["device_kernel"] == kernel, info["device_kernel"]
+    if ksplit is not None:
+        assert info["ksplit"] == ksplit, info["ksplit"]
+    g = torch.Generator(device=DEV)
+    g.manual_seed(7)
+    B = (torch.rand((n, N), device=DEV, generator=g) * 2 - 1).half()
+    C = plan.spmm(B)
+    torch.cuda.synchronize()
+    check(C.float().cpu().numpy(), dense_ref(m, n, row, col, val, B), "f16")
+    # a second launch into a NaN-filled C: every element is written, the K-range arrival
+    # counters re-arm (the same answer bit for bit)
+    C2 = torch.full_like(C, float("nan"))
+    plan.spmm(B, C=C2)
+    torch.cuda.synchronize()
+    assert torch.equal(C, C2)
+    plan.free()
+
+
 def test_c5_two_layer_batch_sequence():
     """two layers of the batch on one rank through generalsparse_amd.batch (bench.py run_c5):
     every launch of the sequence, with its replica and its B/C pair, gives that shape's

@@ -13,6 +13,7 @@ import oracle_ffi as ofi
 torch = pytest.importorskip("torch")
 import generalsparse_amd as gsa  # noqa: E402
 from generalsparse_amd import datasets as ds  # noqa: E402
+from build_flags import need_experiments  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -156,6 +157,7 @@ def test_nm_c3_scale_against_dense():
 def test_nm_ks_and_classic_kernels(shape, N, ks, split):
     """k_nm_mfma_ks (256-row workgroups, K split over NM_SPLIT ranges, slab combine by the
     last arriver) and the classic k_nm_mfma: oracle parity, determinism, replicas"""
+    need_experiments(ks == 1)
     old = {k: gsa.get_config(k) for k in ("NM_KS", "NM_SPLIT")}
     try:
         gsa.set_config("NM_KS", ks)

@@ -14,6 +14,7 @@ import oracle_ffi as ofi
 torch = pytest.importorskip("torch")
 import generalsparse_amd as gsa  # noqa: E402
 from generalsparse_amd import datasets as ds  # noqa: E402
+from build_flags import need_experiments  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -545,7 +546,9 @@ def merge_cases():
 
 @pytest.fixture(params=[0, 1], ids=["k_merge_path", "k_merge_rows"])
 def merge_walk(request):
-    """both merge-path walks (MP_ROWS fixes the kernel at upload)"""
+    """both merge-path walks (MP_ROWS fixes the kernel at upload; k_merge_rows is an
+    experiments-build kernel)"""
+    need_experiments(request.param == 1)
     gsa.set_config("MP_ROWS", request.param)
     yield "k_merge_rows" if request.param else "k_merge_path"
     gsa.set_config("MP_ROWS", 0)
@@ -691,6 +694,7 @@ def test_warp_rows_grouped_passes(groups, N):
 def test_mfma_rows_counter_handoffs(pipe, N, mfma_everywhere):
     """k_mfma_rows with MFMA_FLAGS (the roles hand buffers over through LDS counters, no
     per-chunk barrier): oracle parity, determinism, and the C2 shape against torch"""
+    need_experiments()
     name, p0, p1 = pipe
     gsa.set_config("MFMA_GLDS", 1)
     gsa.set_config("MFMA_FLAGS", 1)
