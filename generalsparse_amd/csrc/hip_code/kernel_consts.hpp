@@ -33,8 +33,17 @@ GSK_HD constexpr uint32_t ks_image_bytes() {
 GSK_HD constexpr bool ks_red_halves(uint32_t CT, uint32_t RT, uint32_t W) {
     return (size_t)W * RT * CT * 1024u + 16u > 160u * 1024u;
 }
+GSK_HD constexpr size_t ks_stage_bytes(uint32_t CT, uint32_t RT, uint32_t W) {
+    return (size_t)W * ((16u * RT + 1u) * kKsStride + 32u * 32u * CT);
+}
+// the W partial tiles (+ the ticket word) fit beside the wave images: each wave stores its
+// tile when its own loop ends, with no barrier before
+GSK_HD constexpr bool ks_red_apart(uint32_t CT, uint32_t RT, uint32_t W) {
+    return ks_stage_bytes(CT, RT, W) + (size_t)W * RT * CT * 1024u + 16u <= 160u * 1024u;
+}
 GSK_HD constexpr size_t ks_lds_bytes(uint32_t CT, uint32_t RT, uint32_t W) {
-    const size_t stage = (size_t)W * ((16u * RT + 1u) * kKsStride + 32u * 32u * CT);
+    const size_t stage = ks_stage_bytes(CT, RT, W);
+    if (ks_red_apart(CT, RT, W)) return stage + (size_t)W * RT * CT * 1024u + 16u;
     const size_t red = (size_t)(ks_red_halves(CT, RT, W) ? W / 2 : W) * RT * CT * 1024u + 16u;
     return stage > red ? stage : red;
 }

@@ -214,7 +214,7 @@ namespace {
 // (kernels/{ks,mfma}_launch.hip); the check and perf_result as for the other families
 std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int repeat) {
     std::ostringstream o;
-    const uint32_t N = L.N, CT = L.kind == mc_layout::NM ? N / 16 : ks_ct(N);
+    const uint32_t N = L.N, CT = L.kind == mc_layout::NM ? std::max<uint32_t>(1, N / 16) : ks_ct(N);
     const char *kname = L.kind == mc_layout::KS ? "k_mfma_ks"
                         : L.kind == mc_layout::BM ? (L.bm.v2 ? "k_mfma_bm2" : "k_mfma_bm")
                         : L.kind == mc_layout::ROWS ? "k_mfma_rows"
@@ -254,7 +254,9 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
           << "    uint16_t *d_pos = up(rdb<uint16_t>(\"TBLOCK_META_mfma_ks_entry_pos_0.bin\"));\n"
           << "    uint16_t *d_val = up(rdb<uint16_t>(\"TBLOCK_META_mfma_ks_entry_val_0.bin\"));\n"
           << "    uint32_t *d_steps = up(rdb<uint32_t>(\"TBLOCK_META_mfma_ks_steps_0.bin\"));\n"
+          << "    // the tagged slabs start (and are left by every launch) all 0\n"
           << "    float *d_ws; uint32_t *d_arr; hipMalloc(&d_ws, " << nwg * ks_col_tiles(N) * 256 * t.RT * CT * 4 << "ull + 16);\n"
+          << "    hipMemset(d_ws, 0, " << nwg * ks_col_tiles(N) * 256 * t.RT * CT * 4 << "ull + 16);\n"
           << "    hipMalloc(&d_arr, " << nb * ks_col_tiles(N) * 4 << "ull + 4); hipMemset(d_arr, 0, " << nb * ks_col_tiles(N) * 4
           << "ull + 4);\n";
         const std::string k = "gsk::k_mfma_ks<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ", " +
@@ -321,7 +323,8 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
                  "u, 0u, " + std::to_string(L.nm_split) + "u, " + std::to_string(L.nm_ncs) + "u, d_ws, d_arr)";
     } else {
         o << "    unsigned char *d_blk = up(rdb<unsigned char>(\"THREAD_META_nm_panels_0.bin\"));\n";
-        const std::string k = "gsk::k_nm_mfma<" + std::to_string(CT) + ">";
+        // N = 8: one half-used 16-column tile (k_nm_mfma's NG)
+        const std::string k = "gsk::k_nm_mfma<" + std::to_string(CT) + (N == 8 ? ", 0, 8>" : ">");
         const size_t lds = (size_t)2 * gsk::kNmKC * 32 * CT;
         setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
                 std::to_string(lds) + ")";

@@ -490,7 +490,7 @@ mc_layout choose_matrix_core_layout(const meta_data_set &m, const kernel_spec &s
     if (dtype != 1) { L.why = "fp32 plan"; return L; }
     const uint64_t row_num = row_num_of_sub_matrix(m, sb);
     const auto &rows = m.u(GLOBAL_META, "nz_row_indices", sb);
-    if (sp.family == KF_ROW_CHUNKS && !sp.interleaved && cfg.NM_MFMA && (Nd == 32 || Nd == 64 || Nd == 128)) {
+    if (sp.family == KF_ROW_CHUNKS && !sp.interleaved && cfg.NM_MFMA && (Nd == 8 || Nd == 16 || Nd == 32 || Nd == 64 || Nd == 128)) {
         // col-direction BMTs that are 2:4 panels: sparse matrix cores, self-contained blocks
         const auto &col = m.u(GLOBAL_META, "nz_col_indices", sb);
         auto vals = m.get_element(GLOBAL_META, "nz_vals", sb)->meta_data_arr;
@@ -501,7 +501,7 @@ mc_layout choose_matrix_core_layout(const meta_data_set &m, const kernel_spec &s
             const uint32_t nch = L.nm_S / 4, nb = (uint32_t)((row_num + 255) / 256);
             uint32_t sp = cfg.NM_SPLIT > 0 ? (uint32_t)cfg.NM_SPLIT : std::max<uint32_t>(1, 256 / std::max<uint32_t>(nb, 1));
             sp = std::max(1u, std::min(sp, nch));
-            L.nm_ks = cfg.NM_KS != 0;
+            L.nm_ks = cfg.NM_KS != 0 && Nd >= 16;
             L.nm_ncs = (nch + sp - 1) / sp;
             L.nm_split = (nch + L.nm_ncs - 1) / L.nm_ncs;
         }

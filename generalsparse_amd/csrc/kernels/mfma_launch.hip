@@ -140,17 +140,17 @@ void debug_mfma_timeline(const plan_state &, const void *, void *, uint32_t, hip
 
 namespace {
 
-template <int CT>
+template <int CT, int NG = 16 * CT>
 void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, void *C, hipStream_t s) {
     const device_plan &d = p.dev;
 #ifdef GS_EXPERIMENTS
     // GS_NM_DEBUG=1/2: diagnostic builds without the loop's B / A loads (wrong results)
     static const int dbg = getenv("GS_NM_DEBUG") ? atoi(getenv("GS_NM_DEBUG")) : 0;
-    auto kern = dbg == 1 ? gsk::k_nm_mfma<CT, 1>
-                         : (dbg == 2 ? gsk::k_nm_mfma<CT, 2> : (dbg == 4 ? gsk::k_nm_mfma<CT, 4> : gsk::k_nm_mfma<CT, 0>));
+    auto kern = dbg == 1 ? gsk::k_nm_mfma<CT, 1, NG>
+                         : (dbg == 2 ? gsk::k_nm_mfma<CT, 2, NG> : (dbg == 4 ? gsk::k_nm_mfma<CT, 4, NG> : gsk::k_nm_mfma<CT, 0, NG>));
 #else
     constexpr int dbg = 0;
-    auto kern = gsk::k_nm_mfma<CT, 0>;
+    auto kern = gsk::k_nm_mfma<CT, 0, NG>;
 #endif
     const size_t lds = (size_t)2 * gsk::kNmKC * 32 * CT + (dbg == 4 ? 4096 : 0);
     static std::mutex mu;
@@ -200,11 +200,13 @@ void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, vo
 
 void launch_nm(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
     switch (N) {
+        case 8: launch_nm_ct<1, 8>(p, a, B, C, s); break;  // one half-used 16-column tile
+        case 16: launch_nm_ct<1>(p, a, B, C, s); break;
         case 32: launch_nm_ct<2>(p, a, B, C, s); break;
         case 64: launch_nm_ct<4>(p, a, B, C, s); break;
         case 128: launch_nm_ct<8>(p, a, B, C, s); break;
         default:
-            throw gs_error("2:4 panel plan (k_nm_mfma) runs N = 32, 64 or 128, not " + std::to_string(N), -2);
+            throw gs_error("2:4 panel plan (k_nm_mfma) runs N = 8, 16, 32, 64 or 128, not " + std::to_string(N), -2);
     }
 }
 

@@ -44,6 +44,12 @@ for slot in [1, 2] + list(range(3, 16)) + [20, 21, 22]:
         continue
     d = (v - t0)[ok]
     out[str(slot)] = [float(np.median(d)), float(np.percentile(d, 90)), int(ok.sum())]
+# per wave index: loop done (slot 20) relative to the workgroup's first stamp
+out["loop_done_by_wave"] = [float(np.median(a[:, w, 20] - t0[:, 0])) for w in range(a.shape[1])]
+out["step0_by_wave"] = [float(np.median(a[:, w, 3] - t0[:, 0])) for w in range(a.shape[1])]
+# spread of loop-done inside a workgroup (max - min over its waves)
+ld = a[:, :, 20] - t0
+out["loop_done_spread_in_wg"] = [float(np.median(ld.max(axis=1) - ld.min(axis=1))), float(np.percentile(ld.max(axis=1) - ld.min(axis=1), 90))]
 span = a[:, :, 22].max(axis=1) - t0[:, 0]
 out["wg_span_clk"] = [float(np.median(span)), float(np.percentile(span, 90)), float(span.max())]
 print(json.dumps(out))

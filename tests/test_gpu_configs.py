@@ -140,8 +140,11 @@ def test_c1_token_test_ig5_18_standin(tmp_path):
 
 
 # ------------------------------------------------------------------ C3
-def test_c3_full_size_against_torch():
-    M, K, N = 28672, 7168, 128
+@pytest.mark.parametrize("N", [8, 128])
+def test_c3_full_size_against_torch(N):
+    """N = 128 (BASELINE configs[2]) and N = 8 (the north_star's narrowest width: one
+    half-used 16-column tile on the sparse matrix cores)"""
+    M, K = 28672, 7168
     row, col, val = ds.two_four(M, K, 30)
     plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline("col_direction_nm", N, 32, 1).compile().upload("f16", 0)
     assert plan.info()["device_kernel"] == "k_nm_mfma"

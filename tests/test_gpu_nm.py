@@ -48,9 +48,10 @@ def thinned(M, K, seed, keep=0.6, empty_rows=()):
 SHAPES = [(128, 256), (96, 512), (200, 1000), (333, 772), (64, 64), (1, 4096)]
 
 
-@pytest.mark.parametrize("N", [32, 64, 128])
+@pytest.mark.parametrize("N", [8, 16, 32, 64, 128])
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: f"{s[0]}x{s[1]}")
 def test_nm_matches_oracle(shape, N):
+    """N = 8 runs one half-used 16-column tile (k_nm_mfma's NG = 8)"""
     M, K = shape
     r, c, v = ds.two_four(M, K, 30 + M)
     plan = plan_for(M, K, r, c, v, N)
@@ -60,7 +61,7 @@ def test_nm_matches_oracle(shape, N):
     check(spmm(plan, B), ref)
 
 
-@pytest.mark.parametrize("N", [32, 128])
+@pytest.mark.parametrize("N", [8, 32, 128])
 def test_nm_thinned_and_empty_rows(N):
     M, K = 300, 1536
     r, c, v = thinned(M, K, 5, empty_rows=(0, 7, 299, 150))
@@ -73,9 +74,10 @@ def test_nm_thinned_and_empty_rows(N):
     assert np.all(C[[0, 7, 150, 299]] == 0)
 
 
-def test_nm_known_answer():
+@pytest.mark.parametrize("N", [8, 128])
+def test_nm_known_answer(N):
     # reference known answer (code_generator.cc:633-637): all-ones A and B => C[i][j] = nnz(row i)
-    M, K, N = 257, 2048, 128
+    M, K = 257, 2048
     r, c, _ = thinned(M, K, 9, keep=0.8)
     plan = plan_for(M, K, r, c, np.ones(len(r), np.float32), N)
     C = spmm(plan, np.ones((K, N), np.float16))
