@@ -70,12 +70,13 @@ def shape_pipeline(shape):
 # per-shape plan candidates for the matrix-core kernels (bench.py searches them for the
 # headline layer): (pipeline, p0, p1, config overrides applied while the plan is uploaded).
 # KS_MIN_ROWS 1000 keeps a block on k_mfma_rows; 56-row blocks of 7168-row shapes are 128
-# row blocks x 2 K ranges on k_mfma_ks
+# row blocks x 2 K ranges on k_mfma_ks; 112-row blocks are exactly 256 workgroups on every
+# OPT-30B shape (7168 rows: 64 blocks x 4 K ranges; fc1: 256 blocks x 1)
 def shape_candidates(shape):
     from .autotune import row_block_rows
     rb = row_block_rows(C5_SHAPES[shape][0])
     return [("tblock_warp_total", rb, 2, {"KS_MIN_ROWS": 1000}), ("block_total", 56, 1, {}),
-            ("block_total", 40, 1, {}), ("block_total", 80, 1, {})]
+            ("block_total", 40, 1, {}), ("block_total", 80, 1, {}), ("block_total", 112, 1, {})]
 
 
 def build_plan(gsa, m, n, row, col, val, N, cand, local):

@@ -2620,8 +2620,7 @@ __global__ __launch_bounds__(256) void k_nm_mfma_ks(const unsigned char *__restr
     const uint32_t c0 = sp * ncs, ncl = min(nch, c0 + ncs) - c0;  // this workgroup's chunks
     const unsigned char *arow = A + (size_t)rg * S * kNmBlockBytes;
     const unsigned char *bbase = reinterpret_cast<const unsigned char *>(B);
-    const uint32_t bk = tid / UB, boff = bk * RBG + (tid % UB) * 16u;  // this thread's first unit
-    const bool bun = tid % UB < UBG;  // the unit exists in HBM (NG = 8: the tile's upper half is zeros)
+    const uint32_t bk = tid / UB, boff = bk * RB + (tid % UB) * 16u;  // this thread's first unit
     auto bdst = [&](uint32_t i) {
         const uint32_t k = bk + i * RPU, s = tid % UB;
         return k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u;
@@ -2888,7 +2887,11 @@ __host__ __device__ constexpr uint32_t merge_path_wave_lds_words(uint32_t S) {
     return (kMpItems * S) / 4u + 2u + (kMpItems * S + 64u) + 2u;
 }
 
-template <class VT, class CT, int CF>
+// STAMPS (diagnostic build only, gs_debug_mfma_timeline on a merge-path plan): lane 0 of
+// every path wave records s_memtime into stamps[w * 16 + slot]: 0 start, 1 first loads
+// issued, per round r < 4: 2 + 3r gathers issued, 3 + 3r rows staged, 4 + 3r walked and
+// scanned; 14 loop done, 15 end (chain arrival)
+template <class VT, class CT, int CF, bool STAMPS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_merge_path(const uint32_t *__restrict__ wz,   // n_waves+1
                                                     const uint32_t *__restrict__ wq,   // n_waves+1
                                                     const uint32_t *__restrict__ ends, // n_crow
@@ -2902,7 +2905,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                                                     uint32_t n_empty, uint32_t fill_blocks,
                                                     const uint32_t *__restrict__ chain,  // 2 n_waves or null
                                                     uint32_t *__restrict__ chain_cnt,    // n_waves, zero between launches
-                                                    uint32_t dbg = 0) {
+                                                    uint32_t dbg = 0, uint64_t *__restrict__ stamps = nullptr) {
     // dbg (diagnostic timing runs only, wrong results): bit 1 gathers B row 0 for every nonzero
     const uint32_t lb = blockIdx.x;  // (XCD-contiguous numbering measured no faster cold on C4)
     if (lb < fill_blocks) {
@@ -2937,7 +2940,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         const bool cok = cw < N;
         const uint32_t c0 = cok ? cw : 0u;
         for (uint32_t w = (lb - fill_blocks) * (blockDim.x >> 6) + wib; w < n_waves; w += waves_total) {
+#define GS_MP_STAMP(slot)                                                                          \
+    if constexpr (STAMPS) {                                                                        \
+        if (lane == 0 && blockIdx.y == 0) stamps[(size_t)w * 16u + (slot)] = __builtin_amdgcn_s_memtime(); \
+    }
+            GS_MP_STAMP(0u);
             const uint32_t zlo = wz[w], wend = wz[w + 1], q0 = wq[w];
+            uint32_t rnd = 0;
             // the wave starts inside row q0 (its partial goes to head_rec)
             const bool head_open = zlo > (q0 ? ends[q0 - 1] : 0u);
             const uint32_t head_first = chain && head_open ? chain[n_waves + w] : 0u;
@@ -2993,6 +3002,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
             const uint32_t zb0 = zlo & ~(kMpItems - 1u);
             load_a(zb0);
             load_s(qs);
+            GS_MP_STAMP(1u);
             for (uint32_t zb = zb0; zb < wend; zb += R8) {
                 const uint32_t zl = max(zb, zlo), ze = min(zb + R8, wend);
                 const uint32_t base = zb + kMpItems * slot;
@@ -3007,6 +3017,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                     const bool valid = z >= zl && z < ze;
                     braw[k] = *reinterpret_cast<const RB *>(B + (size_t)(valid && !(dbg & 2u) ? (uint32_t)cc[k] : 0u) * N + c0);
                 }
+                if (rnd < 4u) GS_MP_STAMP(2u + 3u * rnd);
                 for (uint32_t i = lane; i < fw; i += 64u) wl[i] = 0u;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
@@ -3035,6 +3046,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                     load_a(zb + R8);
                     load_s(qs + nclose);
                 }
+                if (rnd < 4u) GS_MP_STAMP(3u + 3u * rnd);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -3129,8 +3141,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
                 for (int i = 0; i < CF; i++) rc[i] = __shfl(acc[i], (S - 1u) * X + xl, 64);
                 qs += nclose;
+                if (rnd < 4u) GS_MP_STAMP(4u + 3u * rnd);
+                rnd++;
                 __builtin_amdgcn_wave_barrier();
             }
+            GS_MP_STAMP(14u);
             // the row open at the wave's end (if any): its partial joins the row's chain
             if (chain) {
                 if (head_done)  // the slot that closed the head row
@@ -3148,6 +3163,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                     for (int k = 0; k < CF; k++) rec[(size_t)w * N + c0 + k] = rc[k];
                 }
             }
+            GS_MP_STAMP(15u);
+#undef GS_MP_STAMP
         }
     }
 }

@@ -131,10 +131,18 @@ void free_groups(gs_plan *p) {
 
 // replica `replica`'s scratch outputs for dense width N (allocated on first use, grown for a
 // wider N); the row counts are shared
-replica_scratch &ensure_scratch(parent_group &g, int replica, uint32_t N, size_t e) {
+// (the allocation and its synchronous copies are refused under stream capture: run one
+// launch per replica and width before capturing, as for the deferred CSR upload)
+replica_scratch &ensure_scratch(parent_group &g, int replica, uint32_t N, size_t e, hipStream_t stream) {
     if ((size_t)replica >= g.rep.size()) g.rep.resize((size_t)replica + 1);
     replica_scratch &r = g.rep[(size_t)replica];
     if (r.N >= N && g.rows_dev) return r;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    GS_HIP(hipStreamIsCapturing(stream, &cap));
+    if (cap != hipStreamCaptureStatusNone)
+        throw gs::gs_error("sub-matrix scratch outputs of replica " + std::to_string(replica) + " at N=" +
+                               std::to_string(N) + " are allocated on first use: launch once before capturing",
+                           -2);
     GS_HIP(hipSetDevice(g.device));
     free_scratch(r);
     for (size_t i = 0; i < g.subs.size(); i++) {
@@ -169,7 +177,7 @@ void spmm_all(gs_plan *p, int replica, const void *B, void *C, uint32_t N, hipSt
     for (gs::plan_state *s : ks)
         if (s->parent_row_base < 0) gs::launch_spmm(*s, replica, B, C, N, stream);
     for (auto &g : p->groups) {
-        replica_scratch &r = ensure_scratch(g, replica, N, e);
+        replica_scratch &r = ensure_scratch(g, replica, N, e, stream);
         for (size_t i = 0; i < g.subs.size(); i++) {
             gs::memset_rows(r.bufs[i], 0, g.part_rows[i], N, e, stream);
             gs::launch_spmm(*g.subs[i], replica, B, r.bufs[i], N, stream);

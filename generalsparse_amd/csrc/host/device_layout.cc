@@ -244,8 +244,11 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     uint32_t W = kKsWaves;
     uint64_t rmax = 0;
     for (uint64_t g = 0; g < nb; g++) rmax = std::max<uint64_t>(rmax, tb_rows[g + 1] - tb_rows[g]);
-    if (rmax < (uint64_t)std::max<int64_t>(1, min_rows) || rmax > 80) { why = "row blocks outside the k_mfma_ks range"; return false; }
-    const uint32_t RT = std::max<uint32_t>(2, (uint32_t)((rmax + 15) / 16));  // kernels built for RT 2..5
+    if (rmax < (uint64_t)std::max<int64_t>(1, min_rows) || rmax > 128) { why = "row blocks outside the k_mfma_ks range"; return false; }
+    const uint32_t RT = std::max<uint32_t>(2, (uint32_t)((rmax + 15) / 16));  // kernels built for RT 2..8
+    // (RT 6..8 -- 96..128-row blocks: whole CU rounds on the OPT-30B shapes -- for tiles of
+    // at most 32 columns: RT x CT accumulators of 4 VGPRs)
+    if (RT > 5 && CT > 2) { why = "row blocks over 80 rows at N > 32"; return false; }
     if (get_config().KS_WAVES == 16 && gsk::ks_lds_bytes(CT, RT, 16) <= 160 * 1024) W = 16;
     const uint64_t nnz = row_ptr[tb_rows[nb]] - row_ptr[tb_rows[0]];
     if (nnz == 0 || (double)nb * 16 * RT * K > (double)max_fill * nnz) {  // as build_mfma_tiles
@@ -275,10 +278,14 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
         }
     }
     t.GCAP = (uint32_t)gmax;
-    t.MAXG = gmax <= 64 ? 1 : (gmax <= 128 ? 2 : (gmax <= 256 ? 4 : 0));
+    t.MAXG = gmax <= 64 ? 1 : (gmax <= 128 ? 2 : (gmax <= 192 ? 3 : (gmax <= 256 ? 4 : 0)));
     if (!t.MAXG) { why = "a k-step holds more than 256 entry groups"; return false; }
-    GS_CHECK((double)nb * S * t.NS * t.GCAP < 4.0e9, "k_mfma_ks layout exceeds 32-bit group indices");
-    GS_CHECK((double)nb * S * t.NS < 4.0e9, "k_mfma_ks layout exceeds 32-bit step indices");
+    // 32-bit group and step indices (packed steps: about nnz / 8 + nb*S*NS groups; checked
+    // exactly after the build): too large a plan falls back to another kernel
+    if ((double)(row_ptr[tb_rows[nb]] - row_ptr[tb_rows[0]]) / 8.0 + (double)nb * S * t.NS * 2.0 >= 4.0e9) {
+        why = "k_mfma_ks layout exceeds 32-bit group indices";
+        return false;
+    }
     const uint32_t RS = gsk::kKsStride / 2;  // halfwords per image row
     const uint32_t pad_h = 16 * RT * RS;      // the zero row
     t.pos.reserve(row_ptr[tb_rows[nb]] - row_ptr[tb_rows[0]] + (size_t)nb * S * t.NS * 8 + 8);

@@ -44,8 +44,10 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
                       const std::vector<uint64_t> &col, const std::vector<float> &vals, uint64_t K, uint32_t N,
                       size_t lds_budget, int64_t max_fill, mfma_tiles &t, std::string &why);
 
-// k_mfma_ks upload layout: GCAP groups per (BMTB g, K range q, 32-column k-step s) at
-// group ((g*S + q)*NS + s)*GCAP, + one spare group
+// k_mfma_ks upload layout (device_layout.cc build_ks_tiles): the groups of every (BMTB g,
+// K range q, 32-column k-step s) back to back in (unit u = g*S + q, s) order, located by
+// steps[2*(u*NS + s)] = first group and steps[2*(u*NS + s) + 1] = group count (at most
+// GCAP, the plan's largest step: it sets MAXG), + one spare group
 struct ks_tiles {
     uint32_t S = 0, NS = 0, RT = 0, RMAX = 0, MAXG = 0, GCAP = 0, W = 0;
     size_t lds_bytes = 0;

@@ -119,6 +119,8 @@ void combine_parts(const void *const *parts, const uint32_t *rows, uint32_t n, v
 void launch_spmm(plan_state &p, int replica, const void *B, void *C, uint32_t N, hipStream_t stream);
 // uploads the CSR arrays a matrix-core plan deferred (every replica), for a launch at another dense width
 void ensure_csr(plan_state &p);
+void debug_mp_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
+                       size_t n_host);
 void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
                          size_t n_host);
 // mfma_launch.hip: k_mfma_rows / k_nm_mfma (and k_mfma_ks through launch_ks) at the plan's N

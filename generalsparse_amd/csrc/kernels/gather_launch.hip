@@ -22,6 +22,10 @@ namespace {
 
 constexpr int kLdsMaxU = 12;  // 16-B staging registers per thread (k_lds_rows MAXU; device_plan.hip sizes the tiles)
 
+#ifdef GS_EXPERIMENTS
+uint64_t *g_mp_stamps = nullptr;  // set by debug_mp_timeline for one launch (diagnostic build only)
+#endif
+
 // GS_MP_DEBUG (diagnostic timing only): k_merge_path dbg bits
 uint32_t mp_debug() {
 #ifdef GS_EXPERIMENTS
@@ -172,7 +176,15 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
 #else
             GS_CHECK(!d.mp_rows, "k_merge_rows is an experiments-build kernel");
 #endif
-                hipLaunchKernelGGL((gsk::k_merge_path<VT, CT, CF>), dim3(gx + fb, tiles), dim3(256), lds, s, a.a0, a.a1,
+#ifdef GS_EXPERIMENTS
+            if (g_mp_stamps)
+                    hipLaunchKernelGGL((gsk::k_merge_path<VT, CT, CF, true>), dim3(gx + fb, tiles), dim3(256), lds, s, a.a0, a.a1,
+                                   a.a2, a.a3, (uint32_t)d.n_rows_aux, col, val, B, C, a.ws, a.t0, a.ws2, W, N, X, row_base,
+                                   (uint32_t)d.n_out_rows, a.a4, (uint32_t)d.n_fin, fb, fused ? a.t1 : nullptr,
+                                   fused ? a.t2 : nullptr, mp_debug(), g_mp_stamps);
+            else
+#endif
+                    hipLaunchKernelGGL((gsk::k_merge_path<VT, CT, CF>), dim3(gx + fb, tiles), dim3(256), lds, s, a.a0, a.a1,
                                    a.a2, a.a3, (uint32_t)d.n_rows_aux, col, val, B, C, a.ws, a.t0, a.ws2, W, N, X, row_base,
                                    (uint32_t)d.n_out_rows, a.a4, (uint32_t)d.n_fin, fb, fused ? a.t1 : nullptr,
                                    fused ? a.t2 : nullptr, mp_debug());
@@ -227,5 +239,28 @@ void launch_gather(const plan_state &p, const device_arrays &a, const void *B, v
     if (p.dev.dtype == 0) dispatch_vt<float, 4>(p, a, B, C, N, s);
     else dispatch_vt<gsk::f16, 8>(p, a, B, C, N, s);
 }
+
+#ifdef GS_EXPERIMENTS
+// diagnostic: one merge-path launch with s_memtime stamps per path wave (kernel_lib.hpp)
+void debug_mp_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
+                       size_t n_host) {
+    const size_t n = (size_t)p.dev.n_units * 16;
+    uint64_t *dst = nullptr;
+    HIP_OK(hipMalloc(&dst, n * 8));
+    HIP_OK(hipMemsetAsync(dst, 0, n * 8, s));
+    g_mp_stamps = dst;
+    try {
+        launch_gather(p, p.dev.replicas[0], B, C, N, s);
+    } catch (...) {
+        g_mp_stamps = nullptr;
+        (void)hipFree(dst);
+        throw;
+    }
+    g_mp_stamps = nullptr;
+    HIP_OK(hipStreamSynchronize(s));
+    HIP_OK(hipMemcpy(host, dst, std::min(n, n_host) * 8, hipMemcpyDeviceToHost));
+    (void)hipFree(dst);
+}
+#endif
 
 }  // namespace gs

@@ -35,12 +35,18 @@ template <int CT, int RT, int MAXG, bool STAMPS = false, int W = (int)kKsWaves>
 void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s,
                  uint64_t *stamps = nullptr) {
     const device_plan &d = p.dev;
+#ifdef GS_EXPERIMENTS
+    // KS_WAVES = 16 (fixed at upload): every instantiation spills (128 VGPRs at 4 waves per
+    // SIMD; C2 48-98 us against 14-30 us with 8 waves, profiles/r04a), experiments build only
     if constexpr (W == (int)kKsWaves && !STAMPS) {
-        if (d.waves == 16) {  // KS_WAVES = 16, fixed at upload
+        if (d.waves == 16) {
             launch_ks_k<CT, RT, MAXG, false, 16>(p, a, B, C, N, s, stamps);
             return;
         }
     }
+#else
+    GS_CHECK(d.waves == kKsWaves, "k_mfma_ks with 16 waves is an experiments-build variant");
+#endif
     auto kern = gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, STAMPS>;
     // the LDS this instantiation needs at the plan's range width, against what the upload sized
     GS_CHECK(gsk::ks_lds_bytes(CT, RT, W) <= d.lds_bytes, "k_mfma_ks: LDS size disagrees with the upload");
@@ -56,6 +62,7 @@ void launch_ks_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B
     switch (p.dev.seg_cap) {  // MAXG: entry groups per lane per k-step
         case 1: launch_ks_k<CT, RT, 1>(p, a, B, C, N, s); break;
         case 2: launch_ks_k<CT, RT, 2>(p, a, B, C, N, s); break;
+        case 3: launch_ks_k<CT, RT, 3>(p, a, B, C, N, s); break;
         default: launch_ks_k<CT, RT, 4>(p, a, B, C, N, s); break;
     }
 }
@@ -67,7 +74,10 @@ void launch_ks_ct(const plan_state &p, const device_arrays &a, const gsk::f16 *B
         case 3: launch_ks_rt<CT, 3>(p, a, B, C, N, s); break;
         case 4: launch_ks_rt<CT, 4>(p, a, B, C, N, s); break;
         case 5: launch_ks_rt<CT, 5>(p, a, B, C, N, s); break;
-        default: throw gs_error("k_mfma_ks: row tiles outside 2..5");
+        case 6: if constexpr (CT <= 2) { launch_ks_rt<CT, 6>(p, a, B, C, N, s); break; } [[fallthrough]];
+        case 7: if constexpr (CT <= 2) { launch_ks_rt<CT, 7>(p, a, B, C, N, s); break; } [[fallthrough]];
+        case 8: if constexpr (CT <= 2) { launch_ks_rt<CT, 8>(p, a, B, C, N, s); break; } [[fallthrough]];
+        default: throw gs_error("k_mfma_ks: row tiles outside 2..8 (6..8 for N <= 32)");
     }
 }
 

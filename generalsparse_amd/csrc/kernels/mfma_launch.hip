@@ -110,6 +110,10 @@ void debug_mfma_timeline(const plan_state &p, const void *B, void *C, uint32_t N
         debug_bm_timeline(p, B, C, N, s, host, n_host);
         return;
     }
+    if (p.cg && p.cg->get_kernel_spec().family == KF_MERGE_PATH) {
+        debug_mp_timeline(p, B, C, N, s, host, n_host);
+        return;
+    }
     GS_CHECK(p.uploaded && d.mfma && N == d.lds_N && N == 32 && (d.maxr == 2 || d.maxr == 3) &&
                  (d.RSB == 8 || d.RSB == 9),
              "timeline build exists for N=32 matrix-core plans with 17..48-row BMTBs, KC 256/512 only");

@@ -15,11 +15,12 @@ M = K = 5120
 N = int(os.environ.get("SWEEP_N", "32"))
 rows_l = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "40,64,80").split(",")]
 spl_l = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "0,4,8").split(",")]
-wav_l = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "8,16").split(",")]
+wav_l = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "8").split(",")]
+shr_l = [int(x) for x in os.environ.get("SWEEP_SHARE", "32").split(",")]
 row, col, val = ds.pruned_weight(M, K, 0.7, 13)
 for rb in rows_l:
     for ks in spl_l:
-        for w in wav_l:
+        for w, sh in [(w, sh) for w in wav_l for sh in shr_l]:
             gsa.set_config("KS_SPLIT", ks)
             gsa.set_config("KS_WAVES", w)
             try:

@@ -237,6 +237,12 @@ HEADLINE_PLANS = [
     (0.7, "attn", ("tblock_warp_total", 28, 2), "k_mfma_rows", None),
     (0.7, "fc1", ("block_total", 80, 1), "k_mfma_ks", 1),
     (0.7, "fc2", ("block_total", 56, 1), "k_mfma_ks", 2),
+    # 112-row blocks: exactly 256 workgroups on every shape (64 blocks x 4 K ranges; fc1 256 x 1)
+    (0.7, "attn", ("block_total", 112, 1), "k_mfma_ks", 4),
+    (0.7, "fc1", ("block_total", 112, 1), "k_mfma_ks", 1),
+    (0.7, "fc2", ("block_total", 112, 1), "k_mfma_ks", 4),
+    (0.8, "fc1", ("block_total", 112, 1), "k_mfma_ks", 1),
+    (0.8, "fc2", ("block_total", 112, 1), "k_mfma_ks", 4),
 ]
 
 

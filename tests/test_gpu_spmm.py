@@ -389,6 +389,28 @@ def test_mfma_ks_matches_oracle(pipe, N, split, mfma_everywhere):
     assert "k_mfma_ks" in used, used
 
 
+@pytest.mark.parametrize("split", [0, 1, 3])
+@pytest.mark.parametrize("N", [8, 24, 32])
+@pytest.mark.parametrize("rows", [96, 112, 128])
+def test_mfma_ks_tall_blocks_match_oracle(rows, N, split, mfma_everywhere):
+    """96..128-row blocks (RT 6..8: whole CU rounds on the OPT-30B shapes) at N <= 32"""
+    gsa.set_config("KS_SPLIT", split)
+    used = []
+    try:
+        for case, M, K, row, col, val in mfma_cases():
+            plan, C, B = run(M, K, row, col, val, "block_total", rows, 1, N, "f16")
+            info = plan.info()
+            used.append(info["device_kernel"])
+            ref = ofi.spmm_ref(M, N, row, col, val.astype(np.float16).astype(np.float32), B.astype(np.float32), "f64")
+            check(C, ref, "f16")
+            if info["device_kernel"] == "k_mfma_ks":
+                np.testing.assert_array_equal(plan.spmm(torch.from_numpy(B).to(DEV)).float().cpu().numpy(), C)
+            plan.free()
+    finally:
+        gsa.set_config("KS_SPLIT", 0)
+    assert "k_mfma_ks" in used, used
+
+
 def test_mfma_ks_known_answer_and_c2():
     """all-ones known answer bit-exactly, and the C2 shape (80-row blocks, 4 K ranges) against
     a torch fp32 dense product of the same fp16 inputs"""
@@ -718,6 +740,7 @@ def test_mfma_rows_counter_handoffs(pipe, N, mfma_everywhere):
 def test_mfma_ks_16_waves(pipe, N, mfma_everywhere):
     """k_mfma_ks with KS_WAVES=16 (twice the waves per workgroup where their stages fit LDS):
     oracle parity, determinism of the K-range combine"""
+    need_experiments()
     name, p0, p1 = pipe
     gsa.set_config("KS_WAVES", 16)
     try:
