@@ -58,6 +58,9 @@ def parse():
                     help="interleaved timing rounds per candidate plan (the median decides)")
     ap.add_argument("--n-sweep", default="", help="also time the chosen plan family at these dense widths, e.g. 8,32,128")
     ap.add_argument("--layers", type=int, default=48, help="c5: OPT-30B layers in the batch")
+    ap.add_argument("--group", type=int, default=1,
+                    help="c5/c5h: 1 = the batch through gs_spmm_batch (grouped k_mfma_ks launches), 0 = one launch "
+                         "per matrix over --streams streams")
     ap.add_argument("--streams", type=int, default=2,
                     help="c5/c5h: HIP streams the batch's launches rotate over (2: one launch's tail overlaps the "
                          "next one's start; profiles/r03_c5_streams.json)")
@@ -313,7 +316,7 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
                                       bt.C5_SPARSITY, rocsparse=False)
     plans, launches, _ = bt.build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, choice=choice)
     t_setup = time.perf_counter() - t0
-    step, streams = batch_step(launches, N, torch, args.streams)
+    step, streams = batch_step(launches, N, torch, args.streams, group=bool(args.group))
 
     for _ in range(args.warmup):
         step()
@@ -359,7 +362,7 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
                    "plan": {k: per_shape[k]["plan"] for k in plans},
                    "kernel": {k: kernel_label(plans[k].info()) for k in plans},
                    "parallelism": f"LPT batch split x{world} (max rank nnz share {max(load) / total_nnz:.4f})",
-                   "streams": args.streams},
+                   "streams": args.streams, "grouped_launches": bool(args.group)},
         "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9 / world, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / world / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "algorithmic_bytes_per_step": alg, "note": "per GPU, whole step"},
@@ -393,12 +396,28 @@ def timed_batch(step, streams, steps, torch):
     return time.perf_counter() - t0, e0.elapsed_time(e1) * 1e-3
 
 
-def batch_step(launches, N, torch, n_streams):
-    """one pass over a batch of independent SpMMs: launch i on stream i % n_streams (the
-    current stream first), so one launch's tail overlaps the next one's start; with more
-    than one stream every launch writes its own C.  Returns (step, streams)."""
+def batch_step(launches, N, torch, n_streams, group=False):
+    """one pass over a batch of independent SpMMs.  group: the batch through gs_spmm_batch
+    (consecutive K-split entries of one instantiation are one grouped launch; entries sorted
+    by shape so runs are long, then dealt over the streams), every launch with its own C.  Otherwise launch i on stream i % n_streams (the current stream first), so
+    one launch's tail overlaps the next one's start; with more than one stream every launch
+    writes its own C.  Returns (step, streams)."""
+    import generalsparse_amd as gsa
     cur = torch.cuda.current_stream()
     streams = [cur] + [torch.cuda.Stream() for _ in range(max(1, n_streams) - 1)]
+    if group:
+        # sorted by shape, then dealt over the streams: each stream's share is one batch of
+        # long same-shape runs, and the streams' grouped launches overlap each other's tails
+        ents = [(p, r, b, torch.empty_like(c), k) for (p, r, b, c, k) in sorted(launches, key=lambda x: x[4])]
+        bats = [(gsa.Batch([(p, r, b, c) for (p, r, b, c, _) in ents[i::len(streams)]], N), st.cuda_stream)
+                for i, st in enumerate(streams) if ents[i::len(streams)]]
+
+        def gstep():
+            for bat, s in bats:
+                bat.run(s)
+
+        gstep.keep = ents  # the C buffers live as long as the step
+        return gstep, streams
     raw = []
     for i, (p, r, b, c, _) in enumerate(launches):
         if n_streams > 1:
@@ -479,7 +498,7 @@ def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
     # the timed layer: 4 x attn (replicas 0..3), fc1, fc2
     seq = [(0, s, bt.C5_SLOTS[s], bt.C5_SLOTS[:s].count(bt.C5_SLOTS[s])) for s in range(len(bt.C5_SLOTS))]
     plans, launches, _ = bt.build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, sparsity=sp, choice=choice)
-    step, streams = batch_step(launches, N, torch, args.streams)
+    step, streams = batch_step(launches, N, torch, args.streams, group=bool(args.group))
 
     for _ in range(args.warmup):
         step()
@@ -526,7 +545,7 @@ def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
         "config": {"workload": f"OPT-30B decoder layer: 4 x 7168^2, 28672x7168, 7168x28672, {round(sp * 100)}% "
                                f"unstructured, fp16, N={N}", "nnz": nnz_l,
                    "plan": {k: per_shape[k]["plan"] for k in per_shape}, "kernel": {k: per_shape[k]["kernel"] for k in per_shape},
-                   "parallelism": "one GPU", "streams": args.streams},
+                   "parallelism": "one GPU", "streams": args.streams, "grouped_launches": bool(args.group)},
         "roofline": {"bound": "hbm", "achieved": round(alg_l / (ms_step * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg_l / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "algorithmic_bytes_per_step": alg_l,

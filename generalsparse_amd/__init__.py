@@ -22,7 +22,7 @@ import numpy as np
 from . import _lib
 from ._lib import GS_F16, GS_F32, GsError
 
-__all__ = ["Plan", "set_config", "GsError", "GS_F16", "GS_F32", "PIPELINES", "load_library"]
+__all__ = ["Plan", "Batch", "set_config", "GsError", "GS_F16", "GS_F32", "PIPELINES", "load_library"]
 
 # token_test.cc pipelines (+ the two compositions this engine adds)
 PIPELINES = ("thread_total", "warp_total", "block_total", "thread_bit_map", "warp_segment",
@@ -76,6 +76,25 @@ def index_compression_of_array(a, type_ori=16, branch_max=5):
     p = {"coef": int(prm[0]), "intercept": int(prm[1]), "cycle": int(prm[2]),
          "aa": int(prm[3].astype(np.int64)), "bb": int(prm[4].astype(np.int64))}
     return kind.value.decode(), p, bool(ex.value)
+
+
+class Batch:
+    """a fixed list of SpMMs (plan, replica, B, C) run by gs_spmm_batch: consecutive K-split
+    matrix-core entries of one instantiation are one grouped launch (k_mfma_ks_group).  The
+    argument arrays are built once; run() enqueues the whole batch on a stream."""
+
+    def __init__(self, entries, N):
+        self._L = _lib.load()
+        n = len(entries)
+        self.plans = [e[0] for e in entries]  # keeps the plans alive
+        self._p = (ctypes.c_void_p * n)(*[e[0]._h for e in entries])
+        self._r = (ctypes.c_int * n)(*[int(e[1]) for e in entries])
+        self._b = (ctypes.c_void_p * n)(*[e[2] if isinstance(e[2], int) else e[2].data_ptr() for e in entries])
+        self._c = (ctypes.c_void_p * n)(*[e[3] if isinstance(e[3], int) else e[3].data_ptr() for e in entries])
+        self.n, self.N = n, int(N)
+
+    def run(self, stream=0):
+        _lib.check(self._L.gs_spmm_batch(self._p, self._r, self._b, self._c, self.n, self.N, ctypes.c_void_p(stream)))
 
 
 class Plan:

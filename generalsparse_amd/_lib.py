@@ -64,6 +64,8 @@ SIGNATURES = {
     "gs_spmm": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
     "gs_spmm_replica": ([ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                          ctypes.c_void_p], ctypes.c_int),
+    "gs_spmm_batch": ([ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_void_p),
+                       ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
     "gs_spmm_rotate": ([ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                         ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
     "gs_plan_info_get": ([ctypes.c_void_p, ctypes.POINTER(GsPlanInfo)], ctypes.c_int),

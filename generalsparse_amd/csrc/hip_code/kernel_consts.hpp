@@ -19,6 +19,9 @@ constexpr int kMfmaWaves = 16, kMfmaCompute = 6, kMfmaBWaves = 4, kMfmaAWaves = 
 // GLDS = g > 0: g waves issue the B rows (LDS-DMA), the other 10 - g load and scatter entries
 constexpr int kMfmaBWavesG = 2, kMfmaAWavesG = 8;
 
+// k_mfma_ks_group: entries of one grouped launch (kernel arguments, ~3.2 KB of the 4 KB)
+constexpr int kKsGroupMax = 32;
+
 // k_mfma_ks: wave image row stride (conflict-free ds_read_b128 fragment reads)
 constexpr uint32_t kKsStride = 96;
 

@@ -1565,15 +1565,14 @@ __device__ constexpr int vmcnt_imm() {
 // STAMPS (diagnostic build only, gs_debug_mfma_timeline): lane 0 of every wave records
 // s_memtime into stamps[(workgroup * W + wave) * 32 + slot]: 0 start, 1 loads issued,
 // 3 + i after step i (i < 16), 20 loop done, 21 reduced, 22 end
-template <int CT, int RT, int W, int D, int MAXG, bool STAMPS = false>
-__global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__ bmtb_first_row,  // nb+1
-                                                    const u32x4 *__restrict__ tP,  // 8 x u16 position per group
-                                                    const u32x4 *__restrict__ tV,  // 8 x f16 value per group
-                                                    const u32x2 *__restrict__ steps,  // per (unit, k-step): first group, count
-                                                    const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K,
-                                                    uint32_t N, uint32_t S, uint32_t NS, uint32_t nwg,
-                                                    uint32_t row_base, float *__restrict__ slabs,
-                                                    uint32_t *__restrict__ arrivals, uint64_t *__restrict__ stamps = nullptr) {
+// the body of k_mfma_ks for workgroup bx of a launch of nwg workgroups (k_mfma_ks: the
+// whole grid; k_mfma_ks_group: one entry's share of it)
+template <int CT, int RT, int W, int D, int MAXG, bool STAMPS>
+__device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_row, const u32x4 *__restrict__ tP,
+                                        const u32x4 *__restrict__ tV, const u32x2 *__restrict__ steps,
+                                        const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K, uint32_t N, uint32_t S,
+                                        uint32_t NS, uint32_t nwg, uint32_t row_base, float *__restrict__ slabs,
+                                        uint32_t *__restrict__ arrivals, uint64_t *__restrict__ stamps, uint32_t bx) {
     constexpr uint32_t RB = 32 * CT;  // bytes per LDS B row (a 16*CT-column tile)
     constexpr uint32_t UB = 2 * CT;   // 16-B units per B row
     constexpr uint32_t IMG = ks_image_bytes<RT>();
@@ -1581,7 +1580,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t u = xcd_block(blockIdx.x, nwg);  // nwg == gridDim.x (an argument: kernarg preload)
+    const uint32_t u = xcd_block(bx, nwg);
     const uint32_t g = u / S, q = u - g * S;
 #define GS_KS_STAMP(slot)                                                                          \
     if constexpr (STAMPS) {                                                                        \
@@ -1869,6 +1868,58 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
     }
     GS_KS_STAMP(22u);
 #undef GS_KS_STAMP
+}
+
+template <int CT, int RT, int W, int D, int MAXG, bool STAMPS = false>
+__global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__ bmtb_first_row,  // nb+1
+                                                    const u32x4 *__restrict__ tP,  // 8 x u16 position per group
+                                                    const u32x4 *__restrict__ tV,  // 8 x f16 value per group
+                                                    const u32x2 *__restrict__ steps,  // per (unit, k-step): first group, count
+                                                    const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K,
+                                                    uint32_t N, uint32_t S, uint32_t NS, uint32_t nwg,
+                                                    uint32_t row_base, float *__restrict__ slabs,
+                                                    uint32_t *__restrict__ arrivals, uint64_t *__restrict__ stamps = nullptr) {
+    // nwg == gridDim.x (an argument: kernarg preload)
+    ks_body<CT, RT, W, D, MAXG, STAMPS>(bmtb_first_row, tP, tV, steps, B, C, K, N, S, NS, nwg, row_base, slabs, arrivals,
+                                        stamps, blockIdx.x);
+}
+
+// ---------------------------------------------------------------------------
+// k_mfma_ks_group -- several k_mfma_ks launches of one instantiation as one grid (a layer's
+// or a batch's SpMMs; gs_spmm_batch): entry i owns workgroups [begin[i], begin[i+1]) and runs
+// them as its own launch would.  One launch instead of one per matrix: no kernel boundary
+// between the matrices, and one matrix's last workgroups overlap the next one's first.  The
+// entries are kernel arguments (ks_group_args, read through the kernarg segment with scalar
+// loads); every entry has its own plan replica (distinct K-range tickets and slabs).
+// ---------------------------------------------------------------------------
+struct ks_entry {  // 96 B
+    const uint32_t *tbr;
+    const u32x4 *tP, *tV;
+    const u32x2 *steps;
+    const f16 *B;
+    f16 *C;
+    float *slabs;
+    uint32_t *arrivals;
+    uint32_t K, S, NS, nwg, row_base, pad0, pad1, pad2;
+};
+// kKsGroupMax: kernel_consts.hpp
+struct ks_group_args {
+    uint32_t begin[kKsGroupMax + 1];  // first workgroup of each entry (+ the total)
+    uint32_t n, N, pad[2];
+    ks_entry e[kKsGroupMax];
+};
+
+template <int CT, int RT, int W, int D, int MAXG>
+__global__ __launch_bounds__(64 * W) void k_mfma_ks_group(ks_group_args args) {
+    const uint32_t bx = blockIdx.x, n = args.n;
+    uint32_t sel = 0;
+#pragma unroll
+    for (int i = 1; i < kKsGroupMax; i++)
+        if ((uint32_t)i < n && args.begin[i] <= bx) sel = (uint32_t)i;
+    sel = __builtin_amdgcn_readfirstlane(sel);
+    const ks_entry &e = args.e[sel];  // kernel arguments: scalar loads at a computed offset
+    ks_body<CT, RT, W, D, MAXG, false>(e.tbr, e.tP, e.tV, e.steps, e.B, e.C, e.K, args.N, e.S, e.NS, e.nwg, e.row_base,
+                                       e.slabs, e.arrivals, nullptr, bx - args.begin[sel]);
 }
 
 #ifdef GS_EXPERIMENTS  // opt-in, measured slower than k_mfma_rows / k_mfma_ks (make EXPERIMENTS=1)

@@ -776,6 +776,42 @@ int gs_spmm_rotate(gs_plan_t *p, int count, int first, const void *const *B_ptrs
     });
 }
 
+int gs_spmm_batch(gs_plan_t *const *plans, const int *replicas, const void *const *B, void *const *C, int n, int N,
+                  gs_stream_t stream) {
+    return guard([&] {
+        GS_CHECK(plans && replicas && B && C && n >= 0 && N > 0, "bad argument");
+        hipStream_t s = (hipStream_t)stream;
+        std::vector<gs::ks_group_item> grp;
+        uint32_t key = 0;
+        auto flush = [&] {
+            if (grp.size() == 1)
+                gs::launch_spmm(*const_cast<gs::plan_state *>(grp[0].p), grp[0].replica, grp[0].B, grp[0].C, (uint32_t)N, s);
+            else if (!grp.empty())
+                gs::launch_ks_group(grp, (uint32_t)N, s);
+            grp.clear();
+            key = 0;
+        };
+        for (int i = 0; i < n; i++) {
+            gs_plan *p = plans[i];
+            GS_CHECK(p && B[i] && C[i], "bad batch entry " + std::to_string(i));
+            GS_CHECK(replicas[i] >= 0 && (size_t)replicas[i] < p->st.dev.replicas.size(),
+                     "batch entry " + std::to_string(i) + ": bad replica index");
+            const uint32_t k = divided(p) ? 0u : gs::ks_group_key(p->st, (uint32_t)N);
+            if (k == 0) {
+                flush();
+                spmm_all(p, replicas[i], B[i], C[i], (uint32_t)N, s);
+                continue;
+            }
+            bool dup = false;  // a (plan, replica) twice in one grid would share tickets and slabs
+            for (const auto &x : grp) dup |= x.p == &p->st && x.replica == replicas[i];
+            if (k != key || grp.size() == (size_t)gsk::kKsGroupMax || dup) flush();
+            key = k;
+            grp.push_back({&p->st, replicas[i], B[i], C[i]});
+        }
+        flush();
+    });
+}
+
 int gs_spmm(gs_plan_t *p, const void *B, void *C, int N, gs_stream_t stream) {
     return gs_spmm_replica(p, 0, B, C, N, stream);
 }

@@ -130,6 +130,16 @@ void launch_nm(const plan_state &p, const device_arrays &a, const void *B, void 
 void launch_gather(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s);
 // ks_launch.hip: k_mfma_ks (K-split, wave-autonomous matrix-core row blocks)
 void launch_ks(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s);
+// grouped k_mfma_ks launches (gs_spmm_batch): one grid over up to 32 entries of one
+// instantiation (equal nonzero ks_group_key); every entry a distinct (plan, replica)
+struct ks_group_item {
+    const plan_state *p;
+    int replica;
+    const void *B;
+    void *C;
+};
+uint32_t ks_group_key(const plan_state &p, uint32_t N);  // 0: not groupable
+void launch_ks_group(const std::vector<ks_group_item> &it, uint32_t N, hipStream_t s);
 void launch_bm(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s);
 void debug_bm_timeline(const plan_state &p, const void *B, void *C, uint32_t N, hipStream_t s, uint64_t *host,
                        size_t n_host);

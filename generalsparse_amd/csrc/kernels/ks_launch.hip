@@ -4,6 +4,7 @@
 #include "../hip_code/kernel_lib.hpp"
 #include "../host/gs_plan.hpp"
 
+#include <cstring>
 #include <map>
 #include <mutex>
 
@@ -150,6 +151,81 @@ void launch_bm(const plan_state &, const device_arrays &, const void *, void *, 
     throw gs_error("k_mfma_bm is an experiments-build kernel (make -C generalsparse_amd/csrc exp)", -2);
 }
 #endif
+
+// ---- grouped launches (gs_spmm_batch): N = 32 (CT = 2), 8 waves, one instantiation per group
+namespace {
+template <int RT, int MAXG>
+void launch_ks_group_k(const std::vector<ks_group_item> &it, uint32_t N, hipStream_t s) {
+    auto kern = gsk::k_mfma_ks_group<2, RT, (int)kKsWaves, (int)kKsDepth, MAXG>;
+    GS_CHECK(!it.empty() && it.size() <= (size_t)gsk::kKsGroupMax, "k_mfma_ks_group: 1..32 entries");
+    gsk::ks_group_args args;
+    std::memset(&args, 0, sizeof(args));
+    size_t lds = 0;
+    uint32_t wg = 0;
+    for (size_t i = 0; i < it.size(); i++) {
+        const plan_state &p = *it[i].p;
+        const device_plan &d = p.dev;
+        const device_arrays &a = d.replicas[(size_t)it[i].replica];
+        GS_CHECK(gsk::ks_lds_bytes(2, RT, kKsWaves) <= d.lds_bytes, "k_mfma_ks_group: LDS size disagrees with the upload");
+        lds = std::max(lds, d.lds_bytes);
+        gsk::ks_entry &e = args.e[i];
+        e.tbr = a.t0;
+        e.tP = (const gsk::u32x4 *)a.tcol;
+        e.tV = (const gsk::u32x4 *)a.tval;
+        e.steps = (const gsk::u32x2 *)a.t1;
+        e.B = (const gsk::f16 *)it[i].B;
+        e.C = (gsk::f16 *)it[i].C;
+        e.slabs = a.ws;
+        e.arrivals = a.t2;
+        e.K = (uint32_t)p.K;
+        e.S = d.ksplit;
+        e.NS = d.ks_ns;
+        e.nwg = (uint32_t)d.n_rows_aux * d.ksplit;
+        e.row_base = (uint32_t)d.row_base;
+        args.begin[i] = wg;
+        wg += e.nwg;
+    }
+    args.begin[it.size()] = wg;
+    args.n = (uint32_t)it.size();
+    args.N = N;
+    grant_lds(it[0].p->dev.device, kern, lds);
+    hipLaunchKernelGGL(kern, dim3(wg, ks_col_tiles(N)), dim3(64 * kKsWaves), lds, s, args);
+    HIP_OK(hipGetLastError());
+}
+
+template <int RT>
+void launch_ks_group_rt(const std::vector<ks_group_item> &it, uint32_t N, hipStream_t s) {
+    switch (it[0].p->dev.seg_cap) {
+        case 1: launch_ks_group_k<RT, 1>(it, N, s); break;
+        case 2: launch_ks_group_k<RT, 2>(it, N, s); break;
+        case 3: launch_ks_group_k<RT, 3>(it, N, s); break;
+        default: launch_ks_group_k<RT, 4>(it, N, s); break;
+    }
+}
+}  // namespace
+
+uint32_t ks_group_key(const plan_state &p, uint32_t N) {
+    const device_plan &d = p.dev;
+    if (!p.uploaded || !d.mfma || !d.ks || d.pad_rows || N != 32 || d.lds_N != 32 || d.waves != kKsWaves) return 0;
+    return (d.maxr << 8) | d.seg_cap;  // RT, MAXG: one instantiation
+}
+
+void launch_ks_group(const std::vector<ks_group_item> &it, uint32_t N, hipStream_t s) {
+    GS_CHECK(!it.empty(), "empty group");
+    const uint32_t key = ks_group_key(*it[0].p, N);
+    GS_CHECK(key != 0, "k_mfma_ks_group: not a groupable k_mfma_ks plan");
+    for (const auto &x : it) GS_CHECK(ks_group_key(*x.p, N) == key, "k_mfma_ks_group: entries of different instantiations");
+    switch (it[0].p->dev.maxr) {
+        case 2: launch_ks_group_rt<2>(it, N, s); break;
+        case 3: launch_ks_group_rt<3>(it, N, s); break;
+        case 4: launch_ks_group_rt<4>(it, N, s); break;
+        case 5: launch_ks_group_rt<5>(it, N, s); break;
+        case 6: launch_ks_group_rt<6>(it, N, s); break;
+        case 7: launch_ks_group_rt<7>(it, N, s); break;
+        case 8: launch_ks_group_rt<8>(it, N, s); break;
+        default: throw gs_error("k_mfma_ks_group: row tiles outside 2..8");
+    }
+}
 
 void launch_ks(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
     const gsk::f16 *b = (const gsk::f16 *)B;

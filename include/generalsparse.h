@@ -112,6 +112,14 @@ int gs_spmm_replica(gs_plan_t *p, int replica, const void *B, void *C, int N, gs
  * (bench rotation without a host round trip per launch) */
 int gs_spmm_rotate(gs_plan_t *p, int count, int first, const void *const *B_ptrs, void *const *C_ptrs, int n_ptrs,
                    int N, gs_stream_t stream);
+/* n SpMMs (plans[i], replicas[i], B[i], C[i]) enqueued on `stream` in order: a batch of
+ * independent matrices (a layer's weights).  Replaces the reference's one launch per
+ * sub-matrix in its multi-kernel executor (operator_executer.hpp:62-76, executor.cc:6-104):
+ * consecutive entries whose plans run the K-split matrix-core kernel at N = 32 with one
+ * instantiation (up to 32 of them, each a distinct (plan, replica)) are ONE grouped launch
+ * (k_mfma_ks_group); the others launch as gs_spmm_replica does. */
+int gs_spmm_batch(gs_plan_t *const *plans, const int *replicas, const void *const *B, void *const *C, int n, int N,
+                  gs_stream_t stream);
 
 int gs_plan_info_get(gs_plan_t *p, gs_plan_info *info);
 int gs_plan_array_count(gs_plan_t *p);

@@ -758,3 +758,36 @@ def test_mfma_ks_16_waves(pipe, N, mfma_everywhere):
             assert 16 in waves, waves
     finally:
         gsa.set_config("KS_WAVES", 8)
+
+
+def test_batch_grouped_launch_matches_single_launches():
+    """gs_spmm_batch: consecutive K-split entries of one instantiation run as one grouped
+    launch (k_mfma_ks_group); every C equals its single launch bit for bit, across group
+    boundaries (another kernel family in between, a (plan, replica) repeated, more than 32
+    entries)"""
+    N = 32
+    mats = [ds.pruned_weight(700, 3000, 0.7, 41), ds.pruned_weight(700, 3000, 0.7, 42)]
+    plans = []
+    for r, c, v in mats:
+        p = gsa.Plan.from_coo(700, 3000, r, c, v).run_pipeline("block_total", N, 80, 1).compile().upload("f16", 0)
+        assert p.info()["device_kernel"] == "k_mfma_ks", p.info()
+        for _ in range(35):
+            p.add_replica()
+        plans.append(p)
+    r, c, v = ds.random_rows(500, 3000, 20.0, seed=43)
+    pg = gsa.Plan.from_coo(500, 3000, r, c, v).run_pipeline("warp_segment", N, 4, 1).compile().upload("f16", 0)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(11)
+    Bs = [(torch.rand((3000, N), device=DEV, generator=g) * 2 - 1).half() for _ in range(3)]
+    entries = [(plans[0], 0, Bs[0]), (plans[0], 1, Bs[1]), (plans[1], 0, Bs[2]), (pg, 0, Bs[0]), (plans[1], 1, Bs[0]),
+               (plans[0], 1, Bs[2]), (plans[1], 2, Bs[1])]
+    entries += [(plans[k % 2], 3 + k // 2, Bs[k % 3]) for k in range(40)]
+    Cs = [torch.full((p.info()["rows"], N), float("nan"), device=DEV, dtype=torch.float16) for (p, _, _) in entries]
+    gsa.Batch([(p, rep, b, cc) for (p, rep, b), cc in zip(entries, Cs)], N).run(torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for (p, rep, b), cc in zip(entries, Cs):
+        ref = p.spmm(b, replica=rep)
+        torch.cuda.synchronize()
+        assert torch.equal(cc, ref), (rep,)
+    for p in plans + [pg]:
+        p.free()
