@@ -58,12 +58,14 @@ def parse():
                     help="interleaved timing rounds per candidate plan (the median decides)")
     ap.add_argument("--n-sweep", default="", help="also time the chosen plan family at these dense widths, e.g. 8,32,128")
     ap.add_argument("--layers", type=int, default=48, help="c5: OPT-30B layers in the batch")
-    ap.add_argument("--group", type=int, default=1,
-                    help="c5/c5h: 1 = the batch through gs_spmm_batch (grouped k_mfma_ks launches), 0 = one launch "
-                         "per matrix over --streams streams")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--group", type=int, default=-1,
+                    help="c5/c5h: 1 = the batch through gs_spmm_batch (grouped k_mfma_ks launches, dealt over "
+                         "--streams), 0 = one launch per matrix over --streams streams; -1 = the measured best: "
+                         "c5h grouped on one stream (57.2 vs 54.9 TFLOP/s), c5 per matrix over two streams (61.7 vs "
+                         "58.7-60.0; profiles/r04g_*)")
+    ap.add_argument("--streams", type=int, default=-1,
                     help="c5/c5h: HIP streams the batch's launches rotate over (2: one launch's tail overlaps the "
-                         "next one's start; profiles/r03_c5_streams.json)")
+                         "next one's start; profiles/r03_c5_streams.json); -1 = as --group -1 picks")
     ap.add_argument("--shard", choices=("batch", "rows", "nnz"), default="batch",
                     help="c4/c4o with N>1: batch = a matrix per rank (weak); rows / nnz = one matrix split "
                          "over the ranks (strong; nnz splits rows and combines them with one all-reduce)")
@@ -79,6 +81,10 @@ def parse():
 def resolve_workload(a, world):
     if a.workload is None:
         a.workload = "c5" if world > 1 else "c2"
+    if a.group < 0:
+        a.group = 1 if a.workload == "c5h" else 0
+    if a.streams < 0:
+        a.streams = 1 if a.workload == "c5h" else 2
     dflt = {"c1": (47894, 41550, 8), "c2": (5120, 5120, 32), "c3": (28672, 7168, 128), "c4": (1000005, 1000005, 8),
             "c4o": (3072441, 3072441, 8), "c5": (7168, 7168, 32), "c5h": (7168, 7168, 32)}[a.workload]
     a.M, a.K, a.N = a.M or dflt[0], a.K or dflt[1], a.N or dflt[2]
@@ -139,6 +145,9 @@ CANDIDATES_C1 = [("thread_total", 4, 1), ("tblock_warp_total", 4, 1), ("tblock_w
 # C4: merge-path levels (WARP, work_size p0) and the balanced / row-per-thread plans
 CANDIDATES_C4 = [("merge_path", 256, 1), ("merge_path", 512, 1), ("merge_path", 1024, 1), ("balanced_block_total", 2048, 1),
                  ("thread_total", 4, 1)]
+# com-Orkut stand-in (234M nonzeros): the merge-path levels only (each plan of it is ~2 GB on the
+# device and minutes of host work; the balanced / row-per-thread plans are 4x-30x slower on C4)
+CANDIDATES_C4O = [("merge_path", 512, 1), ("merge_path", 1024, 1)]
 
 
 def kernel_label(info):
@@ -344,7 +353,7 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
     if os.path.exists(tf) and args.layers == 48:
         try:
             tj = json.load(open(tf))
-            if kinds == {tj.get("kernel")}:  # measured on the same kernels
+            if "+".join(sorted(kinds)) == tj.get("kernel"):  # measured on the same kernels
                 traffic = int(tj["hbm_bytes_per_step"] / world)
         except Exception:
             traffic = None
@@ -656,10 +665,14 @@ def main():
         cand_list = CANDIDATES_C1
     elif args.workload in ("c4", "c4o"):
         one = args.shard != "batch"
-        row, col, val = ds.rmat(M, wl["nnz"], wl["seed"] + (0 if one else rank), symmetric=wl["symmetric"])
+        if args.workload == "c4o":  # 234M nonzeros: drawn on the GPU (numpy takes minutes)
+            row, col, val = ds.rmat_torch(M, wl["nnz"], wl["seed"] + (0 if one else rank), dev, symmetric=True)
+            cand_list = CANDIDATES_C4O
+        else:
+            row, col, val = ds.rmat(M, wl["nnz"], wl["seed"] + (0 if one else rank), symmetric=wl["symmetric"])
+            cand_list = CANDIDATES_C4
         nnz = len(row)
         alg_bytes = algorithmic_bytes(M, K, N, nnz, e, s_idx)
-        cand_list = CANDIDATES_C4
         if one:  # one matrix over the ranks: this rank's rows / nonzeros
             from generalsparse_amd import shard as sd
             full_flops = 2.0 * nnz * N

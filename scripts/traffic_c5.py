@@ -1,6 +1,6 @@
 """HBM bytes of one C5 batch step from the FETCH_SIZE / WRITE_SIZE passes over a
 --layers L run of bench.py --workload c5 (W warm-up + K timed steps): the k_mfma_rows
-dispatches of the run summed, divided by the steps run (W + K) and by L, times the
+(gsk::) dispatches of the run summed, divided by the steps run (W + K) and by L, times the
 48 layers of the batch.  FETCH_SIZE x2 on gfx950 (MI355X_MICROARCH.md §HBM), KiB -> bytes.
 usage: traffic_c5.py <pmc root> <layers> <steps run> <out json>"""
 import csv
@@ -14,19 +14,21 @@ from generalsparse_amd import batch as bt  # noqa: E402
 
 root, layers, steps, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
 tot = {}
+kinds = set()
 for name in ("FETCH_SIZE", "WRITE_SIZE"):
     per = {}
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] == name and "k_mfma_rows" in r["Kernel_Name"]:
+            if r["Counter_Name"] == name and "gsk" in r["Kernel_Name"]:
                 per[(f, r["Dispatch_Id"])] = per.get((f, r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
+                kinds.add(r["Kernel_Name"].split("<")[0].split("::")[-1].split("(")[0].strip())
     tot[name] = (sum(per.values()), len(per))
 layer_read = tot["FETCH_SIZE"][0] * 1024 * 2 / steps / layers
 layer_write = tot["WRITE_SIZE"][0] * 1024 / steps / layers
 e, N = 2, 32
 alg_layer = sum(bt.nnz_of_shape(k) * (e + 2) + (bt.C5_SHAPES[k][0] + 1) * 4 + bt.C5_SHAPES[k][1] * N * e +
                 bt.C5_SHAPES[k][0] * N * e for k in bt.C5_SLOTS)
-res = {"kernel": "k_mfma_rows", "layers_profiled": layers, "steps_profiled": steps,
+res = {"kernel": "+".join(sorted(kinds)), "layers_profiled": layers, "steps_profiled": steps,
        "dispatches": {"FETCH_SIZE": tot["FETCH_SIZE"][1], "WRITE_SIZE": tot["WRITE_SIZE"][1]},
        "hbm_read_bytes_per_layer": int(layer_read), "hbm_write_bytes_per_layer": int(layer_write),
        "hbm_bytes_per_step": int((layer_read + layer_write) * 48), "algorithmic_bytes_per_step": alg_layer * 48,
