@@ -138,7 +138,7 @@ def test_col_direction_matches_oracle(pipe, N, dtype):
         assert plan.info()["kernel_name"].startswith("k_row_chunks"), plan.info()["kernel_name"]
         # 2:4 rows of an fp16 plan at N = 32/64/128 run on the sparse matrix cores
         # (tests/test_gpu_nm.py); everything else on the row-chunk kernel
-        nm = case == "2:4" and dtype == "f16" and N in (32, 64, 128) and "interleaved" not in name
+        nm = case == "2:4" and dtype == "f16" and N in (8, 16, 32, 64, 128) and "interleaved" not in name
         assert plan.info()["lds_stage"] == (3 if nm else 0), (case, plan.info())
         v = val.astype(np.float16).astype(np.float32) if dtype == "f16" else val
         ref = ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64")
