@@ -1572,7 +1572,8 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
                                         const u32x4 *__restrict__ tV, const u32x2 *__restrict__ steps,
                                         const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K, uint32_t N, uint32_t S,
                                         uint32_t NS, uint32_t nwg, uint32_t row_base, float *__restrict__ slabs,
-                                        uint32_t *__restrict__ arrivals, uint64_t *__restrict__ stamps, uint32_t bx) {
+                                        uint32_t *__restrict__ arrivals, uint64_t *__restrict__ stamps, uint32_t bx,
+                                        uint32_t prio) {
     constexpr uint32_t RB = 32 * CT;  // bytes per LDS B row (a 16*CT-column tile)
     constexpr uint32_t UB = 2 * CT;   // 16-B units per B row
     constexpr uint32_t IMG = ks_image_bytes<RT>();
@@ -1724,10 +1725,17 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
             if (i < 16u) GS_KS_STAMP(3u + i);
         }
     };
+    // prio (KS_PRIO): the younger half of the waves (the second wave of each SIMD, the one
+    // that loses issue arbitration) at s_setprio 1 -- 1: for its whole loop, 2: for the
+    // first half of its steps
+    const bool young = wv >= W / 2u;
+    if (prio && young) __builtin_amdgcn_s_setprio(1);
     for (uint32_t i0 = 0; i0 < nsw; i0 += D) {
 #pragma unroll
         for (int d = 0; d < D; d++) step(i0 + d, NX[d], CN[d], P[d], V[d], BR[d]);
+        if (prio == 2u && young && i0 + D >= nsw / 2u && i0 < nsw / 2u) __builtin_amdgcn_s_setprio(0);
     }
+    if (prio && young) __builtin_amdgcn_s_setprio(0);
     GS_KS_STAMP(20u);
     // ---- K-split ticket: wave 0 takes its row block's arrival ticket as soon as its own
     // loop ends, so the add's round trip overlaps the partial-tile reduction below
@@ -1878,10 +1886,11 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
                                                     const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K,
                                                     uint32_t N, uint32_t S, uint32_t NS, uint32_t nwg,
                                                     uint32_t row_base, float *__restrict__ slabs,
-                                                    uint32_t *__restrict__ arrivals, uint64_t *__restrict__ stamps = nullptr) {
+                                                    uint32_t *__restrict__ arrivals, uint64_t *__restrict__ stamps = nullptr,
+                                                    uint32_t prio = 0) {
     // nwg == gridDim.x (an argument: kernarg preload)
     ks_body<CT, RT, W, D, MAXG, STAMPS>(bmtb_first_row, tP, tV, steps, B, C, K, N, S, NS, nwg, row_base, slabs, arrivals,
-                                        stamps, blockIdx.x);
+                                        stamps, blockIdx.x, prio);
 }
 
 // ---------------------------------------------------------------------------
@@ -1905,7 +1914,7 @@ struct ks_entry {  // 96 B
 // kKsGroupMax: kernel_consts.hpp
 struct ks_group_args {
     uint32_t begin[kKsGroupMax + 1];  // first workgroup of each entry (+ the total)
-    uint32_t n, N, pad[2];
+    uint32_t n, N, pad[2];  // pad[0]: k_mfma_ks's prio
     ks_entry e[kKsGroupMax];
 };
 
@@ -1919,7 +1928,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks_group(ks_group_args args) {
     sel = __builtin_amdgcn_readfirstlane(sel);
     const ks_entry &e = args.e[sel];  // kernel arguments: scalar loads at a computed offset
     ks_body<CT, RT, W, D, MAXG, false>(e.tbr, e.tP, e.tV, e.steps, e.B, e.C, e.K, args.N, e.S, e.NS, e.nwg, e.row_base,
-                                       e.slabs, e.arrivals, nullptr, bx - args.begin[sel]);
+                                       e.slabs, e.arrivals, nullptr, bx - args.begin[sel], args.pad[0]);
 }
 
 #ifdef GS_EXPERIMENTS  // opt-in, measured slower than k_mfma_rows / k_mfma_ks (make EXPERIMENTS=1)

@@ -54,7 +54,8 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
     grant_lds(d.device, kern, d.lds_bytes);
     hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit, ks_col_tiles(N)), dim3(64 * W), d.lds_bytes, s, a.t0,
                        (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, (const gsk::u32x2 *)a.t1, B, C,
-                       (uint32_t)p.K, N, d.ksplit, d.ks_ns, (uint32_t)d.n_rows_aux * d.ksplit, (uint32_t)d.row_base, a.ws, a.t2, stamps);
+                       (uint32_t)p.K, N, d.ksplit, d.ks_ns, (uint32_t)d.n_rows_aux * d.ksplit, (uint32_t)d.row_base, a.ws, a.t2, stamps,
+                       (uint32_t)get_config().KS_PRIO);
     HIP_OK(hipGetLastError());
 }
 
@@ -188,6 +189,7 @@ void launch_ks_group_k(const std::vector<ks_group_item> &it, uint32_t N, hipStre
     args.begin[it.size()] = wg;
     args.n = (uint32_t)it.size();
     args.N = N;
+    args.pad[0] = (uint32_t)get_config().KS_PRIO;
     grant_lds(it[0].p->dev.device, kern, lds);
     hipLaunchKernelGGL(kern, dim3(wg, ks_col_tiles(N)), dim3(64 * kKsWaves), lds, s, args);
     HIP_OK(hipGetLastError());

@@ -16,17 +16,18 @@ N = int(os.environ.get("SWEEP_N", "32"))
 rows_l = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "40,64,80").split(",")]
 spl_l = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "0,4,8").split(",")]
 wav_l = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "8").split(",")]
-shr_l = [int(x) for x in os.environ.get("SWEEP_SHARE", "32").split(",")]
+prio_l = [int(x) for x in os.environ.get("SWEEP_PRIO", "1").split(",")]
 row, col, val = ds.pruned_weight(M, K, 0.7, 13)
 for rb in rows_l:
     for ks in spl_l:
-        for w, sh in [(w, sh) for w in wav_l for sh in shr_l]:
+        for w, pr in [(w, pr) for w in wav_l for pr in prio_l]:
             gsa.set_config("KS_SPLIT", ks)
             gsa.set_config("KS_WAVES", w)
+            gsa.set_config("KS_PRIO", pr)
             try:
                 plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline("block_total", N, rb, 1).compile().upload("f16", 0)
             except Exception as ex:
-                print(json.dumps({"rows": rb, "split": ks, "waves": w, "error": str(ex)}), flush=True)
+                print(json.dumps({"rows": rb, "split": ks, "waves": w, "prio": pr, "error": str(ex)}), flush=True)
                 continue
             info = plan.info()
             reps = 12
@@ -44,8 +45,9 @@ for rb in rows_l:
                 e1.record()
                 torch.cuda.synchronize()
                 best = min(best, e0.elapsed_time(e1) / 200 * 1e3)
-            print(json.dumps({"rows": rb, "split": ks, "waves": w, "kernel": info["device_kernel"],
+            print(json.dumps({"rows": rb, "split": ks, "waves": w, "prio": pr, "kernel": info["device_kernel"],
                               "ksplit": info.get("ksplit"), "us": round(best, 2)}), flush=True)
             plan.free()
 gsa.set_config("KS_SPLIT", 0)
 gsa.set_config("KS_WAVES", 8)
+gsa.set_config("KS_PRIO", 1)

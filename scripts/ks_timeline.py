@@ -18,6 +18,7 @@ M = K = 5120
 N = 32
 P0 = int(sys.argv[1]) if len(sys.argv) > 1 else 80
 row, col, val = ds.pruned_weight(M, K, 0.7, 13)
+gsa.set_config("KS_PRIO", int(os.environ.get("KS_PRIO", "1")))
 plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline("block_total", N, P0, 1).compile().upload("f16", 0)
 info = plan.info()
 B = torch.randn((K, N), device="cuda", dtype=torch.float16)

@@ -45,7 +45,7 @@ def thinned(M, K, seed, keep=0.6, empty_rows=()):
     return r[m], c[m], v[m]
 
 
-SHAPES = [(128, 256), (96, 512), (200, 1000), (333, 772), (64, 64), (1, 4096)]
+SHAPES = [(128, 256), (96, 512), (200, 1000), (333, 772), (64, 64), (1, 4096), (1792, 768)]
 
 
 @pytest.mark.parametrize("N", [8, 16, 32, 64, 128])
