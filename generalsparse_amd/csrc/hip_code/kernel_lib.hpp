@@ -1561,6 +1561,8 @@ __device__ constexpr int vmcnt_imm() {
 }
 
 // kKsStride, ks_image_bytes, ks_lds_bytes: kernel_consts.hpp
+// 8 bytes at a 2-byte-aligned address (k_mfma_kb / k_mfma_bm value windows)
+typedef uint32_t u32x2_a2 __attribute__((ext_vector_type(2), aligned(2)));
 
 // STAMPS (diagnostic build only, gs_debug_mfma_timeline): lane 0 of every wave records
 // s_memtime into stamps[(workgroup * W + wave) * 32 + slot]: 0 start, 1 loads issued,
@@ -1931,6 +1933,318 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks_group(ks_group_args args) {
                                        e.slabs, e.arrivals, nullptr, bx - args.begin[sel], args.pad[0]);
 }
 
+// ---------------------------------------------------------------------------
+// k_mfma_kb -- k_mfma_ks's K split and per-wave pipeline on k_mfma_bm's bitmap layout: no
+// dense image, no entry scatter.  Per (unit u = row block g x K range q, 32-column k-step s)
+// one 8-byte record per lane l (byte t < RT: the occupancy of row 16t + l%16, columns
+// 32s + 8(l/16) + [0, 8) -- exactly the 8 halves lane l holds of tile t's A operand of
+// v_mfma_f32_16x16x32_f16 -- bytes 6..7: the lane's first value from the step's base
+// sbase[u*NS + s]) and the step's values, lane after lane, tile after tile (host layout:
+// device_layout.cc build_bm_tiles).  A is ~2.4 B per nonzero at 30% density (k_mfma_ks:
+// 4 B).  Wave w runs steps w, w+W, ...: a slot's record and base are loaded one round (D
+// steps) ahead of its value windows (two 8-byte windows per tile, 2-byte aligned: the low
+// nibble's values and the high nibble's), expanded into the tile's fragment by four
+// v_perm_b32 with selectors from a 16-entry LDS table; B rows as k_mfma_ks (registers ->
+// the wave's LDS stage, b_piece-permuted, ds_read_b64_tr_b16 fragments).  Epilogue as
+// k_mfma_ks (wave partial tiles summed in wave order, tagged-slab K-range combine).
+// ---------------------------------------------------------------------------
+template <int CT, int RT, int W, int D, bool STAMPS>
+__device__ __forceinline__ void kb_body(const uint32_t *__restrict__ bmtb_first_row, const uint2 *__restrict__ rec,
+                                        const uint32_t *__restrict__ sbase, const f16 *__restrict__ vals,
+                                        const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K, uint32_t N, uint32_t S,
+                                        uint32_t NS, uint32_t nwg, uint32_t row_base, float *__restrict__ slabs,
+                                        uint32_t *__restrict__ arrivals, uint64_t *__restrict__ stamps, uint32_t bx,
+                                        uint32_t prio) {
+    static_assert(RT >= 1 && RT <= 6, "six mask bytes per record");
+    constexpr uint32_t RB = 32 * CT;  // bytes per LDS B row (a 16*CT-column tile)
+    constexpr uint32_t UB = 2 * CT;   // 16-B units per B row
+    constexpr uint32_t STG = 32u * RB;  // one k-step of B rows
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t u = xcd_block(bx, nwg);
+    const uint32_t g = u / S, q = u - g * S;
+#define GS_KB_STAMP(slot)                                                                          \
+    if constexpr (STAMPS) {                                                                        \
+        if (lane == 0) stamps[((size_t)blockIdx.x * W + wv) * 32u + (slot)] = __builtin_amdgcn_s_memtime(); \
+    }
+    GS_KB_STAMP(0u);
+    const uint32_t k0 = q * NS * 32u;
+    const uint32_t col0 = blockIdx.y * 16u * CT, nv = min(16u * CT, N - col0);
+    uint2 *lut = reinterpret_cast<uint2 *>(lds);
+    unsigned char *bst = lds + 128u + wv * STG;
+    const u32x4 zero4 = {0u, 0u, 0u, 0u};
+    if (tid < 16u) lut[tid] = make_uint2(bm_sel(tid, 0), bm_sel(tid, 1));
+
+    const uint32_t nsw = NS > wv ? (NS - wv + W - 1u) / W : 0u;
+    const size_t ubase = (size_t)u * NS;
+    u32x4 BR[D][CT];
+    uint2 RC[D];           // per slot: record of the step whose value windows it holds
+    u32x2_a2 VV[D][RT][2];  // ... and the windows
+    uint2 NX[D];           // per slot: record of the step the slot loads next
+    uint32_t NB[D];        // ... and its value base
+    uint32_t vz;
+    __asm__ volatile("v_mov_b32 %0, 0" : "=v"(vz));
+    auto st_of = [&](uint32_t i) -> uint32_t { return __builtin_amdgcn_readfirstlane(i < nsw ? wv + i * W : 0u); };
+    auto mbyte = [](const uint2 &r, int t) -> uint32_t {
+        return t < 4 ? (r.x >> (8 * t)) & 0xffu : (r.y >> (8 * (t - 4))) & 0xffu;
+    };
+    // record + base of step i (vector loads, in order with the windows: see k_mfma_ks)
+    auto load_rec = [&](uint32_t i, uint2 &NX_, uint32_t &NB_) {
+        const uint32_t st = st_of(i);
+        NX_ = rec[(ubase + st) * 64u + lane + vz];
+        NB_ = sbase[ubase + st + vz];
+    };
+    auto load_b = [&](uint32_t i, u32x4 (&B_)[CT]) {
+        const uint32_t kr = k0 + st_of(i) * 32u;
+#pragma unroll
+        for (int c = 0; c < CT; c++) {
+            const uint32_t un = lane + 64u * c;
+            const uint32_t k = kr + un / UB, cu = (un % UB) * 8u;
+            B_[c] = *reinterpret_cast<const u32x4 *>(B + (size_t)(k < K ? k : K - 1u) * N + col0 + (cu < nv ? cu : 0u));
+        }
+    };
+    // the slot takes over the record it loaded a round ago, issues its value windows, and
+    // loads the record of its step a round ahead
+    auto load_v = [&](uint32_t i, uint2 &NX_, uint32_t &NB_, uint2 &RC_, u32x2_a2 (&VV_)[RT][2]) {
+        RC_ = NX_;
+        uint32_t p = NB_ + (RC_.y >> 16);
+#pragma unroll
+        for (int t = 0; t < RT; t++) {
+            const uint32_t m = mbyte(RC_, t);
+            VV_[t][0] = *reinterpret_cast<const u32x2_a2 *>(vals + p);
+            VV_[t][1] = *reinterpret_cast<const u32x2_a2 *>(vals + p + __builtin_popcount(m & 15u));
+            p += __builtin_popcount(m);
+        }
+        load_rec(i + D, NX_, NB_);
+    };
+#pragma unroll
+    for (int d = 0; d < D; d++) load_rec((uint32_t)d, NX[d], NB[d]);
+#pragma unroll
+    for (int d = 0; d < D; d++) load_b((uint32_t)d, BR[d]);
+#pragma unroll
+    for (int d = 0; d < D; d++) load_v((uint32_t)d, NX[d], NB[d], RC[d], VV[d]);
+    // the selector table (written by wave 0) before any wave expands a fragment
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __asm__ volatile("" ::: "memory");
+    GS_KB_STAMP(1u);
+
+    f4v acc[RT][CT];
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+
+    auto step = [&](uint32_t i, uint2 &NX_, uint32_t &NB_, uint2 &RC_, u32x2_a2 (&VV_)[RT][2], u32x4 (&B_)[CT]) {
+        const bool live = i < nsw;  // wave-uniform
+        h8v av[RT], bv[CT];
+        if (live) {
+            const uint32_t kr = k0 + (wv + i * W) * 32u;
+#pragma unroll
+            for (int c = 0; c < CT; c++) {
+                const uint32_t un = lane + 64u * c, k = un / UB, s = un % UB;
+                *reinterpret_cast<u32x4 *>(bst + k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u) =
+                    kr + k < K && s * 8u < nv ? B_[c] : zero4;
+            }
+            const uint32_t kb = 8u * (lane >> 4);
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) {
+                s4v t2[2];
+#pragma unroll
+                for (int hh = 0; hh < 2; hh++) {
+                    const uint32_t k = kb + 4u * hh + ((lane & 15u) >> 2);
+                    t2[hh] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s4v *)(bst + k * RB + b_piece<CT>(k, ct) * 32u + (lane & 3u) * 8u));
+                }
+                __builtin_memcpy(&bv[ct], t2, 16);
+            }
+#pragma unroll
+            for (int t = 0; t < RT; t++) {
+                const uint32_t m = mbyte(RC_, t);
+                const uint2 sl = lut[m & 15u], sh = lut[m >> 4];
+                const u32x2_a2 lo = VV_[t][0], hi = VV_[t][1];
+                uint32_t w4[4];
+                w4[0] = __builtin_amdgcn_perm(lo.y, lo.x, sl.x);
+                w4[1] = __builtin_amdgcn_perm(lo.y, lo.x, sl.y);
+                w4[2] = __builtin_amdgcn_perm(hi.y, hi.x, sh.x);
+                w4[3] = __builtin_amdgcn_perm(hi.y, hi.x, sh.y);
+                __builtin_memcpy(&av[t], w4, 16);
+            }
+        }
+        load_b(i + D, B_);
+        load_v(i + D, NX_, NB_, RC_, VV_);
+        if (live) {
+#pragma unroll
+            for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+                for (int ct = 0; ct < CT; ct++)
+                    acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[rt], bv[ct], acc[rt][ct], 0, 0, 0);
+            if (i < 16u) GS_KB_STAMP(3u + i);
+        }
+    };
+    const bool young = wv >= W / 2u;
+    if (prio && young) __builtin_amdgcn_s_setprio(1);
+    for (uint32_t i0 = 0; i0 < nsw; i0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; d++) step(i0 + d, NX[d], NB[d], RC[d], VV[d], BR[d]);
+    }
+    if (prio && young) __builtin_amdgcn_s_setprio(0);
+    GS_KB_STAMP(20u);
+    // ---- K-split ticket: wave 0 takes its row block's arrival ticket as soon as its own
+    // loop ends, so the add's round trip overlaps the partial-tile reduction below
+    uint32_t *arr = arrivals + (size_t)g * gridDim.y + blockIdx.y;
+    uint32_t ticket = 0;
+    if (S > 1 && wv == 0 && lane == 0) ticket = __hip_atomic_fetch_add(arr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // ---- wave partial tiles -> LDS (the trailing loads write registers only), summed in
+    // wave order.  Item t = (tile, lane) of a 16x16 tile: the 4 rows 4*(lane/16)+i of
+    // column lane%16.  When the W partial tiles fit LDS beside the wave images (APART), each
+    // wave stores its tile as soon as its loop ends, without waiting for the others
+    constexpr bool APART = kb_red_apart(CT, RT, W);
+    f4v *red = reinterpret_cast<f4v *>(lds + (APART ? kb_stage_bytes(CT, W) : 0u));
+    constexpr bool HALVES = !APART && ks_red_halves(CT, RT, W);
+    constexpr uint32_t WR = HALVES ? W / 2 : W;  // partial tiles summed from LDS
+    uint32_t *flag = reinterpret_cast<uint32_t *>(reinterpret_cast<unsigned char *>(red) + (size_t)WR * RT * CT * 1024u);
+    if constexpr (!APART) {
+        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __asm__ volatile("" ::: "memory");
+    }
+    if constexpr (HALVES) {
+        if (wv >= WR) {
+#pragma unroll
+            for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+                for (int ct = 0; ct < CT; ct++) red[(((wv - WR) * RT + rt) * CT + ct) * 64u + lane] = acc[rt][ct];
+        }
+        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __asm__ volatile("" ::: "memory");
+        if (wv < WR) {
+#pragma unroll
+            for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+                for (int ct = 0; ct < CT; ct++) acc[rt][ct] += red[((wv * RT + rt) * CT + ct) * 64u + lane];
+        }
+        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __asm__ volatile("" ::: "memory");
+    }
+    if (wv < WR) {
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) red[((wv * RT + rt) * CT + ct) * 64u + lane] = acc[rt][ct];
+    }
+    if (S > 1 && wv == 0 && lane == 0) *flag = ticket;  // (waits for the add's return)
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __asm__ volatile("" ::: "memory");
+    constexpr uint32_t NI = RT * CT * 64u, NT = 64u * W;
+    const uint32_t r0 = bmtb_first_row[g], R = bmtb_first_row[g + 1] - r0;
+    auto item_sum = [&](uint32_t t) {
+        f4v sum = red[t];
+#pragma unroll
+        for (uint32_t w = 1; w < WR; w++) sum += red[w * NI + t];
+        return sum;
+    };
+    auto store_item = [&](uint32_t t, const f4v &v) {
+        const uint32_t ln = t & 63u, tt = t >> 6, rt = tt / CT, ct = tt % CT;
+        const uint32_t col = 16u * ct + (ln & 15u), rb = 16u * rt + 4u * (ln >> 4);
+        if (col >= nv) return;
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++)
+            if (rb + i < R) C[(size_t)(row_base + r0 + rb + i) * N + col0 + col] = (f16)v[i];
+    };
+    GS_KB_STAMP(21u);
+    if (S == 1) {
+        for (uint32_t t = tid; t < NI; t += NT) store_item(t, item_sum(t));
+        GS_KB_STAMP(22u);
+        return;
+    }
+    // ---- K-split combine by tagged slabs.  Every fp32 word of a published slab carries
+    // its own validity tag in the low mantissa bit (1 = published this launch; the reader
+    // drops the bit, a 2^-24 relative truncation), so no store needs to be drained before a
+    // signal and the workgroup that drew the last ticket publishes nothing: the others
+    // store their slab with 16-B write-through (sc1) stores and finish; the last one loads
+    // each other slab word with agent-scope (sc1) loads until its tag is set -- its writer
+    // holds an earlier ticket, so it is running and its stores are issued or about to be --
+    // sums the S partials in q order (deterministic) and writes C, then clears the words it
+    // read back to 0 ("consumed") with sc1 stores and re-arms the ticket counter.  Every
+    // access to the slabs is sc1 (MI355X_MICROARCH.md §Workgroup dispatch, Valid forms: the
+    // R2 granule, here one naturally aligned word).  The next launch on the stream starts
+    // after these stores complete, so it finds every slab word at 0.
+    const uint32_t tk = *flag;
+    f4v *slab = reinterpret_cast<f4v *>(slabs) + ((size_t)u * gridDim.y + blockIdx.y) * NI;
+    if (tk != S - 1u) {
+        for (uint32_t t = tid; t < NI; t += NT) {
+            const f4v v = item_sum(t);
+            u32x4 w;
+            __builtin_memcpy(&w, &v, 16);
+            w[0] |= 1u; w[1] |= 1u; w[2] |= 1u; w[3] |= 1u;
+            __asm__ volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(slab + t), "v"(w) : "memory");
+        }
+        GS_KB_STAMP(22u);
+        return;
+    }
+    if (tid == 0) __hip_atomic_store(arr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const f4v *base = reinterpret_cast<const f4v *>(slabs) + blockIdx.y * NI;
+    const size_t qstride = (size_t)gridDim.y * NI;  // slab of (g, qq) = base + (g*S + qq) * qstride
+    for (uint32_t t = tid; t < NI; t += NT) {
+        const f4v own = item_sum(t);
+        f4v sum = {0.f, 0.f, 0.f, 0.f};
+        for (uint32_t qq = 0; qq < S; qq++) {
+            if (qq == q) {  // truncated as a published word is (whichever workgroup is last: deterministic)
+                u32x4 w;
+                __builtin_memcpy(&w, &own, 16);
+                w[0] &= ~1u; w[1] &= ~1u; w[2] &= ~1u; w[3] &= ~1u;
+                f4v x;
+                __builtin_memcpy(&x, &w, 16);
+                sum += x;
+                continue;
+            }
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(base + ((size_t)g * S + qq) * qstride + t);
+            u32x4 w;
+            auto load4 = [&]() {
+#pragma unroll
+                for (int i = 0; i < 4; i++) w[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            };
+            load4();
+            // bounded wait (a writer that never stores would be a bug: NaN, not a hang)
+            for (uint32_t tries = 0; !(w[0] & w[1] & w[2] & w[3] & 1u); tries++) {
+                if (tries > (1u << 20)) {
+                    w = u32x4{0x7fc00001u, 0x7fc00001u, 0x7fc00001u, 0x7fc00001u};
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+                load4();
+            }
+            w[0] &= ~1u; w[1] &= ~1u; w[2] &= ~1u; w[3] &= ~1u;
+            f4v x;
+            __builtin_memcpy(&x, &w, 16);
+            sum += x;
+            const u32x4 zero = {0u, 0u, 0u, 0u};
+            __asm__ volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(src), "v"(zero) : "memory");
+        }
+        store_item(t, sum);
+    }
+    GS_KB_STAMP(22u);
+#undef GS_KB_STAMP
+}
+
+template <int CT, int RT, int W, int D, bool STAMPS = false>
+__global__ __launch_bounds__(64 * W) void k_mfma_kb(const uint32_t *__restrict__ bmtb_first_row,  // nb+1
+                                                    const uint2 *__restrict__ rec,       // (u*NS + step)*64 + lane
+                                                    const uint32_t *__restrict__ sbase,  // u*NS + step
+                                                    const f16 *__restrict__ vals, const f16 *__restrict__ B,
+                                                    f16 *__restrict__ C, uint32_t K, uint32_t N, uint32_t S,
+                                                    uint32_t NS, uint32_t nwg, uint32_t row_base,
+                                                    float *__restrict__ slabs, uint32_t *__restrict__ arrivals,
+                                                    uint64_t *__restrict__ stamps = nullptr, uint32_t prio = 0) {
+    kb_body<CT, RT, W, D, STAMPS>(bmtb_first_row, rec, sbase, vals, B, C, K, N, S, NS, nwg, row_base, slabs, arrivals,
+                                  stamps, blockIdx.x, prio);
+}
+
 #ifdef GS_EXPERIMENTS  // opt-in, measured slower than k_mfma_rows / k_mfma_ks (make EXPERIMENTS=1)
 // ---------------------------------------------------------------------------
 // k_mfma_bm -- BMTB row blocks on the matrix cores from a bitmap layout, with the
@@ -1960,7 +2274,6 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks_group(ks_group_args args) {
 // Rows of B past K are read as row K-1 against zero A columns (a non-finite B value
 // there gives NaN: the documented matrix-core deviation).
 // ---------------------------------------------------------------------------
-typedef uint32_t u32x2_a2 __attribute__((ext_vector_type(2), aligned(2)));
 
 // STAMPS (diagnostic build only, gs_debug_mfma_timeline): lane 0 of every wave records
 // s_memtime into stamps[(workgroup * W + wave) * 16 + slot]: 0 start, 1 B + records issued,

@@ -216,7 +216,7 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
     std::ostringstream o;
     const uint32_t N = L.N, CT = L.kind == mc_layout::NM ? std::max<uint32_t>(1, N / 16) : ks_ct(N);
     const char *kname = L.kind == mc_layout::KS ? "k_mfma_ks"
-                        : L.kind == mc_layout::BM ? (L.bm.v2 ? "k_mfma_bm2" : "k_mfma_bm")
+                        : L.kind == mc_layout::BM ? (L.bm.kb ? "k_mfma_kb" : L.bm.v2 ? "k_mfma_bm2" : "k_mfma_bm")
                         : L.kind == mc_layout::ROWS ? "k_mfma_rows"
                         : (L.nm_ks ? "k_nm_mfma_ks" : "k_nm_mfma");
     o << "// kernel_file.hip -- generated by generalsparse_amd code_generator: the matrix-core kernel " << kname << "\n"
@@ -279,7 +279,10 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
           << "    float *d_ws; uint32_t *d_arr; hipMalloc(&d_ws, " << nwg * ks_col_tiles(N) * 256 * t.RT * CT * 4 << "ull + 16);\n"
           << "    hipMalloc(&d_arr, " << nb * ks_col_tiles(N) * t.RT * 4 << "ull + 4); hipMemset(d_arr, 0, "
           << nb * ks_col_tiles(N) * t.RT * 4 << "ull + 4);\n";
-        const std::string k = t.v2 ? "gsk::k_mfma_bm2<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ">"
+        if (t.kb) o << "    hipMemset(d_ws, 0, " << nwg * ks_col_tiles(N) * 256 * t.RT * CT * 4 << "ull + 16);\n";
+        const std::string k = t.kb ? "gsk::k_mfma_kb<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ", " +
+                                         std::to_string(t.W) + ", " + std::to_string(kKsDepth) + ">"
+                            : t.v2 ? "gsk::k_mfma_bm2<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ">"
                                    : "gsk::k_mfma_bm<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ", " +
                                          std::to_string(t.W) + ", " + std::to_string(gsk::bm_nbt(CT, t.RT)) + ">";
         setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
@@ -287,7 +290,8 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
         launch = k + "<<<dim3(" + std::to_string(nwg) + ", " + std::to_string(ks_col_tiles(N)) + "), " +
                  std::to_string(64 * t.W) + ", " + std::to_string(t.lds_bytes) +
                  ">>>(d_tbr, (const uint2 *)d_rec, d_sb, (const gsk::f16 *)d_val, d_B, d_C, (uint32_t)K, N, " +
-                 std::to_string(t.S) + "u, " + std::to_string(t.NS) + "u, " + std::to_string(nwg) + "u, 0u, d_ws, d_arr)";
+                 std::to_string(t.S) + "u, " + std::to_string(t.NS) + "u, " + std::to_string(nwg) + "u, 0u, d_ws, d_arr" +
+                 (t.kb ? ", nullptr, " + std::to_string(get_config().KS_PRIO) + "u)" : std::string(")"));
     } else if (L.kind == mc_layout::ROWS) {
         const mfma_tiles &t = L.rows;
         const uint64_t nb = L.tbr.size() - 1;

@@ -342,8 +342,10 @@ bool build_bm_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
         why = "row blocks too sparse for dense tiles";
         return false;
     }
-    const uint32_t W = waves == 4 ? 4u : 8u;
-    uint64_t S = s_cfg > 0 ? (uint64_t)s_cfg : std::max<uint64_t>(1, std::min<uint64_t>(8, 256 / nb));
+    const bool kb = get_config().BM_KB;
+    const uint32_t W = kb || waves != 4 ? 8u : 4u;
+    uint64_t S = s_cfg > 0 ? (uint64_t)s_cfg
+                           : kb ? std::min<uint64_t>(8, (256 + nb - 1) / nb) : std::max<uint64_t>(1, std::min<uint64_t>(8, 256 / nb));
     S = std::max<uint64_t>(1, std::min<uint64_t>(S, (K + 31) / 32));
     const uint64_t KR = ((K + S - 1) / S + 31) / 32 * 32;
     S = (K + KR - 1) / KR;
@@ -355,7 +357,9 @@ bool build_bm_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     t.lds_bytes = gsk::bm_lds_bytes(ks_ct(N), RT, W);
     // k_mfma_bm2 when the range's B slice fits LDS next to the selector table
     const size_t slice = 128u + (size_t)t.NS * 32u * 32u * ks_ct(N);
-    t.v2 = get_config().BM_V2 && slice <= 160u * 1024u;
+    t.kb = kb;
+    if (kb) t.lds_bytes = gsk::kb_lds_bytes(ks_ct(N), RT, W);
+    t.v2 = !kb && get_config().BM_V2 && slice <= 160u * 1024u;
     if (t.v2) {
         t.lds_bytes = slice;
         t.W = RT;

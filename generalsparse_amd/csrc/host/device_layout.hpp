@@ -70,6 +70,7 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
 // values (f16 bits) lane after lane, tile after tile, ascending columns (+ 16 halves pad)
 struct bm_tiles {
     uint32_t S = 0, NS = 0, RT = 0, RMAX = 0, W = 0;
+    bool kb = false;  // k_mfma_kb (8 waves, k_mfma_ks pipeline)
     bool v2 = false;  // k_mfma_bm2 (one wave per row tile, B slice resident in LDS)
     size_t lds_bytes = 0;
     std::vector<uint32_t> rec;

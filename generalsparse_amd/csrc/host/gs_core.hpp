@@ -92,6 +92,7 @@ struct config_t {
     bool MFMA_BM = false;        // fp16 BMTB row blocks of <= 96 rows: bitmap records, k_mfma_bm
     int64_t BM_SPLIT = 0;        // k_mfma_bm K ranges per row block (0: fill the CUs)
     int64_t BM_WAVES = 8;        // k_mfma_bm waves per workgroup (4 or 8)
+    bool BM_KB = false;          // ... k_mfma_kb (k_mfma_ks pipeline on the bitmap layout)
     bool BM_V2 = false;          // ... k_mfma_bm2 (one wave per row tile) when the B slice fits LDS
                                  // (C2 22.9 us against 18.4 for k_mfma_bm, profiles/r03_c2_bm_timeline.json)
     bool MFMA_KS = true;         // row blocks of >= KS_MIN_ROWS rows: K-split, B-stationary k_mfma_ks

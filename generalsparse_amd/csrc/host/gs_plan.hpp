@@ -48,6 +48,7 @@ struct device_plan {
                         // (t0 BMTB rows, tcol/tval groups; ks_ns k-steps per range,
                         // RT in maxr, MAXG in seg_cap, ws slabs + t2 arrivals when ksplit > 1)
     uint32_t ks_ns = 0, ks_gcap = 0;
+    bool bmkb = false;  // ... k_mfma_kb: k_mfma_ks pipeline on the bitmap layout (8 waves)
     bool bm2 = false;   // ... k_mfma_bm2: one wave per row tile (W = RT), B slice of ks_ns k-steps in LDS
     bool bm = false;    // k_mfma_bm: bitmap records (tcol), step bases (t1), values (tval), t0 BMTB rows;
                         // ksplit K ranges of ks_ns k-steps, RT in maxr, W in waves

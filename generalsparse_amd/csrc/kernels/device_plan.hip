@@ -343,7 +343,8 @@ void upload_plan(plan_state &p, int dtype, int device) {
             d.mfma = true;
             d.bm = true;
             d.bm2 = bt.v2;
-            d.kernel = bt.v2 ? "k_mfma_bm2" : "k_mfma_bm";
+            d.bmkb = bt.kb;
+            d.kernel = bt.kb ? "k_mfma_kb" : bt.v2 ? "k_mfma_bm2" : "k_mfma_bm";
             d.lds_N = mc.N;
             d.ksplit = bt.S;
             d.ks_ns = bt.NS;

@@ -112,8 +112,23 @@ void launch_bm2_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B
 }
 
 template <int CT, int RT>
+void launch_kb_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
+    const device_plan &d = p.dev;
+    auto kern = gsk::k_mfma_kb<CT, RT, (int)kKsWaves, (int)kKsDepth>;
+    GS_CHECK(d.waves == kKsWaves && gsk::kb_lds_bytes(CT, RT, kKsWaves) <= d.lds_bytes,
+             "k_mfma_kb: LDS size disagrees with the upload");
+    grant_lds(d.device, kern, d.lds_bytes);
+    const uint32_t nwg = (uint32_t)d.n_rows_aux * d.ksplit;
+    hipLaunchKernelGGL(kern, dim3(nwg, ks_col_tiles(N)), dim3(64 * kKsWaves), d.lds_bytes, s, a.t0, (const uint2 *)a.tcol,
+                       a.t1, (const gsk::f16 *)a.tval, B, C, (uint32_t)p.K, N, d.ksplit, d.ks_ns, nwg,
+                       (uint32_t)d.row_base, a.ws, a.t2, nullptr, (uint32_t)get_config().KS_PRIO);
+    HIP_OK(hipGetLastError());
+}
+
+template <int CT, int RT>
 void launch_bm_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
-    if (p.dev.bm2) launch_bm2_k<CT, RT>(p, a, B, C, N, s);
+    if (p.dev.bmkb) launch_kb_k<CT, RT>(p, a, B, C, N, s);
+    else if (p.dev.bm2) launch_bm2_k<CT, RT>(p, a, B, C, N, s);
     else if (p.dev.waves == 4) launch_bm_k<CT, RT, 4>(p, a, B, C, N, s);
     else launch_bm_k<CT, RT, 8>(p, a, B, C, N, s);
 }

@@ -17,11 +17,16 @@ rows_l = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "40,64,80").spl
 spl_l = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "0,4,8").split(",")]
 wav_l = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "8").split(",")]
 prio_l = [int(x) for x in os.environ.get("SWEEP_PRIO", "1").split(",")]
+KB = int(os.environ.get("SWEEP_KB", "0"))  # k_mfma_kb (bitmap layout; experiments build)
+if KB:
+    gsa.set_config("MFMA_BM", 1)
+    gsa.set_config("BM_KB", 1)
 row, col, val = ds.pruned_weight(M, K, 0.7, 13)
 for rb in rows_l:
     for ks in spl_l:
         for w, pr in [(w, pr) for w in wav_l for pr in prio_l]:
             gsa.set_config("KS_SPLIT", ks)
+            gsa.set_config("BM_SPLIT", ks)
             gsa.set_config("KS_WAVES", w)
             gsa.set_config("KS_PRIO", pr)
             try:
@@ -46,7 +51,7 @@ for rb in rows_l:
                 torch.cuda.synchronize()
                 best = min(best, e0.elapsed_time(e1) / 200 * 1e3)
             print(json.dumps({"rows": rb, "split": ks, "waves": w, "prio": pr, "kernel": info["device_kernel"],
-                              "ksplit": info.get("ksplit"), "us": round(best, 2)}), flush=True)
+                              "ksplit": info.get("ksplit"), "bytes_A": info.get("bytes_A"), "us": round(best, 2)}), flush=True)
             plan.free()
 gsa.set_config("KS_SPLIT", 0)
 gsa.set_config("KS_WAVES", 8)
