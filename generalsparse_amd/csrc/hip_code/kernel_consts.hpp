@@ -51,15 +51,17 @@ GSK_HD constexpr size_t ks_lds_bytes(uint32_t CT, uint32_t RT, uint32_t W) {
     return stage > red ? stage : red;
 }
 
-// k_mfma_kb: the selector table (128 B) + W wave stages of one k-step of B rows, then the W
-// partial tiles (+ the ticket word) when they fit beside them
-GSK_HD constexpr size_t kb_stage_bytes(uint32_t CT, uint32_t W) { return 128u + (size_t)W * 32u * 32u * CT; }
-GSK_HD constexpr bool kb_red_apart(uint32_t CT, uint32_t RT, uint32_t W) {
-    return kb_stage_bytes(CT, W) + (size_t)W * RT * CT * 1024u + 16u <= 160u * 1024u;
+// k_mfma_kb: the selector table (128 B) + W wave slots (one k-step of B rows + NVB KB of
+// values), then the W partial tiles (+ the ticket word) when they fit beside them
+GSK_HD constexpr size_t kb_stage_bytes(uint32_t CT, uint32_t W, uint32_t NVB) {
+    return 128u + (size_t)W * (32u * 32u * CT + 1024u * NVB);
 }
-GSK_HD constexpr size_t kb_lds_bytes(uint32_t CT, uint32_t RT, uint32_t W) {
-    const size_t st = kb_stage_bytes(CT, W);
-    if (kb_red_apart(CT, RT, W)) return st + (size_t)W * RT * CT * 1024u + 16u;
+GSK_HD constexpr bool kb_red_apart(uint32_t CT, uint32_t RT, uint32_t W, uint32_t NVB) {
+    return kb_stage_bytes(CT, W, NVB) + (size_t)W * RT * CT * 1024u + 16u <= 160u * 1024u;
+}
+GSK_HD constexpr size_t kb_lds_bytes(uint32_t CT, uint32_t RT, uint32_t W, uint32_t NVB) {
+    const size_t st = kb_stage_bytes(CT, W, NVB);
+    if (kb_red_apart(CT, RT, W, NVB)) return st + (size_t)W * RT * CT * 1024u + 16u;
     const size_t red = (size_t)(ks_red_halves(CT, RT, W) ? W / 2 : W) * RT * CT * 1024u + 16u;
     return st > red ? st : red;
 }

@@ -1941,14 +1941,19 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks_group(ks_group_args args) {
 // v_mfma_f32_16x16x32_f16 -- bytes 6..7: the lane's first value from the step's base
 // sbase[u*NS + s]) and the step's values, lane after lane, tile after tile (host layout:
 // device_layout.cc build_bm_tiles).  A is ~2.4 B per nonzero at 30% density (k_mfma_ks:
-// 4 B).  Wave w runs steps w, w+W, ...: a slot's record and base are loaded one round (D
-// steps) ahead of its value windows (two 8-byte windows per tile, 2-byte aligned: the low
-// nibble's values and the high nibble's), expanded into the tile's fragment by four
-// v_perm_b32 with selectors from a 16-entry LDS table; B rows as k_mfma_ks (registers ->
-// the wave's LDS stage, b_piece-permuted, ds_read_b64_tr_b16 fragments).  Epilogue as
-// k_mfma_ks (wave partial tiles summed in wave order, tagged-slab K-range combine).
+// 4 B).  Wave w runs steps w, w+W, ...: a slot's record and value bounds are loaded one
+// round (D steps) ahead of its values; the values are fetched as whole 16-B units (the
+// step's run from its 16-B-aligned start, NVB KB at most: one full wave load per KB, lanes
+// past the run re-read the first unit) and staged through the wave's LDS slot with B's rows
+// (b_piece-permuted, ds_read_b64_tr_b16 fragments); each lane reads its two 8-byte windows
+// per tile there and expands them into the tile's fragment by four v_perm_b32 with
+// selectors from a 16-entry LDS table.  (The first version loaded the windows straight from
+// HBM: 2 x RT 8-byte loads per lane and step at 2-byte alignment, ~40% of each request
+// used -- C2 21.1 us; the windows alone cost 11.5 us of it.)  Epilogue as k_mfma_ks (wave
+// partial tiles summed in wave order, tagged-slab K-range combine).
 // ---------------------------------------------------------------------------
-template <int CT, int RT, int W, int D, bool STAMPS>
+// DBG (experiments diagnostics, wrong results): 2 = no value loads, 3 = no B loads
+template <int CT, int RT, int W, int D, int NVB, bool STAMPS, int DBG = 0>
 __device__ __forceinline__ void kb_body(const uint32_t *__restrict__ bmtb_first_row, const uint2 *__restrict__ rec,
                                         const uint32_t *__restrict__ sbase, const f16 *__restrict__ vals,
                                         const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K, uint32_t N, uint32_t S,
@@ -1956,6 +1961,7 @@ __device__ __forceinline__ void kb_body(const uint32_t *__restrict__ bmtb_first_
                                         uint32_t *__restrict__ arrivals, uint64_t *__restrict__ stamps, uint32_t bx,
                                         uint32_t prio) {
     static_assert(RT >= 1 && RT <= 6, "six mask bytes per record");
+    static_assert(NVB >= 1 && NVB <= 4, "1..4 KB of values per step");
     constexpr uint32_t RB = 32 * CT;  // bytes per LDS B row (a 16*CT-column tile)
     constexpr uint32_t UB = 2 * CT;   // 16-B units per B row
     constexpr uint32_t STG = 32u * RB;  // one k-step of B rows
@@ -1972,28 +1978,31 @@ __device__ __forceinline__ void kb_body(const uint32_t *__restrict__ bmtb_first_
     const uint32_t k0 = q * NS * 32u;
     const uint32_t col0 = blockIdx.y * 16u * CT, nv = min(16u * CT, N - col0);
     uint2 *lut = reinterpret_cast<uint2 *>(lds);
-    unsigned char *bst = lds + 128u + wv * STG;
+    unsigned char *bst = lds + 128u + wv * (STG + NVB * 1024u);
+    unsigned char *vst = bst + STG;  // the step's values (16-B-aligned run start at byte 0)
     const u32x4 zero4 = {0u, 0u, 0u, 0u};
     if (tid < 16u) lut[tid] = make_uint2(bm_sel(tid, 0), bm_sel(tid, 1));
 
     const uint32_t nsw = NS > wv ? (NS - wv + W - 1u) / W : 0u;
     const size_t ubase = (size_t)u * NS;
     u32x4 BR[D][CT];
-    uint2 RC[D];           // per slot: record of the step whose value windows it holds
-    u32x2_a2 VV[D][RT][2];  // ... and the windows
-    uint2 NX[D];           // per slot: record of the step the slot loads next
-    uint32_t NB[D];        // ... and its value base
+    u32x4 VR[D][NVB];  // per slot: the values of the step it holds (16-B units)
+    uint2 RC[D];       // ... its record
+    uint32_t RL[D];    // ... and its first value's offset (halves) from the run's aligned start
+    uint2 NX[D];       // per slot: record of the step the slot loads next
+    uint32_t NB[D], NE[D];  // ... and its value bounds [sbase[s], sbase[s+1])
     uint32_t vz;
     __asm__ volatile("v_mov_b32 %0, 0" : "=v"(vz));
     auto st_of = [&](uint32_t i) -> uint32_t { return __builtin_amdgcn_readfirstlane(i < nsw ? wv + i * W : 0u); };
     auto mbyte = [](const uint2 &r, int t) -> uint32_t {
         return t < 4 ? (r.x >> (8 * t)) & 0xffu : (r.y >> (8 * (t - 4))) & 0xffu;
     };
-    // record + base of step i (vector loads, in order with the windows: see k_mfma_ks)
-    auto load_rec = [&](uint32_t i, uint2 &NX_, uint32_t &NB_) {
+    // record + value bounds of step i (vector loads, in order with the values: see k_mfma_ks)
+    auto load_rec = [&](uint32_t i, uint2 &NX_, uint32_t &NB_, uint32_t &NE_) {
         const uint32_t st = st_of(i);
         NX_ = rec[(ubase + st) * 64u + lane + vz];
         NB_ = sbase[ubase + st + vz];
+        NE_ = sbase[ubase + st + 1u + vz];
     };
     auto load_b = [&](uint32_t i, u32x4 (&B_)[CT]) {
         const uint32_t kr = k0 + st_of(i) * 32u;
@@ -2001,29 +2010,31 @@ __device__ __forceinline__ void kb_body(const uint32_t *__restrict__ bmtb_first_
         for (int c = 0; c < CT; c++) {
             const uint32_t un = lane + 64u * c;
             const uint32_t k = kr + un / UB, cu = (un % UB) * 8u;
-            B_[c] = *reinterpret_cast<const u32x4 *>(B + (size_t)(k < K ? k : K - 1u) * N + col0 + (cu < nv ? cu : 0u));
+            if constexpr (DBG == 3) B_[c] = u32x4{k, cu, k, cu};
+            else B_[c] = *reinterpret_cast<const u32x4 *>(B + (size_t)(k < K ? k : K - 1u) * N + col0 + (cu < nv ? cu : 0u));
         }
     };
-    // the slot takes over the record it loaded a round ago, issues its value windows, and
+    // the slot takes over the record it loaded a round ago, issues its step's values, and
     // loads the record of its step a round ahead
-    auto load_v = [&](uint32_t i, uint2 &NX_, uint32_t &NB_, uint2 &RC_, u32x2_a2 (&VV_)[RT][2]) {
+    auto load_v = [&](uint32_t i, uint2 &NX_, uint32_t &NB_, uint32_t &NE_, uint2 &RC_, uint32_t &RL_,
+                      u32x4 (&VR_)[NVB]) {
         RC_ = NX_;
-        uint32_t p = NB_ + (RC_.y >> 16);
+        const uint32_t b0 = NB_ & ~7u, len = NE_ - b0;  // halves from the aligned start
+        RL_ = NB_ - b0;
 #pragma unroll
-        for (int t = 0; t < RT; t++) {
-            const uint32_t m = mbyte(RC_, t);
-            VV_[t][0] = *reinterpret_cast<const u32x2_a2 *>(vals + p);
-            VV_[t][1] = *reinterpret_cast<const u32x2_a2 *>(vals + p + __builtin_popcount(m & 15u));
-            p += __builtin_popcount(m);
+        for (int j = 0; j < NVB; j++) {
+            const uint32_t h = 8u * (lane + 64u * j);
+            if constexpr (DBG == 2) VR_[j] = u32x4{RC_.x, RC_.y, RC_.x, RC_.y};
+            else VR_[j] = *reinterpret_cast<const u32x4 *>(vals + b0 + (h < len ? h : 0u));
         }
-        load_rec(i + D, NX_, NB_);
+        load_rec(i + D, NX_, NB_, NE_);
     };
 #pragma unroll
-    for (int d = 0; d < D; d++) load_rec((uint32_t)d, NX[d], NB[d]);
+    for (int d = 0; d < D; d++) load_rec((uint32_t)d, NX[d], NB[d], NE[d]);
 #pragma unroll
     for (int d = 0; d < D; d++) load_b((uint32_t)d, BR[d]);
 #pragma unroll
-    for (int d = 0; d < D; d++) load_v((uint32_t)d, NX[d], NB[d], RC[d], VV[d]);
+    for (int d = 0; d < D; d++) load_v((uint32_t)d, NX[d], NB[d], NE[d], RC[d], RL[d], VR[d]);
     // the selector table (written by wave 0) before any wave expands a fragment
     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -2036,7 +2047,8 @@ __device__ __forceinline__ void kb_body(const uint32_t *__restrict__ bmtb_first_
 #pragma unroll
         for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
 
-    auto step = [&](uint32_t i, uint2 &NX_, uint32_t &NB_, uint2 &RC_, u32x2_a2 (&VV_)[RT][2], u32x4 (&B_)[CT]) {
+    auto step = [&](uint32_t i, uint2 &NX_, uint32_t &NB_, uint32_t &NE_, uint2 &RC_, uint32_t &RL_,
+                    u32x4 (&VR_)[NVB], u32x4 (&B_)[CT]) {
         const bool live = i < nsw;  // wave-uniform
         h8v av[RT], bv[CT];
         if (live) {
@@ -2047,6 +2059,8 @@ __device__ __forceinline__ void kb_body(const uint32_t *__restrict__ bmtb_first_
                 *reinterpret_cast<u32x4 *>(bst + k * RB + b_piece<CT>(k, s >> 1) * 32u + (s & 1u) * 16u) =
                     kr + k < K && s * 8u < nv ? B_[c] : zero4;
             }
+#pragma unroll
+            for (int j = 0; j < NVB; j++) *reinterpret_cast<u32x4 *>(vst + (lane + 64u * j) * 16u) = VR_[j];
             const uint32_t kb = 8u * (lane >> 4);
 #pragma unroll
             for (int ct = 0; ct < CT; ct++) {
@@ -2059,11 +2073,14 @@ __device__ __forceinline__ void kb_body(const uint32_t *__restrict__ bmtb_first_
                 }
                 __builtin_memcpy(&bv[ct], t2, 16);
             }
+            uint32_t p = RL_ + (RC_.y >> 16);
 #pragma unroll
             for (int t = 0; t < RT; t++) {
                 const uint32_t m = mbyte(RC_, t);
                 const uint2 sl = lut[m & 15u], sh = lut[m >> 4];
-                const u32x2_a2 lo = VV_[t][0], hi = VV_[t][1];
+                const u32x2_a2 lo = *reinterpret_cast<const u32x2_a2 *>(vst + 2u * p);
+                const u32x2_a2 hi = *reinterpret_cast<const u32x2_a2 *>(vst + 2u * (p + __builtin_popcount(m & 15u)));
+                p += __builtin_popcount(m);
                 uint32_t w4[4];
                 w4[0] = __builtin_amdgcn_perm(lo.y, lo.x, sl.x);
                 w4[1] = __builtin_amdgcn_perm(lo.y, lo.x, sl.y);
@@ -2073,7 +2090,7 @@ __device__ __forceinline__ void kb_body(const uint32_t *__restrict__ bmtb_first_
             }
         }
         load_b(i + D, B_);
-        load_v(i + D, NX_, NB_, RC_, VV_);
+        load_v(i + D, NX_, NB_, NE_, RC_, RL_, VR_);
         if (live) {
 #pragma unroll
             for (int rt = 0; rt < RT; rt++)
@@ -2087,7 +2104,7 @@ __device__ __forceinline__ void kb_body(const uint32_t *__restrict__ bmtb_first_
     if (prio && young) __builtin_amdgcn_s_setprio(1);
     for (uint32_t i0 = 0; i0 < nsw; i0 += D) {
 #pragma unroll
-        for (int d = 0; d < D; d++) step(i0 + d, NX[d], NB[d], RC[d], VV[d], BR[d]);
+        for (int d = 0; d < D; d++) step(i0 + d, NX[d], NB[d], NE[d], RC[d], RL[d], VR[d], BR[d]);
     }
     if (prio && young) __builtin_amdgcn_s_setprio(0);
     GS_KB_STAMP(20u);
@@ -2100,8 +2117,8 @@ __device__ __forceinline__ void kb_body(const uint32_t *__restrict__ bmtb_first_
     // wave order.  Item t = (tile, lane) of a 16x16 tile: the 4 rows 4*(lane/16)+i of
     // column lane%16.  When the W partial tiles fit LDS beside the wave images (APART), each
     // wave stores its tile as soon as its loop ends, without waiting for the others
-    constexpr bool APART = kb_red_apart(CT, RT, W);
-    f4v *red = reinterpret_cast<f4v *>(lds + (APART ? kb_stage_bytes(CT, W) : 0u));
+    constexpr bool APART = kb_red_apart(CT, RT, W, NVB);
+    f4v *red = reinterpret_cast<f4v *>(lds + (APART ? kb_stage_bytes(CT, W, NVB) : 0u));
     constexpr bool HALVES = !APART && ks_red_halves(CT, RT, W);
     constexpr uint32_t WR = HALVES ? W / 2 : W;  // partial tiles summed from LDS
     uint32_t *flag = reinterpret_cast<uint32_t *>(reinterpret_cast<unsigned char *>(red) + (size_t)WR * RT * CT * 1024u);
@@ -2232,16 +2249,16 @@ __device__ __forceinline__ void kb_body(const uint32_t *__restrict__ bmtb_first_
 #undef GS_KB_STAMP
 }
 
-template <int CT, int RT, int W, int D, bool STAMPS = false>
+template <int CT, int RT, int W, int D, int NVB, bool STAMPS = false, int DBG = 0>
 __global__ __launch_bounds__(64 * W) void k_mfma_kb(const uint32_t *__restrict__ bmtb_first_row,  // nb+1
                                                     const uint2 *__restrict__ rec,       // (u*NS + step)*64 + lane
-                                                    const uint32_t *__restrict__ sbase,  // u*NS + step
+                                                    const uint32_t *__restrict__ sbase,  // u*NS + step (+1)
                                                     const f16 *__restrict__ vals, const f16 *__restrict__ B,
                                                     f16 *__restrict__ C, uint32_t K, uint32_t N, uint32_t S,
                                                     uint32_t NS, uint32_t nwg, uint32_t row_base,
                                                     float *__restrict__ slabs, uint32_t *__restrict__ arrivals,
                                                     uint64_t *__restrict__ stamps = nullptr, uint32_t prio = 0) {
-    kb_body<CT, RT, W, D, STAMPS>(bmtb_first_row, rec, sbase, vals, B, C, K, N, S, NS, nwg, row_base, slabs, arrivals,
+    kb_body<CT, RT, W, D, NVB, STAMPS, DBG>(bmtb_first_row, rec, sbase, vals, B, C, K, N, S, NS, nwg, row_base, slabs, arrivals,
                                   stamps, blockIdx.x, prio);
 }
 
@@ -2282,7 +2299,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_kb(const uint32_t *__restrict__
 template <int CT, int RT, int W, int NBT, bool STAMPS = false>
 __global__ __launch_bounds__(64 * W) void k_mfma_bm(const uint32_t *__restrict__ bmtb_first_row,  // nb+1
                                                     const uint2 *__restrict__ rec,       // (u*NS + step)*64 + lane
-                                                    const uint32_t *__restrict__ sbase,  // u*NS + step
+                                                    const uint32_t *__restrict__ sbase,  // u*NS + step (+1)
                                                     const f16 *__restrict__ vals, const f16 *__restrict__ B,
                                                     f16 *__restrict__ C, uint32_t K, uint32_t N, uint32_t S,
                                                     uint32_t NS, uint32_t nwg, uint32_t row_base,

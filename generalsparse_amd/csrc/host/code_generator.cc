@@ -281,7 +281,8 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
           << nb * ks_col_tiles(N) * t.RT * 4 << "ull + 4);\n";
         if (t.kb) o << "    hipMemset(d_ws, 0, " << nwg * ks_col_tiles(N) * 256 * t.RT * CT * 4 << "ull + 16);\n";
         const std::string k = t.kb ? "gsk::k_mfma_kb<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ", " +
-                                         std::to_string(t.W) + ", " + std::to_string(kKsDepth) + ">"
+                                         std::to_string(t.W) + ", " + std::to_string(kKsDepth) + ", " +
+                                         std::to_string(t.NVB) + ">"
                             : t.v2 ? "gsk::k_mfma_bm2<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ">"
                                    : "gsk::k_mfma_bm<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ", " +
                                          std::to_string(t.W) + ", " + std::to_string(gsk::bm_nbt(CT, t.RT)) + ">";

@@ -358,7 +358,6 @@ bool build_bm_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     // k_mfma_bm2 when the range's B slice fits LDS next to the selector table
     const size_t slice = 128u + (size_t)t.NS * 32u * 32u * ks_ct(N);
     t.kb = kb;
-    if (kb) t.lds_bytes = gsk::kb_lds_bytes(ks_ct(N), RT, W);
     t.v2 = !kb && get_config().BM_V2 && slice <= 160u * 1024u;
     if (t.v2) {
         t.lds_bytes = slice;
@@ -405,6 +404,16 @@ bool build_bm_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     }
     t.sbase[nst] = (uint32_t)run;
     t.val.assign(run + 16, 0);
+    if (kb) {
+        // k_mfma_kb fetches a step's run in whole 16-B units from its aligned start: NVB KB
+        uint64_t umax = 1;
+        for (uint64_t x = 0; x < nst; x++) umax = std::max<uint64_t>(umax, (t.sbase[x + 1] - (t.sbase[x] & ~7u) + 7) / 8);
+        t.NVB = (uint32_t)((umax + 63) / 64);
+        if (t.NVB == 3) t.NVB = 4;
+        if (t.NVB > 4) { why = "a k-step holds more than 4 KB of values (k_mfma_kb)"; return false; }
+        t.lds_bytes = gsk::kb_lds_bytes(ks_ct(N), RT, W, t.NVB);
+        if (t.lds_bytes > 160 * 1024) { why = "k_mfma_kb slots exceed LDS"; return false; }
+    }
     for (uint64_t g = 0; g < nb; g++)
         for (uint64_t i = 0; i < tb_rows[g + 1] - tb_rows[g]; i++)
             for (uint64_t e = row_ptr[tb_rows[g] + i]; e < row_ptr[tb_rows[g] + i + 1]; e++) {

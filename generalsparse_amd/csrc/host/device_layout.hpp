@@ -14,7 +14,9 @@
 namespace gs {
 
 constexpr uint32_t kMfmaThreads = 64 * gsk::kMfmaWaves;
-constexpr uint32_t kKsWaves = 8, kKsDepth = 4;  // k_mfma_ks workgroup waves, entry sets in flight
+// k_mfma_ks workgroup waves, entry sets in flight per wave (look-ahead D: 2 measured fastest
+// over C2 and the OPT-30B shapes -- 1-12% under D = 4, D = 1 / 3 / 6 slower, profiles/r04o_*)
+constexpr uint32_t kKsWaves = 8, kKsDepth = 2;
 
 // fp32 -> fp16 bits, round to nearest even (bit-identical to the device conversion)
 uint16_t f32_to_f16_bits(float f);
@@ -71,6 +73,7 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
 struct bm_tiles {
     uint32_t S = 0, NS = 0, RT = 0, RMAX = 0, W = 0;
     bool kb = false;  // k_mfma_kb (8 waves, k_mfma_ks pipeline)
+    uint32_t NVB = 0;  // ... KB of values per k-step (1, 2 or 4)
     bool v2 = false;  // k_mfma_bm2 (one wave per row tile, B slice resident in LDS)
     size_t lds_bytes = 0;
     std::vector<uint32_t> rec;

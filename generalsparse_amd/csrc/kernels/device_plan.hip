@@ -344,6 +344,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
             d.bm = true;
             d.bm2 = bt.v2;
             d.bmkb = bt.kb;
+            d.seg_cap = bt.NVB;  // k_mfma_kb: KB of values per k-step
             d.kernel = bt.kb ? "k_mfma_kb" : bt.v2 ? "k_mfma_bm2" : "k_mfma_bm";
             d.lds_N = mc.N;
             d.ksplit = bt.S;

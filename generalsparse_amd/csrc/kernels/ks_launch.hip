@@ -45,6 +45,22 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
             return;
         }
     }
+    // GS_KS_DEPTH=1/3/4 (look-ahead sweep against kKsDepth = 2, N = 32 on the C2 / attn / fc1 instantiations)
+    if constexpr (W == (int)kKsWaves && !STAMPS && CT == 2 &&
+                  ((RT == 3 && MAXG == 1) || (RT == 4 && MAXG == 2) || (RT == 5 && MAXG <= 2) || (RT == 7 && MAXG == 3))) {
+        static const int dep = getenv("GS_KS_DEPTH") ? atoi(getenv("GS_KS_DEPTH")) : 0;
+        if (dep == 1 || dep == 3 || dep == 4) {
+            auto kd = dep == 1 ? gsk::k_mfma_ks<CT, RT, W, 1, MAXG, false>
+                               : dep == 3 ? gsk::k_mfma_ks<CT, RT, W, 3, MAXG, false> : gsk::k_mfma_ks<CT, RT, W, 4, MAXG, false>;
+            grant_lds(d.device, kd, d.lds_bytes);
+            hipLaunchKernelGGL(kd, dim3((uint32_t)d.n_rows_aux * d.ksplit, ks_col_tiles(N)), dim3(64 * W), d.lds_bytes, s,
+                               a.t0, (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, (const gsk::u32x2 *)a.t1, B, C,
+                               (uint32_t)p.K, N, d.ksplit, d.ks_ns, (uint32_t)d.n_rows_aux * d.ksplit, (uint32_t)d.row_base,
+                               a.ws, a.t2, stamps, (uint32_t)get_config().KS_PRIO);
+            HIP_OK(hipGetLastError());
+            return;
+        }
+    }
 #else
     GS_CHECK(d.waves == kKsWaves, "k_mfma_ks with 16 waves is an experiments-build variant");
 #endif
@@ -111,11 +127,17 @@ void launch_bm2_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B
     HIP_OK(hipGetLastError());
 }
 
-template <int CT, int RT>
+template <int CT, int RT, int NVB>
 void launch_kb_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
     const device_plan &d = p.dev;
-    auto kern = gsk::k_mfma_kb<CT, RT, (int)kKsWaves, (int)kKsDepth>;
-    GS_CHECK(d.waves == kKsWaves && gsk::kb_lds_bytes(CT, RT, kKsWaves) <= d.lds_bytes,
+    // GS_KB_DEBUG=2/3 (diagnostics, wrong results): no value loads / no B loads
+    static const int dbg = getenv("GS_KB_DEBUG") ? atoi(getenv("GS_KB_DEBUG")) : 0;
+    auto kern = gsk::k_mfma_kb<CT, RT, (int)kKsWaves, (int)kKsDepth, NVB>;
+    if constexpr (CT == 2 && NVB <= 2) {  // (N = 32 only)
+        if (dbg == 2) kern = gsk::k_mfma_kb<CT, RT, (int)kKsWaves, (int)kKsDepth, NVB, false, 2>;
+        if (dbg == 3) kern = gsk::k_mfma_kb<CT, RT, (int)kKsWaves, (int)kKsDepth, NVB, false, 3>;
+    }
+    GS_CHECK(d.waves == kKsWaves && gsk::kb_lds_bytes(CT, RT, kKsWaves, NVB) <= d.lds_bytes,
              "k_mfma_kb: LDS size disagrees with the upload");
     grant_lds(d.device, kern, d.lds_bytes);
     const uint32_t nwg = (uint32_t)d.n_rows_aux * d.ksplit;
@@ -127,7 +149,13 @@ void launch_kb_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
 
 template <int CT, int RT>
 void launch_bm_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
-    if (p.dev.bmkb) launch_kb_k<CT, RT>(p, a, B, C, N, s);
+    if (p.dev.bmkb) {
+        switch (p.dev.seg_cap) {  // NVB
+            case 1: launch_kb_k<CT, RT, 1>(p, a, B, C, N, s); break;
+            case 2: launch_kb_k<CT, RT, 2>(p, a, B, C, N, s); break;
+            default: launch_kb_k<CT, RT, 4>(p, a, B, C, N, s); break;
+        }
+    }
     else if (p.dev.bm2) launch_bm2_k<CT, RT>(p, a, B, C, N, s);
     else if (p.dev.waves == 4) launch_bm_k<CT, RT, 4>(p, a, B, C, N, s);
     else launch_bm_k<CT, RT, 8>(p, a, B, C, N, s);

@@ -14,7 +14,8 @@ import generalsparse_amd as gsa  # noqa: E402
 from generalsparse_amd import _lib  # noqa: E402
 from generalsparse_amd import datasets as ds  # noqa: E402
 
-M = K = 5120
+M = int(os.environ.get("TL_M", "5120"))  # TL_M / TL_K: another shape (attn: 7168)
+K = int(os.environ.get("TL_K", str(M)))
 N = 32
 P0 = int(sys.argv[1]) if len(sys.argv) > 1 else 80
 row, col, val = ds.pruned_weight(M, K, 0.7, 13)
@@ -37,7 +38,7 @@ t0 = a[:, :, 0].min(axis=1)[:, None]
 glob0 = a[:, :, 0].min()
 # s_memtime is per XCD (clocks of different XCDs are not aligned): every delta is taken
 # inside one workgroup (from its first stamp)
-out = {"ksplit": info["ksplit"], "rows": P0}
+out = {"M": M, "K": K, "ksplit": info["ksplit"], "rows": P0}
 for slot in [1, 2] + list(range(3, 16)) + [20, 21, 22]:
     v = a[:, :, slot]
     ok = v > 0
