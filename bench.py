@@ -408,7 +408,7 @@ def timed_batch(step, streams, steps, torch):
 def batch_step(launches, N, torch, n_streams, group=False):
     """one pass over a batch of independent SpMMs.  group: the batch through gs_spmm_batch
     (consecutive K-split entries of one instantiation are one grouped launch; entries sorted
-    by shape so runs are long, then dealt over the streams), every launch with its own C.  Otherwise launch i on stream i % n_streams (the current stream first), so
+    largest matrix first, same shapes together, then dealt over the streams), every launch with its own C.  Otherwise launch i on stream i % n_streams (the current stream first), so
     one launch's tail overlaps the next one's start; with more than one stream every launch
     writes its own C.  Returns (step, streams)."""
     import generalsparse_amd as gsa
@@ -417,7 +417,10 @@ def batch_step(launches, N, torch, n_streams, group=False):
     if group:
         # sorted by shape, then dealt over the streams: each stream's share is one batch of
         # long same-shape runs, and the streams' grouped launches overlap each other's tails
-        ents = [(p, r, b, torch.empty_like(c), k) for (p, r, b, c, k) in sorted(launches, key=lambda x: x[4])]
+        # largest matrices first (their workgroups run longest: a grouped launch dispatches its
+        # entries in order, so the short ones fill the tail), same shapes together
+        ents = [(p, r, b, torch.empty_like(c), k)
+                for (p, r, b, c, k) in sorted(launches, key=lambda x: (-x[3].shape[0] * x[2].shape[0], x[4]))]
         bats = [(gsa.Batch([(p, r, b, c) for (p, r, b, c, _) in ents[i::len(streams)]], N), st.cuda_stream)
                 for i, st in enumerate(streams) if ents[i::len(streams)]]
 
@@ -506,8 +509,52 @@ def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
                                       rocsparse=not args.no_rocsparse)
     # the timed layer: 4 x attn (replicas 0..3), fc1, fc2
     seq = [(0, s, bt.C5_SLOTS[s], bt.C5_SLOTS[:s].count(bt.C5_SLOTS[s])) for s in range(len(bt.C5_SLOTS))]
-    plans, launches, _ = bt.build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, sparsity=sp, choice=choice)
-    step, streams = batch_step(launches, N, torch, args.streams, group=bool(args.group))
+
+    def build_layer(ch):
+        plans, launches, _ = bt.build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, sparsity=sp, choice=ch)
+        step, streams = batch_step(launches, N, torch, args.streams, group=bool(args.group))
+        return plans, step, streams
+
+    plans, step, streams = build_layer(choice)
+    # layer-level choice (grouped launches): the four attn SpMMs on their fastest K-split plan
+    # run as ONE grouped k_mfma_ks launch, which a per-shape search (each launch alone) does
+    # not see; both layers are timed and the faster kept
+    layer_search = None
+    if args.group:
+        # attn's K-split candidates within 15% of its best alone (a variant whose instantiation
+        # matches fc1 / fc2's joins their grouped launch: the layer becomes fewer launches)
+        ks = sorted((v["kernel_us"], key) for key, v in per_shape["attn"]["variants"].items()
+                    if v.get("kernel") == "k_mfma_ks")
+        cands = {("%s(%d,%d)%s" % (c[0], c[1], c[2], "".join(f" {a}={b}" for a, b in c[3].items()))): c
+                 for c in bt.shape_candidates("attn")}
+        alts = [key for us, key in ks if us <= 1.15 * ks[0][0] and key != per_shape["attn"]["plan"]] if ks else []
+        if alts:
+            best_ms = layer_ms(step, streams, torch)
+            layer_search = {"per_shape_best": {"attn": per_shape["attn"]["plan"], "layer_ms": round(best_ms, 5)},
+                            "attn_alternatives": {}, "kept": per_shape["attn"]["plan"]}
+            for alt_key in alts:
+                plans2, step2, streams2 = build_layer(dict(choice, attn=cands[alt_key]))
+                t_b = layer_ms(step2, streams2, torch)
+                layer_search["attn_alternatives"][alt_key] = round(t_b, 5)
+                if t_b < best_ms:
+                    for p in plans.values():
+                        p.free()
+                    plans, step, streams, best_ms = plans2, step2, streams2, t_b
+                    layer_search["kept"] = alt_key
+                else:
+                    for p in plans2.values():
+                        p.free()
+                del step2
+            if layer_search["kept"] != per_shape["attn"]["plan"]:
+                k2 = layer_search["kept"]
+                per_shape["attn"]["plan_alone_best"] = per_shape["attn"]["plan"]
+                per_shape["attn"]["plan"] = k2
+                per_shape["attn"]["kernel"] = per_shape["attn"]["variants"][k2]["kernel"]
+                per_shape["attn"]["kernel_us"] = per_shape["attn"]["variants"][k2]["kernel_us"]
+                per_shape["attn"]["gflops"] = round(2.0 * per_shape["attn"]["nnz"] * N / (per_shape["attn"]["kernel_us"] * 1e-6) / 1e9, 1)
+                per_shape["attn"]["hbm_frac"] = round(algorithmic_bytes(per_shape["attn"]["M"], per_shape["attn"]["K"], N,
+                                                                        per_shape["attn"]["nnz"], e, 2)
+                                                      / (per_shape["attn"]["kernel_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
 
     for _ in range(args.warmup):
         step()
@@ -561,6 +608,7 @@ def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
                      "note": "whole layer step (six launches over the streams, HIP events); per-kernel fractions in "
                              "per_shape.hbm_frac, their serial sum in serial_kernels"},
         "per_shape": per_shape,
+        "layer_search": layer_search,
         "speedup_vs_rocsparse": round(rs_l / ms_step, 3) if rs_l else None,
         "rocsparse_layer_ms": round(rs_l, 4) if rs_l else None,
     }
@@ -568,6 +616,15 @@ def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
         print(json.dumps(out), flush=True)
     for p in plans.values():
         p.free()
+
+
+def layer_ms(step, streams, torch, warm=10, reps=30):
+    """event time (ms) of one layer step, all streams joined (the c5h layer-level choice)"""
+    for _ in range(warm):
+        step()
+    torch.cuda.synchronize()
+    _, ev_s = timed_batch(step, streams, reps, torch)
+    return ev_s / reps * 1e3
 
 
 def replicas_for(info, K, N, e, rotation_mb):

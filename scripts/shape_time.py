@@ -18,6 +18,9 @@ sp = float(sys.argv[3]) if len(sys.argv) > 3 else 0.7
 m, n = bt.C5_SHAPES[shape]
 row, col, val = ds.pruned_weight(m, n, sp, bt.shape_seed(0, shape))
 cand = bt.shape_candidates(shape)[ci]
+for kv in os.environ.get("SWEEP_CFG", "").split(","):  # KEY=VALUE config overrides
+    if kv:
+        gsa.set_config(kv.split("=")[0], int(kv.split("=")[1]))
 plan = bt.build_plan(gsa, m, n, row, col, val, N, cand, 0)
 info = plan.info()
 abytes = len(row) * 4
@@ -37,6 +40,6 @@ for _ in range(3):
     torch.cuda.synchronize()
     best = min(best, e0.elapsed_time(e1) / 60 * 1e3)
 print(json.dumps({"shape": shape, "cand": str(cand[:3]), "kernel": info["device_kernel"], "ksplit": info.get("ksplit"),
-                  "reps": reps, "us": round(best, 2), "env": {k: v for k, v in os.environ.items() if k.startswith("GS_KS")}}),
+                  "reps": reps, "us": round(best, 2), "env": {k: v for k, v in os.environ.items() if k.startswith("GS_KS") or k == "SWEEP_CFG"}}),
       flush=True)
 plan.free()
