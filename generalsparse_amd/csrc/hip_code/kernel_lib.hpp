@@ -1811,68 +1811,67 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
         return;
     }
     // ---- K-split combine by tagged slabs.  Every fp32 word of a published slab carries
-    // its own validity tag in the low mantissa bit (1 = published this launch; the reader
-    // drops the bit, a 2^-24 relative truncation), so no store needs to be drained before a
-    // signal and the workgroup that drew the last ticket publishes nothing: the others
-    // store their slab with 16-B write-through (sc1) stores and finish; the last one loads
-    // each other slab word with agent-scope (sc1) loads until its tag is set -- its writer
-    // holds an earlier ticket, so it is running and its stores are issued or about to be --
-    // sums the S partials in q order (deterministic) and writes C, then clears the words it
-    // read back to 0 ("consumed") with sc1 stores and re-arms the ticket counter.  Every
-    // access to the slabs is sc1 (MI355X_MICROARCH.md §Workgroup dispatch, Valid forms: the
-    // R2 granule, here one naturally aligned word).  The next launch on the stream starts
-    // after these stores complete, so it finds every slab word at 0.
-    const uint32_t tk = *flag;
+    // its own validity tag in the low mantissa bit (the reader drops the bit, a 2^-24
+    // relative truncation), so no store needs to be drained before a signal: every workgroup
+    // stores its slab with 16-B write-through (sc1) stores, and the one that drew the last
+    // ticket loads each other slab word with agent-scope (sc1) loads until its tag reads
+    // this launch's value -- its writer holds an earlier ticket, so it is running and its
+    // stores are issued or about to be -- sums the S partials in q order (deterministic) and
+    // writes C.  The tag alternates from launch to launch: the arrival counter holds
+    // (epoch << 16) | arrivals, the tag is epoch ^ 1, and the last workgroup re-arms the
+    // counter with the epoch flipped and no arrivals.  Every slab word then holds the
+    // previous launch's tag when a launch starts (the last workgroup stores its own slab
+    // too), and the zero-filled first state reads as "tag 0, epoch 0" -- so no slab is
+    // cleared after use ((S - 1) fewer slab stores than clearing, the last workgroup's own
+    // store issued before it waits).  Every access to the slabs is sc1 (MI355X_MICROARCH.md
+    // Workgroup dispatch, Valid forms: the R2 granule, here one naturally aligned word).
+    // The next launch on the stream starts after these stores complete.
+    const uint32_t tk = *flag & 0xffffu, tag = ((*flag >> 16) & 1u) ^ 1u;
     f4v *slab = reinterpret_cast<f4v *>(slabs) + ((size_t)u * gridDim.y + blockIdx.y) * NI;
+    auto tagged = [&](const f4v &v) {
+        u32x4 w;
+        __builtin_memcpy(&w, &v, 16);
+        w[0] = (w[0] & ~1u) | tag; w[1] = (w[1] & ~1u) | tag; w[2] = (w[2] & ~1u) | tag; w[3] = (w[3] & ~1u) | tag;
+        return w;
+    };
+    for (uint32_t t = tid; t < NI; t += NT) {
+        const u32x4 w = tagged(item_sum(t));
+        __asm__ volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(slab + t), "v"(w) : "memory");
+    }
     if (tk != S - 1u) {
-        for (uint32_t t = tid; t < NI; t += NT) {
-            const f4v v = item_sum(t);
-            u32x4 w;
-            __builtin_memcpy(&w, &v, 16);
-            w[0] |= 1u; w[1] |= 1u; w[2] |= 1u; w[3] |= 1u;
-            __asm__ volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(slab + t), "v"(w) : "memory");
-        }
         GS_KS_STAMP(22u);
         return;
     }
-    if (tid == 0) __hip_atomic_store(arr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_store(arr, tag << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const f4v *base = reinterpret_cast<const f4v *>(slabs) + blockIdx.y * NI;
     const size_t qstride = (size_t)gridDim.y * NI;  // slab of (g, qq) = base + (g*S + qq) * qstride
     for (uint32_t t = tid; t < NI; t += NT) {
-        const f4v own = item_sum(t);
         f4v sum = {0.f, 0.f, 0.f, 0.f};
         for (uint32_t qq = 0; qq < S; qq++) {
-            if (qq == q) {  // truncated as a published word is (whichever workgroup is last: deterministic)
-                u32x4 w;
-                __builtin_memcpy(&w, &own, 16);
-                w[0] &= ~1u; w[1] &= ~1u; w[2] &= ~1u; w[3] &= ~1u;
-                f4v x;
-                __builtin_memcpy(&x, &w, 16);
-                sum += x;
-                continue;
-            }
-            const uint32_t *src = reinterpret_cast<const uint32_t *>(base + ((size_t)g * S + qq) * qstride + t);
             u32x4 w;
-            auto load4 = [&]() {
+            if (qq == q) {  // truncated as a published word is (whichever workgroup is last: deterministic)
+                w = tagged(item_sum(t));
+            } else {
+                const uint32_t *src = reinterpret_cast<const uint32_t *>(base + ((size_t)g * S + qq) * qstride + t);
+                auto load4 = [&]() {
 #pragma unroll
-                for (int i = 0; i < 4; i++) w[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            };
-            load4();
-            // bounded wait (a writer that never stores would be a bug: NaN, not a hang)
-            for (uint32_t tries = 0; !(w[0] & w[1] & w[2] & w[3] & 1u); tries++) {
-                if (tries > (1u << 20)) {
-                    w = u32x4{0x7fc00001u, 0x7fc00001u, 0x7fc00001u, 0x7fc00001u};
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
+                    for (int i = 0; i < 4; i++) w[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                };
                 load4();
+                // bounded wait (a writer that never stores would be a bug: NaN, not a hang)
+                for (uint32_t tries = 0; ((w[0] ^ tag) | (w[1] ^ tag) | (w[2] ^ tag) | (w[3] ^ tag)) & 1u; tries++) {
+                    if (tries > (1u << 20)) {
+                        w = u32x4{0x7fc00000u | tag, 0x7fc00000u | tag, 0x7fc00000u | tag, 0x7fc00000u | tag};
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                    load4();
+                }
             }
             w[0] &= ~1u; w[1] &= ~1u; w[2] &= ~1u; w[3] &= ~1u;
             f4v x;
             __builtin_memcpy(&x, &w, 16);
             sum += x;
-            const u32x4 zero = {0u, 0u, 0u, 0u};
-            __asm__ volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(src), "v"(zero) : "memory");
         }
         store_item(t, sum);
     }
@@ -2180,68 +2179,67 @@ __device__ __forceinline__ void kb_body(const uint32_t *__restrict__ bmtb_first_
         return;
     }
     // ---- K-split combine by tagged slabs.  Every fp32 word of a published slab carries
-    // its own validity tag in the low mantissa bit (1 = published this launch; the reader
-    // drops the bit, a 2^-24 relative truncation), so no store needs to be drained before a
-    // signal and the workgroup that drew the last ticket publishes nothing: the others
-    // store their slab with 16-B write-through (sc1) stores and finish; the last one loads
-    // each other slab word with agent-scope (sc1) loads until its tag is set -- its writer
-    // holds an earlier ticket, so it is running and its stores are issued or about to be --
-    // sums the S partials in q order (deterministic) and writes C, then clears the words it
-    // read back to 0 ("consumed") with sc1 stores and re-arms the ticket counter.  Every
-    // access to the slabs is sc1 (MI355X_MICROARCH.md §Workgroup dispatch, Valid forms: the
-    // R2 granule, here one naturally aligned word).  The next launch on the stream starts
-    // after these stores complete, so it finds every slab word at 0.
-    const uint32_t tk = *flag;
+    // its own validity tag in the low mantissa bit (the reader drops the bit, a 2^-24
+    // relative truncation), so no store needs to be drained before a signal: every workgroup
+    // stores its slab with 16-B write-through (sc1) stores, and the one that drew the last
+    // ticket loads each other slab word with agent-scope (sc1) loads until its tag reads
+    // this launch's value -- its writer holds an earlier ticket, so it is running and its
+    // stores are issued or about to be -- sums the S partials in q order (deterministic) and
+    // writes C.  The tag alternates from launch to launch: the arrival counter holds
+    // (epoch << 16) | arrivals, the tag is epoch ^ 1, and the last workgroup re-arms the
+    // counter with the epoch flipped and no arrivals.  Every slab word then holds the
+    // previous launch's tag when a launch starts (the last workgroup stores its own slab
+    // too), and the zero-filled first state reads as "tag 0, epoch 0" -- so no slab is
+    // cleared after use ((S - 1) fewer slab stores than clearing, the last workgroup's own
+    // store issued before it waits).  Every access to the slabs is sc1 (MI355X_MICROARCH.md
+    // Workgroup dispatch, Valid forms: the R2 granule, here one naturally aligned word).
+    // The next launch on the stream starts after these stores complete.
+    const uint32_t tk = *flag & 0xffffu, tag = ((*flag >> 16) & 1u) ^ 1u;
     f4v *slab = reinterpret_cast<f4v *>(slabs) + ((size_t)u * gridDim.y + blockIdx.y) * NI;
+    auto tagged = [&](const f4v &v) {
+        u32x4 w;
+        __builtin_memcpy(&w, &v, 16);
+        w[0] = (w[0] & ~1u) | tag; w[1] = (w[1] & ~1u) | tag; w[2] = (w[2] & ~1u) | tag; w[3] = (w[3] & ~1u) | tag;
+        return w;
+    };
+    for (uint32_t t = tid; t < NI; t += NT) {
+        const u32x4 w = tagged(item_sum(t));
+        __asm__ volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(slab + t), "v"(w) : "memory");
+    }
     if (tk != S - 1u) {
-        for (uint32_t t = tid; t < NI; t += NT) {
-            const f4v v = item_sum(t);
-            u32x4 w;
-            __builtin_memcpy(&w, &v, 16);
-            w[0] |= 1u; w[1] |= 1u; w[2] |= 1u; w[3] |= 1u;
-            __asm__ volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(slab + t), "v"(w) : "memory");
-        }
         GS_KB_STAMP(22u);
         return;
     }
-    if (tid == 0) __hip_atomic_store(arr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_store(arr, tag << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const f4v *base = reinterpret_cast<const f4v *>(slabs) + blockIdx.y * NI;
     const size_t qstride = (size_t)gridDim.y * NI;  // slab of (g, qq) = base + (g*S + qq) * qstride
     for (uint32_t t = tid; t < NI; t += NT) {
-        const f4v own = item_sum(t);
         f4v sum = {0.f, 0.f, 0.f, 0.f};
         for (uint32_t qq = 0; qq < S; qq++) {
-            if (qq == q) {  // truncated as a published word is (whichever workgroup is last: deterministic)
-                u32x4 w;
-                __builtin_memcpy(&w, &own, 16);
-                w[0] &= ~1u; w[1] &= ~1u; w[2] &= ~1u; w[3] &= ~1u;
-                f4v x;
-                __builtin_memcpy(&x, &w, 16);
-                sum += x;
-                continue;
-            }
-            const uint32_t *src = reinterpret_cast<const uint32_t *>(base + ((size_t)g * S + qq) * qstride + t);
             u32x4 w;
-            auto load4 = [&]() {
+            if (qq == q) {  // truncated as a published word is (whichever workgroup is last: deterministic)
+                w = tagged(item_sum(t));
+            } else {
+                const uint32_t *src = reinterpret_cast<const uint32_t *>(base + ((size_t)g * S + qq) * qstride + t);
+                auto load4 = [&]() {
 #pragma unroll
-                for (int i = 0; i < 4; i++) w[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            };
-            load4();
-            // bounded wait (a writer that never stores would be a bug: NaN, not a hang)
-            for (uint32_t tries = 0; !(w[0] & w[1] & w[2] & w[3] & 1u); tries++) {
-                if (tries > (1u << 20)) {
-                    w = u32x4{0x7fc00001u, 0x7fc00001u, 0x7fc00001u, 0x7fc00001u};
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
+                    for (int i = 0; i < 4; i++) w[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                };
                 load4();
+                // bounded wait (a writer that never stores would be a bug: NaN, not a hang)
+                for (uint32_t tries = 0; ((w[0] ^ tag) | (w[1] ^ tag) | (w[2] ^ tag) | (w[3] ^ tag)) & 1u; tries++) {
+                    if (tries > (1u << 20)) {
+                        w = u32x4{0x7fc00000u | tag, 0x7fc00000u | tag, 0x7fc00000u | tag, 0x7fc00000u | tag};
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                    load4();
+                }
             }
             w[0] &= ~1u; w[1] &= ~1u; w[2] &= ~1u; w[3] &= ~1u;
             f4v x;
             __builtin_memcpy(&x, &w, 16);
             sum += x;
-            const u32x4 zero = {0u, 0u, 0u, 0u};
-            __asm__ volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(src), "v"(zero) : "memory");
         }
         store_item(t, sum);
     }

@@ -25,11 +25,13 @@ if [ "$PART" = "b" ]; then
     echo "prof $wl done"
   done
 fi
-if [ "$PART" = "c" ]; then
+if [ "$PART" = "c" ] || [ "$PART" = "c5t" ]; then
   mkdir -p $OUT/tc5
   timeout -s KILL 400 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/tc5/fetch -o p -- python3 bench.py --workload c5 --layers 2 --steps 3 --warmup 1 --no-cpu > $OUT/tc5/fetch.log 2>&1
   timeout -s KILL 400 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/tc5/write -o p -- python3 bench.py --workload c5 --layers 2 --steps 3 --warmup 1 --no-cpu > $OUT/tc5/write.log 2>&1
   python3 scripts/traffic_c5.py $OUT/tc5 2 4 $OUT/traffic_c5.json
+fi
+if [ "$PART" = "c" ] || [ "$PART" = "c5ht" ]; then
   rm -rf $OUT/tc5h; mkdir -p $OUT/tc5h
   for sc in $(python3 scripts/traffic_c5h.py list); do
     s=${sc%%:*}; c=${sc##*:}
@@ -38,6 +40,8 @@ if [ "$PART" = "c" ]; then
     echo "tc5h $s $c"
   done
   python3 scripts/traffic_c5h.py summarize $OUT/tc5h 8 $OUT/traffic_c5h.json > /dev/null
+fi
+if [ "$PART" = "c" ] || [ "$PART" = "c4ot" ]; then
   mkdir -p $OUT/tc4o
   timeout -s KILL 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/tc4o/fetch -o p -- python3 bench.py --workload c4o --pipeline merge_path --p0 512 --steps 3 --warmup 1 --search-reps 2 --search-rounds 1 --no-cpu --no-rocsparse > $OUT/tc4o/fetch.log 2>&1
   timeout -s KILL 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/tc4o/write -o p -- python3 bench.py --workload c4o --pipeline merge_path --p0 512 --steps 3 --warmup 1 --search-reps 2 --search-rounds 1 --no-cpu --no-rocsparse > $OUT/tc4o/write.log 2>&1
