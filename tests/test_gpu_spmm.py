@@ -411,6 +411,40 @@ def test_mfma_ks_tall_blocks_match_oracle(rows, N, split, mfma_everywhere):
     assert "k_mfma_ks" in used, used
 
 
+@pytest.mark.parametrize("split", [2, 4])
+def test_mfma_ks_slab_tags_alternate_over_launches(split, mfma_everywhere):
+    """The K-split combine's slab tags alternate per launch (epoch in the arrival counter, no
+    slab cleared after use): a stale slab from the previous launch must never be taken for a
+    fresh one.  Seven launches with a different B each, a replica added after an odd number of
+    launches (it copies the slab / counter state), launches alternating between the two, and a
+    repeat of the first B at the end: every result equals its first computation bit for bit
+    and the oracle within the fp16 tolerance."""
+    gsa.set_config("KS_SPLIT", split)
+    try:
+        r, c, v = ds.pruned_weight(640, 2048, 0.7, 5)
+        plan = gsa.Plan.from_coo(640, 2048, r, c, v).run_pipeline("block_total", 32, 80, 1).compile().upload("f16", 0)
+        assert plan.info()["device_kernel"] == "k_mfma_ks" and plan.info()["ksplit"] == split
+        rng = np.random.default_rng(11)
+        Bs = [rng.uniform(-1, 1, (2048, 32)).astype(np.float16) for _ in range(4)]
+        vf = v.astype(np.float16).astype(np.float32)
+        first = {}
+        order = [(0, 0), (1, 0), (2, 0), "add", (3, 1), (0, 0), (1, 1), (2, 0), (3, 0), (0, 1)]
+        for step in order:
+            if step == "add":
+                plan.add_replica()
+                continue
+            b, rep = step
+            C = plan.spmm(torch.from_numpy(Bs[b]).to(DEV), replica=rep).float().cpu().numpy()
+            if b in first:
+                np.testing.assert_array_equal(C, first[b])
+            else:
+                check(C, ofi.spmm_ref(640, 32, r, c, vf, Bs[b].astype(np.float32), "f64"), "f16")
+                first[b] = C
+        plan.free()
+    finally:
+        gsa.set_config("KS_SPLIT", 0)
+
+
 def test_mfma_ks_known_answer_and_c2():
     """all-ones known answer bit-exactly, and the C2 shape (80-row blocks, 4 K ranges) against
     a torch fp32 dense product of the same fp16 inputs"""
