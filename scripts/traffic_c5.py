@@ -7,6 +7,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -15,14 +16,23 @@ from generalsparse_amd import batch as bt  # noqa: E402
 root, layers, steps, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
 tot = {}
 kinds = set()
+# only the timed region's launches: the last (W + K) x L x 6 gsk dispatches of the run (the
+# plan search and the rocSPARSE comparator launch before it)
+keep = steps * layers * len(bt.C5_SLOTS)
+kind_re = re.compile(r"gsk(?:::|\d+)(k_[a-z0-9_]+?)(?:I|<|\()")
 for name in ("FETCH_SIZE", "WRITE_SIZE"):
-    per = {}
+    per, nm = {}, {}
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] == name and "gsk" in r["Kernel_Name"]:
-                per[(f, r["Dispatch_Id"])] = per.get((f, r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
-                kinds.add(r["Kernel_Name"].split("<")[0].split("::")[-1].split("(")[0].strip())
-    tot[name] = (sum(per.values()), len(per))
+                key = (f, int(r["Dispatch_Id"]))
+                per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
+                nm[key] = r["Kernel_Name"]
+    last = sorted(per)[-keep:]
+    for key in last:
+        m = kind_re.search(nm[key])
+        kinds.add(m.group(1) if m else nm[key])
+    tot[name] = (sum(per[k] for k in last), len(last))
 layer_read = tot["FETCH_SIZE"][0] * 1024 * 2 / steps / layers
 layer_write = tot["WRITE_SIZE"][0] * 1024 / steps / layers
 e, N = 2, 32
