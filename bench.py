@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--rotation-mb", type=float, default=640.0)
     ap.add_argument("--no-rocsparse", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-north-star", action="store_true",
+                    help="c2: skip the north_star object (the OPT-30B 70% layer timed in the same run)")
     ap.add_argument("--p0", type=int, default=None, help="with --pipeline: run only this plan parameter")
     ap.add_argument("--p1", type=int, default=None)
     ap.add_argument("--workload", choices=("c1", "c2", "c3", "c4", "c4o", "c5", "c5h"), default=None,
@@ -165,6 +167,17 @@ def algorithmic_bytes_24(M, K, N, nnz, e):
     return nnz * e + nnz // 4 + K * N * e + M * N * e
 
 
+def mark(torch):
+    """GS_BENCH_MARK=1: one tiny fill kernel on the current stream, launched right before the
+    first and right after the last timed launch, so that scripts/timed_stats.py can keep only
+    the timed region's dispatches of a rocprofv3 kernel trace (the plan search's launches of
+    the same kernels are left out)"""
+    if os.environ.get("GS_BENCH_MARK") == "1":
+        if not hasattr(mark, "buf"):
+            mark.buf = torch.zeros(1, device="cuda")
+        mark.buf.fill_(1.0)
+
+
 def time_plan(plan, Bs, Cs, N, steps, warmup, torch, dist=None):
     """returns (host wall seconds for `steps` launches, seconds by HIP events on the launch
     stream over the same `steps` launches), each the max over ranks.  The event time is the
@@ -178,10 +191,12 @@ def time_plan(plan, Bs, Cs, N, steps, warmup, torch, dist=None):
     torch.cuda.synchronize()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
+    mark(torch)
     t0 = time.perf_counter()
     e0.record(stream)
     plan.spmm_rotate(steps, 0, Bs, Cs)
     e1.record(stream)
+    mark(torch)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist is not None:
@@ -333,7 +348,7 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    wall, ev_s = timed_batch(step, streams, args.steps, torch)
+    wall, ev_s = timed_batch(step, streams, args.steps, torch, marked=True)
     wall = max_over_ranks(wall, dist, torch)
     ev_s = max_over_ranks(ev_s, dist, torch)
     if dist is not None:
@@ -384,7 +399,7 @@ def run_c5(args, torch, gsa, ds, rank, world, local, dev, dist):
         p.free()
 
 
-def timed_batch(step, streams, steps, torch):
+def timed_batch(step, streams, steps, torch, marked=False):
     """`steps` calls of a batch step over its streams; returns (host wall s, HIP-event s).
     The events sit on the first stream; the other streams wait for the start event and the
     first stream waits for their last launches before the stop event."""
@@ -392,6 +407,8 @@ def timed_batch(step, streams, steps, torch):
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
+    if marked:
+        mark(torch)
     t0 = time.perf_counter()
     e0.record(cur)
     for s in streams[1:]:
@@ -401,6 +418,8 @@ def timed_batch(step, streams, steps, torch):
     for s in streams[1:]:
         cur.wait_event(s.record_event())
     e1.record(cur)
+    if marked:
+        mark(torch)
     torch.cuda.synchronize()
     return time.perf_counter() - t0, e0.elapsed_time(e1) * 1e-3
 
@@ -429,6 +448,7 @@ def batch_step(launches, N, torch, n_streams, group=False):
                 bat.run(s)
 
         gstep.keep = ents  # the C buffers live as long as the step
+        gstep.launches = lambda: [n for bat, _ in bats for n in bat.launches()]  # entries per launch
         return gstep, streams
     raw = []
     for i, (p, r, b, c, _) in enumerate(launches):
@@ -495,45 +515,76 @@ def search_shapes(args, torch, gsa, ds, rank, local, dev, shapes, sp, rocsparse=
     return choice, per_shape
 
 
-def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
-    """north_star headline: one OPT-30B decoder layer's six pruned weights
-    (q, k, v, out 7168^2; fc1 28672x7168; fc2 7168x28672) at 70% unstructured, fp16, N=32,
-    one GPU.  Per shape: the plan search over generalsparse_amd.batch.shape_candidates
-    (event time with rotated replicas) and rocSPARSE 7.2 CSR SpMM (fp16 A/B, fp32 C) on the
-    same matrix.  The timed step = the layer's six SpMMs, one plan replica per instance (the
-    layer's A is ~800 MB, past the 256 MB Infinity Cache)."""
+# the headline layer's plan when no search runs (the default bench line's north_star object):
+# block_total(112,1) on all six slots -- the r04 layer search's pick (profiles/r04y_c5h_bench.json:
+# attn, fc1 and fc2 on 112-row k_mfma_ks blocks, the layer ONE grouped launch)
+HEADLINE_CHOICE = ("block_total", 112, 1, {})
+NORTH_STAR_TARGET = {"speedup_vs_rocsparse": 1.5, "hbm_frac": 0.5}
+
+
+def layer_consts(N, sp):
+    """(nnz, flops, algorithmic bytes) of one OPT-30B layer step (six SpMMs)"""
+    from generalsparse_amd import batch as bt
+    nnz_l = sum(bt.nnz_of_shape(k, sp) for k in bt.C5_SLOTS)
+    alg_l = sum(algorithmic_bytes(*bt.C5_SHAPES[k], N, bt.nnz_of_shape(k, sp), 2, 2) for k in bt.C5_SLOTS)
+    return nnz_l, 2.0 * nnz_l * N, alg_l
+
+
+def layer_traffic(N, sp, plans_by_shape):
+    """L2->fabric bytes of the layer step from the PMC passes of the headline candidates
+    (profiles/traffic_c5h.json, per (shape, plan)); None unless every slot's plan was measured"""
+    from generalsparse_amd import batch as bt
+    tf = os.path.join(ROOT, "profiles", "traffic_c5h.json")
+    if not os.path.exists(tf):
+        return None, {}
+    try:
+        tj = json.load(open(tf))
+        if tj["N"] != N or abs(tj["sparsity"] - sp) > 1e-9:
+            return None, {}
+        pl = tj["per_launch"]
+        per = {k: pl.get(k, {}).get(plans_by_shape[k], {}).get("hbm_bytes") for k in plans_by_shape}
+        if all(per.get(k) for k in bt.C5_SLOTS):
+            return sum(per[k] for k in bt.C5_SLOTS), per
+        return None, per
+    except Exception:
+        return None, {}
+
+
+def cand_key(c):
+    return "%s(%d,%d)%s" % (c[0], c[1], c[2], "".join(f" {a}={b}" for a, b in c[3].items()))
+
+
+def headline_layer(args, torch, gsa, ds, rank, local, dev, choice, steps, warmup, per_shape=None, rs_per_shape=None):
+    """The north_star headline: one OPT-30B decoder layer's six pruned weights
+    (q, k, v, out 7168^2; fc1 28672x7168; fc2 7168x28672) at `args.sparsity`, fp16, N=32, one
+    GPU, with the per-shape plans of `choice`.  The timed step = the layer's six SpMMs, one plan
+    replica per instance (the layer's A is ~750 MB, past the 256 MB Infinity Cache), through
+    gs_spmm_batch (grouped k_mfma_ks launches) when args.group.  With `per_shape` (the c5h
+    search's results) and grouped launches, attn's K-split alternatives within 15% are also
+    timed as whole layers and the fastest layer kept.  Returns (line dict, plans, step)."""
     from generalsparse_amd import batch as bt
     N, sp = args.N, args.sparsity
-    e = 2
-    choice, per_shape = search_shapes(args, torch, gsa, ds, rank, local, dev, list(bt.C5_SHAPES), sp,
-                                      rocsparse=not args.no_rocsparse)
-    # the timed layer: 4 x attn (replicas 0..3), fc1, fc2
     seq = [(0, s, bt.C5_SLOTS[s], bt.C5_SLOTS[:s].count(bt.C5_SLOTS[s])) for s in range(len(bt.C5_SLOTS))]
 
     def build_layer(ch):
-        plans, launches, _ = bt.build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, sparsity=sp, choice=ch)
+        plans, launches, coo = bt.build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, sparsity=sp, choice=ch,
+                                                   keep_coo=rs_per_shape is None and not args.no_rocsparse)
         step, streams = batch_step(launches, N, torch, args.streams, group=bool(args.group))
-        return plans, step, streams
+        return plans, step, streams, coo
 
-    plans, step, streams = build_layer(choice)
-    # layer-level choice (grouped launches): the four attn SpMMs on their fastest K-split plan
-    # run as ONE grouped k_mfma_ks launch, which a per-shape search (each launch alone) does
-    # not see; both layers are timed and the faster kept
+    plans, step, streams, coo = build_layer(choice)
     layer_search = None
-    if args.group:
-        # attn's K-split candidates within 15% of its best alone (a variant whose instantiation
-        # matches fc1 / fc2's joins their grouped launch: the layer becomes fewer launches)
+    if args.group and per_shape is not None:
         ks = sorted((v["kernel_us"], key) for key, v in per_shape["attn"]["variants"].items()
                     if v.get("kernel") == "k_mfma_ks")
-        cands = {("%s(%d,%d)%s" % (c[0], c[1], c[2], "".join(f" {a}={b}" for a, b in c[3].items()))): c
-                 for c in bt.shape_candidates("attn")}
+        cands = {cand_key(c): c for c in bt.shape_candidates("attn")}
         alts = [key for us, key in ks if us <= 1.15 * ks[0][0] and key != per_shape["attn"]["plan"]] if ks else []
         if alts:
             best_ms = layer_ms(step, streams, torch)
             layer_search = {"per_shape_best": {"attn": per_shape["attn"]["plan"], "layer_ms": round(best_ms, 5)},
                             "attn_alternatives": {}, "kept": per_shape["attn"]["plan"]}
             for alt_key in alts:
-                plans2, step2, streams2 = build_layer(dict(choice, attn=cands[alt_key]))
+                plans2, step2, streams2, _ = build_layer(dict(choice, attn=cands[alt_key]))
                 t_b = layer_ms(step2, streams2, torch)
                 layer_search["attn_alternatives"][alt_key] = round(t_b, 5)
                 if t_b < best_ms:
@@ -546,72 +597,87 @@ def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
                         p.free()
                 del step2
             if layer_search["kept"] != per_shape["attn"]["plan"]:
+                e = 2
                 k2 = layer_search["kept"]
-                per_shape["attn"]["plan_alone_best"] = per_shape["attn"]["plan"]
-                per_shape["attn"]["plan"] = k2
-                per_shape["attn"]["kernel"] = per_shape["attn"]["variants"][k2]["kernel"]
-                per_shape["attn"]["kernel_us"] = per_shape["attn"]["variants"][k2]["kernel_us"]
-                per_shape["attn"]["gflops"] = round(2.0 * per_shape["attn"]["nnz"] * N / (per_shape["attn"]["kernel_us"] * 1e-6) / 1e9, 1)
-                per_shape["attn"]["hbm_frac"] = round(algorithmic_bytes(per_shape["attn"]["M"], per_shape["attn"]["K"], N,
-                                                                        per_shape["attn"]["nnz"], e, 2)
-                                                      / (per_shape["attn"]["kernel_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
-
-    for _ in range(args.warmup):
+                ps = per_shape["attn"]
+                ps["plan_alone_best"] = ps["plan"]
+                ps["plan"], ps["kernel"], ps["kernel_us"] = k2, ps["variants"][k2]["kernel"], ps["variants"][k2]["kernel_us"]
+                ps["gflops"] = round(2.0 * ps["nnz"] * N / (ps["kernel_us"] * 1e-6) / 1e9, 1)
+                ps["hbm_frac"] = round(algorithmic_bytes(ps["M"], ps["K"], N, ps["nnz"], e, 2)
+                                       / (ps["kernel_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+    launches_per_step = step.launches() if hasattr(step, "launches") else None
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
-    wall, ev_s = timed_batch(step, streams, args.steps, torch)
-    ms_step = ev_s / args.steps * 1e3
-    # the layer's kernels one at a time (each shape's search time = its own launch alone):
-    # their serial sum against the overlapped layer step
-    serial_ms = sum(per_shape[k]["kernel_us"] for k in bt.C5_SLOTS) * 1e-3
-    nnz_l = sum(bt.nnz_of_shape(k, sp) for k in bt.C5_SLOTS)
-    flops_l = 2.0 * nnz_l * N
-    alg_l = sum(algorithmic_bytes(*bt.C5_SHAPES[k], N, bt.nnz_of_shape(k, sp), e, 2) for k in bt.C5_SLOTS)
-    # L2->fabric bytes per launch of each (shape, plan) from the PMC passes of
-    # scripts/gpu_traffic_c5h.sh, summed over the six slots with the plans the search chose
-    traffic = None
-    tf = os.path.join(ROOT, "profiles", "traffic_c5h.json")
-    if os.path.exists(tf):
-        try:
-            tj = json.load(open(tf))
-            if tj["N"] == N and abs(tj["sparsity"] - sp) < 1e-9:
-                pl = tj["per_launch"]
-                for k in per_shape:
-                    per_shape[k]["traffic"] = pl.get(k, {}).get(per_shape[k]["plan"], {}).get("hbm_bytes")
-                if all(per_shape[k]["traffic"] for k in bt.C5_SLOTS):
-                    traffic = sum(per_shape[k]["traffic"] for k in bt.C5_SLOTS)
-        except Exception:
-            traffic = None
+    wall, ev_s = timed_batch(step, streams, steps, torch, marked=True)
+    ms_step = ev_s / steps * 1e3
+    nnz_l, flops_l, alg_l = layer_consts(N, sp)
+    plan_of = {k: (per_shape[k]["plan"] if per_shape else cand_key(choice[k])) for k in bt.C5_SHAPES}
+    traffic, traffic_per = layer_traffic(N, sp, plan_of)
+    if rs_per_shape is None and not args.no_rocsparse:
+        rs_per_shape = {}
+        for k, (m, n) in bt.C5_SHAPES.items():
+            row, col, val = coo[k]
+            copies = max(2, int(math.ceil(args.rotation_mb * 1e6 / (len(row) * 6 + n * N * 2))))
+            rs_per_shape[k] = rocsparse_baseline(m, n, N, row, col, val, min(copies, 20), dtype=1)
     rs_l = None
-    if all(per_shape[k]["rocsparse_f16"] for k in bt.C5_SHAPES):
-        rs_l = sum(per_shape[k]["rocsparse_f16"]["ms"] for k in bt.C5_SLOTS)
-    out = {
-        "metric": "SpMM GFLOP/s + achieved HBM GB/s vs rocSPARSE, OPT-30B 70%-pruned layer fp16 N=32 (north_star headline)",
-        "value": round(flops_l * args.steps / ev_s / 1e9, 1), "unit": "GFLOP/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms_step, 5), "higher_is_better": True, "scaling": "weak",
+    if rs_per_shape and all(rs_per_shape.get(k) for k in bt.C5_SHAPES):
+        rs_l = sum(rs_per_shape[k]["ms"] for k in bt.C5_SLOTS)
+    frac = alg_l / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS
+    line = {
+        "metric": "SpMM GFLOP/s + achieved HBM GB/s vs rocSPARSE, OPT-30B %d%%-pruned layer fp16 N=32 (north_star headline)"
+                  % round(sp * 100),
+        "value": round(flops_l * steps / ev_s / 1e9, 1), "unit": "GFLOP/s", "steps": steps, "warmup": warmup,
+        "ms_per_step": round(ms_step, 5), "higher_is_better": True,
         "timing": "HIP events around the K timed steps (all streams joined)",
-        "wall_ms_per_step": round(wall / args.steps * 1e3, 5),
-        "serial_kernels": {"ms": round(serial_ms, 5), "gflops": round(flops_l / (serial_ms * 1e-3) / 1e9, 1),
-                           "hbm_frac": round(alg_l / (serial_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                           "note": "sum of the six launches timed alone (per_shape kernel_us); the layer step "
-                                   "overlaps them over the streams"},
-        "vs_baseline": None, "dtype": "f16 (fp32 accumulate)",
+        "wall_ms_per_step": round(wall / steps * 1e3, 5),
+        "dtype": "f16 (fp32 accumulate)",
         "data": "synthetic (one seeded magnitude-pruned Gaussian per shape; each layer instance streams its own HBM "
                 "copy of A); OPT-30B weights are not available offline",
         "config": {"workload": f"OPT-30B decoder layer: 4 x 7168^2, 28672x7168, 7168x28672, {round(sp * 100)}% "
-                               f"unstructured, fp16, N={N}", "nnz": nnz_l,
-                   "plan": {k: per_shape[k]["plan"] for k in per_shape}, "kernel": {k: per_shape[k]["kernel"] for k in per_shape},
-                   "parallelism": "one GPU", "streams": args.streams, "grouped_launches": bool(args.group)},
+                               f"unstructured, fp16, N={N}", "nnz": nnz_l, "plan": plan_of,
+                   "kernel": {k: kernel_label(plans[k].info()) for k in plans},
+                   "launches_per_step": launches_per_step, "streams": args.streams,
+                   "grouped_launches": bool(args.group)},
         "roofline": {"bound": "hbm", "achieved": round(alg_l / (ms_step * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(alg_l / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "algorithmic_bytes_per_step": alg_l,
-                     "note": "whole layer step (six launches over the streams, HIP events); per-kernel fractions in "
-                             "per_shape.hbm_frac, their serial sum in serial_kernels"},
-        "per_shape": per_shape,
-        "layer_search": layer_search,
+                     "unit": "GB/s", "frac": round(frac, 4), "traffic": traffic, "algorithmic_bytes_per_step": alg_l,
+                     "note": "whole layer step (HIP events); traffic = the PMC bytes of the same (shape, plan) "
+                             "launches, profiles/traffic_c5h.json"},
         "speedup_vs_rocsparse": round(rs_l / ms_step, 3) if rs_l else None,
         "rocsparse_layer_ms": round(rs_l, 4) if rs_l else None,
+        "rocsparse_per_shape": rs_per_shape,
+        "layer_search": layer_search,
     }
+    line["target"] = dict(NORTH_STAR_TARGET)
+    line["met"] = bool(rs_l and rs_l / ms_step >= NORTH_STAR_TARGET["speedup_vs_rocsparse"]
+                       and frac >= NORTH_STAR_TARGET["hbm_frac"])
+    if traffic_per:
+        line["traffic_per_launch"] = traffic_per
+    return line, plans
+
+
+def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
+    """north_star headline as its own line: the per-shape plan search over
+    generalsparse_amd.batch.shape_candidates (event time with rotated replicas, rocSPARSE 7.2
+    CSR SpMM fp16 A/B fp32 C on the same matrix), the layer-level attn choice, then the timed
+    layer (headline_layer)."""
+    from generalsparse_amd import batch as bt
+    N, sp = args.N, args.sparsity
+    choice, per_shape = search_shapes(args, torch, gsa, ds, rank, local, dev, list(bt.C5_SHAPES), sp,
+                                      rocsparse=not args.no_rocsparse)
+    rs = {k: per_shape[k]["rocsparse_f16"] for k in per_shape} if not args.no_rocsparse else {}
+    out, plans = headline_layer(args, torch, gsa, ds, rank, local, dev, choice, args.steps, args.warmup,
+                                per_shape=per_shape, rs_per_shape=rs)
+    nnz_l, flops_l, alg_l = layer_consts(N, sp)
+    # the layer's kernels one at a time (each shape's search time = its own launch alone)
+    serial_ms = sum(per_shape[k]["kernel_us"] for k in bt.C5_SLOTS) * 1e-3
+    out["serial_kernels"] = {"ms": round(serial_ms, 5), "gflops": round(flops_l / (serial_ms * 1e-3) / 1e9, 1),
+                             "hbm_frac": round(alg_l / (serial_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                             "note": "sum of the six launches timed alone (per_shape kernel_us)"}
+    for k in per_shape:
+        per_shape[k]["traffic"] = out.get("traffic_per_launch", {}).get(k)
+    out.update({"n_gpus": world, "scaling": "weak", "vs_baseline": None, "per_shape": per_shape})
+    out["config"]["parallelism"] = "one GPU"
     if rank == 0:
         print(json.dumps(out), flush=True)
     for p in plans.values():
@@ -860,9 +926,25 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         share = {"c3": 8, "c4o": 64}.get(args.workload, 1)
         out["cpu_baseline"] = cpu_baseline(M, K, N, row, col, val, row_share=share)
+    plan.free()
+    del Bs, Cs
+    torch.cuda.empty_cache()
+    if args.workload == "c2" and world == 1 and not args.no_north_star and args.N == 32:
+        # the north_star target (OPT-30B 70%-pruned weights at N=32, >= 1.5x rocSPARSE and >= 50%
+        # of HBM) timed in the same run: one layer, the headline plans, no search
+        from generalsparse_amd import batch as bt
+        a2 = argparse.Namespace(**vars(args))
+        a2.group, a2.streams = 1, 1
+        try:
+            ns, plans = headline_layer(a2, torch, gsa, ds, rank, local, dev, {k: HEADLINE_CHOICE for k in bt.C5_SHAPES},
+                                       max(args.steps, 20), max(args.warmup, 10))
+            for p in plans.values():
+                p.free()
+            out["north_star"] = ns
+        except Exception as ex:  # the C2 line must not be lost to a failure of the extra object
+            out["north_star"] = {"error": f"{type(ex).__name__}: {ex}"}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    plan.free()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -96,6 +96,16 @@ class Batch:
     def run(self, stream=0):
         _lib.check(self._L.gs_spmm_batch(self._p, self._r, self._b, self._c, self.n, self.N, ctypes.c_void_p(stream)))
 
+    def launches(self):
+        """entries per launch, as run() enqueues them (gs_batch_launches): a grouped
+        k_mfma_ks_group launch carries up to 32 entries"""
+        cap = max(1, self.n)
+        out = (ctypes.c_int * cap)()
+        k = self._L.gs_batch_launches(self._p, self._r, self.n, self.N, out, cap)
+        if k < 0:
+            _lib.check(k)
+        return [out[i] for i in range(min(k, cap))]
+
 
 class Plan:
     """A GeneralSparse plan: metadata set + operator history + code generator +
@@ -276,6 +286,13 @@ class Plan:
     def set_array_entry(self, key, i, value):
         """metadata editing (tools / tests): entry i of an integer plan array"""
         _lib.check(self._L.gs_plan_array_set_u64(self._h, key.encode(), int(i), int(value)))
+        return self
+
+    def device_status(self, stream=0):
+        """synchronises `stream` and raises GsError (code GS_ERR_DEVICE) if a launch of this
+        plan reported a device fault since the last call (gs_plan_device_status: a K-split
+        combine that gave up waiting for a partial slab)"""
+        _lib.check(self._L.gs_plan_device_status(self._h, ctypes.c_void_p(stream)))
         return self
 
     def log(self):

@@ -68,6 +68,9 @@ SIGNATURES = {
                        ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
     "gs_spmm_rotate": ([ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                         ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
+    "gs_batch_launches": ([ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_int,
+                           ctypes.POINTER(ctypes.c_int), ctypes.c_int], ctypes.c_int),
+    "gs_plan_device_status": ([ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     "gs_plan_info_get": ([ctypes.c_void_p, ctypes.POINTER(GsPlanInfo)], ctypes.c_int),
     "gs_plan_array_count": ([ctypes.c_void_p], ctypes.c_int),
     "gs_plan_array_key": ([ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
@@ -117,7 +120,12 @@ class GsError(RuntimeError):
     pass
 
 
+GS_ERR_DEVICE = -4  # include/generalsparse.h: a kernel reported a fault in its device error word
+
+
 def check(rc):
     if rc != 0:
-        raise GsError(f"generalsparse error {rc}: {load().gs_last_error().decode()}")
+        e = GsError(f"generalsparse error {rc}: {load().gs_last_error().decode()}")
+        e.code = rc
+        raise e
     return rc

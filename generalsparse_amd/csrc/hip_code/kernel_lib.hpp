@@ -1564,6 +1564,48 @@ __device__ constexpr int vmcnt_imm() {
 // 8 bytes at a 2-byte-aligned address (k_mfma_kb / k_mfma_bm value windows)
 typedef uint32_t u32x2_a2 __attribute__((ext_vector_type(2), aligned(2)));
 
+// K-split combine: the last ticket holder's read of 4 words of another workgroup's slab
+// (each word tagged in its low mantissa bit): agent-scope (sc1) loads until every tag reads
+// `tag`.  The writer holds an earlier ticket, so it is resident and its stores are issued or
+// about to be; the wait is bounded by wall time (s_memrealtime, 100 MHz: 0.2 s) all the same.
+// Past the bound the words read as NaN and bit 0 of the plan replica's device error word
+// (`err`, the word after the arrival counters) is set: gs_plan_device_status reports it as
+// GS_ERR_DEVICE, so a lost slab is an error at the C ABI, not silent NaNs in C.  `force`
+// (experiments build, KS_FORCE_TIMEOUT) takes the timeout path at once (the test of that chain).
+__device__ __forceinline__ u32x4 ks_slab_wait(const uint32_t *src, uint32_t tag, uint32_t *err, bool force) {
+    u32x4 w;
+    auto load4 = [&]() {
+#pragma unroll
+        for (int i = 0; i < 4; i++) w[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    auto stale = [&]() { return (((w[0] ^ tag) | (w[1] ^ tag) | (w[2] ^ tag) | (w[3] ^ tag)) & 1u) != 0u; };
+    bool lost = force;
+    if (!lost) {
+        load4();
+        if (stale()) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            do {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {
+                    lost = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+                load4();
+            } while (stale());
+        }
+    }
+    if (lost) {
+        w = u32x4{0x7fc00000u | tag, 0x7fc00000u | tag, 0x7fc00000u | tag, 0x7fc00000u | tag};
+        __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return w;
+}
+#ifdef GS_EXPERIMENTS
+#define GS_KS_FORCE(prio) (((prio) & 16u) != 0u)
+#else
+#define GS_KS_FORCE(prio) false
+#endif
+
 // STAMPS (diagnostic build only, gs_debug_mfma_timeline): lane 0 of every wave records
 // s_memtime into stamps[(workgroup * W + wave) * 32 + slot]: 0 start, 1 loads issued,
 // 3 + i after step i (i < 16), 20 loop done, 21 reduced, 22 end
@@ -1728,16 +1770,16 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
         }
     };
     // prio (KS_PRIO): the younger half of the waves (the second wave of each SIMD, the one
-    // that loses issue arbitration) at s_setprio 1 -- 1: for its whole loop, 2: for the
+    // that loses issue arbitration) at s_setprio 1 -- prio & 3 = 1: for its whole loop, 2: for the
     // first half of its steps
     const bool young = wv >= W / 2u;
-    if (prio && young) __builtin_amdgcn_s_setprio(1);
+    if ((prio & 3u) && young) __builtin_amdgcn_s_setprio(1);
     for (uint32_t i0 = 0; i0 < nsw; i0 += D) {
 #pragma unroll
         for (int d = 0; d < D; d++) step(i0 + d, NX[d], CN[d], P[d], V[d], BR[d]);
-        if (prio == 2u && young && i0 + D >= nsw / 2u && i0 < nsw / 2u) __builtin_amdgcn_s_setprio(0);
+        if ((prio & 3u) == 2u && young && i0 + D >= nsw / 2u && i0 < nsw / 2u) __builtin_amdgcn_s_setprio(0);
     }
-    if (prio && young) __builtin_amdgcn_s_setprio(0);
+    if ((prio & 3u) && young) __builtin_amdgcn_s_setprio(0);
     GS_KS_STAMP(20u);
     // ---- K-split ticket: wave 0 takes its row block's arrival ticket as soon as its own
     // loop ends, so the add's round trip overlaps the partial-tile reduction below
@@ -1845,6 +1887,7 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
     if (tid == 0) __hip_atomic_store(arr, tag << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const f4v *base = reinterpret_cast<const f4v *>(slabs) + blockIdx.y * NI;
     const size_t qstride = (size_t)gridDim.y * NI;  // slab of (g, qq) = base + (g*S + qq) * qstride
+    uint32_t *err = arrivals + (size_t)(nwg / S) * gridDim.y;  // the replica's device error word
     for (uint32_t t = tid; t < NI; t += NT) {
         f4v sum = {0.f, 0.f, 0.f, 0.f};
         for (uint32_t qq = 0; qq < S; qq++) {
@@ -1852,21 +1895,8 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
             if (qq == q) {  // truncated as a published word is (whichever workgroup is last: deterministic)
                 w = tagged(item_sum(t));
             } else {
-                const uint32_t *src = reinterpret_cast<const uint32_t *>(base + ((size_t)g * S + qq) * qstride + t);
-                auto load4 = [&]() {
-#pragma unroll
-                    for (int i = 0; i < 4; i++) w[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                };
-                load4();
-                // bounded wait (a writer that never stores would be a bug: NaN, not a hang)
-                for (uint32_t tries = 0; ((w[0] ^ tag) | (w[1] ^ tag) | (w[2] ^ tag) | (w[3] ^ tag)) & 1u; tries++) {
-                    if (tries > (1u << 20)) {
-                        w = u32x4{0x7fc00000u | tag, 0x7fc00000u | tag, 0x7fc00000u | tag, 0x7fc00000u | tag};
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                    load4();
-                }
+                w = ks_slab_wait(reinterpret_cast<const uint32_t *>(base + ((size_t)g * S + qq) * qstride + t), tag, err,
+                                 GS_KS_FORCE(prio));
             }
             w[0] &= ~1u; w[1] &= ~1u; w[2] &= ~1u; w[3] &= ~1u;
             f4v x;
@@ -1896,8 +1926,9 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
 
 // ---------------------------------------------------------------------------
 // k_mfma_ks_group -- several k_mfma_ks launches of one instantiation as one grid (a layer's
-// or a batch's SpMMs; gs_spmm_batch): entry i owns workgroups [begin[i], begin[i+1]) and runs
-// them as its own launch would.  One launch instead of one per matrix: no kernel boundary
+// or a batch's SpMMs; gs_spmm_batch): entry i owns workgroups [begin[i], begin[i] + nwg_i) and
+// runs them as its own launch would (begin[i] a multiple of 8: the entry's block numbers keep
+// the XCD residues xcd_block assumes; the blocks up to begin[i+1] exit at once).  One launch instead of one per matrix: no kernel boundary
 // between the matrices, and one matrix's last workgroups overlap the next one's first.  The
 // entries are kernel arguments (ks_group_args, read through the kernarg segment with scalar
 // loads); every entry has its own plan replica (distinct K-range tickets and slabs).
@@ -1928,6 +1959,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks_group(ks_group_args args) {
         if ((uint32_t)i < n && args.begin[i] <= bx) sel = (uint32_t)i;
     sel = __builtin_amdgcn_readfirstlane(sel);
     const ks_entry &e = args.e[sel];  // kernel arguments: scalar loads at a computed offset
+    if (bx - args.begin[sel] >= e.nwg) return;  // padding up to the next entry's multiple of 8
     ks_body<CT, RT, W, D, MAXG, false>(e.tbr, e.tP, e.tV, e.steps, e.B, e.C, e.K, args.N, e.S, e.NS, e.nwg, e.row_base,
                                        e.slabs, e.arrivals, nullptr, bx - args.begin[sel], args.pad[0]);
 }
@@ -2100,12 +2132,12 @@ __device__ __forceinline__ void kb_body(const uint32_t *__restrict__ bmtb_first_
         }
     };
     const bool young = wv >= W / 2u;
-    if (prio && young) __builtin_amdgcn_s_setprio(1);
+    if ((prio & 3u) && young) __builtin_amdgcn_s_setprio(1);
     for (uint32_t i0 = 0; i0 < nsw; i0 += D) {
 #pragma unroll
         for (int d = 0; d < D; d++) step(i0 + d, NX[d], NB[d], NE[d], RC[d], RL[d], VR[d], BR[d]);
     }
-    if (prio && young) __builtin_amdgcn_s_setprio(0);
+    if ((prio & 3u) && young) __builtin_amdgcn_s_setprio(0);
     GS_KB_STAMP(20u);
     // ---- K-split ticket: wave 0 takes its row block's arrival ticket as soon as its own
     // loop ends, so the add's round trip overlaps the partial-tile reduction below
@@ -2213,6 +2245,7 @@ __device__ __forceinline__ void kb_body(const uint32_t *__restrict__ bmtb_first_
     if (tid == 0) __hip_atomic_store(arr, tag << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const f4v *base = reinterpret_cast<const f4v *>(slabs) + blockIdx.y * NI;
     const size_t qstride = (size_t)gridDim.y * NI;  // slab of (g, qq) = base + (g*S + qq) * qstride
+    uint32_t *err = arrivals + (size_t)(nwg / S) * gridDim.y;  // the replica's device error word
     for (uint32_t t = tid; t < NI; t += NT) {
         f4v sum = {0.f, 0.f, 0.f, 0.f};
         for (uint32_t qq = 0; qq < S; qq++) {
@@ -2220,21 +2253,8 @@ __device__ __forceinline__ void kb_body(const uint32_t *__restrict__ bmtb_first_
             if (qq == q) {  // truncated as a published word is (whichever workgroup is last: deterministic)
                 w = tagged(item_sum(t));
             } else {
-                const uint32_t *src = reinterpret_cast<const uint32_t *>(base + ((size_t)g * S + qq) * qstride + t);
-                auto load4 = [&]() {
-#pragma unroll
-                    for (int i = 0; i < 4; i++) w[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                };
-                load4();
-                // bounded wait (a writer that never stores would be a bug: NaN, not a hang)
-                for (uint32_t tries = 0; ((w[0] ^ tag) | (w[1] ^ tag) | (w[2] ^ tag) | (w[3] ^ tag)) & 1u; tries++) {
-                    if (tries > (1u << 20)) {
-                        w = u32x4{0x7fc00000u | tag, 0x7fc00000u | tag, 0x7fc00000u | tag, 0x7fc00000u | tag};
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                    load4();
-                }
+                w = ks_slab_wait(reinterpret_cast<const uint32_t *>(base + ((size_t)g * S + qq) * qstride + t), tag, err,
+                                 GS_KS_FORCE(prio));
             }
             w[0] &= ~1u; w[1] &= ~1u; w[2] &= ~1u; w[3] &= ~1u;
             f4v x;

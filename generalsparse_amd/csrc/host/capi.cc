@@ -776,39 +776,85 @@ int gs_spmm_rotate(gs_plan_t *p, int count, int first, const void *const *B_ptrs
     });
 }
 
+namespace {
+// the launches of a batch (gs_spmm_batch): runs of consecutive entries that are one grouped
+// k_mfma_ks launch (key != 0; up to 32, each (plan, replica) once), single entries otherwise
+struct batch_launch {
+    uint32_t key;
+    std::vector<int> idx;
+};
+std::vector<batch_launch> plan_batch(gs_plan_t *const *plans, const int *replicas, int n, int N) {
+    std::vector<batch_launch> out;
+    for (int i = 0; i < n; i++) {
+        gs_plan *p = plans[i];
+        GS_CHECK(p, "bad batch entry " + std::to_string(i));
+        GS_CHECK(replicas[i] >= 0 && (size_t)replicas[i] < p->st.dev.replicas.size(),
+                 "batch entry " + std::to_string(i) + ": bad replica index");
+        const uint32_t k = divided(p) ? 0u : gs::ks_group_key(p->st, (uint32_t)N);
+        bool join = k != 0 && !out.empty() && out.back().key == k && out.back().idx.size() < (size_t)gsk::kKsGroupMax;
+        if (join)  // a (plan, replica) twice in one grid would share tickets and slabs
+            for (int j : out.back().idx) join &= !(plans[j] == p && replicas[j] == replicas[i]);
+        if (join)
+            out.back().idx.push_back(i);
+        else
+            out.push_back({k, {i}});
+    }
+    return out;
+}
+}  // namespace
+
 int gs_spmm_batch(gs_plan_t *const *plans, const int *replicas, const void *const *B, void *const *C, int n, int N,
                   gs_stream_t stream) {
     return guard([&] {
         GS_CHECK(plans && replicas && B && C && n >= 0 && N > 0, "bad argument");
         hipStream_t s = (hipStream_t)stream;
-        std::vector<gs::ks_group_item> grp;
-        uint32_t key = 0;
-        auto flush = [&] {
-            if (grp.size() == 1)
-                gs::launch_spmm(*const_cast<gs::plan_state *>(grp[0].p), grp[0].replica, grp[0].B, grp[0].C, (uint32_t)N, s);
-            else if (!grp.empty())
-                gs::launch_ks_group(grp, (uint32_t)N, s);
-            grp.clear();
-            key = 0;
-        };
-        for (int i = 0; i < n; i++) {
-            gs_plan *p = plans[i];
-            GS_CHECK(p && B[i] && C[i], "bad batch entry " + std::to_string(i));
-            GS_CHECK(replicas[i] >= 0 && (size_t)replicas[i] < p->st.dev.replicas.size(),
-                     "batch entry " + std::to_string(i) + ": bad replica index");
-            const uint32_t k = divided(p) ? 0u : gs::ks_group_key(p->st, (uint32_t)N);
-            if (k == 0) {
-                flush();
-                spmm_all(p, replicas[i], B[i], C[i], (uint32_t)N, s);
+        for (int i = 0; i < n; i++) GS_CHECK(B[i] && C[i], "bad batch entry " + std::to_string(i));
+        for (const batch_launch &l : plan_batch(plans, replicas, n, N)) {
+            if (l.idx.size() == 1) {
+                const int i = l.idx[0];
+                if (l.key == 0)
+                    spmm_all(plans[i], replicas[i], B[i], C[i], (uint32_t)N, s);
+                else
+                    gs::launch_spmm(plans[i]->st, replicas[i], B[i], C[i], (uint32_t)N, s);
                 continue;
             }
-            bool dup = false;  // a (plan, replica) twice in one grid would share tickets and slabs
-            for (const auto &x : grp) dup |= x.p == &p->st && x.replica == replicas[i];
-            if (k != key || grp.size() == (size_t)gsk::kKsGroupMax || dup) flush();
-            key = k;
-            grp.push_back({&p->st, replicas[i], B[i], C[i]});
+            std::vector<gs::ks_group_item> grp;
+            for (int i : l.idx) grp.push_back({&plans[i]->st, replicas[i], B[i], C[i]});
+            gs::launch_ks_group(grp, (uint32_t)N, s);
         }
-        flush();
+    });
+}
+
+int gs_batch_launches(gs_plan_t *const *plans, const int *replicas, int n, int N, int *entries_per_launch, int cap) {
+    int count = 0;
+    const int rc = guard([&] {
+        GS_CHECK(plans && replicas && n >= 0 && N > 0 && (cap == 0 || entries_per_launch), "bad argument");
+        const auto ls = plan_batch(plans, replicas, n, N);
+        count = (int)ls.size();
+        for (int i = 0; i < count && i < cap; i++) entries_per_launch[i] = (int)ls[(size_t)i].idx.size();
+    });
+    return rc < 0 ? rc : count;
+}
+
+int gs_plan_device_status(gs_plan_t *p, gs_stream_t stream) {
+    return guard([&] {
+        GS_CHECK(p, "null plan");
+        GS_HIP(hipStreamSynchronize((hipStream_t)stream));
+        std::string what;
+        for (gs::plan_state *k : kernel_states(p, false)) {
+            if (!k->uploaded || !k->dev.err_at) continue;
+            for (size_t r = 0; r < k->dev.replicas.size(); r++) {
+                uint32_t *w = k->dev.replicas[r].t2 + k->dev.err_at;
+                uint32_t v = 0;
+                GS_HIP(hipMemcpy(&v, w, sizeof(v), hipMemcpyDeviceToHost));
+                if (!v) continue;
+                GS_HIP(hipMemset(w, 0, sizeof(v)));  // reported once
+                what += (what.empty() ? "" : ", ") + k->dev.kernel + " replica " + std::to_string(r);
+            }
+        }
+        if (!what.empty())
+            throw gs::gs_error("K-split combine timed out waiting for a partial slab (" + what +
+                                   "): the affected rows of C hold NaN", GS_ERR_DEVICE);
     });
 }
 

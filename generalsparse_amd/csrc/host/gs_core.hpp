@@ -101,6 +101,7 @@ struct config_t {
     int64_t MP_SOLO = 16;        // k_merge_rows: rows of at most this many nonzeros are one slot's
     int64_t KS_WAVES = 8;        // k_mfma_ks waves per workgroup (8 or 16)
     int64_t KS_SPLIT = 0;        // k_mfma_ks K ranges per row block (0: the fewest that fit LDS and fill the CUs)
+    int64_t KS_FORCE_TIMEOUT = 0;  // experiments build: the K-split combine takes its timeout path (test of the error word)
     int64_t KS_PRIO = 1;         // k_mfma_ks: the younger waves at s_setprio 1 (1: whole loop, 2: first half, 0: off)
 };
 // Process-wide config: loaded once from $GS_CONFIG or ./global_config.json if

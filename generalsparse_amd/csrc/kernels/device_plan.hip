@@ -333,7 +333,9 @@ void upload_plan(plan_state &p, int dtype, int device) {
             if (kt.S > 1) {
                 const uint32_t nt = ks_col_tiles(mc.N), CT = ks_ct(mc.N);
                 a.ws = dev_copy(d, std::vector<float>((size_t)nb * kt.S * nt * 256 * kt.RT * CT, 0.f));
-                a.t2 = dev_copy(d, std::vector<uint32_t>((size_t)nb * nt, 0u));  // arrival counters
+                // arrival counters, then the replica's device error word (ks_slab_wait)
+                a.t2 = dev_copy(d, std::vector<uint32_t>((size_t)nb * nt + 1u, 0u));
+                d.err_at = (uint64_t)nb * nt;
             }
             return true;
         }
@@ -365,7 +367,8 @@ void upload_plan(plan_state &p, int dtype, int device) {
                 const uint32_t nt = ks_col_tiles(mc.N), CT = ks_ct(mc.N);
                 a.ws = dev_copy(d, std::vector<float>((size_t)nb * bt.S * nt * 256 * bt.RT * CT, 0.f));
                 // arrival counters: per (row block, column tile), per row tile too for k_mfma_bm2
-                a.t2 = dev_copy(d, std::vector<uint32_t>((size_t)nb * nt * (bt.v2 ? bt.RT : 1u), 0u));
+                a.t2 = dev_copy(d, std::vector<uint32_t>((size_t)nb * nt * (bt.v2 ? bt.RT : 1u) + 1u, 0u));
+                if (bt.kb) d.err_at = (uint64_t)nb * nt;  // k_mfma_kb: the device error word after the counters
             }
             return true;
         }

@@ -18,6 +18,13 @@ namespace gs {
 
 namespace {
 
+// k_mfma_ks's prio argument: KS_PRIO in bits 0..1; bit 4 (experiments build) forces the K-split
+// combine's timeout path (KS_FORCE_TIMEOUT, the test of the device error word)
+uint32_t ks_prio_arg() {
+    const config_t c = get_config();
+    return (uint32_t)(c.KS_PRIO & 3) | (c.KS_FORCE_TIMEOUT ? 16u : 0u);
+}
+
 template <class KERN>
 void grant_lds(int device, KERN kern, size_t bytes) {
     // dynamic LDS above 64 KB is opted into once per kernel and device
@@ -56,7 +63,7 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
             hipLaunchKernelGGL(kd, dim3((uint32_t)d.n_rows_aux * d.ksplit, ks_col_tiles(N)), dim3(64 * W), d.lds_bytes, s,
                                a.t0, (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, (const gsk::u32x2 *)a.t1, B, C,
                                (uint32_t)p.K, N, d.ksplit, d.ks_ns, (uint32_t)d.n_rows_aux * d.ksplit, (uint32_t)d.row_base,
-                               a.ws, a.t2, stamps, (uint32_t)get_config().KS_PRIO);
+                               a.ws, a.t2, stamps, ks_prio_arg());
             HIP_OK(hipGetLastError());
             return;
         }
@@ -71,7 +78,7 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
     hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit, ks_col_tiles(N)), dim3(64 * W), d.lds_bytes, s, a.t0,
                        (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, (const gsk::u32x2 *)a.t1, B, C,
                        (uint32_t)p.K, N, d.ksplit, d.ks_ns, (uint32_t)d.n_rows_aux * d.ksplit, (uint32_t)d.row_base, a.ws, a.t2, stamps,
-                       (uint32_t)get_config().KS_PRIO);
+                       ks_prio_arg());
     HIP_OK(hipGetLastError());
 }
 
@@ -143,7 +150,7 @@ void launch_kb_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
     const uint32_t nwg = (uint32_t)d.n_rows_aux * d.ksplit;
     hipLaunchKernelGGL(kern, dim3(nwg, ks_col_tiles(N)), dim3(64 * kKsWaves), d.lds_bytes, s, a.t0, (const uint2 *)a.tcol,
                        a.t1, (const gsk::f16 *)a.tval, B, C, (uint32_t)p.K, N, d.ksplit, d.ks_ns, nwg,
-                       (uint32_t)d.row_base, a.ws, a.t2, nullptr, (uint32_t)get_config().KS_PRIO);
+                       (uint32_t)d.row_base, a.ws, a.t2, nullptr, ks_prio_arg());
     HIP_OK(hipGetLastError());
 }
 
@@ -227,12 +234,14 @@ void launch_ks_group_k(const std::vector<ks_group_item> &it, uint32_t N, hipStre
         e.nwg = (uint32_t)d.n_rows_aux * d.ksplit;
         e.row_base = (uint32_t)d.row_base;
         args.begin[i] = wg;
-        wg += e.nwg;
+        // each entry starts on a multiple of 8 workgroups (idle ones in between exit at once), so
+        // its entry-relative block numbers share XCDs as the global ones do (xcd_block)
+        wg += (e.nwg + 7u) & ~7u;
     }
     args.begin[it.size()] = wg;
     args.n = (uint32_t)it.size();
     args.N = N;
-    args.pad[0] = (uint32_t)get_config().KS_PRIO;
+    args.pad[0] = ks_prio_arg();
     grant_lds(it[0].p->dev.device, kern, lds);
     hipLaunchKernelGGL(kern, dim3(wg, ks_col_tiles(N)), dim3(64 * kKsWaves), lds, s, args);
     HIP_OK(hipGetLastError());

@@ -35,7 +35,8 @@ extern "C" {
 typedef struct gs_plan gs_plan_t;
 typedef void *gs_stream_t; /* hipStream_t; NULL = default stream */
 
-enum { GS_OK = 0, GS_ERR = -1, GS_ERR_ARG = -2, GS_ERR_HIP = -3 };
+enum { GS_OK = 0, GS_ERR = -1, GS_ERR_ARG = -2, GS_ERR_HIP = -3,
+       GS_ERR_DEVICE = -4 /* a kernel reported a fault in its device error word (gs_plan_device_status) */ };
 enum { GS_F32 = 0, GS_F16 = 1 };
 
 typedef struct {
@@ -120,6 +121,17 @@ int gs_spmm_rotate(gs_plan_t *p, int count, int first, const void *const *B_ptrs
  * (k_mfma_ks_group); the others launch as gs_spmm_replica does. */
 int gs_spmm_batch(gs_plan_t *const *plans, const int *replicas, const void *const *B, void *const *C, int n, int N,
                   gs_stream_t stream);
+
+/* how gs_spmm_batch would enqueue the batch: returns the number of launches (< 0: error) and
+ * the entries each launch carries in entries_per_launch[0 .. min(count, cap)) (a grouped
+ * k_mfma_ks_group launch carries up to 32) */
+int gs_batch_launches(gs_plan_t *const *plans, const int *replicas, int n, int N, int *entries_per_launch, int cap);
+/* synchronises `stream` and reads the plan's device error words (every replica, every
+ * sub-matrix kernel): GS_ERR_DEVICE when a launch reported a fault since the last call --
+ * a K-split combine that gave up waiting for a partial slab (its rows of C are NaN) --
+ * 0 otherwise.  The words are cleared once reported.  The reference asserts on the host
+ * after its kernels (executor.cc:6-104 checks cudaGetLastError); this is the device side. */
+int gs_plan_device_status(gs_plan_t *p, gs_stream_t stream);
 
 int gs_plan_info_get(gs_plan_t *p, gs_plan_info *info);
 int gs_plan_array_count(gs_plan_t *p);

@@ -1,34 +1,54 @@
 #!/bin/bash
-# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel stats and
-# the HBM-traffic PMC passes of the bench's best plan.
-# Every GPU step has its own time limit; a fault/abort/timeout (exit >= 124 or
-# 134/139) ends the session, an ordinary test failure (exit 1) does not.
+# One GPU-box session (replaces the per-round scripts/gpu_r0*.sh one-offs, which live on in
+# git history).  Usage: TAG=r05a PARTS="tests bench prof" WLS="c2 c5h" scripts/gpu_session.sh
+# Parts (any subset, run in this order):
+#   tests   the -m gpu suite, then smoke()
+#   bench   one bench line per workload in $WLS (steps / warm-up from scripts/session_params.sh)
+#   prof    rocprofv3 --kernel-trace --stats of the same bench command, per workload
+#   pmc     FETCH_SIZE / WRITE_SIZE passes per workload in $PMC_WLS (traffic_<wl>.json)
+#   sq      SQ / GRBM passes (MFMA utilisation) per workload in $PMC_WLS
+# Every GPU step runs under its own time limit; the first failing step ends the session
+# (set -e), so nothing else touches the GPU after a fault, abort or timeout.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out
-OUT=gpurun_out
-TAG=${1:-r01}
-STEPS=${STEPS:-200}
-ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ] || [ "$rc" -eq 5 ]; }
-step() {
-  local name=$1; shift
-  echo "== $name: $*" | tee -a $OUT/session.log
-  "$@" > $OUT/$name.log 2>&1
-  local rc=$?
-  echo "== $name exit $rc" | tee -a $OUT/session.log
-  tail -3 $OUT/$name.log
-  ok $rc || { echo "stopping after $name (exit $rc)"; exit $rc; }
-}
-rocm-smi --showproductname > $OUT/rocm_smi.log 2>&1 || true
-nproc > $OUT/nproc.log; lscpu | grep -E "Model name|^CPU\(s\)" >> $OUT/nproc.log || true
-[ -n "$SKIP_TESTS" ] || step pytest_gpu timeout -k 10 900 python -m pytest tests -m gpu -q
-step smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench timeout -k 10 600 python bench.py --steps $STEPS --warmup 20
+. scripts/session_params.sh
+TAG=${TAG:-r05}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
 export TMPDIR=/tmp
-step prof timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o prof -- python3 bench.py --steps $STEPS --warmup 20 --no-cpu --no-rocsparse
-BEST=$(python3 -c "
-import json
-d=[json.loads(l) for l in open('$OUT/bench.log') if l.startswith('{')][-1]
-n,a=d['config']['plan'].split('('); a=a.rstrip(')').split(','); print(n,a[0],a[1])" 2>/dev/null || echo "block_total 20 1")
-step pmc_fetch timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_$TAG/fetch -o p -- python3 scripts/prof_one.py $BEST f16 32 100
-step pmc_write timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_$TAG/write -o p -- python3 scripts/prof_one.py $BEST f16 32 100
-echo "session done"
+set -e
+has() { [[ " $PARTS " == *" $1 "* ]]; }
+if has tests; then
+  timeout -k 10 1100 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
+    > $OUT/gputest.log 2>&1 || { tail -40 $OUT/gputest.log; exit 1; }
+  tail -2 $OUT/gputest.log
+  timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+  tail -8 $OUT/smoke.log
+fi
+for wl in $WLS; do
+  steps=$(bench_steps $wl); psteps=$(prof_steps $wl)
+  if has bench; then
+    timeout -k 10 900 python3 -u bench.py --workload $wl --steps $steps --warmup 20 ${BENCH_ARGS:-} > $OUT/bench_$wl.log 2>&1
+    tail -1 $OUT/bench_$wl.log | cut -c1-300
+  fi
+  if has prof; then
+    timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$wl -o p -- \
+      python3 bench.py --workload $wl --steps $psteps --warmup 10 --no-cpu --no-rocsparse ${BENCH_ARGS:-} > $OUT/prof_$wl.log 2>&1
+    echo "prof $wl done"
+  fi
+done
+for wl in ${PMC_WLS:-}; do
+  cmd=$(pmc_cmd $wl)
+  if has pmc; then
+    for c in FETCH_SIZE WRITE_SIZE; do
+      timeout -s KILL 600 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $OUT/pmc_$wl/$c -o p -- $cmd \
+        > $OUT/pmc_$wl/$c.log 2>&1 || { mkdir -p $OUT/pmc_$wl; echo "pmc $wl $c failed"; exit 1; }
+    done
+    echo "pmc $wl done"
+  fi
+  if has sq; then
+    timeout -s KILL 600 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
+      --output-format csv -d $OUT/sq_$wl -o p -- $cmd > $OUT/sq_$wl.log 2>&1
+    echo "sq $wl done"
+  fi
+done
+echo "session $TAG done"

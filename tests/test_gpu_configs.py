@@ -272,6 +272,49 @@ def test_batch_and_headline_plans_against_torch(sp, shape, cand, kernel, ksplit)
     plan.free()
 
 
+def test_headline_layer_one_grouped_launch_against_torch():
+    """The north_star headline layer exactly as bench.py times it: one OPT-30B
+    decoder layer at 70% -- 4 x attn 7168^2, fc1 28672x7168, fc2 7168x28672, every shape on
+    block_total(112,1) (k_mfma_ks, 112-row blocks; attn and fc2 in 4 K ranges, fc1 in 1) --
+    through one gsa.Batch.  The batch must be ONE k_mfma_ks_group launch carrying all six
+    entries, and every C must equal a torch fp32 dense product of the same fp16 inputs (fp16
+    tolerance) and, bit for bit, the same plan launched alone."""
+    N = 32
+    plans, entries, refs = {}, [], []
+    g = torch.Generator(device=DEV)
+    g.manual_seed(21)
+    for k in ("attn", "fc1", "fc2"):
+        m, n = bt.C5_SHAPES[k]
+        row, col, val = ds.pruned_weight(m, n, 0.7, bt.shape_seed(0, k))
+        p = gsa.Plan.from_coo(m, n, row, col, val).run_pipeline("block_total", N, 112, 1).compile().upload("f16", 0)
+        info = p.info()
+        assert info["device_kernel"] == "k_mfma_ks" and info["ksplit"] == (1 if k == "fc1" else 4), info
+        if k == "attn":
+            for _ in range(3):
+                p.add_replica()
+        plans[k] = (p, row, col, val)
+    for slot, k in enumerate(bt.C5_SLOTS):
+        p, row, col, val = plans[k]
+        m, n = bt.C5_SHAPES[k]
+        rep = bt.C5_SLOTS[:slot].count(k)
+        B = (torch.rand((n, N), device=DEV, generator=g) * 2 - 1).half()
+        C = torch.full((m, N), float("nan"), device=DEV, dtype=torch.float16)
+        entries.append((p, rep, B, C))
+        refs.append(dense_ref(m, n, row, col, val, B))
+    bat = gsa.Batch(entries, N)
+    assert bat.launches() == [6], bat.launches()
+    bat.run(torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for (p, rep, B, C), ref in zip(entries, refs):
+        check(C.float().cpu().numpy(), ref, "f16")
+        alone = p.spmm(B, replica=rep)
+        torch.cuda.synchronize()
+        assert torch.equal(alone, C)
+    for p, *_ in plans.values():
+        p.device_status()
+        p.free()
+
+
 def test_c5_two_layer_batch_sequence():
     """two layers of the batch on one rank through generalsparse_amd.batch (bench.py run_c5):
     every launch of the sequence, with its replica and its B/C pair, gives that shape's

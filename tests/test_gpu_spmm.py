@@ -470,6 +470,64 @@ def test_mfma_ks_known_answer_and_c2():
     assert torch.equal(plan.spmm(B * 2).float(), 2 * C)  # linearity, deterministic
 
 
+def test_c2_driver_plan_block_total_40_against_torch():
+    """The plan the driver's C2 line runs: block_total(40,1) on k_mfma_ks with
+    two K ranges (128 row blocks of 40 rows = 256 workgroups), at full C2 size against a torch
+    fp32 dense product of the same fp16 inputs; a second launch into a NaN-filled C is the
+    same bit for bit, linearity is exact, and the device error word stays clear."""
+    M = K = 5120
+    N = 32
+    r, c, v = ds.pruned_weight(M, K, 0.7, 13)
+    A = torch.zeros((M, K), dtype=torch.float32)
+    A[torch.from_numpy(r.astype(np.int64)), torch.from_numpy(c.astype(np.int64))] = torch.from_numpy(v).half().float()
+    B = torch.randn((K, N), device=DEV, dtype=torch.float16)
+    ref = A.to(DEV) @ B.float()
+    plan = gsa.Plan.from_coo(M, K, r, c, v).run_pipeline("block_total", N, 40, 1).compile().upload("f16", 0)
+    info = plan.info()
+    assert info["device_kernel"] == "k_mfma_ks" and info["ksplit"] == 2, info
+    C = plan.spmm(B).float()
+    err = ((C - ref).abs() / ref.abs().clamp(min=1.0)).max().item()
+    assert err <= 1e-1, err
+    C2 = torch.full((M, N), float("nan"), device=DEV, dtype=torch.float16)
+    plan.spmm(B, C=C2)
+    assert torch.equal(C2.float(), C)
+    assert torch.equal(plan.spmm(B * 2).float(), 2 * C)
+    plan.device_status()
+    plan.free()
+
+
+def test_ks_combine_timeout_is_reported_at_the_abi(mfma_everywhere):
+    """A K-split combine that gives up waiting for a partial slab sets the replica's device
+    error word: gs_plan_device_status reports GS_ERR_DEVICE once and clears it (VERDICT r04
+    #8).  The timeout path is forced by the experiments build's KS_FORCE_TIMEOUT; the
+    default build refuses that switch, and there a clean run reports nothing."""
+    r, c, v = ds.pruned_weight(640, 2048, 0.7, 5)
+    plan = gsa.Plan.from_coo(640, 2048, r, c, v).run_pipeline("block_total", 32, 80, 1).compile().upload("f16", 0)
+    assert plan.info()["device_kernel"] == "k_mfma_ks" and plan.info()["ksplit"] > 1
+    B = torch.from_numpy(np.random.default_rng(3).uniform(-1, 1, (2048, 32)).astype(np.float16)).to(DEV)
+    good = plan.spmm(B)
+    plan.device_status()
+    from build_flags import EXPERIMENTS
+    if not EXPERIMENTS:
+        with pytest.raises(gsa.GsError):
+            gsa.set_config("KS_FORCE_TIMEOUT", 1)
+        plan.free()
+        return
+    gsa.set_config("KS_FORCE_TIMEOUT", 1)
+    try:
+        bad = plan.spmm(B)
+        with pytest.raises(gsa.GsError) as ei:
+            plan.device_status()
+        assert ei.value.code == -4 and "timed out" in str(ei.value)
+        assert torch.isnan(bad.float()).any()
+    finally:
+        gsa.set_config("KS_FORCE_TIMEOUT", 0)
+    plan.device_status()  # reported once, then clear
+    assert torch.equal(plan.spmm(B), good)
+    plan.device_status()
+    plan.free()
+
+
 @pytest.mark.parametrize("kernel", ["k_mfma_rows", "k_mfma_ks"])
 def test_mfma_unsorted_columns_and_duplicates(kernel, mfma_everywhere):
     """the reference accepts any column order inside a row and its gather kernels
