@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Matrix-core utilisation of a kernel from one rocprofv3 --pmc pass (SURVEY
+§8d): usage mfma_util.py <pmc dir> <kernel substring> <out.json> <workload>
+[mfma instructions per dispatch] [cycles per mfma].
+
+Counters (scripts/gpu_session.sh part `sq`): SQ_VALU_MFMA_BUSY_CYCLES (matrix-pipe busy cycles,
+summed over every SIMD of the chip), GRBM_GUI_ACTIVE (GPU-busy cycles, summed over the 8 XCDs,
+MI355X_MICROARCH.md DVFS item), SQ_WAVE_CYCLES / SQ_BUSY_CYCLES (context).
+  mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)
+i.e. the fraction of the kernel's busy cycles, per SIMD, in which its matrix pipe was busy.
+With the analytic instruction count the same ratio is also given from first principles:
+  mfma_util_analytic = n_mfma x cycles per MFMA / (GRBM_GUI_ACTIVE / 8 x 1024)."""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+from collections import defaultdict
+
+SIMDS = 1024  # 256 CUs x 4 SIMDs
+XCDS = 8
+
+
+def main():
+    d, kern, dst, wl = sys.argv[1:5]
+    n_mfma = float(sys.argv[5]) if len(sys.argv) > 5 else None
+    cyc = float(sys.argv[6]) if len(sys.argv) > 6 else None
+    per = defaultdict(lambda: defaultdict(float))
+    dur = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if kern not in r["Kernel_Name"]:
+                continue
+            key = (f, r["Dispatch_Id"])
+            per[key][r["Counter_Name"]] += float(r["Counter_Value"])
+            dur[key] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    assert per, f"no dispatch of {kern} in {d}"
+    keys = list(per)
+    med = {c: statistics.median(per[k][c] for k in keys) for c in per[keys[0]]}
+    active = med["GRBM_GUI_ACTIVE"] / XCDS
+    out = {"workload": wl, "kernel": kern, "dispatches": len(keys), "counters_median": med,
+           "kernel_ns_median": statistics.median(dur.values()),
+           "clock_ghz_est": round(active / statistics.median(dur.values()), 3),
+           "mfma_util": round(med["SQ_VALU_MFMA_BUSY_CYCLES"] / (active * SIMDS), 4),
+           "formula": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)"}
+    if n_mfma and cyc:
+        out["mfma_util_analytic"] = round(n_mfma * cyc / (active * SIMDS), 4)
+        out["analytic"] = {"mfma_per_dispatch": n_mfma, "cycles_per_mfma": cyc}
+    json.dump(out, open(dst, "w"), indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -2,7 +2,7 @@
 """Per-kernel statistics of the TIMED regions of a bench.py run under
 `rocprofv3 --kernel-trace` with GS_BENCH_MARK=1.
 
-bench.py launches one tiny fill kernel right before the first and right after the last
+bench.py launches one tiny spin kernel (torch.cuda._sleep) right before the first and right after the last
 timed launch of each measured region (bench.mark); this script keeps only the dispatches
 strictly between each pair of markers, so the plan search's launches of the same kernels
 are not averaged in.  usage: timed_stats.py <rocprof output dir> <out.csv> [expected
@@ -13,7 +13,7 @@ import os
 import statistics
 import sys
 
-MARK = "FillFunctor"
+MARK = "spin_kernel"
 
 
 def regions(rows):
