@@ -901,7 +901,8 @@ def main():
         try:
             mj = json.load(open(mf))
             if mj.get("kernel") == kernel_label(info):
-                mfma = {k: mj[k] for k in ("mfma_util", "mfma_util_analytic", "formula") if k in mj}
+                mfma = {k: mj[k] for k in ("mfma_util", "formula", "mfma_util_grbm", "analytic", "kernel_ns_median")
+                        if k in mj}
                 mfma["source"] = os.path.relpath(mf, ROOT)
         except Exception:
             mfma = None

@@ -3207,6 +3207,29 @@ __global__ __launch_bounds__(256) void k_nm_mfma_ks(const unsigned char *__restr
 }
 
 #endif  // GS_EXPERIMENTS (k_nm_mfma_ks)
+// k_permute_rows -- B gathered into a merge-path plan's column order (MP_COL_PERM): row i of
+// Bp is row perm[i] of B (perm: the original column of renumbered column i, most nonzeros
+// first).  16 B per thread when a row is whole 16-B units, one element per thread otherwise.
+template <class VT>
+__global__ __launch_bounds__(256) void k_permute_rows(const VT *__restrict__ B, VT *__restrict__ Bp,
+                                                      const uint32_t *__restrict__ perm, uint32_t K, uint32_t N) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    if ((N * sizeof(VT)) % 16u == 0) {
+        const uint32_t upr = N * (uint32_t)sizeof(VT) / 16u;
+        const uint64_t total = (uint64_t)K * upr;
+        for (uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x; t < total; t += stride) {
+            const uint32_t i = (uint32_t)(t / upr), u = (uint32_t)(t - (uint64_t)i * upr);
+            reinterpret_cast<u32x4 *>(Bp)[t] = reinterpret_cast<const u32x4 *>(B)[(size_t)perm[i] * upr + u];
+        }
+    } else {
+        const uint64_t total = (uint64_t)K * N;
+        for (uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x; t < total; t += stride) {
+            const uint32_t i = (uint32_t)(t / N), j = (uint32_t)(t - (uint64_t)i * N);
+            Bp[t] = B[(size_t)perm[i] * N + j];
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // k_merge_path -- merge-path levels (merge_path_{thread,warp,tblock}_operator +
 // the level's total-reduce token).  The plan's

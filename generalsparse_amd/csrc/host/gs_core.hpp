@@ -98,6 +98,9 @@ struct config_t {
     bool MFMA_KS = true;         // row blocks of >= KS_MIN_ROWS rows: K-split, B-stationary k_mfma_ks
     int64_t KS_MIN_ROWS = 40;    // ... from this many rows per BMTB (shorter blocks: k_mfma_rows)
     bool MP_ROWS = false;        // merge-path plans: k_merge_rows (product/row walk) instead of k_merge_path
+    int64_t MP_COL_PERM = -1;    // merge-path plans: columns renumbered by degree, B gathered into that order per
+                                 // launch (1 on, 0 off, -1 auto: B of at least 64 MB, past the L2s and a quarter
+                                 // of the Infinity Cache)
     int64_t MP_SOLO = 16;        // k_merge_rows: rows of at most this many nonzeros are one slot's
     int64_t KS_WAVES = 8;        // k_mfma_ks waves per workgroup (8 or 16)
     int64_t KS_SPLIT = 0;        // k_mfma_ks K ranges per row block (0: the fewest that fit LDS and fill the CUs)

@@ -220,7 +220,29 @@ void upload_csr(plan_state &p, device_arrays &a) {
     const auto &col = m.u(GLOBAL_META, sp.interleaved ? "nz_col_indices_after_interlance_storage" : "nz_col_indices", sb);
     auto vals = m.get_element(GLOBAL_META, sp.interleaved ? "nz_vals_after_interlance_storage" : "nz_vals", sb)->meta_data_arr;
     const uint64_t nnz = col.size();
-    if (d.col_bytes == 2) {
+    if (d.col_perm) {
+        // MP_COL_PERM: columns renumbered by degree (most nonzeros first, ties by column), so
+        // the B rows the power-law hubs gather share 128-B lines and stay in L2; each launch
+        // first gathers B into that order (k_permute_rows).  Only the device copy of the
+        // column indices changes; the order of every row's entries, so every sum, is the same
+        std::vector<uint32_t> deg(p.K, 0u), perm(p.K), rank(p.K);
+        for (uint64_t c : col) deg[c]++;
+        for (uint32_t i = 0; i < (uint32_t)p.K; i++) perm[i] = i;
+        std::stable_sort(perm.begin(), perm.end(), [&](uint32_t x, uint32_t y) { return deg[x] > deg[y]; });
+        for (uint32_t i = 0; i < (uint32_t)p.K; i++) rank[perm[i]] = i;
+        std::vector<uint32_t> c32(nnz);
+        for (uint64_t i = 0; i < nnz; i++) c32[i] = rank[col[i]];
+        if (d.col_bytes == 2) {
+            std::vector<uint16_t> c16(c32.begin(), c32.end());
+            a.col = dev_copy(d, c16, kPad);
+        } else {
+            a.col = dev_copy(d, c32, kPad);
+        }
+        a.cperm = dev_copy(d, perm);
+        const size_t bb = (size_t)p.K * d.ws_n * (d.dtype == 0 ? 4u : 2u);
+        HIP_OK(hipMalloc(&a.bperm, std::max<size_t>(bb, 16)));
+        d.allocations.push_back(a.bperm);
+    } else if (d.col_bytes == 2) {
         std::vector<uint16_t> c16(col.begin(), col.end());
         a.col = dev_copy(d, c16, kPad);
     } else {
@@ -630,6 +652,9 @@ void upload_plan(plan_state &p, int dtype, int device) {
                 d.mp_rows = cfg.MP_ROWS;
                 d.mp_solo = (uint32_t)std::max<int64_t>(1, cfg.MP_SOLO);
                 d.kernel = d.mp_rows ? "k_merge_rows" : "k_merge_path";
+                const uint64_t b_bytes = p.K * (uint64_t)Nd * (dtype == 0 ? 4u : 2u);
+                d.col_perm = !sp.interleaved && p.K < (1ull << 32) &&
+                             (cfg.MP_COL_PERM > 0 || (cfg.MP_COL_PERM < 0 && b_bytes >= (64ull << 20)));
             }
             break;
         }
@@ -699,6 +724,8 @@ void add_replica(plan_state &p) {
     r.t4 = (uint32_t *)dup(s.t4);
     r.ws = (float *)dup(s.ws);
     r.ws2 = (float *)dup(s.ws2);
+    r.cperm = (uint32_t *)dup(s.cperm);
+    r.bperm = dup(s.bperm);
     r.pad_out = dup(s.pad_out);
     p.dev.replicas.push_back(r);
 }

@@ -165,6 +165,14 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
             const uint32_t fb = d.n_fin ? (uint32_t)std::min<uint64_t>(256, (d.n_fin * N / 4 + 1023) / 1024) : 0u;
             // one column tile: split rows are combined inside the launch (chain arrivals)
             const bool fused = tiles == 1 && !(mp_debug() & 4u);
+            if (d.col_perm) {  // B into the plan's column order first (MP_COL_PERM, upload_csr)
+                const uint64_t units = (uint64_t)p.K * N * sizeof(VT) / (N * sizeof(VT) % 16 == 0 ? 16u : sizeof(VT));
+                const uint32_t pb = (uint32_t)std::min<uint64_t>((units + 255) / 256, 8192);
+                hipLaunchKernelGGL((gsk::k_permute_rows<VT>), dim3(std::max(pb, 1u)), dim3(256), 0, s, B, (VT *)a.bperm,
+                                   a.cperm, (uint32_t)p.K, N);
+                HIP_OK(hipGetLastError());
+                B = (const VT *)a.bperm;
+            }
 #ifdef GS_EXPERIMENTS
             if (d.mp_rows)
                 hipLaunchKernelGGL((gsk::k_merge_rows<VT, CT, CF>), dim3(gx + fb, tiles), dim3(256),

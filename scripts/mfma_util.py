@@ -6,10 +6,14 @@
 Counters (scripts/gpu_session.sh part `sq`): SQ_VALU_MFMA_BUSY_CYCLES (matrix-pipe busy cycles,
 summed over every SIMD of the chip), GRBM_GUI_ACTIVE (GPU-busy cycles, summed over the 8 XCDs,
 MI355X_MICROARCH.md DVFS item), SQ_WAVE_CYCLES / SQ_BUSY_CYCLES (context).
-  mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)
+  mfma_util_grbm = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)
 i.e. the fraction of the kernel's busy cycles, per SIMD, in which its matrix pipe was busy.
-With the analytic instruction count the same ratio is also given from first principles:
-  mfma_util_analytic = n_mfma x cycles per MFMA / (GRBM_GUI_ACTIVE / 8 x 1024)."""
+GRBM_GUI_ACTIVE over-counts on dispatches shorter than ~0.3 ms (MI355X_MICROARCH.md, DVFS
+give-back: the implied clock reads 2.6-3.7 GHz here), so the figure reported first is the
+pessimistic one, against the peak clock over the kernel's own duration:
+  mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel ns x 2.4 GHz)
+and the GRBM-based ratio beside it (mfma_util_grbm).  The busy counter is checked against the
+analytic instruction count (n_mfma x cycles per MFMA) when that is given."""
 import csv
 import glob
 import json
@@ -42,11 +46,14 @@ def main():
     out = {"workload": wl, "kernel": kern, "dispatches": len(keys), "counters_median": med,
            "kernel_ns_median": statistics.median(dur.values()),
            "clock_ghz_est": round(active / statistics.median(dur.values()), 3),
-           "mfma_util": round(med["SQ_VALU_MFMA_BUSY_CYCLES"] / (active * SIMDS), 4),
-           "formula": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)"}
+           "mfma_util": round(med["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * statistics.median(dur.values()) * 2.4), 4),
+           "formula": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel ns x 2.4 GHz)",
+           "mfma_util_grbm": round(med["SQ_VALU_MFMA_BUSY_CYCLES"] / (active * SIMDS), 4),
+           "formula_grbm": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)"}
     if n_mfma and cyc:
-        out["mfma_util_analytic"] = round(n_mfma * cyc / (active * SIMDS), 4)
-        out["analytic"] = {"mfma_per_dispatch": n_mfma, "cycles_per_mfma": cyc}
+        out["analytic"] = {"mfma_per_dispatch": n_mfma, "cycles_per_mfma": cyc,
+                           "busy_cycles": n_mfma * cyc,
+                           "counter_over_analytic": round(med["SQ_VALU_MFMA_BUSY_CYCLES"] / (n_mfma * cyc), 4)}
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out))
 

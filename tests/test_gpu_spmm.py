@@ -681,6 +681,36 @@ def test_merge_path_matches_oracle(ws, level, N, dtype, merge_walk):
         check(C, ref, dtype)
 
 
+@pytest.mark.parametrize("dtype", ["f32", "f16"])
+@pytest.mark.parametrize("N", [8, 3])
+def test_merge_path_column_permutation_is_exact(N, dtype):
+    """MP_COL_PERM renumbers a merge-path plan's columns by degree on the device and gathers B
+    into that order per launch (k_permute_rows): only where B rows sit in memory changes, the
+    order of every row's entries does not, so C is bit-identical to the unpermuted plan's (and
+    matches the oracle); replicas carry their own permuted B"""
+    M = 3000
+    row, col, val = ds.rmat(M, 60000, seed=9)
+    npdt = np.float16 if dtype == "f16" else np.float32
+    B = np.random.default_rng(4).uniform(-1, 1, (M, N)).astype(npdt)
+    outs = []
+    for perm in (0, 1):
+        gsa.set_config("MP_COL_PERM", perm)
+        try:
+            plan = gsa.Plan.from_coo(M, M, row, col, val).run_pipeline("merge_path", N, 512, 1).compile().upload(dtype, 0)
+        finally:
+            gsa.set_config("MP_COL_PERM", -1)
+        plan.add_replica()
+        Bt = torch.from_numpy(B).to(DEV)
+        C0 = plan.spmm(Bt).float().cpu().numpy()
+        C1 = plan.spmm(Bt, replica=1).float().cpu().numpy()
+        np.testing.assert_array_equal(C0, C1)
+        outs.append(C0)
+        plan.free()
+    np.testing.assert_array_equal(outs[0], outs[1])
+    vv = val.astype(npdt).astype(np.float32)
+    check(outs[1], ofi.spmm_ref(M, N, row, col, vv, B.astype(np.float32), "f64"), dtype)
+
+
 def test_merge_path_deterministic_and_no_stale_state(merge_walk):
     """two launches give bit-identical C (no floating-point atomics: a split row's partials
     are combined in wave order by the last arriver on an integer arrival counter, and the
