@@ -239,7 +239,8 @@ void upload_csr(plan_state &p, device_arrays &a) {
             a.col = dev_copy(d, c32, kPad);
         }
         a.cperm = dev_copy(d, perm);
-        const size_t bb = (size_t)p.K * d.ws_n * (d.dtype == 0 ? 4u : 2u);
+        // the gathered B: K rows of the plan's dense width (launches check N <= ws_n = that width)
+        const size_t bb = (size_t)p.K * (size_t)std::max<int64_t>(1, get_config().DENSE_MATRIX_SIZE) * (d.dtype == 0 ? 4u : 2u);
         HIP_OK(hipMalloc(&a.bperm, std::max<size_t>(bb, 16)));
         d.allocations.push_back(a.bperm);
     } else if (d.col_bytes == 2) {
@@ -325,7 +326,15 @@ void upload_plan(plan_state &p, int dtype, int device) {
     const bool defer_csr = dtype == 1 && get_config().MFMA_TILES &&
                            (sp.family == KF_WARP_TOTAL || sp.family == KF_BLOCK_TOTAL) &&
                            m.is_exist(TBLOCK_META, "first_row_indices", sb);
+    if (sp.family == KF_MERGE_PATH) {
+        // MP_COL_PERM (decided before the CSR upload, which renumbers the columns)
+        const config_t cfg = get_config();
+        const uint64_t b_bytes = p.K * (uint64_t)std::max<int64_t>(1, cfg.DENSE_MATRIX_SIZE) * (dtype == 0 ? 4u : 2u);
+        d.col_perm = !sp.interleaved && p.K < (1ull << 32) &&
+                     (cfg.MP_COL_PERM > 0 || (cfg.MP_COL_PERM < 0 && b_bytes >= (64ull << 20)));
+    }
     if (!defer_csr) upload_csr(p, a);
+    GS_CHECK(!d.col_perm || (a.cperm && a.bperm), "merge-path column permutation: arrays not uploaded");
     uint64_t row_num = row_num_of_sub_matrix(m, sb);
     // matrix-core row blocks for fp16 plans with BMTBs (tried before the other kernels)
     auto try_mfma = [&](const std::vector<uint32_t> &) {
@@ -652,9 +661,6 @@ void upload_plan(plan_state &p, int dtype, int device) {
                 d.mp_rows = cfg.MP_ROWS;
                 d.mp_solo = (uint32_t)std::max<int64_t>(1, cfg.MP_SOLO);
                 d.kernel = d.mp_rows ? "k_merge_rows" : "k_merge_path";
-                const uint64_t b_bytes = p.K * (uint64_t)Nd * (dtype == 0 ? 4u : 2u);
-                d.col_perm = !sp.interleaved && p.K < (1ull << 32) &&
-                             (cfg.MP_COL_PERM > 0 || (cfg.MP_COL_PERM < 0 && b_bytes >= (64ull << 20)));
             }
             break;
         }

@@ -166,6 +166,7 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
             // one column tile: split rows are combined inside the launch (chain arrivals)
             const bool fused = tiles == 1 && !(mp_debug() & 4u);
             if (d.col_perm) {  // B into the plan's column order first (MP_COL_PERM, upload_csr)
+                GS_CHECK(a.cperm && a.bperm, "merge-path column permutation without its device arrays");
                 const uint64_t units = (uint64_t)p.K * N * sizeof(VT) / (N * sizeof(VT) % 16 == 0 ? 16u : sizeof(VT));
                 const uint32_t pb = (uint32_t)std::min<uint64_t>((units + 255) / 256, 8192);
                 hipLaunchKernelGGL((gsk::k_permute_rows<VT>), dim3(std::max(pb, 1u)), dim3(256), 0, s, B, (VT *)a.bperm,
