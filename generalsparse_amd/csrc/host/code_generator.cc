@@ -214,7 +214,9 @@ namespace {
 // (kernels/{ks,mfma}_launch.hip); the check and perf_result as for the other families
 std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int repeat) {
     std::ostringstream o;
-    const uint32_t N = L.N, CT = L.kind == mc_layout::NM ? std::max<uint32_t>(1, N / 16) : ks_ct(N);
+    const uint32_t N = L.N, CT = L.kind == mc_layout::NM ? std::max<uint32_t>(1, N / 16)
+                                                         : (L.kind == mc_layout::KS ? L.ks.CT : ks_ct(N));
+    const uint32_t NT = L.kind == mc_layout::KS ? ks_col_tiles_ct(N, CT) : ks_col_tiles(N);
     const char *kname = L.kind == mc_layout::KS ? "k_mfma_ks"
                         : L.kind == mc_layout::BM ? (L.bm.kb ? "k_mfma_kb" : L.bm.v2 ? "k_mfma_bm2" : "k_mfma_bm")
                         : L.kind == mc_layout::ROWS ? "k_mfma_rows"
@@ -255,15 +257,15 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
           << "    uint16_t *d_val = up(rdb<uint16_t>(\"TBLOCK_META_mfma_ks_entry_val_0.bin\"));\n"
           << "    uint32_t *d_steps = up(rdb<uint32_t>(\"TBLOCK_META_mfma_ks_steps_0.bin\"));\n"
           << "    // the tagged slabs start (and are left by every launch) all 0\n"
-          << "    float *d_ws; uint32_t *d_arr; hipMalloc(&d_ws, " << nwg * ks_col_tiles(N) * 256 * t.RT * CT * 4 << "ull + 16);\n"
-          << "    hipMemset(d_ws, 0, " << nwg * ks_col_tiles(N) * 256 * t.RT * CT * 4 << "ull + 16);\n"
-          << "    hipMalloc(&d_arr, " << nb * ks_col_tiles(N) * 4 << "ull + 4); hipMemset(d_arr, 0, " << nb * ks_col_tiles(N) * 4
+          << "    float *d_ws; uint32_t *d_arr; hipMalloc(&d_ws, " << nwg * NT * 256 * t.RT * CT * 4 << "ull + 16);\n"
+          << "    hipMemset(d_ws, 0, " << nwg * NT * 256 * t.RT * CT * 4 << "ull + 16);\n"
+          << "    hipMalloc(&d_arr, " << nb * NT * 4 << "ull + 4); hipMemset(d_arr, 0, " << nb * NT * 4
           << "ull + 4);\n";
         const std::string k = "gsk::k_mfma_ks<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ", " +
                               std::to_string(t.W) + ", " + std::to_string(kKsDepth) + ", " + std::to_string(t.MAXG) + ">";
         setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
                 std::to_string(t.lds_bytes) + ")";
-        launch = k + "<<<dim3(" + std::to_string(nwg) + ", " + std::to_string(ks_col_tiles(N)) + "), " +
+        launch = k + "<<<dim3(" + std::to_string(nwg) + ", " + std::to_string(NT) + "), " +
                  std::to_string(64 * t.W) + ", " + std::to_string(t.lds_bytes) +
                  ">>>(d_tbr, (const gsk::u32x4 *)d_pos, (const gsk::u32x4 *)d_val, (const gsk::u32x2 *)d_steps, d_B, d_C, "
                  "(uint32_t)K, N, " + std::to_string(t.S) + "u, " + std::to_string(t.NS) + "u, " + std::to_string(nwg) + "u, 0u, d_ws, d_arr, nullptr, " +

@@ -239,17 +239,18 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     const uint64_t nb = tb_rows.size() - 1;
     if (nb == 0 || K == 0) { why = "empty plan"; return false; }
     if (N == 0 || N % 8 != 0) { why = "N must be a multiple of 8"; return false; }
-    const uint32_t CT = ks_ct(N);
     // KS_WAVES = 16: twice the waves (more loads in flight per CU) when their stages fit LDS
     uint32_t W = kKsWaves;
     uint64_t rmax = 0;
     for (uint64_t g = 0; g < nb; g++) rmax = std::max<uint64_t>(rmax, tb_rows[g + 1] - tb_rows[g]);
     if (rmax < (uint64_t)std::max<int64_t>(1, min_rows) || rmax > 128) { why = "row blocks outside the k_mfma_ks range"; return false; }
     const uint32_t RT = std::max<uint32_t>(2, (uint32_t)((rmax + 15) / 16));  // kernels built for RT 2..8
+    const uint32_t CT = ks_ct_rt(N, RT);
+    t.CT = CT;
     // (RT 6..8 -- 96..128-row blocks: whole CU rounds on the OPT-30B shapes -- for tiles of
     // at most 32 columns: RT x CT accumulators of 4 VGPRs)
     if (RT > 5 && CT > 2) { why = "row blocks over 80 rows at N > 32"; return false; }
-    if (get_config().KS_WAVES == 16 && gsk::ks_lds_bytes(CT, RT, 16) <= 160 * 1024) W = 16;
+    if (get_config().KS_WAVES == 16 && CT <= 4 && gsk::ks_lds_bytes(CT, RT, 16) <= 160 * 1024) W = 16;
     const uint64_t nnz = row_ptr[tb_rows[nb]] - row_ptr[tb_rows[0]];
     if (nnz == 0 || (double)nb * 16 * RT * K > (double)max_fill * nnz) {  // as build_mfma_tiles
         why = "row blocks too sparse for dense tiles";
@@ -336,6 +337,7 @@ bool build_bm_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     uint64_t rmax = 0;
     for (uint64_t g = 0; g < nb; g++) rmax = std::max<uint64_t>(rmax, tb_rows[g + 1] - tb_rows[g]);
     if (rmax == 0 || rmax > 96) { why = "row blocks outside the k_mfma_bm range (1..96 rows)"; return false; }
+    if (N > 64) { why = "k_mfma_bm layouts cover up to 64 columns"; return false; }
     const uint32_t RT = (uint32_t)((rmax + 15) / 16);
     const uint64_t nnz = row_ptr[tb_rows[nb]] - row_ptr[tb_rows[0]];
     if (nnz == 0 || (double)nb * 16 * RT * K > (double)max_fill * nnz) {

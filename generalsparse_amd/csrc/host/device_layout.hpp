@@ -52,6 +52,7 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
 // GCAP, the plan's largest step: it sets MAXG), + one spare group
 struct ks_tiles {
     uint32_t S = 0, NS = 0, RT = 0, RMAX = 0, MAXG = 0, GCAP = 0, W = 0;
+    uint32_t CT = 0;  // 16-column MFMA tiles per workgroup (ks_ct_rt)
     size_t lds_bytes = 0;
     std::vector<uint16_t> pos, val;  // 8 u16 per group each
     std::vector<uint32_t> steps;     // per (unit, k-step): first group, group count
@@ -61,6 +62,11 @@ struct ks_tiles {
 // tile), ks_col_tiles(N) tiles in the grid's y dimension (N = 128: two)
 inline uint32_t ks_ct(uint32_t N) { return N <= 16 ? 1u : (N <= 32 ? 2u : 4u); }
 inline uint32_t ks_col_tiles(uint32_t N) { return (N + 16 * ks_ct(N) - 1) / (16 * ks_ct(N)); }
+// k_mfma_ks's own choice: N >= 128 with row blocks of at most 48 rows (RT <= 3) runs 128 columns
+// per workgroup (CT = 8: 96 fp32 accumulators, 255 VGPRs, no spill), so A is read once at N = 128
+// instead of once per 64-column tile; taller blocks keep CT = 4 (their accumulators would spill)
+inline uint32_t ks_ct_rt(uint32_t N, uint32_t RT) { return N >= 128 && RT <= 3 ? 8u : ks_ct(N); }
+inline uint32_t ks_col_tiles_ct(uint32_t N, uint32_t CT) { return (N + 16 * CT - 1) / (16 * CT); }
 
 bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
                     const std::vector<uint64_t> &col, const std::vector<float> &vals, uint64_t K, uint32_t N,

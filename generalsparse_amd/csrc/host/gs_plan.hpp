@@ -39,6 +39,7 @@ struct device_plan {
     uint64_t n_units = 0;     // BMTs / BMWs / BMTBs the grid walks
     uint64_t n_rows_aux = 0;  // rows covered (thread_total: rows incl. trailing empty)
     uint64_t row_base = 0;
+    uint32_t ks_ctw = 0;      // k_mfma_ks: 16-column tiles per workgroup (ks_tiles::CT)
     uint64_t err_at = 0;      // K-split combine: index of the device error word in t2 (0: none)
     uint64_t nnz_stored = 0;  // padded nnz on device
     size_t bytes_A = 0;       // device bytes of A per replica (metadata + cols + vals)

@@ -356,13 +356,14 @@ void upload_plan(plan_state &p, int dtype, int device) {
             d.n_rows_aux = nb;
             const size_t before = d.bytes_A;
             d.ks_gcap = kt.GCAP;
+            d.ks_ctw = kt.CT;
             a.t0 = dev_copy(d, to_u32(mc.tbr, "BMTB first_row_indices"));
             a.tcol = dev_copy(d, kt.pos);
             a.tval = dev_copy(d, kt.val);
             a.t1 = dev_copy(d, kt.steps);
             d.bytes_tile = d.bytes_A - before;
             if (kt.S > 1) {
-                const uint32_t nt = ks_col_tiles(mc.N), CT = ks_ct(mc.N);
+                const uint32_t CT = kt.CT, nt = ks_col_tiles_ct(mc.N, CT);
                 a.ws = dev_copy(d, std::vector<float>((size_t)nb * kt.S * nt * 256 * kt.RT * CT, 0.f));
                 // arrival counters, then the replica's device error word (ks_slab_wait)
                 a.t2 = dev_copy(d, std::vector<uint32_t>((size_t)nb * nt + 1u, 0u));

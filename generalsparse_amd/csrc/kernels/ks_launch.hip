@@ -60,7 +60,7 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
             auto kd = dep == 1 ? gsk::k_mfma_ks<CT, RT, W, 1, MAXG, false>
                                : dep == 3 ? gsk::k_mfma_ks<CT, RT, W, 3, MAXG, false> : gsk::k_mfma_ks<CT, RT, W, 4, MAXG, false>;
             grant_lds(d.device, kd, d.lds_bytes);
-            hipLaunchKernelGGL(kd, dim3((uint32_t)d.n_rows_aux * d.ksplit, ks_col_tiles(N)), dim3(64 * W), d.lds_bytes, s,
+            hipLaunchKernelGGL(kd, dim3((uint32_t)d.n_rows_aux * d.ksplit, ks_col_tiles_ct(N, CT)), dim3(64 * W), d.lds_bytes, s,
                                a.t0, (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, (const gsk::u32x2 *)a.t1, B, C,
                                (uint32_t)p.K, N, d.ksplit, d.ks_ns, (uint32_t)d.n_rows_aux * d.ksplit, (uint32_t)d.row_base,
                                a.ws, a.t2, stamps, ks_prio_arg());
@@ -75,7 +75,7 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
     // the LDS this instantiation needs at the plan's range width, against what the upload sized
     GS_CHECK(gsk::ks_lds_bytes(CT, RT, W) <= d.lds_bytes, "k_mfma_ks: LDS size disagrees with the upload");
     grant_lds(d.device, kern, d.lds_bytes);
-    hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit, ks_col_tiles(N)), dim3(64 * W), d.lds_bytes, s, a.t0,
+    hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit, ks_col_tiles_ct(N, CT)), dim3(64 * W), d.lds_bytes, s, a.t0,
                        (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, (const gsk::u32x2 *)a.t1, B, C,
                        (uint32_t)p.K, N, d.ksplit, d.ks_ns, (uint32_t)d.n_rows_aux * d.ksplit, (uint32_t)d.row_base, a.ws, a.t2, stamps,
                        ks_prio_arg());
@@ -94,6 +94,13 @@ void launch_ks_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B
 
 template <int CT>
 void launch_ks_ct(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
+    if constexpr (CT == 8) {  // 128 columns per workgroup: row blocks of up to 48 rows (ks_ct_rt)
+        switch (p.dev.maxr) {
+            case 2: launch_ks_rt<CT, 2>(p, a, B, C, N, s); return;
+            case 3: launch_ks_rt<CT, 3>(p, a, B, C, N, s); return;
+            default: throw gs_error("k_mfma_ks: 128-column tiles take row blocks of up to 48 rows");
+        }
+    }
     switch (p.dev.maxr) {  // RT: 16-row tiles per row block (the upload builds RT >= 2)
         case 2: launch_ks_rt<CT, 2>(p, a, B, C, N, s); break;
         case 3: launch_ks_rt<CT, 3>(p, a, B, C, N, s); break;
@@ -285,10 +292,13 @@ void launch_ks(const plan_state &p, const device_arrays &a, const void *B, void 
     const gsk::f16 *b = (const gsk::f16 *)B;
     gsk::f16 *c = (gsk::f16 *)C;
     GS_CHECK(N == p.dev.lds_N, "k_mfma_ks runs the plan's dense width");
-    switch (ks_ct(N)) {  // 16-column tiles per workgroup; ks_col_tiles(N) workgroups across N
+    GS_CHECK(p.dev.ks_ctw == ks_ct_rt(N, p.dev.maxr), "k_mfma_ks: column tiles disagree with the upload");
+    switch (p.dev.ks_ctw) {  // 16-column tiles per workgroup; ks_col_tiles_ct(N, CT) workgroups across N
         case 1: launch_ks_ct<1>(p, a, b, c, N, s); break;
         case 2: launch_ks_ct<2>(p, a, b, c, N, s); break;
-        default: launch_ks_ct<4>(p, a, b, c, N, s); break;
+        case 4: launch_ks_ct<4>(p, a, b, c, N, s); break;
+        case 8: launch_ks_ct<8>(p, a, b, c, N, s); break;
+        default: throw gs_error("k_mfma_ks: bad column tile count");
     }
 }
 
