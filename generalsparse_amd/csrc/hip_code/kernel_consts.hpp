@@ -41,12 +41,14 @@ GSK_HD constexpr size_t ks_stage_bytes(uint32_t CT, uint32_t RT, uint32_t W) {
 }
 // the W partial tiles (+ the ticket word) fit beside the wave images: each wave stores its
 // tile when its own loop ends, with no barrier before
-GSK_HD constexpr bool ks_red_apart(uint32_t CT, uint32_t RT, uint32_t W) {
-    return ks_stage_bytes(CT, RT, W) + (size_t)W * RT * CT * 1024u + 16u <= 160u * 1024u;
+// (ap = false: never apart -- the partial tiles reuse the stage LDS after a barrier, so more
+// workgroups fit a CU: KS_APART)
+GSK_HD constexpr bool ks_red_apart(uint32_t CT, uint32_t RT, uint32_t W, bool ap = true) {
+    return ap && ks_stage_bytes(CT, RT, W) + (size_t)W * RT * CT * 1024u + 16u <= 160u * 1024u;
 }
-GSK_HD constexpr size_t ks_lds_bytes(uint32_t CT, uint32_t RT, uint32_t W) {
+GSK_HD constexpr size_t ks_lds_bytes(uint32_t CT, uint32_t RT, uint32_t W, bool ap = true) {
     const size_t stage = ks_stage_bytes(CT, RT, W);
-    if (ks_red_apart(CT, RT, W)) return stage + (size_t)W * RT * CT * 1024u + 16u;
+    if (ks_red_apart(CT, RT, W, ap)) return stage + (size_t)W * RT * CT * 1024u + 16u;
     const size_t red = (size_t)(ks_red_halves(CT, RT, W) ? W / 2 : W) * RT * CT * 1024u + 16u;
     return stage > red ? stage : red;
 }
@@ -105,5 +107,10 @@ GSK_HD constexpr size_t bm_lds_bytes(uint32_t CT, uint32_t RT, uint32_t W) {
 // k_nm_mfma: 8 waves, 4,608-B blocks per (64 rows, 64-column k-step), B chunks of 256 rows
 constexpr int kNmWaves = 8;
 constexpr uint32_t kNmBlockBytes = 4608, kNmKC = 256;
+// k_nm_mfma4: two B chunk buffers, or the four q = 1 wave tiles of the k-phase sum (+ ticket)
+GSK_HD constexpr size_t nm4_lds_bytes(uint32_t CT) {
+    const size_t bufs = (size_t)2 * kNmKC * 32u * CT, red = (size_t)4 * 4 * CT * 64 * 16 + 16;
+    return bufs > red ? bufs : red;
+}
 
 }  // namespace gsk

@@ -1611,7 +1611,7 @@ __device__ __forceinline__ u32x4 ks_slab_wait(const uint32_t *src, uint32_t tag,
 // 3 + i after step i (i < 16), 20 loop done, 21 reduced, 22 end
 // the body of k_mfma_ks for workgroup bx of a launch of nwg workgroups (k_mfma_ks: the
 // whole grid; k_mfma_ks_group: one entry's share of it)
-template <int CT, int RT, int W, int D, int MAXG, bool STAMPS>
+template <int CT, int RT, int W, int D, int MAXG, bool STAMPS, bool AP = true>
 __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_row, const u32x4 *__restrict__ tP,
                                         const u32x4 *__restrict__ tV, const u32x2 *__restrict__ steps,
                                         const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K, uint32_t N, uint32_t S,
@@ -1790,7 +1790,7 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
     // wave order.  Item t = (tile, lane) of a 16x16 tile: the 4 rows 4*(lane/16)+i of
     // column lane%16.  When the W partial tiles fit LDS beside the wave images (APART), each
     // wave stores its tile as soon as its loop ends, without waiting for the others
-    constexpr bool APART = ks_red_apart(CT, RT, W);
+    constexpr bool APART = ks_red_apart(CT, RT, W, AP);
     f4v *red = reinterpret_cast<f4v *>(lds + (APART ? (size_t)W * (IMG + STG) : 0u));
     constexpr bool HALVES = !APART && ks_red_halves(CT, RT, W);
     constexpr uint32_t WR = HALVES ? W / 2 : W;  // partial tiles summed from LDS
@@ -1909,7 +1909,7 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
 #undef GS_KS_STAMP
 }
 
-template <int CT, int RT, int W, int D, int MAXG, bool STAMPS = false>
+template <int CT, int RT, int W, int D, int MAXG, bool STAMPS = false, bool AP = true>
 __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__ bmtb_first_row,  // nb+1
                                                     const u32x4 *__restrict__ tP,  // 8 x u16 position per group
                                                     const u32x4 *__restrict__ tV,  // 8 x f16 value per group
@@ -1920,8 +1920,8 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
                                                     uint32_t *__restrict__ arrivals, uint64_t *__restrict__ stamps = nullptr,
                                                     uint32_t prio = 0) {
     // nwg == gridDim.x (an argument: kernarg preload)
-    ks_body<CT, RT, W, D, MAXG, STAMPS>(bmtb_first_row, tP, tV, steps, B, C, K, N, S, NS, nwg, row_base, slabs, arrivals,
-                                        stamps, blockIdx.x, prio);
+    ks_body<CT, RT, W, D, MAXG, STAMPS, AP>(bmtb_first_row, tP, tV, steps, B, C, K, N, S, NS, nwg, row_base, slabs,
+                                            arrivals, stamps, blockIdx.x, prio);
 }
 
 // ---------------------------------------------------------------------------
@@ -3207,6 +3207,239 @@ __global__ __launch_bounds__(256) void k_nm_mfma_ks(const unsigned char *__restr
 }
 
 #endif  // GS_EXPERIMENTS (k_nm_mfma_ks)
+
+// ---------------------------------------------------------------------------
+// k_nm_mfma4 -- the same 2:4 panels (build_nm_panels blocks) for wide B (N = 128, CT = 8),
+// with a quarter of k_nm_mfma's B bytes per row.
+// Why: a k_nm_mfma workgroup (128 rows, all of K) takes in 1.8 MB of B for its 1.0 MB of A,
+// and one CU's intake is the sum of its A (HBM, ~24 GB/s per CU) and B (L2, ~70 GB/s)
+// streams (DESIGN §4 model: 43 + 26 us on C3).  Here a workgroup owns 256 rows (four 64-row
+// groups) over one of S K ranges: B per CU halves (0.9 MB at S = 2), A per CU is unchanged,
+// the grid stays 224 workgroups on C3.
+// Waves: 8 = four row groups x two k-phases; wave (rh, q) takes k-steps 4c+q and 4c+q+2 of
+// every 256-row chunk c of its range (its 64 x 128 fp32 tile: 128 accumulator registers).
+// B chunks go to LDS by LDS-DMA (global_load_lds_dwordx4: no register staging, no LDS store
+// cycles; b_piece's XOR rides on the source address), two 64 KB buffers, one chunk ahead;
+// A blocks two chunks ahead in registers.  One barrier per chunk.  Epilogue: the two
+// k-phase tiles summed through LDS (q0 + q1), then, with S > 1, the tagged-slab K-split
+// combine of k_mfma_ks (ks_slab_wait; sums in K-range order: deterministic).  K must be a
+// multiple of 256 (whole chunks; the upload checks).
+// ---------------------------------------------------------------------------
+template <int CT>
+__global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma4(const unsigned char *__restrict__ A,
+                                                            const f16 *__restrict__ B, f16 *__restrict__ C,
+                                                            uint32_t K, uint32_t S64, uint32_t rows, uint32_t row_base,
+                                                            uint32_t S, uint32_t ncs, uint32_t nwg,
+                                                            float *__restrict__ slabs, uint32_t *__restrict__ arrivals,
+                                                            uint32_t flags) {
+    constexpr uint32_t N = 16 * CT, RB = 32 * CT, UB = 2 * CT;
+    constexpr uint32_t szB = kNmKC * RB;               // one chunk of B rows in LDS
+    constexpr uint32_t NBW = szB / 16u / (64u * kNmWaves);  // LDS-DMA wave-instructions per wave per chunk
+    static_assert(CT == 8 || CT == 4, "k_nm_mfma4: 64- or 128-column tiles");
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t rh = wv >> 1, q = wv & 1u;
+    const uint32_t u = xcd_block(blockIdx.x, nwg);
+    const uint32_t g = u / S, qs = u - g * S;
+    const uint32_t rg = g * 4u + rh;
+    const uint32_t nch = S64 / 4u, c0 = qs * ncs, nc = min(ncs, nch - c0);  // this range's chunks
+    const unsigned char *arow = A + (size_t)rg * S64 * kNmBlockBytes;
+
+    // ---- B chunk c -> LDS buffer c & 1 by LDS-DMA: wave-instruction i of wave wv fills the
+    // 1 KB at unit (wv*NBW + i)*64 (lane-linear); the piece permutation is applied to the source
+    // Instruction i of wave wv reads B rows k = (wv*NBW + i)*RPI + lane/UB.  b_piece's swizzle of
+    // row k depends on i only through bit 3 of k (bit 1 of i at RPI = 4 rows per instruction,
+    // CT = 8; bit 0 at RPI = 8, CT = 4): two per-lane source offsets, one per parity, cover all
+    static_assert(64 % UB == 0, "whole B rows per wave-instruction");
+    constexpr uint32_t RPI = 64u / UB;
+    auto par_of = [](uint32_t i) -> uint32_t { return RPI == 4 ? (i >> 1) & 1u : i & 1u; };
+    auto i0_of = [](uint32_t par) -> uint32_t { return RPI == 4 ? 2u * par : par; };
+    uint32_t boff[2];
+#pragma unroll
+    for (uint32_t par = 0; par < 2; par++) {
+        const uint32_t k = (wv * NBW + i0_of(par)) * RPI + lane / UB, sp = lane % UB;
+        boff[par] = (k * N + (b_piece<CT>(k, sp >> 1) * 2u + (sp & 1u)) * 8u) * 2u;
+    }
+    auto issue_b = [&](uint32_t c) {
+        const unsigned char *src0 = reinterpret_cast<const unsigned char *>(B) + (size_t)(c0 + c) * kNmKC * N * 2u;
+        unsigned char *buf = lds + (c & 1u) * szB;
+#pragma unroll
+        for (uint32_t i = 0; i < NBW; i++) {
+            const uint32_t par = par_of(i);
+            const uint32_t u0 = (wv * NBW + i) * 64u;
+            __builtin_amdgcn_global_load_lds((const void *)(src0 + boff[par] + (i - i0_of(par)) * RPI * N * 2u),
+                                             (__attribute__((address_space(3))) void *)(buf + u0 * 16u), 16, 0, 0);
+        }
+    };
+    // ---- A blocks of chunk c: k-steps 4c+q and 4c+q+2 (positions + four 16-row tiles each)
+    u32x4 av0[2][4], av1[2][4];
+    uint2 ai0[2], ai1[2];
+#define GS_NM4_ALOAD(c, V, I)                                                                       \
+    {                                                                                             \
+        _Pragma("unroll") for (int j = 0; j < 2; j++) {                                           \
+            const unsigned char *blk_ = arow + (size_t)(4u * (c0 + (c)) + q + 2u * j) * kNmBlockBytes; \
+            I[j] = *reinterpret_cast<const uint2 *>(blk_ + lane * 8u);                            \
+            _Pragma("unroll") for (int rt = 0; rt < 4; rt++) V[j][rt] =                           \
+                *reinterpret_cast<const u32x4 *>(blk_ + 512u + rt * 1024u + lane * 16u);          \
+        }                                                                                         \
+    }
+    f4v acc[4][CT];
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
+    // transposed B reads: row k = 64*kk + klane + {0, 4, 32, 36} keeps klane's swizzle bits
+    // (k & 3 and bit 3: klane & 7 <= 3, so +4 carries nowhere), so piece ct of row k sits at
+    // fb[h] ^ (ct << 5) + 64*kk*RB, fb[h] = the row's byte offset + its swizzled piece 0
+    const uint32_t klane = 8u * (lane >> 4) + ((lane & 15u) >> 2);
+    uint32_t fb[4];
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+        const uint32_t k = klane + 32u * (h >> 1) + 4u * (h & 1);
+        fb[h] = k * RB + b_piece<CT>(k, 0) * 32u + (lane & 3u) * 8u;
+    }
+#define GS_NM4_BFRAG(lb_, kk, ct, BF)                                                               \
+    {                                                                                             \
+        s4v t_[4];                                                                                \
+        _Pragma("unroll") for (int h = 0; h < 4; h++)                                             \
+            t_[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(                                      \
+                (lds_s4v *)(lb_ + 64u * (kk) * RB + (fb[h] ^ ((uint32_t)(ct) << 5))));           \
+        __builtin_memcpy(&BF, t_, 32);                                                            \
+    }
+#define GS_NM4_COMPUTE(c, V, I)                                                                     \
+    {                                                                                             \
+        const unsigned char *lb_ = lds + ((uint32_t)(c) & 1u) * szB;                              \
+        _Pragma("unroll") for (int j = 0; j < 2; j++) {                                           \
+            h8v av_[4];                                                                           \
+            _Pragma("unroll") for (int rt = 0; rt < 4; rt++) __builtin_memcpy(&av_[rt], &V[j][rt], 16); \
+            const int ix0_ = (int)I[j].x, ix1_ = (int)I[j].y;                                     \
+            h16v bf_[2];                                                                          \
+            GS_NM4_BFRAG(lb_, q + 2u * j, 0, bf_[0]);                                             \
+            _Pragma("unroll") for (int ct = 0; ct < CT; ct++) {                                   \
+                if (ct + 1 < CT) GS_NM4_BFRAG(lb_, q + 2u * j, ct + 1, bf_[(ct + 1) & 1]);        \
+                const h16v b_ = bf_[ct & 1];                                                      \
+                acc[0][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[0], b_, acc[0][ct], ix0_, 0, 0); \
+                acc[1][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[1], b_, acc[1][ct], ix0_, 0, 1); \
+                acc[2][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[2], b_, acc[2][ct], ix1_, 0, 0); \
+                acc[3][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[3], b_, acc[3][ct], ix1_, 0, 1); \
+            }                                                                                     \
+        }                                                                                         \
+    }
+    // prologue: B(0), A(0), A(1); B(0) and A(0) retired (A(1)'s 10 loads left in flight)
+    issue_b(0u);
+    GS_NM4_ALOAD(0u, av0, ai0);
+    if (nc > 1u) {
+        GS_NM4_ALOAD(1u, av1, ai1);
+        __asm__ volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    } else {
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    // iteration c: B(c+1) -> the other buffer (read last in c-1, before the barrier), compute c,
+    // A(c+2) into c's register set, retire B(c+1) and A(c+1) (A(c+2) left in flight), barrier
+#define GS_NM4_ITER(c, V, I)                                                                        \
+    {                                                                                             \
+        if ((c) + 1u < nc) issue_b((c) + 1u);                                                     \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        GS_NM4_COMPUTE(c, V, I);                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        if ((c) + 2u < nc) {                                                                      \
+            GS_NM4_ALOAD((c) + 2u, V, I);                                                         \
+            __asm__ volatile("s_waitcnt vmcnt(10)" ::: "memory");                                 \
+        } else {                                                                                  \
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");                                  \
+        }                                                                                         \
+        __builtin_amdgcn_s_barrier();                                                             \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+    }
+    uint32_t c = 0;
+    for (; c + 1u < nc; c += 2u) {
+        GS_NM4_ITER(c, av0, ai0);
+        GS_NM4_ITER(c + 1u, av1, ai1);
+    }
+    if (c < nc) GS_NM4_ITER(c, av0, ai0);
+#undef GS_NM4_ITER
+#undef GS_NM4_COMPUTE
+#undef GS_NM4_BFRAG
+#undef GS_NM4_ALOAD
+    // ---- K-split ticket (wave 0), then the two k-phase tiles summed in LDS: q1 -> q0
+    uint32_t *arr = arrivals + g;
+    uint32_t ticket = 0;
+    if (S > 1 && wv == 0 && lane == 0) ticket = __hip_atomic_fetch_add(arr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    f4v *red = reinterpret_cast<f4v *>(lds);
+    constexpr uint32_t TW = 4 * CT * 64;  // f4v per wave tile
+    uint32_t *flag = reinterpret_cast<uint32_t *>(lds + 4u * TW * 16u);  // (nm4_lds_bytes: after the tiles)
+    if (q == 1u) {
+#pragma unroll
+        for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) red[rh * TW + (rt * CT + ct) * 64u + lane] = acc[rt][ct];
+    }
+    if (S > 1 && wv == 0 && lane == 0) *flag = ticket;
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __asm__ volatile("" ::: "memory");
+    if (q == 1u) return;
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) acc[rt][ct] += red[rh * TW + (rt * CT + ct) * 64u + lane];
+    auto store_c = [&](int rt, int ct, const f4v &v) {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) {
+            const uint32_t r = rg * 64u + rt * 16u + 4u * (lane >> 4) + i;
+            if (r < rows) C[(size_t)(row_base + r) * N + ct * 16u + (lane & 15u)] = (f16)v[i];
+        }
+    };
+    if (S == 1) {
+#pragma unroll
+        for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+            for (int ct = 0; ct < CT; ct++) store_c(rt, ct, acc[rt][ct]);
+        return;
+    }
+    // ---- tagged-slab combine (k_mfma_ks's protocol): slab of unit u = [rh][rt][ct][lane] f4v
+    const uint32_t tk = *flag & 0xffffu, tag = ((*flag >> 16) & 1u) ^ 1u;
+    auto tagged = [&](const f4v &v) {
+        u32x4 w;
+        __builtin_memcpy(&w, &v, 16);
+        w[0] = (w[0] & ~1u) | tag; w[1] = (w[1] & ~1u) | tag; w[2] = (w[2] & ~1u) | tag; w[3] = (w[3] & ~1u) | tag;
+        return w;
+    };
+    f4v *slab = reinterpret_cast<f4v *>(slabs) + (size_t)u * 4u * TW + rh * TW;
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) {
+            const u32x4 w = tagged(acc[rt][ct]);
+            __asm__ volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(slab + (rt * CT + ct) * 64u + lane), "v"(w) : "memory");
+        }
+    if (tk != S - 1u) return;
+    if (wv == 0 && lane == 0) __hip_atomic_store(arr, tag << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t *err = arrivals + nwg / S;  // the replica's device error word
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+        for (int ct = 0; ct < CT; ct++) {
+            f4v sum = {0.f, 0.f, 0.f, 0.f};
+            for (uint32_t qq = 0; qq < S; qq++) {
+                u32x4 w;
+                if (qq == qs) {
+                    w = tagged(acc[rt][ct]);
+                } else {
+                    const f4v *src = reinterpret_cast<const f4v *>(slabs) + (size_t)(g * S + qq) * 4u * TW + rh * TW +
+                                     (rt * CT + ct) * 64u + lane;
+                    w = ks_slab_wait(reinterpret_cast<const uint32_t *>(src), tag, err, GS_KS_FORCE(flags));
+                }
+                w[0] &= ~1u; w[1] &= ~1u; w[2] &= ~1u; w[3] &= ~1u;
+                f4v x;
+                __builtin_memcpy(&x, &w, 16);
+                sum += x;
+            }
+            store_c(rt, ct, sum);
+        }
+}
 // k_permute_rows -- B gathered into a merge-path plan's column order (MP_COL_PERM): row i of
 // Bp is row perm[i] of B (perm: the original column of renumbered column i, most nonzeros
 // first).  16 B per thread when a row is whole 16-B units, one element per thread otherwise.

@@ -220,7 +220,7 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
     const char *kname = L.kind == mc_layout::KS ? "k_mfma_ks"
                         : L.kind == mc_layout::BM ? (L.bm.kb ? "k_mfma_kb" : L.bm.v2 ? "k_mfma_bm2" : "k_mfma_bm")
                         : L.kind == mc_layout::ROWS ? "k_mfma_rows"
-                        : (L.nm_ks ? "k_nm_mfma_ks" : "k_nm_mfma");
+                        : (L.nm_ks ? "k_nm_mfma_ks" : (L.nm4 ? "k_nm_mfma4" : "k_nm_mfma"));
     o << "// kernel_file.hip -- generated by generalsparse_amd code_generator: the matrix-core kernel " << kname << "\n"
       << "// build: sh make_kernel.sh; run: ./a.out [matrix.mtx] [N]  -> perf_result (ms, GFLOP/s)\n"
       << (L.kind == mc_layout::BM || L.nm_ks || L.rows_flags ? "#define GS_EXPERIMENTS  // an experiments-build kernel\n" : "")
@@ -262,7 +262,8 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
           << "    hipMalloc(&d_arr, " << nb * NT * 4 << "ull + 4); hipMemset(d_arr, 0, " << nb * NT * 4
           << "ull + 4);\n";
         const std::string k = "gsk::k_mfma_ks<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ", " +
-                              std::to_string(t.W) + ", " + std::to_string(kKsDepth) + ", " + std::to_string(t.MAXG) + ">";
+                              std::to_string(t.W) + ", " + std::to_string(kKsDepth) + ", " + std::to_string(t.MAXG) +
+                              (t.AP ? std::string(">") : std::string(", false, false>"));
         setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
                 std::to_string(t.lds_bytes) + ")";
         launch = k + "<<<dim3(" + std::to_string(nwg) + ", " + std::to_string(NT) + "), " +
@@ -329,6 +330,21 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
         launch = k + "<<<" + std::to_string(nb * L.nm_split) + ", 256, " + std::to_string(lds) +
                  ">>>(d_blk, d_B, d_C, (uint32_t)K, " + std::to_string(L.nm_S) + "u, " + std::to_string(L.nm_rows) +
                  "u, 0u, " + std::to_string(L.nm_split) + "u, " + std::to_string(L.nm_ncs) + "u, d_ws, d_arr)";
+    } else if (L.nm4) {
+        const uint64_t nb = (L.nm_rows + 255) / 256, nwg = nb * L.nm_split;
+        o << "    unsigned char *d_blk = up(rdb<unsigned char>(\"THREAD_META_nm_panels_0.bin\"));\n"
+          << "    // the tagged slabs and the arrival counters start all 0\n"
+          << "    float *d_ws; uint32_t *d_arr; hipMalloc(&d_ws, " << nwg * 256 * N * 4 << "ull + 16); hipMemset(d_ws, 0, "
+          << nwg * 256 * N * 4 << "ull + 16);\n"
+          << "    hipMalloc(&d_arr, " << (nb + 1) * 4 << "ull); hipMemset(d_arr, 0, " << (nb + 1) * 4 << "ull);\n";
+        const std::string k = "gsk::k_nm_mfma4<" + std::to_string(CT) + ">";
+        const size_t lds = gsk::nm4_lds_bytes(CT);
+        setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
+                std::to_string(lds) + ")";
+        launch = k + "<<<" + std::to_string(nwg) + ", " + std::to_string(64 * gsk::kNmWaves) + ", " + std::to_string(lds) +
+                 ">>>(d_blk, d_B, d_C, (uint32_t)K, " + std::to_string(L.nm_S) + "u, " + std::to_string(L.nm_rows) +
+                 "u, 0u, " + std::to_string(L.nm_split) + "u, " + std::to_string(L.nm_ncs) + "u, " + std::to_string(nwg) +
+                 "u, d_ws, d_arr, 0u)";
     } else {
         o << "    unsigned char *d_blk = up(rdb<unsigned char>(\"THREAD_META_nm_panels_0.bin\"));\n";
         // N = 8: one half-used 16-column tile (k_nm_mfma's NG)

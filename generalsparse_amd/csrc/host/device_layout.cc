@@ -257,7 +257,15 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
         return false;
     }
     // K ranges: enough workgroups for the 256 CUs (each reads only its range's B rows)
-    t.lds_bytes = gsk::ks_lds_bytes(CT, RT, W);
+    // KS_APART: the overlapped layout (0) is built for N = 32 and row tiles 2..5; auto (-1) keeps the
+    // apart layout only when it holds as many workgroups per CU as the overlapped one
+    {
+        const int64_t ap = get_config().KS_APART;
+        const bool can_overlap = CT == 2 && RT <= 5 && W == kKsWaves;
+        const size_t la = gsk::ks_lds_bytes(CT, RT, W, true), lo = gsk::ks_lds_bytes(CT, RT, W, false);
+        t.AP = !can_overlap || ap > 0 || (ap < 0 && (160u * 1024u) / la >= (160u * 1024u) / lo);
+    }
+    t.lds_bytes = gsk::ks_lds_bytes(CT, RT, W, t.AP);
     if (t.lds_bytes > 160 * 1024) { why = "k_mfma_ks wave stages exceed LDS"; return false; }
     uint64_t S = s_cfg > 0 ? (uint64_t)s_cfg : std::min<uint64_t>(8, (256 + nb - 1) / nb);
     S = std::max<uint64_t>(1, std::min<uint64_t>(S, (K + 31) / 32));
@@ -281,6 +289,11 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     t.GCAP = (uint32_t)gmax;
     t.MAXG = gmax <= 64 ? 1 : (gmax <= 128 ? 2 : (gmax <= 192 ? 3 : (gmax <= 256 ? 4 : 0)));
     if (!t.MAXG) { why = "a k-step holds more than 256 entry groups"; return false; }
+    if (!t.AP && t.MAXG > 2) {  // the overlapped layout is instantiated for MAXG <= 2 only
+        t.AP = true;
+        t.lds_bytes = gsk::ks_lds_bytes(CT, RT, W, true);
+        if (t.lds_bytes > 160 * 1024) { why = "k_mfma_ks wave stages exceed LDS"; return false; }
+    }
     // 32-bit group and step indices (packed steps: about nnz / 8 + nb*S*NS groups; checked
     // exactly after the build): too large a plan falls back to another kernel
     if ((double)(row_ptr[tb_rows[nb]] - row_ptr[tb_rows[0]]) / 8.0 + (double)nb * S * t.NS * 2.0 >= 4.0e9) {
@@ -337,7 +350,6 @@ bool build_bm_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     uint64_t rmax = 0;
     for (uint64_t g = 0; g < nb; g++) rmax = std::max<uint64_t>(rmax, tb_rows[g + 1] - tb_rows[g]);
     if (rmax == 0 || rmax > 96) { why = "row blocks outside the k_mfma_bm range (1..96 rows)"; return false; }
-    if (N > 64) { why = "k_mfma_bm layouts cover up to 64 columns"; return false; }
     const uint32_t RT = (uint32_t)((rmax + 15) / 16);
     const uint64_t nnz = row_ptr[tb_rows[nb]] - row_ptr[tb_rows[0]];
     if (nnz == 0 || (double)nb * 16 * RT * K > (double)max_fill * nnz) {
@@ -524,6 +536,8 @@ mc_layout choose_matrix_core_layout(const meta_data_set &m, const kernel_spec &s
             uint32_t sp = cfg.NM_SPLIT > 0 ? (uint32_t)cfg.NM_SPLIT : std::max<uint32_t>(1, 256 / std::max<uint32_t>(nb, 1));
             sp = std::max(1u, std::min(sp, nch));
             L.nm_ks = cfg.NM_KS != 0 && Nd >= 16;
+            L.nm4 = !L.nm_ks && K % gsk::kNmKC == 0 && nch >= 2 &&
+                    ((cfg.NM_V4 > 0 && (Nd == 64 || Nd == 128)) || (cfg.NM_V4 < 0 && Nd == 128));
             L.nm_ncs = (nch + sp - 1) / sp;
             L.nm_split = (nch + L.nm_ncs - 1) / L.nm_ncs;
         }

@@ -53,6 +53,7 @@ bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<ui
 struct ks_tiles {
     uint32_t S = 0, NS = 0, RT = 0, RMAX = 0, MAXG = 0, GCAP = 0, W = 0;
     uint32_t CT = 0;  // 16-column MFMA tiles per workgroup (ks_ct_rt)
+    bool AP = true;   // partial tiles beside the stages (ks_red_apart; KS_APART)
     size_t lds_bytes = 0;
     std::vector<uint16_t> pos, val;  // 8 u16 per group each
     std::vector<uint32_t> steps;     // per (unit, k-step): first group, group count
@@ -115,6 +116,7 @@ struct mc_layout {
     uint32_t nm_S = 0;                  // ... k-steps per row group
     uint64_t nm_rows = 0;
     bool nm_ks = false;                    // k_nm_mfma_ks (256-row workgroups, K split) instead of k_nm_mfma
+    bool nm4 = false;                      // k_nm_mfma4 (256-row workgroups of 8 waves, K split, B by LDS-DMA)
     uint32_t nm_split = 1, nm_ncs = 0;     // ... K ranges per row block, 256-column chunks per range
     std::string why;  // why NONE
 };

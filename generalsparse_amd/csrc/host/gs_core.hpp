@@ -104,6 +104,11 @@ struct config_t {
     int64_t MP_SOLO = 16;        // k_merge_rows: rows of at most this many nonzeros are one slot's
     int64_t KS_WAVES = 8;        // k_mfma_ks waves per workgroup (8 or 16)
     int64_t KS_SPLIT = 0;        // k_mfma_ks K ranges per row block (0: the fewest that fit LDS and fill the CUs)
+    int64_t NM_V4 = -1;          // 2:4 panels on k_nm_mfma4 (256-row workgroups, K split): 1 at N = 64 / 128, 0 never,
+                                 // -1 at N = 128 (K a multiple of 256)
+    int64_t KS_APART = 1;        // k_mfma_ks: partial tiles beside the wave stages when they fit (1), never (0: the
+                                 // stage LDS is reused, more workgroups per CU; N = 32, RT <= 5), or only when that
+                                 // keeps the workgroups per CU (-1)
     int64_t KS_FORCE_TIMEOUT = 0;  // experiments build: the K-split combine takes its timeout path (test of the error word)
     int64_t KS_PRIO = 1;         // k_mfma_ks: the younger waves at s_setprio 1 (1: whole loop, 2: first half, 0: off)
 };

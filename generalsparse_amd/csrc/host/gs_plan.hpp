@@ -40,6 +40,7 @@ struct device_plan {
     uint64_t n_rows_aux = 0;  // rows covered (thread_total: rows incl. trailing empty)
     uint64_t row_base = 0;
     uint32_t ks_ctw = 0;      // k_mfma_ks: 16-column tiles per workgroup (ks_tiles::CT)
+    bool ks_ap = true;        // k_mfma_ks: partial tiles beside the stages (ks_tiles::AP)
     uint64_t err_at = 0;      // K-split combine: index of the device error word in t2 (0: none)
     uint64_t nnz_stored = 0;  // padded nnz on device
     size_t bytes_A = 0;       // device bytes of A per replica (metadata + cols + vals)
@@ -47,6 +48,7 @@ struct device_plan {
     bool lds = false;
     bool nm_ks = false;  // k_nm_mfma_ks (ksplit K ranges of ncs chunks; ws slabs + t2 counters when ksplit > 1)
     bool nm = false;    // k_nm_mfma: 2:4 panels of a col-direction plan (A blocks in tcol; k-steps in KC)
+    bool nm4 = false;   // ... on k_nm_mfma4 (256-row workgroups, ksplit K ranges of ncs chunks)
     bool mfma = false;  // k_mfma_rows (uses KC, nc, lds_bytes; log2 KC in RSB; RT in maxr; RMAX in rpw_max)
     bool ks = false;    // k_mfma_ks: K split over ksplit workgroups per row block, B slice in LDS
                         // (t0 BMTB rows, tcol/tval groups; ks_ns k-steps per range,

@@ -297,13 +297,14 @@ void upload_plan(plan_state &p, int dtype, int device) {
     if (mc.kind == mc_layout::NM) {
         // col-direction BMTs that are 2:4 panels: sparse matrix cores, self-contained blocks
         d.nm = true;
-        d.kernel = mc.nm_ks ? "k_nm_mfma_ks" : "k_nm_mfma";
+        d.kernel = mc.nm_ks ? "k_nm_mfma_ks" : (mc.nm4 ? "k_nm_mfma4" : "k_nm_mfma");
+        d.nm4 = mc.nm4;
         d.KC = mc.nm_S;
         d.n_rows_aux = mc.nm_rows;
         d.n_units = m.u(THREAD_META, "first_nz_indices", sb).size() - 1;
         d.waves = mc.nm_ks ? 4 : gsk::kNmWaves;
         d.nm_ks = mc.nm_ks;
-        d.ksplit = mc.nm_ks ? mc.nm_split : 1;
+        d.ksplit = mc.nm_ks || mc.nm4 ? mc.nm_split : 1;
         d.ncs = mc.nm_ncs;
         a.tcol = dev_copy(d, mc.nm_blk);
         d.bytes_tile = d.bytes_A;
@@ -311,6 +312,12 @@ void upload_plan(plan_state &p, int dtype, int device) {
             const uint64_t ngr = (mc.nm_rows + 255) / 256 * 4;
             a.ws = dev_copy(d, std::vector<float>((size_t)ngr * mc.nm_split * 64 * mc.N, 0.f));
             a.t2 = dev_copy(d, std::vector<uint32_t>((size_t)ngr, 0u));
+        }
+        if (mc.nm4 && mc.nm_split > 1) {  // tagged fp32 slabs (256 x N per unit), counters + the device error word
+            const uint64_t nb = (mc.nm_rows + 255) / 256;
+            a.ws = dev_copy(d, std::vector<float>((size_t)nb * mc.nm_split * 256 * mc.N, 0.f));
+            a.t2 = dev_copy(d, std::vector<uint32_t>((size_t)nb + 1u, 0u));
+            d.err_at = nb;
         }
         d.replicas.push_back(a);
         p.uploaded = true;
@@ -357,6 +364,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
             const size_t before = d.bytes_A;
             d.ks_gcap = kt.GCAP;
             d.ks_ctw = kt.CT;
+            d.ks_ap = kt.AP;
             a.t0 = dev_copy(d, to_u32(mc.tbr, "BMTB first_row_indices"));
             a.tcol = dev_copy(d, kt.pos);
             a.tval = dev_copy(d, kt.val);

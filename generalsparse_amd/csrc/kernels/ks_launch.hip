@@ -72,8 +72,14 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
     GS_CHECK(d.waves == kKsWaves, "k_mfma_ks with 16 waves is an experiments-build variant");
 #endif
     auto kern = gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, STAMPS>;
+    if (!d.ks_ap) {  // KS_APART = 0: the partial tiles reuse the stage LDS (N = 32, RT <= 5, MAXG <= 2)
+        if constexpr (CT == 2 && RT <= 5 && MAXG <= 2 && W == (int)kKsWaves)
+            kern = gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, STAMPS, false>;
+        else
+            throw gs_error("k_mfma_ks: the overlapped-LDS layout is built for N = 32, RT <= 5, MAXG <= 2");
+    }
     // the LDS this instantiation needs at the plan's range width, against what the upload sized
-    GS_CHECK(gsk::ks_lds_bytes(CT, RT, W) <= d.lds_bytes, "k_mfma_ks: LDS size disagrees with the upload");
+    GS_CHECK(gsk::ks_lds_bytes(CT, RT, W, d.ks_ap) <= d.lds_bytes, "k_mfma_ks: LDS size disagrees with the upload");
     grant_lds(d.device, kern, d.lds_bytes);
     hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit, ks_col_tiles_ct(N, CT)), dim3(64 * W), d.lds_bytes, s, a.t0,
                        (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, (const gsk::u32x2 *)a.t1, B, C,
@@ -267,7 +273,8 @@ void launch_ks_group_rt(const std::vector<ks_group_item> &it, uint32_t N, hipStr
 
 uint32_t ks_group_key(const plan_state &p, uint32_t N) {
     const device_plan &d = p.dev;
-    if (!p.uploaded || !d.mfma || !d.ks || d.pad_rows || N != 32 || d.lds_N != 32 || d.waves != kKsWaves) return 0;
+    if (!p.uploaded || !d.mfma || !d.ks || d.pad_rows || N != 32 || d.lds_N != 32 || d.waves != kKsWaves || !d.ks_ap)
+        return 0;
     return (d.maxr << 8) | d.seg_cap;  // RT, MAXG: one instantiation
 }
 

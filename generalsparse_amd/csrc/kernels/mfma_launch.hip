@@ -202,7 +202,42 @@ void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, vo
 
 }  // namespace
 
+template <int CT>
+void launch_nm4(const plan_state &p, const device_arrays &a, const void *B, void *C, hipStream_t s) {
+    const device_plan &d = p.dev;
+    auto kern = gsk::k_nm_mfma4<CT>;
+    const size_t lds = gsk::nm4_lds_bytes(CT);
+    static std::mutex mu;
+    static std::map<std::pair<int, const void *>, bool> granted;
+    {
+        std::lock_guard<std::mutex> l(mu);
+        bool &g = granted[{d.device, reinterpret_cast<const void *>(kern)}];
+        if (!g) {
+            HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds));
+            g = true;
+        }
+    }
+    const uint32_t nb = (uint32_t)((d.n_rows_aux + 255) / 256), nch = d.KC / 4;
+    GS_CHECK(p.K % gsk::kNmKC == 0 && d.ksplit >= 1 && d.ncs >= 1 && (d.ksplit - 1) * d.ncs < nch &&
+                 (d.ksplit == 1 || (a.ws && a.t2)),
+             "k_nm_mfma4: K ranges disagree with the upload");
+    const uint32_t nwg = nb * d.ksplit;
+    const config_t cfg = get_config();
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(64 * gsk::kNmWaves), lds, s, (const unsigned char *)a.tcol,
+                       (const gsk::f16 *)B, (gsk::f16 *)C, (uint32_t)p.K, d.KC, (uint32_t)d.n_rows_aux,
+                       (uint32_t)d.row_base, d.ksplit, d.ncs, nwg, a.ws, a.t2, cfg.KS_FORCE_TIMEOUT ? 16u : 0u);
+    HIP_OK(hipGetLastError());
+}
+
 void launch_nm(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
+    if (p.dev.nm4) {
+        switch (N) {
+            case 64: launch_nm4<4>(p, a, B, C, s); return;
+            case 128: launch_nm4<8>(p, a, B, C, s); return;
+            default: throw gs_error("k_nm_mfma4 plan built for N = 64 / 128, not " + std::to_string(N), -2);
+        }
+    }
     switch (N) {
         case 8: launch_nm_ct<1, 8>(p, a, B, C, s); break;  // one half-used 16-column tile
         case 16: launch_nm_ct<1>(p, a, B, C, s); break;

@@ -167,7 +167,8 @@ def test_nm_ks_and_classic_kernels(shape, N, ks, split):
         M, K = shape
         r, c, v = thinned(M, K, 70 + M, keep=0.8, empty_rows=(0, M // 2) if M > 2 else ())
         plan = plan_for(M, K, r, c, v, N)
-        assert plan.info()["device_kernel"] == ("k_nm_mfma_ks" if ks else "k_nm_mfma"), plan.info()
+        classic = "k_nm_mfma4" if N == 128 and K % 256 == 0 else "k_nm_mfma"
+        assert plan.info()["device_kernel"] == ("k_nm_mfma_ks" if ks else classic), plan.info()
         B = np.random.default_rng(M + N).uniform(-1, 1, (K, N)).astype(np.float16)
         ref = ofi.spmm_ref(M, N, r, c, v.astype(np.float16).astype(np.float32), B.astype(np.float32), "f64")
         C = spmm(plan, B)
@@ -178,6 +179,46 @@ def test_nm_ks_and_classic_kernels(shape, N, ks, split):
         torch.cuda.synchronize()
         np.testing.assert_array_equal(C1.float().cpu().numpy(), C)
         plan.free()
+    finally:
+        for k, val in old.items():
+            gsa.set_config(k, val)
+
+
+@pytest.mark.parametrize("split", [0, 1, 2, 3])
+@pytest.mark.parametrize("N", [64, 128])
+@pytest.mark.parametrize("shape", [(512, 1024), (333, 2048), (1, 4096), (1000, 768), (256, 512)],
+                         ids=lambda s: f"{s[0]}x{s[1]}")
+def test_nm4_matches_oracle(shape, N, split):
+    """k_nm_mfma4 (256-row workgroups of four row groups x two k-phases, K split over NM_SPLIT
+    ranges, B by LDS-DMA, tagged-slab combine): oracle parity (rows not a multiple of 256, empty
+    rows, one-chunk ranges), bit-identical relaunch and replica, and agreement with k_nm_mfma
+    within the fp16 rounding of the final store"""
+    M, K = shape
+    old = {k: gsa.get_config(k) for k in ("NM_V4", "NM_SPLIT")}
+    try:
+        gsa.set_config("NM_SPLIT", split)
+        r, c, v = thinned(M, K, 90 + M, keep=0.85, empty_rows=(0, M // 2) if M > 2 else ())
+        gsa.set_config("NM_V4", 1)
+        plan = plan_for(M, K, r, c, v, N)
+        info = plan.info()
+        assert info["device_kernel"] == "k_nm_mfma4", info
+        B = np.random.default_rng(M + N + split).uniform(-1, 1, (K, N)).astype(np.float16)
+        ref = ofi.spmm_ref(M, N, r, c, v.astype(np.float16).astype(np.float32), B.astype(np.float32), "f64")
+        C = spmm(plan, B)
+        check(C, ref)
+        np.testing.assert_array_equal(spmm(plan, B), C)  # counters re-armed, slab tags alternate
+        plan.add_replica()
+        C1 = plan.spmm(torch.from_numpy(B).to(DEV), replica=1)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(C1.float().cpu().numpy(), C)
+        plan.device_status()
+        plan.free()
+        gsa.set_config("NM_V4", 0)
+        p2 = plan_for(M, K, r, c, v, N)
+        assert p2.info()["device_kernel"] == "k_nm_mfma"
+        C2 = spmm(p2, B)
+        p2.free()
+        np.testing.assert_allclose(C, C2, rtol=2e-3, atol=2e-3)
     finally:
         for k, val in old.items():
             gsa.set_config(k, val)

@@ -411,6 +411,35 @@ def test_mfma_ks_tall_blocks_match_oracle(rows, N, split, mfma_everywhere):
     assert "k_mfma_ks" in used, used
 
 
+@pytest.mark.parametrize("split", [1, 2, 4])
+@pytest.mark.parametrize("rows", [40, 64, 80])
+def test_mfma_ks_overlapped_lds_layout(rows, split, mfma_everywhere):
+    """KS_APART = 0: the partial tiles reuse the stage LDS after the loop barrier (more
+    workgroups per CU); same sums in the same order as the apart layout: bit-identical C"""
+    N = 32
+    r, c, v = ds.pruned_weight(640, 2048, 0.7, 6)
+    B = torch.from_numpy(np.random.default_rng(2).uniform(-1, 1, (2048, N)).astype(np.float16)).to(DEV)
+    outs = []
+    gsa.set_config("KS_SPLIT", split)
+    try:
+        for ap in (1, 0):
+            gsa.set_config("KS_APART", ap)
+            plan = gsa.Plan.from_coo(640, 2048, r, c, v).run_pipeline("block_total", N, rows, 1).compile().upload("f16", 0)
+            info = plan.info()
+            assert info["device_kernel"] == "k_mfma_ks" and info["ksplit"] == split, info
+            outs.append((plan.spmm(B).float().cpu().numpy(), info["lds_bytes"]))
+            plan.spmm(B)
+            plan.device_status()
+            plan.free()
+    finally:
+        gsa.set_config("KS_APART", 1)
+        gsa.set_config("KS_SPLIT", 0)
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    assert outs[1][1] <= outs[0][1]
+    check(outs[1][0], ofi.spmm_ref(640, N, r, c, v.astype(np.float16).astype(np.float32),
+                                   B.cpu().numpy().astype(np.float32), "f64"), "f16")
+
+
 @pytest.mark.parametrize("split", [2, 4])
 def test_mfma_ks_slab_tags_alternate_over_launches(split, mfma_everywhere):
     """The K-split combine's slab tags alternate per launch (epoch in the arrival counter, no
