@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "idx_formula.hpp"
 #include "kernel_consts.hpp"
 
@@ -1611,7 +1613,10 @@ __device__ __forceinline__ u32x4 ks_slab_wait(const uint32_t *src, uint32_t tag,
 // 3 + i after step i (i < 16), 20 loop done, 21 reduced, 22 end
 // the body of k_mfma_ks for workgroup bx of a launch of nwg workgroups (k_mfma_ks: the
 // whole grid; k_mfma_ks_group: one entry's share of it)
-template <int CT, int RT, int W, int D, int MAXG, bool STAMPS, bool AP = true>
+// P8 (KS_POS8, device_layout.cc pos8_step): tP holds 8 bytes per group -- byte e = bit e of the
+// group's 8 x 16 segment id in bit 7, the entry's (row % 8) << 4 | column % 16 below; the image
+// halfword of a segment sg's entry is 384 * (sg >> 1) + 16 * (sg & 1) + 48 * (b >> 4) + (b & 15)
+template <int CT, int RT, int W, int D, int MAXG, bool STAMPS, bool AP = true, bool P8 = false>
 __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_row, const u32x4 *__restrict__ tP,
                                         const u32x4 *__restrict__ tV, const u32x2 *__restrict__ steps,
                                         const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K, uint32_t N, uint32_t S,
@@ -1645,7 +1650,10 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
     // its groups, so the groups' addresses wait on a load issued a round earlier
     const uint32_t nsw = NS > wv ? (NS - wv + W - 1u) / W : 0u;
     const size_t ubase = (size_t)u * NS;
-    u32x4 P[D][MAXG], V[D][MAXG], BR[D][CT];
+    using PV = typename std::conditional<P8, u32x2, u32x4>::type;
+    const PV *tPp = reinterpret_cast<const PV *>(tP);
+    PV P[D][MAXG];
+    u32x4 V[D][MAXG], BR[D][CT];
     u32x2 NX[D];      // per slot: record of the step the slot loads next
     uint32_t CN[D];   // per slot: group count of the step whose groups it holds
     // the record is read by a vector load (vmcnt, in order with the groups): a scalar load
@@ -1673,7 +1681,7 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
             B_[c] = *reinterpret_cast<const u32x4 *>(B + (size_t)(k < K ? k : K - 1u) * N + col0 + (cu < nv ? cu : 0u));
         }
     };
-    auto load_g = [&](uint32_t i, u32x2 &NX_, uint32_t &CN_, u32x4 (&P_)[MAXG], u32x4 (&V_)[MAXG]) {
+    auto load_g = [&](uint32_t i, u32x2 &NX_, uint32_t &CN_, PV (&P_)[MAXG], u32x4 (&V_)[MAXG]) {
         const uint32_t b0 = __builtin_amdgcn_readfirstlane(NX_[0]);
         const uint32_t gc = __builtin_amdgcn_readfirstlane(NX_[1]);
         CN_ = gc;
@@ -1682,7 +1690,7 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
         for (int j = 0; j < MAXG; j++) {
             const uint32_t qg = lane + 64u * j;
             const size_t at = (size_t)b0 + (qg < gc ? qg : 0u);
-            P_[j] = tP[at];
+            P_[j] = tPp[at];
             V_[j] = tV[at];
         }
     };
@@ -1706,7 +1714,25 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
 
     // step i on its set, then the set is reloaded with step i + D (issued whether or not
     // step i exists: every loop iteration issues the same loads)
-    auto step = [&](uint32_t i, u32x2 &NX_, uint32_t &CN_, u32x4 (&P_)[MAXG], u32x4 (&V_)[MAXG], u32x4 (&B_)[CT]) {
+    // image halfword of entry e of a group (u16 position, or P8's segment + 7-bit position)
+    auto ent_h = [&](const PV &p, uint32_t hb, int e) -> uint32_t {
+        if constexpr (P8) {
+            const uint32_t b = (p[e >> 2] >> (8 * (e & 3))) & 0x7fu;
+            return hb + 48u * (b >> 4) + (b & 15u);
+        } else {
+            return (p[e >> 1] >> (16 * (e & 1))) & 0xffffu;
+        }
+    };
+    auto grp_hb = [&](const PV &p) -> uint32_t {
+        if constexpr (P8) {
+            const uint32_t x = p[0], y = p[1];
+            const uint32_t sg = ((x >> 7) & 1u) | ((x >> 14) & 2u) | ((x >> 21) & 4u) | ((x >> 28) & 8u) | ((y >> 3) & 16u);
+            return 384u * (sg >> 1) + 16u * (sg & 1u);
+        } else {
+            return 0u;
+        }
+    };
+    auto step = [&](uint32_t i, u32x2 &NX_, uint32_t &CN_, PV (&P_)[MAXG], u32x4 (&V_)[MAXG], u32x4 (&B_)[CT]) {
         const bool live = i < nsw;  // wave-uniform
         const uint32_t gc = CN_;
         h8v av[RT], bv[CT];
@@ -1723,9 +1749,10 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
 #pragma unroll
             for (int j = 0; j < MAXG; j++) {
                 if (lane + 64u * j < gc) {
+                    const uint32_t hb = grp_hb(P_[j]);
 #pragma unroll
                     for (int e = 0; e < 8; e++) {
-                        const uint32_t h = (P_[j][e >> 1] >> (16 * (e & 1))) & 0xffffu;
+                        const uint32_t h = ent_h(P_[j], hb, e);
                         const uint16_t v = (uint16_t)((V_[j][e >> 1] >> (16 * (e & 1))) & 0xffffu);
                         *reinterpret_cast<uint16_t *>(img + h * 2u) = v;
                     }
@@ -1750,11 +1777,9 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
 #pragma unroll
             for (int j = 0; j < MAXG; j++) {
                 if (lane + 64u * j < gc) {
+                    const uint32_t hb = grp_hb(P_[j]);
 #pragma unroll
-                    for (int e = 0; e < 8; e++) {
-                        const uint32_t h = (P_[j][e >> 1] >> (16 * (e & 1))) & 0xffffu;
-                        *reinterpret_cast<uint16_t *>(img + h * 2u) = (uint16_t)0;
-                    }
+                    for (int e = 0; e < 8; e++) *reinterpret_cast<uint16_t *>(img + ent_h(P_[j], hb, e) * 2u) = (uint16_t)0;
                 }
             }
         }
@@ -1909,7 +1934,7 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
 #undef GS_KS_STAMP
 }
 
-template <int CT, int RT, int W, int D, int MAXG, bool STAMPS = false, bool AP = true>
+template <int CT, int RT, int W, int D, int MAXG, bool STAMPS = false, bool AP = true, bool P8 = false>
 __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__ bmtb_first_row,  // nb+1
                                                     const u32x4 *__restrict__ tP,  // 8 x u16 position per group
                                                     const u32x4 *__restrict__ tV,  // 8 x f16 value per group
@@ -1920,8 +1945,8 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
                                                     uint32_t *__restrict__ arrivals, uint64_t *__restrict__ stamps = nullptr,
                                                     uint32_t prio = 0) {
     // nwg == gridDim.x (an argument: kernarg preload)
-    ks_body<CT, RT, W, D, MAXG, STAMPS, AP>(bmtb_first_row, tP, tV, steps, B, C, K, N, S, NS, nwg, row_base, slabs,
-                                            arrivals, stamps, blockIdx.x, prio);
+    ks_body<CT, RT, W, D, MAXG, STAMPS, AP, P8>(bmtb_first_row, tP, tV, steps, B, C, K, N, S, NS, nwg, row_base, slabs,
+                                                arrivals, stamps, blockIdx.x, prio);
 }
 
 // ---------------------------------------------------------------------------
@@ -1950,7 +1975,7 @@ struct ks_group_args {
     ks_entry e[kKsGroupMax];
 };
 
-template <int CT, int RT, int W, int D, int MAXG>
+template <int CT, int RT, int W, int D, int MAXG, bool P8 = false>
 __global__ __launch_bounds__(64 * W) void k_mfma_ks_group(ks_group_args args) {
     const uint32_t bx = blockIdx.x, n = args.n;
     uint32_t sel = 0;
@@ -1960,7 +1985,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks_group(ks_group_args args) {
     sel = __builtin_amdgcn_readfirstlane(sel);
     const ks_entry &e = args.e[sel];  // kernel arguments: scalar loads at a computed offset
     if (bx - args.begin[sel] >= e.nwg) return;  // padding up to the next entry's multiple of 8
-    ks_body<CT, RT, W, D, MAXG, false>(e.tbr, e.tP, e.tV, e.steps, e.B, e.C, e.K, args.N, e.S, e.NS, e.nwg, e.row_base,
+    ks_body<CT, RT, W, D, MAXG, false, true, P8>(e.tbr, e.tP, e.tV, e.steps, e.B, e.C, e.K, args.N, e.S, e.NS, e.nwg, e.row_base,
                                        e.slabs, e.arrivals, nullptr, bx - args.begin[sel], args.pad[0]);
 }
 

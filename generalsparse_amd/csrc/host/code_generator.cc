@@ -253,7 +253,8 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
         const uint64_t nb = L.tbr.size() - 1, nwg = nb * t.S;
         o << "    auto tbr = rd(\"TBLOCK_META_first_row_indices_0\");\n"
           << "    std::vector<uint32_t> t32(tbr.begin(), tbr.end()); uint32_t *d_tbr = up(t32);\n"
-          << "    uint16_t *d_pos = up(rdb<uint16_t>(\"TBLOCK_META_mfma_ks_entry_pos_0.bin\"));\n"
+          << (t.P8 ? "    uint8_t *d_pos = up(rdb<uint8_t>(\"TBLOCK_META_mfma_ks_entry_pos_0.bin\"));  // 8-bit positions\n"
+                   : "    uint16_t *d_pos = up(rdb<uint16_t>(\"TBLOCK_META_mfma_ks_entry_pos_0.bin\"));\n")
           << "    uint16_t *d_val = up(rdb<uint16_t>(\"TBLOCK_META_mfma_ks_entry_val_0.bin\"));\n"
           << "    uint32_t *d_steps = up(rdb<uint32_t>(\"TBLOCK_META_mfma_ks_steps_0.bin\"));\n"
           << "    // the tagged slabs start (and are left by every launch) all 0\n"
@@ -263,7 +264,7 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
           << "ull + 4);\n";
         const std::string k = "gsk::k_mfma_ks<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ", " +
                               std::to_string(t.W) + ", " + std::to_string(kKsDepth) + ", " + std::to_string(t.MAXG) +
-                              (t.AP ? std::string(">") : std::string(", false, false>"));
+                              (t.P8 ? std::string(", false, true, true>") : t.AP ? std::string(">") : std::string(", false, false>"));
         setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
                 std::to_string(t.lds_bytes) + ")";
         launch = k + "<<<dim3(" + std::to_string(nwg) + ", " + std::to_string(NT) + "), " +
@@ -607,7 +608,10 @@ uint64_t code_generator::generate_final_program(int repeat, const std::string &r
     uint64_t id = meta->output_format_to_dir(root, spec.arrays, &dir);
     const mc_layout L = emitted_layout(*meta, spec, sub);
     if (L.kind == mc_layout::KS) {
-        write_bin(dir + "/TBLOCK_META_mfma_ks_entry_pos_0.bin", L.ks.pos);
+        if (L.ks.P8)
+            write_bin(dir + "/TBLOCK_META_mfma_ks_entry_pos_0.bin", L.ks.pos8);
+        else
+            write_bin(dir + "/TBLOCK_META_mfma_ks_entry_pos_0.bin", L.ks.pos);
         write_bin(dir + "/TBLOCK_META_mfma_ks_entry_val_0.bin", L.ks.val);
         write_bin(dir + "/TBLOCK_META_mfma_ks_steps_0.bin", L.ks.steps);
     } else if (L.kind == mc_layout::BM) {

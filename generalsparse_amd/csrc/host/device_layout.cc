@@ -143,6 +143,65 @@ static void bank_order_segment(const std::vector<uint16_t> &pos, const std::vect
     for (const auto &bk : bucket) GS_CHECK(bk.empty(), "bank ordering lost an entry");
 }
 
+// KS_POS8 layout of one k-step (k_mfma_ks with P8): the step's entries split into segments of
+// 8 rows x 16 columns of the wave image -- segment sg = (row / 8) * 2 + column / 16, so row tile
+// rt holds segments 4rt .. 4rt+3 -- and every group of 8 entries lies in ONE segment.  Byte e of
+// a group: bit 7 = bit e of the segment id, bits 0-6 = (row % 8) << 4 | column % 16, so a group
+// costs 8 + 16 bytes (3 B per nonzero against 4 B with u16 image positions).  A segment's last
+// group is padded with copies of its first entry (the same value written twice to one place:
+// the scatter and the clear are idempotent).  Inside a segment the entries are dealt to its
+// groups so that each slot e falls on distinct LDS write banks where possible (as
+// bank_order_segment).  Appends to out_pos8 / out_val; returns the groups written.
+static size_t pos8_step(const std::vector<uint16_t> &row, const std::vector<uint16_t> &colw,
+                        const std::vector<uint16_t> &hv, uint32_t RS, std::vector<uint8_t> &out_pos8,
+                        std::vector<uint16_t> &out_val) {
+    const size_t n = row.size();
+    uint32_t nseg = 0;
+    for (size_t i = 0; i < n; i++) nseg = std::max<uint32_t>(nseg, (uint32_t)((row[i] / 8) * 2 + colw[i] / 16) + 1);
+    std::vector<std::vector<uint32_t>> seg(nseg);
+    for (uint32_t i = 0; i < n; i++) seg[(row[i] / 8) * 2 + colw[i] / 16].push_back(i);
+    size_t groups = 0;
+    std::vector<std::vector<uint32_t>> bucket(32);
+    for (uint32_t sg = 0; sg < nseg; sg++) {
+        const auto &es = seg[sg];
+        if (es.empty()) continue;
+        GS_CHECK(sg < 256, "KS_POS8: segment id beyond 8 bits");
+        const size_t ng = (es.size() + 7) / 8;
+        for (auto &b : bucket) b.clear();
+        for (uint32_t i : es) bucket[((uint32_t)row[i] * RS + colw[i]) / 2 % 32].push_back(i);
+        std::vector<uint32_t> slot(ng * 8, UINT32_MAX);
+        std::vector<int> order(32);
+        for (int e = 0; e < 8; e++) {  // slot e of the segment's groups on distinct banks, fullest first
+            for (int k = 0; k < 32; k++) order[k] = k;
+            std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return bucket[a].size() > bucket[b].size(); });
+            size_t l = 0;
+            bool progress = true;
+            while (l < ng && progress) {
+                progress = false;
+                for (int k = 0; k < 32 && l < ng; k++) {
+                    auto &bk = bucket[order[k]];
+                    if (bk.empty()) continue;
+                    slot[l * 8 + e] = bk.back();
+                    bk.pop_back();
+                    l++;
+                    progress = true;
+                }
+            }
+        }
+        for (const auto &bk : bucket) GS_CHECK(bk.empty(), "KS_POS8: bank ordering lost an entry");
+        const uint32_t first = slot[0];
+        for (size_t gi = 0; gi < ng; gi++)
+            for (int e = 0; e < 8; e++) {
+                const uint32_t i = slot[gi * 8 + e] == UINT32_MAX ? first : slot[gi * 8 + e];
+                const uint8_t p7 = (uint8_t)(((row[i] % 8) << 4) | (colw[i] % 16));
+                out_pos8.push_back((uint8_t)((((sg >> e) & 1u) << 7) | p7));
+                out_val.push_back(hv[i]);
+            }
+        groups += ng;
+    }
+    return groups;
+}
+
 bool build_mfma_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,
                       const std::vector<uint64_t> &col, const std::vector<float> &vals, uint64_t K, uint32_t N,
                       size_t lds_budget, int64_t max_fill, mfma_tiles &t, std::string &why) {
@@ -276,14 +335,32 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     t.RT = RT;
     t.RMAX = (uint32_t)rmax;
     t.W = W;
-    // pass 1: the largest step (entries of a row block in 32 columns)
+    // KS_POS8 (8-bit positions in 8 x 16 segments; N = 32, RT <= 8: segment ids < 32)
+    t.P8 = get_config().KS_POS8 && CT == 2 && W == kKsWaves;
+    // pass 1: the largest step (entries of a row block in 32 columns; P8: groups per segment)
     uint64_t gmax = 1;
     {
-        std::vector<uint32_t> cnt((size_t)S * t.NS);
+        const uint32_t nsg = 4 * RT;
+        std::vector<uint32_t> cnt((size_t)S * t.NS * (t.P8 ? nsg : 1u));
         for (uint64_t g = 0; g < nb; g++) {
             std::fill(cnt.begin(), cnt.end(), 0u);
-            for (uint64_t e = row_ptr[tb_rows[g]]; e < row_ptr[tb_rows[g + 1]]; e++) cnt[col[e] / 32]++;
-            for (uint32_t c : cnt) gmax = std::max<uint64_t>(gmax, (c + 7) / 8);
+            for (uint64_t r = tb_rows[g]; r < tb_rows[g + 1]; r++)
+                for (uint64_t e = row_ptr[r]; e < row_ptr[r + 1]; e++) {
+                    const uint64_t st = col[e] / 32;
+                    if (t.P8)
+                        cnt[st * nsg + ((r - tb_rows[g]) / 8) * 2 + (col[e] % 32) / 16]++;
+                    else
+                        cnt[st]++;
+                }
+            if (t.P8) {
+                for (size_t st = 0; st < (size_t)S * t.NS; st++) {
+                    uint64_t ngs = 0;
+                    for (uint32_t k = 0; k < nsg; k++) ngs += (cnt[st * nsg + k] + 7) / 8;
+                    gmax = std::max<uint64_t>(gmax, ngs);
+                }
+            } else {
+                for (uint32_t c : cnt) gmax = std::max<uint64_t>(gmax, (c + 7) / 8);
+            }
         }
     }
     t.GCAP = (uint32_t)gmax;
@@ -302,11 +379,14 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     }
     const uint32_t RS = gsk::kKsStride / 2;  // halfwords per image row
     const uint32_t pad_h = 16 * RT * RS;      // the zero row
-    t.pos.reserve(row_ptr[tb_rows[nb]] - row_ptr[tb_rows[0]] + (size_t)nb * S * t.NS * 8 + 8);
-    t.val.reserve(t.pos.capacity());
+    if (t.P8)
+        t.pos8.reserve(row_ptr[tb_rows[nb]] - row_ptr[tb_rows[0]] + (size_t)nb * S * t.NS * 8 * RT + 8);
+    else
+        t.pos.reserve(row_ptr[tb_rows[nb]] - row_ptr[tb_rows[0]] + (size_t)nb * S * t.NS * 8 + 8);
+    t.val.reserve(t.P8 ? t.pos8.capacity() : t.pos.capacity());
     t.steps.reserve((size_t)nb * S * t.NS * 2);
     std::vector<uint64_t> cur;
-    std::vector<uint16_t> pos, hv;
+    std::vector<uint16_t> pos, hv, prow, pcol;
     for (uint64_t g = 0; g < nb; g++) {
         const uint64_t r0 = tb_rows[g], R = tb_rows[g + 1] - r0;
         cur.assign(R, 0);
@@ -316,23 +396,36 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
                 const uint64_t base = q * KR + 32ull * s, lim = base + 32;
                 pos.clear();
                 hv.clear();
+                prow.clear();
+                pcol.clear();
                 for (uint64_t i = 0; i < R; i++) {
                     uint64_t e = cur[i];
                     for (; e < row_ptr[r0 + i + 1] && col[e] < lim; e++) {
                         pos.push_back((uint16_t)(i * RS + (col[e] - base)));
+                        prow.push_back((uint16_t)i);
+                        pcol.push_back((uint16_t)(col[e] - base));
                         hv.push_back(f32_to_f16_bits(vals[e]));
                     }
                     cur[i] = e;
                 }
-                const size_t before = t.pos.size();
-                bank_order_segment(pos, hv, pad_h, t.pos, t.val, RS / 2);  // pads stay inside the zero row
-                const size_t ng = (t.pos.size() - before) / 8;
+                size_t before, ng;
+                if (t.P8) {
+                    before = t.pos8.size();
+                    ng = pos8_step(prow, pcol, hv, RS, t.pos8, t.val);
+                } else {
+                    before = t.pos.size();
+                    bank_order_segment(pos, hv, pad_h, t.pos, t.val, RS / 2);  // pads stay inside the zero row
+                    ng = (t.pos.size() - before) / 8;
+                }
                 GS_CHECK(ng <= t.GCAP, "k_mfma_ks step exceeds its capacity");
                 t.steps.push_back((uint32_t)(before / 8));
                 t.steps.push_back((uint32_t)ng);
             }
     }
-    t.pos.insert(t.pos.end(), 8, (uint16_t)pad_h);  // spare group: loads past a wave's last step
+    if (t.P8)
+        t.pos8.insert(t.pos8.end(), 8, (uint8_t)0);  // spare group: loads past a wave's last step (never scattered)
+    else
+        t.pos.insert(t.pos.end(), 8, (uint16_t)pad_h);  // spare group: loads past a wave's last step
     t.val.insert(t.val.end(), 8, 0);
     return true;
 }

@@ -54,8 +54,10 @@ struct ks_tiles {
     uint32_t S = 0, NS = 0, RT = 0, RMAX = 0, MAXG = 0, GCAP = 0, W = 0;
     uint32_t CT = 0;  // 16-column MFMA tiles per workgroup (ks_ct_rt)
     bool AP = true;   // partial tiles beside the stages (ks_red_apart; KS_APART)
+    bool P8 = false;  // 8-bit positions (KS_POS8): pos8 instead of pos, see build_ks_tiles
     size_t lds_bytes = 0;
     std::vector<uint16_t> pos, val;  // 8 u16 per group each
+    std::vector<uint8_t> pos8;       // P8: 8 bytes per group
     std::vector<uint32_t> steps;     // per (unit, k-step): first group, group count
 };
 

@@ -106,6 +106,7 @@ struct config_t {
     int64_t KS_SPLIT = 0;        // k_mfma_ks K ranges per row block (0: the fewest that fit LDS and fill the CUs)
     int64_t NM_V4 = -1;          // 2:4 panels on k_nm_mfma4 (256-row workgroups, K split): 1 at N = 64 / 128, 0 never,
                                  // -1 at N = 128 (K a multiple of 256)
+    int64_t KS_POS8 = 0;         // k_mfma_ks at N = 32: 8-bit entry positions in 8 x 16 segments (3 B per nonzero)
     int64_t KS_APART = 1;        // k_mfma_ks: partial tiles beside the wave stages when they fit (1), never (0: the
                                  // stage LDS is reused, more workgroups per CU; N = 32, RT <= 5), or only when that
                                  // keeps the workgroups per CU (-1)

@@ -365,8 +365,9 @@ void upload_plan(plan_state &p, int dtype, int device) {
             d.ks_gcap = kt.GCAP;
             d.ks_ctw = kt.CT;
             d.ks_ap = kt.AP;
+            d.ks_p8 = kt.P8;
             a.t0 = dev_copy(d, to_u32(mc.tbr, "BMTB first_row_indices"));
-            a.tcol = dev_copy(d, kt.pos);
+            a.tcol = kt.P8 ? (void *)dev_copy(d, kt.pos8) : (void *)dev_copy(d, kt.pos);
             a.tval = dev_copy(d, kt.val);
             a.t1 = dev_copy(d, kt.steps);
             d.bytes_tile = d.bytes_A - before;

@@ -72,6 +72,14 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
     GS_CHECK(d.waves == kKsWaves, "k_mfma_ks with 16 waves is an experiments-build variant");
 #endif
     auto kern = gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, STAMPS>;
+    if (d.ks_p8) {  // KS_POS8: 8-bit entry positions (N = 32, 8 waves, the apart layout)
+        if constexpr (CT == 2 && W == (int)kKsWaves && !STAMPS) {
+            GS_CHECK(d.ks_ap, "k_mfma_ks: 8-bit positions are built with the apart LDS layout");
+            kern = gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, false, true, true>;
+        } else {
+            throw gs_error("k_mfma_ks: 8-bit positions are built for N = 32, 8 waves");
+        }
+    }
     if (!d.ks_ap) {  // KS_APART = 0: the partial tiles reuse the stage LDS (N = 32, RT <= 5, MAXG <= 2)
         if constexpr (CT == 2 && RT <= 5 && MAXG <= 2 && W == (int)kKsWaves)
             kern = gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, STAMPS, false>;
@@ -220,7 +228,8 @@ void launch_bm(const plan_state &, const device_arrays &, const void *, void *, 
 namespace {
 template <int RT, int MAXG>
 void launch_ks_group_k(const std::vector<ks_group_item> &it, uint32_t N, hipStream_t s) {
-    auto kern = gsk::k_mfma_ks_group<2, RT, (int)kKsWaves, (int)kKsDepth, MAXG>;
+    auto kern = it[0].p->dev.ks_p8 ? gsk::k_mfma_ks_group<2, RT, (int)kKsWaves, (int)kKsDepth, MAXG, true>
+                                   : gsk::k_mfma_ks_group<2, RT, (int)kKsWaves, (int)kKsDepth, MAXG, false>;
     GS_CHECK(!it.empty() && it.size() <= (size_t)gsk::kKsGroupMax, "k_mfma_ks_group: 1..32 entries");
     gsk::ks_group_args args;
     std::memset(&args, 0, sizeof(args));
@@ -275,7 +284,7 @@ uint32_t ks_group_key(const plan_state &p, uint32_t N) {
     const device_plan &d = p.dev;
     if (!p.uploaded || !d.mfma || !d.ks || d.pad_rows || N != 32 || d.lds_N != 32 || d.waves != kKsWaves || !d.ks_ap)
         return 0;
-    return (d.maxr << 8) | d.seg_cap;  // RT, MAXG: one instantiation
+    return (d.ks_p8 ? 1u << 16 : 0u) | (d.maxr << 8) | d.seg_cap;  // P8, RT, MAXG: one instantiation
 }
 
 void launch_ks_group(const std::vector<ks_group_item> &it, uint32_t N, hipStream_t s) {

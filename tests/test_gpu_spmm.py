@@ -440,6 +440,46 @@ def test_mfma_ks_overlapped_lds_layout(rows, split, mfma_everywhere):
                                    B.cpu().numpy().astype(np.float32), "f64"), "f16")
 
 
+@pytest.mark.parametrize("split", [0, 1, 3])
+@pytest.mark.parametrize("rows", [40, 56, 80, 112, 128])
+def test_mfma_ks_pos8_layout_is_exact(rows, split, mfma_everywhere):
+    """KS_POS8: 8-bit entry positions in 8 x 16 segments (3 B per nonzero) build the same wave
+    images as the u16 positions, so C is bit-identical (and matches the oracle), single and
+    grouped launches alike"""
+    N = 32
+    cases = [ds.pruned_weight(640, 2048, 0.7, 8), ds.random_rows(640, 2048, 400.0, seed=3, empty_frac=0.2)]
+    gsa.set_config("KS_SPLIT", split)
+    try:
+        for r, c, v in cases:
+            B = torch.from_numpy(np.random.default_rng(5).uniform(-1, 1, (2048, N)).astype(np.float16)).to(DEV)
+            outs, plans = [], []
+            for p8 in (0, 1):
+                gsa.set_config("KS_POS8", p8)
+                plan = gsa.Plan.from_coo(640, 2048, r, c, v).run_pipeline("block_total", N, rows, 1).compile().upload("f16", 0)
+                info = plan.info()
+                assert info["device_kernel"] == "k_mfma_ks", info
+                outs.append((plan.spmm(B).float().cpu().numpy(), info["tile_bytes"]))
+                plans.append(plan)
+            np.testing.assert_array_equal(outs[0][0], outs[1][0])
+            assert outs[1][1] < outs[0][1], (outs[1][1], outs[0][1])
+            check(outs[1][0], ofi.spmm_ref(640, N, r, c, v.astype(np.float16).astype(np.float32),
+                                           B.cpu().numpy().astype(np.float32), "f64"), "f16")
+            # grouped: two P8 entries in one k_mfma_ks_group launch
+            plans[1].add_replica()
+            Cs = [torch.full((640, N), float("nan"), device=DEV, dtype=torch.float16) for _ in range(2)]
+            bat = gsa.Batch([(plans[1], 0, B, Cs[0]), (plans[1], 1, B, Cs[1])], N)
+            assert bat.launches() == [2]
+            bat.run(torch.cuda.current_stream().cuda_stream)
+            for cc in Cs:
+                np.testing.assert_array_equal(cc.float().cpu().numpy(), outs[0][0])
+            for p in plans:
+                p.device_status()
+                p.free()
+    finally:
+        gsa.set_config("KS_POS8", 0)
+        gsa.set_config("KS_SPLIT", 0)
+
+
 @pytest.mark.parametrize("split", [2, 4])
 def test_mfma_ks_slab_tags_alternate_over_launches(split, mfma_everywhere):
     """The K-split combine's slab tags alternate per launch (epoch in the arrival counter, no
