@@ -3465,10 +3465,11 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma4(const unsigned char 
             store_c(rt, ct, sum);
         }
 }
-// k_permute_rows -- B gathered into a merge-path plan's column order (MP_COL_PERM): row i of
-// Bp is row perm[i] of B (perm: the original column of renumbered column i, most nonzeros
-// first).  16 B per thread when a row is whole 16-B units, one element per thread otherwise.
-template <class VT>
+// k_permute_rows -- B into a merge-path plan's column order (MP_COL_PERM): row i of Bp is row
+// perm[i] of B (perm: the original column of renumbered column i, most nonzeros first), read
+// by a gather; SCATTER: perm[i] is the new place of column i, B read in order and each row
+// written to its place.  16 B per thread when a row is whole 16-B units, one element otherwise.
+template <class VT, bool SCATTER>
 __global__ __launch_bounds__(256) void k_permute_rows(const VT *__restrict__ B, VT *__restrict__ Bp,
                                                       const uint32_t *__restrict__ perm, uint32_t K, uint32_t N) {
     const uint64_t stride = (uint64_t)gridDim.x * 256u;
@@ -3477,13 +3478,19 @@ __global__ __launch_bounds__(256) void k_permute_rows(const VT *__restrict__ B, 
         const uint64_t total = (uint64_t)K * upr;
         for (uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x; t < total; t += stride) {
             const uint32_t i = (uint32_t)(t / upr), u = (uint32_t)(t - (uint64_t)i * upr);
-            reinterpret_cast<u32x4 *>(Bp)[t] = reinterpret_cast<const u32x4 *>(B)[(size_t)perm[i] * upr + u];
+            if constexpr (SCATTER)
+                reinterpret_cast<u32x4 *>(Bp)[(size_t)perm[i] * upr + u] = reinterpret_cast<const u32x4 *>(B)[t];
+            else
+                reinterpret_cast<u32x4 *>(Bp)[t] = reinterpret_cast<const u32x4 *>(B)[(size_t)perm[i] * upr + u];
         }
     } else {
         const uint64_t total = (uint64_t)K * N;
         for (uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x; t < total; t += stride) {
             const uint32_t i = (uint32_t)(t / N), j = (uint32_t)(t - (uint64_t)i * N);
-            Bp[t] = B[(size_t)perm[i] * N + j];
+            if constexpr (SCATTER)
+                Bp[(size_t)perm[i] * N + j] = B[t];
+            else
+                Bp[t] = B[(size_t)perm[i] * N + j];
         }
     }
 }

@@ -22,7 +22,8 @@ struct device_arrays {
     uint64_t *m0 = nullptr;
     float *ws = nullptr;  // k_mfma_rows K-split slabs (per replica: a replica never runs concurrently with itself)
     float *ws2 = nullptr;  // k_merge_path: partials of the rows each wave closes first (head_rec)
-    uint32_t *cperm = nullptr;  // merge path, MP_COL_PERM: original column of each renumbered column
+    uint32_t *cperm = nullptr;  // merge path, MP_COL_PERM: original column of each renumbered column (or, with
+                                // perm_scatter, the new place of each column)
     void *bperm = nullptr;      // ... B gathered into that order (K x the plan's N, per replica)
 };
 
@@ -62,7 +63,8 @@ struct device_plan {
 
     bool mp_rows = false;   // merge-path plans: k_merge_rows (fixed at upload, MP_ROWS), else k_merge_path
     uint32_t mp_solo = 16;
-    bool col_perm = false;  // merge path: columns renumbered by degree (cperm / bperm)  // k_merge_rows: slot-alone row length (MP_SOLO)
+    bool col_perm = false;  // merge path: columns renumbered by degree (cperm / bperm)
+    bool perm_scatter = false;  // ... cperm holds each column's new place (k_permute_rows scatters)  // k_merge_rows: slot-alone row length (MP_SOLO)
     // k_mfma_rows variant fixed at upload (device_layout.cc): GLDS / B ring depth / compute
     // waves / entry groups per thread -- the launch uses these, not the config of the moment
     int mfma_glds = 2, mfma_nbg = 3, mfma_wct = 6, mfma_maxa = 1;

@@ -228,7 +228,23 @@ void upload_csr(plan_state &p, device_arrays &a) {
         std::vector<uint32_t> deg(p.K, 0u), perm(p.K), rank(p.K);
         for (uint64_t c : col) deg[c]++;
         for (uint32_t i = 0; i < (uint32_t)p.K; i++) perm[i] = i;
-        std::stable_sort(perm.begin(), perm.end(), [&](uint32_t x, uint32_t y) { return deg[x] > deg[y]; });
+        const uint64_t hot = (uint64_t)std::max<int64_t>(0, get_config().MP_PERM_HOT);
+        if (hot == 0 || hot >= p.K) {
+            std::stable_sort(perm.begin(), perm.end(), [&](uint32_t x, uint32_t y) { return deg[x] > deg[y]; });
+        } else {  // MP_PERM_HOT: the `hot` densest columns first (by degree), the rest in their own order
+            std::vector<uint32_t> byd(perm);
+            std::nth_element(byd.begin(), byd.begin() + hot, byd.end(), [&](uint32_t x, uint32_t y) {
+                return deg[x] != deg[y] ? deg[x] > deg[y] : x < y;
+            });
+            byd.resize(hot);
+            std::sort(byd.begin(), byd.end(), [&](uint32_t x, uint32_t y) { return deg[x] != deg[y] ? deg[x] > deg[y] : x < y; });
+            std::vector<uint8_t> is_hot(p.K, 0);
+            for (uint32_t c : byd) is_hot[c] = 1;
+            size_t w = 0;
+            for (uint32_t c : byd) perm[w++] = c;
+            for (uint32_t c = 0; c < (uint32_t)p.K; c++)
+                if (!is_hot[c]) perm[w++] = c;
+        }
         for (uint32_t i = 0; i < (uint32_t)p.K; i++) rank[perm[i]] = i;
         std::vector<uint32_t> c32(nnz);
         for (uint64_t i = 0; i < nnz; i++) c32[i] = rank[col[i]];
@@ -238,7 +254,8 @@ void upload_csr(plan_state &p, device_arrays &a) {
         } else {
             a.col = dev_copy(d, c32, kPad);
         }
-        a.cperm = dev_copy(d, perm);
+        d.perm_scatter = get_config().MP_PERM_SCATTER != 0;
+        a.cperm = dev_copy(d, d.perm_scatter ? rank : perm);  // scatter: new place of each column
         // the gathered B: K rows of the plan's dense width (launches check N <= ws_n = that width)
         const size_t bb = (size_t)p.K * (size_t)std::max<int64_t>(1, get_config().DENSE_MATRIX_SIZE) * (d.dtype == 0 ? 4u : 2u);
         HIP_OK(hipMalloc(&a.bperm, std::max<size_t>(bb, 16)));

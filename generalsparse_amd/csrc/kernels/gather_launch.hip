@@ -169,8 +169,12 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
                 GS_CHECK(a.cperm && a.bperm, "merge-path column permutation without its device arrays");
                 const uint64_t units = (uint64_t)p.K * N * sizeof(VT) / (N * sizeof(VT) % 16 == 0 ? 16u : sizeof(VT));
                 const uint32_t pb = (uint32_t)std::min<uint64_t>((units + 255) / 256, 8192);
-                hipLaunchKernelGGL((gsk::k_permute_rows<VT>), dim3(std::max(pb, 1u)), dim3(256), 0, s, B, (VT *)a.bperm,
-                                   a.cperm, (uint32_t)p.K, N);
+                if (d.perm_scatter)
+                    hipLaunchKernelGGL((gsk::k_permute_rows<VT, true>), dim3(std::max(pb, 1u)), dim3(256), 0, s, B,
+                                       (VT *)a.bperm, a.cperm, (uint32_t)p.K, N);
+                else
+                    hipLaunchKernelGGL((gsk::k_permute_rows<VT, false>), dim3(std::max(pb, 1u)), dim3(256), 0, s, B,
+                                       (VT *)a.bperm, a.cperm, (uint32_t)p.K, N);
                 HIP_OK(hipGetLastError());
                 B = (const VT *)a.bperm;
             }

@@ -750,9 +750,10 @@ def test_merge_path_matches_oracle(ws, level, N, dtype, merge_walk):
         check(C, ref, dtype)
 
 
+@pytest.mark.parametrize("variant", [{}, {"MP_PERM_SCATTER": 1}, {"MP_PERM_HOT": 300}])
 @pytest.mark.parametrize("dtype", ["f32", "f16"])
 @pytest.mark.parametrize("N", [8, 3])
-def test_merge_path_column_permutation_is_exact(N, dtype):
+def test_merge_path_column_permutation_is_exact(N, dtype, variant):
     """MP_COL_PERM renumbers a merge-path plan's columns by degree on the device and gathers B
     into that order per launch (k_permute_rows): only where B rows sit in memory changes, the
     order of every row's entries does not, so C is bit-identical to the unpermuted plan's (and
@@ -764,10 +765,14 @@ def test_merge_path_column_permutation_is_exact(N, dtype):
     outs = []
     for perm in (0, 1):
         gsa.set_config("MP_COL_PERM", perm)
+        for k, v in variant.items():
+            gsa.set_config(k, v)
         try:
             plan = gsa.Plan.from_coo(M, M, row, col, val).run_pipeline("merge_path", N, 512, 1).compile().upload(dtype, 0)
         finally:
             gsa.set_config("MP_COL_PERM", -1)
+            for k in variant:
+                gsa.set_config(k, 0)
         plan.add_replica()
         Bt = torch.from_numpy(B).to(DEV)
         C0 = plan.spmm(Bt).float().cpu().numpy()
