@@ -1975,7 +1975,7 @@ struct ks_group_args {
     ks_entry e[kKsGroupMax];
 };
 
-template <int CT, int RT, int W, int D, int MAXG, bool P8 = false>
+template <int CT, int RT, int W, int D, int MAXG, bool P8 = false, bool AP = true>
 __global__ __launch_bounds__(64 * W) void k_mfma_ks_group(ks_group_args args) {
     const uint32_t bx = blockIdx.x, n = args.n;
     uint32_t sel = 0;
@@ -1985,7 +1985,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks_group(ks_group_args args) {
     sel = __builtin_amdgcn_readfirstlane(sel);
     const ks_entry &e = args.e[sel];  // kernel arguments: scalar loads at a computed offset
     if (bx - args.begin[sel] >= e.nwg) return;  // padding up to the next entry's multiple of 8
-    ks_body<CT, RT, W, D, MAXG, false, true, P8>(e.tbr, e.tP, e.tV, e.steps, e.B, e.C, e.K, args.N, e.S, e.NS, e.nwg, e.row_base,
+    ks_body<CT, RT, W, D, MAXG, false, AP, P8>(e.tbr, e.tP, e.tV, e.steps, e.B, e.C, e.K, args.N, e.S, e.NS, e.nwg, e.row_base,
                                        e.slabs, e.arrivals, nullptr, bx - args.begin[sel], args.pad[0]);
 }
 

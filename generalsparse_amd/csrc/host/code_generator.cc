@@ -264,7 +264,7 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
           << "ull + 4);\n";
         const std::string k = "gsk::k_mfma_ks<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ", " +
                               std::to_string(t.W) + ", " + std::to_string(kKsDepth) + ", " + std::to_string(t.MAXG) +
-                              (t.P8 ? std::string(", false, true, true>") : t.AP ? std::string(">") : std::string(", false, false>"));
+                              std::string(", false, ") + (t.AP ? "true" : "false") + ", " + (t.P8 ? "true" : "false") + ">";
         setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
                 std::to_string(t.lds_bytes) + ")";
         launch = k + "<<<dim3(" + std::to_string(nwg) + ", " + std::to_string(NT) + "), " +

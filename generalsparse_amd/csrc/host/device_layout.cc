@@ -310,6 +310,9 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     // at most 32 columns: RT x CT accumulators of 4 VGPRs)
     if (RT > 5 && CT > 2) { why = "row blocks over 80 rows at N > 32"; return false; }
     if (get_config().KS_WAVES == 16 && CT <= 4 && gsk::ks_lds_bytes(CT, RT, 16) <= 160 * 1024) W = 16;
+    // KS_WAVES = 4 (N = 32): 256-thread workgroups with the overlapped LDS layout, two per CU, so one
+    // workgroup's prologue and combine overlap the other's loop (grouped multi-round launches)
+    if (get_config().KS_WAVES == 4 && CT == 2) W = 4;
     const uint64_t nnz = row_ptr[tb_rows[nb]] - row_ptr[tb_rows[0]];
     if (nnz == 0 || (double)nb * 16 * RT * K > (double)max_fill * nnz) {  // as build_mfma_tiles
         why = "row blocks too sparse for dense tiles";
@@ -320,9 +323,9 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     // apart layout only when it holds as many workgroups per CU as the overlapped one
     {
         const int64_t ap = get_config().KS_APART;
-        const bool can_overlap = CT == 2 && RT <= 5 && W == kKsWaves;
+        const bool can_overlap = CT == 2 && ((RT <= 5 && W == kKsWaves) || W == 4);
         const size_t la = gsk::ks_lds_bytes(CT, RT, W, true), lo = gsk::ks_lds_bytes(CT, RT, W, false);
-        t.AP = !can_overlap || ap > 0 || (ap < 0 && (160u * 1024u) / la >= (160u * 1024u) / lo);
+        t.AP = W != 4 && (!can_overlap || ap > 0 || (ap < 0 && (160u * 1024u) / la >= (160u * 1024u) / lo));
     }
     t.lds_bytes = gsk::ks_lds_bytes(CT, RT, W, t.AP);
     if (t.lds_bytes > 160 * 1024) { why = "k_mfma_ks wave stages exceed LDS"; return false; }
@@ -336,7 +339,7 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     t.RMAX = (uint32_t)rmax;
     t.W = W;
     // KS_POS8 (8-bit positions in 8 x 16 segments; N = 32, RT <= 8: segment ids < 32)
-    t.P8 = get_config().KS_POS8 && CT == 2 && W == kKsWaves;
+    t.P8 = get_config().KS_POS8 && CT == 2 && (W == kKsWaves || W == 4);
     // pass 1: the largest step (entries of a row block in 32 columns; P8: groups per segment)
     uint64_t gmax = 1;
     {
@@ -366,7 +369,7 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     t.GCAP = (uint32_t)gmax;
     t.MAXG = gmax <= 64 ? 1 : (gmax <= 128 ? 2 : (gmax <= 192 ? 3 : (gmax <= 256 ? 4 : 0)));
     if (!t.MAXG) { why = "a k-step holds more than 256 entry groups"; return false; }
-    if (!t.AP && t.MAXG > 2) {  // the overlapped layout is instantiated for MAXG <= 2 only
+    if (!t.AP && t.MAXG > 2 && W != 4) {  // the 8-wave overlapped layout is instantiated for MAXG <= 2 only
         t.AP = true;
         t.lds_bytes = gsk::ks_lds_bytes(CT, RT, W, true);
         if (t.lds_bytes > 160 * 1024) { why = "k_mfma_ks wave stages exceed LDS"; return false; }

@@ -190,7 +190,7 @@ bool experiments_key(const std::string &k) {
 
 void set_config(const std::string &key, int64_t value) {
 #ifndef GS_EXPERIMENTS
-    if ((value != 0 && experiments_key(key)) || (key == "KS_WAVES" && value != 8))
+    if ((value != 0 && experiments_key(key)) || (key == "KS_WAVES" && value != 8 && value != 4))
         throw gs_error(key + " selects an experiments-build kernel (make -C generalsparse_amd/csrc exp)", -2);
 #endif
     std::lock_guard<std::mutex> l(g_cfg_mu);

@@ -69,8 +69,28 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
         }
     }
 #else
-    GS_CHECK(d.waves == kKsWaves, "k_mfma_ks with 16 waves is an experiments-build variant");
+    GS_CHECK(d.waves == kKsWaves || d.waves == 4, "k_mfma_ks with 16 waves is an experiments-build variant");
 #endif
+    // KS_WAVES = 4: 256-thread workgroups, overlapped LDS (two per CU), N = 32
+    if constexpr (W == (int)kKsWaves && !STAMPS) {
+        if (d.waves == 4) {
+            if constexpr (CT == 2) {
+                GS_CHECK(!d.ks_ap, "k_mfma_ks with 4 waves runs the overlapped LDS layout");
+                auto k4 = d.ks_p8 ? gsk::k_mfma_ks<CT, RT, 4, (int)kKsDepth, MAXG, false, false, true>
+                                  : gsk::k_mfma_ks<CT, RT, 4, (int)kKsDepth, MAXG, false, false, false>;
+                GS_CHECK(gsk::ks_lds_bytes(CT, RT, 4, false) <= d.lds_bytes, "k_mfma_ks: LDS size disagrees with the upload");
+                grant_lds(d.device, k4, d.lds_bytes);
+                hipLaunchKernelGGL(k4, dim3((uint32_t)d.n_rows_aux * d.ksplit, ks_col_tiles_ct(N, CT)), dim3(256), d.lds_bytes,
+                                   s, a.t0, (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, (const gsk::u32x2 *)a.t1, B,
+                                   C, (uint32_t)p.K, N, d.ksplit, d.ks_ns, (uint32_t)d.n_rows_aux * d.ksplit,
+                                   (uint32_t)d.row_base, a.ws, a.t2, stamps, ks_prio_arg());
+                HIP_OK(hipGetLastError());
+                return;
+            } else {
+                throw gs_error("k_mfma_ks with 4 waves is built for N = 32");
+            }
+        }
+    }
     auto kern = gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, STAMPS>;
     if (d.ks_p8) {  // KS_POS8: 8-bit entry positions (N = 32, 8 waves, the apart layout)
         if constexpr (CT == 2 && W == (int)kKsWaves && !STAMPS) {
@@ -226,10 +246,17 @@ void launch_bm(const plan_state &, const device_arrays &, const void *, void *, 
 
 // ---- grouped launches (gs_spmm_batch): N = 32 (CT = 2), 8 waves, one instantiation per group
 namespace {
-template <int RT, int MAXG>
+template <int RT, int MAXG, int W = (int)kKsWaves>
 void launch_ks_group_k(const std::vector<ks_group_item> &it, uint32_t N, hipStream_t s) {
-    auto kern = it[0].p->dev.ks_p8 ? gsk::k_mfma_ks_group<2, RT, (int)kKsWaves, (int)kKsDepth, MAXG, true>
-                                   : gsk::k_mfma_ks_group<2, RT, (int)kKsWaves, (int)kKsDepth, MAXG, false>;
+    if constexpr (W == (int)kKsWaves) {
+        if (it[0].p->dev.waves == 4) {  // KS_WAVES = 4: 256-thread workgroups, overlapped LDS
+            launch_ks_group_k<RT, MAXG, 4>(it, N, s);
+            return;
+        }
+    }
+    constexpr bool AP = W == (int)kKsWaves;
+    auto kern = it[0].p->dev.ks_p8 ? gsk::k_mfma_ks_group<2, RT, W, (int)kKsDepth, MAXG, true, AP>
+                                   : gsk::k_mfma_ks_group<2, RT, W, (int)kKsDepth, MAXG, false, AP>;
     GS_CHECK(!it.empty() && it.size() <= (size_t)gsk::kKsGroupMax, "k_mfma_ks_group: 1..32 entries");
     gsk::ks_group_args args;
     std::memset(&args, 0, sizeof(args));
@@ -239,7 +266,7 @@ void launch_ks_group_k(const std::vector<ks_group_item> &it, uint32_t N, hipStre
         const plan_state &p = *it[i].p;
         const device_plan &d = p.dev;
         const device_arrays &a = d.replicas[(size_t)it[i].replica];
-        GS_CHECK(gsk::ks_lds_bytes(2, RT, kKsWaves) <= d.lds_bytes, "k_mfma_ks_group: LDS size disagrees with the upload");
+        GS_CHECK(gsk::ks_lds_bytes(2, RT, W, AP) <= d.lds_bytes, "k_mfma_ks_group: LDS size disagrees with the upload");
         lds = std::max(lds, d.lds_bytes);
         gsk::ks_entry &e = args.e[i];
         e.tbr = a.t0;
@@ -265,7 +292,7 @@ void launch_ks_group_k(const std::vector<ks_group_item> &it, uint32_t N, hipStre
     args.N = N;
     args.pad[0] = ks_prio_arg();
     grant_lds(it[0].p->dev.device, kern, lds);
-    hipLaunchKernelGGL(kern, dim3(wg, ks_col_tiles(N)), dim3(64 * kKsWaves), lds, s, args);
+    hipLaunchKernelGGL(kern, dim3(wg, ks_col_tiles(N)), dim3(64 * W), lds, s, args);
     HIP_OK(hipGetLastError());
 }
 
@@ -282,9 +309,9 @@ void launch_ks_group_rt(const std::vector<ks_group_item> &it, uint32_t N, hipStr
 
 uint32_t ks_group_key(const plan_state &p, uint32_t N) {
     const device_plan &d = p.dev;
-    if (!p.uploaded || !d.mfma || !d.ks || d.pad_rows || N != 32 || d.lds_N != 32 || d.waves != kKsWaves || !d.ks_ap)
-        return 0;
-    return (d.ks_p8 ? 1u << 16 : 0u) | (d.maxr << 8) | d.seg_cap;  // P8, RT, MAXG: one instantiation
+    const bool w8 = d.waves == kKsWaves && d.ks_ap, w4 = d.waves == 4 && !d.ks_ap;
+    if (!p.uploaded || !d.mfma || !d.ks || d.pad_rows || N != 32 || d.lds_N != 32 || !(w8 || w4)) return 0;
+    return (w4 ? 1u << 17 : 0u) | (d.ks_p8 ? 1u << 16 : 0u) | (d.maxr << 8) | d.seg_cap;  // waves, P8, RT, MAXG
 }
 
 void launch_ks_group(const std::vector<ks_group_item> &it, uint32_t N, hipStream_t s) {

@@ -480,6 +480,42 @@ def test_mfma_ks_pos8_layout_is_exact(rows, split, mfma_everywhere):
         gsa.set_config("KS_SPLIT", 0)
 
 
+@pytest.mark.parametrize("p8", [0, 1])
+@pytest.mark.parametrize("rows,split", [(40, 2), (80, 4), (112, 1), (112, 4), (128, 3)])
+def test_mfma_ks_four_waves(rows, split, p8, mfma_everywhere):
+    """KS_WAVES = 4: 256-thread K-split workgroups with the overlapped LDS layout (two per CU);
+    each wave takes every fourth k-step, so the sums differ from the 8-wave kernel's by rounding
+    only: oracle parity, a bit-identical relaunch, and one grouped launch of two replicas equal
+    to their single launches"""
+    N = 32
+    r, c, v = ds.pruned_weight(640, 2048, 0.7, 12)
+    B = torch.from_numpy(np.random.default_rng(7).uniform(-1, 1, (2048, N)).astype(np.float16)).to(DEV)
+    gsa.set_config("KS_SPLIT", split)
+    gsa.set_config("KS_WAVES", 4)
+    gsa.set_config("KS_POS8", p8)
+    try:
+        plan = gsa.Plan.from_coo(640, 2048, r, c, v).run_pipeline("block_total", N, rows, 1).compile().upload("f16", 0)
+    finally:
+        gsa.set_config("KS_SPLIT", 0)
+        gsa.set_config("KS_WAVES", 8)
+        gsa.set_config("KS_POS8", 0)
+    info = plan.info()
+    assert info["device_kernel"] == "k_mfma_ks" and info["lds_waves"] == 4 and info["ksplit"] == split, info
+    C = plan.spmm(B).float().cpu().numpy()
+    check(C, ofi.spmm_ref(640, N, r, c, v.astype(np.float16).astype(np.float32), B.cpu().numpy().astype(np.float32),
+                          "f64"), "f16")
+    np.testing.assert_array_equal(plan.spmm(B).float().cpu().numpy(), C)
+    plan.add_replica()
+    Cs = [torch.full((640, N), float("nan"), device=DEV, dtype=torch.float16) for _ in range(2)]
+    bat = gsa.Batch([(plan, 0, B, Cs[0]), (plan, 1, B, Cs[1])], N)
+    assert bat.launches() == [2]
+    bat.run(torch.cuda.current_stream().cuda_stream)
+    for cc in Cs:
+        np.testing.assert_array_equal(cc.float().cpu().numpy(), C)
+    plan.device_status()
+    plan.free()
+
+
 @pytest.mark.parametrize("split", [2, 4])
 def test_mfma_ks_slab_tags_alternate_over_launches(split, mfma_everywhere):
     """The K-split combine's slab tags alternate per launch (epoch in the arrival counter, no
