@@ -1,0 +1,93 @@
+#!/bin/bash
+# Round-5 A/B experiments on one GPU box (replaces one script per experiment).
+# Usage: TAG=r05x bash scripts/gpu_experiments.sh <name> [<name> ...]
+#   ks_apart  C2: apart vs overlapped K-split LDS layouts, K splits 2/4/8
+#   n128      k_mfma_ks 128-column tiles: parity, C2 dense-width sweep 8/32/128 (+ DRAM=1: com-Orkut
+#             TCC_EA0_RDREQ vs TCC_EA0_RDREQ_DRAM)
+#   nm4       k_nm_mfma4: 2:4 parity, C3 K-split variants against k_nm_mfma
+#   pos8      8-bit K-split positions and 4-wave workgroups: parity, C2 + north_star layer, 20-row S=1
+#   c4perm    merge-path column permutation: parity, webbase on/off, com-Orkut line + PMC traffic
+#   c4perm2   com-Orkut: gather / scatter / hot-only permutations
+# Every GPU step runs under its own time limit; the first failure ends the session (set -e).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${TAG:-r05x}; mkdir -p $OUT; export TMPDIR=/tmp
+set -e
+pyt() {  # pytest subset: <log> <files/-k ...>
+  local log=$1; shift
+  timeout -k 10 600 python3 -u -m pytest "$@" -x -q --timeout 200 --timeout-method thread > $OUT/$log 2>&1 || { tail -30 $OUT/$log; exit 1; }
+  tail -1 $OUT/$log
+}
+line() {  # bench line summary: <log> <label>
+  python3 -c "
+import json
+d=[json.loads(l) for l in open('$OUT/$1') if l.startswith('{')][-1]
+ns=d.get('north_star') or {}
+print('$2', d['config'].get('plan'), d['config'].get('kernel'), 'us', round(d['ms_per_step']*1e3,2), 'frac', d['roofline']['frac'],
+      'hot_us', round((d['roofline'].get('hot_cache_kernel_ms') or 0)*1e3,2),
+      'layer_us', round((ns.get('ms_per_step') or 0)*1e3,1), 'layer_frac', (ns.get('roofline') or {}).get('frac'))"
+}
+bench() {  # <label> <bench args...>
+  local tag=$1; shift
+  timeout -k 10 900 python3 -u bench.py "$@" > $OUT/b_$tag.log 2>&1
+  line b_$tag.log "$tag"
+}
+for ex in "$@"; do
+  echo "== $ex"
+  case $ex in
+    ks_apart)
+      pyt pytest_apart.log tests/test_gpu_spmm.py -k "overlapped or known_answer_and_c2 or driver_plan"
+      c2="--workload c2 --steps 200 --warmup 50 --no-cpu --no-rocsparse --no-north-star --pipeline block_total"
+      bench base $c2 --p0 40
+      bench ap0_s2 $c2 --p0 40 --config KS_APART=0
+      bench ap0_s4 $c2 --p0 40 --config KS_APART=0 --config KS_SPLIT=4
+      bench ap1_s4 $c2 --p0 40 --config KS_SPLIT=4
+      bench ap0_80s4 $c2 --p0 80 --config KS_APART=0
+      bench ap0_80s8 $c2 --p0 80 --config KS_APART=0 --config KS_SPLIT=8 ;;
+    n128)
+      pyt pytest_ks.log tests/test_gpu_spmm.py -k "mfma_ks or slab or c2"
+      bench c2_nsweep --workload c2 --steps 100 --warmup 20 --no-cpu --no-rocsparse --no-north-star --n-sweep 8,32,128
+      if [ -n "$DRAM" ]; then
+        timeout -s KILL 600 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum --output-format csv -d $OUT/dram_c4o -o p -- \
+          python3 bench.py --workload c4o --pipeline merge_path --p0 512 --steps 3 --warmup 1 --search-reps 2 --search-rounds 1 --no-cpu --no-rocsparse > $OUT/dram_c4o.log 2>&1
+      fi ;;
+    nm4)
+      pyt pytest_nm.log tests/test_gpu_nm.py
+      c3="--workload c3 --steps 100 --warmup 20 --no-cpu --no-rocsparse"
+      bench c3_v4auto $c3
+      bench c3_v4s1 $c3 --config NM_SPLIT=1
+      bench c3_v4s3 $c3 --config NM_SPLIT=3
+      bench c3_v4s4 $c3 --config NM_SPLIT=4
+      bench c3_classic $c3 --config NM_V4=0 ;;
+    pos8)
+      pyt pytest_p8.log tests/test_gpu_spmm.py -k "pos8 or mfma_ks or batch or four_waves"
+      c2="--workload c2 --steps 200 --warmup 50 --no-cpu --no-rocsparse"
+      bench c2_p80 $c2 --config KS_POS8=0
+      bench c2_p81 $c2 --config KS_POS8=1
+      bench c2_w4 $c2 --config KS_WAVES=4
+      bench c2_w4p8 $c2 --config KS_WAVES=4 --config KS_POS8=1
+      bench c2_20s1 $c2 --no-north-star --pipeline block_total --p0 20 --config KS_MIN_ROWS=16
+      bench c2_20s1p8 $c2 --no-north-star --pipeline block_total --p0 20 --config KS_MIN_ROWS=16 --config KS_POS8=1 ;;
+    c4perm)
+      pyt pytest_mp.log tests/test_gpu_spmm.py -k "column_permutation or merge_path"
+      c4="--workload c4 --pipeline merge_path --steps 200 --warmup 20 --no-cpu --no-rocsparse"
+      bench c4_perm0 $c4 --config MP_COL_PERM=0
+      bench c4_perm1 $c4 --config MP_COL_PERM=1
+      bench c4o --workload c4o --steps 20 --warmup 5
+      mkdir -p $OUT/tc4o
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 600 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $OUT/tc4o/$c -o p -- python3 bench.py --workload c4o \
+          --pipeline merge_path --p0 512 --steps 3 --warmup 1 --search-reps 2 --search-rounds 1 --no-cpu --no-rocsparse > $OUT/tc4o/$c.log 2>&1
+      done
+      python3 scripts/traffic_summary.py $OUT/tc4o k_merge_path $OUT/traffic_c4o.json 2083887320 || true
+      python3 scripts/traffic_summary.py $OUT/tc4o k_permute_rows $OUT/traffic_c4o_permute.json || true ;;
+    c4perm2)
+      pyt pytest_perm.log tests/test_gpu_spmm.py -k "column_permutation"
+      c4o="--workload c4o --pipeline merge_path --p0 1024 --steps 20 --warmup 5 --search-reps 5 --search-rounds 1 --no-cpu --no-rocsparse"
+      bench c4o_gather $c4o
+      bench c4o_scatter $c4o --config MP_PERM_SCATTER=1
+      bench c4o_hot256k $c4o --config MP_PERM_HOT=262144
+      bench c4o_hot1m $c4o --config MP_PERM_HOT=1048576 ;;
+    *) echo "unknown experiment $ex"; exit 2 ;;
+  esac
+done
+echo "session $TAG done"
