@@ -3258,9 +3258,11 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma4(const unsigned char 
                                                             float *__restrict__ slabs, uint32_t *__restrict__ arrivals,
                                                             uint32_t flags) {
     constexpr uint32_t N = 16 * CT, RB = 32 * CT, UB = 2 * CT;
-    constexpr uint32_t szB = kNmKC * RB;               // one chunk of B rows in LDS
-    constexpr uint32_t NBW = szB / 16u / (64u * kNmWaves);  // LDS-DMA wave-instructions per wave per chunk
+    constexpr uint32_t HR = kNmKC / 2;                       // B rows of a half chunk (two k-steps)
+    constexpr uint32_t szH = HR * RB;                         // one ring slot
+    constexpr uint32_t NBW = szH / 16u / (64u * kNmWaves);    // LDS-DMA wave-instructions per wave per half
     static_assert(CT == 8 || CT == 4, "k_nm_mfma4: 64- or 128-column tiles");
+    static_assert(4 * szH <= 160u * 1024u, "four ring slots");
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -3269,13 +3271,14 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma4(const unsigned char 
     const uint32_t g = u / S, qs = u - g * S;
     const uint32_t rg = g * 4u + rh;
     const uint32_t nch = S64 / 4u, c0 = qs * ncs, nc = min(ncs, nch - c0);  // this range's chunks
+    const uint32_t nh = 2u * nc;                                             // ... and half chunks
     const unsigned char *arow = A + (size_t)rg * S64 * kNmBlockBytes;
 
-    // ---- B chunk c -> LDS buffer c & 1 by LDS-DMA: wave-instruction i of wave wv fills the
-    // 1 KB at unit (wv*NBW + i)*64 (lane-linear); the piece permutation is applied to the source
-    // Instruction i of wave wv reads B rows k = (wv*NBW + i)*RPI + lane/UB.  b_piece's swizzle of
-    // row k depends on i only through bit 3 of k (bit 1 of i at RPI = 4 rows per instruction,
-    // CT = 8; bit 0 at RPI = 8, CT = 4): two per-lane source offsets, one per parity, cover all
+    // ---- B half chunk h (k-steps 2h, 2h+1 of the range) -> ring slot h & 3 by LDS-DMA:
+    // wave-instruction i of wave wv fills the 1 KB at unit (wv*NBW + i)*64 (lane-linear), rows
+    // k = (wv*NBW + i)*RPI + lane/UB of the half; the piece permutation rides on the source
+    // address.  b_piece's swizzle of row k depends on i only through bit 3 of k (bit 1 of i at
+    // RPI = 4 rows per instruction, CT = 8; bit 0 at RPI = 8, CT = 4): two per-lane offsets
     static_assert(64 % UB == 0, "whole B rows per wave-instruction");
     constexpr uint32_t RPI = 64u / UB;
     auto par_of = [](uint32_t i) -> uint32_t { return RPI == 4 ? (i >> 1) & 1u : i & 1u; };
@@ -3286,9 +3289,9 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma4(const unsigned char 
         const uint32_t k = (wv * NBW + i0_of(par)) * RPI + lane / UB, sp = lane % UB;
         boff[par] = (k * N + (b_piece<CT>(k, sp >> 1) * 2u + (sp & 1u)) * 8u) * 2u;
     }
-    auto issue_b = [&](uint32_t c) {
-        const unsigned char *src0 = reinterpret_cast<const unsigned char *>(B) + (size_t)(c0 + c) * kNmKC * N * 2u;
-        unsigned char *buf = lds + (c & 1u) * szB;
+    auto issue_b = [&](uint32_t h) {
+        const unsigned char *src0 = reinterpret_cast<const unsigned char *>(B) + ((size_t)c0 * kNmKC + (size_t)h * HR) * N * 2u;
+        unsigned char *buf = lds + (h & 3u) * szH;
 #pragma unroll
         for (uint32_t i = 0; i < NBW; i++) {
             const uint32_t par = par_of(i);
@@ -3297,93 +3300,95 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma4(const unsigned char 
                                              (__attribute__((address_space(3))) void *)(buf + u0 * 16u), 16, 0, 0);
         }
     };
-    // ---- A blocks of chunk c: k-steps 4c+q and 4c+q+2 (positions + four 16-row tiles each)
-    u32x4 av0[2][4], av1[2][4];
-    uint2 ai0[2], ai1[2];
-#define GS_NM4_ALOAD(c, V, I)                                                                       \
+    // ---- A block of half h for this wave: k-step 2h + q of the range (positions + four tiles)
+    u32x4 av[3][4];
+    uint2 ai[3];
+#define GS_NM4_ALOAD(h, V, I)                                                                       \
     {                                                                                             \
-        _Pragma("unroll") for (int j = 0; j < 2; j++) {                                           \
-            const unsigned char *blk_ = arow + (size_t)(4u * (c0 + (c)) + q + 2u * j) * kNmBlockBytes; \
-            I[j] = *reinterpret_cast<const uint2 *>(blk_ + lane * 8u);                            \
-            _Pragma("unroll") for (int rt = 0; rt < 4; rt++) V[j][rt] =                           \
-                *reinterpret_cast<const u32x4 *>(blk_ + 512u + rt * 1024u + lane * 16u);          \
-        }                                                                                         \
+        const unsigned char *blk_ = arow + (size_t)(4u * c0 + 2u * (h) + q) * kNmBlockBytes;     \
+        I = *reinterpret_cast<const uint2 *>(blk_ + lane * 8u);                                   \
+        _Pragma("unroll") for (int rt = 0; rt < 4; rt++) V[rt] =                                  \
+            *reinterpret_cast<const u32x4 *>(blk_ + 512u + rt * 1024u + lane * 16u);              \
     }
+    constexpr int NAL = 5;  // vector loads of one A block
     f4v acc[4][CT];
 #pragma unroll
     for (int rt = 0; rt < 4; rt++)
 #pragma unroll
         for (int ct = 0; ct < CT; ct++) acc[rt][ct] = f4v{0.f, 0.f, 0.f, 0.f};
-    // transposed B reads: row k = 64*kk + klane + {0, 4, 32, 36} keeps klane's swizzle bits
+    // transposed B reads: row k = 64*q + klane + {0, 4, 32, 36} keeps klane's swizzle bits
     // (k & 3 and bit 3: klane & 7 <= 3, so +4 carries nowhere), so piece ct of row k sits at
-    // fb[h] ^ (ct << 5) + 64*kk*RB, fb[h] = the row's byte offset + its swizzled piece 0
+    // fb[h] ^ (ct << 5) + 64*q*RB, fb[h] = the row's byte offset + its swizzled piece 0
     const uint32_t klane = 8u * (lane >> 4) + ((lane & 15u) >> 2);
     uint32_t fb[4];
 #pragma unroll
-    for (int h = 0; h < 4; h++) {
-        const uint32_t k = klane + 32u * (h >> 1) + 4u * (h & 1);
-        fb[h] = k * RB + b_piece<CT>(k, 0) * 32u + (lane & 3u) * 8u;
+    for (int hh = 0; hh < 4; hh++) {
+        const uint32_t k = klane + 32u * (hh >> 1) + 4u * (hh & 1);
+        fb[hh] = 64u * q * RB + k * RB + b_piece<CT>(k, 0) * 32u + (lane & 3u) * 8u;
     }
-#define GS_NM4_BFRAG(lb_, kk, ct, BF)                                                               \
+#define GS_NM4_BFRAG(lb_, ct, BF)                                                                   \
     {                                                                                             \
         s4v t_[4];                                                                                \
-        _Pragma("unroll") for (int h = 0; h < 4; h++)                                             \
-            t_[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(                                      \
-                (lds_s4v *)(lb_ + 64u * (kk) * RB + (fb[h] ^ ((uint32_t)(ct) << 5))));           \
+        _Pragma("unroll") for (int hh = 0; hh < 4; hh++)                                          \
+            t_[hh] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v *)(lb_ + (fb[hh] ^ ((uint32_t)(ct) << 5)))); \
         __builtin_memcpy(&BF, t_, 32);                                                            \
     }
-#define GS_NM4_COMPUTE(c, V, I)                                                                     \
+#define GS_NM4_COMPUTE(h, V, I)                                                                     \
     {                                                                                             \
-        const unsigned char *lb_ = lds + ((uint32_t)(c) & 1u) * szB;                              \
-        _Pragma("unroll") for (int j = 0; j < 2; j++) {                                           \
-            h8v av_[4];                                                                           \
-            _Pragma("unroll") for (int rt = 0; rt < 4; rt++) __builtin_memcpy(&av_[rt], &V[j][rt], 16); \
-            const int ix0_ = (int)I[j].x, ix1_ = (int)I[j].y;                                     \
-            h16v bf_[2];                                                                          \
-            GS_NM4_BFRAG(lb_, q + 2u * j, 0, bf_[0]);                                             \
-            _Pragma("unroll") for (int ct = 0; ct < CT; ct++) {                                   \
-                if (ct + 1 < CT) GS_NM4_BFRAG(lb_, q + 2u * j, ct + 1, bf_[(ct + 1) & 1]);        \
-                const h16v b_ = bf_[ct & 1];                                                      \
-                acc[0][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[0], b_, acc[0][ct], ix0_, 0, 0); \
-                acc[1][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[1], b_, acc[1][ct], ix0_, 0, 1); \
-                acc[2][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[2], b_, acc[2][ct], ix1_, 0, 0); \
-                acc[3][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[3], b_, acc[3][ct], ix1_, 0, 1); \
-            }                                                                                     \
+        const unsigned char *lb_ = lds + ((uint32_t)(h) & 3u) * szH;                              \
+        h8v av_[4];                                                                               \
+        _Pragma("unroll") for (int rt = 0; rt < 4; rt++) __builtin_memcpy(&av_[rt], &V[rt], 16);  \
+        const int ix0_ = (int)I.x, ix1_ = (int)I.y;                                               \
+        h16v bf_[2];                                                                              \
+        GS_NM4_BFRAG(lb_, 0, bf_[0]);                                                             \
+        _Pragma("unroll") for (int ct = 0; ct < CT; ct++) {                                       \
+            if (ct + 1 < CT) GS_NM4_BFRAG(lb_, ct + 1, bf_[(ct + 1) & 1]);                        \
+            const h16v b_ = bf_[ct & 1];                                                          \
+            acc[0][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[0], b_, acc[0][ct], ix0_, 0, 0); \
+            acc[1][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[1], b_, acc[1][ct], ix0_, 0, 1); \
+            acc[2][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[2], b_, acc[2][ct], ix1_, 0, 0); \
+            acc[3][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[3], b_, acc[3][ct], ix1_, 0, 1); \
         }                                                                                         \
     }
-    // prologue: B(0), A(0), A(1); B(0) and A(0) retired (A(1)'s 10 loads left in flight)
+    // prologue: B halves 0, 1 and A blocks 0, 1, 2 in flight; half 0 retired (B(1), A(1), A(2)
+    // left in flight: NBW + 2 * NAL loads)
     issue_b(0u);
-    GS_NM4_ALOAD(0u, av0, ai0);
-    if (nc > 1u) {
-        GS_NM4_ALOAD(1u, av1, ai1);
-        __asm__ volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    GS_NM4_ALOAD(0u, av[0], ai[0]);
+    issue_b(1u);  // nh >= 2 (a range holds whole chunks)
+    GS_NM4_ALOAD(1u, av[1], ai[1]);
+    if (nh > 2u) {
+        GS_NM4_ALOAD(2u, av[2], ai[2]);
+        __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"(NBW + 2 * NAL) : "memory");
     } else {
-        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"(NBW + NAL) : "memory");
     }
     __builtin_amdgcn_s_barrier();
-    // iteration c: B(c+1) -> the other buffer (read last in c-1, before the barrier), compute c,
-    // A(c+2) into c's register set, retire B(c+1) and A(c+1) (A(c+2) left in flight), barrier
-#define GS_NM4_ITER(c, V, I)                                                                        \
+    // half iteration h: B(h+2) -> slot (h+2)&3 (read last in h-2, two barriers ago), compute h,
+    // A(h+3) into h's register set, retire B(h+1) and A(h+1) (B(h+2), A(h+2), A(h+3) left in
+    // flight), barrier.  B is issued two half iterations ahead, A three.
+#define GS_NM4_ITER(h, SET)                                                                         \
     {                                                                                             \
-        if ((c) + 1u < nc) issue_b((c) + 1u);                                                     \
+        const bool b2_ = (h) + 2u < nh, a3_ = (h) + 3u < nh;                                      \
+        if (b2_) issue_b((h) + 2u);                                                               \
         __builtin_amdgcn_sched_barrier(0);                                                        \
-        GS_NM4_COMPUTE(c, V, I);                                                                  \
+        GS_NM4_COMPUTE(h, av[SET], ai[SET]);                                                      \
         __builtin_amdgcn_sched_barrier(0);                                                        \
-        if ((c) + 2u < nc) {                                                                      \
-            GS_NM4_ALOAD((c) + 2u, V, I);                                                         \
-            __asm__ volatile("s_waitcnt vmcnt(10)" ::: "memory");                                 \
-        } else {                                                                                  \
-            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");                                  \
-        }                                                                                         \
+        if (a3_) GS_NM4_ALOAD((h) + 3u, av[SET], ai[SET]);                                        \
+        /* younger than B(h+1) and A(h+1): A(h+2) (if any), B(h+2), A(h+3) */                      \
+        if (a3_) __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"(NBW + 2 * NAL) : "memory");         \
+        else if (b2_) __asm__ volatile("s_waitcnt vmcnt(%0)" ::"n"(NBW + NAL) : "memory");        \
+        else __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");                                 \
         __builtin_amdgcn_s_barrier();                                                             \
         __builtin_amdgcn_sched_barrier(0);                                                        \
     }
-    uint32_t c = 0;
-    for (; c + 1u < nc; c += 2u) {
-        GS_NM4_ITER(c, av0, ai0);
-        GS_NM4_ITER(c + 1u, av1, ai1);
+    uint32_t h = 0;
+    for (; h + 2u < nh; h += 3u) {
+        GS_NM4_ITER(h, 0);
+        GS_NM4_ITER(h + 1u, 1);
+        GS_NM4_ITER(h + 2u, 2);
     }
-    if (c < nc) GS_NM4_ITER(c, av0, ai0);
+    if (h < nh) GS_NM4_ITER(h, 0);
+    if (h + 1u < nh) GS_NM4_ITER(h + 1u, 1);
 #undef GS_NM4_ITER
 #undef GS_NM4_COMPUTE
 #undef GS_NM4_BFRAG

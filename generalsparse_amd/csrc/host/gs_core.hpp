@@ -108,7 +108,7 @@ struct config_t {
     int64_t MP_SOLO = 16;        // k_merge_rows: rows of at most this many nonzeros are one slot's
     int64_t KS_WAVES = 8;        // k_mfma_ks waves per workgroup (8 or 16)
     int64_t KS_SPLIT = 0;        // k_mfma_ks K ranges per row block (0: the fewest that fit LDS and fill the CUs)
-    int64_t NM_V4 = -1;          // 2:4 panels on k_nm_mfma4 (256-row workgroups, K split): 1 at N = 64 / 128, 0 never,
+    int64_t NM_V4 = 0;           // 2:4 panels on k_nm_mfma4 (256-row workgroups, K split): 1 at N = 64 / 128, 0 never,
                                  // -1 at N = 128 (K a multiple of 256)
     int64_t KS_POS8 = 0;         // k_mfma_ks at N = 32: 8-bit entry positions in 8 x 16 segments (3 B per nonzero)
     int64_t KS_APART = 1;        // k_mfma_ks: partial tiles beside the wave stages when they fit (1), never (0: the

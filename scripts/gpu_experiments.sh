@@ -8,6 +8,8 @@
 #   pos8      8-bit K-split positions and 4-wave workgroups: parity, C2 + north_star layer, 20-row S=1
 #   c4perm    merge-path column permutation: parity, webbase on/off, com-Orkut line + PMC traffic
 #   c4perm2   com-Orkut: gather / scatter / hot-only permutations
+#   nm4b      k_nm_mfma4 (half-chunk B ring) against k_nm_mfma on C3
+#   exptimeout  the forced K-split timeout test on the experiments library
 # Every GPU step runs under its own time limit; the first failure ends the session (set -e).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-r05x}; mkdir -p $OUT; export TMPDIR=/tmp
@@ -58,6 +60,15 @@ for ex in "$@"; do
       bench c3_v4s3 $c3 --config NM_SPLIT=3
       bench c3_v4s4 $c3 --config NM_SPLIT=4
       bench c3_classic $c3 --config NM_V4=0 ;;
+    nm4b)
+      pyt pytest_nm.log tests/test_gpu_nm.py
+      c3="--workload c3 --steps 100 --warmup 20 --no-cpu --no-rocsparse"
+      bench c3_classic $c3
+      bench c3_v4s2 $c3 --config NM_V4=-1
+      bench c3_v4s1 $c3 --config NM_V4=-1 --config NM_SPLIT=1
+      bench c3_v4s3 $c3 --config NM_V4=-1 --config NM_SPLIT=3 ;;
+    exptimeout)
+      GS_LIBRARY=$PWD/generalsparse_amd/libgeneralsparse_exp.so pyt pytest_exp_timeout.log tests/test_gpu_spmm.py -k "timeout_is_reported" -rA ;;
     pos8)
       pyt pytest_p8.log tests/test_gpu_spmm.py -k "pos8 or mfma_ks or batch or four_waves"
       c2="--workload c2 --steps 200 --warmup 50 --no-cpu --no-rocsparse"

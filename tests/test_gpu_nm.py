@@ -167,7 +167,8 @@ def test_nm_ks_and_classic_kernels(shape, N, ks, split):
         M, K = shape
         r, c, v = thinned(M, K, 70 + M, keep=0.8, empty_rows=(0, M // 2) if M > 2 else ())
         plan = plan_for(M, K, r, c, v, N)
-        classic = "k_nm_mfma4" if N == 128 and K % 256 == 0 else "k_nm_mfma"
+        v4 = gsa.get_config("NM_V4")
+        classic = "k_nm_mfma4" if K % 256 == 0 and ((v4 < 0 and N == 128) or (v4 > 0 and N in (64, 128))) else "k_nm_mfma"
         assert plan.info()["device_kernel"] == ("k_nm_mfma_ks" if ks else classic), plan.info()
         B = np.random.default_rng(M + N).uniform(-1, 1, (K, N)).astype(np.float16)
         ref = ofi.spmm_ref(M, N, r, c, v.astype(np.float16).astype(np.float32), B.astype(np.float32), "f64")
