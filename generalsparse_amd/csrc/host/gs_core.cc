@@ -185,12 +185,12 @@ config_t get_config() {
 // measured slower than the default kernels, parity-tested there
 bool experiments_key(const std::string &k) {
     return k == "MFMA_BM" || k == "NM_KS" || k == "MFMA_FLAGS" || k == "BM_V2" || k == "BM_KB" || k == "MP_ROWS" ||
-           k == "KS_FORCE_TIMEOUT";
+           k == "KS_FORCE_TIMEOUT" || k == "KS_POS8" || k == "NM_V4";
 }
 
 void set_config(const std::string &key, int64_t value) {
 #ifndef GS_EXPERIMENTS
-    if ((value != 0 && experiments_key(key)) || (key == "KS_WAVES" && value != 8 && value != 4))
+    if ((value != 0 && experiments_key(key)) || (key == "KS_WAVES" && value != 8) || (key == "KS_APART" && value != 1))
         throw gs_error(key + " selects an experiments-build kernel (make -C generalsparse_amd/csrc exp)", -2);
 #endif
     std::lock_guard<std::mutex> l(g_cfg_mu);

@@ -68,10 +68,8 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
             return;
         }
     }
-#else
-    GS_CHECK(d.waves == kKsWaves || d.waves == 4, "k_mfma_ks with 16 waves is an experiments-build variant");
-#endif
-    // KS_WAVES = 4: 256-thread workgroups, overlapped LDS (two per CU), N = 32
+    // measured slower than the default form, experiments build only:
+    // KS_WAVES = 4 (256-thread workgroups, overlapped LDS), KS_POS8 (8-bit positions), KS_APART = 0
     if constexpr (W == (int)kKsWaves && !STAMPS) {
         if (d.waves == 4) {
             if constexpr (CT == 2) {
@@ -91,7 +89,12 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
             }
         }
     }
+#else
+    GS_CHECK(d.waves == kKsWaves && !d.ks_p8 && d.ks_ap,
+             "k_mfma_ks with 4 or 16 waves, 8-bit positions or the overlapped LDS layout: experiments build");
+#endif
     auto kern = gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, STAMPS>;
+#ifdef GS_EXPERIMENTS
     if (d.ks_p8) {  // KS_POS8: 8-bit entry positions (N = 32, 8 waves, the apart layout)
         if constexpr (CT == 2 && W == (int)kKsWaves && !STAMPS) {
             GS_CHECK(d.ks_ap, "k_mfma_ks: 8-bit positions are built with the apart LDS layout");
@@ -106,6 +109,7 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
         else
             throw gs_error("k_mfma_ks: the overlapped-LDS layout is built for N = 32, RT <= 5, MAXG <= 2");
     }
+#endif
     // the LDS this instantiation needs at the plan's range width, against what the upload sized
     GS_CHECK(gsk::ks_lds_bytes(CT, RT, W, d.ks_ap) <= d.lds_bytes, "k_mfma_ks: LDS size disagrees with the upload");
     grant_lds(d.device, kern, d.lds_bytes);
@@ -248,15 +252,19 @@ void launch_bm(const plan_state &, const device_arrays &, const void *, void *, 
 namespace {
 template <int RT, int MAXG, int W = (int)kKsWaves>
 void launch_ks_group_k(const std::vector<ks_group_item> &it, uint32_t N, hipStream_t s) {
+    constexpr bool AP = W == (int)kKsWaves;
+#ifdef GS_EXPERIMENTS
     if constexpr (W == (int)kKsWaves) {
         if (it[0].p->dev.waves == 4) {  // KS_WAVES = 4: 256-thread workgroups, overlapped LDS
             launch_ks_group_k<RT, MAXG, 4>(it, N, s);
             return;
         }
     }
-    constexpr bool AP = W == (int)kKsWaves;
     auto kern = it[0].p->dev.ks_p8 ? gsk::k_mfma_ks_group<2, RT, W, (int)kKsDepth, MAXG, true, AP>
                                    : gsk::k_mfma_ks_group<2, RT, W, (int)kKsDepth, MAXG, false, AP>;
+#else
+    auto kern = gsk::k_mfma_ks_group<2, RT, W, (int)kKsDepth, MAXG, false, AP>;
+#endif
     GS_CHECK(!it.empty() && it.size() <= (size_t)gsk::kKsGroupMax, "k_mfma_ks_group: 1..32 entries");
     gsk::ks_group_args args;
     std::memset(&args, 0, sizeof(args));

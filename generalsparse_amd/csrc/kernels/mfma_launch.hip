@@ -202,6 +202,7 @@ void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, vo
 
 }  // namespace
 
+#ifdef GS_EXPERIMENTS  // k_nm_mfma4: measured slower than k_nm_mfma on C3
 template <int CT>
 void launch_nm4(const plan_state &p, const device_arrays &a, const void *B, void *C, hipStream_t s) {
     const device_plan &d = p.dev;
@@ -230,13 +231,19 @@ void launch_nm4(const plan_state &p, const device_arrays &a, const void *B, void
     HIP_OK(hipGetLastError());
 }
 
+#endif
+
 void launch_nm(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
     if (p.dev.nm4) {
+#ifdef GS_EXPERIMENTS
         switch (N) {
             case 64: launch_nm4<4>(p, a, B, C, s); return;
             case 128: launch_nm4<8>(p, a, B, C, s); return;
             default: throw gs_error("k_nm_mfma4 plan built for N = 64 / 128, not " + std::to_string(N), -2);
         }
+#else
+        throw gs_error("k_nm_mfma4 is an experiments-build kernel (make -C generalsparse_amd/csrc exp)", -2);
+#endif
     }
     switch (N) {
         case 8: launch_nm_ct<1, 8>(p, a, B, C, s); break;  // one half-used 16-column tile

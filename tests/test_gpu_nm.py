@@ -194,6 +194,7 @@ def test_nm4_matches_oracle(shape, N, split):
     ranges, B by LDS-DMA, tagged-slab combine): oracle parity (rows not a multiple of 256, empty
     rows, one-chunk ranges), bit-identical relaunch and replica, and agreement with k_nm_mfma
     within the fp16 rounding of the final store"""
+    need_experiments()
     M, K = shape
     old = {k: gsa.get_config(k) for k in ("NM_V4", "NM_SPLIT")}
     try:

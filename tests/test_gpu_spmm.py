@@ -416,6 +416,7 @@ def test_mfma_ks_tall_blocks_match_oracle(rows, N, split, mfma_everywhere):
 def test_mfma_ks_overlapped_lds_layout(rows, split, mfma_everywhere):
     """KS_APART = 0: the partial tiles reuse the stage LDS after the loop barrier (more
     workgroups per CU); same sums in the same order as the apart layout: bit-identical C"""
+    need_experiments()
     N = 32
     r, c, v = ds.pruned_weight(640, 2048, 0.7, 6)
     B = torch.from_numpy(np.random.default_rng(2).uniform(-1, 1, (2048, N)).astype(np.float16)).to(DEV)
@@ -446,6 +447,7 @@ def test_mfma_ks_pos8_layout_is_exact(rows, split, mfma_everywhere):
     """KS_POS8: 8-bit entry positions in 8 x 16 segments (3 B per nonzero) build the same wave
     images as the u16 positions, so C is bit-identical (and matches the oracle), single and
     grouped launches alike"""
+    need_experiments()
     N = 32
     cases = [ds.pruned_weight(640, 2048, 0.7, 8), ds.random_rows(640, 2048, 400.0, seed=3, empty_frac=0.2)]
     gsa.set_config("KS_SPLIT", split)
@@ -487,6 +489,7 @@ def test_mfma_ks_four_waves(rows, split, p8, mfma_everywhere):
     each wave takes every fourth k-step, so the sums differ from the 8-wave kernel's by rounding
     only: oracle parity, a bit-identical relaunch, and one grouped launch of two replicas equal
     to their single launches"""
+    need_experiments()
     N = 32
     r, c, v = ds.pruned_weight(640, 2048, 0.7, 12)
     B = torch.from_numpy(np.random.default_rng(7).uniform(-1, 1, (2048, N)).astype(np.float16)).to(DEV)
