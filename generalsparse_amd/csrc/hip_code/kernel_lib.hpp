@@ -65,12 +65,36 @@ __device__ __forceinline__ void store_f32(VT *__restrict__ p, const float (&in)[
     *reinterpret_cast<R *>(p) = r;
 }
 
-// SCF contiguous sparse entries (cols or vals) in one load
+// Loads of the operand a launch reads exactly once (A's entries, groups, panels).  GS_A_NT=1
+// (make A_NT=1): the non-temporal form (global_load ... nt), which the XCD's L2 holds at low
+// retention, so the stream does not push out the rows of B that other workgroups re-read.
+template <class T>
+__device__ __forceinline__ T ld_once(const T *p) {
+#if defined(GS_A_NT) && GS_A_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+template <int BYTES> struct raw_ext;
+template <> struct raw_ext<1> { typedef uint8_t t; };
+template <> struct raw_ext<2> { typedef uint16_t t; };
+template <> struct raw_ext<4> { typedef uint32_t t; };
+template <> struct raw_ext<8> { typedef u32x2 t; };
+template <> struct raw_ext<16> { typedef u32x4 t; };
+
+// SCF contiguous sparse entries (cols or vals) in one load (read once: ld_once)
 template <class T, int SCF>
 __device__ __forceinline__ void load_raw(const T *__restrict__ p, T (&out)[SCF]) {
-    typedef typename raw_vec<SCF * sizeof(T)>::t R;
-    R r = *reinterpret_cast<const R *>(p);
-    __builtin_memcpy(out, &r, sizeof(R));
+    if constexpr (SCF * sizeof(T) <= 16) {
+        typedef typename raw_ext<SCF * sizeof(T)>::t R;
+        R r = ld_once(reinterpret_cast<const R *>(p));
+        __builtin_memcpy(out, &r, sizeof(R));
+    } else {
+        static_assert(SCF * sizeof(T) == 32, "8 to 32 bytes");
+        u32x4 r[2] = {ld_once(reinterpret_cast<const u32x4 *>(p)), ld_once(reinterpret_cast<const u32x4 *>(p) + 1)};
+        __builtin_memcpy(out, r, 32);
+    }
 }
 
 template <int CF>
@@ -1690,8 +1714,8 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
         for (int j = 0; j < MAXG; j++) {
             const uint32_t qg = lane + 64u * j;
             const size_t at = (size_t)b0 + (qg < gc ? qg : 0u);
-            P_[j] = tPp[at];
-            V_[j] = tV[at];
+            P_[j] = ld_once(tPp + at);
+            V_[j] = ld_once(tV + at);
         }
     };
 #pragma unroll
@@ -2829,9 +2853,10 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
     if (DBG != 2 || (uint32_t)(c) < 2u) {                                                         \
         const uint32_t cc_ = jr(min((uint32_t)(c), nch - 1u));                                    \
         const unsigned char *blk_ = arow + (size_t)(4u * cc_ + q) * kNmBlockBytes;                \
-        I = *reinterpret_cast<const uint2 *>(blk_ + lane * 8u);                                   \
+        const u32x2 i_ = ld_once(reinterpret_cast<const u32x2 *>(blk_ + lane * 8u));              \
+        I = make_uint2(i_[0], i_[1]);                                                             \
         _Pragma("unroll") for (int rt = 0; rt < 4; rt++) V[rt] =                                  \
-            *reinterpret_cast<const u32x4 *>(blk_ + 512u + rt * 1024u + lane * 16u);              \
+            ld_once(reinterpret_cast<const u32x4 *>(blk_ + 512u + rt * 1024u + lane * 16u));      \
     }
     u32x4 bs[NBU];
     // whole chunks: one lane offset, uniform bases; the last partial chunk clamps rows
@@ -3306,9 +3331,10 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma4(const unsigned char 
 #define GS_NM4_ALOAD(h, V, I)                                                                       \
     {                                                                                             \
         const unsigned char *blk_ = arow + (size_t)(4u * c0 + 2u * (h) + q) * kNmBlockBytes;     \
-        I = *reinterpret_cast<const uint2 *>(blk_ + lane * 8u);                                   \
+        const u32x2 i_ = ld_once(reinterpret_cast<const u32x2 *>(blk_ + lane * 8u));              \
+        I = make_uint2(i_[0], i_[1]);                                                             \
         _Pragma("unroll") for (int rt = 0; rt < 4; rt++) V[rt] =                                  \
-            *reinterpret_cast<const u32x4 *>(blk_ + 512u + rt * 1024u + lane * 16u);              \
+            ld_once(reinterpret_cast<const u32x4 *>(blk_ + 512u + rt * 1024u + lane * 16u));      \
     }
     constexpr int NAL = 5;  // vector loads of one A block
     f4v acc[4][CT];

@@ -98,6 +98,23 @@ for ex in "$@"; do
       bench c4o_scatter $c4o --config MP_PERM_SCATTER=1
       bench c4o_hot256k $c4o --config MP_PERM_HOT=262144
       bench c4o_hot1m $c4o --config MP_PERM_HOT=1048576 ;;
+    nt)  # A's once-read loads non-temporal (libgeneralsparse_var.so built with VAR_FLAGS=-DGS_A_NT=1)
+      VAR=$PWD/generalsparse_amd/libgeneralsparse_var.so
+      GS_LIBRARY=$VAR pyt pytest_nt.log tests/test_gpu_spmm.py tests/test_gpu_nm.py -k "c2 or mfma_ks or nm or merge_path or headline"
+      c2="--workload c2 --steps 200 --warmup 50 --no-cpu --no-rocsparse"
+      bench c2_base $c2
+      GS_LIBRARY=$VAR bench c2_nt $c2
+      c3="--workload c3 --steps 100 --warmup 20 --no-cpu --no-rocsparse"
+      bench c3_base $c3
+      GS_LIBRARY=$VAR bench c3_nt $c3
+      c1="--workload c1 --steps 200 --warmup 20 --no-cpu --no-rocsparse"
+      bench c1_base $c1
+      GS_LIBRARY=$VAR bench c1_nt $c1
+      c4o="--workload c4o --pipeline merge_path --p0 1024 --steps 20 --warmup 5 --search-reps 5 --search-rounds 1 --no-cpu --no-rocsparse"
+      bench c4o_base $c4o
+      GS_LIBRARY=$VAR bench c4o_nt $c4o
+      GS_LIBRARY=$VAR bench c2_nt2 $c2
+      bench c2_base2 $c2 ;;
     *) echo "unknown experiment $ex"; exit 2 ;;
   esac
 done
