@@ -133,13 +133,17 @@ WORKLOADS["c2"]["dtype"] = "f16"
 # (pipeline, p0, p1).  tblock_warp_total(rows per BMTB, rows per BMW) runs the
 # LDS-stationary-B kernel when its BMTBs fit one workgroup; the others are the
 # reference's token_test plans on the gather kernels.
+# A 4th element holds config overrides set while the candidate is built and uploaded: KS_NT = the
+# k_mfma_ks groups by non-temporal loads (C2 -4%, profiles/r05l_nt.txt).
 CANDIDATES = [("block_total", 20, 1), ("block_total", 10, 1), ("block_total", 40, 1), ("block_total", 80, 1),
+              ("block_total", 40, 1, {"KS_NT": 1}), ("block_total", 80, 1, {"KS_NT": 1}),
               ("tblock_warp_total", 20, 2), ("tblock_warp_total", 4, 1), ("warp_segment", 4, 1),
               ("thread_total", 4, 1)]
 
 
 # C3: the col-direction plan (32-nnz BMTs = 64-column k-steps of a 2:4 row)
-CANDIDATES_C3 = [("col_direction_nm", 32, 1)]
+# (NM_NT: A's panel blocks by non-temporal loads, on by default: C3 72.0 -> 66.9 us, profiles/r05l_nt.txt)
+CANDIDATES_C3 = [("col_direction_nm", 32, 1), ("col_direction_nm", 32, 1, {"NM_NT": 0})]
 
 # C1: token_test's default (thread_total, sparse_cf 4) and the row-block / merge-path plans
 CANDIDATES_C1 = [("thread_total", 4, 1), ("tblock_warp_total", 4, 1), ("tblock_warp_total", 32, 8), ("merge_path", 512, 1)]
@@ -549,7 +553,7 @@ def layer_traffic(N, sp, plans_by_shape):
 
 
 def cand_key(c):
-    return "%s(%d,%d)%s" % (c[0], c[1], c[2], "".join(f" {a}={b}" for a, b in c[3].items()))
+    return "%s(%d,%d)%s" % (c[0], c[1], c[2], "".join(f" {a}={b}" for a, b in (c[3] if len(c) > 3 else {}).items()))
 
 
 def headline_layer(args, torch, gsa, ds, rank, local, dev, choice, steps, warmup, per_shape=None, rs_per_shape=None):
@@ -721,11 +725,21 @@ def event_ms(plan, Bs, Cs, reps, torch, warm=20, rotate=True):
 
 
 def build_plan(gsa, M, K, row, col, val, cand, N, dt, local, rotation_mb, e, tdt, dev, torch):
-    name, p0, p1 = cand
-    t0 = time.perf_counter()
-    plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline(name, N, p0, p1).compile()
-    t_plan = time.perf_counter() - t0
-    plan.upload(dt, local)
+    """a candidate's plan with its replicas and B / C buffers; cand = (pipeline, p0, p1[, config
+    overrides held while the plan is compiled and uploaded])"""
+    name, p0, p1 = cand[:3]
+    over = cand[3] if len(cand) > 3 else {}
+    old = {k: gsa.get_config(k) for k in over}
+    try:
+        for k, v in over.items():
+            gsa.set_config(k, v)
+        t0 = time.perf_counter()
+        plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline(name, N, p0, p1).compile()
+        t_plan = time.perf_counter() - t0
+        plan.upload(dt, local)
+    finally:
+        for k, v in old.items():
+            gsa.set_config(k, v)
     info = plan.info()
     reps = replicas_for(info, K, N, e, rotation_mb)
     for _ in range(reps - 1):
@@ -843,7 +857,7 @@ def main():
             plan_.free()
 
     for cand in cands:
-        key = f"{cand[0]}({cand[1]},{cand[2]})"
+        key = cand_key(cand)
         try:
             plan, Bs, Cs, reps, t_plan = build_plan(gsa, M, K, row, col, val, cand, N, dt, local, args.rotation_mb, e,
                                                     tdt, dev, torch)
@@ -890,7 +904,7 @@ def main():
     if os.path.exists(tf):
         try:
             tj = json.load(open(tf))
-            if tj.get("kernel") in (None, kernel_label(info)):
+            if tj.get("kernel") in (None, kernel_label(info)) and tj.get("plan") in (None, key):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -900,7 +914,7 @@ def main():
     if os.path.exists(mf) and kernel_label(info).startswith(("k_mfma", "k_nm")):
         try:
             mj = json.load(open(mf))
-            if mj.get("kernel") == kernel_label(info):
+            if mj.get("kernel") == kernel_label(info) and mj.get("plan") in (None, key):
                 mfma = {k: mj[k] for k in ("mfma_util", "formula", "mfma_util_grbm", "analytic", "kernel_ns_median")
                         if k in mj}
                 mfma["source"] = os.path.relpath(mf, ROOT)
@@ -970,7 +984,7 @@ def n_sweep(gsa, M, K, row, col, val, cands, args, dt, local, e, tdt, dev, torch
     for n in [int(x) for x in args.n_sweep.split(",") if x]:
         tried, best = {}, None
         for cand in cands:
-            key = "%s(%d,%d)" % cand
+            key = cand_key(cand)
             try:
                 plan, Bs, Cs, reps, _ = build_plan(gsa, M, K, row, col, val, cand, n, dt, local, args.rotation_mb, e,
                                                    tdt, dev, torch)
@@ -1016,7 +1030,9 @@ def rocsparse_compare(gsa, M, K, N, row, col, val, dt, cands, args, local, flops
         res["speedup_vs_rocsparse"] = round(ours / rs16["gflops"], 3)
     tried, best32 = {}, None
     for cand in cands:
-        key = "%s(%d,%d)" % cand
+        if len(cand) > 3:  # config variants of the fp16 matrix-core kernels (KS_NT, NM_NT): no fp32 plan
+            continue
+        key = cand_key(cand)
         try:
             plan, Bs, Cs, reps, _ = build_plan(gsa, M, K, row, col, val, cand, N, "f32", local, args.rotation_mb, 4,
                                                torch.float32, dev, torch)

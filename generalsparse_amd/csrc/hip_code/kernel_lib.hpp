@@ -76,6 +76,13 @@ __device__ __forceinline__ T ld_once(const T *p) {
     return *p;
 #endif
 }
+// the same, chosen per instantiation (k_mfma_ks KS_NT, k_nm_mfma NM_NT): NT loads bypass the CU's
+// L1 and stream through L2 (MI355X_MICROARCH.md: nt loads are L2-served)
+template <bool NT, class T>
+__device__ __forceinline__ T ld_once_if(const T *p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return ld_once(p);
+}
 template <int BYTES> struct raw_ext;
 template <> struct raw_ext<1> { typedef uint8_t t; };
 template <> struct raw_ext<2> { typedef uint16_t t; };
@@ -1560,7 +1567,8 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
 // the step's 32 B rows and its entries (upload layout: the step's groups back to back,
 // each 8 x [u16 halfword position in the wave's dense image] + 8 x [f16 value], found by
 // the step's {first group, group count} record, loaded D steps ahead of the groups;
-// padding inside a group writes 0 into the image's zero row), stores the B rows into its private stage (32-B pieces
+// padding inside a group writes 0 into the image's zero row; NT: the groups by non-temporal
+// loads when NTL & 1, B's rows when NTL & 2: KS_NT), stores the B rows into its private stage (32-B pieces
 // permuted by b_piece so the ds_read_b64_tr_b16 fragment reads are conflict-free),
 // scatters the entries into its private image of 16*RT+1 rows x 96 B (conflict-free
 // ds_read_b128), reads the RT A fragments and the CT B fragments, writes zeros back at
@@ -1640,7 +1648,7 @@ __device__ __forceinline__ u32x4 ks_slab_wait(const uint32_t *src, uint32_t tag,
 // P8 (KS_POS8, device_layout.cc pos8_step): tP holds 8 bytes per group -- byte e = bit e of the
 // group's 8 x 16 segment id in bit 7, the entry's (row % 8) << 4 | column % 16 below; the image
 // halfword of a segment sg's entry is 384 * (sg >> 1) + 16 * (sg & 1) + 48 * (b >> 4) + (b & 15)
-template <int CT, int RT, int W, int D, int MAXG, bool STAMPS, bool AP = true, bool P8 = false>
+template <int CT, int RT, int W, int D, int MAXG, bool STAMPS, bool AP = true, bool P8 = false, int NTL = 0>
 __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_row, const u32x4 *__restrict__ tP,
                                         const u32x4 *__restrict__ tV, const u32x2 *__restrict__ steps,
                                         const f16 *__restrict__ B, f16 *__restrict__ C, uint32_t K, uint32_t N, uint32_t S,
@@ -1702,7 +1710,8 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
             const uint32_t k = kr + un / UB, cu = (un % UB) * 8u;
             // columns past N (a partial column tile: N = 8, 24, ...) read column 0 and are
             // stored as zeros below
-            B_[c] = *reinterpret_cast<const u32x4 *>(B + (size_t)(k < K ? k : K - 1u) * N + col0 + (cu < nv ? cu : 0u));
+            B_[c] = ld_once_if<(NTL & 2) != 0>(
+                reinterpret_cast<const u32x4 *>(B + (size_t)(k < K ? k : K - 1u) * N + col0 + (cu < nv ? cu : 0u)));
         }
     };
     auto load_g = [&](uint32_t i, u32x2 &NX_, uint32_t &CN_, PV (&P_)[MAXG], u32x4 (&V_)[MAXG]) {
@@ -1714,8 +1723,8 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
         for (int j = 0; j < MAXG; j++) {
             const uint32_t qg = lane + 64u * j;
             const size_t at = (size_t)b0 + (qg < gc ? qg : 0u);
-            P_[j] = ld_once(tPp + at);
-            V_[j] = ld_once(tV + at);
+            P_[j] = ld_once_if<(NTL & 1) != 0>(tPp + at);
+            V_[j] = ld_once_if<(NTL & 1) != 0>(tV + at);
         }
     };
 #pragma unroll
@@ -1958,7 +1967,7 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
 #undef GS_KS_STAMP
 }
 
-template <int CT, int RT, int W, int D, int MAXG, bool STAMPS = false, bool AP = true, bool P8 = false>
+template <int CT, int RT, int W, int D, int MAXG, bool STAMPS = false, bool AP = true, bool P8 = false, int NTL = 0>
 __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__ bmtb_first_row,  // nb+1
                                                     const u32x4 *__restrict__ tP,  // 8 x u16 position per group
                                                     const u32x4 *__restrict__ tV,  // 8 x f16 value per group
@@ -1969,7 +1978,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
                                                     uint32_t *__restrict__ arrivals, uint64_t *__restrict__ stamps = nullptr,
                                                     uint32_t prio = 0) {
     // nwg == gridDim.x (an argument: kernarg preload)
-    ks_body<CT, RT, W, D, MAXG, STAMPS, AP, P8>(bmtb_first_row, tP, tV, steps, B, C, K, N, S, NS, nwg, row_base, slabs,
+    ks_body<CT, RT, W, D, MAXG, STAMPS, AP, P8, NTL>(bmtb_first_row, tP, tV, steps, B, C, K, N, S, NS, nwg, row_base, slabs,
                                                 arrivals, stamps, blockIdx.x, prio);
 }
 
@@ -1999,7 +2008,7 @@ struct ks_group_args {
     ks_entry e[kKsGroupMax];
 };
 
-template <int CT, int RT, int W, int D, int MAXG, bool P8 = false, bool AP = true>
+template <int CT, int RT, int W, int D, int MAXG, bool P8 = false, bool AP = true, int NTL = 0>
 __global__ __launch_bounds__(64 * W) void k_mfma_ks_group(ks_group_args args) {
     const uint32_t bx = blockIdx.x, n = args.n;
     uint32_t sel = 0;
@@ -2009,7 +2018,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks_group(ks_group_args args) {
     sel = __builtin_amdgcn_readfirstlane(sel);
     const ks_entry &e = args.e[sel];  // kernel arguments: scalar loads at a computed offset
     if (bx - args.begin[sel] >= e.nwg) return;  // padding up to the next entry's multiple of 8
-    ks_body<CT, RT, W, D, MAXG, false, AP, P8>(e.tbr, e.tP, e.tV, e.steps, e.B, e.C, e.K, args.N, e.S, e.NS, e.nwg, e.row_base,
+    ks_body<CT, RT, W, D, MAXG, false, AP, P8, NTL>(e.tbr, e.tP, e.tV, e.steps, e.B, e.C, e.K, args.N, e.S, e.NS, e.nwg, e.row_base,
                                        e.slabs, e.arrivals, nullptr, bx - args.begin[sel], args.pad[0]);
 }
 
@@ -2814,7 +2823,7 @@ typedef _Float16 h16v __attribute__((ext_vector_type(16)));
 // 4 = s_memtime phase stamps of waves 0/4 of workgroups 0 and 100, printed
 // NG: the dense width in HBM (B and C row length); NG = 8 runs one 16-column tile whose
 // columns 8..15 are zeros in LDS and never stored (N = 8, the half-used tile of C3's N sweep)
-template <int CT, int DBG = 0, int NG = 16 * CT>
+template <int CT, int DBG = 0, int NG = 16 * CT, bool NT = false>
 __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *__restrict__ A,
                                                            const f16 *__restrict__ B, f16 *__restrict__ C,
                                                            uint32_t K, uint32_t S, uint32_t rows,
@@ -2853,10 +2862,10 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
     if (DBG != 2 || (uint32_t)(c) < 2u) {                                                         \
         const uint32_t cc_ = jr(min((uint32_t)(c), nch - 1u));                                    \
         const unsigned char *blk_ = arow + (size_t)(4u * cc_ + q) * kNmBlockBytes;                \
-        const u32x2 i_ = ld_once(reinterpret_cast<const u32x2 *>(blk_ + lane * 8u));              \
+        const u32x2 i_ = ld_once_if<NT>(reinterpret_cast<const u32x2 *>(blk_ + lane * 8u));      \
         I = make_uint2(i_[0], i_[1]);                                                             \
         _Pragma("unroll") for (int rt = 0; rt < 4; rt++) V[rt] =                                  \
-            ld_once(reinterpret_cast<const u32x4 *>(blk_ + 512u + rt * 1024u + lane * 16u));      \
+            ld_once_if<NT>(reinterpret_cast<const u32x4 *>(blk_ + 512u + rt * 1024u + lane * 16u)); \
     }
     u32x4 bs[NBU];
     // whole chunks: one lane offset, uniform bases; the last partial chunk clamps rows

@@ -264,7 +264,8 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
           << "ull + 4);\n";
         const std::string k = "gsk::k_mfma_ks<" + std::to_string(CT) + ", " + std::to_string(t.RT) + ", " +
                               std::to_string(t.W) + ", " + std::to_string(kKsDepth) + ", " + std::to_string(t.MAXG) +
-                              std::string(", false, ") + (t.AP ? "true" : "false") + ", " + (t.P8 ? "true" : "false") + ">";
+                              std::string(", false, ") + (t.AP ? "true" : "false") + ", " + (t.P8 ? "true" : "false") +
+                              (t.NT ? ", " + std::to_string(t.NT) + ">" : ">");
         setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
                 std::to_string(t.lds_bytes) + ")";
         launch = k + "<<<dim3(" + std::to_string(nwg) + ", " + std::to_string(NT) + "), " +
@@ -349,7 +350,8 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
     } else {
         o << "    unsigned char *d_blk = up(rdb<unsigned char>(\"THREAD_META_nm_panels_0.bin\"));\n";
         // N = 8: one half-used 16-column tile (k_nm_mfma's NG)
-        const std::string k = "gsk::k_nm_mfma<" + std::to_string(CT) + (N == 8 ? ", 0, 8>" : ">");
+        const std::string k = "gsk::k_nm_mfma<" + std::to_string(CT) + ", 0, " + std::to_string(N == 8 ? 8 : 16 * CT) +
+                              (L.nm_nt ? ", true>" : ">");
         const size_t lds = (size_t)2 * gsk::kNmKC * 32 * CT;
         setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
                 std::to_string(lds) + ")";

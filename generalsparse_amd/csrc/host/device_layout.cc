@@ -340,6 +340,7 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     t.W = W;
     // KS_POS8 (8-bit positions in 8 x 16 segments; N = 32, RT <= 8: segment ids < 32)
     t.P8 = get_config().KS_POS8 && CT == 2 && (W == kKsWaves || W == 4);
+    t.NT = CT == 2 && W == kKsWaves && !t.P8 && t.AP ? (uint32_t)(get_config().KS_NT & 3) : 0u;
     // pass 1: the largest step (entries of a row block in 32 columns; P8: groups per segment)
     uint64_t gmax = 1;
     {
@@ -634,6 +635,7 @@ mc_layout choose_matrix_core_layout(const meta_data_set &m, const kernel_spec &s
             L.nm_ks = cfg.NM_KS != 0 && Nd >= 16;
             L.nm4 = !L.nm_ks && K % gsk::kNmKC == 0 && nch >= 2 &&
                     ((cfg.NM_V4 > 0 && (Nd == 64 || Nd == 128)) || (cfg.NM_V4 < 0 && Nd == 128));
+            L.nm_nt = cfg.NM_NT != 0 && !L.nm_ks && !L.nm4;
             L.nm_ncs = (nch + sp - 1) / sp;
             L.nm_split = (nch + L.nm_ncs - 1) / L.nm_ncs;
         }

@@ -55,6 +55,7 @@ struct ks_tiles {
     uint32_t CT = 0;  // 16-column MFMA tiles per workgroup (ks_ct_rt)
     bool AP = true;   // partial tiles beside the stages (ks_red_apart; KS_APART)
     bool P8 = false;  // 8-bit positions (KS_POS8): pos8 instead of pos, see build_ks_tiles
+    uint32_t NT = 0;  // non-temporal loads, bit 0 A's groups, bit 1 B's rows (KS_NT; N = 32, 8 waves, apart layout)
     size_t lds_bytes = 0;
     std::vector<uint16_t> pos, val;  // 8 u16 per group each
     std::vector<uint8_t> pos8;       // P8: 8 bytes per group
@@ -119,6 +120,7 @@ struct mc_layout {
     uint64_t nm_rows = 0;
     bool nm_ks = false;                    // k_nm_mfma_ks (256-row workgroups, K split) instead of k_nm_mfma
     bool nm4 = false;                      // k_nm_mfma4 (256-row workgroups of 8 waves, K split, B by LDS-DMA)
+    bool nm_nt = false;                    // k_nm_mfma: A's panel blocks by non-temporal loads (NM_NT)
     uint32_t nm_split = 1, nm_ncs = 0;     // ... K ranges per row block, 256-column chunks per range
     std::string why;  // why NONE
 };

@@ -316,6 +316,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
         d.nm = true;
         d.kernel = mc.nm_ks ? "k_nm_mfma_ks" : (mc.nm4 ? "k_nm_mfma4" : "k_nm_mfma");
         d.nm4 = mc.nm4;
+        d.nm_nt = mc.nm_nt;
         d.KC = mc.nm_S;
         d.n_rows_aux = mc.nm_rows;
         d.n_units = m.u(THREAD_META, "first_nz_indices", sb).size() - 1;
@@ -383,6 +384,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
             d.ks_ctw = kt.CT;
             d.ks_ap = kt.AP;
             d.ks_p8 = kt.P8;
+            d.ks_nt = kt.NT;
             a.t0 = dev_copy(d, to_u32(mc.tbr, "BMTB first_row_indices"));
             a.tcol = kt.P8 ? (void *)dev_copy(d, kt.pos8) : (void *)dev_copy(d, kt.pos);
             a.tval = dev_copy(d, kt.val);

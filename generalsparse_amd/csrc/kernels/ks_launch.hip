@@ -94,6 +94,16 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
              "k_mfma_ks with 4 or 16 waves, 8-bit positions or the overlapped LDS layout: experiments build");
 #endif
     auto kern = gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, STAMPS>;
+    if (d.ks_nt) {  // KS_NT: A's groups (1) and B's rows (2) by non-temporal loads (N = 32, 8 waves, the apart layout)
+        if constexpr (CT == 2 && W == (int)kKsWaves && !STAMPS) {
+            GS_CHECK(d.ks_ap && !d.ks_p8, "k_mfma_ks: non-temporal loads are built for the apart layout, 16-bit positions");
+            kern = d.ks_nt == 1   ? gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, false, true, false, 1>
+                   : d.ks_nt == 2 ? gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, false, true, false, 2>
+                                  : gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, false, true, false, 3>;
+        } else {
+            throw gs_error("k_mfma_ks: non-temporal loads are built for N = 32, 8 waves");
+        }
+    }
 #ifdef GS_EXPERIMENTS
     if (d.ks_p8) {  // KS_POS8: 8-bit entry positions (N = 32, 8 waves, the apart layout)
         if constexpr (CT == 2 && W == (int)kKsWaves && !STAMPS) {
@@ -265,6 +275,12 @@ void launch_ks_group_k(const std::vector<ks_group_item> &it, uint32_t N, hipStre
 #else
     auto kern = gsk::k_mfma_ks_group<2, RT, W, (int)kKsDepth, MAXG, false, AP>;
 #endif
+    if constexpr (AP) {
+        const uint32_t nt = it[0].p->dev.ks_nt;
+        if (nt) kern = nt == 1   ? gsk::k_mfma_ks_group<2, RT, W, (int)kKsDepth, MAXG, false, true, 1>
+                       : nt == 2 ? gsk::k_mfma_ks_group<2, RT, W, (int)kKsDepth, MAXG, false, true, 2>
+                                 : gsk::k_mfma_ks_group<2, RT, W, (int)kKsDepth, MAXG, false, true, 3>;
+    }
     GS_CHECK(!it.empty() && it.size() <= (size_t)gsk::kKsGroupMax, "k_mfma_ks_group: 1..32 entries");
     gsk::ks_group_args args;
     std::memset(&args, 0, sizeof(args));
@@ -319,7 +335,7 @@ uint32_t ks_group_key(const plan_state &p, uint32_t N) {
     const device_plan &d = p.dev;
     const bool w8 = d.waves == kKsWaves && d.ks_ap, w4 = d.waves == 4 && !d.ks_ap;
     if (!p.uploaded || !d.mfma || !d.ks || d.pad_rows || N != 32 || d.lds_N != 32 || !(w8 || w4)) return 0;
-    return (w4 ? 1u << 17 : 0u) | (d.ks_p8 ? 1u << 16 : 0u) | (d.maxr << 8) | d.seg_cap;  // waves, P8, RT, MAXG
+    return (d.ks_nt << 18) | (w4 ? 1u << 17 : 0u) | (d.ks_p8 ? 1u << 16 : 0u) | (d.maxr << 8) | d.seg_cap;  // NT, waves, P8, RT, MAXG
 }
 
 void launch_ks_group(const std::vector<ks_group_item> &it, uint32_t N, hipStream_t s) {

@@ -152,9 +152,11 @@ void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, vo
     static const int dbg = getenv("GS_NM_DEBUG") ? atoi(getenv("GS_NM_DEBUG")) : 0;
     auto kern = dbg == 1 ? gsk::k_nm_mfma<CT, 1, NG>
                          : (dbg == 2 ? gsk::k_nm_mfma<CT, 2, NG> : (dbg == 4 ? gsk::k_nm_mfma<CT, 4, NG> : gsk::k_nm_mfma<CT, 0, NG>));
+    if (d.nm_nt && dbg == 0) kern = gsk::k_nm_mfma<CT, 0, NG, true>;
 #else
     constexpr int dbg = 0;
-    auto kern = gsk::k_nm_mfma<CT, 0, NG>;
+    // NM_NT (fixed at upload): A's panel blocks by non-temporal loads
+    auto kern = d.nm_nt ? gsk::k_nm_mfma<CT, 0, NG, true> : gsk::k_nm_mfma<CT, 0, NG>;
 #endif
     const size_t lds = (size_t)2 * gsk::kNmKC * 32 * CT + (dbg == 4 ? 4096 : 0);
     static std::mutex mu;

@@ -10,6 +10,9 @@
 #   c4perm2   com-Orkut: gather / scatter / hot-only permutations
 #   nm4b      k_nm_mfma4 (half-chunk B ring) against k_nm_mfma on C3
 #   exptimeout  the forced K-split timeout test on the experiments library
+#   nt        A's once-read loads non-temporal (make var VAR_FLAGS=-DGS_A_NT=1): parity, C2/C3/C1/c4o A/B
+#   nt2       the same on the north_star layer (c5h) with its per-shape search
+#   nt3       KS_NT masks on C2 + the north_star layer, NM_NT over the C3 dense-width sweep
 # Every GPU step runs under its own time limit; the first failure ends the session (set -e).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-r05x}; mkdir -p $OUT; export TMPDIR=/tmp
@@ -115,6 +118,27 @@ for ex in "$@"; do
       GS_LIBRARY=$VAR bench c4o_nt $c4o
       GS_LIBRARY=$VAR bench c2_nt2 $c2
       bench c2_base2 $c2 ;;
+    nt2)  # the layer and its shapes alone, default vs non-temporal A loads
+      VAR=$PWD/generalsparse_amd/libgeneralsparse_var.so
+      c5h="--workload c5h --steps 50 --warmup 5 --search-reps 5 --search-rounds 1 --no-cpu --no-rocsparse"
+      bench c5h_base $c5h
+      GS_LIBRARY=$VAR bench c5h_nt $c5h
+      for t in c5h_base c5h_nt; do python3 -c "
+import json
+d=[json.loads(l) for l in open('$OUT/b_$t.log') if l.startswith('{')][-1]
+print('$t', d['ms_per_step'], {k: (v['plan'], v['kernel_us'], {c: x['kernel_us'] for c, x in v['variants'].items()}) for k, v in d['per_shape'].items()})"; done ;;
+    nt3)  # KS_NT masks (bit 0 A's groups, bit 1 B's rows) on C2 40-row S=2 and the north_star layer; NM_NT at N = 8 / 32 / 128
+      pyt pytest_nt3.log tests/test_gpu_spmm.py tests/test_gpu_nm.py -k "nontemporal or driver_plan or headline"
+      c2="--workload c2 --steps 200 --warmup 50 --no-cpu --no-rocsparse --pipeline block_total --p0 40"
+      for x in 0 1 2 3 0 1 2 3; do bench c2_nt$x $c2 --config KS_NT=$x; done
+      c3="--workload c3 --steps 100 --warmup 20 --no-cpu --no-rocsparse --pipeline col_direction_nm --n-sweep 8,32,128"
+      for x in 0 1; do
+        bench c3_nmnt$x $c3 --config NM_NT=$x
+        python3 -c "
+import json
+d=[json.loads(l) for l in open('$OUT/b_c3_nmnt$x.log') if l.startswith('{')][-1]
+print('c3 NM_NT=$x sweep', [(r['N'], r.get('kernel_ms')) for r in d.get('n_sweep', [])])"
+      done ;;
     *) echo "unknown experiment $ex"; exit 2 ;;
   esac
 done

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Matrix-core utilisation of a kernel from one rocprofv3 --pmc pass (SURVEY
 §8d): usage mfma_util.py <pmc dir> <kernel substring> <out.json> <workload>
-[mfma instructions per dispatch] [cycles per mfma].
+[mfma instructions per dispatch] [cycles per mfma] [plan label].
 
 Counters (scripts/gpu_session.sh part `sq`): SQ_VALU_MFMA_BUSY_CYCLES (matrix-pipe busy cycles,
 summed over every SIMD of the chip), GRBM_GUI_ACTIVE (GPU-busy cycles, summed over the 8 XCDs,
@@ -30,6 +30,7 @@ def main():
     d, kern, dst, wl = sys.argv[1:5]
     n_mfma = float(sys.argv[5]) if len(sys.argv) > 5 else None
     cyc = float(sys.argv[6]) if len(sys.argv) > 6 else None
+    plan = sys.argv[7] if len(sys.argv) > 7 else None
     per = defaultdict(lambda: defaultdict(float))
     dur = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
@@ -43,7 +44,7 @@ def main():
     keys = list(per)
     med = {c: statistics.median(per[k][c] for k in keys) for c in per[keys[0]]}
     active = med["GRBM_GUI_ACTIVE"] / XCDS
-    out = {"workload": wl, "kernel": kern, "dispatches": len(keys), "counters_median": med,
+    out = {"workload": wl, "kernel": kern, "plan": plan, "dispatches": len(keys), "counters_median": med,
            "kernel_ns_median": statistics.median(dur.values()),
            "clock_ghz_est": round(active / statistics.median(dur.values()), 3),
            "mfma_util": round(med["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * statistics.median(dur.values()) * 2.4), 4),

@@ -1,7 +1,7 @@
 """HBM bytes per launch of one kernel from the FETCH_SIZE / WRITE_SIZE passes
 (MI355X_MICROARCH.md: FETCH_SIZE reports half the bytes of wide streaming
 reads on gfx950 -> x2; both counters are in KiB).  Writes profiles/<out>.json.
-usage: traffic_summary.py <pmc dir> <kernel substring> <out json> [algorithmic bytes]"""
+usage: traffic_summary.py <pmc dir> <kernel substring> <out json> [algorithmic bytes] [plan label]"""
 import csv
 import glob
 import json
@@ -9,7 +9,8 @@ import os
 import sys
 
 root, filt, out = sys.argv[1], sys.argv[2], sys.argv[3]
-alg = int(sys.argv[4]) if len(sys.argv) > 4 else None
+alg = int(sys.argv[4]) if len(sys.argv) > 4 and sys.argv[4] else None
+plan = sys.argv[5] if len(sys.argv) > 5 else None
 vals = {}
 for name in ("FETCH_SIZE", "WRITE_SIZE"):
     per = {}
@@ -21,7 +22,7 @@ for name in ("FETCH_SIZE", "WRITE_SIZE"):
     vals[name + "_dispatches"] = len(per)
 fetch_b = vals["FETCH_SIZE"] * 1024 * 2
 write_b = vals["WRITE_SIZE"] * 1024
-res = {"kernel": filt, "fetch_size_kib_raw": round(vals["FETCH_SIZE"], 1), "write_size_kib": round(vals["WRITE_SIZE"], 1),
+res = {"kernel": filt, "plan": plan, "fetch_size_kib_raw": round(vals["FETCH_SIZE"], 1), "write_size_kib": round(vals["WRITE_SIZE"], 1),
        "dispatches": vals["FETCH_SIZE_dispatches"], "hbm_read_bytes_per_launch": int(fetch_b),
        "hbm_write_bytes_per_launch": int(write_b), "hbm_bytes_per_launch": int(fetch_b + write_b),
        "correction": "FETCH_SIZE x2 (gfx950 streaming-read undercount), KiB -> bytes"}

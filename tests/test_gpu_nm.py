@@ -224,3 +224,27 @@ def test_nm4_matches_oracle(shape, N, split):
     finally:
         for k, val in old.items():
             gsa.set_config(k, val)
+
+
+@pytest.mark.parametrize("N", [8, 32, 128])
+@pytest.mark.parametrize("shape", [(333, 772), (1792, 768), (1, 4096)], ids=lambda s: f"{s[0]}x{s[1]}")
+def test_nm_nontemporal_loads_bit_identical(shape, N):
+    """NM_NT (default 1: A's panel blocks by non-temporal loads) changes the cache policy of
+    the loads only: the result equals the NM_NT=0 kernel's bit for bit, and the oracle's"""
+    M, K = shape
+    r, c, v = ds.two_four(M, K, 70 + M)
+    B = np.random.default_rng(M * N).uniform(-1, 1, (K, N)).astype(np.float16)
+    out = {}
+    old = gsa.get_config("NM_NT")
+    try:
+        for nt in (0, 1):
+            gsa.set_config("NM_NT", nt)
+            plan = plan_for(M, K, r, c, v, N)
+            assert plan.info()["device_kernel"] == "k_nm_mfma", plan.info()
+            out[nt] = spmm(plan, B)
+            plan.free()
+    finally:
+        gsa.set_config("NM_NT", old)
+    assert np.array_equal(out[0], out[1])
+    ref = ofi.spmm_ref(M, N, r, c, v.astype(np.float16).astype(np.float32), B.astype(np.float32), "f64")
+    check(out[1], ref)

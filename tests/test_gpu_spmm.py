@@ -482,6 +482,48 @@ def test_mfma_ks_pos8_layout_is_exact(rows, split, mfma_everywhere):
         gsa.set_config("KS_SPLIT", 0)
 
 
+@pytest.mark.parametrize("split", [0, 1, 3])
+@pytest.mark.parametrize("rows", [40, 80, 112])
+def test_mfma_ks_nontemporal_loads_bit_identical(rows, split, mfma_everywhere):
+    """KS_NT (a plan-search variant of the default build): A's groups and / or B's rows by
+    non-temporal loads -- the same kernel arithmetic, so C is the KS_NT=0 kernel's bit for bit (and the oracle's),
+    single and grouped launches alike; a group does not mix the two forms"""
+    N = 32
+    cases = [ds.pruned_weight(640, 2048, 0.7, 9), ds.random_rows(640, 2048, 400.0, seed=4, empty_frac=0.2)]
+    gsa.set_config("KS_SPLIT", split)
+    try:
+        for r, c, v in cases:
+            B = torch.from_numpy(np.random.default_rng(6).uniform(-1, 1, (2048, N)).astype(np.float16)).to(DEV)
+            outs, plans = [], []
+            for nt in (0, 1, 3, 2):  # bit 0: A's groups, bit 1: B's rows
+                gsa.set_config("KS_NT", nt)
+                plan = gsa.Plan.from_coo(640, 2048, r, c, v).run_pipeline("block_total", N, rows, 1).compile().upload("f16", 0)
+                assert plan.info()["device_kernel"] == "k_mfma_ks", plan.info()
+                outs.append(plan.spmm(B).float().cpu().numpy())
+                plans.append(plan)
+            gsa.set_config("KS_NT", 0)
+            for o in outs[1:]:
+                np.testing.assert_array_equal(outs[0], o)
+            check(outs[1], ofi.spmm_ref(640, N, r, c, v.astype(np.float16).astype(np.float32),
+                                        B.cpu().numpy().astype(np.float32), "f64"), "f16")
+            plans[1].add_replica()
+            Cs = [torch.full((640, N), float("nan"), device=DEV, dtype=torch.float16) for _ in range(3)]
+            bat = gsa.Batch([(plans[1], 0, B, Cs[0]), (plans[1], 1, B, Cs[1])], N)
+            assert bat.launches() == [2]
+            bat.run(torch.cuda.current_stream().cuda_stream)
+            mixed = gsa.Batch([(plans[0], 0, B, Cs[2]), (plans[1], 0, B, Cs[0])], N)
+            assert sorted(mixed.launches()) == [1, 1]
+            mixed.run(torch.cuda.current_stream().cuda_stream)
+            for cc in Cs:
+                np.testing.assert_array_equal(cc.float().cpu().numpy(), outs[0])
+            for p in plans:
+                p.device_status()
+                p.free()
+    finally:
+        gsa.set_config("KS_NT", 0)
+        gsa.set_config("KS_SPLIT", 0)
+
+
 @pytest.mark.parametrize("p8", [0, 1])
 @pytest.mark.parametrize("rows,split", [(40, 2), (80, 4), (112, 1), (112, 4), (128, 3)])
 def test_mfma_ks_four_waves(rows, split, p8, mfma_everywhere):

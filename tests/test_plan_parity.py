@@ -345,3 +345,27 @@ def test_binary_plan_file_round_trip(tmp_path, name, N, p0, p1):
     bad.write_bytes(b"not a plan")
     with pytest.raises(gsa.GsError):
         gsa.Plan.load(bad)
+
+
+@pytest.mark.parametrize("nt", [0, 1])
+def test_generate_program_carries_nontemporal_variants(tmp_path, nt):
+    """KS_NT / NM_NT reach the emitted program: it launches the same k_mfma_ks / k_nm_mfma
+    instantiation gs_spmm does (the 9th / 4th template argument)"""
+    old = {k: gsa.get_config(k) for k in ("HALF", "KS_NT", "NM_NT")}
+    try:
+        gsa.set_config("HALF", 1)
+        gsa.set_config("KS_NT", nt)
+        gsa.set_config("NM_NT", nt)
+        (tmp_path / "ks").mkdir()
+        (tmp_path / "nm").mkdir()
+        r, c, v = ds.pruned_weight(320, 1024, 0.7, 41)
+        p = gsa.Plan.from_coo(320, 1024, r, c, v).run_pipeline("block_total", 32, 40, 1).compile()
+        src = open(os.path.join(p.generate_program(tmp_path / "ks", repeat=10), "kernel_file.hip")).read()
+        assert re.search(r"gsk::k_mfma_ks<2, 3, 8, \d, \d, false, true, false%s>" % (", 1" if nt else ""), src), src[:2000]
+        r, c, v = ds.two_four(256, 512, 41)
+        p = gsa.Plan.from_coo(256, 512, r, c, v).run_pipeline("col_direction_nm", 32, 32, 1).compile()
+        src = open(os.path.join(p.generate_program(tmp_path / "nm", repeat=10), "kernel_file.hip")).read()
+        assert ("gsk::k_nm_mfma<2, 0, 32%s>" % (", true" if nt else "")) in src, src[:2000]
+    finally:
+        for k, val in old.items():
+            gsa.set_config(k, val)
