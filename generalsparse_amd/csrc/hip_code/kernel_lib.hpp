@@ -1568,7 +1568,7 @@ __global__ __launch_bounds__(64 * kMfmaWaves) void k_mfma_rows(
 // each 8 x [u16 halfword position in the wave's dense image] + 8 x [f16 value], found by
 // the step's {first group, group count} record, loaded D steps ahead of the groups;
 // padding inside a group writes 0 into the image's zero row; NT: the groups by non-temporal
-// loads when NTL & 1, B's rows when NTL & 2: KS_NT), stores the B rows into its private stage (32-B pieces
+// loads when NTL & 1 (KS_NT; B's rows when NTL & 2, not instantiated: slower), stores the B rows into its private stage (32-B pieces
 // permuted by b_piece so the ds_read_b64_tr_b16 fragment reads are conflict-free),
 // scatters the entries into its private image of 16*RT+1 rows x 96 B (conflict-free
 // ds_read_b128), reads the RT A fragments and the CT B fragments, writes zeros back at

@@ -55,7 +55,7 @@ struct ks_tiles {
     uint32_t CT = 0;  // 16-column MFMA tiles per workgroup (ks_ct_rt)
     bool AP = true;   // partial tiles beside the stages (ks_red_apart; KS_APART)
     bool P8 = false;  // 8-bit positions (KS_POS8): pos8 instead of pos, see build_ks_tiles
-    uint32_t NT = 0;  // non-temporal loads, bit 0 A's groups, bit 1 B's rows (KS_NT; N = 32, 8 waves, apart layout)
+    uint32_t NT = 0;  // k_mfma_ks NTL: 1 = A's groups by non-temporal loads (KS_NT; N = 32, 8 waves, apart layout)
     size_t lds_bytes = 0;
     std::vector<uint16_t> pos, val;  // 8 u16 per group each
     std::vector<uint8_t> pos8;       // P8: 8 bytes per group

@@ -116,9 +116,11 @@ struct config_t {
                                  // keeps the workgroups per CU (-1)
     int64_t KS_FORCE_TIMEOUT = 0;  // experiments build: the K-split combine takes its timeout path (test of the error word)
     int64_t KS_PRIO = 1;         // k_mfma_ks: the younger waves at s_setprio 1 (1: whole loop, 2: first half, 0: off)
-    int64_t KS_NT = 0;           // k_mfma_ks at N = 32: non-temporal loads (L1 bypassed), bit 0 A's groups, bit 1 B's
-                                 // rows; a plan-search variant (A only: C2 -4%, the headline layer +1.5%, r05l / r05m)
-    int64_t NM_NT = 1;           // k_nm_mfma: A's panel blocks by non-temporal loads (C3 N = 128: 72.0 -> 66.9 us)
+    int64_t KS_NT = 0;           // k_mfma_ks at N = 32: A's groups by non-temporal loads; a plan-search variant (C2
+                                 // 13.8 -> 12.9 us, the headline layer 165.7 -> 167.8 us; B's rows as well: 14.1 us,
+                                 // profiles/r05n_nt3.txt)
+    int64_t NM_NT = 1;           // k_nm_mfma: A's panel blocks by non-temporal loads (C3 at N = 8 / 32 / 128: -10 / -6 /
+                                 // -6.5%, profiles/r05n_nt3.txt)
 };
 // Process-wide config: loaded once from $GS_CONFIG or ./global_config.json if
 // present (flat JSON object of scalars), defaults otherwise.

@@ -94,12 +94,11 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
              "k_mfma_ks with 4 or 16 waves, 8-bit positions or the overlapped LDS layout: experiments build");
 #endif
     auto kern = gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, STAMPS>;
-    if (d.ks_nt) {  // KS_NT: A's groups (1) and B's rows (2) by non-temporal loads (N = 32, 8 waves, the apart layout)
+    if (d.ks_nt) {  // KS_NT: A's groups by non-temporal loads (N = 32, 8 waves, the apart layout)
         if constexpr (CT == 2 && W == (int)kKsWaves && !STAMPS) {
             GS_CHECK(d.ks_ap && !d.ks_p8, "k_mfma_ks: non-temporal loads are built for the apart layout, 16-bit positions");
-            kern = d.ks_nt == 1   ? gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, false, true, false, 1>
-                   : d.ks_nt == 2 ? gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, false, true, false, 2>
-                                  : gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, false, true, false, 3>;
+            GS_CHECK(d.ks_nt == 1, "k_mfma_ks: KS_NT is built for A's groups (1)");
+            kern = gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, false, true, false, 1>;
         } else {
             throw gs_error("k_mfma_ks: non-temporal loads are built for N = 32, 8 waves");
         }
@@ -276,10 +275,7 @@ void launch_ks_group_k(const std::vector<ks_group_item> &it, uint32_t N, hipStre
     auto kern = gsk::k_mfma_ks_group<2, RT, W, (int)kKsDepth, MAXG, false, AP>;
 #endif
     if constexpr (AP) {
-        const uint32_t nt = it[0].p->dev.ks_nt;
-        if (nt) kern = nt == 1   ? gsk::k_mfma_ks_group<2, RT, W, (int)kKsDepth, MAXG, false, true, 1>
-                       : nt == 2 ? gsk::k_mfma_ks_group<2, RT, W, (int)kKsDepth, MAXG, false, true, 2>
-                                 : gsk::k_mfma_ks_group<2, RT, W, (int)kKsDepth, MAXG, false, true, 3>;
+        if (it[0].p->dev.ks_nt) kern = gsk::k_mfma_ks_group<2, RT, W, (int)kKsDepth, MAXG, false, true, 1>;
     }
     GS_CHECK(!it.empty() && it.size() <= (size_t)gsk::kKsGroupMax, "k_mfma_ks_group: 1..32 entries");
     gsk::ks_group_args args;

@@ -31,8 +31,10 @@ for wl in $WLS; do
     tail -1 $OUT/bench_$wl.log | cut -c1-300
   fi
   if has prof; then
-    timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$wl -o p -- \
+    # GS_BENCH_MARK=1: spin-kernel markers around the timed region, so timed_stats.py keeps only its dispatches
+    GS_BENCH_MARK=1 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$wl -o p -- \
       python3 bench.py --workload $wl --steps $psteps --warmup 10 --no-cpu --no-rocsparse ${BENCH_ARGS:-} > $OUT/prof_$wl.log 2>&1
+    python3 scripts/timed_stats.py $OUT/prof_$wl $OUT/prof_${wl}_timed_stats.csv > /dev/null || echo "timed_stats $wl: no marked region"
     echo "prof $wl done"
   fi
 done
