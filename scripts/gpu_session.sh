@@ -41,9 +41,10 @@ done
 for wl in ${PMC_WLS:-}; do
   cmd=$(pmc_cmd $wl)
   if has pmc; then
+    mkdir -p $OUT/pmc_$wl
     for c in FETCH_SIZE WRITE_SIZE; do
       timeout -s KILL 600 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $OUT/pmc_$wl/$c -o p -- $cmd \
-        > $OUT/pmc_$wl/$c.log 2>&1 || { mkdir -p $OUT/pmc_$wl; echo "pmc $wl $c failed"; exit 1; }
+        > $OUT/pmc_$wl/$c.log 2>&1 || { echo "pmc $wl $c failed"; exit 1; }
     done
     echo "pmc $wl done"
   fi

@@ -18,6 +18,7 @@ import csv
 import glob
 import json
 import os
+import re
 import statistics
 import sys
 from collections import defaultdict
@@ -44,7 +45,8 @@ def main():
     keys = list(per)
     med = {c: statistics.median(per[k][c] for k in keys) for c in per[keys[0]]}
     active = med["GRBM_GUI_ACTIVE"] / XCDS
-    out = {"workload": wl, "kernel": kern, "plan": plan, "dispatches": len(keys), "counters_median": med,
+    label = re.match(r"k_[a-z0-9_]+", kern).group(0) if re.match(r"k_[a-z0-9_]+", kern) else kern
+    out = {"workload": wl, "kernel": label, "filter": kern, "plan": plan, "dispatches": len(keys), "counters_median": med,
            "kernel_ns_median": statistics.median(dur.values()),
            "clock_ghz_est": round(active / statistics.median(dur.values()), 3),
            "mfma_util": round(med["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * statistics.median(dur.values()) * 2.4), 4),

@@ -3,6 +3,7 @@
 reads on gfx950 -> x2; both counters are in KiB).  Writes profiles/<out>.json.
 usage: traffic_summary.py <pmc dir> <kernel substring> <out json> [algorithmic bytes] [plan label]"""
 import csv
+import re
 import glob
 import json
 import os
@@ -22,7 +23,9 @@ for name in ("FETCH_SIZE", "WRITE_SIZE"):
     vals[name + "_dispatches"] = len(per)
 fetch_b = vals["FETCH_SIZE"] * 1024 * 2
 write_b = vals["WRITE_SIZE"] * 1024
-res = {"kernel": filt, "plan": plan, "fetch_size_kib_raw": round(vals["FETCH_SIZE"], 1), "write_size_kib": round(vals["WRITE_SIZE"], 1),
+# the kernel family (the bench matches on it): the filter may be a mangled instantiation
+label = re.match(r"k_[a-z0-9_]+", filt).group(0) if re.match(r"k_[a-z0-9_]+", filt) else filt
+res = {"kernel": label, "filter": filt, "plan": plan, "fetch_size_kib_raw": round(vals["FETCH_SIZE"], 1), "write_size_kib": round(vals["WRITE_SIZE"], 1),
        "dispatches": vals["FETCH_SIZE_dispatches"], "hbm_read_bytes_per_launch": int(fetch_b),
        "hbm_write_bytes_per_launch": int(write_b), "hbm_bytes_per_launch": int(fetch_b + write_b),
        "correction": "FETCH_SIZE x2 (gfx950 streaming-read undercount), KiB -> bytes"}
