@@ -1714,9 +1714,9 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
                 reinterpret_cast<const u32x4 *>(B + (size_t)(k < K ? k : K - 1u) * N + col0 + (cu < nv ? cu : 0u)));
         }
     };
-    auto load_g = [&](uint32_t i, u32x2 &NX_, uint32_t &CN_, PV (&P_)[MAXG], u32x4 (&V_)[MAXG]) {
-        const uint32_t b0 = __builtin_amdgcn_readfirstlane(NX_[0]);
-        const uint32_t gc = __builtin_amdgcn_readfirstlane(NX_[1]);
+    // the groups of step i (b0: first group, gc: count), then the record of step i + D
+    auto load_g_at = [&](uint32_t i, uint32_t b0, uint32_t gc, u32x2 &NX_, uint32_t &CN_, PV (&P_)[MAXG],
+                         u32x4 (&V_)[MAXG]) {
         CN_ = gc;
         NX_ = rec_of(i + D);
 #pragma unroll
@@ -1727,13 +1727,31 @@ __device__ __forceinline__ void ks_body(const uint32_t *__restrict__ bmtb_first_
             V_[j] = ld_once_if<(NTL & 1) != 0>(tV + at);
         }
     };
+    auto load_g = [&](uint32_t i, u32x2 &NX_, uint32_t &CN_, PV (&P_)[MAXG], u32x4 (&V_)[MAXG]) {
+        load_g_at(i, __builtin_amdgcn_readfirstlane(NX_[0]), __builtin_amdgcn_readfirstlane(NX_[1]), NX_, CN_, P_, V_);
+    };
+    // head steps (device_layout.cc ks_tiles::GH, prio bits 8..17): the first D steps of every wave
+    // sit at (unit * min(W * D, NS) + step) * GH, padded with zero-row groups, so the prologue issues their
+    // groups with the B rows at once instead of a record round trip later
+    const uint32_t GH = (prio >> 8) & 0x3ffu;
+    if (GH) {
 #pragma unroll
-    for (int d = 0; d < D; d++) NX[d] = rec_of((uint32_t)d);
+        for (int d = 0; d < D; d++) load_b((uint32_t)d, BR[d]);
 #pragma unroll
-    for (int d = 0; d < D; d++) load_b((uint32_t)d, BR[d]);
-    for (uint32_t x = lane; x < IMG / 16u; x += 64u) *reinterpret_cast<u32x4 *>(img + x * 16u) = zero4;
+        for (int d = 0; d < D; d++) {
+            const uint32_t st = (uint32_t)d < nsw ? wv + (uint32_t)d * W : 0u;
+            load_g_at((uint32_t)d, (u * min((uint32_t)(W * D), NS) + st) * GH, GH, NX[d], CN[d], P[d], V[d]);
+        }
+        for (uint32_t x = lane; x < IMG / 16u; x += 64u) *reinterpret_cast<u32x4 *>(img + x * 16u) = zero4;
+    } else {
 #pragma unroll
-    for (int d = 0; d < D; d++) load_g((uint32_t)d, NX[d], CN[d], P[d], V[d]);
+        for (int d = 0; d < D; d++) NX[d] = rec_of((uint32_t)d);
+#pragma unroll
+        for (int d = 0; d < D; d++) load_b((uint32_t)d, BR[d]);
+        for (uint32_t x = lane; x < IMG / 16u; x += 64u) *reinterpret_cast<u32x4 *>(img + x * 16u) = zero4;
+#pragma unroll
+        for (int d = 0; d < D; d++) load_g((uint32_t)d, NX[d], CN[d], P[d], V[d]);
+    }
     GS_KS_STAMP(1u);
 
     f4v acc[RT][CT];
@@ -2019,7 +2037,7 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks_group(ks_group_args args) {
     const ks_entry &e = args.e[sel];  // kernel arguments: scalar loads at a computed offset
     if (bx - args.begin[sel] >= e.nwg) return;  // padding up to the next entry's multiple of 8
     ks_body<CT, RT, W, D, MAXG, false, AP, P8, NTL>(e.tbr, e.tP, e.tV, e.steps, e.B, e.C, e.K, args.N, e.S, e.NS, e.nwg, e.row_base,
-                                       e.slabs, e.arrivals, nullptr, bx - args.begin[sel], args.pad[0]);
+                                       e.slabs, e.arrivals, nullptr, bx - args.begin[sel], args.pad[0] | (e.pad0 << 8));
 }
 
 // ---------------------------------------------------------------------------

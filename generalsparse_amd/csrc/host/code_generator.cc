@@ -272,7 +272,7 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
                  std::to_string(64 * t.W) + ", " + std::to_string(t.lds_bytes) +
                  ">>>(d_tbr, (const gsk::u32x4 *)d_pos, (const gsk::u32x4 *)d_val, (const gsk::u32x2 *)d_steps, d_B, d_C, "
                  "(uint32_t)K, N, " + std::to_string(t.S) + "u, " + std::to_string(t.NS) + "u, " + std::to_string(nwg) + "u, 0u, d_ws, d_arr, nullptr, " +
-                 std::to_string(get_config().KS_PRIO) + "u)";
+                 std::to_string((uint32_t)get_config().KS_PRIO | (t.GH << 8)) + "u)";
     } else if (L.kind == mc_layout::BM) {
         const bm_tiles &t = L.bm;
         const uint64_t nb = L.tbr.size() - 1, nwg = nb * t.S;

@@ -367,6 +367,27 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
             }
         }
     }
+    // head steps (ks_tiles::GH): used when padding them to the largest costs at most 6% more groups
+    const uint32_t HS = std::min<uint32_t>(W * kKsDepth, t.NS);  // head slots per unit
+    if (!t.P8 && get_config().KS_HEAD) {
+        uint64_t gh = 1, head_groups = 0, all_groups = 0;
+        std::vector<uint32_t> c2((size_t)S * t.NS);
+        for (uint64_t g = 0; g < nb; g++) {
+            std::fill(c2.begin(), c2.end(), 0u);
+            for (uint64_t r = tb_rows[g]; r < tb_rows[g + 1]; r++)
+                for (uint64_t e = row_ptr[r]; e < row_ptr[r + 1]; e++) c2[col[e] / 32]++;
+            for (size_t st = 0; st < c2.size(); st++) {
+                const uint64_t ng = (c2[st] + 7) / 8;
+                all_groups += ng;
+                if (st % t.NS < HS) {
+                    head_groups += ng;
+                    gh = std::max(gh, ng);
+                }
+            }
+        }
+        const uint64_t padded = (uint64_t)nb * S * HS * gh;
+        if ((double)(padded - head_groups) <= 0.06 * (double)all_groups && (double)padded < 2.0e9) t.GH = (uint32_t)gh;
+    }
     t.GCAP = (uint32_t)gmax;
     t.MAXG = gmax <= 64 ? 1 : (gmax <= 128 ? 2 : (gmax <= 192 ? 3 : (gmax <= 256 ? 4 : 0)));
     if (!t.MAXG) { why = "a k-step holds more than 256 entry groups"; return false; }
@@ -389,8 +410,12 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
         t.pos.reserve(row_ptr[tb_rows[nb]] - row_ptr[tb_rows[0]] + (size_t)nb * S * t.NS * 8 + 8);
     t.val.reserve(t.P8 ? t.pos8.capacity() : t.pos.capacity());
     t.steps.reserve((size_t)nb * S * t.NS * 2);
+    if (t.GH) {  // the head region first: every slot a zero-row group until its step fills it
+        t.pos.assign((size_t)nb * S * HS * t.GH * 8, (uint16_t)pad_h);
+        t.val.assign(t.pos.size(), 0);
+    }
     std::vector<uint64_t> cur;
-    std::vector<uint16_t> pos, hv, prow, pcol;
+    std::vector<uint16_t> pos, hv, prow, pcol, hpos, hval;
     for (uint64_t g = 0; g < nb; g++) {
         const uint64_t r0 = tb_rows[g], R = tb_rows[g + 1] - r0;
         cur.assign(R, 0);
@@ -413,7 +438,16 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
                     cur[i] = e;
                 }
                 size_t before, ng;
-                if (t.P8) {
+                if (t.GH && s < HS) {  // a head step: its fixed slot
+                    hpos.clear();
+                    hval.clear();
+                    bank_order_segment(pos, hv, pad_h, hpos, hval, RS / 2);
+                    ng = hpos.size() / 8;
+                    GS_CHECK(ng <= t.GH, "k_mfma_ks head step exceeds its slot");
+                    before = (((size_t)g * S + q) * HS + s) * t.GH * 8;
+                    std::copy(hpos.begin(), hpos.end(), t.pos.begin() + before);
+                    std::copy(hval.begin(), hval.end(), t.val.begin() + before);
+                } else if (t.P8) {
                     before = t.pos8.size();
                     ng = pos8_step(prow, pcol, hv, RS, t.pos8, t.val);
                 } else {

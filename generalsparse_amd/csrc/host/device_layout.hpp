@@ -56,6 +56,12 @@ struct ks_tiles {
     bool AP = true;   // partial tiles beside the stages (ks_red_apart; KS_APART)
     bool P8 = false;  // 8-bit positions (KS_POS8): pos8 instead of pos, see build_ks_tiles
     uint32_t NT = 0;  // k_mfma_ks NTL: 1 = A's groups by non-temporal loads (KS_NT; N = 32, 8 waves, apart layout)
+    // head steps (KS_HEAD): the first W x kKsDepth k-steps of every unit -- the ones each wave loads
+    // in its prologue -- have their groups at a fixed place, (unit * HS + step) * GH with HS =
+    // min(W * kKsDepth, NS), padded with
+    // zero-row groups to GH groups, so the prologue's group loads need no record round trip; their
+    // records still describe them (first group, count), so a kernel may also take them by record
+    uint32_t GH = 0;  // groups per head step (0: no head region)
     size_t lds_bytes = 0;
     std::vector<uint16_t> pos, val;  // 8 u16 per group each
     std::vector<uint8_t> pos8;       // P8: 8 bytes per group

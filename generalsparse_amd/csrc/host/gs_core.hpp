@@ -119,6 +119,8 @@ struct config_t {
     int64_t KS_NT = 0;           // k_mfma_ks at N = 32: A's groups by non-temporal loads; a plan-search variant (C2
                                  // 13.8 -> 12.9 us, the headline layer 165.7 -> 167.8 us; B's rows as well: 14.1 us,
                                  // profiles/r05n_nt3.txt)
+    int64_t KS_HEAD = 1;         // k_mfma_ks: the head steps (each wave's first kKsDepth k-steps) at fixed, padded
+                                 // places, loaded without their records (when the padding costs <= 6% more groups)
     int64_t NM_NT = 1;           // k_nm_mfma: A's panel blocks by non-temporal loads (C3 at N = 8 / 32 / 128: -10 / -6 /
                                  // -6.5%, profiles/r05n_nt3.txt)
 };

@@ -43,6 +43,7 @@ struct device_plan {
     uint32_t ks_ctw = 0;      // k_mfma_ks: 16-column tiles per workgroup (ks_tiles::CT)
     bool ks_ap = true;        // k_mfma_ks: partial tiles beside the stages (ks_tiles::AP)
     bool ks_p8 = false;       // k_mfma_ks: 8-bit entry positions (ks_tiles::P8, KS_POS8)
+    uint32_t ks_gh = 0;       // k_mfma_ks: groups per head step (ks_tiles::GH; 0: every step by record)
     uint32_t ks_nt = 0;       // k_mfma_ks: non-temporal loads of A's groups (NTL bit 0; ks_tiles::NT, KS_NT)
     bool nm_nt = false;       // k_nm_mfma: non-temporal panel loads (NM_NT)
     uint64_t err_at = 0;      // K-split combine: index of the device error word in t2 (0: none)

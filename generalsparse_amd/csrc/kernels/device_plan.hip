@@ -385,6 +385,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
             d.ks_ap = kt.AP;
             d.ks_p8 = kt.P8;
             d.ks_nt = kt.NT;
+            d.ks_gh = kt.GH;
             a.t0 = dev_copy(d, to_u32(mc.tbr, "BMTB first_row_indices"));
             a.tcol = kt.P8 ? (void *)dev_copy(d, kt.pos8) : (void *)dev_copy(d, kt.pos);
             a.tval = dev_copy(d, kt.val);

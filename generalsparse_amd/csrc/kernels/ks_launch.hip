@@ -81,7 +81,7 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
                 hipLaunchKernelGGL(k4, dim3((uint32_t)d.n_rows_aux * d.ksplit, ks_col_tiles_ct(N, CT)), dim3(256), d.lds_bytes,
                                    s, a.t0, (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, (const gsk::u32x2 *)a.t1, B,
                                    C, (uint32_t)p.K, N, d.ksplit, d.ks_ns, (uint32_t)d.n_rows_aux * d.ksplit,
-                                   (uint32_t)d.row_base, a.ws, a.t2, stamps, ks_prio_arg());
+                                   (uint32_t)d.row_base, a.ws, a.t2, stamps, ks_prio_arg() | (d.ks_gh << 8));
                 HIP_OK(hipGetLastError());
                 return;
             } else {
@@ -125,7 +125,7 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
     hipLaunchKernelGGL(kern, dim3((uint32_t)d.n_rows_aux * d.ksplit, ks_col_tiles_ct(N, CT)), dim3(64 * W), d.lds_bytes, s, a.t0,
                        (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, (const gsk::u32x2 *)a.t1, B, C,
                        (uint32_t)p.K, N, d.ksplit, d.ks_ns, (uint32_t)d.n_rows_aux * d.ksplit, (uint32_t)d.row_base, a.ws, a.t2, stamps,
-                       ks_prio_arg());
+                       ks_prio_arg() | (d.ks_gh << 8));
     HIP_OK(hipGetLastError());
 }
 
@@ -302,6 +302,7 @@ void launch_ks_group_k(const std::vector<ks_group_item> &it, uint32_t N, hipStre
         e.NS = d.ks_ns;
         e.nwg = (uint32_t)d.n_rows_aux * d.ksplit;
         e.row_base = (uint32_t)d.row_base;
+        e.pad0 = d.ks_gh;  // the entry's head-step group count (ks_body's prio bits 8..17)
         args.begin[i] = wg;
         // each entry starts on a multiple of 8 workgroups (idle ones in between exit at once), so
         // its entry-relative block numbers share XCDs as the global ones do (xcd_block)

@@ -13,6 +13,8 @@
 #   nt        A's once-read loads non-temporal (make var VAR_FLAGS=-DGS_A_NT=1): parity, C2/C3/C1/c4o A/B
 #   nt2       the same on the north_star layer (c5h) with its per-shape search
 #   nt3       KS_NT masks on C2 + the north_star layer, NM_NT over the C3 dense-width sweep
+#   nmphase   k_nm_mfma phase stamps + no-B / no-A loop timings on C3 (experiments build)
+#   head      KS_HEAD A/B on C2 (KS_NT=1) and the north_star layer
 # Every GPU step runs under its own time limit; the first failure ends the session (set -e).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-r05x}; mkdir -p $OUT; export TMPDIR=/tmp
@@ -139,6 +141,15 @@ import json
 d=[json.loads(l) for l in open('$OUT/b_c3_nmnt$x.log') if l.startswith('{')][-1]
 print('c3 NM_NT=$x sweep', [(r['N'], r.get('kernel_ms')) for r in d.get('n_sweep', [])])"
       done ;;
+    nmphase)  # k_nm_mfma phase stamps and the loop without B / A loads (experiments build)
+      EXP=$PWD/generalsparse_amd/libgeneralsparse_exp.so
+      for dbg in 0 1 2; do GS_LIBRARY=$EXP GS_NM_DEBUG=$dbg timeout -k 10 300 python3 -u scripts/nm_phases.py 128 50; done
+      GS_LIBRARY=$EXP GS_NM_DEBUG=4 timeout -k 10 300 python3 -u scripts/nm_phases.py 128 > $OUT/nm_stamps.txt 2>&1
+      grep "wave" $OUT/nm_stamps.txt | head -30 ;;
+    head)  # KS_HEAD (head steps at fixed slots) on C2 40-row (with KS_NT=1) + the north_star layer
+      pyt pytest_head.log tests/test_gpu_spmm.py -k "head_steps or nontemporal or driver_plan or headline or mfma_ks_matches"
+      c2="--workload c2 --steps 200 --warmup 50 --no-cpu --no-rocsparse --pipeline block_total --p0 40 --config KS_NT=1"
+      for x in 0 1 0 1; do bench c2_head$x $c2 --config KS_HEAD=$x; done ;;
     *) echo "unknown experiment $ex"; exit 2 ;;
   esac
 done

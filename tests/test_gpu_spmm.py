@@ -524,6 +524,46 @@ def test_mfma_ks_nontemporal_loads_bit_identical(rows, split, mfma_everywhere):
         gsa.set_config("KS_SPLIT", 0)
 
 
+@pytest.mark.parametrize("nt", [0, 1])
+@pytest.mark.parametrize("rows,split", [(40, 0), (40, 2), (80, 4), (112, 1), (112, 4), (128, 3)])
+def test_mfma_ks_head_steps_bit_identical(rows, split, nt, mfma_everywhere):
+    """KS_HEAD (default 1): each wave's first k-steps at fixed, padded slots, loaded without their
+    records -- the padding groups write zeros into the image's zero row, so C is the record-only
+    layout's bit for bit (single and grouped launches, with and without KS_NT), and the oracle's"""
+    N = 32
+    cases = [ds.pruned_weight(640, 2048, 0.7, 10), ds.random_rows(640, 2048, 400.0, seed=5, empty_frac=0.2)]
+    gsa.set_config("KS_SPLIT", split)
+    gsa.set_config("KS_NT", nt)
+    try:
+        for r, c, v in cases:
+            B = torch.from_numpy(np.random.default_rng(7).uniform(-1, 1, (2048, N)).astype(np.float16)).to(DEV)
+            outs, plans = [], []
+            for head in (0, 1):
+                gsa.set_config("KS_HEAD", head)
+                plan = gsa.Plan.from_coo(640, 2048, r, c, v).run_pipeline("block_total", N, rows, 1).compile().upload("f16", 0)
+                assert plan.info()["device_kernel"] == "k_mfma_ks", plan.info()
+                outs.append(plan.spmm(B).float().cpu().numpy())
+                plans.append(plan)
+            gsa.set_config("KS_HEAD", 1)
+            np.testing.assert_array_equal(outs[0], outs[1])
+            check(outs[1], ofi.spmm_ref(640, N, r, c, v.astype(np.float16).astype(np.float32),
+                                        B.cpu().numpy().astype(np.float32), "f64"), "f16")
+            plans[1].add_replica()
+            Cs = [torch.full((640, N), float("nan"), device=DEV, dtype=torch.float16) for _ in range(3)]
+            bat = gsa.Batch([(plans[1], 0, B, Cs[0]), (plans[0], 0, B, Cs[1]), (plans[1], 1, B, Cs[2])], N)
+            assert bat.launches() == [3]  # head and record-only entries share the instantiation
+            bat.run(torch.cuda.current_stream().cuda_stream)
+            for cc in Cs:
+                np.testing.assert_array_equal(cc.float().cpu().numpy(), outs[0])
+            for p in plans:
+                p.device_status()
+                p.free()
+    finally:
+        gsa.set_config("KS_HEAD", 1)
+        gsa.set_config("KS_NT", 0)
+        gsa.set_config("KS_SPLIT", 0)
+
+
 @pytest.mark.parametrize("p8", [0, 1])
 @pytest.mark.parametrize("rows,split", [(40, 2), (80, 4), (112, 1), (112, 4), (128, 3)])
 def test_mfma_ks_four_waves(rows, split, p8, mfma_everywhere):
