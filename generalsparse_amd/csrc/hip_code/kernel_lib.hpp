@@ -291,6 +291,8 @@ __device__ __forceinline__ void wave_row(const uint32_t b, const uint32_t e, con
     }
 }
 
+constexpr uint32_t kWarpRowsMaxChunks = 3;  // k_warp_rows: SCF-chunks per slot in one grouped pass (WARP_ROWS_CHUNKS)
+
 template <class VT, class CT, int CF, int SCF, bool FX>
 __device__ __forceinline__ void warp_rows_body(const uint32_t *__restrict__ bmw_first_row,  // n_bmw+1
                                                    const idx_formula f_row,
@@ -299,7 +301,7 @@ __device__ __forceinline__ void warp_rows_body(const uint32_t *__restrict__ bmw_
                                                    const uint32_t *__restrict__ row_ptr,        // rows+1 (CSR)
                                                    const CT *__restrict__ col, const VT *__restrict__ val,
                                                    const VT *__restrict__ B, VT *__restrict__ C, uint32_t n_bmw,
-                                                   uint32_t N, uint32_t X, uint32_t row_base, uint32_t G) {
+                                                   uint32_t N, uint32_t X, uint32_t row_base, uint32_t G, uint32_t nch) {
     // G slots per row (a power of two <= S): the wave takes S/G consecutive rows of the BMW at
     // a time, so rows much shorter than S*SCF nonzeros do not leave most slots idle (C1: rows
     // of ~37 nonzeros against 128-nonzero wave passes at N = 8)
@@ -329,9 +331,12 @@ __device__ __forceinline__ void warp_rows_body(const uint32_t *__restrict__ bmw_
             idx_range<FX>(bmw_first_row, f_row, w, r_begin, r_end);
             if (RP > 1 && r_end - r_begin <= 63u) {
                 // grouped passes, software-pipelined: the BMW's row starts in one load (lane i
-                // holds row_ptr[r_begin + i]); the first chunk of pass ps+1 is loaded before the
-                // B gathers of pass ps, so a pass waits on one gather latency, not three
+                // holds row_ptr[r_begin + i]); a pass gives each slot up to nch SCF-chunks of its
+                // row at once (all their A loads, then all their B gathers in flight: one gather
+                // round trip per pass, not one per chunk), and pass ps+1's chunks are loaded before
+                // the gathers of pass ps, so a pass waits on one gather latency, not three
                 typedef typename raw_vec<CF * sizeof(VT)>::t RB;
+                constexpr uint32_t MC = kWarpRowsMaxChunks;
                 const uint32_t nr = r_end - r_begin, npass = (nr + RP - 1) / RP;
                 const uint32_t rpv = lane <= nr ? row_ptr[r_begin + lane] : 0u;
                 auto bounds = [&](uint32_t ps, uint32_t &b, uint32_t &e) {  // rows past the end: b == e
@@ -339,11 +344,8 @@ __device__ __forceinline__ void warp_rows_body(const uint32_t *__restrict__ bmw_
                     b = (uint32_t)__shfl((int)rpv, (int)min(i, nr), 64);
                     e = (uint32_t)__shfl((int)rpv, (int)min(i + 1u, nr), 64);
                 };
-                auto chunk = [&](uint32_t q, uint32_t b, uint32_t e, const CT (&cc)[SCF], const VT (&vv)[SCF],
-                                 float (&acc)[CF]) {
-                    RB braw[SCF];
-#pragma unroll
-                    for (int j = 0; j < SCF; j++) braw[j] = *reinterpret_cast<const RB *>(B + (size_t)cc[j] * N + c0);
+                auto fma_chunk = [&](uint32_t q, uint32_t b, uint32_t e, const VT (&vv)[SCF], const RB (&braw)[SCF],
+                                     float (&acc)[CF]) {
 #pragma unroll
                     for (int j = 0; j < SCF; j++) {
                         const float v = (q + j >= b && q + j < e) ? (float)vv[j] : 0.f;
@@ -353,35 +355,66 @@ __device__ __forceinline__ void warp_rows_body(const uint32_t *__restrict__ bmw_
                         for (int k = 0; k < CF; k++) acc[k] = __builtin_fmaf(v, (float)bt[k], acc[k]);
                     }
                 };
+                auto chunk = [&](uint32_t q, uint32_t b, uint32_t e, const CT (&cc)[SCF], const VT (&vv)[SCF],
+                                 float (&acc)[CF]) {
+                    RB braw[SCF];
+#pragma unroll
+                    for (int j = 0; j < SCF; j++) braw[j] = *reinterpret_cast<const RB *>(B + (size_t)cc[j] * N + c0);
+                    fma_chunk(q, b, e, vv, braw, acc);
+                };
+                // chunk c of a pass: entries p + c*S*SCF .. (chunks past the row: column 0, value 0)
+                CT cn[MC][SCF];
+                VT vn[MC][SCF];
+                auto load_pass = [&](uint32_t p, uint32_t e) {
+#pragma unroll
+                    for (uint32_t c = 0; c < MC; c++) {
+                        if (c >= nch) break;
+                        const uint32_t q = p + c * S * SCF;
+                        if (q < e) {
+                            load_raw<CT, SCF>(col + q, cn[c]);
+                            load_raw<VT, SCF>(val + q, vn[c]);
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < SCF; j++) { cn[c][j] = (CT)0; vn[c][j] = (VT)0.f; }
+                        }
+                    }
+                };
                 uint32_t b, e;
                 bounds(0u, b, e);
                 uint32_t p = (b & ~(uint32_t)(SCF - 1)) + slot * SCF;
-                CT cn[SCF];
-                VT vn[SCF];
-                if (p < e) {
-                    load_raw<CT, SCF>(col + p, cn);
-                    load_raw<VT, SCF>(val + p, vn);
-                }
+                load_pass(p, e);
                 for (uint32_t ps = 0; ps < npass; ps++) {
-                    CT cc[SCF];
-                    VT vv[SCF];
+                    CT cc[MC][SCF];
+                    VT vv[MC][SCF];
 #pragma unroll
-                    for (int j = 0; j < SCF; j++) { cc[j] = cn[j]; vv[j] = vn[j]; }
+                    for (uint32_t c = 0; c < MC; c++)
+#pragma unroll
+                        for (int j = 0; j < SCF; j++) { cc[c][j] = cn[c][j]; vv[c][j] = vn[c][j]; }
                     const uint32_t cb = b, ce = e, cp = p;
                     if (ps + 1 < npass) {
                         bounds(ps + 1u, b, e);
                         p = (b & ~(uint32_t)(SCF - 1)) + slot * SCF;
-                        if (p < e) {
-                            load_raw<CT, SCF>(col + p, cn);
-                            load_raw<VT, SCF>(val + p, vn);
-                        }
+                        load_pass(p, e);
                     }
                     float acc[CF];
 #pragma unroll
                     for (int k = 0; k < CF; k++) acc[k] = 0.f;
                     if (cp < ce) {
-                        chunk(cp, cb, ce, cc, vv, acc);
-                        for (uint32_t q = cp + S * SCF; q < ce; q += S * SCF) {  // rest of a long row
+                        // every chunk's gathers before any chunk's FMAs
+                        RB braw[MC][SCF];
+#pragma unroll
+                        for (uint32_t c = 0; c < MC; c++) {
+                            if (c >= nch) break;
+#pragma unroll
+                            for (int j = 0; j < SCF; j++)
+                                braw[c][j] = *reinterpret_cast<const RB *>(B + (size_t)cc[c][j] * N + c0);
+                        }
+#pragma unroll
+                        for (uint32_t c = 0; c < MC; c++) {
+                            if (c >= nch) break;
+                            fma_chunk(cp + c * S * SCF, cb, ce, vv[c], braw[c], acc);
+                        }
+                        for (uint32_t q = cp + nch * S * SCF; q < ce; q += S * SCF) {  // rest of a long row
                             CT cq[SCF];
                             VT vq[SCF];
                             load_raw<CT, SCF>(col + q, cq);
@@ -416,18 +449,19 @@ __device__ __forceinline__ void warp_rows_body(const uint32_t *__restrict__ bmw_
 }
 
 template <class VT, class CT, int CF, int SCF>
-__global__ __launch_bounds__(256) void k_warp_rows(const uint32_t *__restrict__ bmw_first_row, const idx_formula f_row,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_warp_rows(const uint32_t *__restrict__ bmw_first_row, const idx_formula f_row,
                                                    const uint32_t *__restrict__ bmw_of_bmtb, const idx_formula f_bmw,
                                                    const uint32_t *__restrict__ row_ptr, const CT *__restrict__ col,
                                                    const VT *__restrict__ val, const VT *__restrict__ B, VT *__restrict__ C,
                                                    uint32_t n_bmw, uint32_t N, uint32_t X, uint32_t row_base,
-                                                   uint32_t G = 64) {
+                                                   uint32_t G = 64, uint32_t nch = 1) {
+    nch = nch < 1u ? 1u : (nch > kWarpRowsMaxChunks ? kWarpRowsMaxChunks : nch);
     if (f_row.kind == IDX_ARRAY && f_bmw.kind == IDX_ARRAY)
         warp_rows_body<VT, CT, CF, SCF, false>(bmw_first_row, f_row, bmw_of_bmtb, f_bmw, row_ptr, col, val, B, C, n_bmw, N, X,
-                                               row_base, G);
+                                               row_base, G, nch);
     else
         warp_rows_body<VT, CT, CF, SCF, true>(bmw_first_row, f_row, bmw_of_bmtb, f_bmw, row_ptr, col, val, B, C, n_bmw, N, X,
-                                              row_base, G);
+                                              row_base, G, nch);
 }
 
 // ---------------------------------------------------------------------------

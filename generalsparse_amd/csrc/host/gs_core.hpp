@@ -81,6 +81,7 @@ struct config_t {
     bool LDS_STAGE_B = true;  // warp_total inside BMTBs: stage B chunks in LDS (k_lds_rows)
     bool MFMA_TILES = true;   // fp16 BMTB row blocks on the matrix cores (k_mfma_rows)
     int64_t MFMA_KROT = 0;
+    int64_t WARP_ROWS_CHUNKS = 3;  // k_warp_rows grouped passes: SCF-chunks per slot in one pass (1..3)
     int64_t WARP_ROWS_GROUPS = 1;  // k_warp_rows: several short rows of a BMW per wave pass    // k_mfma_rows / k_nm_mfma: each workgroup starts at its own K chunk
     int64_t MFMA_MAX_FILL = 16;  // ... when (padded row-block area) / nnz <= this
     bool NM_MFMA = true;         // col-direction plans whose rows are 2:4 panels: sparse matrix cores (k_nm_mfma)

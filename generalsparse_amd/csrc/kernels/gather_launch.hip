@@ -101,16 +101,18 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
             uint32_t gx;
             if (sp.tblock_parent) gx = (uint32_t)d.n_rows_aux;
             else gx = (uint32_t)std::min<uint64_t>((d.n_units + 3) / 4, 1u << 16);
-            // slots per row: enough SCF-chunks for the plan's mean row, the rest of the wave on the
-            // next rows of the BMW (only when BMWs hold several rows)
-            uint32_t G = 64u / X;
+            // slots per row: enough for the plan's mean row in WARP_ROWS_CHUNKS SCF-chunks per slot
+            // (taken in one pass: one gather round trip), the rest of the wave on the next rows of
+            // the BMW (only when BMWs hold several rows)
+            uint32_t G = 64u / X, nch = 1;
             if (d.bmw_rows_max > 1 && get_config().WARP_ROWS_GROUPS) {
-                const uint32_t need = (uint32_t)std::max<double>(1.0, std::ceil(d.mean_row_nnz / 4.0));
+                nch = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(gsk::kWarpRowsMaxChunks, get_config().WARP_ROWS_CHUNKS));
+                const uint32_t need = (uint32_t)std::max<double>(1.0, std::ceil(d.mean_row_nnz / (4.0 * nch)));
                 G = std::min<uint32_t>(G, pow2ceil(need));
             }
             hipLaunchKernelGGL((gsk::k_warp_rows<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
                                a.a0, d.f0, sp.tblock_parent ? a.a1 : nullptr, sp.tblock_parent ? d.f1 : gsk::idx_formula(), a.a2, col, val, B, C, (uint32_t)d.n_units, N,
-                               X, row_base, G);
+                               X, row_base, G, nch);
             break;
         }
         case KF_BLOCK_TOTAL: {

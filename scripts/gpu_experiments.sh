@@ -15,6 +15,7 @@
 #   nt3       KS_NT masks on C2 + the north_star layer, NM_NT over the C3 dense-width sweep
 #   nmphase   k_nm_mfma phase stamps + no-B / no-A loop timings on C3 (experiments build)
 #   head      KS_HEAD A/B on C2 (KS_NT=1) and the north_star layer
+#   c1chunks  k_warp_rows SCF-chunks per slot per pass (WARP_ROWS_CHUNKS) on C1
 # Every GPU step runs under its own time limit; the first failure ends the session (set -e).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-r05x}; mkdir -p $OUT; export TMPDIR=/tmp
@@ -150,6 +151,11 @@ print('c3 NM_NT=$x sweep', [(r['N'], r.get('kernel_ms')) for r in d.get('n_sweep
       pyt pytest_head.log tests/test_gpu_spmm.py -k "head_steps or nontemporal or driver_plan or headline or mfma_ks_matches"
       c2="--workload c2 --steps 200 --warmup 50 --no-cpu --no-rocsparse --pipeline block_total --p0 40 --config KS_NT=1"
       for x in 0 1 0 1; do bench c2_head$x $c2 --config KS_HEAD=$x; done ;;
+    c1chunks)  # k_warp_rows chunks per slot per pass on C1 (and the C2 / C4 gather candidates' parity)
+      pyt pytest_chunks.log tests/test_gpu_spmm.py -k "warp_rows_chunks or PIPES or pipes"
+      c1="--workload c1 --steps 200 --warmup 20 --no-cpu --no-rocsparse --pipeline tblock_warp_total --p0 32 --p1 8"
+      for x in 1 2 3 1 2 3; do bench c1_ch$x $c1 --config WARP_ROWS_CHUNKS=$x; done
+      bench c1_auto --workload c1 --steps 200 --warmup 20 --no-cpu ;;
     *) echo "unknown experiment $ex"; exit 2 ;;
   esac
 done

@@ -1108,3 +1108,32 @@ def test_batch_grouped_launch_matches_single_launches():
         assert torch.equal(cc, ref), (rep,)
     for p in plans + [pg]:
         p.free()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f16"])
+@pytest.mark.parametrize("chunks", [1, 2, 3])
+@pytest.mark.parametrize("p0,p1", [(32, 8), (8, 8), (16, 4)])
+def test_warp_rows_chunks_per_pass(p0, p1, chunks, dtype):
+    """k_warp_rows grouped passes with WARP_ROWS_CHUNKS SCF-chunks per slot (all A loads, then all
+    gathers of a pass in flight): every case of coo_cases plus a C1-like matrix (Poisson rows of
+    ~37 nonzeros, some past the pass capacity) against the oracle"""
+    old = gsa.get_config("WARP_ROWS_CHUNKS")
+    gsa.set_config("WARP_ROWS_CHUNKS", chunks)
+    try:
+        cases = list(coo_cases())
+        cases.append(("c1_like", 4000, 3000, *ds.random_rows(4000, 3000, 37.4, seed=18)))
+        r, c, v = ds.random_rows(800, 3000, 37.4, seed=19)
+        keep = ((r % 97) != 5) & (r != 7)  # some empty rows; row 7 rebuilt as a 300-nonzero row
+        r2 = np.concatenate([r[keep], np.full(300, 7, r.dtype)])
+        c2 = np.concatenate([c[keep], np.arange(300, dtype=c.dtype) * 9])
+        v2 = np.concatenate([v[keep], np.ones(300, v.dtype)])
+        o = np.lexsort((c2, r2))
+        cases.append(("c1_long_rows", 800, 3000, r2[o], c2[o], v2[o]))
+        for case, M, K, row, col, val in cases:
+            plan, C, B = run(M, K, row, col, val, "tblock_warp_total", p0, p1, 8, dtype)
+            v32 = val.astype(np.float16).astype(np.float32) if dtype == "f16" else val.astype(np.float32)
+            ref = ofi.spmm_ref(M, 8, row, col, v32, B.astype(np.float32), "f64")
+            check(C, ref, dtype)
+            plan.free()
+    finally:
+        gsa.set_config("WARP_ROWS_CHUNKS", old)
