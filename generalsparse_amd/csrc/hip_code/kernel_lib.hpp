@@ -90,23 +90,6 @@ template <> struct raw_ext<4> { typedef uint32_t t; };
 template <> struct raw_ext<8> { typedef u32x2 t; };
 template <> struct raw_ext<16> { typedef u32x4 t; };
 
-// one raw B-row piece (4..32 bytes) by a non-temporal load
-template <class RB>
-__device__ __forceinline__ RB ld_nt_raw(const void *p) {
-    RB r;
-    if constexpr (sizeof(RB) <= 16) {
-        typedef typename raw_ext<sizeof(RB)>::t R;
-        const R x = __builtin_nontemporal_load(reinterpret_cast<const R *>(p));
-        __builtin_memcpy(&r, &x, sizeof(RB));
-    } else {
-        static_assert(sizeof(RB) == 32, "4 to 32 bytes");
-        const u32x4 x[2] = {__builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p)),
-                            __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p) + 1)};
-        __builtin_memcpy(&r, x, 32);
-    }
-    return r;
-}
-
 // SCF contiguous sparse entries (cols or vals) in one load (read once: ld_once)
 template <class T, int SCF>
 __device__ __forceinline__ void load_raw(const T *__restrict__ p, T (&out)[SCF]) {
@@ -3710,11 +3693,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                                                     uint32_t n_empty, uint32_t fill_blocks,
                                                     const uint32_t *__restrict__ chain,  // 2 n_waves or null
                                                     uint32_t *__restrict__ chain_cnt,    // n_waves, zero between launches
-                                                    uint32_t dbg = 0, uint64_t *__restrict__ stamps = nullptr,
-                                                    uint32_t hot = 0xffffffffu) {
+                                                    uint32_t dbg = 0, uint64_t *__restrict__ stamps = nullptr) {
     // dbg (diagnostic timing runs only, wrong results): bit 1 gathers B row 0 for every nonzero
-    // hot (MP_HOT_NT, column-permuted plans): B rows of columns >= hot -- the rarely used ones after
-    // the degree renumbering -- are gathered by non-temporal loads, so they do not evict hot rows
     const uint32_t lb = blockIdx.x;  // (XCD-contiguous numbering measured no faster cold on C4)
     if (lb < fill_blocks) {
         // the first fill_blocks workgroups zero the empty rows (listed; 16-B stores when a
@@ -3823,10 +3803,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                 for (uint32_t k = 0; k < kMpItems; k++) {
                     const uint32_t z = base + k;
                     const bool valid = z >= zl && z < ze;
-                    const uint32_t ci = valid && !(dbg & 2u) ? (uint32_t)cc[k] : 0u;
-                    const VT *bp = B + (size_t)ci * N + c0;
-                    if (ci < hot) braw[k] = *reinterpret_cast<const RB *>(bp);
-                    else braw[k] = ld_nt_raw<RB>(bp);
+                    braw[k] = *reinterpret_cast<const RB *>(B + (size_t)(valid && !(dbg & 2u) ? (uint32_t)cc[k] : 0u) * N + c0);
                 }
                 if (rnd < 4u) GS_MP_STAMP(2u + 3u * rnd);
                 for (uint32_t i = lane; i < fw; i += 64u) wl[i] = 0u;

@@ -106,8 +106,6 @@ struct config_t {
                                  // their new places) instead of a gather
     int64_t MP_PERM_HOT = 0;     // MP_COL_PERM: 0 = every column sorted by degree; H > 0 = only the H densest columns
                                  // move to the front (by degree), the others keep their order after them
-    int64_t MP_HOT_NT = 0;       // column-permuted merge-path plans: gathers of columns >= this by non-temporal loads
-                                 // (0: all plain)
     int64_t MP_SOLO = 16;        // k_merge_rows: rows of at most this many nonzeros are one slot's
     int64_t KS_WAVES = 8;        // k_mfma_ks waves per workgroup (8 or 16)
     int64_t KS_SPLIT = 0;        // k_mfma_ks K ranges per row block (0: the fewest that fit LDS and fill the CUs)

@@ -26,13 +26,6 @@ constexpr int kLdsMaxU = 12;  // 16-B staging registers per thread (k_lds_rows M
 uint64_t *g_mp_stamps = nullptr;  // set by debug_mp_timeline for one launch (diagnostic build only)
 #endif
 
-// MP_HOT_NT: on a column-permuted merge-path plan, B rows of columns past the first MP_HOT_NT (the
-// least used after the degree renumbering) are gathered by non-temporal loads; 0 = every gather plain
-uint32_t mp_hot(const device_plan &d) {
-    const int64_t h = get_config().MP_HOT_NT;
-    return d.col_perm && h > 0 ? (uint32_t)std::min<int64_t>(h, 0xffffffffll) : 0xffffffffu;
-}
-
 // GS_MP_DEBUG (diagnostic timing only): k_merge_path dbg bits
 uint32_t mp_debug() {
 #ifdef GS_EXPERIMENTS
@@ -203,13 +196,13 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
                     hipLaunchKernelGGL((gsk::k_merge_path<VT, CT, CF, true>), dim3(gx + fb, tiles), dim3(256), lds, s, a.a0, a.a1,
                                    a.a2, a.a3, (uint32_t)d.n_rows_aux, col, val, B, C, a.ws, a.t0, a.ws2, W, N, X, row_base,
                                    (uint32_t)d.n_out_rows, a.a4, (uint32_t)d.n_fin, fb, fused ? a.t1 : nullptr,
-                                   fused ? a.t2 : nullptr, mp_debug(), g_mp_stamps, mp_hot(d));
+                                   fused ? a.t2 : nullptr, mp_debug(), g_mp_stamps);
             else
 #endif
                     hipLaunchKernelGGL((gsk::k_merge_path<VT, CT, CF>), dim3(gx + fb, tiles), dim3(256), lds, s, a.a0, a.a1,
                                    a.a2, a.a3, (uint32_t)d.n_rows_aux, col, val, B, C, a.ws, a.t0, a.ws2, W, N, X, row_base,
                                    (uint32_t)d.n_out_rows, a.a4, (uint32_t)d.n_fin, fb, fused ? a.t1 : nullptr,
-                                   fused ? a.t2 : nullptr, mp_debug(), nullptr, mp_hot(d));
+                                   fused ? a.t2 : nullptr, mp_debug());
             HIP_OK(hipGetLastError());
             if (fused) break;
             GS_CHECK((uint64_t)W * N < 0xffffffffull, "merge-path fix-up indices exceed 32 bits");

@@ -16,7 +16,6 @@
 #   nmphase   k_nm_mfma phase stamps + no-B / no-A loop timings on C3 (experiments build)
 #   head      KS_HEAD A/B on C2 (KS_NT=1) and the north_star layer
 #   c1chunks  k_warp_rows SCF-chunks per slot per pass (WARP_ROWS_CHUNKS) on C1
-#   mphot     com-Orkut: MP_HOT_NT sweep (non-temporal gathers of the cold columns)
 # Every GPU step runs under its own time limit; the first failure ends the session (set -e).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-r05x}; mkdir -p $OUT; export TMPDIR=/tmp
@@ -157,10 +156,6 @@ print('c3 NM_NT=$x sweep', [(r['N'], r.get('kernel_ms')) for r in d.get('n_sweep
       c1="--workload c1 --steps 200 --warmup 20 --no-cpu --no-rocsparse --pipeline tblock_warp_total --p0 32 --p1 8"
       for x in 1 2 3 1 2 3; do bench c1_ch$x $c1 --config WARP_ROWS_CHUNKS=$x; done
       bench c1_auto --workload c1 --steps 200 --warmup 20 --no-cpu ;;
-    mphot)  # com-Orkut: non-temporal gathers of the cold columns (MP_HOT_NT) on one plan, interleaved
-      pyt pytest_mphot.log tests/test_gpu_spmm.py -k "column_permutation or merge_path"
-      timeout -k 10 900 python3 -u scripts/mp_hot_sweep.py 0,32768,131072,524288,2097152 3 10 > $OUT/mp_hot.log 2>&1
-      tail -1 $OUT/mp_hot.log ;;
     *) echo "unknown experiment $ex"; exit 2 ;;
   esac
 done

@@ -906,31 +906,6 @@ def test_merge_path_column_permutation_is_exact(N, dtype, variant):
     check(outs[1], ofi.spmm_ref(M, N, row, col, vv, B.astype(np.float32), "f64"), dtype)
 
 
-@pytest.mark.parametrize("dtype", ["f32", "f16"])
-def test_merge_path_cold_gathers_nontemporal_is_exact(dtype):
-    """MP_HOT_NT (read at launch): on a column-permuted merge-path plan the gathers of columns past
-    the first H are non-temporal loads -- a cache policy, not a different sum: C is bit-identical
-    for every H"""
-    M, N = 3000, 8
-    row, col, val = ds.rmat(M, 60000, seed=11)
-    B = torch.from_numpy(np.random.default_rng(5).uniform(-1, 1, (M, N)).astype(np.float16 if dtype == "f16" else np.float32)).to(DEV)
-    gsa.set_config("MP_COL_PERM", 1)
-    try:
-        plan = gsa.Plan.from_coo(M, M, row, col, val).run_pipeline("merge_path", N, 512, 1).compile().upload(dtype, 0)
-    finally:
-        gsa.set_config("MP_COL_PERM", -1)
-    outs = []
-    try:
-        for h in (0, 1, 100, 1000, 1 << 30):
-            gsa.set_config("MP_HOT_NT", h)
-            outs.append(plan.spmm(B).float().cpu().numpy())
-    finally:
-        gsa.set_config("MP_HOT_NT", 0)
-    for o in outs[1:]:
-        np.testing.assert_array_equal(outs[0], o)
-    plan.free()
-
-
 def test_merge_path_deterministic_and_no_stale_state(merge_walk):
     """two launches give bit-identical C (no floating-point atomics: a split row's partials
     are combined in wave order by the last arriver on an integer arrival counter, and the
