@@ -156,6 +156,15 @@ print('c3 NM_NT=$x sweep', [(r['N'], r.get('kernel_ms')) for r in d.get('n_sweep
       c1="--workload c1 --steps 200 --warmup 20 --no-cpu --no-rocsparse --pipeline tblock_warp_total --p0 32 --p1 8"
       for x in 1 2 3 1 2 3; do bench c1_ch$x $c1 --config WARP_ROWS_CHUNKS=$x; done
       bench c1_auto --workload c1 --steps 200 --warmup 20 --no-cpu ;;
+    n128b)  # C2 at N = 128: row-block height x K split on k_mfma_ks (CT = 8 up to 48 rows)
+      for p0 in 32 40 48; do for sp in 0 3 4; do
+        timeout -k 10 600 python3 -u bench.py --workload c2 --steps 20 --warmup 5 --no-cpu --no-rocsparse --no-north-star \
+          --pipeline block_total --p0 $p0 --n-sweep 128 --config KS_SPLIT=$sp > $OUT/n128_${p0}_$sp.log 2>&1
+        python3 -c "
+import json
+d=[json.loads(l) for l in open('$OUT/n128_${p0}_$sp.log') if l.startswith('{')][-1]
+print('rows $p0 split $sp', [(r['N'], r.get('kernel'), r.get('kernel_ms'), r.get('hbm_frac')) for r in d['n_sweep']])"
+      done; done ;;
     *) echo "unknown experiment $ex"; exit 2 ;;
   esac
 done
