@@ -340,7 +340,7 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     t.W = W;
     // KS_POS8 (8-bit positions in 8 x 16 segments; N = 32, RT <= 8: segment ids < 32)
     t.P8 = get_config().KS_POS8 && CT == 2 && (W == kKsWaves || W == 4);
-    t.NT = CT == 2 && W == kKsWaves && !t.P8 && t.AP && get_config().KS_NT ? 1u : 0u;
+    t.NT = (CT == 2 || CT == 8) && W == kKsWaves && !t.P8 && t.AP && get_config().KS_NT ? 1u : 0u;
     // pass 1: the largest step (entries of a row block in 32 columns; P8: groups per segment)
     uint64_t gmax = 1;
     {

@@ -94,13 +94,13 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
              "k_mfma_ks with 4 or 16 waves, 8-bit positions or the overlapped LDS layout: experiments build");
 #endif
     auto kern = gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, STAMPS>;
-    if (d.ks_nt) {  // KS_NT: A's groups by non-temporal loads (N = 32, 8 waves, the apart layout)
-        if constexpr (CT == 2 && W == (int)kKsWaves && !STAMPS) {
+    if (d.ks_nt) {  // KS_NT: A's groups by non-temporal loads (N = 32 / 128, 8 waves, the apart layout)
+        if constexpr ((CT == 2 || CT == 8) && W == (int)kKsWaves && !STAMPS) {
             GS_CHECK(d.ks_ap && !d.ks_p8, "k_mfma_ks: non-temporal loads are built for the apart layout, 16-bit positions");
             GS_CHECK(d.ks_nt == 1, "k_mfma_ks: KS_NT is built for A's groups (1)");
             kern = gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, false, true, false, 1>;
         } else {
-            throw gs_error("k_mfma_ks: non-temporal loads are built for N = 32, 8 waves");
+            throw gs_error("k_mfma_ks: non-temporal loads are built for N = 32 and 128-column tiles, 8 waves");
         }
     }
 #ifdef GS_EXPERIMENTS

@@ -165,6 +165,13 @@ import json
 d=[json.loads(l) for l in open('$OUT/n128_${p0}_$sp.log') if l.startswith('{')][-1]
 print('rows $p0 split $sp', [(r['N'], r.get('kernel'), r.get('kernel_ms'), r.get('hbm_frac')) for r in d['n_sweep']])"
       done; done ;;
+    n128nt)  # C2 at N = 128 with KS_NT on the 128-column tiles: parity, then the dense-width sweep (candidates incl. KS_NT)
+      pyt pytest_n128nt.log tests/test_gpu_spmm.py -k "nontemporal"
+      bench c2_nsweep --workload c2 --steps 20 --warmup 5 --no-cpu --no-rocsparse --no-north-star --n-sweep 8,32,128
+      python3 -c "
+import json
+d=[json.loads(l) for l in open('$OUT/b_c2_nsweep.log') if l.startswith('{')][-1]
+for r in d['n_sweep']: print(r['N'], r.get('plan'), r.get('kernel_ms'), r.get('hbm_frac'), {k: v.get('kernel_ms') for k, v in r['tried'].items()})" ;;
     *) echo "unknown experiment $ex"; exit 2 ;;
   esac
 done
