@@ -172,6 +172,8 @@ print('rows $p0 split $sp', [(r['N'], r.get('kernel'), r.get('kernel_ms'), r.get
 import json
 d=[json.loads(l) for l in open('$OUT/b_c2_nsweep.log') if l.startswith('{')][-1]
 for r in d['n_sweep']: print(r['N'], r.get('plan'), r.get('kernel_ms'), r.get('hbm_frac'), {k: v.get('kernel_ms') for k, v in r['tried'].items()})" ;;
+    graph)  # C2 launches in a HIP graph vs one by one
+      for x in "40 200 KS_NT=1" "40 200 KS_NT=0" "80 200 KS_NT=1"; do timeout -k 10 300 python3 -u scripts/graph_probe.py $x; done ;;
     *) echo "unknown experiment $ex"; exit 2 ;;
   esac
 done
