@@ -702,6 +702,27 @@ def replicas_for(info, K, N, e, rotation_mb):
     return max(2, int(math.ceil(rotation_mb * 1e6 / (read_A + K * N * e))))
 
 
+def stream_copy_gbs(torch, dev, mib=2048, reps=10):
+    """STREAM-copy bandwidth of this GPU (SURVEY 8d's measured denominator): a torch copy of
+    `mib` MiB of fp32, read + written bytes over the HIP-event time of `reps` copies"""
+    n = mib * (1 << 20) // 4
+    a = torch.empty(n, dtype=torch.float32, device=dev).uniform_()
+    b = torch.empty_like(a)
+    for _ in range(3):
+        b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbs = 2.0 * n * 4 * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return round(gbs, 1)
+
+
 def event_ms(plan, Bs, Cs, reps, torch, warm=20, rotate=True):
     """average kernel time (ms) of `reps` launches from HIP events on the launch stream"""
     stream = torch.cuda.current_stream()
@@ -889,6 +910,7 @@ def main():
     else:
         wall, ev_s = time_plan(plan, Bs, Cs, N, args.steps, args.warmup, torch, dist)
     hot_ms = event_ms(plan, Bs, Cs, 100, torch, rotate=False)
+    copy_gbs = stream_copy_gbs(torch, dev)
     # value and ms_per_step from the HIP events around the K timed steps (max over ranks);
     # the host wall time of the same region is reported beside them
     ev_ms = ev_s / args.steps * 1e3
@@ -937,6 +959,10 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": round(ev_ms, 5),
                      "hot_cache_kernel_ms": round(hot_ms, 5),
+                     "measured_copy_gbs": copy_gbs, "frac_of_measured_copy": round(achieved / copy_gbs, 4),
+                     "measured_copy_note": "STREAM-copy peak measured on this GPU after the timed region (SURVEY "
+                                           "8d): torch copy of 2 GiB fp32, bytes read + written; `peak` stays "
+                                           "the 8 TB/s datasheet figure",
                      "mfma_util": mfma["mfma_util"] if mfma else None, "mfma": mfma},
         "variants": variants,
     }
@@ -965,6 +991,8 @@ def main():
                                        max(args.steps, 20), max(args.warmup, 10))
             for p in plans.values():
                 p.free()
+            ns["roofline"]["measured_copy_gbs"] = copy_gbs
+            ns["roofline"]["frac_of_measured_copy"] = round(ns["roofline"]["achieved"] / copy_gbs, 4)
             out["north_star"] = ns
         except Exception as ex:  # the C2 line must not be lost to a failure of the extra object
             out["north_star"] = {"error": f"{type(ex).__name__}: {ex}"}
