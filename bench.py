@@ -172,21 +172,12 @@ def algorithmic_bytes_24(M, K, N, nnz, e):
 
 
 def mark(torch):
-    """GS_BENCH_MARK=1: one tiny spin kernel on the current stream right after the last timed
-    launch; with the pre-roll spin before the first (preroll) it brackets the timed region, so
-    that scripts/timed_stats.py can keep only the timed region's dispatches of a rocprofv3
-    kernel trace (the plan search's launches of the same kernels are left out)"""
+    """GS_BENCH_MARK=1: one tiny fill kernel on the current stream, launched right before the
+    first and right after the last timed launch, so that scripts/timed_stats.py can keep only
+    the timed region's dispatches of a rocprofv3 kernel trace (the plan search's launches of
+    the same kernels are left out)"""
     if os.environ.get("GS_BENCH_MARK") == "1":
         torch.cuda._sleep(64)  # a kernel of its own name (spin), launched nowhere else
-
-
-def preroll(torch):
-    """a ~30 us spin kernel on the current stream right before the start event: the GPU is busy
-    while the host enqueues the event and the first timed launches, so the event interval holds
-    the K steps back to back rather than the host's first-launch latency as well (20 timed C2
-    steps: 13.4 us per step without it against 12.5 us for 200).  Not counted as a step; the
-    opening marker of the timed region for timed_stats.py."""
-    torch.cuda._sleep(60000)
 
 
 def time_plan(plan, Bs, Cs, N, steps, warmup, torch, dist=None):
@@ -202,7 +193,7 @@ def time_plan(plan, Bs, Cs, N, steps, warmup, torch, dist=None):
     torch.cuda.synchronize()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
-    preroll(torch)
+    mark(torch)
     t0 = time.perf_counter()
     e0.record(stream)
     plan.spmm_rotate(steps, 0, Bs, Cs)
@@ -419,7 +410,7 @@ def timed_batch(step, streams, steps, torch, marked=False):
     e1 = torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     if marked:
-        preroll(torch)
+        mark(torch)
     t0 = time.perf_counter()
     e0.record(cur)
     for s in streams[1:]:
@@ -982,8 +973,7 @@ def main():
         "metric": wl["metric"],
         "value": round(value, 1), "unit": "GFLOP/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 5), "higher_is_better": True,
-        "timing": "HIP events on the launch stream around the K timed steps (a ~30 us spin kernel queued ahead of "
-                  "the start event keeps the host's first-launch latency out of the interval), max over ranks",
+        "timing": "HIP events on the launch stream around the K timed steps, max over ranks",
         "wall_ms_per_step": round(wall / args.steps * 1e3, 5), "wall_value": round(wall_value, 1),
         "scaling": "weak" if shards is None else "strong", "vs_baseline": None,
         "dtype": "f16 (fp32 accumulate)" if dt == "f16" else "f32", "data": wl["data"],
