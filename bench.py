@@ -196,7 +196,9 @@ def time_plan(plan, Bs, Cs, N, steps, warmup, torch, dist=None):
     mark(torch)
     t0 = time.perf_counter()
     e0.record(stream)
-    plan.spmm_rotate(steps, 0, Bs, Cs)
+    # the rotation continues after the warm-up steps' copies (a timed step never reuses one
+    # that a warm-up step left in the Infinity Cache)
+    plan.spmm_rotate(steps, warmup, Bs, Cs)
     e1.record(stream)
     mark(torch)
     torch.cuda.synchronize()
