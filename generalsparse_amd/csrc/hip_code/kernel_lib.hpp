@@ -291,9 +291,9 @@ __device__ __forceinline__ void wave_row(const uint32_t b, const uint32_t e, con
     }
 }
 
-constexpr uint32_t kWarpRowsMaxChunks = 3;  // k_warp_rows: SCF-chunks per slot in one grouped pass (WARP_ROWS_CHUNKS)
+constexpr uint32_t kWarpRowsMaxChunks = 3;  // k_warp_rows_mc: SCF-chunks per slot in one grouped pass (WARP_ROWS_CHUNKS)
 
-template <class VT, class CT, int CF, int SCF, bool FX>
+template <class VT, class CT, int CF, int SCF, bool FX, uint32_t MC = 1>
 __device__ __forceinline__ void warp_rows_body(const uint32_t *__restrict__ bmw_first_row,  // n_bmw+1
                                                    const idx_formula f_row,
                                                    const uint32_t *__restrict__ bmw_of_bmtb,    // n_bmtb+1 or null
@@ -336,7 +336,6 @@ __device__ __forceinline__ void warp_rows_body(const uint32_t *__restrict__ bmw_
                 // round trip per pass, not one per chunk), and pass ps+1's chunks are loaded before
                 // the gathers of pass ps, so a pass waits on one gather latency, not three
                 typedef typename raw_vec<CF * sizeof(VT)>::t RB;
-                constexpr uint32_t MC = kWarpRowsMaxChunks;
                 const uint32_t nr = r_end - r_begin, npass = (nr + RP - 1) / RP;
                 const uint32_t rpv = lane <= nr ? row_ptr[r_begin + lane] : 0u;
                 auto bounds = [&](uint32_t ps, uint32_t &b, uint32_t &e) {  // rows past the end: b == e
@@ -448,20 +447,46 @@ __device__ __forceinline__ void warp_rows_body(const uint32_t *__restrict__ bmw_
     }
 }
 
+template <class VT, class CT, int CF, int SCF, uint32_t MC>
+__device__ __forceinline__ void warp_rows_kernel(const uint32_t *__restrict__ bmw_first_row, const idx_formula f_row,
+                                                 const uint32_t *__restrict__ bmw_of_bmtb, const idx_formula f_bmw,
+                                                 const uint32_t *__restrict__ row_ptr, const CT *__restrict__ col,
+                                                 const VT *__restrict__ val, const VT *__restrict__ B, VT *__restrict__ C,
+                                                 uint32_t n_bmw, uint32_t N, uint32_t X, uint32_t row_base, uint32_t G,
+                                                 uint32_t nch) {
+    nch = nch < 1u ? 1u : (nch > MC ? MC : nch);
+    if (f_row.kind == IDX_ARRAY && f_bmw.kind == IDX_ARRAY)
+        warp_rows_body<VT, CT, CF, SCF, false, MC>(bmw_first_row, f_row, bmw_of_bmtb, f_bmw, row_ptr, col, val, B, C, n_bmw,
+                                                   N, X, row_base, G, nch);
+    else
+        warp_rows_body<VT, CT, CF, SCF, true, MC>(bmw_first_row, f_row, bmw_of_bmtb, f_bmw, row_ptr, col, val, B, C, n_bmw,
+                                                  N, X, row_base, G, nch);
+}
+
+// one SCF-chunk per slot and pass (registers as the plan needs them)
 template <class VT, class CT, int CF, int SCF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_warp_rows(const uint32_t *__restrict__ bmw_first_row, const idx_formula f_row,
+__global__ __launch_bounds__(256) void k_warp_rows(const uint32_t *__restrict__ bmw_first_row, const idx_formula f_row,
                                                    const uint32_t *__restrict__ bmw_of_bmtb, const idx_formula f_bmw,
                                                    const uint32_t *__restrict__ row_ptr, const CT *__restrict__ col,
                                                    const VT *__restrict__ val, const VT *__restrict__ B, VT *__restrict__ C,
                                                    uint32_t n_bmw, uint32_t N, uint32_t X, uint32_t row_base,
-                                                   uint32_t G = 64, uint32_t nch = 1) {
-    nch = nch < 1u ? 1u : (nch > kWarpRowsMaxChunks ? kWarpRowsMaxChunks : nch);
-    if (f_row.kind == IDX_ARRAY && f_bmw.kind == IDX_ARRAY)
-        warp_rows_body<VT, CT, CF, SCF, false>(bmw_first_row, f_row, bmw_of_bmtb, f_bmw, row_ptr, col, val, B, C, n_bmw, N, X,
-                                               row_base, G, nch);
-    else
-        warp_rows_body<VT, CT, CF, SCF, true>(bmw_first_row, f_row, bmw_of_bmtb, f_bmw, row_ptr, col, val, B, C, n_bmw, N, X,
-                                              row_base, G, nch);
+                                                   uint32_t G = 64) {
+    warp_rows_kernel<VT, CT, CF, SCF, 1>(bmw_first_row, f_row, bmw_of_bmtb, f_bmw, row_ptr, col, val, B, C, n_bmw, N, X,
+                                         row_base, G, 1u);
+}
+
+// up to kWarpRowsMaxChunks SCF-chunks per slot and pass, at most 128 VGPRs (four waves per SIMD):
+// launched for fp32 values, u16 columns and 4-entry chunks of 16-B B pieces (C1: fp32, N = 8), the
+// instantiations that fit 128 registers without spilling
+template <class VT, class CT, int CF, int SCF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_warp_rows_mc(
+    const uint32_t *__restrict__ bmw_first_row, const idx_formula f_row, const uint32_t *__restrict__ bmw_of_bmtb,
+    const idx_formula f_bmw, const uint32_t *__restrict__ row_ptr, const CT *__restrict__ col, const VT *__restrict__ val,
+    const VT *__restrict__ B, VT *__restrict__ C, uint32_t n_bmw, uint32_t N, uint32_t X, uint32_t row_base, uint32_t G,
+    uint32_t nch) {
+    static_assert(SCF <= 4 && CF * sizeof(VT) <= 16, "k_warp_rows_mc: 4-entry chunks, B pieces of at most 16 B");
+    warp_rows_kernel<VT, CT, CF, SCF, kWarpRowsMaxChunks>(bmw_first_row, f_row, bmw_of_bmtb, f_bmw, row_ptr, col, val, B, C,
+                                                          n_bmw, N, X, row_base, G, nch);
 }
 
 // ---------------------------------------------------------------------------

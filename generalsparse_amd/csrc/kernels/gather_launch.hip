@@ -110,9 +110,26 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
                 const uint32_t need = (uint32_t)std::max<double>(1.0, std::ceil(d.mean_row_nnz / (4.0 * nch)));
                 G = std::min<uint32_t>(G, pow2ceil(need));
             }
-            hipLaunchKernelGGL((gsk::k_warp_rows<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
-                               a.a0, d.f0, sp.tblock_parent ? a.a1 : nullptr, sp.tblock_parent ? d.f1 : gsk::idx_formula(), a.a2, col, val, B, C, (uint32_t)d.n_units, N,
-                               X, row_base, G, nch);
+            bool mc = false;
+            if constexpr (SCF <= 4 && CF * sizeof(VT) == 16 && sizeof(VT) == 4 && sizeof(CT) == 2) {  // spill-free at 128 VGPRs
+                if (nch > 1) {  // several chunks per slot and pass: the 128-VGPR multi-chunk kernel
+                    hipLaunchKernelGGL((gsk::k_warp_rows_mc<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
+                                       a.a0, d.f0, sp.tblock_parent ? a.a1 : nullptr, sp.tblock_parent ? d.f1 : gsk::idx_formula(), a.a2, col,
+                                       val, B, C, (uint32_t)d.n_units, N, X, row_base, G, nch);
+                    mc = true;
+                }
+            }
+            if (!mc) {
+                // one chunk per slot and pass: slots per row for the mean row in one chunk each
+                if (nch > 1) {
+                    nch = 1;
+                    if (d.bmw_rows_max > 1 && get_config().WARP_ROWS_GROUPS)
+                        G = std::min<uint32_t>(64u / X, pow2ceil((uint32_t)std::max<double>(1.0, std::ceil(d.mean_row_nnz / 4.0))));
+                }
+                hipLaunchKernelGGL((gsk::k_warp_rows<VT, CT, CF, SCF>), dim3(std::max(gx, 1u), tiles), dim3(256), 0, s,
+                                   a.a0, d.f0, sp.tblock_parent ? a.a1 : nullptr, sp.tblock_parent ? d.f1 : gsk::idx_formula(), a.a2, col, val, B, C, (uint32_t)d.n_units, N,
+                                   X, row_base, G);
+            }
             break;
         }
         case KF_BLOCK_TOTAL: {
