@@ -391,9 +391,14 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     t.GCAP = (uint32_t)gmax;
     t.MAXG = gmax <= 64 ? 1 : (gmax <= 128 ? 2 : (gmax <= 192 ? 3 : (gmax <= 256 ? 4 : 0)));
     if (!t.MAXG) { why = "a k-step holds more than 256 entry groups"; return false; }
+    if (t.CT == 8 && !ks_ct8_fits(RT, t.MAXG)) {  // a 128-column instantiation that would spill: 64-column tiles
+        t.CT = 4;
+        t.NT = 0;  // (KS_NT is built for 32- and 128-column tiles)
+        t.lds_bytes = gsk::ks_lds_bytes(4, RT, W, t.AP);
+    }
     if (!t.AP && t.MAXG > 2 && W != 4) {  // the 8-wave overlapped layout is instantiated for MAXG <= 2 only
         t.AP = true;
-        t.lds_bytes = gsk::ks_lds_bytes(CT, RT, W, true);
+        t.lds_bytes = gsk::ks_lds_bytes(t.CT, RT, W, true);
         if (t.lds_bytes > 160 * 1024) { why = "k_mfma_ks wave stages exceed LDS"; return false; }
     }
     // 32-bit group and step indices (packed steps: about nnz / 8 + nb*S*NS groups; checked

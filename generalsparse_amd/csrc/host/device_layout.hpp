@@ -76,6 +76,9 @@ inline uint32_t ks_col_tiles(uint32_t N) { return (N + 16 * ks_ct(N) - 1) / (16 
 // per workgroup (CT = 8: 96 fp32 accumulators, 255 VGPRs, no spill), so A is read once at N = 128
 // instead of once per 64-column tile; taller blocks keep CT = 4 (their accumulators would spill)
 inline uint32_t ks_ct_rt(uint32_t N, uint32_t RT) { return N >= 128 && RT <= 3 ? 8u : ks_ct(N); }
+// ... and the 128-column instantiations that hold their registers (no spill): 32-row blocks with up to
+// 192 entry groups per k-step, 48-row blocks with up to 64; other plans at N >= 128 take CT = 4
+inline bool ks_ct8_fits(uint32_t RT, uint32_t MAXG) { return (RT == 2 && MAXG <= 3) || (RT == 3 && MAXG == 1); }
 inline uint32_t ks_col_tiles_ct(uint32_t N, uint32_t CT) { return (N + 16 * CT - 1) / (16 * CT); }
 
 bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint32_t> &row_ptr,

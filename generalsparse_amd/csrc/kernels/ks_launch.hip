@@ -131,11 +131,24 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
 
 template <int CT, int RT>
 void launch_ks_rt(const plan_state &p, const device_arrays &a, const gsk::f16 *B, gsk::f16 *C, uint32_t N, hipStream_t s) {
-    switch (p.dev.seg_cap) {  // MAXG: entry groups per lane per k-step
-        case 1: launch_ks_k<CT, RT, 1>(p, a, B, C, N, s); break;
-        case 2: launch_ks_k<CT, RT, 2>(p, a, B, C, N, s); break;
-        case 3: launch_ks_k<CT, RT, 3>(p, a, B, C, N, s); break;
-        default: launch_ks_k<CT, RT, 4>(p, a, B, C, N, s); break;
+    if constexpr (CT == 8) {  // 128-column tiles: only the (RT, MAXG) pairs that do not spill (ks_ct8_fits)
+        GS_CHECK(ks_ct8_fits(RT, p.dev.seg_cap), "k_mfma_ks: 128-column tile instantiation not built for this plan");
+        if constexpr (RT == 2) {
+            switch (p.dev.seg_cap) {
+                case 1: launch_ks_k<CT, RT, 1>(p, a, B, C, N, s); break;
+                case 2: launch_ks_k<CT, RT, 2>(p, a, B, C, N, s); break;
+                default: launch_ks_k<CT, RT, 3>(p, a, B, C, N, s); break;
+            }
+        } else {
+            launch_ks_k<CT, RT, 1>(p, a, B, C, N, s);
+        }
+    } else {
+        switch (p.dev.seg_cap) {  // MAXG: entry groups per lane per k-step
+            case 1: launch_ks_k<CT, RT, 1>(p, a, B, C, N, s); break;
+            case 2: launch_ks_k<CT, RT, 2>(p, a, B, C, N, s); break;
+            case 3: launch_ks_k<CT, RT, 3>(p, a, B, C, N, s); break;
+            default: launch_ks_k<CT, RT, 4>(p, a, B, C, N, s); break;
+        }
     }
 }
 
@@ -147,16 +160,17 @@ void launch_ks_ct(const plan_state &p, const device_arrays &a, const gsk::f16 *B
             case 3: launch_ks_rt<CT, 3>(p, a, B, C, N, s); return;
             default: throw gs_error("k_mfma_ks: 128-column tiles take row blocks of up to 48 rows");
         }
-    }
-    switch (p.dev.maxr) {  // RT: 16-row tiles per row block (the upload builds RT >= 2)
-        case 2: launch_ks_rt<CT, 2>(p, a, B, C, N, s); break;
-        case 3: launch_ks_rt<CT, 3>(p, a, B, C, N, s); break;
-        case 4: launch_ks_rt<CT, 4>(p, a, B, C, N, s); break;
-        case 5: launch_ks_rt<CT, 5>(p, a, B, C, N, s); break;
-        case 6: if constexpr (CT <= 2) { launch_ks_rt<CT, 6>(p, a, B, C, N, s); break; } [[fallthrough]];
-        case 7: if constexpr (CT <= 2) { launch_ks_rt<CT, 7>(p, a, B, C, N, s); break; } [[fallthrough]];
-        case 8: if constexpr (CT <= 2) { launch_ks_rt<CT, 8>(p, a, B, C, N, s); break; } [[fallthrough]];
-        default: throw gs_error("k_mfma_ks: row tiles outside 2..8 (6..8 for N <= 32)");
+    } else {
+        switch (p.dev.maxr) {  // RT: 16-row tiles per row block (the upload builds RT >= 2)
+            case 2: launch_ks_rt<CT, 2>(p, a, B, C, N, s); break;
+            case 3: launch_ks_rt<CT, 3>(p, a, B, C, N, s); break;
+            case 4: launch_ks_rt<CT, 4>(p, a, B, C, N, s); break;
+            case 5: launch_ks_rt<CT, 5>(p, a, B, C, N, s); break;
+            case 6: if constexpr (CT <= 2) { launch_ks_rt<CT, 6>(p, a, B, C, N, s); break; } [[fallthrough]];
+            case 7: if constexpr (CT <= 2) { launch_ks_rt<CT, 7>(p, a, B, C, N, s); break; } [[fallthrough]];
+            case 8: if constexpr (CT <= 2) { launch_ks_rt<CT, 8>(p, a, B, C, N, s); break; } [[fallthrough]];
+            default: throw gs_error("k_mfma_ks: row tiles outside 2..8 (6..8 for N <= 32)");
+        }
     }
 }
 
@@ -356,7 +370,9 @@ void launch_ks(const plan_state &p, const device_arrays &a, const void *B, void 
     const gsk::f16 *b = (const gsk::f16 *)B;
     gsk::f16 *c = (gsk::f16 *)C;
     GS_CHECK(N == p.dev.lds_N, "k_mfma_ks runs the plan's dense width");
-    GS_CHECK(p.dev.ks_ctw == ks_ct_rt(N, p.dev.maxr), "k_mfma_ks: column tiles disagree with the upload");
+    GS_CHECK(p.dev.ks_ctw == ks_ct_rt(N, p.dev.maxr) || (p.dev.ks_ctw == 4 && ks_ct_rt(N, p.dev.maxr) == 8 &&
+                                                         !ks_ct8_fits(p.dev.maxr, p.dev.seg_cap)),
+             "k_mfma_ks: column tiles disagree with the upload");
     switch (p.dev.ks_ctw) {  // 16-column tiles per workgroup; ks_col_tiles_ct(N, CT) workgroups across N
         case 1: launch_ks_ct<1>(p, a, b, c, N, s); break;
         case 2: launch_ks_ct<2>(p, a, b, c, N, s); break;
