@@ -175,13 +175,14 @@ for r in d['n_sweep']: print(r['N'], r.get('plan'), r.get('kernel_ms'), r.get('h
     graph)  # C2 launches in a HIP graph vs one by one
       for x in "40 200 KS_NT=1" "40 200 KS_NT=0" "80 200 KS_NT=1"; do timeout -k 10 300 python3 -u scripts/graph_probe.py $x; done ;;
     wrows)  # k_warp_rows / k_warp_rows_mc after the split: parity, C1 line, C2 gather candidates
-      pyt pytest_wrows.log tests/test_gpu_spmm.py -k "warp_rows or PIPES or pipes or tblock"
+      pyt pytest_wrows.log tests/test_gpu_spmm.py -k "warp_rows or PIPES or pipes or tblock or mfma_ks or nontemporal or head"
       bench c1 --workload c1 --steps 200 --warmup 20 --no-cpu --no-rocsparse
-      bench c2 --workload c2 --steps 200 --warmup 20 --no-cpu --no-rocsparse --no-north-star
+      bench c2 --workload c2 --steps 200 --warmup 20 --no-cpu --no-rocsparse --no-north-star --n-sweep 128
       python3 -c "
 import json
 d=[json.loads(l) for l in open('$OUT/b_c2.log') if l.startswith('{')][-1]
-print({k: v.get('kernel_ms') for k, v in d['variants'].items()})" ;;
+print({k: v.get('kernel_ms') for k, v in d['variants'].items()})
+print('N=128', [(r.get('plan'), r.get('kernel_ms'), r.get('hbm_frac'), {k: v.get('kernel_ms') for k, v in r['tried'].items()}) for r in d['n_sweep']])" ;;
     *) echo "unknown experiment $ex"; exit 2 ;;
   esac
 done
