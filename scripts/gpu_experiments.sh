@@ -183,6 +183,9 @@ import json
 d=[json.loads(l) for l in open('$OUT/b_c2.log') if l.startswith('{')][-1]
 print({k: v.get('kernel_ms') for k, v in d['variants'].items()})
 print('N=128', [(r.get('plan'), r.get('kernel_ms'), r.get('hbm_frac'), {k: v.get('kernel_ms') for k, v in r['tried'].items()}) for r in d['n_sweep']])" ;;
+    prio)  # KS_PRIO re-check on the round-5 kernel (head steps, KS_NT) : C2 + the north_star layer
+      c2="--workload c2 --steps 200 --warmup 50 --no-cpu --no-rocsparse --pipeline block_total --p0 40 --config KS_NT=1"
+      for x in 1 0 2 1 0 2; do bench c2_prio$x $c2 --config KS_PRIO=$x; done ;;
     *) echo "unknown experiment $ex"; exit 2 ;;
   esac
 done
