@@ -2897,7 +2897,8 @@ typedef _Float16 h16v __attribute__((ext_vector_type(16)));
 // kNmWaves, kNmBlockBytes, kNmKC: kernel_consts.hpp
 
 // DBG (diagnostic builds only, GS_NM_DEBUG): 1 = no B loads in the loop, 2 = no A loads,
-// 4 = s_memtime phase stamps of waves 0/4 of workgroups 0 and 100, printed
+// 4 = s_memtime phase stamps of waves 0/4 of workgroups 0 and 100, printed, 8 = the transposed B
+// fragment reads of odd n-tiles skipped (half the LDS reads; wrong results)
 // NG: the dense width in HBM (B and C row length); NG = 8 runs one 16-column tile whose
 // columns 8..15 are zeros in LDS and never stored (N = 8, the half-used tile of C3's N sweep)
 template <int CT, int DBG = 0, int NG = 16 * CT, bool NT = false>
@@ -3004,7 +3005,7 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
         h16v bf_[2];                                                                              \
         GS_NM_BFRAG(lb_, 0, bf_[0]);                                                              \
         _Pragma("unroll") for (int ct = 0; ct < CT; ct++) {                                       \
-            if (ct + 1 < CT) GS_NM_BFRAG(lb_, ct + 1, bf_[(ct + 1) & 1]);                         \
+            if (ct + 1 < CT && !(DBG == 8 && ((ct + 1) & 1))) GS_NM_BFRAG(lb_, ct + 1, bf_[(ct + 1) & 1]); \
             const h16v b_ = bf_[ct & 1];                                                          \
             acc[0][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[0], b_, acc[0][ct], ix0_, 0, 0); \
             acc[1][ct] = __builtin_amdgcn_smfmac_f32_16x16x64_f16(av_[1], b_, acc[1][ct], ix0_, 0, 1); \

@@ -152,6 +152,7 @@ void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, vo
     static const int dbg = getenv("GS_NM_DEBUG") ? atoi(getenv("GS_NM_DEBUG")) : 0;
     auto kern = dbg == 1 ? gsk::k_nm_mfma<CT, 1, NG>
                          : (dbg == 2 ? gsk::k_nm_mfma<CT, 2, NG> : (dbg == 4 ? gsk::k_nm_mfma<CT, 4, NG> : gsk::k_nm_mfma<CT, 0, NG>));
+    if (dbg == 8) kern = gsk::k_nm_mfma<CT, 8, NG>;
     if (d.nm_nt && dbg == 0) kern = gsk::k_nm_mfma<CT, 0, NG, true>;
 #else
     constexpr int dbg = 0;

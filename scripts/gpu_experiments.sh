@@ -144,7 +144,7 @@ print('c3 NM_NT=$x sweep', [(r['N'], r.get('kernel_ms')) for r in d.get('n_sweep
       done ;;
     nmphase)  # k_nm_mfma phase stamps and the loop without B / A loads (experiments build)
       EXP=$PWD/generalsparse_amd/libgeneralsparse_exp.so
-      for dbg in 0 1 2; do GS_LIBRARY=$EXP GS_NM_DEBUG=$dbg timeout -k 10 300 python3 -u scripts/nm_phases.py 128 50; done
+      for dbg in 0 1 2 8; do GS_LIBRARY=$EXP GS_NM_DEBUG=$dbg timeout -k 10 300 python3 -u scripts/nm_phases.py 128 50; done
       GS_LIBRARY=$EXP GS_NM_DEBUG=4 timeout -k 10 300 python3 -u scripts/nm_phases.py 128 > $OUT/nm_stamps.txt 2>&1
       grep "wave" $OUT/nm_stamps.txt | head -30 ;;
     head)  # KS_HEAD (head steps at fixed slots) on C2 40-row (with KS_NT=1) + the north_star layer

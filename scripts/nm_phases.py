@@ -1,8 +1,9 @@
 """C3 k_nm_mfma phase attribution (diagnostic; experiments build, GS_LIBRARY=...exp.so).
 GS_NM_DEBUG=4: s_memtime stamps per half iteration (B staged to LDS / B loads issued / compute /
 A loads issued / barrier passed) of waves 0 and 4 of workgroups 0 and 100, printed by the kernel;
-GS_NM_DEBUG=1 / 2: the loop without B / A loads (wrong results, timing only).
-usage: GS_NM_DEBUG=<0|1|2|4> nm_phases.py [N] [launches]"""
+GS_NM_DEBUG=1 / 2: the loop without B / A loads, 8: without the odd n-tiles' B fragment reads
+(wrong results, timing only).
+usage: GS_NM_DEBUG=<0|1|2|4|8> nm_phases.py [N] [launches]"""
 import os
 import sys
 
