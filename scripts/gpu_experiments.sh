@@ -186,6 +186,10 @@ print('N=128', [(r.get('plan'), r.get('kernel_ms'), r.get('hbm_frac'), {k: v.get
     prio)  # KS_PRIO re-check on the round-5 kernel (head steps, KS_NT) : C2 + the north_star layer
       c2="--workload c2 --steps 200 --warmup 50 --no-cpu --no-rocsparse --pipeline block_total --p0 40 --config KS_NT=1"
       for x in 1 0 2 1 0 2; do bench c2_prio$x $c2 --config KS_PRIO=$x; done ;;
+    krot)  # C3 k_nm_mfma: every workgroup from its own B chunk (MFMA_KROT=1) vs all from chunk 0
+      pyt pytest_krot.log tests/test_gpu_nm.py -k "c3_scale or linearity"
+      c3="--workload c3 --steps 100 --warmup 20 --no-cpu --no-rocsparse --pipeline col_direction_nm"
+      for x in 0 1 0 1; do bench c3_krot$x $c3 --config MFMA_KROT=$x; done ;;
     *) echo "unknown experiment $ex"; exit 2 ;;
   esac
 done
