@@ -357,7 +357,7 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
                 std::to_string(lds) + ")";
         launch = k + "<<<" + std::to_string((L.nm_rows + 127) / 128) + ", " + std::to_string(64 * gsk::kNmWaves) + ", " +
                  std::to_string(lds) + ">>>(d_blk, d_B, d_C, (uint32_t)K, " + std::to_string(L.nm_S) + "u, " +
-                 std::to_string(L.nm_rows) + "u, 0u, 0u)";
+                 std::to_string(L.nm_rows) + "u, 0u, " + std::to_string((uint32_t)get_config().NM_KROT) + "u)";
     }
     o << "    std::vector<VT> hB(K * N, (VT)1.0f);  // x_arr = 1 (code_generator.cc:464-467)\n"
       << "    VT *d_B = up(hB, 0); VT *d_C; hipMalloc(&d_C, M * N * sizeof(VT)); hipMemset(d_C, 0, M * N * sizeof(VT));\n"

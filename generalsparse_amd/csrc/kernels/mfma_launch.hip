@@ -199,7 +199,7 @@ void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, vo
     const uint32_t wg = (uint32_t)((d.n_rows_aux + 127) / 128);
     hipLaunchKernelGGL(kern, dim3(wg), dim3(64 * gsk::kNmWaves), lds, s, (const unsigned char *)a.tcol,
                        (const gsk::f16 *)B, (gsk::f16 *)C, (uint32_t)p.K, d.KC, (uint32_t)d.n_rows_aux,
-                       (uint32_t)d.row_base, (uint32_t)get_config().MFMA_KROT);
+                       (uint32_t)d.row_base, (uint32_t)get_config().NM_KROT);
     HIP_OK(hipGetLastError());
 }
 
