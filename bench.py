@@ -687,7 +687,7 @@ def run_c5h(args, torch, gsa, ds, rank, world, local, dev, dist):
                                       rocsparse=not args.no_rocsparse)
     rs = {k: per_shape[k]["rocsparse_f16"] for k in per_shape} if not args.no_rocsparse else {}
     out, plans = headline_layer(args, torch, gsa, ds, rank, local, dev, choice, args.steps, args.warmup,
-                                per_shape=per_shape, rs_per_shape=rs)
+                                per_shape=per_shape, rs_per_shape=rs, settle_ms=200.0)
     nnz_l, flops_l, alg_l = layer_consts(N, sp)
     # the layer's kernels one at a time (each shape's search time = its own launch alone)
     serial_ms = sum(per_shape[k]["kernel_us"] for k in bt.C5_SLOTS) * 1e-3
