@@ -146,7 +146,10 @@ CANDIDATES = [("block_total", 20, 1), ("block_total", 10, 1), ("block_total", 40
 CANDIDATES_C3 = [("col_direction_nm", 32, 1), ("col_direction_nm", 32, 1, {"NM_NT": 0})]
 
 # C1: token_test's default (thread_total, sparse_cf 4) and the row-block / merge-path plans
-CANDIDATES_C1 = [("thread_total", 4, 1), ("tblock_warp_total", 4, 1), ("tblock_warp_total", 32, 8), ("merge_path", 512, 1)]
+# (tblock_warp_total(64, 16): 16-row BMWs, two per wave pass of k_warp_rows_mc, 16.2 us against
+# 17.8 for (32, 8), profiles/r05ae_c1_plans.txt)
+CANDIDATES_C1 = [("thread_total", 4, 1), ("tblock_warp_total", 4, 1), ("tblock_warp_total", 32, 8),
+                 ("tblock_warp_total", 32, 16), ("tblock_warp_total", 64, 16), ("merge_path", 512, 1)]
 
 # C4: merge-path levels (WARP, work_size p0) and the balanced / row-per-thread plans
 CANDIDATES_C4 = [("merge_path", 256, 1), ("merge_path", 512, 1), ("merge_path", 1024, 1), ("balanced_block_total", 2048, 1),
