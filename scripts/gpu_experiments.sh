@@ -195,6 +195,11 @@ print('N=128', [(r.get('plan'), r.get('kernel_ms'), r.get('hbm_frac'), {k: v.get
         set -- $pp
         bench c1_$1_$2 --workload c1 --steps 200 --warmup 20 --no-cpu --no-rocsparse --pipeline tblock_warp_total --p0 $1 --p1 $2
       done ;;
+    c4plans)  # C4 webbase: other plans beside the merge path
+      for pp in "tblock_warp_total 32 8" "tblock_warp_total 64 16" "tblock_warp_total 128 32" "merge_path 128 1" "merge_path 256 1" "balanced_warp_total 64 1" "balanced_warp_total 256 1"; do
+        set -- $pp
+        bench c4_$1_$2_$3 --workload c4 --steps 200 --warmup 20 --no-cpu --no-rocsparse --pipeline $1 --p0 $2 --p1 $3 || true
+      done ;;
     *) echo "unknown experiment $ex"; exit 2 ;;
   esac
 done
