@@ -200,6 +200,12 @@ print('N=128', [(r.get('plan'), r.get('kernel_ms'), r.get('hbm_frac'), {k: v.get
         set -- $pp
         bench c4_$1_$2_$3 --workload c4 --steps 200 --warmup 20 --no-cpu --no-rocsparse --pipeline $1 --p0 $2 --p1 $3 || true
       done ;;
+    c2rows)  # C2 k_mfma_ks row-block height x K split with KS_NT=1 and head steps
+      c2="--workload c2 --steps 200 --warmup 20 --no-cpu --no-rocsparse --no-north-star --pipeline block_total --config KS_NT=1"
+      for pp in "32 0" "40 0" "48 0" "56 0" "64 0" "80 0" "48 2" "56 2" "64 2" "40 3"; do
+        set -- $pp
+        bench c2_$1_$2 $c2 --p0 $1 --config KS_SPLIT=$2 --config KS_MIN_ROWS=32 || true
+      done ;;
     *) echo "unknown experiment $ex"; exit 2 ;;
   esac
 done
