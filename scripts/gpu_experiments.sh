@@ -191,8 +191,8 @@ print('N=128', [(r.get('plan'), r.get('kernel_ms'), r.get('hbm_frac'), {k: v.get
       c3="--workload c3 --steps 100 --warmup 20 --no-cpu --no-rocsparse --pipeline col_direction_nm"
       for x in 0 1 0 1; do bench c3_krot$x $c3 --config MFMA_KROT=$x; done ;;
     c1plans)  # C1: tblock_warp_total(rows per BMTB, rows per BMW) sweep on k_warp_rows_mc
-      for pp in "16 8" "32 8" "64 8" "128 8" "32 16" "64 16" "32 4" "64 32"; do
-        set -- $pp
+      for pp in ${C1PLANS:-16_8 32_8 64_8 128_8 32_16 64_16 32_4 64_32}; do
+        set -- ${pp/_/ }
         bench c1_$1_$2 --workload c1 --steps 200 --warmup 20 --no-cpu --no-rocsparse --pipeline tblock_warp_total --p0 $1 --p1 $2
       done ;;
     c4plans)  # C4 webbase: other plans beside the merge path
