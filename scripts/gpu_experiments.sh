@@ -206,6 +206,14 @@ print('N=128', [(r.get('plan'), r.get('kernel_ms'), r.get('hbm_frac'), {k: v.get
         set -- $pp
         bench c2_$1_$2 $c2 --p0 $1 --config KS_SPLIT=$2 --config KS_MIN_ROWS=32 || true
       done ;;
+    c5grp)  # C5 batch: launches per matrix over two streams (default) vs grouped k_mfma_ks launches
+      bench c5_streams --workload c5 --steps 20 --warmup 10 --no-cpu --no-rocsparse
+      bench c5_group --workload c5 --steps 20 --warmup 10 --no-cpu --no-rocsparse --group 1 --streams 1
+      bench c5_group2 --workload c5 --steps 20 --warmup 10 --no-cpu --no-rocsparse --group 1 --streams 2 ;;
+    c4owork)  # com-Orkut merge-path work size
+      for ws in 2048 4096; do
+        bench c4o_$ws --workload c4o --pipeline merge_path --p0 $ws --steps 20 --warmup 5 --search-reps 5 --search-rounds 1 --no-cpu --no-rocsparse || true
+      done ;;
     *) echo "unknown experiment $ex"; exit 2 ;;
   esac
 done
