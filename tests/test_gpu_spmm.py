@@ -183,6 +183,39 @@ def test_replicas_and_stream():
     assert plan.info()["replicas"] == 3
 
 
+def test_operands_are_checked_before_any_launch():
+    """a C the kernels would write out of bounds (short, strided, wrong dtype) and a B of the
+    wrong shape are refused by spmm / rotation / Batch; C is left untouched; a checked
+    rotation then runs the same SpMM as spmm"""
+    M, K, N = 300, 200, 16
+    row, col, val = ds.random_rows(M, K, 12.0, seed=5)
+    plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline("block_total", N, 40, 1).compile().upload("f16", 0)
+    B = torch.rand((K, N), device=DEV, dtype=torch.float16)
+    good = torch.empty((M, N), device=DEV, dtype=torch.float16)
+    bad_C = [torch.zeros((M - 1, N), device=DEV, dtype=torch.float16),
+             torch.zeros((N, M), device=DEV, dtype=torch.float16).t(),
+             torch.zeros((M, N), device=DEV, dtype=torch.float32),
+             torch.zeros((M, N + 8), device=DEV, dtype=torch.float16)]
+    for C in bad_C:
+        with pytest.raises((ValueError, TypeError)):
+            plan.spmm(B, C=C)
+        with pytest.raises(ValueError):
+            plan.rotation([B], [C])
+        with pytest.raises(ValueError):
+            gsa.Batch([(plan, 0, B, C)], N)
+        assert not C.any()
+    with pytest.raises(ValueError):
+        plan.spmm(torch.rand((K + 1, N), device=DEV, dtype=torch.float16))
+    with pytest.raises(ValueError):
+        plan.rotation([B, B], [good])
+    with pytest.raises(ValueError):
+        plan.rotation([B, torch.rand((K, 2 * N), device=DEV, dtype=torch.float16)], [good, good.clone()])
+    ref = plan.spmm(B)
+    plan.rotation([B], [good]).run(3, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(good, ref)
+
+
 def test_c2_full_size_against_torch():
     """BASELINE configs[1] shape: OPT-13B q_proj stand-in 5120x5120, 70% pruned, fp16, N=32"""
     M = K = 5120
