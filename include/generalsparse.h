@@ -74,6 +74,10 @@ const char *gs_version(void);
 
 void gs_opts_default(gs_opts *o);
 
+/* Both readers refuse (GS_ERR -1, gs_last_error names the cause) a matrix without entries
+ * (struct.cc:258), rows out of order (struct.cc:120-131), a .mtx index that is not a decimal
+ * >= 1, and any index past 2^32; the dims grow to the largest index + 1.  row / col / val hold
+ * nnz entries each (val may be NULL: every value 1). */
 int gs_plan_create_from_mtx(const char *path, int ones_values, gs_plan_t **out);
 int gs_plan_create_from_coo(uint64_t n_rows, uint64_t n_cols, uint64_t nnz, const uint64_t *row,
                             const uint64_t *col, const float *val, gs_plan_t **out);
@@ -105,7 +109,9 @@ int gs_plan_generate_program(gs_plan_t *p, const char *root_dir, int repeat, cha
 int gs_plan_upload(gs_plan_t *p, int dtype, int device);
 int gs_plan_add_replica(gs_plan_t *p);
 /* C = A * B.  B: K x N row-major, C: M x N row-major, device pointers of the
- * plan's dtype.  Enqueued on `stream`; returns without synchronising. */
+ * plan's dtype.  Enqueued on `stream`; returns without synchronising.  The library cannot
+ * see the extents behind raw pointers: the caller guarantees K x N readable and M x N
+ * writable elements (the Python Plan.spmm / Rotation / Batch check their tensors). */
 int gs_spmm(gs_plan_t *p, const void *B, void *C, int N, gs_stream_t stream);
 int gs_spmm_replica(gs_plan_t *p, int replica, const void *B, void *C, int N, gs_stream_t stream);
 /* `count` SpMMs enqueued back to back from native code, call i using replica
