@@ -802,6 +802,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N > 1 path on a one-GPU box: every rank on cuda:0, the barrier and the
+    # max-over-ranks on gloo (RCCL takes one rank per device).  Timings are contended: the line
+    # is a functional check of the multi-rank path, never a scaling number.
+    shared = os.environ.get("GS_BENCH_SHARED_GPU") == "1" and world > 1
+    if shared:
+        local = 0
     if world != args.gpus and rank == 0:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the real world size",
               file=sys.stderr, flush=True)
@@ -810,7 +816,10 @@ def main():
     if world > 1:
         import torch.distributed as td
         torch.cuda.set_device(local)
-        td.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if shared:
+            td.init_process_group("gloo")
+        else:
+            td.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         dist = td
     else:
         torch.cuda.set_device(0)
