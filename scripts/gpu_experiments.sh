@@ -10,6 +10,7 @@
 #   c4perm2   com-Orkut: gather / scatter / hot-only permutations
 #   nm4b      k_nm_mfma4 (half-chunk B ring) against k_nm_mfma on C3
 #   exptimeout  the forced K-split timeout test on the experiments library
+#   sched     LLVM scheduling strategies (max-ilp / max-memory-clause variant builds) on C2 / C3 / C1
 #   nt        A's once-read loads non-temporal (make var VAR_FLAGS=-DGS_A_NT=1): parity, C2/C3/C1/c4o A/B
 #   nt2       the same on the north_star layer (c5h) with its per-shape search
 #   nt3       KS_NT masks on C2 + the north_star layer, NM_NT over the C3 dense-width sweep
@@ -214,6 +215,36 @@ print('N=128', [(r.get('plan'), r.get('kernel_ms'), r.get('hbm_frac'), {k: v.get
       for ws in 2048 4096; do
         bench c4o_$ws --workload c4o --pipeline merge_path --p0 $ws --steps 20 --warmup 5 --search-reps 5 --search-rounds 1 --no-cpu --no-rocsparse || true
       done ;;
+    sched)  # LLVM scheduling strategies for the device code: libgeneralsparse_var_ilp.so
+      # (VAR_FLAGS="-mllvm -amdgpu-sched-strategy=max-ilp") and _mclause.so (max-memory-clause)
+      ILP=$PWD/generalsparse_amd/libgeneralsparse_var_ilp.so
+      MCL=$PWD/generalsparse_amd/libgeneralsparse_var_mclause.so
+      GS_LIBRARY=$ILP pyt pytest_ilp.log tests/test_gpu_spmm.py tests/test_gpu_nm.py -k "driver_plan or nontemporal or head_steps or nm_matches"
+      GS_LIBRARY=$MCL pyt pytest_mcl.log tests/test_gpu_spmm.py tests/test_gpu_nm.py -k "driver_plan or nontemporal or head_steps or nm_matches"
+      c2="--workload c2 --steps 200 --warmup 20 --no-cpu --no-rocsparse --no-north-star --pipeline block_total --p0 40 --config KS_NT=1"
+      c3="--workload c3 --steps 100 --warmup 20 --no-cpu --no-rocsparse"
+      c1="--workload c1 --steps 200 --warmup 20 --no-cpu --no-rocsparse"
+      for r in 1 2; do
+        bench c2_base$r $c2; GS_LIBRARY=$ILP bench c2_ilp$r $c2; GS_LIBRARY=$MCL bench c2_mcl$r $c2
+      done
+      bench c3_base $c3; GS_LIBRARY=$ILP bench c3_ilp $c3; GS_LIBRARY=$MCL bench c3_mcl $c3
+      bench c1_base $c1; GS_LIBRARY=$ILP bench c1_ilp $c1; GS_LIBRARY=$MCL bench c1_mcl $c1 ;;
+    sched2)  # max-ilp repeat: C2 x4, C1 x2, the north_star layer (c5h) x1, alternating
+      ILP=$PWD/generalsparse_amd/libgeneralsparse_var_ilp.so
+      c2="--workload c2 --steps 200 --warmup 20 --no-cpu --no-rocsparse --no-north-star --pipeline block_total --p0 40 --config KS_NT=1"
+      c1="--workload c1 --steps 200 --warmup 20 --no-cpu --no-rocsparse --pipeline tblock_warp_total --p0 64 --p1 16"
+      c5h="--workload c5h --steps 100 --warmup 10 --search-reps 5 --search-rounds 1 --no-cpu --no-rocsparse"
+      for r in 1 2 3 4; do bench c2_base$r $c2; GS_LIBRARY=$ILP bench c2_ilp$r $c2; done
+      for r in 1 2; do bench c1_base$r $c1; GS_LIBRARY=$ILP bench c1_ilp$r $c1; done
+      bench c5h_base $c5h; GS_LIBRARY=$ILP bench c5h_ilp $c5h ;;
+    sched3)  # max-ilp on the gather kernels: C4 webbase (k_merge_path) x2, com-Orkut x1, C1 x1
+      ILP=$PWD/generalsparse_amd/libgeneralsparse_var_ilp.so
+      c4="--workload c4 --steps 200 --warmup 20 --no-cpu --no-rocsparse --pipeline merge_path --p0 256"
+      c4o="--workload c4o --pipeline merge_path --p0 2048 --steps 20 --warmup 5 --search-reps 5 --search-rounds 1 --no-cpu --no-rocsparse"
+      c1="--workload c1 --steps 200 --warmup 20 --no-cpu --no-rocsparse --pipeline tblock_warp_total --p0 64 --p1 16"
+      for r in 1 2; do bench c4_base$r $c4; GS_LIBRARY=$ILP bench c4_ilp$r $c4; done
+      bench c4o_base $c4o; GS_LIBRARY=$ILP bench c4o_ilp $c4o
+      GS_LIBRARY=$ILP bench c1_ilp3 $c1; bench c1_base3 $c1 ;;
     *) echo "unknown experiment $ex"; exit 2 ;;
   esac
 done
