@@ -291,7 +291,13 @@ __device__ __forceinline__ void wave_row(const uint32_t b, const uint32_t e, con
     }
 }
 
-constexpr uint32_t kWarpRowsMaxChunks = 3;  // k_warp_rows_mc: SCF-chunks per slot in one grouped pass (WARP_ROWS_CHUNKS)
+#ifndef GS_WR_MAXCH  // A/B builds only (make var VAR_FLAGS=...): chunk capacity and waves per SIMD of k_warp_rows_mc
+#define GS_WR_MAXCH 3
+#endif
+#ifndef GS_WR_WPE
+#define GS_WR_WPE 4
+#endif
+constexpr uint32_t kWarpRowsMaxChunks = GS_WR_MAXCH;  // k_warp_rows_mc: SCF-chunks per slot in one grouped pass (WARP_ROWS_CHUNKS)
 
 template <class VT, class CT, int CF, int SCF, bool FX, uint32_t MC = 1>
 __device__ __forceinline__ void warp_rows_body(const uint32_t *__restrict__ bmw_first_row,  // n_bmw+1
@@ -479,7 +485,7 @@ __global__ __launch_bounds__(256) void k_warp_rows(const uint32_t *__restrict__ 
 // launched for fp32 values, u16 columns and 4-entry chunks of 16-B B pieces (C1: fp32, N = 8), the
 // instantiations that fit 128 registers without spilling
 template <class VT, class CT, int CF, int SCF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_warp_rows_mc(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_WR_WPE))) void k_warp_rows_mc(
     const uint32_t *__restrict__ bmw_first_row, const idx_formula f_row, const uint32_t *__restrict__ bmw_of_bmtb,
     const idx_formula f_bmw, const uint32_t *__restrict__ row_ptr, const CT *__restrict__ col, const VT *__restrict__ val,
     const VT *__restrict__ B, VT *__restrict__ C, uint32_t n_bmw, uint32_t N, uint32_t X, uint32_t row_base, uint32_t G,

@@ -245,6 +245,20 @@ print('N=128', [(r.get('plan'), r.get('kernel_ms'), r.get('hbm_frac'), {k: v.get
       for r in 1 2; do bench c4_base$r $c4; GS_LIBRARY=$ILP bench c4_ilp$r $c4; done
       bench c4o_base $c4o; GS_LIBRARY=$ILP bench c4o_ilp $c4o
       GS_LIBRARY=$ILP bench c1_ilp3 $c1; bench c1_base3 $c1 ;;
+    c1ilp)  # C1 under the max-ilp gather build: chunks per pass x plan
+      for pp in "64 16 3" "64 16 2" "64 16 1" "32 16 3" "48 16 3" "64 8 3" "64 16 3" "32 8 2"; do
+        set -- $pp
+        bench c1_$1_$2_ch$3 --workload c1 --steps 200 --warmup 20 --no-cpu --no-rocsparse --pipeline tblock_warp_total --p0 $1 --p1 $2 --config WARP_ROWS_CHUNKS=$3 || true
+      done ;;
+    c1mc5)  # k_warp_rows_mc with 5-chunk capacity at 3 waves per SIMD (libgeneralsparse_var.so built with
+      # VAR_FLAGS="-DGS_WR_MAXCH=5 -DGS_WR_WPE=3") against the default (3 chunks, 4 waves)
+      VAR=$PWD/generalsparse_amd/libgeneralsparse_var.so
+      GS_LIBRARY=$VAR pyt pytest_mc5.log tests/test_gpu_spmm.py -k "warp_rows_chunks or spmm_matches_oracle"
+      c1="--workload c1 --steps 200 --warmup 20 --no-cpu --no-rocsparse --pipeline tblock_warp_total --p0 64 --p1 16"
+      bench c1_def $c1
+      for x in 3 4 5; do GS_LIBRARY=$VAR bench c1_mc5_ch$x $c1 --config WARP_ROWS_CHUNKS=$x; done
+      GS_LIBRARY=$VAR bench c1_mc5_128_32_ch5 --workload c1 --steps 200 --warmup 20 --no-cpu --no-rocsparse --pipeline tblock_warp_total --p0 128 --p1 32 --config WARP_ROWS_CHUNKS=5
+      bench c1_def2 $c1 ;;
     *) echo "unknown experiment $ex"; exit 2 ;;
   esac
 done
