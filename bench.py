@@ -983,7 +983,7 @@ def main():
         try:
             mj = json.load(open(mf))
             if mj.get("kernel") == kernel_label(info) and mj.get("plan") in (None, key):
-                mfma = {k: mj[k] for k in ("mfma_util", "formula", "mfma_util_grbm", "analytic", "kernel_ns_median")
+                mfma = {k: mj[k] for k in ("mfma_util", "formula", "mfma_util_at_clock_est", "clock_ghz_est", "analytic", "kernel_ns_median")
                         if k in mj}
                 mfma["source"] = os.path.relpath(mf, ROOT)
         except Exception:

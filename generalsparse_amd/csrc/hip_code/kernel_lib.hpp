@@ -1682,12 +1682,23 @@ __device__ __forceinline__ u32x4 ks_slab_wait(const uint32_t *src, uint32_t tag,
     if (!lost) {
         load4();
         if (stale()) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            // the bound needs 0.2 s of wall time AND 1024 polls since the last gap: a gap of
+            // over 1 ms between two polls means this wave was switched out (CWSR time slicing),
+            // so the bound restarts rather than counting the time the writer could not run
+            uint64_t t0 = __builtin_amdgcn_s_memrealtime(), prev = t0;
+            uint32_t polls = 0;
             do {
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {
+                const uint64_t t = __builtin_amdgcn_s_memrealtime();
+                if (t - prev > 100000ull) {
+                    t0 = t;
+                    polls = 0;
+                }
+                prev = t;
+                if (t - t0 > 20000000ull && polls >= 1024u) {
                     lost = true;
                     break;
                 }
+                polls++;
                 __builtin_amdgcn_s_sleep(2);
                 load4();
             } while (stale());

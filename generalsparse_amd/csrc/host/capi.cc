@@ -839,7 +839,11 @@ int gs_batch_launches(gs_plan_t *const *plans, const int *replicas, int n, int N
 int gs_plan_device_status(gs_plan_t *p, gs_stream_t stream) {
     return guard([&] {
         GS_CHECK(p, "null plan");
-        GS_HIP(hipStreamSynchronize((hipStream_t)stream));
+        // every stream of the device, not only `stream`: launches of this plan on side streams
+        // (Rotation, Batch, multi-stream C5) must have finished before the words are read and
+        // cleared, or a fault bit could be missed or cleared unreported
+        (void)stream;
+        GS_HIP(hipDeviceSynchronize());
         std::string what;
         for (gs::plan_state *k : kernel_states(p, false)) {
             if (!k->uploaded || !k->dev.err_at) continue;
@@ -905,6 +909,8 @@ int gs_plan_info_get(gs_plan_t *p, gs_plan_info *info) {
             std::strncpy(info->device_kernel, dk.c_str(), sizeof(info->device_kernel) - 1);
             info->index_formulas = s.dev.index_formulas;
             info->index_bytes_saved = s.dev.index_bytes_saved;
+            info->ks_nt = s.dev.ks ? s.dev.ks_nt : 0;
+            info->ks_head_groups = s.dev.ks ? s.dev.ks_gh : 0;
         }
     });
 }

@@ -72,6 +72,19 @@ std::string get_metadata_item_name(POS_TYPE pos, const std::string &name, int su
 }
 
 // ---------------------------------------------------------------- config
+// switches that select kernels kept only in the experiments build (make -C csrc exp):
+// measured slower than the default kernels, parity-tested there
+bool experiments_key(const std::string &k) {
+    return k == "MFMA_BM" || k == "NM_KS" || k == "MFMA_FLAGS" || k == "BM_V2" || k == "BM_KB" || k == "MP_ROWS" ||
+           k == "KS_FORCE_TIMEOUT" || k == "KS_POS8" || k == "NM_V4";
+}
+
+// a key / value the release build refuses, whether from set_config or a JSON config file
+[[maybe_unused]] static bool refused_in_release(const std::string &k, int64_t value, bool is_true) {
+    const bool on = value != 0 || is_true;
+    return (on && experiments_key(k)) || (k == "KS_WAVES" && value != 8) || (k == "KS_APART" && value != 1 && !is_true);
+}
+
 namespace {
 std::mutex g_cfg_mu;
 bool g_cfg_loaded = false;
@@ -167,6 +180,12 @@ void load_json(config_t &c, const std::string &path) {
             while (!val.empty() && isspace((unsigned char)val.back())) val.pop_back();
             p = v1;
         }
+#ifndef GS_EXPERIMENTS
+        // the experiments-build switches are refused here as in set_config: a plan built with
+        // one would reach release kernels that do not read its layout
+        if (refused_in_release(key, std::atoi(val.c_str()), val == "true"))
+            throw gs_error(key + " in " + path + " selects an experiments-build kernel", -2);
+#endif
         apply_kv(c, key, val);
     }
 }
@@ -186,16 +205,9 @@ config_t get_config() {
     return g_cfg;
 }
 
-// switches that select kernels kept only in the experiments build (make -C csrc exp):
-// measured slower than the default kernels, parity-tested there
-bool experiments_key(const std::string &k) {
-    return k == "MFMA_BM" || k == "NM_KS" || k == "MFMA_FLAGS" || k == "BM_V2" || k == "BM_KB" || k == "MP_ROWS" ||
-           k == "KS_FORCE_TIMEOUT" || k == "KS_POS8" || k == "NM_V4";
-}
-
 void set_config(const std::string &key, int64_t value) {
 #ifndef GS_EXPERIMENTS
-    if ((value != 0 && experiments_key(key)) || (key == "KS_WAVES" && value != 8) || (key == "KS_APART" && value != 1))
+    if (refused_in_release(key, value, false))
         throw gs_error(key + " selects an experiments-build kernel (make -C generalsparse_amd/csrc exp)", -2);
 #endif
     std::lock_guard<std::mutex> l(g_cfg_mu);
@@ -353,9 +365,11 @@ uint64_t meta_data_set::output_format_to_dir(const std::string &root, const std:
 }
 
 // ---------------------------------------------------------------- reader
-// Index bound of every entry point: the device layouts keep row / column indices in 32 bits
-// (the reference's int reader keeps unsigned int, struct.cc:263-270).
-static constexpr uint64_t kMaxIndex = 0xffffffffull;
+// Index bound of every entry point: the device layouts keep row / column COUNTS in 32 bits
+// ((uint32_t)n_rows_aux, K < 2^32 in the MP_COL_PERM gate), so the largest index is 2^32 - 2
+// and a dimension at most 2^32 - 1 (the reference's int reader keeps unsigned int,
+// struct.cc:263-270).
+static constexpr uint64_t kMaxIndex = 0xfffffffeull;
 
 // one 1-based .mtx index token: decimal digits up to the next space / end of token, value >= 1
 // (the reference's stoul would take "0" to an index of -1 and garbage to 0 - 1)
@@ -365,7 +379,7 @@ static uint64_t mtx_index(const char *tok, const char *end) {
     char *stop = nullptr;
     uint64_t v = std::strtoull(tok, &stop, 10);
     GS_CHECK(stop == end || *stop == ' ' || *stop == '\t', "malformed mtx index");
-    GS_CHECK(v >= 1 && v - 1 <= kMaxIndex, "mtx index out of range (1-based, at most 2^32)");
+    GS_CHECK(v >= 1 && v - 1 <= kMaxIndex, "mtx index out of range (1-based, at most 2^32 - 1)");
     return v - 1;
 }
 
@@ -468,10 +482,10 @@ std::shared_ptr<meta_data_set> create_init_metadata_set_from_coo(uint64_t n_rows
     GS_CHECK(n_rows > 0 && n_cols > 0, "matrix dims must be positive");
     uint64_t max_row = n_rows - 1, max_col = n_cols - 1;
     std::vector<uint64_t> r(row, row + nnz), c(col, col + nnz);
-    GS_CHECK(max_row <= kMaxIndex && max_col <= kMaxIndex, "matrix dims above 2^32");
+    GS_CHECK(max_row <= kMaxIndex && max_col <= kMaxIndex, "matrix dims above 2^32 - 1");
     for (uint64_t i = 0; i < nnz; i++) {
         GS_CHECK(i == 0 || r[i] >= r[i - 1], "COO entries are not row-sorted (struct.cc:125)");
-        GS_CHECK(r[i] <= kMaxIndex && c[i] <= kMaxIndex, "COO index out of range (at most 2^32)");
+        GS_CHECK(r[i] <= kMaxIndex && c[i] <= kMaxIndex, "COO index out of range (at most 2^32 - 2)");
         max_row = std::max(max_row, r[i]);
         max_col = std::max(max_col, c[i]);
     }

@@ -286,6 +286,7 @@ void launch_ks_group_k(const std::vector<ks_group_item> &it, uint32_t N, hipStre
     auto kern = it[0].p->dev.ks_p8 ? gsk::k_mfma_ks_group<2, RT, W, (int)kKsDepth, MAXG, true, AP>
                                    : gsk::k_mfma_ks_group<2, RT, W, (int)kKsDepth, MAXG, false, AP>;
 #else
+    GS_CHECK(!it[0].p->dev.ks_p8, "k_mfma_ks_group: 8-bit positions are an experiments-build layout");
     auto kern = gsk::k_mfma_ks_group<2, RT, W, (int)kKsDepth, MAXG, false, AP>;
 #endif
     if constexpr (AP) {
@@ -346,6 +347,11 @@ uint32_t ks_group_key(const plan_state &p, uint32_t N) {
     const device_plan &d = p.dev;
     const bool w8 = d.waves == kKsWaves && d.ks_ap, w4 = d.waves == 4 && !d.ks_ap;
     if (!p.uploaded || !d.mfma || !d.ks || d.pad_rows || N != 32 || d.lds_N != 32 || !(w8 || w4)) return 0;
+#ifndef GS_EXPERIMENTS
+    // the release build instantiates the grouped kernel for 16-byte u16-position groups on 8
+    // waves only: any other layout runs as single launches (which refuse it themselves)
+    if (d.ks_p8 || !w8) return 0;
+#endif
     return (d.ks_nt << 18) | (w4 ? 1u << 17 : 0u) | (d.ks_p8 ? 1u << 16 : 0u) | (d.maxr << 8) | d.seg_cap;  // NT, waves, P8, RT, MAXG
 }
 

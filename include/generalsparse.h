@@ -67,6 +67,8 @@ typedef struct {
     char device_kernel[32];       /* the device kernel gs_spmm launches at the plan's N (first sub-matrix) */
     int index_formulas;           /* index arrays the kernel evaluates as formulas (MODEL_DRIVEN_COMPRESS) */
     uint64_t index_bytes_saved;   /* u32 index bytes per replica those formulas keep out of HBM */
+    uint32_t ks_nt;               /* k_mfma_ks: A's groups by non-temporal loads (KS_NT) */
+    uint32_t ks_head_groups;      /* k_mfma_ks: groups per head step (KS_HEAD; 0: every step by record) */
 } gs_plan_info;
 
 const char *gs_last_error(void);
@@ -76,7 +78,7 @@ void gs_opts_default(gs_opts *o);
 
 /* Both readers refuse (GS_ERR -1, gs_last_error names the cause) a matrix without entries
  * (struct.cc:258), rows out of order (struct.cc:120-131), a .mtx index that is not a decimal
- * >= 1, and any index past 2^32; the dims grow to the largest index + 1.  row / col / val hold
+ * >= 1, and any index past 2^32 - 2 (dims at most 2^32 - 1); the dims grow to the largest index + 1.  row / col / val hold
  * nnz entries each (val may be NULL: every value 1). */
 int gs_plan_create_from_mtx(const char *path, int ones_values, gs_plan_t **out);
 int gs_plan_create_from_coo(uint64_t n_rows, uint64_t n_cols, uint64_t nnz, const uint64_t *row,
@@ -132,7 +134,9 @@ int gs_spmm_batch(gs_plan_t *const *plans, const int *replicas, const void *cons
  * the entries each launch carries in entries_per_launch[0 .. min(count, cap)) (a grouped
  * k_mfma_ks_group launch carries up to 32) */
 int gs_batch_launches(gs_plan_t *const *plans, const int *replicas, int n, int N, int *entries_per_launch, int cap);
-/* synchronises `stream` and reads the plan's device error words (every replica, every
+/* synchronises the device (every stream: launches of the plan on side streams must have
+ * ended before the words are read and cleared; `stream` is kept for the signature) and reads
+ * the plan's device error words (every replica, every
  * sub-matrix kernel): GS_ERR_DEVICE when a launch reported a fault since the last call --
  * a K-split combine that gave up waiting for a partial slab (its rows of C are NaN) --
  * 0 otherwise.  The words are cleared once reported.  The reference asserts on the host

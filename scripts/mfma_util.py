@@ -9,10 +9,15 @@ MI355X_MICROARCH.md DVFS item), SQ_WAVE_CYCLES / SQ_BUSY_CYCLES (context).
   mfma_util_grbm = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)
 i.e. the fraction of the kernel's busy cycles, per SIMD, in which its matrix pipe was busy.
 GRBM_GUI_ACTIVE over-counts on dispatches shorter than ~0.3 ms (MI355X_MICROARCH.md, DVFS
-give-back: the implied clock reads 2.6-3.7 GHz here), so the figure reported first is the
-pessimistic one, against the peak clock over the kernel's own duration:
-  mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel ns x 2.4 GHz)
-and the GRBM-based ratio beside it (mfma_util_grbm).  The busy counter is checked against the
+give-back: GRBM_GUI_ACTIVE / 8 / duration reads 2.6-3.8 GHz on these ~13-70 us dispatches, above
+the 2.4 GHz the chip can run), so every figure divides by the PMC pass's own
+dispatch duration (Start / End timestamps of the counter-collection record, not the duration of
+another run) and a clock that is at most the 2.4 GHz peak:
+  clock_ghz_est  = min(2.4, GRBM_GUI_ACTIVE / 8 / dispatch ns)   (the raw quotient is kept as
+                   clock_ghz_grbm_raw)
+  mfma_util      = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x dispatch ns x 2.4 GHz)      (vs peak)
+  mfma_util_at_clock_est = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x dispatch ns x clock_ghz_est)
+Both equal when GRBM reads high (clock_ghz_est = 2.4).  The busy counter is checked against the
 analytic instruction count (n_mfma x cycles per MFMA) when that is given."""
 import csv
 import glob
@@ -25,6 +30,7 @@ from collections import defaultdict
 
 SIMDS = 1024  # 256 CUs x 4 SIMDs
 XCDS = 8
+PEAK_GHZ = 2.4  # MI355X peak engine clock
 
 
 def main():
@@ -45,14 +51,19 @@ def main():
     keys = list(per)
     med = {c: statistics.median(per[k][c] for k in keys) for c in per[keys[0]]}
     active = med["GRBM_GUI_ACTIVE"] / XCDS
+    ns = statistics.median(dur.values())  # the PMC pass's own dispatch durations
+    raw = active / ns
+    clk = min(PEAK_GHZ, raw)
     label = re.match(r"k_[a-z0-9_]+", kern).group(0) if re.match(r"k_[a-z0-9_]+", kern) else kern
+    busy = med["SQ_VALU_MFMA_BUSY_CYCLES"]
     out = {"workload": wl, "kernel": label, "filter": kern, "plan": plan, "dispatches": len(keys), "counters_median": med,
-           "kernel_ns_median": statistics.median(dur.values()),
-           "clock_ghz_est": round(active / statistics.median(dur.values()), 3),
-           "mfma_util": round(med["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * statistics.median(dur.values()) * 2.4), 4),
-           "formula": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel ns x 2.4 GHz)",
-           "mfma_util_grbm": round(med["SQ_VALU_MFMA_BUSY_CYCLES"] / (active * SIMDS), 4),
-           "formula_grbm": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)"}
+           "kernel_ns_median": ns, "kernel_ns_source": "this PMC pass's dispatch timestamps",
+           "clock_ghz_grbm_raw": round(raw, 3), "clock_ghz_est": round(clk, 3),
+           "mfma_util": round(busy / (SIMDS * ns * PEAK_GHZ), 4),
+           "formula": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x dispatch ns x 2.4 GHz)",
+           "mfma_util_at_clock_est": round(busy / (SIMDS * ns * clk), 4),
+           "formula_at_clock_est": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x dispatch ns x min(2.4, GRBM_GUI_ACTIVE/8/ns))"}
+    assert out["clock_ghz_est"] <= PEAK_GHZ
     if n_mfma and cyc:
         out["analytic"] = {"mfma_per_dispatch": n_mfma, "cycles_per_mfma": cyc,
                            "busy_cycles": n_mfma * cyc,

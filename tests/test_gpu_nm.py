@@ -29,7 +29,9 @@ def spmm(plan, B):
     return C.float().cpu().numpy()
 
 
-def check(C, ref, tol=1e-1):
+def check(C, ref, tol=2.0 ** -9):
+    """k_nm_mfma / k_row_chunks accumulate in fp32 and round to fp16 once: the tight fp16 line
+    (tests/tolerance.py) inside the contract's 1e-1"""
     err = np.abs(C - ref) / np.maximum(1.0, np.abs(ref))
     assert err.max() <= tol, f"max rel err {err.max()} > {tol}"
 

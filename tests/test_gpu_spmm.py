@@ -28,7 +28,7 @@ PIPES = [("thread_total", 4, 1), ("thread_total", 8, 1), ("warp_total", 0, 1), (
          ("balanced_block_total", 512, 1), ("balanced_thread_total", 64, 1),
          ("tblock_thread_total", 16, 1), ("tblock_thread_total", 20, 3), ("tblock_warp_thread_total", 16, 2)]
 BALANCED = ("balanced_warp_total", "balanced_block_total", "balanced_thread_total")
-TOL = {"f32": 1e-3, "f16": 1e-1}
+from tolerance import TOL, bound  # noqa: E402  (contract line + the tight fp16 line, tests/tolerance.py)
 
 
 def run(M, K, row, col, val, pipeline, p0, p1, N, dtype, B=None, seed=0):
@@ -42,9 +42,13 @@ def run(M, K, row, col, val, pipeline, p0, p1, N, dtype, B=None, seed=0):
     return plan, C.float().cpu().numpy(), B
 
 
-def check(C, ref, dtype):
+def check(C, ref, dtype, plan=None):
+    """the contract tolerance, and 2^-9 for the fp16 results of fp32-accumulating kernels
+    (every kernel but the bitmap family's fp16 atomics, tests/tolerance.py)"""
+    kernel = plan.info()["device_kernel"] if plan is not None else None
     err = np.abs(C - ref) / np.maximum(1.0, np.abs(ref))
-    assert err.max() <= TOL[dtype], f"max rel err {err.max()} > {TOL[dtype]}"
+    b = bound(dtype, kernel)
+    assert err.max() <= b, f"max rel err {err.max()} > {b} ({kernel})"
 
 
 def coo_cases():
@@ -69,7 +73,7 @@ def test_spmm_matches_oracle(pipe, N, dtype):
         plan, C, B = run(M, K, row, col, val, name, p0, p1, N, dtype)
         v = val.astype(np.float16).astype(np.float32) if dtype == "f16" else val
         ref = ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64")
-        check(C, ref, dtype)
+        check(C, ref, dtype, plan)
 
 
 @pytest.mark.parametrize("dtype", ["f32", "f16"])
@@ -107,7 +111,7 @@ def test_block_rows_short_and_long_rows(pipe, N, dtype):
     plan, C, B = run(M, K, row, col, val, name, p0, p1, N, dtype)
     assert plan.info()["device_kernel"] == "k_block_rows"
     v = val.astype(np.float16).astype(np.float32) if dtype == "f16" else val
-    check(C, ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64"), dtype)
+    check(C, ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64"), dtype, plan)
 
 
 # col-direction pipelines (K5 warp_bit_map / K7 tblock_bit_map): BMTs are 64-nnz
@@ -142,10 +146,10 @@ def test_col_direction_matches_oracle(pipe, N, dtype):
         assert plan.info()["lds_stage"] == (3 if nm else 0), (case, plan.info())
         v = val.astype(np.float16).astype(np.float32) if dtype == "f16" else val
         ref = ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64")
-        check(C, ref, dtype)
+        check(C, ref, dtype, plan)
         # the workspace is re-zeroed by the finalize pass: a second launch agrees
         C2 = plan.spmm(torch.from_numpy(B).to(DEV)).float().cpu().numpy()
-        check(C2, ref, dtype)
+        check(C2, ref, dtype, plan)
 
 
 @pytest.mark.parametrize("dtype", ["f32", "f16"])
@@ -234,7 +238,7 @@ def test_c2_full_size_against_torch():
         C = plan.spmm(B).float()
         torch.cuda.synchronize()
         err = ((C - ref).abs() / ref.abs().clamp(min=1.0)).max().item()
-        assert err <= 1e-1, (name, err)
+        assert err <= bound("f16", plan.info()["device_kernel"]), (name, plan.info()["device_kernel"], err)
         # linearity: A(2B) = 2 AB.  Deterministic families (no atomics) are exact;
         # the bitmap family adds open row partials into fp16 C with atomics, as the
         # reference's warp_segment kernel does: each add rounds to fp16 (ulp 2^-5 at
@@ -300,13 +304,13 @@ def test_lds_stage_matches_oracle(pipe, dtype, N, no_mfma):
         assert info["lds_stage"] == 1 and info["lds_n"] == N, (case, info)
         v = val.astype(np.float16).astype(np.float32) if dtype == "f16" else val
         ref = ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64")
-        check(C, ref, dtype)
+        check(C, ref, dtype, plan)
         # a different dense width than the plan's falls back to the gather kernel
         N2 = N + 1
         B2 = np.random.default_rng(1).uniform(-1, 1, (K, N2)).astype(B.dtype)
         C2 = plan.spmm(torch.from_numpy(B2).to(DEV)).float().cpu().numpy()
         ref2 = ofi.spmm_ref(M, N2, row, col, v, B2.astype(np.float32), "f64")
-        check(C2, ref2, dtype)
+        check(C2, ref2, dtype, plan)
         plan.free()
 
 
@@ -692,7 +696,7 @@ def test_mfma_ks_known_answer_and_c2():
     assert info["device_kernel"] == "k_mfma_ks" and info["ksplit"] == 4, info
     C = plan.spmm(B).float()
     err = ((C - ref).abs() / ref.abs().clamp(min=1.0)).max().item()
-    assert err <= 1e-1, err
+    assert err <= bound("f16", info["device_kernel"]), err
     assert torch.equal(plan.spmm(B * 2).float(), 2 * C)  # linearity, deterministic
 
 
@@ -713,7 +717,7 @@ def test_c2_driver_plan_block_total_40_against_torch():
     assert info["device_kernel"] == "k_mfma_ks" and info["ksplit"] == 2, info
     C = plan.spmm(B).float()
     err = ((C - ref).abs() / ref.abs().clamp(min=1.0)).max().item()
-    assert err <= 1e-1, err
+    assert err <= bound("f16", info["device_kernel"]), err
     C2 = torch.full((M, N), float("nan"), device=DEV, dtype=torch.float16)
     plan.spmm(B, C=C2)
     assert torch.equal(C2.float(), C)
@@ -774,7 +778,20 @@ def test_mfma_unsorted_columns_and_duplicates(kernel, mfma_everywhere):
     plan, C, B = run(M, K, r2, c2, v2, "block_total", 20 if kernel == "k_mfma_rows" else 48, 1, N, "f16")
     assert plan.info()["device_kernel"] == kernel
     ref = ofi.spmm_ref(M, N, r2, c2, v2.astype(np.float16).astype(np.float32), B.astype(np.float32), "f64")
-    check(C, ref, "f16")
+    # contract line against the entries as given: a repeated coordinate is rounded to fp16
+    # once as its sum (the layout's value), not once per entry, so the tight line does not
+    # hold against this reference (~2^-11 of each combined value)
+    err = np.abs(C - ref) / np.maximum(1.0, np.abs(ref))
+    assert err.max() <= TOL["f16"], err.max()
+    # tight line against the canonical matrix the layout holds: duplicates summed in double,
+    # rounded to fp32, then to fp16 (device_layout.cc canonical_rows)
+    key = r2.astype(np.int64) * K + c2.astype(np.int64)
+    uk, inv = np.unique(key, return_inverse=True)
+    vs = np.zeros(len(uk), np.float64)
+    np.add.at(vs, inv, v2.astype(np.float64))
+    rc, cc = (uk // K).astype(np.uint64), (uk % K).astype(np.uint64)
+    vc = vs.astype(np.float32).astype(np.float16).astype(np.float32)
+    check(C, ofi.spmm_ref(M, N, rc, cc, vc, B.astype(np.float32), "f64"), "f16", plan)
 
 
 def test_mfma_non_finite_B_deviation(mfma_everywhere):
@@ -904,7 +921,7 @@ def test_merge_path_matches_oracle(ws, level, N, dtype, merge_walk):
         assert plan.info()["device_kernel"] == merge_walk
         v = val.astype(np.float16).astype(np.float32) if dtype == "f16" else val
         ref = ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64")
-        check(C, ref, dtype)
+        check(C, ref, dtype, plan)
 
 
 @pytest.mark.parametrize("variant", [{}, {"MP_PERM_SCATTER": 1}, {"MP_PERM_HOT": 300}])
@@ -1169,7 +1186,7 @@ def test_warp_rows_chunks_per_pass(p0, p1, chunks, dtype):
             plan, C, B = run(M, K, row, col, val, "tblock_warp_total", p0, p1, 8, dtype)
             v32 = val.astype(np.float16).astype(np.float32) if dtype == "f16" else val.astype(np.float32)
             ref = ofi.spmm_ref(M, 8, row, col, v32, B.astype(np.float32), "f64")
-            check(C, ref, dtype)
+            check(C, ref, dtype, plan)
             plan.free()
     finally:
         gsa.set_config("WARP_ROWS_CHUNKS", old)
