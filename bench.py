@@ -130,33 +130,8 @@ WORKLOADS = {
 WORKLOADS["c2"]["dtype"] = "f16"
 
 
-# (pipeline, p0, p1).  tblock_warp_total(rows per BMTB, rows per BMW) runs the
-# LDS-stationary-B kernel when its BMTBs fit one workgroup; the others are the
-# reference's token_test plans on the gather kernels.
-# A 4th element holds config overrides set while the candidate is built and uploaded: KS_NT = the
-# k_mfma_ks groups by non-temporal loads (C2 -4%, profiles/r05l_nt.txt).
-CANDIDATES = [("block_total", 20, 1), ("block_total", 10, 1), ("block_total", 40, 1), ("block_total", 80, 1),
-              ("block_total", 40, 1, {"KS_NT": 1}), ("block_total", 80, 1, {"KS_NT": 1}),
-              ("tblock_warp_total", 20, 2), ("tblock_warp_total", 4, 1), ("warp_segment", 4, 1),
-              ("thread_total", 4, 1)]
-
-
-# C3: the col-direction plan (32-nnz BMTs = 64-column k-steps of a 2:4 row)
-# (NM_NT: A's panel blocks by non-temporal loads, on by default: C3 72.0 -> 66.9 us, profiles/r05l_nt.txt)
-CANDIDATES_C3 = [("col_direction_nm", 32, 1), ("col_direction_nm", 32, 1, {"NM_NT": 0})]
-
-# C1: token_test's default (thread_total, sparse_cf 4) and the row-block / merge-path plans
-# (tblock_warp_total(64, 16): 16-row BMWs, two per wave pass of k_warp_rows_mc, 16.2 us against
-# 17.8 for (32, 8), profiles/r05ae_c1_plans.txt)
-CANDIDATES_C1 = [("thread_total", 4, 1), ("tblock_warp_total", 4, 1), ("tblock_warp_total", 32, 8),
-                 ("tblock_warp_total", 32, 16), ("tblock_warp_total", 64, 16), ("merge_path", 512, 1)]
-
-# C4: merge-path levels (WARP, work_size p0) and the balanced / row-per-thread plans
-CANDIDATES_C4 = [("merge_path", 256, 1), ("merge_path", 512, 1), ("merge_path", 1024, 1), ("balanced_block_total", 2048, 1),
-                 ("thread_total", 4, 1)]
-# com-Orkut stand-in (234M nonzeros): the merge-path levels only (each plan of it is ~2 GB on the
-# device and minutes of host work; the balanced / row-per-thread plans are 4x-30x slower on C4)
-CANDIDATES_C4O = [("merge_path", 512, 1), ("merge_path", 1024, 1), ("merge_path", 2048, 1)]  # (2048: -1.5%, r05ai)
+# The plan candidates of every workload live in generalsparse_amd/autotune.py (CANDIDATES,
+# WORKLOAD_CLASS, shape_candidates): the product's search and this bench search the same space.
 
 
 def kernel_label(info):
@@ -561,7 +536,8 @@ def layer_traffic(N, sp, plans_by_shape):
 
 
 def cand_key(c):
-    return "%s(%d,%d)%s" % (c[0], c[1], c[2], "".join(f" {a}={b}" for a, b in (c[3] if len(c) > 3 else {}).items()))
+    from generalsparse_amd.autotune import cand_key as ck
+    return ck(c)
 
 
 def headline_layer(args, torch, gsa, ds, rank, local, dev, choice, steps, warmup, per_shape=None, rs_per_shape=None,
@@ -772,19 +748,10 @@ def event_ms(plan, Bs, Cs, reps, torch, warm=20, rotate=True):
 def build_plan(gsa, M, K, row, col, val, cand, N, dt, local, rotation_mb, e, tdt, dev, torch):
     """a candidate's plan with its replicas and B / C buffers; cand = (pipeline, p0, p1[, config
     overrides held while the plan is compiled and uploaded])"""
-    name, p0, p1 = cand[:3]
-    over = cand[3] if len(cand) > 3 else {}
-    old = {k: gsa.get_config(k) for k in over}
-    try:
-        for k, v in over.items():
-            gsa.set_config(k, v)
-        t0 = time.perf_counter()
-        plan = gsa.Plan.from_coo(M, K, row, col, val).run_pipeline(name, N, p0, p1).compile()
-        t_plan = time.perf_counter() - t0
-        plan.upload(dt, local)
-    finally:
-        for k, v in old.items():
-            gsa.set_config(k, v)
+    from generalsparse_amd.autotune import build_candidate
+    t0 = time.perf_counter()
+    plan = build_candidate(M, K, row, col, val, cand, N, dt, local)
+    t_plan = time.perf_counter() - t0  # transforms + compile + upload
     info = plan.info()
     reps = replicas_for(info, K, N, e, rotation_mb)
     for _ in range(reps - 1):
@@ -841,6 +808,7 @@ def main():
         if dist is not None:
             dist.destroy_process_group()
         return
+    from generalsparse_amd import autotune as at
     M, K, N = args.M, args.K, args.N
     wl = WORKLOADS[args.workload]
     dt = wl["dtype"]
@@ -851,15 +819,15 @@ def main():
         row, col, val = ds.random_rows(M, K, 1790490 / 47894, 18)
         nnz = len(row)
         alg_bytes = algorithmic_bytes(M, K, N, nnz, e, s_idx)
-        cand_list = CANDIDATES_C1
+        cand_list = at.CANDIDATES[at.WORKLOAD_CLASS["c1"]]
     elif args.workload in ("c4", "c4o"):
         one = args.shard != "batch"
         if args.workload == "c4o":  # 234M nonzeros: drawn on the GPU (numpy takes minutes)
             row, col, val = ds.rmat_torch(M, wl["nnz"], wl["seed"] + (0 if one else rank), dev, symmetric=True)
-            cand_list = CANDIDATES_C4O
+            cand_list = at.CANDIDATES[at.WORKLOAD_CLASS["c4o"]]
         else:
             row, col, val = ds.rmat(M, wl["nnz"], wl["seed"] + (0 if one else rank), symmetric=wl["symmetric"])
-            cand_list = CANDIDATES_C4
+            cand_list = at.CANDIDATES[at.WORKLOAD_CLASS["c4"]]
         nnz = len(row)
         alg_bytes = algorithmic_bytes(M, K, N, nnz, e, s_idx)
         if one:  # one matrix over the ranks: this rank's rows / nonzeros
@@ -871,12 +839,12 @@ def main():
         row, col, val = ds.two_four(M, K, 30 + rank)
         nnz = len(row)
         alg_bytes = algorithmic_bytes_24(M, K, N, nnz, e)
-        cand_list = CANDIDATES_C3
+        cand_list = at.CANDIDATES[at.WORKLOAD_CLASS["c3"]]
     else:
         row, col, val = ds.pruned_weight(M, K, args.sparsity, shard_seed(rank))
         nnz = len(row)
         alg_bytes = algorithmic_bytes(M, K, N, nnz, e, s_idx)
-        cand_list = CANDIDATES
+        cand_list = at.CANDIDATES[at.WORKLOAD_CLASS["c2"]]
     flops = 2.0 * nnz * N
 
     cands = cand_list if args.pipeline == "auto" else [c for c in cand_list if c[0] == args.pipeline] or \

@@ -33,7 +33,8 @@ class GsPlanInfo(ctypes.Structure):
                 ("lds_bytes", ctypes.c_uint64), ("tile_bytes", ctypes.c_uint64), ("ksplit", ctypes.c_uint32),
                 ("n_kernels", ctypes.c_int), ("device_kernel", ctypes.c_char * 32),
                 ("index_formulas", ctypes.c_int), ("index_bytes_saved", ctypes.c_uint64),
-                ("ks_nt", ctypes.c_uint32), ("ks_head_groups", ctypes.c_uint32)]
+                ("ks_nt", ctypes.c_uint32), ("ks_head_groups", ctypes.c_uint32),
+                ("nm_tiles", ctypes.c_uint32)]
 
 
 # every symbol include/generalsparse.h declares, with its ctypes signature

@@ -67,32 +67,17 @@ def shape_pipeline(shape):
     return ("tblock_warp_total", row_block_rows(C5_SHAPES[shape][0]), 2)
 
 
-# per-shape plan candidates for the matrix-core kernels (bench.py searches them for the
-# headline layer): (pipeline, p0, p1, config overrides applied while the plan is uploaded).
-# KS_MIN_ROWS 1000 keeps a block on k_mfma_rows; 56-row blocks of 7168-row shapes are 128
-# row blocks x 2 K ranges on k_mfma_ks; 112-row blocks are exactly 256 workgroups on every
-# OPT-30B shape (7168 rows: 64 blocks x 4 K ranges; fc1: 256 blocks x 1)
 def shape_candidates(shape):
-    from .autotune import row_block_rows
-    rb = row_block_rows(C5_SHAPES[shape][0])
-    return [("tblock_warp_total", rb, 2, {"KS_MIN_ROWS": 1000}), ("block_total", 56, 1, {}),
-            ("block_total", 40, 1, {}), ("block_total", 80, 1, {}), ("block_total", 112, 1, {})]
+    """per-shape plan candidates for the matrix-core kernels (bench.py searches them for the
+    headline layer): autotune.shape_candidates of the shape's row count"""
+    from .autotune import shape_candidates as sc
+    return sc(C5_SHAPES[shape][0])
 
 
 def build_plan(gsa, m, n, row, col, val, N, cand, local):
-    """a shape's plan from a candidate (pipeline, p0, p1[, config overrides])"""
-    name, p0, p1 = cand[:3]
-    over = cand[3] if len(cand) > 3 else {}
-    old = {k: gsa.get_config(k) for k in over}
-    for k, v in over.items():
-        gsa.set_config(k, v)
-    try:
-        plan = gsa.Plan.from_coo(m, n, row, col, val).run_pipeline(name, N, p0, p1).compile()
-        plan.upload("f16", local)
-    finally:
-        for k, v in old.items():
-            gsa.set_config(k, v)
-    return plan
+    """a shape's plan from a candidate (pipeline, p0, p1[, config overrides]): autotune.build_candidate"""
+    from .autotune import build_candidate
+    return build_candidate(m, n, row, col, val, cand, N, "f16", local)
 
 
 def build_rank_batch(seq, rank, N, gsa, ds, torch, dev, local, pipeline=None, keep_coo=False,

@@ -107,6 +107,10 @@ GSK_HD constexpr size_t bm_lds_bytes(uint32_t CT, uint32_t RT, uint32_t W) {
 // k_nm_mfma: 8 waves, 4,608-B blocks per (64 rows, 64-column k-step), B chunks of 256 rows
 constexpr int kNmWaves = 8;
 constexpr uint32_t kNmBlockBytes = 4608, kNmKC = 256;
+// bytes per (workgroup of T 16-row tiles, 64-column k-step): two wave sets of ceil(T/2) and T/2
+// tiles, each 512 B of positions + 1 KB of values per tile (T = 8: two 4,608-B blocks).  Set rh's
+// blocks of all k-steps are contiguous: set 0 at w * S * this, set 1 after set 0's S blocks.
+GSK_HD constexpr uint32_t nm_wg_block_bytes(uint32_t T) { return 1024u + 1024u * T; }
 // k_nm_mfma4: two B chunk buffers, or the four q = 1 wave tiles of the k-phase sum (+ ticket)
 GSK_HD constexpr size_t nm4_lds_bytes(uint32_t CT) {
     const size_t bufs = (size_t)2 * kNmKC * 32u * CT, red = (size_t)4 * 4 * CT * 64 * 16 + 16;

@@ -2918,12 +2918,18 @@ typedef _Float16 h16v __attribute__((ext_vector_type(16)));
 // fragment reads of odd n-tiles skipped (half the LDS reads; wrong results)
 // NG: the dense width in HBM (B and C row length); NG = 8 runs one 16-column tile whose
 // columns 8..15 are zeros in LDS and never stored (N = 8, the half-used tile of C3's N sweep)
-template <int CT, int DBG = 0, int NG = 16 * CT, bool NT = false>
+// TT: 16-row tiles per workgroup (nm_tiles; kernel_consts.hpp nm_wg_block_bytes): the wave set rh
+// = 0 takes the first G0 = ceil(TT/2) tiles, rh = 1 the other G1 = TT/2 (TT = 8: two 64-row groups,
+// the original layout).  TT = 7 spreads C3's 1,792 tiles over exactly 256 workgroups (one per
+// CU) where TT = 8 leaves 32 CUs idle; the guards `rt < G` fold away for the tiles both sets hold.
+template <int CT, int DBG = 0, int NG = 16 * CT, bool NT = false, int TT = 8>
 __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *__restrict__ A,
                                                            const f16 *__restrict__ B, f16 *__restrict__ C,
                                                            uint32_t K, uint32_t S, uint32_t rows,
                                                            uint32_t row_base, uint32_t krot = 0) {
     static_assert(NG == 16 * CT || (CT == 1 && NG == 8), "NG: 16*CT, or 8 in one half-used tile");
+    static_assert(TT >= 2 && TT <= 8, "2..8 tiles per workgroup");
+    constexpr uint32_t G0 = (TT + 1) / 2, G1 = TT / 2;
     constexpr uint32_t N = NG, RB = 32 * CT, UB = 2 * CT;
     constexpr uint32_t RBG = 2 * NG, UBG = RBG / 16;  // B row bytes / 16-B units in HBM
     constexpr uint32_t szB = kNmKC * RB;
@@ -2935,13 +2941,15 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t rh = wv >> 2, q = wv & 3u;
-    const uint32_t rg = blockIdx.x * 2u + rh;
+    const uint32_t G = rh ? G1 : G0;                             // this wave set's tiles
+    const uint32_t r0 = blockIdx.x * 16u * TT + rh * 16u * G0;   // its first row
+    const uint32_t BB = 512u + 1024u * G;                        // its block bytes per k-step
     const uint32_t nch = S / 4u;
     // chunk order (krot, as in k_mfma_rows): iteration c works on chunk jr(c), every
     // workgroup starting at its own chunk so they do not all pull the same B rows at once
     const uint32_t rot = krot ? blockIdx.x % nch : 0u;
     auto jr = [&](uint32_t c) -> uint32_t { const uint32_t x = c + rot; return x >= nch ? x - nch : x; };
-    const unsigned char *arow = A + (size_t)rg * S * kNmBlockBytes;
+    const unsigned char *arow = A + (size_t)blockIdx.x * S * nm_wg_block_bytes(TT) + (size_t)rh * S * (512u + 1024u * G0);
     const unsigned char *bbase = reinterpret_cast<const unsigned char *>(B);
     const uint32_t bk = tid / UB, boff = bk * RBG + (tid % UB) * 16u;  // this thread's first unit
     const bool bun = tid % UB < UBG;  // the unit exists in HBM (NG = 8: the tile's upper half is zeros)
@@ -2956,10 +2964,10 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
 #define GS_NM_ALOAD(c, V, I)                                                                        \
     if (DBG != 2 || (uint32_t)(c) < 2u) {                                                         \
         const uint32_t cc_ = jr(min((uint32_t)(c), nch - 1u));                                    \
-        const unsigned char *blk_ = arow + (size_t)(4u * cc_ + q) * kNmBlockBytes;                \
+        const unsigned char *blk_ = arow + (size_t)(4u * cc_ + q) * BB;                           \
         const u32x2 i_ = ld_once_if<NT>(reinterpret_cast<const u32x2 *>(blk_ + lane * 8u));      \
         I = make_uint2(i_[0], i_[1]);                                                             \
-        _Pragma("unroll") for (int rt = 0; rt < 4; rt++) V[rt] =                                  \
+        _Pragma("unroll") for (int rt = 0; rt < 4; rt++) if ((uint32_t)rt < G) V[rt] =            \
             ld_once_if<NT>(reinterpret_cast<const u32x4 *>(blk_ + 512u + rt * 1024u + lane * 16u)); \
     }
     u32x4 bs[NBU];
@@ -3012,7 +3020,9 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
         __builtin_memcpy(&BF, t_, 32);                                                            \
     }
     // B fragments double-buffered in registers: the reads of n-tile ct+1 are in
-    // flight while the four smfmac of n-tile ct run
+    // flight while the four smfmac of n-tile ct run.  A wave set with G < 4 tiles runs the
+    // smfmac of its missing tiles on whatever their (never loaded) registers hold: no branch
+    // splits the issue-ordered region, and those accumulators are never stored
 #define GS_NM_COMPUTE(c, V, I)                                                                      \
     {                                                                                             \
         const unsigned char *lb_ = lds + ((uint32_t)(c) & 1u) * szB;                              \
@@ -3133,8 +3143,9 @@ __global__ __launch_bounds__(64 * kNmWaves) void k_nm_mfma(const unsigned char *
                 const f4v v = acc[rt][ct] + red[rh * TW + (rt * CT + ct) * 64 + lane];
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    const uint32_t r = rg * 64u + rt * 16u + 4u * (lane >> 4) + i;
-                    if (r < rows && ct * 16u + (lane & 15u) < N) C[(size_t)(row_base + r) * N + ct * 16u + (lane & 15u)] = (f16)v[i];
+                    const uint32_t r = r0 + rt * 16u + 4u * (lane >> 4) + i;
+                    if ((uint32_t)rt < G && r < rows && ct * 16u + (lane & 15u) < N)
+                        C[(size_t)(row_base + r) * N + ct * 16u + (lane & 15u)] = (f16)v[i];
                 }
             }
         }

@@ -911,6 +911,7 @@ int gs_plan_info_get(gs_plan_t *p, gs_plan_info *info) {
             info->index_bytes_saved = s.dev.index_bytes_saved;
             info->ks_nt = s.dev.ks ? s.dev.ks_nt : 0;
             info->ks_head_groups = s.dev.ks ? s.dev.ks_gh : 0;
+            info->nm_tiles = s.dev.nm ? s.dev.nm_tiles : 0;
         }
     });
 }

@@ -350,12 +350,14 @@ std::string matrix_core_source(const meta_data_set &m, const mc_layout &L, int r
     } else {
         o << "    unsigned char *d_blk = up(rdb<unsigned char>(\"THREAD_META_nm_panels_0.bin\"));\n";
         // N = 8: one half-used 16-column tile (k_nm_mfma's NG)
+        // TT: 16-row tiles per workgroup (the layout's nm_T)
         const std::string k = "gsk::k_nm_mfma<" + std::to_string(CT) + ", 0, " + std::to_string(N == 8 ? 8 : 16 * CT) +
-                              (L.nm_nt ? ", true>" : ">");
+                              (L.nm_nt ? ", true, " : ", false, ") + std::to_string(L.nm_T) + ">";
         const size_t lds = (size_t)2 * gsk::kNmKC * 32 * CT;
         setup = "hipFuncSetAttribute((const void *)" + k + ", hipFuncAttributeMaxDynamicSharedMemorySize, " +
                 std::to_string(lds) + ")";
-        launch = k + "<<<" + std::to_string((L.nm_rows + 127) / 128) + ", " + std::to_string(64 * gsk::kNmWaves) + ", " +
+        launch = k + "<<<" + std::to_string((L.nm_rows + 16 * L.nm_T - 1) / (16 * L.nm_T)) + ", " +
+                 std::to_string(64 * gsk::kNmWaves) + ", " +
                  std::to_string(lds) + ">>>(d_blk, d_B, d_C, (uint32_t)K, " + std::to_string(L.nm_S) + "u, " +
                  std::to_string(L.nm_rows) + "u, 0u, " + std::to_string((uint32_t)get_config().NM_KROT) + "u)";
     }

@@ -585,18 +585,27 @@ bool build_bm_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
 // plan, value 0) are summed.  Returns false (and why) when a group holds more
 // than two distinct columns or the panels would store over twice the entries
 // (beyond 4M value slots).
+// T = 16-row tiles per k_nm_mfma workgroup (nm_tiles): its two wave sets hold G0 = ceil(T/2)
+// and G1 = T/2 tiles; per (workgroup w, set rh, k-step s) one block of 512 B of positions +
+// G_rh KB of values at w * S * nm_wg_block_bytes(T) + rh * S * (512 + 1024 G0) + s * (512 + 1024
+// G_rh).  T = 8 is the 64-row-group layout (group g = 2w + rh at g * S * 4608), rounded to whole
+// 256-row blocks as k_nm_mfma_ks / k_nm_mfma4 read it.
 bool build_nm_panels(const std::vector<uint64_t> &rows, const std::vector<uint64_t> &col, const universal_array &vals,
-                     uint64_t row_num, uint64_t K, std::vector<unsigned char> &blk, uint32_t &S, std::string &why) {
+                     uint64_t row_num, uint64_t K, std::vector<unsigned char> &blk, uint32_t &S, std::string &why,
+                     uint32_t T) {
     const uint64_t nnz = col.size();
     if (row_num == 0 || K == 0 || nnz == 0) { why = "empty sub-matrix"; return false; }
+    if (T < 2 || T > 8) { why = "2..8 tiles per workgroup"; return false; }
     const uint64_t S64 = (K + gsk::kNmKC - 1) / gsk::kNmKC * 4;  // k-steps, whole 256-column chunks
-    const uint64_t ng = (row_num + 255) / 256 * 4;               // 64-row groups, whole 256-row workgroups
-    const double slots = (double)ng * 64.0 * (double)S64 * 32.0;
+    const uint64_t rows_wg = 16ull * T;
+    const uint64_t nwg = T == 8 ? (row_num + 255) / 256 * 2 : (row_num + rows_wg - 1) / rows_wg;
+    const uint64_t G0 = (T + 1) / 2, WB = gsk::nm_wg_block_bytes(T);
+    const double slots = (double)nwg * (double)rows_wg * (double)S64 * 32.0;
     if (slots > 2.0 * (double)nnz && slots > (double)(1 << 22)) {  // small plans always qualify
         why = "2:4 panels would store over twice the entries";
         return false;
     }
-    if (S64 > 0xffffffffull || ng * S64 * gsk::kNmBlockBytes > (1ull << 40)) { why = "too large"; return false; }
+    if (S64 > 0xffffffffull || nwg * S64 * WB > (1ull << 40)) { why = "too large"; return false; }
     std::vector<uint64_t> rp(row_num + 1, 0);
     for (uint64_t r : rows) {
         if (r >= row_num) { why = "row index beyond row count"; return false; }
@@ -605,11 +614,17 @@ bool build_nm_panels(const std::vector<uint64_t> &rows, const std::vector<uint64
     for (uint64_t i = 0; i < row_num; i++) rp[i + 1] += rp[i];
     std::vector<uint64_t> cur(rp.begin(), rp.end() - 1), ord(nnz);
     for (uint64_t e = 0; e < nnz; e++) ord[cur[rows[e]]++] = e;
-    blk.assign(ng * S64 * gsk::kNmBlockBytes, 0);
-    for (uint64_t b = 0; b < ng * S64; b++) {  // default positions (0, 1) in every group
-        uint16_t *ix = reinterpret_cast<uint16_t *>(blk.data() + b * gsk::kNmBlockBytes);
-        for (int i = 0; i < 256; i++) ix[i] = 0x4444;
-    }
+    // block of (workgroup w, set rh, k-step s)
+    auto block = [&](uint64_t w, uint64_t rh, uint64_t s) {
+        return blk.data() + w * S64 * WB + rh * S64 * (512 + 1024 * G0) + s * (512 + 1024 * (rh ? T / 2 : G0));
+    };
+    blk.assign(nwg * S64 * WB, 0);
+    for (uint64_t w = 0; w < nwg; w++)  // default positions (0, 1) in every group
+        for (uint64_t rh = 0; rh < 2; rh++)
+            for (uint64_t s = 0; s < S64; s++) {
+                uint16_t *ix = reinterpret_cast<uint16_t *>(block(w, rh, s));
+                for (int i = 0; i < 256; i++) ix[i] = 0x4444;
+            }
     const uint64_t Kp = S64 * 64;
     std::vector<float> dv(Kp, 0.f);
     std::vector<uint8_t> has(Kp, 0);
@@ -621,7 +636,8 @@ bool build_nm_panels(const std::vector<uint64_t> &rows, const std::vector<uint64
             has[c] = 1;
             dv[c] += (float)vals.read_float_from_arr(ord[e]);
         }
-        const uint64_t rg = r / 64, rt = (r % 64) / 16, rr = r % 16;
+        const uint64_t w = r / rows_wg, within = r % rows_wg, rh = within >= 16 * G0 ? 1 : 0;
+        const uint64_t rt = (within - rh * 16 * G0) / 16, rr = r % 16;
         for (uint64_t gi = 0; gi < Kp / 4; gi++) {
             int pos[2], n = 0;
             for (int p = 0; p < 4; p++)
@@ -636,7 +652,7 @@ bool build_nm_panels(const std::vector<uint64_t> &rows, const std::vector<uint64
             if (n == 1) pos[1] = pos[0] == 3 ? 2 : 3;  // zero partner at another position
             const int lo = std::min(pos[0], pos[1]), hi = std::max(pos[0], pos[1]);
             const uint64_t s = gi / 16, j = gi % 16, g = j / 4, sg = j % 4, lane = g * 16 + rr;
-            unsigned char *b = blk.data() + (rg * S64 + s) * gsk::kNmBlockBytes;
+            unsigned char *b = block(w, rh, s);
             uint16_t *v = reinterpret_cast<uint16_t *>(b + 512 + rt * 1024 + lane * 16) + sg * 2;
             v[0] = has[4 * gi + lo] ? f32_to_f16_bits(dv[4 * gi + lo]) : 0;
             v[1] = has[4 * gi + hi] ? f32_to_f16_bits(dv[4 * gi + hi]) : 0;
@@ -652,6 +668,29 @@ bool build_nm_panels(const std::vector<uint64_t> &rows, const std::vector<uint64
     return true;
 }
 
+uint32_t nm_tiles_for(uint64_t row_num, int64_t cfg_tiles, uint32_t N) {
+    if (cfg_tiles > 0) {
+        GS_CHECK(cfg_tiles == 2 || cfg_tiles == 4 || cfg_tiles == 7 || cfg_tiles == 8, "NM_TILES: 2, 4, 7 or 8");
+        return (uint32_t)cfg_tiles;
+    }
+    const uint64_t tiles = (row_num + 15) / 16;
+    uint32_t best = 8;
+    uint64_t best_load = ~0ull;
+    for (uint32_t T : {8u, 7u, 4u, 2u}) {
+        // N = 128: B (1.8 MB per workgroup at K = 7168) is two thirds of a CU's intake, and 256
+        // workgroups of 7 tiles ran 2% slower than 224 of 8 (profiles/r06c_ab_c3.txt); at N <= 64
+        // the 7-tile grid is 2-4% faster
+        if (T == 7 && N >= 128) continue;
+        const uint64_t wgs = T == 8 ? (row_num + 255) / 256 * 2 : (tiles + T - 1) / T;
+        const uint64_t load = (wgs + 255) / 256 * T;  // tiles per CU, one workgroup per CU at a time
+        if (load < best_load) {
+            best_load = load;
+            best = T;
+        }
+    }
+    return best;
+}
+
 mc_layout choose_matrix_core_layout(const meta_data_set &m, const kernel_spec &sp, int sb, uint64_t K, int dtype) {
     mc_layout L;
     const config_t cfg = get_config();
@@ -664,7 +703,10 @@ mc_layout choose_matrix_core_layout(const meta_data_set &m, const kernel_spec &s
         // col-direction BMTs that are 2:4 panels: sparse matrix cores, self-contained blocks
         const auto &col = m.u(GLOBAL_META, "nz_col_indices", sb);
         auto vals = m.get_element(GLOBAL_META, "nz_vals", sb)->meta_data_arr;
-        if (build_nm_panels(rows, col, *vals, row_num, K, L.nm_blk, L.nm_S, L.why)) {
+        // the experiments-build 256-row kernels read the T = 8 layout only
+        const bool v256 = cfg.NM_KS != 0 || cfg.NM_V4 != 0;
+        L.nm_T = v256 ? 8u : nm_tiles_for(row_num, cfg.NM_TILES, L.N);
+        if (build_nm_panels(rows, col, *vals, row_num, K, L.nm_blk, L.nm_S, L.why, L.nm_T)) {
             L.kind = mc_layout::NM;
             L.nm_rows = row_num;
             // k_nm_mfma_ks (NM_KS): 256-row workgroups, K split so they cover the CUs

@@ -106,7 +106,12 @@ bool build_bm_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
 
 // k_nm_mfma upload layout: one 4,608-B block per (64-row group, 64-column k-step)
 bool build_nm_panels(const std::vector<uint64_t> &rows, const std::vector<uint64_t> &col, const universal_array &vals,
-                     uint64_t row_num, uint64_t K, std::vector<unsigned char> &blk, uint32_t &S, std::string &why);
+                     uint64_t row_num, uint64_t K, std::vector<unsigned char> &blk, uint32_t &S, std::string &why,
+                     uint32_t T = 8);
+// k_nm_mfma's 16-row tiles per workgroup for a row count (NM_TILES = 0): among T = 8, 7, 4, 2
+// (7 only below N = 128) the fewest tiles per CU (ceil(workgroups / 256 CUs) x T), ties to the
+// larger T
+uint32_t nm_tiles_for(uint64_t row_num, int64_t cfg_tiles, uint32_t N);
 
 // The matrix-core layout gs_spmm runs for a compiled plan at its dense width
 // (DENSE_MATRIX_SIZE), chosen and built once here for both the device upload and the
@@ -126,6 +131,7 @@ struct mc_layout {
     bm_tiles bm;
     std::vector<unsigned char> nm_blk;  // k_nm_mfma blocks
     uint32_t nm_S = 0;                  // ... k-steps per row group
+    uint32_t nm_T = 8;                  // ... 16-row tiles per workgroup (nm_tiles_for)
     uint64_t nm_rows = 0;
     bool nm_ks = false;                    // k_nm_mfma_ks (256-row workgroups, K split) instead of k_nm_mfma
     bool nm4 = false;                      // k_nm_mfma4 (256-row workgroups of 8 waves, K split, B by LDS-DMA)

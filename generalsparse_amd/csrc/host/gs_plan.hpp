@@ -46,6 +46,7 @@ struct device_plan {
     uint32_t ks_gh = 0;       // k_mfma_ks: groups per head step (ks_tiles::GH; 0: every step by record)
     uint32_t ks_nt = 0;       // k_mfma_ks: non-temporal loads of A's groups (NTL bit 0; ks_tiles::NT, KS_NT)
     bool nm_nt = false;       // k_nm_mfma: non-temporal panel loads (NM_NT)
+    uint32_t nm_tiles = 8;    // k_nm_mfma: 16-row tiles per workgroup (mc_layout::nm_T)
     uint64_t err_at = 0;      // K-split combine: index of the device error word in t2 (0: none)
     uint64_t nnz_stored = 0;  // padded nnz on device
     size_t bytes_A = 0;       // device bytes of A per replica (metadata + cols + vals)

@@ -317,6 +317,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
         d.kernel = mc.nm_ks ? "k_nm_mfma_ks" : (mc.nm4 ? "k_nm_mfma4" : "k_nm_mfma");
         d.nm4 = mc.nm4;
         d.nm_nt = mc.nm_nt;
+        d.nm_tiles = mc.nm_T;
         d.KC = mc.nm_S;
         d.n_rows_aux = mc.nm_rows;
         d.n_units = m.u(THREAD_META, "first_nz_indices", sb).size() - 1;

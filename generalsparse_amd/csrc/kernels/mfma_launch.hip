@@ -144,20 +144,21 @@ void debug_mfma_timeline(const plan_state &, const void *, void *, uint32_t, hip
 
 namespace {
 
-template <int CT, int NG = 16 * CT>
-void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, void *C, hipStream_t s) {
+template <int CT, int NG, int TT>
+void launch_nm_ctt(const plan_state &p, const device_arrays &a, const void *B, void *C, hipStream_t s) {
     const device_plan &d = p.dev;
 #ifdef GS_EXPERIMENTS
     // GS_NM_DEBUG=1/2: diagnostic builds without the loop's B / A loads (wrong results)
     static const int dbg = getenv("GS_NM_DEBUG") ? atoi(getenv("GS_NM_DEBUG")) : 0;
-    auto kern = dbg == 1 ? gsk::k_nm_mfma<CT, 1, NG>
-                         : (dbg == 2 ? gsk::k_nm_mfma<CT, 2, NG> : (dbg == 4 ? gsk::k_nm_mfma<CT, 4, NG> : gsk::k_nm_mfma<CT, 0, NG>));
-    if (dbg == 8) kern = gsk::k_nm_mfma<CT, 8, NG>;
-    if (d.nm_nt && dbg == 0) kern = gsk::k_nm_mfma<CT, 0, NG, true>;
+    auto kern = dbg == 1 ? gsk::k_nm_mfma<CT, 1, NG, false, TT>
+                         : (dbg == 2 ? gsk::k_nm_mfma<CT, 2, NG, false, TT>
+                                     : (dbg == 4 ? gsk::k_nm_mfma<CT, 4, NG, false, TT> : gsk::k_nm_mfma<CT, 0, NG, false, TT>));
+    if (dbg == 8) kern = gsk::k_nm_mfma<CT, 8, NG, false, TT>;
+    if (d.nm_nt && dbg == 0) kern = gsk::k_nm_mfma<CT, 0, NG, true, TT>;
 #else
     constexpr int dbg = 0;
     // NM_NT (fixed at upload): A's panel blocks by non-temporal loads
-    auto kern = d.nm_nt ? gsk::k_nm_mfma<CT, 0, NG, true> : gsk::k_nm_mfma<CT, 0, NG>;
+    auto kern = d.nm_nt ? gsk::k_nm_mfma<CT, 0, NG, true, TT> : gsk::k_nm_mfma<CT, 0, NG, false, TT>;
 #endif
     const size_t lds = (size_t)2 * gsk::kNmKC * 32 * CT + (dbg == 4 ? 4096 : 0);
     static std::mutex mu;
@@ -173,6 +174,7 @@ void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, vo
     }
 #ifdef GS_EXPERIMENTS
     if (d.nm_ks) {
+        GS_CHECK(d.nm_tiles == 8, "k_nm_mfma_ks reads the 64-row-group layout");
         auto kk = gsk::k_nm_mfma_ks<CT>;
         const size_t lds2 = (size_t)2 * gsk::kNmKC * 32 * CT;
         static std::mutex mu2;
@@ -196,7 +198,7 @@ void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, vo
 #else
     GS_CHECK(!d.nm_ks, "k_nm_mfma_ks is an experiments-build kernel");
 #endif
-    const uint32_t wg = (uint32_t)((d.n_rows_aux + 127) / 128);
+    const uint32_t wg = (uint32_t)((d.n_rows_aux + 16 * TT - 1) / (16 * TT));
     hipLaunchKernelGGL(kern, dim3(wg), dim3(64 * gsk::kNmWaves), lds, s, (const unsigned char *)a.tcol,
                        (const gsk::f16 *)B, (gsk::f16 *)C, (uint32_t)p.K, d.KC, (uint32_t)d.n_rows_aux,
                        (uint32_t)d.row_base, (uint32_t)get_config().NM_KROT);
@@ -235,6 +237,17 @@ void launch_nm4(const plan_state &p, const device_arrays &a, const void *B, void
 }
 
 #endif
+
+template <int CT, int NG = 16 * CT>
+void launch_nm_ct(const plan_state &p, const device_arrays &a, const void *B, void *C, hipStream_t s) {
+    switch (p.dev.nm_tiles) {  // 16-row tiles per workgroup (device_layout.cc nm_tiles_for)
+        case 8: launch_nm_ctt<CT, NG, 8>(p, a, B, C, s); break;
+        case 7: launch_nm_ctt<CT, NG, 7>(p, a, B, C, s); break;
+        case 4: launch_nm_ctt<CT, NG, 4>(p, a, B, C, s); break;
+        case 2: launch_nm_ctt<CT, NG, 2>(p, a, B, C, s); break;
+        default: throw gs_error("k_nm_mfma: tiles per workgroup outside 2, 4, 7, 8");
+    }
+}
 
 void launch_nm(const plan_state &p, const device_arrays &a, const void *B, void *C, uint32_t N, hipStream_t s) {
     if (p.dev.nm4) {

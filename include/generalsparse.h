@@ -69,6 +69,7 @@ typedef struct {
     uint64_t index_bytes_saved;   /* u32 index bytes per replica those formulas keep out of HBM */
     uint32_t ks_nt;               /* k_mfma_ks: A's groups by non-temporal loads (KS_NT) */
     uint32_t ks_head_groups;      /* k_mfma_ks: groups per head step (KS_HEAD; 0: every step by record) */
+    uint32_t nm_tiles;            /* k_nm_mfma: 16-row tiles per workgroup (NM_TILES / the upload's rule) */
 } gs_plan_info;
 
 const char *gs_last_error(void);

@@ -152,7 +152,9 @@ def test_c3_integer_known_answer(N):
     row, col, _ = ds.two_four(M, K, 3)
     val = int_values(len(row), 9)
     plan = build(M, K, row, col, val, "col_direction_nm", 32, 1, N)
-    assert plan.info()["device_kernel"] == "k_nm_mfma", plan.info()
+    info = plan.info()
+    # 1,792 sixteen-row tiles: 256 workgroups of 7 (one per CU) below N = 128, 224 of 8 at N = 128
+    assert info["device_kernel"] == "k_nm_mfma" and info["nm_tiles"] == (8 if N == 128 else 7), info
     B = int_B(K, N, 4)
     ref = exact_fp16(M, K, row, col, val, B)
     C = plan.spmm(B)

@@ -250,3 +250,26 @@ def test_nm_nontemporal_loads_bit_identical(shape, N):
     assert np.array_equal(out[0], out[1])
     ref = ofi.spmm_ref(M, N, r, c, v.astype(np.float16).astype(np.float32), B.astype(np.float32), "f64")
     check(out[1], ref)
+
+
+@pytest.mark.parametrize("tiles", [2, 4, 7, 8])
+@pytest.mark.parametrize("N", [8, 32, 128])
+@pytest.mark.parametrize("shape", [(1000, 768), (112 * 3, 512), (1792, 1024), (17, 4096)], ids=lambda s: f"{s[0]}x{s[1]}")
+def test_nm_tiles_per_workgroup(shape, N, tiles):
+    """k_nm_mfma with 2 / 4 / 7 / 8 sixteen-row tiles per workgroup (NM_TILES; the wave sets
+    hold ceil(T/2) and T/2 tiles, the layout one block per set and k-step): row counts that
+    end inside a tile, inside a wave set and inside a workgroup, against the oracle"""
+    M, K = shape
+    r, c, v = thinned(M, K, 40 + M, keep=0.9, empty_rows=(0, M - 1))
+    gsa.set_config("NM_TILES", tiles)
+    try:
+        plan = plan_for(M, K, r, c, v, N)
+    finally:
+        gsa.set_config("NM_TILES", 0)
+    assert plan.info()["device_kernel"] == "k_nm_mfma", plan.info()
+    B = np.random.default_rng(M + N).uniform(-1, 1, (K, N)).astype(np.float16)
+    ref = ofi.spmm_ref(M, N, r, c, v.astype(np.float16).astype(np.float32), B.astype(np.float32), "f64")
+    assert plan.info()["nm_tiles"] == tiles
+    C = spmm(plan, B)
+    check(C, ref)
+

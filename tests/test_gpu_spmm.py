@@ -1004,6 +1004,29 @@ def test_autotune_picks_a_timed_variant(tmp_path):
     check(C.float().cpu().numpy(), ofi.spmm_ref(M, 8, r, c, v, B, "f64"), "f32")
 
 
+def test_autotune_on_c2_finds_the_measured_plan():
+    """the product's search (autotune's default candidates, the same table
+    bench.py searches) on C2 returns the plan the C2 line measures: k_mfma_ks with 2 K ranges
+    (block_total(40,1), with or without KS_NT), and that plan is parity-green"""
+    from generalsparse_amd.autotune import autotune
+    M = K = 5120
+    N = 32
+    r, c, v = ds.pruned_weight(M, K, 0.7, 13)
+    plan, res = autotune(M, K, r, c, v, N, "f16", reps=50, rotation_mb=640)
+    info = plan.info()
+    best = min((t, k) for k, t in res.items() if isinstance(t, float))
+    assert info["device_kernel"] == "k_mfma_ks" and info["ksplit"] == 2, (info, res)
+    assert best[1].startswith("block_total(40,1)"), res
+    B = torch.randn((K, N), device=DEV, dtype=torch.float16)
+    A = torch.zeros((M, K), dtype=torch.float32)
+    A[torch.from_numpy(r.astype(np.int64)), torch.from_numpy(c.astype(np.int64))] = torch.from_numpy(v).half().float()
+    ref = A.to(DEV) @ B.float()
+    C = plan.spmm(B).float()
+    err = ((C - ref).abs() / ref.abs().clamp(min=1.0)).max().item()
+    assert err <= bound("f16", info["device_kernel"]), err
+    plan.free()
+
+
 # §8f rank 3: one kernel per sub-matrix of a row division, run in sequence by gs_spmm
 SUB_MIXES = [
     ("merge_path", 64, 1, "thread_total", 4, 1),

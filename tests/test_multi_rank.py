@@ -243,3 +243,21 @@ def test_row_block_rows_fill_whole_cu_rounds():
         rounds = math.ceil(math.ceil(M / r) / 256)
         assert rounds == max(1, math.ceil(M / (256 * 64)))
         assert r == 1 or math.ceil(math.ceil(M / (r - 1)) / 256) > rounds
+
+
+def test_bench_searches_the_product_plan_space():
+    """bench.py keeps no candidate table of its own; every workload searches
+    autotune.CANDIDATES through WORKLOAD_CLASS, and the C5 shapes autotune.shape_candidates"""
+    import os
+    from generalsparse_amd import autotune as at
+    from generalsparse_amd import batch as bt
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")).read()
+    assert "CANDIDATES = [" not in src and "CANDIDATES_C" not in src
+    for wl in ("c1", "c2", "c3", "c4", "c4o"):
+        assert f'at.WORKLOAD_CLASS["{wl}"]' in src
+        assert at.CANDIDATES[at.WORKLOAD_CLASS[wl]]
+    assert ("block_total", 40, 1, {"KS_NT": 1}) in at.CANDIDATES["f16"]
+    assert bt.shape_candidates("fc1") == at.shape_candidates(28672)
+    assert at.candidates_for(5120, 5120, 7864320, "f16")[:len(at.CANDIDATES["f16"])] == at.CANDIDATES["f16"]
+    assert at.candidates_for(28672, 7168, 1, "f16", two_four=True) == at.CANDIDATES["f16_2to4"]
+    assert at.candidates_for(1, 1, 234_000_000, "f32", powerlaw=True) == at.CANDIDATES["f32_powerlaw_large"]

@@ -350,7 +350,7 @@ def test_binary_plan_file_round_trip(tmp_path, name, N, p0, p1):
 @pytest.mark.parametrize("nt", [0, 1])
 def test_generate_program_carries_nontemporal_variants(tmp_path, nt):
     """KS_NT / NM_NT reach the emitted program: it launches the same k_mfma_ks / k_nm_mfma
-    instantiation gs_spmm does (the 9th / 4th template argument)"""
+    instantiation gs_spmm does (the 9th / 4th template argument; k_nm_mfma's 5th: tiles per workgroup)"""
     old = {k: gsa.get_config(k) for k in ("HALF", "KS_NT", "NM_NT")}
     try:
         gsa.set_config("HALF", 1)
@@ -365,7 +365,8 @@ def test_generate_program_carries_nontemporal_variants(tmp_path, nt):
         r, c, v = ds.two_four(256, 512, 41)
         p = gsa.Plan.from_coo(256, 512, r, c, v).run_pipeline("col_direction_nm", 32, 32, 1).compile()
         src = open(os.path.join(p.generate_program(tmp_path / "nm", repeat=10), "kernel_file.hip")).read()
-        assert ("gsk::k_nm_mfma<2, 0, 32%s>" % (", true" if nt else "")) in src, src[:2000]
+        # 16 tiles: 8 workgroups of 2 tiles (the upload's nm_tiles_for rule, TT = last argument)
+        assert ("gsk::k_nm_mfma<2, 0, 32, %s, 2>" % ("true" if nt else "false")) in src, src[:2000]
     finally:
         for k, val in old.items():
             gsa.set_config(k, val)
