@@ -1010,6 +1010,10 @@ __device__ __forceinline__ void static_for(F &&f) {
     }
 }
 
+typedef float f4v __attribute__((ext_vector_type(4)));
+// K split (ksp > 1, LDS_KSPLIT): workgroup u = g * ksp + q walks the chunks [q * ncs, +ncs) of
+// BMTB g only, publishes its rows' fp32 partials and the last of the ksp workgroups sums them in q
+// order (deterministic) -- for plans with too few BMTBs to fill the CUs (upload rule).
 template <class VT, int CF, int MAXR, int MAXU>
 __global__ __launch_bounds__(1024) void k_lds_rows(
     const uint32_t *__restrict__ bmtb_first_row,  // n_bmtb+1
@@ -1019,13 +1023,16 @@ __global__ __launch_bounds__(1024) void k_lds_rows(
     const uint32_t *__restrict__ seg_row_off,     // n_bmtb*nc*(rpw_max+1): row starts inside (g, j)
     const uint16_t *__restrict__ tcol, const VT *__restrict__ tval, const VT *__restrict__ B, VT *__restrict__ C,
     uint32_t K, uint32_t N, uint32_t X, uint32_t KC, uint32_t nc, uint32_t RSB, uint32_t rpw_max, uint32_t seg_cap,
-    uint32_t row_base) {
+    uint32_t row_base, uint32_t ksp = 1, uint32_t ncs = 0, float *__restrict__ slabs = nullptr,
+    uint32_t *__restrict__ arrivals = nullptr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     typedef typename raw_vec<CF * sizeof(VT)>::t RB;
     const uint32_t tid = threadIdx.x, nthr = blockDim.x;
     const uint32_t lane = tid & 63u, wib = tid >> 6;
     const uint32_t xl = lane & (X - 1u), slot = lane / X, S = 64u / X;
-    const uint32_t g = blockIdx.x;
+    // K split (LDS_KSPLIT): workgroup u = g * ksp + q walks chunks [q * ncs, +ncs) of BMTB g
+    const uint32_t g = ksp > 1u ? blockIdx.x / ksp : blockIdx.x, q = ksp > 1u ? blockIdx.x % ksp : 0u;
+    const uint32_t j0 = q * (ksp > 1u ? ncs : 0u), j1 = ksp > 1u ? min(nc, j0 + ncs) : nc;
     const uint32_t r_first = bmtb_first_row[g];
     const uint32_t bmw = bmw_of_bmtb[g] + wib;
     uint32_t t0 = 0, nt = 0;
@@ -1044,7 +1051,7 @@ __global__ __launch_bounds__(1024) void k_lds_rows(
 
     u32x4 stage[MAXU];  // native vectors (HIP's uint4 is a union struct that defeats SROA)
     uint32_t stage_r;
-    uint32_t s_lo = seg_start[g * nc], s_hi = seg_start[g * nc + 1];
+    uint32_t s_lo = seg_start[g * nc + j0], s_hi = seg_start[g * nc + j0 + 1];
 
     float acc[MAXR][CF];
 #pragma unroll
@@ -1077,8 +1084,8 @@ __global__ __launch_bounds__(1024) void k_lds_rows(
         stage_r = seg_row_off[(size_t)(g * nc + (j)) * (rpw_max + 1) + ridx];                          \
     }
 
-    GS_STAGE_LOAD(0u, s_lo, s_hi);
-    for (uint32_t j = 0; j < nc; j++) {
+    GS_STAGE_LOAD(j0, s_lo, s_hi);
+    for (uint32_t j = j0; j < j1; j++) {
         // registers -> LDS (B rows at RSB stride, A segment contiguous)
         {
             const uint32_t UBt = min(KC, K - j * KC) * UB;
@@ -1094,7 +1101,7 @@ __global__ __launch_bounds__(1024) void k_lds_rows(
         }
         __syncthreads();
         const uint32_t len = s_hi - s_lo;
-        if (j + 1 < nc) {  // in flight during this chunk's compute
+        if (j + 1 < j1) {  // in flight during this chunk's compute
             const uint32_t n_lo = s_hi, n_hi = seg_start[g * nc + j + 2];
             GS_STAGE_LOAD(j + 1, n_lo, n_hi);
             s_lo = n_lo;
@@ -1144,10 +1151,58 @@ __global__ __launch_bounds__(1024) void k_lds_rows(
     }
 #undef GS_STAGE_LOAD
 #pragma unroll
+    for (int t = 0; t < MAXR; t++)
+        if ((uint32_t)t < nt) wave_reduce_slots<CF>(acc[t], (int)X);
+    if (ksp <= 1u) {
+#pragma unroll
+        for (int t = 0; t < MAXR; t++)
+            if ((uint32_t)t < nt && slot == 0) store_f32<VT, CF>(C + (size_t)(r_first + t0 + t + row_base) * N + c0, acc[t]);
+        return;
+    }
+    // K-split hand-off (k_mfma_ks's drain form, MI355X_MICROARCH.md §Correctness boundaries: sc1
+    // stores, every storing wave's vmcnt(0), a barrier, one agent-scope arrival add; the last
+    // adder loads the other slabs with sc1 loads): slab (g, q) holds the BMTB's rows x N fp32
+    // partials of K range q; the last of the S workgroups sums them in q order (its own from
+    // registers: the same bits it stored), so C is the same whichever workgroup arrives last
+    const size_t slab_rows = (size_t)rpw_max;
+    if (slot == 0) {
+#pragma unroll
+        for (int t = 0; t < MAXR; t++) {
+            if ((uint32_t)t < nt) {
+                float *dst = slabs + (((size_t)g * ksp + q) * slab_rows + t0 + t) * N + c0;
+#pragma unroll
+                for (int k = 0; k < CF; k += 4) {
+                    const f4v v = {acc[t][k], acc[t][k + 1], acc[t][k + 2], acc[t][k + 3]};
+                    __asm__ volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst + k), "v"(v) : "memory");
+                }
+            }
+        }
+    }
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    uint32_t *flag = lRp;  // the row offsets are no longer read
+    if (tid == 0) *flag = __hip_atomic_fetch_add(arrivals + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*flag != ksp - 1u) return;
+    if (tid == 0) __hip_atomic_store(arrivals + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (slot != 0) return;
+#pragma unroll
     for (int t = 0; t < MAXR; t++) {
         if ((uint32_t)t < nt) {
-            wave_reduce_slots<CF>(acc[t], (int)X);
-            if (slot == 0) store_f32<VT, CF>(C + (size_t)(r_first + t0 + t + row_base) * N + c0, acc[t]);
+            float sum[CF];
+#pragma unroll
+            for (int k = 0; k < CF; k++) sum[k] = 0.f;
+            for (uint32_t qq = 0; qq < ksp; qq++) {
+                if (qq == q) {
+#pragma unroll
+                    for (int k = 0; k < CF; k++) sum[k] += acc[t][k];
+                    continue;
+                }
+                const float *src = slabs + (((size_t)g * ksp + qq) * slab_rows + t0 + t) * N + c0;
+#pragma unroll
+                for (int k = 0; k < CF; k++) sum[k] += __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            store_f32<VT, CF>(C + (size_t)(r_first + t0 + t + row_base) * N + c0, sum);
         }
     }
 }

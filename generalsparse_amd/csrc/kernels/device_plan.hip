@@ -534,6 +534,18 @@ void upload_plan(plan_state &p, int dtype, int device) {
                                     t, why)) {
                     d.lds = true;
                     d.kernel = "k_lds_rows";
+                    // LDS_KSPLIT: S workgroups per BMTB, each over ncs consecutive chunks of K
+                    // (every K range non-empty), fp32 slabs + one arrival counter per BMTB.  0 (auto):
+                    // plans of under 128 BMTBs split K until ~256 workgroups (a workgroup's time
+                    // is its nonzeros: C2 fp32 (20,2) 41.5 us = (40,4) in 2 K ranges 44.5 us,
+                    // profiles/r06f_lds_ksplit.txt, so full grids gain nothing from a split)
+                    const uint64_t nbt0 = m.u(TBLOCK_META, "first_row_indices", sb).size() - 1;
+                    const int64_t cfg_ks = get_config().LDS_KSPLIT;
+                    const uint32_t want = cfg_ks > 0 ? (uint32_t)cfg_ks
+                                                     : (nbt0 < 128 ? (uint32_t)std::max<uint64_t>(1, 256 / std::max<uint64_t>(nbt0, 1)) : 1u);
+                    const uint32_t ncs = (t.nc + std::min(want, t.nc) - 1) / std::min(want, t.nc);
+                    d.ksplit = (t.nc + ncs - 1) / ncs;
+                    d.ncs = ncs;
                     d.lds_N = Nd;
                     d.KC = t.KC; d.nc = t.nc; d.RSB = t.RSB; d.rpw_max = t.rpw_max; d.seg_cap = t.seg_cap;
                     d.waves = t.waves; d.maxr = t.maxr; d.lds_bytes = t.lds_bytes;
@@ -554,6 +566,11 @@ void upload_plan(plan_state &p, int dtype, int device) {
                         a.tval = dev_copy(d, v, kPad);
                     }
                     d.bytes_tile = d.bytes_A - before;
+                    if (d.ksplit > 1) {
+                        const uint64_t nbt = m.u(TBLOCK_META, "first_row_indices", sb).size() - 1;
+                        a.ws = dev_copy(d, std::vector<float>((size_t)nbt * d.ksplit * t.rpw_max * Nd, 0.f));
+                        a.t3 = dev_copy(d, std::vector<uint32_t>((size_t)nbt, 0u));
+                    }
                 }
             }
             upload_groups(!d.lds);

@@ -47,11 +47,13 @@ void launch_lds(const plan_state &p, const device_arrays &a, const VT *B, VT *C,
     const device_plan &d = p.dev;
     const uint32_t X = N * (uint32_t)sizeof(VT) / 16u;
     const uint32_t nb = (uint32_t)d.n_rows_aux;
-    const dim3 grid(nb), block(64 * d.waves);
+    const uint32_t ksp = d.ksplit > 1 ? d.ksplit : 1u;
+    GS_CHECK(ksp == 1 || (a.ws && a.t3 && d.ncs > 0 && (ksp - 1) * d.ncs < d.nc), "k_lds_rows: K ranges disagree with the upload");
+    const dim3 grid(nb * ksp), block(64 * d.waves);
     const uint32_t K = (uint32_t)p.K;
 #define GS_LDS_ARGS                                                                                              \
     a.t0, a.a1, a.a0, a.t1, a.t2, (const uint16_t *)a.tcol, (const VT *)a.tval, B, C, K, N, X, d.KC, d.nc, d.RSB, \
-        d.rpw_max, d.seg_cap, (uint32_t)d.row_base
+        d.rpw_max, d.seg_cap, (uint32_t)d.row_base, ksp, d.ncs, a.ws, a.t3
     auto go = [&](auto kern) {
         // dynamic LDS above 64 KB must be opted into, once per kernel and device
         static std::mutex mu;

@@ -25,6 +25,11 @@ elif WL == "c4":
     N = 8
     row, col, val = ds.rmat(M, 3105536, 1, symmetric=False)
     dt, tdt = "f32", torch.float32
+elif WL == "pw":  # any pruned-weight shape: M, K, SP (sparsity), DT (f16 / f32)
+    M, K, N = int(os.environ["M"]), int(os.environ["K"]), 32
+    row, col, val = ds.pruned_weight(M, K, float(os.environ.get("SP", "0.7")), 13)
+    dt = os.environ.get("DT", "f16")
+    tdt = torch.float16 if dt == "f16" else torch.float32
 else:
     M = K = 5120
     N = 32
@@ -53,13 +58,14 @@ R = max(r for _, _, r in plans)
 Bs = [torch.randn((K, N), device="cuda", dtype=tdt) for _ in range(R)]
 Cs = [torch.empty((M, N), device="cuda", dtype=tdt) for _ in range(R)]
 ref = None
-same = []
+same, rel = [], []
 for v, p, r in plans:
     C = p.spmm(Bs[0])
     torch.cuda.synchronize()
     if ref is None:
         ref = C.clone()
     same.append(bool(torch.equal(C, ref)))
+    rel.append(((C.float() - ref.float()).abs() / ref.float().abs().clamp(min=1.0)).max().item())
 res = [[] for _ in plans]
 for rnd in range(ROUNDS):
     for i, (v, p, r) in enumerate(plans):
@@ -75,5 +81,5 @@ for rnd in range(ROUNDS):
 for i, (v, p, r) in enumerate(plans):
     info = p.info()
     print(json.dumps({"variant": v, "kernel": info["device_kernel"], "us": [round(t, 2) for t in res[i]],
-                      "median_us": round(sorted(res[i])[len(res[i]) // 2], 2), "bit_identical_to_first": same[i],
+                      "median_us": round(sorted(res[i])[len(res[i]) // 2], 2), "bit_identical_to_first": same[i], "max_rel_diff_to_first": rel[i],
                       "replicas": r, "nm_tiles": info.get("nm_tiles"), "ksplit": info.get("ksplit")}))

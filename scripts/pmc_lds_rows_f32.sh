@@ -1,0 +1,4 @@
+cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; OUT=gpurun_out/r06g; mkdir -p $OUT
+timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS --output-format csv -d $OUT/lds -o p -- python3 scripts/prof_one.py tblock_warp_total 20 2 f32 32 50 > $OUT/lds.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $OUT/wait -o p -- python3 scripts/prof_one.py tblock_warp_total 20 2 f32 32 50 > $OUT/wait.log 2>&1 || exit 1
+echo done

@@ -315,6 +315,36 @@ def test_lds_stage_matches_oracle(pipe, dtype, N, no_mfma):
 
 
 @pytest.mark.parametrize("dtype", ["f32", "f16"])
+@pytest.mark.parametrize("ksplit", [0, 2, 3])
+def test_lds_stage_k_split(dtype, ksplit, no_mfma):
+    """k_lds_rows with its BMTBs' K split over workgroups (LDS_KSPLIT; 0 = the upload's rule:
+    plans of under 128 BMTBs split until ~256 workgroups): the fp32 slab combine against the
+    oracle, a relaunch into a NaN-filled C bit for bit (the arrival counters re-arm), and the
+    unsplit plan within the tolerance"""
+    M, K = 600, 30000
+    row, col, val = ds.random_rows(M, K, 400.0, seed=21, empty_frac=0.05)
+    N = 32
+    gsa.set_config("LDS_KSPLIT", ksplit)
+    try:
+        plan, C, B = run(M, K, row, col, val, "tblock_warp_total", 20, 2, N, dtype)
+    finally:
+        gsa.set_config("LDS_KSPLIT", 0)
+    info = plan.info()
+    assert info["device_kernel"] == "k_lds_rows" and info["ksplit"] > 1, info
+    if ksplit:
+        assert info["ksplit"] == ksplit, info
+    v = val.astype(np.float16).astype(np.float32) if dtype == "f16" else val
+    check(C, ofi.spmm_ref(M, N, row, col, v, B.astype(np.float32), "f64"), dtype, plan)
+    Bt = torch.from_numpy(B).to(DEV)
+    C2 = torch.full((M, N), float("nan"), device=DEV, dtype=Bt.dtype)
+    plan.spmm(Bt, C=C2)
+    plan.spmm(Bt, C=C2)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(C2.float().cpu().numpy(), C)
+    plan.free()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f16"])
 def test_lds_stage_known_answer(dtype, no_mfma):
     M, K, N = 700, 9000, 32
     row, col, _ = ds.random_rows(M, K, 60.0, seed=8, empty_frac=0.1)
