@@ -33,7 +33,10 @@ CANDIDATES = {
                      ("balanced_block_total", 2048, 1), ("thread_total", 4, 1)],
     # over 50M nonzeros (com-Orkut): merge-path levels only (each plan is ~2 GB on the device and
     # minutes of host work; the balanced / row-per-thread plans are 4x-30x slower on C4)
-    "f32_powerlaw_large": [("merge_path", 512, 1), ("merge_path", 1024, 1), ("merge_path", 2048, 1)],
+    # (MP_COL_PARTS 4: the degree-ranked columns in 4 partitions, one pass each -- fabric reads 6.78x
+    # -> 3.5x the algorithmic bytes at an even time, profiles/r06l_c4o_parts.txt)
+    "f32_powerlaw_large": [("merge_path", 512, 1), ("merge_path", 1024, 1), ("merge_path", 2048, 1),
+                           ("merge_path", 1024, 1, {"MP_COL_PARTS": 4})],
 }
 # the bench workloads (BASELINE.json configs) and the class each searches
 WORKLOAD_CLASS = {"c1": "f32", "c2": "f16", "c3": "f16_2to4", "c4": "f32_powerlaw", "c4o": "f32_powerlaw_large"}

@@ -944,6 +944,20 @@ __global__ __launch_bounds__(256) void k_combine_parts(const VT *const *__restri
     }
 }
 
+// MP_COL_PARTS: C += the fp32 outputs of column partitions 1..n-1, added in partition order
+// (deterministic), C rounded once
+struct mp_part_outs {
+    const float *p[8];
+};
+template <class VT>
+__global__ __launch_bounds__(256) void k_add_parts(VT *__restrict__ C, mp_part_outs parts, uint32_t n, uint64_t total) {
+    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (uint64_t)gridDim.x * 256) {
+        float s = (float)C[e];
+        for (uint32_t q = 0; q < n; q++) s += parts.p[q][e];
+        C[e] = (VT)s;
+    }
+}
+
 template <class VT>
 __global__ __launch_bounds__(256) void k_finalize_rows(const uint32_t *__restrict__ rows, uint32_t n_rows,
                                                        float *__restrict__ ws, VT *__restrict__ C, uint32_t N) {

@@ -25,7 +25,12 @@ struct device_arrays {
     uint32_t *cperm = nullptr;  // merge path, MP_COL_PERM: original column of each renumbered column (or, with
                                 // perm_scatter, the new place of each column)
     void *bperm = nullptr;      // ... B gathered into that order (K x the plan's N, per replica)
+    // merge path, MP_COL_PARTS: kMpPartPtrs device arrays per column partition (mp_part_* below)
+    std::vector<void *> pp;
 };
+// per column partition x: pp[x * kMpPartPtrs + i], i = the mp_part_* index
+enum { MP_PART_COL, MP_PART_VAL, MP_PART_WZ, MP_PART_WQ, MP_PART_ENDS, MP_PART_RID, MP_PART_EMPTY, MP_PART_WS,
+       MP_PART_WS2, MP_PART_T0, MP_PART_CHAIN, MP_PART_CNT, MP_PART_OUT, kMpPartPtrs };
 
 struct device_plan {
     int device = 0;
@@ -47,6 +52,11 @@ struct device_plan {
     uint32_t ks_nt = 0;       // k_mfma_ks: non-temporal loads of A's groups (NTL bit 0; ks_tiles::NT, KS_NT)
     bool nm_nt = false;       // k_nm_mfma: non-temporal panel loads (NM_NT)
     uint32_t nm_tiles = 8;    // k_nm_mfma: 16-row tiles per workgroup (mc_layout::nm_T)
+    // merge path, MP_COL_PARTS: the columns (renumbered by degree, MP_COL_PERM) dealt round-robin
+    // over mp_parts partitions; one k_merge_path per partition, each over its own CSR and wave
+    // ranges, so every pass gathers B rows of one partition only (its hubs fit each XCD's L2)
+    uint32_t mp_parts = 0;
+    std::vector<uint32_t> mp_part_W, mp_part_rows, mp_part_fin;
     uint64_t err_at = 0;      // K-split combine: index of the device error word in t2 (0: none)
     uint64_t nnz_stored = 0;  // padded nnz on device
     size_t bytes_A = 0;       // device bytes of A per replica (metadata + cols + vals)

@@ -209,6 +209,133 @@ bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uin
 
 }  // namespace
 
+// merge-path levels of a compact CSR walked at `work_size` steps of the path (rows consumed +
+// nonzeros consumed): level w at diagonal p = w * work_size has consumed j rows (row i is consumed
+// at path position ends[i] + i + 1) and p - j nonzeros -- the split the reference's merge-path
+// operators produce (get_begin_rows_of_level_after_merge_path.cc), for CSRs the plan never held
+// (the column partitions of MP_COL_PARTS)
+static void merge_path_levels(const std::vector<uint64_t> &rows, uint64_t row_num, uint64_t work_size,
+                              std::vector<uint64_t> &lr, std::vector<uint64_t> &ln) {
+    std::vector<uint64_t> cnt(row_num, 0);
+    for (uint64_t r : rows) cnt[r]++;
+    std::vector<uint64_t> ends, crow;
+    uint64_t acc = 0;
+    for (uint64_t r = 0; r < row_num; r++)
+        if (cnt[r]) {
+            acc += cnt[r];
+            ends.push_back(acc);
+            crow.push_back(r);
+        }
+    lr.clear();
+    ln.clear();
+    uint64_t j = 0;
+    for (uint64_t p = 0;; p += work_size) {
+        while (j < ends.size() && ends[j] + j + 1 <= p) j++;
+        if (j >= ends.size()) break;
+        lr.push_back(crow[j]);
+        ln.push_back(p - j);
+    }
+    ln.push_back(acc);
+}
+
+// MP_COL_PARTS upload: columns ranked by degree (as MP_COL_PERM), rank r in partition r % P at
+// position base[r % P] + r / P of the gathered B (k_permute_rows); per partition its entries in
+// row order (so every row's partial sums its entries in the plan's order), the merge-path wave
+// ranges of that CSR, the in-launch combine state and (partitions >= 1) an fp32 output that
+// k_add_parts adds to C in partition order (deterministic)
+static void upload_col_parts(plan_state &p, device_arrays &a, const std::vector<uint64_t> &col,
+                             const universal_array &vals) {
+    device_plan &d = p.dev;
+    const kernel_spec &sp = p.cg->get_kernel_spec();
+    const meta_data_set &m = *p.meta;
+    const int sb = p.cg->get_sub_matrix_id();
+    const uint32_t P = d.mp_parts;
+    const uint64_t K = p.K, nnz = col.size();
+    const auto &rows = m.u(GLOBAL_META, "nz_row_indices", sb);
+    const uint64_t row_num = row_num_of_sub_matrix(m, sb);
+    std::vector<uint32_t> deg(K, 0u), perm(K), pos(K);
+    for (uint64_t c : col) deg[c]++;
+    for (uint32_t i = 0; i < (uint32_t)K; i++) perm[i] = i;
+    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t x, uint32_t y) { return deg[x] > deg[y]; });
+    std::vector<uint64_t> base(P + 1, 0);
+    for (uint32_t x = 0; x < P; x++) base[x + 1] = base[x] + (K > x ? (K - x + P - 1) / P : 0);
+    std::vector<uint32_t> gather(K);
+    for (uint32_t r = 0; r < (uint32_t)K; r++) {
+        const uint32_t c = perm[r], q = (uint32_t)(base[r % P] + r / P);
+        pos[c] = q;
+        gather[q] = c;
+    }
+    a.cperm = dev_copy(d, gather);
+    const uint32_t Nd = (uint32_t)std::max<int64_t>(1, get_config().DENSE_MATRIX_SIZE);
+    const size_t bb = (size_t)K * Nd * (d.dtype == 0 ? 4u : 2u);
+    HIP_OK(hipMalloc(&a.bperm, std::max<size_t>(bb, 16)));
+    d.allocations.push_back(a.bperm);
+    const uint32_t cfv = d.dtype == 0 ? 4u : 8u, cf = Nd % cfv == 0 ? cfv : 1u;
+    const uint32_t X = std::min<uint32_t>(64u, pow2ceil_u((Nd + cf - 1) / cf));
+    const uint64_t target = (uint64_t)gsk::kMpItems * (64u / X);
+    a.pp.assign((size_t)P * kMpPartPtrs, nullptr);
+    d.mp_part_W.assign(P, 0);
+    d.mp_part_rows.assign(P, 0);
+    d.mp_part_fin.assign(P, 0);
+    std::vector<uint8_t> part(nnz);
+    std::vector<uint64_t> cnt(P, 0);
+    for (uint64_t e = 0; e < nnz; e++) {
+        const uint32_t q = pos[col[e]];
+        uint32_t x = 0;
+        while (q >= base[x + 1]) x++;
+        part[e] = (uint8_t)x;
+        cnt[x]++;
+    }
+    for (uint32_t x = 0; x < P; x++) {
+        std::vector<uint64_t> rx;
+        std::vector<uint32_t> cx;
+        std::vector<float> vx;
+        rx.reserve(cnt[x]);
+        cx.reserve(cnt[x]);
+        vx.reserve(cnt[x]);
+        for (uint64_t e = 0; e < nnz; e++)
+            if (part[e] == x) {
+                rx.push_back(rows[e]);
+                cx.push_back(pos[col[e]]);
+                vx.push_back((float)vals.read_float_from_arr(e));
+            }
+        GS_CHECK(!rx.empty(), "MP_COL_PARTS: a column partition without entries (fewer columns than partitions?)");
+        void **pp = &a.pp[(size_t)x * kMpPartPtrs];
+        if (d.col_bytes == 2) {
+            std::vector<uint16_t> c16(cx.begin(), cx.end());
+            pp[MP_PART_COL] = dev_copy(d, c16, kPad);
+        } else {
+            pp[MP_PART_COL] = dev_copy(d, cx, kPad);
+        }
+        pp[MP_PART_VAL] = dev_copy(d, vx, kPad);
+        std::vector<uint64_t> lr, ln;
+        merge_path_levels(rx, row_num, (uint64_t)sp.work_size, lr, ln);
+        gsk_host::merge_path_layout lay;
+        std::string why;
+        GS_CHECK(gsk_host::merge_path_device_layout(rx, row_num, lr, ln, (uint64_t)sp.work_size, (uint32_t)d.row_base, target,
+                                                     lay, why, d.n_out_rows, 2 * target),
+                 "merge-path layout of column partition " + std::to_string(x) + ": " + why);
+        pp[MP_PART_WZ] = dev_copy(d, lay.wz);
+        pp[MP_PART_WQ] = dev_copy(d, lay.wq);
+        pp[MP_PART_ENDS] = dev_copy(d, lay.ends);
+        pp[MP_PART_RID] = dev_copy(d, lay.rid);
+        pp[MP_PART_EMPTY] = lay.empty.empty() ? nullptr : dev_copy(d, lay.empty);
+        const uint32_t W = (uint32_t)(lay.wz.size() - 1);
+        pp[MP_PART_WS] = dev_copy(d, std::vector<float>((size_t)W * Nd, 0.f));
+        pp[MP_PART_WS2] = dev_copy(d, std::vector<float>((size_t)W * Nd, 0.f));
+        pp[MP_PART_T0] = dev_copy(d, std::vector<uint32_t>(W, 0xffffffffu));
+        pp[MP_PART_CHAIN] = dev_copy(d, lay.chain);
+        pp[MP_PART_CNT] = dev_copy(d, std::vector<uint32_t>(W, 0u));
+        if (x > 0) pp[MP_PART_OUT] = dev_copy(d, std::vector<float>((size_t)d.n_out_rows * Nd, 0.f));
+        d.mp_part_W[x] = W;
+        d.mp_part_rows[x] = (uint32_t)lay.ends.size();
+        d.mp_part_fin[x] = (uint32_t)lay.empty.size();
+    }
+    // the whole-matrix CSR is not uploaded: part 0's columns stand in for it (non-null)
+    a.col = a.pp[MP_PART_COL];
+    a.val = a.pp[MP_PART_VAL];
+}
+
 // the plan's column indices (u16 when they fit, else u32) and values (plan dtype) of
 // one replica, padded for the kernels' aligned over-reads
 void upload_csr(plan_state &p, device_arrays &a) {
@@ -220,6 +347,10 @@ void upload_csr(plan_state &p, device_arrays &a) {
     const auto &col = m.u(GLOBAL_META, sp.interleaved ? "nz_col_indices_after_interlance_storage" : "nz_col_indices", sb);
     auto vals = m.get_element(GLOBAL_META, sp.interleaved ? "nz_vals_after_interlance_storage" : "nz_vals", sb)->meta_data_arr;
     const uint64_t nnz = col.size();
+    if (d.mp_parts > 1) {
+        upload_col_parts(p, a, col, *vals);
+        return;
+    }
     if (d.col_perm) {
         // MP_COL_PERM: columns renumbered by degree (most nonzeros first, ties by column), so
         // the B rows the power-law hubs gather share 128-B lines and stay in L2; each launch
@@ -358,6 +489,11 @@ void upload_plan(plan_state &p, int dtype, int device) {
         const uint64_t b_bytes = p.K * (uint64_t)std::max<int64_t>(1, cfg.DENSE_MATRIX_SIZE) * (dtype == 0 ? 4u : 2u);
         d.col_perm = !sp.interleaved && p.K < (1ull << 32) &&
                      (cfg.MP_COL_PERM > 0 || (cfg.MP_COL_PERM < 0 && b_bytes >= (64ull << 20)));
+        // MP_COL_PARTS (fp32 plans of the whole matrix, one column tile: N <= 32): the renumbered
+        // columns dealt over P partitions, one merge-path pass each (upload_col_parts)
+        const int64_t Nd = std::max<int64_t>(1, cfg.DENSE_MATRIX_SIZE);
+        if (d.col_perm && dtype == 0 && sb == 0 && !pidx && cfg.MP_COL_PARTS > 1 && Nd <= 32 && p.K >= 64 * (uint64_t)cfg.MP_COL_PARTS)
+            d.mp_parts = (uint32_t)std::min<int64_t>(cfg.MP_COL_PARTS, 8);
     }
     if (!defer_csr) upload_csr(p, a);
     GS_CHECK(!d.col_perm || (a.cperm && a.bperm), "merge-path column permutation: arrays not uploaded");
@@ -682,6 +818,13 @@ void upload_plan(plan_state &p, int dtype, int device) {
             const uint32_t cfv = dtype == 0 ? 4u : 8u, cf = Nd % cfv == 0 ? cfv : 1u;
             const uint32_t X = std::min<uint32_t>(64u, pow2ceil_u((Nd + cf - 1) / cf));
             const uint64_t target = (uint64_t)gsk::kMpItems * (64u / X);  // >= one round per wave
+            if (d.mp_parts > 1) {  // the partitions' layouts are built with their CSRs (upload_col_parts)
+                d.scf = 8;
+                d.ws_n = Nd;
+                d.n_units = d.mp_part_W[0];
+                d.kernel = "k_merge_path";
+                break;
+            }
             gsk_host::merge_path_layout lay;
             std::string why;
             GS_CHECK(gsk_host::merge_path_device_layout(rows, row_num, m.u(L, "first_row_indices_without_ending", sb),
@@ -761,8 +904,8 @@ void add_replica(plan_state &p) {
         p.dev.allocations.push_back(dst);
         return dst;
     };
-    r.col = dup(s.col);
-    r.val = dup(s.val);
+    r.col = s.pp.empty() ? dup(s.col) : nullptr;  // MP_COL_PARTS: stand-ins for part 0 (below)
+    r.val = s.pp.empty() ? dup(s.val) : nullptr;
     r.a0 = (uint32_t *)dup(s.a0);
     r.a1 = (uint32_t *)dup(s.a1);
     r.a2 = (uint32_t *)dup(s.a2);
@@ -781,6 +924,11 @@ void add_replica(plan_state &p) {
     r.cperm = (uint32_t *)dup(s.cperm);
     r.bperm = dup(s.bperm);
     r.pad_out = dup(s.pad_out);
+    for (size_t i = 0; i < s.pp.size(); i++) r.pp[i] = dup(s.pp[i]);
+    if (!s.pp.empty()) {  // the whole-matrix stand-ins point at part 0 (upload_col_parts)
+        r.col = r.pp[MP_PART_COL];
+        r.val = r.pp[MP_PART_VAL];
+    }
     p.dev.replicas.push_back(r);
 }
 

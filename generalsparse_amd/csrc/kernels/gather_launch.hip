@@ -186,6 +186,41 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
             const uint32_t fb = d.n_fin ? (uint32_t)std::min<uint64_t>(256, (d.n_fin * N / 4 + 1023) / 1024) : 0u;
             // one column tile: split rows are combined inside the launch (chain arrivals)
             const bool fused = tiles == 1 && !(mp_debug() & 4u);
+            if (d.mp_parts > 1) {
+                // MP_COL_PARTS: B gathered into partition order, one merge-path pass per column
+                // partition (part 0 into C, the others into their fp32 outputs), then C += them
+                GS_CHECK(fused && sizeof(VT) == 4 && a.pp.size() == (size_t)d.mp_parts * kMpPartPtrs && a.cperm && a.bperm,
+                         "merge-path column partitions: fp32, one column tile, arrays uploaded");
+                const uint64_t units = (uint64_t)p.K * N * sizeof(VT) / (N * sizeof(VT) % 16 == 0 ? 16u : sizeof(VT));
+                const uint32_t pb = (uint32_t)std::min<uint64_t>((units + 255) / 256, 8192);
+                hipLaunchKernelGGL((gsk::k_permute_rows<VT, false>), dim3(std::max(pb, 1u)), dim3(256), 0, s, B,
+                                   (VT *)a.bperm, a.cperm, (uint32_t)p.K, N);
+                HIP_OK(hipGetLastError());
+                gsk::mp_part_outs outs{};
+                for (uint32_t x = 0; x < d.mp_parts; x++) {
+                    void *const *pp = &a.pp[(size_t)x * kMpPartPtrs];
+                    const uint32_t Wx = d.mp_part_W[x], nfin = d.mp_part_fin[x];
+                    const uint32_t gxx = std::min<uint32_t>((Wx + 3) / 4, 1u << 16);
+                    const uint32_t fbx = nfin ? (uint32_t)std::min<uint64_t>(256, ((uint64_t)nfin * N / 4 + 1023) / 1024) : 0u;
+                    VT *Cx = x == 0 ? C : (VT *)pp[MP_PART_OUT];
+                    if (x > 0) outs.p[x - 1] = (const float *)pp[MP_PART_OUT];
+                    hipLaunchKernelGGL((gsk::k_merge_path<VT, CT, CF>),
+                                       dim3(gxx + fbx, 1), dim3(256), lds, s,
+                                       (const uint32_t *)pp[MP_PART_WZ], (const uint32_t *)pp[MP_PART_WQ],
+                                       (const uint32_t *)pp[MP_PART_ENDS], (const uint32_t *)pp[MP_PART_RID],
+                                       d.mp_part_rows[x], (const CT *)pp[MP_PART_COL], (const VT *)pp[MP_PART_VAL],
+                                       (const VT *)a.bperm, Cx, (float *)pp[MP_PART_WS], (uint32_t *)pp[MP_PART_T0],
+                                       (float *)pp[MP_PART_WS2], Wx, N, X, row_base, (uint32_t)d.n_out_rows,
+                                       (const uint32_t *)pp[MP_PART_EMPTY], nfin, fbx, (const uint32_t *)pp[MP_PART_CHAIN],
+                                       (uint32_t *)pp[MP_PART_CNT], mp_debug(), nullptr);
+                    HIP_OK(hipGetLastError());
+                }
+                const uint64_t total = (uint64_t)d.n_out_rows * N;
+                const uint32_t ab = (uint32_t)std::min<uint64_t>((total + 255) / 256, 8192);
+                hipLaunchKernelGGL((gsk::k_add_parts<VT>), dim3(std::max(ab, 1u)), dim3(256), 0, s, C, outs, d.mp_parts - 1, total);
+                HIP_OK(hipGetLastError());
+                break;
+            }
             if (d.col_perm) {  // B into the plan's column order first (MP_COL_PERM, upload_csr)
                 GS_CHECK(a.cperm && a.bperm, "merge-path column permutation without its device arrays");
                 const uint64_t units = (uint64_t)p.K * N * sizeof(VT) / (N * sizeof(VT) % 16 == 0 ? 16u : sizeof(VT));
@@ -218,10 +253,11 @@ void launch_family(const plan_state &p, const device_arrays &a, const VT *B, VT 
                                    fused ? a.t2 : nullptr, mp_debug(), g_mp_stamps);
             else
 #endif
-                    hipLaunchKernelGGL((gsk::k_merge_path<VT, CT, CF>), dim3(gx + fb, tiles), dim3(256), lds, s, a.a0, a.a1,
+                    hipLaunchKernelGGL((gsk::k_merge_path<VT, CT, CF>),
+                                   dim3(gx + fb, tiles), dim3(256), lds, s, a.a0, a.a1,
                                    a.a2, a.a3, (uint32_t)d.n_rows_aux, col, val, B, C, a.ws, a.t0, a.ws2, W, N, X, row_base,
                                    (uint32_t)d.n_out_rows, a.a4, (uint32_t)d.n_fin, fb, fused ? a.t1 : nullptr,
-                                   fused ? a.t2 : nullptr, mp_debug());
+                                   fused ? a.t2 : nullptr, mp_debug(), nullptr);
             HIP_OK(hipGetLastError());
             if (fused) break;
             GS_CHECK((uint64_t)W * N < 0xffffffffull, "merge-path fix-up indices exceed 32 bits");

@@ -954,6 +954,44 @@ def test_merge_path_matches_oracle(ws, level, N, dtype, merge_walk):
         check(C, ref, dtype, plan)
 
 
+@pytest.mark.parametrize("parts", [2, 4, 8])
+@pytest.mark.parametrize("N", [8, 3, 32])
+@pytest.mark.parametrize("ws", [512, 37])
+def test_merge_path_column_partitions(parts, N, ws):
+    """MP_COL_PARTS (fp32 merge-path plans with MP_COL_PERM): the degree-ranked columns dealt
+    over P partitions, one k_merge_path pass per partition over its own CSR and wave ranges,
+    the partitions' fp32 outputs added to C in partition order: against the oracle, relaunches
+    into NaN-filled C bit for bit (the chains' counters re-arm), a replica the same bits"""
+    M = 3000
+    row, col, val = ds.rmat(M, 60000, seed=9)
+    # a few rows over many waves and empty rows: chains inside a partition
+    row = np.concatenate([row, np.full(4000, 1500, np.uint64)])
+    col = np.concatenate([col, np.arange(4000, dtype=np.uint64) % M])
+    val = np.concatenate([val, np.linspace(-1, 1, 4000).astype(np.float32)])
+    key = np.unique(row.astype(np.int64) * M + col.astype(np.int64), return_index=True)[1]
+    row, col, val = row[key], col[key], val[key]
+    B = np.random.default_rng(4).uniform(-1, 1, (M, N)).astype(np.float32)
+    gsa.set_config("MP_COL_PERM", 1)
+    gsa.set_config("MP_COL_PARTS", parts)
+    try:
+        plan = gsa.Plan.from_coo(M, M, row, col, val).run_pipeline("merge_path", N, ws, 1).compile().upload("f32", 0)
+    finally:
+        gsa.set_config("MP_COL_PARTS", 0)
+        gsa.set_config("MP_COL_PERM", -1)
+    assert plan.info()["device_kernel"] == "k_merge_path"
+    Bt = torch.from_numpy(B).to(DEV)
+    C = plan.spmm(Bt)
+    torch.cuda.synchronize()
+    check(C.cpu().numpy(), ofi.spmm_ref(M, N, row, col, val, B, "f64"), "f32", plan)
+    plan.add_replica()
+    for rep in (0, 1, 0):
+        C2 = torch.full((M, N), float("nan"), device=DEV)
+        plan.spmm(Bt, C=C2, replica=rep)
+        torch.cuda.synchronize()
+        assert torch.equal(C2, C)
+    plan.free()
+
+
 @pytest.mark.parametrize("variant", [{}, {"MP_PERM_SCATTER": 1}, {"MP_PERM_HOT": 300}])
 @pytest.mark.parametrize("dtype", ["f32", "f16"])
 @pytest.mark.parametrize("N", [8, 3])
