@@ -2145,6 +2145,55 @@ __global__ __launch_bounds__(64 * W) void k_mfma_ks(const uint32_t *__restrict__
                                                 arrivals, stamps, blockIdx.x, prio);
 }
 
+#ifdef GS_EXPERIMENTS
+// ---------------------------------------------------------------------------
+// k_mfma_ks_persist (KS_PERSIST = the grid): a persistent grid over
+// the plan's units (row block, K range) -- workgroup b runs unit b, then units pulled from its
+// XCD's head (queue[xcc]: unit grid + xcc + 8 n), until the units run out.  The pull for the next
+// unit is issued as the current one starts (its round trip overlaps the unit's first loads);
+// the units' K-range combine is k_mfma_ks's (tickets + tagged slabs in q order), so C is the
+// same bits as the static launch's whichever workgroup runs a unit.  The last workgroup out
+// re-arms the nine queue words (8 heads + the exit count).
+// ---------------------------------------------------------------------------
+template <int CT, int RT, int W, int D, int MAXG, int NTL = 0>
+__global__ __launch_bounds__(64 * W) void k_mfma_ks_persist(const uint32_t *__restrict__ bmtb_first_row,
+                                                            const u32x4 *__restrict__ tP, const u32x4 *__restrict__ tV,
+                                                            const u32x2 *__restrict__ steps, const f16 *__restrict__ B,
+                                                            f16 *__restrict__ C, uint32_t K, uint32_t N, uint32_t S,
+                                                            uint32_t NS, uint32_t nunits, uint32_t row_base,
+                                                            float *__restrict__ slabs, uint32_t *__restrict__ arrivals,
+                                                            uint32_t prio, uint32_t *__restrict__ queue) {
+    __shared__ uint32_t next_sh;
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+    xcc &= 7u;
+    const uint32_t grid = gridDim.x;
+    uint32_t u = blockIdx.x, qx = xcc, tried = 0;
+    while (u < nunits) {
+        uint32_t pulled = 0;
+        if (threadIdx.x == 0) pulled = __hip_atomic_fetch_add(queue + qx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ks_body<CT, RT, W, D, MAXG, false, true, false, NTL>(bmtb_first_row, tP, tV, steps, B, C, K, N, S, NS, nunits,
+                                                          row_base, slabs, arrivals, nullptr, u, prio);
+        __syncthreads();
+        if (threadIdx.x == 0) next_sh = pulled;
+        __syncthreads();
+        u = grid + qx + 8u * next_sh;
+        __syncthreads();
+        // this XCD's units are done: take the other heads' in turn (correct whatever the placement)
+        while (u >= nunits && ++tried < 8u) {
+            qx = (qx + 1u) & 7u;
+            if (threadIdx.x == 0) next_sh = __hip_atomic_fetch_add(queue + qx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            u = grid + qx + 8u * next_sh;
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x == 0 && __hip_atomic_fetch_add(queue + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == grid - 1u) {
+        for (int i = 0; i < 9; i++) __hip_atomic_store(queue + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+#endif  // GS_EXPERIMENTS (k_mfma_ks_persist)
+
 // ---------------------------------------------------------------------------
 // k_mfma_ks_group -- several k_mfma_ks launches of one instantiation as one grid (a layer's
 // or a batch's SpMMs; gs_spmm_batch): entry i owns workgroups [begin[i], begin[i] + nwg_i) and

@@ -76,7 +76,7 @@ std::string get_metadata_item_name(POS_TYPE pos, const std::string &name, int su
 // measured slower than the default kernels, parity-tested there
 bool experiments_key(const std::string &k) {
     return k == "MFMA_BM" || k == "NM_KS" || k == "MFMA_FLAGS" || k == "BM_V2" || k == "BM_KB" || k == "MP_ROWS" ||
-           k == "KS_FORCE_TIMEOUT" || k == "KS_POS8" || k == "NM_V4";
+           k == "KS_FORCE_TIMEOUT" || k == "KS_POS8" || k == "NM_V4" || k == "KS_PERSIST";
 }
 
 // a key / value the release build refuses, whether from set_config or a JSON config file
@@ -144,6 +144,7 @@ void apply_kv(config_t &c, const std::string &k, const std::string &v) {
     else if (k == "NM_TILES") c.NM_TILES = i();
     else if (k == "LDS_KSPLIT") c.LDS_KSPLIT = i();
     else if (k == "MP_COL_PARTS") c.MP_COL_PARTS = i();
+    else if (k == "KS_PERSIST") c.KS_PERSIST = i();
     else if (k == "KS_HEAD") c.KS_HEAD = i();
     else if (k == "NM_NT") c.NM_NT = i();
     else if (k == "MP_ROWS") c.MP_ROWS = b();
@@ -232,7 +233,7 @@ int64_t get_config_int(const std::string &k) {
     GS_KEY(SHARED_MEM_TOTAL_SIZE) GS_KEY(MAX_DIV_TIMES_OF_DIV) GS_KEY(MFMA_GLDS) GS_KEY(MFMA_COMPUTE_WAVES)
     GS_KEY(MFMA_GLDS_NBUF) GS_KEY(MODEL_DRIVEN_COMPRESS) GS_KEY(LDS_STAGE_B) GS_KEY(MFMA_TILES) GS_KEY(MFMA_KROT)
     GS_KEY(WARP_ROWS_GROUPS) GS_KEY(WARP_ROWS_CHUNKS) GS_KEY(MFMA_MAX_FILL) GS_KEY(NM_MFMA) GS_KEY(MFMA_KSPLIT) GS_KEY(MFMA_KS)
-    GS_KEY(NM_KS) GS_KEY(NM_SPLIT) GS_KEY(MFMA_FLAGS) GS_KEY(MFMA_BM) GS_KEY(BM_SPLIT) GS_KEY(BM_WAVES) GS_KEY(BM_V2) GS_KEY(BM_KB) GS_KEY(KS_MIN_ROWS) GS_KEY(KS_SPLIT) GS_KEY(KS_WAVES) GS_KEY(KS_PRIO) GS_KEY(KS_FORCE_TIMEOUT) GS_KEY(KS_APART) GS_KEY(NM_V4) GS_KEY(KS_POS8) GS_KEY(KS_NT) GS_KEY(NM_KROT) GS_KEY(NM_TILES) GS_KEY(LDS_KSPLIT) GS_KEY(MP_COL_PARTS) GS_KEY(KS_HEAD) GS_KEY(NM_NT) GS_KEY(MP_ROWS) GS_KEY(MP_SOLO) GS_KEY(MP_COL_PERM) GS_KEY(MP_PERM_HOT) GS_KEY(MP_PERM_SCATTER)
+    GS_KEY(NM_KS) GS_KEY(NM_SPLIT) GS_KEY(MFMA_FLAGS) GS_KEY(MFMA_BM) GS_KEY(BM_SPLIT) GS_KEY(BM_WAVES) GS_KEY(BM_V2) GS_KEY(BM_KB) GS_KEY(KS_MIN_ROWS) GS_KEY(KS_SPLIT) GS_KEY(KS_WAVES) GS_KEY(KS_PRIO) GS_KEY(KS_FORCE_TIMEOUT) GS_KEY(KS_APART) GS_KEY(NM_V4) GS_KEY(KS_POS8) GS_KEY(KS_NT) GS_KEY(NM_KROT) GS_KEY(NM_TILES) GS_KEY(LDS_KSPLIT) GS_KEY(MP_COL_PARTS) GS_KEY(KS_PERSIST) GS_KEY(KS_HEAD) GS_KEY(NM_NT) GS_KEY(MP_ROWS) GS_KEY(MP_SOLO) GS_KEY(MP_COL_PERM) GS_KEY(MP_PERM_HOT) GS_KEY(MP_PERM_SCATTER)
 #undef GS_KEY
     throw gs_error("get_config_int: no integer key " + k);
 }

@@ -50,6 +50,7 @@ struct device_plan {
     bool ks_p8 = false;       // k_mfma_ks: 8-bit entry positions (ks_tiles::P8, KS_POS8)
     uint32_t ks_gh = 0;       // k_mfma_ks: groups per head step (ks_tiles::GH; 0: every step by record)
     uint32_t ks_nt = 0;       // k_mfma_ks: non-temporal loads of A's groups (NTL bit 0; ks_tiles::NT, KS_NT)
+    uint32_t ks_persist = 0;  // k_mfma_ks: persistent grid of this many workgroups pulling units (KS_PERSIST, experiments)
     bool nm_nt = false;       // k_nm_mfma: non-temporal panel loads (NM_NT)
     uint32_t nm_tiles = 8;    // k_nm_mfma: 16-row tiles per workgroup (mc_layout::nm_T)
     // merge path, MP_COL_PARTS: the columns (renumbered by degree, MP_COL_PERM) dealt round-robin

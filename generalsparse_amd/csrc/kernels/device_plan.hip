@@ -523,6 +523,8 @@ void upload_plan(plan_state &p, int dtype, int device) {
             d.ks_p8 = kt.P8;
             d.ks_nt = kt.NT;
             d.ks_gh = kt.GH;
+            d.ks_persist = (uint32_t)std::max<int64_t>(0, get_config().KS_PERSIST);
+            if (d.ks_persist) a.t3 = dev_copy(d, std::vector<uint32_t>(9, 0u));  // 8 XCD heads + the exit count
             a.t0 = dev_copy(d, to_u32(mc.tbr, "BMTB first_row_indices"));
             a.tcol = kt.P8 ? (void *)dev_copy(d, kt.pos8) : (void *)dev_copy(d, kt.pos);
             a.tval = dev_copy(d, kt.val);

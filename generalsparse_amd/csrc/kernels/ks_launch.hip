@@ -119,6 +119,28 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
             throw gs_error("k_mfma_ks: the overlapped-LDS layout is built for N = 32, RT <= 5, MAXG <= 2");
     }
 #endif
+#ifdef GS_EXPERIMENTS
+    // KS_PERSIST (fixed at upload): a persistent grid of d.ks_persist workgroups pulling units
+    if (d.ks_persist) {
+        if constexpr (W == (int)kKsWaves && !STAMPS && (CT == 2 || CT == 8)) {
+            GS_CHECK(d.ks_ap && !d.ks_p8 && a.t3 && ks_col_tiles_ct(N, CT) == 1, "k_mfma_ks_persist: 8 waves, apart layout, one column tile");
+            auto kp = d.ks_nt ? gsk::k_mfma_ks_persist<CT, RT, W, (int)kKsDepth, MAXG, 1>
+                              : gsk::k_mfma_ks_persist<CT, RT, W, (int)kKsDepth, MAXG, 0>;
+            grant_lds(d.device, kp, d.lds_bytes);
+            const uint32_t nunits = (uint32_t)d.n_rows_aux * d.ksplit;
+            hipLaunchKernelGGL(kp, dim3(std::min(d.ks_persist, nunits)), dim3(64 * W), d.lds_bytes, s, a.t0,
+                               (const gsk::u32x4 *)a.tcol, (const gsk::u32x4 *)a.tval, (const gsk::u32x2 *)a.t1, B, C,
+                               (uint32_t)p.K, N, d.ksplit, d.ks_ns, nunits, (uint32_t)d.row_base, a.ws, a.t2,
+                               ks_prio_arg() | (d.ks_gh << 8), a.t3);
+            HIP_OK(hipGetLastError());
+            return;
+        } else {
+            throw gs_error("k_mfma_ks_persist is built for N = 32 and 128-column tiles, 8 waves");
+        }
+    }
+#else
+    GS_CHECK(!d.ks_persist, "k_mfma_ks_persist is an experiments-build kernel");
+#endif
     // the LDS this instantiation needs at the plan's range width, against what the upload sized
     GS_CHECK(gsk::ks_lds_bytes(CT, RT, W, d.ks_ap) <= d.lds_bytes, "k_mfma_ks: LDS size disagrees with the upload");
     grant_lds(d.device, kern, d.lds_bytes);
@@ -346,7 +368,7 @@ void launch_ks_group_rt(const std::vector<ks_group_item> &it, uint32_t N, hipStr
 uint32_t ks_group_key(const plan_state &p, uint32_t N) {
     const device_plan &d = p.dev;
     const bool w8 = d.waves == kKsWaves && d.ks_ap, w4 = d.waves == 4 && !d.ks_ap;
-    if (!p.uploaded || !d.mfma || !d.ks || d.pad_rows || N != 32 || d.lds_N != 32 || !(w8 || w4)) return 0;
+    if (!p.uploaded || !d.mfma || !d.ks || d.pad_rows || N != 32 || d.lds_N != 32 || !(w8 || w4) || d.ks_persist) return 0;
 #ifndef GS_EXPERIMENTS
     // the release build instantiates the grouped kernel for 16-byte u16-position groups on 8
     // waves only: any other layout runs as single launches (which refuse it themselves)

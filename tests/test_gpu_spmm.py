@@ -1281,3 +1281,40 @@ def test_warp_rows_chunks_per_pass(p0, p1, chunks, dtype):
             plan.free()
     finally:
         gsa.set_config("WARP_ROWS_CHUNKS", old)
+
+
+@pytest.mark.parametrize("rows,split,grid", [(40, 2, 256), (40, 4, 256), (80, 4, 256), (40, 4, 64), (48, 3, 7)])
+def test_mfma_ks_persistent_grid_is_exact(rows, split, grid):
+    """KS_PERSIST (experiments build): a persistent grid pulling (row block,
+    K range) units from per-XCD heads computes the same bits as the static k_mfma_ks launch
+    (the K-range combine is the same tickets + tagged slabs in q order), relaunch after
+    relaunch (the heads re-arm), also with fewer workgroups than XCD heads (stealing)"""
+    need_experiments()
+    M = K = 5120 if grid >= 64 else 1536
+    N = 32
+    r, c, v = ds.pruned_weight(M, K, 0.7, 13)
+    B = torch.randn((K, N), device=DEV, dtype=torch.float16)
+    outs = []
+    for persist in (0, grid):
+        gsa.set_config("KS_SPLIT", split)
+        gsa.set_config("KS_PERSIST", persist)
+        gsa.set_config("KS_NT", 1)
+        try:
+            plan = gsa.Plan.from_coo(M, K, r, c, v).run_pipeline("block_total", N, rows, 1).compile().upload("f16", 0)
+        finally:
+            gsa.set_config("KS_SPLIT", 0)
+            gsa.set_config("KS_PERSIST", 0)
+            gsa.set_config("KS_NT", 0)
+        info = plan.info()
+        assert info["device_kernel"] == "k_mfma_ks" and info["ksplit"] == split, info
+        for _ in range(3):
+            C = torch.full((M, N), float("nan"), device=DEV, dtype=torch.float16)
+            plan.spmm(B, C=C)
+            torch.cuda.synchronize()
+            outs.append(C.clone())
+        plan.device_status()
+        plan.free()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    vf = v.astype(np.float16).astype(np.float32)
+    check(outs[0].float().cpu().numpy(), ofi.spmm_ref(M, N, r, c, vf, B.float().cpu().numpy(), "f64"), "f16")
