@@ -313,6 +313,9 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     // KS_WAVES = 4 (N = 32): 256-thread workgroups with the overlapped LDS layout, two per CU, so one
     // workgroup's prologue and combine overlap the other's loop (grouped multi-round launches)
     if (get_config().KS_WAVES == 4 && CT == 2) W = 4;
+    // KS_WAVES = 12 (N = 32, RT <= 5, experiments): three waves per SIMD, the stages and the apart
+    // partial tiles still within 160 KB (C2 40-row blocks: 155 KB)
+    if (get_config().KS_WAVES == 12 && CT == 2 && RT <= 5 && gsk::ks_lds_bytes(CT, RT, 12) <= 160 * 1024) W = 12;
     const uint64_t nnz = row_ptr[tb_rows[nb]] - row_ptr[tb_rows[0]];
     if (nnz == 0 || (double)nb * 16 * RT * K > (double)max_fill * nnz) {  // as build_mfma_tiles
         why = "row blocks too sparse for dense tiles";
@@ -340,7 +343,7 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     t.W = W;
     // KS_POS8 (8-bit positions in 8 x 16 segments; N = 32, RT <= 8: segment ids < 32)
     t.P8 = get_config().KS_POS8 && CT == 2 && (W == kKsWaves || W == 4);
-    t.NT = (CT == 2 || CT == 8) && W == kKsWaves && !t.P8 && t.AP && get_config().KS_NT ? 1u : 0u;
+    t.NT = (CT == 2 || CT == 8) && (W == kKsWaves || W == 12) && !t.P8 && t.AP && get_config().KS_NT ? 1u : 0u;
     // pass 1: the largest step (entries of a row block in 32 columns; P8: groups per segment)
     uint64_t gmax = 1;
     {

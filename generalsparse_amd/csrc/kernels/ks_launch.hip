@@ -51,6 +51,13 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
             launch_ks_k<CT, RT, MAXG, false, 16>(p, a, B, C, N, s, stamps);
             return;
         }
+        // KS_WAVES = 12 (N = 32, RT <= 5): three waves per SIMD (r06 A/B)
+        if constexpr (CT == 2 && RT <= 5) {
+            if (d.waves == 12) {
+                launch_ks_k<CT, RT, MAXG, false, 12>(p, a, B, C, N, s, stamps);
+                return;
+            }
+        }
     }
     // GS_KS_DEPTH=1/3/4 (look-ahead sweep against kKsDepth = 2, N = 32 on the C2 / attn / fc1 instantiations)
     if constexpr (W == (int)kKsWaves && !STAMPS && CT == 2 &&
@@ -95,7 +102,7 @@ void launch_ks_k(const plan_state &p, const device_arrays &a, const gsk::f16 *B,
 #endif
     auto kern = gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, STAMPS>;
     if (d.ks_nt) {  // KS_NT: A's groups by non-temporal loads (N = 32 / 128, 8 waves, the apart layout)
-        if constexpr ((CT == 2 || CT == 8) && W == (int)kKsWaves && !STAMPS) {
+        if constexpr ((CT == 2 || CT == 8) && (W == (int)kKsWaves || W == 12) && !STAMPS) {
             GS_CHECK(d.ks_ap && !d.ks_p8, "k_mfma_ks: non-temporal loads are built for the apart layout, 16-bit positions");
             GS_CHECK(d.ks_nt == 1, "k_mfma_ks: KS_NT is built for A's groups (1)");
             kern = gsk::k_mfma_ks<CT, RT, W, (int)kKsDepth, MAXG, false, true, false, 1>;
