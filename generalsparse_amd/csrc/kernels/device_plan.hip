@@ -133,7 +133,14 @@ bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uin
     if (waves > 16) { why = "more than 16 BMWs per BMTB"; return false; }
     if (maxr > 4) { why = "more than 4 rows per BMW"; return false; }
     maxr = maxr <= 1 ? 1 : (maxr <= 2 ? 2 : 4);
-    const uint32_t RSB = N * vbytes + (UB % 2 == 0 ? 16u : 0u);  // odd count of 16-B units
+    // B rows in LDS at an odd count of 16-B units (bank spread for random rows), except fp32 at
+    // N = 32 (8 lanes x 16 B per row, 8 slots per wave): rows at 128 B, so a row starts on bank 0
+    // or 32 by its parity, and each row's entries are ordered so that the slots whose B reads
+    // share an LDS cycle (ds_read_b128 lane groups: slots {0,3} and {1,2} of each half-wave) read
+    // rows of opposite parity -- conflict-free (pair_banks below; r06 PMC: 42% of the LDS cycles
+    // were bank conflicts with the odd stride)
+    const bool pair_banks = vbytes == 4 && N == 32;
+    const uint32_t RSB = pair_banks ? N * vbytes : N * vbytes + (UB % 2 == 0 ? 16u : 0u);
     const uint32_t ebytes = 2 + vbytes;
     const uint64_t nthr = 64ull * waves;
     const uint64_t max_kc = std::min<uint64_t>(K, 65536);
@@ -196,6 +203,42 @@ bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uin
                 }
                 cur[i] = e;
                 while ((t.tcol.size() - base) % 4) { t.tcol.push_back(0); t.src.push_back(~0u); }
+                if (pair_banks) {
+                    // per 32-entry block of the row (slot s takes entries 4s..4s+3, entry q in the
+                    // q-th read): the reads of slots (0,3), (1,2), (4,7), (5,6) at one q get one
+                    // even and one odd column while both kinds last (any entry order sums the row)
+                    static const int pairs[4][2] = {{0, 3}, {1, 2}, {4, 7}, {5, 6}};
+                    const size_t rs = base + off[i], re = t.tcol.size();
+                    for (size_t b0 = rs; b0 < re; b0 += 32) {
+                        const size_t n = std::min<size_t>(32, re - b0);
+                        std::vector<std::pair<uint16_t, uint32_t>> ev, od;
+                        for (size_t k = 0; k < n; k++) (t.tcol[b0 + k] & 1u ? od : ev).push_back({t.tcol[b0 + k], t.src[b0 + k]});
+                        auto take = [&](bool want_odd) {
+                            auto &v = (want_odd && !od.empty()) || ev.empty() ? od : ev;
+                            const auto x = v.back();
+                            v.pop_back();
+                            return x;
+                        };
+                        for (int q = 0; q < 4; q++)
+                            for (const auto &pr : pairs) {
+                                const size_t pa = (size_t)pr[0] * 4 + q, pb = (size_t)pr[1] * 4 + q;
+                                if (pa < n) {
+                                    const auto x = take(ev.size() < od.size());
+                                    t.tcol[b0 + pa] = x.first;
+                                    t.src[b0 + pa] = x.second;
+                                    if (pb < n) {
+                                        const auto y = take(!(x.first & 1u));
+                                        t.tcol[b0 + pb] = y.first;
+                                        t.src[b0 + pb] = y.second;
+                                    }
+                                } else if (pb < n) {
+                                    const auto y = take(false);
+                                    t.tcol[b0 + pb] = y.first;
+                                    t.src[b0 + pb] = y.second;
+                                }
+                            }
+                    }
+                }
             }
             for (uint64_t i = nr; i <= rpw; i++) off[i] = (uint32_t)(t.tcol.size() - base);
             while ((t.tcol.size() - base) % 8) { t.tcol.push_back(0); t.src.push_back(~0u); }
