@@ -15,11 +15,12 @@ import math
 CANDIDATES = {
     # fp16 unstructured pruned weights (C2, OPT q_proj-like): k_mfma_ks row blocks with a K split
     # (block_total(40,1) KS_NT=1: 2 K ranges, A's groups by non-temporal loads -- the C2 winner,
-    # profiles/r05n_nt3.txt), k_mfma_rows (tblock_warp_total(20,2)) and the gather families
+    # profiles/r05n_nt3.txt), k_mfma_rows (tblock_warp_total(20,2)) and the gather families; at fp32
+    # (the comparator's search) tblock_warp_total(24,2) on k_lds_rows_dma is the fastest (r06 ab_dma)
     "f16": [("block_total", 20, 1), ("block_total", 10, 1), ("block_total", 40, 1), ("block_total", 80, 1),
             ("block_total", 40, 1, {"KS_NT": 1}), ("block_total", 80, 1, {"KS_NT": 1}),
-            ("tblock_warp_total", 20, 2), ("tblock_warp_total", 4, 1), ("warp_segment", 4, 1),
-            ("thread_total", 4, 1)],
+            ("tblock_warp_total", 20, 2), ("tblock_warp_total", 24, 2), ("tblock_warp_total", 4, 1),
+            ("warp_segment", 4, 1), ("thread_total", 4, 1)],
     # fp16 2:4 structured (C3): the col-direction plan (32-nnz BMTs = 64-column k-steps) on the sparse
     # matrix cores; NM_NT (A's panel blocks by non-temporal loads) is the default, NM_TILES the
     # 16-row tiles per workgroup (0: the upload's rule)

@@ -1223,6 +1223,148 @@ __global__ __launch_bounds__(1024) void k_lds_rows(
 
 
 // ---------------------------------------------------------------------------
+// k_lds_rows_dma -- k_lds_rows for fp32 B at N = 32 (LDS_DMA): B rows sit in LDS at 128 B, exactly
+// their HBM image, so each chunk's B rows and A segment (u16 columns, fp32 values) go to LDS by
+// LDS-DMA (global_load_lds_dwordx4: no register staging, no ds_write phase) into one of two
+// buffers: chunk j+1 lands while chunk j is computed, one barrier per chunk.  A wave's row offsets
+// in the chunk come from scalar loads.  Same compute loop, K split and slab combine as k_lds_rows;
+// entries are in the parity-paired order (conflict-free B reads).
+// ---------------------------------------------------------------------------
+template <int MAXR>
+__global__ __launch_bounds__(1024) void k_lds_rows_dma(
+    const uint32_t *__restrict__ bmtb_first_row, const uint32_t *__restrict__ bmw_of_bmtb,
+    const uint32_t *__restrict__ bmw_first_row, const uint32_t *__restrict__ seg_start,
+    const uint32_t *__restrict__ seg_row_off, const uint16_t *__restrict__ tcol, const float *__restrict__ tval,
+    const float *__restrict__ B, float *__restrict__ C, uint32_t K, uint32_t KC, uint32_t nc, uint32_t rpw_max,
+    uint32_t seg_cap, uint32_t row_base, uint32_t ksp, uint32_t ncs, float *__restrict__ slabs,
+    uint32_t *__restrict__ arrivals) {
+    constexpr uint32_t N = 32, CF = 4, X = 8, S = 8, RSB = 128;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint32_t tid = threadIdx.x, nthr = blockDim.x, nwv = nthr >> 6;
+    const uint32_t lane = tid & 63u, wib = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t xl = lane & (X - 1u), slot = lane / X;
+    const uint32_t g = ksp > 1u ? blockIdx.x / ksp : blockIdx.x, q = ksp > 1u ? blockIdx.x % ksp : 0u;
+    const uint32_t j0 = q * (ksp > 1u ? ncs : 0u), j1 = ksp > 1u ? min(nc, j0 + ncs) : nc;
+    const uint32_t r_first = bmtb_first_row[g];
+    const uint32_t bmw = bmw_of_bmtb[g] + wib;
+    uint32_t t0 = 0, nt = 0;
+    if (bmw < bmw_of_bmtb[g + 1]) {
+        t0 = bmw_first_row[bmw] - r_first;
+        nt = bmw_first_row[bmw + 1] - bmw_first_row[bmw];
+    }
+    t0 = __builtin_amdgcn_readfirstlane(t0);
+    nt = __builtin_amdgcn_readfirstlane(nt);
+    // one buffer: B rows [0, KC*128), columns [cap*2), values [cap*4)
+    const uint32_t lB = KC * RSB, lV = lB + seg_cap * 2u, szBuf = lV + seg_cap * 4u;
+    const uint32_t c0 = xl * CF, cb = c0 * 4u;
+    float acc[MAXR][CF];
+#pragma unroll
+    for (int t = 0; t < MAXR; t++)
+#pragma unroll
+        for (int k = 0; k < CF; k++) acc[t][k] = 0.f;
+    // LDS-DMA of chunk j into buffer b: every wave takes 1 KB blocks (64 lanes x 16 B) of the three
+    // contiguous source ranges in turn; lanes past a range's end are masked off
+    auto issue = [&](uint32_t j, uint32_t b) {
+        unsigned char *dst = lds + b * szBuf;
+        const uint32_t kc0 = j * KC, rows = min(KC, K - kc0);
+        const uint32_t s0 = seg_start[g * nc + j], len = seg_start[g * nc + j + 1] - s0;
+        const unsigned char *srcs[3] = {reinterpret_cast<const unsigned char *>(B + (size_t)kc0 * N),
+                                        reinterpret_cast<const unsigned char *>(tcol + s0),
+                                        reinterpret_cast<const unsigned char *>(tval + s0)};
+        const uint32_t units[3] = {rows * (RSB / 16u), len / 8u, len / 4u};
+        const uint32_t dofs[3] = {0u, lB, lV};
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            for (uint32_t ib = wib; ib * 64u < units[r]; ib += nwv) {
+                const uint32_t u = ib * 64u + lane;
+                if (u < units[r])
+                    __builtin_amdgcn_global_load_lds((const void *)(srcs[r] + (size_t)u * 16u),
+                                                     (__attribute__((address_space(3))) void *)(dst + dofs[r] + ib * 1024u), 16, 0, 0);
+            }
+        }
+    };
+    issue(j0, 0u);
+    __syncthreads();  // vmcnt(0): chunk j0 landed
+    for (uint32_t j = j0; j < j1; j++) {
+        const uint32_t b = (j - j0) & 1u;
+        if (j + 1 < j1) issue(j + 1, b ^ 1u);  // lands while chunk j is computed
+        const unsigned char *lAc = lds + b * szBuf + lB;
+        const unsigned char *lAv = lds + b * szBuf + lV;
+        const unsigned char *lBb = lds + b * szBuf;
+        const uint32_t *ro = seg_row_off + (size_t)(g * nc + j) * (rpw_max + 1) + t0;  // this wave's row offsets
+#pragma unroll
+        for (int t = 0; t < MAXR; t++) {
+            if ((uint32_t)t < nt) {
+                const uint32_t e0 = ro[t], e1 = ro[t + 1];
+                for (uint32_t p0 = e0 + slot * 4u; p0 < e1; p0 += S * 4u) {
+                    const uint2 craw = *reinterpret_cast<const uint2 *>(lAc + p0 * 2u);
+                    const uint32_t cc[4] = {craw.x & 0xffffu, craw.x >> 16, craw.y & 0xffffu, craw.y >> 16};
+                    uint4 braw[4];
+#pragma unroll
+                    for (int qq = 0; qq < 4; qq++) braw[qq] = *reinterpret_cast<const uint4 *>(lBb + cc[qq] * RSB + cb);
+                    const float4 vv = *reinterpret_cast<const float4 *>(lAv + p0 * 4u);
+                    const float vq[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+                    for (int qq = 0; qq < 4; qq++) {
+                        float bt[CF];
+                        __builtin_memcpy(bt, &braw[qq], 16);
+#pragma unroll
+                        for (int k = 0; k < CF; k++) acc[t][k] = __builtin_fmaf(vq[qq], bt[k], acc[t][k]);
+                    }
+                }
+            }
+        }
+        __syncthreads();  // chunk j+1 landed (every wave's vmcnt(0)), chunk j consumed
+    }
+#pragma unroll
+    for (int t = 0; t < MAXR; t++)
+        if ((uint32_t)t < nt) wave_reduce_slots<CF>(acc[t], (int)X);
+    if (ksp <= 1u) {
+#pragma unroll
+        for (int t = 0; t < MAXR; t++)
+            if ((uint32_t)t < nt && slot == 0) store_f32<float, CF>(C + (size_t)(r_first + t0 + t + row_base) * N + c0, acc[t]);
+        return;
+    }
+    // K-split hand-off: as k_lds_rows (sc1 slab stores, vmcnt(0), barrier, one arrival add)
+    const size_t slab_rows = (size_t)rpw_max;
+    if (slot == 0) {
+#pragma unroll
+        for (int t = 0; t < MAXR; t++) {
+            if ((uint32_t)t < nt) {
+                float *dst = slabs + (((size_t)g * ksp + q) * slab_rows + t0 + t) * N + c0;
+                const f4v v = {acc[t][0], acc[t][1], acc[t][2], acc[t][3]};
+                __asm__ volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(v) : "memory");
+            }
+        }
+    }
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    uint32_t *flag = reinterpret_cast<uint32_t *>(lds);
+    if (tid == 0) *flag = __hip_atomic_fetch_add(arrivals + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*flag != ksp - 1u) return;
+    if (tid == 0) __hip_atomic_store(arrivals + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (slot != 0) return;
+#pragma unroll
+    for (int t = 0; t < MAXR; t++) {
+        if ((uint32_t)t < nt) {
+            float sum[CF] = {0.f, 0.f, 0.f, 0.f};
+            for (uint32_t qq = 0; qq < ksp; qq++) {
+                if (qq == q) {
+#pragma unroll
+                    for (int k = 0; k < CF; k++) sum[k] += acc[t][k];
+                    continue;
+                }
+                const float *src = slabs + (((size_t)g * ksp + qq) * slab_rows + t0 + t) * N + c0;
+#pragma unroll
+                for (int k = 0; k < CF; k++) sum[k] += __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            store_f32<float, CF>(C + (size_t)(r_first + t0 + t + row_base) * N + c0, sum);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // BMTB row blocks on the matrix cores (MI355X layout of a tblock/warp/block-
 // total plan whose row blocks are dense enough).  Workgroup g owns BMTB g
 // (R <= RMAX <= 16*RT rows) and walks K in chunks of KC = 2^LGKC columns.

@@ -124,6 +124,7 @@ struct config_t {
                                  // places, loaded without their records (when the padding costs <= 6% more groups)
     int64_t KS_PERSIST = 0;      // k_mfma_ks: persistent grid size pulling (row block, K range) units (experiments build)
     int64_t MP_COL_PARTS = 0;    // merge path with MP_COL_PERM, fp32: column partitions, one pass each (0/1: off)
+    int64_t LDS_DMA = 1;         // k_lds_rows at fp32 N = 32: chunks by LDS-DMA into two buffers (k_lds_rows_dma)
     int64_t LDS_KSPLIT = 0;      // k_lds_rows: workgroups per BMTB, each over a K range (fp32 slab combine; 0 auto)
     int64_t NM_TILES = 0;        // k_nm_mfma: 16-row tiles per workgroup (0: nm_tiles_for; 2, 4, 7, 8)
     int64_t NM_KROT = 1;         // k_nm_mfma: each workgroup walks K from its own 256-row B chunk (C3 -3%,

@@ -53,6 +53,7 @@ struct device_plan {
     uint32_t ks_persist = 0;  // k_mfma_ks: persistent grid of this many workgroups pulling units (KS_PERSIST, experiments)
     bool nm_nt = false;       // k_nm_mfma: non-temporal panel loads (NM_NT)
     uint32_t nm_tiles = 8;    // k_nm_mfma: 16-row tiles per workgroup (mc_layout::nm_T)
+    bool lds_dma = false;     // k_lds_rows_dma: fp32 N = 32 chunks by LDS-DMA into two buffers (LDS_DMA)
     // merge path, MP_COL_PARTS: the columns (renumbered by degree, MP_COL_PERM) dealt round-robin
     // over mp_parts partitions; one k_merge_path per partition, each over its own CSR and wave
     // ranges, so every pass gathers B rows of one partition only (its hubs fit each XCD's L2)

@@ -113,7 +113,7 @@ constexpr int kLdsMaxU = 12;  // 16-B staging registers per thread (k_lds_rows M
 bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint64_t> &tb_bmw,
                      const std::vector<uint64_t> &bmw_rows, const std::vector<uint32_t> &row_ptr,
                      const std::vector<uint64_t> &col, uint64_t K, uint32_t N, uint32_t vbytes, size_t lds_budget,
-                     lds_tiles &t, std::string &why) {
+                     lds_tiles &t, std::string &why, bool dma = false) {
     const uint64_t nb = tb_rows.size() - 1;
     if (nb == 0 || K == 0) { why = "empty plan"; return false; }
     if ((N * vbytes) % 16 != 0) { why = "B rows are not whole 16-B units"; return false; }
@@ -145,7 +145,7 @@ bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uin
     const uint64_t nthr = 64ull * waves;
     const uint64_t max_kc = std::min<uint64_t>(K, 65536);
     // smallest chunk count whose largest segment still fits LDS and the staging registers
-    uint64_t nc = std::max<uint64_t>(1, (K * RSB + lds_budget / 2) / (lds_budget * 3 / 4));
+    uint64_t nc = std::max<uint64_t>(1, (K * RSB * (dma ? 2 : 1) + lds_budget / 2) / (lds_budget * 3 / 4));
     std::vector<uint32_t> cap_of(0);
     for (;; nc++) {
         uint64_t KC = (K + nc - 1) / nc;
@@ -171,7 +171,16 @@ bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uin
         }
         const uint64_t lds = KC * RSB + cap * ebytes + (rpw + 1) * 4;
         const uint64_t units = KC * UB + cap * ebytes / 16;
-        if (lds <= lds_budget && units <= (uint64_t)kLdsMaxU * nthr) {
+        if (dma) {  // k_lds_rows_dma: two buffers of B rows + columns + values (row offsets by scalar loads)
+            const uint64_t buf = KC * RSB + std::max<uint64_t>(cap, 8) * ebytes;
+            if (2 * buf <= lds_budget) {
+                t.KC = (uint32_t)KC;
+                t.nc = (uint32_t)ncc;
+                t.seg_cap = (uint32_t)std::max<uint64_t>(cap, 8);
+                t.lds_bytes = (size_t)(2 * buf + 15) / 16 * 16;
+                break;
+            }
+        } else if (lds <= lds_budget && units <= (uint64_t)kLdsMaxU * nthr) {
             t.KC = (uint32_t)KC;
             t.nc = (uint32_t)ncc;
             t.seg_cap = (uint32_t)std::max<uint64_t>(cap, 8);
@@ -710,11 +719,14 @@ void upload_plan(plan_state &p, int dtype, int device) {
                 std::string why;
                 const uint32_t Nd = (uint32_t)get_config().DENSE_MATRIX_SIZE;
                 const size_t budget = (size_t)std::min<int64_t>(get_config().SHARED_MEM_TOTAL_SIZE, 160 * 1024);
+                // LDS_DMA (fp32 at N = 32): chunks by LDS-DMA into two buffers (k_lds_rows_dma)
+                const bool dma = dtype == 0 && Nd == 32 && get_config().LDS_DMA != 0;
                 if (build_lds_tiles(m.u(TBLOCK_META, "first_row_indices", sb), m.u(TBLOCK_META, "first_BMW_indices", sb),
                                     m.u(WARP_META, "first_row_indices", sb), rp, col, p.K, Nd, dtype ? 2u : 4u, budget,
-                                    t, why)) {
+                                    t, why, dma)) {
                     d.lds = true;
-                    d.kernel = "k_lds_rows";
+                    d.lds_dma = dma;
+                    d.kernel = dma ? "k_lds_rows_dma" : "k_lds_rows";
                     // LDS_KSPLIT: S workgroups per BMTB, each over ncs consecutive chunks of K
                     // (every K range non-empty), fp32 slabs + one arrival counter per BMTB.  0 (auto):
                     // plans of under 128 BMTBs split K until ~256 workgroups (a workgroup's time

@@ -69,6 +69,32 @@ void launch_lds(const plan_state &p, const device_arrays &a, const VT *B, VT *C,
         }
         hipLaunchKernelGGL(kern, grid, block, d.lds_bytes, s, GS_LDS_ARGS);
     };
+    if constexpr (sizeof(VT) == 4 && CF == 4) {
+        if (d.lds_dma) {  // LDS_DMA: fp32 N = 32, chunks by LDS-DMA into two buffers
+            GS_CHECK(N == 32, "k_lds_rows_dma is built for N = 32");
+            auto gd = [&](auto kern) {
+                static std::mutex mu;
+                static std::map<std::pair<int, const void *>, size_t> granted;
+                {
+                    std::lock_guard<std::mutex> l(mu);
+                    size_t &g = granted[{d.device, reinterpret_cast<const void *>(kern)}];
+                    if (g < d.lds_bytes) {
+                        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.lds_bytes));
+                        g = d.lds_bytes;
+                    }
+                }
+                hipLaunchKernelGGL(kern, grid, block, d.lds_bytes, s, a.t0, a.a1, a.a0, a.t1, a.t2, (const uint16_t *)a.tcol,
+                                   (const float *)a.tval, (const float *)B, (float *)C, K, d.KC, d.nc, d.rpw_max, d.seg_cap,
+                                   (uint32_t)d.row_base, ksp, d.ncs, a.ws, a.t3);
+            };
+            if (d.maxr == 1) gd(gsk::k_lds_rows_dma<1>);
+            else if (d.maxr == 2) gd(gsk::k_lds_rows_dma<2>);
+            else gd(gsk::k_lds_rows_dma<4>);
+            return;
+        }
+    }
+    GS_CHECK(!d.lds_dma, "k_lds_rows_dma: fp32 plans at N = 32 only");
     if (d.maxr == 1) go(gsk::k_lds_rows<VT, CF, 1, kLdsMaxU>);
     else if (d.maxr == 2) go(gsk::k_lds_rows<VT, CF, 2, kLdsMaxU>);
     else go(gsk::k_lds_rows<VT, CF, 4, kLdsMaxU>);

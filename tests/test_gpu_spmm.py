@@ -330,7 +330,7 @@ def test_lds_stage_k_split(dtype, ksplit, no_mfma):
     finally:
         gsa.set_config("LDS_KSPLIT", 0)
     info = plan.info()
-    assert info["device_kernel"] == "k_lds_rows" and info["ksplit"] > 1, info
+    assert info["device_kernel"].startswith("k_lds_rows") and info["ksplit"] > 1, info
     if ksplit:
         assert info["ksplit"] == ksplit, info
     v = val.astype(np.float16).astype(np.float32) if dtype == "f16" else val
@@ -342,6 +342,31 @@ def test_lds_stage_k_split(dtype, ksplit, no_mfma):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(C2.float().cpu().numpy(), C)
     plan.free()
+
+
+@pytest.mark.parametrize("ksplit", [1, 0, 3])
+def test_lds_stage_dma_fp32(ksplit, no_mfma):
+    """LDS_DMA (fp32, N = 32): k_lds_rows_dma stages every chunk's B rows and A segment by
+    LDS-DMA into two buffers (chunk j+1 lands while chunk j is computed): against the oracle on
+    every LDS case (including 40,000 columns: many chunks), with and without the K split, and a
+    relaunch into NaN-filled C bit for bit"""
+    assert gsa.get_config("LDS_DMA") == 1  # the default
+    gsa.set_config("LDS_KSPLIT", ksplit)
+    try:
+        for case, M, K, row, col, val in lds_cases():
+            for p0, p1 in ((20, 2), (16, 4), (64, 4)):
+                plan, C, B = run(M, K, row, col, val, "tblock_warp_total", p0, p1, 32, "f32")
+                info = plan.info()
+                assert info["device_kernel"] == "k_lds_rows_dma", (case, info)
+                check(C, ofi.spmm_ref(M, 32, row, col, val, B, "f64"), "f32", plan)
+                Bt = torch.from_numpy(B).to(DEV)
+                C2 = torch.full((M, 32), float("nan"), device=DEV)
+                plan.spmm(Bt, C=C2)
+                torch.cuda.synchronize()
+                np.testing.assert_array_equal(C2.cpu().numpy(), C)
+                plan.free()
+    finally:
+        gsa.set_config("LDS_KSPLIT", 0)
 
 
 @pytest.mark.parametrize("dtype", ["f32", "f16"])
