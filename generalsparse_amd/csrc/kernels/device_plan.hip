@@ -718,9 +718,12 @@ void upload_plan(plan_state &p, int dtype, int device) {
                 lds_tiles t;
                 std::string why;
                 const uint32_t Nd = (uint32_t)get_config().DENSE_MATRIX_SIZE;
-                const size_t budget = (size_t)std::min<int64_t>(get_config().SHARED_MEM_TOTAL_SIZE, 160 * 1024);
-                // LDS_DMA (fp32 at N = 32): chunks by LDS-DMA into two buffers (k_lds_rows_dma)
+                size_t budget = (size_t)std::min<int64_t>(get_config().SHARED_MEM_TOTAL_SIZE, 160 * 1024);
+                // LDS_DMA (fp32 at N = 32): chunks by LDS-DMA into two buffers (k_lds_rows_dma), at most
+                // 80 KB per workgroup so two share a CU (their barriers and DMA waits interleave; the auto
+                // K split below makes the grid two per CU): C2 fp32 (20,2) 37.7 -> 34.4 us (r06r)
                 const bool dma = dtype == 0 && Nd == 32 && get_config().LDS_DMA != 0;
+                if (dma) budget = std::min<size_t>(budget, 80 * 1024);
                 if (build_lds_tiles(m.u(TBLOCK_META, "first_row_indices", sb), m.u(TBLOCK_META, "first_BMW_indices", sb),
                                     m.u(WARP_META, "first_row_indices", sb), rp, col, p.K, Nd, dtype ? 2u : 4u, budget,
                                     t, why, dma)) {
@@ -732,10 +735,12 @@ void upload_plan(plan_state &p, int dtype, int device) {
                     // plans of under 128 BMTBs split K until ~256 workgroups (a workgroup's time
                     // is its nonzeros: C2 fp32 (20,2) 41.5 us = (40,4) in 2 K ranges 44.5 us,
                     // profiles/r06f_lds_ksplit.txt, so full grids gain nothing from a split)
+                    // With LDS-DMA (two workgroups per CU) the auto split aims at ~512 workgroups.
                     const uint64_t nbt0 = m.u(TBLOCK_META, "first_row_indices", sb).size() - 1;
                     const int64_t cfg_ks = get_config().LDS_KSPLIT;
+                    const uint64_t wg_aim = dma ? 512 : 256;
                     const uint32_t want = cfg_ks > 0 ? (uint32_t)cfg_ks
-                                                     : (nbt0 < 128 ? (uint32_t)std::max<uint64_t>(1, 256 / std::max<uint64_t>(nbt0, 1)) : 1u);
+                                                     : (nbt0 * 2 <= wg_aim ? (uint32_t)std::max<uint64_t>(1, wg_aim / std::max<uint64_t>(nbt0, 1)) : 1u);
                     const uint32_t ncs = (t.nc + std::min(want, t.nc) - 1) / std::min(want, t.nc);
                     d.ksplit = (t.nc + ncs - 1) / ncs;
                     d.ncs = ncs;
