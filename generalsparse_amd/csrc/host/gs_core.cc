@@ -145,6 +145,7 @@ void apply_kv(config_t &c, const std::string &k, const std::string &v) {
     else if (k == "LDS_KSPLIT") c.LDS_KSPLIT = i();
     else if (k == "LDS_DMA") c.LDS_DMA = i();
     else if (k == "MP_COL_PARTS") c.MP_COL_PARTS = i();
+    else if (k == "MP_HUB_COLS") c.MP_HUB_COLS = i();
     else if (k == "KS_PERSIST") c.KS_PERSIST = i();
     else if (k == "KS_HEAD") c.KS_HEAD = i();
     else if (k == "NM_NT") c.NM_NT = i();
@@ -234,7 +235,7 @@ int64_t get_config_int(const std::string &k) {
     GS_KEY(SHARED_MEM_TOTAL_SIZE) GS_KEY(MAX_DIV_TIMES_OF_DIV) GS_KEY(MFMA_GLDS) GS_KEY(MFMA_COMPUTE_WAVES)
     GS_KEY(MFMA_GLDS_NBUF) GS_KEY(MODEL_DRIVEN_COMPRESS) GS_KEY(LDS_STAGE_B) GS_KEY(MFMA_TILES) GS_KEY(MFMA_KROT)
     GS_KEY(WARP_ROWS_GROUPS) GS_KEY(WARP_ROWS_CHUNKS) GS_KEY(MFMA_MAX_FILL) GS_KEY(NM_MFMA) GS_KEY(MFMA_KSPLIT) GS_KEY(MFMA_KS)
-    GS_KEY(NM_KS) GS_KEY(NM_SPLIT) GS_KEY(MFMA_FLAGS) GS_KEY(MFMA_BM) GS_KEY(BM_SPLIT) GS_KEY(BM_WAVES) GS_KEY(BM_V2) GS_KEY(BM_KB) GS_KEY(KS_MIN_ROWS) GS_KEY(KS_SPLIT) GS_KEY(KS_WAVES) GS_KEY(KS_PRIO) GS_KEY(KS_FORCE_TIMEOUT) GS_KEY(KS_APART) GS_KEY(NM_V4) GS_KEY(KS_POS8) GS_KEY(KS_NT) GS_KEY(NM_KROT) GS_KEY(NM_TILES) GS_KEY(LDS_KSPLIT) GS_KEY(LDS_DMA) GS_KEY(MP_COL_PARTS) GS_KEY(KS_PERSIST) GS_KEY(KS_HEAD) GS_KEY(NM_NT) GS_KEY(MP_ROWS) GS_KEY(MP_SOLO) GS_KEY(MP_COL_PERM) GS_KEY(MP_PERM_HOT) GS_KEY(MP_PERM_SCATTER)
+    GS_KEY(NM_KS) GS_KEY(NM_SPLIT) GS_KEY(MFMA_FLAGS) GS_KEY(MFMA_BM) GS_KEY(BM_SPLIT) GS_KEY(BM_WAVES) GS_KEY(BM_V2) GS_KEY(BM_KB) GS_KEY(KS_MIN_ROWS) GS_KEY(KS_SPLIT) GS_KEY(KS_WAVES) GS_KEY(KS_PRIO) GS_KEY(KS_FORCE_TIMEOUT) GS_KEY(KS_APART) GS_KEY(NM_V4) GS_KEY(KS_POS8) GS_KEY(KS_NT) GS_KEY(NM_KROT) GS_KEY(NM_TILES) GS_KEY(LDS_KSPLIT) GS_KEY(LDS_DMA) GS_KEY(MP_COL_PARTS) GS_KEY(MP_HUB_COLS) GS_KEY(KS_PERSIST) GS_KEY(KS_HEAD) GS_KEY(NM_NT) GS_KEY(MP_ROWS) GS_KEY(MP_SOLO) GS_KEY(MP_COL_PERM) GS_KEY(MP_PERM_HOT) GS_KEY(MP_PERM_SCATTER)
 #undef GS_KEY
     throw gs_error("get_config_int: no integer key " + k);
 }

@@ -123,6 +123,7 @@ struct config_t {
     int64_t KS_HEAD = 1;         // k_mfma_ks: the head steps (each wave's first kKsDepth k-steps) at fixed, padded
                                  // places, loaded without their records (when the padding costs <= 6% more groups)
     int64_t KS_PERSIST = 0;      // k_mfma_ks: persistent grid size pulling (row block, K range) units (experiments build)
+    int64_t MP_HUB_COLS = 0;     // MP_COL_PARTS = 2: partition 0 = this many densest columns (0: round-robin)
     int64_t MP_COL_PARTS = 0;    // merge path with MP_COL_PERM, fp32: column partitions, one pass each (0/1: off)
     int64_t LDS_DMA = 1;         // k_lds_rows at fp32 N = 32: chunks by LDS-DMA into two buffers (k_lds_rows_dma)
     int64_t LDS_KSPLIT = 0;      // k_lds_rows: workgroups per BMTB, each over a K range (fp32 slab combine; 0 auto)

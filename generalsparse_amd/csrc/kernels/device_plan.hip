@@ -310,10 +310,20 @@ static void upload_col_parts(plan_state &p, device_arrays &a, const std::vector<
     for (uint32_t i = 0; i < (uint32_t)K; i++) perm[i] = i;
     std::stable_sort(perm.begin(), perm.end(), [&](uint32_t x, uint32_t y) { return deg[x] > deg[y]; });
     std::vector<uint64_t> base(P + 1, 0);
-    for (uint32_t x = 0; x < P; x++) base[x + 1] = base[x] + (K > x ? (K - x + P - 1) / P : 0);
+    // MP_HUB_COLS = H (P = 2): partition 0 = the H densest columns (the hubs, whose B rows stay in
+    // the XCDs' L2s, so a round of that pass never waits on an Infinity-Cache / HBM gather),
+    // partition 1 = the rest; else ranks are dealt round-robin over the P partitions
+    const uint64_t hub = P == 2 ? (uint64_t)std::max<int64_t>(0, get_config().MP_HUB_COLS) : 0;
+    if (hub > 0 && hub < K) {
+        base[1] = hub;
+        base[2] = K;
+    } else {
+        for (uint32_t x = 0; x < P; x++) base[x + 1] = base[x] + (K > x ? (K - x + P - 1) / P : 0);
+    }
     std::vector<uint32_t> gather(K);
     for (uint32_t r = 0; r < (uint32_t)K; r++) {
-        const uint32_t c = perm[r], q = (uint32_t)(base[r % P] + r / P);
+        const uint32_t c = perm[r];
+        const uint32_t q = hub > 0 && hub < K ? r : (uint32_t)(base[r % P] + r / P);
         pos[c] = q;
         gather[q] = c;
     }

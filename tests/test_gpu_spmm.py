@@ -979,10 +979,10 @@ def test_merge_path_matches_oracle(ws, level, N, dtype, merge_walk):
         check(C, ref, dtype, plan)
 
 
-@pytest.mark.parametrize("parts", [2, 4, 8])
+@pytest.mark.parametrize("parts,hub", [(2, 0), (4, 0), (8, 0), (2, 300)])
 @pytest.mark.parametrize("N", [8, 3, 32])
 @pytest.mark.parametrize("ws", [512, 37])
-def test_merge_path_column_partitions(parts, N, ws):
+def test_merge_path_column_partitions(parts, hub, N, ws):
     """MP_COL_PARTS (fp32 merge-path plans with MP_COL_PERM): the degree-ranked columns dealt
     over P partitions, one k_merge_path pass per partition over its own CSR and wave ranges,
     the partitions' fp32 outputs added to C in partition order: against the oracle, relaunches
@@ -998,10 +998,12 @@ def test_merge_path_column_partitions(parts, N, ws):
     B = np.random.default_rng(4).uniform(-1, 1, (M, N)).astype(np.float32)
     gsa.set_config("MP_COL_PERM", 1)
     gsa.set_config("MP_COL_PARTS", parts)
+    gsa.set_config("MP_HUB_COLS", hub)  # (2, 300): the 300 densest columns, then the rest
     try:
         plan = gsa.Plan.from_coo(M, M, row, col, val).run_pipeline("merge_path", N, ws, 1).compile().upload("f32", 0)
     finally:
         gsa.set_config("MP_COL_PARTS", 0)
+        gsa.set_config("MP_HUB_COLS", 0)
         gsa.set_config("MP_COL_PERM", -1)
     assert plan.info()["device_kernel"] == "k_merge_path"
     Bt = torch.from_numpy(B).to(DEV)
