@@ -321,7 +321,6 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
         why = "row blocks too sparse for dense tiles";
         return false;
     }
-    // K ranges: enough workgroups for the 256 CUs (each reads only its range's B rows)
     // KS_APART: the overlapped layout (0) is built for N = 32 and row tiles 2..5; auto (-1) keeps the
     // apart layout only when it holds as many workgroups per CU as the overlapped one
     {
@@ -332,12 +331,6 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     }
     t.lds_bytes = gsk::ks_lds_bytes(CT, RT, W, t.AP);
     if (t.lds_bytes > 160 * 1024) { why = "k_mfma_ks wave stages exceed LDS"; return false; }
-    uint64_t S = s_cfg > 0 ? (uint64_t)s_cfg : std::min<uint64_t>(8, (256 + nb - 1) / nb);
-    S = std::max<uint64_t>(1, std::min<uint64_t>(S, (K + 31) / 32));
-    uint64_t KR = ((K + S - 1) / S + 31) / 32 * 32;
-    S = (K + KR - 1) / KR;
-    t.S = (uint32_t)S;
-    t.NS = (uint32_t)(KR / 32);
     t.RT = RT;
     t.RMAX = (uint32_t)rmax;
     t.W = W;
@@ -348,7 +341,7 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
     uint64_t gmax = 1;
     {
         const uint32_t nsg = 4 * RT;
-        std::vector<uint32_t> cnt((size_t)S * t.NS * (t.P8 ? nsg : 1u));
+        std::vector<uint32_t> cnt((size_t)((K + 31) / 32) * (t.P8 ? nsg : 1u));
         for (uint64_t g = 0; g < nb; g++) {
             std::fill(cnt.begin(), cnt.end(), 0u);
             for (uint64_t r = tb_rows[g]; r < tb_rows[g + 1]; r++)
@@ -360,7 +353,7 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
                         cnt[st]++;
                 }
             if (t.P8) {
-                for (size_t st = 0; st < (size_t)S * t.NS; st++) {
+                for (size_t st = 0; st < cnt.size() / nsg; st++) {
                     uint64_t ngs = 0;
                     for (uint32_t k = 0; k < nsg; k++) ngs += (cnt[st * nsg + k] + 7) / 8;
                     gmax = std::max<uint64_t>(gmax, ngs);
@@ -370,6 +363,32 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
             }
         }
     }
+    t.GCAP = (uint32_t)gmax;
+    t.MAXG = gmax <= 64 ? 1 : (gmax <= 128 ? 2 : (gmax <= 192 ? 3 : (gmax <= 256 ? 4 : 0)));
+    if (!t.MAXG) { why = "a k-step holds more than 256 entry groups"; return false; }
+    if (t.CT == 8 && !ks_ct8_fits(RT, t.MAXG)) {  // a 128-column instantiation that would spill: 64-column tiles
+        t.CT = 4;
+        t.NT = 0;  // (KS_NT is built for 32- and 128-column tiles)
+        t.lds_bytes = gsk::ks_lds_bytes(4, RT, W, t.AP);
+    }
+    if (!t.AP && t.MAXG > 2 && W != 4) {  // the 8-wave overlapped layout is instantiated for MAXG <= 2 only
+        t.AP = true;
+        t.lds_bytes = gsk::ks_lds_bytes(t.CT, RT, W, true);
+        if (t.lds_bytes > 160 * 1024) { why = "k_mfma_ks wave stages exceed LDS"; return false; }
+    }
+    // K ranges (auto): enough workgroups for the 256 CUs over row blocks x column tiles (the grid's
+    // y dimension: N = 128 on 64-column tiles is two) -- each workgroup reads only its range's B rows,
+    // and a split past one CU round adds B rows per CU and a slab combine without filling more CUs
+    // (C2 N = 128, 80-row blocks: 2 K ranges x 2 column tiles 21.5 us, 4 K ranges 33.4 us; r06x)
+    {
+        const uint64_t ctiles = ks_col_tiles_ct(N, t.CT);
+        uint64_t S = s_cfg > 0 ? (uint64_t)s_cfg : std::min<uint64_t>(8, (256 + nb * ctiles - 1) / (nb * ctiles));
+        S = std::max<uint64_t>(1, std::min<uint64_t>(S, (K + 31) / 32));
+        const uint64_t KR = ((K + S - 1) / S + 31) / 32 * 32;
+        t.S = (uint32_t)((K + KR - 1) / KR);
+        t.NS = (uint32_t)(KR / 32);
+    }
+    const uint64_t S = t.S, KR = (uint64_t)t.NS * 32;
     // head steps (ks_tiles::GH): used when padding them to the largest costs at most 6% more groups
     const uint32_t HS = std::min<uint32_t>(W * kKsDepth, t.NS);  // head slots per unit
     if (!t.P8 && get_config().KS_HEAD) {
@@ -390,19 +409,6 @@ bool build_ks_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint
         }
         const uint64_t padded = (uint64_t)nb * S * HS * gh;
         if ((double)(padded - head_groups) <= 0.06 * (double)all_groups && (double)padded < 2.0e9) t.GH = (uint32_t)gh;
-    }
-    t.GCAP = (uint32_t)gmax;
-    t.MAXG = gmax <= 64 ? 1 : (gmax <= 128 ? 2 : (gmax <= 192 ? 3 : (gmax <= 256 ? 4 : 0)));
-    if (!t.MAXG) { why = "a k-step holds more than 256 entry groups"; return false; }
-    if (t.CT == 8 && !ks_ct8_fits(RT, t.MAXG)) {  // a 128-column instantiation that would spill: 64-column tiles
-        t.CT = 4;
-        t.NT = 0;  // (KS_NT is built for 32- and 128-column tiles)
-        t.lds_bytes = gsk::ks_lds_bytes(4, RT, W, t.AP);
-    }
-    if (!t.AP && t.MAXG > 2 && W != 4) {  // the 8-wave overlapped layout is instantiated for MAXG <= 2 only
-        t.AP = true;
-        t.lds_bytes = gsk::ks_lds_bytes(t.CT, RT, W, true);
-        if (t.lds_bytes > 160 * 1024) { why = "k_mfma_ks wave stages exceed LDS"; return false; }
     }
     // 32-bit group and step indices (packed steps: about nnz / 8 + nb*S*NS groups; checked
     // exactly after the build): too large a plan falls back to another kernel
