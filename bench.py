@@ -1089,7 +1089,9 @@ def rocsparse_compare(gsa, M, K, N, row, col, val, dt, cands, args, local, flops
     if rs16:
         res["speedup_vs_rocsparse"] = round(ours / rs16["gflops"], 3)
     tried, best32 = {}, None
-    for cand in cands:
+    from generalsparse_amd import autotune as at
+    extra = at.F32_EXTRA.get(at.WORKLOAD_CLASS.get(args.workload, ""), []) if args.pipeline == "auto" else []
+    for cand in list(cands) + [c for c in extra if c not in cands]:
         if len(cand) > 3:  # config variants of the fp16 matrix-core kernels (KS_NT, NM_NT): no fp32 plan
             continue
         key = cand_key(cand)

@@ -39,6 +39,10 @@ CANDIDATES = {
     "f32_powerlaw_large": [("merge_path", 512, 1), ("merge_path", 1024, 1), ("merge_path", 2048, 1),
                            ("merge_path", 1024, 1, {"MP_COL_PARTS": 4})],
 }
+# plans that exist only in the fp32 form of a class: k_lds_rows_rs (fp32 at N = 32, BMWs of 5..8
+# rows, one row per slot -- C2 fp32 30.1 us at (64,8) against 34.5 us for k_lds_rows_dma's (20,2),
+# profiles/r06y_lds_rows_rs.txt); the fp32 comparator of an fp16 class searches these as well
+F32_EXTRA = {"f16": [("tblock_warp_total", 64, 8), ("tblock_warp_total", 72, 8)]}
 # the bench workloads (BASELINE.json configs) and the class each searches
 WORKLOAD_CLASS = {"c1": "f32", "c2": "f16", "c3": "f16_2to4", "c4": "f32_powerlaw", "c4o": "f32_powerlaw_large"}
 
@@ -78,7 +82,7 @@ def candidates_for(M, K, nnz, dtype, two_four=False, powerlaw=False):
         return c
     if powerlaw:
         return list(CANDIDATES["f32_powerlaw_large" if nnz > 50_000_000 else "f32_powerlaw"])
-    return list(CANDIDATES["f32"])
+    return list(CANDIDATES["f32"]) + [c for c in F32_EXTRA["f16"] if c not in CANDIDATES["f32"]]
 
 
 def cand_key(c):

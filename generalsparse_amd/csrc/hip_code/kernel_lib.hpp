@@ -1365,6 +1365,148 @@ __global__ __launch_bounds__(1024) void k_lds_rows_dma(
 }
 
 // ---------------------------------------------------------------------------
+// k_lds_rows_rs -- k_lds_rows_dma with one row per slot (fp32, N = 32, BMWs of 5..8 rows): slot s of
+// a wave walks row s of its BMW four entries at a time (its 8 lanes x 16 B cover the row of C), so
+// a row's chunk segment costs ceil(len / 4) iterations of the slot instead of ceil(len / 32) of the
+// whole wave per row (k_lds_rows_dma: a 72-entry segment runs 3 iterations = 96 slots, 75% used),
+// and no cross-slot reduction is left at the end.  Taller BMTBs (64 rows in 8-row BMWs) also cut
+// the B rows a CU stages per nonzero.  Bank order (device_plan.hip, rowslot): slots {0, 1, 4, 5}
+// take entries of column parity k & 1, slots {2, 3, 6, 7} the opposite, so the ds_read_b128 lane
+// groups (slots {0,3} and {1,2} of each half-wave) read rows of opposite parity while both kinds
+// last.  A slot's row offsets in the chunk come by vector loads (one per chunk, issued with the
+// chunk's DMA).  Same DMA double buffer, K split and slab combine as k_lds_rows_dma.
+// The chunks' DMA is issued by inline asm (lds_dma16): with the builtin, hipcc's wait inserter puts a
+// vmcnt(0) before every LDS read of the issuing wave (the DMA writes LDS), so each wave would wait
+// for its share of chunk j+1 before computing chunk j; the kernel retires the DMA itself with
+// vmcnt(0) right before each chunk barrier, the only point where the other buffer changes hands.
+// (RS: rows per slot, 1; a template so that every translation unit's copy is one symbol)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void lds_dma16(const void *src, const unsigned char *dst) {
+    const uint32_t la = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char *)dst);
+    __asm__ volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(la) : "memory");
+}
+template <int RS = 1>
+__global__ __launch_bounds__(1024) void k_lds_rows_rs(
+    const uint32_t *__restrict__ bmtb_first_row, const uint32_t *__restrict__ bmw_of_bmtb,
+    const uint32_t *__restrict__ bmw_first_row, const uint32_t *__restrict__ seg_start,
+    const uint32_t *__restrict__ seg_row_off, const uint16_t *__restrict__ tcol, const float *__restrict__ tval,
+    const float *__restrict__ B, float *__restrict__ C, uint32_t K, uint32_t KC, uint32_t nc, uint32_t rpw_max,
+    uint32_t seg_cap, uint32_t row_base, uint32_t ksp, uint32_t ncs, float *__restrict__ slabs,
+    uint32_t *__restrict__ arrivals) {
+    constexpr uint32_t N = 32, CF = 4, X = 8, RSB = 128;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint32_t tid = threadIdx.x, nthr = blockDim.x, nwv = nthr >> 6;
+    const uint32_t lane = tid & 63u, wib = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t xl = lane & (X - 1u), slot = lane / X;
+    const uint32_t g = ksp > 1u ? blockIdx.x / ksp : blockIdx.x, q = ksp > 1u ? blockIdx.x % ksp : 0u;
+    const uint32_t j0 = q * (ksp > 1u ? ncs : 0u), j1 = ksp > 1u ? min(nc, j0 + ncs) : nc;
+    const uint32_t r_first = bmtb_first_row[g];
+    const uint32_t bmw = bmw_of_bmtb[g] + wib;
+    uint32_t t0 = 0, nt = 0;
+    if (bmw < bmw_of_bmtb[g + 1]) {
+        t0 = bmw_first_row[bmw] - r_first;
+        nt = bmw_first_row[bmw + 1] - bmw_first_row[bmw];
+    }
+    t0 = __builtin_amdgcn_readfirstlane(t0);
+    nt = __builtin_amdgcn_readfirstlane(nt);
+    const bool has_row = slot < nt;
+    const uint32_t rl = t0 + (has_row ? slot : 0u);  // this slot's row in the BMTB (rl + 1 <= rpw_max)
+    const uint32_t lB = KC * RSB, lV = lB + seg_cap * 2u, szBuf = lV + seg_cap * 4u;
+    const uint32_t cb = xl * 16u;
+    float acc[CF] = {0.f, 0.f, 0.f, 0.f};
+    auto issue = [&](uint32_t j, uint32_t b) {
+        unsigned char *dst = lds + b * szBuf;
+        const uint32_t kc0 = j * KC, rows = min(KC, K - kc0);
+        const uint32_t s0 = seg_start[g * nc + j], len = seg_start[g * nc + j + 1] - s0;
+        const unsigned char *srcs[3] = {reinterpret_cast<const unsigned char *>(B + (size_t)kc0 * N),
+                                        reinterpret_cast<const unsigned char *>(tcol + s0),
+                                        reinterpret_cast<const unsigned char *>(tval + s0)};
+        const uint32_t units[3] = {rows * (RSB / 16u), len / 8u, len / 4u};
+        const uint32_t dofs[3] = {0u, lB, lV};
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            for (uint32_t ib = wib; ib * 64u < units[r]; ib += nwv) {
+                const uint32_t u = ib * 64u + lane;
+                if (u < units[r]) lds_dma16(srcs[r] + (size_t)u * 16u, dst + dofs[r] + ib * 1024u);
+            }
+        }
+    };
+    // the slot's row bounds in chunk j (segment-relative entry indices)
+    auto row_off = [&](uint32_t j) {
+        const uint32_t *ro = seg_row_off + (size_t)(g * nc + j) * (rpw_max + 1) + rl;
+        return make_uint2(ro[0], ro[1]);
+    };
+    uint2 ro_n = row_off(j0);
+    issue(j0, 0u);
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // chunk j0 landed
+    for (uint32_t j = j0; j < j1; j++) {
+        const uint32_t b = (j - j0) & 1u;
+        const uint2 ro = ro_n;
+        if (j + 1 < j1) {
+            ro_n = row_off(j + 1);
+            issue(j + 1, b ^ 1u);  // lands while chunk j is computed
+        }
+        const unsigned char *lAc = lds + b * szBuf + lB;
+        const unsigned char *lAv = lds + b * szBuf + lV;
+        const unsigned char *lBb = lds + b * szBuf + cb;
+        if (has_row) {
+            for (uint32_t p0 = ro.x; p0 < ro.y; p0 += 4u) {
+                const uint2 craw = *reinterpret_cast<const uint2 *>(lAc + p0 * 2u);
+                const uint32_t cc[4] = {craw.x & 0xffffu, craw.x >> 16, craw.y & 0xffffu, craw.y >> 16};
+                uint4 braw[4];
+#pragma unroll
+                for (int qq = 0; qq < 4; qq++) braw[qq] = *reinterpret_cast<const uint4 *>(lBb + cc[qq] * RSB);
+                const float4 vv = *reinterpret_cast<const float4 *>(lAv + p0 * 4u);
+                const float vq[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+                for (int qq = 0; qq < 4; qq++) {
+                    float bt[CF];
+                    __builtin_memcpy(bt, &braw[qq], 16);
+#pragma unroll
+                    for (int k = 0; k < CF; k++) acc[k] = __builtin_fmaf(vq[qq], bt[k], acc[k]);
+                }
+            }
+        }
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // chunk j+1 landed (every wave's vmcnt(0)), chunk j consumed
+    }
+    const uint32_t c0 = xl * CF;
+    if (ksp <= 1u) {
+        if (has_row) store_f32<float, CF>(C + (size_t)(r_first + rl + row_base) * N + c0, acc);
+        return;
+    }
+    // K-split hand-off: as k_lds_rows_dma (sc1 slab stores, vmcnt(0), barrier, one arrival add)
+    const size_t slab_rows = (size_t)rpw_max;
+    if (has_row) {
+        float *dst = slabs + (((size_t)g * ksp + q) * slab_rows + rl) * N + c0;
+        const f4v v = {acc[0], acc[1], acc[2], acc[3]};
+        __asm__ volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(v) : "memory");
+    }
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    uint32_t *flag = reinterpret_cast<uint32_t *>(lds);
+    if (tid == 0) *flag = __hip_atomic_fetch_add(arrivals + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*flag != ksp - 1u) return;
+    if (tid == 0) __hip_atomic_store(arrivals + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!has_row) return;
+    float sum[CF] = {0.f, 0.f, 0.f, 0.f};
+    for (uint32_t qq = 0; qq < ksp; qq++) {
+        if (qq == q) {
+#pragma unroll
+            for (int k = 0; k < CF; k++) sum[k] += acc[k];
+            continue;
+        }
+        const float *src = slabs + (((size_t)g * ksp + qq) * slab_rows + rl) * N + c0;
+#pragma unroll
+        for (int k = 0; k < CF; k++) sum[k] += __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    store_f32<float, CF>(C + (size_t)(r_first + rl + row_base) * N + c0, sum);
+}
+
+// ---------------------------------------------------------------------------
 // BMTB row blocks on the matrix cores (MI355X layout of a tblock/warp/block-
 // total plan whose row blocks are dense enough).  Workgroup g owns BMTB g
 // (R <= RMAX <= 16*RT rows) and walks K in chunks of KC = 2^LGKC columns.

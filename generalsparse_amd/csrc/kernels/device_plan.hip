@@ -131,8 +131,10 @@ bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uin
         for (uint64_t w = w0; w < w1; w++) maxr = std::max<uint32_t>(maxr, (uint32_t)(bmw_rows[w + 1] - bmw_rows[w]));
     }
     if (waves > 16) { why = "more than 16 BMWs per BMTB"; return false; }
-    if (maxr > 4) { why = "more than 4 rows per BMW"; return false; }
-    maxr = maxr <= 1 ? 1 : (maxr <= 2 ? 2 : 4);
+    // BMWs of 5..8 rows: one row per slot (k_lds_rows_rs; fp32 N = 32 by LDS-DMA only)
+    const bool rowslot = dma && vbytes == 4 && N == 32 && maxr > 4 && maxr <= 8;
+    if (maxr > 4 && !rowslot) { why = "more than 4 rows per BMW"; return false; }
+    maxr = maxr <= 1 ? 1 : (maxr <= 2 ? 2 : (maxr <= 4 ? 4 : 8));
     // B rows in LDS at an odd count of 16-B units (bank spread for random rows), except fp32 at
     // N = 32 (8 lanes x 16 B per row, 8 slots per wave): rows at 128 B, so a row starts on bank 0
     // or 32 by its parity, and each row's entries are ordered so that the slots whose B reads
@@ -196,9 +198,13 @@ bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uin
     t.seg_start.assign(1, 0);
     t.seg_row_off.assign(nb * t.nc * (rpw + 1), 0);
     std::vector<uint64_t> cur(rpw);
+    std::vector<uint32_t> slot_of(rpw);  // rowslot: a row's slot = its place in its BMW
     for (uint64_t g = 0; g < nb; g++) {
         const uint64_t r0 = tb_rows[g], nr = tb_rows[g + 1] - r0;
         for (uint64_t i = 0; i < nr; i++) cur[i] = row_ptr[r0 + i];
+        if (rowslot)
+            for (uint64_t w = tb_bmw[g]; w < tb_bmw[g + 1]; w++)
+                for (uint64_t r = bmw_rows[w]; r < bmw_rows[w + 1]; r++) slot_of[r - r0] = (uint32_t)(r - bmw_rows[w]);
         for (uint32_t j = 0; j < t.nc; j++) {
             const uint64_t lim = (uint64_t)(j + 1) * t.KC, base = t.tcol.size();
             uint32_t *off = &t.seg_row_off[(g * t.nc + j) * (rpw + 1)];
@@ -212,7 +218,24 @@ bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uin
                 }
                 cur[i] = e;
                 while ((t.tcol.size() - base) % 4) { t.tcol.push_back(0); t.src.push_back(~0u); }
-                if (pair_banks) {
+                if (rowslot) {
+                    // slot s reads entry 4i + q of its row in the q-th read of iteration i: slots
+                    // {0,1,4,5} take column parity k & 1 at entry k, slots {2,3,6,7} the opposite
+                    // (the b128 lane groups pair slots {0,3} and {1,2} of each half-wave)
+                    const size_t rs = base + off[i], re = t.tcol.size();
+                    const uint32_t ph = (slot_of[i] & 2u) ? 1u : 0u;
+                    std::vector<std::pair<uint16_t, uint32_t>> ev, od;
+                    for (size_t k = rs; k < re; k++) (t.tcol[k] & 1u ? od : ev).push_back({t.tcol[k], t.src[k]});
+                    std::reverse(ev.begin(), ev.end());
+                    std::reverse(od.begin(), od.end());
+                    for (size_t k = rs; k < re; k++) {
+                        const bool want_odd = ((k - rs + ph) & 1u) != 0u;
+                        auto &v = (want_odd && !od.empty()) || ev.empty() ? od : ev;
+                        t.tcol[k] = v.back().first;
+                        t.src[k] = v.back().second;
+                        v.pop_back();
+                    }
+                } else if (pair_banks) {
                     // per 32-entry block of the row (slot s takes entries 4s..4s+3, entry q in the
                     // q-th read): the reads of slots (0,3), (1,2), (4,7), (5,6) at one q get one
                     // even and one odd column while both kinds last (any entry order sums the row)
@@ -739,7 +762,7 @@ void upload_plan(plan_state &p, int dtype, int device) {
                                     t, why, dma)) {
                     d.lds = true;
                     d.lds_dma = dma;
-                    d.kernel = dma ? "k_lds_rows_dma" : "k_lds_rows";
+                    d.kernel = t.maxr == 8 ? "k_lds_rows_rs" : (dma ? "k_lds_rows_dma" : "k_lds_rows");
                     // LDS_KSPLIT: S workgroups per BMTB, each over ncs consecutive chunks of K
                     // (every K range non-empty), fp32 slabs + one arrival counter per BMTB.  0 (auto):
                     // plans of under 128 BMTBs split K until ~256 workgroups (a workgroup's time

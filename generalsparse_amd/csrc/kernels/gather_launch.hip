@@ -88,7 +88,8 @@ void launch_lds(const plan_state &p, const device_arrays &a, const VT *B, VT *C,
                                    (const float *)a.tval, (const float *)B, (float *)C, K, d.KC, d.nc, d.rpw_max, d.seg_cap,
                                    (uint32_t)d.row_base, ksp, d.ncs, a.ws, a.t3);
             };
-            if (d.maxr == 1) gd(gsk::k_lds_rows_dma<1>);
+            if (d.maxr == 8) gd(gsk::k_lds_rows_rs<1>);  // one row per slot (BMWs of 5..8 rows)
+            else if (d.maxr == 1) gd(gsk::k_lds_rows_dma<1>);
             else if (d.maxr == 2) gd(gsk::k_lds_rows_dma<2>);
             else gd(gsk::k_lds_rows_dma<4>);
             return;

@@ -369,6 +369,36 @@ def test_lds_stage_dma_fp32(ksplit, no_mfma):
         gsa.set_config("LDS_KSPLIT", 0)
 
 
+@pytest.mark.parametrize("ksplit", [1, 0, 3])
+def test_lds_stage_rowslot_fp32(ksplit, no_mfma):
+    """BMWs of 5..8 rows at fp32, N = 32: k_lds_rows_rs (one row per slot, rows' entries in the
+    slot-parity order) against the oracle on every LDS case, with and without the K split, a
+    relaunch into NaN-filled C bit for bit, and the all-ones known answer exactly
+    (code_generator.cc:633-637: every C[i][j] is row i's nonzero count)"""
+    gsa.set_config("LDS_KSPLIT", ksplit)
+    try:
+        for case, M, K, row, col, val in lds_cases():
+            for p0, p1 in ((64, 8), (40, 5), (48, 6), (16, 8)):
+                plan, C, B = run(M, K, row, col, val, "tblock_warp_total", p0, p1, 32, "f32")
+                info = plan.info()
+                assert info["device_kernel"] == "k_lds_rows_rs", (case, p0, p1, info)
+                check(C, ofi.spmm_ref(M, 32, row, col, val, B, "f64"), "f32", plan)
+                Bt = torch.from_numpy(B).to(DEV)
+                C2 = torch.full((M, 32), float("nan"), device=DEV)
+                plan.spmm(Bt, C=C2)
+                torch.cuda.synchronize()
+                np.testing.assert_array_equal(C2.cpu().numpy(), C)
+                plan.free()
+            ones, C1, _ = run(M, K, row, col, np.ones(len(row), np.float32), "tblock_warp_total", 64, 8, 32, "f32",
+                              B=np.ones((K, 32), np.float32))
+            assert ones.info()["device_kernel"] == "k_lds_rows_rs"
+            nnz_row = np.bincount(row.astype(np.int64), minlength=M).astype(np.float32)
+            np.testing.assert_array_equal(C1, np.repeat(nnz_row[:, None], 32, axis=1))
+            ones.free()
+    finally:
+        gsa.set_config("LDS_KSPLIT", 0)
+
+
 @pytest.mark.parametrize("dtype", ["f32", "f16"])
 def test_lds_stage_known_answer(dtype, no_mfma):
     M, K, N = 700, 9000, 32
