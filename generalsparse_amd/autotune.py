@@ -40,7 +40,7 @@ CANDIDATES = {
                            ("merge_path", 1024, 1, {"MP_COL_PARTS": 4})],
 }
 # plans that exist only in the fp32 form of a class: k_lds_rows_rs (fp32 at N = 32, BMWs of 5..8
-# rows, one row per slot -- C2 fp32 30.1 us at (64,8) against 34.5 us for k_lds_rows_dma's (20,2),
+# rows, one row per slot -- C2 fp32 29.4 us at (64,8) against 35.4 us for k_lds_rows_dma's (20,2),
 # profiles/r06y_lds_rows_rs.txt); the fp32 comparator of an fp16 class searches these as well
 F32_EXTRA = {"f16": [("tblock_warp_total", 64, 8), ("tblock_warp_total", 72, 8)]}
 # the bench workloads (BASELINE.json configs) and the class each searches

@@ -1374,7 +1374,8 @@ __global__ __launch_bounds__(1024) void k_lds_rows_dma(
 // take entries of column parity k & 1, slots {2, 3, 6, 7} the opposite, so the ds_read_b128 lane
 // groups (slots {0,3} and {1,2} of each half-wave) read rows of opposite parity while both kinds
 // last.  A slot's row offsets in the chunk come by vector loads (one per chunk, issued with the
-// chunk's DMA).  Same DMA double buffer, K split and slab combine as k_lds_rows_dma.
+// chunk's DMA).  The columns arrive as LDS byte offsets of their B rows (column x 128, device_plan.hip).
+// Same DMA double buffer, K split and slab combine as k_lds_rows_dma.
 // The chunks' DMA is issued by inline asm (lds_dma16): with the builtin, hipcc's wait inserter puts a
 // vmcnt(0) before every LDS read of the issuing wave (the DMA writes LDS), so each wave would wait
 // for its share of chunk j+1 before computing chunk j; the kernel retires the DMA itself with
@@ -1457,7 +1458,7 @@ __global__ __launch_bounds__(1024) void k_lds_rows_rs(
                 const uint32_t cc[4] = {craw.x & 0xffffu, craw.x >> 16, craw.y & 0xffffu, craw.y >> 16};
                 uint4 braw[4];
 #pragma unroll
-                for (int qq = 0; qq < 4; qq++) braw[qq] = *reinterpret_cast<const uint4 *>(lBb + cc[qq] * RSB);
+                for (int qq = 0; qq < 4; qq++) braw[qq] = *reinterpret_cast<const uint4 *>(lBb + cc[qq]);  // byte offsets
                 const float4 vv = *reinterpret_cast<const float4 *>(lAv + p0 * 4u);
                 const float vq[4] = {vv.x, vv.y, vv.z, vv.w};
 #pragma unroll

@@ -191,6 +191,7 @@ bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uin
         }
         if (nc > K) { why = "no chunking fits LDS"; return false; }
     }
+    if (rowslot && (uint64_t)t.KC * RSB > 65536) { why = "row-per-slot chunks over 511 B rows"; return false; }
     t.RSB = RSB;
     t.rpw_max = rpw;
     t.waves = waves;
@@ -273,6 +274,10 @@ bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uin
                 }
             }
             for (uint64_t i = nr; i <= rpw; i++) off[i] = (uint32_t)(t.tcol.size() - base);
+            // rowslot: the chunk's columns as LDS byte offsets of their B rows (column x 128 B, < 64 KB
+            // for KC <= 511), so the kernel adds its lane's 16-B piece and reads (no shift, no mask)
+            if (rowslot)
+                for (size_t k = base; k < t.tcol.size(); k++) t.tcol[k] = (uint16_t)(t.tcol[k] * RSB);
             while ((t.tcol.size() - base) % 8) { t.tcol.push_back(0); t.src.push_back(~0u); }
             GS_CHECK(t.tcol.size() - base <= t.seg_cap, "LDS tile segment exceeds its capacity");
             GS_CHECK(t.tcol.size() < 0xffffffffull, "LDS tile layout exceeds 32-bit offsets");
