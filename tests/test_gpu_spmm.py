@@ -1216,14 +1216,17 @@ def test_divided_plan_file_computes_the_same(tmp_path):
 def test_warp_rows_grouped_passes(groups, N):
     """k_warp_rows with several short rows of a BMW per wave pass (WARP_ROWS_GROUPS, the
     software-pipelined path; C1-like rows of ~37 nonzeros in BMWs of 8 rows) and without:
-    both match the oracle"""
+    both match the oracle (LDS staging off: at fp32 N = 32 these BMWs of 8 rows would run
+    k_lds_rows_rs)"""
     M, K = 3000, 2000
     row, col, val = ds.random_rows(M, K, 37.0, seed=6, empty_frac=0.05)
     gsa.set_config("WARP_ROWS_GROUPS", groups)
+    gsa.set_config("LDS_STAGE_B", 0)
     try:
         plan, C, B = run(M, K, row, col, val, "tblock_warp_total", 32, 8, N, "f32")
     finally:
         gsa.set_config("WARP_ROWS_GROUPS", 1)
+        gsa.set_config("LDS_STAGE_B", 1)
     assert plan.info()["device_kernel"].startswith("k_warp_rows"), plan.info()["device_kernel"]
     check(C, ofi.spmm_ref(M, N, row, col, val, B, "f64"), "f32")
     plan.free()
