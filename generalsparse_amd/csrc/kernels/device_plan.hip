@@ -113,7 +113,7 @@ constexpr int kLdsMaxU = 12;  // 16-B staging registers per thread (k_lds_rows M
 bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uint64_t> &tb_bmw,
                      const std::vector<uint64_t> &bmw_rows, const std::vector<uint32_t> &row_ptr,
                      const std::vector<uint64_t> &col, uint64_t K, uint32_t N, uint32_t vbytes, size_t lds_budget,
-                     lds_tiles &t, std::string &why, bool dma = false) {
+                     lds_tiles &t, std::string &why, bool dma = false, uint64_t want = 1) {
     const uint64_t nb = tb_rows.size() - 1;
     if (nb == 0 || K == 0) { why = "empty plan"; return false; }
     if ((N * vbytes) % 16 != 0) { why = "B rows are not whole 16-B units"; return false; }
@@ -148,12 +148,21 @@ bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uin
     const uint64_t max_kc = std::min<uint64_t>(K, 65536);
     // smallest chunk count whose largest segment still fits LDS and the staging registers
     uint64_t nc = std::max<uint64_t>(1, (K * RSB * (dma ? 2 : 1) + lds_budget / 2) / (lds_budget * 3 / 4));
-    std::vector<uint32_t> cap_of(0);
+    // want > 1 (the plan's K split): past the first chunk count that fits, a few more are tried and
+    // the one with the fewest columns in the longest K range is kept -- a range is whole chunks, so
+    // 32 chunks in 6 ranges (6+6+6+6+6+2) run 6 chunks of 160 columns where 36 would run 6 of 144
+    // (C2 fp32 (64,8): 27.6 -> 25.8 us, profiles/r06zj)
+    bool found = false;
+    uint64_t nc_first = 0, best_cost = 0;
     for (;; nc++) {
         uint64_t KC = (K + nc - 1) / nc;
         KC = (KC + 7) / 8 * 8;
         if (KC > max_kc) continue;
-        if (KC < 64 && nc > 1) { why = "column chunks would be under 64 rows of B"; return false; }
+        if (KC < 64 && nc > 1) {
+            if (found) break;
+            why = "column chunks would be under 64 rows of B";
+            return false;
+        }
         const uint64_t ncc = (K + KC - 1) / KC;
         uint64_t cap = 0;
         std::vector<uint64_t> segl(ncc);
@@ -173,23 +182,31 @@ bool build_lds_tiles(const std::vector<uint64_t> &tb_rows, const std::vector<uin
         }
         const uint64_t lds = KC * RSB + cap * ebytes + (rpw + 1) * 4;
         const uint64_t units = KC * UB + cap * ebytes / 16;
-        if (dma) {  // k_lds_rows_dma: two buffers of B rows + columns + values (row offsets by scalar loads)
-            const uint64_t buf = KC * RSB + std::max<uint64_t>(cap, 8) * ebytes;
-            if (2 * buf <= lds_budget) {
+        // k_lds_rows_dma / _rs: two buffers of B rows + columns + values (row offsets by loads)
+        const uint64_t buf = KC * RSB + std::max<uint64_t>(cap, 8) * ebytes;
+        const bool fits = dma ? 2 * buf <= lds_budget : lds <= lds_budget && units <= (uint64_t)kLdsMaxU * nthr;
+        if (fits) {
+            const uint64_t w = std::max<uint64_t>(1, std::min<uint64_t>(want, ncc));
+            const uint64_t cost = (ncc + w - 1) / w * KC;  // columns of the longest K range
+            if (!found || cost < best_cost) {
                 t.KC = (uint32_t)KC;
                 t.nc = (uint32_t)ncc;
                 t.seg_cap = (uint32_t)std::max<uint64_t>(cap, 8);
-                t.lds_bytes = (size_t)(2 * buf + 15) / 16 * 16;
-                break;
+                t.lds_bytes = dma ? (size_t)(2 * buf + 15) / 16 * 16
+                                  : (size_t)(KC * RSB + (uint64_t)t.seg_cap * ebytes + (rpw + 1) * 4 + 15) / 16 * 16;
+                best_cost = cost;
             }
-        } else if (lds <= lds_budget && units <= (uint64_t)kLdsMaxU * nthr) {
-            t.KC = (uint32_t)KC;
-            t.nc = (uint32_t)ncc;
-            t.seg_cap = (uint32_t)std::max<uint64_t>(cap, 8);
-            t.lds_bytes = (size_t)(KC * RSB + (uint64_t)t.seg_cap * ebytes + (rpw + 1) * 4 + 15) / 16 * 16;
-            break;
+            if (!found) {
+                found = true;
+                nc_first = nc;
+            }
         }
-        if (nc > K) { why = "no chunking fits LDS"; return false; }
+        if (found && (want <= 1 || nc >= nc_first + 2 * want)) break;
+        if (nc > K) {
+            if (found) break;
+            why = "no chunking fits LDS";
+            return false;
+        }
     }
     if (rowslot && (uint64_t)t.KC * RSB > 65536) { why = "row-per-slot chunks over 511 B rows"; return false; }
     t.RSB = RSB;
@@ -762,23 +779,23 @@ void upload_plan(plan_state &p, int dtype, int device) {
                 // K split below makes the grid two per CU): C2 fp32 (20,2) 37.7 -> 34.4 us (r06r)
                 const bool dma = dtype == 0 && Nd == 32 && get_config().LDS_DMA != 0;
                 if (dma) budget = std::min<size_t>(budget, 80 * 1024);
+                // LDS_KSPLIT: S workgroups per BMTB, each over ncs consecutive chunks of K
+                // (every K range non-empty), fp32 slabs + one arrival counter per BMTB.  0 (auto):
+                // plans of under 128 BMTBs split K until ~256 workgroups (a workgroup's time
+                // is its nonzeros: C2 fp32 (20,2) 41.5 us = (40,4) in 2 K ranges 44.5 us,
+                // profiles/r06f_lds_ksplit.txt, so full grids gain nothing from a split)
+                // With LDS-DMA (two workgroups per CU) the auto split aims at ~512 workgroups.
+                const uint64_t nbt0 = m.u(TBLOCK_META, "first_row_indices", sb).size() - 1;
+                const int64_t cfg_ks = get_config().LDS_KSPLIT;
+                const uint64_t wg_aim = dma ? 512 : 256;
+                const uint32_t want = cfg_ks > 0 ? (uint32_t)cfg_ks
+                                                 : (nbt0 * 2 <= wg_aim ? (uint32_t)std::max<uint64_t>(1, wg_aim / std::max<uint64_t>(nbt0, 1)) : 1u);
                 if (build_lds_tiles(m.u(TBLOCK_META, "first_row_indices", sb), m.u(TBLOCK_META, "first_BMW_indices", sb),
                                     m.u(WARP_META, "first_row_indices", sb), rp, col, p.K, Nd, dtype ? 2u : 4u, budget,
-                                    t, why, dma)) {
+                                    t, why, dma, want)) {
                     d.lds = true;
                     d.lds_dma = dma;
                     d.kernel = t.maxr == 8 ? "k_lds_rows_rs" : (dma ? "k_lds_rows_dma" : "k_lds_rows");
-                    // LDS_KSPLIT: S workgroups per BMTB, each over ncs consecutive chunks of K
-                    // (every K range non-empty), fp32 slabs + one arrival counter per BMTB.  0 (auto):
-                    // plans of under 128 BMTBs split K until ~256 workgroups (a workgroup's time
-                    // is its nonzeros: C2 fp32 (20,2) 41.5 us = (40,4) in 2 K ranges 44.5 us,
-                    // profiles/r06f_lds_ksplit.txt, so full grids gain nothing from a split)
-                    // With LDS-DMA (two workgroups per CU) the auto split aims at ~512 workgroups.
-                    const uint64_t nbt0 = m.u(TBLOCK_META, "first_row_indices", sb).size() - 1;
-                    const int64_t cfg_ks = get_config().LDS_KSPLIT;
-                    const uint64_t wg_aim = dma ? 512 : 256;
-                    const uint32_t want = cfg_ks > 0 ? (uint32_t)cfg_ks
-                                                     : (nbt0 * 2 <= wg_aim ? (uint32_t)std::max<uint64_t>(1, wg_aim / std::max<uint64_t>(nbt0, 1)) : 1u);
                     const uint32_t ncs = (t.nc + std::min(want, t.nc) - 1) / std::min(want, t.nc);
                     d.ksplit = (t.nc + ncs - 1) / ncs;
                     d.ncs = ncs;
