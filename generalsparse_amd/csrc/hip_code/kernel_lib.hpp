@@ -4151,7 +4151,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                                                     const uint32_t *__restrict__ chain,  // 2 n_waves or null
                                                     uint32_t *__restrict__ chain_cnt,    // n_waves, zero between launches
                                                     uint32_t dbg = 0, uint64_t *__restrict__ stamps = nullptr) {
-    // dbg (diagnostic timing runs only, wrong results): bit 1 gathers B row 0 for every nonzero
+    // dbg (diagnostic timing runs only, wrong results): bit 1 gathers B row 0 for every nonzero;
+    // experiments build: bit 8 skips the slot scans (row-start prefix and the segmented carry
+    // scan), bit 16 treats every position as inside a row (no row closes or emits in a round)
     const uint32_t lb = blockIdx.x;  // (XCD-contiguous numbering measured no faster cold on C4)
     if (lb < fill_blocks) {
         // the first fill_blocks workgroups zero the empty rows (listed; 16-B stores when a
@@ -4301,14 +4303,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                 uint32_t bits = (uint32_t)flags[fo + kMpItems] << 8;
 #pragma unroll
                 for (uint32_t k = 0; k < 4; k++) bits |= ((f8.x >> (8 * k)) & 1u) << k | ((f8.y >> (8 * k)) & 1u) << (k + 4);
+#ifdef GS_EXPERIMENTS
+                if (dbg & 16u) bits = 0u;
+                const bool scans = !(dbg & 8u);
+#else
+                constexpr bool scans = true;
+#endif
                 const uint32_t pc = (uint32_t)__builtin_popcount(bits & 0xffu);
                 uint32_t incl = pc;
+                if (scans) {
 #pragma unroll
-                for (uint32_t st = 0; st < 6; st++) {
-                    const uint32_t off = X << st;
-                    if (off >= 64u) break;
-                    const uint32_t t = __shfl_up(incl, off, 64);
-                    if (lane >= off) incl += t;
+                    for (uint32_t st = 0; st < 6; st++) {
+                        const uint32_t off = X << st;
+                        if (off >= 64u) break;
+                        const uint32_t t = __shfl_up(incl, off, 64);
+                        if (lane >= off) incl += t;
+                    }
                 }
                 uint32_t qcur = qs + incl - pc;  // row open before this slot's first position
                 float acc[CF], h[CF];
@@ -4359,7 +4369,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
                 for (uint32_t st = 0; st < 6; st++) {
                     const uint32_t off = X << st;
-                    if (off >= 64u) break;
+                    if (off >= 64u || !scans) break;
                     const uint32_t ts = __shfl_up(stop, off, 64);
                     float t[CF];
 #pragma unroll
