@@ -36,8 +36,9 @@ CANDIDATES = {
     # minutes of host work; the balanced / row-per-thread plans are 4x-30x slower on C4)
     # (MP_COL_PARTS 4: the degree-ranked columns in 4 partitions, one pass each -- fabric reads 6.78x
     # -> 3.5x the algorithmic bytes at an even time, profiles/r06l_c4o_parts.txt)
+    # (MP_COL_PARTS 2 at merge_path(2048): 1.90 against 1.97 ms unpartitioned, profiles/r06zq_c4o_parts.txt)
     "f32_powerlaw_large": [("merge_path", 512, 1), ("merge_path", 1024, 1), ("merge_path", 2048, 1),
-                           ("merge_path", 1024, 1, {"MP_COL_PARTS": 4})],
+                           ("merge_path", 1024, 1, {"MP_COL_PARTS": 4}), ("merge_path", 2048, 1, {"MP_COL_PARTS": 2})],
 }
 # plans that exist only in the fp32 form of a class: k_lds_rows_rs (fp32 at N = 32, BMWs of 5..8
 # rows, one row per slot -- C2 fp32 29.4 us at (64,8) against 35.4 us for k_lds_rows_dma's (20,2),
